@@ -1,0 +1,166 @@
+"""Typed configuration: every env var of the reference under the same name,
+plus the reference's hard-coded values as overridable settings whose
+defaults equal the reference.
+
+Reference sources: ``cmd/downloader/downloader.go:26,45-58,62,68,81-95,147``,
+``internal/rabbitmq/client.go:107-108,308``,
+``internal/uploader/uploader.go:25-40``,
+``internal/uploader/minio_credential_provider.go:24-30``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+from dataclasses import dataclass, field, fields
+from typing import Mapping
+
+
+def _env_bool(v: str | None, default: bool) -> bool:
+    if v is None or v == "":
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+@dataclass
+class Config:
+    # --- logging / profiling (downloader.go:26,45-52) ---
+    cpuprofile: str = ""
+    log_level: str = ""
+    log_format: str = ""
+
+    # --- broker (downloader.go:54-58, client.go:308) ---
+    rabbitmq_endpoint: str = "127.0.0.1:5672"
+    rabbitmq_endpoint_defaulted: bool = True
+    rabbitmq_username: str = ""
+    rabbitmq_password: str = ""
+    rabbitmq_vhost: str = "/"
+    heartbeat_s: int = 30
+
+    # --- topology (hard-coded in the reference) ---
+    consume_topic: str = "v1.download"          # downloader.go:68
+    publish_topic: str = "v1.convert"           # downloader.go:147
+    num_shard_queues: int = 2                   # client.go:108
+    prefetch: int = 1                           # downloader.go:62
+
+    # --- job processing ---
+    concurrency: int = 1                        # one job loop (downloader.go:103)
+    max_retries: int = 5                        # B4 fix: X-Retries budget
+    retry_delay_s: float = 10.0                 # delivery.go:72
+    dead_letter_topic: str = ""                 # "" => drop after max_retries (nack)
+    cleanup: bool = False                       # B15: off for parity
+
+    # --- download (downloader.go:81-93, torrent.go:67) ---
+    download_dir: str = ""                      # default $CWD/downloading
+    progress_interval_s: float = 1.0            # http.go:45, torrent.go:83
+    progress_log_interval_s: float = 5.0        # downloader.go:115
+    metadata_timeout_s: float = 600.0           # torrent.go:67
+    bt_listen_port: int = 0                     # 0 = ephemeral
+    bt_dht: bool = True
+    bt_utp: bool = True
+    bt_bootstrap: str = "router.bittorrent.com:6881,dht.transmissionbt.com:6881"
+    gpu_verify: str = "auto"                    # auto|on|off (HIP batch piece hashing)
+
+    # --- upload (downloader.go:95, uploader.go) ---
+    bucket: str = "triton-staging"
+    s3_endpoint: str = ""
+    s3_access_key: str = ""
+    s3_secret_key: str = ""
+    s3_region: str = "us-east-1"
+    s3_part_size: int = 64 * 1024 * 1024
+    s3_multipart_threshold: int = 64 * 1024 * 1024
+    s3_parallel_parts: int = 4
+    aws_access_key_id: str = ""
+    aws_secret_access_key: str = ""
+    aws_session_token: str = ""
+    minio_access_key: str = ""
+    minio_secret_key: str = ""
+
+    # --- observability ---
+    metrics_addr: str = ""                      # "host:port" → /metrics
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] | None = None, argv: list[str] | None = None) -> "Config":
+        env = os.environ if env is None else env
+        c = cls()
+        g = env.get
+        c.log_level = g("LOG_LEVEL", "")
+        c.log_format = g("LOG_FORMAT", "")
+        ep = g("RABBITMQ_ENDPOINT", "")
+        if ep:
+            c.rabbitmq_endpoint, c.rabbitmq_endpoint_defaulted = ep, False
+        c.rabbitmq_username = g("RABBITMQ_USERNAME", "")
+        c.rabbitmq_password = g("RABBITMQ_PASSWORD", "")
+        c.rabbitmq_vhost = g("RABBITMQ_VHOST", "/") or "/"
+        c.s3_endpoint = g("S3_ENDPOINT", "")
+        c.s3_access_key = g("S3_ACCESS_KEY", "")
+        c.s3_secret_key = g("S3_SECRET_KEY", "")
+        c.s3_region = g("S3_REGION", c.s3_region) or c.s3_region
+        c.aws_access_key_id = g("AWS_ACCESS_KEY_ID", "") or g("AWS_ACCESS_KEY", "")
+        c.aws_secret_access_key = g("AWS_SECRET_ACCESS_KEY", "") or g("AWS_SECRET_KEY", "")
+        c.aws_session_token = g("AWS_SESSION_TOKEN", "")
+        c.minio_access_key = g("MINIO_ACCESS_KEY", "")
+        c.minio_secret_key = g("MINIO_SECRET_KEY", "")
+        # Extensions (TRITONDL_*) for values the reference hard-codes.
+        ints = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES": "num_shard_queues",
+                "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port",
+                "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
+                "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s"}
+        floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
+                  "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s"}
+        strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
+                "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
+                "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap"}
+        for k, a in ints.items():
+            if g("TRITONDL_" + k):
+                setattr(c, a, int(g("TRITONDL_" + k)))
+        for k, a in floats.items():
+            if g("TRITONDL_" + k):
+                setattr(c, a, float(g("TRITONDL_" + k)))
+        for k, a in strs.items():
+            if g("TRITONDL_" + k) is not None and g("TRITONDL_" + k) != "":
+                setattr(c, a, g("TRITONDL_" + k))
+        c.cleanup = _env_bool(g("TRITONDL_CLEANUP"), c.cleanup)
+        c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
+        c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
+        if argv is not None:
+            c.apply_args(parse_args(argv))
+        if not c.download_dir:
+            c.download_dir = os.path.join(os.getcwd(), "downloading")
+        return c
+
+    def apply_args(self, ns: argparse.Namespace) -> None:
+        for f in fields(self):
+            v = getattr(ns, f.name, None)
+            if v is not None:
+                setattr(self, f.name, v)
+
+    def rabbitmq_url(self) -> str:
+        """amqp://user:pass@endpoint/vhost with credentials URL-escaped (B14 fix)."""
+        from urllib.parse import quote
+        user = quote(self.rabbitmq_username, safe="")
+        pw = quote(self.rabbitmq_password, safe="")
+        vh = "" if self.rabbitmq_vhost == "/" else "/" + quote(self.rabbitmq_vhost, safe="")
+        return f"amqp://{user}:{pw}@{self.rabbitmq_endpoint}{vh}"
+
+
+def build_arg_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="tritondl", description="media ingest worker (downloader-go capabilities)")
+    # Go's flag package accepts both -cpuprofile and --cpuprofile.
+    p.add_argument("-cpuprofile", "--cpuprofile", dest="cpuprofile", default=None,
+                   help="write cpu profile to file")
+    p.add_argument("--concurrency", type=int, default=None, help="jobs in flight per process (reference: 1)")
+    p.add_argument("--prefetch", type=int, default=None, help="AMQP QoS prefetch (reference: 1)")
+    p.add_argument("--download-dir", dest="download_dir", default=None)
+    p.add_argument("--bucket", default=None)
+    p.add_argument("--consume-topic", dest="consume_topic", default=None)
+    p.add_argument("--publish-topic", dest="publish_topic", default=None)
+    p.add_argument("--metrics-addr", dest="metrics_addr", default=None)
+    p.add_argument("--cleanup", dest="cleanup", action="store_true", default=None)
+    p.add_argument("--gpu-verify", dest="gpu_verify", choices=["auto", "on", "off"], default=None)
+    return p
+
+
+def parse_args(argv: list[str]) -> argparse.Namespace:
+    return build_arg_parser().parse_args(argv)
