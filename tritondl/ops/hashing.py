@@ -1,0 +1,112 @@
+"""Python surface of the native hashing layer.
+
+Host module ``tritondl._hash_host`` (C++/OpenSSL) is mandatory: importing
+this module fails loudly if it has not been built (``python
+tools/build_native.py``) — there is no silent pure-Python fallback.
+
+GPU module ``tritondl._gpu_hash`` (HIP, gfx950) is used for batched piece
+verification when a device is present (``device="auto"``) or demanded
+(``device="gpu"``: raises if unavailable).
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+from typing import Sequence
+
+try:
+    from .. import _hash_host as _host  # type: ignore[attr-defined]
+except ImportError as e:  # pragma: no cover - exercised only on broken builds
+    raise ImportError("tritondl native host hashing extension is not built; run "
+                      "`python tools/build_native.py` (or __graft_entry__.build())") from e
+
+DIGEST_LEN = {"sha1": 20, "sha256": 32, "md5": 16}
+
+Hasher = _host.Hasher
+
+
+def digest(kind: str, data) -> bytes:
+    return _host.digest(kind, data)
+
+
+def hash_file(path: str, kinds: Sequence[str] = ("sha256",), offset: int = 0, length: int = -1,
+              bufsize: int = 1 << 20) -> dict:
+    """One pass over (part of) a file computing several digests; adds ``size``."""
+    return _host.hash_file(path, list(kinds), offset, length, bufsize)
+
+
+def hmac_sha256(key: bytes, msg: bytes) -> bytes:
+    return _host.hmac_sha256(key, msg)
+
+
+def chunk_signatures(signing_key: bytes, amzdate: str, scope: str, seed_signature: str, data,
+                     chunk_size: int) -> list[str]:
+    return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size)
+
+
+# ----------------------------------------------------------------- GPU
+
+_gpu_mod = None
+_gpu_lock = threading.Lock()
+_gpu_hashers: dict[int, object] = {}
+
+
+def _load_gpu():
+    global _gpu_mod
+    if _gpu_mod is None:
+        from .. import _gpu_hash  # type: ignore[attr-defined]
+        _gpu_mod = _gpu_hash
+    return _gpu_mod
+
+
+def gpu_module():
+    """Return the HIP extension module (raises ImportError if not built)."""
+    return _load_gpu()
+
+
+def gpu_available() -> bool:
+    if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off":
+        return False
+    try:
+        return _load_gpu().device_count() > 0
+    except Exception:
+        return False
+
+
+def gpu_hasher(device: int = 0, batch_bytes: int = 256 << 20, reader_threads: int = 8):
+    with _gpu_lock:
+        h = _gpu_hashers.get(device)
+        if h is None or h.batch_bytes != max(batch_bytes, 1 << 20):
+            h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads)
+            _gpu_hashers[device] = h
+        return h
+
+
+def _resolve(device: str) -> str:
+    if device == "auto":
+        return "gpu" if gpu_available() else "cpu"
+    if device == "gpu" and not gpu_available():
+        raise RuntimeError("GPU hashing requested but no HIP device / _gpu_hash extension available")
+    if device not in ("cpu", "gpu"):
+        raise ValueError(f"device must be auto|cpu|gpu, got {device!r}")
+    return device
+
+
+def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", threads: int = 0) -> bytes:
+    """Concatenated digests of ``data`` split into ``piece_len`` pieces."""
+    dev = _resolve(device)
+    if dev == "gpu":
+        return gpu_hasher().hash_buffer(kind, data, piece_len)
+    return _host.piece_hashes(kind, data, piece_len, threads)
+
+
+def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: bytes, kind: str = "sha1",
+                  device: str = "cpu", threads: int = 0) -> bytes:
+    """Verify the torrent layout ``files`` [(path, length), ...] against
+    ``expected`` (concatenated digests).  Returns one byte (0/1) per piece."""
+    dev = _resolve(device)
+    files = [(str(p), int(n)) for p, n in files]
+    if dev == "gpu":
+        return gpu_hasher().verify_files(files, piece_len, expected, kind)
+    return _host.verify_pieces(files, piece_len, expected, threads, kind)
