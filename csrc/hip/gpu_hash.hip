@@ -13,7 +13,8 @@
 //    one wave per SIMD across the 256 CUs (8 XCDs) instead of stacking.
 //  * The kernel is VALU-bound (~700 int ops / 64 B block): rounds are fully
 //    unrolled so the 16-word message window lives in VGPRs; rotates lower to
-//    v_alignbit_b32, Ch/Maj to v_bfi_b32, byte swaps to v_perm_b32.
+//    v_alignbit_b32, xor3/Ch/Maj to ONE gfx950 v_bitop3_b32 each, byte swaps
+//    to v_perm_b32.
 //  * Loads are 4 x dwordx4 per 64-byte block per lane, and the NEXT block is
 //    prefetched into registers before compressing the current one so HBM
 //    latency hides under ~1.5k cycles of ALU work.  Lanes stride by
@@ -52,6 +53,18 @@ namespace py = pybind11;
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+// gfx950 v_bitop3_b32: any 3-input bitwise function in ONE VALU op (truth table
+// over S0=0xF0, S1=0xCC, S2=0xAA).  hipcc does not fuse xor chains / Ch / Maj
+// into it on its own (measured: 292 v_xor_b32 per SHA-1 block before).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch3(uint32_t x, uint32_t y, uint32_t z) {  // (x&y)|(~x&z)
+  return __builtin_amdgcn_bitop3_b32(x, y, z, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj3(uint32_t x, uint32_t y, uint32_t z) {  // majority
+  return __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8);
+}
 
 __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
@@ -61,21 +74,21 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
     if (t < 16) {
       wt = w[t];
     } else {
-      wt = rotl32(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+      wt = rotl32(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
       w[t & 15] = wt;
     }
     uint32_t f, k;
     if (t < 20) {
-      f = (b & c) | (~b & d);  // Ch  -> v_bfi_b32
+      f = ch3(b, c, d);
       k = 0x5A827999u;
     } else if (t < 40) {
-      f = b ^ c ^ d;
+      f = xor3(b, c, d);
       k = 0x6ED9EBA1u;
     } else if (t < 60) {
-      f = (b & c) | (d & (b ^ c));  // Maj -> v_bfi_b32
+      f = maj3(b, c, d);
       k = 0x8F1BBCDCu;
     } else {
-      f = b ^ c ^ d;
+      f = xor3(b, c, d);
       k = 0xCA62C1D6u;
     }
     uint32_t tmp = rotl32(a, 5) + f + e + k + wt;
@@ -110,16 +123,16 @@ __device__ __forceinline__ void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       wt = w[t];
     } else {
       uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
       w[t & 15] = wt;
     }
-    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-    uint32_t ch = (e & f) | (~e & g);
+    uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    uint32_t ch = ch3(e, f, g);
     uint32_t t1 = hh + S1 + ch + K[t] + wt;
-    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-    uint32_t maj = (a & b) | (c & (a ^ b));
+    uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    uint32_t maj = maj3(a, b, c);
     uint32_t t2 = S0 + maj;
     hh = g;
     g = f;

@@ -55,6 +55,15 @@ _gpu_hashers: dict[int, object] = {}
 def _load_gpu():
     global _gpu_mod
     if _gpu_mod is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 and
+        # loads it by a different file name, so it must be mapped FIRST; our
+        # extension's DT_NEEDED libamdhip64.so.7 then binds to that same copy.
+        # (Loaded the other way round, two HSA runtimes fight over the device
+        # and torch reports "No HIP GPUs are available".)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         from .. import _gpu_hash  # type: ignore[attr-defined]
         _gpu_mod = _gpu_hash
     return _gpu_mod
