@@ -1,0 +1,287 @@
+"""AMQP layer: codec, connection ↔ fake broker, and the job client
+(topology, fan-in, round-robin publish, X-Retries, reconnect)."""
+
+import asyncio
+from decimal import Decimal
+
+import pytest
+
+from tritondl.amqp import codec
+from tritondl.amqp.client import Client, _parse_retries
+from tritondl.amqp.codec import Method, Properties
+from tritondl.amqp.connection import ChannelClosed, Connection, ConnectionClosed, PublishNacked, parse_url
+from tritondl.fakes.broker import Broker
+from tritondl.utils.backoff import ExponentialBackoff
+
+
+def run(coro, timeout=20):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+# ------------------------------------------------------------------ codec
+
+
+def test_table_roundtrip():
+    t = {"a": 1, "b": "str", "c": True, "d": 2**40, "e": 1.5, "f": {"x": [1, "y", None]}, "g": b"\x00\x01",
+         "h": Decimal("1.25")}
+    assert codec.decode_table(codec.encode_table(t)) == t
+
+
+def test_method_roundtrip_with_bits():
+    m = Method("queue.declare", {"queue": "q", "passive": False, "durable": True, "exclusive": False,
+                                 "auto_delete": True, "nowait": False, "arguments": {"x-max": 5}})
+    d = codec.decode_method(codec.encode_method(m))
+    assert d.name == "queue.declare" and d.durable and d.auto_delete and not d.exclusive
+    assert d.arguments == {"x-max": 5}
+    # bit packing: 5 consecutive bits -> one octet
+    raw = codec.encode_method(m)
+    assert raw.endswith(codec.encode_table({"x-max": 5}))
+
+
+def test_header_roundtrip():
+    p = Properties(content_type="application/octet-stream", delivery_mode=2, headers={"X-Retries": 3},
+                   message_id="m1", timestamp=123)
+    cid, size, q = codec.decode_header(codec.encode_header(60, 99, p))
+    assert (cid, size) == (60, 99) and q == p
+
+
+def test_parse_url():
+    p = parse_url("amqp://u%40x:p%2F@h:1234/v%2Fh")
+    assert (p.username, p.password, p.host, p.port, p.vhost) == ("u@x", "p/", "h", 1234, "v/h")
+    p = parse_url("amqp://:@127.0.0.1:5672")
+    assert p.vhost == "/" and p.username == ""
+
+
+def test_parse_retries():
+    assert _parse_retries(None) == 0
+    assert _parse_retries({"X-Retries": 4}) == 4
+    assert _parse_retries({"X-Retries": "4"}) == 0
+    assert _parse_retries({"X-Retries": 2**40}) == 0
+
+
+# ------------------------------------------------------- connection/broker
+
+
+def test_publish_consume_ack_and_prefetch():
+    async def main():
+        b = await Broker().start()
+        conn = await Connection.open(b.url)
+        ch = await conn.channel()
+        await ch.exchange_declare("ex", "direct", durable=True)
+        await ch.queue_declare("q", durable=True)
+        await ch.queue_bind("q", "ex", "q")
+        await ch.confirm_select()
+        for i in range(5):
+            await ch.basic_publish("ex", "q", f"m{i}".encode(), Properties(delivery_mode=2))
+        cch = await conn.channel()
+        await cch.basic_qos(2, 0, True)
+        got = []
+        await cch.basic_consume("q", got.append)
+        await asyncio.sleep(0.05)
+        assert [m.body for m in got] == [b"m0", b"m1"]  # prefetch 2, nothing acked yet
+        await got[0].ack()
+        await asyncio.sleep(0.05)
+        assert len(got) == 3
+        await got[1].nack(requeue=True)
+        await asyncio.sleep(0.05)
+        assert got[-1].body == b"m1" and got[-1].redelivered
+        # large body is split over frames
+        big = bytes(range(256)) * 4000
+        await ch.basic_publish("ex", "q", big)
+        acked = 1
+        for _ in range(50):
+            for m in got[acked:]:
+                if m.body != b"m1" or m.redelivered:
+                    await m.ack()
+            acked = len(got)
+            await asyncio.sleep(0.02)
+            if any(m.body == big for m in got):
+                break
+        assert any(m.body == big for m in got)
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_close_requeues_unacked_and_channel_errors():
+    async def main():
+        b = await Broker().start()
+        c1 = await Connection.open(b.url)
+        ch = await c1.channel()
+        await ch.queue_declare("q")
+        await ch.basic_publish("", "q", b"job")
+        got = []
+        await ch.basic_consume("q", got.append)
+        await asyncio.sleep(0.05)
+        assert len(got) == 1 and not got[0].redelivered
+        await c1.close()
+        c2 = await Connection.open(b.url)
+        ch2 = await c2.channel()
+        got2 = []
+        await ch2.basic_consume("q", got2.append)
+        await asyncio.sleep(0.05)
+        assert got2[0].body == b"job" and got2[0].redelivered
+        # inequivalent redeclare -> channel closed 406, connection survives
+        with pytest.raises(ChannelClosed) as ei:
+            await ch2.queue_declare("q", durable=True)
+        assert ei.value.code == codec.PRECONDITION_FAILED
+        ch3 = await c2.channel()
+        with pytest.raises(ChannelClosed) as ei:
+            await ch3.queue_declare("nope", passive=True)
+        assert ei.value.code == codec.NOT_FOUND
+        assert not c2.is_closed
+        await c2.close()
+        await b.stop()
+    run(main())
+
+
+def test_confirms_nack_injection_and_dead_letter():
+    async def main():
+        b = await Broker().start()
+        conn = await Connection.open(b.url)
+        ch = await conn.channel()
+        await ch.exchange_declare("dlx", "fanout")
+        await ch.queue_declare("dead")
+        await ch.queue_bind("dead", "dlx")
+        await ch.queue_declare("work", arguments={"x-dead-letter-exchange": "dlx"})
+        await ch.confirm_select()
+        b.fail_next_publishes(1)
+        with pytest.raises(PublishNacked):
+            await ch.basic_publish("", "work", b"x")
+        await ch.basic_publish("", "work", b"y")
+        m = await ch.basic_get("work")
+        assert m.body == b"y"
+        await m.nack(requeue=False)
+        await asyncio.sleep(0.02)
+        assert b.queue_depth("dead") == 1
+        assert b.drain_queue("dead")[0].props.headers["x-death"][0]["queue"] == "work"
+        assert await ch.basic_get("work") is None
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_auth_refused_and_blocked():
+    async def main():
+        b = await Broker(username="u", password="p").start()
+        with pytest.raises(ConnectionClosed):
+            await Connection.open(f"amqp://u:wrong@{b.endpoint}/")
+        conn = await Connection.open(f"amqp://u:p@{b.endpoint}/")
+        ch = await conn.channel()
+        await ch.queue_declare("q")
+        b.set_blocked(True)
+        await asyncio.sleep(0.02)
+        t = asyncio.ensure_future(ch.basic_publish("", "q", b"z"))
+        await asyncio.sleep(0.05)
+        assert not t.done()
+        b.set_blocked(False)
+        await asyncio.wait_for(t, 2)
+        await asyncio.sleep(0.05)
+        assert b.queue_depth("q") == 1
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_heartbeat_detects_dead_peer():
+    async def main():
+        # a "server" that completes the handshake and then goes silent
+        b = await Broker(heartbeat=1).start()
+        conn = await Connection.open(b.url, heartbeat=1)
+        for c in list(b.conns):  # stop reading/writing on the server side
+            c.closed = True
+        err = await asyncio.wait_for(conn.wait_closed(), 5)
+        assert "heartbeat" in str(err) or isinstance(err, ConnectionClosed)
+        await b.stop()
+    run(main())
+
+
+# ------------------------------------------------------------------ client
+
+
+def test_client_topology_fanin_and_round_robin():
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        stream = await cl.consume("v1.download")
+        assert {"v1.download-0", "v1.download-1"} <= set(b.queues)
+        ex = b.exchanges["v1.download"]
+        assert ex.type == "direct" and ex.durable
+        assert sorted(x[:2] for x in ex.bindings) == [("v1.download-0", "v1.download-0"),
+                                                       ("v1.download-1", "v1.download-1")]
+        for i in range(4):
+            await cl.publish("v1.download", f"j{i}".encode())
+        rks = [m.routing_key for m in b.published]
+        assert rks == ["v1.download-0", "v1.download-1"] * 2
+        assert all(m.props.delivery_mode == 2 and m.props.content_type == "application/octet-stream"
+                   for m in b.published)
+        seen = []
+        async for d in stream:
+            seen.append(d.body)
+            await d.ack()
+            if len(seen) == 4:
+                break
+        assert sorted(seen) == [b"j0", b"j1", b"j2", b"j3"]
+        await cl.close()
+        await b.stop()
+    run(main())
+
+
+def test_client_retry_increments_x_retries():
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1, retry_delay=0).connect()
+        await cl.consume("t")
+        await cl.publish("t", b"job")
+        d = await cl.get(2)
+        assert d.metadata.retries == 0
+        await d.retry()
+        d2 = await cl.get(2)
+        assert d2.body == b"job" and d2.metadata.retries == 1 and d2.routing_key == d.routing_key
+        await d2.nack()
+        await asyncio.sleep(0.05)
+        assert b.queue_depth("t-0") + b.queue_depth("t-1") == 0
+        await cl.close()
+        await b.stop()
+    run(main())
+
+
+def test_client_reconnects_and_redelivers():
+    async def main():
+        b = await Broker().start()
+        cl = Client(b.url, prefetch=1, heartbeat=0,
+                    backoff=ExponentialBackoff(initial=0.02, max_interval=0.1, max_elapsed=10))
+        await cl.connect()
+        await cl.consume("t")
+        await cl.publish("t", b"a")
+        d = await cl.get(2)
+        assert d.body == b"a" and not d.redelivered
+        await b.drop_connections()
+        for _ in range(100):
+            if cl.reconnects and cl.connected:
+                break
+            await asyncio.sleep(0.02)
+        assert cl.reconnects == 1
+        await d.ack()  # stale: must not raise
+        d2 = await cl.get(3)
+        assert d2.body == b"a" and d2.redelivered
+        await d2.ack()
+        await cl.publish("t", b"b")  # publisher channel re-created on the new connection
+        d3 = await cl.get(2)
+        assert d3.body == b"b"
+        await d3.ack()
+        await cl.close()
+        await b.stop()
+    run(main())
+
+
+def test_client_publish_retries_after_nack():
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url).connect()
+        b.fail_next_publishes(2)
+        await cl.publish("v1.convert", b"c")
+        assert b.queue_depth("v1.convert-0") == 1
+        await cl.close()
+        await b.stop()
+    run(main())

@@ -369,6 +369,7 @@ class Channel:
         self.on_return: Callable[[Message], Any] | None = None
         self.on_cancel: Callable[[str], Any] | None = None
         self._get_waiter: asyncio.Future | None = None
+        self._pending_consume_cb: DeliverCallback | None = None
         self.flow_active = asyncio.Event()
         self.flow_active.set()
         self._close_callbacks: list[Callable[[AMQPError], Any]] = []
@@ -454,6 +455,8 @@ class Channel:
             if self._get_waiter and not self._get_waiter.done():
                 self._get_waiter.set_result(None)
             return
+        if n == "basic.consume_ok" and self._pending_consume_cb is not None:
+            self._consumers[m.consumer_tag] = self._pending_consume_cb
         if self._waiter is not None and not self._waiter.done() and n in self._expect:
             self._waiter.set_result(m)
 
@@ -565,30 +568,16 @@ class Channel:
 
     async def basic_consume(self, queue: str, callback: DeliverCallback, *, consumer_tag: str = "",
                             no_ack: bool = False, exclusive: bool = False, arguments: dict | None = None) -> str:
-        # Register under a provisional key so deliveries that race consume_ok are not lost.
-        async with self._rpc_lock:
-            self._check()
-            loop = asyncio.get_running_loop()
-            self._waiter = loop.create_future()
-            self._expect = ("basic.consume_ok",)
-            pending: list[Message] = []
-            if consumer_tag:
-                self._consumers[consumer_tag] = callback
-            else:
-                self._consumers[""] = lambda m: pending.append(m)
-            self.conn._send_method(self.id, Method("basic.consume", {
+        # The callback is bound to the server-assigned tag by the READER as soon as
+        # consume_ok arrives, so deliveries in the same read batch are not lost.
+        self._pending_consume_cb = callback
+        try:
+            r = await self._rpc(Method("basic.consume", {
                 "queue": queue, "consumer_tag": consumer_tag, "no_ack": no_ack, "exclusive": exclusive,
-                "arguments": arguments or {}}))
-            try:
-                r = await self._waiter
-            finally:
-                self._waiter = None
-                self._consumers.pop("", None)
-        tag = r.consumer_tag
-        self._consumers[tag] = callback
-        for m in pending:
-            callback(m)
-        return tag
+                "arguments": arguments or {}}), "basic.consume_ok")
+        finally:
+            self._pending_consume_cb = None
+        return r.consumer_tag
 
     async def basic_cancel(self, consumer_tag: str) -> None:
         await self._rpc(Method("basic.cancel", {"consumer_tag": consumer_tag}), "basic.cancel_ok")

@@ -1,0 +1,682 @@
+"""In-process AMQP 0-9-1 broker (asyncio, TCP) — the RabbitMQ stand-in for
+tests, the smoke check and bench.py.  The reference had no fake broker at all
+(zero coverage of the messaging layer).
+
+Implements the RabbitMQ semantics the worker depends on:
+
+* PLAIN auth, tune/open, heartbeats, channel open/close/flow;
+* direct / fanout / topic exchanges plus the default exchange; durable /
+  argument equivalence checks (406 PRECONDITION_FAILED on mismatch);
+* queues with round-robin consumers, ``basic.qos`` prefetch (RabbitMQ
+  reading: ``global=true`` → per-channel limit, ``false`` → per-consumer);
+* manual ack/nack/reject (+``multiple``), requeue with ``redelivered``;
+  unacked messages requeued when a channel or connection closes;
+* dead-lettering via ``x-dead-letter-exchange`` / ``-routing-key``;
+* ``basic.get``, ``basic.cancel``, publisher confirms, ``mandatory`` returns;
+* fault injection: :meth:`drop_connections`, :meth:`set_blocked`,
+  :meth:`fail_next_publishes` (nack), accept-delay.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import collections
+import itertools
+import re
+from dataclasses import dataclass, field
+from typing import Any
+
+from ..amqp import codec
+from ..amqp.codec import Method, Properties
+
+
+@dataclass
+class QMsg:
+    body: bytes
+    props: Properties
+    exchange: str
+    routing_key: str
+    redelivered: bool = False
+
+
+@dataclass
+class Exchange:
+    name: str
+    type: str
+    durable: bool
+    auto_delete: bool = False
+    internal: bool = False
+    arguments: dict = field(default_factory=dict)
+    bindings: list[tuple[str, str, dict]] = field(default_factory=list)  # (queue, rk, args)
+
+
+@dataclass
+class Queue:
+    name: str
+    durable: bool
+    exclusive: bool = False
+    auto_delete: bool = False
+    arguments: dict = field(default_factory=dict)
+    messages: collections.deque = field(default_factory=collections.deque)
+    consumers: list = field(default_factory=list)  # [_Consumer]
+    rr: int = 0
+    owner: Any = None
+    delivered_total: int = 0
+
+
+class _Consumer:
+    def __init__(self, ch: "_ServerChannel", tag: str, queue: Queue, no_ack: bool, prefetch: int) -> None:
+        self.ch = ch
+        self.tag = tag
+        self.queue = queue
+        self.no_ack = no_ack
+        self.prefetch = prefetch
+        self.unacked = 0
+
+
+class ChannelError(Exception):
+    def __init__(self, code: int, text: str, cm: tuple[int, int] = (0, 0)) -> None:
+        super().__init__(text)
+        self.code, self.text, self.cm = code, text, cm
+
+
+class ConnError(ChannelError):
+    pass
+
+
+def _topic_match(pattern: str, key: str) -> bool:
+    """AMQP topic match: ``*`` = exactly one word, ``#`` = zero or more words."""
+    pw, kw = pattern.split("."), key.split(".")
+
+    def m(i: int, j: int) -> bool:
+        if i == len(pw):
+            return j == len(kw)
+        if pw[i] == "#":
+            return any(m(i + 1, k) for k in range(j, len(kw) + 1))
+        if j == len(kw):
+            return False
+        return (pw[i] == "*" or pw[i] == kw[j]) and m(i + 1, j + 1)
+
+    return m(0, 0)
+
+
+class _ServerChannel:
+    def __init__(self, conn: "_ServerConn", cid: int) -> None:
+        self.conn = conn
+        self.id = cid
+        self.prefetch_channel = 0      # global=true
+        self.prefetch_consumer = 0     # global=false (applies to new consumers)
+        self.unacked: dict[int, tuple[QMsg, Queue, _Consumer | None]] = {}
+        self.tags = itertools.count(1)
+        self.consumers: dict[str, _Consumer] = {}
+        self.confirm = False
+        self.pub_seq = 0
+        self.pending: tuple[Method, Properties | None, int, list[bytes]] | None = None
+        self.flow = True
+
+    def channel_unacked(self) -> int:
+        return len(self.unacked)
+
+
+class _ServerConn:
+    def __init__(self, broker: "Broker", reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        self.broker = broker
+        self.reader = reader
+        self.writer = writer
+        self.channels: dict[int, _ServerChannel] = {}
+        self.frame_max = codec.DEFAULT_FRAME_MAX
+        self.open = False
+        self.closed = False
+        self.client_properties: dict = {}
+        self.user = ""
+
+    def send(self, data: bytes) -> None:
+        if not self.closed and not self.writer.is_closing():
+            self.writer.write(data)
+
+    def send_method(self, ch: int, m: Method) -> None:
+        self.send(codec.method_frame(ch, m))
+
+
+class Broker:
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, *, username: str | None = None,
+                 password: str | None = None, heartbeat: int = 0, frame_max: int = codec.DEFAULT_FRAME_MAX) -> None:
+        self.host = host
+        self.port = port
+        self.username = username
+        self.password = password
+        self.heartbeat = heartbeat
+        self.frame_max = frame_max
+        self.exchanges: dict[str, Exchange] = {"": Exchange("", "direct", True),
+                                               "amq.direct": Exchange("amq.direct", "direct", True),
+                                               "amq.fanout": Exchange("amq.fanout", "fanout", True),
+                                               "amq.topic": Exchange("amq.topic", "topic", True)}
+        self.queues: dict[str, Queue] = {}
+        self.conns: set[_ServerConn] = set()
+        self._server: asyncio.AbstractServer | None = None
+        self._ctag = itertools.count(1)
+        self._qname = itertools.count(1)
+        self.blocked = False
+        self.fail_publishes = 0
+        self.published: list[QMsg] = []
+        self.stats = collections.Counter()
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self) -> "Broker":
+        self._server = await asyncio.start_server(self._handle, self.host, self.port)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self
+
+    @property
+    def url(self) -> str:
+        u = self.username or "guest"
+        p = self.password or "guest"
+        return f"amqp://{u}:{p}@{self.host}:{self.port}/"
+
+    @property
+    def endpoint(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    async def stop(self) -> None:
+        if self._server is not None:
+            self._server.close()
+            await self.drop_connections()
+            await self._server.wait_closed()
+            self._server = None
+
+    async def drop_connections(self, code: int = codec.CONNECTION_FORCED, text: str = "broker forced close",
+                               graceful: bool = False) -> None:
+        """Fault injection: kill every client connection (unacked messages are requeued)."""
+        for c in list(self.conns):
+            if graceful:
+                c.send_method(0, Method("connection.close", {"reply_code": code, "reply_text": text}))
+            self._teardown(c)
+            try:
+                c.writer.transport.abort() if not graceful else c.writer.close()
+            except Exception:
+                pass
+        await asyncio.sleep(0)
+
+    def set_blocked(self, blocked: bool) -> None:
+        self.blocked = blocked
+        for c in self.conns:
+            if c.open:
+                c.send_method(0, Method("connection.blocked", {"reason": "low on memory"}) if blocked
+                              else Method("connection.unblocked"))
+
+    def fail_next_publishes(self, n: int) -> None:
+        """Fault injection: nack the next ``n`` confirmed publishes."""
+        self.fail_publishes = n
+
+    # ------------------------------------------------------------ introspection
+    def queue_depth(self, name: str) -> int:
+        q = self.queues.get(name)
+        return len(q.messages) if q else 0
+
+    def unacked_count(self) -> int:
+        return sum(len(ch.unacked) for c in self.conns for ch in c.channels.values())
+
+    def drain_queue(self, name: str) -> list[QMsg]:
+        q = self.queues.get(name)
+        if q is None:
+            return []
+        out = list(q.messages)
+        q.messages.clear()
+        return out
+
+    def inject(self, exchange: str, routing_key: str, body: bytes, props: Properties | None = None) -> int:
+        """Publish from outside any connection (test producer). Returns #queues routed."""
+        return self._route(QMsg(body, props or Properties(), exchange, routing_key))
+
+    # ------------------------------------------------------------ connection
+    async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        c = _ServerConn(self, reader, writer)
+        self.conns.add(c)
+        try:
+            hdr = await reader.readexactly(8)
+            if hdr != codec.PROTOCOL_HEADER:
+                writer.write(codec.PROTOCOL_HEADER)
+                return
+            c.send_method(0, Method("connection.start", {
+                "version_major": 0, "version_minor": 9,
+                "server_properties": {"product": "tritondl-fakebroker", "version": "3.8-compat",
+                                      "capabilities": {"publisher_confirms": True, "basic.nack": True,
+                                                       "consumer_cancel_notify": True,
+                                                       "connection.blocked": True, "per_consumer_qos": True}},
+                "mechanisms": b"PLAIN AMQPLAIN", "locales": b"en_US"}))
+            while True:
+                ftype, ch, payload = await codec.read_frame(reader)
+                try:
+                    self._on_frame(c, ftype, ch, payload)
+                except ConnError as e:
+                    c.send_method(0, Method("connection.close", {"reply_code": e.code, "reply_text": e.text[:255],
+                                                                 "class_id": e.cm[0], "method_id": e.cm[1]}))
+                    await writer.drain()
+                    break
+                except ChannelError as e:
+                    sc = c.channels.pop(ch, None)
+                    if sc is not None:
+                        self._close_channel(sc)
+                    c.send_method(ch, Method("channel.close", {"reply_code": e.code, "reply_text": e.text[:255],
+                                                               "class_id": e.cm[0], "method_id": e.cm[1]}))
+                if c.closed:
+                    break
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionError, OSError, codec.FrameError):
+            pass
+        finally:
+            self._teardown(c)
+            try:
+                writer.close()
+            except Exception:
+                pass
+
+    def _teardown(self, c: _ServerConn) -> None:
+        if c in self.conns:
+            self.conns.discard(c)
+        c.closed = True
+        for ch in list(c.channels.values()):
+            self._close_channel(ch)
+        c.channels.clear()
+        for q in [q for q in self.queues.values() if q.exclusive and q.owner is c]:
+            self.queues.pop(q.name, None)
+
+    def _close_channel(self, ch: _ServerChannel) -> None:
+        for cons in list(ch.consumers.values()):
+            self._remove_consumer(cons)
+        # requeue unacked in original order, marked redelivered
+        for tag in sorted(ch.unacked, reverse=True):
+            msg, q, _cons = ch.unacked[tag]
+            msg.redelivered = True
+            if q.name in self.queues:
+                q.messages.appendleft(msg)
+        touched = {q.name for _m, q, _c in ch.unacked.values()}
+        ch.unacked.clear()
+        for name in touched:
+            if name in self.queues:
+                self._dispatch(self.queues[name])
+
+    def _remove_consumer(self, cons: _Consumer) -> None:
+        if cons in cons.queue.consumers:
+            cons.queue.consumers.remove(cons)
+        cons.ch.consumers.pop(cons.tag, None)
+        if cons.queue.auto_delete and not cons.queue.consumers and cons.queue.name in self.queues:
+            self.queues.pop(cons.queue.name, None)
+
+    # ------------------------------------------------------------ frames
+    def _on_frame(self, c: _ServerConn, ftype: int, ch: int, payload: bytes) -> None:
+        if ftype == codec.FRAME_HEARTBEAT:
+            return
+        if ftype == codec.FRAME_METHOD:
+            m = codec.decode_method(payload)
+            if ch == 0:
+                self._on_conn_method(c, m)
+                return
+            if m.name == "channel.open":
+                if ch in c.channels:
+                    raise ConnError(codec.CHANNEL_ERROR, "channel already open", m.ids)
+                c.channels[ch] = _ServerChannel(c, ch)
+                c.send_method(ch, Method("channel.open_ok", {"channel_id": b""}))
+                return
+            sc = c.channels.get(ch)
+            if sc is None:
+                if m.name == "channel.close_ok":
+                    return
+                raise ConnError(codec.CHANNEL_ERROR, f"channel {ch} not open", m.ids)
+            if m.name in codec.CONTENT_METHODS:
+                sc.pending = (m, None, 0, [])
+                return
+            self._on_chan_method(c, sc, m)
+        elif ftype == codec.FRAME_HEADER:
+            sc = c.channels.get(ch)
+            if sc is None or sc.pending is None:
+                raise ConnError(codec.UNEXPECTED_FRAME, "unexpected header frame")
+            _cid, size, props = codec.decode_header(payload)
+            sc.pending = (sc.pending[0], props, size, [])
+            if size == 0:
+                self._publish(c, sc)
+        elif ftype == codec.FRAME_BODY:
+            sc = c.channels.get(ch)
+            if sc is None or sc.pending is None or sc.pending[1] is None:
+                raise ConnError(codec.UNEXPECTED_FRAME, "unexpected body frame")
+            sc.pending[3].append(payload)
+            if sum(len(p) for p in sc.pending[3]) >= sc.pending[2]:
+                self._publish(c, sc)
+
+    def _on_conn_method(self, c: _ServerConn, m: Method) -> None:
+        n = m.name
+        if n == "connection.start_ok":
+            c.client_properties = m.client_properties
+            resp = m.response
+            if m.mechanism == "PLAIN":
+                parts = resp.split(b"\x00")
+                user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else ("", "")
+            else:  # AMQPLAIN: a field table without its length prefix
+                t = codec._Reader(struct_pack_len(resp)).table()
+                user, pw = str(t.get("LOGIN", "")), str(t.get("PASSWORD", ""))
+            if self.username is not None and (user != self.username or pw != (self.password or "")):
+                raise ConnError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - Login was refused", m.ids)
+            c.user = user
+            c.send_method(0, Method("connection.tune", {"channel_max": 2047, "frame_max": self.frame_max,
+                                                        "heartbeat": self.heartbeat}))
+        elif n == "connection.tune_ok":
+            c.frame_max = m.frame_max or self.frame_max
+        elif n == "connection.open":
+            c.open = True
+            c.send_method(0, Method("connection.open_ok"))
+            if self.blocked:
+                c.send_method(0, Method("connection.blocked", {"reason": "low on memory"}))
+        elif n == "connection.close":
+            c.send_method(0, Method("connection.close_ok"))
+            c.closed = True
+        elif n == "connection.close_ok":
+            c.closed = True
+
+    def _on_chan_method(self, c: _ServerConn, ch: _ServerChannel, m: Method) -> None:
+        n = m.name
+        a = m.args
+        ok = lambda name, **kw: c.send_method(ch.id, Method(name, kw))  # noqa: E731
+        if n == "channel.close":
+            c.channels.pop(ch.id, None)
+            self._close_channel(ch)
+            ok("channel.close_ok")
+        elif n == "channel.flow":
+            ch.flow = a["active"]
+            ok("channel.flow_ok", active=ch.flow)
+            for cons in ch.consumers.values():
+                self._dispatch(cons.queue)
+        elif n == "basic.qos":
+            if a["global_"]:
+                ch.prefetch_channel = a["prefetch_count"]
+            else:
+                ch.prefetch_consumer = a["prefetch_count"]
+            ok("basic.qos_ok")
+        elif n == "exchange.declare":
+            self._exchange_declare(m)
+            if not a["nowait"]:
+                ok("exchange.declare_ok")
+        elif n == "exchange.delete":
+            if a["exchange"] not in self.exchanges:
+                raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{a['exchange']}'", m.ids)
+            self.exchanges.pop(a["exchange"])
+            if not a["nowait"]:
+                ok("exchange.delete_ok")
+        elif n == "queue.declare":
+            q = self._queue_declare(c, m)
+            if not a["nowait"]:
+                ok("queue.declare_ok", queue=q.name, message_count=len(q.messages), consumer_count=len(q.consumers))
+        elif n == "queue.bind":
+            q = self._get_queue(a["queue"], m)
+            ex = self.exchanges.get(a["exchange"])
+            if ex is None:
+                raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{a['exchange']}'", m.ids)
+            b = (q.name, a["routing_key"], a["arguments"] or {})
+            if b not in ex.bindings:
+                ex.bindings.append(b)
+            if not a["nowait"]:
+                ok("queue.bind_ok")
+        elif n == "queue.unbind":
+            ex = self.exchanges.get(a["exchange"])
+            if ex is not None:
+                ex.bindings = [b for b in ex.bindings if not (b[0] == a["queue"] and b[1] == a["routing_key"])]
+            ok("queue.unbind_ok")
+        elif n == "queue.purge":
+            q = self._get_queue(a["queue"], m)
+            cnt = len(q.messages)
+            q.messages.clear()
+            if not a["nowait"]:
+                ok("queue.purge_ok", message_count=cnt)
+        elif n == "queue.delete":
+            q = self._get_queue(a["queue"], m)
+            cnt = len(q.messages)
+            for cons in list(q.consumers):
+                cons.ch.conn.send_method(cons.ch.id, Method("basic.cancel", {"consumer_tag": cons.tag}))
+                self._remove_consumer(cons)
+            self.queues.pop(q.name, None)
+            for ex in self.exchanges.values():
+                ex.bindings = [b for b in ex.bindings if b[0] != q.name]
+            if not a["nowait"]:
+                ok("queue.delete_ok", message_count=cnt)
+        elif n == "basic.consume":
+            q = self._get_queue(a["queue"], m)
+            if a["exclusive"] and q.consumers:
+                raise ChannelError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - queue in use", m.ids)
+            tag = a["consumer_tag"] or f"amq.ctag-{next(self._ctag)}"
+            if tag in ch.consumers:
+                raise ConnError(codec.NOT_ALLOWED, "NOT_ALLOWED - attempt to reuse consumer tag", m.ids)
+            cons = _Consumer(ch, tag, q, a["no_ack"], ch.prefetch_consumer)
+            ch.consumers[tag] = cons
+            q.consumers.append(cons)
+            if not a["nowait"]:
+                ok("basic.consume_ok", consumer_tag=tag)
+            self._dispatch(q)
+        elif n == "basic.cancel":
+            cons = ch.consumers.get(a["consumer_tag"])
+            if cons is not None:
+                self._remove_consumer(cons)
+            if not a["nowait"]:
+                ok("basic.cancel_ok", consumer_tag=a["consumer_tag"])
+        elif n in ("basic.ack", "basic.nack", "basic.reject"):
+            self._settle(ch, m)
+        elif n == "basic.get":
+            q = self._get_queue(a["queue"], m)
+            if not q.messages:
+                ok("basic.get_empty")
+            else:
+                msg = q.messages.popleft()
+                tag = next(ch.tags)
+                if not a["no_ack"]:
+                    ch.unacked[tag] = (msg, q, None)
+                c.send(b"".join(codec.content_frames(ch.id, Method("basic.get_ok", {
+                    "delivery_tag": tag, "redelivered": msg.redelivered, "exchange": msg.exchange,
+                    "routing_key": msg.routing_key, "message_count": len(q.messages)}), msg.body, msg.props,
+                    c.frame_max)))
+        elif n in ("basic.recover", "basic.recover_async"):
+            self._close_channel_unacked_only(ch)
+            if n == "basic.recover":
+                ok("basic.recover_ok")
+        elif n == "confirm.select":
+            ch.confirm = True
+            if not a["nowait"]:
+                ok("confirm.select_ok")
+        else:
+            raise ConnError(codec.NOT_IMPLEMENTED, f"method {n} not implemented", m.ids)
+
+    def _close_channel_unacked_only(self, ch: _ServerChannel) -> None:
+        for tag in sorted(ch.unacked, reverse=True):
+            msg, q, cons = ch.unacked.pop(tag)
+            if cons:
+                cons.unacked -= 1
+            msg.redelivered = True
+            q.messages.appendleft(msg)
+            self._dispatch(q)
+
+    # ------------------------------------------------------------ entities
+    def _exchange_declare(self, m: Method) -> None:
+        a = m.args
+        name = a["exchange"]
+        ex = self.exchanges.get(name)
+        if a["passive"]:
+            if ex is None:
+                raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{name}'", m.ids)
+            return
+        if name.startswith("amq.") and ex is None:
+            raise ChannelError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - reserved name", m.ids)
+        if a["type"] not in ("direct", "fanout", "topic", "headers"):
+            raise ConnError(codec.COMMAND_INVALID, f"COMMAND_INVALID - unknown exchange type '{a['type']}'", m.ids)
+        if ex is not None:
+            if ex.type != a["type"] or ex.durable != a["durable"] or ex.auto_delete != a["auto_delete"] or \
+                    ex.internal != a["internal"]:
+                raise ChannelError(codec.PRECONDITION_FAILED,
+                                   f"PRECONDITION_FAILED - inequivalent arg for exchange '{name}'", m.ids)
+            return
+        self.exchanges[name] = Exchange(name, a["type"], a["durable"], a["auto_delete"], a["internal"],
+                                        a["arguments"] or {})
+
+    def _queue_declare(self, c: _ServerConn, m: Method) -> Queue:
+        a = m.args
+        name = a["queue"] or f"amq.gen-{next(self._qname)}"
+        q = self.queues.get(name)
+        if a["passive"]:
+            if q is None:
+                raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no queue '{name}'", m.ids)
+            return q
+        if q is not None:
+            if q.exclusive and q.owner is not c:
+                raise ChannelError(codec.RESOURCE_LOCKED, "RESOURCE_LOCKED - exclusive queue", m.ids)
+            if q.durable != a["durable"] or q.auto_delete != a["auto_delete"] or \
+                    (q.arguments or {}) != (a["arguments"] or {}):
+                raise ChannelError(codec.PRECONDITION_FAILED,
+                                   f"PRECONDITION_FAILED - inequivalent arg for queue '{name}'", m.ids)
+            return q
+        q = Queue(name, a["durable"], a["exclusive"], a["auto_delete"], a["arguments"] or {},
+                  owner=c if a["exclusive"] else None)
+        self.queues[name] = q
+        return q
+
+    def _get_queue(self, name: str, m: Method) -> Queue:
+        q = self.queues.get(name)
+        if q is None:
+            raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no queue '{name}'", m.ids)
+        return q
+
+    # ------------------------------------------------------------ messages
+    def _route(self, msg: QMsg) -> int:
+        ex = self.exchanges.get(msg.exchange)
+        if ex is None:
+            return -1
+        targets: list[str] = []
+        if msg.exchange == "":
+            if msg.routing_key in self.queues:
+                targets = [msg.routing_key]
+        else:
+            for qname, rk, _args in ex.bindings:
+                if ex.type == "fanout" or (ex.type == "direct" and rk == msg.routing_key) or \
+                        (ex.type == "topic" and _topic_match(rk, msg.routing_key)):
+                    if qname not in targets:
+                        targets.append(qname)
+        for t in targets:
+            q = self.queues.get(t)
+            if q is None:
+                continue
+            q.messages.append(QMsg(msg.body, msg.props, msg.exchange, msg.routing_key))
+            self._dispatch(q)
+        self.stats["routed"] += len(targets)
+        return len(targets)
+
+    def _publish(self, c: _ServerConn, ch: _ServerChannel) -> None:
+        assert ch.pending is not None
+        m, props, _size, parts = ch.pending
+        ch.pending = None
+        msg = QMsg(b"".join(parts), props or Properties(), m.exchange, m.routing_key)
+        self.stats["published"] += 1
+        if ch.confirm:
+            ch.pub_seq += 1
+        if m.exchange not in self.exchanges:
+            raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{m.exchange}'", (60, 40))
+        if ch.confirm and self.fail_publishes > 0:
+            self.fail_publishes -= 1
+            c.send_method(ch.id, Method("basic.nack", {"delivery_tag": ch.pub_seq}))
+            return
+        self.published.append(msg)
+        n = self._route(msg)
+        if n == 0 and m.mandatory:
+            c.send(b"".join(codec.content_frames(ch.id, Method("basic.return", {
+                "reply_code": codec.NO_ROUTE, "reply_text": "NO_ROUTE", "exchange": m.exchange,
+                "routing_key": m.routing_key}), msg.body, msg.props, c.frame_max)))
+        if ch.confirm:
+            c.send_method(ch.id, Method("basic.ack", {"delivery_tag": ch.pub_seq}))
+
+    def _can_deliver(self, cons: _Consumer) -> bool:
+        ch = cons.ch
+        if ch.conn.closed or not ch.flow:
+            return False
+        if cons.no_ack:
+            return True
+        if ch.prefetch_channel and ch.channel_unacked() >= ch.prefetch_channel:
+            return False
+        if cons.prefetch and cons.unacked >= cons.prefetch:
+            return False
+        return True
+
+    def _dispatch(self, q: Queue) -> None:
+        while q.messages and q.consumers:
+            n = len(q.consumers)
+            chosen = None
+            for i in range(n):
+                cons = q.consumers[(q.rr + i) % n]
+                if self._can_deliver(cons):
+                    chosen = cons
+                    q.rr = (q.rr + i + 1) % n
+                    break
+            if chosen is None:
+                return
+            msg = q.messages.popleft()
+            ch = chosen.ch
+            tag = next(ch.tags)
+            if not chosen.no_ack:
+                ch.unacked[tag] = (msg, q, chosen)
+                chosen.unacked += 1
+            q.delivered_total += 1
+            ch.conn.send(b"".join(codec.content_frames(ch.id, Method("basic.deliver", {
+                "consumer_tag": chosen.tag, "delivery_tag": tag, "redelivered": msg.redelivered,
+                "exchange": msg.exchange, "routing_key": msg.routing_key}), msg.body, msg.props,
+                ch.conn.frame_max)))
+
+    def _settle(self, ch: _ServerChannel, m: Method) -> None:
+        tag = m.delivery_tag
+        multiple = m.args.get("multiple", False)
+        requeue = m.args.get("requeue", m.name != "basic.ack")
+        if m.name == "basic.ack":
+            requeue = False
+        if multiple:
+            tags = sorted(t for t in ch.unacked if t <= tag) if tag else sorted(ch.unacked)
+        else:
+            if tag not in ch.unacked:
+                raise ChannelError(codec.PRECONDITION_FAILED, f"PRECONDITION_FAILED - unknown delivery tag {tag}",
+                                   m.ids)
+            tags = [tag]
+        touched: set[str] = set()
+        for t in tags:
+            msg, q, cons = ch.unacked.pop(t)
+            if cons is not None:
+                cons.unacked -= 1
+            touched.add(q.name)
+            if m.name == "basic.ack":
+                self.stats["acked"] += 1
+                continue
+            if requeue:
+                msg.redelivered = True
+                q.messages.appendleft(msg)
+                self.stats["requeued"] += 1
+            else:
+                self.stats["dead"] += 1
+                self._dead_letter(q, msg)
+        for name in touched:
+            if name in self.queues:
+                self._dispatch(self.queues[name])
+        for cons in ch.consumers.values():
+            self._dispatch(cons.queue)
+
+    def _dead_letter(self, q: Queue, msg: QMsg) -> None:
+        dlx = q.arguments.get("x-dead-letter-exchange")
+        if dlx is None:
+            return
+        rk = q.arguments.get("x-dead-letter-routing-key", msg.routing_key)
+        props = msg.props
+        hdrs = dict(props.headers or {})
+        hdrs["x-death"] = [{"queue": q.name, "reason": "rejected", "exchange": msg.exchange,
+                            "routing-keys": [msg.routing_key], "count": 1}]
+        new_props = Properties(**{**props.__dict__, "headers": hdrs})
+        self._route(QMsg(msg.body, new_props, dlx, rk))
+
+
+def struct_pack_len(b: bytes) -> bytes:
+    import struct
+    return struct.pack(">I", len(b)) + b
+
+
+async def run_broker(host: str = "127.0.0.1", port: int = 5672) -> None:  # pragma: no cover - manual use
+    b = await Broker(host, port).start()
+    print(f"fake broker listening on {b.endpoint}", flush=True)
+    await asyncio.Event().wait()
