@@ -303,7 +303,7 @@ std::string hex(const std::string& d) {
 //   prev_sig + "\n" + hex(sha256("")) + "\n" + hex(sha256(chunk))
 std::vector<std::string> chunk_signatures(const std::string& signing_key, const std::string& amzdate,
                                           const std::string& scope, const std::string& seed_sig,
-                                          const py::buffer& data, size_t chunk_size) {
+                                          const py::buffer& data, size_t chunk_size, bool include_final) {
   py::buffer_info bi;
   BufView v = view_of(data, bi);
   std::vector<std::string> sigs;
@@ -321,6 +321,7 @@ std::vector<std::string> chunk_signatures(const std::string& signing_key, const 
       sigs.push_back(prev);
       off += len;
       if (len == 0) break;
+      if (off >= v.len && !include_final) break;
     }
   }
   return sigs;
@@ -355,6 +356,6 @@ PYBIND11_MODULE(_hash_host, m) {
         py::arg("threads") = 0, py::arg("kind") = "sha1");
   m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) { return py::bytes(hmac256(k, msg)); });
   m.def("chunk_signatures", &chunk_signatures, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
-        py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"));
+        py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true);
   m.def("default_threads", &default_threads);
 }

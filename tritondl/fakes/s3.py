@@ -1,0 +1,338 @@
+"""In-process S3 server (aiohttp.web) that VERIFIES SigV4 — the MinIO/S3
+stand-in for tests, smoke and bench (the reference had none).
+
+Supports: HEAD/PUT bucket (path-style and virtual-host style), PUT object
+(plain, UNSIGNED-PAYLOAD, signed SHA-256, and aws-chunked streaming with
+per-chunk signature verification), multipart (initiate / upload part /
+complete / abort), GET/HEAD/DELETE object, ListObjectsV2.
+
+Storage modes: ``memory`` (default), ``disk`` (under ``root``) or
+``discard`` (keep only size + ETag — for throughput benches).
+Fault injection: :meth:`fail_next` returns 5xx for the next N requests.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import hmac
+import itertools
+import os
+import re
+from dataclasses import dataclass, field
+from urllib.parse import parse_qsl, unquote
+
+from aiohttp import web
+
+from ..s3 import sigv4
+
+_AUTH_RE = re.compile(r"AWS4-HMAC-SHA256 Credential=([^/]+)/([^,]+), *SignedHeaders=([^,]+), *Signature=([0-9a-f]+)")
+
+
+@dataclass
+class Obj:
+    size: int
+    etag: str
+    data: bytes | None = None
+    path: str | None = None
+    content_type: str = ""
+
+
+@dataclass
+class Upload:
+    bucket: str
+    key: str
+    parts: dict = field(default_factory=dict)  # n -> Obj
+
+
+def _xml_err(status: int, code: str, msg: str) -> web.Response:
+    body = f"<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>{code}</Code><Message>{msg}</Message></Error>"
+    return web.Response(status=status, body=body.encode(), content_type="application/xml")
+
+
+class FakeS3:
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, *, access_key: str | None = None,
+                 secret_key: str | None = None, region: str = "us-east-1", store: str = "memory",
+                 root: str | None = None) -> None:
+        self.host, self.port = host, port
+        self.access_key, self.secret_key = access_key, secret_key
+        self.region = region
+        self.store = store
+        self.root = root
+        self.buckets: dict[str, dict[str, Obj]] = {}
+        self.uploads: dict[str, Upload] = {}
+        self._ids = itertools.count(1)
+        self._fail = 0
+        self._fail_status = 503
+        self.requests: list[tuple[str, str]] = []
+        self.bytes_received = 0
+        self._runner: web.AppRunner | None = None
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self) -> "FakeS3":
+        app = web.Application(client_max_size=1 << 40)
+        app.router.add_route("*", "/{tail:.*}", self._handle)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        return self
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+    @property
+    def endpoint(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    def fail_next(self, n: int, status: int = 503) -> None:
+        self._fail, self._fail_status = n, status
+
+    def object_bytes(self, bucket: str, key: str) -> bytes:
+        o = self.buckets[bucket][key]
+        if o.data is not None:
+            return o.data
+        if o.path is not None:
+            with open(o.path, "rb") as f:
+                return f.read()
+        raise KeyError("object content discarded")
+
+    # ------------------------------------------------------------ routing
+    def _split(self, request: web.Request) -> tuple[str, str]:
+        raw = request.raw_path.split("?", 1)[0]
+        host = request.headers.get("Host", "").split(":")[0]
+        if host.count(".") and not re.match(r"^\d+\.\d+\.\d+\.\d+$", host) and host not in ("localhost",) \
+                and not host.startswith(self.host):
+            bucket = host.split(".", 1)[0]
+            return bucket, unquote(raw[1:])
+        parts = raw[1:].split("/", 1)
+        bucket = unquote(parts[0]) if parts and parts[0] else ""
+        key = unquote(parts[1]) if len(parts) > 1 else ""
+        return bucket, key
+
+    def _verify(self, request: web.Request) -> tuple[bytes, str, str, str] | web.Response | None:
+        """Return (signing_key, seed_sig, amzdate, scope) for signed requests,
+        None for allowed anonymous ones, or an error response."""
+        auth = request.headers.get("Authorization")
+        if auth is None:
+            if self.access_key is None:
+                return None
+            return _xml_err(403, "AccessDenied", "Anonymous access denied")
+        m = _AUTH_RE.match(auth)
+        if not m:
+            return _xml_err(400, "AuthorizationHeaderMalformed", "bad Authorization header")
+        akid, scope_rest, signed_headers, sig = m.groups()
+        if self.access_key is not None and akid != self.access_key:
+            return _xml_err(403, "InvalidAccessKeyId", "unknown access key")
+        secret = self.secret_key or ""
+        date, region, service, _term = scope_rest.split("/")
+        amzdate = request.headers.get("x-amz-date", "")
+        hdrs = {}
+        for h in signed_headers.split(";"):
+            v = request.headers.get(h)
+            if v is None:
+                return _xml_err(400, "SignatureDoesNotMatch", f"signed header {h} missing")
+            hdrs[h] = v
+        query = parse_qsl(request.query_string, keep_blank_values=True)
+        phash = request.headers.get("x-amz-content-sha256", "")
+        raw_path = request.raw_path.split("?", 1)[0]
+        s = sigv4.sign(request.method, raw_path, query, hdrs, phash, akid, secret, region, amzdate,
+                       service=service, path_is_encoded=True)
+        if not hmac.compare_digest(s.signature, sig):
+            return _xml_err(403, "SignatureDoesNotMatch",
+                            "The request signature we calculated does not match the signature you provided.")
+        return s.key, sig, amzdate, s.scope
+
+    async def _read_body(self, request: web.Request, auth) -> bytes:
+        phash = request.headers.get("x-amz-content-sha256", sigv4.UNSIGNED_PAYLOAD)
+        if phash == sigv4.STREAMING_PAYLOAD:
+            if not isinstance(auth, tuple):
+                raise _BadReq(400, "InvalidRequest", "streaming payload needs a signature")
+            return await self._read_chunked(request, auth)
+        data = await request.read()
+        self.bytes_received += len(data)
+        if phash not in (sigv4.UNSIGNED_PAYLOAD, "") and auth is not None:
+            if hashlib.sha256(data).hexdigest() != phash:
+                raise _BadReq(400, "XAmzContentSHA256Mismatch", "payload hash mismatch")
+        return data
+
+    async def _read_chunked(self, request: web.Request, auth) -> bytes:
+        key, prev, amzdate, scope = auth
+        decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
+        out = bytearray()
+        rd = request.content
+        empty = hashlib.sha256(b"").hexdigest()
+        while True:
+            line = await rd.readline()
+            self.bytes_received += len(line)
+            m = re.match(rb"^([0-9a-fA-F]+);chunk-signature=([0-9a-f]{64})\r\n$", line)
+            if not m:
+                raise _BadReq(400, "IncompleteBody", "malformed aws-chunked framing")
+            n = int(m.group(1), 16)
+            data = await rd.readexactly(n) if n else b""
+            crlf = await rd.readexactly(2)
+            self.bytes_received += n + 2
+            if crlf != b"\r\n":
+                raise _BadReq(400, "IncompleteBody", "chunk not terminated")
+            sts = "\n".join(["AWS4-HMAC-SHA256-PAYLOAD", amzdate, scope, prev, empty,
+                             hashlib.sha256(data).hexdigest()])
+            want = hmac.new(key, sts.encode(), hashlib.sha256).hexdigest()
+            if want != m.group(2).decode():
+                raise _BadReq(403, "SignatureDoesNotMatch", "chunk signature mismatch")
+            prev = want
+            if n == 0:
+                break
+            out += data
+        if decoded_len >= 0 and decoded_len != len(out):
+            raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
+        return bytes(out)
+
+    def _save(self, data: bytes, content_type: str = "") -> Obj:
+        etag = hashlib.md5(data).hexdigest()
+        if self.store == "discard":
+            return Obj(len(data), etag, content_type=content_type)
+        if self.store == "disk":
+            assert self.root
+            p = os.path.join(self.root, f"obj-{next(self._ids)}")
+            with open(p, "wb") as f:
+                f.write(data)
+            return Obj(len(data), etag, path=p, content_type=content_type)
+        return Obj(len(data), etag, data=data, content_type=content_type)
+
+    async def _handle(self, request: web.Request) -> web.StreamResponse:
+        self.requests.append((request.method, request.raw_path))
+        if self._fail > 0:
+            self._fail -= 1
+            await request.read()
+            return _xml_err(self._fail_status, "ServiceUnavailable", "injected failure")
+        auth = self._verify(request)
+        if isinstance(auth, web.Response):
+            await request.read()
+            return auth
+        bucket, key = self._split(request)
+        q = dict(parse_qsl(request.query_string, keep_blank_values=True))
+        try:
+            if not key:
+                return await self._bucket_op(request, bucket, q, auth)
+            return await self._object_op(request, bucket, key, q, auth)
+        except _BadReq as e:
+            return _xml_err(e.status, e.code, e.msg)
+
+    async def _bucket_op(self, request: web.Request, bucket: str, q: dict, auth) -> web.StreamResponse:
+        m = request.method
+        if m == "HEAD":
+            return web.Response(status=200 if bucket in self.buckets else 404)
+        if m == "PUT":
+            await self._read_body(request, auth)
+            if bucket in self.buckets:
+                return _xml_err(409, "BucketAlreadyOwnedByYou", "bucket exists")
+            self.buckets[bucket] = {}
+            return web.Response(status=200, headers={"Location": "/" + bucket})
+        if m == "GET" and bucket in self.buckets:
+            if "location" in q:
+                return web.Response(body=b"<LocationConstraint/>", content_type="application/xml")
+            prefix = q.get("prefix", "")
+            keys = sorted(k for k in self.buckets[bucket] if k.startswith(prefix))
+            items = "".join(f"<Contents><Key>{_xml_escape(k)}</Key><Size>{self.buckets[bucket][k].size}</Size>"
+                            f"<ETag>\"{self.buckets[bucket][k].etag}\"</ETag></Contents>" for k in keys)
+            body = (f"<ListBucketResult xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\"><Name>{bucket}</Name>"
+                    f"<Prefix>{prefix}</Prefix><KeyCount>{len(keys)}</KeyCount><IsTruncated>false</IsTruncated>"
+                    f"{items}</ListBucketResult>")
+            return web.Response(body=body.encode(), content_type="application/xml")
+        if bucket not in self.buckets:
+            return _xml_err(404, "NoSuchBucket", "The specified bucket does not exist")
+        return _xml_err(405, "MethodNotAllowed", m)
+
+    async def _object_op(self, request: web.Request, bucket: str, key: str, q: dict, auth) -> web.StreamResponse:
+        m = request.method
+        if bucket not in self.buckets:
+            await request.read()
+            return _xml_err(404, "NoSuchBucket", "The specified bucket does not exist")
+        objs = self.buckets[bucket]
+        if m == "PUT" and "uploadId" in q:
+            up = self.uploads.get(q["uploadId"])
+            if up is None:
+                await request.read()
+                return _xml_err(404, "NoSuchUpload", "no such upload")
+            data = await self._read_body(request, auth)
+            o = self._save(data)
+            up.parts[int(q["partNumber"])] = o
+            return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
+        if m == "PUT":
+            data = await self._read_body(request, auth)
+            o = self._save(data, request.headers.get("Content-Type", ""))
+            objs[key] = o
+            return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
+        if m == "POST" and "uploads" in q:
+            await self._read_body(request, auth)
+            uid = f"upload-{next(self._ids)}"
+            self.uploads[uid] = Upload(bucket, key)
+            body = (f"<InitiateMultipartUploadResult xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\">"
+                    f"<Bucket>{bucket}</Bucket><Key>{_xml_escape(key)}</Key><UploadId>{uid}</UploadId>"
+                    f"</InitiateMultipartUploadResult>")
+            return web.Response(body=body.encode(), content_type="application/xml")
+        if m == "POST" and "uploadId" in q:
+            body = await self._read_body(request, auth)
+            up = self.uploads.pop(q["uploadId"], None)
+            if up is None:
+                return _xml_err(404, "NoSuchUpload", "no such upload")
+            nums = [int(x) for x in re.findall(rb"<PartNumber>(\d+)</PartNumber>", body)]
+            tags = [x.decode().strip('"') for x in re.findall(rb"<ETag>([^<]*)</ETag>", body)]
+            if nums != sorted(nums) or any(up.parts.get(n) is None or up.parts[n].etag != t
+                                           for n, t in zip(nums, tags)):
+                return _xml_err(400, "InvalidPart", "parts mismatch")
+            if self.store == "memory":
+                data = b"".join(up.parts[n].data or b"" for n in nums)
+                o = self._save(data)
+            else:
+                size = sum(up.parts[n].size for n in nums)
+                o = Obj(size, "")
+                if self.store == "disk":
+                    assert self.root
+                    p = os.path.join(self.root, f"obj-{next(self._ids)}")
+                    with open(p, "wb") as f:
+                        for n in nums:
+                            with open(up.parts[n].path or "", "rb") as pf:
+                                f.write(pf.read())
+                    o.path = p
+            md5s = b"".join(bytes.fromhex(up.parts[n].etag) for n in nums)
+            o.etag = hashlib.md5(md5s).hexdigest() + f"-{len(nums)}"
+            objs[up.key] = o
+            rb = (f"<CompleteMultipartUploadResult xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\">"
+                  f"<Bucket>{bucket}</Bucket><Key>{_xml_escape(up.key)}</Key><ETag>\"{o.etag}\"</ETag>"
+                  f"</CompleteMultipartUploadResult>")
+            return web.Response(body=rb.encode(), content_type="application/xml")
+        if m == "DELETE" and "uploadId" in q:
+            self.uploads.pop(q["uploadId"], None)
+            return web.Response(status=204)
+        if m in ("GET", "HEAD"):
+            o = objs.get(key)
+            if o is None:
+                return _xml_err(404, "NoSuchKey", "The specified key does not exist.")
+            hdrs = {"ETag": f"\"{o.etag}\"", "Content-Length": str(o.size)}
+            if m == "HEAD":
+                return web.Response(status=200, headers=hdrs)
+            return web.Response(status=200, body=self.object_bytes(bucket, key), headers={"ETag": hdrs["ETag"]})
+        if m == "DELETE":
+            objs.pop(key, None)
+            return web.Response(status=204)
+        return _xml_err(405, "MethodNotAllowed", m)
+
+
+class _BadReq(Exception):
+    def __init__(self, status: int, code: str, msg: str) -> None:
+        super().__init__(msg)
+        self.status, self.code, self.msg = status, code, msg
+
+
+def _xml_escape(s: str) -> str:
+    return s.replace("&", "&amp;").replace("<", "&lt;").replace(">", "&gt;")
+
+
+async def _main() -> None:  # pragma: no cover - manual use
+    s = await FakeS3(port=9000).start()
+    print("fake s3 on", s.endpoint, flush=True)
+    await asyncio.Event().wait()

@@ -41,8 +41,10 @@ def hmac_sha256(key: bytes, msg: bytes) -> bytes:
 
 
 def chunk_signatures(signing_key: bytes, amzdate: str, scope: str, seed_signature: str, data,
-                     chunk_size: int) -> list[str]:
-    return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size)
+                     chunk_size: int, include_final: bool = True) -> list[str]:
+    """aws-chunked signature chain over ``data`` (one per ``chunk_size`` chunk,
+    plus the terminating empty chunk when ``include_final``)."""
+    return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size, include_final)
 
 
 # ----------------------------------------------------------------- GPU

@@ -1,0 +1,373 @@
+"""Async S3 client (aiohttp) with SigV4, bucket ensure, streaming PutObject
+and parallel multipart upload.
+
+Capability of the minio-go v6 calls the reference makes
+(``internal/uploader/uploader.go:43-51,64-65,89``): ``NewWithOptions{Secure,
+Creds, BucketLookupAuto}``, ``BucketExists``, ``MakeBucket``,
+``PutObjectWithContext`` (single PUT below the multipart threshold, multipart
+above it).  Memory stays O(part_size × parallel_parts) regardless of file
+size; file reads and chunk signing run in worker threads
+(the native hash module releases the GIL), so several uploads overlap.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import os
+import re
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass
+from typing import AsyncIterator
+from urllib.parse import urlparse
+
+import aiohttp
+from multidict import CIMultiDict
+from yarl import URL
+
+from ..ops import hashing
+from ..utils.backoff import ExponentialBackoff
+from ..utils.log import log
+from . import sigv4
+from .credentials import Chain, Provider, Value, default_chain
+
+S3_NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
+_DNS_BUCKET = re.compile(r"^[a-z0-9][a-z0-9.-]{1,61}[a-z0-9]$")
+
+
+class S3Error(Exception):
+    def __init__(self, status: int, code: str = "", message: str = "", resource: str = "") -> None:
+        super().__init__(f"S3 {status} {code}: {message} ({resource})")
+        self.status, self.code, self.message, self.resource = status, code, message, resource
+
+
+def _parse_error(status: int, body: bytes, resource: str) -> S3Error:
+    code = msg = ""
+    try:
+        root = ET.fromstring(body)
+        code = (root.findtext("Code") or "")
+        msg = (root.findtext("Message") or "")
+    except ET.ParseError:
+        msg = body[:200].decode(errors="replace")
+    return S3Error(status, code, msg, resource)
+
+
+@dataclass
+class Endpoint:
+    host: str           # host[:port] as sent in the Host header
+    secure: bool
+
+    @classmethod
+    def parse(cls, s3_endpoint: str) -> "Endpoint":
+        """Reference parsing of ``S3_ENDPOINT`` (``uploader.go:25-40``): TLS iff
+        scheme is https; keep hostname[:port]."""
+        if s3_endpoint and "://" not in s3_endpoint:
+            s3_endpoint = "http://" + s3_endpoint  # bare host[:port] (Go would yield an empty host)
+        u = urlparse(s3_endpoint)
+        host = u.hostname or ""
+        if u.port:
+            host = f"{host}:{u.port}"
+        return cls(host, u.scheme == "https")
+
+    @property
+    def base(self) -> str:
+        return ("https://" if self.secure else "http://") + self.host
+
+
+class S3Client:
+    def __init__(self, endpoint: Endpoint | str, creds: Provider | None = None, *, region: str = "us-east-1",
+                 lookup: str = "auto", payload_mode: str = "auto", part_size: int = 64 << 20,
+                 multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
+                 io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None) -> None:
+        self.ep = Endpoint.parse(endpoint) if isinstance(endpoint, str) else endpoint
+        self.creds = creds or default_chain()
+        self.region = region
+        self.lookup = lookup
+        self.payload_mode = payload_mode
+        self.part_size = max(part_size, 5 << 20)
+        self.multipart_threshold = multipart_threshold
+        self.parallel_parts = max(1, parallel_parts)
+        self.max_retries = max_retries
+        self.io_block = max(io_block, sigv4.STREAM_CHUNK)
+        self._session = session
+        self._own_session = session is None
+
+    async def _sess(self) -> aiohttp.ClientSession:
+        if self._session is None or self._session.closed:
+            self._session = aiohttp.ClientSession(
+                timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=300),
+                connector=aiohttp.TCPConnector(limit=64), auto_decompress=False)
+            self._own_session = True
+        return self._session
+
+    async def close(self) -> None:
+        if self._own_session and self._session is not None:
+            await self._session.close()
+            self._session = None
+
+    # ------------------------------------------------------------ helpers
+    def _virtual(self, bucket: str) -> bool:
+        if self.lookup == "dns":
+            return True
+        if self.lookup == "path" or not bucket:
+            return False
+        host = self.ep.host.split(":")[0]
+        # BucketLookupAuto: virtual-host style for AWS / Aliyun style endpoints only
+        return (host.endswith("amazonaws.com") or host.endswith("aliyuncs.com")) and \
+            bool(_DNS_BUCKET.match(bucket)) and "." not in bucket
+
+    def _target(self, bucket: str, key: str = "") -> tuple[str, str]:
+        ekey = sigv4.uri_encode(key, encode_slash=False) if key else ""
+        if self._virtual(bucket):
+            return f"{bucket}.{self.ep.host}", "/" + ekey
+        path = "/" + bucket if bucket else "/"
+        if key:
+            path += "/" + ekey
+        return self.ep.host, path
+
+    def _payload_mode(self) -> str:
+        if self.payload_mode != "auto":
+            return self.payload_mode
+        return "unsigned" if self.ep.secure else "streaming"
+
+    def _creds(self) -> Value:
+        return self.creds.retrieve()
+
+    async def _do(self, method: str, bucket: str, key: str = "", query: dict | None = None,
+                  headers: dict | None = None, body: bytes | None = None, *, body_factory=None,
+                  payload_hash: str | None = None, expect: tuple[int, ...] = (200,),
+                  retry: bool = True) -> tuple[int, dict, bytes]:
+        """One signed request with retries on connection errors / 5xx."""
+        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
+        attempt = 0
+        while True:
+            attempt += 1
+            host, path = self._target(bucket, key)
+            amzdate, _ = sigv4.amz_dates()
+            hdrs = {"host": host, "x-amz-date": amzdate}
+            hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
+            cred = self._creds()
+            data = body
+            if body_factory is not None:
+                data, phash, extra = await body_factory(cred, amzdate, host, path, query, hdrs)
+                hdrs.update(extra)
+            else:
+                phash = payload_hash or (hashing.digest("sha256", body or b"").hex() if body is not None
+                                         else sigv4.EMPTY_SHA256)
+                if body is not None:
+                    hdrs["content-length"] = str(len(body))
+            hdrs["x-amz-content-sha256"] = phash
+            if not cred.anonymous:
+                if cred.session_token:
+                    hdrs["x-amz-security-token"] = cred.session_token
+                signed = sigv4.sign(method, path, query, hdrs, phash, cred.access_key_id, cred.secret_access_key,
+                                    self.region, amzdate, path_is_encoded=True)
+                if callable(getattr(data, "bind_seed", None)):
+                    data.bind_seed(signed)
+                hdrs["authorization"] = signed.authorization
+            url = URL(f"{'https' if self.ep.secure else 'http'}://{host}{path}" +
+                      (("?" + sigv4.canonical_query(query)) if query else ""), encoded=True)
+            send_headers = {k: v for k, v in hdrs.items() if k != "host"}
+            send_headers["Host"] = host
+            try:
+                sess = await self._sess()
+                payload = data.stream() if hasattr(data, "stream") else data
+                async with sess.request(method, url, headers=send_headers, data=payload,
+                                        skip_auto_headers=("Content-Type",)) as r:
+                    rbody = await r.read()
+                    if r.status in expect:
+                        return r.status, CIMultiDict(r.headers), rbody
+                    err = _parse_error(r.status, rbody, f"{method} {path}")
+                    if r.status < 500 or not retry or attempt > self.max_retries:
+                        raise err
+            except (aiohttp.ClientError, asyncio.TimeoutError, ConnectionError) as e:
+                if not retry or attempt > self.max_retries:
+                    raise S3Error(0, "ConnectionError", str(e), f"{method} {path}") from e
+                err = e  # type: ignore[assignment]
+            d = pol.next_delay() or 1.0
+            log.with_fields(error=str(err), attempt=attempt).warn("s3 request failed; retrying in %.2fs", d)
+            await asyncio.sleep(d)
+
+    # ------------------------------------------------------------ buckets
+    async def bucket_exists(self, bucket: str) -> bool:
+        try:
+            await self._do("HEAD", bucket, expect=(200,))
+            return True
+        except S3Error as e:
+            if e.status == 404 or e.code == "NoSuchBucket":
+                return False
+            raise
+
+    async def make_bucket(self, bucket: str, location: str = "") -> None:
+        body = None
+        if location and location != "us-east-1":
+            body = (f'<CreateBucketConfiguration xmlns="http://s3.amazonaws.com/doc/2006-03-01/">'
+                    f"<LocationConstraint>{location}</LocationConstraint></CreateBucketConfiguration>").encode()
+        await self._do("PUT", bucket, body=body if body is not None else b"", expect=(200,))
+
+    # ------------------------------------------------------------ objects
+    async def put_object(self, bucket: str, key: str, src: str | bytes, size: int | None = None,
+                         content_type: str = "application/octet-stream") -> str:
+        """Upload a file path (streamed) or bytes; returns the ETag."""
+        if size is None:
+            size = len(src) if isinstance(src, (bytes, bytearray)) else os.path.getsize(src)
+        if size >= self.multipart_threshold and size > self.part_size:
+            return await self._put_multipart(bucket, key, src, size, content_type)
+        return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type})
+
+    async def _put_range(self, bucket: str, key: str, src: str | bytes, offset: int, length: int,
+                         headers: dict, query: dict | None = None) -> str:
+        mode = self._payload_mode()
+        factory = _BodyFactory(self, src, offset, length, mode)
+        _st, rh, _b = await self._do("PUT", bucket, key, query=query, headers=headers, body_factory=factory)
+        return rh.get("ETag", "").strip('"')
+
+    async def _put_multipart(self, bucket: str, key: str, src: str | bytes, size: int, content_type: str) -> str:
+        _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
+                                       headers={"content-type": content_type}, body=b"")
+        root = ET.fromstring(body)
+        upload_id = root.findtext(f"{S3_NS}UploadId") or root.findtext("UploadId") or ""
+        if not upload_id:
+            raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
+        nparts = (size + self.part_size - 1) // self.part_size
+        etags: list[str] = [""] * nparts
+        sem = asyncio.Semaphore(self.parallel_parts)
+
+        async def one(i: int) -> None:
+            async with sem:
+                off = i * self.part_size
+                ln = min(self.part_size, size - off)
+                etags[i] = await self._put_range(bucket, key, src, off, ln, {},
+                                                 query={"partNumber": str(i + 1), "uploadId": upload_id})
+        try:
+            await asyncio.gather(*(one(i) for i in range(nparts)))
+            xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
+                          for i, e in enumerate(etags))
+            cbody = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
+            _st, _h, rb = await self._do("POST", bucket, key, query={"uploadId": upload_id}, body=cbody)
+            if b"<Error>" in rb:
+                raise _parse_error(200, rb, f"complete {key}")
+            r = ET.fromstring(rb)
+            return (r.findtext(f"{S3_NS}ETag") or r.findtext("ETag") or "").strip('"')
+        except BaseException:
+            try:
+                await self._do("DELETE", bucket, key, query={"uploadId": upload_id}, expect=(204, 200),
+                               retry=False)
+            except Exception:
+                pass
+            raise
+
+    async def get_object(self, bucket: str, key: str) -> bytes:
+        _st, _h, b = await self._do("GET", bucket, key)
+        return b
+
+    async def stat_object(self, bucket: str, key: str) -> dict:
+        _st, h, _b = await self._do("HEAD", bucket, key)
+        return h
+
+    async def delete_object(self, bucket: str, key: str) -> None:
+        await self._do("DELETE", bucket, key, expect=(204, 200))
+
+    async def list_objects(self, bucket: str, prefix: str = "") -> list[str]:
+        keys: list[str] = []
+        token = None
+        while True:
+            q = {"list-type": "2", "prefix": prefix}
+            if token:
+                q["continuation-token"] = token
+            _st, _h, b = await self._do("GET", bucket, query=q)
+            root = ET.fromstring(b)
+            for c in root.iter():
+                if c.tag.endswith("Contents"):
+                    k = c.find(f"{S3_NS}Key")
+                    if k is None:
+                        k = c.find("Key")
+                    keys.append(k.text or "")
+            trunc = (root.findtext(f"{S3_NS}IsTruncated") or root.findtext("IsTruncated") or "false")
+            token = root.findtext(f"{S3_NS}NextContinuationToken") or root.findtext("NextContinuationToken")
+            if trunc != "true" or not token:
+                return keys
+
+
+class _StreamBody:
+    """Payload for one PUT: plain bytes, or an aws-chunked stream signed
+    incrementally once the seed signature is known."""
+
+    def __init__(self, client: S3Client, src: str | bytes, offset: int, length: int, mode: str,
+                 scope: str = "", amzdate: str = "") -> None:
+        self.client = client
+        self.src = src
+        self.offset = offset
+        self.length = length
+        self.mode = mode
+        self.scope = scope
+        self.amzdate = amzdate
+        self.signer: sigv4.ChunkSigner | None = None
+
+    def bind_seed(self, signed: sigv4.Signed) -> None:
+        if self.mode == "streaming":
+            self.signer = sigv4.ChunkSigner(signed.key, signed.amzdate, signed.scope, signed.signature)
+
+    async def _blocks(self) -> AsyncIterator[bytes]:
+        loop = asyncio.get_running_loop()
+        blk = self.client.io_block
+        if isinstance(self.src, (bytes, bytearray, memoryview)):
+            mv = memoryview(self.src)[self.offset:self.offset + self.length]
+            for i in range(0, self.length, blk):
+                yield bytes(mv[i:i + blk])
+            return
+        fd = os.open(self.src, os.O_RDONLY)
+        try:
+            pos, end = self.offset, self.offset + self.length
+            while pos < end:
+                n = min(blk, end - pos)
+                data = await loop.run_in_executor(None, os.pread, fd, n, pos)
+                if len(data) != n:
+                    raise S3Error(0, "ShortRead", f"file shrank while uploading ({pos + len(data)} < {end})")
+                pos += n
+                yield data
+        finally:
+            os.close(fd)
+
+    async def stream(self) -> AsyncIterator[bytes]:
+        loop = asyncio.get_running_loop()
+        if self.mode != "streaming":
+            async for b in self._blocks():
+                yield b
+            return
+        assert self.signer is not None, "seed signature not bound"
+        async for b in self._blocks():
+            out = await loop.run_in_executor(None, self.signer.feed, b)
+            if out:
+                yield out
+        yield self.signer.finish()
+
+
+class _BodyFactory:
+    """Builds the body + payload hash + extra headers for each (re)try."""
+
+    def __init__(self, client: S3Client, src: str | bytes, offset: int, length: int, mode: str) -> None:
+        self.client, self.src, self.offset, self.length, self.mode = client, src, offset, length, mode
+
+    async def __call__(self, cred: Value, amzdate: str, host: str, path: str, query, hdrs):
+        mode = self.mode
+        if cred.anonymous and mode == "streaming":
+            mode = "unsigned"  # chunk signatures need credentials
+        body = _StreamBody(self.client, self.src, self.offset, self.length, mode)
+        if mode == "streaming":
+            extra = {"content-encoding": "aws-chunked", "x-amz-decoded-content-length": str(self.length),
+                     "content-length": str(sigv4.chunked_length(self.length))}
+            return body, sigv4.STREAMING_PAYLOAD, extra
+        extra = {"content-length": str(self.length)}
+        if mode == "signed":
+            loop = asyncio.get_running_loop()
+            if isinstance(self.src, (bytes, bytearray)):
+                h = hashing.digest("sha256", memoryview(self.src)[self.offset:self.offset + self.length]).hex()
+            else:
+                d = await loop.run_in_executor(None, hashing.hash_file, self.src, ["sha256"], self.offset,
+                                               self.length)
+                h = d["sha256"].hex()
+            return body, h, extra
+        return body, sigv4.UNSIGNED_PAYLOAD, extra
+
+
+__all__ = ["S3Client", "S3Error", "Endpoint", "Chain"]

@@ -1,0 +1,103 @@
+"""Media uploader — reference component C9 (``internal/uploader/uploader.go``).
+
+* ``Uploader.from_env(bucket)`` parses ``S3_ENDPOINT`` (TLS iff https,
+  host[:port]) and uses the credential chain ``[EnvGeneric, EnvAWS,
+  EnvMinio]`` with auto bucket lookup (``uploader.go:24-59``).
+* ``upload_files(media_id, base_dir, files)`` ensures the bucket exists
+  (creating it in region ``""`` if missing, ``:64-70``) and streams every file
+  to ``<mediaId>/original/<base64.StdEncoding(basename)>`` (``:72-94``) —
+  the std alphabet may contain ``/`` which creates extra key "directories";
+  kept for compatibility with the downstream converter.
+
+Deviations (defect B8): any per-file failure fails the job (the reference
+logged and skipped, and always returned nil), file handles are always
+closed, and uploads of a job's files run concurrently (bounded).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import base64
+import os
+from dataclasses import dataclass
+
+from ..utils.gocompat import go_base, go_join
+from ..utils.log import log
+from .client import S3Client, S3Error
+from .credentials import default_chain
+
+
+def object_key(media_id: str, file_name: str) -> str:
+    """``filepath.Join(mediaId, "original/", base64.StdEncoding(basename))``."""
+    enc = base64.b64encode(go_base(file_name).encode("utf-8", "surrogateescape")).decode()
+    return go_join(media_id, "original/", enc)
+
+
+@dataclass
+class UploadResult:
+    key: str
+    size: int
+    etag: str
+
+
+class UploadError(Exception):
+    pass
+
+
+class Uploader:
+    def __init__(self, bucket: str, client: S3Client, *, file_concurrency: int = 2) -> None:
+        self.bucket = bucket
+        self.client = client
+        self.file_concurrency = max(1, file_concurrency)
+        self._bucket_ok = False
+
+    @classmethod
+    def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "us-east-1",
+                 part_size: int = 64 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
+                 env=None) -> "Uploader":
+        ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
+        client = S3Client(ep, default_chain(env), region=region, part_size=part_size,
+                          multipart_threshold=multipart_threshold, parallel_parts=parallel_parts)
+        return cls(bucket, client)
+
+    async def ensure_bucket(self) -> None:
+        if self._bucket_ok:
+            return
+        try:
+            exists = await self.client.bucket_exists(self.bucket)
+        except S3Error as e:
+            log.warn("failed to check bucket: %s", e)
+            return
+        if not exists:
+            try:
+                await self.client.make_bucket(self.bucket, "")
+                log.info("created bucket")
+            except S3Error as e:
+                if e.code not in ("BucketAlreadyOwnedByYou", "BucketAlreadyExists"):
+                    log.warn("failed to create bucket: %s", e)
+                    return
+        self._bucket_ok = True
+
+    async def upload_files(self, media_id: str, base_dir: str, files: list[str]) -> list[UploadResult]:
+        await self.ensure_bucket()
+        sem = asyncio.Semaphore(self.file_concurrency)
+
+        async def one(path: str) -> UploadResult:
+            async with sem:
+                try:
+                    size = os.stat(path).st_size
+                except OSError as e:
+                    raise UploadError(f"failed to stat file {path}: {e}") from e
+                key = object_key(media_id, path)
+                log.info("starting upload of file '%s'", go_base(key))
+                try:
+                    etag = await self.client.put_object(self.bucket, key, path, size)
+                except (S3Error, OSError) as e:
+                    raise UploadError(f"failed to upload file {path}: {e}") from e
+                log.info("finished upload")
+                return UploadResult(key, size, etag)
+
+        return list(await asyncio.gather(*(one(f) for f in files)))
+
+    async def close(self) -> None:
+        await self.client.close()
