@@ -1,0 +1,163 @@
+"""Dispatcher routing (reference downloader.go:138-176 semantics) and the
+HTTP downloader against the fake origin: naming, resume, segmentation,
+retries, error surfacing."""
+
+import asyncio
+import os
+
+import pytest
+
+from tritondl.fakes.origin import Origin
+from tritondl.fetch.http import HTTPDownloader, HTTPDownloadError, filename_from_disposition
+from tritondl.fetch.registry import ClientRegister, Dispatcher, ProgressTracker, UnsupportedError
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+class FakeImpl:
+    def __init__(self, name, protocols=(), exts=()):
+        self.reg = ClientRegister(name, list(protocols), list(exts))
+        self.calls = []
+
+    def register(self):
+        return self.reg
+
+    async def download(self, base_dir, progress, url):
+        self.calls.append((base_dir, url))
+        progress(url, 50)
+        progress(url, 100)
+
+
+def test_dispatch_rules(tmp_path):
+    torrent = FakeImpl("torrent", ["magnet"], [".torrent"])
+    http = FakeImpl("http", ["http", "https"])
+    d = Dispatcher(str(tmp_path), [torrent, http])
+    assert d.select("magnet:?xt=urn:btih:abc") is torrent
+    assert d.select("http://h/x/file.torrent") is torrent        # ext wins for http(s)
+    assert d.select("https://h/movie.mkv") is http
+    assert d.select("https://h/movie.torrent?x=1") is torrent
+    with pytest.raises(UnsupportedError) as ei:
+        d.select("ftp://h/a.zip")
+    assert str(ei.value) == "unsupported fileext '.zip' or protocol 'ftp'"
+    with pytest.raises(UnsupportedError):
+        d.select("ftp://h/a.torrent")                              # ext only applies to http(s)
+    with pytest.raises(ValueError, match="invalid baseDir"):
+        Dispatcher("relative/dir", [http])
+    out = run(d.download("job1", "http://h/f.mkv"))
+    assert out == str(tmp_path / "job1") and os.path.isdir(out)
+    assert http.calls == [(out, "http://h/f.mkv")]
+    with pytest.raises(ValueError):
+        d.job_dir("../escape")
+
+
+def test_progress_tracker_drops_at_100():
+    t = ProgressTracker(interval=0)
+    from tritondl.fetch.registry import ProgressUpdate
+    t.update(ProgressUpdate("u", 10))
+    assert t.progress == {"u": 10}
+    t.update(ProgressUpdate("u", 100))
+    assert t.progress == {}
+
+
+def test_content_disposition():
+    assert filename_from_disposition('attachment; filename="a b.mkv"') == "a b.mkv"
+    assert filename_from_disposition("attachment; filename*=UTF-8''%C3%A9t%C3%A9.mp4") == "été.mp4"
+    assert filename_from_disposition('attachment; filename="../../etc/passwd"') == "passwd"
+
+
+class Sink:
+    def __init__(self):
+        self.events = []
+
+    def __call__(self, url, p):
+        self.events.append(p)
+
+
+def _dl(**kw):
+    kw.setdefault("progress_interval", 0.01)
+    return HTTPDownloader(**kw)
+
+
+def test_http_download_basic_and_skip_existing(tmp_path):
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(3_000_000)
+        url = o.add("/media/Movie%20One.mkv", data)
+        h = _dl()
+        s = Sink()
+        await h.download(str(tmp_path), s, url)
+        assert (tmp_path / "Movie One.mkv").read_bytes() == data
+        assert s.events[-1] == 100 and not (tmp_path / "Movie One.mkv.part").exists()
+        n = len(o.requests)
+        await h.download(str(tmp_path), s, url)       # already complete: only the HEAD probe
+        assert [r[0] for r in o.requests[n:]] == ["HEAD"]
+        await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_http_disposition_name_and_no_head(tmp_path):
+    async def main():
+        o = await Origin().start()
+        o.head = False
+        url = o.add("/dl", b"abc" * 1000, disposition='attachment; filename="show.s01e01.mkv"')
+        h = _dl()
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "show.s01e01.mkv").read_bytes() == b"abc" * 1000
+        await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_http_resume_after_cut(tmp_path):
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(5_000_000)
+        url = o.add("/f.mp4", data)
+        o.cut_after, o.cut_times = 1_500_000, 1
+        h = _dl(max_retries=0, write_block=256 * 1024)
+        with pytest.raises(HTTPDownloadError):
+            await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "f.mp4.part").exists() and (tmp_path / "f.mp4.part.meta").exists()
+        h2 = _dl()
+        await h2.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "f.mp4").read_bytes() == data
+        ranges = [r[2] for r in o.requests if r[0] == "GET"]
+        assert ranges[-1].startswith("bytes=") and ranges[-1] != "bytes=0-"
+        await h.close()
+        await h2.close()
+        await o.stop()
+    run(main())
+
+
+def test_http_in_process_retry_and_segments(tmp_path):
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(9_000_000)
+        url = o.add("/big.webm", data)
+        o.cut_after, o.cut_times = 700_000, 2
+        h = _dl(segments=4, segment_threshold=1_000_000, write_block=512 * 1024)
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "big.webm").read_bytes() == data
+        gets = [r for r in o.requests if r[0] == "GET"]
+        assert len({r[2] for r in gets}) >= 4
+        await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_http_errors_surface(tmp_path):
+    async def main():
+        o = await Origin().start()
+        h = _dl(max_retries=1)
+        with pytest.raises(Exception):
+            await h.download(str(tmp_path), Sink(), o.url("/missing.mkv"))
+        url = o.add("/x.mkv", b"z" * 10)
+        o.fail = 1  # HEAD gets 500 -> falls back to ranged GET probe
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "x.mkv").read_bytes() == b"z" * 10
+        await h.close()
+        await o.stop()
+    run(main())

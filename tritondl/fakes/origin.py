@@ -1,0 +1,133 @@
+"""In-process HTTP origin (aiohttp.web) with Range / HEAD / ETag /
+Content-Disposition and fault injection — the stand-in for the media
+servers the HTTP downloader talks to (the reference had no test origin).
+
+Fault knobs: ``ranges`` (advertise/honour Range), ``head`` (support HEAD),
+``cut_after`` (drop the connection after N body bytes, once per request
+count in ``cut_times``), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import os
+import re
+from dataclasses import dataclass
+
+from aiohttp import web
+
+
+@dataclass
+class Blob:
+    data: bytes | None = None
+    path: str | None = None
+    disposition: str | None = None
+    etag: str = ""
+
+    def size(self) -> int:
+        return len(self.data) if self.data is not None else os.path.getsize(self.path or "")
+
+    def read(self, start: int, end: int) -> bytes:
+        if self.data is not None:
+            return self.data[start:end]
+        with open(self.path or "", "rb") as f:
+            f.seek(start)
+            return f.read(end - start)
+
+
+class Origin:
+    def __init__(self, host: str = "127.0.0.1", port: int = 0) -> None:
+        self.host, self.port = host, port
+        self.blobs: dict[str, Blob] = {}
+        self.ranges = True
+        self.head = True
+        self.cut_after: int | None = None
+        self.cut_times = 0
+        self.fail = 0
+        self.rate: float | None = None
+        self.requests: list[tuple[str, str, str]] = []
+        self._runner: web.AppRunner | None = None
+
+    def add(self, path: str, data: bytes | None = None, *, file: str | None = None,
+            disposition: str | None = None) -> str:
+        etag = '"' + (hashlib.md5(data).hexdigest() if data is not None else f"f{os.path.getmtime(file or '')}") + '"'
+        self.blobs[path] = Blob(data, file, disposition, etag)
+        return self.url(path)
+
+    def url(self, path: str) -> str:
+        return f"http://{self.host}:{self.port}{path}"
+
+    async def start(self) -> "Origin":
+        app = web.Application()
+        app.router.add_route("*", "/{tail:.*}", self._handle)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        return self
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+    async def _handle(self, request: web.Request) -> web.StreamResponse:
+        self.requests.append((request.method, request.path, request.headers.get("Range", "")))
+        if self.fail > 0:
+            self.fail -= 1
+            return web.Response(status=500, text="injected")
+        blob = self.blobs.get(request.raw_path.split("?", 1)[0]) or self.blobs.get(request.path)
+        if blob is None:
+            return web.Response(status=404, text="not found")
+        size = blob.size()
+        hdrs = {"ETag": blob.etag, "Last-Modified": "Mon, 01 Jan 2024 00:00:00 GMT"}
+        if self.ranges:
+            hdrs["Accept-Ranges"] = "bytes"
+        if blob.disposition:
+            hdrs["Content-Disposition"] = blob.disposition
+        if request.method == "HEAD":
+            if not self.head:
+                return web.Response(status=405)
+            hdrs["Content-Length"] = str(size)
+            return web.Response(status=200, headers=hdrs)
+        if request.method != "GET":
+            return web.Response(status=405)
+        start, end, status = 0, size, 200
+        rng = request.headers.get("Range")
+        if rng and self.ranges:
+            ir = request.headers.get("If-Range")
+            if ir is None or ir == blob.etag or ir == hdrs["Last-Modified"]:
+                m = re.match(r"bytes=(\d+)-(\d*)$", rng)
+                if not m:
+                    return web.Response(status=416)
+                start = int(m.group(1))
+                end = int(m.group(2)) + 1 if m.group(2) else size
+                end = min(end, size)
+                if start >= size:
+                    return web.Response(status=416, headers={"Content-Range": f"bytes */{size}"})
+                status = 206
+                hdrs["Content-Range"] = f"bytes {start}-{end - 1}/{size}"
+        hdrs["Content-Length"] = str(end - start)
+        resp = web.StreamResponse(status=status, headers=hdrs)
+        await resp.prepare(request)
+        sent = 0
+        step = 1 << 20
+        pos = start
+        while pos < end:
+            n = min(step, end - pos)
+            if self.cut_after is not None and self.cut_times > 0 and sent + n > self.cut_after:
+                n = self.cut_after - sent
+                if n > 0:
+                    await resp.write(blob.read(pos, pos + n))
+                self.cut_times -= 1
+                request.transport.close()  # type: ignore[union-attr]
+                return resp
+            await resp.write(blob.read(pos, pos + n))
+            pos += n
+            sent += n
+            if self.rate:
+                await asyncio.sleep(n / self.rate)
+        await resp.write_eof()
+        return resp
