@@ -1,0 +1,212 @@
+"""End-to-end job harness: the BASELINE.json config "Single HTTP download
+job via local RabbitMQ, 10 MB file", used by ``bench.py``, ``smoke()`` and
+the integration tests.
+
+Layout per worker (rank): the fake broker, HTTP origin and S3 each run in
+their OWN process (``tritondl.fakes.serve``) — as the real RabbitMQ / media
+server / MinIO would — and the worker (``Service``) runs in this process
+exactly as in production: AMQP consume from ``v1.download-{0,1}`` → HTTP
+fetch into ``downloading/<id>/`` → select → SigV4 aws-chunked PUT to
+``triton-staging/<id>/original/<b64>`` → publish ``v1.convert`` → ack.
+A producer connection publishes the ``api.Download`` jobs; completion is
+observed as the job's ack, and each ``Convert`` is checked on the way out.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import hashlib
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+from dataclasses import dataclass, field
+
+from .amqp.client import Client
+from .amqp.codec import Properties
+from .amqp.connection import Connection
+from .models import Convert, Download, Media, SourceType
+from .s3.client import S3Client
+from .s3.credentials import Static
+from .s3.uploader import Uploader
+from .service import Service
+from .utils.config import Config
+
+AK, SK = "benchaccess", "benchsecret"
+
+
+class Backend:
+    def __init__(self, kind: str, extra: list[str] | None = None) -> None:
+        self.kind = kind
+        self.extra = extra or []
+        self.proc: asyncio.subprocess.Process | None = None
+        self.info: dict = {}
+
+    async def start(self) -> "Backend":
+        self.proc = await asyncio.create_subprocess_exec(
+            sys.executable, "-m", "tritondl.fakes.serve", self.kind, *self.extra,
+            stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert self.proc.stdout is not None
+        line = await asyncio.wait_for(self.proc.stdout.readline(), 120)
+        if not line:
+            raise RuntimeError(f"fake {self.kind} failed to start")
+        self.info = json.loads(line)
+        return self
+
+    async def stop(self) -> None:
+        p = self.proc
+        if p is None:
+            return
+        with contextlib.suppress(Exception):
+            if p.stdin:
+                p.stdin.close()
+        try:
+            await asyncio.wait_for(p.wait(), 10)
+        except asyncio.TimeoutError:
+            p.kill()  # our own child, by PID
+            await p.wait()
+        self.proc = None
+
+
+@dataclass
+class JobStack:
+    """Fakes + worker + producer for N synthetic jobs."""
+
+    file_size: int = 10 * 1024 * 1024
+    concurrency: int = 1
+    prefetch: int = 1
+    workdir: str | None = None
+    inproc: bool = False
+    tag: str = "r0"
+    backends: list = field(default_factory=list)
+    svc: Service | None = None
+    producer: Connection | None = None
+    _n: int = 0
+
+    async def setup(self) -> None:
+        if self.workdir is None:
+            self.workdir = tempfile.mkdtemp(prefix="tritondl-bench-")
+        if self.inproc:
+            from .fakes.broker import Broker
+            from .fakes.s3 import FakeS3
+            from .fakes.serve import SyntheticOrigin
+            b = await Broker().start()
+            o = await SyntheticOrigin().start()
+            s = await FakeS3(store="memory", access_key=AK, secret_key=SK).start()
+            self.backends = [b, o, s]
+            broker_url, origin_url, s3_url = b.url, f"http://{o.host}:{o.port}", s.endpoint
+        else:
+            bk = await Backend("broker").start()
+            og = await Backend("origin").start()
+            s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+            self.backends = [bk, og, s3]
+            broker_url, origin_url, s3_url = bk.info["url"], og.info["url"], s3.info["url"]
+        self.origin_url = origin_url
+        cfg = Config()
+        cfg.download_dir = os.path.join(self.workdir, "downloading")
+        cfg.concurrency = self.concurrency
+        cfg.prefetch = self.prefetch
+        cfg.cleanup = True          # keep disk bounded across thousands of bench jobs
+        cfg.retry_delay_s = 0.0
+        cfg.max_retries = 0
+        cfg.progress_log_interval_s = 0
+        cfg.heartbeat_s = 0
+        amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=0, retry_delay=0)
+        up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode="streaming"))
+        self.svc = Service(cfg, amqp=amqp, uploader=up)
+        await self.svc.start()
+        self.producer = await Connection.open(broker_url, heartbeat=0)
+        self.pch = await self.producer.channel()
+        await self.pch.confirm_select()
+        self.convert_ch = await self.producer.channel()
+        self.converts: list[Convert] = []
+
+        def on_convert(m) -> None:
+            self.converts.append(Convert.decode(m.body))
+            asyncio.ensure_future(m.ack())
+
+        # the worker declared v1.convert-{0,1} on its first publish; declare them here too
+        for i in range(2):
+            await self.convert_ch.queue_declare(f"v1.convert-{i}", durable=True)
+        await self.convert_ch.basic_consume("v1.convert-0", on_convert)
+        await self.convert_ch.basic_consume("v1.convert-1", on_convert)
+
+    def job_body(self, i: int) -> tuple[str, bytes]:
+        mid = f"bench-{self.tag}-{i}"
+        url = f"{self.origin_url}/synthetic/{self.file_size}/movie-{i}.mkv"
+        d = Download(created_at="now", media=Media(id=mid, name=f"movie {i}", source=SourceType.HTTP,
+                                                      source_uri=url))
+        return mid, d.encode()
+
+    async def submit(self, n: int) -> list[str]:
+        ids = []
+        for _ in range(n):
+            i = self._n
+            self._n += 1
+            mid, body = self.job_body(i)
+            await self.pch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
+                                         Properties(delivery_mode=2, content_type="application/octet-stream"))
+            ids.append(mid)
+        return ids
+
+    async def wait_done(self, total: int, timeout: float = 600) -> None:
+        assert self.svc is not None
+        t0 = time.monotonic()
+        while len(self.svc.results) < total:
+            if time.monotonic() - t0 > timeout:
+                raise TimeoutError(f"only {len(self.svc.results)}/{total} jobs finished")
+            await asyncio.sleep(0.001)
+
+    async def run_jobs(self, n: int) -> float:
+        """Submit n jobs and wait for all to finish; returns elapsed seconds."""
+        assert self.svc is not None
+        base = len(self.svc.results)
+        t0 = time.perf_counter()
+        await self.submit(n)
+        await self.wait_done(base + n)
+        dt = time.perf_counter() - t0
+        bad = [r for r in self.svc.results[base:] if not r.ok or r.bytes != self.file_size]
+        if bad:
+            raise RuntimeError(f"{len(bad)} jobs failed: {bad[0]}")
+        return dt
+
+    async def teardown(self) -> None:
+        if self.producer is not None:
+            with contextlib.suppress(Exception):
+                await self.producer.close()
+        if self.svc is not None:
+            await self.svc.shutdown(grace=10)
+        for b in self.backends:
+            with contextlib.suppress(Exception):
+                await b.stop()
+        if self.workdir and os.path.isdir(self.workdir):
+            shutil.rmtree(self.workdir, ignore_errors=True)
+
+
+def run_single_job_smoke(size: int = 1 << 20) -> None:
+    """One Download job end-to-end through in-process fakes; asserts the
+    Convert message carries the job's Media verbatim and S3 got the bytes."""
+    async def main() -> None:
+        st = JobStack(file_size=size, inproc=True, tag="smoke")
+        await st.setup()
+        try:
+            await st.run_jobs(1)
+            for _ in range(200):
+                if st.converts:
+                    break
+                await asyncio.sleep(0.01)
+            assert st.converts, "no v1.convert published"
+            c = st.converts[0]
+            assert c.media is not None and c.media.id == "bench-smoke-0"
+            from .fakes.serve import synthetic_bytes
+            s3 = st.backends[2]
+            from .s3.uploader import object_key
+            got = s3.object_bytes("triton-staging", object_key(c.media.id, "movie-0.mkv"))
+            assert hashlib.md5(got).digest() == hashlib.md5(synthetic_bytes(size)).digest()
+        finally:
+            await st.teardown()
+    asyncio.run(asyncio.wait_for(main(), 120))

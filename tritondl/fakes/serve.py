@@ -1,0 +1,82 @@
+"""Run one fake backend in its own process (so benches measure the worker,
+not the fakes competing for its event loop).
+
+    python -m tritondl.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
+
+Prints ONE JSON line ``{"kind":..., "endpoint": ..., "url": ...}`` on stdout
+once listening, then serves until stdin closes or SIGTERM.  The origin also
+serves ``/synthetic/<bytes>/<name>``: deterministic pseudo-random content of
+the requested size (generated once per size, cached in memory).
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import sys
+
+import numpy as np
+
+from .broker import Broker
+from .origin import Blob, Origin
+from .s3 import FakeS3
+
+
+def synthetic_bytes(size: int, seed: int = 1234) -> bytes:
+    return np.random.default_rng(seed).integers(0, 256, size, dtype=np.uint8).tobytes()
+
+
+class SyntheticOrigin(Origin):
+    def __init__(self, *a, **kw) -> None:
+        super().__init__(*a, **kw)
+        self._cache: dict[int, Blob] = {}
+
+    async def _handle(self, request):  # type: ignore[override]
+        parts = request.path.split("/")
+        if len(parts) >= 4 and parts[1] == "synthetic" and parts[2].isdigit():
+            size = int(parts[2])
+            blob = self._cache.get(size)
+            if blob is None:
+                blob = self._cache[size] = Blob(synthetic_bytes(size), etag=f'"syn-{size}"')
+            self.blobs[request.path] = blob
+        return await super()._handle(request)
+
+
+async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None) -> None:
+    if kind == "broker":
+        srv = await Broker(port=port).start()
+        info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.url}
+    elif kind == "origin":
+        srv = await SyntheticOrigin(port=port).start()
+        info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}", "url": f"http://{srv.host}:{srv.port}"}
+    elif kind == "s3":
+        srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk).start()
+        info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.endpoint}
+    else:
+        raise SystemExit(f"unknown kind {kind}")
+    print(json.dumps(info), flush=True)
+    loop = asyncio.get_running_loop()
+    stop = asyncio.Event()
+    for s in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(s, stop.set)
+    loop.add_reader(sys.stdin.fileno(), lambda: stop.set() if not os.read(sys.stdin.fileno(), 4096) else None)
+    await stop.wait()
+    await srv.stop()
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kind", choices=["broker", "origin", "s3"])
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--s3-store", default="discard", choices=["memory", "discard", "disk"])
+    ap.add_argument("--access-key", default=None)
+    ap.add_argument("--secret-key", default=None)
+    a = ap.parse_args()
+    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key))
+
+
+if __name__ == "__main__":
+    main()

@@ -115,6 +115,7 @@ class Dispatcher:
         if not base_dir or not os.path.isabs(base_dir):
             raise ValueError("invalid baseDir")
         self.base_dir = base_dir
+        self.impls = list(impls)
         self.protocol_impl: dict[str, list[ClientImpl]] = {}
         self.file_exts_impl: dict[str, list[ClientImpl]] = {}
         self.tracker = ProgressTracker(progress_log_interval)
@@ -135,6 +136,12 @@ class Dispatcher:
 
     async def stop(self) -> None:
         await self.tracker.stop()
+        seen = set()
+        for impl in self.impls:
+            close = getattr(impl, "close", None)
+            if close is not None and id(impl) not in seen:
+                seen.add(id(impl))
+                await close()
 
     def select(self, url: str) -> ClientImpl:
         u = urlparse(url)

@@ -1,0 +1,268 @@
+"""Job orchestrator — reference component C1 (``cmd/downloader/downloader.go``).
+
+Per job (``downloader.go:103-155``): decode ``api.Download`` → download via
+the dispatcher → select media files → upload to S3 → publish
+``api.Convert{CreatedAt: time.Now().String(), Media: job.Media}`` on
+``v1.convert`` → ack.  Undecodable bodies are nacked without requeue
+(``:106-111``).  Startup wiring (``:28-98``): logging from env, broker
+endpoint default ``127.0.0.1:5672`` (warned), prefetch 1, consume
+``v1.download``, impls ``[torrent, http]``, bucket ``triton-staging``,
+download dir ``$CWD/downloading``; SIGINT/SIGTERM/SIGHUP → graceful
+shutdown (``:158-173``).
+
+Differences, all documented fixes:
+
+* B4 — a failed job is not left unacked (which stalled the channel at
+  prefetch 1): it is re-published with ``X-Retries+1`` (the reference's
+  unused ``Delivery.Error``) and dead-lettered / dropped after
+  ``max_retries``;
+* B12 — broker connect errors are checked before use;
+* ``concurrency`` job loops per process (default 1 = reference), each job
+  fully async so downloads / uploads of different jobs overlap;
+* in-flight jobs are drained on shutdown (the Go job goroutine was never
+  joined); the work dir can optionally be cleaned after success (B15).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import os
+import shutil
+import signal
+import sys
+import time
+from dataclasses import dataclass
+
+from .amqp.client import Client, Delivery
+from .fetch.http import HTTPDownloader
+from .fetch.registry import ClientImpl, Dispatcher
+from .models import Convert, DecodeError, Download
+from .s3.uploader import Uploader
+from .select import dir_media
+from .utils.config import Config
+from .utils.gocompat import go_time_string
+from .utils.log import log
+from .utils.metrics import Metrics, serve_metrics
+from .utils.profiler import CPUProfiler
+
+
+def default_impls(cfg: Config) -> list[ClientImpl]:
+    """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
+    http = HTTPDownloader(progress_interval=cfg.progress_interval_s)
+    impls: list[ClientImpl] = []
+    try:
+        from .fetch.bt.client import TorrentDownloader
+        impls.append(TorrentDownloader.from_config(cfg, http=http))
+    except ImportError as e:  # pragma: no cover - BT stack always ships
+        log.warn("bittorrent downloader unavailable: %s", e)
+    impls.append(http)
+    return impls
+
+
+@dataclass
+class JobResult:
+    ok: bool
+    stage: str = ""
+    error: str = ""
+    files: int = 0
+    bytes: int = 0
+    seconds: float = 0.0
+
+
+class Service:
+    def __init__(self, cfg: Config, *, amqp: Client | None = None, dispatcher: Dispatcher | None = None,
+                 uploader: Uploader | None = None, metrics: Metrics | None = None) -> None:
+        self.cfg = cfg
+        self.amqp = amqp
+        self.dispatcher = dispatcher
+        self.uploader = uploader
+        self.metrics = metrics or Metrics()
+        self._workers: list[asyncio.Task] = []
+        self._stop = asyncio.Event()
+        self._inflight = 0
+        self._metrics_runner = None
+        self.results: list[JobResult] = []
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self) -> None:
+        cfg = self.cfg
+        if self.amqp is None:
+            if cfg.rabbitmq_endpoint_defaulted:
+                log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)
+            log.info("connecting to rabbitmq ...")
+            self.amqp = Client(cfg.rabbitmq_url(), prefetch=cfg.prefetch, num_shard_queues=cfg.num_shard_queues,
+                               heartbeat=cfg.heartbeat_s, retry_delay=cfg.retry_delay_s)
+            await self.amqp.connect()
+            log.info("connected")
+        else:
+            self.amqp.set_prefetch(cfg.prefetch)
+            if not self.amqp.connected:
+                await self.amqp.connect()
+        if self.dispatcher is None:
+            self.dispatcher = Dispatcher(cfg.download_dir, default_impls(cfg), cfg.progress_log_interval_s)
+        self.dispatcher.start()
+        if self.uploader is None:
+            self.uploader = Uploader.from_env(cfg.bucket, cfg.s3_endpoint, region=cfg.s3_region,
+                                              part_size=cfg.s3_part_size,
+                                              multipart_threshold=cfg.s3_multipart_threshold,
+                                              parallel_parts=cfg.s3_parallel_parts)
+        if cfg.metrics_addr:
+            self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr,
+                                                       health=lambda: self.amqp is not None and self.amqp.connected)
+        await self.amqp.consume(cfg.consume_topic)
+        for i in range(max(1, cfg.concurrency)):
+            self._workers.append(asyncio.ensure_future(self._worker(i)))
+
+    async def _worker(self, idx: int) -> None:
+        assert self.amqp is not None
+        while not self._stop.is_set():
+            getter = asyncio.ensure_future(self.amqp.get())
+            stopper = asyncio.ensure_future(self._stop.wait())
+            done, _ = await asyncio.wait({getter, stopper}, return_when=asyncio.FIRST_COMPLETED)
+            if getter not in done:
+                getter.cancel()
+                with contextlib.suppress(asyncio.CancelledError):
+                    await getter
+                return
+            stopper.cancel()
+            d = getter.result()
+            if d is None:
+                return
+            self._inflight += 1
+            self.metrics.set("jobs_inflight", self._inflight)
+            try:
+                await self.handle(d)
+            finally:
+                self._inflight -= 1
+                self.metrics.set("jobs_inflight", self._inflight)
+
+    async def handle(self, msg: Delivery) -> JobResult:
+        """Process one delivery end-to-end; always settles it."""
+        t0 = time.monotonic()
+        try:
+            job = Download.decode(msg.body)
+            if job.media is None:
+                raise DecodeError("missing media")
+        except DecodeError as e:
+            log.with_field("event", "decode-message").error(
+                "failed to unmarshal rabbitmq message into protobuf format: %s", e)
+            try:
+                await msg.nack()
+            except Exception as ne:
+                log.warn("failed to nack failed message: %s", ne)
+            self.metrics.inc("jobs", status="undecodable")
+            return self._record(JobResult(False, "decode", str(e)))
+
+        log.with_field("job", job.to_dict()).info("got message")
+        stage = "download"
+        nbytes = 0
+        try:
+            assert self.dispatcher is not None and self.uploader is not None and self.amqp is not None
+            t = time.monotonic()
+            dl_dir = await self.dispatcher.download(job.media.id, job.media.source_uri)
+            self.metrics.observe("stage_seconds", time.monotonic() - t, stage="download")
+            stage = "select"
+            files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
+            log.info("found %d files", len(files))
+            stage = "upload"
+            t = time.monotonic()
+            res = await self.uploader.upload_files(job.media.id, dl_dir, files)
+            nbytes = sum(r.size for r in res)
+            self.metrics.observe("stage_seconds", time.monotonic() - t, stage="upload")
+            stage = "publish"
+            log.info("creating v1.convert message")
+            conv = Convert.from_download(job, go_time_string())
+            await self.amqp.publish(self.cfg.publish_topic, conv.encode())
+            stage = "ack"
+            log.with_field("job", job.to_dict()).info("finished processing")
+            await msg.ack()
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - any stage failure must settle the message
+            log.with_fields(stage=stage, error=str(e)).error("job failed")
+            self.metrics.inc("jobs", status="failed", stage=stage)
+            await self._dispose_failed(msg, stage, e)
+            return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
+        if self.cfg.cleanup:
+            await asyncio.get_running_loop().run_in_executor(None, shutil.rmtree, dl_dir, True)
+        dt = time.monotonic() - t0
+        self.metrics.inc("jobs", status="ok")
+        self.metrics.inc("bytes_uploaded", nbytes)
+        self.metrics.observe("job_seconds", dt)
+        return self._record(JobResult(True, "done", files=len(files), bytes=nbytes, seconds=dt))
+
+    def _record(self, r: JobResult) -> JobResult:
+        self.results.append(r)
+        if len(self.results) > 10000:
+            del self.results[:5000]
+        return r
+
+    async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> None:
+        """B4 fix: requeue with X-Retries+1, dead-letter after max_retries."""
+        assert self.amqp is not None
+        try:
+            if msg.metadata.retries < self.cfg.max_retries:
+                log.with_fields(retries=msg.metadata.retries + 1).warn("scheduling job retry")
+                await msg.retry(self.cfg.retry_delay_s)
+                return
+            if self.cfg.dead_letter_topic:
+                hdrs = dict(msg.msg.properties.headers or {})
+                hdrs.update({"X-Retries": msg.metadata.retries, "X-Failed-Stage": stage,
+                             "X-Error": str(err)[:512]})
+                await self.amqp.publish(self.cfg.dead_letter_topic, msg.body, headers=hdrs)
+                await msg.ack()
+            else:
+                await msg.nack(requeue=False)
+            self.metrics.inc("jobs_dead_lettered")
+        except Exception as e:  # noqa: BLE001
+            log.with_field("error", str(e)).error("failed to dispose failed job; broker will redeliver")
+
+    async def shutdown(self, grace: float = 30.0) -> None:
+        log.info("shutting down")
+        self._stop.set()
+        if self._workers:
+            done, pending = await asyncio.wait(self._workers, timeout=grace)
+            for t in pending:
+                t.cancel()
+            for t in pending:
+                with contextlib.suppress(BaseException):
+                    await t
+        if self.dispatcher is not None:
+            await self.dispatcher.stop()
+        if self.uploader is not None:
+            await self.uploader.close()
+        if self.amqp is not None:
+            await self.amqp.close()
+        if self._metrics_runner is not None:
+            await self._metrics_runner.cleanup()
+        log.info("finished shutdown")
+
+    async def run_forever(self) -> None:
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for s in (signal.SIGINT, signal.SIGTERM, signal.SIGHUP):
+            with contextlib.suppress(NotImplementedError, RuntimeError):
+                loop.add_signal_handler(s, stop.set)
+        await self.start()
+        await stop.wait()
+        await self.shutdown()
+
+
+def main(argv: list[str] | None = None) -> int:
+    cfg = Config.from_env(argv=list(sys.argv[1:] if argv is None else argv))
+    log.configure(cfg.log_level, cfg.log_format)
+    prof = CPUProfiler(cfg.cpuprofile)
+    prof.start()
+    try:
+        asyncio.run(Service(cfg).run_forever())
+    except Exception as e:  # log.Fatal equivalent
+        log.error("fatal: %s", e)
+        prof.stop()
+        return 1
+    prof.stop()
+    return 0
+
+
+if __name__ == "__main__":  # pragma: no cover
+    sys.exit(main())

@@ -1,0 +1,110 @@
+"""Minimal Prometheus-text metrics (the reference had none):
+counters, gauges and fixed-bucket histograms, plus an optional aiohttp
+``/metrics`` + ``/healthz`` endpoint.  Single event loop → no locking
+needed on the hot path; the exposition snapshot is taken on the loop too.
+"""
+
+from __future__ import annotations
+
+import bisect
+import time
+from dataclasses import dataclass, field
+
+_DEF_BUCKETS = (0.01, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 300, 900, 3600)
+
+
+@dataclass
+class _Hist:
+    buckets: tuple[float, ...] = _DEF_BUCKETS
+    counts: list[int] = field(default_factory=list)
+    total: float = 0.0
+    n: int = 0
+
+    def __post_init__(self) -> None:
+        self.counts = [0] * (len(self.buckets) + 1)
+
+    def observe(self, v: float) -> None:
+        self.counts[bisect.bisect_left(self.buckets, v)] += 1
+        self.total += v
+        self.n += 1
+
+
+class Metrics:
+    def __init__(self, prefix: str = "tritondl") -> None:
+        self.prefix = prefix
+        self.counters: dict[tuple[str, tuple], float] = {}
+        self.gauges: dict[tuple[str, tuple], float] = {}
+        self.hists: dict[tuple[str, tuple], _Hist] = {}
+        self.started = time.time()
+
+    @staticmethod
+    def _k(name: str, labels: dict | None) -> tuple[str, tuple]:
+        return name, tuple(sorted((labels or {}).items()))
+
+    def inc(self, name: str, v: float = 1.0, **labels) -> None:
+        k = self._k(name, labels)
+        self.counters[k] = self.counters.get(k, 0.0) + v
+
+    def set(self, name: str, v: float, **labels) -> None:
+        self.gauges[self._k(name, labels)] = v
+
+    def observe(self, name: str, v: float, **labels) -> None:
+        k = self._k(name, labels)
+        h = self.hists.get(k)
+        if h is None:
+            h = self.hists[k] = _Hist()
+        h.observe(v)
+
+    def get(self, name: str, **labels) -> float:
+        k = self._k(name, labels)
+        return self.counters.get(k, self.gauges.get(k, 0.0))
+
+    def render(self) -> str:
+        p = self.prefix
+        out: list[str] = []
+
+        def lab(items: tuple, extra: str = "") -> str:
+            parts = [f'{k}="{v}"' for k, v in items]
+            if extra:
+                parts.append(extra)
+            return "{" + ",".join(parts) + "}" if parts else ""
+
+        for (n, ls), v in sorted(self.counters.items()):
+            out.append(f"{p}_{n}_total{lab(ls)} {v}")
+        for (n, ls), v in sorted(self.gauges.items()):
+            out.append(f"{p}_{n}{lab(ls)} {v}")
+        for (n, ls), h in sorted(self.hists.items(), key=lambda x: x[0]):
+            acc = 0
+            for b, c in zip(h.buckets, h.counts):
+                acc += c
+                le = 'le="%s"' % b
+                out.append(f"{p}_{n}_bucket{lab(ls, le)} {acc}")
+            le = 'le="+Inf"'
+            out.append(f"{p}_{n}_bucket{lab(ls, le)} {h.n}")
+            out.append(f"{p}_{n}_sum{lab(ls)} {h.total}")
+            out.append(f"{p}_{n}_count{lab(ls)} {h.n}")
+        out.append(f"{p}_uptime_seconds {time.time() - self.started:.3f}")
+        return "\n".join(out) + "\n"
+
+
+async def serve_metrics(metrics: Metrics, addr: str, health=None):
+    """Start ``/metrics`` and ``/healthz`` on ``host:port``; returns the runner."""
+    from aiohttp import web
+
+    host, _, port = addr.rpartition(":")
+    app = web.Application()
+
+    async def m(_req):
+        return web.Response(text=metrics.render(), content_type="text/plain")
+
+    async def hz(_req):
+        ok = True if health is None else bool(health())
+        return web.Response(status=200 if ok else 503, text="ok" if ok else "unhealthy")
+
+    app.router.add_get("/metrics", m)
+    app.router.add_get("/healthz", hz)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, host or "0.0.0.0", int(port))
+    await site.start()
+    return runner
