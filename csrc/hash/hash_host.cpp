@@ -327,6 +327,63 @@ std::vector<std::string> chunk_signatures(const std::string& signing_key, const 
   return sigs;
 }
 
+// Fused aws-chunked encoder: for every chunk, SHA-256 it (while it is hot in
+// cache), chain the HMAC signature and copy it behind its
+// "<hex>;chunk-signature=<sig>\r\n" header into ONE pre-sized output buffer.
+// Replaces a Python loop of slices/concats that cost ~2.5x the hashing.
+py::tuple aws_chunk_encode(const std::string& signing_key, const std::string& amzdate, const std::string& scope,
+                           const std::string& prev_sig, const py::buffer& data, size_t chunk_size, bool final_chunk) {
+  if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
+  py::buffer_info bi;
+  BufView v = view_of(data, bi);
+  auto hexlen = [](size_t n) {
+    size_t l = 1;
+    while (n >>= 4) ++l;
+    return l;
+  };
+  const size_t sig_part = 17 + 64 + 2;  // ";chunk-signature=" + sig + CRLF
+  size_t total = 0;
+  for (size_t off = 0; off < v.len; off += chunk_size) {
+    size_t n = std::min(chunk_size, v.len - off);
+    total += hexlen(n) + sig_part + n + 2;
+  }
+  if (final_chunk) total += 1 + sig_part + 2;
+  PyObject* out = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(total));
+  if (!out) throw py::error_already_set();
+  py::bytes result = py::reinterpret_steal<py::bytes>(out);
+  char* dst = PyBytes_AS_STRING(out);
+  std::string prev = prev_sig;
+  {
+    py::gil_scoped_release nogil;
+    const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+    const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
+    size_t w = 0;
+    auto emit = [&](const char* p, size_t n) {
+      std::string h = hex(one_shot(EVP_sha256(), p, n));
+      prev = hex(hmac256(signing_key, head + prev + "\n" + empty_hash + "\n" + h));
+      char hx[32];
+      int hl = snprintf(hx, sizeof hx, "%zx", n);
+      std::memcpy(dst + w, hx, hl);
+      w += hl;
+      std::memcpy(dst + w, ";chunk-signature=", 17);
+      w += 17;
+      std::memcpy(dst + w, prev.data(), 64);
+      w += 64;
+      dst[w++] = '\r';
+      dst[w++] = '\n';
+      if (n) {
+        std::memcpy(dst + w, p, n);
+        w += n;
+      }
+      dst[w++] = '\r';
+      dst[w++] = '\n';
+    };
+    for (size_t off = 0; off < v.len; off += chunk_size) emit(v.ptr + off, std::min(chunk_size, v.len - off));
+    if (final_chunk) emit(nullptr, 0);
+  }
+  return py::make_tuple(result, prev);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hash_host, m) {
@@ -358,4 +415,6 @@ PYBIND11_MODULE(_hash_host, m) {
   m.def("chunk_signatures", &chunk_signatures, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
         py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true);
   m.def("default_threads", &default_threads);
+  m.def("aws_chunk_encode", &aws_chunk_encode, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
+        py::arg("prev_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("final") = false);
 }

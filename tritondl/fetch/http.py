@@ -255,21 +255,21 @@ class HTTPDownloader:
                                 pos = 0
                             else:
                                 raise _FatalHTTPError("origin ignored Range request")
-                    buf = bytearray()
+                    bufs: list[bytes] = []
+                    nbuf = 0
                     wpos = pos
                     async for chunk in r.content.iter_chunked(self.chunk):
-                        buf += chunk
-                        if len(buf) >= self.write_block:
-                            n = len(buf)
-                            await loop.run_in_executor(None, _pwrite_all, fd, bytes(buf), wpos)
-                            wpos += n
-                            done[i] += n
-                            buf.clear()
-                    if buf:
-                        n = len(buf)
-                        await loop.run_in_executor(None, _pwrite_all, fd, bytes(buf), wpos)
-                        wpos += n
-                        done[i] += n
+                        bufs.append(chunk)
+                        nbuf += len(chunk)
+                        if nbuf >= self.write_block:
+                            await loop.run_in_executor(None, _pwritev_all, fd, bufs, wpos)
+                            wpos += nbuf
+                            done[i] += nbuf
+                            bufs, nbuf = [], 0
+                    if bufs:
+                        await loop.run_in_executor(None, _pwritev_all, fd, bufs, wpos)
+                        wpos += nbuf
+                        done[i] += nbuf
                     if end >= 0 and start + done[i] < end:
                         raise HTTPDownloadError("connection closed early")
                     return
@@ -281,6 +281,14 @@ class HTTPDownloader:
                 d = min(0.2 * 2 ** attempt, 5.0)
                 log.with_fields(error=str(e), attempt=attempt, segment=i).warn("download stream failed; retrying")
                 await asyncio.sleep(d)
+
+
+def _pwritev_all(fd: int, bufs: list[bytes], pos: int) -> None:
+    """Vectored write of the received chunks — no concatenation copy."""
+    total = sum(len(b) for b in bufs)
+    n = os.pwritev(fd, bufs, pos)
+    if n < total:  # short write: finish the remainder the slow way
+        _pwrite_all(fd, b"".join(bufs)[n:], pos + n)
 
 
 def _pwrite_all(fd: int, data: bytes, pos: int) -> None:

@@ -47,6 +47,12 @@ def chunk_signatures(signing_key: bytes, amzdate: str, scope: str, seed_signatur
     return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size, include_final)
 
 
+def aws_chunk_encode(signing_key: bytes, amzdate: str, scope: str, prev_signature: str, data, chunk_size: int,
+                     final: bool = False) -> tuple[bytes, str]:
+    """Fused aws-chunked framing + signature chain; returns (encoded, last_signature)."""
+    return _host.aws_chunk_encode(signing_key, amzdate, scope, prev_signature, data, chunk_size, final)
+
+
 # ----------------------------------------------------------------- GPU
 
 _gpu_mod = None

@@ -307,39 +307,62 @@ class _StreamBody:
         if self.mode == "streaming":
             self.signer = sigv4.ChunkSigner(signed.key, signed.amzdate, signed.scope, signed.signature)
 
-    async def _blocks(self) -> AsyncIterator[bytes]:
-        loop = asyncio.get_running_loop()
-        blk = self.client.io_block
-        if isinstance(self.src, (bytes, bytearray, memoryview)):
-            mv = memoryview(self.src)[self.offset:self.offset + self.length]
-            for i in range(0, self.length, blk):
-                yield bytes(mv[i:i + blk])
-            return
-        fd = os.open(self.src, os.O_RDONLY)
-        try:
-            pos, end = self.offset, self.offset + self.length
-            while pos < end:
-                n = min(blk, end - pos)
-                data = await loop.run_in_executor(None, os.pread, fd, n, pos)
-                if len(data) != n:
-                    raise S3Error(0, "ShortRead", f"file shrank while uploading ({pos + len(data)} < {end})")
-                pos += n
-                yield data
-        finally:
-            os.close(fd)
+    def _read(self, fd: int | None, pos: int, n: int) -> bytes:
+        if fd is None:
+            return bytes(memoryview(self.src)[pos:pos + n])  # type: ignore[arg-type]
+        data = os.pread(fd, n, pos)
+        if len(data) != n:
+            raise S3Error(0, "ShortRead", f"file shrank while uploading ({pos + len(data)} < {pos + n})")
+        return data
+
+    def _produce_block(self, fd: int | None, pos: int, n: int, last: bool) -> bytes:
+        """Worker thread: read one block and (streaming mode) aws-chunk-encode it."""
+        data = self._read(fd, pos, n)
+        if self.signer is None:
+            return data
+        out = self.signer.feed(data)
+        if last:
+            out += self.signer.finish()
+        return out
 
     async def stream(self) -> AsyncIterator[bytes]:
+        """Body generator with a 2-deep read→sign pipeline running ahead of
+        the socket writer (the native encoder releases the GIL)."""
+        if self.mode == "streaming":
+            assert self.signer is not None, "seed signature not bound"
         loop = asyncio.get_running_loop()
-        if self.mode != "streaming":
-            async for b in self._blocks():
-                yield b
-            return
-        assert self.signer is not None, "seed signature not bound"
-        async for b in self._blocks():
-            out = await loop.run_in_executor(None, self.signer.feed, b)
-            if out:
-                yield out
-        yield self.signer.finish()
+        blk = self.client.io_block
+        fd = None if isinstance(self.src, (bytes, bytearray, memoryview)) else os.open(self.src, os.O_RDONLY)
+        q: asyncio.Queue = asyncio.Queue(maxsize=2)
+
+        async def produce() -> None:
+            try:
+                pos, end = self.offset, self.offset + self.length
+                if pos == end and self.signer is not None:
+                    await q.put(self.signer.finish())
+                while pos < end:
+                    n = min(blk, end - pos)
+                    out = await loop.run_in_executor(None, self._produce_block, fd, pos, n, pos + n >= end)
+                    pos += n
+                    if out:
+                        await q.put(out)
+                await q.put(None)
+            except BaseException as e:  # noqa: BLE001 - forwarded to the consumer
+                await q.put(e)
+
+        task = asyncio.ensure_future(produce())
+        try:
+            while True:
+                item = await q.get()
+                if item is None:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            task.cancel()
+            if fd is not None:
+                os.close(fd)
 
 
 class _BodyFactory:

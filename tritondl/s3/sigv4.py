@@ -117,45 +117,26 @@ class ChunkSigner:
         self.chunk = chunk
         self._buf = bytearray()
 
-    def _emit(self, data: bytes | memoryview) -> bytes:
-        n = len(data)
-        full = n - n % self.chunk
-        if full == 0:
-            return b""
-        view = memoryview(data)[:full]
-        sigs = hashing.chunk_signatures(self.key, self.amzdate, self.scope, self.prev, view, self.chunk,
-                                        include_final=False)
-        out = bytearray()
-        for i, s in enumerate(sigs):
-            piece = view[i * self.chunk:(i + 1) * self.chunk]
-            out += f"{len(piece):x};chunk-signature={s}\r\n".encode()
-            out += piece
-            out += b"\r\n"
-        self.prev = sigs[-1]
-        return bytes(out)
+    def _encode(self, data, final: bool) -> bytes:
+        out, self.prev = hashing.aws_chunk_encode(self.key, self.amzdate, self.scope, self.prev, data,
+                                                  self.chunk, final)
+        return out
 
     def feed(self, data: bytes) -> bytes:
+        """Encode every whole chunk available; keep the remainder buffered."""
         if self._buf:
             self._buf += data
             data = bytes(self._buf)
             self._buf.clear()
         n = len(data)
         full = n - n % self.chunk
-        out = self._emit(memoryview(data)[:full]) if full else b""
+        out = self._encode(memoryview(data)[:full], False) if full else b""
         if full < n:
-            self._buf += data[full:]
+            self._buf += memoryview(data)[full:]
         return out
 
     def finish(self) -> bytes:
-        out = bytearray()
-        if self._buf:
-            rest = bytes(self._buf)
-            self._buf.clear()
-            sigs = hashing.chunk_signatures(self.key, self.amzdate, self.scope, self.prev, rest, len(rest),
-                                            include_final=False)
-            out += f"{len(rest):x};chunk-signature={sigs[0]}\r\n".encode() + rest + b"\r\n"
-            self.prev = sigs[0]
-        final = hashing.chunk_signatures(self.key, self.amzdate, self.scope, self.prev, b"", self.chunk)
-        self.prev = final[-1]
-        out += f"0;chunk-signature={self.prev}\r\n\r\n".encode()
-        return bytes(out)
+        """Encode the buffered tail (one short chunk) plus the final empty chunk."""
+        rest = bytes(self._buf)
+        self._buf.clear()
+        return self._encode(rest, True)
