@@ -1,0 +1,223 @@
+"""BitTorrent stack: bencode, metainfo/magnets, and full downloads against a
+local swarm (HTTP tracker, UDP tracker, DHT, direct peers, .torrent over
+HTTP, resume from partial data, corrupt seeder)."""
+
+import asyncio
+import hashlib
+import os
+
+import pytest
+
+from tritondl.fakes.origin import Origin
+from tritondl.fakes.swarm import (DHTNetwork, HTTPTracker, Seeder, UDPTracker, magnet_for, make_payload,
+                                  torrent_file_bytes, torrent_for)
+from tritondl.fetch.bt import bencode
+from tritondl.fetch.bt.client import TorrentDownloader, TorrentError
+from tritondl.fetch.bt.metainfo import Metainfo, MetainfoError, parse_magnet
+from tritondl.fetch.bt.torrent import TorrentConfig
+from tritondl.fetch.bt.tracker import Announce, parse_compact
+from tritondl.select import dir_media
+
+
+def run(coro, timeout=90):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+# ----------------------------------------------------------------- bencode
+
+
+def test_bencode_roundtrip_and_errors():
+    v = {b"a": [1, -2, b"xyz", {b"n": 0}], b"b": b""}
+    assert bencode.decode(bencode.encode(v)) == v
+    assert bencode.encode({"b": 1, "a": 2}) == b"d1:ai2e1:bi1ee"
+    for bad in [b"i01e", b"i-0e", b"3:ab", b"l", b"d1:ai1e", b"x", b"i1ei2e", b"02:ab"]:
+        with pytest.raises(bencode.BencodeError):
+            bencode.decode(bad)
+
+
+def test_spans_give_raw_info():
+    info = b"d4:name1:x12:piece lengthi16384e6:pieces0:6:lengthi0ee"
+    d, spans = bencode.decode_with_spans(b"d8:announce3:url4:info" + info + b"e")
+    s, e = spans[b"info"]
+    assert (b"d8:announce3:url4:info" + info + b"e")[s:e] == info
+
+
+# ----------------------------------------------------------------- metainfo
+
+
+def test_metainfo_single_and_multi(tmp_path):
+    make_payload(str(tmp_path / "show"), {"season 1/e1.mkv": 100_000, "season 1/e2.mkv": 50_001})
+    info = torrent_for(str(tmp_path / "show"), 32768)
+    assert info.multi and info.name == "show" and info.total_length == 150_001
+    assert info.num_pieces == -(-150_001 // 32768)
+    mi = Metainfo.parse(torrent_file_bytes(info, ["http://t/announce"]))
+    assert mi.infohash == info.infohash and mi.announce == [["http://t/announce"]]
+    paths = info.file_paths("/base")
+    assert paths[0][0] == "/base/show/season 1/e1.mkv"
+    single = torrent_for(str(tmp_path / "show" / "season 1" / "e2.mkv"), 16384)
+    assert not single.multi and single.file_paths("/b") == [("/b/e2.mkv", 50_001)]
+
+
+def test_metainfo_rejects_traversal():
+    bad = bencode.encode({b"name": b"x", b"piece length": 16384, b"pieces": b"",
+                          b"files": [{b"length": 0, b"path": [b"..", b"etc"]}]})
+    with pytest.raises(MetainfoError):
+        from tritondl.fetch.bt.metainfo import Info
+        Info.parse(bad)
+
+
+def test_magnet_parse():
+    ih = hashlib.sha1(b"x").digest()
+    m = parse_magnet(f"magnet:?xt=urn:btih:{ih.hex()}&dn=My%20Show&tr=http%3A%2F%2Ft%2Fa&x.pe=1.2.3.4:5")
+    assert m.infohash == ih and m.display_name == "My Show" and m.trackers == ["http://t/a"]
+    assert m.peers == [("1.2.3.4", 5)]
+    import base64
+    m2 = parse_magnet("magnet:?xt=urn:btih:" + base64.b32encode(ih).decode())
+    assert m2.infohash == ih
+    assert parse_magnet(m.uri()).infohash == ih
+    with pytest.raises(MetainfoError):
+        parse_magnet("magnet:?dn=x")
+
+
+def test_compact_peers():
+    assert parse_compact(bytes([127, 0, 0, 1, 0x1A, 0xE1])) == [("127.0.0.1", 6881)]
+
+
+# ----------------------------------------------------------------- swarm
+
+
+def _dl(**kw):
+    cfg = TorrentConfig(listen_host="127.0.0.1", tracker_min_interval=0.5, dht_interval=0.5,
+                        verify_device="cpu", request_timeout=3)
+    return TorrentDownloader(cfg, progress_interval=0.05, use_dht=kw.pop("use_dht", False), **kw)
+
+
+class Sink:
+    def __init__(self):
+        self.p = []
+
+    def __call__(self, url, p):
+        self.p.append(p)
+
+
+def _check_tree(src_root, dst_root):
+    for root, _d, files in os.walk(src_root):
+        for f in files:
+            a = os.path.join(root, f)
+            b = os.path.join(dst_root, os.path.relpath(a, os.path.dirname(src_root)))
+            assert open(a, "rb").read() == open(b, "rb").read(), b
+
+
+def test_magnet_via_http_tracker_multi_file(tmp_path):
+    async def main():
+        src = tmp_path / "src" / "My.Show"
+        make_payload(str(src), {"season 1/e1.mkv": 700_000, "season 1/e2.mkv": 333_333, "notes.txt": 1000})
+        info = torrent_for(str(src), 65536)
+        tr = await HTTPTracker().start()
+        seeds = [await Seeder(info, str(tmp_path / "src"), trackers=[tr.url]).start() for _ in range(2)]
+        await asyncio.sleep(0.2)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        sink = Sink()
+        await _dl().download(str(dst), sink, magnet_for(info, [tr.url]))
+        _check_tree(str(src), str(dst))
+        assert sink.p[-1] == 100
+        files = dir_media(str(dst))   # sole top-level dir "My.Show" -> season dirs
+        assert [os.path.basename(f) for f in files] == ["e1.mkv", "e2.mkv"]
+        for s in seeds:
+            await s.stop()
+        await tr.stop()
+    run(main())
+
+
+def test_magnet_via_udp_tracker_single_file(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"movie.mkv": 1_234_567})
+        info = torrent_for(str(src / "movie.mkv"), 32768)
+        ut = await UDPTracker().start()
+        s = await Seeder(info, str(src), trackers=[ut.url]).start()
+        await asyncio.sleep(0.2)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        await _dl().download(str(dst), Sink(), magnet_for(info, [ut.url]))
+        assert (dst / "movie.mkv").read_bytes() == (src / "movie.mkv").read_bytes()
+        await s.stop()
+        ut.stop()
+    run(main())
+
+
+def test_magnet_via_dht_only(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"movie.mp4": 600_000})
+        info = torrent_for(str(src / "movie.mp4"), 16384)
+        net = await DHTNetwork(5).start()
+        s = await Seeder(info, str(src), dht_bootstrap=net.bootstrap).start()
+        await s.dht.announce_peer(info.infohash, s.torrent.port)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        await _dl(use_dht=True, dht_bootstrap=net.bootstrap).download(str(dst), Sink(), magnet_for(info))
+        assert (dst / "movie.mp4").read_bytes() == (src / "movie.mp4").read_bytes()
+        await s.stop()
+        net.stop()
+    run(main())
+
+
+def test_torrent_file_over_http_and_resume(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"film.webm": 2_000_000})
+        info = torrent_for(str(src / "film.webm"), 65536)
+        s = await Seeder(info, str(src)).start()
+        o = await Origin().start()
+        tor = torrent_file_bytes(info)
+        url = o.add("/x/film.torrent", tor)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        # partial pre-existing data: first half correct, second half garbage
+        data = (src / "film.webm").read_bytes()
+        (dst / "film.webm").write_bytes(data[:1_000_000] + os.urandom(1_000_000))
+        d = _dl(extra_trackers=[])
+        t, dht = await d.open(str(dst), url)
+        t.add_peer_addr(s.addr)
+        await t.download_all()
+        pre = t.nhave
+        assert 0 < pre < info.num_pieces       # resume kept the verified half
+        await asyncio.wait_for(t.complete.wait(), 30)
+        await t.close()
+        assert (dst / "film.webm").read_bytes() == data
+        await s.stop()
+        await o.stop()
+    run(main())
+
+
+def test_corrupt_seeder_is_banned_and_good_one_used(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"a.mkv": 500_000})
+        info = torrent_for(str(src / "a.mkv"), 32768)
+        bad = await Seeder(info, str(src), corrupt=True).start()
+        good = await Seeder(info, str(src)).start()
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        await _dl().download(str(dst), Sink(), magnet_for(info, peers=[bad.addr, good.addr]))
+        assert (dst / "a.mkv").read_bytes() == (src / "a.mkv").read_bytes()
+        await bad.stop()
+        await good.stop()
+    run(main())
+
+
+def test_metadata_timeout_and_unsupported_scheme(tmp_path):
+    async def main():
+        d = _dl(metadata_timeout=0.3)
+        with pytest.raises(TorrentError, match="failed to get metadata"):
+            await d.download(str(tmp_path), Sink(), "magnet:?xt=urn:btih:" + "ab" * 20)
+        with pytest.raises(TorrentError, match="unsupported scheme 'ftp'"):
+            await d.download(str(tmp_path), Sink(), "ftp://x/a.torrent")
+    run(main())
+
+
+def test_announce_dataclass():
+    a = Announce(b"\x01" * 20, b"-TD0100-" + b"x" * 12, 6881)
+    assert a.event == "started"

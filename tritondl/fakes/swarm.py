@@ -1,0 +1,203 @@
+"""Local BitTorrent swarm for tests/benches: HTTP tracker, UDP tracker
+(BEP 15), DHT nodes and seeders (our own :class:`Torrent` in seed mode) —
+all on 127.0.0.1.  The reference had no swarm fixture."""
+
+from __future__ import annotations
+
+import asyncio
+import os
+import random
+import struct
+import time
+
+from aiohttp import web
+
+from ..fetch.bt import bencode
+from ..fetch.bt.dht import DHTNode
+from ..fetch.bt.metainfo import Info, Magnet, Metainfo, make_info
+from ..fetch.bt.torrent import Torrent, TorrentConfig
+from ..fetch.bt.tracker import compact_peers
+
+
+class HTTPTracker:
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, interval: int = 5) -> None:
+        self.host, self.port, self.interval = host, port, interval
+        self.swarms: dict[bytes, dict[tuple[str, int], float]] = {}
+        self.announces = 0
+        self._runner: web.AppRunner | None = None
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}/announce"
+
+    async def start(self) -> "HTTPTracker":
+        app = web.Application()
+        app.router.add_get("/announce", self._announce)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        return self
+
+    async def stop(self) -> None:
+        if self._runner:
+            await self._runner.cleanup()
+
+    async def _announce(self, req: web.Request) -> web.Response:
+        from urllib.parse import parse_qs, unquote_to_bytes
+        self.announces += 1
+        raw = req.query_string
+        q = {}
+        for part in raw.split("&"):
+            k, _, v = part.partition("=")
+            q[k] = unquote_to_bytes(v)
+        ih = q.get("info_hash", b"")
+        port = int(q.get("port", b"0") or 0)
+        ip = req.remote or "127.0.0.1"
+        sw = self.swarms.setdefault(ih, {})
+        me = (ip, port)
+        if q.get("event") == b"stopped":
+            sw.pop(me, None)
+        elif port:
+            sw[me] = time.monotonic()
+        peers = [p for p in sw if p != me]
+        _ = parse_qs
+        body = bencode.encode({b"interval": self.interval, b"peers": compact_peers(peers),
+                               b"complete": len(sw), b"incomplete": 0})
+        return web.Response(body=body, content_type="text/plain")
+
+
+class UDPTracker(asyncio.DatagramProtocol):
+    def __init__(self) -> None:
+        self.swarms: dict[bytes, set[tuple[str, int]]] = {}
+        self.conn_ids: set[int] = set()
+        self.transport: asyncio.DatagramTransport | None = None
+        self.port = 0
+
+    async def start(self, host: str = "127.0.0.1", port: int = 0) -> "UDPTracker":
+        loop = asyncio.get_running_loop()
+        self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(host, port))
+        self.port = self.transport.get_extra_info("sockname")[1]
+        return self
+
+    @property
+    def url(self) -> str:
+        return f"udp://127.0.0.1:{self.port}/announce"
+
+    def stop(self) -> None:
+        if self.transport:
+            self.transport.close()
+
+    def datagram_received(self, data: bytes, addr) -> None:
+        if len(data) < 16:
+            return
+        conn_id, action, tid = struct.unpack(">QII", data[:16])
+        if action == 0 and conn_id == 0x41727101980:
+            cid = random.getrandbits(63)
+            self.conn_ids.add(cid)
+            self.transport.sendto(struct.pack(">IIQ", 0, tid, cid), addr)  # type: ignore[union-attr]
+        elif action == 1 and conn_id in self.conn_ids and len(data) >= 98:
+            ih = data[16:36]
+            port = struct.unpack(">H", data[96:98])[0]
+            sw = self.swarms.setdefault(ih, set())
+            me = (addr[0], port)
+            peers = [p for p in sw if p != me]
+            sw.add(me)
+            self.transport.sendto(struct.pack(">IIIII", 1, tid, 10, 0, len(sw)) + compact_peers(peers),  # type: ignore[union-attr]
+                                  addr)
+        else:
+            self.transport.sendto(struct.pack(">II", 3, tid) + b"bad request", addr)  # type: ignore[union-attr]
+
+
+class DHTNetwork:
+    def __init__(self, n: int = 4) -> None:
+        self.n = n
+        self.nodes: list[DHTNode] = []
+
+    async def start(self) -> "DHTNetwork":
+        first = await DHTNode(host="127.0.0.1").start()
+        self.nodes = [first]
+        for _ in range(self.n - 1):
+            nd = await DHTNode(host="127.0.0.1", bootstrap=[first.addr]).start()
+            self.nodes.append(nd)
+        for nd in self.nodes[1:]:
+            await nd.bootstrap()
+        await first.bootstrap()
+        return self
+
+    @property
+    def bootstrap(self) -> list[tuple[str, int]]:
+        return [self.nodes[0].addr]
+
+    def stop(self) -> None:
+        for nd in self.nodes:
+            nd.stop()
+
+
+class Seeder:
+    """Seed an existing file/dir: serves pieces to any peer that connects."""
+
+    def __init__(self, info: Info, data_dir: str, *, trackers: list[str] | None = None,
+                 dht_bootstrap: list[tuple[str, int]] | None = None, corrupt: bool = False) -> None:
+        self.info = info
+        self.data_dir = data_dir
+        self.trackers = trackers or []
+        self.dht_bootstrap = dht_bootstrap
+        self.corrupt = corrupt
+        self.torrent: Torrent | None = None
+        self.dht: DHTNode | None = None
+
+    async def start(self) -> "Seeder":
+        if self.dht_bootstrap is not None:
+            self.dht = await DHTNode(host="127.0.0.1", bootstrap=self.dht_bootstrap).start()
+            await self.dht.bootstrap()
+        cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, tracker_min_interval=1.0, dht_interval=1.0,
+                            verify_device="cpu")
+        t = Torrent(self.info.infohash, self.data_dir, cfg, info=self.info, trackers=self.trackers, dht=self.dht)
+        await t.start()
+        await t.download_all()
+        assert t.complete.is_set(), "seeder data does not verify"
+        if self.corrupt:
+            orig = t._on_request
+
+            async def bad(p, pl):  # flip bytes in every served block
+                i, off, n = struct.unpack(">III", pl[:12])
+                data = await asyncio.get_running_loop().run_in_executor(None, t.storage.read, i, off, n)
+                p.wire.piece(i, off, bytes(x ^ 0xFF for x in data))
+            t._on_request = bad  # type: ignore[assignment]
+            _ = orig
+        self.torrent = t
+        return self
+
+    @property
+    def addr(self) -> tuple[str, int]:
+        assert self.torrent is not None
+        return ("127.0.0.1", self.torrent.port)
+
+    async def stop(self) -> None:
+        if self.torrent is not None:
+            await self.torrent.close()
+        if self.dht is not None:
+            self.dht.stop()
+
+
+def make_payload(root: str, files: dict[str, int], seed: int = 7) -> None:
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    for rel, n in files.items():
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
+
+
+def torrent_for(path: str, piece_length: int = 256 * 1024) -> Info:
+    return make_info(path, piece_length)
+
+
+def magnet_for(info: Info, trackers: list[str] | None = None, peers: list[tuple[str, int]] | None = None) -> str:
+    return Magnet(info.infohash, info.name, trackers or [], peers or []).uri()
+
+
+def torrent_file_bytes(info: Info, trackers: list[str] | None = None) -> bytes:
+    return Metainfo(info, [[t] for t in (trackers or [])]).encode()

@@ -1,0 +1,148 @@
+"""BitTorrent downloader plug-in — reference component C7
+(``internal/downloader/torrent/torrent.go``).
+
+Registration: name ``torrent``, protocol ``magnet``, extension ``.torrent``
+(``torrent.go:26-36``).  ``download``: a fresh client per call rooted at the
+job dir ("to prevent state leakage", ``:43``); add the magnet; wait ≤ 10 min
+for metadata (``failed to get metadata``; cancellable, ``:66-76``); download
+everything; report ``BytesCompleted / TotalLength * 100`` every second
+(``:82-101``); wait for completion; final 100 (``:110-113``).
+
+Fixes: ``.torrent`` URLs over http(s) — which the reference routed here by
+extension and then rejected as ``unsupported scheme`` (defect B3) — are
+fetched and started from their metainfo; waiting for completion honours
+cancellation (B9: anacrolix ``WaitAll`` did not).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+from urllib.parse import urlparse
+
+import aiohttp
+
+from ...utils.log import log
+from ..registry import ClientRegister, ProgressSink
+from .dht import DHTNode
+from .metainfo import Magnet, Metainfo, MetainfoError, parse_magnet
+from .torrent import Torrent, TorrentConfig
+
+
+class TorrentError(Exception):
+    pass
+
+
+def _parse_hostports(s: str) -> list[tuple[str, int]]:
+    out = []
+    for part in (s or "").split(","):
+        part = part.strip()
+        if not part:
+            continue
+        h, _, p = part.rpartition(":")
+        if h and p.isdigit():
+            out.append((h, int(p)))
+    return out
+
+
+class TorrentDownloader:
+    def __init__(self, cfg: TorrentConfig | None = None, *, metadata_timeout: float = 600.0,
+                 progress_interval: float = 1.0, use_dht: bool = True,
+                 dht_bootstrap: list[tuple[str, int]] | None = None, extra_trackers: list[str] | None = None,
+                 http_session: aiohttp.ClientSession | None = None) -> None:
+        self.cfg = cfg or TorrentConfig()
+        self.metadata_timeout = metadata_timeout
+        self.progress_interval = progress_interval
+        self.use_dht = use_dht
+        self.dht_bootstrap = dht_bootstrap or []
+        self.extra_trackers = extra_trackers or []
+        self._http = http_session
+
+    @classmethod
+    def from_config(cls, c, http=None) -> "TorrentDownloader":
+        tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, verify_device=c.gpu_verify
+                           if c.gpu_verify in ("auto", "cpu", "gpu") else ("cpu" if c.gpu_verify == "off" else "auto"))
+        return cls(tc, metadata_timeout=c.metadata_timeout_s, progress_interval=c.progress_interval_s,
+                   use_dht=c.bt_dht, dht_bootstrap=_parse_hostports(c.bt_bootstrap))
+
+    def register(self) -> ClientRegister:
+        return ClientRegister(name="torrent", protocols=["magnet"], file_extensions=[".torrent"])
+
+    async def _fetch_torrent_file(self, url: str) -> bytes:
+        own = self._http is None
+        s = self._http or aiohttp.ClientSession()
+        try:
+            async with s.get(url, timeout=aiohttp.ClientTimeout(total=120)) as r:
+                if r.status != 200:
+                    raise TorrentError(f"failed to fetch torrent file: HTTP {r.status}")
+                data = await r.content.read(16 * 1024 * 1024 + 1)
+                if len(data) > 16 * 1024 * 1024:
+                    raise TorrentError("torrent file too large")
+                return data
+        except aiohttp.ClientError as e:
+            raise TorrentError(f"failed to fetch torrent file: {e}") from e
+        finally:
+            if own:
+                await s.close()
+
+    async def open(self, base_dir: str, url: str) -> tuple[Torrent, DHTNode | None]:
+        u = urlparse(url)
+        info = None
+        trackers: list[str] = list(self.extra_trackers)
+        peers: list[tuple[str, int]] = []
+        name = ""
+        if u.scheme == "magnet":
+            try:
+                m: Magnet = parse_magnet(url)
+            except MetainfoError as e:
+                raise TorrentError(f"failed to add torrent: {e}") from e
+            ih, trackers, peers, name = m.infohash, trackers + m.trackers, m.peers, m.display_name
+        elif u.scheme in ("http", "https"):
+            try:
+                mi = Metainfo.parse(await self._fetch_torrent_file(url))
+            except MetainfoError as e:
+                raise TorrentError(f"failed to add torrent: {e}") from e
+            ih, info = mi.infohash, mi.info
+            trackers += [t for tier in mi.announce for t in tier]
+        else:
+            raise TorrentError(f"unsupported scheme '{u.scheme}'")
+        dht = None
+        if self.use_dht:
+            dht = await DHTNode(bootstrap=self.dht_bootstrap).start()
+            asyncio.ensure_future(dht.bootstrap())
+        t = Torrent(ih, base_dir, self.cfg, info=info, trackers=trackers, peers=peers, dht=dht, name_hint=name)
+        await t.start()
+        return t, dht
+
+    async def download(self, base_dir: str, progress: ProgressSink, url: str) -> None:
+        t, dht = await self.open(base_dir, url)
+        stop = asyncio.Event()
+        rep: asyncio.Task | None = None
+        try:
+            log.info("fetching torrent metadata")
+            try:
+                await asyncio.wait_for(t.got_info.wait(), self.metadata_timeout)
+            except asyncio.TimeoutError as e:
+                raise TorrentError("failed to get metadata") from e
+            log.info("fetched torrent metadata")
+            await t.download_all()
+            total = t.info.total_length if t.info else 0
+
+            async def reporter() -> None:
+                while not stop.is_set():
+                    await asyncio.sleep(self.progress_interval)
+                    progress(url, (t.bytes_completed() / total * 100) if total else 100.0)
+
+            rep = asyncio.ensure_future(reporter())
+            log.info("waiting for torrent download")
+            await t.complete.wait()
+            progress(url, 100)
+        finally:
+            stop.set()
+            if rep is not None:
+                rep.cancel()
+                with contextlib.suppress(BaseException):
+                    await rep
+            await t.close()
+            if dht is not None:
+                dht.stop()

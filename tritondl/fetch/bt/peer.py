@@ -1,0 +1,204 @@
+"""BitTorrent peer wire protocol: handshake + messages (BEP 3), Fast
+extension subset (BEP 6: have_all / have_none / reject), extension protocol
+(BEP 10) and ut_metadata (BEP 9).
+
+Transport-agnostic: works over any asyncio (reader, writer) pair — TCP, or
+the native uTP transport (:mod:`tritondl.fetch.bt.utp`).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import struct
+from dataclasses import dataclass, field
+
+from . import bencode
+
+PSTR = b"BitTorrent protocol"
+HANDSHAKE_LEN = 49 + len(PSTR)
+
+CHOKE, UNCHOKE, INTERESTED, NOT_INTERESTED, HAVE, BITFIELD, REQUEST, PIECE, CANCEL, PORT = range(10)
+SUGGEST, HAVE_ALL, HAVE_NONE, REJECT, ALLOWED_FAST = 0x0D, 0x0E, 0x0F, 0x10, 0x11
+EXTENDED = 20
+EXT_HANDSHAKE = 0
+UT_METADATA_ID = 3            # the id WE assign to ut_metadata in our extended handshake
+META_REQUEST, META_DATA, META_REJECT = 0, 1, 2
+MAX_MSG = 2 * 1024 * 1024 + 13
+
+
+def reserved_bytes(dht: bool = True, fast: bool = True, extended: bool = True) -> bytes:
+    r = bytearray(8)
+    if extended:
+        r[5] |= 0x10
+    if fast:
+        r[7] |= 0x04
+    if dht:
+        r[7] |= 0x01
+    return bytes(r)
+
+
+class PeerError(Exception):
+    pass
+
+
+@dataclass
+class Handshake:
+    reserved: bytes
+    infohash: bytes
+    peer_id: bytes
+
+    @property
+    def extended(self) -> bool:
+        return bool(self.reserved[5] & 0x10)
+
+    @property
+    def fast(self) -> bool:
+        return bool(self.reserved[7] & 0x04)
+
+    @property
+    def dht(self) -> bool:
+        return bool(self.reserved[7] & 0x01)
+
+
+def encode_handshake(infohash: bytes, peer_id: bytes, reserved: bytes | None = None) -> bytes:
+    return bytes([len(PSTR)]) + PSTR + (reserved or reserved_bytes()) + infohash + peer_id
+
+
+async def read_handshake(reader: asyncio.StreamReader) -> Handshake:
+    b = await reader.readexactly(HANDSHAKE_LEN)
+    if b[0] != len(PSTR) or b[1:20] != PSTR:
+        raise PeerError("bad protocol string in handshake")
+    return Handshake(b[20:28], b[28:48], b[48:68])
+
+
+@dataclass
+class ExtHandshake:
+    m: dict[str, int] = field(default_factory=dict)
+    metadata_size: int | None = None
+    reqq: int | None = None
+    v: str = ""
+    port: int | None = None
+
+
+class Wire:
+    """Framed message reader/writer over one connection."""
+
+    def __init__(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        self.reader = reader
+        self.writer = writer
+        self.closed = False
+
+    async def read(self) -> tuple[int, bytes] | None:
+        """Next message as (id, payload); None for keep-alive."""
+        hdr = await self.reader.readexactly(4)
+        (n,) = struct.unpack(">I", hdr)
+        if n == 0:
+            return None
+        if n > MAX_MSG:
+            raise PeerError(f"message too large ({n})")
+        body = await self.reader.readexactly(n)
+        return body[0], body[1:]
+
+    def send(self, mid: int, payload: bytes = b"") -> None:
+        if self.closed:
+            return
+        self.writer.write(struct.pack(">IB", len(payload) + 1, mid) + payload)
+
+    def send_raw(self, data: bytes) -> None:
+        if not self.closed:
+            self.writer.write(data)
+
+    def keepalive(self) -> None:
+        if not self.closed:
+            self.writer.write(b"\x00\x00\x00\x00")
+
+    async def drain(self) -> None:
+        await self.writer.drain()
+
+    # -- typed senders ------------------------------------------------------
+    def have(self, i: int) -> None:
+        self.send(HAVE, struct.pack(">I", i))
+
+    def bitfield(self, bits: bytes) -> None:
+        self.send(BITFIELD, bits)
+
+    def request(self, i: int, off: int, n: int) -> None:
+        self.send(REQUEST, struct.pack(">III", i, off, n))
+
+    def cancel(self, i: int, off: int, n: int) -> None:
+        self.send(CANCEL, struct.pack(">III", i, off, n))
+
+    def reject(self, i: int, off: int, n: int) -> None:
+        self.send(REJECT, struct.pack(">III", i, off, n))
+
+    def piece(self, i: int, off: int, data: bytes) -> None:
+        if not self.closed:
+            self.writer.write(struct.pack(">IBII", len(data) + 9, PIECE, i, off))
+            self.writer.write(data)
+
+    def extended(self, ext_id: int, payload: bytes) -> None:
+        self.send(EXTENDED, bytes([ext_id]) + payload)
+
+    def ext_handshake(self, metadata_size: int | None, port: int | None = None, reqq: int = 512) -> None:
+        d: dict = {b"m": {b"ut_metadata": UT_METADATA_ID}, b"v": b"tritondl/0.1", b"reqq": reqq}
+        if metadata_size:
+            d[b"metadata_size"] = metadata_size
+        if port:
+            d[b"p"] = port
+        self.extended(EXT_HANDSHAKE, bencode.encode(d))
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            try:
+                self.writer.close()
+            except Exception:
+                pass
+
+
+def parse_ext_handshake(payload: bytes) -> ExtHandshake:
+    try:
+        d = bencode.decode(payload, allow_trailing=True)
+    except bencode.BencodeError as e:
+        raise PeerError(f"bad extended handshake: {e}") from e
+    if not isinstance(d, dict):
+        raise PeerError("extended handshake is not a dict")
+    m = {}
+    for k, v in (d.get(b"m") or {}).items():
+        if isinstance(v, int):
+            m[k.decode(errors="replace")] = v
+    ms = d.get(b"metadata_size")
+    return ExtHandshake(m, ms if isinstance(ms, int) and ms > 0 else None,
+                        d.get(b"reqq") if isinstance(d.get(b"reqq"), int) else None,
+                        (d.get(b"v") or b"").decode(errors="replace") if isinstance(d.get(b"v"), bytes) else "",
+                        d.get(b"p") if isinstance(d.get(b"p"), int) else None)
+
+
+def meta_msg(msg_type: int, piece: int, total_size: int | None = None, data: bytes = b"") -> bytes:
+    d: dict = {b"msg_type": msg_type, b"piece": piece}
+    if total_size is not None:
+        d[b"total_size"] = total_size
+    return bencode.encode(d) + data
+
+
+def parse_meta_msg(payload: bytes) -> tuple[dict, bytes]:
+    d, n = bencode.decode_prefix(payload)
+    if not isinstance(d, dict):
+        raise PeerError("bad ut_metadata message")
+    return d, payload[n:]
+
+
+def bits_to_set(bits: bytes, n: int) -> set[int]:
+    out = set()
+    for i in range(n):
+        if bits[i >> 3] & (0x80 >> (i & 7)):
+            out.add(i)
+    return out
+
+
+def set_to_bits(have: set[int] | list[bool], n: int) -> bytes:
+    b = bytearray((n + 7) // 8)
+    it = have if isinstance(have, set) else {i for i, v in enumerate(have) if v}
+    for i in it:
+        b[i >> 3] |= 0x80 >> (i & 7)
+    return bytes(b)

@@ -1,0 +1,637 @@
+"""One torrent's swarm session: peer discovery, metadata exchange, piece
+picking, block pipelining, verification, storage and seeding.
+
+This is the capability of the ~10 anacrolix/torrent calls the reference makes
+(``internal/downloader/torrent/torrent.go:40-106``: NewClient with file
+storage, AddMagnet, GotInfo, DownloadAll, BytesCompleted, Info().TotalLength,
+WaitAll, Close), implemented from the BEPs:
+
+* discovery: magnet ``x.pe`` peers, every tracker (HTTP / UDP), the DHT
+  (``get_peers`` + ``announce_peer``), and inbound connections on our
+  listen port;
+* metadata (magnet → info dict) over ut_metadata, verified against the
+  info-hash;
+* rarest-first piece picking with an end-game mode; up to ``pipeline``
+  outstanding 16 KiB block requests per unchoked peer;
+* every completed piece is SHA-1 verified (worker thread) before it is
+  written and announced with HAVE; peers sending bad data are dropped;
+* we serve requests from interested peers while downloading (and after, if
+  ``seed``), like anacrolix's default client;
+* resume: existing data is batch-verified at start (HIP kernel when a GPU
+  helps, see :mod:`.storage`), so a redelivered job continues.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import hashlib
+import math
+import os
+import random
+import struct
+import time
+from dataclasses import dataclass, field
+
+from ...utils.log import log
+from . import peer as pw
+from .dht import DHTNode
+from .metainfo import BLOCK, Info, MetainfoError
+from .storage import CompletionDB, FileStorage
+from .tracker import Announce, TrackerError, announce, new_peer_id
+
+
+@dataclass
+class TorrentConfig:
+    max_peers: int = 60
+    pipeline: int = 128
+    listen_host: str = "0.0.0.0"
+    listen_port: int = 0
+    announce_host: str | None = None
+    seed: bool = False
+    request_timeout: float = 20.0
+    connect_timeout: float = 5.0
+    verify_device: str = "auto"
+    tracker_min_interval: float = 30.0
+    dht_interval: float = 60.0
+    max_bad_pieces: int = 3
+    utp: bool = False
+
+
+@dataclass
+class _Piece:
+    size: int
+    nblocks: int
+    buf: bytearray
+    received: set = field(default_factory=set)            # block indexes
+    requested: dict = field(default_factory=dict)          # block idx -> set(peer keys)
+
+
+class _Peer:
+    def __init__(self, wire: pw.Wire, addr: tuple[str, int], hs: pw.Handshake, n: int) -> None:
+        self.wire = wire
+        self.addr = addr
+        self.hs = hs
+        self.key = addr
+        self.have = bytearray(n)
+        self.nhave = 0
+        self.peer_choking = True
+        self.peer_interested = False
+        self.am_interested = False
+        self.ext: pw.ExtHandshake | None = None
+        self.outstanding: dict[tuple[int, int], float] = {}
+        self.bad = 0
+        self.downloaded = 0
+        self.meta_requested = False
+
+    def set_have(self, i: int) -> bool:
+        if 0 <= i < len(self.have) and not self.have[i]:
+            self.have[i] = 1
+            self.nhave += 1
+            return True
+        return False
+
+
+class Torrent:
+    def __init__(self, infohash: bytes, base_dir: str, cfg: TorrentConfig | None = None, *,
+                 info: Info | None = None, trackers: list[str] | None = None,
+                 peers: list[tuple[str, int]] | None = None, dht: DHTNode | None = None,
+                 peer_id: bytes | None = None, name_hint: str = "") -> None:
+        self.infohash = infohash
+        self.base_dir = base_dir
+        self.cfg = cfg or TorrentConfig()
+        self.trackers = list(trackers or [])
+        self.static_peers = list(peers or [])
+        self.dht = dht
+        self.peer_id = peer_id or new_peer_id()
+        self.name_hint = name_hint
+        self.info: Info | None = None
+        self.storage: FileStorage | None = None
+        self.db: CompletionDB | None = None
+        self.have = bytearray()
+        self.nhave = 0
+        self.avail: list[int] = []
+        self.pieces: dict[int, _Piece] = {}
+        self.peers: dict[tuple[str, int], _Peer] = {}
+        self.known: set[tuple[str, int]] = set()
+        self.connecting: set[tuple[str, int]] = set()
+        self.banned: set[tuple[str, int]] = set()
+        self.got_info = asyncio.Event()
+        self.complete = asyncio.Event()
+        self._downloading = False
+        self._meta_size: int | None = None
+        self._meta: dict[int, bytes] = {}
+        self._tasks: set[asyncio.Task] = set()
+        self._server: asyncio.AbstractServer | None = None
+        self.port = 0
+        self.uploaded = 0
+        self.downloaded = 0
+        self.closed = False
+        self._wake = asyncio.Event()
+        if info is not None:
+            self._set_info(info)
+
+    # ------------------------------------------------------------ lifecycle
+    def _spawn(self, coro) -> asyncio.Task:
+        t = asyncio.ensure_future(coro)
+        self._tasks.add(t)
+        t.add_done_callback(self._tasks.discard)
+        return t
+
+    async def start(self) -> None:
+        self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
+        self.port = self._server.sockets[0].getsockname()[1]
+        for p in self.static_peers:
+            self.add_peer_addr(p)
+        for url in self.trackers:
+            self._spawn(self._tracker_loop(url))
+        if self.dht is not None:
+            self._spawn(self._dht_loop())
+        self._spawn(self._timeout_loop())
+
+    async def close(self) -> None:
+        if self.closed:
+            return
+        self.closed = True
+        if self._server is not None:
+            self._server.close()
+        for p in list(self.peers.values()):
+            p.wire.close()
+        for t in list(self._tasks):
+            t.cancel()
+        for t in list(self._tasks):
+            with contextlib.suppress(BaseException):
+                await t
+        if self.storage is not None:
+            self.storage.close()
+        if self.db is not None:
+            self.db.close()
+        if self._server is not None:
+            with contextlib.suppress(Exception):
+                await self._server.wait_closed()
+
+    # ------------------------------------------------------------ info / storage
+    def _set_info(self, info: Info) -> None:
+        if info.infohash != self.infohash:
+            raise MetainfoError("info dict does not match info-hash")
+        self.info = info
+        n = info.num_pieces
+        self.have = bytearray(n)
+        self.avail = [0] * n
+        for p in self.peers.values():
+            p.have = bytearray(n) if len(p.have) != n else p.have
+        self.got_info.set()
+
+    async def download_all(self) -> None:
+        """Open storage, verify existing data (resume), start fetching all pieces."""
+        assert self.info is not None
+        os.makedirs(self.base_dir, exist_ok=True)
+        self.db = CompletionDB(os.path.join(self.base_dir, ".torrent.db"))
+        self.storage = FileStorage(self.base_dir, self.info, self.db)
+        self.storage.open()
+        loop = asyncio.get_running_loop()
+        have = await loop.run_in_executor(None, self.storage.verify_existing, self.cfg.verify_device)
+        for i in have:
+            self.have[i] = 1
+        self.nhave = len(have)
+        self._downloading = True
+        if self.nhave == self.info.num_pieces:
+            self.complete.set()
+        for p in list(self.peers.values()):
+            self._send_have_state(p)
+            self._update_interest(p)
+            self._fill(p)
+
+    def bytes_completed(self) -> int:
+        if self.info is None:
+            return 0
+        done = sum(self.info.piece_size(i) for i in range(self.info.num_pieces) if self.have[i])
+        partial = sum(len(pc.received) * BLOCK for pc in self.pieces.values())
+        return min(done + partial, self.info.total_length)
+
+    # ------------------------------------------------------------ discovery
+    def add_peer_addr(self, addr: tuple[str, int]) -> None:
+        if self.closed or addr in self.banned or addr[1] <= 0:
+            return
+        if addr in self.peers or addr in self.connecting:
+            return
+        if addr[1] == self.port and addr[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host):
+            return
+        self.known.add(addr)
+        if len(self.peers) + len(self.connecting) < self.cfg.max_peers:
+            self.connecting.add(addr)
+            self._spawn(self._connect(addr))
+
+    async def _tracker_loop(self, url: str) -> None:
+        event = "started"
+        while not self.closed:
+            left = (self.info.total_length - self.bytes_completed()) if self.info else 1 << 40
+            a = Announce(self.infohash, self.peer_id, self.port, self.uploaded, self.downloaded, left, event)
+            interval = self.cfg.tracker_min_interval
+            try:
+                res = await announce(url, a)
+                for p in res.peers:
+                    self.add_peer_addr(p)
+                interval = max(self.cfg.tracker_min_interval, min(res.interval, 1800))
+                event = ""
+            except (TrackerError, OSError) as e:
+                log.with_fields(tracker=url, error=str(e)).debug("tracker announce failed")
+            if self.complete.is_set() and event != "completed" and event == "":
+                with contextlib.suppress(TrackerError, OSError):
+                    await announce(url, Announce(self.infohash, self.peer_id, self.port, self.uploaded,
+                                                 self.downloaded, 0, "completed"))
+                event = "done"
+            await asyncio.sleep(interval if not self._starving() else min(interval, 5.0))
+
+    def _starving(self) -> bool:
+        return not self.peers
+
+    async def _dht_loop(self) -> None:
+        assert self.dht is not None
+        while not self.closed:
+            try:
+                for p in await self.dht.get_peers(self.infohash):
+                    self.add_peer_addr(p)
+                await self.dht.announce_peer(self.infohash, self.port)
+            except Exception as e:  # noqa: BLE001 - discovery is best-effort
+                log.with_field("error", str(e)).debug("dht lookup failed")
+            await asyncio.sleep(self.cfg.dht_interval if self.peers else min(self.cfg.dht_interval, 5.0))
+
+    # ------------------------------------------------------------ connections
+    async def _connect(self, addr: tuple[str, int]) -> None:
+        try:
+            reader, writer = await asyncio.wait_for(asyncio.open_connection(*addr), self.cfg.connect_timeout)
+        except (OSError, asyncio.TimeoutError):
+            self.connecting.discard(addr)
+            return
+        try:
+            writer.write(pw.encode_handshake(self.infohash, self.peer_id))
+            hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
+        except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError):
+            self.connecting.discard(addr)
+            writer.close()
+            return
+        self.connecting.discard(addr)
+        await self._run_peer(reader, writer, addr, hs)
+
+    async def _on_inbound(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        addr = writer.get_extra_info("peername")[:2]
+        try:
+            hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
+            if hs.infohash != self.infohash:
+                writer.close()
+                return
+            writer.write(pw.encode_handshake(self.infohash, self.peer_id))
+        except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError):
+            writer.close()
+            return
+        await self._run_peer(reader, writer, addr, hs)
+
+    async def _run_peer(self, reader, writer, addr, hs: pw.Handshake) -> None:
+        if hs.infohash != self.infohash or hs.peer_id == self.peer_id or addr in self.peers or self.closed:
+            writer.close()
+            return
+        n = self.info.num_pieces if self.info else 0
+        p = _Peer(pw.Wire(reader, writer), addr, hs, n)
+        self.peers[addr] = p
+        try:
+            if hs.extended:
+                p.wire.ext_handshake(len(self.info.raw) if self.info else None, self.port)
+            if self.info is not None and self._downloading:
+                self._send_have_state(p)
+            await self._peer_loop(p)
+        except (OSError, asyncio.IncompleteReadError, pw.PeerError, ConnectionError) as e:
+            log.with_fields(peer=f"{addr[0]}:{addr[1]}", error=str(e) or type(e).__name__).debug("peer closed")
+        finally:
+            self._drop_peer(p)
+
+    def _drop_peer(self, p: _Peer) -> None:
+        p.wire.close()
+        if self.peers.get(p.key) is p:
+            del self.peers[p.key]
+        if self.info is not None:
+            for i in range(len(p.have)):
+                if p.have[i] and i < len(self.avail):
+                    self.avail[i] -= 1
+        self._release(p)
+        # top up from known addresses
+        for a in list(self.known - set(self.peers) - self.connecting - self.banned)[:4]:
+            self.add_peer_addr(a)
+
+    def _release(self, p: _Peer) -> None:
+        for (i, off) in list(p.outstanding):
+            pc = self.pieces.get(i)
+            if pc is not None:
+                s = pc.requested.get(off // BLOCK)
+                if s is not None:
+                    s.discard(p.key)
+                    if not s:
+                        del pc.requested[off // BLOCK]
+        p.outstanding.clear()
+        for q in self.peers.values():
+            if q is not p:
+                self._fill(q)
+
+    def _send_have_state(self, p: _Peer) -> None:
+        assert self.info is not None
+        n = self.info.num_pieces
+        if p.hs.fast and self.nhave == n:
+            p.wire.send(pw.HAVE_ALL)
+        elif p.hs.fast and self.nhave == 0:
+            p.wire.send(pw.HAVE_NONE)
+        elif self.nhave:
+            p.wire.bitfield(pw.set_to_bits(list(map(bool, self.have)), n))
+        p.wire.send(pw.UNCHOKE)  # we unchoke everyone (no tit-for-tat needed for a leech/seed job)
+
+    # ------------------------------------------------------------ peer loop
+    async def _peer_loop(self, p: _Peer) -> None:
+        last = time.monotonic()
+        while not self.closed:
+            try:
+                m = await asyncio.wait_for(p.wire.read(), 120)
+            except asyncio.TimeoutError:
+                p.wire.keepalive()
+                continue
+            if m is None:
+                continue
+            mid, pl = m
+            if mid == pw.PIECE:
+                await self._on_block(p, pl)
+            elif mid == pw.HAVE:
+                (i,) = struct.unpack(">I", pl[:4])
+                self._peer_has(p, [i])
+            elif mid == pw.BITFIELD:
+                if self.info is not None:
+                    self._peer_has(p, sorted(pw.bits_to_set(pl, self.info.num_pieces)))
+                else:
+                    p.pending_bitfield = pl  # type: ignore[attr-defined]
+            elif mid == pw.HAVE_ALL:
+                if self.info is not None:
+                    self._peer_has(p, range(self.info.num_pieces))
+                else:
+                    p.pending_have_all = True  # type: ignore[attr-defined]
+            elif mid == pw.HAVE_NONE:
+                pass
+            elif mid == pw.UNCHOKE:
+                p.peer_choking = False
+                self._fill(p)
+            elif mid == pw.CHOKE:
+                p.peer_choking = True
+                if not p.hs.fast:
+                    self._release(p)
+            elif mid == pw.INTERESTED:
+                p.peer_interested = True
+            elif mid == pw.NOT_INTERESTED:
+                p.peer_interested = False
+            elif mid == pw.REQUEST:
+                await self._on_request(p, pl)
+            elif mid == pw.REJECT:
+                i, off, _n = struct.unpack(">III", pl[:12])
+                self._unrequest(p, i, off)
+                self._fill(p)
+            elif mid == pw.CANCEL:
+                pass
+            elif mid == pw.EXTENDED:
+                await self._on_extended(p, pl)
+            now = time.monotonic()
+            if now - last > 1.0:
+                last = now
+                await p.wire.drain()
+
+    def _peer_has(self, p: _Peer, idxs) -> None:
+        if self.info is None:
+            return
+        for i in idxs:
+            if p.set_have(i):
+                self.avail[i] += 1
+        self._update_interest(p)
+        self._fill(p)
+
+    def _update_interest(self, p: _Peer) -> None:
+        if self.info is None or not self._downloading:
+            return
+        want = any(p.have[i] and not self.have[i] for i in range(len(p.have))) if p.nhave else False
+        if want != p.am_interested:
+            p.am_interested = want
+            p.wire.send(pw.INTERESTED if want else pw.NOT_INTERESTED)
+
+    # ------------------------------------------------------------ requests
+    def _pick(self, p: _Peer) -> tuple[int, int, int] | None:
+        """Next (piece, offset, length) to request from p; None if nothing."""
+        assert self.info is not None
+        # 1) continue pieces already in progress
+        for i, pc in self.pieces.items():
+            if not p.have[i]:
+                continue
+            for b in range(pc.nblocks):
+                if b not in pc.received and b not in pc.requested:
+                    return i, b * BLOCK, min(BLOCK, pc.size - b * BLOCK)
+        # 2) start the rarest piece this peer has (random tie-break)
+        best, best_av = None, math.inf
+        n = self.info.num_pieces
+        start = random.randrange(n) if n else 0
+        for k in range(n):
+            i = (start + k) % n
+            if p.have[i] and not self.have[i] and i not in self.pieces and self.avail[i] < best_av:
+                best, best_av = i, self.avail[i]
+                if best_av <= 1:
+                    break
+        if best is not None:
+            size = self.info.piece_size(best)
+            pc = _Piece(size, -(-size // BLOCK), bytearray(size))
+            self.pieces[best] = pc
+            return best, 0, min(BLOCK, size)
+        # 3) end game: duplicate outstanding requests of other peers
+        for i, pc in self.pieces.items():
+            if not p.have[i]:
+                continue
+            for b, who in pc.requested.items():
+                if b not in pc.received and p.key not in who and len(who) < 3:
+                    return i, b * BLOCK, min(BLOCK, pc.size - b * BLOCK)
+        return None
+
+    def _fill(self, p: _Peer) -> None:
+        if self.info is None or not self._downloading or p.peer_choking or p.wire.closed:
+            return
+        while len(p.outstanding) < self.cfg.pipeline:
+            nxt = self._pick(p)
+            if nxt is None:
+                break
+            i, off, n = nxt
+            pc = self.pieces[i]
+            pc.requested.setdefault(off // BLOCK, set()).add(p.key)
+            p.outstanding[(i, off)] = time.monotonic()
+            p.wire.request(i, off, n)
+
+    def _unrequest(self, p: _Peer, i: int, off: int) -> None:
+        p.outstanding.pop((i, off), None)
+        pc = self.pieces.get(i)
+        if pc is not None:
+            s = pc.requested.get(off // BLOCK)
+            if s is not None:
+                s.discard(p.key)
+                if not s:
+                    del pc.requested[off // BLOCK]
+
+    async def _on_block(self, p: _Peer, pl: bytes) -> None:
+        i, off = struct.unpack(">II", pl[:8])
+        data = pl[8:]
+        p.outstanding.pop((i, off), None)
+        pc = self.pieces.get(i)
+        if pc is None or self.info is None or self.have[i]:
+            self._fill(p)
+            return
+        b = off // BLOCK
+        if off % BLOCK or b >= pc.nblocks or off + len(data) > pc.size:
+            raise pw.PeerError("bad block geometry")
+        if b not in pc.received:
+            pc.buf[off:off + len(data)] = data
+            pc.received.add(b)
+            p.downloaded += len(data)
+            self.downloaded += len(data)
+            # cancel duplicates (end game)
+            for other in pc.requested.pop(b, set()):
+                q = self.peers.get(other)
+                if q is not None and q is not p and (i, off) in q.outstanding:
+                    q.outstanding.pop((i, off), None)
+                    q.wire.cancel(i, off, len(data))
+        else:
+            pc.requested.pop(b, None)
+        if len(pc.received) == pc.nblocks:
+            del self.pieces[i]
+            await self._finish_piece(i, pc, p)
+        self._fill(p)
+
+    async def _finish_piece(self, i: int, pc: _Piece, src: _Peer) -> None:
+        assert self.info is not None and self.storage is not None
+        loop = asyncio.get_running_loop()
+        data = bytes(pc.buf)
+        expect = self.info.piece_hash(i)
+        st = self.storage
+
+        def verify_and_write() -> bool:
+            if hashlib.sha1(data).digest() != expect:
+                return False
+            st.write(i, 0, data)
+            return True
+
+        ok = await loop.run_in_executor(None, verify_and_write)
+        if not ok:
+            src.bad += 1
+            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
+            if src.bad >= self.cfg.max_bad_pieces:
+                self.banned.add(src.addr)
+                src.wire.close()
+            return
+        if self.have[i]:
+            return
+        self.have[i] = 1
+        self.nhave += 1
+        st.mark(i, True)
+        for q in list(self.peers.values()):
+            q.wire.have(i)
+            if q.am_interested and not any(q.have[k] and not self.have[k] for k in range(len(q.have))):
+                q.am_interested = False
+                q.wire.send(pw.NOT_INTERESTED)
+        if self.nhave == self.info.num_pieces:
+            self.complete.set()
+
+    async def _on_request(self, p: _Peer, pl: bytes) -> None:
+        i, off, n = struct.unpack(">III", pl[:12])
+        if self.info is None or self.storage is None or i >= len(self.have) or not self.have[i] or \
+                n > 128 * 1024 or off + n > self.info.piece_size(i):
+            if p.hs.fast:
+                p.wire.reject(i, off, n)
+            return
+        loop = asyncio.get_running_loop()
+        data = await loop.run_in_executor(None, self.storage.read, i, off, n)
+        p.wire.piece(i, off, data)
+        self.uploaded += len(data)
+
+    async def _timeout_loop(self) -> None:
+        while not self.closed:
+            await asyncio.sleep(2.0)
+            now = time.monotonic()
+            for p in list(self.peers.values()):
+                stale = [k for k, t in p.outstanding.items() if now - t > self.cfg.request_timeout]
+                if stale and len(stale) == len(p.outstanding):
+                    for (i, off) in stale:
+                        self._unrequest(p, i, off)
+                    p.peer_choking = True  # treat as snubbed until it sends something
+                    for q in self.peers.values():
+                        if q is not p:
+                            self._fill(q)
+            # metadata retry
+            if self.info is None:
+                for p in self.peers.values():
+                    if p.ext and "ut_metadata" in p.ext.m and self._meta_size:
+                        self._request_metadata(p)
+
+    # ------------------------------------------------------------ extensions
+    async def _on_extended(self, p: _Peer, pl: bytes) -> None:
+        if not pl:
+            return
+        eid, body = pl[0], pl[1:]
+        if eid == pw.EXT_HANDSHAKE:
+            p.ext = pw.parse_ext_handshake(body)
+            if self.info is None and "ut_metadata" in p.ext.m and p.ext.metadata_size:
+                if self._meta_size is None and 0 < p.ext.metadata_size < 16 * 1024 * 1024:
+                    self._meta_size = p.ext.metadata_size
+                self._request_metadata(p)
+            return
+        if eid == pw.UT_METADATA_ID:
+            d, data = pw.parse_meta_msg(body)
+            t, piece = d.get(b"msg_type"), d.get(b"piece")
+            if t == pw.META_REQUEST:
+                their = (p.ext.m.get("ut_metadata") if p.ext else None)
+                if not their:
+                    return
+                if self.info is None or not isinstance(piece, int) or piece * BLOCK >= len(self.info.raw):
+                    p.wire.extended(their, pw.meta_msg(pw.META_REJECT, piece or 0))
+                else:
+                    raw = self.info.raw
+                    p.wire.extended(their, pw.meta_msg(pw.META_DATA, piece, len(raw),
+                                                       raw[piece * BLOCK:(piece + 1) * BLOCK]))
+            elif t == pw.META_DATA and self.info is None and isinstance(piece, int):
+                self._meta[piece] = data
+                self._check_metadata()
+            elif t == pw.META_REJECT:
+                p.meta_requested = False
+
+    def _request_metadata(self, p: _Peer) -> None:
+        if self.info is not None or not self._meta_size or p.meta_requested or not p.ext:
+            return
+        their = p.ext.m.get("ut_metadata")
+        if not their:
+            return
+        p.meta_requested = True
+        for k in range(-(-self._meta_size // BLOCK)):
+            if k not in self._meta:
+                p.wire.extended(their, pw.meta_msg(pw.META_REQUEST, k))
+
+    def _check_metadata(self) -> None:
+        if self._meta_size is None:
+            return
+        n = -(-self._meta_size // BLOCK)
+        if len(self._meta) < n or any(k not in self._meta for k in range(n)):
+            return
+        raw = b"".join(self._meta[k] for k in range(n))[:self._meta_size]
+        if hashlib.sha1(raw).digest() != self.infohash:
+            log.warn("received metadata does not match info-hash; retrying")
+            self._meta.clear()
+            for p in self.peers.values():
+                p.meta_requested = False
+            return
+        try:
+            info = Info.parse(raw)
+        except MetainfoError as e:
+            log.warn("bad metadata: %s", e)
+            self._meta.clear()
+            return
+        self._set_info(info)
+        for p in self.peers.values():
+            pend = getattr(p, "pending_bitfield", None)
+            if pend is not None:
+                self._peer_has(p, sorted(pw.bits_to_set(pend, info.num_pieces)))
+            if getattr(p, "pending_have_all", False):
+                self._peer_has(p, range(info.num_pieces))
