@@ -50,7 +50,7 @@ class Env:
         for k, v in cfgkw.items():
             setattr(cfg, k, v)
         self.cfg = cfg
-        http = HTTPDownloader(progress_interval=0.05)
+        http = HTTPDownloader(progress_interval=0.05, max_retries=1)
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", tracker_min_interval=0.5,
                                              verify_device="cpu"), progress_interval=0.05, use_dht=False)
         self.svc = Service(cfg, amqp=Client(self.broker.url, heartbeat=0, retry_delay=0,
@@ -230,4 +230,34 @@ def test_cli_runs_and_writes_cpuprofile(tmp_path):
         assert prof.exists() and prof.stat().st_size > 0
         await s.stop()
         await b.stop()
+    run(main())
+
+
+def test_stream_upload_overlaps_and_fails_cleanly(tmp_path):
+    async def main():
+        e = await Env().up(tmp_path, max_retries=0)
+        data = os.urandom(6_000_000)
+        url = e.origin.add("/stream.mkv", data)
+        e.origin.rate = 20_000_000
+        seen_put_before_done = []
+        final = str(tmp_path / "downloading" / "s1" / "stream.mkv")
+
+        class Rec(list):
+            def append(self, x):
+                if x[0] == "PUT" and "s1" in x[1]:
+                    seen_put_before_done.append(not os.path.exists(final))
+                super().append(x)
+        e.s3.requests = Rec()
+        e.submit(Media(id="s1", source_uri=url))
+        res = await e.wait_results(1)
+        assert res[0].ok and e.s3.object_bytes("triton-staging", object_key("s1", "stream.mkv")) == data
+        assert seen_put_before_done == [True]   # the PUT started while the file was still .part
+        # a download that dies mid-way must not leave an object behind
+        url2 = e.origin.add("/dies.mkv", data)
+        e.origin.cut_after, e.origin.cut_times = 1_000_000, 100
+        e.submit(Media(id="s2", source_uri=url2))
+        res = await e.wait_results(2, timeout=60)
+        assert not res[1].ok
+        assert object_key("s2", "dies.mkv") not in e.s3.buckets["triton-staging"]
+        await e.down()
     run(main())

@@ -138,13 +138,20 @@ class HTTPDownloader:
 
     # ------------------------------------------------------------ download
     async def download(self, base_dir: str, progress: ProgressSink, url: str) -> None:
+        h = await self.start(base_dir, progress, url)
+        await h.wait()
+
+    async def start(self, base_dir: str, progress: ProgressSink, url: str) -> "DownloadHandle":
+        """Probe and start the transfer; returns a handle exposing the
+        destination, the size and a contiguous-bytes watermark so a consumer
+        (the streaming uploader) can read the file while it is written."""
         probe = await self._probe(url)
         dst = os.path.join(base_dir, probe.filename)
         part, meta_path = dst + ".part", dst + ".part.meta"
         if probe.size is not None and os.path.exists(dst) and os.path.getsize(dst) == probe.size:
             log.with_field("file", dst).info("file already downloaded; skipping")
             progress(url, 100)
-            return
+            return DownloadHandle.finished(dst, probe.size)
         validator = probe.etag or probe.last_modified
         segs = self._plan(probe)
         meta = self._load_meta(meta_path)
@@ -161,8 +168,14 @@ class HTTPDownloader:
                     os.ftruncate(fd, probe.size)
             finally:
                 os.close(fd)
+        h = DownloadHandle(dst, part, probe.size, segs)
+        h.task = asyncio.ensure_future(self._run(h, probe, url, validator, meta_path, progress))
+        return h
+
+    async def _run(self, h: "DownloadHandle", probe: _Probe, url: str, validator: str, meta_path: str,
+                   progress: ProgressSink) -> None:
+        segs, done = h.segs, h.done
         state = {"url": url, "validator": validator, "size": probe.size, "segments": segs}
-        done = [s[2] for s in segs]
         t0 = time.monotonic()
 
         def sync_save() -> None:
@@ -178,29 +191,33 @@ class HTTPDownloader:
                 progress(url, min(pct, 99.99))
                 sync_save()
 
-        fd = os.open(part, os.O_WRONLY)
+        fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
         try:
-            await asyncio.gather(*(self._fetch_segment(url, fd, i, segs, done, validator, probe)
+            await asyncio.gather(*(self._fetch_segment(url, fd, i, segs, done, validator, probe, h)
                                    for i in range(len(segs))))
-        except BaseException:
+        except BaseException as e:
             sync_save()
+            h._fail(e)
             raise
         finally:
             rep.cancel()
             os.close(fd)
         total = sum(done)
         if probe.size is not None and total != probe.size:
-            raise HTTPDownloadError(f"short download: {total} of {probe.size} bytes")
+            err = HTTPDownloadError(f"short download: {total} of {probe.size} bytes")
+            h._fail(err)
+            raise err
         if probe.size is None:
-            os.truncate(part, total)
-        os.replace(part, dst)
+            os.truncate(h.part, total)
+        os.replace(h.part, h.dst)
         try:
             os.remove(meta_path)
         except FileNotFoundError:
             pass
+        h._finish(total)
         dt = time.monotonic() - t0
-        log.with_fields(file=dst, bytes=total, mbps=round(total / max(dt, 1e-9) / 1e6, 1)).info("download finished")
+        log.with_fields(file=h.dst, bytes=total, mbps=round(total / max(dt, 1e-9) / 1e6, 1)).info("download finished")
         progress(url, 100)
 
     def _plan(self, p: _Probe) -> list[list[int]]:
@@ -230,7 +247,7 @@ class HTTPDownloader:
             pass
 
     async def _fetch_segment(self, url: str, fd: int, i: int, segs: list[list[int]], done: list[int],
-                             validator: str, probe: _Probe) -> None:
+                             validator: str, probe: _Probe, h: "DownloadHandle | None" = None) -> None:
         start, end, _ = segs[i]
         attempt = 0
         loop = asyncio.get_running_loop()
@@ -266,10 +283,14 @@ class HTTPDownloader:
                             wpos += nbuf
                             done[i] += nbuf
                             bufs, nbuf = [], 0
+                            if h is not None:
+                                h._progressed()
                     if bufs:
                         await loop.run_in_executor(None, _pwritev_all, fd, bufs, wpos)
                         wpos += nbuf
                         done[i] += nbuf
+                        if h is not None:
+                            h._progressed()
                     if end >= 0 and start + done[i] < end:
                         raise HTTPDownloadError("connection closed early")
                     return
@@ -281,6 +302,82 @@ class HTTPDownloader:
                 d = min(0.2 * 2 ** attempt, 5.0)
                 log.with_fields(error=str(e), attempt=attempt, segment=i).warn("download stream failed; retrying")
                 await asyncio.sleep(d)
+
+
+class DownloadHandle:
+    """A running (or finished) HTTP transfer.  ``watermark()`` is the length
+    of the contiguous prefix already on disk; ``wait_bytes(n)`` blocks until
+    n bytes are readable (or the transfer fails)."""
+
+    def __init__(self, dst: str, part: str, size: int | None, segs: list[list[int]]) -> None:
+        self.dst = dst
+        self.part = part
+        self.size = size
+        self.segs = segs
+        self.done = [s[2] for s in segs]
+        self.task: asyncio.Task | None = None
+        self._event = asyncio.Event()
+        self._error: BaseException | None = None
+        self._complete = False
+        self._read_fd: int | None = None
+
+    @classmethod
+    def finished(cls, dst: str, size: int) -> "DownloadHandle":
+        h = cls(dst, dst, size, [[0, size, size]])
+        h._complete = True
+        return h
+
+    @property
+    def filename(self) -> str:
+        return os.path.basename(self.dst)
+
+    def watermark(self) -> int:
+        if self._complete:
+            return self.size or 0
+        w = 0
+        for (start, end, _d), done in zip(self.segs, self.done):
+            w = start + done
+            if end < 0 or start + done < end:
+                break
+        return w
+
+    def _progressed(self) -> None:
+        self._event.set()
+
+    def _fail(self, e: BaseException) -> None:
+        self._error = e
+        self._event.set()
+
+    def _finish(self, total: int) -> None:
+        self.size = total
+        self._complete = True
+        self._event.set()
+
+    async def wait_bytes(self, n: int) -> None:
+        while self.watermark() < n:
+            if self._error is not None:
+                raise HTTPDownloadError(f"source transfer failed: {self._error}")
+            if self._complete:
+                raise HTTPDownloadError("source shorter than expected")
+            self._event.clear()
+            await self._event.wait()
+
+    def open_reader(self) -> int:
+        """An fd on the file being written (stays valid across the final rename)."""
+        if not self._complete:
+            try:
+                return os.open(self.part, os.O_RDONLY)
+            except FileNotFoundError:  # renamed to dst in between
+                pass
+        return os.open(self.dst, os.O_RDONLY)
+
+    async def wait(self) -> None:
+        if self.task is not None:
+            await self.task
+
+    def cancel(self) -> None:
+        if self.task is not None and not self.task.done():
+            self.task.cancel()
 
 
 def _pwritev_all(fd: int, bufs: list[bytes], pos: int) -> None:

@@ -205,23 +205,33 @@ class S3Client:
         await self._do("PUT", bucket, body=body if body is not None else b"", expect=(200,))
 
     # ------------------------------------------------------------ objects
-    async def put_object(self, bucket: str, key: str, src: str | bytes, size: int | None = None,
-                         content_type: str = "application/octet-stream") -> str:
-        """Upload a file path (streamed) or bytes; returns the ETag."""
-        if size is None:
-            size = len(src) if isinstance(src, (bytes, bytearray)) else os.path.getsize(src)
-        if size >= self.multipart_threshold and size > self.part_size:
-            return await self._put_multipart(bucket, key, src, size, content_type)
-        return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type})
+    async def put_object(self, bucket: str, key: str, src: str | bytes | int, size: int | None = None,
+                         content_type: str = "application/octet-stream", wait_bytes=None) -> str:
+        """Upload a file path or fd (streamed) or bytes; returns the ETag.
 
-    async def _put_range(self, bucket: str, key: str, src: str | bytes, offset: int, length: int,
-                         headers: dict, query: dict | None = None) -> str:
+        ``wait_bytes(n)`` (optional coroutine) is awaited before bytes < n are
+        read — lets the upload follow a file that is still being downloaded."""
+        if size is None:
+            if isinstance(src, (bytes, bytearray)):
+                size = len(src)
+            elif isinstance(src, int):
+                size = os.fstat(src).st_size
+            else:
+                size = os.path.getsize(src)
+        if size >= self.multipart_threshold and size > self.part_size:
+            return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes)
+        return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type},
+                                     wait_bytes=wait_bytes)
+
+    async def _put_range(self, bucket: str, key: str, src: str | bytes | int, offset: int, length: int,
+                         headers: dict, query: dict | None = None, wait_bytes=None) -> str:
         mode = self._payload_mode()
-        factory = _BodyFactory(self, src, offset, length, mode)
+        factory = _BodyFactory(self, src, offset, length, mode, wait_bytes)
         _st, rh, _b = await self._do("PUT", bucket, key, query=query, headers=headers, body_factory=factory)
         return rh.get("ETag", "").strip('"')
 
-    async def _put_multipart(self, bucket: str, key: str, src: str | bytes, size: int, content_type: str) -> str:
+    async def _put_multipart(self, bucket: str, key: str, src: str | bytes | int, size: int, content_type: str,
+                             wait_bytes=None) -> str:
         _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
                                        headers={"content-type": content_type}, body=b"")
         root = ET.fromstring(body)
@@ -237,7 +247,8 @@ class S3Client:
                 off = i * self.part_size
                 ln = min(self.part_size, size - off)
                 etags[i] = await self._put_range(bucket, key, src, off, ln, {},
-                                                 query={"partNumber": str(i + 1), "uploadId": upload_id})
+                                                 query={"partNumber": str(i + 1), "uploadId": upload_id},
+                                                 wait_bytes=wait_bytes)
         try:
             await asyncio.gather(*(one(i) for i in range(nparts)))
             xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
@@ -292,8 +303,9 @@ class _StreamBody:
     """Payload for one PUT: plain bytes, or an aws-chunked stream signed
     incrementally once the seed signature is known."""
 
-    def __init__(self, client: S3Client, src: str | bytes, offset: int, length: int, mode: str,
-                 scope: str = "", amzdate: str = "") -> None:
+    def __init__(self, client: S3Client, src: str | bytes | int, offset: int, length: int, mode: str,
+                 scope: str = "", amzdate: str = "", wait_bytes=None) -> None:
+        self.wait_bytes = wait_bytes
         self.client = client
         self.src = src
         self.offset = offset
@@ -332,7 +344,12 @@ class _StreamBody:
             assert self.signer is not None, "seed signature not bound"
         loop = asyncio.get_running_loop()
         blk = self.client.io_block
-        fd = None if isinstance(self.src, (bytes, bytearray, memoryview)) else os.open(self.src, os.O_RDONLY)
+        if isinstance(self.src, (bytes, bytearray, memoryview)):
+            fd = None
+        elif isinstance(self.src, int):
+            fd = os.dup(self.src)
+        else:
+            fd = os.open(self.src, os.O_RDONLY)
         q: asyncio.Queue = asyncio.Queue(maxsize=2)
 
         async def produce() -> None:
@@ -342,6 +359,8 @@ class _StreamBody:
                     await q.put(self.signer.finish())
                 while pos < end:
                     n = min(blk, end - pos)
+                    if self.wait_bytes is not None:
+                        await self.wait_bytes(pos + n)
                     out = await loop.run_in_executor(None, self._produce_block, fd, pos, n, pos + n >= end)
                     pos += n
                     if out:
@@ -368,14 +387,16 @@ class _StreamBody:
 class _BodyFactory:
     """Builds the body + payload hash + extra headers for each (re)try."""
 
-    def __init__(self, client: S3Client, src: str | bytes, offset: int, length: int, mode: str) -> None:
+    def __init__(self, client: S3Client, src: str | bytes | int, offset: int, length: int, mode: str,
+                 wait_bytes=None) -> None:
         self.client, self.src, self.offset, self.length, self.mode = client, src, offset, length, mode
+        self.wait_bytes = wait_bytes
 
     async def __call__(self, cred: Value, amzdate: str, host: str, path: str, query, hdrs):
         mode = self.mode
         if cred.anonymous and mode == "streaming":
             mode = "unsigned"  # chunk signatures need credentials
-        body = _StreamBody(self.client, self.src, self.offset, self.length, mode)
+        body = _StreamBody(self.client, self.src, self.offset, self.length, mode, wait_bytes=self.wait_bytes)
         if mode == "streaming":
             extra = {"content-encoding": "aws-chunked", "x-amz-decoded-content-length": str(self.length),
                      "content-length": str(sigv4.chunked_length(self.length))}
@@ -383,10 +404,13 @@ class _BodyFactory:
         extra = {"content-length": str(self.length)}
         if mode == "signed":
             loop = asyncio.get_running_loop()
+            if self.wait_bytes is not None:
+                await self.wait_bytes(self.offset + self.length)
             if isinstance(self.src, (bytes, bytearray)):
                 h = hashing.digest("sha256", memoryview(self.src)[self.offset:self.offset + self.length]).hex()
             else:
-                d = await loop.run_in_executor(None, hashing.hash_file, self.src, ["sha256"], self.offset,
+                path = f"/proc/self/fd/{self.src}" if isinstance(self.src, int) else self.src
+                d = await loop.run_in_executor(None, hashing.hash_file, path, ["sha256"], self.offset,
                                                self.length)
                 h = d["sha256"].hex()
             return body, h, extra

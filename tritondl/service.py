@@ -39,9 +39,9 @@ from .fetch.http import HTTPDownloader
 from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
 from .s3.uploader import Uploader
-from .select import dir_media
+from .select import MEDIA_EXTS, dir_media
 from .utils.config import Config
-from .utils.gocompat import go_time_string
+from .utils.gocompat import go_ext, go_time_string
 from .utils.log import log
 from .utils.metrics import Metrics, serve_metrics
 from .utils.profiler import CPUProfiler
@@ -160,14 +160,16 @@ class Service:
         try:
             assert self.dispatcher is not None and self.uploader is not None and self.amqp is not None
             t = time.monotonic()
-            dl_dir = await self.dispatcher.download(job.media.id, job.media.source_uri)
+            dl_dir, streamed = await self._download(job.media.id, job.media.source_uri)
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="download")
             stage = "select"
             files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
             log.info("found %d files", len(files))
             stage = "upload"
             t = time.monotonic()
-            res = await self.uploader.upload_files(job.media.id, dl_dir, files)
+            rest = [f for f in files if f not in streamed]
+            res = list(streamed.values()) + (await self.uploader.upload_files(job.media.id, dl_dir, rest)
+                                             if rest else [])
             nbytes = sum(r.size for r in res)
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="upload")
             stage = "publish"
@@ -191,6 +193,40 @@ class Service:
         self.metrics.inc("bytes_uploaded", nbytes)
         self.metrics.observe("job_seconds", dt)
         return self._record(JobResult(True, "done", files=len(files), bytes=nbytes, seconds=dt))
+
+    async def _download(self, media_id: str, url: str) -> tuple[str, dict]:
+        """Download the job's source.  For single-file HTTP sources whose file
+        the selector will pick (a top-level media file — the root is always
+        walked), the S3 upload is started right away and follows the download's
+        contiguous-bytes watermark, so fetch and upload overlap instead of
+        running back to back.  Returns (job dir, {path: UploadResult})."""
+        assert self.dispatcher is not None and self.uploader is not None
+        impl = self.dispatcher.select(url)
+        if not (self.cfg.stream_upload and isinstance(impl, HTTPDownloader)):
+            return await self.dispatcher.download(media_id, url), {}
+        d = self.dispatcher.job_dir(media_id)
+        os.makedirs(d, mode=0o755, exist_ok=True)
+        h = await impl.start(d, self.dispatcher.sink, url)
+        up: asyncio.Task | None = None
+        fd = None
+        if h.size and go_ext(h.filename) in MEDIA_EXTS:
+            fd = h.open_reader()
+            up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes))
+        try:
+            await h.wait()
+            if up is None:
+                return d, {}
+            return d, {h.dst: await up}
+        except BaseException:
+            h.cancel()
+            if up is not None:
+                up.cancel()
+                with contextlib.suppress(BaseException):
+                    await up
+            raise
+        finally:
+            if fd is not None:
+                os.close(fd)
 
     def _record(self, r: JobResult) -> JobResult:
         self.results.append(r)

@@ -49,6 +49,7 @@ class Config:
     retry_delay_s: float = 10.0                 # delivery.go:72
     dead_letter_topic: str = ""                 # "" => drop after max_retries (nack)
     cleanup: bool = False                       # B15: off for parity
+    stream_upload: bool = True                  # overlap HTTP fetch with S3 upload
 
     # --- download (downloader.go:81-93, torrent.go:67) ---
     download_dir: str = ""                      # default $CWD/downloading
@@ -122,6 +123,7 @@ class Config:
             if g("TRITONDL_" + k) is not None and g("TRITONDL_" + k) != "":
                 setattr(c, a, g("TRITONDL_" + k))
         c.cleanup = _env_bool(g("TRITONDL_CLEANUP"), c.cleanup)
+        c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
         if argv is not None:
