@@ -1,0 +1,82 @@
+"""Multi-process worker pool: competing consumers across processes, crash
+detection + restart with the crashed worker's job redelivered, topology."""
+
+import asyncio
+import os
+import signal
+import time
+
+from tritondl.amqp.codec import Properties
+from tritondl.fakes.broker import Broker
+from tritondl.fakes.origin import Origin
+from tritondl.fakes.s3 import FakeS3
+from tritondl.models import Download, Media
+from tritondl.parallel import WorkerPool, plan
+from tritondl.s3.uploader import object_key
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_plan_shapes():
+    p = plan(None, gpus=8, cpus=64)
+    assert len(p) == 8 and [w.gpu for w in p] == list(range(8)) and len(p[0].cpus) == 8
+    assert p[3].env()["HIP_VISIBLE_DEVICES"] == "3" and p[3].env()["RANK"] == "3"
+    q = plan(None, gpus=0, cpus=8, cpus_per_worker=2)
+    assert len(q) == 4 and q[0].gpu is None and q[0].env()["TRITONDL_GPU_VERIFY"] == "off"
+    r = plan(2, gpus=1, cpus=4, base_port=7000, node_rank=1, nnodes=2)
+    assert [w.rank for w in r] == [2, 3] and r[1].bt_listen_port == 7001 and r[0].world_size == 4
+
+
+def test_pool_competing_consumers_and_restart(tmp_path):
+    async def main():
+        b = await Broker().start()
+        o = await Origin().start()
+        s = await FakeS3().start()
+        o.rate = 8_000_000
+        env = {"RABBITMQ_ENDPOINT": b.endpoint, "RABBITMQ_USERNAME": "guest", "RABBITMQ_PASSWORD": "guest",
+               "S3_ENDPOINT": s.endpoint, "PYTHONPATH": ROOT, "TRITONDL_RETRY_DELAY": "0",
+               "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning", "TRITONDL_PROGRESS_LOG_INTERVAL": "0"}
+        pool = WorkerPool(plan(2, gpus=0, cpus=2), env=env, cwd=str(tmp_path), grace=10, backoff_initial=0.1)
+        await pool.start()
+        for _ in range(300):
+            qs = [b.queues.get(f"v1.download-{i}") for i in range(2)]
+            if all(q is not None and len(q.consumers) == 2 for q in qs):
+                break
+            await asyncio.sleep(0.05)
+        assert all(len(b.queues[f"v1.download-{i}"].consumers) == 2 for i in range(2))
+        users = {c.ch.conn for q in b.queues.values() for c in q.consumers}
+        assert len(users) == 2   # two worker processes, one connection each
+
+        def submit(i):
+            url = o.add(f"/j{i}.mkv", bytes([i]) * 800_000)
+            body = Download(created_at="t", media=Media(id=f"j{i}", source_uri=url)).encode()
+            b.inject("v1.download", f"v1.download-{i % 2}", body, Properties(delivery_mode=2))
+
+        for i in range(4):
+            submit(i)
+        await asyncio.sleep(0.15)
+        victim = pool.pids()[0]
+        os.kill(victim, signal.SIGKILL)     # crash one worker mid-job (by exact PID)
+        t0 = time.monotonic()
+        while True:
+            objs = s.buckets.get("triton-staging", {})
+            if all(object_key(f"j{i}", f"j{i}.mkv") in objs for i in range(4)):
+                break
+            assert time.monotonic() - t0 < 60, sorted(objs)
+            await asyncio.sleep(0.1)
+        for _ in range(100):
+            if len(pool.pids()) == 2 and victim not in pool.pids():
+                break
+            await asyncio.sleep(0.1)
+        assert len(pool.pids()) == 2 and victim not in pool.pids()   # restarted
+        assert any(rc == -signal.SIGKILL for _r, rc in pool.exits)
+        for _ in range(300):   # the restarted worker is back on both shard queues
+            if all(len(b.queues[f"v1.download-{i}"].consumers) == 2 for i in range(2)):
+                break
+            await asyncio.sleep(0.05)
+        await pool.stop()
+        assert all(rc == 0 for _r, rc in pool.exits if rc != -signal.SIGKILL)
+        await s.stop()
+        await o.stop()
+        await b.stop()
+    asyncio.run(asyncio.wait_for(main(), 120))

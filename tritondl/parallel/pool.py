@@ -1,0 +1,147 @@
+"""Multi-process worker pool with failure detection and restart.
+
+Each worker is a full ingest service process (``python -m tritondl``)
+consuming the same sharded queues — competing consumers, the reference's
+scale-out model — so jobs spread across workers and a
+crashed worker's unacked job is redelivered by the broker to a survivor.
+
+The supervisor:
+
+* starts N workers with per-worker env (rank, GPU, BT port, CPU affinity);
+* detects exits (any non-zero exit or signal death) and restarts the
+  worker with exponential backoff; a worker that crash-loops
+  (``max_restarts`` within ``restart_window``) is given up on;
+* on SIGTERM/SIGINT forwards SIGTERM to every worker, waits ``grace`` s,
+  then SIGKILLs stragglers — by PID, never by name.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import os
+import signal
+import sys
+import time
+from dataclasses import dataclass, field
+
+from ..utils.log import log
+from .topology import WorkerSpec, plan
+
+
+@dataclass
+class _Worker:
+    spec: WorkerSpec
+    proc: asyncio.subprocess.Process | None = None
+    restarts: list[float] = field(default_factory=list)
+    given_up: bool = False
+    started_at: float = 0.0
+
+
+class WorkerPool:
+    def __init__(self, specs: list[WorkerSpec], *, argv: list[str] | None = None, env: dict | None = None,
+                 max_restarts: int = 5, restart_window: float = 60.0, grace: float = 30.0,
+                 backoff_initial: float = 0.5, backoff_max: float = 30.0, cwd: str | None = None,
+                 module: str = "tritondl") -> None:
+        self.workers = [_Worker(s) for s in specs]
+        self.argv = argv or []
+        self.env = env or {}
+        self.max_restarts = max_restarts
+        self.restart_window = restart_window
+        self.grace = grace
+        self.backoff_initial = backoff_initial
+        self.backoff_max = backoff_max
+        self.cwd = cwd
+        self.module = module
+        self._stopping = False
+        self._tasks: list[asyncio.Task] = []
+        self.exits: list[tuple[int, int | None]] = []   # (rank, returncode)
+
+    async def _spawn(self, w: _Worker) -> None:
+        env = dict(os.environ)
+        env.update(self.env)
+        env.update(w.spec.env())
+        kw = {}
+        if w.spec.cpus and hasattr(os, "sched_setaffinity"):
+            cpus = set(w.spec.cpus)
+            kw["preexec_fn"] = lambda: os.sched_setaffinity(0, cpus)
+        w.proc = await asyncio.create_subprocess_exec(sys.executable, "-m", self.module, *self.argv, env=env,
+                                                      cwd=self.cwd, **kw)
+        w.started_at = time.monotonic()
+        log.with_fields(rank=w.spec.rank, pid=w.proc.pid, gpu=w.spec.gpu).info("worker started")
+
+    async def _watch(self, w: _Worker) -> None:
+        delay = self.backoff_initial
+        while not self._stopping:
+            await self._spawn(w)
+            assert w.proc is not None
+            rc = await w.proc.wait()
+            self.exits.append((w.spec.rank, rc))
+            if self._stopping:
+                return
+            now = time.monotonic()
+            if now - w.started_at > self.restart_window:
+                delay = self.backoff_initial  # it ran healthily for a while
+            w.restarts = [t for t in w.restarts if now - t < self.restart_window] + [now]
+            if len(w.restarts) > self.max_restarts:
+                w.given_up = True
+                log.with_fields(rank=w.spec.rank, rc=rc).error("worker is crash-looping; giving up on it")
+                return
+            log.with_fields(rank=w.spec.rank, rc=rc, restart_in=round(delay, 2)).warn("worker died; restarting")
+            await asyncio.sleep(delay)
+            delay = min(delay * 2, self.backoff_max)
+
+    async def start(self) -> None:
+        for w in self.workers:
+            self._tasks.append(asyncio.ensure_future(self._watch(w)))
+        # wait until every worker has a process
+        for _ in range(200):
+            if all(w.proc is not None for w in self.workers):
+                break
+            await asyncio.sleep(0.01)
+
+    def pids(self) -> list[int]:
+        return [w.proc.pid for w in self.workers if w.proc is not None and w.proc.returncode is None]
+
+    async def stop(self) -> None:
+        self._stopping = True
+        procs = [w.proc for w in self.workers if w.proc is not None and w.proc.returncode is None]
+        for p in procs:
+            with contextlib.suppress(ProcessLookupError):
+                p.send_signal(signal.SIGTERM)
+        try:
+            await asyncio.wait_for(asyncio.gather(*(p.wait() for p in procs)), self.grace)
+        except asyncio.TimeoutError:
+            for p in procs:
+                if p.returncode is None:
+                    with contextlib.suppress(ProcessLookupError):
+                        p.kill()
+            await asyncio.gather(*(p.wait() for p in procs))
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            with contextlib.suppress(BaseException):
+                await t
+
+    async def run_until_signalled(self) -> None:
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for s in (signal.SIGINT, signal.SIGTERM, signal.SIGHUP):
+            with contextlib.suppress(NotImplementedError, RuntimeError):
+                loop.add_signal_handler(s, stop.set)
+        await self.start()
+        await stop.wait()
+        await self.stop()
+
+
+def main(argv: list[str] | None = None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(prog="python -m tritondl.parallel",
+                                 description="run N competing ingest workers on this node")
+    ap.add_argument("--workers", type=int, default=None, help="default: one per GPU (or per 2 CPUs)")
+    ap.add_argument("--base-port", type=int, default=0, help="BitTorrent listen port of worker 0 (+rank)")
+    ap.add_argument("--grace", type=float, default=30.0)
+    a, rest = ap.parse_known_args(argv)
+    pool = WorkerPool(plan(a.workers, base_port=a.base_port), argv=rest, grace=a.grace)
+    asyncio.run(pool.run_until_signalled())
+    return 0

@@ -1,0 +1,69 @@
+"""Worker topology for one node: how many ingest workers to run and which
+GPU / CPU set each one gets.
+
+The reference scales by running more service replicas that compete for
+the sharded queues (job-level data parallelism, prefetch 1,
+one job per process).  On an MI355X node we run one worker per GPU by default
+(each owns that GPU for batch piece verification through
+``HIP_VISIBLE_DEVICES``), or one per ``cpus_per_worker`` CPUs on GPU-less
+hosts.  ``RANK`` / ``LOCAL_RANK`` / ``WORLD_SIZE`` follow torchrun's contract
+so a worker can also be launched by ``torch.distributed.run``.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+
+@dataclass
+class WorkerSpec:
+    rank: int
+    local_rank: int
+    world_size: int
+    gpu: int | None
+    cpus: list[int] = field(default_factory=list)
+    bt_listen_port: int = 0
+
+    def env(self) -> dict[str, str]:
+        e = {"RANK": str(self.rank), "LOCAL_RANK": str(self.local_rank), "WORLD_SIZE": str(self.world_size),
+             "TRITONDL_BT_LISTEN_PORT": str(self.bt_listen_port)}
+        if self.gpu is not None:
+            e["HIP_VISIBLE_DEVICES"] = str(self.gpu)
+        else:
+            e["TRITONDL_GPU_VERIFY"] = "off"
+        return e
+
+
+def detect_gpus() -> int:
+    """Number of visible HIP devices, without initialising a HIP runtime."""
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis:
+        return len([x for x in vis.split(",") if x.strip() != ""])
+    try:
+        return len([d for d in os.listdir("/dev/dri") if d.startswith("renderD")]) if os.path.exists(
+            "/sys/module/amdgpu") else 0
+    except OSError:
+        return 0
+
+
+def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | None = None,
+         cpus_per_worker: int = 2, base_port: int = 0, node_rank: int = 0, nnodes: int = 1) -> list[WorkerSpec]:
+    gpus = detect_gpus() if gpus is None else gpus
+    if cpus is None:
+        avail = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+            list(range(os.cpu_count() or 1))
+        cpus = len(avail)
+    else:
+        avail = list(range(cpus))
+    if workers is None:
+        workers = gpus if gpus > 0 else max(1, cpus // max(1, cpus_per_worker))
+    world = workers * nnodes
+    out = []
+    per = max(1, cpus // workers)
+    for i in range(workers):
+        gpu = (i % gpus) if gpus > 0 else None
+        cset = avail[i * per:(i + 1) * per] if cpus >= workers else []
+        out.append(WorkerSpec(node_rank * workers + i, i, world, gpu, cset,
+                              (base_port + i) if base_port else 0))
+    return out
