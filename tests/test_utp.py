@@ -1,0 +1,132 @@
+"""Native uTP (BEP 29): engine-level transfers over a simulated lossy FIFO
+link, the asyncio socket wrapper on localhost, and a BitTorrent download
+forced over uTP."""
+
+import asyncio
+import os
+import random
+
+import pytest
+
+from tritondl import _utp
+from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+from tritondl.fetch.bt.client import TorrentDownloader
+from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+from tritondl.fetch.bt.utp import UtpSocket
+
+
+def _simulate(loss: float, n: int, seed: int = 1, reorder: bool = False):
+    rnd = random.Random(seed)
+    a, b = _utp.Engine(seed), _utp.Engine(seed + 1)
+    now = 0
+    ca = a.connect("B", now)
+    data = rnd.randbytes(n)
+    sent, got, cb = 0, bytearray(), None
+    wire, last = [], {}
+    for _ in range(400_000):
+        now += 1000
+        if sent < n:
+            sent += a.write(ca, data[sent:sent + 65536])
+        elif sent == n:
+            a.close(ca, now)
+            sent += 1
+        for eng, name in ((a, "A"), (b, "B")):
+            for addr, pkt in eng.outgoing():
+                if rnd.random() < loss:
+                    continue
+                t = now + 5000 + rnd.randint(0, 3000 if reorder else 500)
+                if not reorder:
+                    t = max(t, last.get(name, 0))
+                    last[name] = t
+                wire.append((t, addr, pkt, name))
+        wire.sort(key=lambda x: x[0])
+        while wire and wire[0][0] <= now:
+            _, dst, pkt, src = wire.pop(0)
+            (b if dst == "B" else a).incoming(pkt, src, now)
+        for c in b.accepted():
+            cb = c
+        if cb is not None:
+            got += b.read(cb)
+            if b.eof(cb):
+                break
+        a.tick(now)
+        b.tick(now)
+    return bytes(got) == data, (cb is not None and b.eof(cb)), a.stats(ca)
+
+
+@pytest.mark.parametrize("loss,reorder", [(0.0, False), (0.03, False), (0.05, True)])
+def test_engine_reliable_in_order_delivery(loss, reorder):
+    ok, eof, st = _simulate(loss, 300_000, reorder=reorder)
+    assert ok and eof, st
+    if loss:
+        assert st["retransmits"] > 0
+
+
+def test_engine_rejects_garbage_and_resets_unknown():
+    e = _utp.Engine(3)
+    assert e.incoming(b"\x00" * 5, "X:1", 0) == -1
+    # DATA for an unknown connection -> we answer with a RESET
+    pkt = bytes([0x01, 0, 0x12, 0x34]) + b"\x00" * 16
+    assert e.incoming(pkt, "X:1", 0) == -1
+    out = e.outgoing()
+    assert out and out[0][1][0] >> 4 == 3
+
+
+def test_asyncio_socket_pair_transfer():
+    async def main():
+        srv = await UtpSocket().start("127.0.0.1", 0)
+        cli = await UtpSocket().start("127.0.0.1", 0)
+        data = os.urandom(3_000_000)
+
+        async def echo_len():
+            r, w, _ = await srv.accept()
+            got = await r.readexactly(len(data))
+            w.write(len(got).to_bytes(8, "big") + got[-16:])
+            await w.drain()
+            return got
+
+        t = asyncio.ensure_future(echo_len())
+        r, w = await cli.connect("127.0.0.1", srv.port)
+        w.write(data)
+        await w.drain()
+        resp = await asyncio.wait_for(r.readexactly(24), 30)
+        assert int.from_bytes(resp[:8], "big") == len(data) and resp[8:] == data[-16:]
+        assert await t == data
+        w.close()
+        cli.close()
+        srv.close()
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_utp_connect_timeout():
+    async def main():
+        cli = await UtpSocket().start("127.0.0.1", 0)
+        with pytest.raises(ConnectionError):
+            await cli.connect("127.0.0.1", 9, timeout=0.3)   # nothing listens there
+        cli.close()
+    asyncio.run(main())
+
+
+def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"film.mkv": 1_500_000})
+        info = torrent_for(str(src / "film.mkv"), 65536)
+        seed = Seeder(info, str(src))
+        cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, verify_device="cpu", utp=True)
+        st = Torrent(info.infohash, str(src), cfg, info=info)
+        await st.start()
+        await st.download_all()
+
+        async def no_tcp(self, addr):
+            raise OSError("tcp disabled for this test")
+        monkeypatch.setattr(Torrent, "_dial_tcp", no_tcp)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        dl = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", utp=True, verify_device="cpu"),
+                               progress_interval=0.05, use_dht=False)
+        await dl.download(str(dst), lambda u, p: None, magnet_for(info, peers=[("127.0.0.1", st.port)]))
+        assert (dst / "film.mkv").read_bytes() == (src / "film.mkv").read_bytes()
+        await st.close()
+        _ = seed
+    asyncio.run(asyncio.wait_for(main(), 60))

@@ -124,6 +124,7 @@ class Torrent:
         self._tasks: set[asyncio.Task] = set()
         self._server: asyncio.AbstractServer | None = None
         self.port = 0
+        self.utp = None
         self.uploaded = 0
         self.downloaded = 0
         self.closed = False
@@ -141,6 +142,14 @@ class Torrent:
     async def start(self) -> None:
         self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
         self.port = self._server.sockets[0].getsockname()[1]
+        if self.cfg.utp:
+            from .utp import UtpSocket
+            try:  # uTP shares the TCP port number, as anacrolix/libutp do
+                self.utp = await UtpSocket().start(self.cfg.listen_host, self.port)
+                self._spawn(self._utp_accept_loop())
+            except OSError as e:
+                log.with_field("error", str(e)).warn("uTP disabled: cannot bind UDP port")
+                self.utp = None
         for p in self.static_peers:
             self.add_peer_addr(p)
         for url in self.trackers:
@@ -149,12 +158,20 @@ class Torrent:
             self._spawn(self._dht_loop())
         self._spawn(self._timeout_loop())
 
+    async def _utp_accept_loop(self) -> None:
+        assert self.utp is not None
+        while not self.closed:
+            r, w, _addr = await self.utp.accept()
+            self._spawn(self._on_inbound(r, w))
+
     async def close(self) -> None:
         if self.closed:
             return
         self.closed = True
         if self._server is not None:
             self._server.close()
+        if self.utp is not None:
+            self.utp.close()
         for p in list(self.peers.values()):
             p.wire.close()
         for t in list(self._tasks):
@@ -258,20 +275,47 @@ class Torrent:
             await asyncio.sleep(self.cfg.dht_interval if self.peers else min(self.cfg.dht_interval, 5.0))
 
     # ------------------------------------------------------------ connections
-    async def _connect(self, addr: tuple[str, int]) -> None:
-        try:
-            reader, writer = await asyncio.wait_for(asyncio.open_connection(*addr), self.cfg.connect_timeout)
-        except (OSError, asyncio.TimeoutError):
-            self.connecting.discard(addr)
-            return
+    async def _dial_tcp(self, addr: tuple[str, int]):
+        return await asyncio.wait_for(asyncio.open_connection(*addr), self.cfg.connect_timeout)
+
+    async def _dial_utp(self, addr: tuple[str, int]):
+        assert self.utp is not None
+        return await self.utp.connect(addr[0], addr[1], self.cfg.connect_timeout)
+
+    async def _dial_and_handshake(self, dial, addr):
+        reader, writer = await dial(addr)
         try:
             writer.write(pw.encode_handshake(self.infohash, self.peer_id))
             hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
-        except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError):
-            self.connecting.discard(addr)
+        except BaseException:
             writer.close()
-            return
+            raise
+        return reader, writer, hs
+
+    async def _connect(self, addr: tuple[str, int]) -> None:
+        """Dial TCP and (if enabled) uTP concurrently; the first transport to
+        complete the BitTorrent handshake wins (anacrolix dials both too)."""
+        dials = [self._dial_tcp] + ([self._dial_utp] if self.utp is not None else [])
+        tasks = [asyncio.ensure_future(self._dial_and_handshake(d, addr)) for d in dials]
+        won = None
+        try:
+            for fut in asyncio.as_completed(tasks):
+                try:
+                    won = await fut
+                    break
+                except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError, ConnectionError):
+                    continue
+        finally:
+            for t in tasks:
+                if not t.done():
+                    t.cancel()
+            for t in tasks:
+                if t.done() and not t.cancelled() and t.exception() is None and t.result() is not won:
+                    t.result()[1].close()
         self.connecting.discard(addr)
+        if won is None:
+            return
+        reader, writer, hs = won
         await self._run_peer(reader, writer, addr, hs)
 
     async def _on_inbound(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:

@@ -1,0 +1,252 @@
+"""asyncio front-end for the native uTP engine (``tritondl._utp``, C++).
+
+One UDP socket per :class:`UtpSocket` multiplexes every uTP connection (as
+libutp / anacrolix do, sharing the BitTorrent listen port number).  Each
+connection is exposed as a standard ``(asyncio.StreamReader,
+asyncio.StreamWriter)`` pair, so the peer-wire code runs unchanged over TCP
+or uTP.  Python only moves datagrams and bytes; sequencing, SACK, RTO and
+LEDBAT live in C++.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import time
+
+try:
+    from ... import _utp  # type: ignore[attr-defined]
+except ImportError as e:  # pragma: no cover - built by tools/build_native.py
+    raise ImportError("tritondl native uTP extension is not built; run `python tools/build_native.py`") from e
+
+TICK = 0.01
+HIGH_WATER = 1 << 20
+
+
+def _now_us() -> int:
+    return time.monotonic_ns() // 1000
+
+
+def _key(addr: tuple[str, int]) -> str:
+    return f"{addr[0]}:{addr[1]}"
+
+
+def _addr(key: str) -> tuple[str, int]:
+    h, _, p = key.rpartition(":")
+    return h, int(p)
+
+
+class UtpError(ConnectionError):
+    pass
+
+
+class _UtpTransport(asyncio.Transport):
+    def __init__(self, sock: "UtpSocket", cid: int, peer: tuple[str, int]) -> None:
+        super().__init__()
+        self.sock = sock
+        self.cid = cid
+        self.peer = peer
+        self._closing = False
+        self._buf = bytearray()
+        self._protocol: asyncio.Protocol | None = None
+        self._paused = False
+
+    def get_extra_info(self, name, default=None):
+        if name == "peername":
+            return self.peer
+        if name == "sockname":
+            return self.sock.local_addr
+        if name == "socket":
+            return None
+        return default
+
+    def is_closing(self) -> bool:
+        return self._closing
+
+    def set_protocol(self, protocol) -> None:
+        self._protocol = protocol
+
+    def get_protocol(self):
+        return self._protocol
+
+    def write(self, data) -> None:
+        if self._closing:
+            return
+        self._buf += data
+        self._push()
+        self.sock._flush()
+
+    def _push(self) -> None:
+        eng = self.sock.engine
+        if self._buf:
+            n = eng.write(self.cid, bytes(self._buf[:HIGH_WATER]))
+            if n:
+                del self._buf[:n]
+        pend = len(self._buf) + eng.send_buffered(self.cid)
+        if self._protocol is not None:
+            if not self._paused and pend > 4 * HIGH_WATER:
+                self._paused = True
+                self._protocol.pause_writing()
+            elif self._paused and pend < HIGH_WATER:
+                self._paused = False
+                self._protocol.resume_writing()
+
+    def can_write_eof(self) -> bool:
+        return False
+
+    def get_write_buffer_size(self) -> int:
+        return len(self._buf) + self.sock.engine.send_buffered(self.cid)
+
+    def close(self) -> None:
+        if self._closing:
+            return
+        self._closing = True
+        if self._buf:
+            self.sock.engine.write(self.cid, bytes(self._buf))
+            self._buf.clear()
+        self.sock.engine.close(self.cid, _now_us())
+        self.sock.engine.forget(self.cid)
+        self.sock._flush()
+
+    def abort(self) -> None:
+        self._closing = True
+        self.sock.engine.abort(self.cid)
+        self.sock.engine.forget(self.cid)
+        self.sock._flush()
+
+
+class _Stream:
+    def __init__(self, sock: "UtpSocket", cid: int, peer: tuple[str, int]) -> None:
+        loop = asyncio.get_running_loop()
+        self.reader = asyncio.StreamReader(limit=1 << 22)
+        self.protocol = asyncio.StreamReaderProtocol(self.reader)
+        self.transport = _UtpTransport(sock, cid, peer)
+        self.transport.set_protocol(self.protocol)
+        self.protocol.connection_made(self.transport)
+        self.writer = asyncio.StreamWriter(self.transport, self.protocol, self.reader, loop)
+        self.connected = asyncio.Event()
+        self.eof = False
+
+
+class UtpSocket(asyncio.DatagramProtocol):
+    def __init__(self, seed: int = 0) -> None:
+        self.engine = _utp.Engine(seed)
+        self.transport: asyncio.DatagramTransport | None = None
+        self.streams: dict[int, _Stream] = {}
+        self.accept_q: asyncio.Queue = asyncio.Queue()
+        self.local_addr: tuple[str, int] = ("0.0.0.0", 0)
+        self._ticker: asyncio.Task | None = None
+        self.other_datagram = None   # optional handler for non-uTP datagrams (e.g. DHT on a shared port)
+
+    async def start(self, host: str = "0.0.0.0", port: int = 0) -> "UtpSocket":
+        loop = asyncio.get_running_loop()
+        self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(host, port))
+        self.local_addr = self.transport.get_extra_info("sockname")[:2]
+        self._ticker = asyncio.ensure_future(self._tick_loop())
+        return self
+
+    @property
+    def port(self) -> int:
+        return self.local_addr[1]
+
+    def close(self) -> None:
+        for s in list(self.streams.values()):
+            if not s.transport.is_closing():
+                s.transport.abort()
+            if not s.eof:
+                s.eof = True
+                s.reader.feed_eof()
+        self._flush()
+        if self._ticker is not None:
+            self._ticker.cancel()
+        if self.transport is not None:
+            self.transport.close()
+            self.transport = None
+
+    # ------------------------------------------------------------ io
+    def datagram_received(self, data: bytes, addr) -> None:
+        if not data or (data[0] & 0x0F) != 1 or (data[0] >> 4) > 4:
+            if self.other_datagram is not None:
+                self.other_datagram(data, addr)
+            return
+        cid = self.engine.incoming(data, _key(addr[:2]), _now_us())
+        for new in self.engine.accepted():
+            s = _Stream(self, new, _addr(self.stats(new).get("addr", _key(addr[:2]))))
+            s.connected.set()
+            self.streams[new] = s
+            self.accept_q.put_nowait(s)
+        if cid > 0:
+            self._service(cid)
+        self._flush()
+
+    def error_received(self, exc: Exception) -> None:  # ICMP errors etc.
+        pass
+
+    def _service(self, cid: int) -> None:
+        s = self.streams.get(cid)
+        if s is None:
+            return
+        st = self.engine.state(cid)
+        if st >= _utp.CONNECTED and not s.connected.is_set() and st != _utp.RESET:
+            s.connected.set()
+        data = self.engine.read(cid)
+        if data:
+            s.reader.feed_data(data)
+        if not s.eof and (self.engine.eof(cid) or st == _utp.RESET):
+            s.eof = True
+            if st == _utp.RESET and not s.connected.is_set():
+                s.connected.set()
+            s.reader.feed_eof()
+        s.transport._push()
+
+    def _flush(self) -> None:
+        if self.transport is None:
+            return
+        for key, pkt in self.engine.outgoing():
+            self.transport.sendto(pkt, _addr(key))
+
+    async def _tick_loop(self) -> None:
+        try:
+            while True:
+                await asyncio.sleep(TICK)
+                self.engine.tick(_now_us())
+                for cid in list(self.streams):
+                    self._service(cid)
+                    if self.streams[cid].eof and self.streams[cid].transport.is_closing():
+                        del self.streams[cid]
+                self._flush()
+        except asyncio.CancelledError:
+            pass
+
+    def stats(self, cid: int) -> dict:
+        return self.engine.stats(cid)
+
+    # ------------------------------------------------------------ api
+    async def connect(self, host: str, port: int, timeout: float = 5.0
+                      ) -> tuple[asyncio.StreamReader, asyncio.StreamWriter]:
+        cid = self.engine.connect(_key((host, port)), _now_us())
+        s = _Stream(self, cid, (host, port))
+        self.streams[cid] = s
+        self._flush()
+        try:
+            await asyncio.wait_for(s.connected.wait(), timeout)
+        except asyncio.TimeoutError:
+            s.transport.abort()
+            raise UtpError(f"uTP connect to {host}:{port} timed out") from None
+        if self.engine.state(cid) == _utp.RESET:
+            raise UtpError(f"uTP connection to {host}:{port} reset")
+        return s.reader, s.writer
+
+    async def accept(self) -> tuple[asyncio.StreamReader, asyncio.StreamWriter, tuple[str, int]]:
+        s = await self.accept_q.get()
+        return s.reader, s.writer, s.transport.peer
+
+
+async def serve(sock: UtpSocket, handler) -> asyncio.Task:
+    """Run ``handler(reader, writer)`` for every accepted connection."""
+    async def loop():
+        with contextlib.suppress(asyncio.CancelledError):
+            while True:
+                r, w, _a = await sock.accept()
+                asyncio.ensure_future(handler(r, w))
+    return asyncio.ensure_future(loop())
