@@ -1,0 +1,262 @@
+// Host hashing core (OpenSSL EVP; no Python) — shared by the pybind11 module
+// hash_host.cpp and the sanitizer self-test csrc/tests/native_selftest.cpp.
+//
+// Everything here is thread-safe and allocation-bounded by its inputs.
+#pragma once
+
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+namespace tritondl_hash {
+
+inline const EVP_MD* md_for(const std::string& kind) {
+  if (kind == "sha1") return EVP_sha1();
+  if (kind == "sha256") return EVP_sha256();
+  if (kind == "md5") return EVP_md5();
+  throw std::invalid_argument("unknown hash kind: " + kind);
+}
+
+struct MdCtx {
+  EVP_MD_CTX* ctx;
+  explicit MdCtx(const EVP_MD* md) : ctx(EVP_MD_CTX_new()) {
+    if (!ctx || EVP_DigestInit_ex(ctx, md, nullptr) != 1) throw std::runtime_error("EVP init failed");
+  }
+  ~MdCtx() { EVP_MD_CTX_free(ctx); }
+  MdCtx(const MdCtx&) = delete;
+  MdCtx& operator=(const MdCtx&) = delete;
+  void update(const void* p, size_t n) {
+    if (n && EVP_DigestUpdate(ctx, p, n) != 1) throw std::runtime_error("EVP update failed");
+  }
+  std::string final() {
+    unsigned char out[EVP_MAX_MD_SIZE];
+    unsigned int len = 0;
+    if (EVP_DigestFinal_ex(ctx, out, &len) != 1) throw std::runtime_error("EVP final failed");
+    return std::string(reinterpret_cast<char*>(out), len);
+  }
+};
+
+inline std::string one_shot(const EVP_MD* md, const void* p, size_t n) {
+  MdCtx c(md);
+  c.update(p, n);
+  return c.final();
+}
+
+inline std::string hex(const std::string& d) {
+  static const char* hx = "0123456789abcdef";
+  std::string out;
+  out.reserve(d.size() * 2);
+  for (unsigned char ch : d) {
+    out.push_back(hx[ch >> 4]);
+    out.push_back(hx[ch & 15]);
+  }
+  return out;
+}
+
+inline std::string hmac256(const std::string& key, const std::string& msg) {
+  unsigned char out[32];
+  unsigned int len = 32;
+  if (!HMAC(EVP_sha256(), key.data(), static_cast<int>(key.size()),
+            reinterpret_cast<const unsigned char*>(msg.data()), msg.size(), out, &len))
+    throw std::runtime_error("HMAC failed");
+  return std::string(reinterpret_cast<char*>(out), len);
+}
+
+// pread that loops over short reads; returns bytes read (may be < n at EOF)
+inline size_t pread_full(int fd, char* dst, size_t n, off_t off) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = ::pread(fd, dst + got, n - got, off + static_cast<off_t>(got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return got;
+    }
+    if (r == 0) break;
+    got += static_cast<size_t>(r);
+  }
+  return got;
+}
+
+template <class F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  if (threads <= 1 || n <= 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> ts;
+  int t = static_cast<int>(std::min<size_t>(static_cast<size_t>(threads), n));
+  for (int k = 0; k < t; ++k)
+    ts.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
+    });
+  for (auto& th : ts) th.join();
+}
+
+inline int default_threads() {
+  unsigned h = std::thread::hardware_concurrency();
+  return h ? static_cast<int>(std::min(h, 32u)) : 4;
+}
+
+// Concatenated per-piece digests of a contiguous buffer.
+inline std::string piece_hashes(const EVP_MD* md, const char* data, size_t len, size_t piece_len, int threads) {
+  if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
+  const size_t n = (len + piece_len - 1) / piece_len;
+  const size_t dl = static_cast<size_t>(EVP_MD_size(md));
+  std::string out(n * dl, '\0');
+  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t i) {
+    const size_t off = i * piece_len;
+    const std::string d = one_shot(md, data + off, std::min(piece_len, len - off));
+    std::memcpy(&out[i * dl], d.data(), dl);
+  });
+  return out;
+}
+
+struct FileSpan {
+  std::string path;
+  long long length;
+  long long start;  // offset of this file in the torrent's concatenated stream
+};
+
+// Verify a torrent's pieces against the concatenated file layout; one byte per
+// piece (1 = verified, 0 = mismatch / missing / short data).
+inline std::string verify_pieces(const std::vector<std::pair<std::string, long long>>& files, size_t piece_len,
+                                 const std::string& expected, int threads, const EVP_MD* md) {
+  const size_t dl = static_cast<size_t>(EVP_MD_size(md));
+  if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
+  if (expected.size() % dl) throw std::invalid_argument("expected digest blob has wrong size");
+  std::vector<FileSpan> spans;
+  long long total = 0;
+  for (auto& f : files) {
+    if (f.second < 0) throw std::invalid_argument("negative file length");
+    spans.push_back({f.first, f.second, total});
+    total += f.second;
+  }
+  const size_t n = expected.size() / dl;
+  const size_t need = total > 0 ? (static_cast<size_t>(total) + piece_len - 1) / piece_len : 0;
+  if (n != need) throw std::invalid_argument("piece count does not match total length");
+  std::string ok(n, '\0');
+  std::vector<int> fds(spans.size(), -1);
+  for (size_t i = 0; i < spans.size(); ++i) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
+  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
+    const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
+    const long long plen = std::min<long long>(static_cast<long long>(piece_len), total - pstart);
+    std::vector<char> buf(static_cast<size_t>(plen));
+    long long filled = 0;
+    size_t lo = 0, hi = spans.size();  // last span starting at or before pstart
+    while (hi - lo > 1) {
+      size_t mid = (lo + hi) / 2;
+      if (spans[mid].start <= pstart) lo = mid; else hi = mid;
+    }
+    for (size_t s = lo; s < spans.size() && filled < plen; ++s) {
+      const long long fstart = spans[s].start, flen = spans[s].length;
+      const long long a = std::max(pstart + filled, fstart);
+      const long long e = std::min(pstart + plen, fstart + flen);
+      if (e <= a) continue;
+      if (a != pstart + filled || fds[s] < 0) return;
+      const size_t want = static_cast<size_t>(e - a);
+      if (pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) return;
+      filled += static_cast<long long>(want);
+    }
+    if (filled != plen) return;
+    const std::string d = one_shot(md, buf.data(), buf.size());
+    if (std::memcmp(d.data(), expected.data() + p * dl, dl) == 0) ok[p] = 1;
+  });
+  for (int fd : fds)
+    if (fd >= 0) ::close(fd);
+  return ok;
+}
+
+// aws-chunked (STREAMING-AWS4-HMAC-SHA256-PAYLOAD) signature chain over
+// chunk_size chunks of [data, data+len) (+ the final empty chunk when
+// include_final).  String to sign per chunk:
+//   "AWS4-HMAC-SHA256-PAYLOAD\n" amzdate "\n" scope "\n" prev "\n" hex(sha256("")) "\n" hex(sha256(chunk))
+inline std::vector<std::string> chunk_signatures(const std::string& key, const std::string& amzdate,
+                                                 const std::string& scope, const std::string& seed,
+                                                 const char* data, size_t len, size_t chunk_size,
+                                                 bool include_final) {
+  if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
+  std::vector<std::string> sigs;
+  const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+  const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
+  std::string prev = seed;
+  size_t off = 0;
+  while (true) {
+    const size_t n = std::min(chunk_size, len - off);
+    prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + hex(one_shot(EVP_sha256(), data + off, n))));
+    sigs.push_back(prev);
+    off += n;
+    if (n == 0) break;
+    if (off >= len && !include_final) break;
+  }
+  return sigs;
+}
+
+inline size_t hexlen(size_t n) {
+  size_t l = 1;
+  while (n >>= 4) ++l;
+  return l;
+}
+
+// Exact size of the aws-chunked encoding of len bytes.
+inline size_t aws_chunk_encoded_size(size_t len, size_t chunk_size, bool final_chunk) {
+  const size_t sig_part = 17 + 64 + 2;  // ";chunk-signature=" + sig + CRLF
+  size_t total = 0;
+  for (size_t off = 0; off < len; off += chunk_size) {
+    const size_t n = std::min(chunk_size, len - off);
+    total += hexlen(n) + sig_part + n + 2;
+  }
+  if (final_chunk) total += 1 + sig_part + 2;
+  return total;
+}
+
+// Fused aws-chunked encoder into dst (which must hold aws_chunk_encoded_size
+// bytes): hash each chunk while hot in cache, chain its signature, copy it
+// behind its header.  Returns the last signature.
+inline std::string aws_chunk_encode(const std::string& key, const std::string& amzdate, const std::string& scope,
+                                    std::string prev, const char* data, size_t len, size_t chunk_size,
+                                    bool final_chunk, char* dst) {
+  if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
+  const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+  const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
+  size_t w = 0;
+  auto emit = [&](const char* p, size_t n) {
+    const std::string h = hex(one_shot(EVP_sha256(), p, n));
+    prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + h));
+    char hx[32];
+    const int hl = std::snprintf(hx, sizeof hx, "%zx", n);
+    std::memcpy(dst + w, hx, static_cast<size_t>(hl));
+    w += static_cast<size_t>(hl);
+    std::memcpy(dst + w, ";chunk-signature=", 17);
+    w += 17;
+    std::memcpy(dst + w, prev.data(), 64);
+    w += 64;
+    dst[w++] = '\r';
+    dst[w++] = '\n';
+    if (n) {
+      std::memcpy(dst + w, p, n);
+      w += n;
+    }
+    dst[w++] = '\r';
+    dst[w++] = '\n';
+  };
+  for (size_t off = 0; off < len; off += chunk_size) emit(data + off, std::min(chunk_size, len - off));
+  if (final_chunk) emit(nullptr, 0);
+  return prev;
+}
+
+}  // namespace tritondl_hash

@@ -1,0 +1,158 @@
+// Native self-test for the host C++ cores, built by tools/native_selftest.py
+// with -fsanitize=address,undefined (and a -fsanitize=thread variant for the
+// threaded piece verifier).  Host code only: the GPU kernels are verified by
+// the gpu-marked pytest suite against hashlib.
+#include <cassert>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../hash/hash_core.h"
+#include "../utp/utp_engine.h"
+
+using namespace tritondl_hash;
+
+static int failures = 0;
+#define CHECK(cond)                                                        \
+  do {                                                                     \
+    if (!(cond)) {                                                         \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                          \
+    }                                                                      \
+  } while (0)
+
+static void test_vectors() {
+  CHECK(hex(one_shot(EVP_sha1(), "abc", 3)) == "a9993e364706816aba3e25717850c26c9cd0d89d");
+  CHECK(hex(one_shot(EVP_sha256(), "abc", 3)) ==
+        "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad");
+  CHECK(hex(one_shot(EVP_md5(), "abc", 3)) == "900150983cd24fb0d6963f7d28e17f72");
+}
+
+static std::string signing_key(const std::string& secret, const std::string& date) {
+  std::string k = hmac256("AWS4" + secret, date);
+  k = hmac256(k, "us-east-1");
+  k = hmac256(k, "s3");
+  return hmac256(k, "aws4_request");
+}
+
+static void test_aws_chunked() {
+  // AWS S3 SigV4 streaming example: 66560 bytes of 'a', 64 KiB chunks
+  const std::string key = signing_key("wJalrXUtnFEMI/K7MDENG/bPxRfiCYEXAMPLEKEY", "20130524");
+  const std::string data(66560, 'a');
+  const std::string scope = "20130524/us-east-1/s3/aws4_request";
+  const std::string seed = "4f232c4386841ef735655705268965c44a0e4690baa4adea153f7db9fa80a0a9";
+  auto sigs = chunk_signatures(key, "20130524T000000Z", scope, seed, data.data(), data.size(), 65536, true);
+  CHECK(sigs.size() == 3);
+  CHECK(sigs[0] == "ad80c730a21e5b8d04586a2213dd63b9a0e99e0e2307b0ade35a65485a288648");
+  CHECK(sigs[2] == "b6c6ea8a5354eaf15b3cb7646744f4275b71ea724fed81ceb9323e279d449df9");
+  std::string out(aws_chunk_encoded_size(data.size(), 65536, true), '\0');
+  std::string last = aws_chunk_encode(key, "20130524T000000Z", scope, seed, data.data(), data.size(), 65536, true,
+                                      &out[0]);
+  CHECK(out.size() == 66824);
+  CHECK(last == sigs[2]);
+  CHECK(out.compare(out.size() - 4, 4, "\r\n\r\n") == 0);
+}
+
+static void test_pieces_and_verify() {
+  std::mt19937 rng(7);
+  std::string blob(1 << 20, '\0');
+  for (auto& ch : blob) ch = static_cast<char>(rng());
+  const size_t pl = 32768;
+  std::string ph = piece_hashes(EVP_sha1(), blob.data(), blob.size(), pl, 4);
+  CHECK(ph.size() == (blob.size() / pl) * 20);
+  for (size_t i = 0; i < blob.size() / pl; ++i)
+    CHECK(ph.compare(i * 20, 20, one_shot(EVP_sha1(), blob.data() + i * pl, pl)) == 0);
+  // two files forming the torrent stream
+  char tmpl[] = "/tmp/tdl_selftestXXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  if (!dir) return;
+  std::string a = std::string(dir) + "/a", b = std::string(dir) + "/b";
+  const size_t cut = 300001;
+  FILE* fa = std::fopen(a.c_str(), "wb");
+  std::fwrite(blob.data(), 1, cut, fa);
+  std::fclose(fa);
+  FILE* fb = std::fopen(b.c_str(), "wb");
+  std::fwrite(blob.data() + cut, 1, blob.size() - cut, fb);
+  std::fclose(fb);
+  std::vector<std::pair<std::string, long long>> files = {{a, (long long)cut}, {b, (long long)(blob.size() - cut)}};
+  std::string ok = verify_pieces(files, pl, ph, 8, EVP_sha1());
+  CHECK(ok == std::string(ok.size(), '\1'));
+  // corrupt one byte inside piece 20
+  FILE* fc = std::fopen(b.c_str(), "r+b");
+  std::fseek(fc, 20 * pl - cut + 5, SEEK_SET);
+  std::fputc('X', fc);
+  std::fclose(fc);
+  ok = verify_pieces(files, pl, ph, 8, EVP_sha1());
+  int bad = 0;
+  for (char ch : ok) bad += ch == 0;
+  CHECK(bad == 1 && ok[20] == 0);
+  std::remove(a.c_str());
+  ok = verify_pieces(files, pl, ph, 8, EVP_sha1());  // missing file -> its pieces fail, no crash
+  CHECK(ok[0] == 0);
+  std::remove(b.c_str());
+  rmdir(dir);
+}
+
+static void test_utp(double loss, size_t n, unsigned seed) {
+  using tritondl_utp::Engine;
+  std::mt19937_64 rng(seed);
+  std::uniform_real_distribution<double> u(0, 1);
+  Engine A(seed), B(seed + 1);
+  int64_t now = 0;
+  int ca = A.connect("B", now);
+  std::string data(n, '\0');
+  for (auto& ch : data) ch = static_cast<char>(rng());
+  size_t sent = 0;
+  bool closed = false;
+  std::string got;
+  int cb = -1;
+  struct Pkt { int64_t at; std::string dst, src, bytes; };
+  std::vector<Pkt> wire;
+  int64_t last_a = 0, last_b = 0;
+  for (int step = 0; step < 300000; ++step) {
+    now += 1000;
+    if (sent < n) sent += A.write(ca, data.substr(sent, 65536));
+    else if (!closed) { A.close(ca, now); closed = true; }
+    for (Engine* e : {&A, &B}) {
+      const std::string src = e == &A ? "A" : "B";
+      for (auto& o : e->outgoing()) {
+        if (u(rng) < loss) continue;
+        int64_t& last = e == &A ? last_a : last_b;
+        int64_t at = std::max<int64_t>(now + 5000 + static_cast<int64_t>(u(rng) * 500), last);
+        last = at;
+        wire.push_back({at, o.first, src, o.second});
+      }
+    }
+    std::stable_sort(wire.begin(), wire.end(), [](const Pkt& x, const Pkt& y) { return x.at < y.at; });
+    size_t k = 0;
+    for (; k < wire.size() && wire[k].at <= now; ++k) (wire[k].dst == "B" ? B : A).incoming(wire[k].bytes, wire[k].src, now);
+    wire.erase(wire.begin(), wire.begin() + static_cast<long>(k));
+    for (int c : B.accepted()) cb = c;
+    if (cb >= 0) {
+      got += B.read(cb);
+      if (B.eof(cb)) break;
+    }
+    A.tick(now);
+    B.tick(now);
+  }
+  CHECK(got == data);
+  CHECK(cb >= 0 && B.eof(cb));
+}
+
+int main(int argc, char** argv) {
+  bool quick = argc > 1 && std::string(argv[1]) == "--quick";
+  test_vectors();
+  test_aws_chunked();
+  test_pieces_and_verify();
+  test_utp(0.0, quick ? 100000 : 400000, 1);
+  test_utp(0.03, quick ? 60000 : 200000, 2);
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::puts("native selftest OK");
+  return 0;
+}
