@@ -135,16 +135,17 @@ py::bytes py_verify_pieces(const std::vector<std::pair<std::string, long long>>&
 
 std::vector<std::string> py_chunk_signatures(const std::string& key, const std::string& amzdate,
                                              const std::string& scope, const std::string& seed,
-                                             const py::buffer& data, size_t chunk_size, bool include_final) {
+                                             const py::buffer& data, size_t chunk_size, bool include_final,
+                                             int threads) {
   py::buffer_info bi;
   BufView v = view_of(data, bi);
   py::gil_scoped_release nogil;
-  return chunk_signatures(key, amzdate, scope, seed, v.ptr, v.len, chunk_size, include_final);
+  return chunk_signatures(key, amzdate, scope, seed, v.ptr, v.len, chunk_size, include_final, threads);
 }
 
 py::tuple py_aws_chunk_encode(const std::string& key, const std::string& amzdate, const std::string& scope,
                               const std::string& prev_sig, const py::buffer& data, size_t chunk_size,
-                              bool final_chunk) {
+                              bool final_chunk, int threads) {
   if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
   py::buffer_info bi;
   BufView v = view_of(data, bi);
@@ -156,9 +157,24 @@ py::tuple py_aws_chunk_encode(const std::string& key, const std::string& amzdate
   std::string last;
   {
     py::gil_scoped_release nogil;
-    last = aws_chunk_encode(key, amzdate, scope, prev_sig, v.ptr, v.len, chunk_size, final_chunk, dst);
+    last = aws_chunk_encode(key, amzdate, scope, prev_sig, v.ptr, v.len, chunk_size, final_chunk, dst, threads);
   }
   return py::make_tuple(result, last);
+}
+
+py::tuple py_aws_chunk_decode(const std::string& key, const std::string& amzdate, const std::string& scope,
+                              const std::string& seed, const py::buffer& raw, int threads, bool want_data,
+                              bool require_final) {
+  py::buffer_info bi;
+  BufView v = view_of(raw, bi);
+  std::string decoded, err;
+  {
+    py::gil_scoped_release nogil;
+    err = aws_chunk_decode(key, amzdate, scope, seed, v.ptr, v.len, threads, want_data ? &decoded : nullptr,
+                           require_final);
+  }
+  if (!err.empty()) return py::make_tuple(false, py::none(), err);
+  return py::make_tuple(true, want_data ? py::object(py::bytes(decoded)) : py::object(py::none()), std::string());
 }
 
 }  // namespace
@@ -190,8 +206,14 @@ PYBIND11_MODULE(_hash_host, m) {
         py::arg("threads") = 0, py::arg("kind") = "sha1");
   m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) { return py::bytes(hmac256(k, msg)); });
   m.def("chunk_signatures", &py_chunk_signatures, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
-        py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true);
+        py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true,
+        py::arg("threads") = 1);
   m.def("aws_chunk_encode", &py_aws_chunk_encode, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
-        py::arg("prev_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("final") = false);
+        py::arg("prev_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("final") = false,
+        py::arg("threads") = 1);
   m.def("default_threads", &default_threads);
+  m.def("aws_chunk_decode", &py_aws_chunk_decode, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
+        py::arg("seed_signature"), py::arg("raw"), py::arg("threads") = 1, py::arg("want_data") = true,
+        py::arg("require_final") = true,
+        "verify + decode an aws-chunked body -> (ok, decoded|None, error)");
 }

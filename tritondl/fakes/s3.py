@@ -162,48 +162,31 @@ class FakeS3:
 
     async def _read_chunked(self, request: web.Request, auth) -> bytes:
         """Decode an aws-chunked body and verify EVERY chunk signature while it
-        streams in: complete chunks are batched (~1 MiB) and each batch's
-        signature chain is recomputed by the native helper in a worker thread,
-        seeded with the previous batch's claimed last signature (so batches
-        verify in parallel; a forged claim fails its own batch)."""
+        streams in.  Frame boundaries are tracked here; each ~1 MiB run of
+        whole frames is verified + decoded by the native parser in a worker
+        thread (payload SHA-256 map + signature-chain scan), seeded with the
+        previous run's last *claimed* signature — so runs verify in parallel
+        and a forged claim still fails its own run."""
         key, seed, amzdate, scope = auth
         decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
         loop = asyncio.get_running_loop()
         from ..ops import hashing
         buf = bytearray()
-        pos = 0
-        out: list[bytes] = []
-        batch: list[bytes] = []
-        batch_sigs: list[str] = []
-        batch_bytes = 0
+        pos = 0           # parse cursor in buf
+        run_start = 0     # start of the current run of whole frames
         prev = seed
-        checks: list[asyncio.Future] = []
+        last_sig = seed
+        runs: list[asyncio.Future] = []
         finished = False
 
-        def verify(prev_sig: str, chunks: list[bytes], sigs: list[str]) -> bool:
-            body = [c for c in chunks if c]
-            has_final = len(body) < len(chunks)  # the zero-length chunk only ever comes last
-            size = len(body[0]) if body else 1
-            if all(len(c) == size for c in body[:-1]) and (not body or len(body[-1]) <= size):
-                want = hashing.chunk_signatures(key, amzdate, scope, prev_sig, b"".join(body), size,
-                                                include_final=has_final)
-                return want == sigs
-            empty = hashlib.sha256(b"").hexdigest()
-            p = prev_sig
-            for c, sg in zip(chunks, sigs):
-                sts = "\n".join(["AWS4-HMAC-SHA256-PAYLOAD", amzdate, scope, p, empty,
-                                 hashlib.sha256(c).hexdigest()])
-                p = hmac.new(key, sts.encode(), hashlib.sha256).hexdigest()
-                if p != sg:
-                    return False
-            return True
-
-        def flush() -> None:
-            nonlocal batch, batch_sigs, batch_bytes, prev
-            if batch:
-                checks.append(loop.run_in_executor(None, verify, prev, batch, batch_sigs))
-                prev = batch_sigs[-1]
-                batch, batch_sigs, batch_bytes = [], [], 0
+        def dispatch(end: int, final: bool) -> None:
+            nonlocal run_start, prev
+            if end > run_start:
+                chunk = bytes(buf[run_start:end])
+                runs.append(loop.run_in_executor(None, hashing.aws_chunk_decode, key, amzdate, scope, prev, chunk,
+                                                 2, True, final))
+                prev = last_sig
+                run_start = end
 
         async for data in request.content.iter_chunked(1 << 20):
             self.bytes_received += len(data)
@@ -218,31 +201,29 @@ class FakeS3:
                 if not m:
                     raise _BadReq(400, "IncompleteBody", "malformed aws-chunked framing")
                 n = int(m.group(1), 16)
-                a = eol + 2
-                if len(buf) < a + n + 2:
+                if len(buf) < eol + 2 + n + 2:
                     break
-                if buf[a + n:a + n + 2] != b"\r\n":
-                    raise _BadReq(400, "IncompleteBody", "chunk not terminated")
-                chunk = bytes(buf[a:a + n])
-                batch.append(chunk)
-                batch_sigs.append(m.group(2).decode())
-                batch_bytes += n
-                if n:
-                    out.append(chunk)
-                pos = a + n + 2
+                last_sig = m.group(2).decode()
+                pos = eol + 2 + n + 2
                 if n == 0:
                     finished = True
-                elif batch_bytes >= (1 << 20):
-                    flush()
-            if pos > (4 << 20):
-                del buf[:pos]
-                pos = 0
+                elif pos - run_start >= (1 << 20):
+                    dispatch(pos, False)
+            if run_start > (8 << 20):   # drop verified-and-dispatched bytes
+                del buf[:run_start]
+                pos -= run_start
+                run_start = 0
         if not finished:
             raise _BadReq(400, "IncompleteBody", "missing final chunk")
-        flush()
-        if not all(await asyncio.gather(*checks)):
-            raise _BadReq(403, "SignatureDoesNotMatch", "chunk signature mismatch")
-        data = b"".join(out)
+        if pos != len(buf):
+            raise _BadReq(400, "IncompleteBody", "trailing bytes after final chunk")
+        dispatch(pos, True)
+        results = await asyncio.gather(*runs)
+        for ok, _d, err in results:
+            if not ok:
+                code = 403 if "signature" in err else 400
+                raise _BadReq(code, "SignatureDoesNotMatch" if code == 403 else "IncompleteBody", err)
+        data = b"".join(d for _ok, d, _e in results)
         if decoded_len >= 0 and decoded_len != len(data):
             raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
         return data

@@ -41,16 +41,27 @@ def hmac_sha256(key: bytes, msg: bytes) -> bytes:
 
 
 def chunk_signatures(signing_key: bytes, amzdate: str, scope: str, seed_signature: str, data,
-                     chunk_size: int, include_final: bool = True) -> list[str]:
+                     chunk_size: int, include_final: bool = True, threads: int = 1) -> list[str]:
     """aws-chunked signature chain over ``data`` (one per ``chunk_size`` chunk,
-    plus the terminating empty chunk when ``include_final``)."""
-    return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size, include_final)
+    plus the terminating empty chunk when ``include_final``).  The per-chunk
+    SHA-256 map runs on ``threads`` threads (0 = all); the HMAC chain is serial."""
+    return _host.chunk_signatures(signing_key, amzdate, scope, seed_signature, data, chunk_size, include_final,
+                                  threads)
 
 
 def aws_chunk_encode(signing_key: bytes, amzdate: str, scope: str, prev_signature: str, data, chunk_size: int,
-                     final: bool = False) -> tuple[bytes, str]:
-    """Fused aws-chunked framing + signature chain; returns (encoded, last_signature)."""
-    return _host.aws_chunk_encode(signing_key, amzdate, scope, prev_signature, data, chunk_size, final)
+                     final: bool = False, threads: int = 1) -> tuple[bytes, str]:
+    """Fused aws-chunked framing + signature chain; returns (encoded, last_signature).
+    Hash+copy is a parallel map over chunks (``threads``), the chain a serial scan."""
+    return _host.aws_chunk_encode(signing_key, amzdate, scope, prev_signature, data, chunk_size, final, threads)
+
+
+def aws_chunk_decode(signing_key: bytes, amzdate: str, scope: str, seed_signature: str, raw, threads: int = 1,
+                     want_data: bool = True, require_final: bool = True) -> tuple[bool, bytes | None, str]:
+    """Verify every chunk signature of an aws-chunked body (or, with
+    ``require_final=False``, a run of whole frames) and decode it."""
+    return _host.aws_chunk_decode(signing_key, amzdate, scope, seed_signature, raw, threads, want_data,
+                                  require_final)
 
 
 # ----------------------------------------------------------------- GPU

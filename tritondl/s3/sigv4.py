@@ -26,6 +26,7 @@ UNSIGNED_PAYLOAD = "UNSIGNED-PAYLOAD"
 STREAMING_PAYLOAD = "STREAMING-AWS4-HMAC-SHA256-PAYLOAD"
 EMPTY_SHA256 = hashlib.sha256(b"").hexdigest()
 STREAM_CHUNK = 64 * 1024
+SIGN_THREADS = 4
 
 
 def uri_encode(s: str, encode_slash: bool = True) -> str:
@@ -109,7 +110,9 @@ class ChunkSigner:
     """Incremental aws-chunked encoder: feed data blocks (any size), get
     encoded bytes; ``finish()`` emits the trailing zero-length chunk."""
 
-    def __init__(self, key: bytes, amzdate: str, scope: str, seed_signature: str, chunk: int = STREAM_CHUNK):
+    def __init__(self, key: bytes, amzdate: str, scope: str, seed_signature: str, chunk: int = STREAM_CHUNK,
+                 threads: int = SIGN_THREADS):
+        self.threads = threads
         self.key = key
         self.amzdate = amzdate
         self.scope = scope
@@ -119,7 +122,7 @@ class ChunkSigner:
 
     def _encode(self, data, final: bool) -> bytes:
         out, self.prev = hashing.aws_chunk_encode(self.key, self.amzdate, self.scope, self.prev, data,
-                                                  self.chunk, final)
+                                                  self.chunk, final, self.threads)
         return out
 
     def feed(self, data: bytes) -> bytes:
