@@ -299,22 +299,62 @@ struct Span {
   long long start, length;
 };
 
+// Host pipeline: disk / host memory -> pinned staging (2 slots) -> HBM
+// window -> ONE kernel over every piece of the window -> digests.
+//
+// Why windows: the kernel's parallel axis is the piece (one lane each), so a
+// 256 MiB batch of 1 MiB pieces is only 256 lanes (4 waves on a 256-CU chip).
+// Accumulating the copies into a multi-GB HBM window (MI355X: 288 GB) first
+// gives the launch thousands of lanes; two windows alternate so the copies of
+// window k+1 (copy stream) overlap the kernel of window k (compute stream),
+// and the pinned staging slots are recycled as soon as their H2D completes.
 class GpuHasher {
  public:
-  GpuHasher(int device, size_t batch_bytes, int reader_threads)
-      : device_(device), batch_(std::max<size_t>(batch_bytes, 1 << 20)), readers_(std::max(1, reader_threads)) {
+  GpuHasher(int device, size_t stage_bytes, int reader_threads, size_t window_bytes)
+      : device_(device),
+        stage_req_(std::max<size_t>(stage_bytes, 1 << 20)),
+        readers_(std::max(1, reader_threads)),
+        window_req_(window_bytes) {
     HIP_CHECK(hipSetDevice(device_));
-    for (int s = 0; s < kSlots; ++s) {
-      HIP_CHECK(hipStreamCreateWithFlags(&slot_[s].stream, hipStreamNonBlocking));
-      HIP_CHECK(hipEventCreateWithFlags(&slot_[s].done, hipEventDisableTiming));
+    HIP_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&compute_stream_, hipStreamNonBlocking));
+    for (auto& st : stage_) HIP_CHECK(hipEventCreateWithFlags(&st.free_ev, hipEventDisableTiming));
+    for (auto& w : win_) {
+      HIP_CHECK(hipEventCreateWithFlags(&w.copied, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     }
   }
   ~GpuHasher() {
     hipSetDevice(device_);
-    for (int s = 0; s < kSlots; ++s) {
-      free_slot(slot_[s]);
-      hipEventDestroy(slot_[s].done);
-      hipStreamDestroy(slot_[s].stream);
+    hipStreamSynchronize(copy_stream_);
+    hipStreamSynchronize(compute_stream_);
+    release();
+    for (auto& st : stage_) hipEventDestroy(st.free_ev);
+    for (auto& w : win_) {
+      hipEventDestroy(w.copied);
+      hipEventDestroy(w.done);
+    }
+    hipStreamDestroy(copy_stream_);
+    hipStreamDestroy(compute_stream_);
+  }
+
+  // Free cached staging / window memory.
+  void release() {
+    for (auto& st : stage_) {
+      if (st.h) hipHostFree(st.h);
+      st.h = nullptr;
+      st.cap = 0;
+      st.used = false;
+    }
+    for (auto& w : win_) {
+      if (w.d) hipFree(w.d);
+      if (w.d_out) hipFree(w.d_out);
+      if (w.h_out) hipHostFree(w.h_out);
+      w.d = nullptr;
+      w.d_out = nullptr;
+      w.h_out = nullptr;
+      w.cap = w.out_cap = 0;
+      w.pending = false;
     }
   }
 
@@ -330,7 +370,7 @@ class GpuHasher {
     std::string out(n * dl, '\0');
     {
       py::gil_scoped_release nogil;
-      run_batches(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, std::vector<char>&) {
+      run_windows(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, char*) {
         copy_parallel(dst, src + off, len);
       }, [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>&) {
         std::memcpy(&out[first * dl], digests, count * dl);
@@ -349,22 +389,26 @@ class GpuHasher {
     std::vector<Span> spans;
     long long total = 0;
     for (auto& f : files) {
+      if (f.second < 0) throw std::invalid_argument("negative file length");
       spans.push_back({::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
       total += f.second;
     }
+    auto close_all = [&] {
+      for (auto& s : spans)
+        if (s.fd >= 0) ::close(s.fd);
+    };
     const size_t n = expected.size() / dl;
     const size_t need = total > 0 ? (static_cast<size_t>(total) + piece_len - 1) / piece_len : 0;
     if (n != need) {
-      for (auto& s : spans)
-        if (s.fd >= 0) ::close(s.fd);
+      close_all();
       throw std::invalid_argument("piece count does not match total length");
     }
     std::string ok(n, '\0');
     {
       py::gil_scoped_release nogil;
       try {
-        run_batches(alg, piece_len, static_cast<size_t>(total), n,
-                    [&](uint8_t* dst, size_t off, size_t len, std::vector<char>& complete) {
+        run_windows(alg, piece_len, static_cast<size_t>(total), n,
+                    [&](uint8_t* dst, size_t off, size_t len, char* complete) {
                       read_spans(spans, dst, off, len, piece_len, complete);
                     },
                     [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>& complete) {
@@ -373,62 +417,73 @@ class GpuHasher {
                                         std::memcmp(digests + k * dl, expected.data() + (first + k) * dl, dl) == 0;
                     });
       } catch (...) {
-        for (auto& s : spans)
-          if (s.fd >= 0) ::close(s.fd);
+        close_all();
         throw;
       }
     }
-    for (auto& s : spans)
-      if (s.fd >= 0) ::close(s.fd);
+    close_all();
     return py::bytes(ok);
   }
 
-  size_t batch_bytes() const { return batch_; }
+  size_t batch_bytes() const { return stage_req_; }
+  size_t last_window_bytes() const { return last_window_; }
+  size_t window_bytes_for(size_t total, size_t piece_len) {
+    size_t budget = window_req_;
+    if (budget == 0) {
+      size_t free_b = 0, tot_b = 0;
+      if (hipMemGetInfo(&free_b, &tot_b) != hipSuccess) free_b = 8ull << 30;
+      budget = std::min<size_t>(free_b / 3, 48ull << 30);  // two windows + headroom
+    }
+    const size_t aligned = (total + piece_len - 1) / piece_len * piece_len;
+    const size_t per = std::max<size_t>(1, budget / piece_len) * piece_len;
+    return std::max(piece_len, std::min(aligned, per));
+  }
 
  private:
-  static constexpr int kSlots = 2;
-  struct Slot {
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    uint8_t* h_data = nullptr;
-    uint8_t* d_data = nullptr;
+  static constexpr int kStages = 2;
+  struct Stage {
+    uint8_t* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t free_ev = nullptr;
+    bool used = false;
+  };
+  struct Window {
+    uint8_t* d = nullptr;
+    size_t cap = 0;
     uint32_t* d_out = nullptr;
     uint8_t* h_out = nullptr;
-    size_t cap = 0, out_cap = 0;
+    size_t out_cap = 0;
+    hipEvent_t copied = nullptr, done = nullptr;
     bool pending = false;
     size_t first = 0, count = 0;
     std::vector<char> complete;
   };
 
-  void free_slot(Slot& s) {
-    if (s.h_data) hipHostFree(s.h_data);
-    if (s.d_data) hipFree(s.d_data);
-    if (s.d_out) hipFree(s.d_out);
-    if (s.h_out) hipHostFree(s.h_out);
-    s.h_data = s.d_data = nullptr;
-    s.d_out = nullptr;
-    s.h_out = nullptr;
-    s.cap = s.out_cap = 0;
+  void ensure_stage(Stage& st, size_t bytes) {
+    if (st.cap >= bytes) return;
+    if (st.used) HIP_CHECK(hipEventSynchronize(st.free_ev));
+    if (st.h) HIP_CHECK(hipHostFree(st.h));
+    st.h = nullptr;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st.h), bytes, hipHostMallocDefault));
+    st.cap = bytes;
+    st.used = false;
   }
 
-  void ensure(Slot& s, size_t bytes, size_t out_bytes) {
-    if (s.cap < bytes) {
-      if (s.h_data) HIP_CHECK(hipHostFree(s.h_data));
-      if (s.d_data) HIP_CHECK(hipFree(s.d_data));
-      s.h_data = nullptr;
-      s.d_data = nullptr;
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_data), bytes, hipHostMallocDefault));
-      HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_data), bytes));
-      s.cap = bytes;
+  void ensure_window(Window& w, size_t bytes, size_t out_bytes) {
+    if (w.cap < bytes) {
+      if (w.d) HIP_CHECK(hipFree(w.d));
+      w.d = nullptr;
+      HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&w.d), bytes));
+      w.cap = bytes;
     }
-    if (s.out_cap < out_bytes) {
-      if (s.h_out) HIP_CHECK(hipHostFree(s.h_out));
-      if (s.d_out) HIP_CHECK(hipFree(s.d_out));
-      s.h_out = nullptr;
-      s.d_out = nullptr;
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), out_bytes, hipHostMallocDefault));
-      HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&s.d_out), out_bytes));
-      s.out_cap = out_bytes;
+    if (w.out_cap < out_bytes) {
+      if (w.d_out) HIP_CHECK(hipFree(w.d_out));
+      if (w.h_out) HIP_CHECK(hipHostFree(w.h_out));
+      w.d_out = nullptr;
+      w.h_out = nullptr;
+      HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&w.d_out), out_bytes));
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&w.h_out), out_bytes, hipHostMallocDefault));
+      w.out_cap = out_bytes;
     }
   }
 
@@ -449,85 +504,96 @@ class GpuHasher {
     for (auto& th : ts) th.join();
   }
 
-  // Read [off, off+len) of the concatenated layout; complete[k] = piece k of this batch fully read.
+  // Read [off, off+len) (piece-aligned) of the concatenated layout into dst;
+  // complete[k] is cleared for every piece k of this range not fully read.
   void read_spans(const std::vector<Span>& spans, uint8_t* dst, size_t off, size_t len, size_t piece_len,
-                  std::vector<char>& complete) {
+                  char* complete) {
     const size_t np = (len + piece_len - 1) / piece_len;
-    complete.assign(np, 1);
-    std::vector<std::pair<size_t, size_t>> bad;  // byte ranges (batch-relative) that failed
     std::atomic<size_t> next{0};
-    std::vector<std::thread> ts;
-    std::vector<std::vector<std::pair<size_t, size_t>>> badt(readers_);
-    // split the batch into per-piece work items; workers pread whatever files overlap
-    auto work = [&](int tid) {
+    auto work = [&] {
       for (size_t k; (k = next.fetch_add(1)) < np;) {
-        size_t a = k * piece_len, e = std::min(len, a + piece_len);
-        long long ga = static_cast<long long>(off + a), ge = static_cast<long long>(off + e);
+        const size_t a = k * piece_len, e = std::min(len, a + piece_len);
+        const long long ga = static_cast<long long>(off + a), ge = static_cast<long long>(off + e);
         long long cur = ga;
+        bool good = true;
         for (const Span& s : spans) {
           if (s.start + s.length <= cur || s.start >= ge) continue;
-          long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
-          size_t want = static_cast<size_t>(re - ra);
-          size_t got = s.fd >= 0 ? pread_full(s.fd, dst + (ra - static_cast<long long>(off)), want,
-                                              static_cast<off_t>(ra - s.start))
-                                 : 0;
+          const long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
+          const size_t want = static_cast<size_t>(re - ra);
+          uint8_t* p = dst + (ra - static_cast<long long>(off));
+          const size_t got = s.fd >= 0 ? pread_full(s.fd, p, want, static_cast<off_t>(ra - s.start)) : 0;
           if (got != want) {
-            badt[tid].push_back({k, k});
-            std::memset(dst + (ra - static_cast<long long>(off)) + got, 0, want - got);
+            good = false;
+            std::memset(p + got, 0, want - got);
           }
           cur = re;
           if (cur >= ge) break;
         }
-        if (cur < ge) badt[tid].push_back({k, k});
+        if (cur < ge || !good) complete[k] = 0;  // each piece is owned by one worker: no race
       }
     };
-    int t = static_cast<int>(std::min<size_t>(readers_, np));
-    for (int k = 0; k < t; ++k) ts.emplace_back(work, k);
+    std::vector<std::thread> ts;
+    const int t = static_cast<int>(std::min<size_t>(readers_, np));
+    for (int k = 1; k < t; ++k) ts.emplace_back(work);
+    work();
     for (auto& th : ts) th.join();
-    for (auto& v : badt)
-      for (auto& b : v) complete[b.first] = 0;
   }
 
   template <class Fill, class Harvest>
-  void run_batches(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest) {
+  void run_windows(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest) {
     HIP_CHECK(hipSetDevice(device_));
+    if (n == 0) return;
     const int dl = digest_len(alg);
-    const size_t per = std::max<size_t>(1, batch_ / piece_len);  // pieces per batch
-    const size_t bytes = per * piece_len;
-    for (auto& s : slot_) {
-      ensure(s, bytes, per * dl);
-      s.pending = false;
-    }
-    auto drain = [&](Slot& s) {
-      if (!s.pending) return;
-      HIP_CHECK(hipEventSynchronize(s.done));
-      harvest(s.first, s.count, s.h_out, s.complete);
-      s.pending = false;
+    const size_t wbytes = window_bytes_for(total, piece_len);
+    last_window_ = wbytes;
+    const size_t per = wbytes / piece_len;                                   // pieces per window
+    const size_t stage = std::max<size_t>(1, stage_req_ / piece_len) * piece_len;  // piece-aligned staging
+    for (auto& st : stage_) ensure_stage(st, std::min(stage, wbytes));
+    auto drain = [&](Window& w) {
+      if (!w.pending) return;
+      HIP_CHECK(hipEventSynchronize(w.done));
+      harvest(w.first, w.count, w.h_out, w.complete);
+      w.pending = false;
     };
-    size_t b = 0;
-    for (size_t first = 0; first < n; first += per, ++b) {
-      Slot& s = slot_[b % kSlots];
-      drain(s);  // the slot's previous batch (b-2) must be finished before we overwrite it
+    size_t widx = 0, sidx = 0;
+    for (size_t first = 0; first < n; first += per, ++widx) {
+      Window& w = win_[widx % 2];
+      drain(w);  // its previous window (widx-2) must be hashed before we overwrite it
       const size_t count = std::min(per, n - first);
-      const size_t off = first * piece_len;
-      const size_t len = std::min(total - off, count * piece_len);
-      s.complete.assign(count, 1);
-      fill(s.h_data, off, len, s.complete);  // overlaps with the other slot's GPU work
-      HIP_CHECK(hipMemcpyAsync(s.d_data, s.h_data, len, hipMemcpyHostToDevice, s.stream));
-      launch_hash(alg, s.d_data, len, piece_len, static_cast<uint32_t>(count), s.d_out, s.stream);
-      HIP_CHECK(hipMemcpyAsync(s.h_out, s.d_out, count * dl, hipMemcpyDeviceToHost, s.stream));
-      HIP_CHECK(hipEventRecord(s.done, s.stream));
-      s.first = first;
-      s.count = count;
-      s.pending = true;
+      const size_t woff = first * piece_len;
+      const size_t wlen = std::min(total - woff, count * piece_len);
+      ensure_window(w, count * piece_len, count * dl);
+      w.complete.assign(count, 1);
+      for (size_t off = 0; off < wlen; off += stage) {
+        Stage& st = stage_[sidx++ % kStages];
+        if (st.used) HIP_CHECK(hipEventSynchronize(st.free_ev));  // its previous H2D has landed
+        const size_t len = std::min(stage, wlen - off);
+        fill(st.h, woff + off, len, w.complete.data() + off / piece_len);
+        HIP_CHECK(hipMemcpyAsync(w.d + off, st.h, len, hipMemcpyHostToDevice, copy_stream_));
+        HIP_CHECK(hipEventRecord(st.free_ev, copy_stream_));
+        st.used = true;
+      }
+      HIP_CHECK(hipEventRecord(w.copied, copy_stream_));
+      HIP_CHECK(hipStreamWaitEvent(compute_stream_, w.copied, 0));
+      launch_hash(alg, w.d, wlen, piece_len, static_cast<uint32_t>(count), w.d_out, compute_stream_);
+      HIP_CHECK(hipMemcpyAsync(w.h_out, w.d_out, count * dl, hipMemcpyDeviceToHost, compute_stream_));
+      HIP_CHECK(hipEventRecord(w.done, compute_stream_));
+      w.first = first;
+      w.count = count;
+      w.pending = true;
     }
-    for (int k = 0; k < kSlots; ++k) drain(slot_[(b + k) % kSlots]);
+    drain(win_[widx % 2]);
+    drain(win_[(widx + 1) % 2]);
   }
 
   int device_;
-  size_t batch_;
+  size_t stage_req_;
   int readers_;
-  Slot slot_[kSlots];
+  size_t window_req_;
+  size_t last_window_ = 0;
+  hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
+  Stage stage_[kStages];
+  Window win_[2];
 };
 
 int device_count() {
@@ -557,10 +623,15 @@ PYBIND11_MODULE(_gpu_hash, m) {
       py::arg("stream") = 0,
       "Launch on caller-owned device memory (e.g. torch tensors); out holds n*digest_len bytes.");
   py::class_<GpuHasher>(m, "GpuHasher")
-      .def(py::init<int, size_t, int>(), py::arg("device") = 0, py::arg("batch_bytes") = 256u << 20,
-           py::arg("reader_threads") = 8)
+      .def(py::init<int, size_t, int, size_t>(), py::arg("device") = 0, py::arg("batch_bytes") = 256u << 20,
+           py::arg("reader_threads") = 8, py::arg("window_bytes") = 0,
+           "batch_bytes: pinned staging chunk; window_bytes: HBM window per kernel launch (0 = auto, "
+           "a third of free HBM capped at 48 GiB)")
       .def("hash_buffer", &GpuHasher::hash_buffer, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"))
       .def("verify_files", &GpuHasher::verify_files, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
            py::arg("kind") = "sha1")
+      .def("release", &GpuHasher::release)
+      .def("window_bytes_for", &GpuHasher::window_bytes_for)
+      .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)
       .def_property_readonly("batch_bytes", &GpuHasher::batch_bytes);
 }

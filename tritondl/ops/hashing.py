@@ -68,7 +68,7 @@ def aws_chunk_decode(signing_key: bytes, amzdate: str, scope: str, seed_signatur
 
 _gpu_mod = None
 _gpu_lock = threading.Lock()
-_gpu_hashers: dict[int, object] = {}
+_gpu_hashers: dict[tuple, object] = {}
 
 
 def _load_gpu():
@@ -102,12 +102,16 @@ def gpu_available() -> bool:
         return False
 
 
-def gpu_hasher(device: int = 0, batch_bytes: int = 256 << 20, reader_threads: int = 8):
+def gpu_hasher(device: int = 0, batch_bytes: int = 256 << 20, reader_threads: int = 8, window_bytes: int = 0):
+    """Cached per-device :class:`GpuHasher`.  ``batch_bytes`` is the pinned
+    staging chunk; ``window_bytes`` the HBM window hashed per kernel launch
+    (0 = auto: a third of free HBM, capped at 48 GiB)."""
+    key = (device, max(batch_bytes, 1 << 20), window_bytes)
     with _gpu_lock:
-        h = _gpu_hashers.get(device)
-        if h is None or h.batch_bytes != max(batch_bytes, 1 << 20):
-            h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads)
-            _gpu_hashers[device] = h
+        h = _gpu_hashers.get(key)
+        if h is None:
+            h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads, window_bytes)
+            _gpu_hashers[key] = h
         return h
 
 
