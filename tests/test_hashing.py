@@ -161,3 +161,15 @@ def test_gpu_many_small_windows(tmp_path, window_pieces):
     assert h.last_window_bytes == window_pieces * piece_len
     data = os.urandom(piece_len * 23 + 5)
     assert h.hash_buffer("sha256", data, piece_len) == _ref_pieces(data, piece_len, "sha256")
+
+
+def test_choose_device_cost_model(monkeypatch):
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    # many small pieces: GPU (lane-parallel) wins even against a big host
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=64) == "gpu"
+    # few huge pieces: one lane per piece starves the GPU
+    assert hashing.choose_device(64, 16 << 20, 64 * (16 << 20), cpu_threads=16) == "cpu"
+    assert hashing.choose_device(0, 16384, 0) == "cpu"
+    monkeypatch.setattr(hashing, "gpu_available", lambda: False)
+    assert hashing.choose_device(65536, 16384, 65536 * 16384) == "cpu"
+    assert hashing.effective_cpus() >= 1

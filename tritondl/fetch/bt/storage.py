@@ -23,9 +23,6 @@ from ...utils.log import log
 from .metainfo import Info
 
 DB_NAME = ".torrent.db"
-# GPU batch verify wins only with enough independent pieces (one lane per
-# piece, ~55 MB/s per lane; measured profiles/r01_hash_v2_bitop3).
-GPU_MIN_PIECES = 8192
 
 
 class CompletionDB:
@@ -130,7 +127,7 @@ class FileStorage:
             return set()
         dev = device
         if device == "auto":
-            dev = "gpu" if (n >= GPU_MIN_PIECES and hashing.gpu_available()) else "cpu"
+            dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length)
         ok = hashing.verify_pieces(self.layout, self.info.piece_length, self.info.pieces, device=dev)
         have = {i for i, v in enumerate(ok) if v}
         if self.db is not None:

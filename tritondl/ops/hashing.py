@@ -125,12 +125,46 @@ def _resolve(device: str) -> str:
     return device
 
 
+# Cost model for device="auto" batch verification, calibrated on MI355X with
+# the box's 16-CPU share (profiles/r01_hash_v3_windows): the GPU path is
+# bounded by host->HBM copies (~45 GB/s) plus, because the kernel runs one lane
+# per piece, the per-lane SHA-1 rate (~55 MB/s) for one piece; the host path
+# runs ~1.5 GB/s per SHA-NI thread plus ~15 us of per-piece overhead.
+GPU_COPY_BPS = 45e9
+GPU_LANE_BPS = 55e6
+GPU_SETUP_S = 5e-3
+CPU_THREAD_BPS = 1.5e9
+CPU_PIECE_S = 15e-6
+
+
+def effective_cpus() -> int:
+    """CPUs this process may actually use: affinity mask and cgroup v2 quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def choose_device(n_pieces: int, piece_len: int, total: int, cpu_threads: int | None = None) -> str:
+    if n_pieces == 0 or not gpu_available():
+        return "cpu"
+    thr = max(1, min(cpu_threads or effective_cpus(), n_pieces))
+    t_gpu = total / GPU_COPY_BPS + piece_len / GPU_LANE_BPS + GPU_SETUP_S
+    t_cpu = (total / CPU_THREAD_BPS + n_pieces * CPU_PIECE_S) / thr
+    return "gpu" if t_gpu < t_cpu else "cpu"
+
+
 def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", threads: int = 0) -> bytes:
     """Concatenated digests of ``data`` split into ``piece_len`` pieces."""
     dev = _resolve(device)
     if dev == "gpu":
         return gpu_hasher().hash_buffer(kind, data, piece_len)
-    return _host.piece_hashes(kind, data, piece_len, threads)
+    return _host.piece_hashes(kind, data, piece_len, threads or effective_cpus())
 
 
 def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: bytes, kind: str = "sha1",
@@ -141,4 +175,4 @@ def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: by
     files = [(str(p), int(n)) for p, n in files]
     if dev == "gpu":
         return gpu_hasher().verify_files(files, piece_len, expected, kind)
-    return _host.verify_pieces(files, piece_len, expected, threads, kind)
+    return _host.verify_pieces(files, piece_len, expected, threads or effective_cpus(), kind)
