@@ -165,8 +165,8 @@ def test_gpu_many_small_windows(tmp_path, window_pieces):
 
 def test_choose_device_cost_model(monkeypatch):
     monkeypatch.setattr(hashing, "gpu_available", lambda: True)
-    # many small pieces: GPU (lane-parallel) wins even against a big host
-    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=64) == "gpu"
+    # many small pieces: GPU (lane-parallel) wins against a per-GPU host share
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=16) == "gpu"
     # few huge pieces: one lane per piece starves the GPU
     assert hashing.choose_device(64, 16 << 20, 64 * (16 << 20), cpu_threads=16) == "cpu"
     assert hashing.choose_device(0, 16384, 0) == "cpu"
