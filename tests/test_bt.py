@@ -221,3 +221,25 @@ def test_metadata_timeout_and_unsupported_scheme(tmp_path):
 def test_announce_dataclass():
     a = Announce(b"\x01" * 20, b"-TD0100-" + b"x" * 12, 6881)
     assert a.event == "started"
+
+
+def test_only_corrupt_seeder_never_completes_and_gets_banned(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"a.mkv": 200_000})
+        info = torrent_for(str(src / "a.mkv"), 32768)
+        bad = await Seeder(info, str(src), corrupt=True).start()
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        d = _dl()
+        t, _ = await d.open(str(dst), magnet_for(info, peers=[bad.addr]))
+        await asyncio.wait_for(t.got_info.wait(), 10)
+        await t.download_all()
+        for _ in range(100):
+            if bad.addr in t.banned:
+                break
+            await asyncio.sleep(0.05)
+        assert bad.addr in t.banned and t.nhave == 0
+        await t.close()
+        await bad.stop()
+    run(main())

@@ -159,14 +159,11 @@ class Seeder:
         await t.download_all()
         assert t.complete.is_set(), "seeder data does not verify"
         if self.corrupt:
-            orig = t._on_request
-
-            async def bad(p, pl):  # flip bytes in every served block
+            def bad(p, pl):  # serve every block with its bytes flipped
                 i, off, n = struct.unpack(">III", pl[:12])
-                data = await asyncio.get_running_loop().run_in_executor(None, t.storage.read, i, off, n)
+                data = t.storage.read(i, off, n)
                 p.wire.piece(i, off, bytes(x ^ 0xFF for x in data))
             t._on_request = bad  # type: ignore[assignment]
-            _ = orig
         self.torrent = t
         return self
 

@@ -389,58 +389,59 @@ class Torrent:
 
     # ------------------------------------------------------------ peer loop
     async def _peer_loop(self, p: _Peer) -> None:
-        last = time.monotonic()
+        last_drain = time.monotonic()
+        p.last_recv = time.monotonic()
         while not self.closed:
-            try:
-                m = await asyncio.wait_for(p.wire.read(), 120)
-            except asyncio.TimeoutError:
-                p.wire.keepalive()
-                continue
-            if m is None:
-                continue
-            mid, pl = m
-            if mid == pw.PIECE:
-                await self._on_block(p, pl)
-            elif mid == pw.HAVE:
-                (i,) = struct.unpack(">I", pl[:4])
-                self._peer_has(p, [i])
-            elif mid == pw.BITFIELD:
-                if self.info is not None:
-                    self._peer_has(p, sorted(pw.bits_to_set(pl, self.info.num_pieces)))
-                else:
-                    p.pending_bitfield = pl  # type: ignore[attr-defined]
-            elif mid == pw.HAVE_ALL:
-                if self.info is not None:
-                    self._peer_has(p, range(self.info.num_pieces))
-                else:
-                    p.pending_have_all = True  # type: ignore[attr-defined]
-            elif mid == pw.HAVE_NONE:
-                pass
-            elif mid == pw.UNCHOKE:
-                p.peer_choking = False
-                self._fill(p)
-            elif mid == pw.CHOKE:
-                p.peer_choking = True
-                if not p.hs.fast:
-                    self._release(p)
-            elif mid == pw.INTERESTED:
-                p.peer_interested = True
-            elif mid == pw.NOT_INTERESTED:
-                p.peer_interested = False
-            elif mid == pw.REQUEST:
-                await self._on_request(p, pl)
-            elif mid == pw.REJECT:
-                i, off, _n = struct.unpack(">III", pl[:12])
-                self._unrequest(p, i, off)
-                self._fill(p)
-            elif mid == pw.CANCEL:
-                pass
-            elif mid == pw.EXTENDED:
-                await self._on_extended(p, pl)
+            msgs = await p.wire.read_batch()
+            p.last_recv = time.monotonic()
+            for m in msgs:
+                if m is None:
+                    continue
+                await self._dispatch(p, m[0], m[1])
             now = time.monotonic()
-            if now - last > 1.0:
-                last = now
+            if now - last_drain > 0.5 or p.wire.writer.transport.get_write_buffer_size() > (4 << 20):
+                last_drain = now
                 await p.wire.drain()
+
+    async def _dispatch(self, p: _Peer, mid: int, pl: bytes) -> None:
+        if mid == pw.PIECE:
+            await self._on_block(p, pl)
+        elif mid == pw.HAVE:
+            (i,) = struct.unpack(">I", pl[:4])
+            self._peer_has(p, [i])
+        elif mid == pw.BITFIELD:
+            if self.info is not None:
+                self._peer_has(p, sorted(pw.bits_to_set(pl, self.info.num_pieces)))
+            else:
+                p.pending_bitfield = pl  # type: ignore[attr-defined]
+        elif mid == pw.HAVE_ALL:
+            if self.info is not None:
+                self._peer_has(p, range(self.info.num_pieces))
+            else:
+                p.pending_have_all = True  # type: ignore[attr-defined]
+        elif mid == pw.HAVE_NONE:
+            pass
+        elif mid == pw.UNCHOKE:
+            p.peer_choking = False
+            self._fill(p)
+        elif mid == pw.CHOKE:
+            p.peer_choking = True
+            if not p.hs.fast:
+                self._release(p)
+        elif mid == pw.INTERESTED:
+            p.peer_interested = True
+        elif mid == pw.NOT_INTERESTED:
+            p.peer_interested = False
+        elif mid == pw.REQUEST:
+            self._on_request(p, pl)
+        elif mid == pw.REJECT:
+            i, off, _n = struct.unpack(">III", pl[:12])
+            self._unrequest(p, i, off)
+            self._fill(p)
+        elif mid == pw.CANCEL:
+            pass
+        elif mid == pw.EXTENDED:
+            await self._on_extended(p, pl)
 
     def _peer_has(self, p: _Peer, idxs) -> None:
         if self.info is None:
@@ -580,15 +581,15 @@ class Torrent:
         if self.nhave == self.info.num_pieces:
             self.complete.set()
 
-    async def _on_request(self, p: _Peer, pl: bytes) -> None:
+    def _on_request(self, p: _Peer, pl: bytes) -> None:
         i, off, n = struct.unpack(">III", pl[:12])
         if self.info is None or self.storage is None or i >= len(self.have) or not self.have[i] or \
                 n > 128 * 1024 or off + n > self.info.piece_size(i):
             if p.hs.fast:
                 p.wire.reject(i, off, n)
             return
-        loop = asyncio.get_running_loop()
-        data = await loop.run_in_executor(None, self.storage.read, i, off, n)
+        # a 16 KiB pread from the page cache costs less than a thread hop
+        data = self.storage.read(i, off, n)
         p.wire.piece(i, off, data)
         self.uploaded += len(data)
 
@@ -597,6 +598,12 @@ class Torrent:
             await asyncio.sleep(2.0)
             now = time.monotonic()
             for p in list(self.peers.values()):
+                if now - getattr(p, "last_keepalive", 0) > 90:
+                    p.last_keepalive = now  # type: ignore[attr-defined]
+                    p.wire.keepalive()
+                if now - getattr(p, "last_recv", now) > 300:
+                    p.wire.close()  # silent for 5 minutes: drop
+                    continue
                 stale = [k for k, t in p.outstanding.items() if now - t > self.cfg.request_timeout]
                 if stale and len(stale) == len(p.outstanding):
                     for (i, off) in stale:
