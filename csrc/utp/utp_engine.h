@@ -55,6 +55,38 @@ uint32_t get32(const uint8_t* p) {
   return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
 }
 
+// FIFO byte buffer with O(1) amortised pop-front (std::string::erase(0, n)
+// per 1380-byte packet was an O(pending) memmove: quadratic at 8 MiB buffers).
+struct ByteQueue {
+  std::string buf;
+  size_t off = 0;
+  size_t size() const { return buf.size() - off; }
+  bool empty() const { return off == buf.size(); }
+  void append(const char* p, size_t n) {
+    if (off && off == buf.size()) {
+      buf.clear();
+      off = 0;
+    }
+    buf.append(p, n);
+  }
+  std::string take(size_t n) {
+    std::string r = buf.substr(off, n);
+    off += r.size();
+    if (off == buf.size()) {
+      buf.clear();
+      off = 0;
+    } else if (off >= (1u << 20) && off * 2 >= buf.size()) {
+      buf.erase(0, off);
+      off = 0;
+    }
+    return r;
+  }
+  void clear() {
+    buf.clear();
+    off = 0;
+  }
+};
+
 struct OutPkt {
   uint16_t seq;
   uint8_t type;
@@ -77,7 +109,7 @@ struct Conn {
   bool got_syn_ack = false;
   // send side
   std::deque<OutPkt> inflight;          // unacked, ordered by seq
-  std::string pending;                  // bytes not yet packetized
+  ByteQueue pending;                    // bytes not yet packetized
   uint32_t cur_window = 0;              // bytes in flight
   double max_window = kMinWindow * 4;   // LEDBAT cwnd
   uint32_t peer_wnd = kRecvWindow;
@@ -101,6 +133,7 @@ struct Conn {
   bool closing = false;                 // app called close: FIN after pending drains
   int64_t last_recv = 0;
   bool forget = false;                  // app is done with it: free once closed
+  bool in_batch = false;                // touched in the current receive batch
   // stats
   uint64_t bytes_sent = 0, bytes_recv = 0, retransmits = 0, timeouts = 0, fast_retransmits = 0;
 };
@@ -206,8 +239,34 @@ class Engine {
       }
       accept_data(c, h.seq, payload, h.type == ST_FIN);
     }
-    flush(c, now);
+    if (batch_) {
+      // defer: one flush (so one cumulative ACK + SACK) per connection per
+      // receive batch instead of one ACK per data packet
+      if (!c.in_batch) {
+        c.in_batch = true;
+        touched_.push_back(c.id);
+      }
+    } else {
+      flush(c, now);
+    }
     return c.id;
+  }
+
+  // Receive batching: between begin_batch() and end_batch(), incoming() only
+  // updates state; end_batch() flushes every touched connection once and
+  // returns their ids (the app then drains each one's inbuf once).
+  void begin_batch() { batch_ = true; }
+  std::vector<int> end_batch(int64_t now) {
+    batch_ = false;
+    std::vector<int> ids;
+    ids.swap(touched_);
+    for (int id : ids) {
+      Conn* c = get(id);
+      if (!c) continue;
+      c->in_batch = false;
+      flush(*c, now);
+    }
+    return ids;
   }
 
   size_t write(int id, const std::string& data) {
@@ -568,10 +627,9 @@ class Engine {
         OutPkt o;
         o.seq = c.seq_nr++;
         o.type = ST_DATA;
-        o.payload = c.pending.substr(0, n);
+        o.payload = c.pending.take(n);
         o.sent_at = now;
         o.transmissions = 1;
-        c.pending.erase(0, n);
         std::string pkt = header(c, ST_DATA, o.seq, now, nullptr);
         pkt += o.payload;
         out_.emplace_back(c.addr, std::move(pkt));
@@ -595,6 +653,8 @@ class Engine {
   std::unordered_map<std::string, int> by_key_;
   std::vector<std::pair<std::string, std::string>> out_;
   std::vector<int> accepted_;
+  bool batch_ = false;
+  std::vector<int> touched_;
 };
 
 }  // namespace tritondl_utp

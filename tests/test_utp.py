@@ -130,3 +130,27 @@ def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
         await st.close()
         _ = seed
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_receive_batch_coalesces_acks():
+    """Inside begin_batch/end_batch a burst of DATA yields one cumulative ACK."""
+    a, b = _utp.Engine(11), _utp.Engine(12)
+    cid = a.connect("B:1", 0)
+    for k, pkt in a.outgoing():
+        b.incoming(pkt, "A:1", 1)
+    (sid,) = b.accepted()
+    for k, pkt in b.outgoing():
+        a.incoming(pkt, "B:1", 2)
+    a.outgoing()
+    assert a.write(cid, b"x" * (_utp.MSS * 6)) == _utp.MSS * 6
+    a.tick(3)
+    burst = [p for _k, p in a.outgoing()]
+    assert len(burst) >= 4
+    b.begin_batch()
+    for p in burst:
+        b.incoming(p, "A:1", 4)
+    assert b.outgoing() == []            # nothing sent mid-batch
+    assert b.end_batch(5) == [sid]
+    acks = b.outgoing()
+    assert len(acks) == 1 and acks[0][1][0] >> 4 == 2     # one ST_STATE
+    assert b.read(sid) == b"x" * (_utp.MSS * len(burst))

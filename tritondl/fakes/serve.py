@@ -2,6 +2,7 @@
 not the fakes competing for its event loop).
 
     python -m tritondl.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
+    python -m tritondl.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
 
 Prints ONE JSON line ``{"kind":..., "endpoint": ..., "url": ...}`` on stdout
 once listening, then serves until stdin closes or SIGTERM.  The origin also
@@ -45,7 +46,28 @@ class SyntheticOrigin(Origin):
         return await super()._handle(request)
 
 
-async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None) -> None:
+async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
+                 seed_path: str | None = None, piece_kb: int = 1024) -> None:
+    if kind == "seed":
+        from ..fetch.bt.torrent import Torrent, TorrentConfig
+        from .swarm import magnet_for, torrent_for
+        assert seed_path, "--path required"
+        info = torrent_for(seed_path, piece_kb << 10)
+        cfg = TorrentConfig(listen_host="127.0.0.1", listen_port=port, seed=True, verify_device="cpu", utp=True)
+        srv = Torrent(info.infohash, os.path.dirname(os.path.abspath(seed_path)), cfg, info=info)
+        await srv.start()
+        await srv.download_all()
+        info_d = {"kind": kind, "endpoint": f"127.0.0.1:{srv.port}", "url": magnet_for(info),
+                  "infohash": info.infohash.hex(), "bytes": info.total_length}
+        print(json.dumps(info_d), flush=True)
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for sg in (signal.SIGTERM, signal.SIGINT):
+            loop.add_signal_handler(sg, stop.set)
+        loop.add_reader(sys.stdin.fileno(), lambda: stop.set() if not os.read(sys.stdin.fileno(), 4096) else None)
+        await stop.wait()
+        await srv.close()
+        return
     if kind == "broker":
         srv = await Broker(port=port).start()
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.url}
@@ -69,13 +91,15 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["broker", "origin", "s3"])
+    ap.add_argument("kind", choices=["broker", "origin", "s3", "seed"])
+    ap.add_argument("--path", default=None, help="seed: file or directory to seed")
+    ap.add_argument("--piece-kb", type=int, default=1024)
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--s3-store", default="discard", choices=["memory", "discard", "disk"])
     ap.add_argument("--access-key", default=None)
     ap.add_argument("--secret-key", default=None)
     a = ap.parse_args()
-    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key))
+    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb))
 
 
 if __name__ == "__main__":

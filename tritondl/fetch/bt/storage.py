@@ -31,6 +31,9 @@ class CompletionDB:
         self._lock = threading.Lock()
         self.conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
         self.conn.execute("PRAGMA journal_mode=WAL")
+        # WAL + NORMAL: no fsync per piece mark; a crash can only forget the
+        # newest marks, which resume re-verification recovers anyway.
+        self.conn.execute("PRAGMA synchronous=NORMAL")
         self.conn.execute("CREATE TABLE IF NOT EXISTS piece_completion (infohash BLOB NOT NULL, "
                           "idx INTEGER NOT NULL, complete INTEGER NOT NULL, PRIMARY KEY (infohash, idx))")
 

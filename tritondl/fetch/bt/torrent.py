@@ -65,6 +65,32 @@ class _Piece:
     buf: bytearray
     received: set = field(default_factory=set)            # block indexes
     requested: dict = field(default_factory=dict)          # block idx -> set(peer keys)
+    next_b: int = 0                                        # blocks < next_b were handed out once
+    redo: list = field(default_factory=list)               # handed-out blocks whose requests all lapsed
+
+    def take(self) -> int | None:
+        """Next never-requested (or lapsed) block; O(1) amortised instead of a
+        per-call scan over every block (the scan was half the leecher's CPU)."""
+        while self.redo:
+            b = self.redo.pop()
+            if b not in self.received and b not in self.requested:
+                return b
+        if self.next_b < self.nblocks:
+            self.next_b += 1
+            return self.next_b - 1
+        return None
+
+    def lapse(self, b: int, key) -> bool:
+        """Drop key's request for block b; True if b became requestable again."""
+        s = self.requested.get(b)
+        if s is not None:
+            s.discard(key)
+            if not s:
+                del self.requested[b]
+                if b not in self.received:
+                    self.redo.append(b)
+                    return True
+        return False
 
 
 class _Peer:
@@ -112,6 +138,9 @@ class Torrent:
         self.nhave = 0
         self.avail: list[int] = []
         self.pieces: dict[int, _Piece] = {}
+        self.open_pieces: dict[int, _Piece] = {}        # subset of pieces with blocks left to hand out
+        self.verifying: set[int] = set()                # complete pieces being hashed/written
+        self._finishers: set[asyncio.Task] = set()
         self.peers: dict[tuple[str, int], _Peer] = {}
         self.known: set[tuple[str, int]] = set()
         self.connecting: set[tuple[str, int]] = set()
@@ -177,6 +206,9 @@ class Torrent:
         for t in list(self._tasks):
             t.cancel()
         for t in list(self._tasks):
+            with contextlib.suppress(BaseException):
+                await t
+        for t in list(self._finishers):   # executor hash/write jobs must land before storage closes
             with contextlib.suppress(BaseException):
                 await t
         if self.storage is not None:
@@ -365,12 +397,8 @@ class Torrent:
     def _release(self, p: _Peer) -> None:
         for (i, off) in list(p.outstanding):
             pc = self.pieces.get(i)
-            if pc is not None:
-                s = pc.requested.get(off // BLOCK)
-                if s is not None:
-                    s.discard(p.key)
-                    if not s:
-                        del pc.requested[off // BLOCK]
+            if pc is not None and pc.lapse(off // BLOCK, p.key):
+                self.open_pieces[i] = pc
         p.outstanding.clear()
         for q in self.peers.values():
             if q is not p:
@@ -452,10 +480,14 @@ class Torrent:
         self._update_interest(p)
         self._fill(p)
 
+    def _wants(self, p: _Peer) -> bool:
+        """Does p have any piece we lack?  (bitwise over the whole bitmap, in C)"""
+        return bool(int.from_bytes(p.have, "little") & ~int.from_bytes(self.have, "little"))
+
     def _update_interest(self, p: _Peer) -> None:
         if self.info is None or not self._downloading:
             return
-        want = any(p.have[i] and not self.have[i] for i in range(len(p.have))) if p.nhave else False
+        want = self._wants(p) if p.nhave else False
         if want != p.am_interested:
             p.am_interested = want
             p.wire.send(pw.INTERESTED if want else pw.NOT_INTERESTED)
@@ -464,20 +496,27 @@ class Torrent:
     def _pick(self, p: _Peer) -> tuple[int, int, int] | None:
         """Next (piece, offset, length) to request from p; None if nothing."""
         assert self.info is not None
-        # 1) continue pieces already in progress
-        for i, pc in self.pieces.items():
-            if not p.have[i]:
-                continue
-            for b in range(pc.nblocks):
-                if b not in pc.received and b not in pc.requested:
+        # 1) continue in-progress pieces that still have unrequested blocks
+        exhausted = []
+        try:
+            for i, pc in self.open_pieces.items():
+                if not p.have[i]:
+                    continue
+                b = pc.take()
+                if b is not None:
                     return i, b * BLOCK, min(BLOCK, pc.size - b * BLOCK)
+                exhausted.append(i)
+        finally:
+            for i in exhausted:
+                del self.open_pieces[i]
         # 2) start the rarest piece this peer has (random tie-break)
         best, best_av = None, math.inf
         n = self.info.num_pieces
         start = random.randrange(n) if n else 0
         for k in range(n):
             i = (start + k) % n
-            if p.have[i] and not self.have[i] and i not in self.pieces and self.avail[i] < best_av:
+            if p.have[i] and not self.have[i] and i not in self.pieces and self.avail[i] < best_av \
+                    and i not in self.verifying:
                 best, best_av = i, self.avail[i]
                 if best_av <= 1:
                     break
@@ -485,6 +524,9 @@ class Torrent:
             size = self.info.piece_size(best)
             pc = _Piece(size, -(-size // BLOCK), bytearray(size))
             self.pieces[best] = pc
+            pc.next_b = 1
+            if pc.nblocks > 1:
+                self.open_pieces[best] = pc
             return best, 0, min(BLOCK, size)
         # 3) end game: duplicate outstanding requests of other peers
         for i, pc in self.pieces.items():
@@ -511,12 +553,8 @@ class Torrent:
     def _unrequest(self, p: _Peer, i: int, off: int) -> None:
         p.outstanding.pop((i, off), None)
         pc = self.pieces.get(i)
-        if pc is not None:
-            s = pc.requested.get(off // BLOCK)
-            if s is not None:
-                s.discard(p.key)
-                if not s:
-                    del pc.requested[off // BLOCK]
+        if pc is not None and pc.lapse(off // BLOCK, p.key):
+            self.open_pieces[i] = pc
 
     async def _on_block(self, p: _Peer, pl: bytes) -> None:
         i, off = struct.unpack(">II", pl[:8])
@@ -543,14 +581,20 @@ class Torrent:
         else:
             pc.requested.pop(b, None)
         if len(pc.received) == pc.nblocks:
+            # hash+write off-loop; keep requesting meanwhile (the piece stays
+            # out of the picker via `verifying` until it lands or fails)
             del self.pieces[i]
-            await self._finish_piece(i, pc, p)
+            self.open_pieces.pop(i, None)
+            self.verifying.add(i)
+            t = asyncio.get_running_loop().create_task(self._finish_piece(i, pc, p))
+            self._finishers.add(t)
+            t.add_done_callback(self._finishers.discard)
         self._fill(p)
 
     async def _finish_piece(self, i: int, pc: _Piece, src: _Peer) -> None:
         assert self.info is not None and self.storage is not None
         loop = asyncio.get_running_loop()
-        data = bytes(pc.buf)
+        data = pc.buf                     # no longer shared: the piece left self.pieces
         expect = self.info.piece_hash(i)
         st = self.storage
 
@@ -558,9 +602,13 @@ class Torrent:
             if hashlib.sha1(data).digest() != expect:
                 return False
             st.write(i, 0, data)
+            st.mark(i, True)
             return True
 
-        ok = await loop.run_in_executor(None, verify_and_write)
+        try:
+            ok = await loop.run_in_executor(None, verify_and_write)
+        finally:
+            self.verifying.discard(i)
         if not ok:
             src.bad += 1
             log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
@@ -572,10 +620,9 @@ class Torrent:
             return
         self.have[i] = 1
         self.nhave += 1
-        st.mark(i, True)
         for q in list(self.peers.values()):
             q.wire.have(i)
-            if q.am_interested and not any(q.have[k] and not self.have[k] for k in range(len(q.have))):
+            if q.am_interested and q.have[i] and not self._wants(q):
                 q.am_interested = False
                 q.wire.send(pw.NOT_INTERESTED)
         if self.nhave == self.info.num_pieces:

@@ -4,14 +4,16 @@ One UDP socket per :class:`UtpSocket` multiplexes every uTP connection (as
 libutp / anacrolix do, sharing the BitTorrent listen port number).  Each
 connection is exposed as a standard ``(asyncio.StreamReader,
 asyncio.StreamWriter)`` pair, so the peer-wire code runs unchanged over TCP
-or uTP.  Python only moves datagrams and bytes; sequencing, SACK, RTO and
-LEDBAT live in C++.
+or uTP.  Python never touches individual datagrams: the event loop only
+reports the socket readable/writable and the native ``Pump`` drains it with
+recvmmsg / sendmmsg; sequencing, SACK, RTO and LEDBAT live in C++.
 """
 
 from __future__ import annotations
 
 import asyncio
 import contextlib
+import socket
 import time
 
 try:
@@ -128,20 +130,32 @@ class _Stream:
         self.eof = False
 
 
-class UtpSocket(asyncio.DatagramProtocol):
+class UtpSocket:
     def __init__(self, seed: int = 0) -> None:
         self.engine = _utp.Engine(seed)
-        self.transport: asyncio.DatagramTransport | None = None
+        self._sock: socket.socket | None = None
+        self._pump = None
+        self._writing = False
         self.streams: dict[int, _Stream] = {}
         self.accept_q: asyncio.Queue = asyncio.Queue()
         self.local_addr: tuple[str, int] = ("0.0.0.0", 0)
         self._ticker: asyncio.Task | None = None
+        self._loop: asyncio.AbstractEventLoop | None = None
         self.other_datagram = None   # optional handler for non-uTP datagrams (e.g. DHT on a shared port)
 
     async def start(self, host: str = "0.0.0.0", port: int = 0) -> "UtpSocket":
-        loop = asyncio.get_running_loop()
-        self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(host, port))
-        self.local_addr = self.transport.get_extra_info("sockname")[:2]
+        self._loop = asyncio.get_running_loop()
+        fam = socket.AF_INET6 if ":" in host else socket.AF_INET
+        sock = socket.socket(fam, socket.SOCK_DGRAM)
+        sock.setblocking(False)
+        for opt in (socket.SO_RCVBUF, socket.SO_SNDBUF):
+            with contextlib.suppress(OSError):
+                sock.setsockopt(socket.SOL_SOCKET, opt, 8 << 20)   # capped by rmem_max/wmem_max
+        sock.bind((host, port))
+        self._sock = sock
+        self._pump = _utp.Pump(self.engine, sock.fileno())
+        self.local_addr = sock.getsockname()[:2]
+        self._loop.add_reader(sock.fileno(), self._on_readable)
         self._ticker = asyncio.ensure_future(self._tick_loop())
         return self
 
@@ -159,16 +173,33 @@ class UtpSocket(asyncio.DatagramProtocol):
         self._flush()
         if self._ticker is not None:
             self._ticker.cancel()
-        if self.transport is not None:
-            self.transport.close()
-            self.transport = None
+        if self._sock is not None:
+            with contextlib.suppress(Exception):
+                self._loop.remove_reader(self._sock.fileno())   # type: ignore[union-attr]
+                self._loop.remove_writer(self._sock.fileno())   # type: ignore[union-attr]
+            self._sock.close()
+            self._sock = None
 
     # ------------------------------------------------------------ io
-    def datagram_received(self, data: bytes, addr) -> None:
-        if not data or (data[0] & 0x0F) != 1 or (data[0] >> 4) > 4:
-            if self.other_datagram is not None:
-                self.other_datagram(data, addr)
+    def _on_readable(self) -> None:
+        if self._sock is None:
             return
+        touched, others = self._pump.recv(_now_us())
+        for new in self.engine.accepted():
+            st = self.stats(new)
+            s = _Stream(self, new, _addr(st["addr"]))
+            s.connected.set()
+            self.streams[new] = s
+            self.accept_q.put_nowait(s)
+        for cid in touched:
+            self._service(cid)
+        if others and self.other_datagram is not None:
+            for data, addr in others:
+                self.other_datagram(data, addr)
+        self._flush()
+
+    def datagram_received(self, data: bytes, addr) -> None:
+        """Feed one datagram by hand (tests / a foreign socket owner)."""
         cid = self.engine.incoming(data, _key(addr[:2]), _now_us())
         for new in self.engine.accepted():
             s = _Stream(self, new, _addr(self.stats(new).get("addr", _key(addr[:2]))))
@@ -200,10 +231,18 @@ class UtpSocket(asyncio.DatagramProtocol):
         s.transport._push()
 
     def _flush(self) -> None:
-        if self.transport is None:
+        if self._sock is None:
+            self.engine.outgoing()          # closed: drop
             return
-        for key, pkt in self.engine.outgoing():
-            self.transport.sendto(pkt, _addr(key))
+        if self._pump.send() and not self._writing:
+            self._writing = True
+            self._loop.add_writer(self._sock.fileno(), self._on_writable)   # type: ignore[union-attr]
+
+    def _on_writable(self) -> None:
+        if self._sock is None or not self._pump.send():
+            self._writing = False
+            if self._sock is not None:
+                self._loop.remove_writer(self._sock.fileno())   # type: ignore[union-attr]
 
     async def _tick_loop(self) -> None:
         try:
