@@ -181,6 +181,25 @@ py::tuple py_aws_chunk_decode(const std::string& key, const std::string& amzdate
 
 PYBIND11_MODULE(_hash_host, m) {
   m.doc() = "tritondl host hashing (OpenSSL EVP, GIL-free, threaded piece verification)";
+  py::class_<Rc4>(m, "Rc4")
+      .def(py::init([](py::bytes key, size_t drop) {
+             std::string k = key;
+             if (k.empty()) throw std::invalid_argument("RC4 key must not be empty");
+             auto* r = new Rc4(reinterpret_cast<const uint8_t*>(k.data()), k.size());
+             if (drop) r->discard(drop);
+             return r;
+           }),
+           py::arg("key"), py::arg("drop") = 1024)
+      .def("crypt", [](Rc4& r, const py::buffer& b) {
+        py::buffer_info bi;
+        BufView v = view_of(b, bi);
+        std::string out(v.len, '\0');
+        {
+          py::gil_scoped_release nogil;
+          r.crypt(reinterpret_cast<const uint8_t*>(v.ptr), reinterpret_cast<uint8_t*>(out.data()), v.len);
+        }
+        return py::bytes(out);
+      });
   py::class_<Hasher>(m, "Hasher")
       .def(py::init<const std::string&>())
       .def("update", &Hasher::update)

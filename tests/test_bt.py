@@ -243,3 +243,124 @@ def test_only_corrupt_seeder_never_completes_and_gets_banned(tmp_path):
         await t.close()
         await bad.stop()
     run(main())
+
+
+# ----------------------------------------------------------------- PEX / web seeds
+
+
+def test_pex_message_roundtrip():
+    from tritondl.fetch.bt import peer as pw
+    msg = pw.pex_msg([("10.0.0.1", 6881), ("::1", 7000)], [("10.0.0.2", 1)], {("10.0.0.1", 6881): 0x12})
+    d = bencode.decode(msg)
+    assert d[b"added.f"] == b"\x12" and len(d[b"added"]) == 6 and len(d[b"added6"]) == 18
+    added, dropped = pw.parse_pex(msg)
+    assert added == [("10.0.0.1", 6881), ("::1", 7000)] and dropped == [("10.0.0.2", 1)]
+
+
+def test_pex_introduces_second_seeder(tmp_path):
+    """The leecher only knows seeder A; A (connected to B) gossips B via
+    ut_pex and the leecher dials B."""
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"m.mkv": 400_000})
+        info = torrent_for(str(src / "m.mkv"), 16384)
+        b = await Seeder(info, str(src)).start()
+        a = await Seeder(info, str(src)).start()
+        a.torrent.add_peer_addr(b.addr)
+        for _ in range(100):
+            if b.addr in a.torrent.peers:
+                break
+            await asyncio.sleep(0.02)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        d = _dl()
+        d.cfg.pex_interval = 0.1
+        t, _ = await d.open(str(dst), magnet_for(info, peers=[a.addr]))
+        for _ in range(200):
+            a.torrent.pex_round()
+            if b.addr in t.peers:
+                break
+            await asyncio.sleep(0.05)
+        assert b.addr in t.peers and t.pex_learned >= 1
+        await t.close()
+        await a.stop()
+        await b.stop()
+    run(main())
+
+
+def test_private_torrent_disables_pex(tmp_path):
+    from tritondl.fetch.bt.metainfo import make_info
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"p.mkv": 50_000})
+        info = make_info(str(src / "p.mkv"), 16384, private=True)
+        s = await Seeder(info, str(src)).start()
+        assert s.torrent.private
+        from tritondl.fetch.bt import peer as pw
+        # a ut_pex message to a private torrent is ignored
+        s.torrent.cfg.pex = True
+        class P:  # minimal stand-in peer
+            ext = None
+        await s.torrent._on_extended(P(), bytes([pw.UT_PEX_ID]) + pw.pex_msg([("10.9.9.9", 5)], []))
+        assert ("10.9.9.9", 5) not in s.torrent.known
+        await s.stop()
+    run(main())
+
+
+def test_webseed_only_multi_file_torrent_file(tmp_path):
+    """No peers at all: a .torrent with url-list downloads entirely from the
+    HTTP web seed (BEP 19 multi-file layout, pieces straddling files)."""
+    async def main():
+        src = tmp_path / "src" / "Show"
+        make_payload(str(src), {"a b.mkv": 300_001, "sub/c.srt": 70_000, "d.txt": 5})
+        info = torrent_for(str(src), 32768)
+        o = await Origin().start()
+        for rel in ("a b.mkv", "sub/c.srt", "d.txt"):
+            from urllib.parse import quote
+            o.add("/seed/Show/" + quote(rel), (src / rel).read_bytes())
+        url = o.add("/t/show.torrent", torrent_file_bytes(info, url_list=[f"http://127.0.0.1:{o.port}/seed/"]))
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        d = _dl()
+        t, _ = await d.open(str(dst), url)
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 30)
+        ws = t.webseed_clients[0]
+        assert ws.pieces_ok == info.num_pieces
+        await t.close()
+        _check_tree(str(src), str(dst))
+        await o.stop()
+    run(main())
+
+
+def test_webseed_via_magnet_ws_single_file_and_bad_seed_dropped(tmp_path):
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"film.mkv": 200_000})
+        info = torrent_for(str(src / "film.mkv"), 16384)
+        seeder = await Seeder(info, str(src)).start()   # metadata source (ut_metadata)
+        o = await Origin().start()
+        o.add("/good/film.mkv", (src / "film.mkv").read_bytes())
+        o.add("/bad/film.mkv", os.urandom(200_000))
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        good = f"http://127.0.0.1:{o.port}/good/film.mkv"
+        bad = f"http://127.0.0.1:{o.port}/bad/film.mkv"
+        m = magnet_for(info, peers=[seeder.addr], web_seeds=[bad, good])
+        assert parse_magnet(m).web_seeds == [bad, good]
+        await seeder.stop()                   # after metadata, only the web seeds remain
+        d = _dl()
+        t, _ = await d.open(str(dst), m)
+        seeder2 = await Seeder(info, str(src)).start()
+        t.add_peer_addr(seeder2.addr)
+        await asyncio.wait_for(t.got_info.wait(), 10)
+        await seeder2.stop()
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 30)
+        wbad, wgood = t.webseed_clients
+        assert wbad.dead and wbad.pieces_ok == 0 and wgood.pieces_ok > 0
+        await t.close()
+        assert (dst / "film.mkv").read_bytes() == (src / "film.mkv").read_bytes()
+        await seeder.stop()
+        await o.stop()
+    run(main())

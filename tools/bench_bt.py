@@ -29,6 +29,7 @@ async def main() -> int:
     ap.add_argument("--piece-kb", type=int, default=1024)
     ap.add_argument("--utp", action="store_true", help="disable TCP dialing: uTP only")
     ap.add_argument("--profile", default="")
+    ap.add_argument("--encryption", default="allow", help="MSE policy for seeders and leecher")
     a = ap.parse_args()
     from tritondl.bench_job import Backend
     from tritondl.fakes.swarm import make_payload
@@ -43,7 +44,8 @@ async def main() -> int:
         src = os.path.join(td, "src")
         make_payload(src, {"movie.mkv": a.mb << 20})
         seeds = [await Backend("seed", ["--path", os.path.join(src, "movie.mkv"), "--piece-kb",
-                                        str(a.piece_kb)]).start() for _ in range(a.seeds)]
+                                        str(a.piece_kb), "--encryption", a.encryption]).start()
+                 for _ in range(a.seeds)]
         magnet = seeds[0].info["url"]
         peers = "&".join(f"x.pe={s.info['endpoint']}" for s in seeds)
         magnet = magnet + "&" + peers
@@ -53,7 +55,8 @@ async def main() -> int:
             Torrent._dial_tcp = no_tcp  # type: ignore[assignment]
         dst = os.path.join(td, "dst")
         os.makedirs(dst)
-        d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True),
+        d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
+                                            encryption=a.encryption),
                               progress_interval=1.0, use_dht=False)
         prof = None
         if a.profile:
@@ -70,7 +73,8 @@ async def main() -> int:
         assert os.path.getsize(os.path.join(dst, "movie.mkv")) == a.mb << 20
         print(json.dumps({"metric": "bt_ingest_MB_per_sec", "value": round(a.mb * 1.048576 / dt, 1),
                           "seconds": round(dt, 3), "mb": a.mb, "seeds": a.seeds, "piece_kb": a.piece_kb,
-                          "transport": "utp" if a.utp else "tcp+utp"}), flush=True)
+                          "transport": "utp" if a.utp else "tcp+utp",
+                          "encryption": a.encryption}), flush=True)
     finally:
         for s in seeds:
             await s.stop()

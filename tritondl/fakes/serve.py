@@ -47,13 +47,14 @@ class SyntheticOrigin(Origin):
 
 
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
-                 seed_path: str | None = None, piece_kb: int = 1024) -> None:
+                 seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow") -> None:
     if kind == "seed":
         from ..fetch.bt.torrent import Torrent, TorrentConfig
         from .swarm import magnet_for, torrent_for
         assert seed_path, "--path required"
         info = torrent_for(seed_path, piece_kb << 10)
-        cfg = TorrentConfig(listen_host="127.0.0.1", listen_port=port, seed=True, verify_device="cpu", utp=True)
+        cfg = TorrentConfig(listen_host="127.0.0.1", listen_port=port, seed=True, verify_device="cpu", utp=True,
+                            encryption=encryption)
         srv = Torrent(info.infohash, os.path.dirname(os.path.abspath(seed_path)), cfg, info=info)
         await srv.start()
         await srv.download_all()
@@ -94,12 +95,13 @@ def main() -> None:
     ap.add_argument("kind", choices=["broker", "origin", "s3", "seed"])
     ap.add_argument("--path", default=None, help="seed: file or directory to seed")
     ap.add_argument("--piece-kb", type=int, default=1024)
+    ap.add_argument("--encryption", default="allow", help="seed: MSE policy")
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--s3-store", default="discard", choices=["memory", "discard", "disk"])
     ap.add_argument("--access-key", default=None)
     ap.add_argument("--secret-key", default=None)
     a = ap.parse_args()
-    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb))
+    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption))
 
 
 if __name__ == "__main__":

@@ -139,12 +139,14 @@ class Seeder:
     """Seed an existing file/dir: serves pieces to any peer that connects."""
 
     def __init__(self, info: Info, data_dir: str, *, trackers: list[str] | None = None,
-                 dht_bootstrap: list[tuple[str, int]] | None = None, corrupt: bool = False) -> None:
+                 dht_bootstrap: list[tuple[str, int]] | None = None, corrupt: bool = False,
+                 encryption: str = "allow") -> None:
         self.info = info
         self.data_dir = data_dir
         self.trackers = trackers or []
         self.dht_bootstrap = dht_bootstrap
         self.corrupt = corrupt
+        self.encryption = encryption
         self.torrent: Torrent | None = None
         self.dht: DHTNode | None = None
 
@@ -153,7 +155,7 @@ class Seeder:
             self.dht = await DHTNode(host="127.0.0.1", bootstrap=self.dht_bootstrap).start()
             await self.dht.bootstrap()
         cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, tracker_min_interval=1.0, dht_interval=1.0,
-                            verify_device="cpu")
+                            verify_device="cpu", encryption=self.encryption)
         t = Torrent(self.info.infohash, self.data_dir, cfg, info=self.info, trackers=self.trackers, dht=self.dht)
         await t.start()
         await t.download_all()
@@ -192,9 +194,10 @@ def torrent_for(path: str, piece_length: int = 256 * 1024) -> Info:
     return make_info(path, piece_length)
 
 
-def magnet_for(info: Info, trackers: list[str] | None = None, peers: list[tuple[str, int]] | None = None) -> str:
-    return Magnet(info.infohash, info.name, trackers or [], peers or []).uri()
+def magnet_for(info: Info, trackers: list[str] | None = None, peers: list[tuple[str, int]] | None = None,
+               web_seeds: list[str] | None = None) -> str:
+    return Magnet(info.infohash, info.name, trackers or [], peers or [], web_seeds or []).uri()
 
 
-def torrent_file_bytes(info: Info, trackers: list[str] | None = None) -> bytes:
-    return Metainfo(info, [[t] for t in (trackers or [])]).encode()
+def torrent_file_bytes(info: Info, trackers: list[str] | None = None, url_list: list[str] | None = None) -> bytes:
+    return Metainfo(info, [[t] for t in (trackers or [])], url_list=url_list or []).encode()

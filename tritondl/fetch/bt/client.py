@@ -60,7 +60,8 @@ class TorrentDownloader:
 
     @classmethod
     def from_config(cls, c, http=None) -> "TorrentDownloader":
-        tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, verify_device=c.gpu_verify
+        tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, pex=c.bt_pex, encryption=c.bt_encryption,
+                           verify_device=c.gpu_verify
                            if c.gpu_verify in ("auto", "cpu", "gpu") else ("cpu" if c.gpu_verify == "off" else "auto"))
         return cls(tc, metadata_timeout=c.metadata_timeout_s, progress_interval=c.progress_interval_s,
                    use_dht=c.bt_dht, dht_bootstrap=_parse_hostports(c.bt_bootstrap))
@@ -91,12 +92,14 @@ class TorrentDownloader:
         trackers: list[str] = list(self.extra_trackers)
         peers: list[tuple[str, int]] = []
         name = ""
+        webseeds: list[str] = []
         if u.scheme == "magnet":
             try:
                 m: Magnet = parse_magnet(url)
             except MetainfoError as e:
                 raise TorrentError(f"failed to add torrent: {e}") from e
             ih, trackers, peers, name = m.infohash, trackers + m.trackers, m.peers, m.display_name
+            webseeds = list(m.web_seeds)
         elif u.scheme in ("http", "https"):
             try:
                 mi = Metainfo.parse(await self._fetch_torrent_file(url))
@@ -104,13 +107,15 @@ class TorrentDownloader:
                 raise TorrentError(f"failed to add torrent: {e}") from e
             ih, info = mi.infohash, mi.info
             trackers += [t for tier in mi.announce for t in tier]
+            webseeds = list(mi.url_list)
         else:
             raise TorrentError(f"unsupported scheme '{u.scheme}'")
         dht = None
         if self.use_dht:
             dht = await DHTNode(bootstrap=self.dht_bootstrap).start()
             asyncio.ensure_future(dht.bootstrap())
-        t = Torrent(ih, base_dir, self.cfg, info=info, trackers=trackers, peers=peers, dht=dht, name_hint=name)
+        t = Torrent(ih, base_dir, self.cfg, info=info, trackers=trackers, peers=peers, dht=dht, name_hint=name,
+                    webseeds=webseeds)
         await t.start()
         return t, dht
 

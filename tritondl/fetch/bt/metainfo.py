@@ -153,6 +153,8 @@ class Metainfo:
         if self.announce:
             d[b"announce"] = self.announce[0][0].encode()
             d[b"announce-list"] = [[u.encode() for u in t] for t in self.announce]
+        if self.url_list:
+            d[b"url-list"] = [u.encode() for u in self.url_list]
         return _encode_with_raw(d)
 
 
@@ -192,6 +194,7 @@ class Magnet:
             parts.append("dn=" + quote(self.display_name))
         parts += ["tr=" + quote(t, safe="") for t in self.trackers]
         parts += [f"x.pe={h}:{p}" for h, p in self.peers]
+        parts += ["ws=" + quote(w, safe="") for w in self.web_seeds]
         return "magnet:?" + "&".join(parts)
 
 

@@ -1,6 +1,6 @@
 """BitTorrent peer wire protocol: handshake + messages (BEP 3), Fast
 extension subset (BEP 6: have_all / have_none / reject), extension protocol
-(BEP 10) and ut_metadata (BEP 9).
+(BEP 10), ut_metadata (BEP 9) and ut_pex peer exchange (BEP 11).
 
 Transport-agnostic: works over any asyncio (reader, writer) pair — TCP, or
 the native uTP transport (:mod:`tritondl.fetch.bt.utp`).
@@ -22,6 +22,8 @@ SUGGEST, HAVE_ALL, HAVE_NONE, REJECT, ALLOWED_FAST = 0x0D, 0x0E, 0x0F, 0x10, 0x1
 EXTENDED = 20
 EXT_HANDSHAKE = 0
 UT_METADATA_ID = 3            # the id WE assign to ut_metadata in our extended handshake
+UT_PEX_ID = 1                 # ... and to ut_pex
+PEX_MAX_ADDED = 50            # BEP 11: at most 50 added / 50 dropped per message
 META_REQUEST, META_DATA, META_REJECT = 0, 1, 2
 MAX_MSG = 2 * 1024 * 1024 + 13
 
@@ -64,11 +66,14 @@ def encode_handshake(infohash: bytes, peer_id: bytes, reserved: bytes | None = N
     return bytes([len(PSTR)]) + PSTR + (reserved or reserved_bytes()) + infohash + peer_id
 
 
-async def read_handshake(reader: asyncio.StreamReader) -> Handshake:
-    b = await reader.readexactly(HANDSHAKE_LEN)
-    if b[0] != len(PSTR) or b[1:20] != PSTR:
+def parse_handshake(b: bytes) -> Handshake:
+    if len(b) != HANDSHAKE_LEN or b[0] != len(PSTR) or b[1:20] != PSTR:
         raise PeerError("bad protocol string in handshake")
     return Handshake(b[20:28], b[28:48], b[48:68])
+
+
+async def read_handshake(reader) -> Handshake:
+    return parse_handshake(await reader.readexactly(HANDSHAKE_LEN))
 
 
 @dataclass
@@ -193,8 +198,12 @@ class Wire:
     def extended(self, ext_id: int, payload: bytes) -> None:
         self.send(EXTENDED, bytes([ext_id]) + payload)
 
-    def ext_handshake(self, metadata_size: int | None, port: int | None = None, reqq: int = 512) -> None:
-        d: dict = {b"m": {b"ut_metadata": UT_METADATA_ID}, b"v": b"tritondl/0.1", b"reqq": reqq}
+    def ext_handshake(self, metadata_size: int | None, port: int | None = None, reqq: int = 512,
+                      pex: bool = True) -> None:
+        m = {b"ut_metadata": UT_METADATA_ID}
+        if pex:
+            m[b"ut_pex"] = UT_PEX_ID
+        d: dict = {b"m": m, b"v": b"tritondl/0.1", b"reqq": reqq}
         if metadata_size:
             d[b"metadata_size"] = metadata_size
         if port:
@@ -227,6 +236,51 @@ def parse_ext_handshake(payload: bytes) -> ExtHandshake:
                         d.get(b"reqq") if isinstance(d.get(b"reqq"), int) else None,
                         (d.get(b"v") or b"").decode(errors="replace") if isinstance(d.get(b"v"), bytes) else "",
                         d.get(b"p") if isinstance(d.get(b"p"), int) else None)
+
+
+def pex_msg(added: list[tuple[str, int]], dropped: list[tuple[str, int]],
+            flags: dict[tuple[str, int], int] | None = None) -> bytes:
+    """ut_pex payload: compact IPv4 (``added``/``dropped``) and IPv6
+    (``added6``/``dropped6``) peer lists with one flag byte per added peer
+    (0x02 seed, 0x04 supports uTP, 0x10 reachable/outgoing-connectable)."""
+    import ipaddress
+    d: dict = {}
+    for key, peers in ((b"added", added), (b"dropped", dropped)):
+        v4 = [a for a in peers if ":" not in a[0]]
+        v6 = [a for a in peers if ":" in a[0]]
+        d[key] = b"".join(ipaddress.IPv4Address(h).packed + struct.pack(">H", pt) for h, pt in v4)
+        if v6:
+            d[key + b"6"] = b"".join(ipaddress.IPv6Address(h).packed + struct.pack(">H", pt) for h, pt in v6)
+        if key == b"added":
+            fl = flags or {}
+            d[b"added.f"] = bytes(fl.get(a, 0) for a in v4)
+            if v6:
+                d[b"added6.f"] = bytes(fl.get(a, 0) for a in v6)
+    return bencode.encode(d)
+
+
+def parse_pex(payload: bytes) -> tuple[list[tuple[str, int]], list[tuple[str, int]]]:
+    """-> (added, dropped) from a ut_pex message (IPv4 and IPv6)."""
+    import ipaddress
+    try:
+        d = bencode.decode(payload, allow_trailing=True)
+    except bencode.BencodeError as e:
+        raise PeerError(f"bad ut_pex message: {e}") from e
+    if not isinstance(d, dict):
+        raise PeerError("ut_pex message is not a dict")
+
+    def compact(b, step):
+        out = []
+        if not isinstance(b, bytes):
+            return out
+        for k in range(0, len(b) - step + 1, step):
+            (port,) = struct.unpack(">H", b[k + step - 2:k + step])
+            if port:
+                out.append((str(ipaddress.ip_address(b[k:k + step - 2])), port))
+        return out
+    added = compact(d.get(b"added"), 6) + compact(d.get(b"added6"), 18)
+    dropped = compact(d.get(b"dropped"), 6) + compact(d.get(b"dropped6"), 18)
+    return added, dropped
 
 
 def meta_msg(msg_type: int, piece: int, total_size: int | None = None, data: bytes = b"") -> bytes:

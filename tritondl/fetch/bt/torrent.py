@@ -34,6 +34,7 @@ import time
 from dataclasses import dataclass, field
 
 from ...utils.log import log
+from . import mse
 from . import peer as pw
 from .dht import DHTNode
 from .metainfo import BLOCK, Info, MetainfoError
@@ -56,6 +57,10 @@ class TorrentConfig:
     dht_interval: float = 60.0
     max_bad_pieces: int = 3
     utp: bool = False
+    pex: bool = True                 # BEP 11 peer exchange (off for private torrents regardless)
+    pex_interval: float = 60.0
+    webseed_conns: int = 4           # BEP 19: concurrent piece fetches per web seed
+    encryption: str = "allow"        # MSE/PE policy: disable | allow | prefer | require (see .mse)
 
 
 @dataclass
@@ -106,6 +111,8 @@ class _Peer:
         self.am_interested = False
         self.ext: pw.ExtHandshake | None = None
         self.outstanding: dict[tuple[int, int], float] = {}
+        self.listen_addr: tuple[str, int] | None = None   # where others can dial it (PEX)
+        self.pex_sent: set[tuple[str, int]] = set()
         self.bad = 0
         self.downloaded = 0
         self.meta_requested = False
@@ -122,12 +129,17 @@ class Torrent:
     def __init__(self, infohash: bytes, base_dir: str, cfg: TorrentConfig | None = None, *,
                  info: Info | None = None, trackers: list[str] | None = None,
                  peers: list[tuple[str, int]] | None = None, dht: DHTNode | None = None,
-                 peer_id: bytes | None = None, name_hint: str = "") -> None:
+                 peer_id: bytes | None = None, name_hint: str = "",
+                 webseeds: list[str] | None = None) -> None:
         self.infohash = infohash
         self.base_dir = base_dir
         self.cfg = cfg or TorrentConfig()
         self.trackers = list(trackers or [])
         self.static_peers = list(peers or [])
+        self.webseeds = list(dict.fromkeys(webseeds or []))
+        self.ws_busy: set[int] = set()                  # pieces a web seed is fetching
+        self.webseed_clients: list = []
+        self.pex_learned = 0
         self.dht = dht
         self.peer_id = peer_id or new_peer_id()
         self.name_hint = name_hint
@@ -186,6 +198,14 @@ class Torrent:
         if self.dht is not None:
             self._spawn(self._dht_loop())
         self._spawn(self._timeout_loop())
+        if self.cfg.pex:
+            self._spawn(self._pex_loop())
+        if self.webseeds:
+            from .webseed import WebSeed
+            for url in self.webseeds:
+                ws = WebSeed(self, url, self.cfg.webseed_conns)
+                self.webseed_clients.append(ws)
+                self._spawn(ws.run())
 
     async def _utp_accept_loop(self) -> None:
         assert self.utp is not None
@@ -292,12 +312,18 @@ class Torrent:
                 event = "done"
             await asyncio.sleep(interval if not self._starving() else min(interval, 5.0))
 
+    @property
+    def private(self) -> bool:
+        return bool(self.info is not None and self.info.private)
+
     def _starving(self) -> bool:
         return not self.peers
 
     async def _dht_loop(self) -> None:
         assert self.dht is not None
         while not self.closed:
+            if self.private:
+                return                   # BEP 27: private torrents use their trackers only
             try:
                 for p in await self.dht.get_peers(self.infohash):
                     self.add_peer_addr(p)
@@ -315,9 +341,25 @@ class Torrent:
         return await self.utp.connect(addr[0], addr[1], self.cfg.connect_timeout)
 
     async def _dial_and_handshake(self, dial, addr):
+        policy = self.cfg.encryption
+        ours = pw.encode_handshake(self.infohash, self.peer_id)
+        if policy in ("prefer", "require"):
+            reader, writer = await dial(addr)
+            try:
+                provide = mse.CRYPTO_RC4 if policy == "require" else mse.CRYPTO_RC4 | mse.CRYPTO_PLAIN
+                reader, writer, _sel = await mse.initiate(reader, writer, self.infohash, ours, provide,
+                                                          self.cfg.connect_timeout)
+                hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
+                return reader, writer, hs
+            except BaseException as e:
+                writer.close()
+                if policy == "require" or not isinstance(e, (OSError, asyncio.TimeoutError,
+                                                             asyncio.IncompleteReadError, pw.PeerError)):
+                    raise
+                # "prefer": the peer does not speak MSE; redial in plaintext
         reader, writer = await dial(addr)
         try:
-            writer.write(pw.encode_handshake(self.infohash, self.peer_id))
+            writer.write(ours)
             hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
         except BaseException:
             writer.close()
@@ -348,12 +390,26 @@ class Torrent:
         if won is None:
             return
         reader, writer, hs = won
-        await self._run_peer(reader, writer, addr, hs)
+        await self._run_peer(reader, writer, addr, hs, inbound=False)
 
     async def _on_inbound(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         addr = writer.get_extra_info("peername")[:2]
+        policy = self.cfg.encryption
         try:
-            hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
+            first = await asyncio.wait_for(reader.readexactly(len(mse.PLAIN_PREFIX)), self.cfg.connect_timeout)
+            if first == mse.PLAIN_PREFIX:
+                if policy == "require":
+                    raise pw.PeerError("plaintext connection refused (encryption required)")
+                rest = await asyncio.wait_for(reader.readexactly(pw.HANDSHAKE_LEN - len(first)),
+                                              self.cfg.connect_timeout)
+                hs = pw.parse_handshake(first + rest)
+            else:
+                if policy == "disable":
+                    raise pw.PeerError("encrypted connection refused (encryption disabled)")
+                reader, writer, _sel = await mse.respond(reader, writer, first, self.infohash,
+                                                         allow_plain=policy != "require",
+                                                         timeout=self.cfg.connect_timeout)
+                hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
             if hs.infohash != self.infohash:
                 writer.close()
                 return
@@ -361,18 +417,21 @@ class Torrent:
         except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError):
             writer.close()
             return
-        await self._run_peer(reader, writer, addr, hs)
+        await self._run_peer(reader, writer, addr, hs, inbound=True)
 
-    async def _run_peer(self, reader, writer, addr, hs: pw.Handshake) -> None:
+    async def _run_peer(self, reader, writer, addr, hs: pw.Handshake, inbound: bool = True) -> None:
         if hs.infohash != self.infohash or hs.peer_id == self.peer_id or addr in self.peers or self.closed:
             writer.close()
             return
         n = self.info.num_pieces if self.info else 0
         p = _Peer(pw.Wire(reader, writer), addr, hs, n)
+        if not inbound:
+            p.listen_addr = addr
         self.peers[addr] = p
         try:
             if hs.extended:
-                p.wire.ext_handshake(len(self.info.raw) if self.info else None, self.port)
+                p.wire.ext_handshake(len(self.info.raw) if self.info else None, self.port,
+                                     pex=self.cfg.pex and not self.private)
             if self.info is not None and self._downloading:
                 self._send_have_state(p)
             await self._peer_loop(p)
@@ -516,7 +575,7 @@ class Torrent:
         for k in range(n):
             i = (start + k) % n
             if p.have[i] and not self.have[i] and i not in self.pieces and self.avail[i] < best_av \
-                    and i not in self.verifying:
+                    and i not in self.verifying and i not in self.ws_busy:
                 best, best_av = i, self.avail[i]
                 if best_av <= 1:
                     break
@@ -592,9 +651,20 @@ class Torrent:
         self._fill(p)
 
     async def _finish_piece(self, i: int, pc: _Piece, src: _Peer) -> None:
+        ok = await self.commit_piece(i, pc.buf)   # the buffer is no longer shared: the piece left self.pieces
+        if not ok:
+            src.bad += 1
+            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
+            if src.bad >= self.cfg.max_bad_pieces:
+                self.banned.add(src.addr)
+                src.wire.close()
+
+    async def commit_piece(self, i: int, data) -> bool:
+        """Verify a whole piece off-loop, write it and record completion; then
+        announce it.  Shared by peer downloads and web seeds.  False on a hash
+        mismatch (nothing is written)."""
         assert self.info is not None and self.storage is not None
         loop = asyncio.get_running_loop()
-        data = pc.buf                     # no longer shared: the piece left self.pieces
         expect = self.info.piece_hash(i)
         st = self.storage
 
@@ -605,19 +675,15 @@ class Torrent:
             st.mark(i, True)
             return True
 
+        self.verifying.add(i)
         try:
             ok = await loop.run_in_executor(None, verify_and_write)
         finally:
             self.verifying.discard(i)
         if not ok:
-            src.bad += 1
-            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
-            if src.bad >= self.cfg.max_bad_pieces:
-                self.banned.add(src.addr)
-                src.wire.close()
-            return
+            return False
         if self.have[i]:
-            return
+            return True
         self.have[i] = 1
         self.nhave += 1
         for q in list(self.peers.values()):
@@ -627,6 +693,7 @@ class Torrent:
                 q.wire.send(pw.NOT_INTERESTED)
         if self.nhave == self.info.num_pieces:
             self.complete.set()
+        return True
 
     def _on_request(self, p: _Peer, pl: bytes) -> None:
         i, off, n = struct.unpack(">III", pl[:12])
@@ -665,6 +732,39 @@ class Torrent:
                     if p.ext and "ut_metadata" in p.ext.m and self._meta_size:
                         self._request_metadata(p)
 
+    async def _pex_loop(self) -> None:
+        """BEP 11: every ``pex_interval`` tell each ut_pex-capable peer which
+        dialable peers joined / left since the last message to it."""
+        while not self.closed:
+            await asyncio.sleep(self.cfg.pex_interval)
+            if self.private:
+                return
+            self.pex_round()
+
+    def pex_round(self) -> None:
+        live = {q.listen_addr: q for q in self.peers.values() if q.listen_addr is not None}
+        for p in list(self.peers.values()):
+            their = p.ext.m.get("ut_pex") if p.ext else None
+            if not their or p.wire.closed:
+                continue
+            cur = set(live) - {p.listen_addr}
+            added = [a for a in cur if a not in p.pex_sent][:pw.PEX_MAX_ADDED]
+            dropped = [a for a in p.pex_sent if a not in cur][:pw.PEX_MAX_ADDED]
+            if not added and not dropped:
+                continue
+            flags = {}
+            for a in added:
+                q = live[a]
+                f = 0x10                                   # we dialled / it told us its port
+                if q.nhave and q.nhave == len(q.have):
+                    f |= 0x02
+                if type(q.wire.writer.transport).__name__ == "_UtpTransport":
+                    f |= 0x04                              # reached over uTP
+                flags[a] = f
+            p.wire.extended(their, pw.pex_msg(added, dropped, flags))
+            p.pex_sent.update(added)
+            p.pex_sent.difference_update(dropped)
+
     # ------------------------------------------------------------ extensions
     async def _on_extended(self, p: _Peer, pl: bytes) -> None:
         if not pl:
@@ -672,10 +772,21 @@ class Torrent:
         eid, body = pl[0], pl[1:]
         if eid == pw.EXT_HANDSHAKE:
             p.ext = pw.parse_ext_handshake(body)
+            if p.listen_addr is None and p.ext.port and 0 < p.ext.port < 65536:
+                p.listen_addr = (p.addr[0], p.ext.port)
             if self.info is None and "ut_metadata" in p.ext.m and p.ext.metadata_size:
                 if self._meta_size is None and 0 < p.ext.metadata_size < 16 * 1024 * 1024:
                     self._meta_size = p.ext.metadata_size
                 self._request_metadata(p)
+            return
+        if eid == pw.UT_PEX_ID:
+            if not self.cfg.pex or self.private:
+                return
+            added, _dropped = pw.parse_pex(body)
+            for a in added[:pw.PEX_MAX_ADDED]:
+                if a not in self.known and a not in self.peers:
+                    self.pex_learned += 1
+                self.add_peer_addr(a)
             return
         if eid == pw.UT_METADATA_ID:
             d, data = pw.parse_meta_msg(body)

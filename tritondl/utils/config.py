@@ -59,6 +59,8 @@ class Config:
     bt_listen_port: int = 0                     # 0 = ephemeral
     bt_dht: bool = True
     bt_utp: bool = True
+    bt_pex: bool = True
+    bt_encryption: str = "allow"                # MSE/PE: disable | allow | prefer | require
     bt_bootstrap: str = "router.bittorrent.com:6881,dht.transmissionbt.com:6881"
     gpu_verify: str = "auto"                    # auto|on|off (HIP batch piece hashing)
 
@@ -112,7 +114,8 @@ class Config:
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s"}
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
-                "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap"}
+                "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
+                "BT_ENCRYPTION": "bt_encryption"}
         for k, a in ints.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, int(g("TRITONDL_" + k)))
@@ -126,6 +129,9 @@ class Config:
         c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
+        c.bt_pex = _env_bool(g("TRITONDL_BT_PEX"), c.bt_pex)
+        if c.bt_encryption not in ("disable", "allow", "prefer", "require"):
+            raise ValueError(f"TRITONDL_BT_ENCRYPTION must be disable|allow|prefer|require, got {c.bt_encryption!r}")
         if argv is not None:
             c.apply_args(parse_args(argv))
         if not c.download_dir:
