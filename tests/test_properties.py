@@ -1,0 +1,238 @@
+"""Property-based tests (hypothesis) for every hand-written codec: bencode,
+AMQP field tables and frames, protobuf varints and the Download envelope,
+peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
+native aws-chunked encoder/decoder pair.  Decoders must round-trip what the
+encoders produce and reject garbage only with their own error types."""
+
+import asyncio
+import math
+
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from tritondl.amqp import codec
+from tritondl.fetch.bt import bencode
+from tritondl.fetch.bt import peer as pw
+from tritondl.models import messages, wire
+from tritondl.ops import hashing
+
+SETTINGS = settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+
+# ----------------------------------------------------------------- bencode
+
+bvals = st.recursive(
+    st.integers(min_value=-(2**70), max_value=2**70) | st.binary(max_size=40),
+    lambda kids: st.lists(kids, max_size=5) | st.dictionaries(st.binary(max_size=10), kids, max_size=5),
+    max_leaves=25)
+
+
+@SETTINGS
+@given(bvals)
+def test_bencode_roundtrip(v):
+    assert bencode.decode(bencode.encode(v)) == v
+
+
+@SETTINGS
+@given(st.binary(max_size=64))
+def test_bencode_garbage_only_raises_bencode_error(b):
+    try:
+        v = bencode.decode(b)
+    except bencode.BencodeError:
+        return
+    assert bencode.encode(v) == b     # anything accepted is canonical
+
+
+# ----------------------------------------------------------------- AMQP tables
+
+keys = st.text(min_size=1, max_size=20).filter(lambda k: len(k.encode()) <= 255)
+scalars = (st.booleans() | st.integers(min_value=-(2**63), max_value=2**63 - 1)
+           | st.floats(allow_nan=False) | st.text(max_size=30) | st.none()
+           | st.binary(max_size=30).filter(lambda b: _not_utf8(b)))
+
+
+def _not_utf8(b: bytes) -> bool:
+    try:
+        b.decode("utf-8")
+        return False
+    except UnicodeDecodeError:
+        return True
+
+
+tables = st.recursive(scalars, lambda kids: st.lists(kids, max_size=4) | st.dictionaries(keys, kids, max_size=4),
+                      max_leaves=20)
+
+
+def _norm(v):
+    if isinstance(v, tuple):
+        return [_norm(x) for x in v]
+    if isinstance(v, list):
+        return [_norm(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _norm(x) for k, x in v.items()}
+    return v
+
+
+@SETTINGS
+@given(st.dictionaries(keys, tables, max_size=6))
+def test_amqp_table_roundtrip(t):
+    got = codec.decode_table(codec.encode_table(t))
+    assert got == _norm(t) or _float_eq(got, _norm(t))
+
+
+def _float_eq(a, b):
+    if isinstance(a, float) and isinstance(b, float):
+        return a == b or (math.isinf(a) and a == b)
+    if isinstance(a, dict) and isinstance(b, dict):
+        return a.keys() == b.keys() and all(_float_eq(a[k], b[k]) for k in a)
+    if isinstance(a, list) and isinstance(b, list):
+        return len(a) == len(b) and all(_float_eq(x, y) for x, y in zip(a, b))
+    return a == b
+
+
+@SETTINGS
+@given(st.binary(max_size=80))
+def test_amqp_table_garbage_raises_frame_error(b):
+    try:
+        codec.decode_table(b)
+    except codec.AMQPError:
+        pass
+
+
+@SETTINGS
+@given(st.binary(max_size=3000), st.integers(min_value=4096, max_value=8192),
+       st.text(max_size=20), st.dictionaries(keys, st.integers(min_value=-5, max_value=5), max_size=3))
+def test_amqp_content_frames_roundtrip(body, frame_max, ctype, headers):
+    m = codec.Method("basic.publish", {"exchange": "x", "routing_key": "rk"})
+    props = codec.Properties(content_type=ctype or None, headers=headers or None, delivery_mode=2)
+    frames = codec.content_frames(1, m, body, props, frame_max)
+    buf = b"".join(frames)
+    pos, out = 0, []
+    while pos < len(buf):
+        ftype, ch, size = __import__("struct").unpack(">BHI", buf[pos:pos + 7])
+        assert size + 8 <= frame_max and buf[pos + 7 + size] == 0xCE
+        out.append((ftype, buf[pos + 7:pos + 7 + size]))
+        pos += 8 + size
+    assert out[0][0] == 1 and codec.decode_method(out[0][1]).name == "basic.publish"
+    cls, size, p2 = codec.decode_header(out[1][1])
+    assert size == len(body) and p2.content_type == (ctype or None) and (p2.headers or None) == (headers or None)
+    assert b"".join(x[1] for x in out[2:]) == body
+
+
+# ----------------------------------------------------------------- protobuf
+
+
+@SETTINGS
+@given(st.integers(min_value=0, max_value=2**64 - 1))
+def test_varint_roundtrip(v):
+    enc = wire.encode_varint(v)
+    assert wire.decode_varint(enc, 0) == (v, len(enc))
+
+
+@SETTINGS
+@given(st.integers(min_value=-(2**63), max_value=-1))
+def test_negative_varint_is_twos_complement(v):
+    enc = wire.encode_varint(v)
+    assert len(enc) == 10 and wire.decode_varint(enc, 0)[0] == v + 2**64
+
+
+media = st.builds(messages.Media, id=st.text(max_size=20), name=st.text(max_size=20),
+                  creator=st.integers(0, 3), creator_id=st.text(max_size=10), type=st.integers(0, 2),
+                  source=st.integers(0, 4), source_uri=st.text(max_size=40), metadata=st.integers(0, 3),
+                  metadata_id=st.text(max_size=10), status=st.integers(-(2**63), 2**63 - 1))
+
+
+@SETTINGS
+@given(st.text(max_size=30), media)
+def test_download_envelope_roundtrip(created, m):
+    d = messages.Download(created_at=created, media=m)
+    back = messages.Download.decode(d.encode())
+    assert back.created_at == created and back.media == m
+    # Convert.from_download re-emits the media bytes verbatim
+    c = messages.Convert.from_download(back, "t")
+    assert messages.Convert.decode(c.encode()).media == m
+
+
+@SETTINGS
+@given(st.binary(max_size=60))
+def test_envelope_garbage_raises_decode_error(b):
+    try:
+        messages.Download.decode(b)
+    except wire.DecodeError:
+        pass
+
+
+# ----------------------------------------------------------------- peer wire
+
+
+class _FakeReader:
+    def __init__(self, chunks):
+        self.chunks = list(chunks)
+
+    async def read(self, n):
+        return self.chunks.pop(0) if self.chunks else b""
+
+
+msgs = st.lists(st.one_of(st.none(), st.tuples(st.integers(0, 20), st.binary(max_size=300))), max_size=30)
+
+
+@SETTINGS
+@given(msgs, st.lists(st.integers(1, 97), min_size=1, max_size=50))
+def test_wire_parses_any_segmentation(ms, cuts):
+    import struct
+    stream = b"".join(b"\x00\x00\x00\x00" if m is None else struct.pack(">IB", len(m[1]) + 1, m[0]) + m[1]
+                      for m in ms)
+    chunks, pos, k = [], 0, 0
+    while pos < len(stream):
+        n = cuts[k % len(cuts)]
+        chunks.append(stream[pos:pos + n])
+        pos += n
+        k += 1
+
+    async def run():
+        w = pw.Wire(_FakeReader(chunks), None)
+        out = []
+        while len(out) < len(ms):
+            out += await w.read_batch()
+        return out
+    got = asyncio.run(run()) if ms else []
+    assert got == [None if m is None else (m[0], m[1]) for m in ms]
+
+
+# ----------------------------------------------------------------- crypto / S3 framing
+
+
+@SETTINGS
+@given(st.binary(min_size=1, max_size=64), st.binary(max_size=5000), st.integers(1, 4999))
+def test_rc4_split_stream_symmetry(key, data, cut):
+    a, b = hashing._host.Rc4(key), hashing._host.Rc4(key)
+    ct = a.crypt(data[:cut]) + a.crypt(data[cut:])
+    assert b.crypt(ct) == data
+
+
+KEY = bytes(range(32))
+SCOPE = "20130524/us-east-1/s3/aws4_request"
+DATE = "20130524T000000Z"
+SEED = "4f232c4386841ef735655705268965c44a0e4690baa4adea153f7db9fa80a0a9"
+
+
+@SETTINGS
+@given(st.binary(max_size=20000), st.sampled_from([8192, 16384, 65536]), st.sampled_from([1, 3]))
+def test_aws_chunked_encode_decode_roundtrip(data, chunk, threads):
+    enc, last = hashing.aws_chunk_encode(KEY, DATE, SCOPE, SEED, data, chunk, final=True, threads=threads)
+    ok, dec, err = hashing.aws_chunk_decode(KEY, DATE, SCOPE, SEED, enc, threads=threads)
+    assert ok and dec == data and err == ""
+    sigs = hashing.chunk_signatures(KEY, DATE, SCOPE, SEED, data, chunk, include_final=True, threads=threads)
+    assert sigs[-1] == last
+    if enc:
+        bad = bytearray(enc)
+        bad[-40] ^= 1                         # flip a bit inside the final signature / frame
+        ok2, _d, _e = hashing.aws_chunk_decode(KEY, DATE, SCOPE, SEED, bytes(bad))
+        assert not ok2
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65])
+def test_aws_chunked_boundaries(n):
+    data = bytes(range(256)) * 1 + b"z" * n
+    enc, _ = hashing.aws_chunk_encode(KEY, DATE, SCOPE, SEED, data, 8192, final=True)
+    assert hashing.aws_chunk_decode(KEY, DATE, SCOPE, SEED, enc)[1] == data
