@@ -141,7 +141,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8",
-            "data": "synthetic (deterministic pseudo-random 10 MiB payload; local fake broker/origin/S3)",
+            "data": f"synthetic (deterministic pseudo-random {file_size / 2**20:g} MiB payload; "
+                    "local fake broker/origin/S3)",
             "config": {"model": CONFIG_NAME, "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency)},

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Node throughput benchmark ("8 worker processes × 100 small
+HTTP jobs → jobs/sec").
+
+The fake broker, origin and S3 run as separate processes; ``WorkerPool``
+starts N real worker processes (``python -m tritondl``, competing consumers on
+the sharded queues, exactly the production launcher); this process publishes
+the jobs and counts the ``v1.convert`` messages.  Warm-up: one job per worker
+first, so every worker has connected and consumed before the clock starts.
+
+    python tools/bench_pool.py --workers 8 --jobs 100 --file-kb 1024
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+async def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--jobs", type=int, default=100)
+    ap.add_argument("--file-kb", type=int, default=1024)
+    ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
+    a = ap.parse_args()
+    from tritondl.amqp.codec import Properties
+    from tritondl.amqp.connection import Connection
+    from tritondl.bench_job import AK, SK, Backend
+    from tritondl.models import Convert, Download, Media, SourceType
+    from tritondl.parallel import WorkerPool, plan
+
+    work = tempfile.mkdtemp(prefix="tdl-poolbench-", dir=os.environ.get("TMPDIR", "/tmp"))
+    backends: list[Backend] = []
+    pool = None
+    prod = None
+    try:
+        bk = await Backend("broker").start()
+        og = await Backend("origin").start()
+        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+        backends = [bk, og, s3]
+        env = {"RABBITMQ_ENDPOINT": bk.info["endpoint"], "RABBITMQ_USERNAME": "guest",
+               "RABBITMQ_PASSWORD": "guest", "S3_ENDPOINT": s3.info["url"], "AWS_ACCESS_KEY_ID": AK,
+               "AWS_SECRET_ACCESS_KEY": SK, "PYTHONPATH": ROOT, "TRITONDL_RETRY_DELAY": "0",
+               "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning", "TRITONDL_PROGRESS_LOG_INTERVAL": "0",
+               "TRITONDL_CLEANUP": "1", "TRITONDL_CONCURRENCY": str(a.concurrency),
+               "TRITONDL_PREFETCH": str(a.concurrency), "TRITONDL_GPU_VERIFY": "off"}
+        ncpu = len(os.sched_getaffinity(0))
+        pool = WorkerPool(plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)),
+                          env=env, cwd=work, grace=10)
+        await pool.start()
+        prod = await Connection.open(bk.info["url"], heartbeat=0)
+        pch = await prod.channel()
+        await pch.confirm_select()
+        cch = await prod.channel()
+        done: list[float] = []
+        ids: set[str] = set()
+        got = asyncio.Event()
+        target = [0]
+
+        def on_convert(m) -> None:
+            c = Convert.decode(m.body)
+            if c.media is not None and c.media.id not in ids:
+                ids.add(c.media.id)
+                done.append(time.perf_counter())
+                if len(done) >= target[0]:
+                    got.set()
+            asyncio.ensure_future(m.ack())
+        await pch.exchange_declare("v1.download", "direct", durable=True)
+        for i in range(2):
+            await pch.queue_declare(f"v1.download-{i}", durable=True)
+            await pch.queue_bind(f"v1.download-{i}", "v1.download", f"v1.download-{i}")
+            await cch.queue_declare(f"v1.convert-{i}", durable=True)
+            await cch.basic_consume(f"v1.convert-{i}", on_convert)
+        size = a.file_kb << 10
+        n_sub = [0]
+
+        async def submit(n: int) -> None:
+            for _ in range(n):
+                i = n_sub[0]
+                n_sub[0] += 1
+                url = f"{og.info['url']}/synthetic/{size}/clip-{i}.mkv"
+                body = Download(created_at="now", media=Media(id=f"pool-{i}", name=f"clip {i}",
+                                                              source=SourceType.HTTP, source_uri=url)).encode()
+                await pch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
+                                        Properties(delivery_mode=2, content_type="application/octet-stream"))
+
+        # warm-up: every worker connected and through one job
+        target[0] = 2 * a.workers
+        await submit(target[0])
+        await asyncio.wait_for(got.wait(), 180)
+        got.clear()
+        base = len(done)
+        target[0] = base + a.jobs
+        t0 = time.perf_counter()
+        await submit(a.jobs)
+        await asyncio.wait_for(got.wait(), 600)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"metric": "pool_jobs_per_sec", "value": round(a.jobs / dt, 2), "seconds": round(dt, 3),
+                          "workers": a.workers, "jobs": a.jobs, "file_kb": a.file_kb,
+                          "concurrency_per_worker": a.concurrency,
+                          "ingest_MB_per_sec": round(a.jobs * size / dt / 1e6, 1)}), flush=True)
+    finally:
+        if prod is not None:
+            await prod.close()
+        if pool is not None:
+            await pool.stop()
+        for b in backends:
+            await b.stop()
+        shutil.rmtree(work, ignore_errors=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(asyncio.run(main()))

@@ -10,4 +10,6 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke o
 step bench_c1 300 python bench.py --steps 100 --warmup 10 &&
 step bench_c4 300 python bench.py --steps 200 --warmup 20 --concurrency 4 &&
 step bench_bt_tcp 300 python tools/bench_bt.py --mb 1024 --seeds 4 &&
-step bench_bt_utp 300 python tools/bench_bt.py --mb 1024 --seeds 4 --utp
+step bench_bt_utp 300 python tools/bench_bt.py --mb 1024 --seeds 4 --utp &&
+step bench_1g 300 python bench.py --file-mb 1024 --steps 3 --warmup 1 &&
+step bench_pool8 300 python tools/bench_pool.py --workers 8 --jobs 100 --file-kb 1024

@@ -147,12 +147,15 @@ class FakeS3:
                             "The request signature we calculated does not match the signature you provided.")
         return s.key, sig, amzdate, s.scope
 
-    async def _read_body(self, request: web.Request, auth) -> bytes:
+    async def _read_body(self, request: web.Request, auth, keep: bool = True):
+        """Verified request body.  ``keep=False`` (object data in discard
+        mode): aws-chunked bodies are verified without materialising the
+        decoded bytes and only their length is returned (as ``_Sized``)."""
         phash = request.headers.get("x-amz-content-sha256", sigv4.UNSIGNED_PAYLOAD)
         if phash == sigv4.STREAMING_PAYLOAD:
             if not isinstance(auth, tuple):
                 raise _BadReq(400, "InvalidRequest", "streaming payload needs a signature")
-            return await self._read_chunked(request, auth)
+            return await self._read_chunked(request, auth, keep)
         data = await request.read()
         self.bytes_received += len(data)
         if phash not in (sigv4.UNSIGNED_PAYLOAD, "") and auth is not None:
@@ -160,7 +163,7 @@ class FakeS3:
                 raise _BadReq(400, "XAmzContentSHA256Mismatch", "payload hash mismatch")
         return data
 
-    async def _read_chunked(self, request: web.Request, auth) -> bytes:
+    async def _read_chunked(self, request: web.Request, auth, keep: bool = True):
         """Decode an aws-chunked body and verify EVERY chunk signature while it
         streams in.  Frame boundaries are tracked here; each ~1 MiB run of
         whole frames is verified + decoded by the native parser in a worker
@@ -178,13 +181,19 @@ class FakeS3:
         last_sig = seed
         runs: list[asyncio.Future] = []
         finished = False
+        decoded = [0]        # payload bytes dispatched (keep=False)
+        frame_bytes = [0]    # payload bytes in the current run
 
         def dispatch(end: int, final: bool) -> None:
             nonlocal run_start, prev
             if end > run_start:
-                chunk = bytes(buf[run_start:end])
+                with memoryview(buf) as mv:
+                    chunk = bytes(mv[run_start:end])
                 runs.append(loop.run_in_executor(None, hashing.aws_chunk_decode, key, amzdate, scope, prev, chunk,
-                                                 2, True, final))
+                                                 2, keep, final))
+                if not keep:
+                    decoded[0] += frame_bytes[0]
+                frame_bytes[0] = 0
                 prev = last_sig
                 run_start = end
 
@@ -205,11 +214,12 @@ class FakeS3:
                     break
                 last_sig = m.group(2).decode()
                 pos = eol + 2 + n + 2
+                frame_bytes[0] += n
                 if n == 0:
                     finished = True
                 elif pos - run_start >= (1 << 20):
                     dispatch(pos, False)
-            if run_start > (8 << 20):   # drop verified-and-dispatched bytes
+            if run_start:               # drop dispatched bytes (keeps buf ~1 run long)
                 del buf[:run_start]
                 pos -= run_start
                 run_start = 0
@@ -223,7 +233,7 @@ class FakeS3:
             if not ok:
                 code = 403 if "signature" in err else 400
                 raise _BadReq(code, "SignatureDoesNotMatch" if code == 403 else "IncompleteBody", err)
-        data = b"".join(d for _ok, d, _e in results)
+        data = b"".join(d for _ok, d, _e in results) if keep else _Sized(decoded[0])
         if decoded_len >= 0 and decoded_len != len(data):
             raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
         return data
@@ -297,12 +307,12 @@ class FakeS3:
             if up is None:
                 await request.read()
                 return _xml_err(404, "NoSuchUpload", "no such upload")
-            data = await self._read_body(request, auth)
+            data = await self._read_body(request, auth, keep=self.store != "discard")
             o = self._save(data)
             up.parts[int(q["partNumber"])] = o
             return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
         if m == "PUT":
-            data = await self._read_body(request, auth)
+            data = await self._read_body(request, auth, keep=self.store != "discard")
             o = self._save(data, request.headers.get("Content-Type", ""))
             objs[key] = o
             return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
@@ -360,6 +370,18 @@ class FakeS3:
             objs.pop(key, None)
             return web.Response(status=204)
         return _xml_err(405, "MethodNotAllowed", m)
+
+
+class _Sized:
+    """Length-only stand-in for a verified body we chose not to keep."""
+
+    __slots__ = ("n",)
+
+    def __init__(self, n: int) -> None:
+        self.n = n
+
+    def __len__(self) -> int:
+        return self.n
 
 
 class _BadReq(Exception):
