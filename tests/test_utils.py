@@ -65,3 +65,13 @@ def test_backoff_grows_and_caps():
     import time
     time.sleep(0.01)
     assert b2.next_delay() is None
+
+
+def test_durafmt_matches_hako_durafmt_format():
+    from tritondl.utils.gocompat import durafmt
+    assert durafmt(10) == "10 seconds"
+    assert durafmt(1) == "1 second"
+    assert durafmt(90.5) == "1 minute 30 seconds 500 milliseconds"
+    assert durafmt(0) == "0 seconds"
+    assert durafmt(3600 * 25) == "1 day 1 hour"
+    assert durafmt(0.000002) == "2 microseconds"

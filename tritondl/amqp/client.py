@@ -35,6 +35,7 @@ from dataclasses import dataclass
 from typing import AsyncIterator
 
 from ..utils.backoff import BackoffExhausted, ExponentialBackoff
+from ..utils.gocompat import durafmt
 from ..utils.log import log
 from . import codec
 from .codec import AMQPError, Properties
@@ -98,6 +99,7 @@ class Delivery:
         The wait is non-blocking here (the Go version slept its goroutine)."""
         d = self.client.retry_delay if delay is None else delay
         if d > 0:
+            log.info("retrying message in %s", durafmt(d))
             await asyncio.sleep(d)
         hdrs = dict(self.msg.properties.headers or {})
         hdrs["X-Retries"] = self.metadata.retries + 1

@@ -89,3 +89,24 @@ def go_time_string(now_ns: int | None = None, mono_ns: int | None = None) -> str
     abbr = lt.tm_zone or "UTC"
     ms, mfrac = divmod(mono_ns, 1_000_000_000)
     return f"{base} {zone} {abbr} m=+{ms}.{mfrac:09d}"
+
+
+_DURAFMT_UNITS = [("year", 365 * 24 * 3600 * 10**6), ("week", 7 * 24 * 3600 * 10**6), ("day", 24 * 3600 * 10**6),
+                  ("hour", 3600 * 10**6), ("minute", 60 * 10**6), ("second", 10**6), ("millisecond", 1000),
+                  ("microsecond", 1)]
+
+
+def durafmt(seconds: float) -> str:
+    """``durafmt.Parse(d).String()`` (hako/durafmt, used for the reference's
+    "retrying message in %s" log line, ``internal/rabbitmq/client.go:208``):
+    every non-zero unit from years down to microseconds, singular/plural,
+    space separated; ``0 seconds`` for zero."""
+    us = int(round(abs(seconds) * 1_000_000))
+    parts = []
+    for name, n in _DURAFMT_UNITS:
+        q, us = divmod(us, n)
+        if q:
+            parts.append(f"{q} {name}" + ("" if q == 1 else "s"))
+    if not parts:
+        return "0 seconds"
+    return ("-" if seconds < 0 else "") + " ".join(parts)
