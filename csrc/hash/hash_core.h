@@ -129,7 +129,7 @@ inline std::string piece_hashes(const EVP_MD* md, const char* data, size_t len, 
 }
 
 struct FileSpan {
-  std::string path;
+  std::string path;  // empty: a BEP 47 padding file (zeros)
   long long length;
   long long start;  // offset of this file in the torrent's concatenated stream
 };
@@ -153,7 +153,8 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
   if (n != need) throw std::invalid_argument("piece count does not match total length");
   std::string ok(n, '\0');
   std::vector<int> fds(spans.size(), -1);
-  for (size_t i = 0; i < spans.size(); ++i) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
+  for (size_t i = 0; i < spans.size(); ++i)
+    if (!spans[i].path.empty()) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
   parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
     const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
     const long long plen = std::min<long long>(static_cast<long long>(piece_len), total - pstart);
@@ -169,8 +170,13 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
       const long long a = std::max(pstart + filled, fstart);
       const long long e = std::min(pstart + plen, fstart + flen);
       if (e <= a) continue;
-      if (a != pstart + filled || fds[s] < 0) return;
       const size_t want = static_cast<size_t>(e - a);
+      if (a == pstart + filled && spans[s].path.empty()) {  // BEP 47 padding file: zeros, not on disk
+        std::memset(buf.data() + filled, 0, want);
+        filled += static_cast<long long>(want);
+        continue;
+      }
+      if (a != pstart + filled || fds[s] < 0) return;
       if (pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) return;
       filled += static_cast<long long>(want);
     }

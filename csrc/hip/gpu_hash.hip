@@ -295,9 +295,10 @@ size_t pread_full(int fd, uint8_t* dst, size_t n, off_t off) {
 }
 
 struct Span {
-  int fd;
+  int fd;  // kZeroSpan: a BEP 47 padding file (all zeros, never on disk)
   long long start, length;
 };
+constexpr int kZeroSpan = -2;
 
 // Host pipeline: disk / host memory -> pinned staging (2 slots) -> HBM
 // window -> ONE kernel over every piece of the window -> digests.
@@ -390,7 +391,7 @@ class GpuHasher {
     long long total = 0;
     for (auto& f : files) {
       if (f.second < 0) throw std::invalid_argument("negative file length");
-      spans.push_back({::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
+      spans.push_back({f.first.empty() ? kZeroSpan : ::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
       total += f.second;
     }
     auto close_all = [&] {
@@ -521,7 +522,13 @@ class GpuHasher {
           const long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
           const size_t want = static_cast<size_t>(re - ra);
           uint8_t* p = dst + (ra - static_cast<long long>(off));
-          const size_t got = s.fd >= 0 ? pread_full(s.fd, p, want, static_cast<off_t>(ra - s.start)) : 0;
+          size_t got = 0;
+          if (s.fd == kZeroSpan) {
+            std::memset(p, 0, want);
+            got = want;
+          } else if (s.fd >= 0) {
+            got = pread_full(s.fd, p, want, static_cast<off_t>(ra - s.start));
+          }
           if (got != want) {
             good = false;
             std::memset(p + got, 0, want - got);

@@ -173,3 +173,24 @@ def test_choose_device_cost_model(monkeypatch):
     monkeypatch.setattr(hashing, "gpu_available", lambda: False)
     assert hashing.choose_device(65536, 16384, 65536 * 16384) == "cpu"
     assert hashing.effective_cpus() >= 1
+
+
+def _padded_layout(tmp_path, piece_len):
+    """Files separated by BEP 47 padding spans (path "" = zeros, not on disk)."""
+    a, b = os.urandom(40_000), os.urandom(70_001)
+    (tmp_path / "a.bin").write_bytes(a)
+    (tmp_path / "b.bin").write_bytes(b)
+    gap = piece_len - len(a) % piece_len
+    files = [(str(tmp_path / "a.bin"), len(a)), ("", gap), (str(tmp_path / "b.bin"), len(b))]
+    return files, _ref_pieces(a + bytes(gap) + b, piece_len, "sha1")
+
+
+def test_verify_pieces_padding_spans_host(tmp_path):
+    files, exp = _padded_layout(tmp_path, 16384)
+    assert all(hashing.verify_pieces(files, 16384, exp, device="cpu"))
+
+
+@pytest.mark.gpu
+def test_verify_pieces_padding_spans_gpu(tmp_path):
+    files, exp = _padded_layout(tmp_path, 16384)
+    assert all(hashing.verify_pieces(files, 16384, exp, device="gpu"))

@@ -29,6 +29,7 @@ class FileEntry:
     path: list[str]      # path components below the torrent root
     length: int
     offset: int          # offset in the concatenated piece stream
+    pad: bool = False    # BEP 47 padding file (attr "p"): zeros, never written to disk
 
 
 def _safe_component(c: bytes | str) -> str:
@@ -67,11 +68,13 @@ class Info:
         return self.piece_length
 
     def file_paths(self, base_dir: str) -> list[tuple[str, int]]:
-        """[(absolute path, length), ...] in stream order."""
+        """[(absolute path, length), ...] in stream order; a BEP 47 padding
+        file's path is "" (zeros, never created — the native verifiers read
+        an empty path as zero bytes)."""
         root = os.path.join(base_dir, self.name) if self.multi else base_dir
         if not self.multi:
             return [(os.path.join(base_dir, self.name), self.files[0].length)]
-        return [(os.path.join(root, *f.path), f.length) for f in self.files]
+        return [("" if f.pad else os.path.join(root, *f.path), f.length) for f in self.files]
 
     @classmethod
     def parse(cls, raw: bytes) -> "Info":
@@ -100,7 +103,8 @@ class Info:
                 ln = int(f[b"length"])
                 if ln < 0:
                     raise MetainfoError("negative length")
-                files.append(FileEntry(path, ln, off))
+                attr = f.get(b"attr", b"")
+                files.append(FileEntry(path, ln, off, isinstance(attr, bytes) and b"p" in attr))
                 off += ln
         else:
             multi = False
@@ -227,8 +231,9 @@ def parse_magnet(uri: str) -> Magnet:
 
 
 def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None,
-              private: bool = False) -> Info:
-    """Build an info dict for a file or directory (used by the test swarm)."""
+              private: bool = False, pad: bool = False) -> Info:
+    """Build an info dict for a file or directory (used by the test swarm).
+    ``pad``: align every file to a piece boundary with BEP 47 padding files."""
     from ...ops import hashing
     if os.path.isdir(base):
         entries = []
@@ -238,8 +243,15 @@ def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None
                 rel = os.path.relpath(full, base).split(os.sep)
                 entries.append((rel, full))
         entries.sort()
-        files = [{b"length": os.path.getsize(f), b"path": [c.encode() for c in rel]} for rel, f in entries]
-        layout = [(f, os.path.getsize(f)) for _rel, f in entries]
+        files, layout = [], []
+        for k, (rel, f) in enumerate(entries):
+            n = os.path.getsize(f)
+            files.append({b"length": n, b"path": [c.encode() for c in rel]})
+            layout.append((f, n))
+            if pad and k < len(entries) - 1 and n % piece_length:
+                gap = piece_length - n % piece_length
+                files.append({b"attr": b"p", b"length": gap, b"path": [b".pad", str(gap).encode()]})
+                layout.append(("", gap))
         d = {b"name": (name or os.path.basename(base.rstrip("/"))).encode(), b"piece length": piece_length,
              b"files": files}
     else:
@@ -248,7 +260,10 @@ def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None
              b"length": os.path.getsize(base)}
     total = sum(n for _p, n in layout)
     blob = bytearray()
-    for p, _n in layout:
+    for p, n in layout:
+        if not p:
+            blob += bytes(n)
+            continue
         with open(p, "rb") as f:
             blob += f.read()
     d[b"pieces"] = hashing.piece_hashes(bytes(blob), piece_length, "sha1") if total else b""

@@ -71,6 +71,8 @@ class FileStorage:
 
     def open(self) -> None:
         for i, (p, n) in enumerate(self.layout):
+            if not p:
+                continue                 # BEP 47 padding file: never created
             os.makedirs(os.path.dirname(p), exist_ok=True)
             fd = os.open(p, os.O_RDWR | os.O_CREAT, 0o644)
             if os.fstat(fd).st_size > n:
@@ -99,6 +101,9 @@ class FileStorage:
         mv = memoryview(data)
         pos = 0
         for i, fofs, n in self._spans(gofs, len(data)):
+            if i not in self._fds:       # padding: nothing to store
+                pos += n
+                continue
             chunk = mv[pos:pos + n]
             w = 0
             while w < n:
@@ -109,7 +114,7 @@ class FileStorage:
         gofs = piece * self.info.piece_length + offset
         out = bytearray()
         for i, fofs, n in self._spans(gofs, length):
-            out += os.pread(self._fds[i], n, fofs)
+            out += os.pread(self._fds[i], n, fofs) if i in self._fds else bytes(n)
         return bytes(out)
 
     def read_piece(self, piece: int) -> bytes:
@@ -126,7 +131,7 @@ class FileStorage:
         n = self.info.num_pieces
         if n == 0:
             return set()
-        if not any(os.path.exists(p) and os.path.getsize(p) for p, _ in self.layout):
+        if not any(p and os.path.exists(p) and os.path.getsize(p) for p, _ in self.layout):
             return set()
         dev = device
         if device == "auto":

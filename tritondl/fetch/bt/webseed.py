@@ -107,12 +107,16 @@ class WebSeed:
             if fe <= start or fs >= end or f.length == 0:
                 continue
             a, b = max(start, fs), min(end, fe)
-            out.append((file_url(self.url, info.name, f.path, info.multi), a - fs, b - a))
+            # BEP 47 padding is never served: an empty URL means zeros
+            out.append(("" if f.pad else file_url(self.url, info.name, f.path, info.multi), a - fs, b - a))
         return out
 
     async def _fetch(self, session: aiohttp.ClientSession, i: int) -> bytearray:
         buf = bytearray()
         for url, off, n in self._spans(i):
+            if not url:
+                buf += bytes(n)
+                continue
             hdr = {"Range": f"bytes={off}-{off + n - 1}"}
             async with session.get(url, headers=hdr) as r:
                 if r.status == 206:
