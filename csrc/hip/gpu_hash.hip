@@ -187,7 +187,7 @@ __global__ __launch_bounds__(64) void hash_pieces_kernel(const uint8_t* __restri
                                                          uint64_t piece_len, uint32_t n_pieces,
                                                          uint32_t* __restrict__ out) {
   using A = Alg<ALG>;
-  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // blockDim = lanes per wave (16/32/64)
   if (i >= n_pieces) return;
   const uint64_t start = static_cast<uint64_t>(i) * piece_len;
   const uint64_t len = min(piece_len, total - start);
@@ -263,13 +263,15 @@ int alg_id(const std::string& kind) {
 int digest_len(int alg) { return alg == 1 ? 20 : 32; }
 
 void launch_hash(int alg, const uint8_t* d_data, uint64_t total, uint64_t piece_len, uint32_t n,
-                 uint32_t* d_out, hipStream_t s) {
+                 uint32_t* d_out, hipStream_t s, int lanes = 64) {
   if (n == 0) return;
   if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
   if ((static_cast<uint64_t>(n) - 1) * piece_len >= total && total > 0)
     throw std::invalid_argument("n_pieces exceeds data length");
   const bool vec = (piece_len % 16 == 0) && (reinterpret_cast<uintptr_t>(d_data) % 16 == 0);
-  dim3 grid((n + 63) / 64), block(64);
+  if (lanes != 16 && lanes != 32 && lanes != 64) throw std::invalid_argument("lanes must be 16, 32 or 64");
+  const uint32_t L = static_cast<uint32_t>(lanes);
+  dim3 grid((n + L - 1) / L), block(L);
   if (alg == 1) {
     if (vec) hash_pieces_kernel<1, true><<<grid, block, 0, s>>>(d_data, total, piece_len, n, d_out);
     else hash_pieces_kernel<1, false><<<grid, block, 0, s>>>(d_data, total, piece_len, n, d_out);
@@ -617,17 +619,17 @@ PYBIND11_MODULE(_gpu_hash, m) {
   m.def(
       "hash_device",
       [](const std::string& kind, uintptr_t data_ptr, uint64_t total, uint64_t piece_len, uintptr_t out_ptr,
-         uintptr_t stream) {
+         uintptr_t stream, int lanes) {
         const int alg = alg_id(kind);
         if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
         const uint64_t n = total ? (total + piece_len - 1) / piece_len : 0;
         if (n > 0xFFFFFFFFull) throw std::invalid_argument("too many pieces");
         launch_hash(alg, reinterpret_cast<const uint8_t*>(data_ptr), total, piece_len, static_cast<uint32_t>(n),
-                    reinterpret_cast<uint32_t*>(out_ptr), reinterpret_cast<hipStream_t>(stream));
+                    reinterpret_cast<uint32_t*>(out_ptr), reinterpret_cast<hipStream_t>(stream), lanes);
         return n;
       },
       py::arg("kind"), py::arg("data_ptr"), py::arg("total"), py::arg("piece_len"), py::arg("out_ptr"),
-      py::arg("stream") = 0,
+      py::arg("stream") = 0, py::arg("lanes") = 64,
       "Launch on caller-owned device memory (e.g. torch tensors); out holds n*digest_len bytes.");
   py::class_<GpuHasher>(m, "GpuHasher")
       .def(py::init<int, size_t, int, size_t>(), py::arg("device") = 0, py::arg("batch_bytes") = 256u << 20,

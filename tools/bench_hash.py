@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kinds", nargs="*", default=["sha1", "sha256"])
     ap.add_argument("--no-files", action="store_true")
+    ap.add_argument("--lanes", type=int, nargs="*", default=[64], help="pieces per wavefront (16/32/64)")
+    ap.add_argument("--kernel-only", action="store_true")
     a = ap.parse_args()
 
     import numpy as np
@@ -58,20 +60,23 @@ def main() -> int:
             n = (total + pl - 1) // pl
             if have_gpu:
                 out = torch.empty(n * dl, dtype=torch.uint8, device="cuda")
-
-                def k():
-                    mod.hash_device(kind, dev.data_ptr(), total, pl, out.data_ptr(), stream)
-                    torch.cuda.synchronize()
-                t = timeit(k, a.reps)
-                res.append({"case": "gpu_kernel", "kind": kind, "piece_kb": pk, "pieces": n,
-                            "GBps": total / t / 1e9, "ms": t * 1e3})
+                for lanes in a.lanes:
+                    def k():
+                        mod.hash_device(kind, dev.data_ptr(), total, pl, out.data_ptr(), stream, lanes)
+                        torch.cuda.synchronize()
+                    t = timeit(k, a.reps)
+                    res.append({"case": "gpu_kernel", "kind": kind, "piece_kb": pk, "pieces": n, "lanes": lanes,
+                                "GBps": total / t / 1e9, "ms": t * 1e3})
+                    print(json.dumps(res[-1]), flush=True)
+                if a.kernel_only:
+                    continue
                 t = timeit(lambda: hashing.piece_hashes(host, pl, kind, device="gpu"), max(1, a.reps // 2))
                 res.append({"case": "gpu_pipeline", "kind": kind, "piece_kb": pk, "GBps": total / t / 1e9,
                             "ms": t * 1e3})
             t = timeit(lambda: hashing.piece_hashes(host, pl, kind, device="cpu"), max(1, a.reps // 2))
             res.append({"case": "cpu_pieces", "kind": kind, "piece_kb": pk, "threads": os.cpu_count(),
                         "GBps": total / t / 1e9, "ms": t * 1e3})
-            for r in res[-3:]:
+            for r in res[-2:]:
                 print(json.dumps(r), flush=True)
     if not a.no_files:
         with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
