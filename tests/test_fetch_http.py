@@ -91,8 +91,13 @@ def test_http_download_basic_and_skip_existing(tmp_path):
         assert (tmp_path / "Movie One.mkv").read_bytes() == data
         assert s.events[-1] == 100 and not (tmp_path / "Movie One.mkv.part").exists()
         n = len(o.requests)
-        await h.download(str(tmp_path), s, url)       # already complete: only the HEAD probe
+        await h.download(str(tmp_path), s, url)       # already complete: only the probe (closed unread)
+        assert [r[0] for r in o.requests[n:]] == ["GET"]
+        h2 = _dl(probe="head")                         # grab's order: HEAD first
+        n = len(o.requests)
+        await h2.download(str(tmp_path), s, url)
         assert [r[0] for r in o.requests[n:]] == ["HEAD"]
+        await h2.close()
         await h.close()
         await o.stop()
     run(main())
@@ -155,9 +160,57 @@ def test_http_errors_surface(tmp_path):
         with pytest.raises(Exception):
             await h.download(str(tmp_path), Sink(), o.url("/missing.mkv"))
         url = o.add("/x.mkv", b"z" * 10)
-        o.fail = 1  # HEAD gets 500 -> falls back to ranged GET probe
+        o.fail = 1  # the probe gets a 500 -> retried
         await h.download(str(tmp_path), Sink(), url)
         assert (tmp_path / "x.mkv").read_bytes() == b"z" * 10
+        hh = _dl(max_retries=1, probe="head")
+        o.fail = 1  # HEAD gets 500 -> falls back to ranged GET probe
+        os.remove(tmp_path / "x.mkv")
+        await hh.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "x.mkv").read_bytes() == b"z" * 10
+        await hh.close()
         await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_get_probe_empty_file_and_rangeless_origin(tmp_path):
+    async def main():
+        o = await Origin().start()
+        h = _dl()
+        url = o.add("/empty.mkv", b"")
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "empty.mkv").read_bytes() == b""
+        o.ranges = False                           # origin ignores Range: 200 + full body
+        data = os.urandom(200_000)
+        url2 = o.add("/full.mkv", data)
+        n = len(o.requests)
+        await h.download(str(tmp_path), Sink(), url2)
+        assert (tmp_path / "full.mkv").read_bytes() == data
+        assert [r[0] for r in o.requests[n:]] == ["GET"]      # the probe WAS the download
+        await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_get_probe_saves_a_round_trip(tmp_path):
+    """With a distant origin the default probe (ranged GET kept open as the
+    data stream) finishes a small download a whole request latency sooner
+    than grab's HEAD-then-GET."""
+    async def main():
+        import time as _t
+        o = await Origin().start()
+        o.latency = 0.15
+        url = o.add("/clip.mkv", os.urandom(10_000))
+        times = {}
+        for mode in ("head", "get"):
+            h = _dl(probe=mode)
+            d = tmp_path / mode
+            os.makedirs(d)
+            t0 = _t.perf_counter()
+            await h.download(str(d), Sink(), url)
+            times[mode] = _t.perf_counter() - t0
+            await h.close()
+        assert times["head"] - times["get"] > 0.1, times
         await o.stop()
     run(main())

@@ -46,6 +46,7 @@ class Origin:
         self.cut_times = 0
         self.fail = 0
         self.rate: float | None = None
+        self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
         self._runner: web.AppRunner | None = None
 
@@ -75,6 +76,8 @@ class Origin:
 
     async def _handle(self, request: web.Request) -> web.StreamResponse:
         self.requests.append((request.method, request.path, request.headers.get("Range", "")))
+        if self.latency:
+            await asyncio.sleep(self.latency)     # emulated one-way network delay per request
         if self.fail > 0:
             self.fail -= 1
             return web.Response(status=500, text="injected")
