@@ -10,8 +10,6 @@ import subprocess
 import sys
 import time
 
-import pytest
-
 from tritondl.amqp.client import Client
 from tritondl.amqp.codec import Properties
 from tritondl.fakes.broker import Broker

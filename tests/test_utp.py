@@ -112,7 +112,6 @@ def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
         src = tmp_path / "src"
         make_payload(str(src), {"film.mkv": 1_500_000})
         info = torrent_for(str(src / "film.mkv"), 65536)
-        seed = Seeder(info, str(src))
         cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, verify_device="cpu", utp=True)
         st = Torrent(info.infohash, str(src), cfg, info=info)
         await st.start()
@@ -128,7 +127,6 @@ def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
         await dl.download(str(dst), lambda u, p: None, magnet_for(info, peers=[("127.0.0.1", st.port)]))
         assert (dst / "film.mkv").read_bytes() == (src / "film.mkv").read_bytes()
         await st.close()
-        _ = seed
     asyncio.run(asyncio.wait_for(main(), 60))
 
 

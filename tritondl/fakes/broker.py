@@ -22,7 +22,6 @@ from __future__ import annotations
 import asyncio
 import collections
 import itertools
-import re
 from dataclasses import dataclass, field
 from typing import Any
 

@@ -45,7 +45,7 @@ class HTTPTracker:
             await self._runner.cleanup()
 
     async def _announce(self, req: web.Request) -> web.Response:
-        from urllib.parse import parse_qs, unquote_to_bytes
+        from urllib.parse import unquote_to_bytes
         self.announces += 1
         raw = req.query_string
         q = {}
@@ -62,7 +62,6 @@ class HTTPTracker:
         elif port:
             sw[me] = time.monotonic()
         peers = [p for p in sw if p != me]
-        _ = parse_qs
         body = bencode.encode({b"interval": self.interval, b"peers": compact_peers(peers),
                                b"complete": len(sw), b"incomplete": 0})
         return web.Response(body=body, content_type="text/plain")
