@@ -354,6 +354,123 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
 }
 
 
+// ---------------------------------------------------------------------------
+// BitTorrent v2 (BEP 52) merkle verification.  Piece p covers bytes
+// [p*piece_len, p*piece_len + real[p]) of the piece-aligned layout; its leaves
+// are SHA-256 of each 16 KiB block (the last one may be short), padded with
+// all-zero hashes to width[p] leaves and reduced pairwise with SHA-256.  The
+// root must equal expected[32p .. 32p+32).  known[p] == 0 -> ok[p] = 0.
+constexpr size_t kMerkleLeaf = 16384;
+
+inline void merkle_reduce(std::vector<unsigned char>& row, size_t width) {
+  // row holds `width` 32-byte nodes; reduce in place to row[0..32)
+  const EVP_MD* md = EVP_sha256();
+  MdCtx ctx(md);
+  while (width > 1) {
+    for (size_t k = 0; k < width / 2; ++k) {
+      unsigned int outl = 0;
+      if (EVP_DigestInit_ex(ctx.ctx, md, nullptr) != 1 || EVP_DigestUpdate(ctx.ctx, row.data() + 64 * k, 64) != 1 ||
+          EVP_DigestFinal_ex(ctx.ctx, row.data() + 32 * k, &outl) != 1)
+        throw std::runtime_error("EVP failed in merkle_reduce");
+    }
+    width /= 2;
+  }
+}
+
+inline bool merkle_piece_ok(const unsigned char* leaves, size_t nleaves, size_t width, const char* expected) {
+  if (width == 0 || (width & (width - 1)) || nleaves > width) return false;
+  std::vector<unsigned char> row(32 * width, 0);
+  std::memcpy(row.data(), leaves, 32 * nleaves);
+  merkle_reduce(row, width);
+  return std::memcmp(row.data(), expected, 32) == 0;
+}
+
+// From precomputed leaf digests of the whole layout (e.g. the HIP kernel at
+// 16 KiB "pieces"); leaf_ok[k] == 0 marks a block that could not be read.
+inline std::string merkle_check(const std::string& leaves, const std::string& leaf_ok, size_t piece_len,
+                                const std::string& expected, const std::vector<long long>& widths,
+                                const std::vector<long long>& reals, const std::string& known, int threads) {
+  if (piece_len == 0 || piece_len % kMerkleLeaf) throw std::invalid_argument("piece_len must be a multiple of 16 KiB");
+  const size_t n = widths.size();
+  if (reals.size() != n || known.size() != n || expected.size() != 32 * n)
+    throw std::invalid_argument("merkle_check: per-piece arrays disagree in length");
+  const size_t nleaf_total = leaves.size() / 32;
+  if (leaf_ok.size() != nleaf_total) throw std::invalid_argument("leaf_ok size mismatch");
+  const size_t per = piece_len / kMerkleLeaf;
+  std::string ok(n, '\0');
+  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
+    if (!known[p] || reals[p] < 0) return;
+    const size_t nl = (static_cast<size_t>(reals[p]) + kMerkleLeaf - 1) / kMerkleLeaf;
+    const size_t first = p * per;
+    if (first + nl > nleaf_total) return;
+    for (size_t k = 0; k < nl; ++k)
+      if (!leaf_ok[first + k]) return;
+    ok[p] = merkle_piece_ok(reinterpret_cast<const unsigned char*>(leaves.data()) + 32 * first, nl,
+                            static_cast<size_t>(widths[p]), expected.data() + 32 * p);
+  });
+  return ok;
+}
+
+// Straight from files (host path): read each piece, hash its leaves, reduce.
+inline std::string merkle_verify(const std::vector<std::pair<std::string, long long>>& files, size_t piece_len,
+                                 const std::string& expected, const std::vector<long long>& widths,
+                                 const std::vector<long long>& reals, const std::string& known, int threads) {
+  if (piece_len == 0 || piece_len % kMerkleLeaf) throw std::invalid_argument("piece_len must be a multiple of 16 KiB");
+  const size_t n = widths.size();
+  if (reals.size() != n || known.size() != n || expected.size() != 32 * n)
+    throw std::invalid_argument("merkle_verify: per-piece arrays disagree in length");
+  std::vector<FileSpan> spans;
+  long long total = 0;
+  for (auto& f : files) {
+    if (f.second < 0) throw std::invalid_argument("negative file length");
+    spans.push_back({f.first, f.second, total});
+    total += f.second;
+  }
+  std::vector<int> fds(spans.size(), -1);
+  for (size_t i = 0; i < spans.size(); ++i)
+    if (!spans[i].path.empty()) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
+  std::string ok(n, '\0');
+  const EVP_MD* md = EVP_sha256();
+  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
+    if (!known[p] || reals[p] < 0 || static_cast<size_t>(reals[p]) > piece_len) return;
+    const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
+    const long long plen = reals[p];
+    if (pstart + plen > total) return;
+    std::vector<char> buf(static_cast<size_t>(plen));
+    long long filled = 0;
+    for (size_t s = 0; s < spans.size() && filled < plen; ++s) {
+      const long long fstart = spans[s].start, flen = spans[s].length;
+      const long long a = std::max(pstart + filled, fstart);
+      const long long e = std::min(pstart + plen, fstart + flen);
+      if (e <= a) continue;
+      const size_t want = static_cast<size_t>(e - a);
+      if (a != pstart + filled) return;
+      if (spans[s].path.empty()) {
+        std::memset(buf.data() + filled, 0, want);
+      } else if (fds[s] < 0 || pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) {
+        return;
+      }
+      filled += static_cast<long long>(want);
+    }
+    if (filled != plen) return;
+    const size_t nl = (static_cast<size_t>(plen) + kMerkleLeaf - 1) / kMerkleLeaf;
+    const size_t width = static_cast<size_t>(widths[p]);
+    if (width == 0 || (width & (width - 1)) || nl > width) return;
+    std::vector<unsigned char> row(32 * width, 0);
+    for (size_t k = 0; k < nl; ++k) {
+      const size_t off = k * kMerkleLeaf;
+      const size_t len = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off);
+      const std::string d = one_shot(md, buf.data() + off, len);
+      std::memcpy(row.data() + 32 * k, d.data(), 32);
+    }
+    merkle_reduce(row, width);
+    ok[p] = std::memcmp(row.data(), expected.data() + 32 * p, 32) == 0;
+  });
+  for (int fd : fds)
+    if (fd >= 0) ::close(fd);
+  return ok;
+}
+
 // RC4 keystream for BitTorrent Message Stream Encryption (MSE/PE).  MSE
 // mandates RC4 (and discarding the first 1024 keystream bytes); OpenSSL 3
 // only ships it in the legacy provider, so it lives here.  Byte-serial by

@@ -181,6 +181,36 @@ py::tuple py_aws_chunk_decode(const std::string& key, const std::string& amzdate
 
 PYBIND11_MODULE(_hash_host, m) {
   m.doc() = "tritondl host hashing (OpenSSL EVP, GIL-free, threaded piece verification)";
+  m.def(
+      "merkle_verify",
+      [](const std::vector<std::pair<std::string, long long>>& files, size_t piece_len, const std::string& expected,
+         const std::vector<long long>& widths, const std::vector<long long>& reals, const std::string& known,
+         int threads) {
+        std::string ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = merkle_verify(files, piece_len, expected, widths, reals, known, threads);
+        }
+        return py::bytes(ok);
+      },
+      py::arg("files"), py::arg("piece_len"), py::arg("expected"), py::arg("widths"), py::arg("reals"),
+      py::arg("known"), py::arg("threads") = 0,
+      "BEP 52 per-piece merkle verification straight from the file layout (threaded).");
+  m.def(
+      "merkle_check",
+      [](const std::string& leaves, const std::string& leaf_ok, size_t piece_len, const std::string& expected,
+         const std::vector<long long>& widths, const std::vector<long long>& reals, const std::string& known,
+         int threads) {
+        std::string ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = merkle_check(leaves, leaf_ok, piece_len, expected, widths, reals, known, threads);
+        }
+        return py::bytes(ok);
+      },
+      py::arg("leaves"), py::arg("leaf_ok"), py::arg("piece_len"), py::arg("expected"), py::arg("widths"),
+      py::arg("reals"), py::arg("known"), py::arg("threads") = 0,
+      "BEP 52 verification from precomputed 16 KiB leaf digests (e.g. the HIP kernel's).");
   py::class_<Rc4>(m, "Rc4")
       .def(py::init([](py::bytes key, size_t drop) {
              std::string k = key;

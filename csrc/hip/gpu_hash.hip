@@ -428,6 +428,46 @@ class GpuHasher {
     return py::bytes(ok);
   }
 
+  // All piece digests of a file layout plus a per-piece "fully read" mask —
+  // used at 16 KiB "pieces" for BitTorrent v2 merkle leaves (host reduces).
+  py::tuple digest_files(const std::vector<std::pair<std::string, long long>>& files, size_t piece_len,
+                         const std::string& kind) {
+    const int alg = alg_id(kind);
+    const int dl = digest_len(alg);
+    if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
+    std::vector<Span> spans;
+    long long total = 0;
+    for (auto& f : files) {
+      if (f.second < 0) throw std::invalid_argument("negative file length");
+      spans.push_back({f.first.empty() ? kZeroSpan : ::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
+      total += f.second;
+    }
+    auto close_all = [&] {
+      for (auto& s : spans)
+        if (s.fd >= 0) ::close(s.fd);
+    };
+    const size_t n = total > 0 ? (static_cast<size_t>(total) + piece_len - 1) / piece_len : 0;
+    std::string digests(n * dl, '\0'), ok(n, '\0');
+    {
+      py::gil_scoped_release nogil;
+      try {
+        run_windows(alg, piece_len, static_cast<size_t>(total), n,
+                    [&](uint8_t* dst, size_t off, size_t len, char* complete) {
+                      read_spans(spans, dst, off, len, piece_len, complete);
+                    },
+                    [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& complete) {
+                      std::memcpy(&digests[first * dl], d, count * dl);
+                      for (size_t k = 0; k < count; ++k) ok[first + k] = complete[k];
+                    });
+      } catch (...) {
+        close_all();
+        throw;
+      }
+    }
+    close_all();
+    return py::make_tuple(py::bytes(digests), py::bytes(ok));
+  }
+
   size_t batch_bytes() const { return stage_req_; }
   size_t last_window_bytes() const { return last_window_; }
   size_t window_bytes_for(size_t total, size_t piece_len) {
@@ -639,6 +679,8 @@ PYBIND11_MODULE(_gpu_hash, m) {
       .def("hash_buffer", &GpuHasher::hash_buffer, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"))
       .def("verify_files", &GpuHasher::verify_files, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
            py::arg("kind") = "sha1")
+      .def("digest_files", &GpuHasher::digest_files, py::arg("files"), py::arg("piece_len"), py::arg("kind") = "sha256",
+           "(digests, fully_read_mask) of every piece of a file layout")
       .def("release", &GpuHasher::release)
       .def("window_bytes_for", &GpuHasher::window_bytes_for)
       .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)

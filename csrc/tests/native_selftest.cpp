@@ -142,11 +142,48 @@ static void test_utp(double loss, size_t n, unsigned seed) {
   CHECK(cb >= 0 && B.eof(cb));
 }
 
+static void test_merkle() {
+  // one file of 3 leaves + 100 bytes in a 64 KiB piece: root over 4 leaves, 4th = zero hash
+  std::mt19937 rng(11);
+  std::string data(3 * kMerkleLeaf + 100, '\0');
+  for (auto& ch : data) ch = static_cast<char>(rng());
+  auto H = [](const std::string& x) { return one_shot(EVP_sha256(), x.data(), x.size()); };
+  std::string l0 = H(data.substr(0, kMerkleLeaf)), l1 = H(data.substr(kMerkleLeaf, kMerkleLeaf)),
+              l2 = H(data.substr(2 * kMerkleLeaf, kMerkleLeaf)), l3 = H(data.substr(3 * kMerkleLeaf));
+  std::string root = H(H(l0 + l1) + H(l2 + l3));  // 4 real leaves
+  std::string leaves = l0 + l1 + l2 + l3;
+  std::string ok = merkle_check(leaves, std::string(4, '\1'), 65536, root, {4}, {(long long)data.size()},
+                                std::string(1, '\1'), 2);
+  CHECK(ok == std::string(1, '\1'));
+  // width 8 pads with four zero leaves
+  std::string z(32, '\0');
+  std::string root8 = H(root + H(H(z + z) + H(z + z)));
+  ok = merkle_check(leaves, std::string(4, '\1'), 131072, root8, {8}, {(long long)data.size()}, std::string(1, '\1'), 1);
+  CHECK(ok == std::string(1, '\1'));
+  // from a file, and an unreadable leaf fails
+  char tmpl[] = "/tmp/tdl_merkleXXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  if (!dir) return;
+  std::string f = std::string(dir) + "/f";
+  FILE* fp = std::fopen(f.c_str(), "wb");
+  std::fwrite(data.data(), 1, data.size(), fp);
+  std::fclose(fp);
+  ok = merkle_verify({{f, (long long)data.size()}}, 65536, root, {4}, {(long long)data.size()}, std::string(1, '\1'), 2);
+  CHECK(ok == std::string(1, '\1'));
+  ok = merkle_check(leaves, std::string("\1\0\1\1", 4), 65536, root, {4}, {(long long)data.size()},
+                    std::string(1, '\1'), 1);
+  CHECK(ok == std::string(1, '\0'));
+  std::remove(f.c_str());
+  rmdir(dir);
+}
+
 int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
   test_aws_chunked();
   test_pieces_and_verify();
+  test_merkle();
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
   if (failures) {

@@ -1,4 +1,12 @@
-"""Torrent metainfo (BEP 3), magnet links (BEP 9) and torrent creation.
+"""Torrent metainfo (BEP 3; v2 and hybrid torrents, BEP 52), magnet links
+(BEP 9, ``btih`` and ``btmh``) and torrent creation.
+
+v2 torrents describe files in a ``file tree`` with per-file merkle roots
+(:mod:`.merkle`); their piece index space is the files laid end to end, each
+starting on a piece boundary.  A pure v2 torrent is mapped onto the same
+``files`` layout the v1 code uses by inserting virtual BEP 47 padding
+entries, so storage, the piece picker and the wire protocol are shared; only
+piece verification differs (:meth:`Info.check_piece`).
 
 ``Info`` is the parsed info dictionary with the file layout used by the
 storage (single-file: ``<name>``; multi-file: ``<name>/<path...>``, the
@@ -14,7 +22,7 @@ import os
 from dataclasses import dataclass, field
 from urllib.parse import parse_qs, quote, unquote, urlparse
 
-from . import bencode
+from . import bencode, merkle
 from .bencode import BencodeError
 
 BLOCK = 16 * 1024  # request/metadata block size
@@ -40,15 +48,35 @@ def _safe_component(c: bytes | str) -> str:
 
 
 @dataclass
+class V2File:
+    path: list[str]
+    length: int
+    root: bytes          # 32-byte pieces root (b"" for empty files)
+    first_piece: int     # index of its first piece in the (piece-aligned) piece space
+    num_pieces: int
+
+
+@dataclass
 class Info:
     name: str
     piece_length: int
-    pieces: bytes                 # concatenated 20-byte SHA-1s
+    pieces: bytes                 # concatenated 20-byte SHA-1s (b"" for pure v2)
     files: list[FileEntry]
     multi: bool
     raw: bytes                    # exact bencoded info dict
     private: bool = False
-    infohash: bytes = b""
+    infohash: bytes = b""         # the 20-byte wire info-hash (v1 SHA-1, or truncated v2 SHA-256)
+    v2_files: list[V2File] = field(default_factory=list)
+    infohash_v2: bytes = b""      # full SHA-256 of the info dict (v2 / hybrid)
+    piece_layers: dict = field(default_factory=dict)   # pieces root -> concatenated piece-layer hashes
+
+    @property
+    def has_v1(self) -> bool:
+        return bool(self.pieces) or (not self.v2_files and self.total_length == 0)
+
+    @property
+    def has_v2(self) -> bool:
+        return bool(self.v2_files)
 
     @property
     def total_length(self) -> int:
@@ -56,7 +84,9 @@ class Info:
 
     @property
     def num_pieces(self) -> int:
-        return len(self.pieces) // 20
+        if self.pieces or not self.v2_files:
+            return len(self.pieces) // 20
+        return sum(f.num_pieces for f in self.v2_files)
 
     def piece_hash(self, i: int) -> bytes:
         return self.pieces[20 * i:20 * i + 20]
@@ -66,6 +96,68 @@ class Info:
             rem = self.total_length - i * self.piece_length
             return rem
         return self.piece_length
+
+    # -- v2 piece verification ------------------------------------------------
+    def v2_piece(self, i: int) -> tuple[bytes | None, int, int]:
+        """(expected hash or None if the piece layer is not known yet, tree
+        width in leaves, real data bytes) of piece ``i`` of a v2 torrent."""
+        lo, hi = 0, len(self.v2_files)
+        while hi - lo > 1:                      # last file whose first piece <= i
+            mid = (lo + hi) // 2
+            if self.v2_files[mid].first_piece <= i:
+                lo = mid
+            else:
+                hi = mid
+        f = self.v2_files[lo]
+        while f.num_pieces == 0 or i >= f.first_piece + f.num_pieces:
+            lo += 1
+            f = self.v2_files[lo]
+        k = i - f.first_piece
+        real = min(self.piece_length, f.length - k * self.piece_length)
+        if f.num_pieces == 1:
+            return f.root, merkle.next_pow2(-(-f.length // merkle.LEAF)), real
+        layer = self.piece_layers.get(f.root)
+        exp = layer[32 * k:32 * k + 32] if layer else None
+        return exp, self.piece_length // merkle.LEAF, real
+
+    def v2_expectations(self) -> tuple[bytes, list[int], list[int], list[int]]:
+        """Batch form for the native verifiers: expected hashes (32 B each,
+        zeros where unknown), tree widths, real lengths and a known-mask."""
+        exp, widths, reals, known = bytearray(), [], [], []
+        for i in range(self.num_pieces):
+            e, w, r = self.v2_piece(i)
+            exp += e if e is not None else bytes(32)
+            widths.append(w)
+            reals.append(r)
+            known.append(e is not None)
+        return bytes(exp), widths, reals, known
+
+    def missing_layers(self) -> list[V2File]:
+        return [f for f in self.v2_files if f.num_pieces > 1 and f.root not in self.piece_layers]
+
+    def set_piece_layer(self, root: bytes, layer: bytes) -> bool:
+        """Accept a piece layer only if it reduces to the file's root."""
+        f = next((x for x in self.v2_files if x.root == root), None)
+        if f is None or len(layer) != 32 * f.num_pieces:
+            return False
+        nodes = [layer[k:k + 32] for k in range(0, len(layer), 32)]
+        if merkle.layer_root(nodes, self.piece_length) != root:
+            return False
+        self.piece_layers[root] = bytes(layer)
+        return True
+
+    def check_piece(self, i: int, data) -> bool | None:
+        """Verify piece ``i``: SHA-1 for v1/hybrid, merkle for pure v2 (None
+        when the v2 piece layer is not known yet)."""
+        if self.pieces:
+            return hashlib.sha1(data).digest() == self.piece_hash(i)
+        exp, width, real = self.v2_piece(i)
+        if exp is None:
+            return None
+        return merkle.piece_root(memoryview(data)[:real], width) == exp
+
+    def matches(self, infohash: bytes) -> bool:
+        return infohash in (self.infohash, self.infohash_v2, self.infohash_v2[:20]) and len(infohash) in (20, 32)
 
     def file_paths(self, base_dir: str) -> list[tuple[str, int]]:
         """[(absolute path, length), ...] in stream order; a BEP 47 padding
@@ -84,6 +176,8 @@ class Info:
             raise MetainfoError(f"bad info dict: {e}") from e
         if not isinstance(d, dict):
             raise MetainfoError("info is not a dict")
+        if d.get(b"meta version") == 2 and b"pieces" not in d:
+            return cls._parse_v2_only(d, raw)
         try:
             name = _safe_component(d[b"name"])
             plen = int(d[b"piece length"])
@@ -92,6 +186,9 @@ class Info:
             raise MetainfoError(f"info dict missing field: {e}") from e
         if plen <= 0 or len(pieces) % 20:
             raise MetainfoError("invalid piece length / pieces")
+        v2_files: list[V2File] = []
+        if d.get(b"meta version") == 2:
+            v2_files = _parse_file_tree(d.get(b"file tree"), plen)
         files: list[FileEntry] = []
         off = 0
         if b"files" in d:
@@ -114,8 +211,74 @@ class Info:
         npieces = len(pieces) // 20
         if npieces != (off + plen - 1) // plen:
             raise MetainfoError(f"piece count {npieces} does not match total length {off}")
-        return cls(name, plen, pieces, files, multi, bytes(raw), bool(d.get(b"private", 0)),
+        info = cls(name, plen, pieces, files, multi, bytes(raw), bool(d.get(b"private", 0)),
                    hashlib.sha1(raw).digest())
+        if v2_files:                                 # hybrid: v1 pieces drive verification
+            real = [f for f in files if not f.pad]
+            if [(f.path, f.length) for f in real] != [(v.path if multi else [name], v.length) for v in v2_files]:
+                raise MetainfoError("hybrid torrent: v1 and v2 file lists differ")
+            info.v2_files = v2_files
+            info.infohash_v2 = hashlib.sha256(raw).digest()
+        return info
+
+    @classmethod
+    def _parse_v2_only(cls, d: dict, raw: bytes) -> "Info":
+        try:
+            name = _safe_component(d[b"name"])
+            plen = int(d[b"piece length"])
+        except (KeyError, TypeError, ValueError) as e:
+            raise MetainfoError(f"info dict missing field: {e}") from e
+        v2 = _parse_file_tree(d.get(b"file tree"), plen)
+        # single file: the tree is exactly {name: {"": ...}}
+        multi = not (len(v2) == 1 and v2[0].path == [name])
+        files: list[FileEntry] = []
+        off = 0
+        for k, v in enumerate(v2):
+            files.append(FileEntry(v.path if multi else [name], v.length, off))
+            off += v.length
+            gap = (-v.length) % plen
+            if gap and k < len(v2) - 1:              # virtual BEP 47 padding: next file on a piece boundary
+                files.append(FileEntry([".pad", str(gap)], gap, off, True))
+                off += gap
+        h2 = hashlib.sha256(raw).digest()
+        return cls(name, plen, b"", files, multi, bytes(raw), bool(d.get(b"private", 0)), h2[:20],
+                   v2_files=v2, infohash_v2=h2)
+
+
+def _parse_file_tree(tree, plen: int) -> list[V2File]:
+    if not isinstance(tree, dict) or not tree:
+        raise MetainfoError("v2 info has no file tree")
+    try:
+        merkle.piece_levels(plen)
+    except ValueError as e:
+        raise MetainfoError(str(e)) from e
+    out: list[V2File] = []
+    piece = 0
+
+    def walk(node: dict, path: list[str], depth: int) -> None:
+        nonlocal piece
+        if depth > 64:
+            raise MetainfoError("file tree too deep")
+        for k in sorted(node):
+            v = node[k]
+            if not isinstance(v, dict):
+                raise MetainfoError("bad file tree node")
+            comp = _safe_component(k)
+            if b"" in v and isinstance(v[b""], dict):
+                leaf = v[b""]
+                ln = leaf.get(b"length")
+                if not isinstance(ln, int) or ln < 0:
+                    raise MetainfoError("bad file length in file tree")
+                root = leaf.get(b"pieces root", b"")
+                if ln > 0 and (not isinstance(root, bytes) or len(root) != 32):
+                    raise MetainfoError("file without a 32-byte pieces root")
+                n = -(-ln // plen)
+                out.append(V2File(path + [comp], ln, root if ln else b"", piece, n))
+                piece += n
+            else:
+                walk(v, path + [comp], depth + 1)
+    walk(tree, [], 0)
+    return out
 
 
 @dataclass
@@ -150,6 +313,11 @@ class Metainfo:
         nodes = [(n[0].decode(), int(n[1])) for n in d.get(b"nodes", []) if isinstance(n, list) and len(n) == 2]
         ul = d.get(b"url-list", [])
         url_list = [ul.decode()] if isinstance(ul, bytes) else [u.decode() for u in ul if isinstance(u, bytes)]
+        layers = d.get(b"piece layers", {})
+        if info.has_v2 and isinstance(layers, dict):
+            for root, layer in layers.items():
+                if isinstance(root, bytes) and isinstance(layer, bytes) and not info.set_piece_layer(root, layer):
+                    raise MetainfoError("piece layer does not match its pieces root")
         return cls(info, tiers, nodes, url_list)
 
     def encode(self) -> bytes:
@@ -159,6 +327,8 @@ class Metainfo:
             d[b"announce-list"] = [[u.encode() for u in t] for t in self.announce]
         if self.url_list:
             d[b"url-list"] = [u.encode() for u in self.url_list]
+        if self.info.piece_layers:
+            d[b"piece layers"] = dict(self.info.piece_layers)
         return _encode_with_raw(d)
 
 
@@ -182,18 +352,22 @@ def _encode_with_raw(d: dict) -> bytes:
 
 @dataclass
 class Magnet:
-    infohash: bytes
+    infohash: bytes                  # 20-byte wire info-hash (btih, or truncated btmh)
     display_name: str = ""
     trackers: list[str] = field(default_factory=list)
     peers: list[tuple[str, int]] = field(default_factory=list)
     web_seeds: list[str] = field(default_factory=list)
+    infohash_v2: bytes = b""         # full SHA-256 from ``xt=urn:btmh:1220...``
+    has_v1: bool = True
 
     @property
     def hex(self) -> str:
         return self.infohash.hex()
 
     def uri(self) -> str:
-        parts = [f"xt=urn:btih:{self.hex}"]
+        parts = [f"xt=urn:btih:{self.hex}"] if self.has_v1 else []
+        if self.infohash_v2:
+            parts.append(f"xt=urn:btmh:1220{self.infohash_v2.hex()}")
         if self.display_name:
             parts.append("dn=" + quote(self.display_name))
         parts += ["tr=" + quote(t, safe="") for t in self.trackers]
@@ -208,8 +382,14 @@ def parse_magnet(uri: str) -> Magnet:
         raise MetainfoError(f"unsupported scheme '{u.scheme}'")
     q = parse_qs(u.query, keep_blank_values=True)
     ih = None
+    ih2 = b""
     for xt in q.get("xt", []):
-        if xt.lower().startswith("urn:btih:"):
+        if xt.lower().startswith("urn:btmh:"):
+            mh = xt[9:]
+            if not mh.lower().startswith("1220") or len(mh) != 68:
+                raise MetainfoError("btmh must be a SHA-256 multihash (1220 + 64 hex)")
+            ih2 = bytes.fromhex(mh[4:])
+        elif xt.lower().startswith("urn:btih:"):
             h = xt[9:]
             if len(h) == 40:
                 ih = bytes.fromhex(h)
@@ -217,24 +397,38 @@ def parse_magnet(uri: str) -> Magnet:
                 ih = base64.b32decode(h.upper())
             else:
                 raise MetainfoError(f"bad btih length {len(h)}")
+    has_v1 = ih is not None
+    if ih is None and ih2:
+        ih = ih2[:20]                # v2-only swarm: peers use the truncated SHA-256
     if ih is None:
-        raise MetainfoError("magnet link has no urn:btih")
+        raise MetainfoError("magnet link has no urn:btih or urn:btmh")
     peers = []
     for pe in q.get("x.pe", []):
         host, _, port = pe.rpartition(":")
         if host and port.isdigit():
             peers.append((host.strip("[]"), int(port)))
-    return Magnet(ih, unquote(q.get("dn", [""])[0]), q.get("tr", []), peers, q.get("ws", []))
+    return Magnet(ih, unquote(q.get("dn", [""])[0]), q.get("tr", []), peers, q.get("ws", []), ih2, has_v1)
 
 
 # ----------------------------------------------------------------- create
 
 
 def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None,
-              private: bool = False, pad: bool = False) -> Info:
+              private: bool = False, pad: bool = False, version: int = 1) -> Info:
     """Build an info dict for a file or directory (used by the test swarm).
-    ``pad``: align every file to a piece boundary with BEP 47 padding files."""
+    ``pad``: align every file to a piece boundary with BEP 47 padding files.
+    ``version``: 1 (BEP 3), 2 (pure BEP 52) or 3 (hybrid v1+v2; implies
+    ``pad``).  For v2/hybrid the returned Info carries its piece layers."""
     from ...ops import hashing
+    if version not in (1, 2, 3):
+        raise ValueError("version must be 1, 2 or 3 (hybrid)")
+    if version != 1:
+        try:
+            merkle.piece_levels(piece_length)
+        except ValueError as e:
+            raise MetainfoError(str(e)) from e
+        pad = True
+    tname = name or os.path.basename(base.rstrip("/"))
     if os.path.isdir(base):
         entries = []
         for root, _dirs, fnames in os.walk(base):
@@ -243,6 +437,29 @@ def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None
                 rel = os.path.relpath(full, base).split(os.sep)
                 entries.append((rel, full))
         entries.sort()
+        multi = True
+    else:
+        entries = [([tname], base)]
+        multi = False
+    d: dict = {b"name": tname.encode(), b"piece length": piece_length}
+    layers: dict[bytes, bytes] = {}
+    if version != 1:
+        tree: dict = {}
+        for rel, f in entries:
+            data = open(f, "rb").read()
+            leaf: dict = {b"length": len(data)}
+            if data:
+                root, layer = merkle.file_root_and_layer(data, piece_length)
+                leaf[b"pieces root"] = root
+                if layer:
+                    layers[root] = b"".join(layer)
+            node = tree
+            for c in rel[:-1]:
+                node = node.setdefault(c.encode(), {})
+            node[rel[-1].encode()] = {b"": leaf}
+        d[b"file tree"] = tree
+        d[b"meta version"] = 2
+    if version != 2:
         files, layout = [], []
         for k, (rel, f) in enumerate(entries):
             n = os.path.getsize(f)
@@ -252,21 +469,23 @@ def make_info(base: str, piece_length: int = 256 * 1024, name: str | None = None
                 gap = piece_length - n % piece_length
                 files.append({b"attr": b"p", b"length": gap, b"path": [b".pad", str(gap).encode()]})
                 layout.append(("", gap))
-        d = {b"name": (name or os.path.basename(base.rstrip("/"))).encode(), b"piece length": piece_length,
-             b"files": files}
-    else:
-        layout = [(base, os.path.getsize(base))]
-        d = {b"name": (name or os.path.basename(base)).encode(), b"piece length": piece_length,
-             b"length": os.path.getsize(base)}
-    total = sum(n for _p, n in layout)
-    blob = bytearray()
-    for p, n in layout:
-        if not p:
-            blob += bytes(n)
-            continue
-        with open(p, "rb") as f:
-            blob += f.read()
-    d[b"pieces"] = hashing.piece_hashes(bytes(blob), piece_length, "sha1") if total else b""
+        if multi:
+            d[b"files"] = files
+        else:
+            d[b"length"] = layout[0][1]
+        total = sum(n for _p, n in layout)
+        blob = bytearray()
+        for p, n in layout:
+            if not p:
+                blob += bytes(n)
+                continue
+            with open(p, "rb") as fh:
+                blob += fh.read()
+        d[b"pieces"] = hashing.piece_hashes(bytes(blob), piece_length, "sha1") if total else b""
     if private:
         d[b"private"] = 1
-    return Info.parse(bencode.encode(d))
+    info = Info.parse(bencode.encode(d))
+    for root, layer in layers.items():
+        if not info.set_piece_layer(root, layer):
+            raise MetainfoError("internal: piece layer does not reduce to its root")
+    return info

@@ -20,6 +20,7 @@ HANDSHAKE_LEN = 49 + len(PSTR)
 CHOKE, UNCHOKE, INTERESTED, NOT_INTERESTED, HAVE, BITFIELD, REQUEST, PIECE, CANCEL, PORT = range(10)
 SUGGEST, HAVE_ALL, HAVE_NONE, REJECT, ALLOWED_FAST = 0x0D, 0x0E, 0x0F, 0x10, 0x11
 EXTENDED = 20
+HASH_REQUEST, HASHES, HASH_REJECT = 21, 22, 23        # BEP 52
 EXT_HANDSHAKE = 0
 UT_METADATA_ID = 3            # the id WE assign to ut_metadata in our extended handshake
 UT_PEX_ID = 1                 # ... and to ut_pex
@@ -28,8 +29,10 @@ META_REQUEST, META_DATA, META_REJECT = 0, 1, 2
 MAX_MSG = 2 * 1024 * 1024 + 13
 
 
-def reserved_bytes(dht: bool = True, fast: bool = True, extended: bool = True) -> bytes:
+def reserved_bytes(dht: bool = True, fast: bool = True, extended: bool = True, v2: bool = True) -> bytes:
     r = bytearray(8)
+    if v2:
+        r[7] |= 0x10          # BEP 52: supports v2 hash requests / messages
     if extended:
         r[5] |= 0x10
     if fast:
@@ -60,6 +63,10 @@ class Handshake:
     @property
     def dht(self) -> bool:
         return bool(self.reserved[7] & 0x01)
+
+    @property
+    def v2(self) -> bool:
+        return bool(self.reserved[7] & 0x10)
 
 
 def encode_handshake(infohash: bytes, peer_id: bytes, reserved: bytes | None = None) -> bytes:
@@ -195,6 +202,15 @@ class Wire:
         self._queue(struct.pack(">IBII", len(data) + 9, PIECE, i, off))
         self._queue(data)
 
+    def hash_request(self, root: bytes, base: int, index: int, length: int, proofs: int) -> None:
+        self.send(HASH_REQUEST, root + struct.pack(">IIII", base, index, length, proofs))
+
+    def hashes(self, root: bytes, base: int, index: int, length: int, proofs: int, hashes: bytes) -> None:
+        self.send(HASHES, root + struct.pack(">IIII", base, index, length, proofs) + hashes)
+
+    def hash_reject(self, root: bytes, base: int, index: int, length: int, proofs: int) -> None:
+        self.send(HASH_REJECT, root + struct.pack(">IIII", base, index, length, proofs))
+
     def extended(self, ext_id: int, payload: bytes) -> None:
         self.send(EXTENDED, bytes([ext_id]) + payload)
 
@@ -281,6 +297,15 @@ def parse_pex(payload: bytes) -> tuple[list[tuple[str, int]], list[tuple[str, in
     added = compact(d.get(b"added"), 6) + compact(d.get(b"added6"), 18)
     dropped = compact(d.get(b"dropped"), 6) + compact(d.get(b"dropped6"), 18)
     return added, dropped
+
+
+def parse_hash_msg(pl: bytes) -> tuple[bytes, int, int, int, int, bytes]:
+    """(pieces root, base layer, index, length, proof layers, hashes) of a
+    BEP 52 hash request / hashes / hash reject message."""
+    if len(pl) < 48 or (len(pl) - 48) % 32:
+        raise PeerError("bad v2 hash message")
+    base, index, length, proofs = struct.unpack(">IIII", pl[32:48])
+    return pl[:32], base, index, length, proofs, pl[48:]
 
 
 def meta_msg(msg_type: int, piece: int, total_size: int | None = None, data: bytes = b"") -> bytes:

@@ -134,9 +134,18 @@ class FileStorage:
         if not any(p and os.path.exists(p) and os.path.getsize(p) for p, _ in self.layout):
             return set()
         dev = device
-        if device == "auto":
-            dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length)
-        ok = hashing.verify_pieces(self.layout, self.info.piece_length, self.info.pieces, device=dev)
+        if self.info.pieces:
+            if device == "auto":
+                dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length)
+            ok = hashing.verify_pieces(self.layout, self.info.piece_length, self.info.pieces, device=dev)
+        else:
+            # pure v2: per-piece merkle roots over 16 KiB leaves — every leaf is
+            # independent, so the GPU sees total/16 KiB lanes whatever the piece size
+            exp, widths, reals, known = self.info.v2_expectations()
+            if device == "auto":
+                dev = hashing.choose_device(-(-self.info.total_length // 16384), 16384, self.info.total_length)
+            ok = hashing.verify_pieces_v2(self.layout, self.info.piece_length, exp, widths, reals, known,
+                                          device=dev)
         have = {i for i, v in enumerate(ok) if v}
         if self.db is not None:
             self.db.set_many(self.info.infohash, {i: bool(v) for i, v in enumerate(ok)})

@@ -34,7 +34,7 @@ import time
 from dataclasses import dataclass, field
 
 from ...utils.log import log
-from . import mse
+from . import merkle, mse
 from . import peer as pw
 from .dht import DHTNode
 from .metainfo import BLOCK, Info, MetainfoError
@@ -61,6 +61,7 @@ class TorrentConfig:
     pex_interval: float = 60.0
     webseed_conns: int = 4           # BEP 19: concurrent piece fetches per web seed
     encryption: str = "allow"        # MSE/PE policy: disable | allow | prefer | require (see .mse)
+    layer_timeout: float = 120.0     # BEP 52: time to fetch piece layers of a v2 magnet
 
 
 @dataclass
@@ -152,6 +153,7 @@ class Torrent:
         self.pieces: dict[int, _Piece] = {}
         self.open_pieces: dict[int, _Piece] = {}        # subset of pieces with blocks left to hand out
         self.verifying: set[int] = set()                # complete pieces being hashed/written
+        self._layer_waiters: dict = {}                  # (root, index, peer) -> future of a v2 hashes reply
         self._finishers: set[asyncio.Task] = set()
         self.peers: dict[tuple[str, int], _Peer] = {}
         self.known: set[tuple[str, int]] = set()
@@ -241,7 +243,7 @@ class Torrent:
 
     # ------------------------------------------------------------ info / storage
     def _set_info(self, info: Info) -> None:
-        if info.infohash != self.infohash:
+        if not info.matches(self.infohash):
             raise MetainfoError("info dict does not match info-hash")
         self.info = info
         n = info.num_pieces
@@ -258,6 +260,11 @@ class Torrent:
         self.db = CompletionDB(os.path.join(self.base_dir, ".torrent.db"))
         self.storage = FileStorage(self.base_dir, self.info, self.db)
         self.storage.open()
+        if self.info.missing_layers():
+            # pure v2 from a magnet: piece layers are not in the info dict;
+            # fetch them (BEP 52 hash requests, merkle-proofed) before any piece
+            # can be verified — resume check included
+            await self._fetch_layers()
         loop = asyncio.get_running_loop()
         have = await loop.run_in_executor(None, self.storage.verify_existing, self.cfg.verify_device)
         for i in have:
@@ -311,6 +318,11 @@ class Torrent:
                                                  self.downloaded, 0, "completed"))
                 event = "done"
             await asyncio.sleep(interval if not self._starving() else min(interval, 5.0))
+
+    def _accepts(self, ih: bytes) -> bool:
+        """Our 20-byte info-hash, or (hybrid) the truncated v2 one."""
+        return ih == self.infohash or (self.info is not None and bool(self.info.infohash_v2)
+                                       and ih == self.info.infohash_v2[:20])
 
     @property
     def private(self) -> bool:
@@ -410,17 +422,17 @@ class Torrent:
                                                          allow_plain=policy != "require",
                                                          timeout=self.cfg.connect_timeout)
                 hs = await asyncio.wait_for(pw.read_handshake(reader), self.cfg.connect_timeout)
-            if hs.infohash != self.infohash:
+            if not self._accepts(hs.infohash):
                 writer.close()
                 return
-            writer.write(pw.encode_handshake(self.infohash, self.peer_id))
+            writer.write(pw.encode_handshake(hs.infohash, self.peer_id))   # answer with the hash they used
         except (OSError, asyncio.TimeoutError, asyncio.IncompleteReadError, pw.PeerError):
             writer.close()
             return
         await self._run_peer(reader, writer, addr, hs, inbound=True)
 
     async def _run_peer(self, reader, writer, addr, hs: pw.Handshake, inbound: bool = True) -> None:
-        if hs.infohash != self.infohash or hs.peer_id == self.peer_id or addr in self.peers or self.closed:
+        if not self._accepts(hs.infohash) or hs.peer_id == self.peer_id or addr in self.peers or self.closed:
             writer.close()
             return
         n = self.info.num_pieces if self.info else 0
@@ -529,6 +541,8 @@ class Torrent:
             pass
         elif mid == pw.EXTENDED:
             await self._on_extended(p, pl)
+        elif mid in (pw.HASH_REQUEST, pw.HASHES, pw.HASH_REJECT):
+            self._on_hash_msg(p, mid, pl)
 
     def _peer_has(self, p: _Peer, idxs) -> None:
         if self.info is None:
@@ -652,6 +666,8 @@ class Torrent:
 
     async def _finish_piece(self, i: int, pc: _Piece, src: _Peer) -> None:
         ok = await self.commit_piece(i, pc.buf)   # the buffer is no longer shared: the piece left self.pieces
+        if ok is None:
+            return                                # unverifiable yet (v2 layer missing): not the peer's fault
         if not ok:
             src.bad += 1
             log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
@@ -659,18 +675,20 @@ class Torrent:
                 self.banned.add(src.addr)
                 src.wire.close()
 
-    async def commit_piece(self, i: int, data) -> bool:
+    async def commit_piece(self, i: int, data) -> bool | None:
         """Verify a whole piece off-loop, write it and record completion; then
         announce it.  Shared by peer downloads and web seeds.  False on a hash
         mismatch (nothing is written)."""
         assert self.info is not None and self.storage is not None
         loop = asyncio.get_running_loop()
-        expect = self.info.piece_hash(i)
         st = self.storage
 
-        def verify_and_write() -> bool:
-            if hashlib.sha1(data).digest() != expect:
-                return False
+        info = self.info
+
+        def verify_and_write() -> bool | None:
+            ok = info.check_piece(i, data)
+            if not ok:
+                return ok                    # False: bad data; None: v2 piece layer unknown
             st.write(i, 0, data)
             st.mark(i, True)
             return True
@@ -681,7 +699,7 @@ class Torrent:
         finally:
             self.verifying.discard(i)
         if not ok:
-            return False
+            return ok
         if self.have[i]:
             return True
         self.have[i] = 1
@@ -765,6 +783,77 @@ class Torrent:
             p.pex_sent.update(added)
             p.pex_sent.difference_update(dropped)
 
+    # ------------------------------------------------------------ BEP 52 piece layers
+    def _layer_geometry(self, f) -> tuple[int, int, int]:
+        """(base layer, request length, proof layers) for fetching f's piece layer."""
+        assert self.info is not None
+        base = merkle.piece_levels(self.info.piece_length)
+        width = merkle.next_pow2(f.num_pieces)
+        length = min(512, width)
+        total_h = width.bit_length() - 1
+        return base, length, total_h - (length.bit_length() - 1)
+
+    def _on_hash_msg(self, p: _Peer, mid: int, pl: bytes) -> None:
+        root, base, index, length, proofs, hashes = pw.parse_hash_msg(pl)
+        info = self.info
+        if mid == pw.HASH_REQUEST:
+            layer = info.piece_layers.get(root) if info is not None else None
+            ans = None
+            if layer is not None and base == merkle.piece_levels(info.piece_length) and length <= 512:
+                nodes = [layer[k:k + 32] for k in range(0, len(layer), 32)]
+                ans = merkle.serve_hashes(nodes, base, index, length, proofs)
+            if ans is None:
+                p.wire.hash_reject(root, base, index, length, proofs)
+            else:
+                p.wire.hashes(root, base, index, length, proofs, ans)
+            return
+        fut = self._layer_waiters.pop((root, index, p.key), None)
+        if fut is None or fut.done():
+            return
+        if mid == pw.HASH_REJECT or info is None:
+            fut.set_result(None)
+            return
+        f = next((x for x in info.v2_files if x.root == root), None)
+        got = merkle.check_hashes(root, base, index, length, hashes, f.num_pieces) if f is not None else None
+        fut.set_result(got)
+
+    async def _fetch_layers(self, timeout: float | None = None) -> None:
+        """Fetch every missing piece layer in merkle-proofed slices of <= 512
+        hashes from v2-capable peers, trying peers in turn per slice."""
+        assert self.info is not None
+        info = self.info
+        deadline = time.monotonic() + (timeout if timeout is not None else self.cfg.layer_timeout)
+        for f in info.missing_layers():
+            base, length, proofs = self._layer_geometry(f)
+            slices: dict[int, list[bytes]] = {}
+            for index in range(0, f.num_pieces, length):
+                tried: set = set()
+                while index not in slices:
+                    if time.monotonic() > deadline or self.closed:
+                        raise MetainfoError(f"could not fetch the piece layer of {'/'.join(f.path)}")
+                    cands = [q for q in self.peers.values() if q.hs.v2 and q.key not in tried and not q.wire.closed]
+                    if not cands:
+                        tried.clear()
+                        await asyncio.sleep(0.2)
+                        continue
+                    q = cands[0]
+                    tried.add(q.key)
+                    fut = asyncio.get_running_loop().create_future()
+                    self._layer_waiters[(f.root, index, q.key)] = fut
+                    q.wire.hash_request(f.root, base, index, length, proofs)
+                    try:
+                        got = await asyncio.wait_for(fut, 10.0)
+                    except asyncio.TimeoutError:
+                        got = None
+                    finally:
+                        self._layer_waiters.pop((f.root, index, q.key), None)
+                    if got is not None:
+                        slices[index] = got
+            layer = b"".join(h for k in sorted(slices) for h in slices[k])[:32 * f.num_pieces]
+            if not info.set_piece_layer(f.root, layer):
+                raise MetainfoError("fetched piece layer does not reduce to its pieces root")
+        log.with_field("files", len(info.v2_files)).debug("v2 piece layers complete")
+
     # ------------------------------------------------------------ extensions
     async def _on_extended(self, p: _Peer, pl: bytes) -> None:
         if not pl:
@@ -825,7 +914,7 @@ class Torrent:
         if len(self._meta) < n or any(k not in self._meta for k in range(n)):
             return
         raw = b"".join(self._meta[k] for k in range(n))[:self._meta_size]
-        if hashlib.sha1(raw).digest() != self.infohash:
+        if hashlib.sha1(raw).digest() != self.infohash and hashlib.sha256(raw).digest()[:20] != self.infohash:
             log.warn("received metadata does not match info-hash; retrying")
             self._meta.clear()
             for p in self.peers.values():

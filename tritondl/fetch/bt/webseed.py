@@ -155,6 +155,8 @@ class WebSeed:
             if ok:
                 self.pieces_ok += 1
                 self.bytes += len(data)
+            elif ok is None:
+                await asyncio.sleep(0.2)     # v2 piece layer not known yet: not the seed's fault
             else:
                 self.bad += 1
                 log.with_fields(webseed=self.url, piece=i).warn("web seed piece failed hash check")

@@ -176,3 +176,22 @@ def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: by
     if dev == "gpu":
         return gpu_hasher().verify_files(files, piece_len, expected, kind)
     return _host.verify_pieces(files, piece_len, expected, threads or effective_cpus(), kind)
+
+
+def verify_pieces_v2(files: Sequence[tuple[str, int]], piece_len: int, expected: bytes, widths: Sequence[int],
+                     reals: Sequence[int], known: Sequence[bool] | None = None, device: str = "cpu",
+                     threads: int = 0) -> bytes:
+    """BitTorrent v2 (BEP 52) verification of a piece-aligned layout: piece p's
+    16 KiB-leaf merkle root (``widths[p]`` leaves, ``reals[p]`` data bytes)
+    must equal ``expected[32p:32p+32]``.  Host: threaded read+hash+reduce per
+    piece.  GPU: the HIP kernel hashes every 16 KiB leaf of the layout (the
+    lane-parallel case it is fastest at), the host reduces the small trees."""
+    dev = _resolve(device)
+    files = [(str(p), int(n)) for p, n in files]
+    n = len(widths)
+    kn = bytes(1 if k else 0 for k in (known if known is not None else [True] * n))
+    thr = threads or effective_cpus()
+    if dev == "gpu":
+        leaves, leaf_ok = gpu_hasher().digest_files(files, 16384, "sha256")
+        return _host.merkle_check(leaves, leaf_ok, piece_len, expected, list(widths), list(reals), kn, thr)
+    return _host.merkle_verify(files, piece_len, expected, list(widths), list(reals), kn, thr)
