@@ -26,10 +26,32 @@
 
 namespace tritondl_hash {
 
+// OpenSSL 3: sha256_md() & co. are legacy handles, and every
+// EVP_DigestInit_ex with one re-fetches the provider implementation through a
+// locked store — with many small digests on many threads (16 KiB merkle
+// leaves, 64 KiB aws-chunks) that lock serialised the workers (v2 verify ran
+// at 1/3 of SHA-256 speed on 16 threads).  Fetch each algorithm once.
+inline const EVP_MD* fetched_md(const char* name, const EVP_MD* legacy) {
+  const EVP_MD* m = EVP_MD_fetch(nullptr, name, nullptr);  // leaked on purpose: process lifetime
+  return m ? m : legacy;
+}
+inline const EVP_MD* sha256_md() {
+  static const EVP_MD* m = fetched_md("SHA256", EVP_sha256());
+  return m;
+}
+inline const EVP_MD* sha1_md() {
+  static const EVP_MD* m = fetched_md("SHA1", EVP_sha1());
+  return m;
+}
+inline const EVP_MD* md5_md() {
+  static const EVP_MD* m = fetched_md("MD5", EVP_md5());
+  return m;
+}
+
 inline const EVP_MD* md_for(const std::string& kind) {
-  if (kind == "sha1") return EVP_sha1();
-  if (kind == "sha256") return EVP_sha256();
-  if (kind == "md5") return EVP_md5();
+  if (kind == "sha1") return sha1_md();
+  if (kind == "sha256") return sha256_md();
+  if (kind == "md5") return md5_md();
   throw std::invalid_argument("unknown hash kind: " + kind);
 }
 
@@ -208,7 +230,7 @@ inline std::vector<std::string> chunk_hashes(const char* data, size_t len, size_
   parallel_for(n, used, [&](size_t i) {
     const size_t off = i * chunk_size;
     const size_t m = off < len ? std::min(chunk_size, len - off) : 0;
-    h[i] = hex(one_shot(EVP_sha256(), m ? data + off : "", m));
+    h[i] = hex(one_shot(sha256_md(), m ? data + off : "", m));
   });
   return h;
 }
@@ -219,7 +241,7 @@ inline std::vector<std::string> chunk_signatures(const std::string& key, const s
                                                  bool include_final, int threads = 1) {
   if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
   const std::vector<std::string> h = chunk_hashes(data, len, chunk_size, include_final, threads);
-  const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
   const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
   std::vector<std::string> sigs;
   sigs.reserve(h.size());
@@ -271,7 +293,7 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
   parallel_for(n, used, [&](size_t i) {
     const size_t m = i < nfull ? std::min(chunk_size, len - i * chunk_size) : 0;
     const char* p = m ? data + i * chunk_size : "";
-    h[i] = hex(one_shot(EVP_sha256(), p, m));
+    h[i] = hex(one_shot(sha256_md(), p, m));
     char hx[32];
     const int hl = std::snprintf(hx, sizeof hx, "%zx", m);
     char* w = dst + frame[i];
@@ -286,7 +308,7 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
     *w++ = '\r';
     *w++ = '\n';
   });
-  const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
   const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
   for (size_t i = 0; i < n; ++i) {
     prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + h[i]));
@@ -340,10 +362,10 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
   for (size_t i = 0; i < frames.size(); ++i) dst_off[i + 1] = dst_off[i] + frames[i].n;
   parallel_for(frames.size(), used, [&](size_t i) {
     const Frame& f = frames[i];
-    h[i] = hex(one_shot(EVP_sha256(), f.n ? raw + f.off : "", f.n));
+    h[i] = hex(one_shot(sha256_md(), f.n ? raw + f.off : "", f.n));
     if (decoded && f.n) std::memcpy(&(*decoded)[dst_off[i]], raw + f.off, f.n);
   });
-  const std::string empty_hash = hex(one_shot(EVP_sha256(), "", 0));
+  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
   const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
   std::string prev = seed;
   for (size_t i = 0; i < frames.size(); ++i) {
@@ -364,7 +386,7 @@ constexpr size_t kMerkleLeaf = 16384;
 
 inline void merkle_reduce(std::vector<unsigned char>& row, size_t width) {
   // row holds `width` 32-byte nodes; reduce in place to row[0..32)
-  const EVP_MD* md = EVP_sha256();
+  const EVP_MD* md = sha256_md();
   MdCtx ctx(md);
   while (width > 1) {
     for (size_t k = 0; k < width / 2; ++k) {
@@ -430,7 +452,7 @@ inline std::string merkle_verify(const std::vector<std::pair<std::string, long l
   for (size_t i = 0; i < spans.size(); ++i)
     if (!spans[i].path.empty()) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
   std::string ok(n, '\0');
-  const EVP_MD* md = EVP_sha256();
+  const EVP_MD* md = sha256_md();
   parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
     if (!known[p] || reals[p] < 0 || static_cast<size_t>(reals[p]) > piece_len) return;
     const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);

@@ -236,3 +236,20 @@ def test_v2_resume_verifies_existing_data(tmp_path):
         await seed.stop()
         await o.stop()
     run(main())
+
+
+def test_gpu_leaf_path_logic_emulated_on_host(tmp_path, monkeypatch):
+    """The GPU path hashes whole 16 KiB blocks of the padded stream and then
+    re-hashes each file's short last leaf on the host; emulate the kernel
+    with the host piece hasher to pin that logic without a device."""
+    info, layout = _v2_layout(tmp_path, piece_len=65536)
+    exp, widths, reals, known = info.v2_expectations()
+
+    class FakeGpu:
+        def digest_files(self, files, pl, kind):
+            blob = b"".join(bytes(n) if not p else open(p, "rb").read() for p, n in files)
+            return hashing._host.piece_hashes(kind, blob, pl, 2), b"\x01" * (-(-len(blob) // pl))
+    monkeypatch.setattr(hashing, "gpu_hasher", lambda *a, **k: FakeGpu())
+    monkeypatch.setattr(hashing, "_resolve", lambda d: d)
+    ok = hashing.verify_pieces_v2(layout, info.piece_length, exp, widths, reals, known, device="gpu")
+    assert ok == b"\x01" * info.num_pieces

@@ -97,6 +97,25 @@ def main() -> int:
                 t = timeit(lambda: hashing.verify_pieces(files, pl, exp, device="gpu"), 2)
                 r = {"case": "gpu_verify", "piece_kb": 1024, "GBps": per * 4 / t / 1e9, "ms": t * 1e3}
                 print(json.dumps(r), flush=True)
+            # BitTorrent v2 (BEP 52): per-piece merkle roots over 16 KiB leaves
+            from tritondl.fetch.bt.metainfo import make_info
+            info = make_info(td, 1 << 20, version=2)
+            layout = info.file_paths(os.path.dirname(td))
+            exp2, widths, reals, known = info.v2_expectations()
+            nbytes = info.total_length
+            cpu = hashing.verify_pieces_v2(layout, info.piece_length, exp2, widths, reals, known, device="cpu")
+            assert all(cpu), "cpu v2 verify mismatch"
+            t = timeit(lambda: hashing.verify_pieces_v2(layout, info.piece_length, exp2, widths, reals, known,
+                                                        device="cpu"), 2)
+            print(json.dumps({"case": "cpu_verify_v2", "piece_kb": 1024, "GBps": nbytes / t / 1e9, "ms": t * 1e3,
+                              "threads": hashing.effective_cpus()}), flush=True)
+            if have_gpu:
+                ok = hashing.verify_pieces_v2(layout, info.piece_length, exp2, widths, reals, known, device="gpu")
+                assert ok == cpu, "gpu v2 verify mismatch"
+                t = timeit(lambda: hashing.verify_pieces_v2(layout, info.piece_length, exp2, widths, reals, known,
+                                                            device="gpu"), 2)
+                print(json.dumps({"case": "gpu_verify_v2", "piece_kb": 1024, "GBps": nbytes / t / 1e9,
+                                  "ms": t * 1e3}), flush=True)
     return 0
 
 

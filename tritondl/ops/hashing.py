@@ -193,5 +193,47 @@ def verify_pieces_v2(files: Sequence[tuple[str, int]], piece_len: int, expected:
     thr = threads or effective_cpus()
     if dev == "gpu":
         leaves, leaf_ok = gpu_hasher().digest_files(files, 16384, "sha256")
-        return _host.merkle_check(leaves, leaf_ok, piece_len, expected, list(widths), list(reals), kn, thr)
+        leaves, leaf_ok = bytearray(leaves), bytearray(leaf_ok)
+        # the kernel hashed whole 16 KiB blocks of the padded stream; a file's
+        # short last leaf must hash only its real bytes: redo those (<= one per file)
+        per = piece_len // 16384
+        for p in range(n):
+            tail = reals[p] % 16384
+            if not kn[p] or not tail:
+                continue
+            k = p * per + reals[p] // 16384
+            data = _read_layout(files, p * piece_len + reals[p] - tail, tail)
+            if data is None:
+                leaf_ok[k] = 0
+            else:
+                leaves[32 * k:32 * k + 32] = _host.digest("sha256", data)
+        return _host.merkle_check(bytes(leaves), bytes(leaf_ok), piece_len, expected, list(widths), list(reals),
+                                  kn, thr)
     return _host.merkle_verify(files, piece_len, expected, list(widths), list(reals), kn, thr)
+
+
+def _read_layout(files: Sequence[tuple[str, int]], off: int, n: int) -> bytes | None:
+    """``n`` bytes at stream offset ``off`` of a file layout ("" = zeros)."""
+    out = bytearray()
+    pos = 0
+    for path, ln in files:
+        a, b = max(off, pos), min(off + n, pos + ln)
+        if a < b:
+            if not path:
+                out += bytes(b - a)
+            else:
+                try:
+                    fd = os.open(path, os.O_RDONLY)
+                except OSError:
+                    return None
+                try:
+                    chunk = os.pread(fd, b - a, a - pos)
+                finally:
+                    os.close(fd)
+                if len(chunk) != b - a:
+                    return None
+                out += chunk
+        pos += ln
+        if pos >= off + n:
+            break
+    return bytes(out) if len(out) == n else None
