@@ -549,16 +549,25 @@ class GpuHasher {
 
   // Read [off, off+len) (piece-aligned) of the concatenated layout into dst;
   // complete[k] is cleared for every piece k of this range not fully read.
+  // Work is split into units of >= 1 MiB (whole pieces), so 16 KiB "pieces"
+  // (v2 merkle leaves) still read with large preads.
   void read_spans(const std::vector<Span>& spans, uint8_t* dst, size_t off, size_t len, size_t piece_len,
                   char* complete) {
     const size_t np = (len + piece_len - 1) / piece_len;
+    const size_t per_unit = std::max<size_t>(1, (1u << 20) / piece_len);
+    const size_t nu = (np + per_unit - 1) / per_unit;
     std::atomic<size_t> next{0};
+    auto fail_range = [&](long long a, long long e) {  // stream offsets -> pieces of this window
+      if (e <= a) return;
+      const size_t k0 = static_cast<size_t>(a - static_cast<long long>(off)) / piece_len;
+      const size_t k1 = (static_cast<size_t>(e - static_cast<long long>(off)) + piece_len - 1) / piece_len;
+      for (size_t k = k0; k < std::min(k1, np); ++k) complete[k] = 0;
+    };
     auto work = [&] {
-      for (size_t k; (k = next.fetch_add(1)) < np;) {
-        const size_t a = k * piece_len, e = std::min(len, a + piece_len);
+      for (size_t u; (u = next.fetch_add(1)) < nu;) {
+        const size_t a = u * per_unit * piece_len, e = std::min(len, a + per_unit * piece_len);
         const long long ga = static_cast<long long>(off + a), ge = static_cast<long long>(off + e);
         long long cur = ga;
-        bool good = true;
         for (const Span& s : spans) {
           if (s.start + s.length <= cur || s.start >= ge) continue;
           const long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
@@ -572,17 +581,17 @@ class GpuHasher {
             got = pread_full(s.fd, p, want, static_cast<off_t>(ra - s.start));
           }
           if (got != want) {
-            good = false;
             std::memset(p + got, 0, want - got);
+            fail_range(ra + static_cast<long long>(got), re);
           }
           cur = re;
           if (cur >= ge) break;
         }
-        if (cur < ge || !good) complete[k] = 0;  // each piece is owned by one worker: no race
+        fail_range(cur, ge);  // a gap nobody covers: incomplete (units own disjoint pieces: no race)
       }
     };
     std::vector<std::thread> ts;
-    const int t = static_cast<int>(std::min<size_t>(readers_, np));
+    const int t = static_cast<int>(std::min<size_t>(readers_, nu));
     for (int k = 1; k < t; ++k) ts.emplace_back(work);
     work();
     for (auto& th : ts) th.join();
