@@ -285,3 +285,34 @@ def test_client_publish_retries_after_nack():
         await cl.close()
         await b.stop()
     run(main())
+
+
+def test_client_resubscribes_after_server_cancel():
+    """A queue deleted under a consumer (or a failover) makes the broker send
+    basic.cancel; the client re-declares the shard queue and consumes again."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        stream = await cl.consume("v1.download")
+        admin = await Connection.open(b.url, heartbeat=0)
+        ach = await admin.channel()
+        await ach.queue_delete("v1.download-1")
+        for _ in range(100):
+            q = b.queues.get("v1.download-1")
+            if q is not None and q.consumers:
+                break
+            await asyncio.sleep(0.02)
+        assert b.queues["v1.download-1"].consumers          # resubscribed
+        await cl.publish("v1.download", b"a")               # -> v1.download-0
+        await cl.publish("v1.download", b"b")               # -> v1.download-1 (the re-created queue)
+        got = []
+        async for d in stream:
+            got.append(d.body)
+            await d.ack()
+            if len(got) == 2:
+                break
+        assert sorted(got) == [b"a", b"b"]
+        await admin.close()
+        await cl.close()
+        await b.stop()
+    run(main())

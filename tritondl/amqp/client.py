@@ -156,6 +156,7 @@ class Client:
         self._declared_pub: set[str] = set()
         self._consumer_chans: list[Channel] = []
         self._closing = False
+        self._bg: set[asyncio.Task] = set()
         self._connected = asyncio.Event()
         self._supervisor: asyncio.Task | None = None
         self._lost = asyncio.Event()
@@ -280,8 +281,30 @@ class Client:
                     return
                 self._out.put_nowait(Delivery(self, m, _gen))
 
+            def on_cancel(tag: str, _ch=ch, _q=q, _cb=on_msg, _gen=gen) -> None:
+                # server-side cancel (queue deleted, node failover): re-declare and re-subscribe
+                log.with_fields(queue=_q, consumer_tag=tag).warn("consumer cancelled by broker; resubscribing")
+                t = asyncio.ensure_future(self._resubscribe(topic, _ch, _q, _cb, _gen))
+                self._bg.add(t)
+                t.add_done_callback(self._bg.discard)
+
+            ch.on_cancel = on_cancel
             await ch.basic_consume(q, on_msg, no_ack=False)
             log.info("worker on queue '%s' started", q)
+
+    async def _resubscribe(self, topic: str, ch: Channel, q: str, cb, gen: int) -> None:
+        pol = ExponentialBackoff(initial=0.05, max_interval=5.0, max_elapsed=None)
+        while not self._closing and gen == self.generation and not ch.is_closed:
+            try:
+                await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
+                await ch.queue_bind(q, topic, q)
+                await ch.basic_consume(q, cb, no_ack=False)
+                log.info("worker on queue '%s' resubscribed", q)
+                return
+            except AMQPError as e:
+                d = pol.next_delay() or 1.0
+                log.with_fields(queue=q, error=str(e)).warn("resubscribe failed; retrying in %.2fs", d)
+                await asyncio.sleep(d)
 
     async def _iter(self) -> AsyncIterator[Delivery]:
         while True:
@@ -369,6 +392,10 @@ class Client:
             self._supervisor.cancel()
             with contextlib.suppress(BaseException):
                 await self._supervisor
+        for t in list(self._bg):
+            t.cancel()
+            with contextlib.suppress(BaseException):
+                await t
         if self.conn is not None:
             for ch in self._consumer_chans:
                 with contextlib.suppress(Exception):
