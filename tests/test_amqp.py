@@ -316,3 +316,32 @@ def test_client_resubscribes_after_server_cancel():
         await cl.close()
         await b.stop()
     run(main())
+
+
+def test_client_reopens_consumer_channel_closed_by_broker():
+    """A 406 (unknown delivery tag) closes a consumer channel on the broker;
+    the client opens a new one and keeps consuming that shard."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        stream = await cl.consume("v1.download")
+        victim = cl._consumer_chans[0]
+        victim.conn._send_method(victim.id, Method("basic.ack", {"delivery_tag": 9999, "multiple": False}))
+        for _ in range(100):
+            if victim.is_closed and len(b.queues["v1.download-0"].consumers) == 1 and \
+                    len(cl._consumer_chans) == 2:
+                break
+            await asyncio.sleep(0.02)
+        assert victim.is_closed and len(cl._consumer_chans) == 2
+        for i in range(4):
+            await cl.publish("v1.download", f"m{i}".encode())
+        got = []
+        async for d in stream:
+            got.append(d.body)
+            await d.ack()
+            if len(got) == 4:
+                break
+        assert sorted(got) == [b"m0", b"m1", b"m2", b"m3"]
+        await cl.close()
+        await b.stop()
+    run(main())

@@ -272,25 +272,58 @@ class Client:
     async def _start_consumers(self, topic: str) -> None:
         gen = self.generation
         for i in range(self.num_shard_queues):
-            q = self.get_rk(topic, i)
-            ch = await self._channel(qos=True)
-            self._consumer_chans.append(ch)
+            await self._start_shard(topic, self.get_rk(topic, i), gen)
 
-            def on_msg(m: Message, _gen=gen) -> None:
-                if m.body is None:  # reference skips nil bodies (client.go:262)
-                    return
-                self._out.put_nowait(Delivery(self, m, _gen))
+    async def _start_shard(self, topic: str, q: str, gen: int, redeclare: bool = False) -> None:
+        """One consumer channel for shard queue ``q``.  It heals itself: a
+        server-side ``basic.cancel`` (queue deleted, failover) re-declares and
+        re-subscribes on the same channel; an unexpected ``channel.close``
+        (e.g. 406 on a late ack) reopens a channel — while the connection
+        lives; connection loss is the supervisor's job."""
+        ch = await self._channel(qos=True)
+        self._consumer_chans.append(ch)
 
-            def on_cancel(tag: str, _ch=ch, _q=q, _cb=on_msg, _gen=gen) -> None:
-                # server-side cancel (queue deleted, node failover): re-declare and re-subscribe
-                log.with_fields(queue=_q, consumer_tag=tag).warn("consumer cancelled by broker; resubscribing")
-                t = asyncio.ensure_future(self._resubscribe(topic, _ch, _q, _cb, _gen))
-                self._bg.add(t)
-                t.add_done_callback(self._bg.discard)
+        def on_msg(m: Message) -> None:
+            if m.body is None:  # reference skips nil bodies (client.go:262)
+                return
+            self._out.put_nowait(Delivery(self, m, gen))
 
-            ch.on_cancel = on_cancel
-            await ch.basic_consume(q, on_msg, no_ack=False)
-            log.info("worker on queue '%s' started", q)
+        def on_cancel(tag: str) -> None:
+            log.with_fields(queue=q, consumer_tag=tag).warn("consumer cancelled by broker; resubscribing")
+            self._spawn_bg(self._resubscribe(topic, ch, q, on_msg, gen))
+
+        def on_close(exc) -> None:
+            if ch in self._consumer_chans:
+                self._consumer_chans.remove(ch)
+            if self._closing or gen != self.generation or getattr(exc, "code", 0) == 200 or \
+                    self.conn is None or self.conn.is_closed or isinstance(exc, ConnectionClosed):
+                return
+            log.with_fields(queue=q, error=str(exc)).warn("consumer channel closed by broker; reopening")
+            self._spawn_bg(self._reopen_shard(topic, q, gen))
+
+        ch.on_cancel = on_cancel
+        ch.add_close_callback(on_close)
+        if redeclare:
+            await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
+            await ch.queue_bind(q, topic, q)
+        await ch.basic_consume(q, on_msg, no_ack=False)
+        log.info("worker on queue '%s' started", q)
+
+    def _spawn_bg(self, coro) -> None:
+        t = asyncio.ensure_future(coro)
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _reopen_shard(self, topic: str, q: str, gen: int) -> None:
+        pol = ExponentialBackoff(initial=0.05, max_interval=5.0, max_elapsed=None)
+        while not self._closing and gen == self.generation and self.conn is not None and not self.conn.is_closed:
+            try:
+                await self._start_shard(topic, q, gen, redeclare=True)
+                return
+            except AMQPError as e:
+                d = pol.next_delay() or 1.0
+                log.with_fields(queue=q, error=str(e)).warn("reopening consumer failed; retrying in %.2fs", d)
+                await asyncio.sleep(d)
 
     async def _resubscribe(self, topic: str, ch: Channel, q: str, cb, gen: int) -> None:
         pol = ExponentialBackoff(initial=0.05, max_interval=5.0, max_elapsed=None)
