@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Resume benchmark: a redelivered torrent job whose data is already on disk
+(the worker crashed after downloading, before the ack — SURVEY.md §5.4).
+The production ``TorrentDownloader`` opens the job from a ``.torrent``,
+batch-verifies the existing files and completes with nothing left to fetch;
+the job time is almost entirely verification, so this is where the HIP
+kernels sit on the service path.
+
+    python tools/bench_resume.py --gb 4 --version 2 --device gpu|cpu|auto
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+async def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gb", type=float, default=4.0)
+    ap.add_argument("--files", type=int, default=4)
+    ap.add_argument("--piece-kb", type=int, default=1024)
+    ap.add_argument("--version", type=int, default=2, choices=[1, 2, 3])
+    ap.add_argument("--device", nargs="*", default=["cpu", "gpu"])
+    a = ap.parse_args()
+    import numpy as np
+
+    from tritondl.fakes.origin import Origin
+    from tritondl.fakes.swarm import torrent_file_bytes
+    from tritondl.fetch.bt.client import TorrentDownloader
+    from tritondl.fetch.bt.metainfo import make_info
+    from tritondl.fetch.bt.torrent import TorrentConfig
+    from tritondl.ops import hashing
+    from tritondl.utils.log import log
+    log.configure("warning", "")
+    td = tempfile.mkdtemp(prefix="tdl-resume-", dir=os.environ.get("TMPDIR", "/tmp"))
+    o = None
+    try:
+        root = os.path.join(td, "job", "Season")
+        os.makedirs(root)
+        total = int(a.gb * (1 << 30))
+        per = total // a.files
+        rng = np.random.default_rng(3)
+        for k in range(a.files):
+            rng.integers(0, 256, per, dtype=np.uint8).tofile(os.path.join(root, f"e{k:02d}.mkv"))
+        t0 = time.perf_counter()
+        info = make_info(root, a.piece_kb << 10, version=a.version)
+        t_make = time.perf_counter() - t0
+        o = await Origin().start()
+        url = o.add("/job.torrent", torrent_file_bytes(info))
+        for dev in a.device:
+            if dev == "gpu" and not hashing.gpu_available():
+                continue
+            # a fresh job dir each run sees the same files but no completion DB
+            db = os.path.join(td, "job", ".torrent.db")
+            for suffix in ("", "-wal", "-shm"):
+                if os.path.exists(db + suffix):
+                    os.remove(db + suffix)
+            d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device=dev), use_dht=False,
+                                  progress_interval=1.0)
+            t0 = time.perf_counter()
+            await d.download(os.path.join(td, "job"), lambda u, p: None, url)
+            dt = time.perf_counter() - t0
+            print(json.dumps({"metric": "resume_job_seconds", "device": dev, "value": round(dt, 3),
+                              "GBps": round(info.total_length / dt / 1e9, 1), "bytes": info.total_length,
+                              "pieces": info.num_pieces, "torrent_version": a.version,
+                              "make_torrent_s": round(t_make, 2)}), flush=True)
+    finally:
+        if o is not None:
+            await o.stop()
+        shutil.rmtree(td, ignore_errors=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(asyncio.run(main()))
