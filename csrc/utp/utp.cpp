@@ -108,13 +108,12 @@ class Pump {
       for (int k = 0; k < n; ++k) {
         const char* d = bufs_.data() + k * kBufSize;
         size_t len = msgs[k].msg_len;
-        auto addr = format_addr(from[k]);
         bool utp = len >= 1 && (static_cast<uint8_t>(d[0]) & 0x0F) == 1 && (static_cast<uint8_t>(d[0]) >> 4) <= 4;
         if (!utp || len < tritondl_utp::kHeader) {
-          others.emplace_back(std::string(d, len), addr);
+          others.emplace_back(std::string(d, len), format_addr(from[k]));
           continue;
         }
-        e_.incoming(std::string(d, len), addr.first + ":" + std::to_string(addr.second), now);
+        e_.incoming(d, len, addr_key(from[k]), now);  // zero-copy into the engine
       }
       got_total += n;
       if (n < kBatch) break;
@@ -128,7 +127,7 @@ class Pump {
 
   // Ship queued packets; returns how many are still queued (socket full).
   size_t send() {
-    for (auto& kv : e_.outgoing()) q_.emplace_back(std::move(kv));
+    for (auto& d : e_.take_datagrams()) q_.push_back(std::move(d));
     while (!q_.empty()) {
       int n = static_cast<int>(std::min<size_t>(kBatch, q_.size()));
       mmsghdr msgs[kBatch];
@@ -136,9 +135,9 @@ class Pump {
       SockAddr to[kBatch];
       int m = 0;
       for (int k = 0; k < n; ++k) {
-        auto& pkt = q_[k];
-        if (!lookup(pkt.first, &to[m])) continue;  // unparseable address: dropped below
-        iov[m] = {const_cast<char*>(pkt.second.data()), pkt.second.size()};
+        auto& dg = q_[k];
+        if (!lookup(*dg.addr, &to[m])) continue;  // unparseable address: dropped below
+        iov[m] = {const_cast<char*>(dg.pkt->data()), dg.pkt->size()};
         std::memset(&msgs[m].msg_hdr, 0, sizeof(msghdr));
         msgs[m].msg_hdr.msg_iov = &iov[m];
         msgs[m].msg_hdr.msg_iovlen = 1;
@@ -159,7 +158,7 @@ class Pump {
       int consumed = 0, sendable = 0;
       while (consumed < n && sendable < sent) {
         SockAddr tmp;
-        if (lookup(q_[consumed].first, &tmp)) ++sendable;
+        if (lookup(*q_[consumed].addr, &tmp)) ++sendable;
         ++consumed;
       }
       q_.erase(q_.begin(), q_.begin() + consumed);
@@ -188,8 +187,29 @@ class Pump {
   Engine& e_;
   int fd_;
   std::vector<char> bufs_;
-  std::deque<std::pair<std::string, std::string>> q_;
+  // "ip:port" engine key of a peer sockaddr, memoised (IPv4: keyed by addr+port)
+  const std::string& addr_key(const sockaddr_storage& ss) {
+    uint64_t k = 0;
+    if (ss.ss_family == AF_INET) {
+      auto* v4 = reinterpret_cast<const sockaddr_in*>(&ss);
+      k = (static_cast<uint64_t>(v4->sin_addr.s_addr) << 16) | v4->sin_port;
+      auto it = keys_.find(k);
+      if (it != keys_.end()) return it->second;
+    }
+    auto a = format_addr(ss);
+    std::string key = a.first + ":" + std::to_string(a.second);
+    if (ss.ss_family != AF_INET) {
+      scratch_ = std::move(key);
+      return scratch_;
+    }
+    if (keys_.size() > 4096) keys_.clear();
+    return keys_.emplace(k, std::move(key)).first->second;
+  }
+
+  std::deque<tritondl_utp::Datagram> q_;
   std::unordered_map<std::string, SockAddr> cache_;
+  std::unordered_map<uint64_t, std::string> keys_;
+  std::string scratch_;
 };
 
 }  // namespace

@@ -69,6 +69,18 @@ struct ByteQueue {
     }
     buf.append(p, n);
   }
+  void take_into(std::string& dst, size_t n) {
+    n = std::min(n, size());
+    dst.append(buf, off, n);
+    off += n;
+    if (off == buf.size()) {
+      buf.clear();
+      off = 0;
+    } else if (off >= (1u << 20) && off * 2 >= buf.size()) {
+      buf.erase(0, off);
+      off = 0;
+    }
+  }
   std::string take(size_t n) {
     std::string r = buf.substr(off, n);
     off += r.size();
@@ -90,7 +102,8 @@ struct ByteQueue {
 struct OutPkt {
   uint16_t seq;
   uint8_t type;
-  std::string payload;
+  std::shared_ptr<const std::string> pkt;  // header + payload as last sent (shared with the send queue)
+  uint32_t psize = 0;                       // payload bytes
   int64_t sent_at = 0;
   int transmissions = 0;
   bool need_resend = false;
@@ -98,9 +111,17 @@ struct OutPkt {
   bool sacked = false;        // selectively acked: kept until the cumulative ack passes it
 };
 
+// One queued datagram: the peer address and packet bytes are shared (refcounted)
+// with the connection / retransmission queue, so queueing copies neither.
+struct Datagram {
+  std::shared_ptr<const std::string> addr;
+  std::shared_ptr<const std::string> pkt;
+};
+
 struct Conn {
   int id = 0;
   std::string addr;
+  std::shared_ptr<const std::string> addr_p;  // same, shared with queued datagrams
   int state = CS_SYN_SENT;
   bool accepted = false;
   uint16_t recv_id = 0, send_id = 0;
@@ -146,12 +167,13 @@ class Engine {
     auto c = std::make_unique<Conn>();
     c->id = next_id_++;
     c->addr = addr;
+    c->addr_p = std::make_shared<const std::string>(addr);
     c->recv_id = static_cast<uint16_t>(rng_());
     c->send_id = static_cast<uint16_t>(c->recv_id + 1);
     c->seq_nr = 1;
     c->state = CS_SYN_SENT;
     c->last_recv = now;
-    by_key_[key(addr, c->recv_id)] = c->id;
+    by_addr_[addr][c->recv_id] = c->id;
     Conn& r = *c;
     conns_[c->id] = std::move(c);
     send_control(r, ST_SYN, now, /*consume_seq=*/true);
@@ -159,8 +181,13 @@ class Engine {
   }
 
   int incoming(const std::string& pkt, const std::string& addr, int64_t now) {
-    if (pkt.size() < kHeader) return -1;
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(pkt.data());
+    return incoming(pkt.data(), pkt.size(), addr, now);
+  }
+
+  // Zero-copy form (the socket pump hands its receive buffers straight in).
+  int incoming(const char* data, size_t size, const std::string& addr, int64_t now) {
+    if (size < kHeader) return -1;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
     Header h{static_cast<uint8_t>(p[0] >> 4), static_cast<uint8_t>(p[0] & 0xF), p[1], get16(p + 2), get32(p + 4),
              get32(p + 8), get32(p + 12), get16(p + 16), get16(p + 18)};
     if (h.ver != 1 || h.type > ST_SYN) return -1;
@@ -169,21 +196,22 @@ class Engine {
     uint8_t ext = h.ext;
     std::string sack;
     while (ext != 0) {
-      if (off + 2 > pkt.size()) return -1;
+      if (off + 2 > size) return -1;
       uint8_t next = p[off], len = p[off + 1];
-      if (off + 2 + len > pkt.size()) return -1;
-      if (ext == 1) sack.assign(pkt.data() + off + 2, len);
+      if (off + 2 + len > size) return -1;
+      if (ext == 1) sack.assign(data + off + 2, len);
       ext = next;
       off += 2 + len;
     }
-    std::string payload = pkt.substr(off);
+    const char* payload = data + off;
+    const size_t payload_n = size - off;
 
     if (h.type == ST_SYN) {
       // new inbound connection (or a retransmitted SYN for one we know)
       uint16_t rid = static_cast<uint16_t>(h.conn_id + 1);
-      auto it = by_key_.find(key(addr, rid));
-      if (it != by_key_.end()) {
-        Conn& c = *conns_[it->second];
+      const int known = find_conn(addr, rid);
+      if (known > 0) {
+        Conn& c = *conns_[known];
         c.need_ack = true;  // our SYN-ACK was lost: answer again
         flush(c, now);
         return c.id;
@@ -191,6 +219,7 @@ class Engine {
       auto c = std::make_unique<Conn>();
       c->id = next_id_++;
       c->addr = addr;
+      c->addr_p = std::make_shared<const std::string>(addr);
       c->recv_id = rid;
       c->send_id = h.conn_id;
       c->seq_nr = static_cast<uint16_t>(rng_());
@@ -201,19 +230,19 @@ class Engine {
       c->last_recv = now;
       c->peer_wnd = h.wnd;
       c->reply_micro = static_cast<uint32_t>(now) - h.ts;
-      by_key_[key(addr, rid)] = c->id;
+      by_addr_[addr][rid] = c->id;
       Conn& r = *c;
       conns_[c->id] = std::move(c);
       accepted_.push_back(r.id);
       send_state(r, now);
       return r.id;
     }
-    auto it = by_key_.find(key(addr, h.conn_id));
-    if (it == by_key_.end()) {
+    const int cid = find_conn(addr, h.conn_id);
+    if (cid <= 0) {
       if (h.type != ST_RESET) send_reset(addr, h.conn_id, h.seq, now);
       return -1;
     }
-    Conn& c = *conns_[it->second];
+    Conn& c = *conns_[cid];
     c.last_recv = now;
     c.reply_micro = static_cast<uint32_t>(now) - h.ts;
     if (h.ts_diff != 0) update_delay(c, h.ts_diff, now);
@@ -237,7 +266,7 @@ class Engine {
         c.fin_received = true;
         c.fin_seq = h.seq;
       }
-      accept_data(c, h.seq, payload, h.type == ST_FIN);
+      accept_data(c, h.seq, payload, payload_n, h.type == ST_FIN);
     }
     if (batch_) {
       // defer: one flush (so one cumulative ACK + SACK) per connection per
@@ -328,7 +357,7 @@ class Engine {
     for (auto it = conns_.begin(); it != conns_.end();) {
       Conn& c = *it->second;
       if (c.state >= CS_CLOSED && c.inbuf.empty() && c.forget) {
-        by_key_.erase(key(c.addr, c.recv_id));
+        erase_conn(c.addr, c.recv_id);
         it = conns_.erase(it);
       } else {
         ++it;
@@ -341,8 +370,18 @@ class Engine {
     if (c) c->forget = true;
   }
 
+  // Copying form (Python API / tests): [(addr, packet)].
   std::vector<std::pair<std::string, std::string>> outgoing() {
     std::vector<std::pair<std::string, std::string>> v;
+    v.reserve(out_.size());
+    for (auto& d : out_) v.emplace_back(*d.addr, *d.pkt);
+    out_.clear();
+    return v;
+  }
+
+  // Zero-copy form for the socket pump.
+  std::vector<Datagram> take_datagrams() {
+    std::vector<Datagram> v;
     v.swap(out_);
     return v;
   }
@@ -401,7 +440,18 @@ class Engine {
   size_t size() const { return conns_.size(); }
 
  private:
-  static std::string key(const std::string& addr, uint16_t id) { return addr + "#" + std::to_string(id); }
+  int find_conn(const std::string& addr, uint16_t id) const {
+    auto a = by_addr_.find(addr);  // no key string is built per packet
+    if (a == by_addr_.end()) return -1;
+    auto b = a->second.find(id);
+    return b == a->second.end() ? -1 : b->second;
+  }
+  void erase_conn(const std::string& addr, uint16_t id) {
+    auto a = by_addr_.find(addr);
+    if (a == by_addr_.end()) return;
+    a->second.erase(id);
+    if (a->second.empty()) by_addr_.erase(a);
+  }
   Conn* get(int id) {
     auto it = conns_.find(id);
     return it == conns_.end() ? nullptr : it->second.get();
@@ -440,7 +490,8 @@ class Engine {
 
   void send_state(Conn& c, int64_t now) {
     std::string sack = build_sack(c);
-    out_.emplace_back(c.addr, header(c, ST_STATE, c.seq_nr, now, sack.empty() ? nullptr : &sack));
+    out_.push_back({c.addr_p, std::make_shared<const std::string>(
+                                 header(c, ST_STATE, c.seq_nr, now, sack.empty() ? nullptr : &sack))});
     c.need_ack = false;
   }
 
@@ -450,7 +501,8 @@ class Engine {
     o.type = type;
     o.sent_at = now;
     o.transmissions = 1;
-    out_.emplace_back(c.addr, header(c, type, o.seq, now, nullptr));
+    o.pkt = std::make_shared<const std::string>(header(c, type, o.seq, now, nullptr));
+    out_.push_back({c.addr_p, o.pkt});
     if (consume_seq) {
       c.seq_nr++;
       c.inflight.push_back(std::move(o));
@@ -467,7 +519,7 @@ class Engine {
     put32(s, 0);
     put16(s, static_cast<uint16_t>(rng_()));
     put16(s, ack);
-    out_.emplace_back(addr, s);
+    out_.push_back({std::make_shared<const std::string>(addr), std::make_shared<const std::string>(std::move(s))});
   }
 
   void update_delay(Conn& c, uint32_t sample, int64_t now) {
@@ -495,8 +547,8 @@ class Engine {
         if (min_rtt_sample < 0 || sample < min_rtt_sample) min_rtt_sample = sample;
       }
       if (!o.sacked) {
-        acked_bytes += static_cast<uint32_t>(o.payload.size());
-        c.cur_window -= std::min<uint32_t>(c.cur_window, static_cast<uint32_t>(o.payload.size()));
+        acked_bytes += static_cast<uint32_t>(o.psize);
+        c.cur_window -= std::min<uint32_t>(c.cur_window, static_cast<uint32_t>(o.psize));
       }
       if (o.type == ST_FIN) c.fin_acked = true;
       c.inflight.pop_front();
@@ -509,8 +561,8 @@ class Engine {
         uint16_t d = seq_diff(o.seq, static_cast<uint16_t>(ack + 2));
         if (!o.sacked && d < sack.size() * 8 && ((static_cast<uint8_t>(sack[d >> 3]) >> (d & 7)) & 1)) {
           o.sacked = true;
-          acked_bytes += static_cast<uint32_t>(o.payload.size());
-          c.cur_window -= std::min<uint32_t>(c.cur_window, static_cast<uint32_t>(o.payload.size()));
+          acked_bytes += static_cast<uint32_t>(o.psize);
+          c.cur_window -= std::min<uint32_t>(c.cur_window, static_cast<uint32_t>(o.psize));
         }
       }
       int after = 0;
@@ -570,20 +622,21 @@ class Engine {
     }
   }
 
-  void accept_data(Conn& c, uint16_t seq, const std::string& payload, bool fin) {
+  void accept_data(Conn& c, uint16_t seq, const char* payload, size_t payload_n, bool fin) {
     uint16_t expect = static_cast<uint16_t>(c.ack_nr + 1);
     if (seq_lt(seq, expect)) {  // duplicate: re-ack
       c.need_ack = true;
       return;
     }
     if (seq != expect) {
-      if (seq_diff(seq, expect) < 1024 && !c.ooo.count(seq)) c.ooo[seq] = fin ? std::string() : payload;
+      if (seq_diff(seq, expect) < 1024 && !c.ooo.count(seq))
+        c.ooo[seq] = fin ? std::string() : std::string(payload, payload_n);
       c.need_ack = true;
       return;
     }
     if (!fin) {
-      c.inbuf += payload;
-      c.bytes_recv += payload.size();
+      c.inbuf.append(payload, payload_n);
+      c.bytes_recv += payload_n;
     }
     c.ack_nr = seq;
     // pull in buffered successors
@@ -613,9 +666,11 @@ class Engine {
       o.sent_at = now;
       o.transmissions++;
       c.retransmits++;
-      std::string pkt = header(c, o.type, o.seq, now, nullptr);
-      pkt += o.payload;
-      out_.emplace_back(c.addr, std::move(pkt));
+      // fresh header (timestamps, ack) in front of the same payload
+      auto np = std::make_shared<std::string>(header(c, o.type, o.seq, now, nullptr));
+      if (o.pkt && o.pkt->size() > kHeader) np->append(*o.pkt, kHeader, std::string::npos);
+      o.pkt = np;
+      out_.push_back({c.addr_p, o.pkt});
       c.need_ack = false;
     }
     // 2) new data within min(cwnd, peer window)
@@ -627,12 +682,13 @@ class Engine {
         OutPkt o;
         o.seq = c.seq_nr++;
         o.type = ST_DATA;
-        o.payload = c.pending.take(n);
+        o.psize = static_cast<uint32_t>(n);
         o.sent_at = now;
         o.transmissions = 1;
-        std::string pkt = header(c, ST_DATA, o.seq, now, nullptr);
-        pkt += o.payload;
-        out_.emplace_back(c.addr, std::move(pkt));
+        auto pk = std::make_shared<std::string>(header(c, ST_DATA, o.seq, now, nullptr));
+        c.pending.take_into(*pk, n);  // one copy: send buffer -> packet
+        o.pkt = pk;
+        out_.push_back({c.addr_p, o.pkt});
         c.cur_window += static_cast<uint32_t>(n);
         c.bytes_sent += n;
         c.inflight.push_back(std::move(o));
@@ -650,8 +706,8 @@ class Engine {
   std::mt19937_64 rng_;
   int next_id_ = 1;
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
-  std::unordered_map<std::string, int> by_key_;
-  std::vector<std::pair<std::string, std::string>> out_;
+  std::unordered_map<std::string, std::unordered_map<uint16_t, int>> by_addr_;
+  std::vector<Datagram> out_;
   std::vector<int> accepted_;
   bool batch_ = false;
   std::vector<int> touched_;

@@ -154,6 +154,10 @@ class Torrent:
         self.open_pieces: dict[int, _Piece] = {}        # subset of pieces with blocks left to hand out
         self.verifying: set[int] = set()                # complete pieces being hashed/written
         self._layer_waiters: dict = {}                  # (root, index, peer) -> future of a v2 hashes reply
+        self._rare: list[int] | None = None             # missing pieces by availability (picker order)
+        self._rare_pos = 0
+        self._rare_t = 0.0
+        self._rare_dirty = True
         self._finishers: set[asyncio.Task] = set()
         self.peers: dict[tuple[str, int], _Peer] = {}
         self.known: set[tuple[str, int]] = set()
@@ -460,6 +464,7 @@ class Torrent:
             for i in range(len(p.have)):
                 if p.have[i] and i < len(self.avail):
                     self.avail[i] -= 1
+                    self._rare_dirty = True
         self._release(p)
         # top up from known addresses
         for a in list(self.known - set(self.peers) - self.connecting - self.banned)[:4]:
@@ -550,6 +555,7 @@ class Torrent:
         for i in idxs:
             if p.set_have(i):
                 self.avail[i] += 1
+                self._rare_dirty = True
         self._update_interest(p)
         self._fill(p)
 
@@ -566,6 +572,16 @@ class Torrent:
             p.wire.send(pw.INTERESTED if want else pw.NOT_INTERESTED)
 
     # ------------------------------------------------------------ requests
+    def _rarest_order(self) -> list[int]:
+        now = time.monotonic()
+        if self._rare is None or (self._rare_dirty and now - self._rare_t > 0.25) or \
+                self._rare_pos >= len(self._rare):
+            idx = [i for i in range(len(self.have)) if not self.have[i]]
+            random.shuffle(idx)
+            idx.sort(key=self.avail.__getitem__)
+            self._rare, self._rare_t, self._rare_dirty, self._rare_pos = idx, now, False, 0
+        return self._rare
+
     def _pick(self, p: _Peer) -> tuple[int, int, int] | None:
         """Next (piece, offset, length) to request from p; None if nothing."""
         assert self.info is not None
@@ -582,17 +598,22 @@ class Torrent:
         finally:
             for i in exhausted:
                 del self.open_pieces[i]
-        # 2) start the rarest piece this peer has (random tie-break)
-        best, best_av = None, math.inf
-        n = self.info.num_pieces
-        start = random.randrange(n) if n else 0
-        for k in range(n):
-            i = (start + k) % n
-            if p.have[i] and not self.have[i] and i not in self.pieces and self.avail[i] < best_av \
-                    and i not in self.verifying and i not in self.ws_busy:
-                best, best_av = i, self.avail[i]
-                if best_av <= 1:
-                    break
+        # 2) start the rarest piece this peer has (random tie-break), from an
+        #    availability-ordered list refreshed at most every 0.25 s — a full
+        #    scan per new piece was O(pieces^2) over a download
+        best = None
+        order = self._rarest_order()
+        pos = self._rare_pos
+        while pos < len(order) and (self.have[order[pos]] or order[pos] in self.pieces
+                                    or order[pos] in self.verifying):
+            pos += 1                       # taken for good (until the next refresh)
+        self._rare_pos = pos
+        for k in range(pos, len(order)):
+            i = order[k]
+            if p.have[i] and not self.have[i] and i not in self.pieces and i not in self.verifying \
+                    and i not in self.ws_busy:
+                best = i
+                break
         if best is not None:
             size = self.info.piece_size(best)
             pc = _Piece(size, -(-size // BLOCK), bytearray(size))
