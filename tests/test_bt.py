@@ -400,3 +400,19 @@ def test_bep47_padding_files_swarm_resume_and_webseed(tmp_path):
         _check_tree(str(src), str(dst2))
         await o.stop()
     run(main())
+
+
+def test_large_torrent_file_over_http_is_read_whole(tmp_path):
+    """A .torrent bigger than one socket read (v2 piece layers, many files)
+    must be read to EOF, not truncated at the first chunk."""
+    async def main():
+        o = await Origin().start()
+        o.rate = 2_000_000          # trickle so the body arrives in many reads
+        pad = bencode.encode({b"info": {b"name": b"x", b"piece length": 16384, b"pieces": b"",
+                                        b"length": 0}, b"comment": b"z" * 300_000})
+        url = o.add("/big.torrent", pad)
+        d = _dl()
+        data = await d._fetch_torrent_file(url)
+        assert data == pad
+        await o.stop()
+    run(main())

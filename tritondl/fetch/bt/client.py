@@ -76,10 +76,16 @@ class TorrentDownloader:
             async with s.get(url, timeout=aiohttp.ClientTimeout(total=120)) as r:
                 if r.status != 200:
                     raise TorrentError(f"failed to fetch torrent file: HTTP {r.status}")
-                data = await r.content.read(16 * 1024 * 1024 + 1)
-                if len(data) > 16 * 1024 * 1024:
-                    raise TorrentError("torrent file too large")
-                return data
+                cap = 64 * 1024 * 1024          # v2 piece layers make big torrents large
+                buf = bytearray()
+                while True:
+                    chunk = await r.content.read(1 << 20)   # read() returns what is buffered: loop to EOF
+                    if not chunk:
+                        break
+                    buf += chunk
+                    if len(buf) > cap:
+                        raise TorrentError("torrent file too large")
+                return bytes(buf)
         except aiohttp.ClientError as e:
             raise TorrentError(f"failed to fetch torrent file: {e}") from e
         finally:
