@@ -115,6 +115,16 @@ def gpu_hasher(device: int = 0, batch_bytes: int = 256 << 20, reader_threads: in
         return h
 
 
+def warm_gpu(device: int = 0) -> bool:
+    """Create the cached hasher and run one tiny batch (HIP context, code
+    object, pinned staging) so the first resume-verify of a job does not pay
+    the one-time setup.  Returns False when no GPU path is available."""
+    if not gpu_available():
+        return False
+    gpu_hasher(device).hash_buffer("sha1", b"\0" * 16384, 16384)
+    return True
+
+
 def _resolve(device: str) -> str:
     if device == "auto":
         return "gpu" if gpu_available() else "cpu"

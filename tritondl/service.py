@@ -70,6 +70,15 @@ class JobResult:
     seconds: float = 0.0
 
 
+def _warm_gpu_quietly() -> bool:
+    try:
+        from .ops import hashing
+        return hashing.warm_gpu()
+    except Exception as e:  # noqa: BLE001 - optional acceleration; verification falls back to the host
+        log.with_field("error", str(e)).debug("GPU hasher warm-up skipped")
+        return False
+
+
 class Service:
     def __init__(self, cfg: Config, *, amqp: Client | None = None, dispatcher: Dispatcher | None = None,
                  uploader: Uploader | None = None, metrics: Metrics | None = None) -> None:
@@ -107,6 +116,9 @@ class Service:
                                               part_size=cfg.s3_part_size,
                                               multipart_threshold=cfg.s3_multipart_threshold,
                                               parallel_parts=cfg.s3_parallel_parts)
+        if cfg.gpu_verify != "off":
+            # HIP context + hasher set-up off the job path (first torrent resume would pay it)
+            self._warmup = asyncio.get_running_loop().run_in_executor(None, _warm_gpu_quietly)
         if cfg.metrics_addr:
             self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr,
                                                        health=lambda: self.amqp is not None and self.amqp.connected)
