@@ -117,7 +117,12 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         barrier()
-        lat = sorted(r.seconds for r in stack.svc.results[-a.steps:])  # type: ignore[union-attr]
+        done = stack.svc.results[-a.steps:]  # type: ignore[union-attr]
+        lat = sorted(r.seconds for r in done)
+        spans: dict[str, list[float]] = {}
+        for r in done:
+            for k, v in r.marks.items():
+                spans.setdefault(k, []).append(v)
     finally:
         loop.run_until_complete(stack.teardown())
         loop.close()
@@ -143,12 +148,15 @@ def main() -> int:
             "dtype": "uint8",
             "data": f"synthetic (deterministic pseudo-random {file_size / 2**20:g} MiB payload; "
                     "local fake broker/origin/S3)",
-            "config": {"model": CONFIG_NAME, "global_batch": world * a.concurrency, "seq_len": None,
+            "config": {"model": CONFIG_NAME if file_size == 10 << 20 else
+                       f"Single HTTP job, {file_size / 2**20:g} MiB file, local origin -> local S3", "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency)},
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
             "job_latency_ms_p50": round(lat[len(lat) // 2] * 1000, 2) if lat else None,
             "job_latency_ms_p90": round(lat[int(len(lat) * 0.9)] * 1000, 2) if lat else None,
+            # median ms from taking the job to the end of each stage (rank 0)
+            "job_spans_ms_p50": {k: round(sorted(v)[len(v) // 2] * 1000, 2) for k, v in spans.items()},
         }
         res.update(extra)
         print(json.dumps(res), flush=True)

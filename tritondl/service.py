@@ -32,7 +32,7 @@ import shutil
 import signal
 import sys
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 from .amqp.client import Client, Delivery
 from .fetch.http import HTTPDownloader
@@ -68,6 +68,8 @@ class JobResult:
     files: int = 0
     bytes: int = 0
     seconds: float = 0.0
+    # per-job span log: stage -> seconds since the job was taken
+    marks: dict = field(default_factory=dict)
 
 
 def _warm_gpu_quietly() -> bool:
@@ -117,8 +119,15 @@ class Service:
                                               multipart_threshold=cfg.s3_multipart_threshold,
                                               parallel_parts=cfg.s3_parallel_parts)
         if cfg.gpu_verify != "off":
-            # HIP context + hasher set-up off the job path (first torrent resume would pay it)
-            self._warmup = asyncio.get_running_loop().run_in_executor(None, _warm_gpu_quietly)
+            # HIP context + hasher set-up off the job path (first torrent resume would pay it).
+            # Finished before consuming: importing torch holds the GIL for ~1-2 s, which would
+            # otherwise stall the event loop under the first jobs.
+            warm = asyncio.get_running_loop().run_in_executor(None, _warm_gpu_quietly)
+            try:
+                await asyncio.wait_for(asyncio.shield(warm), cfg.gpu_warmup_timeout_s)
+            except asyncio.TimeoutError:
+                log.warn("GPU hasher warm-up still running after %.0fs; consuming anyway",
+                         cfg.gpu_warmup_timeout_s)
         if cfg.metrics_addr:
             self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr,
                                                        health=lambda: self.amqp is not None and self.amqp.connected)
@@ -169,14 +178,21 @@ class Service:
         log.with_field("job", job.to_dict()).info("got message")
         stage = "download"
         nbytes = 0
+        marks: dict[str, float] = {}
+
+        def mark(name: str) -> None:
+            marks[name] = time.monotonic() - t0
+
         try:
             assert self.dispatcher is not None and self.uploader is not None and self.amqp is not None
             t = time.monotonic()
-            dl_dir, streamed = await self._download(job.media.id, job.media.source_uri)
+            dl_dir, streamed = await self._download(job.media.id, job.media.source_uri, marks, t0)
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="download")
+            mark("download")
             stage = "select"
             files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
             log.info("found %d files", len(files))
+            mark("select")
             stage = "upload"
             t = time.monotonic()
             rest = [f for f in files if f not in streamed]
@@ -184,13 +200,16 @@ class Service:
                                              if rest else [])
             nbytes = sum(r.size for r in res)
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="upload")
+            mark("upload")
             stage = "publish"
             log.info("creating v1.convert message")
             conv = Convert.from_download(job, go_time_string())
             await self.amqp.publish(self.cfg.publish_topic, conv.encode())
+            mark("publish")
             stage = "ack"
             log.with_field("job", job.to_dict()).info("finished processing")
             await msg.ack()
+            mark("ack")
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - any stage failure must settle the message
@@ -204,9 +223,12 @@ class Service:
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
         self.metrics.observe("job_seconds", dt)
-        return self._record(JobResult(True, "done", files=len(files), bytes=nbytes, seconds=dt))
+        log.with_fields(media_id=job.media.id, bytes=nbytes,
+                        **{k: round(v * 1000, 3) for k, v in marks.items()}).debug("job spans (ms)")
+        return self._record(JobResult(True, "done", files=len(files), bytes=nbytes, seconds=dt, marks=marks))
 
-    async def _download(self, media_id: str, url: str) -> tuple[str, dict]:
+    async def _download(self, media_id: str, url: str, marks: dict | None = None,
+                        t0: float = 0.0) -> tuple[str, dict]:
         """Download the job's source.  For single-file HTTP sources whose file
         the selector will pick (a top-level media file — the root is always
         walked), the S3 upload is started right away and follows the download's
@@ -219,6 +241,8 @@ class Service:
         d = self.dispatcher.job_dir(media_id)
         os.makedirs(d, mode=0o755, exist_ok=True)
         h = await impl.start(d, self.dispatcher.sink, url)
+        if marks is not None:
+            marks["probe"] = time.monotonic() - t0
         up: asyncio.Task | None = None
         fd = None
         if h.size and go_ext(h.filename) in MEDIA_EXTS:
@@ -226,6 +250,8 @@ class Service:
             up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes))
         try:
             await h.wait()
+            if marks is not None:
+                marks["fetched"] = time.monotonic() - t0
             if up is None:
                 return d, {}
             return d, {h.dst: await up}

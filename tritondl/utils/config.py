@@ -63,6 +63,7 @@ class Config:
     bt_encryption: str = "allow"                # MSE/PE: disable | allow | prefer | require
     bt_bootstrap: str = "router.bittorrent.com:6881,dht.transmissionbt.com:6881"
     gpu_verify: str = "auto"                    # auto|on|off (HIP batch piece hashing)
+    gpu_warmup_timeout_s: float = 120.0         # start-up wait for the HIP hasher before consuming
 
     # --- upload (downloader.go:95, uploader.go) ---
     bucket: str = "triton-staging"
@@ -111,7 +112,8 @@ class Config:
                 "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
                 "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
-                  "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s"}
+                  "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
+                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s"}
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
