@@ -149,7 +149,7 @@ def main() -> int:
             "data": f"synthetic (deterministic pseudo-random {file_size / 2**20:g} MiB payload; "
                     "local fake broker/origin/S3)",
             "config": {"model": CONFIG_NAME if file_size == 10 << 20 else
-                       f"Single HTTP job, {file_size / 2**20:g} MiB file, local origin -> local S3", "global_batch": world * a.concurrency, "seq_len": None,
+                       f"Single HTTP download job via local RabbitMQ, {file_size / 2**20:g} MiB file", "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency)},
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
