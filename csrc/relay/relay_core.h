@@ -1,0 +1,786 @@
+// Native data plane for the fetch -> S3 relay (no Python; shared by the
+// pybind11 module relay.cpp and the sanitizer self-test).
+//
+// The Python control plane (asyncio) opens connections, writes/parses HTTP
+// heads, signs requests and handles retries; every BYTE of a job moves here,
+// in threads that never touch the interpreter:
+//
+//   recv_body  : origin socket -> file (pwrite at the segment's offset),
+//                publishing per-segment progress on a Flow;
+//   send_body  : file -> S3 socket as an aws-chunked (SigV4 streaming) or
+//                unsigned body, following the Flow so an upload can run
+//                while the download is still landing.  Chunk SHA-256s run on a
+//                small hasher pool ahead of the sender (the per-chunk HMAC
+//                chain is the only serial part); the sender batches many
+//                frames per writev.  Unsigned bodies go out with sendfile.
+//
+// Reference behaviour replaced: grab's single-stream copy
+// (internal/downloader/http/http.go:36-71) and minio-go's PutObject body
+// (internal/uploader/uploader.go:89) — here they are one fused pipeline.
+#pragma once
+
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/sendfile.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <climits>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "../hash/hash_core.h"
+
+namespace tritondl_relay {
+
+using Clock = std::chrono::steady_clock;
+
+inline double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
+// ---------------------------------------------------------------------------
+// Flow: progress of one download made of contiguous segments
+// [start, end) (end < 0: open-ended, length unknown), shared by the receive
+// pumps (writers) and any number of readers (upload pump, Python waiters).
+class Flow {
+ public:
+  struct Seg {
+    uint64_t start;
+    int64_t end;  // exclusive; < 0 = unknown length
+    uint64_t done;
+  };
+
+  explicit Flow(std::vector<Seg> segs) : segs_(std::move(segs)) {}
+
+  void advance(size_t seg, uint64_t done) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (seg >= segs_.size()) return;
+      if (done > segs_[seg].done) segs_[seg].done = done;
+    }
+    cv_.notify_all();
+  }
+  // All bytes below `total` are on disk (also resolves open-ended segments).
+  void finish(uint64_t total) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      finished_ = true;
+      total_ = total;
+    }
+    cv_.notify_all();
+  }
+  void fail(const std::string& why) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (!failed_) err_ = why;
+      failed_ = true;
+    }
+    cv_.notify_all();
+  }
+  void cancel() {
+    cancel_.store(true);
+    fail("cancelled");
+  }
+  bool cancelled() const { return cancel_.load(std::memory_order_relaxed); }
+
+  uint64_t done(size_t seg) const {
+    std::lock_guard<std::mutex> l(mu_);
+    return seg < segs_.size() ? segs_[seg].done : 0;
+  }
+  size_t nsegs() const { return segs_.size(); }
+  std::string error() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return err_;
+  }
+  bool failed() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return failed_;
+  }
+  bool finished() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return finished_;
+  }
+
+  // Length of the contiguous prefix on disk.
+  uint64_t watermark() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return watermark_locked();
+  }
+
+  // 0 = [a, b) is on disk, 1 = flow failed/cancelled, 2 = timed out,
+  // 3 = the download finished short of b.
+  int wait_covered(uint64_t a, uint64_t b, double timeout_s, const std::atomic<bool>* abort = nullptr) {
+    std::unique_lock<std::mutex> l(mu_);
+    const auto deadline = Clock::now() + std::chrono::duration_cast<Clock::duration>(
+                                             std::chrono::duration<double>(std::max(0.0, timeout_s)));
+    for (;;) {
+      if (covered_locked(a, b)) return 0;
+      if (failed_) return 1;
+      if (finished_) return 3;
+      if (abort && abort->load()) return 1;
+      if (Clock::now() >= deadline) return 2;
+      // short slices so an aborting caller (the upload pump's sender) is seen promptly
+      cv_.wait_for(l, std::chrono::milliseconds(20));
+    }
+  }
+
+ private:
+  uint64_t watermark_locked() const {
+    if (finished_) return total_;
+    uint64_t w = 0;
+    for (const Seg& s : segs_) {
+      w = s.start + s.done;
+      if (s.end < 0 || w < static_cast<uint64_t>(s.end)) break;
+    }
+    return w;
+  }
+  bool covered_locked(uint64_t a, uint64_t b) const {
+    if (b <= a) return true;
+    if (finished_) return b <= total_;
+    uint64_t need = a;  // first byte of [a, b) not yet shown to be on disk
+    for (const Seg& s : segs_) {
+      const uint64_t s_end = s.end < 0 ? UINT64_MAX : static_cast<uint64_t>(s.end);
+      if (s_end <= need || s.start > need) continue;
+      const uint64_t have = s.start + s.done;  // [s.start, have) is on disk
+      if (have <= need) return false;
+      need = std::min(have, s_end);
+      if (need >= b) return true;
+    }
+    return need >= b;
+  }
+
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Seg> segs_;
+  bool finished_ = false;
+  uint64_t total_ = 0;
+  bool failed_ = false;
+  std::string err_;
+  std::atomic<bool> cancel_{false};
+};
+
+// ---------------------------------------------------------------------------
+// Buffer cache.  A 10 MiB job touches ~20 MiB of pump buffers; fresh
+// allocations of that size come from mmap and fault in page by page on every
+// job (thousands of faults), so the pumps borrow buffers that stay mapped.
+class BufCache {
+ public:
+  static BufCache& get() {
+    static BufCache* c = new BufCache();  // process lifetime (pumps may run at exit)
+    return *c;
+  }
+  char* take(size_t n, size_t* cap) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      size_t best = free_.size();
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].second >= n && (best == free_.size() || free_[i].second < free_[best].second)) best = i;
+      if (best != free_.size()) {
+        char* p = free_[best].first;
+        *cap = free_[best].second;
+        cached_ -= *cap;
+        free_.erase(free_.begin() + static_cast<long>(best));
+        return p;
+      }
+    }
+    *cap = n;
+    return new char[n];
+  }
+  void give(char* p, size_t cap) {
+    std::lock_guard<std::mutex> l(mu_);
+    if (cached_ + cap > kMaxCached) {
+      delete[] p;
+      return;
+    }
+    free_.emplace_back(p, cap);
+    cached_ += cap;
+  }
+
+ private:
+  static constexpr size_t kMaxCached = size_t(256) << 20;
+  std::mutex mu_;
+  std::vector<std::pair<char*, size_t>> free_;
+  size_t cached_ = 0;
+};
+
+// RAII borrowed buffer with vector-like grow (contents kept).
+struct Buf {
+  char* p = nullptr;
+  size_t cap = 0;
+  Buf() = default;
+  explicit Buf(size_t n) { p = BufCache::get().take(n, &cap); }
+  ~Buf() {
+    if (p) BufCache::get().give(p, cap);
+  }
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  char* data() { return p; }
+  const char* data() const { return p; }
+  size_t size() const { return cap; }
+  void ensure(size_t n, size_t keep) {
+    if (n <= cap) return;
+    size_t ncap = 0;
+    char* q = BufCache::get().take(std::max(n, cap * 2), &ncap);
+    if (keep) std::memcpy(q, p, keep);
+    if (p) BufCache::get().give(p, cap);
+    p = q;
+    cap = ncap;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// socket helpers (non-blocking fds owned by the asyncio side; the pumps poll)
+
+// 1 = ready, 0 = not yet (slice elapsed), -1 = error/hangup with no data
+inline int wait_fd(int fd, short ev, int ms) {
+  struct pollfd p {};
+  p.fd = fd;
+  p.events = ev;
+  const int r = ::poll(&p, 1, ms);
+  if (r < 0) return errno == EINTR ? 0 : -1;
+  if (r == 0) return 0;
+  if (p.revents & (ev | POLLHUP)) return 1;  // hangup: let recv/send report EOF / EPIPE
+  return (p.revents & (POLLERR | POLLNVAL)) ? -1 : 1;
+}
+
+inline std::string errno_str(const char* what) {
+  return std::string(what) + ": " + std::strerror(errno);
+}
+
+inline bool pwrite_full(int fd, const char* p, size_t n, uint64_t off, std::string* err) {
+  while (n) {
+    const ssize_t w = ::pwrite(fd, p, n, static_cast<off_t>(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      *err = errno_str("pwrite");
+      return false;
+    }
+    p += w;
+    n -= static_cast<size_t>(w);
+    off += static_cast<uint64_t>(w);
+  }
+  return true;
+}
+
+// Write every iovec (partial writes resumed); waits for POLLOUT on EAGAIN.
+inline bool writev_all(int sock, std::vector<struct iovec>& iov, double idle_timeout, const Flow* flow,
+                       std::string* err) {
+  size_t k = 0;
+  auto last = Clock::now();
+  while (k < iov.size()) {
+    const int cnt = static_cast<int>(std::min<size_t>(iov.size() - k, IOV_MAX));
+    struct msghdr mh {};
+    mh.msg_iov = &iov[k];
+    mh.msg_iovlen = static_cast<size_t>(cnt);
+    const ssize_t w = ::sendmsg(sock, &mh, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno != EAGAIN && errno != EWOULDBLOCK) {
+        *err = errno_str("send");
+        return false;
+      }
+      if (flow && flow->cancelled()) {
+        *err = "cancelled";
+        return false;
+      }
+      if (since(last) > idle_timeout) {
+        *err = "send timeout";
+        return false;
+      }
+      if (wait_fd(sock, POLLOUT, 50) < 0) {
+        *err = "socket error while sending";
+        return false;
+      }
+      continue;
+    }
+    last = Clock::now();
+    size_t left = static_cast<size_t>(w);
+    while (left && k < iov.size()) {
+      if (left >= iov[k].iov_len) {
+        left -= iov[k].iov_len;
+        ++k;
+      } else {
+        iov[k].iov_base = static_cast<char*>(iov[k].iov_base) + left;
+        iov[k].iov_len -= left;
+        left = 0;
+      }
+    }
+    while (k < iov.size() && iov[k].iov_len == 0) ++k;
+  }
+  return true;
+}
+
+inline bool send_all(int sock, const char* p, size_t n, double idle_timeout, const Flow* flow, std::string* err) {
+  if (!n) return true;
+  std::vector<struct iovec> iov{{const_cast<char*>(p), n}};
+  return writev_all(sock, iov, idle_timeout, flow, err);
+}
+
+// ---------------------------------------------------------------------------
+// recv_body: stream a response body from `sock` into `fd` at file offset
+// `off` (fd < 0: receive and drop).  `prefix` = body bytes already read
+// together with the head.
+// length < 0: until EOF.  Progress: flow->advance(seg, seg_done0 + received).
+struct RecvResult {
+  uint64_t received = 0;
+  bool eof = false;  // peer closed (normal end for length < 0)
+  std::string err;
+};
+
+inline RecvResult recv_body(int sock, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
+                            Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout,
+                            size_t buf_size = 4u << 20) {
+  RecvResult r;
+  const uint64_t want = length < 0 ? UINT64_MAX : static_cast<uint64_t>(length);
+  if (prefix_len) {
+    const size_t n = static_cast<size_t>(std::min<uint64_t>(prefix_len, want));
+    if (fd >= 0 && !pwrite_full(fd, prefix, n, off, &r.err)) return r;
+    r.received = n;
+    if (flow) flow->advance(seg, seg_done0 + r.received);
+  }
+  Buf buf(std::max<size_t>(buf_size, 64 << 10));
+  auto last = Clock::now();
+  while (r.received < want) {
+    if (flow && flow->cancelled()) {
+      r.err = "cancelled";
+      return r;
+    }
+    const size_t cap = static_cast<size_t>(std::min<uint64_t>(buf.size(), want - r.received));
+    const ssize_t n = ::recv(sock, buf.data(), cap, MSG_DONTWAIT);
+    if (n > 0) {
+      if (fd >= 0 && !pwrite_full(fd, buf.data(), static_cast<size_t>(n), off + r.received, &r.err)) return r;
+      r.received += static_cast<uint64_t>(n);
+      if (flow) flow->advance(seg, seg_done0 + r.received);
+      last = Clock::now();
+      continue;
+    }
+    if (n == 0) {
+      r.eof = true;
+      if (length >= 0) r.err = "connection closed early";
+      return r;
+    }
+    if (errno == EINTR) continue;
+    if (errno != EAGAIN && errno != EWOULDBLOCK) {
+      r.err = errno_str("recv");
+      return r;
+    }
+    if (since(last) > idle_timeout) {
+      r.err = "read timeout";
+      return r;
+    }
+    if (wait_fd(sock, POLLIN, 50) < 0) {
+      r.err = "socket error while receiving";
+      return r;
+    }
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// send_body: request head + body of one PUT.
+//   mode 0: plain body (sendfile from fd), e.g. UNSIGNED-PAYLOAD
+//   mode 1: aws-chunked STREAMING-AWS4-HMAC-SHA256-PAYLOAD, chunk signatures
+//           chained from `seed` with signing key `key`.
+// Body bytes are [off, off+length) of fd; with a flow, each range is awaited
+// before it is read (upload follows the download).
+struct SendResult {
+  uint64_t sent = 0;     // body payload bytes
+  std::string last_sig;  // mode 1: the final chunk's signature
+  std::string err;
+};
+
+struct ChunkSigner {
+  std::string key, head, empty_hash, prev;
+  ChunkSigner(const std::string& k, const std::string& amzdate, const std::string& scope, const std::string& seed)
+      : key(k),
+        head("AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n"),
+        empty_hash(tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), "", 0))),
+        prev(seed) {}
+  const std::string& next(const std::string& chunk_hash_hex) {
+    prev = tritondl_hash::hex(tritondl_hash::hmac256(key, head + prev + "\n" + empty_hash + "\n" + chunk_hash_hex));
+    return prev;
+  }
+};
+
+inline SendResult send_plain(int sock, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
+  SendResult r;
+  const uint64_t step = 4u << 20;
+  auto last = Clock::now();
+  while (r.sent < length) {
+    const uint64_t n = std::min(step, length - r.sent);
+    if (flow) {
+      const int w = flow->wait_covered(off + r.sent, off + r.sent + n, idle_timeout);
+      if (w) {
+        r.err = w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
+                                                                   : "source transfer failed: " + flow->error();
+        return r;
+      }
+    }
+    uint64_t k = 0;
+    while (k < n) {
+      off_t o = static_cast<off_t>(off + r.sent + k);
+      const ssize_t w = ::sendfile(sock, fd, &o, static_cast<size_t>(n - k));
+      if (w > 0) {
+        k += static_cast<uint64_t>(w);
+        last = Clock::now();
+        continue;
+      }
+      if (w == 0) {
+        r.sent += k;
+        r.err = "source file shorter than expected";
+        return r;
+      }
+      if (errno == EINTR) continue;
+      if (errno != EAGAIN && errno != EWOULDBLOCK) {
+        r.sent += k;
+        r.err = errno_str("sendfile");
+        return r;
+      }
+      if ((flow && flow->cancelled()) || since(last) > idle_timeout || wait_fd(sock, POLLOUT, 50) < 0) {
+        r.sent += k;
+        r.err = (flow && flow->cancelled()) ? "cancelled" : "send timeout";
+        return r;
+      }
+    }
+    r.sent += n;
+  }
+  return r;
+}
+
+inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, Flow* flow, ChunkSigner& signer,
+                               size_t chunk, int threads, double idle_timeout, size_t batch = 64) {
+  SendResult r;
+  if (chunk == 0) {
+    r.err = "chunk size must be > 0";
+    return r;
+  }
+  const size_t n = static_cast<size_t>((length + chunk - 1) / chunk);
+  const size_t K = std::max<size_t>(1, std::min<size_t>(n, 2 * batch));  // ring slots
+  batch = std::min(batch, K);
+  Buf ring(K * chunk);
+  std::vector<int64_t> ready(K, -1);       // chunk index held by each slot, once hashed
+  std::vector<std::string> hashes(K);
+  std::mutex mu;
+  std::condition_variable cv_ready, cv_free;
+  int64_t sent_chunks = 0;
+  std::atomic<bool> abort{false};
+  std::string worker_err;
+  std::atomic<size_t> next{0};
+
+  auto set_err = [&](const std::string& e) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (worker_err.empty()) worker_err = e;
+      abort.store(true);
+    }
+    cv_ready.notify_all();
+    cv_free.notify_all();
+  };
+
+  auto hasher = [&] {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      const size_t slot = i % K;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv_free.wait(l, [&] { return abort.load() || static_cast<int64_t>(i) < sent_chunks + static_cast<int64_t>(K); });
+        if (abort.load()) return;
+      }
+      const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
+      const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(i) * chunk));
+      if (flow) {
+        const int w = flow->wait_covered(a, a + m, idle_timeout, &abort);
+        if (w) {
+          if (!abort.load())
+            set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
+                                                                       : "source transfer failed: " + flow->error());
+          return;
+        }
+      }
+      char* dst = ring.data() + slot * chunk;
+      if (tritondl_hash::pread_full(fd, dst, m, static_cast<off_t>(a)) != m) {
+        set_err("source file shorter than expected");
+        return;
+      }
+      std::string h = tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), dst, m));
+      {
+        std::lock_guard<std::mutex> l(mu);
+        hashes[slot] = std::move(h);
+        ready[slot] = static_cast<int64_t>(i);
+      }
+      cv_ready.notify_all();
+    }
+  };
+
+  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, n)));
+  std::vector<std::thread> pool;
+  if (n) {
+    pool.reserve(static_cast<size_t>(nthreads));
+    for (int t = 0; t < nthreads; ++t) pool.emplace_back(hasher);
+  }
+
+  std::vector<std::string> heads;
+  std::vector<struct iovec> iov;
+  static const char crlf[] = "\r\n";
+  size_t i = 0;
+  while (i < n && r.err.empty()) {
+    std::vector<std::string> hs;
+    size_t j = i;
+    {
+      std::unique_lock<std::mutex> l(mu);
+      cv_ready.wait(l, [&] { return abort.load() || ready[i % K] == static_cast<int64_t>(i); });
+      if (abort.load()) {
+        r.err = worker_err;
+        break;
+      }
+      while (j < n && j < i + batch && ready[j % K] == static_cast<int64_t>(j)) {
+        hs.push_back(hashes[j % K]);
+        ++j;
+      }
+    }
+    heads.clear();
+    heads.reserve(j - i);
+    iov.clear();
+    iov.reserve(3 * (j - i));
+    for (size_t c = i; c < j; ++c) {
+      const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(c) * chunk));
+      char hx[32];
+      std::snprintf(hx, sizeof hx, "%zx", m);
+      heads.push_back(std::string(hx) + ";chunk-signature=" + signer.next(hs[c - i]) + "\r\n");
+    }
+    for (size_t c = i; c < j; ++c) {
+      const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(c) * chunk));
+      iov.push_back({const_cast<char*>(heads[c - i].data()), heads[c - i].size()});
+      iov.push_back({ring.data() + (c % K) * chunk, m});
+      iov.push_back({const_cast<char*>(crlf), 2});
+      r.sent += m;
+    }
+    std::string e;
+    if (!writev_all(sock, iov, idle_timeout, flow, &e)) {
+      r.err = e;
+      break;
+    }
+    {
+      std::lock_guard<std::mutex> l(mu);
+      sent_chunks = static_cast<int64_t>(j);
+    }
+    cv_free.notify_all();
+    i = j;
+  }
+  if (!r.err.empty()) {
+    abort.store(true);
+    cv_free.notify_all();
+    cv_ready.notify_all();
+  }
+  for (auto& t : pool) t.join();
+  if (!r.err.empty()) return r;
+  const std::string fin = "0;chunk-signature=" + signer.next(signer.empty_hash) + "\r\n\r\n";
+  std::string e;
+  if (!send_all(sock, fin.data(), fin.size(), idle_timeout, flow, &e)) {
+    r.err = e;
+    return r;
+  }
+  r.last_sig = signer.prev;
+  return r;
+}
+
+inline SendResult send_body(int sock, const std::string& head, int fd, uint64_t off, uint64_t length, Flow* flow,
+                            int mode, const std::string& key, const std::string& amzdate, const std::string& scope,
+                            const std::string& seed, size_t chunk, int threads, double idle_timeout) {
+  SendResult r;
+  if (!send_all(sock, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
+  if (mode == 0) return send_plain(sock, fd, off, length, flow, idle_timeout);
+  ChunkSigner signer(key, amzdate, scope, seed);
+  return send_chunked(sock, fd, off, length, flow, signer, chunk, threads, idle_timeout);
+}
+
+// ---------------------------------------------------------------------------
+// recv_verify_chunked: the SERVER side of send_chunked (the fake S3's PUT
+// path).  Receives exactly raw_len body bytes, parses aws-chunked frames and
+// verifies every chunk signature.  Windows of ~`window` raw bytes alternate
+// between two buffers: while window k is verified (payload SHA-256s as a
+// parallel map, then the serial HMAC chain) window k+1 is being received.
+struct VerifyResult {
+  uint64_t decoded = 0;
+  std::string err;
+  std::string data;  // decoded payload when keep
+};
+
+struct RawFrame {
+  size_t off, n;  // payload offset in its window buffer, payload length
+  size_t sig;     // offset of the 64-hex claimed signature
+};
+
+// Parse whole frames in [0, have); stops at the first incomplete one.
+// Returns the end of the last whole frame; sets *final on the 0-length frame.
+inline size_t parse_frames(const char* raw, size_t have, std::vector<RawFrame>* out, bool* final, std::string* err) {
+  size_t pos = 0;
+  while (pos < have) {
+    size_t hexend = pos;
+    while (hexend < have && hexend - pos < 16 && std::isxdigit(static_cast<unsigned char>(raw[hexend]))) ++hexend;
+    if (hexend == have || hexend + 17 + 64 + 2 > have) {
+      if (hexend - pos >= 16 && hexend < have) *err = "malformed aws-chunked framing";
+      break;  // header incomplete
+    }
+    if (hexend == pos || std::memcmp(raw + hexend, ";chunk-signature=", 17) != 0) {
+      *err = "malformed aws-chunked framing";
+      break;
+    }
+    const size_t n = std::strtoull(std::string(raw + pos, hexend - pos).c_str(), nullptr, 16);
+    const size_t sig = hexend + 17;
+    const size_t a = sig + 64 + 2;
+    if (raw[sig + 64] != '\r' || raw[sig + 65] != '\n') {
+      *err = "malformed chunk header";
+      break;
+    }
+    if (n > (size_t(1) << 40)) {
+      *err = "chunk too large";
+      break;
+    }
+    if (a + n + 2 > have) break;  // payload incomplete
+    if (raw[a + n] != '\r' || raw[a + n + 1] != '\n') {
+      *err = "chunk not terminated";
+      break;
+    }
+    out->push_back({a, n, sig});
+    pos = a + n + 2;
+    if (n == 0) {
+      *final = true;
+      break;
+    }
+  }
+  return pos;
+}
+
+inline VerifyResult recv_verify_chunked(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+                                        const std::string& key, const std::string& amzdate, const std::string& scope,
+                                        const std::string& seed, bool keep, int threads, double idle_timeout,
+                                        size_t window = 4u << 20) {
+  VerifyResult r;
+  Buf buf[2];
+  int cur = 0;
+  size_t have = 0;
+  uint64_t received = 0;
+  ChunkSigner signer(key, amzdate, scope, seed);
+  std::thread verifier;
+  std::string verr;  // verifier error (read after join)
+  bool final_seen = false;
+  const int t = threads <= 0 ? 4 : threads;
+
+  auto join = [&] {
+    if (verifier.joinable()) verifier.join();
+  };
+  auto ensure = [&](Buf& b, size_t n, size_t keep) { b.ensure(n, keep); };
+  const size_t pre = static_cast<size_t>(std::min<uint64_t>(plen, raw_len));
+  ensure(buf[cur], std::max(window, pre) + 1, 0);
+  std::memcpy(buf[cur].data(), prefix, pre);
+  have = pre;
+  received = pre;
+  auto last = Clock::now();
+
+  while (!final_seen) {
+    // fill the current window
+    while (have < window && received < raw_len) {
+      ensure(buf[cur], have + std::min<uint64_t>(window, raw_len - received), have);
+      const size_t cap = static_cast<size_t>(std::min<uint64_t>(buf[cur].size() - have, raw_len - received));
+      const ssize_t n = ::recv(sock, buf[cur].data() + have, cap, MSG_DONTWAIT);
+      if (n > 0) {
+        have += static_cast<size_t>(n);
+        received += static_cast<uint64_t>(n);
+        last = Clock::now();
+        continue;
+      }
+      if (n == 0) {
+        r.err = "client closed inside the request body";
+        break;
+      }
+      if (errno == EINTR) continue;
+      if (errno != EAGAIN && errno != EWOULDBLOCK) {
+        r.err = errno_str("recv");
+        break;
+      }
+      if (since(last) > idle_timeout) {
+        r.err = "read timeout";
+        break;
+      }
+      if (wait_fd(sock, POLLIN, 50) < 0) {
+        r.err = "socket error while receiving";
+        break;
+      }
+    }
+    if (!r.err.empty()) break;
+    std::vector<RawFrame> frames;
+    std::string perr;
+    const size_t end = parse_frames(buf[cur].data(), have, &frames, &final_seen, &perr);
+    if (!perr.empty()) {
+      r.err = perr;
+      break;
+    }
+    if (frames.empty()) {
+      if (received >= raw_len) {
+        r.err = "truncated chunk";
+        break;
+      }
+      window = std::max(window, have + (1u << 20));  // one frame bigger than the window: grow it
+      continue;
+    }
+    join();
+    if (!verr.empty()) {
+      r.err = verr;
+      break;
+    }
+    const int nxt = 1 - cur;
+    ensure(buf[nxt], std::max(window, have - end) + 1, 0);
+    if (have > end) std::memcpy(buf[nxt].data(), buf[cur].data() + end, have - end);
+    const size_t leftover = have - end;
+    const size_t dbase = r.data.size();
+    size_t wtotal = 0;
+    for (const RawFrame& f : frames) wtotal += f.n;
+    r.decoded += wtotal;
+    if (keep) r.data.resize(dbase + wtotal);
+    Buf* wb = &buf[cur];
+    verifier = std::thread([&, wb, frames = std::move(frames), dbase] {
+      const char* raw = wb->data();
+      std::vector<std::string> h(frames.size());
+      std::vector<size_t> doff(frames.size() + 1, 0);
+      for (size_t i = 0; i < frames.size(); ++i) doff[i + 1] = doff[i] + frames[i].n;
+      const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, doff.back() >> 20)));
+      tritondl_hash::parallel_for(frames.size(), used, [&](size_t i) {
+        const RawFrame& f = frames[i];
+        h[i] = tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), f.n ? raw + f.off : "", f.n));
+        if (keep && f.n) std::memcpy(&r.data[dbase + doff[i]], raw + f.off, f.n);
+      });
+      for (size_t i = 0; i < frames.size(); ++i) {
+        if (std::memcmp(signer.next(h[i]).data(), raw + frames[i].sig, 64) != 0) {
+          verr = "chunk signature mismatch";
+          return;
+        }
+      }
+    });
+    cur = nxt;
+    have = leftover;
+  }
+  join();
+  if (r.err.empty() && !verr.empty()) r.err = verr;
+  if (r.err.empty() && (have != 0 || received != raw_len)) r.err = "trailing bytes after final chunk";
+  return r;
+}
+
+// Exact on-the-wire size of an aws-chunked body of `len` payload bytes.
+inline uint64_t chunked_length(uint64_t len, uint64_t chunk) {
+  return tritondl_hash::aws_chunk_encoded_size(static_cast<size_t>(len), static_cast<size_t>(chunk), true);
+}
+
+}  // namespace tritondl_relay

@@ -5,6 +5,8 @@ full job, and prints one JSON line per case:
 
 * ``fetch``   — HTTP download of the file into a job dir (no upload)
 * ``upload``  — S3 PUT of a file already on disk (aws-chunked SigV4 by default)
+* ``upload_*_nullsink`` — the same PUT into a sink that ignores the body
+                (the client's share of the upload)
 * ``sign``    — the aws-chunked encoder alone over an in-memory buffer
 * ``job``     — the whole job (consume → fetch ‖ upload → publish → ack),
                 with the per-stage span medians the service records
@@ -44,6 +46,19 @@ def _stats(xs: list[float], size: int) -> dict:
             "MB_per_sec_p50": round(size / med / 1e6, 1)}
 
 
+def _patch_defaults(cls, kw: str, value: int) -> None:
+    """Override one keyword default of ``cls.__init__`` for every instance
+    this process creates (the job stack builds its own clients)."""
+    if not value:
+        return
+    orig = cls.__init__
+
+    def init(self, *args, **kwargs):
+        kwargs.setdefault(kw, value)
+        orig(self, *args, **kwargs)
+    cls.__init__ = init
+
+
 async def _fetch(origin: str, size: int, reps: int, work: str) -> dict:
     dl = HTTPDownloader(progress_interval=0)
     sink = ProgressSink()
@@ -61,14 +76,14 @@ async def _fetch(origin: str, size: int, reps: int, work: str) -> dict:
     return _stats(ts[2:], size)
 
 
-async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str) -> dict:
+async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str, make_bucket: bool = True) -> dict:
     p = os.path.join(work, "src.mkv")
     with open(p, "wb") as f:
         f.write(os.urandom(size))
     c = S3Client(s3_url, Static(AK, SK), payload_mode=mode)
     ts = []
     try:
-        if not await c.bucket_exists("bd"):
+        if make_bucket and not await c.bucket_exists("bd"):
             await c.make_bucket("bd")
         for i in range(reps + 2):
             t = time.perf_counter()
@@ -77,6 +92,41 @@ async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str) -> di
     finally:
         await c.close()
     return _stats(ts[2:], size)
+
+
+class _NullSink(asyncio.Protocol):
+    """HTTP/1.1 sink: reads each request body by Content-Length, answers 200
+    without looking at it — the client side of an upload, isolated."""
+
+    def connection_made(self, t) -> None:
+        self.t, self.buf, self.need, self.got = t, b"", None, 0
+
+    def data_received(self, d: bytes) -> None:
+        if self.need is None:
+            self.buf += d
+            i = self.buf.find(b"\r\n\r\n")
+            if i < 0:
+                return
+            cl = 0
+            for line in self.buf[:i].split(b"\r\n")[1:]:
+                k, _, v = line.partition(b":")
+                if k.strip().lower() == b"content-length":
+                    cl = int(v)
+            self.need, self.got, self.buf = cl, len(self.buf) - i - 4, b""
+        else:
+            self.got += len(d)
+        if self.got >= self.need:
+            self.t.write(b'HTTP/1.1 200 OK\r\nContent-Length: 0\r\nETag: "0"\r\n\r\n')
+            self.need, self.got = None, 0
+
+
+async def _upload_null(size: int, reps: int, work: str, mode: str) -> dict:
+    srv = await asyncio.get_running_loop().create_server(_NullSink, "127.0.0.1", 0)
+    try:
+        port = srv.sockets[0].getsockname()[1]
+        return await _upload(f"http://127.0.0.1:{port}", size, reps, work, mode, make_bucket=False)
+    finally:
+        srv.close()
 
 
 def _sign(size: int, reps: int) -> dict:
@@ -113,7 +163,14 @@ async def main() -> None:
     ap.add_argument("--file-mb", type=float, default=10)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--payload", default="streaming", choices=["streaming", "unsigned", "signed"])
+    ap.add_argument("--http-bufsize", type=int, default=0, help="worker HTTP client read_bufsize (0 = default)")
+    ap.add_argument("--s3-bufsize", type=int, default=0, help="fake S3 server read_bufsize (0 = default)")
+    ap.add_argument("--io-block", type=int, default=0, help="S3 upload read/sign block (0 = default)")
     a = ap.parse_args()
+    if a.s3_bufsize:
+        os.environ["TRITONDL_FAKE_S3_READ_BUFSIZE"] = str(a.s3_bufsize)
+    _patch_defaults(HTTPDownloader, "read_bufsize", a.http_bufsize)
+    _patch_defaults(S3Client, "io_block", a.io_block)
     log.configure("error", "")
     size = int(a.file_mb * (1 << 20))
     work = tempfile.mkdtemp(prefix="tritondl-bd-")
@@ -124,11 +181,13 @@ async def main() -> None:
         out["sign"] = await asyncio.get_running_loop().run_in_executor(None, _sign, size, a.reps)
         out["fetch"] = await _fetch(og.info["url"], size, a.reps, work)
         out[f"upload_{a.payload}"] = await _upload(s3.info["url"], size, a.reps, work, a.payload)
+        out[f"upload_{a.payload}_nullsink"] = await _upload_null(size, a.reps, work, a.payload)
     finally:
         await og.stop()
         await s3.stop()
         shutil.rmtree(work, ignore_errors=True)
     out["job"] = await _job(size, a.reps)
+    out["knobs"] = {"http_bufsize": a.http_bufsize, "s3_bufsize": a.s3_bufsize, "io_block": a.io_block}
     print(json.dumps(out), flush=True)
 
 

@@ -3,6 +3,7 @@
 
 * ``tritondl/_hash_host*.so``  – g++  (OpenSSL EVP host hashing, pybind11)
 * ``tritondl/_gpu_hash*.so``   – hipcc --offload-arch=gfx950 (HIP kernels)
+* ``tritondl/_relay*.so``      – g++  (native fetch -> S3 data plane, pybind11)
 * ``tritondl/_utp*.so``        – g++  (uTP / LEDBAT transport, pybind11)
 
 Rebuilds only when a source is newer than its output.  ``--force`` rebuilds.
@@ -53,6 +54,13 @@ TARGETS = {
                   "-pthread", "-Wno-unused-result"],
         "libs": [],
     },
+    "_relay": {
+        "srcs": ["csrc/relay/relay.cpp"],
+        "deps": ["csrc/hash/hash_core.h"],
+        "cc": "g++",
+        "flags": ["-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread", "-Wall"],
+        "libs": ["-lcrypto"],
+    },
     "_utp": {
         "srcs": ["csrc/utp/utp.cpp"],
         "cc": "g++",
@@ -72,7 +80,7 @@ def needs_build(name: str, force: bool) -> bool:
         return True
     t = os.path.getmtime(out)
     spec = TARGETS[name]
-    deps = [os.path.join(ROOT, s) for s in spec["srcs"]]
+    deps = [os.path.join(ROOT, s) for s in spec["srcs"] + spec.get("deps", [])]
     for s in spec["srcs"]:
         d = os.path.dirname(os.path.join(ROOT, s))
         deps += [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".cuh"))]

@@ -1,10 +1,13 @@
-"""In-process HTTP origin (aiohttp.web) with Range / HEAD / ETag /
+"""In-process HTTP origin (raw asyncio HTTP, ``rawserver``) with Range / HEAD / ETag /
 Content-Disposition and fault injection — the stand-in for the media
 servers the HTTP downloader talks to (the reference had no test origin).
 
 Fault knobs: ``ranges`` (advertise/honour Range), ``head`` (support HEAD),
 ``cut_after`` (drop the connection after N body bytes, once per request
 count in ``cut_times``), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap).
+Without faults or a rate cap, GET bodies leave through ``sendfile`` from a
+native thread (``SendfileResponse``) — blobs held in memory are mirrored to
+a memfd once.
 """
 
 from __future__ import annotations
@@ -15,7 +18,8 @@ import os
 import re
 from dataclasses import dataclass
 
-from aiohttp import web
+from ..utils import rawhttp
+from . import rawserver as web
 
 
 @dataclass
@@ -35,6 +39,20 @@ class Blob:
             f.seek(start)
             return f.read(end - start)
 
+    def fd(self) -> int:
+        """A read-only fd over the content for sendfile (memfd for in-memory blobs)."""
+        fd = getattr(self, "_fd", None)
+        if fd is None:
+            if self.data is not None:
+                fd = os.memfd_create("origin-blob", os.MFD_CLOEXEC)
+                mv = memoryview(self.data)
+                while mv:
+                    mv = mv[os.write(fd, mv):]
+            else:
+                fd = os.open(self.path or "", os.O_RDONLY | os.O_CLOEXEC)
+            self._fd = fd
+        return fd
+
 
 class Origin:
     def __init__(self, host: str = "127.0.0.1", port: int = 0) -> None:
@@ -48,7 +66,7 @@ class Origin:
         self.rate: float | None = None
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
-        self._runner: web.AppRunner | None = None
+        self._server: web.Server | None = None
 
     def add(self, path: str, data: bytes | None = None, *, file: str | None = None,
             disposition: str | None = None) -> str:
@@ -60,19 +78,14 @@ class Origin:
         return f"http://{self.host}:{self.port}{path}"
 
     async def start(self) -> "Origin":
-        app = web.Application()
-        app.router.add_route("*", "/{tail:.*}", self._handle)
-        self._runner = web.AppRunner(app, access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
-        await site.start()
-        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        self._server = web.Server(self._handle)
+        self.port = await self._server.start(self.host, self.port)
         return self
 
     async def stop(self) -> None:
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
 
     async def _handle(self, request: web.Request) -> web.StreamResponse:
         self.requests.append((request.method, request.path, request.headers.get("Range", "")))
@@ -112,6 +125,8 @@ class Origin:
                     return web.Response(status=416, headers={"Content-Range": f"bytes */{size}"})
                 status = 206
                 hdrs["Content-Range"] = f"bytes {start}-{end - 1}/{size}"
+        if self.cut_after is None and not self.rate and rawhttp.relay_module() is not None:
+            return web.SendfileResponse(status, hdrs, blob.fd(), start, end - start)
         hdrs["Content-Length"] = str(end - start)
         resp = web.StreamResponse(status=status, headers=hdrs)
         await resp.prepare(request)

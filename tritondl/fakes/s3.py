@@ -1,4 +1,4 @@
-"""In-process S3 server (aiohttp.web) that VERIFIES SigV4 — the MinIO/S3
+"""In-process S3 server (raw asyncio HTTP, ``rawserver``) that VERIFIES SigV4 — the MinIO/S3
 stand-in for tests, smoke and bench (the reference had none).
 
 Supports: HEAD/PUT bucket (path-style and virtual-host style), PUT object
@@ -7,7 +7,10 @@ per-chunk signature verification), multipart (initiate / upload part /
 complete / abort), GET/HEAD/DELETE object, ListObjectsV2.
 
 Storage modes: ``memory`` (default), ``disk`` (under ``root``) or
-``discard`` (keep only size + ETag — for throughput benches).
+``discard`` (keep only size + ETag — for throughput benches).  With the
+native relay built, aws-chunked and unsigned PUT bodies are received (and
+every chunk signature verified) by ``_relay.recv_verify_chunked`` /
+``_relay.recv_body`` outside the interpreter, as MinIO would on its own box.
 Fault injection: :meth:`fail_next` returns 5xx for the next N requests.
 """
 
@@ -22,9 +25,9 @@ import re
 from dataclasses import dataclass, field
 from urllib.parse import parse_qsl, unquote
 
-from aiohttp import web
-
 from ..s3 import sigv4
+from ..utils import rawhttp
+from . import rawserver as web
 
 _CHUNK_HDR = re.compile(rb"([0-9a-fA-F]+);chunk-signature=([0-9a-f]{64})\r\n")
 _AUTH_RE = re.compile(r"AWS4-HMAC-SHA256 Credential=([^/]+)/([^,]+), *SignedHeaders=([^,]+), *Signature=([0-9a-f]+)")
@@ -67,23 +70,19 @@ class FakeS3:
         self._fail_status = 503
         self.requests: list[tuple[str, str]] = []
         self.bytes_received = 0
-        self._runner: web.AppRunner | None = None
+        self._server: web.Server | None = None
+        self.native = True
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> "FakeS3":
-        app = web.Application(client_max_size=1 << 40)
-        app.router.add_route("*", "/{tail:.*}", self._handle)
-        self._runner = web.AppRunner(app, access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
-        await site.start()
-        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        self._server = web.Server(self._handle)
+        self.port = await self._server.start(self.host, self.port)
         return self
 
     async def stop(self) -> None:
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
 
     @property
     def endpoint(self) -> str:
@@ -152,16 +151,50 @@ class FakeS3:
         mode): aws-chunked bodies are verified without materialising the
         decoded bytes and only their length is returned (as ``_Sized``)."""
         phash = request.headers.get("x-amz-content-sha256", sigv4.UNSIGNED_PAYLOAD)
+        relay = rawhttp.relay_module() if self.native else None
         if phash == sigv4.STREAMING_PAYLOAD:
             if not isinstance(auth, tuple):
                 raise _BadReq(400, "InvalidRequest", "streaming payload needs a signature")
+            if relay is not None and request.body_length:
+                return await self._read_chunked_native(relay, request, auth, keep)
             return await self._read_chunked(request, auth, keep)
+        if relay is not None and not keep and phash in (sigv4.UNSIGNED_PAYLOAD, "") and request.body_length:
+            n = request.body_length
+            sock, pre = request.take_body()
+            got, _eof, err = await asyncio.get_running_loop().run_in_executor(
+                None, relay.recv_body, sock.fileno(), -1, 0, n, pre, None, 0, 0, 300.0)
+            if err:
+                request.transport.close()
+                raise _BadReq(400, "IncompleteBody", err)
+            self.bytes_received += got
+            return _Sized(got)
         data = await request.read()
         self.bytes_received += len(data)
         if phash not in (sigv4.UNSIGNED_PAYLOAD, "") and auth is not None:
             if hashlib.sha256(data).hexdigest() != phash:
                 raise _BadReq(400, "XAmzContentSHA256Mismatch", "payload hash mismatch")
         return data
+
+    async def _read_chunked_native(self, relay, request: web.Request, auth, keep: bool):
+        """Native receive + per-chunk signature verification (GIL released)."""
+        key, seed, amzdate, scope = auth
+        decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
+        raw_len = request.body_length
+        sock, pre = request.take_body()
+        n, err, data = await asyncio.get_running_loop().run_in_executor(
+            None, relay.recv_verify_chunked, sock.fileno(), raw_len, pre, key, amzdate, scope, seed, keep, 4, 300.0)
+        self.bytes_received += raw_len
+        if err:
+            if "closed" in err or "timeout" in err or "socket" in err or "recv" in err:
+                request.transport.close()
+            else:
+                # the body was consumed up to the error: drop the connection after replying
+                request.transport_close_after = True
+            code = 403 if "signature" in err else 400
+            raise _BadReq(code, "SignatureDoesNotMatch" if code == 403 else "IncompleteBody", err)
+        if decoded_len >= 0 and decoded_len != n:
+            raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
+        return data if keep else _Sized(n)
 
     async def _read_chunked(self, request: web.Request, auth, keep: bool = True):
         """Decode an aws-chunked body and verify EVERY chunk signature while it

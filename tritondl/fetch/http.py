@@ -19,7 +19,12 @@ Beyond the reference:
   on completion, so a crash never leaves a truncated file that looks done,
   and ``If-Range`` guards against resuming onto a changed origin object;
 * large files are fetched as ``segments`` concurrent Range streams written
-  with ``pwrite`` from worker threads (grab used one stream).
+  with ``pwrite`` from worker threads (grab used one stream);
+* plain-``http`` bodies never enter Python: after the head is parsed the
+  socket goes to the native receive pump (``csrc/relay``, GIL released),
+  which writes the file and publishes progress on a native ``Flow`` that
+  the S3 send pump follows (``https``, redirects and chunked / encoded
+  bodies use aiohttp).
 """
 
 from __future__ import annotations
@@ -34,7 +39,9 @@ from email.message import Message as _EmailMsg
 from urllib.parse import unquote, urlparse
 
 import aiohttp
+from yarl import URL
 
+from ..utils import rawhttp
 from ..utils.log import log
 from .registry import ClientRegister, ProgressSink
 
@@ -45,6 +52,33 @@ class HTTPDownloadError(Exception):
 
 class _FatalHTTPError(HTTPDownloadError):
     pass
+
+
+class _RawResponse:
+    """The bits of an aiohttp response this module uses, over a raw socket
+    whose body the native pump reads."""
+
+    def __init__(self, pool: rawhttp.Pool, host: str, port: int, sock, head: rawhttp.Head, url: str) -> None:
+        self.pool, self.host, self.port, self.sock, self.head = pool, host, port, sock, head
+        self.status = head.status
+        self.headers = head.headers
+        self.url = URL(url)
+        self.leftover = head.leftover
+        self.complete = False          # body read to its end (connection reusable)
+
+    def release(self) -> None:
+        if self.sock is None:
+            return
+        if self.complete and self.head.keep_alive:
+            self.pool.release(self.host, self.port, self.sock)
+        else:
+            self.sock.close()
+        self.sock = None
+
+    def close(self) -> None:
+        if self.sock is not None:
+            self.sock.close()
+            self.sock = None
 
 
 @dataclass
@@ -83,7 +117,8 @@ def filename_from_url(url: str) -> str:
 class HTTPDownloader:
     def __init__(self, *, progress_interval: float = 1.0, segments: int = 4, segment_threshold: int = 64 << 20,
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
-                 headers: dict | None = None, max_retries: int = 5, probe: str = "get") -> None:
+                 headers: dict | None = None, max_retries: int = 5, probe: str = "get",
+                 native: bool = True, read_timeout: float = 120.0) -> None:
         self.progress_interval = progress_interval
         self.probe_mode = probe          # "get": ranged GET doubles as the probe; "head": grab-style HEAD first
         self.segments = max(1, segments)
@@ -93,6 +128,10 @@ class HTTPDownloader:
         self._session = session
         self.headers = headers or {"User-Agent": "tritondl/0.1"}
         self.max_retries = max_retries
+        # native data plane (csrc/relay): plain-http bodies go socket -> file in C++
+        self.native = native
+        self.read_timeout = read_timeout
+        self._raw = rawhttp.Pool()
 
     def register(self) -> ClientRegister:
         return ClientRegister(name="http", protocols=["http", "https"])
@@ -105,9 +144,53 @@ class HTTPDownloader:
         return self._session
 
     async def close(self) -> None:
+        self._raw.close()
         if self._session is not None:
             await self._session.close()
             self._session = None
+
+    # ------------------------------------------------------------ transport
+    def _native_for(self, url: str):
+        if not self.native or not url.startswith("http://"):
+            return None
+        return rawhttp.relay_module()
+
+    async def _open(self, url: str, headers: dict):
+        """GET ``url``: a :class:`_RawResponse` on the native path (plain
+        http, identity body, no redirect), else an open aiohttp response."""
+        if self._native_for(url) is not None:
+            r = await self._raw_get(url, headers)
+            if r is not None:
+                return r
+        s = await self._sess()
+        return await s.get(url, headers=headers, allow_redirects=True)
+
+    async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":
+        u = URL(url)
+        host, port = u.raw_host or "", u.port or 80
+        target = u.raw_path_qs or "/"
+        hh = {"Host": host if port == 80 else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
+        head = rawhttp.request_head("GET", target, hh)
+        loop = asyncio.get_running_loop()
+        for _ in range(2):                    # a stale pooled keep-alive socket gets one fresh retry
+            sock, reused = await self._raw.connect(host, port)
+            try:
+                await asyncio.wait_for(loop.sock_sendall(sock, head), self.read_timeout)
+                h = await rawhttp.read_head(sock, self.read_timeout)
+            except (OSError, rawhttp.RawHTTPError) as e:
+                sock.close()
+                if reused:
+                    continue
+                raise aiohttp.ClientConnectionError(str(e)) from e
+            except BaseException:
+                sock.close()
+                raise
+            enc = h.headers.get("Content-Encoding", "identity").lower()
+            if 300 <= h.status < 400 or h.chunked or enc not in ("", "identity"):
+                sock.close()                  # redirect / chunked / encoded body: aiohttp handles these
+                return None
+            return _RawResponse(self._raw, host, port, sock, h, url)
+        raise aiohttp.ClientConnectionError(f"GET {url}: connection reset")
 
     # ------------------------------------------------------------ probe
     async def _probe(self, url: str) -> _Probe:
@@ -138,10 +221,10 @@ class HTTPDownloader:
         attempt = 0
         while True:
             try:
-                r = await s.get(url, headers={**self.headers, "Range": "bytes=0-"}, allow_redirects=True)
+                r = await self._open(url, {**self.headers, "Range": "bytes=0-"})
                 if r.status == 416:                      # empty resource: no satisfiable range
                     r.release()
-                    r = await s.get(url, headers=self.headers, allow_redirects=True)
+                    r = await self._open(url, dict(self.headers))
                 if r.status < 500:
                     break
                 r.release()
@@ -232,14 +315,14 @@ class HTTPDownloader:
 
         def sync_save() -> None:
             for k, sg in enumerate(segs):
-                sg[2] = done[k]
+                sg[2] = h.seg_done(k)
             self._save_meta(meta_path, state)
 
         async def reporter() -> None:
             while True:
                 await asyncio.sleep(self.progress_interval)
                 tot = probe.size or 0
-                pct = (sum(done) / tot * 100) if tot else 0.0
+                pct = (sum(h.seg_done(k) for k in range(len(segs))) / tot * 100) if tot else 0.0
                 progress(url, min(pct, 99.99))
                 sync_save()
 
@@ -331,8 +414,8 @@ class HTTPDownloader:
                     hdrs["Range"] = f"bytes={pos}-" + (f"{end - 1}" if end >= 0 else "")
                     if validator:
                         hdrs["If-Range"] = validator
-                s = await self._sess()
-                async with s.get(url, headers=hdrs, allow_redirects=True) as r:
+                r = await self._open(url, hdrs)
+                try:
                     if r.status >= 400:
                         raise HTTPDownloadError(f"GET {url}: HTTP {r.status}")
                     if "Range" in hdrs and r.status != 206:
@@ -343,7 +426,9 @@ class HTTPDownloader:
                             else:
                                 raise _FatalHTTPError("origin ignored Range request")
                     await self._consume(r, fd, i, segs, done, h, pos, end)
-                    return
+                finally:
+                    r.release()
+                return
             except (aiohttp.ClientError, asyncio.TimeoutError, HTTPDownloadError, ConnectionError) as e:
                 attempt += 1
                 if attempt > self.max_retries or isinstance(e, _FatalHTTPError) or \
@@ -353,9 +438,11 @@ class HTTPDownloader:
                 log.with_fields(error=str(e), attempt=attempt, segment=i).warn("download stream failed; retrying")
                 await asyncio.sleep(d)
 
-    async def _consume(self, r: aiohttp.ClientResponse, fd: int, i: int, segs: list[list[int]], done: list[int],
+    async def _consume(self, r, fd: int, i: int, segs: list[list[int]], done: list[int],
                        h: "DownloadHandle | None", pos: int, end: int) -> None:
         """Stream one response body into the file at ``pos`` (up to ``end``)."""
+        if isinstance(r, _RawResponse):
+            return await self._consume_native(r, fd, i, segs, done, h, pos, end)
         loop = asyncio.get_running_loop()
         start = segs[i][0]
         limit = (end - pos) if end >= 0 else -1
@@ -376,7 +463,7 @@ class HTTPDownloader:
                 done[i] += nbuf
                 bufs, nbuf = [], 0
                 if h is not None:
-                    h._progressed()
+                    h._advance(i, done[i])
                 if limit >= 0 and wpos - pos >= limit and not r.content.at_eof():
                     if segs[i][1] < 0 or len(segs) > 1:
                         break               # more body follows (next segment's bytes): stop here
@@ -385,8 +472,35 @@ class HTTPDownloader:
             wpos += nbuf
             done[i] += nbuf
             if h is not None:
-                h._progressed()
+                h._advance(i, done[i])
         if end >= 0 and start + done[i] < end:
+            raise HTTPDownloadError("connection closed early")
+
+    async def _consume_native(self, r: _RawResponse, fd: int, i: int, segs: list[list[int]], done: list[int],
+                              h: "DownloadHandle | None", pos: int, end: int) -> None:
+        """The body goes socket -> file inside ``_relay.recv_body`` (GIL
+        released), which publishes progress on the handle's native flow."""
+        relay = rawhttp.relay_module()
+        limit = (end - pos) if end >= 0 else -1
+        cl = r.head.content_length
+        if limit >= 0:
+            n = min(limit, cl) if cl is not None else limit
+        else:
+            n = cl if cl is not None else -1
+        prefix, r.leftover = r.leftover, b""
+        flow = h.flow if h is not None else None
+        got, eof, err = await asyncio.get_running_loop().run_in_executor(
+            None, relay.recv_body, r.sock.fileno(), fd, pos, n, prefix, flow, i, done[i], self.read_timeout)
+        done[i] += got
+        if h is not None:
+            h._advance(i, done[i])
+        if err:
+            r.close()
+            raise HTTPDownloadError(err)
+        r.complete = (n < 0 and eof) or (cl is not None and n == cl and len(prefix) <= cl)
+        if n < 0:
+            r.head.keep_alive = False             # close-delimited body
+        if end >= 0 and segs[i][0] + done[i] < end:
             raise HTTPDownloadError("connection closed early")
 
 
@@ -406,6 +520,9 @@ class DownloadHandle:
         self._error: BaseException | None = None
         self._complete = False
         self._read_fd: int | None = None
+        relay = rawhttp.relay_module()
+        # native progress shared with the relay pumps (None without the extension)
+        self.flow = relay.Flow([(st, en, d) for st, en, d in segs]) if relay is not None else None
 
     @classmethod
     def finished(cls, dst: str, size: int) -> "DownloadHandle":
@@ -420,6 +537,8 @@ class DownloadHandle:
     def watermark(self) -> int:
         if self._complete:
             return self.size or 0
+        if self.flow is not None:
+            return self.flow.watermark()
         w = 0
         for (start, end, _d), done in zip(self.segs, self.done):
             w = start + done
@@ -430,16 +549,43 @@ class DownloadHandle:
     def _progressed(self) -> None:
         self._event.set()
 
+    def _advance(self, i: int, done: int) -> None:
+        if self.flow is not None:
+            self.flow.advance(i, done)
+        self._event.set()
+
+    def seg_done(self, i: int) -> int:
+        """Bytes of segment i on disk (the native pump advances the flow
+        while it runs; ``done`` catches up when it returns)."""
+        d = self.done[i]
+        return max(d, self.flow.done(i)) if self.flow is not None else d
+
     def _fail(self, e: BaseException) -> None:
         self._error = e
+        if self.flow is not None:
+            self.flow.fail(str(e) or type(e).__name__)
         self._event.set()
 
     def _finish(self, total: int) -> None:
         self.size = total
         self._complete = True
+        if self.flow is not None:
+            self.flow.finish(total)
         self._event.set()
 
     async def wait_bytes(self, n: int) -> None:
+        if self.flow is not None and not self._complete:
+            loop = asyncio.get_running_loop()
+            while True:
+                if self._error is not None:
+                    raise HTTPDownloadError(f"source transfer failed: {self._error}")
+                r = await loop.run_in_executor(None, self.flow.wait_covered, 0, n, 0.5)
+                if r == 0:
+                    return
+                if r == 1:
+                    raise HTTPDownloadError(f"source transfer failed: {self._error or self.flow.error}")
+                if r == 3:
+                    raise HTTPDownloadError("source shorter than expected")
         while self.watermark() < n:
             if self._error is not None:
                 raise HTTPDownloadError(f"source transfer failed: {self._error}")
@@ -462,6 +608,8 @@ class DownloadHandle:
             await self.task
 
     def cancel(self) -> None:
+        if self.flow is not None:
+            self.flow.cancel()             # stops native pumps blocked on this download
         if self.task is not None and not self.task.done():
             self.task.cancel()
 

@@ -26,6 +26,7 @@ from yarl import URL
 
 from ..ops import hashing
 from ..utils.backoff import ExponentialBackoff
+from ..utils import rawhttp
 from ..utils.log import log
 from . import sigv4
 from .credentials import Chain, Provider, Value, default_chain
@@ -77,7 +78,8 @@ class S3Client:
     def __init__(self, endpoint: Endpoint | str, creds: Provider | None = None, *, region: str = "us-east-1",
                  lookup: str = "auto", payload_mode: str = "auto", part_size: int = 64 << 20,
                  multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
-                 io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None) -> None:
+                 io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
+                 native: bool = True, sign_threads: int = 4) -> None:
         self.ep = Endpoint.parse(endpoint) if isinstance(endpoint, str) else endpoint
         self.creds = creds or default_chain()
         self.region = region
@@ -90,6 +92,10 @@ class S3Client:
         self.io_block = max(io_block, sigv4.STREAM_CHUNK)
         self._session = session
         self._own_session = session is None
+        # native data plane (csrc/relay): file/fd PUT bodies over plain http
+        self.native = native
+        self.sign_threads = sign_threads
+        self._raw = rawhttp.Pool()
 
     async def _sess(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
@@ -100,6 +106,7 @@ class S3Client:
         return self._session
 
     async def close(self) -> None:
+        self._raw.close()
         if self._own_session and self._session is not None:
             await self._session.close()
             self._session = None
@@ -206,11 +213,13 @@ class S3Client:
 
     # ------------------------------------------------------------ objects
     async def put_object(self, bucket: str, key: str, src: str | bytes | int, size: int | None = None,
-                         content_type: str = "application/octet-stream", wait_bytes=None) -> str:
+                         content_type: str = "application/octet-stream", wait_bytes=None, flow=None) -> str:
         """Upload a file path or fd (streamed) or bytes; returns the ETag.
 
         ``wait_bytes(n)`` (optional coroutine) is awaited before bytes < n are
-        read — lets the upload follow a file that is still being downloaded."""
+        read — lets the upload follow a file that is still being downloaded.
+        ``flow`` (a native ``_relay.Flow`` of that download) lets the native
+        send pump follow it without coming back to Python."""
         if size is None:
             if isinstance(src, (bytes, bytearray)):
                 size = len(src)
@@ -219,19 +228,23 @@ class S3Client:
             else:
                 size = os.path.getsize(src)
         if size >= self.multipart_threshold and size > self.part_size:
-            return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes)
+            return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes, flow)
         return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type},
-                                     wait_bytes=wait_bytes)
+                                     wait_bytes=wait_bytes, flow=flow)
 
     async def _put_range(self, bucket: str, key: str, src: str | bytes | int, offset: int, length: int,
-                         headers: dict, query: dict | None = None, wait_bytes=None) -> str:
+                         headers: dict, query: dict | None = None, wait_bytes=None, flow=None) -> str:
         mode = self._payload_mode()
+        relay = rawhttp.relay_module() if self.native else None
+        if relay is not None and not self.ep.secure and mode in ("streaming", "unsigned") and \
+                not isinstance(src, (bytes, bytearray, memoryview)) and (flow is not None or wait_bytes is None):
+            return await self._put_native(relay, bucket, key, src, offset, length, headers, query, mode, flow)
         factory = _BodyFactory(self, src, offset, length, mode, wait_bytes)
         _st, rh, _b = await self._do("PUT", bucket, key, query=query, headers=headers, body_factory=factory)
         return rh.get("ETag", "").strip('"')
 
     async def _put_multipart(self, bucket: str, key: str, src: str | bytes | int, size: int, content_type: str,
-                             wait_bytes=None) -> str:
+                             wait_bytes=None, flow=None) -> str:
         _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
                                        headers={"content-type": content_type}, body=b"")
         root = ET.fromstring(body)
@@ -248,7 +261,7 @@ class S3Client:
                 ln = min(self.part_size, size - off)
                 etags[i] = await self._put_range(bucket, key, src, off, ln, {},
                                                  query={"partNumber": str(i + 1), "uploadId": upload_id},
-                                                 wait_bytes=wait_bytes)
+                                                 wait_bytes=wait_bytes, flow=flow)
         try:
             await asyncio.gather(*(one(i) for i in range(nparts)))
             xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
@@ -266,6 +279,87 @@ class S3Client:
             except Exception:
                 pass
             raise
+
+    async def _put_native(self, relay, bucket: str, key: str, src: str | int, offset: int, length: int,
+                          headers: dict, query: dict | None, mode: str, flow) -> str:
+        """One PUT whose body never enters Python: the head is signed here,
+        then ``_relay.send_body`` writes head + body (aws-chunked with chunk
+        signatures hashed on a native pool, or sendfile for unsigned) from the
+        file straight to the socket; the reply is parsed here.  Same retry
+        policy as :meth:`_do` (connection errors and 5xx)."""
+        loop = asyncio.get_running_loop()
+        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
+        fd = os.dup(src) if isinstance(src, int) else os.open(src, os.O_RDONLY)
+        attempt = 0
+        try:
+            while True:
+                attempt += 1
+                cred = self._creds()
+                m = "unsigned" if (cred.anonymous and mode == "streaming") else mode
+                host, path = self._target(bucket, key)
+                amzdate, _ = sigv4.amz_dates()
+                hdrs = {"host": host, "x-amz-date": amzdate}
+                hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
+                if m == "streaming":
+                    hdrs.update({"content-encoding": "aws-chunked", "x-amz-decoded-content-length": str(length),
+                                 "content-length": str(sigv4.chunked_length(length))})
+                    hdrs["x-amz-content-sha256"] = sigv4.STREAMING_PAYLOAD
+                else:
+                    hdrs["content-length"] = str(length)
+                    hdrs["x-amz-content-sha256"] = sigv4.UNSIGNED_PAYLOAD
+                signed = None
+                if not cred.anonymous:
+                    if cred.session_token:
+                        hdrs["x-amz-security-token"] = cred.session_token
+                    signed = sigv4.sign("PUT", path, query, hdrs, hdrs["x-amz-content-sha256"], cred.access_key_id,
+                                        cred.secret_access_key, self.region, amzdate, path_is_encoded=True)
+                    hdrs["authorization"] = signed.authorization
+                target = path + (("?" + sigv4.canonical_query(query)) if query else "")
+                send = {"Host": host, **{k: v for k, v in hdrs.items() if k != "host"}}
+                head = rawhttp.request_head("PUT", target, send)
+                chost, cport = rawhttp.split_host(host)
+                err: Exception | None = None
+                sock = None
+                try:
+                    sock, reused = await self._raw.connect(chost, cport)
+                    sent, _last, perr = await loop.run_in_executor(
+                        None, relay.send_body, sock.fileno(), head, fd, offset, length, flow,
+                        1 if m == "streaming" else 0, signed.key if signed else b"", amzdate,
+                        signed.scope if signed else "", signed.signature if signed else "", sigv4.STREAM_CHUNK,
+                        self.sign_threads, 300.0)
+                    if perr and ("source" in perr or perr == "cancelled"):
+                        raise S3Error(0, "SourceFailed", perr, f"PUT {path}")
+                    try:
+                        resp = await rawhttp.read_head(sock, 1.0 if perr else 300.0)
+                    except rawhttp.RawHTTPError:
+                        if perr:
+                            if reused and sent == 0:
+                                attempt -= 1          # stale keep-alive socket: not a real attempt
+                            raise rawhttp.RawHTTPError(perr)
+                        raise
+                    body = await rawhttp.read_small_body(sock, resp, 60.0, method="PUT")
+                    if resp.status == 200 and not perr:
+                        if resp.keep_alive:
+                            self._raw.release(chost, cport, sock)
+                            sock = None
+                        return resp.headers.get("ETag", "").strip('"')
+                    err = _parse_error(resp.status, body, f"PUT {path}")
+                    if resp.status < 500 or attempt > self.max_retries:
+                        raise err
+                except (rawhttp.RawHTTPError, OSError, asyncio.TimeoutError) as e:
+                    if attempt > self.max_retries:
+                        raise S3Error(0, "ConnectionError", str(e), f"PUT {path}") from e
+                    err = e
+                finally:
+                    if sock is not None:
+                        sock.close()
+                if attempt <= 0:
+                    continue
+                d = pol.next_delay() or 1.0
+                log.with_fields(error=str(err), attempt=attempt).warn("s3 request failed; retrying in %.2fs", d)
+                await asyncio.sleep(d)
+        finally:
+            os.close(fd)
 
     async def get_object(self, bucket: str, key: str) -> bytes:
         _st, _h, b = await self._do("GET", bucket, key)

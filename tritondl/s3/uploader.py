@@ -99,14 +99,15 @@ class Uploader:
 
         return list(await asyncio.gather(*(one(f) for f in files)))
 
-    async def upload_stream(self, media_id: str, name: str, src: int | str, size: int, wait_bytes=None
-                            ) -> UploadResult:
-        """Upload one file that may still be growing (``wait_bytes`` gates reads)."""
+    async def upload_stream(self, media_id: str, name: str, src: int | str, size: int, wait_bytes=None,
+                            flow=None) -> UploadResult:
+        """Upload one file that may still be growing (``wait_bytes`` gates reads;
+        ``flow`` is the download's native progress, followed without Python)."""
         await self.ensure_bucket()
         key = object_key(media_id, name)
         log.info("starting upload of file '%s'", go_base(key))
         try:
-            etag = await self.client.put_object(self.bucket, key, src, size, wait_bytes=wait_bytes)
+            etag = await self.client.put_object(self.bucket, key, src, size, wait_bytes=wait_bytes, flow=flow)
         except (S3Error, OSError) as e:
             raise UploadError(f"failed to upload file {name}: {e}") from e
         log.info("finished upload")

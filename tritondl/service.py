@@ -247,7 +247,8 @@ class Service:
         fd = None
         if h.size and go_ext(h.filename) in MEDIA_EXTS:
             fd = h.open_reader()
-            up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes))
+            up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes,
+                                                                   flow=h.flow))
         try:
             await h.wait()
             if marks is not None:
