@@ -35,6 +35,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -48,6 +49,18 @@ namespace tritondl_relay {
 using Clock = std::chrono::steady_clock;
 
 inline double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
+// Timed condition wait used only as a polling slice.  system_clock-based
+// (pthread_cond_timedwait): libstdc++'s steady-clock wait_for goes through
+// pthread_cond_clockwait, which ThreadSanitizer does not intercept (false
+// "double lock" reports in the sanitizer self-test).
+template <class Pred>
+inline bool cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& l, int ms, Pred pred) {
+  return cv.wait_until(l, std::chrono::system_clock::now() + std::chrono::milliseconds(ms), pred);
+}
+inline void cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& l, int ms) {
+  cv.wait_until(l, std::chrono::system_clock::now() + std::chrono::milliseconds(ms));
+}
 
 // ---------------------------------------------------------------------------
 // Flow: progress of one download made of contiguous segments
@@ -131,7 +144,7 @@ class Flow {
       if (abort && abort->load()) return 1;
       if (Clock::now() >= deadline) return 2;
       // short slices so an aborting caller (the upload pump's sender) is seen promptly
-      cv_.wait_for(l, std::chrono::milliseconds(20));
+      cv_wait_ms(cv_, l, 20);
     }
   }
 
@@ -664,10 +677,10 @@ inline size_t parse_frames(const char* raw, size_t have, std::vector<RawFrame>* 
   return pos;
 }
 
-inline VerifyResult recv_verify_chunked(int sock, uint64_t raw_len, const char* prefix, size_t plen,
-                                        const std::string& key, const std::string& amzdate, const std::string& scope,
-                                        const std::string& seed, bool keep, int threads, double idle_timeout,
-                                        size_t window = 4u << 20) {
+inline VerifyResult recv_verify_windowed(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+                                         const std::string& key, const std::string& amzdate, const std::string& scope,
+                                         const std::string& seed, bool keep, int threads, double idle_timeout,
+                                         size_t window = 4u << 20) {
   VerifyResult r;
   Buf buf[2];
   int cur = 0;
@@ -776,6 +789,178 @@ inline VerifyResult recv_verify_chunked(int sock, uint64_t raw_len, const char* 
   if (r.err.empty() && !verr.empty()) r.err = verr;
   if (r.err.empty() && (have != 0 || received != raw_len)) r.err = "trailing bytes after final chunk";
   return r;
+}
+
+// Streamed variant for bodies that fit one buffer (every PUT / part our
+// client sends): the receiver thread lands bytes contiguously, parses frames
+// as soon as they are complete and publishes them; a per-request hasher pool
+// hashes published frames in place; the receiver checks the signature chain
+// in order as hashes become ready.  The last frame's hash + HMAC is all that
+// remains after the last byte arrives.
+struct StreamFrame {
+  size_t off, n, sig;
+  unsigned char h[32];
+  std::atomic<uint8_t> ready{0};
+};
+
+inline VerifyResult recv_verify_stream(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+                                       const std::string& key, const std::string& amzdate, const std::string& scope,
+                                       const std::string& seed, bool keep, int threads, double idle_timeout) {
+  VerifyResult r;
+  Buf whole(static_cast<size_t>(raw_len) + 1);
+  char* raw = whole.data();
+  const size_t pre = static_cast<size_t>(std::min<uint64_t>(plen, raw_len));
+  std::memcpy(raw, prefix, pre);
+  size_t have = pre, parsed = 0;
+  constexpr size_t kB = 1024;                                        // frames per table block
+  const size_t max_frames = static_cast<size_t>(raw_len / 86) + 2;  // a frame is >= 86 bytes
+  std::vector<std::unique_ptr<StreamFrame[]>> blocks((max_frames + kB - 1) / kB);
+  auto frame = [&](size_t j) -> StreamFrame& { return blocks[j / kB][j % kB]; };
+  std::mutex mu;
+  std::condition_variable cv_pub, cv_ready;
+  size_t published = 0;  // guarded by mu
+  bool parse_done = false, stop = false;
+  std::atomic<size_t> next{0};
+  bool final_seen = false;
+
+  auto hasher = [&] {
+    for (;;) {
+      const size_t j = next.fetch_add(1);
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv_pub.wait(l, [&] { return stop || j < published || parse_done; });
+        if (stop || j >= published) return;
+      }
+      StreamFrame& f = frame(j);
+      unsigned int len = 32;
+      EVP_Digest(f.n ? raw + f.off : "", f.n, f.h, &len, tritondl_hash::sha256_md(), nullptr);
+      f.ready.store(1, std::memory_order_release);
+      {
+        std::lock_guard<std::mutex> l(mu);  // pairs with the checker's wait
+      }
+      cv_ready.notify_one();
+    }
+  };
+  const int nthreads = std::max(1, threads <= 0 ? 4 : threads);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nthreads; ++t) pool.emplace_back(hasher);
+
+  ChunkSigner signer(key, amzdate, scope, seed);
+  size_t checked = 0;
+  auto check_ready = [&](bool wait_all) -> bool {
+    for (;;) {
+      size_t pub;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        pub = published;
+        if (wait_all && checked < pub && !frame(checked).ready.load(std::memory_order_acquire))
+          cv_wait_ms(cv_ready, l, 5, [&] { return frame(checked).ready.load(std::memory_order_acquire) != 0; });
+      }
+      while (checked < pub && frame(checked).ready.load(std::memory_order_acquire)) {
+        StreamFrame& f = frame(checked);
+        if (std::memcmp(signer.next(tritondl_hash::hex(std::string(reinterpret_cast<char*>(f.h), 32))).data(),
+                        raw + f.sig, 64) != 0)
+          return false;
+        ++checked;
+      }
+      if (!wait_all || checked >= pub) return true;
+    }
+  };
+
+  auto last = Clock::now();
+  bool sig_ok = true;
+  while (r.err.empty()) {
+    // parse every complete frame in [parsed, have)
+    std::vector<RawFrame> fr;
+    std::string perr;
+    bool fin = false;
+    const size_t end = parsed + parse_frames(raw + parsed, have - parsed, &fr, &fin, &perr);
+    if (!perr.empty()) {
+      r.err = perr;
+      break;
+    }
+    if (!fr.empty()) {
+      std::lock_guard<std::mutex> l(mu);
+      for (const RawFrame& x : fr) {
+        const size_t j = published;
+        if (j >= max_frames) {
+          r.err = "too many chunks";
+          break;
+        }
+        if (!blocks[j / kB]) blocks[j / kB].reset(new StreamFrame[kB]);
+        StreamFrame& f = frame(j);
+        f.off = parsed + x.off;
+        f.n = x.n;
+        f.sig = parsed + x.sig;
+        r.decoded += x.n;
+        ++published;
+      }
+      parsed = end;
+    }
+    if (!fr.empty()) cv_pub.notify_all();
+    if (!r.err.empty()) break;
+    if (fin) {
+      final_seen = true;
+      break;
+    }
+    if (!(sig_ok = check_ready(false))) break;
+    if (have >= raw_len) {
+      r.err = "truncated chunk";
+      break;
+    }
+    const ssize_t n = ::recv(sock, raw + have, static_cast<size_t>(raw_len - have), MSG_DONTWAIT);
+    if (n > 0) {
+      have += static_cast<size_t>(n);
+      last = Clock::now();
+      continue;
+    }
+    if (n == 0) {
+      r.err = "client closed inside the request body";
+      break;
+    }
+    if (errno == EINTR) continue;
+    if (errno != EAGAIN && errno != EWOULDBLOCK) {
+      r.err = errno_str("recv");
+      break;
+    }
+    if (since(last) > idle_timeout) {
+      r.err = "read timeout";
+      break;
+    }
+    if (wait_fd(sock, POLLIN, 50) < 0) r.err = "socket error while receiving";
+  }
+  {
+    std::lock_guard<std::mutex> l(mu);
+    parse_done = true;
+    if (!r.err.empty() || !sig_ok) stop = true;
+  }
+  cv_pub.notify_all();
+  if (r.err.empty() && sig_ok) sig_ok = check_ready(true);
+  {
+    std::lock_guard<std::mutex> l(mu);
+    stop = true;
+  }
+  cv_pub.notify_all();
+  for (auto& t : pool) t.join();
+  if (r.err.empty() && !sig_ok) r.err = "chunk signature mismatch";
+  if (r.err.empty() && (!final_seen || parsed != raw_len || have != raw_len)) r.err = "trailing bytes after final chunk";
+  if (r.err.empty() && keep) {
+    r.data.resize(static_cast<size_t>(r.decoded));
+    size_t o = 0;
+    for (size_t j = 0; j < published; ++j) {
+      std::memcpy(&r.data[o], raw + frame(j).off, frame(j).n);
+      o += frame(j).n;
+    }
+  }
+  return r;
+}
+
+inline VerifyResult recv_verify_chunked(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+                                        const std::string& key, const std::string& amzdate, const std::string& scope,
+                                        const std::string& seed, bool keep, int threads, double idle_timeout) {
+  if (raw_len <= (uint64_t(256) << 20))
+    return recv_verify_stream(sock, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
+  return recv_verify_windowed(sock, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
 }
 
 // Exact on-the-wire size of an aws-chunked body of `len` payload bytes.

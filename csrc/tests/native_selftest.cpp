@@ -9,7 +9,14 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <thread>
+
 #include "../hash/hash_core.h"
+#include "../relay/relay_core.h"
 #include "../utp/utp_engine.h"
 
 using namespace tritondl_hash;
@@ -178,12 +185,73 @@ static void test_merkle() {
   rmdir(dir);
 }
 
+// Relay pumps over a socketpair: the chunked sender follows a Flow advanced by
+// a writer thread while the streamed verifier checks every signature — the
+// three-party hand-off (writer / hasher pool / sender, receiver / hasher
+// pool / checker) is what TSan is here for.
+static void test_relay(size_t size) {
+  using namespace tritondl_relay;
+  std::mt19937 rng(11);
+  std::string data(size, '\0');
+  for (auto& c : data) c = static_cast<char>(rng());
+  char path[] = "/tmp/tdl_relayXXXXXX";
+  const int wfd = ::mkstemp(path);
+  CHECK(wfd >= 0);
+  CHECK(::ftruncate(wfd, static_cast<off_t>(size)) == 0);
+  const int rfd = ::open(path, O_RDONLY);
+  int sv[2];
+  CHECK(::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  ::fcntl(sv[0], F_SETFL, O_NONBLOCK);
+  ::fcntl(sv[1], F_SETFL, O_NONBLOCK);
+  const std::string key(32, 'k'), amz = "20260101T000000Z", scope = "20260101/us-east-1/s3/aws4_request",
+                    seed(64, '0');
+  Flow flow({{0, static_cast<int64_t>(size), 0}});
+  std::thread writer([&] {
+    for (size_t off = 0; off < size; off += 100000) {
+      const size_t n = std::min<size_t>(100000, size - off);
+      std::string e;
+      CHECK(pwrite_full(wfd, data.data() + off, n, off, &e));
+      flow.advance(0, off + n);
+    }
+    flow.finish(size);
+  });
+  VerifyResult vr;
+  const uint64_t raw_len = chunked_length(size, 65536);
+  std::thread receiver([&] { vr = recv_verify_chunked(sv[1], raw_len, "", 0, key, amz, scope, seed, true, 3, 10.0); });
+  SendResult sr = send_body(sv[0], "", rfd, 0, size, &flow, 1, key, amz, scope, seed, 65536, 3, 10.0);
+  writer.join();
+  receiver.join();
+  CHECK(sr.err.empty());
+  CHECK(vr.err.empty());
+  CHECK(vr.data == data);
+  // receive pump into a file, plain sender with sendfile
+  char opath[] = "/tmp/tdl_relayoutXXXXXX";
+  const int ofd = ::mkstemp(opath);
+  Flow f2({{0, static_cast<int64_t>(size), 0}});
+  RecvResult rr;
+  std::thread rcv([&] { rr = recv_body(sv[1], ofd, 0, static_cast<int64_t>(size), "", 0, &f2, 0, 0, 10.0); });
+  SendResult ps = send_body(sv[0], "", rfd, 0, size, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
+  rcv.join();
+  CHECK(ps.err.empty() && rr.err.empty() && rr.received == size && f2.watermark() == size);
+  std::string back(size, '\0');
+  CHECK(pread_full(ofd, &back[0], size, 0) == size && back == data);
+  ::close(sv[0]);
+  ::close(sv[1]);
+  ::close(wfd);
+  ::close(rfd);
+  ::close(ofd);
+  ::unlink(path);
+  ::unlink(opath);
+}
+
 int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
   test_aws_chunked();
   test_pieces_and_verify();
   test_merkle();
+  test_relay(quick ? (1u << 20) + 777 : (8u << 20) + 777);
+  test_relay(0);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
   if (failures) {

@@ -76,11 +76,12 @@ async def _fetch(origin: str, size: int, reps: int, work: str) -> dict:
     return _stats(ts[2:], size)
 
 
-async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str, make_bucket: bool = True) -> dict:
+async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str, make_bucket: bool = True,
+                  single: bool = False) -> dict:
     p = os.path.join(work, "src.mkv")
     with open(p, "wb") as f:
         f.write(os.urandom(size))
-    c = S3Client(s3_url, Static(AK, SK), payload_mode=mode)
+    c = S3Client(s3_url, Static(AK, SK), payload_mode=mode, **({"multipart_threshold": 1 << 62} if single else {}))
     ts = []
     try:
         if make_bucket and not await c.bucket_exists("bd"):
@@ -124,7 +125,8 @@ async def _upload_null(size: int, reps: int, work: str, mode: str) -> dict:
     srv = await asyncio.get_running_loop().create_server(_NullSink, "127.0.0.1", 0)
     try:
         port = srv.sockets[0].getsockname()[1]
-        return await _upload(f"http://127.0.0.1:{port}", size, reps, work, mode, make_bucket=False)
+        # the sink speaks no multipart XML: large files go as one PUT (single-stream client rate)
+        return await _upload(f"http://127.0.0.1:{port}", size, reps, work, mode, make_bucket=False, single=True)
     finally:
         srv.close()
 
@@ -141,11 +143,29 @@ def _sign(size: int, reps: int) -> dict:
     return _stats(ts[2:], size)
 
 
+def _trace_summary() -> dict:
+    """Median time of each traced data-plane event relative to its job's start."""
+    from tritondl.utils import rawhttp
+    tr = rawhttp.TRACE or []
+    rel: dict[str, list[float]] = {}
+    t0 = None
+    for ev, t in tr:
+        if ev == "job_start":
+            t0 = t
+            continue
+        if t0 is not None:
+            rel.setdefault(ev, []).append(t - t0)
+    return {k: round(statistics.median(v) * 1e3, 3) for k, v in rel.items()}
+
+
 async def _job(size: int, reps: int) -> dict:
+    from tritondl.utils import rawhttp
     st = JobStack(file_size=size)
     await st.setup()
     try:
         await st.run_jobs(3)
+        if rawhttp.TRACE is not None:
+            rawhttp.TRACE.clear()
         dt = await st.run_jobs(reps)
         res = st.svc.results[-reps:]  # type: ignore[union-attr]
         spans: dict[str, list[float]] = {}
@@ -155,7 +175,8 @@ async def _job(size: int, reps: int) -> dict:
     finally:
         await st.teardown()
     return {"ms_per_job": round(dt / reps * 1e3, 3),
-            "spans_ms_p50": {k: round(statistics.median(v) * 1e3, 3) for k, v in spans.items()}}
+            "spans_ms_p50": {k: round(statistics.median(v) * 1e3, 3) for k, v in spans.items()},
+            "trace_ms_p50": _trace_summary()}
 
 
 async def main() -> None:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Build and run csrc/tests/native_selftest.cpp (host C++ cores: hashing,
-aws-chunked signing, threaded piece verification, uTP engine).
+aws-chunked signing, threaded piece verification, the relay pumps, uTP engine).
 
     python tools/native_selftest.py              # plain -O2 build
     python tools/native_selftest.py --sanitize   # ASan+UBSan build, then TSan build

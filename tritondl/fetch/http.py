@@ -489,8 +489,10 @@ class HTTPDownloader:
             n = cl if cl is not None else -1
         prefix, r.leftover = r.leftover, b""
         flow = h.flow if h is not None else None
+        rawhttp.trace("get_pump_start")
         got, eof, err = await asyncio.get_running_loop().run_in_executor(
             None, relay.recv_body, r.sock.fileno(), fd, pos, n, prefix, flow, i, done[i], self.read_timeout)
+        rawhttp.trace("get_pump_end")
         done[i] += got
         if h is not None:
             h._advance(i, done[i])

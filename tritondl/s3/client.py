@@ -322,6 +322,7 @@ class S3Client:
                 sock = None
                 try:
                     sock, reused = await self._raw.connect(chost, cport)
+                    rawhttp.trace("put_pump_start")
                     sent, _last, perr = await loop.run_in_executor(
                         None, relay.send_body, sock.fileno(), head, fd, offset, length, flow,
                         1 if m == "streaming" else 0, signed.key if signed else b"", amzdate,
@@ -337,7 +338,9 @@ class S3Client:
                                 attempt -= 1          # stale keep-alive socket: not a real attempt
                             raise rawhttp.RawHTTPError(perr)
                         raise
+                    rawhttp.trace("put_pump_end")
                     body = await rawhttp.read_small_body(sock, resp, 60.0, method="PUT")
+                    rawhttp.trace("put_response")
                     if resp.status == 200 and not perr:
                         if resp.keep_alive:
                             self._raw.release(chost, cport, sock)

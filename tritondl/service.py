@@ -40,6 +40,7 @@ from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
 from .s3.uploader import Uploader
 from .select import MEDIA_EXTS, dir_media
+from .utils import rawhttp
 from .utils.config import Config
 from .utils.gocompat import go_ext, go_time_string
 from .utils.log import log
@@ -93,6 +94,7 @@ class Service:
         self._stop = asyncio.Event()
         self._inflight = 0
         self._metrics_runner = None
+        self._cleanups: set[asyncio.Future] = set()
         self.results: list[JobResult] = []
 
     # ------------------------------------------------------------ lifecycle
@@ -161,6 +163,7 @@ class Service:
     async def handle(self, msg: Delivery) -> JobResult:
         """Process one delivery end-to-end; always settles it."""
         t0 = time.monotonic()
+        rawhttp.trace("job_start")
         try:
             job = Download.decode(msg.body)
             if job.media is None:
@@ -218,7 +221,16 @@ class Service:
             await self._dispose_failed(msg, stage, e)
             return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
         if self.cfg.cleanup:
-            await asyncio.get_running_loop().run_in_executor(None, shutil.rmtree, dl_dir, True)
+            # the job is settled: move its dir aside (one rename, so a redelivered job with the
+            # same id starts clean) and delete it off the critical path (drained on shutdown)
+            trash = f"{dl_dir}.deleting-{os.getpid()}-{id(msg):x}"
+            try:
+                os.rename(dl_dir, trash)
+            except OSError:
+                trash = dl_dir
+            c = asyncio.get_running_loop().run_in_executor(None, shutil.rmtree, trash, True)
+            self._cleanups.add(c)
+            c.add_done_callback(self._cleanups.discard)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -303,6 +315,8 @@ class Service:
             for t in pending:
                 with contextlib.suppress(BaseException):
                     await t
+        if self._cleanups:
+            await asyncio.gather(*self._cleanups, return_exceptions=True)
         if self.dispatcher is not None:
             await self.dispatcher.stop()
         if self.uploader is not None:

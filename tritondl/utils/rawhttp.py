@@ -25,6 +25,15 @@ from .log import log
 _relay = None
 _relay_checked = False
 
+# opt-in event trace of the data plane (TRITONDL_TRACE=1): (event, monotonic time)
+TRACE: list[tuple[str, float]] | None = [] if os.environ.get("TRITONDL_TRACE") else None
+
+
+def trace(event: str) -> None:
+    if TRACE is not None:
+        import time
+        TRACE.append((event, time.monotonic()))
+
 
 def relay_module():
     """The ``_relay`` extension, or None (not built / disabled by
