@@ -39,20 +39,21 @@ PYBIND11_MODULE(_relay, m) {
 
   m.def("recv_body",
         [](int sock, int fd, uint64_t off, int64_t length, const py::bytes& prefix, std::shared_ptr<Flow> flow,
-           size_t seg, uint64_t seg_done0, double idle_timeout, size_t buf_size) {
+           size_t seg, uint64_t seg_done0, double idle_timeout, size_t buf_size, bool use_splice) {
           std::string pre = prefix;
           RecvResult r;
           {
             py::gil_scoped_release nogil;
             r = recv_body(sock, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0, idle_timeout,
-                          buf_size);
+                          buf_size, use_splice);
           }
           return py::make_tuple(r.received, r.eof, r.err);
         },
         py::arg("sock"), py::arg("fd"), py::arg("offset"), py::arg("length"), py::arg("prefix"), py::arg("flow"),
         py::arg("seg") = 0, py::arg("seg_done0") = 0, py::arg("idle_timeout") = 120.0,
-        py::arg("buf_size") = 4u << 20,
-        "Stream a body into fd at offset; returns (received, eof, error).");
+        py::arg("buf_size") = 4u << 20, py::arg("splice") = true,
+        "Stream a body into fd at offset (splice socket->pipe->file when possible, else recv+pwrite); "
+        "returns (received, eof, error).");
 
   m.def("send_body",
         [](int sock, const py::bytes& head, int fd, uint64_t off, uint64_t length, std::shared_ptr<Flow> flow, int mode,

@@ -351,9 +351,92 @@ struct RecvResult {
   std::string err;
 };
 
+// Zero-user-copy receive: socket -> pipe (page references move) -> file
+// (one copy into the page cache).  Returns false when splice is unsupported
+// here (then nothing was consumed and the caller falls back to recv+pwrite).
+inline bool splice_body(int sock, int fd, uint64_t off, uint64_t want, RecvResult& r, Flow* flow, size_t seg,
+                        uint64_t seg_done0, double idle_timeout) {
+  int p[2];
+  if (::pipe2(p, O_CLOEXEC | O_NONBLOCK) != 0) return false;
+  ::fcntl(p[1], F_SETPIPE_SZ, 1 << 20);  // best effort; the default is 64 KiB
+  auto last = Clock::now();
+  size_t in_pipe = 0;
+  bool ok = true;
+  while (r.received < want && r.err.empty()) {
+    if (flow && flow->cancelled()) {
+      r.err = "cancelled";
+      break;
+    }
+    const size_t cap = static_cast<size_t>(std::min<uint64_t>(1u << 20, want - r.received));
+    const ssize_t n = ::splice(sock, nullptr, p[1], nullptr, cap, SPLICE_F_MOVE | SPLICE_F_NONBLOCK);
+    if (n > 0) {
+      in_pipe = static_cast<size_t>(n);
+      while (in_pipe) {
+        loff_t o = static_cast<loff_t>(off + r.received);
+        const ssize_t w = ::splice(p[0], nullptr, fd, &o, in_pipe, SPLICE_F_MOVE);
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          if (r.received == 0 && (errno == EINVAL || errno == ENOSYS)) {
+            ok = false;  // filesystem without splice-write support; bytes still sit in the pipe
+            break;
+          }
+          r.err = errno_str("splice to file");
+          break;
+        }
+        in_pipe -= static_cast<size_t>(w);
+        r.received += static_cast<uint64_t>(w);
+      }
+      if (!ok || !r.err.empty()) break;
+      if (flow) flow->advance(seg, seg_done0 + r.received);
+      last = Clock::now();
+      continue;
+    }
+    if (n == 0) {
+      r.eof = true;
+      if (want != UINT64_MAX) r.err = "connection closed early";
+      break;
+    }
+    if (errno == EINTR) continue;
+    if (errno == EINVAL && r.received == 0) {
+      ok = false;  // socket type without splice support
+      break;
+    }
+    if (errno != EAGAIN && errno != EWOULDBLOCK) {
+      r.err = errno_str("splice from socket");
+      break;
+    }
+    if (since(last) > idle_timeout) {
+      r.err = "read timeout";
+      break;
+    }
+    if (wait_fd(sock, POLLIN, 50) < 0) r.err = "socket error while receiving";
+  }
+  if (!ok && in_pipe) {
+    // the file refused splice: move what sits in the pipe with read + pwrite
+    Buf tmp(in_pipe);
+    size_t left = in_pipe;
+    while (left && r.err.empty()) {
+      const ssize_t got = ::read(p[0], tmp.data(), left);
+      if (got <= 0) {
+        if (got < 0 && errno == EINTR) continue;
+        r.err = "pipe drain failed";
+        break;
+      }
+      if (pwrite_full(fd, tmp.data(), static_cast<size_t>(got), off + r.received, &r.err)) {
+        r.received += static_cast<uint64_t>(got);
+        left -= static_cast<size_t>(got);
+      }
+    }
+    if (flow) flow->advance(seg, seg_done0 + r.received);
+  }
+  ::close(p[0]);
+  ::close(p[1]);
+  return ok;  // false: caller continues with recv + pwrite
+}
+
 inline RecvResult recv_body(int sock, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
                             Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout,
-                            size_t buf_size = 4u << 20) {
+                            size_t buf_size = 4u << 20, bool use_splice = true) {
   RecvResult r;
   const uint64_t want = length < 0 ? UINT64_MAX : static_cast<uint64_t>(length);
   if (prefix_len) {
@@ -361,6 +444,10 @@ inline RecvResult recv_body(int sock, int fd, uint64_t off, int64_t length, cons
     if (fd >= 0 && !pwrite_full(fd, prefix, n, off, &r.err)) return r;
     r.received = n;
     if (flow) flow->advance(seg, seg_done0 + r.received);
+  }
+  if (fd >= 0 && use_splice && r.received < want) {
+    if (splice_body(sock, fd, off, want, r, flow, seg, seg_done0, idle_timeout) || !r.err.empty() || r.eof)
+      return r;
   }
   Buf buf(std::max<size_t>(buf_size, 64 << 10));
   auto last = Clock::now();

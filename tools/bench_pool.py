@@ -8,7 +8,7 @@ the sharded queues, exactly the production launcher); this process publishes
 the jobs and counts the ``v1.convert`` messages.  Warm-up: one job per worker
 first, so every worker has connected and consumed before the clock starts.
 
-    python tools/bench_pool.py --workers 8 --jobs 100 --file-kb 1024
+    python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 1024   # 800 jobs
 """
 
 from __future__ import annotations
@@ -29,10 +29,12 @@ sys.path.insert(0, ROOT)
 async def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=8)
-    ap.add_argument("--jobs", type=int, default=100)
+    ap.add_argument("--jobs", type=int, default=0, help="total jobs (default: workers x jobs-per-worker)")
+    ap.add_argument("--jobs-per-worker", type=int, default=100)
     ap.add_argument("--file-kb", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     a = ap.parse_args()
+    a.jobs = a.jobs or a.workers * a.jobs_per_worker
     from tritondl.amqp.codec import Properties
     from tritondl.amqp.connection import Connection
     from tritondl.bench_job import AK, SK, Backend

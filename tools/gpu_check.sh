@@ -12,4 +12,4 @@ step bench_c4 300 python bench.py --steps 200 --warmup 20 --concurrency 4 &&
 step bench_bt_tcp 300 python tools/bench_bt.py --mb 1024 --seeds 4 &&
 step bench_bt_utp 300 python tools/bench_bt.py --mb 1024 --seeds 4 --utp &&
 step bench_1g 300 python bench.py --file-mb 1024 --steps 3 --warmup 1 &&
-step bench_pool8 300 python tools/bench_pool.py --workers 8 --jobs 100 --file-kb 1024
+step bench_pool8 300 python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 1024
