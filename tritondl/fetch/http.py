@@ -131,6 +131,10 @@ class HTTPDownloader:
         # native data plane (csrc/relay): plain-http bodies go socket -> file in C++
         self.native = native
         self.read_timeout = read_timeout
+        # splice(2) socket -> pipe -> file in the receive pump: one copy less, a win on ext4
+        # (3.6 vs 5.9 ms per 10 MiB) but slower on the MI355X box's overlayfs with 4 concurrent
+        # range streams (1 GiB fetch 154 vs 85 ms), so opt-in: TRITONDL_RELAY_SPLICE=1
+        self.splice = os.environ.get("TRITONDL_RELAY_SPLICE", "0").lower() in ("1", "on", "true", "yes")
         self._raw = rawhttp.Pool()
 
     def register(self) -> ClientRegister:
@@ -491,7 +495,8 @@ class HTTPDownloader:
         flow = h.flow if h is not None else None
         rawhttp.trace("get_pump_start")
         got, eof, err = await asyncio.get_running_loop().run_in_executor(
-            None, relay.recv_body, r.sock.fileno(), fd, pos, n, prefix, flow, i, done[i], self.read_timeout)
+            None, relay.recv_body, r.sock.fileno(), fd, pos, n, prefix, flow, i, done[i], self.read_timeout,
+            4 << 20, self.splice)
         rawhttp.trace("get_pump_end")
         done[i] += got
         if h is not None:
