@@ -26,6 +26,8 @@ PYBIND11_MODULE(_relay, m) {
       .def("cancel", &Flow::cancel)
       .def("done", &Flow::done, py::arg("seg"))
       .def("watermark", &Flow::watermark)
+      .def("covered_bytes", &Flow::covered_bytes, py::arg("start"), py::arg("end"))
+      .def("bytes_until_covered", &Flow::bytes_until_covered, py::arg("start"), py::arg("end"))
       .def_property_readonly("cancelled", &Flow::cancelled)
       .def_property_readonly("failed", &Flow::failed)
       .def_property_readonly("finished", &Flow::finished)

@@ -125,6 +125,37 @@ class Flow {
     return finished_;
   }
 
+  // How far the download still is from covering [a, b): each segment fills
+  // sequentially from its frontier, segments in parallel, so this is the
+  // largest number of bytes any one overlapping segment must still receive
+  // (0 = on disk).  Used to schedule multipart uploads in arrival order.
+  uint64_t bytes_until_covered(uint64_t a, uint64_t b) const {
+    std::lock_guard<std::mutex> l(mu_);
+    if (b <= a || finished_) return 0;
+    uint64_t worst = 0;
+    for (const Seg& s : segs_) {
+      const uint64_t s_end = s.end < 0 ? UINT64_MAX : static_cast<uint64_t>(s.end);
+      const uint64_t hi = std::min(b, s_end);
+      if (hi <= std::max(a, s.start)) continue;
+      const uint64_t frontier = s.start + s.done;
+      if (hi > frontier) worst = std::max(worst, hi - frontier);
+    }
+    return worst;
+  }
+
+  // Bytes of [a, b) already on disk (for scheduling uploads of ranges).
+  uint64_t covered_bytes(uint64_t a, uint64_t b) const {
+    std::lock_guard<std::mutex> l(mu_);
+    if (b <= a) return 0;
+    if (finished_) return std::min(b, total_) > a ? std::min(b, total_) - a : 0;
+    uint64_t got = 0;
+    for (const Seg& s : segs_) {
+      const uint64_t lo = std::max(a, s.start), hi = std::min(b, s.start + s.done);
+      if (hi > lo) got += hi - lo;
+    }
+    return got;
+  }
+
   // Length of the contiguous prefix on disk.
   uint64_t watermark() const {
     std::lock_guard<std::mutex> l(mu_);

@@ -63,6 +63,12 @@ def test_flow_coverage_and_states():
     assert f.done(1) == 100
     f.finish(230)
     assert f.wait_covered(0, 230, 0.0) == 0 and f.wait_covered(0, 231, 0.0) == 3
+    # multipart scheduling metric: bytes each overlapping segment still has to receive
+    m = relay.Flow([(0, 400, 0), (400, 800, 0)])
+    m.advance(0, 150)
+    assert m.bytes_until_covered(0, 100) == 0 and m.bytes_until_covered(100, 200) == 50
+    assert m.bytes_until_covered(400, 500) == 100 and m.bytes_until_covered(350, 450) == 250
+    assert m.covered_bytes(100, 500) == 50
     g = relay.Flow([(0, 10, 0)])
     threading.Timer(0.05, g.fail, args=("boom",)).start()
     assert g.wait_covered(0, 10, 5.0) == 1 and g.error == "boom"

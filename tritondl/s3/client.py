@@ -253,17 +253,28 @@ class S3Client:
             raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
         nparts = (size + self.part_size - 1) // self.part_size
         etags: list[str] = [""] * nparts
-        sem = asyncio.Semaphore(self.parallel_parts)
+        todo = list(range(nparts))
 
-        async def one(i: int) -> None:
-            async with sem:
+        def pick() -> int:
+            # Following a download: take the part that will be on disk soonest (a segmented
+            # download fills several regions at once; in part order the uploads would queue
+            # behind the first segment).  Otherwise in order.
+            if flow is None or len(todo) == 1:
+                return todo.pop(0)
+            best = min(range(len(todo)), key=lambda k: (flow.bytes_until_covered(
+                todo[k] * self.part_size, min(size, (todo[k] + 1) * self.part_size)), todo[k]))
+            return todo.pop(best)
+
+        async def worker() -> None:
+            while todo:
+                i = pick()
                 off = i * self.part_size
                 ln = min(self.part_size, size - off)
                 etags[i] = await self._put_range(bucket, key, src, off, ln, {},
                                                  query={"partNumber": str(i + 1), "uploadId": upload_id},
                                                  wait_bytes=wait_bytes, flow=flow)
         try:
-            await asyncio.gather(*(one(i) for i in range(nparts)))
+            await asyncio.gather(*(worker() for _ in range(min(self.parallel_parts, nparts))))
             xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
                           for i, e in enumerate(etags))
             cbody = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
