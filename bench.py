@@ -75,6 +75,11 @@ def main() -> int:
     ap.add_argument("--file-mb", type=float, default=10.0)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     ap.add_argument("--no-gpu-probe", action="store_true")
+    ap.add_argument("--probe-kb", type=int, default=-1,
+                    help="HTTP GET probe size in KiB, the rest as parallel Range streams "
+                         "(-1: worker default, 0: open-ended probe)")
+    ap.add_argument("--http-segments", type=int, default=0, help="max parallel Range streams (0: worker default)")
+    ap.add_argument("--sign-threads", type=int, default=0, help="S3 chunk hashers per PUT (0: worker default)")
     ap.add_argument("--log-level", default="warning")
     a = ap.parse_args()
 
@@ -103,11 +108,15 @@ def main() -> int:
 
     file_size = int(a.file_mb * 1024 * 1024)
     stack = JobStack(file_size=file_size, concurrency=a.concurrency, prefetch=max(1, a.concurrency),
-                     tag=f"r{rank}")
+                     tag=f"r{rank}", http_probe_bytes=(a.probe_kb << 10) if a.probe_kb >= 0 else -1,
+                     http_segments=a.http_segments, sign_threads=a.sign_threads)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
     try:
         loop.run_until_complete(stack.setup())
+        c = stack.cfg
+        knobs = {"http_probe_bytes": c.http_probe_bytes, "http_segments": c.http_segments,
+                 "s3_sign_threads": c.s3_sign_threads} if c is not None else {}
         if a.warmup:
             loop.run_until_complete(stack.run_jobs(a.warmup))
         barrier()
@@ -151,7 +160,8 @@ def main() -> int:
             "config": {"model": CONFIG_NAME if file_size == 10 << 20 else
                        f"Single HTTP download job via local RabbitMQ, {file_size / 2**20:g} MiB file", "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
-                       "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency)},
+                       "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
+                       **knobs},
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
             "job_latency_ms_p50": round(lat[len(lat) // 2] * 1000, 2) if lat else None,
             "job_latency_ms_p90": round(lat[int(len(lat) * 0.9)] * 1000, 2) if lat else None,

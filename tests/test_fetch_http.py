@@ -214,3 +214,46 @@ def test_get_probe_saves_a_round_trip(tmp_path):
         assert times["head"] - times["get"] > 0.1, times
         await o.stop()
     run(main())
+
+
+def test_bounded_probe_segments_mid_size_files(tmp_path):
+    """``probe_bytes``: the GET probe asks for ``bytes=0-(N-1)``; a bigger file's
+    rest is requested at once as up to ``segments`` Range streams, a file that
+    fits the probe stays one request, and a Range-ignoring origin still works."""
+    async def main():
+        o = await Origin().start()
+        pb = 512 * 1024
+        h = _dl(segments=4, probe_bytes=pb, write_block=256 * 1024)
+        data = os.urandom(3_000_000)
+        url = o.add("/mid.mkv", data)
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "mid.mkv").read_bytes() == data
+        rngs = [r[2] for r in o.requests if r[0] == "GET"]
+        assert rngs[0] == f"bytes=0-{pb - 1}"
+        assert len(rngs) == 5 and all(r.startswith("bytes=") for r in rngs)
+        small = os.urandom(100_000)
+        n = len(o.requests)
+        url2 = o.add("/small.mkv", small)
+        await h.download(str(tmp_path), Sink(), url2)
+        assert (tmp_path / "small.mkv").read_bytes() == small
+        assert len(o.requests[n:]) == 1
+        o.ranges = False
+        url3 = o.add("/plain.mkv", data)
+        n = len(o.requests)
+        await h.download(str(tmp_path), Sink(), url3)
+        assert (tmp_path / "plain.mkv").read_bytes() == data
+        assert len(o.requests[n:]) == 1
+        await h.close()
+        await o.stop()
+    run(main())
+
+
+def test_bounded_probe_plan_covers_file():
+    from tritondl.fetch.http import _Probe
+    h = HTTPDownloader(segments=4, probe_bytes=1000)
+    for size, first in ((999, 999), (1000, 1000), (1001, 1000), (2500, 1000), (10_007, 1000)):
+        p = _Probe(size=size, ranges=True, etag="", last_modified="", filename="f", status=206, first_end=first)
+        segs = h._plan(p)
+        assert segs[0][:2] == [0, first]
+        assert all(a[1] == b[0] for a, b in zip(segs, segs[1:]))
+        assert segs[-1][1] == size and len(segs) <= 5

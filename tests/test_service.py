@@ -36,7 +36,7 @@ def run(coro, timeout=90):
 
 
 class Env:
-    async def up(self, tmp_path, **cfgkw):
+    async def up(self, tmp_path, http=None, **cfgkw):
         self.broker = await Broker().start()
         self.origin = await Origin().start()
         self.s3 = await FakeS3(access_key="ak", secret_key="sk").start()
@@ -48,7 +48,7 @@ class Env:
         for k, v in cfgkw.items():
             setattr(cfg, k, v)
         self.cfg = cfg
-        http = HTTPDownloader(progress_interval=0.05, max_retries=1)
+        http = http or HTTPDownloader(progress_interval=0.05, max_retries=1)
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", tracker_min_interval=0.5,
                                              verify_device="cpu"), progress_interval=0.05, use_dht=False)
         self.svc = Service(cfg, amqp=Client(self.broker.url, heartbeat=0, retry_delay=0,

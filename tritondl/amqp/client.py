@@ -406,7 +406,11 @@ class Client:
                     if declare:
                         await self._ensure_publish_topology(exchange)
                     ch = await self._publisher()
-                    await ch.basic_publish(exchange, rk, body, props)
+                    # frames leave in order under the lock; the confirm is awaited outside
+                    # it, so concurrent jobs' publishes share broker round trips
+                    confirm = await ch.basic_publish(exchange, rk, body, props, wait_confirm=False)
+                if confirm is not None:
+                    await confirm
                 log.info("published message on topic %s", exchange)
                 return
             except (AMQPError, ConnectionError, OSError) as e:

@@ -82,6 +82,10 @@ class JobStack:
     workdir: str | None = None
     inproc: bool = False
     tag: str = "r0"
+    http_probe_bytes: int = -1       # -1: worker default (Config)
+    http_segments: int = 0           # 0: worker default
+    sign_threads: int = 0            # 0: worker default
+    cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
     producer: Connection | None = None
@@ -115,8 +119,16 @@ class JobStack:
         cfg.max_retries = 0
         cfg.progress_log_interval_s = 0
         cfg.heartbeat_s = 0
+        if self.http_probe_bytes >= 0:
+            cfg.http_probe_bytes = self.http_probe_bytes
+        if self.http_segments > 0:
+            cfg.http_segments = self.http_segments
+        if self.sign_threads > 0:
+            cfg.s3_sign_threads = self.sign_threads
+        self.cfg = cfg
         amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=0, retry_delay=0)
-        up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode="streaming"))
+        up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode="streaming",
+                                           sign_threads=cfg.s3_sign_threads))
         self.svc = Service(cfg, amqp=amqp, uploader=up)
         await self.svc.start()
         self.producer = await Connection.open(broker_url, heartbeat=0)

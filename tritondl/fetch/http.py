@@ -19,7 +19,11 @@ Beyond the reference:
   on completion, so a crash never leaves a truncated file that looks done,
   and ``If-Range`` guards against resuming onto a changed origin object;
 * large files are fetched as ``segments`` concurrent Range streams written
-  with ``pwrite`` from worker threads (grab used one stream);
+  with ``pwrite`` from worker threads (grab used one stream); with
+  ``probe_bytes`` (the worker's default, ``TRITONDL_HTTP_PROBE_BYTES``) the
+  probe is ``GET bytes=0-(probe_bytes-1)`` and the rest of a bigger file is
+  requested at once as parallel Range streams, so mid-size files are
+  segmented too and no half-read probe connection is dropped;
 * plain-``http`` bodies never enter Python: after the head is parsed the
   socket goes to the native receive pump (``csrc/relay``, GIL released),
   which writes the file and publishes progress on a native ``Flow`` that
@@ -89,6 +93,7 @@ class _Probe:
     last_modified: str
     filename: str
     status: int
+    first_end: int | None = None     # end (exclusive) of the GET probe's 206 body
 
 
 def filename_from_disposition(cd: str | None) -> str:
@@ -118,8 +123,13 @@ class HTTPDownloader:
     def __init__(self, *, progress_interval: float = 1.0, segments: int = 4, segment_threshold: int = 64 << 20,
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
-                 native: bool = True, read_timeout: float = 120.0) -> None:
+                 native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0) -> None:
         self.progress_interval = progress_interval
+        # >0: the GET probe asks for bytes=0-(probe_bytes-1); once its head names the
+        # size, the rest of a bigger file is requested at once as up to `segments`
+        # parallel Range streams (a file that fits stays one request).  0: open-ended
+        # probe, one stream below `segment_threshold` (grab's behaviour)
+        self.probe_bytes = max(0, probe_bytes)
         self.probe_mode = probe          # "get": ranged GET doubles as the probe; "head": grab-style HEAD first
         self.segments = max(1, segments)
         self.segment_threshold = segment_threshold
@@ -225,7 +235,8 @@ class HTTPDownloader:
         attempt = 0
         while True:
             try:
-                r = await self._open(url, {**self.headers, "Range": "bytes=0-"})
+                rng = f"bytes=0-{self.probe_bytes - 1}" if self.probe_bytes else "bytes=0-"
+                r = await self._open(url, {**self.headers, "Range": rng})
                 if r.status == 416:                      # empty resource: no satisfiable range
                     r.release()
                     r = await self._open(url, dict(self.headers))
@@ -249,11 +260,11 @@ class HTTPDownloader:
             r.release()
             raise
         if r.status == 206:
-            m = re.match(r"bytes (\d+)-\d+/(\d+)", r.headers.get("Content-Range", ""))
+            m = re.match(r"bytes (\d+)-(\d+)/(\d+)", r.headers.get("Content-Range", ""))
             if not m or m.group(1) != "0":
                 r.release()
                 raise HTTPDownloadError(f"GET {url}: bad Content-Range {r.headers.get('Content-Range')!r}")
-            p.size, p.ranges = int(m.group(2)), True
+            p.size, p.ranges, p.first_end = int(m.group(3)), True, int(m.group(2)) + 1
         return p, r
 
     def _probe_from(self, r: aiohttp.ClientResponse, url: str) -> _Probe:
@@ -366,6 +377,16 @@ class HTTPDownloader:
         """[[start, end_exclusive_or_-1, done], ...]"""
         if p.size is None:
             return [[0, -1, 0]]
+        if self.probe_bytes and p.ranges and p.first_end is not None:
+            # bounded GET probe: its body is segment 0; the rest goes to up to
+            # `segments` further Range streams, none shorter than the probe's body
+            if p.first_end >= p.size:
+                return [[0, p.size, 0]]
+            rest = p.size - p.first_end
+            k = max(1, min(self.segments, -(-rest // p.first_end)))
+            step = -(-rest // k)
+            return [[0, p.first_end, 0]] + [[p.first_end + i * step, min(p.size, p.first_end + (i + 1) * step), 0]
+                                            for i in range(k) if p.first_end + i * step < p.size]
         n = self.segments if (p.ranges and p.size >= self.segment_threshold) else 1
         step = -(-p.size // n)
         return [[i * step, min(p.size, (i + 1) * step), 0] for i in range(n) if i * step < p.size] or [[0, 0, 0]]
@@ -408,7 +429,7 @@ class HTTPDownloader:
                     except BaseException:
                         r.close()
                         raise
-                    if len(segs) == 1:
+                    if len(segs) == 1 or end == probe.first_end:
                         r.release()          # body read to its end: keep-alive connection back to the pool
                     else:
                         r.close()            # stopped mid-body at the segment boundary: drop it

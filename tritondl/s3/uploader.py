@@ -54,10 +54,11 @@ class Uploader:
     @classmethod
     def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "us-east-1",
                  part_size: int = 64 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
-                 env=None) -> "Uploader":
+                 env=None, sign_threads: int = 4) -> "Uploader":
         ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
         client = S3Client(ep, default_chain(env), region=region, part_size=part_size,
-                          multipart_threshold=multipart_threshold, parallel_parts=parallel_parts)
+                          multipart_threshold=multipart_threshold, parallel_parts=parallel_parts,
+                          sign_threads=sign_threads)
         return cls(bucket, client)
 
     async def ensure_bucket(self) -> None:

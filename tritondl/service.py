@@ -32,6 +32,7 @@ import shutil
 import signal
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
 from .amqp.client import Client, Delivery
@@ -50,7 +51,8 @@ from .utils.profiler import CPUProfiler
 
 def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
-    http = HTTPDownloader(progress_interval=cfg.progress_interval_s)
+    http = HTTPDownloader(progress_interval=cfg.progress_interval_s, segments=cfg.http_segments,
+                          segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes)
     impls: list[ClientImpl] = []
     try:
         from .fetch.bt.client import TorrentDownloader
@@ -100,6 +102,7 @@ class Service:
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
         cfg = self.cfg
+        self._size_executor()
         if self.amqp is None:
             if cfg.rabbitmq_endpoint_defaulted:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)
@@ -119,7 +122,8 @@ class Service:
             self.uploader = Uploader.from_env(cfg.bucket, cfg.s3_endpoint, region=cfg.s3_region,
                                               part_size=cfg.s3_part_size,
                                               multipart_threshold=cfg.s3_multipart_threshold,
-                                              parallel_parts=cfg.s3_parallel_parts)
+                                              parallel_parts=cfg.s3_parallel_parts,
+                                              sign_threads=cfg.s3_sign_threads)
         if cfg.gpu_verify != "off":
             # HIP context + hasher set-up off the job path (first torrent resume would pay it).
             # Finished before consuming: importing torch holds the GIL for ~1-2 s, which would
@@ -136,6 +140,17 @@ class Service:
         await self.amqp.consume(cfg.consume_topic)
         for i in range(max(1, cfg.concurrency)):
             self._workers.append(asyncio.ensure_future(self._worker(i)))
+
+    def _size_executor(self) -> None:
+        """Native pumps block executor threads, and an S3 send pump waits on its
+        download's Flow while that download's receive pumps still need threads:
+        size the loop's default pool (stdlib: min(32, cpus + 4)) so
+        ``concurrency`` jobs' streams can never starve it."""
+        cfg = self.cfg
+        per_job = max(1, cfg.http_segments) + 2 + max(1, cfg.s3_parallel_parts)
+        need = max(1, cfg.concurrency) * per_job + 8
+        asyncio.get_running_loop().set_default_executor(
+            ThreadPoolExecutor(max_workers=max(32, need), thread_name_prefix="tritondl-io"))
 
     async def _worker(self, idx: int) -> None:
         assert self.amqp is not None
@@ -193,7 +208,10 @@ class Service:
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="download")
             mark("download")
             stage = "select"
-            files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
+            if streamed:
+                files = dir_media(dl_dir)      # single-file HTTP job dir: a few entries, no executor hop
+            else:
+                files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
             log.info("found %d files", len(files))
             mark("select")
             stage = "upload"

@@ -50,6 +50,9 @@ class Config:
     dead_letter_topic: str = ""                 # "" => drop after max_retries (nack)
     cleanup: bool = False                       # B15: off for parity
     stream_upload: bool = True                  # overlap HTTP fetch with S3 upload
+    http_segments: int = 4                      # max parallel Range streams per HTTP file
+    http_segment_threshold: int = 64 * 1024 * 1024   # open-ended probe only: segment files at least this big
+    http_probe_bytes: int = 2 * 1024 * 1024     # GET probe = bytes=0-(N-1), the rest as parallel Range streams
 
     # --- download (downloader.go:81-93, torrent.go:67) ---
     download_dir: str = ""                      # default $CWD/downloading
@@ -74,6 +77,7 @@ class Config:
     s3_part_size: int = 64 * 1024 * 1024
     s3_multipart_threshold: int = 64 * 1024 * 1024
     s3_parallel_parts: int = 4
+    s3_sign_threads: int = 4                    # native SHA-256 chunk hashers per streaming PUT
     aws_access_key_id: str = ""
     aws_secret_access_key: str = ""
     aws_session_token: str = ""
@@ -110,7 +114,9 @@ class Config:
         ints = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES": "num_shard_queues",
                 "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port",
                 "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
-                "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s"}
+                "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
+                "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
+                "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
                   "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s"}
