@@ -70,8 +70,8 @@ def _gpu_hash_probe(total_mb: int = 256) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--file-mb", type=float, default=10.0)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     ap.add_argument("--no-gpu-probe", action="store_true")

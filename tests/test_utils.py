@@ -75,3 +75,13 @@ def test_durafmt_matches_hako_durafmt_format():
     assert durafmt(0) == "0 seconds"
     assert durafmt(3600 * 25) == "1 day 1 hour"
     assert durafmt(0.000002) == "2 microseconds"
+
+
+def test_config_data_plane_knobs():
+    from tritondl.utils.config import Config
+    c = Config.from_env({})
+    assert (c.http_probe_bytes, c.http_segments, c.s3_sign_threads) == (0, 4, 4)
+    c = Config.from_env({"TRITONDL_HTTP_PROBE_BYTES": "4194304", "TRITONDL_HTTP_SEGMENTS": "8",
+                         "TRITONDL_HTTP_SEGMENT_THRESHOLD": "1048576", "TRITONDL_S3_SIGN_THREADS": "2"})
+    assert (c.http_probe_bytes, c.http_segments, c.http_segment_threshold, c.s3_sign_threads) == \
+        (4 << 20, 8, 1 << 20, 2)

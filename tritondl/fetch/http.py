@@ -20,7 +20,7 @@ Beyond the reference:
   and ``If-Range`` guards against resuming onto a changed origin object;
 * large files are fetched as ``segments`` concurrent Range streams written
   with ``pwrite`` from worker threads (grab used one stream); with
-  ``probe_bytes`` (the worker's default, ``TRITONDL_HTTP_PROBE_BYTES``) the
+  ``probe_bytes`` (opt-in: ``TRITONDL_HTTP_PROBE_BYTES``) the
   probe is ``GET bytes=0-(probe_bytes-1)`` and the rest of a bigger file is
   requested at once as parallel Range streams, so mid-size files are
   segmented too and no half-read probe connection is dropped;
