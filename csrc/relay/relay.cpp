@@ -1,6 +1,8 @@
-// pybind11 bindings for the native fetch -> S3 data plane (relay_core.h).
-// Every pump releases the GIL for its whole run; Python awaits it from an
-// executor thread while the event loop keeps serving the control plane.
+// pybind11 bindings for the native fetch -> S3 data plane (relay_core.h,
+// stream.h).  Every pump releases the GIL for its whole run; Python awaits it
+// from an executor thread while the event loop keeps serving the control
+// plane.  Pumps take a stream: a `Sock` / `TlsConn` object (abortable), or a
+// bare socket fd (int).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -9,8 +11,33 @@
 namespace py = pybind11;
 using namespace tritondl_relay;
 
+namespace {
+
+// A pump's view of its `sock` argument: a Stream object, or a temporary plain
+// stream over an int fd.
+struct StreamArg {
+  std::shared_ptr<Stream> keep;
+  std::unique_ptr<PlainStream> tmp;
+  Stream* s = nullptr;
+};
+
+StreamArg as_stream(const py::object& o) {
+  StreamArg a;
+  if (py::isinstance<Stream>(o)) {
+    a.keep = o.cast<std::shared_ptr<Stream>>();
+    a.s = a.keep.get();
+  } else {
+    a.tmp.reset(new PlainStream(o.cast<int>()));
+    a.s = a.tmp.get();
+  }
+  return a;
+}
+
+}  // namespace
+
 PYBIND11_MODULE(_relay, m) {
-  m.doc() = "tritondl native data plane: socket->file receive pump, file->socket aws-chunked/plain send pump";
+  m.doc() = "tritondl native data plane: stream->file receive pump, file->stream aws-chunked/plain send pump, "
+            "TLS (OpenSSL) streams";
 
   py::class_<Flow, std::shared_ptr<Flow>>(m, "Flow")
       .def(py::init([](const std::vector<std::tuple<uint64_t, int64_t, uint64_t>>& segs) {
@@ -28,6 +55,8 @@ PYBIND11_MODULE(_relay, m) {
       .def("watermark", &Flow::watermark)
       .def("covered_bytes", &Flow::covered_bytes, py::arg("start"), py::arg("end"))
       .def("bytes_until_covered", &Flow::bytes_until_covered, py::arg("start"), py::arg("end"))
+      .def("frontiers", &Flow::frontiers, "receive frontier of every unfinished segment")
+      .def("open_starts", &Flow::open_starts, "start offset of every unfinished segment")
       .def_property_readonly("cancelled", &Flow::cancelled)
       .def_property_readonly("failed", &Flow::failed)
       .def_property_readonly("finished", &Flow::finished)
@@ -39,14 +68,87 @@ PYBIND11_MODULE(_relay, m) {
            py::arg("start"), py::arg("end"), py::arg("timeout"),
            "0 = on disk, 1 = failed/cancelled, 2 = timeout, 3 = download ended short");
 
+  py::class_<Stream, std::shared_ptr<Stream>>(m, "Stream")
+      .def("abort", &Stream::abort, "stop any pump running on this stream (sticky; the fd stays open)")
+      .def_property_readonly("aborted", &Stream::aborted)
+      .def("fileno", &Stream::fd)
+      .def_property_readonly("plain", &Stream::plain);
+
+  py::class_<PlainStream, Stream, std::shared_ptr<PlainStream>>(m, "Sock")
+      .def(py::init<int>(), py::arg("fd"), "plain stream over a connected non-blocking socket (fd not owned)");
+
+  py::class_<TlsContext, std::shared_ptr<TlsContext>>(m, "TlsContext")
+      .def_static("client", &TlsContext::client, py::arg("ca_pem") = "", py::arg("ca_file") = "",
+                  py::arg("verify") = true,
+                  "client context: trust ca_pem / ca_file, else the system store (SSL_CERT_FILE honoured)")
+      .def_static("server", &TlsContext::server, py::arg("cert_pem"), py::arg("key_pem"))
+      .def_property_readonly("is_server", &TlsContext::is_server)
+      .def_property_readonly("cached_sessions", &TlsContext::cached_sessions);
+
+  py::class_<TlsStream, Stream, std::shared_ptr<TlsStream>>(m, "TlsConn")
+      .def(py::init<std::shared_ptr<TlsContext>, int, const std::string&, const std::string&>(), py::arg("ctx"),
+           py::arg("fd"), py::arg("server_hostname") = "", py::arg("session_key") = "")
+      .def("handshake_step", [](TlsStream& t) {
+             std::string err;
+             const int w = t.handshake_step(&err);
+             if (w < 0) throw std::runtime_error(err);
+             return w;
+           },
+           "one non-blocking handshake step: 0 = done, else the poll events to wait for")
+      .def("handshake", [](TlsStream& t, double timeout) {
+             std::string err;
+             {
+               py::gil_scoped_release nogil;
+               err = t.handshake(timeout);
+             }
+             if (!err.empty()) throw std::runtime_error(err);
+           },
+           py::arg("timeout") = 30.0)
+      .def("read_nb", [](TlsStream& t, size_t n) -> py::object {
+             std::string buf(n, '\0');
+             short want = POLLIN;
+             std::string err;
+             const ssize_t r = t.recv_nb(&buf[0], n, &want, &err);
+             if (r == IO_ERR) throw std::runtime_error(err);
+             if (r == IO_AGAIN) return py::int_(want);
+             return py::bytes(buf.data(), static_cast<size_t>(r));
+           },
+           py::arg("n"), "bytes (b'' = end of stream) or the poll events to wait for")
+      .def("write_nb", [](TlsStream& t, const py::bytes& data) -> py::tuple {
+             std::string d = data;
+             if (d.empty()) return py::make_tuple(0, 0);
+             struct iovec iov{&d[0], d.size()};
+             short want = POLLOUT;
+             std::string err;
+             const ssize_t r = t.send_nb(&iov, 1, &want, &err);
+             if (r == IO_ERR) throw std::runtime_error(err);
+             if (r == IO_AGAIN) return py::make_tuple(0, static_cast<int>(want));
+             return py::make_tuple(static_cast<int64_t>(r), 0);
+           },
+           py::arg("data"), "(bytes written, poll events to wait for); retry unwritten bytes unchanged")
+      .def("pending", &TlsStream::pending)
+      .def("alive", &TlsStream::alive)
+      .def("shutdown_notify", &TlsStream::shutdown_notify)
+      .def_property_readonly("version", &TlsStream::version)
+      .def_property_readonly("cipher", &TlsStream::cipher)
+      .def_property_readonly("resumed", &TlsStream::resumed);
+
+  m.def("make_test_pki", [](const std::vector<std::string>& hosts, long days) {
+          TestPki p = make_test_pki(hosts, days);
+          return py::make_tuple(p.ca_pem, p.cert_pem, p.key_pem);
+        },
+        py::arg("hosts"), py::arg("days") = 30, "throwaway EC P-256 CA + leaf for hosts: (ca_pem, cert_pem, key_pem)");
+
   m.def("recv_body",
-        [](int sock, int fd, uint64_t off, int64_t length, const py::bytes& prefix, std::shared_ptr<Flow> flow,
-           size_t seg, uint64_t seg_done0, double idle_timeout, size_t buf_size, bool use_splice) {
+        [](const py::object& sock, int fd, uint64_t off, int64_t length, const py::bytes& prefix,
+           std::shared_ptr<Flow> flow, size_t seg, uint64_t seg_done0, double idle_timeout, size_t buf_size,
+           bool use_splice) {
           std::string pre = prefix;
+          StreamArg io = as_stream(sock);
           RecvResult r;
           {
             py::gil_scoped_release nogil;
-            r = recv_body(sock, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0, idle_timeout,
+            r = recv_body(*io.s, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0, idle_timeout,
                           buf_size, use_splice);
           }
           return py::make_tuple(r.received, r.eof, r.err);
@@ -54,18 +156,19 @@ PYBIND11_MODULE(_relay, m) {
         py::arg("sock"), py::arg("fd"), py::arg("offset"), py::arg("length"), py::arg("prefix"), py::arg("flow"),
         py::arg("seg") = 0, py::arg("seg_done0") = 0, py::arg("idle_timeout") = 120.0,
         py::arg("buf_size") = 4u << 20, py::arg("splice") = true,
-        "Stream a body into fd at offset (splice socket->pipe->file when possible, else recv+pwrite); "
-        "returns (received, eof, error).");
+        "Stream a body into fd at offset (plain sockets: splice socket->pipe->file when possible, else "
+        "recv+pwrite); returns (received, eof, error).");
 
   m.def("send_body",
-        [](int sock, const py::bytes& head, int fd, uint64_t off, uint64_t length, std::shared_ptr<Flow> flow, int mode,
-           const py::bytes& key, const std::string& amzdate, const std::string& scope, const std::string& seed,
-           size_t chunk, int threads, double idle_timeout) {
+        [](const py::object& sock, const py::bytes& head, int fd, uint64_t off, uint64_t length,
+           std::shared_ptr<Flow> flow, int mode, const py::bytes& key, const std::string& amzdate,
+           const std::string& scope, const std::string& seed, size_t chunk, int threads, double idle_timeout) {
           std::string h = head, k = key;
+          StreamArg io = as_stream(sock);
           SendResult r;
           {
             py::gil_scoped_release nogil;
-            r = send_body(sock, h, fd, off, length, flow.get(), mode, k, amzdate, scope, seed, chunk, threads,
+            r = send_body(*io.s, h, fd, off, length, flow.get(), mode, k, amzdate, scope, seed, chunk, threads,
                           idle_timeout);
           }
           return py::make_tuple(r.sent, r.last_sig, r.err);
@@ -76,13 +179,15 @@ PYBIND11_MODULE(_relay, m) {
         "Send head + body (mode 0 plain / 1 aws-chunked); returns (payload_sent, last_signature, error).");
 
   m.def("recv_verify_chunked",
-        [](int sock, uint64_t raw_len, const py::bytes& prefix, const py::bytes& key, const std::string& amzdate,
-           const std::string& scope, const std::string& seed, bool keep, int threads, double idle_timeout) {
+        [](const py::object& sock, uint64_t raw_len, const py::bytes& prefix, const py::bytes& key,
+           const std::string& amzdate, const std::string& scope, const std::string& seed, bool keep, int threads,
+           double idle_timeout) {
           std::string pre = prefix, k = key;
+          StreamArg io = as_stream(sock);
           VerifyResult r;
           {
             py::gil_scoped_release nogil;
-            r = recv_verify_chunked(sock, raw_len, pre.data(), pre.size(), k, amzdate, scope, seed, keep, threads,
+            r = recv_verify_chunked(*io.s, raw_len, pre.data(), pre.size(), k, amzdate, scope, seed, keep, threads,
                                     idle_timeout);
           }
           return py::make_tuple(r.decoded, r.err, keep ? py::object(py::bytes(r.data)) : py::object(py::none()));

@@ -5,7 +5,7 @@
 // heads, signs requests and handles retries; every BYTE of a job moves here,
 // in threads that never touch the interpreter:
 //
-//   recv_body  : origin socket -> file (pwrite at the segment's offset),
+//   recv_body  : origin stream -> file (pwrite at the segment's offset),
 //                publishing per-segment progress on a Flow;
 //   send_body  : file -> S3 socket as an aws-chunked (SigV4 streaming) or
 //                unsigned body, following the Flow so an upload can run
@@ -13,6 +13,10 @@
 //                small hasher pool ahead of the sender (the per-chunk HMAC
 //                chain is the only serial part); the sender batches many
 //                frames per writev.  Unsigned bodies go out with sendfile.
+//
+// Every pump works on a Stream (stream.h): a bare socket — where the kernel
+// zero-copy paths (splice, sendfile) apply — or a TLS session, so https
+// bodies stay native too.  Stream::abort() stops any pump promptly.
 //
 // Reference behaviour replaced: grab's single-stream copy
 // (internal/downloader/http/http.go:36-71) and minio-go's PutObject body
@@ -43,12 +47,10 @@
 #include <vector>
 
 #include "../hash/hash_core.h"
+#include "stream.h"
 
 namespace tritondl_relay {
 
-using Clock = std::chrono::steady_clock;
-
-inline double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
 
 // Timed condition wait used only as a polling slice.  system_clock-based
 // (pthread_cond_timedwait): libstdc++'s steady-clock wait_for goes through
@@ -141,6 +143,32 @@ class Flow {
       if (hi > frontier) worst = std::max(worst, hi - frontier);
     }
     return worst;
+  }
+
+  // Receive frontier (start + done) of every segment still filling; empty
+  // once finished.  Lets a scheduler rank only the ranges at a frontier
+  // instead of every pending range.
+  std::vector<uint64_t> frontiers() const {
+    std::lock_guard<std::mutex> l(mu_);
+    std::vector<uint64_t> out;
+    if (finished_) return out;
+    for (const Seg& s : segs_) {
+      const uint64_t f = s.start + s.done;
+      if (s.end < 0 || f < static_cast<uint64_t>(s.end)) out.push_back(f);
+    }
+    return out;
+  }
+
+  // Start offset of every segment still filling (see frontiers()).
+  std::vector<uint64_t> open_starts() const {
+    std::lock_guard<std::mutex> l(mu_);
+    std::vector<uint64_t> out;
+    if (finished_) return out;
+    for (const Seg& s : segs_) {
+      const uint64_t f = s.start + s.done;
+      if (s.end < 0 || f < static_cast<uint64_t>(s.end)) out.push_back(s.start);
+    }
+    return out;
   }
 
   // Bytes of [a, b) already on disk (for scheduling uploads of ranges).
@@ -286,21 +314,8 @@ struct Buf {
 // ---------------------------------------------------------------------------
 // socket helpers (non-blocking fds owned by the asyncio side; the pumps poll)
 
-// 1 = ready, 0 = not yet (slice elapsed), -1 = error/hangup with no data
-inline int wait_fd(int fd, short ev, int ms) {
-  struct pollfd p {};
-  p.fd = fd;
-  p.events = ev;
-  const int r = ::poll(&p, 1, ms);
-  if (r < 0) return errno == EINTR ? 0 : -1;
-  if (r == 0) return 0;
-  if (p.revents & (ev | POLLHUP)) return 1;  // hangup: let recv/send report EOF / EPIPE
-  return (p.revents & (POLLERR | POLLNVAL)) ? -1 : 1;
-}
-
-inline std::string errno_str(const char* what) {
-  return std::string(what) + ": " + std::strerror(errno);
-}
+// A pump must stop: its stream was aborted or the download it follows was cancelled.
+inline bool stopped(const Stream& io, const Flow* flow) { return io.aborted() || (flow && flow->cancelled()); }
 
 inline bool pwrite_full(int fd, const char* p, size_t n, uint64_t off, std::string* err) {
   while (n) {
@@ -317,24 +332,18 @@ inline bool pwrite_full(int fd, const char* p, size_t n, uint64_t off, std::stri
   return true;
 }
 
-// Write every iovec (partial writes resumed); waits for POLLOUT on EAGAIN.
-inline bool writev_all(int sock, std::vector<struct iovec>& iov, double idle_timeout, const Flow* flow,
+// Write every iovec (partial writes resumed); waits for writability on EAGAIN.
+inline bool writev_all(Stream& io, std::vector<struct iovec>& iov, double idle_timeout, const Flow* flow,
                        std::string* err) {
   size_t k = 0;
   auto last = Clock::now();
   while (k < iov.size()) {
     const int cnt = static_cast<int>(std::min<size_t>(iov.size() - k, IOV_MAX));
-    struct msghdr mh {};
-    mh.msg_iov = &iov[k];
-    mh.msg_iovlen = static_cast<size_t>(cnt);
-    const ssize_t w = ::sendmsg(sock, &mh, MSG_NOSIGNAL);
-    if (w < 0) {
-      if (errno == EINTR) continue;
-      if (errno != EAGAIN && errno != EWOULDBLOCK) {
-        *err = errno_str("send");
-        return false;
-      }
-      if (flow && flow->cancelled()) {
+    short want = POLLOUT;
+    const ssize_t w = io.send_nb(&iov[k], cnt, &want, err);
+    if (w == IO_ERR) return false;
+    if (w == IO_AGAIN || w == 0) {
+      if (stopped(io, flow)) {
         *err = "cancelled";
         return false;
       }
@@ -342,7 +351,7 @@ inline bool writev_all(int sock, std::vector<struct iovec>& iov, double idle_tim
         *err = "send timeout";
         return false;
       }
-      if (wait_fd(sock, POLLOUT, 50) < 0) {
+      if (wait_fd(io.fd(), want, 50) < 0) {
         *err = "socket error while sending";
         return false;
       }
@@ -365,10 +374,36 @@ inline bool writev_all(int sock, std::vector<struct iovec>& iov, double idle_tim
   return true;
 }
 
-inline bool send_all(int sock, const char* p, size_t n, double idle_timeout, const Flow* flow, std::string* err) {
+inline bool send_all(Stream& io, const char* p, size_t n, double idle_timeout, const Flow* flow, std::string* err) {
   if (!n) return true;
   std::vector<struct iovec> iov{{const_cast<char*>(p), n}};
-  return writev_all(sock, iov, idle_timeout, flow, err);
+  return writev_all(io, iov, idle_timeout, flow, err);
+}
+
+// One receive with waiting: > 0 bytes, 0 = end of stream, -1 = error/stop (*err set).
+inline ssize_t recv_wait(Stream& io, char* p, size_t n, Clock::time_point* last, double idle_timeout,
+                         const Flow* flow, std::string* err) {
+  for (;;) {
+    if (stopped(io, flow)) {
+      *err = "cancelled";
+      return -1;
+    }
+    short want = POLLIN;
+    const ssize_t r = io.recv_nb(p, n, &want, err);
+    if (r >= 0) {
+      if (r > 0) *last = Clock::now();
+      return r;
+    }
+    if (r == IO_ERR) return -1;
+    if (since(*last) > idle_timeout) {
+      *err = "read timeout";
+      return -1;
+    }
+    if (wait_fd(io.fd(), want, 50) < 0) {
+      *err = "socket error while receiving";
+      return -1;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -385,8 +420,9 @@ struct RecvResult {
 // Zero-user-copy receive: socket -> pipe (page references move) -> file
 // (one copy into the page cache).  Returns false when splice is unsupported
 // here (then nothing was consumed and the caller falls back to recv+pwrite).
-inline bool splice_body(int sock, int fd, uint64_t off, uint64_t want, RecvResult& r, Flow* flow, size_t seg,
+inline bool splice_body(Stream& io, int fd, uint64_t off, uint64_t want, RecvResult& r, Flow* flow, size_t seg,
                         uint64_t seg_done0, double idle_timeout) {
+  const int sock = io.fd();
   int p[2];
   if (::pipe2(p, O_CLOEXEC | O_NONBLOCK) != 0) return false;
   ::fcntl(p[1], F_SETPIPE_SZ, 1 << 20);  // best effort; the default is 64 KiB
@@ -394,7 +430,7 @@ inline bool splice_body(int sock, int fd, uint64_t off, uint64_t want, RecvResul
   size_t in_pipe = 0;
   bool ok = true;
   while (r.received < want && r.err.empty()) {
-    if (flow && flow->cancelled()) {
+    if (stopped(io, flow)) {
       r.err = "cancelled";
       break;
     }
@@ -465,10 +501,14 @@ inline bool splice_body(int sock, int fd, uint64_t off, uint64_t want, RecvResul
   return ok;  // false: caller continues with recv + pwrite
 }
 
-inline RecvResult recv_body(int sock, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
+inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
                             Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout,
                             size_t buf_size = 4u << 20, bool use_splice = true) {
   RecvResult r;
+  if (stopped(io, flow)) {  // before touching the file: a cancelled segment writes nothing
+    r.err = "cancelled";
+    return r;
+  }
   const uint64_t want = length < 0 ? UINT64_MAX : static_cast<uint64_t>(length);
   if (prefix_len) {
     const size_t n = static_cast<size_t>(std::min<uint64_t>(prefix_len, want));
@@ -476,42 +516,46 @@ inline RecvResult recv_body(int sock, int fd, uint64_t off, int64_t length, cons
     r.received = n;
     if (flow) flow->advance(seg, seg_done0 + r.received);
   }
-  if (fd >= 0 && use_splice && r.received < want) {
-    if (splice_body(sock, fd, off, want, r, flow, seg, seg_done0, idle_timeout) || !r.err.empty() || r.eof)
+  if (fd >= 0 && use_splice && io.plain() && r.received < want) {
+    if (splice_body(io, fd, off, want, r, flow, seg, seg_done0, idle_timeout) || !r.err.empty() || r.eof)
       return r;
   }
   Buf buf(std::max<size_t>(buf_size, 64 << 10));
   auto last = Clock::now();
   while (r.received < want) {
-    if (flow && flow->cancelled()) {
-      r.err = "cancelled";
-      return r;
-    }
+    // fill the buffer with whatever is ready (TLS yields one record per read),
+    // then one pwrite
     const size_t cap = static_cast<size_t>(std::min<uint64_t>(buf.size(), want - r.received));
-    const ssize_t n = ::recv(sock, buf.data(), cap, MSG_DONTWAIT);
-    if (n > 0) {
-      if (fd >= 0 && !pwrite_full(fd, buf.data(), static_cast<size_t>(n), off + r.received, &r.err)) return r;
-      r.received += static_cast<uint64_t>(n);
-      if (flow) flow->advance(seg, seg_done0 + r.received);
-      last = Clock::now();
-      continue;
-    }
+    size_t have = 0;
+    bool eof = false;
+    const ssize_t n = recv_wait(io, buf.data(), cap, &last, idle_timeout, flow, &r.err);
+    if (n < 0) return r;
     if (n == 0) {
+      eof = true;
+    } else {
+      have = static_cast<size_t>(n);
+      while (have < cap && have < (1u << 20)) {
+        short w = POLLIN;
+        std::string e;
+        const ssize_t m = io.recv_nb(buf.data() + have, cap - have, &w, &e);
+        if (m > 0) {
+          have += static_cast<size_t>(m);
+          continue;
+        }
+        if (m == 0) eof = true;
+        if (m == IO_ERR) r.err = e;
+        break;
+      }
+    }
+    if (have) {
+      if (fd >= 0 && !pwrite_full(fd, buf.data(), have, off + r.received, &r.err)) return r;
+      r.received += have;
+      if (flow) flow->advance(seg, seg_done0 + r.received);
+    }
+    if (!r.err.empty()) return r;
+    if (eof) {
       r.eof = true;
-      if (length >= 0) r.err = "connection closed early";
-      return r;
-    }
-    if (errno == EINTR) continue;
-    if (errno != EAGAIN && errno != EWOULDBLOCK) {
-      r.err = errno_str("recv");
-      return r;
-    }
-    if (since(last) > idle_timeout) {
-      r.err = "read timeout";
-      return r;
-    }
-    if (wait_fd(sock, POLLIN, 50) < 0) {
-      r.err = "socket error while receiving";
+      if (length >= 0 && r.received < want) r.err = "connection closed early";
       return r;
     }
   }
@@ -544,20 +588,34 @@ struct ChunkSigner {
   }
 };
 
-inline SendResult send_plain(int sock, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
+inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
   SendResult r;
   const uint64_t step = 4u << 20;
   auto last = Clock::now();
+  Buf buf(io.plain() ? 0 : static_cast<size_t>(std::min<uint64_t>(step, std::max<uint64_t>(length, 1))));
   while (r.sent < length) {
     const uint64_t n = std::min(step, length - r.sent);
     if (flow) {
-      const int w = flow->wait_covered(off + r.sent, off + r.sent + n, idle_timeout);
+      const int w = flow->wait_covered(off + r.sent, off + r.sent + n, idle_timeout, io.abort_flag());
       if (w) {
-        r.err = w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
-                                                                   : "source transfer failed: " + flow->error();
+        r.err = io.aborted() ? "cancelled"
+                : w == 3     ? "source shorter than expected"
+                : w == 2     ? "timed out waiting for source bytes"
+                             : "source transfer failed: " + flow->error();
         return r;
       }
     }
+    if (!io.plain()) {  // TLS: the record layer needs the bytes in user space
+      const size_t m = static_cast<size_t>(n);
+      if (tritondl_hash::pread_full(fd, buf.data(), m, static_cast<off_t>(off + r.sent)) != m) {
+        r.err = "source file shorter than expected";
+        return r;
+      }
+      if (!send_all(io, buf.data(), m, idle_timeout, flow, &r.err)) return r;
+      r.sent += n;
+      continue;
+    }
+    const int sock = io.fd();
     uint64_t k = 0;
     while (k < n) {
       off_t o = static_cast<off_t>(off + r.sent + k);
@@ -578,9 +636,9 @@ inline SendResult send_plain(int sock, int fd, uint64_t off, uint64_t length, Fl
         r.err = errno_str("sendfile");
         return r;
       }
-      if ((flow && flow->cancelled()) || since(last) > idle_timeout || wait_fd(sock, POLLOUT, 50) < 0) {
+      if (stopped(io, flow) || since(last) > idle_timeout || wait_fd(sock, POLLOUT, 50) < 0) {
         r.sent += k;
-        r.err = (flow && flow->cancelled()) ? "cancelled" : "send timeout";
+        r.err = stopped(io, flow) ? "cancelled" : "send timeout";
         return r;
       }
     }
@@ -589,7 +647,7 @@ inline SendResult send_plain(int sock, int fd, uint64_t off, uint64_t length, Fl
   return r;
 }
 
-inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, Flow* flow, ChunkSigner& signer,
+inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow, ChunkSigner& signer,
                                size_t chunk, int threads, double idle_timeout, size_t batch = 64) {
   SendResult r;
   if (chunk == 0) {
@@ -671,7 +729,15 @@ inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, 
     size_t j = i;
     {
       std::unique_lock<std::mutex> l(mu);
-      cv_ready.wait(l, [&] { return abort.load() || ready[i % K] == static_cast<int64_t>(i); });
+      while (!abort.load() && ready[i % K] != static_cast<int64_t>(i)) {
+        if (io.aborted()) {  // the hashers may sit in a flow wait: stop them too
+          if (worker_err.empty()) worker_err = "cancelled";
+          abort.store(true);
+          cv_free.notify_all();
+          break;
+        }
+        cv_wait_ms(cv_ready, l, 20);
+      }
       if (abort.load()) {
         r.err = worker_err;
         break;
@@ -699,7 +765,7 @@ inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, 
       r.sent += m;
     }
     std::string e;
-    if (!writev_all(sock, iov, idle_timeout, flow, &e)) {
+    if (!writev_all(io, iov, idle_timeout, flow, &e)) {
       r.err = e;
       break;
     }
@@ -719,7 +785,7 @@ inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, 
   if (!r.err.empty()) return r;
   const std::string fin = "0;chunk-signature=" + signer.next(signer.empty_hash) + "\r\n\r\n";
   std::string e;
-  if (!send_all(sock, fin.data(), fin.size(), idle_timeout, flow, &e)) {
+  if (!send_all(io, fin.data(), fin.size(), idle_timeout, flow, &e)) {
     r.err = e;
     return r;
   }
@@ -727,14 +793,14 @@ inline SendResult send_chunked(int sock, int fd, uint64_t off, uint64_t length, 
   return r;
 }
 
-inline SendResult send_body(int sock, const std::string& head, int fd, uint64_t off, uint64_t length, Flow* flow,
+inline SendResult send_body(Stream& io, const std::string& head, int fd, uint64_t off, uint64_t length, Flow* flow,
                             int mode, const std::string& key, const std::string& amzdate, const std::string& scope,
                             const std::string& seed, size_t chunk, int threads, double idle_timeout) {
   SendResult r;
-  if (!send_all(sock, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
-  if (mode == 0) return send_plain(sock, fd, off, length, flow, idle_timeout);
+  if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
+  if (mode == 0) return send_plain(io, fd, off, length, flow, idle_timeout);
   ChunkSigner signer(key, amzdate, scope, seed);
-  return send_chunked(sock, fd, off, length, flow, signer, chunk, threads, idle_timeout);
+  return send_chunked(io, fd, off, length, flow, signer, chunk, threads, idle_timeout);
 }
 
 // ---------------------------------------------------------------------------
@@ -795,7 +861,7 @@ inline size_t parse_frames(const char* raw, size_t have, std::vector<RawFrame>* 
   return pos;
 }
 
-inline VerifyResult recv_verify_windowed(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const char* prefix, size_t plen,
                                          const std::string& key, const std::string& amzdate, const std::string& scope,
                                          const std::string& seed, bool keep, int threads, double idle_timeout,
                                          size_t window = 4u << 20) {
@@ -826,30 +892,14 @@ inline VerifyResult recv_verify_windowed(int sock, uint64_t raw_len, const char*
     while (have < window && received < raw_len) {
       ensure(buf[cur], have + std::min<uint64_t>(window, raw_len - received), have);
       const size_t cap = static_cast<size_t>(std::min<uint64_t>(buf[cur].size() - have, raw_len - received));
-      const ssize_t n = ::recv(sock, buf[cur].data() + have, cap, MSG_DONTWAIT);
+      const ssize_t n = recv_wait(io, buf[cur].data() + have, cap, &last, idle_timeout, nullptr, &r.err);
       if (n > 0) {
         have += static_cast<size_t>(n);
         received += static_cast<uint64_t>(n);
-        last = Clock::now();
         continue;
       }
-      if (n == 0) {
-        r.err = "client closed inside the request body";
-        break;
-      }
-      if (errno == EINTR) continue;
-      if (errno != EAGAIN && errno != EWOULDBLOCK) {
-        r.err = errno_str("recv");
-        break;
-      }
-      if (since(last) > idle_timeout) {
-        r.err = "read timeout";
-        break;
-      }
-      if (wait_fd(sock, POLLIN, 50) < 0) {
-        r.err = "socket error while receiving";
-        break;
-      }
+      if (n == 0) r.err = "client closed inside the request body";
+      break;
     }
     if (!r.err.empty()) break;
     std::vector<RawFrame> frames;
@@ -921,7 +971,7 @@ struct StreamFrame {
   std::atomic<uint8_t> ready{0};
 };
 
-inline VerifyResult recv_verify_stream(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char* prefix, size_t plen,
                                        const std::string& key, const std::string& amzdate, const std::string& scope,
                                        const std::string& seed, bool keep, int threads, double idle_timeout) {
   VerifyResult r;
@@ -1026,26 +1076,14 @@ inline VerifyResult recv_verify_stream(int sock, uint64_t raw_len, const char* p
       r.err = "truncated chunk";
       break;
     }
-    const ssize_t n = ::recv(sock, raw + have, static_cast<size_t>(raw_len - have), MSG_DONTWAIT);
+    const ssize_t n = recv_wait(io, raw + have, static_cast<size_t>(raw_len - have), &last, idle_timeout, nullptr,
+                                &r.err);
     if (n > 0) {
       have += static_cast<size_t>(n);
-      last = Clock::now();
       continue;
     }
-    if (n == 0) {
-      r.err = "client closed inside the request body";
-      break;
-    }
-    if (errno == EINTR) continue;
-    if (errno != EAGAIN && errno != EWOULDBLOCK) {
-      r.err = errno_str("recv");
-      break;
-    }
-    if (since(last) > idle_timeout) {
-      r.err = "read timeout";
-      break;
-    }
-    if (wait_fd(sock, POLLIN, 50) < 0) r.err = "socket error while receiving";
+    if (n == 0) r.err = "client closed inside the request body";
+    break;
   }
   {
     std::lock_guard<std::mutex> l(mu);
@@ -1073,12 +1111,12 @@ inline VerifyResult recv_verify_stream(int sock, uint64_t raw_len, const char* p
   return r;
 }
 
-inline VerifyResult recv_verify_chunked(int sock, uint64_t raw_len, const char* prefix, size_t plen,
+inline VerifyResult recv_verify_chunked(Stream& io, uint64_t raw_len, const char* prefix, size_t plen,
                                         const std::string& key, const std::string& amzdate, const std::string& scope,
                                         const std::string& seed, bool keep, int threads, double idle_timeout) {
   if (raw_len <= (uint64_t(256) << 20))
-    return recv_verify_stream(sock, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
-  return recv_verify_windowed(sock, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
+    return recv_verify_stream(io, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
+  return recv_verify_windowed(io, raw_len, prefix, plen, key, amzdate, scope, seed, keep, threads, idle_timeout);
 }
 
 // Exact on-the-wire size of an aws-chunked body of `len` payload bytes.

@@ -217,8 +217,9 @@ static void test_relay(size_t size) {
   });
   VerifyResult vr;
   const uint64_t raw_len = chunked_length(size, 65536);
-  std::thread receiver([&] { vr = recv_verify_chunked(sv[1], raw_len, "", 0, key, amz, scope, seed, true, 3, 10.0); });
-  SendResult sr = send_body(sv[0], "", rfd, 0, size, &flow, 1, key, amz, scope, seed, 65536, 3, 10.0);
+  PlainStream s0(sv[0]), s1(sv[1]);
+  std::thread receiver([&] { vr = recv_verify_chunked(s1, raw_len, "", 0, key, amz, scope, seed, true, 3, 10.0); });
+  SendResult sr = send_body(s0, "", rfd, 0, size, &flow, 1, key, amz, scope, seed, 65536, 3, 10.0);
   writer.join();
   receiver.join();
   CHECK(sr.err.empty());
@@ -229,8 +230,8 @@ static void test_relay(size_t size) {
   const int ofd = ::mkstemp(opath);
   Flow f2({{0, static_cast<int64_t>(size), 0}});
   RecvResult rr;
-  std::thread rcv([&] { rr = recv_body(sv[1], ofd, 0, static_cast<int64_t>(size), "", 0, &f2, 0, 0, 10.0); });
-  SendResult ps = send_body(sv[0], "", rfd, 0, size, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
+  std::thread rcv([&] { rr = recv_body(s1, ofd, 0, static_cast<int64_t>(size), "", 0, &f2, 0, 0, 10.0); });
+  SendResult ps = send_body(s0, "", rfd, 0, size, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
   rcv.join();
   CHECK(ps.err.empty() && rr.err.empty() && rr.received == size && f2.watermark() == size);
   std::string back(size, '\0');

@@ -230,7 +230,7 @@ def test_bounded_probe_segments_mid_size_files(tmp_path):
         assert (tmp_path / "mid.mkv").read_bytes() == data
         rngs = [r[2] for r in o.requests if r[0] == "GET"]
         assert rngs[0] == f"bytes=0-{pb - 1}"
-        assert len(rngs) == 5 and all(r.startswith("bytes=") for r in rngs)
+        assert len(rngs) == 4 and all(r.startswith("bytes=") for r in rngs)   # probe + segments-1
         small = os.urandom(100_000)
         n = len(o.requests)
         url2 = o.add("/small.mkv", small)
@@ -257,3 +257,46 @@ def test_bounded_probe_plan_covers_file():
         assert segs[0][:2] == [0, first]
         assert all(a[1] == b[0] for a, b in zip(segs, segs[1:]))
         assert segs[-1][1] == size and len(segs) <= 5
+
+
+def test_failed_segment_stops_and_awaits_sibling_pumps(tmp_path):
+    """One Range stream dies for good while its siblings sit in their native
+    pumps (the origin sends 1 MiB bursts with pauses).  By the time the
+    download raises, every sibling pump must have returned — the .part fd and
+    the sockets are closed only then, so no pump can write through a recycled
+    fd number (another job's file, the AMQP socket).  A concurrent download of
+    another file is unaffected."""
+    from tritondl.utils import rawhttp
+
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(12_000_000)
+        other = os.urandom(4_000_000)
+        url = o.add("/seg/bad.mkv", data)
+        url2 = o.add("/seg/good.mkv", other)
+        o.rate = 2_000_000                       # siblings idle between 1 MiB bursts when one is cut
+        # segment 2 dies after its first burst, while segments 0, 1, 3 are mid-body
+        o.cut_after, o.cut_times, o.cut_match = 1_500_000, 1, "bytes=6000000-"
+        h = _dl(segments=4, segment_threshold=1 << 20, max_retries=0)
+        d1, d2 = tmp_path / "a", tmp_path / "b"
+        d1.mkdir()
+        d2.mkdir()
+        with pytest.raises(HTTPDownloadError):
+            await h.download(str(d1), Sink(), url)
+        assert rawhttp.active_pumps() == 0, "sibling pumps still running after the download failed"
+        part = d1 / "bad.mkv.part"
+        size0, mtime0 = part.stat().st_size, part.stat().st_mtime_ns
+        await asyncio.sleep(0.6)                 # the origin keeps sending: nothing may land anywhere
+        assert part.stat().st_mtime_ns == mtime0 and part.stat().st_size == size0
+        # concurrency: one download fails while another runs to completion
+        o.cut_after, o.cut_times, o.cut_match = 1_500_000, 0, "bytes=6000000-"
+        good = asyncio.ensure_future(_dl(segments=4, segment_threshold=1 << 20).download(str(d2), Sink(), url2))
+        await asyncio.sleep(0.05)
+        o.cut_times = 1
+        bad = asyncio.ensure_future(h.download(str(d1), Sink(), url))
+        res = await asyncio.gather(good, bad, return_exceptions=True)
+        assert (d2 / "good.mkv").read_bytes() == other
+        assert res[0] is None
+        await h.close()
+        await o.stop()
+    run(main(), timeout=90)

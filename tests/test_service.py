@@ -125,7 +125,11 @@ def test_magnet_job_end_to_end(tmp_path):
     run(main())
 
 
-def test_undecodable_body_is_nacked(tmp_path):
+def _dlq(broker, topic="v1.download.dead"):
+    return broker.drain_queue(f"{topic}-0") + broker.drain_queue(f"{topic}-1")
+
+
+def test_undecodable_body_is_dead_lettered(tmp_path):
     async def main():
         e = await Env().up(tmp_path)
         e.submit(None, raw=b"\xff\xff\xff")
@@ -133,7 +137,22 @@ def test_undecodable_body_is_nacked(tmp_path):
         assert not res[0].ok and res[0].stage == "decode"
         await asyncio.sleep(0.05)
         assert e.broker.queue_depth("v1.download-0") == 0 and e.broker.unacked_count() == 0
-        assert e.broker.stats["dead"] == 1
+        dead = _dlq(e.broker)
+        assert len(dead) == 1 and dead[0].body == b"\xff\xff\xff"
+        assert dead[0].props.headers["X-Failed-Stage"] == "decode"
+        await e.down()
+    run(main())
+
+
+def test_drop_failed_opt_out_nacks(tmp_path):
+    async def main():
+        e = await Env().up(tmp_path, max_retries=0, drop_failed=True)
+        e.submit(None, raw=b"\xff\xff\xff")
+        e.submit(Media(id="x", source_uri="ftp://h/a.zip"), i=1)
+        await e.wait_results(2)
+        await asyncio.sleep(0.05)
+        assert e.broker.unacked_count() == 0 and e.broker.stats["dead"] == 2
+        assert _dlq(e.broker) == []
         await e.down()
     run(main())
 
@@ -154,15 +173,86 @@ def test_failed_job_retried_then_dead_lettered(tmp_path):
     run(main())
 
 
-def test_unsupported_scheme_dropped_without_dlq(tmp_path):
+def test_unsupported_scheme_dead_lettered(tmp_path):
     async def main():
         e = await Env().up(tmp_path, max_retries=0)
         e.submit(Media(id="x", source_uri="ftp://h/a.zip"))
         res = await e.wait_results(1)
         assert "unsupported fileext '.zip' or protocol 'ftp'" in res[0].error
         await asyncio.sleep(0.05)
-        assert e.broker.unacked_count() == 0 and e.broker.stats["dead"] == 1
+        assert e.broker.unacked_count() == 0
+        dead = _dlq(e.broker)
+        assert len(dead) == 1 and "unsupported fileext" in dead[0].props.headers["X-Error"]
+        assert dead[0].props.headers["X-Original-Routing-Key"] == "v1.download-0"
         await e.down()
+    run(main())
+
+
+def test_s3_outage_longer_than_retry_budget_loses_no_job(tmp_path):
+    """Every retry waits in a broker delay queue (x-message-ttl + DLX back to
+    the shard); once the budget is spent the job lands in the dead-letter
+    queue.  An outage outlasting the whole budget must leave every job in the
+    DLQ — none dropped, none stuck unacked."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=3, retry_delay_s=0.05, retry_backoff=2.0)
+        e.svc.uploader.client.max_retries = 0
+        e.s3.fail_for(60.0)
+        n = 6
+        for k in range(n):
+            url = e.origin.add(f"/o{k}.mkv", os.urandom(20_000))
+            e.submit(Media(id=f"o{k}", source_uri=url), i=k)
+        await e.wait_results(n * 4, timeout=60)          # 1 try + 3 retries each
+        await asyncio.sleep(0.2)
+        dead = _dlq(e.broker)
+        assert sorted(Download.decode(m.body).media.id for m in dead) == [f"o{k}" for k in range(n)]
+        assert all(m.props.headers["X-Retries"] == 3 and m.props.headers["X-Failed-Stage"] == "upload"
+                   for m in dead)
+        assert e.broker.unacked_count() == 0
+        assert all(len(q.messages) == 0 for name, q in e.broker.queues.items() if not name.startswith("v1.convert"))
+        # the delays grew per retry: 50, 100, 200 ms queues were used
+        delay_qs = sorted(q for q in e.broker.queues if ".retry." in q)
+        assert {q.split(".retry.")[1] for q in delay_qs} == {"50ms", "100ms", "200ms"}
+        assert e.broker.stats["expired"] == n * 3
+        assert e.converts() == []
+        await e.down()
+    run(main())
+
+
+def test_failing_job_does_not_hold_the_slot(tmp_path):
+    """The reference's Error() slept 10 s in the job goroutine; here the delay
+    lives in the broker, so the next job starts at once."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=5, retry_delay_s=5.0)
+        e.submit(Media(id="bad", source_uri=e.origin.url("/missing.mkv")))
+        await e.wait_results(1)
+        t0 = time.monotonic()
+        good = e.origin.add("/ok.mkv", os.urandom(50_000))
+        e.submit(Media(id="good", source_uri=good), i=1)
+        res = await e.wait_results(2, timeout=10)
+        assert res[1].ok and time.monotonic() - t0 < 2.0
+        assert e.broker.queue_depth("v1.download-0.retry.5000ms") == 1
+        held = e.broker.queues["v1.download-0.retry.5000ms"].messages[0]
+        assert held.props.headers["X-Retries"] == 1
+        assert e.broker.unacked_count() == 0
+        await e.down()
+    run(main())
+
+
+def test_empty_s3_endpoint_is_fatal_before_consuming(tmp_path):
+    """Reference: NewUploader error → log.Fatal before the job loop
+    (downloader.go:95-98).  The worker must exit non-zero without taking a job."""
+    async def main():
+        b = await Broker().start()
+        b.inject("", "nothing", b"")        # no-op; the broker has no queues yet
+        env = dict(os.environ, RABBITMQ_ENDPOINT=b.endpoint, RABBITMQ_USERNAME="guest", RABBITMQ_PASSWORD="guest",
+                   S3_ENDPOINT="", TRITONDL_DOWNLOAD_DIR=str(tmp_path / "dl"), TRITONDL_GPU_VERIFY="off")
+        p = await asyncio.create_subprocess_exec(sys.executable, "-m", "tritondl", cwd=ROOT, env=env,
+                                                 stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.STDOUT)
+        out, _ = await asyncio.wait_for(p.communicate(), 60)
+        assert p.returncode != 0, out.decode()
+        assert b"S3_ENDPOINT" in out
+        assert b.stats["published"] == 0 and not b.conns and "v1.download-0" not in b.queues
+        await b.stop()
     run(main())
 
 

@@ -3,7 +3,7 @@
 
 * ``tritondl/_hash_host*.so``  – g++  (OpenSSL EVP host hashing, pybind11)
 * ``tritondl/_gpu_hash*.so``   – hipcc --offload-arch=gfx950 (HIP kernels)
-* ``tritondl/_relay*.so``      – g++  (native fetch -> S3 data plane, pybind11)
+* ``tritondl/_relay*.so``      – g++  (native fetch -> S3 data plane + OpenSSL TLS streams, pybind11)
 * ``tritondl/_utp*.so``        – g++  (uTP / LEDBAT transport, pybind11)
 
 Rebuilds only when a source is newer than its output.  ``--force`` rebuilds.
@@ -59,7 +59,7 @@ TARGETS = {
         "deps": ["csrc/hash/hash_core.h"],
         "cc": "g++",
         "flags": ["-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread", "-Wall"],
-        "libs": ["-lcrypto"],
+        "libs": ["-lssl", "-lcrypto"],
     },
     "_utp": {
         "srcs": ["csrc/utp/utp.cpp"],

@@ -22,7 +22,7 @@ SRC = os.path.join(ROOT, "csrc", "tests", "native_selftest.cpp")
 
 def build_and_run(flags: list[str], label: str, quick: bool) -> int:
     out = os.path.join(tempfile.gettempdir(), f"tritondl_selftest_{label}")
-    cmd = ["g++", "-std=c++17", "-g", *flags, SRC, "-o", out, "-lcrypto", "-pthread"]
+    cmd = ["g++", "-std=c++17", "-g", *flags, SRC, "-o", out, "-lssl", "-lcrypto", "-pthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         print(r.stdout, r.stderr, file=sys.stderr)

@@ -94,19 +94,26 @@ class Delivery:
         await self._settle(lambda: self.msg.nack(requeue=requeue))
 
     async def retry(self, delay: float | None = None) -> None:
-        """Reference ``Error()``: wait, ack, re-publish the same body to the
-        same exchange/routing key with ``X-Retries + 1`` (``delivery.go:66-84``).
-        The wait is non-blocking here (the Go version slept its goroutine)."""
+        """Reference ``Error()``: re-publish the same body with ``X-Retries + 1``
+        after ``delay`` and ack (``delivery.go:66-84``).
+
+        The Go version slept its goroutine for the delay (``:72``), holding the
+        job slot.  Here the wait happens in the broker: the copy is published
+        (confirmed) to a per-shard delay queue whose ``x-message-ttl`` is the
+        delay and whose dead-letter target is the original exchange/routing key,
+        then the original is acked — the caller's slot is free at once, and a
+        crash at any point duplicates the job instead of losing it."""
         d = self.client.retry_delay if delay is None else delay
-        if d > 0:
-            log.info("retrying message in %s", durafmt(d))
-            await asyncio.sleep(d)
         hdrs = dict(self.msg.properties.headers or {})
         hdrs["X-Retries"] = self.metadata.retries + 1
+        hdrs.pop("x-death", None)
         props = Properties(headers=hdrs, delivery_mode=self.msg.properties.delivery_mode or codec.PERSISTENT,
                            content_type=self.msg.properties.content_type)
-        # publish first (confirmed), then ack: a crash in between duplicates instead of losing the job
-        await self.client.publish_raw(self.msg.exchange, self.msg.routing_key, self.msg.body, props)
+        if d > 0:
+            log.info("retrying message in %s", durafmt(d))
+            await self.client.publish_delayed(self.msg.exchange, self.msg.routing_key, self.msg.body, props, d)
+        else:
+            await self.client.publish_raw(self.msg.exchange, self.msg.routing_key, self.msg.body, props)
         await self.ack()
 
     async def _settle(self, fn) -> None:
@@ -154,6 +161,7 @@ class Client:
         self._pub_lock = asyncio.Lock()
         self._rk_index: dict[str, itertools.cycle] = {}
         self._declared_pub: set[str] = set()
+        self._declared_delay: set[str] = set()
         self._consumer_chans: list[Channel] = []
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -189,6 +197,7 @@ class Client:
         self.generation += 1
         self._pub = None
         self._declared_pub.clear()
+        self._declared_delay.clear()
         self._consumer_chans = []
         self._lost.clear()
         conn.add_close_callback(self._on_conn_lost)
@@ -396,6 +405,44 @@ class Client:
     async def publish_raw(self, exchange: str, routing_key: str, body: bytes, props: Properties,
                           max_attempts: int = 8) -> None:
         await self._publish_retry(exchange, routing_key, body, props, max_attempts, declare=False)
+
+    def delay_queue_name(self, routing_key: str, delay: float) -> str:
+        return f"{routing_key}.retry.{int(round(delay * 1000))}ms"
+
+    async def _ensure_delay_queue(self, exchange: str, routing_key: str, delay: float) -> str:
+        """Durable queue ``<rk>.retry.<ms>ms``: ``x-message-ttl`` = delay, expired
+        messages dead-letter back to ``exchange`` with the original routing key.
+        One queue per (shard, delay) so every message in it has the same TTL
+        (RabbitMQ only expires at the queue head)."""
+        name = self.delay_queue_name(routing_key, delay)
+        if name in self._declared_delay:
+            return name
+        ch = await self._publisher()
+        await ch.queue_declare(name, durable=True, arguments={
+            "x-message-ttl": int(round(delay * 1000)), "x-dead-letter-exchange": exchange,
+            "x-dead-letter-routing-key": routing_key})
+        self._declared_delay.add(name)
+        return name
+
+    async def publish_delayed(self, exchange: str, routing_key: str, body: bytes, props: Properties, delay: float,
+                              max_attempts: int = 8) -> None:
+        """Confirmed publish that reaches ``exchange``/``routing_key`` after ``delay`` seconds."""
+        pol = ExponentialBackoff(initial=0.05, multiplier=2.0, max_interval=5.0, max_elapsed=None)
+        for attempt in range(1, max_attempts + 1):
+            try:
+                async with self._pub_lock:
+                    q = await self._ensure_delay_queue(exchange, routing_key, delay)
+                    ch = await self._publisher()
+                    confirm = await ch.basic_publish("", q, body, props, wait_confirm=False)
+                if confirm is not None:
+                    await confirm
+                return
+            except (AMQPError, ConnectionError, OSError) as e:
+                if attempt == max_attempts or self._closing:
+                    raise
+                d = pol.next_delay() or 0.0
+                log.with_fields(error=str(e), attempt=attempt).warn("delayed publish failed; retrying in %.2fs", d)
+                await asyncio.sleep(d)
 
     async def _publish_retry(self, exchange: str, rk: str, body: bytes, props: Properties, max_attempts: int,
                              declare: bool) -> None:

@@ -602,12 +602,21 @@ class Channel:
             "exchange": exchange, "routing_key": routing_key, "mandatory": mandatory, "immediate": immediate}),
             body, properties or Properties(), self.conn.frame_max or codec.DEFAULT_FRAME_MAX)
         fut = None
+        seq = 0
         if self.confirm_mode:
             self._pub_seq += 1
+            seq = self._pub_seq
             fut = asyncio.get_running_loop().create_future()
-            self._unconfirmed[self._pub_seq] = fut
+            self._unconfirmed[seq] = fut
         self.conn._write(b"".join(frames))
-        await self.conn.drain()
+        try:
+            await self.conn.drain()
+        except BaseException:
+            # nobody will await this confirm: drop it so its eventual failure is not orphaned
+            if fut is not None:
+                self._unconfirmed.pop(seq, None)
+                fut.cancel()
+            raise
         if fut is not None and wait_confirm:
             await fut
             return None

@@ -11,7 +11,10 @@ Implements the RabbitMQ semantics the worker depends on:
   reading: ``global=true`` → per-channel limit, ``false`` → per-consumer);
 * manual ack/nack/reject (+``multiple``), requeue with ``redelivered``;
   unacked messages requeued when a channel or connection closes;
-* dead-lettering via ``x-dead-letter-exchange`` / ``-routing-key``;
+* dead-lettering via ``x-dead-letter-exchange`` / ``-routing-key`` on
+  reject/nack and on expiry (queue ``x-message-ttl`` and per-message
+  ``expiration``, expired at the queue head like RabbitMQ) — the delayed
+  retry queues of :mod:`tritondl.amqp.client` are built on that;
 * ``basic.get``, ``basic.cancel``, publisher confirms, ``mandatory`` returns;
 * fault injection: :meth:`drop_connections`, :meth:`set_blocked`,
   :meth:`fail_next_publishes` (nack), accept-delay.
@@ -22,6 +25,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import itertools
+import time
 from dataclasses import dataclass, field
 from typing import Any
 
@@ -36,6 +40,7 @@ class QMsg:
     exchange: str
     routing_key: str
     redelivered: bool = False
+    expires_at: float | None = None     # monotonic deadline (queue / message TTL)
 
 
 @dataclass
@@ -558,7 +563,12 @@ class Broker:
             q = self.queues.get(t)
             if q is None:
                 continue
-            q.messages.append(QMsg(msg.body, msg.props, msg.exchange, msg.routing_key))
+            qm = QMsg(msg.body, msg.props, msg.exchange, msg.routing_key)
+            ttl = self._ttl_ms(q, msg.props)
+            if ttl is not None:
+                qm.expires_at = time.monotonic() + ttl / 1000.0
+                self._schedule_expiry(q.name, ttl / 1000.0)
+            q.messages.append(qm)
             self._dispatch(q)
         self.stats["routed"] += len(targets)
         return len(targets)
@@ -598,7 +608,46 @@ class Broker:
             return False
         return True
 
+    @staticmethod
+    def _ttl_ms(q: Queue, props: Properties) -> int | None:
+        """Effective TTL: the lower of queue ``x-message-ttl`` and the message's
+        ``expiration`` (a decimal string of milliseconds, RabbitMQ's reading)."""
+        ttls = []
+        qt = q.arguments.get("x-message-ttl")
+        if isinstance(qt, int) and not isinstance(qt, bool) and qt >= 0:
+            ttls.append(qt)
+        exp = getattr(props, "expiration", None)
+        if exp:
+            try:
+                ttls.append(max(0, int(exp)))
+            except ValueError:
+                pass
+        return min(ttls) if ttls else None
+
+    def _schedule_expiry(self, qname: str, delay: float) -> None:
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            return
+        loop.call_later(delay + 0.001, self._expire_head, qname)
+
+    def _expire_head(self, qname: str) -> None:
+        """Expire messages at the queue head (RabbitMQ only expires there) and
+        dead-letter them with reason ``expired``."""
+        q = self.queues.get(qname)
+        if q is None:
+            return
+        now = time.monotonic()
+        while q.messages and q.messages[0].expires_at is not None and q.messages[0].expires_at <= now:
+            msg = q.messages.popleft()
+            self.stats["expired"] += 1
+            self._dead_letter(q, msg, "expired")
+        if q.messages and q.messages[0].expires_at is not None:
+            self._schedule_expiry(qname, max(0.0, q.messages[0].expires_at - now))
+
     def _dispatch(self, q: Queue) -> None:
+        if q.messages and q.messages[0].expires_at is not None and q.messages[0].expires_at <= time.monotonic():
+            self._expire_head(q.name)
         while q.messages and q.consumers:
             n = len(q.consumers)
             chosen = None
@@ -657,16 +706,23 @@ class Broker:
         for cons in ch.consumers.values():
             self._dispatch(cons.queue)
 
-    def _dead_letter(self, q: Queue, msg: QMsg) -> None:
+    def _dead_letter(self, q: Queue, msg: QMsg, reason: str = "rejected") -> None:
         dlx = q.arguments.get("x-dead-letter-exchange")
         if dlx is None:
+            self.stats["dropped"] += 1
             return
         rk = q.arguments.get("x-dead-letter-routing-key", msg.routing_key)
         props = msg.props
         hdrs = dict(props.headers or {})
-        hdrs["x-death"] = [{"queue": q.name, "reason": "rejected", "exchange": msg.exchange,
-                            "routing-keys": [msg.routing_key], "count": 1}]
-        new_props = Properties(**{**props.__dict__, "headers": hdrs})
+        deaths = [d for d in (hdrs.get("x-death") or []) if isinstance(d, dict)]
+        prev = next((d for d in deaths if d.get("queue") == q.name and d.get("reason") == reason), None)
+        if prev is not None:
+            deaths.remove(prev)
+        deaths.insert(0, {"queue": q.name, "reason": reason, "exchange": msg.exchange,
+                          "routing-keys": [msg.routing_key], "count": (prev or {}).get("count", 0) + 1})
+        hdrs["x-death"] = deaths
+        # RabbitMQ strips the per-message TTL when dead-lettering (no instant re-expiry)
+        new_props = Properties(**{**props.__dict__, "headers": hdrs, "expiration": None})
         self._route(QMsg(msg.body, new_props, dlx, rk))
 
 

@@ -2,9 +2,10 @@
 Content-Disposition and fault injection — the stand-in for the media
 servers the HTTP downloader talks to (the reference had no test origin).
 
+``tls=(cert_pem, key_pem)`` serves https (OpenSSL via the relay module).
 Fault knobs: ``ranges`` (advertise/honour Range), ``head`` (support HEAD),
 ``cut_after`` (drop the connection after N body bytes, once per request
-count in ``cut_times``), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap).
+count in ``cut_times``; ``cut_match`` limits it to one Range), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap).
 Without faults or a rate cap, GET bodies leave through ``sendfile`` from a
 native thread (``SendfileResponse``) — blobs held in memory are mirrored to
 a memfd once.
@@ -55,13 +56,16 @@ class Blob:
 
 
 class Origin:
-    def __init__(self, host: str = "127.0.0.1", port: int = 0) -> None:
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, *, tls: tuple[str, str] | None = None) -> None:
+        """``tls``: (cert_pem, key_pem) to serve https."""
         self.host, self.port = host, port
+        self.tls = tls
         self.blobs: dict[str, Blob] = {}
         self.ranges = True
         self.head = True
         self.cut_after: int | None = None
         self.cut_times = 0
+        self.cut_match: str | None = None       # only cut requests whose Range header starts with this
         self.fail = 0
         self.rate: float | None = None
         self.latency = 0.0
@@ -75,10 +79,10 @@ class Origin:
         return self.url(path)
 
     def url(self, path: str) -> str:
-        return f"http://{self.host}:{self.port}{path}"
+        return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}{path}"
 
     async def start(self) -> "Origin":
-        self._server = web.Server(self._handle)
+        self._server = web.Server(self._handle, tls=self.tls)
         self.port = await self._server.start(self.host, self.port)
         return self
 
@@ -135,7 +139,8 @@ class Origin:
         pos = start
         while pos < end:
             n = min(step, end - pos)
-            if self.cut_after is not None and self.cut_times > 0 and sent + n > self.cut_after:
+            if self.cut_after is not None and self.cut_times > 0 and sent + n > self.cut_after and \
+                    (self.cut_match is None or (rng or "").startswith(self.cut_match)):
                 n = self.cut_after - sent
                 if n > 0:
                     await resp.write(blob.read(pos, pos + n))

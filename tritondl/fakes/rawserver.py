@@ -11,8 +11,10 @@ Python:
   (sendfile from a native thread).
 
 Keep-alive, Content-Length and chunked request bodies; one task per
-connection.  Not a general web server — a stand-in for MinIO / a media
-origin on the same box.
+connection; optional TLS (``Server(handler, tls=(cert_pem, key_pem))``) with
+the relay module's OpenSSL streams, so the native hooks work over https too.
+Not a general web server — a stand-in for MinIO / a media origin on the same
+box.
 """
 
 from __future__ import annotations
@@ -137,15 +139,16 @@ class Request:
                 return b"".join(parts)
             parts.append(d)
 
-    def take_body(self) -> tuple[socket.socket, bytes]:
-        """Hand the raw body to a native pump: returns (socket, bytes already
-        buffered).  The caller must consume exactly ``body_length`` bytes."""
+    def take_body(self):
+        """Hand the raw body to a native pump: returns (native stream — a
+        ``_relay.Sock`` or ``_relay.TlsConn`` —, bytes already buffered).  The
+        caller must consume exactly ``body_length`` bytes."""
         assert not self._chunked, "take_body needs a Content-Length body"
         self._taken = True
         pre, self._buf = self._buf, b""
         n = min(len(pre), self._remaining)
         self._remaining = 0
-        return self._conn.sock, pre[:n]
+        return self._conn.raw.native, pre[:n]
 
 
 class Response:
@@ -203,19 +206,23 @@ class _Conn:
         self.loop = asyncio.get_running_loop()
         self.closed = False
         self.streamed: StreamResponse | None = None
+        tls = None
+        if server.tls is not None:
+            tls = rawhttp.relay_module().TlsConn(server.tls, sock.fileno())
+        self.raw = rawhttp.RawConn(sock, tls)
 
     async def recv(self, n: int) -> bytes:
         if self.closed:
             return b""
         try:
-            return await self.loop.sock_recv(self.sock, n)
+            return await self.raw.recv(n)
         except OSError:
             return b""
 
     async def send(self, data: bytes) -> None:
         if self.closed:
             raise ConnectionResetError("connection closed")
-        await self.loop.sock_sendall(self.sock, data)
+        await self.raw.sendall(data)
 
     def abort(self) -> None:
         if not self.closed:
@@ -226,6 +233,8 @@ class _Conn:
     async def serve(self) -> None:
         buf = b""
         try:
+            if self.raw.tls is not None:
+                await self.raw.handshake(30.0)
             while not self.closed:
                 while b"\r\n\r\n" not in buf:
                     d = await self.recv(256 << 10)
@@ -271,17 +280,18 @@ class _Conn:
             return
         finally:
             self.closed = True
-            self.sock.close()
+            self.raw.close()
 
     async def _sendfile(self, resp: SendfileResponse) -> None:
         head = _head_bytes(resp.status, resp.headers, resp.length)
         relay = rawhttp.relay_module()
         if relay is None:
+            assert self.raw.tls is None, "TLS needs the relay extension"
             await self.send(head)
             await self.loop.sock_sendfile(self.sock, _FdFile(resp.fd), resp.offset, resp.length)
             return
-        _sent, _sig, err = await self.loop.run_in_executor(
-            None, relay.send_body, self.sock.fileno(), head, resp.fd, resp.offset, resp.length, None, 0)
+        _sent, _sig, err = await rawhttp.run_pump(self.raw, relay.send_body, head, resp.fd, resp.offset,
+                                                  resp.length, None, 0)
         if err:
             raise ConnectionResetError(err)
 
@@ -309,8 +319,10 @@ class _FdFile:
 
 
 class Server:
-    def __init__(self, handler) -> None:
+    def __init__(self, handler, tls: tuple[str, str] | None = None) -> None:
+        """``tls``: (cert_pem, key_pem) to serve https."""
         self.handler = handler
+        self.tls = rawhttp.relay_module().TlsContext.server(*tls) if tls is not None else None
         self._srv: asyncio.base_events.Server | None = None
         self._conns: set[asyncio.Task] = set()
         self.port = 0

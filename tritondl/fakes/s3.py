@@ -11,7 +11,16 @@ Storage modes: ``memory`` (default), ``disk`` (under ``root``) or
 native relay built, aws-chunked and unsigned PUT bodies are received (and
 every chunk signature verified) by ``_relay.recv_verify_chunked`` /
 ``_relay.recv_body`` outside the interpreter, as MinIO would on its own box.
-Fault injection: :meth:`fail_next` returns 5xx for the next N requests.
+Fault injection: :meth:`fail_next` returns 5xx for the next N requests,
+:meth:`fail_for` for every request during an outage window.
+
+AWS behaviours the client must cope with (minio-go does): every bucket lives
+in a region (``create_bucket(name, region)``, or a ``LocationConstraint``);
+a request signed for another region gets 400 ``AuthorizationHeaderMalformed``
+naming the bucket's ``<Region>`` (and ``x-amz-bucket-region``), while
+``GET ?location`` answers for any signing region.  Part numbers are limited to
+1..10000 and every part but the last must be ≥ 5 MiB (``strict_parts``).
+``tls=(cert_pem, key_pem)`` serves https.
 """
 
 from __future__ import annotations
@@ -22,6 +31,7 @@ import hmac
 import itertools
 import os
 import re
+import time
 from dataclasses import dataclass, field
 from urllib.parse import parse_qsl, unquote
 
@@ -49,16 +59,22 @@ class Upload:
     parts: dict = field(default_factory=dict)  # n -> Obj
 
 
-def _xml_err(status: int, code: str, msg: str) -> web.Response:
-    body = f"<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>{code}</Code><Message>{msg}</Message></Error>"
+def _xml_err(status: int, code: str, msg: str, region: str = "") -> web.Response:
+    reg = f"<Region>{region}</Region>" if region else ""
+    body = (f"<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>{code}</Code><Message>{msg}</Message>"
+            f"{reg}</Error>")
     return web.Response(status=status, body=body.encode(), content_type="application/xml")
 
 
 class FakeS3:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, *, access_key: str | None = None,
                  secret_key: str | None = None, region: str = "us-east-1", store: str = "memory",
-                 root: str | None = None) -> None:
+                 root: str | None = None, tls: tuple[str, str] | None = None, strict_parts: bool = True) -> None:
         self.host, self.port = host, port
+        self.tls = tls
+        self.strict_parts = strict_parts
+        self.bucket_regions: dict[str, str] = {}
+        self._outage_until = 0.0
         self.access_key, self.secret_key = access_key, secret_key
         self.region = region
         self.store = store
@@ -75,7 +91,7 @@ class FakeS3:
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> "FakeS3":
-        self._server = web.Server(self._handle)
+        self._server = web.Server(self._handle, tls=self.tls)
         self.port = await self._server.start(self.host, self.port)
         return self
 
@@ -86,10 +102,22 @@ class FakeS3:
 
     @property
     def endpoint(self) -> str:
-        return f"http://{self.host}:{self.port}"
+        return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}"
 
     def fail_next(self, n: int, status: int = 503) -> None:
         self._fail, self._fail_status = n, status
+
+    def fail_for(self, seconds: float, status: int = 503) -> None:
+        """Outage: every request gets ``status`` for the next ``seconds``."""
+        self._outage_until, self._fail_status = time.monotonic() + seconds, status
+
+    def create_bucket(self, name: str, region: str | None = None) -> None:
+        self.buckets.setdefault(name, {})
+        self.bucket_regions[name] = region or self.region
+
+    def delete_bucket(self, name: str) -> None:
+        self.buckets.pop(name, None)
+        self.bucket_regions.pop(name, None)
 
     def object_bytes(self, bucket: str, key: str) -> bytes:
         o = self.buckets[bucket][key]
@@ -129,6 +157,7 @@ class FakeS3:
             return _xml_err(403, "InvalidAccessKeyId", "unknown access key")
         secret = self.secret_key or ""
         date, region, service, _term = scope_rest.split("/")
+        request.signed_region = region
         amzdate = request.headers.get("x-amz-date", "")
         hdrs = {}
         for h in signed_headers.split(";"):
@@ -160,9 +189,9 @@ class FakeS3:
             return await self._read_chunked(request, auth, keep)
         if relay is not None and not keep and phash in (sigv4.UNSIGNED_PAYLOAD, "") and request.body_length:
             n = request.body_length
-            sock, pre = request.take_body()
+            stream, pre = request.take_body()
             got, _eof, err = await asyncio.get_running_loop().run_in_executor(
-                None, relay.recv_body, sock.fileno(), -1, 0, n, pre, None, 0, 0, 300.0)
+                None, relay.recv_body, stream, -1, 0, n, pre, None, 0, 0, 300.0)
             if err:
                 request.transport.close()
                 raise _BadReq(400, "IncompleteBody", err)
@@ -180,9 +209,9 @@ class FakeS3:
         key, seed, amzdate, scope = auth
         decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
         raw_len = request.body_length
-        sock, pre = request.take_body()
+        stream, pre = request.take_body()
         n, err, data = await asyncio.get_running_loop().run_in_executor(
-            None, relay.recv_verify_chunked, sock.fileno(), raw_len, pre, key, amzdate, scope, seed, keep, 4, 300.0)
+            None, relay.recv_verify_chunked, stream, raw_len, pre, key, amzdate, scope, seed, keep, 4, 300.0)
         self.bytes_received += raw_len
         if err:
             if "closed" in err or "timeout" in err or "socket" in err or "recv" in err:
@@ -287,16 +316,28 @@ class FakeS3:
 
     async def _handle(self, request: web.Request) -> web.StreamResponse:
         self.requests.append((request.method, request.raw_path))
-        if self._fail > 0:
-            self._fail -= 1
+        if self._fail > 0 or time.monotonic() < self._outage_until:
+            self._fail = max(0, self._fail - 1)
             await request.read()
             return _xml_err(self._fail_status, "ServiceUnavailable", "injected failure")
+        request.signed_region = None
         auth = self._verify(request)
         if isinstance(auth, web.Response):
             await request.read()
             return auth
         bucket, key = self._split(request)
         q = dict(parse_qsl(request.query_string, keep_blank_values=True))
+        # region check (AWS): requests on a bucket must be signed for its region;
+        # GET ?location answers whatever the signing region
+        breg = self.bucket_regions.get(bucket, self.region) if bucket in self.buckets else None
+        sreg = request.signed_region
+        if breg is not None and sreg is not None and sreg != breg and not (request.method == "GET" and not key
+                                                                           and "location" in q):
+            await request.read()
+            r = _xml_err(400, "AuthorizationHeaderMalformed",
+                         f"the region '{sreg}' is wrong; expecting '{breg}'", region=breg)
+            r.headers["x-amz-bucket-region"] = breg
+            return r
         try:
             if not key:
                 return await self._bucket_op(request, bucket, q, auth)
@@ -309,14 +350,24 @@ class FakeS3:
         if m == "HEAD":
             return web.Response(status=200 if bucket in self.buckets else 404)
         if m == "PUT":
-            await self._read_body(request, auth)
+            body = await self._read_body(request, auth)
             if bucket in self.buckets:
                 return _xml_err(409, "BucketAlreadyOwnedByYou", "bucket exists")
-            self.buckets[bucket] = {}
+            mm = re.search(rb"<LocationConstraint>([^<]*)</LocationConstraint>", bytes(body or b""))
+            loc = mm.group(1).decode() if mm else "us-east-1"
+            sreg = getattr(request, "signed_region", None)
+            if sreg is not None and sreg != loc:
+                return _xml_err(400, "AuthorizationHeaderMalformed",
+                                f"the region '{sreg}' is wrong; expecting '{loc}'", region=loc)
+            self.create_bucket(bucket, loc)
             return web.Response(status=200, headers={"Location": "/" + bucket})
         if m == "GET" and bucket in self.buckets:
             if "location" in q:
-                return web.Response(body=b"<LocationConstraint/>", content_type="application/xml")
+                reg = self.bucket_regions.get(bucket, self.region)
+                val = "" if reg == "us-east-1" else reg
+                body = (f'<?xml version="1.0" encoding="UTF-8"?><LocationConstraint '
+                        f'xmlns="http://s3.amazonaws.com/doc/2006-03-01/">{val}</LocationConstraint>')
+                return web.Response(body=body.encode(), content_type="application/xml")
             prefix = q.get("prefix", "")
             keys = sorted(k for k in self.buckets[bucket] if k.startswith(prefix))
             items = "".join(f"<Contents><Key>{_xml_escape(k)}</Key><Size>{self.buckets[bucket][k].size}</Size>"
@@ -340,6 +391,10 @@ class FakeS3:
             if up is None:
                 await request.read()
                 return _xml_err(404, "NoSuchUpload", "no such upload")
+            pn = int(q.get("partNumber", "0") or 0)
+            if self.strict_parts and not 1 <= pn <= 10000:
+                await request.read()
+                return _xml_err(400, "InvalidArgument", "Part number must be an integer between 1 and 10000")
             data = await self._read_body(request, auth, keep=self.store != "discard")
             o = self._save(data)
             up.parts[int(q["partNumber"])] = o
@@ -367,6 +422,10 @@ class FakeS3:
             if nums != sorted(nums) or any(up.parts.get(n) is None or up.parts[n].etag != t
                                            for n, t in zip(nums, tags)):
                 return _xml_err(400, "InvalidPart", "parts mismatch")
+            if self.strict_parts and (len(nums) > 10000 or
+                                      any(up.parts[n].size < (5 << 20) for n in nums[:-1])):
+                return _xml_err(400, "EntityTooSmall", "Your proposed upload is smaller than the minimum "
+                                "allowed object size.")
             if self.store == "memory":
                 data = b"".join(up.parts[n].data or b"" for n in nums)
                 o = self._save(data)

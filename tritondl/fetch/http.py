@@ -24,11 +24,15 @@ Beyond the reference:
   probe is ``GET bytes=0-(probe_bytes-1)`` and the rest of a bigger file is
   requested at once as parallel Range streams, so mid-size files are
   segmented too and no half-read probe connection is dropped;
-* plain-``http`` bodies never enter Python: after the head is parsed the
-  socket goes to the native receive pump (``csrc/relay``, GIL released),
-  which writes the file and publishes progress on a native ``Flow`` that
-  the S3 send pump follows (``https``, redirects and chunked / encoded
-  bodies use aiohttp).
+* ``http`` and ``https`` bodies never enter Python: after the head is
+  parsed the connection (a plain socket, or an OpenSSL TLS session driven by
+  the relay module) goes to the native receive pump (``csrc/relay``, GIL
+  released), which writes the file and publishes progress on a native
+  ``Flow`` that the S3 send pump follows (redirects and chunked / encoded
+  bodies use aiohttp);
+* when one segment fails, its siblings are cancelled and their pumps
+  stopped and awaited before the file or any socket is closed (no write
+  through a recycled fd number).
 """
 
 from __future__ import annotations
@@ -59,11 +63,12 @@ class _FatalHTTPError(HTTPDownloadError):
 
 
 class _RawResponse:
-    """The bits of an aiohttp response this module uses, over a raw socket
-    whose body the native pump reads."""
+    """The bits of an aiohttp response this module uses, over a raw
+    connection (plain or TLS) whose body the native pump reads."""
 
-    def __init__(self, pool: rawhttp.Pool, host: str, port: int, sock, head: rawhttp.Head, url: str) -> None:
-        self.pool, self.host, self.port, self.sock, self.head = pool, host, port, sock, head
+    def __init__(self, pool: rawhttp.Pool, host: str, port: int, conn: rawhttp.RawConn, head: rawhttp.Head,
+                 url: str) -> None:
+        self.pool, self.host, self.port, self.sock, self.head = pool, host, port, conn, head
         self.status = head.status
         self.headers = head.headers
         self.url = URL(url)
@@ -123,7 +128,8 @@ class HTTPDownloader:
     def __init__(self, *, progress_interval: float = 1.0, segments: int = 4, segment_threshold: int = 64 << 20,
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
-                 native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0) -> None:
+                 native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
+                 ca_pem: str = "", ca_file: str = "") -> None:
         self.progress_interval = progress_interval
         # >0: the GET probe asks for bytes=0-(probe_bytes-1); once its head names the
         # size, the rest of a bigger file is requested at once as up to `segments`
@@ -146,15 +152,31 @@ class HTTPDownloader:
         # range streams (1 GiB fetch 154 vs 85 ms), so opt-in: TRITONDL_RELAY_SPLICE=1
         self.splice = os.environ.get("TRITONDL_RELAY_SPLICE", "0").lower() in ("1", "on", "true", "yes")
         self._raw = rawhttp.Pool()
+        # https trust: a private CA (PEM text / file), else the system store
+        self.ca_pem, self.ca_file = ca_pem, ca_file or os.environ.get("TRITONDL_CA_FILE", "")
+        self._ntls = None
+
+    def _tls_ctx(self):
+        if self._ntls is None:
+            relay = rawhttp.relay_module()
+            if self.ca_pem and relay is not None:
+                self._ntls = relay.TlsContext.client(ca_pem=self.ca_pem)
+            else:
+                self._ntls = rawhttp.client_tls_context(self.ca_file)
+        return self._ntls
 
     def register(self) -> ClientRegister:
         return ClientRegister(name="http", protocols=["http", "https"])
 
     async def _sess(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
+            ssl_ctx: object = True
+            if self.ca_pem or self.ca_file:
+                import ssl
+                ssl_ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
             self._session = aiohttp.ClientSession(
                 timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=120),
-                connector=aiohttp.TCPConnector(limit=64), auto_decompress=False)
+                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx), auto_decompress=False)
         return self._session
 
     async def close(self) -> None:
@@ -165,7 +187,7 @@ class HTTPDownloader:
 
     # ------------------------------------------------------------ transport
     def _native_for(self, url: str):
-        if not self.native or not url.startswith("http://"):
+        if not self.native or not url.startswith(("http://", "https://")):
             return None
         return rawhttp.relay_module()
 
@@ -181,29 +203,36 @@ class HTTPDownloader:
 
     async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":
         u = URL(url)
-        host, port = u.raw_host or "", u.port or 80
+        secure = u.scheme == "https"
+        dport = 443 if secure else 80
+        host, port = u.raw_host or "", u.port or dport
         target = u.raw_path_qs or "/"
-        hh = {"Host": host if port == 80 else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
+        hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
         head = rawhttp.request_head("GET", target, hh)
-        loop = asyncio.get_running_loop()
-        for _ in range(2):                    # a stale pooled keep-alive socket gets one fresh retry
-            sock, reused = await self._raw.connect(host, port)
+        tls = self._tls_ctx() if secure else None
+        if secure and tls is None:
+            return None
+        for _ in range(2):                    # a stale pooled keep-alive connection gets one fresh retry
             try:
-                await asyncio.wait_for(loop.sock_sendall(sock, head), self.read_timeout)
-                h = await rawhttp.read_head(sock, self.read_timeout)
+                conn, reused = await self._raw.connect(host, port, timeout=30.0, tls=tls)
             except (OSError, rawhttp.RawHTTPError) as e:
-                sock.close()
+                raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
+            try:
+                await asyncio.wait_for(conn.sendall(head), self.read_timeout)
+                h = await rawhttp.read_head(conn, self.read_timeout)
+            except (OSError, rawhttp.RawHTTPError) as e:
+                conn.close()
                 if reused:
                     continue
                 raise aiohttp.ClientConnectionError(str(e)) from e
             except BaseException:
-                sock.close()
+                conn.close()
                 raise
             enc = h.headers.get("Content-Encoding", "identity").lower()
             if 300 <= h.status < 400 or h.chunked or enc not in ("", "identity"):
-                sock.close()                  # redirect / chunked / encoded body: aiohttp handles these
+                conn.close()                  # redirect / chunked / encoded body: aiohttp handles these
                 return None
-            return _RawResponse(self._raw, host, port, sock, h, url)
+            return _RawResponse(self._raw, host, port, conn, h, url)
         raise aiohttp.ClientConnectionError(f"GET {url}: connection reset")
 
     # ------------------------------------------------------------ probe
@@ -343,15 +372,23 @@ class HTTPDownloader:
 
         fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
+        tasks = [asyncio.ensure_future(self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
+                                                           first if i == 0 else None))
+                 for i in range(len(segs))]
         try:
-            await asyncio.gather(*(self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
-                                                       first if i == 0 else None)
-                                   for i in range(len(segs))))
+            await asyncio.gather(*tasks)
         except BaseException as e:
+            # stop every sibling and WAIT for it: their native pumps write through
+            # `fd` and read their own sockets, which must stay open until they return
+            h._fail(e)                       # the error a following upload reports
+            if h.flow is not None:
+                h.flow.cancel()
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
             if first is not None:
                 first.close()
             sync_save()
-            h._fail(e)
             raise
         finally:
             rep.cancel()
@@ -379,11 +416,12 @@ class HTTPDownloader:
             return [[0, -1, 0]]
         if self.probe_bytes and p.ranges and p.first_end is not None:
             # bounded GET probe: its body is segment 0; the rest goes to up to
-            # `segments` further Range streams, none shorter than the probe's body
+            # `segments - 1` further Range streams, none shorter than the probe's body
             if p.first_end >= p.size:
                 return [[0, p.size, 0]]
             rest = p.size - p.first_end
-            k = max(1, min(self.segments, -(-rest // p.first_end)))
+            # the probe is one of the `segments` streams: at most segments-1 more
+            k = max(1, min(max(1, self.segments - 1), -(-rest // p.first_end)))
             step = -(-rest // k)
             return [[0, p.first_end, 0]] + [[p.first_end + i * step, min(p.size, p.first_end + (i + 1) * step), 0]
                                             for i in range(k) if p.first_end + i * step < p.size]
@@ -456,6 +494,8 @@ class HTTPDownloader:
                 return
             except (aiohttp.ClientError, asyncio.TimeoutError, HTTPDownloadError, ConnectionError) as e:
                 attempt += 1
+                if h is not None and h.flow is not None and h.flow.cancelled:
+                    raise _FatalHTTPError(f"segment {i} of {url}: download cancelled") from e
                 if attempt > self.max_retries or isinstance(e, _FatalHTTPError) or \
                         (isinstance(e, HTTPDownloadError) and "HTTP 4" in str(e)):
                     raise HTTPDownloadError(f"segment {i} of {url} failed: {e}") from e
@@ -515,15 +555,16 @@ class HTTPDownloader:
         prefix, r.leftover = r.leftover, b""
         flow = h.flow if h is not None else None
         rawhttp.trace("get_pump_start")
-        got, eof, err = await asyncio.get_running_loop().run_in_executor(
-            None, relay.recv_body, r.sock.fileno(), fd, pos, n, prefix, flow, i, done[i], self.read_timeout,
-            4 << 20, self.splice)
+        got, eof, err = await rawhttp.run_pump(
+            r.sock, relay.recv_body, fd, pos, n, prefix, flow, i, done[i], self.read_timeout, 4 << 20, self.splice)
         rawhttp.trace("get_pump_end")
         done[i] += got
         if h is not None:
             h._advance(i, done[i])
         if err:
             r.close()
+            if err == "cancelled" or (flow is not None and flow.cancelled):
+                raise _FatalHTTPError(f"segment {i}: cancelled")
             raise HTTPDownloadError(err)
         r.complete = (n < 0 and eof) or (cl is not None and n == cl and len(prefix) <= cl)
         if n < 0:

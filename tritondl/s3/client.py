@@ -8,6 +8,19 @@ Creds, BucketLookupAuto}``, ``BucketExists``, ``MakeBucket``,
 above it).  Memory stays O(part_size × parallel_parts) regardless of file
 size; file reads and chunk signing run in worker threads
 (the native hash module releases the GIL), so several uploads overlap.
+
+minio-go library behaviours the reference relied on without naming them:
+
+* no Region in ``NewWithOptions`` (``uploader.go:43-51``) means minio looks
+  the bucket's region up (``GET /<bucket>?location``, cached per bucket) and
+  signs with it; a reply of ``AuthorizationHeaderMalformed`` /
+  ``InvalidRegion`` / a 301 naming ``x-amz-bucket-region`` re-signs with the
+  region S3 names (:meth:`S3Client.bucket_region`);
+* ``PutObject`` sizes parts so an object never needs more than 10,000 parts
+  and refuses objects over 5 TiB (minio ``optimalPartInfo``; :func:`plan_parts`);
+* an empty or malformed endpoint is an error when the client is built
+  (minio ``NewWithOptions`` → ``log.Fatal`` in ``downloader.go:95-98``;
+  :meth:`Endpoint.parse`).
 """
 
 from __future__ import annotations
@@ -33,23 +46,57 @@ from .credentials import Chain, Provider, Value, default_chain
 
 S3_NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
 _DNS_BUCKET = re.compile(r"^[a-z0-9][a-z0-9.-]{1,61}[a-z0-9]$")
+_HOST = re.compile(r"^(?:[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)*$")
+
+# S3 limits (minio-go constants.go): parts per upload, object / part / single-PUT sizes
+MAX_PARTS = 10000
+MIN_PART_SIZE = 5 << 20
+MAX_PART_SIZE = 5 << 30
+MAX_SINGLE_PUT = 5 << 30
+MAX_OBJECT_SIZE = 5 << 40
+DEFAULT_REGION = "us-east-1"
+_REGION_CODES = ("AuthorizationHeaderMalformed", "InvalidRegion", "PermanentRedirect", "IllegalLocationConstraintException")
 
 
 class S3Error(Exception):
-    def __init__(self, status: int, code: str = "", message: str = "", resource: str = "") -> None:
+    def __init__(self, status: int, code: str = "", message: str = "", resource: str = "",
+                 region: str = "") -> None:
         super().__init__(f"S3 {status} {code}: {message} ({resource})")
         self.status, self.code, self.message, self.resource = status, code, message, resource
+        self.region = region          # the bucket's region when S3 names it (XML <Region> / x-amz-bucket-region)
 
 
-def _parse_error(status: int, body: bytes, resource: str) -> S3Error:
-    code = msg = ""
-    try:
-        root = ET.fromstring(body)
-        code = (root.findtext("Code") or "")
-        msg = (root.findtext("Message") or "")
-    except ET.ParseError:
-        msg = body[:200].decode(errors="replace")
-    return S3Error(status, code, msg, resource)
+def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Error:
+    code = msg = region = ""
+    if body:
+        try:
+            root = ET.fromstring(body)
+            code = (root.findtext("Code") or "")
+            msg = (root.findtext("Message") or "")
+            region = (root.findtext("Region") or "")
+        except ET.ParseError:
+            msg = body[:200].decode(errors="replace")
+    if headers is not None:
+        region = region or headers.get("x-amz-bucket-region", "") or ""
+    if not code:     # HEAD replies carry no body: name the error like minio does
+        code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
+                resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
+    return S3Error(status, code, msg, resource, region)
+
+
+def plan_parts(size: int, part_size: int) -> tuple[int, int]:
+    """(part size, part count) for a multipart upload of ``size`` bytes.
+
+    minio-go ``optimalPartInfo``: the smallest multiple of the configured part
+    size that keeps the upload within 10,000 parts; objects over 5 TiB are
+    refused before any byte is sent."""
+    if size > MAX_OBJECT_SIZE:
+        raise S3Error(0, "EntityTooLarge", f"object of {size} bytes exceeds the 5 TiB S3 maximum")
+    base = max(part_size, MIN_PART_SIZE)
+    need = -(-size // MAX_PARTS)
+    ps = base if need <= base else -(-need // base) * base
+    ps = min(ps, MAX_PART_SIZE)
+    return ps, max(1, -(-size // ps))
 
 
 @dataclass
@@ -60,13 +107,36 @@ class Endpoint:
     @classmethod
     def parse(cls, s3_endpoint: str) -> "Endpoint":
         """Reference parsing of ``S3_ENDPOINT`` (``uploader.go:25-40``): TLS iff
-        scheme is https; keep hostname[:port]."""
-        if s3_endpoint and "://" not in s3_endpoint:
-            s3_endpoint = "http://" + s3_endpoint  # bare host[:port] (Go would yield an empty host)
-        u = urlparse(s3_endpoint)
+        scheme is https; keep hostname[:port].  An endpoint minio-go would
+        refuse (empty, no host, bad host or port) raises ``ValueError``."""
+        raw = s3_endpoint or ""
+        if raw.strip() == "":
+            raise ValueError("S3_ENDPOINT is empty: endpoint url cannot be empty")
+        if "://" not in raw:
+            raw = "http://" + raw  # bare host[:port] (Go would yield an empty host)
+        u = urlparse(raw)
+        if u.scheme not in ("http", "https"):
+            raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: scheme must be http or https")
         host = u.hostname or ""
-        if u.port:
-            host = f"{host}:{u.port}"
+        try:
+            port = u.port
+        except ValueError as e:
+            raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: invalid port") from e
+        if not host:
+            raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: no host")
+        if ":" in host:                 # IPv6 literal
+            try:
+                import ipaddress
+                ipaddress.IPv6Address(host)
+            except ValueError as e:
+                raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: invalid host") from e
+            host = f"[{host}]"
+        elif not _HOST.match(host):
+            raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: {host!r} is not a valid domain name or ip address")
+        if u.path not in ("", "/"):
+            raise ValueError(f"S3_ENDPOINT {s3_endpoint!r}: endpoint url cannot have a path")
+        if port:
+            host = f"{host}:{port}"
         return cls(host, u.scheme == "https")
 
     @property
@@ -75,14 +145,15 @@ class Endpoint:
 
 
 class S3Client:
-    def __init__(self, endpoint: Endpoint | str, creds: Provider | None = None, *, region: str = "us-east-1",
+    def __init__(self, endpoint: Endpoint | str, creds: Provider | None = None, *, region: str = "",
                  lookup: str = "auto", payload_mode: str = "auto", part_size: int = 64 << 20,
                  multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
                  io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
-                 native: bool = True, sign_threads: int = 4) -> None:
+                 native: bool = True, sign_threads: int = 4, ca_pem: str = "", ca_file: str = "") -> None:
         self.ep = Endpoint.parse(endpoint) if isinstance(endpoint, str) else endpoint
         self.creds = creds or default_chain()
-        self.region = region
+        self.region = region            # "" = discover each bucket's region (minio-go without Region)
+        self._regions: dict[str, str] = {}
         self.lookup = lookup
         self.payload_mode = payload_mode
         self.part_size = max(part_size, 5 << 20)
@@ -96,12 +167,37 @@ class S3Client:
         self.native = native
         self.sign_threads = sign_threads
         self._raw = rawhttp.Pool()
+        # TLS trust for https endpoints: a private CA (PEM text / file), else the system store
+        self.ca_pem, self.ca_file = ca_pem, ca_file or os.environ.get("TRITONDL_CA_FILE", "")
+        self._ntls = None
+
+    def _ssl(self):
+        """Python ``ssl`` context for the aiohttp control requests (None = default)."""
+        if not (self.ep.secure and (self.ca_pem or self.ca_file)):
+            return None
+        import ssl
+        ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
+        return ctx
+
+    def _tls_ctx(self):
+        """Native client TLS context for the relay pumps (None for plain http)."""
+        if not self.ep.secure:
+            return None
+        if self._ntls is None:
+            relay = rawhttp.relay_module()
+            if self.ca_pem and relay is not None:
+                self._ntls = relay.TlsContext.client(ca_pem=self.ca_pem)
+            else:
+                self._ntls = rawhttp.client_tls_context(self.ca_file)
+        return self._ntls
 
     async def _sess(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
+            ssl_ctx = self._ssl()
             self._session = aiohttp.ClientSession(
                 timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=300),
-                connector=aiohttp.TCPConnector(limit=64), auto_decompress=False)
+                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx if ssl_ctx is not None else True),
+                auto_decompress=False)
             self._own_session = True
         return self._session
 
@@ -122,9 +218,9 @@ class S3Client:
         return (host.endswith("amazonaws.com") or host.endswith("aliyuncs.com")) and \
             bool(_DNS_BUCKET.match(bucket)) and "." not in bucket
 
-    def _target(self, bucket: str, key: str = "") -> tuple[str, str]:
+    def _target(self, bucket: str, key: str = "", path_style: bool = False) -> tuple[str, str]:
         ekey = sigv4.uri_encode(key, encode_slash=False) if key else ""
-        if self._virtual(bucket):
+        if not path_style and self._virtual(bucket):
             return f"{bucket}.{self.ep.host}", "/" + ekey
         path = "/" + bucket if bucket else "/"
         if key:
@@ -139,16 +235,65 @@ class S3Client:
     def _creds(self) -> Value:
         return self.creds.retrieve()
 
+    # ------------------------------------------------------------ regions
+    async def bucket_region(self, bucket: str) -> str:
+        """Signing region for ``bucket``: the configured one, else the cached
+        ``GET ?location`` answer (minio-go ``getBucketLocation``)."""
+        if self.region:
+            return self.region
+        if not bucket:
+            return DEFAULT_REGION
+        r = self._regions.get(bucket)
+        if r is not None:
+            return r
+        try:
+            _st, _h, body = await self._do("GET", bucket, query={"location": ""}, region=DEFAULT_REGION,
+                                           path_style=True)
+            loc = ""
+            try:
+                root = ET.fromstring(body)
+                loc = (root.text or "").strip()
+            except ET.ParseError:
+                pass
+            r = {"": DEFAULT_REGION, "EU": "eu-west-1"}.get(loc, loc)
+        except S3Error as e:
+            # minio: access-denied / wrong-region replies still name a usable region
+            if e.code in _REGION_CODES + ("AccessDenied",):
+                r = e.region or DEFAULT_REGION
+            elif e.code == "NoSuchBucket":
+                return DEFAULT_REGION       # not cached: the bucket may be created next
+            else:
+                raise
+        self._regions[bucket] = r
+        return r
+
+    def forget_bucket(self, bucket: str) -> None:
+        """Drop cached facts about ``bucket`` (deleted / recreated elsewhere)."""
+        self._regions.pop(bucket, None)
+
+    def _learn_region(self, bucket: str, err: S3Error, used: str) -> bool:
+        """True when ``err`` says the request was signed for the wrong region and
+        names the right one (cached; the caller re-signs without counting a try)."""
+        if self.region or not bucket or not err.region or err.region == used:
+            return False
+        if err.code in _REGION_CODES or err.status in (301, 400):
+            log.with_fields(bucket=bucket, region=err.region).info("bucket region discovered")
+            self._regions[bucket] = err.region
+            return True
+        return False
+
     async def _do(self, method: str, bucket: str, key: str = "", query: dict | None = None,
                   headers: dict | None = None, body: bytes | None = None, *, body_factory=None,
                   payload_hash: str | None = None, expect: tuple[int, ...] = (200,),
-                  retry: bool = True) -> tuple[int, dict, bytes]:
+                  retry: bool = True, region: str | None = None, path_style: bool = False) -> tuple[int, dict, bytes]:
         """One signed request with retries on connection errors / 5xx."""
         pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         attempt = 0
+        region_hops = 0
         while True:
             attempt += 1
-            host, path = self._target(bucket, key)
+            host, path = self._target(bucket, key, path_style)
+            sreg = region if region is not None else await self.bucket_region(bucket)
             amzdate, _ = sigv4.amz_dates()
             hdrs = {"host": host, "x-amz-date": amzdate}
             hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
@@ -167,7 +312,7 @@ class S3Client:
                 if cred.session_token:
                     hdrs["x-amz-security-token"] = cred.session_token
                 signed = sigv4.sign(method, path, query, hdrs, phash, cred.access_key_id, cred.secret_access_key,
-                                    self.region, amzdate, path_is_encoded=True)
+                                    sreg, amzdate, path_is_encoded=True)
                 if callable(getattr(data, "bind_seed", None)):
                     data.bind_seed(signed)
                 hdrs["authorization"] = signed.authorization
@@ -179,11 +324,15 @@ class S3Client:
                 sess = await self._sess()
                 payload = data.stream() if hasattr(data, "stream") else data
                 async with sess.request(method, url, headers=send_headers, data=payload,
-                                        skip_auto_headers=("Content-Type",)) as r:
+                                        skip_auto_headers=("Content-Type",), allow_redirects=False) as r:
                     rbody = await r.read()
                     if r.status in expect:
                         return r.status, CIMultiDict(r.headers), rbody
-                    err = _parse_error(r.status, rbody, f"{method} {path}")
+                    err = _parse_error(r.status, rbody, f"{method} {path}", r.headers)
+                    if region is None and region_hops < 2 and self._learn_region(bucket, err, sreg):
+                        region_hops += 1
+                        attempt -= 1
+                        continue
                     if r.status < 500 or not retry or attempt > self.max_retries:
                         raise err
             except (aiohttp.ClientError, asyncio.TimeoutError, ConnectionError) as e:
@@ -205,11 +354,16 @@ class S3Client:
             raise
 
     async def make_bucket(self, bucket: str, location: str = "") -> None:
+        """minio ``MakeBucket``: location "" → the client's region, else us-east-1;
+        the request is signed for that location and the answer cached."""
+        location = location or self.region or DEFAULT_REGION
         body = None
-        if location and location != "us-east-1":
+        if location != DEFAULT_REGION:
             body = (f'<CreateBucketConfiguration xmlns="http://s3.amazonaws.com/doc/2006-03-01/">'
                     f"<LocationConstraint>{location}</LocationConstraint></CreateBucketConfiguration>").encode()
-        await self._do("PUT", bucket, body=body if body is not None else b"", expect=(200,))
+        await self._do("PUT", bucket, body=body if body is not None else b"", expect=(200,), region=location)
+        if not self.region:
+            self._regions[bucket] = location
 
     # ------------------------------------------------------------ objects
     async def put_object(self, bucket: str, key: str, src: str | bytes | int, size: int | None = None,
@@ -227,7 +381,7 @@ class S3Client:
                 size = os.fstat(src).st_size
             else:
                 size = os.path.getsize(src)
-        if size >= self.multipart_threshold and size > self.part_size:
+        if size > MAX_SINGLE_PUT or (size >= self.multipart_threshold and size > self.part_size):
             return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes, flow)
         return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type},
                                      wait_bytes=wait_bytes, flow=flow)
@@ -236,7 +390,7 @@ class S3Client:
                          headers: dict, query: dict | None = None, wait_bytes=None, flow=None) -> str:
         mode = self._payload_mode()
         relay = rawhttp.relay_module() if self.native else None
-        if relay is not None and not self.ep.secure and mode in ("streaming", "unsigned") and \
+        if relay is not None and mode in ("streaming", "unsigned") and \
                 not isinstance(src, (bytes, bytearray, memoryview)) and (flow is not None or wait_bytes is None):
             return await self._put_native(relay, bucket, key, src, offset, length, headers, query, mode, flow)
         factory = _BodyFactory(self, src, offset, length, mode, wait_bytes)
@@ -245,36 +399,35 @@ class S3Client:
 
     async def _put_multipart(self, bucket: str, key: str, src: str | bytes | int, size: int, content_type: str,
                              wait_bytes=None, flow=None) -> str:
+        plan_parts(size, self.part_size)           # refuse > 5 TiB before initiating
         _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
                                        headers={"content-type": content_type}, body=b"")
         root = ET.fromstring(body)
         upload_id = root.findtext(f"{S3_NS}UploadId") or root.findtext("UploadId") or ""
         if not upload_id:
             raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
-        nparts = (size + self.part_size - 1) // self.part_size
+        part_size, nparts = plan_parts(size, self.part_size)
         etags: list[str] = [""] * nparts
-        todo = list(range(nparts))
-
-        def pick() -> int:
-            # Following a download: take the part that will be on disk soonest (a segmented
-            # download fills several regions at once; in part order the uploads would queue
-            # behind the first segment).  Otherwise in order.
-            if flow is None or len(todo) == 1:
-                return todo.pop(0)
-            best = min(range(len(todo)), key=lambda k: (flow.bytes_until_covered(
-                todo[k] * self.part_size, min(size, (todo[k] + 1) * self.part_size)), todo[k]))
-            return todo.pop(best)
+        todo = _PartQueue(nparts, part_size, size, flow)
 
         async def worker() -> None:
             while todo:
-                i = pick()
-                off = i * self.part_size
-                ln = min(self.part_size, size - off)
+                i = todo.pick()
+                off = i * part_size
+                ln = min(part_size, size - off)
                 etags[i] = await self._put_range(bucket, key, src, off, ln, {},
                                                  query={"partNumber": str(i + 1), "uploadId": upload_id},
                                                  wait_bytes=wait_bytes, flow=flow)
+        workers = [asyncio.ensure_future(worker()) for _ in range(min(self.parallel_parts, nparts))]
         try:
-            await asyncio.gather(*(worker() for _ in range(min(self.parallel_parts, nparts))))
+            try:
+                await asyncio.gather(*workers)
+            except BaseException:
+                # stop the siblings and wait for them (their native pumps hold fds)
+                for w in workers:
+                    w.cancel()
+                await asyncio.gather(*workers, return_exceptions=True)
+                raise
             xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
                           for i, e in enumerate(etags))
             cbody = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
@@ -297,17 +450,23 @@ class S3Client:
         then ``_relay.send_body`` writes head + body (aws-chunked with chunk
         signatures hashed on a native pool, or sendfile for unsigned) from the
         file straight to the socket; the reply is parsed here.  Same retry
-        policy as :meth:`_do` (connection errors and 5xx)."""
-        loop = asyncio.get_running_loop()
+        policy as :meth:`_do` (connection errors and 5xx).
+
+        The pump owns ``sock`` and ``fd`` while it runs: if this coroutine is
+        cancelled the pump is stopped (socket shut down, native cancel token
+        set) and awaited before either is closed, so a reused fd number can
+        never receive its writes."""
         pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         fd = os.dup(src) if isinstance(src, int) else os.open(src, os.O_RDONLY)
         attempt = 0
+        region_hops = 0
         try:
             while True:
                 attempt += 1
                 cred = self._creds()
                 m = "unsigned" if (cred.anonymous and mode == "streaming") else mode
                 host, path = self._target(bucket, key)
+                sreg = await self.bucket_region(bucket)
                 amzdate, _ = sigv4.amz_dates()
                 hdrs = {"host": host, "x-amz-date": amzdate}
                 hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
@@ -323,26 +482,26 @@ class S3Client:
                     if cred.session_token:
                         hdrs["x-amz-security-token"] = cred.session_token
                     signed = sigv4.sign("PUT", path, query, hdrs, hdrs["x-amz-content-sha256"], cred.access_key_id,
-                                        cred.secret_access_key, self.region, amzdate, path_is_encoded=True)
+                                        cred.secret_access_key, sreg, amzdate, path_is_encoded=True)
                     hdrs["authorization"] = signed.authorization
                 target = path + (("?" + sigv4.canonical_query(query)) if query else "")
                 send = {"Host": host, **{k: v for k, v in hdrs.items() if k != "host"}}
                 head = rawhttp.request_head("PUT", target, send)
-                chost, cport = rawhttp.split_host(host)
+                chost, cport = rawhttp.split_host(host, 443 if self.ep.secure else 80)
                 err: Exception | None = None
-                sock = None
+                conn = None
                 try:
-                    sock, reused = await self._raw.connect(chost, cport)
+                    conn, reused = await self._raw.connect(chost, cport, tls=self._tls_ctx())
                     rawhttp.trace("put_pump_start")
-                    sent, _last, perr = await loop.run_in_executor(
-                        None, relay.send_body, sock.fileno(), head, fd, offset, length, flow,
+                    sent, _last, perr = await rawhttp.run_pump(
+                        conn, relay.send_body, head, fd, offset, length, flow,
                         1 if m == "streaming" else 0, signed.key if signed else b"", amzdate,
                         signed.scope if signed else "", signed.signature if signed else "", sigv4.STREAM_CHUNK,
                         self.sign_threads, 300.0)
                     if perr and ("source" in perr or perr == "cancelled"):
                         raise S3Error(0, "SourceFailed", perr, f"PUT {path}")
                     try:
-                        resp = await rawhttp.read_head(sock, 1.0 if perr else 300.0)
+                        resp = await rawhttp.read_head(conn, 1.0 if perr else 300.0)
                     except rawhttp.RawHTTPError:
                         if perr:
                             if reused and sent == 0:
@@ -350,14 +509,18 @@ class S3Client:
                             raise rawhttp.RawHTTPError(perr)
                         raise
                     rawhttp.trace("put_pump_end")
-                    body = await rawhttp.read_small_body(sock, resp, 60.0, method="PUT")
+                    body = await rawhttp.read_small_body(conn, resp, 60.0, method="PUT")
                     rawhttp.trace("put_response")
                     if resp.status == 200 and not perr:
                         if resp.keep_alive:
-                            self._raw.release(chost, cport, sock)
-                            sock = None
+                            self._raw.release(chost, cport, conn)
+                            conn = None
                         return resp.headers.get("ETag", "").strip('"')
-                    err = _parse_error(resp.status, body, f"PUT {path}")
+                    err = _parse_error(resp.status, body, f"PUT {path}", resp.headers)
+                    if region_hops < 2 and self._learn_region(bucket, err, sreg):
+                        region_hops += 1
+                        attempt -= 1
+                        continue
                     if resp.status < 500 or attempt > self.max_retries:
                         raise err
                 except (rawhttp.RawHTTPError, OSError, asyncio.TimeoutError) as e:
@@ -365,8 +528,8 @@ class S3Client:
                         raise S3Error(0, "ConnectionError", str(e), f"PUT {path}") from e
                     err = e
                 finally:
-                    if sock is not None:
-                        sock.close()
+                    if conn is not None:
+                        conn.close()
                 if attempt <= 0:
                     continue
                 d = pol.next_delay() or 1.0
@@ -405,6 +568,61 @@ class S3Client:
             token = root.findtext(f"{S3_NS}NextContinuationToken") or root.findtext("NextContinuationToken")
             if trunc != "true" or not token:
                 return keys
+
+
+class _PartQueue:
+    """Pending part numbers of one multipart upload, handed out in the order
+    their bytes land on disk.
+
+    Following a segmented download, a segment fills front to back, so within
+    a segment the part that will be complete soonest is its first pending one;
+    only those (one per unfinished segment, plus the start of every run of
+    pending parts) are ranked with ``Flow.bytes_until_covered``.  Each pick
+    costs O(runs + segments), not O(pending parts), so 10,000-part uploads stay
+    cheap.  Without a flow (or once it finished) parts go in order."""
+
+    def __init__(self, nparts: int, part_size: int, size: int, flow=None) -> None:
+        self.part_size, self.size, self.flow = part_size, size, flow
+        self._todo = list(range(nparts))          # ascending
+        self._runs = {0} if nparts else set()     # parts that start a run of pending parts
+
+    def __len__(self) -> int:
+        return len(self._todo)
+
+    def __bool__(self) -> bool:
+        return bool(self._todo)
+
+    def _take(self, part: int) -> int:
+        import bisect
+        self._todo.pop(bisect.bisect_left(self._todo, part))
+        self._runs.discard(part)
+        nxt = part + 1
+        k = bisect.bisect_left(self._todo, nxt)
+        if k < len(self._todo) and self._todo[k] == nxt:
+            self._runs.add(nxt)
+        return part
+
+    def _candidates(self) -> set[int]:
+        import bisect
+        todo = self._todo
+        cand = set(self._runs)
+        starts = getattr(self.flow, "open_starts", None)
+        if starts is not None:
+            last = max(0, (self.size - 1) // self.part_size)
+            for st in starts():
+                k = bisect.bisect_left(todo, min(st // self.part_size, last))
+                if k < len(todo):
+                    cand.add(todo[k])
+        return cand
+
+    def pick(self) -> int:
+        todo = self._todo
+        flow = self.flow
+        if flow is None or len(todo) == 1 or flow.finished:
+            return self._take(todo[0])
+        ps, size = self.part_size, self.size
+        best = min(self._candidates(), key=lambda p: (flow.bytes_until_covered(p * ps, min(size, (p + 1) * ps)), p))
+        return self._take(best)
 
 
 class _StreamBody:

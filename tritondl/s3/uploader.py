@@ -12,6 +12,13 @@
 Deviations (defect B8): any per-file failure fails the job (the reference
 logged and skipped, and always returned nil), file handles are always
 closed, and uploads of a job's files run concurrently (bounded).
+
+The reference re-checked the bucket on every ``UploadFiles`` (one HEAD per
+job).  Here the check is cached, and a ``NoSuchBucket`` reply (bucket
+deleted or recreated — possibly in another region) drops the cache, re-runs
+the ensure step and retries the upload once, so the worker heals without a
+restart.  ``from_env`` refuses an unusable ``S3_ENDPOINT`` (``ValueError``),
+as ``minio.NewWithOptions`` did (fatal in ``downloader.go:95-98``).
 """
 
 from __future__ import annotations
@@ -23,7 +30,7 @@ from dataclasses import dataclass
 
 from ..utils.gocompat import go_base, go_join
 from ..utils.log import log
-from .client import S3Client, S3Error
+from .client import Endpoint, S3Client, S3Error
 from .credentials import default_chain
 
 
@@ -46,16 +53,18 @@ class UploadError(Exception):
 
 class Uploader:
     def __init__(self, bucket: str, client: S3Client, *, file_concurrency: int = 2) -> None:
+        self.heals = 0
         self.bucket = bucket
         self.client = client
         self.file_concurrency = max(1, file_concurrency)
         self._bucket_ok = False
 
     @classmethod
-    def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "us-east-1",
+    def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "",
                  part_size: int = 64 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
                  env=None, sign_threads: int = 4) -> "Uploader":
         ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
+        Endpoint.parse(ep)                       # ValueError on an endpoint minio-go would refuse
         client = S3Client(ep, default_chain(env), region=region, part_size=part_size,
                           multipart_threshold=multipart_threshold, parallel_parts=parallel_parts,
                           sign_threads=sign_threads)
@@ -79,6 +88,20 @@ class Uploader:
                     return
         self._bucket_ok = True
 
+    async def _healing(self, put):
+        """Run ``put()``; on NoSuchBucket re-ensure the bucket and retry once."""
+        try:
+            return await put()
+        except S3Error as e:
+            if e.code != "NoSuchBucket":
+                raise
+            log.with_field("bucket", self.bucket).warn("bucket vanished; re-creating it and retrying the upload")
+            self._bucket_ok = False
+            self.client.forget_bucket(self.bucket)
+            self.heals += 1
+            await self.ensure_bucket()
+            return await put()
+
     async def upload_files(self, media_id: str, base_dir: str, files: list[str]) -> list[UploadResult]:
         await self.ensure_bucket()
         sem = asyncio.Semaphore(self.file_concurrency)
@@ -92,7 +115,7 @@ class Uploader:
                 key = object_key(media_id, path)
                 log.info("starting upload of file '%s'", go_base(key))
                 try:
-                    etag = await self.client.put_object(self.bucket, key, path, size)
+                    etag = await self._healing(lambda: self.client.put_object(self.bucket, key, path, size))
                 except (S3Error, OSError) as e:
                     raise UploadError(f"failed to upload file {path}: {e}") from e
                 log.info("finished upload")
@@ -108,7 +131,8 @@ class Uploader:
         key = object_key(media_id, name)
         log.info("starting upload of file '%s'", go_base(key))
         try:
-            etag = await self.client.put_object(self.bucket, key, src, size, wait_bytes=wait_bytes, flow=flow)
+            etag = await self._healing(lambda: self.client.put_object(self.bucket, key, src, size,
+                                                                      wait_bytes=wait_bytes, flow=flow))
         except (S3Error, OSError) as e:
             raise UploadError(f"failed to upload file {name}: {e}") from e
         log.info("finished upload")

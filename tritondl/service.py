@@ -3,8 +3,9 @@
 Per job (``downloader.go:103-155``): decode ``api.Download`` → download via
 the dispatcher → select media files → upload to S3 → publish
 ``api.Convert{CreatedAt: time.Now().String(), Media: job.Media}`` on
-``v1.convert`` → ack.  Undecodable bodies are nacked without requeue
-(``:106-111``).  Startup wiring (``:28-98``): logging from env, broker
+``v1.convert`` → ack.  Undecodable bodies are not retried (the reference
+nacked them, ``:106-111``); they go to the dead-letter topic like any job
+that exhausted its retries.  Startup wiring (``:28-98``): logging from env, broker
 endpoint default ``127.0.0.1:5672`` (warned), prefetch 1, consume
 ``v1.download``, impls ``[torrent, http]``, bucket ``triton-staging``,
 download dir ``$CWD/downloading``; SIGINT/SIGTERM/SIGHUP → graceful
@@ -14,8 +15,15 @@ Differences, all documented fixes:
 
 * B4 — a failed job is not left unacked (which stalled the channel at
   prefetch 1): it is re-published with ``X-Retries+1`` (the reference's
-  unused ``Delivery.Error``) and dead-lettered / dropped after
-  ``max_retries``;
+  unused ``Delivery.Error``) through a broker-side delay queue (the job slot
+  is freed at once; the delay grows per retry) and, after ``max_retries``,
+  published to the durable dead-letter topic ``<consume_topic>.dead`` with
+  ``X-Failed-Stage`` / ``X-Error`` and acked.  A job is never dropped unless
+  ``drop_failed`` is set; if even the dead-letter publish fails the delivery
+  stays unacked and the broker redelivers it;
+* an unusable ``S3_ENDPOINT`` is fatal at start-up, before the broker is
+  dialled (the reference ``log.Fatal``-ed in ``NewUploader``,
+  ``downloader.go:95-98``);
 * B12 — broker connect errors are checked before use;
 * ``concurrency`` job loops per process (default 1 = reference), each job
   fully async so downloads / uploads of different jobs overlap;
@@ -39,7 +47,7 @@ from .amqp.client import Client, Delivery
 from .fetch.http import HTTPDownloader
 from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
-from .s3.uploader import Uploader
+from .s3.uploader import UploadError, Uploader
 from .select import MEDIA_EXTS, dir_media
 from .utils import rawhttp
 from .utils.config import Config
@@ -103,6 +111,14 @@ class Service:
     async def start(self) -> None:
         cfg = self.cfg
         self._size_executor()
+        if self.uploader is None:
+            # NewUploader (downloader.go:95-98) was fatal on a bad S3_ENDPOINT: validate
+            # before dialling the broker so a misconfigured worker never takes a job
+            self.uploader = Uploader.from_env(cfg.bucket, cfg.s3_endpoint, region=cfg.s3_region,
+                                              part_size=cfg.s3_part_size,
+                                              multipart_threshold=cfg.s3_multipart_threshold,
+                                              parallel_parts=cfg.s3_parallel_parts,
+                                              sign_threads=cfg.s3_sign_threads)
         if self.amqp is None:
             if cfg.rabbitmq_endpoint_defaulted:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)
@@ -118,12 +134,6 @@ class Service:
         if self.dispatcher is None:
             self.dispatcher = Dispatcher(cfg.download_dir, default_impls(cfg), cfg.progress_log_interval_s)
         self.dispatcher.start()
-        if self.uploader is None:
-            self.uploader = Uploader.from_env(cfg.bucket, cfg.s3_endpoint, region=cfg.s3_region,
-                                              part_size=cfg.s3_part_size,
-                                              multipart_threshold=cfg.s3_multipart_threshold,
-                                              parallel_parts=cfg.s3_parallel_parts,
-                                              sign_threads=cfg.s3_sign_threads)
         if cfg.gpu_verify != "off":
             # HIP context + hasher set-up off the job path (first torrent resume would pay it).
             # Finished before consuming: importing torch holds the GIL for ~1-2 s, which would
@@ -186,11 +196,8 @@ class Service:
         except DecodeError as e:
             log.with_field("event", "decode-message").error(
                 "failed to unmarshal rabbitmq message into protobuf format: %s", e)
-            try:
-                await msg.nack()
-            except Exception as ne:
-                log.warn("failed to nack failed message: %s", ne)
             self.metrics.inc("jobs", status="undecodable")
+            await self._dead_letter(msg, "decode", e)
             return self._record(JobResult(False, "decode", str(e)))
 
         log.with_field("job", job.to_dict()).info("got message")
@@ -234,6 +241,8 @@ class Service:
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - any stage failure must settle the message
+            if isinstance(e, UploadError):
+                stage = "upload"             # a streamed upload fails inside the download stage
             log.with_fields(stage=stage, error=str(e)).error("job failed")
             self.metrics.inc("jobs", status="failed", stage=stage)
             await self._dispose_failed(msg, stage, e)
@@ -304,24 +313,39 @@ class Service:
         return r
 
     async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> None:
-        """B4 fix: requeue with X-Retries+1, dead-letter after max_retries."""
+        """B4 fix: retry with X-Retries+1 through a broker delay queue (the slot
+        is free at once), dead-letter after ``max_retries``."""
         assert self.amqp is not None
         try:
             if msg.metadata.retries < self.cfg.max_retries:
-                log.with_fields(retries=msg.metadata.retries + 1).warn("scheduling job retry")
-                await msg.retry(self.cfg.retry_delay_s)
+                d = self.cfg.retry_delay_for(msg.metadata.retries)
+                log.with_fields(retries=msg.metadata.retries + 1, delay_s=d).warn("scheduling job retry")
+                await msg.retry(d)
+                self.metrics.inc("jobs_retried")
                 return
-            if self.cfg.dead_letter_topic:
-                hdrs = dict(msg.msg.properties.headers or {})
-                hdrs.update({"X-Retries": msg.metadata.retries, "X-Failed-Stage": stage,
-                             "X-Error": str(err)[:512]})
-                await self.amqp.publish(self.cfg.dead_letter_topic, msg.body, headers=hdrs)
-                await msg.ack()
-            else:
+        except Exception as e:  # noqa: BLE001
+            log.with_field("error", str(e)).error("failed to schedule retry; broker will redeliver")
+            return
+        await self._dead_letter(msg, stage, err)
+
+    async def _dead_letter(self, msg: Delivery, stage: str, err: Exception) -> None:
+        """Publish the job (confirmed) to the durable dead-letter topic, then ack.
+        On any failure the delivery stays unacked, so the broker keeps it."""
+        assert self.amqp is not None
+        try:
+            if self.cfg.drop_failed:
                 await msg.nack(requeue=False)
+                self.metrics.inc("jobs_dropped")
+                return
+            hdrs = dict(msg.msg.properties.headers or {})
+            hdrs.update({"X-Retries": msg.metadata.retries, "X-Failed-Stage": stage, "X-Error": str(err)[:512],
+                         "X-Original-Routing-Key": msg.routing_key})
+            await self.amqp.publish(self.cfg.dlq_topic, msg.body, headers=hdrs)
+            await msg.ack()
+            log.with_fields(topic=self.cfg.dlq_topic, stage=stage).warn("job dead-lettered")
             self.metrics.inc("jobs_dead_lettered")
         except Exception as e:  # noqa: BLE001
-            log.with_field("error", str(e)).error("failed to dispose failed job; broker will redeliver")
+            log.with_field("error", str(e)).error("failed to dead-letter job; broker will redeliver")
 
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")

@@ -46,8 +46,11 @@ class Config:
     # --- job processing ---
     concurrency: int = 1                        # one job loop (downloader.go:103)
     max_retries: int = 5                        # B4 fix: X-Retries budget
-    retry_delay_s: float = 10.0                 # delivery.go:72
-    dead_letter_topic: str = ""                 # "" => drop after max_retries (nack)
+    retry_delay_s: float = 10.0                 # delivery.go:72 (first retry; waited in a broker delay queue)
+    retry_backoff: float = 2.0                  # delay multiplier per retry (1.0 = the reference's fixed 10 s)
+    retry_delay_max_s: float = 300.0            # cap on one retry delay
+    dead_letter_topic: str = ""                 # "" => "<consume_topic>.dead"
+    drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
     cleanup: bool = False                       # B15: off for parity
     stream_upload: bool = True                  # overlap HTTP fetch with S3 upload
     http_segments: int = 4                      # max parallel Range streams per HTTP file
@@ -74,7 +77,7 @@ class Config:
     s3_endpoint: str = ""
     s3_access_key: str = ""
     s3_secret_key: str = ""
-    s3_region: str = "us-east-1"
+    s3_region: str = ""                         # "" => discover per bucket (GET ?location), like minio-go
     s3_part_size: int = 64 * 1024 * 1024
     s3_multipart_threshold: int = 64 * 1024 * 1024
     s3_parallel_parts: int = 4
@@ -119,6 +122,7 @@ class Config:
                 "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
                 "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
+                  "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
                   "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s"}
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
@@ -135,6 +139,7 @@ class Config:
             if g("TRITONDL_" + k) is not None and g("TRITONDL_" + k) != "":
                 setattr(c, a, g("TRITONDL_" + k))
         c.cleanup = _env_bool(g("TRITONDL_CLEANUP"), c.cleanup)
+        c.drop_failed = _env_bool(g("TRITONDL_DROP_FAILED"), c.drop_failed)
         c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
@@ -152,6 +157,18 @@ class Config:
             v = getattr(ns, f.name, None)
             if v is not None:
                 setattr(self, f.name, v)
+
+    @property
+    def dlq_topic(self) -> str:
+        """Where a job goes after ``max_retries`` (never dropped unless ``drop_failed``)."""
+        return self.dead_letter_topic or f"{self.consume_topic}.dead"
+
+    def retry_delay_for(self, retries: int) -> float:
+        """Delay before retry number ``retries + 1``: ``retry_delay_s`` growing by
+        ``retry_backoff`` per retry, capped at ``retry_delay_max_s``."""
+        if self.retry_delay_s <= 0:
+            return 0.0
+        return min(self.retry_delay_max_s, self.retry_delay_s * self.retry_backoff ** max(0, retries))
 
     def rabbitmq_url(self) -> str:
         """amqp://user:pass@endpoint/vhost with credentials URL-escaped (B14 fix)."""

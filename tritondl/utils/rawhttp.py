@@ -1,14 +1,20 @@
-"""Plain-HTTP/1.1 plumbing for the native data plane (``csrc/relay/``).
+"""HTTP/1.1 plumbing for the native data plane (``csrc/relay/``).
 
-The control plane stays in asyncio: connect, write a request head, parse a
-response head, read small bodies (S3 replies).  Large bodies never pass
-through Python — the socket's fd is handed to ``_relay.recv_body`` /
-``_relay.send_body``, which run in an executor thread with the GIL
-released.  While a pump owns a socket, asyncio does not touch it.
+The control plane stays in asyncio: connect (and, for ``https``, drive the
+TLS handshake), write a request head, parse a response head, read small
+bodies (S3 replies).  Large bodies never pass through Python — the
+connection's native stream (``_relay.Sock`` or ``_relay.TlsConn``) is handed
+to ``_relay.recv_body`` / ``_relay.send_body``, which run in an executor
+thread with the GIL released.  While a pump owns a connection, asyncio does
+not touch it; :func:`run_pump` makes sure a cancelled caller stops the pump
+and waits for it before the socket or file can be closed.
 
-Scope (everything else falls back to aiohttp in the callers): ``http://``
-only (TLS stays in Python's ssl), identity transfer coding for downloads,
-no redirects.  Idle keep-alive sockets are pooled per (host, port).
+TLS is OpenSSL inside the relay module (non-blocking steps driven from the
+event loop for handshakes and heads; the pumps encrypt/decrypt off-loop), so
+``https`` origins and S3 endpoints keep the native path.  Scope (everything
+else falls back to aiohttp in the callers): identity transfer coding for
+downloads, no redirects.  Idle keep-alive connections are pooled per
+(host, port, tls).
 """
 
 from __future__ import annotations
@@ -88,20 +94,144 @@ def split_host(hostport: str, default_port: int = 80) -> tuple[str, int]:
     return hostport, default_port
 
 
+class RawConn:
+    """A connected, non-blocking stream: a plain socket, or a TLS session
+    (``_relay.TlsConn``) over one.  ``native`` is what the relay pumps take.
+    Owns the socket; :meth:`close` closes it."""
+
+    pool_key: tuple | None = None
+
+    def __init__(self, sock: socket.socket, tls=None) -> None:
+        self.sock = sock
+        self.tls = tls
+        relay = relay_module()
+        self.native = tls if tls is not None else (relay.Sock(sock.fileno()) if relay is not None else None)
+        self._loop = asyncio.get_running_loop()
+
+    @property
+    def secure(self) -> bool:
+        return self.tls is not None
+
+    def fileno(self) -> int:
+        return self.sock.fileno()
+
+    async def _wait(self, events: int) -> None:
+        """Wait until the socket is readable (POLLIN=1) / writable (POLLOUT=4)."""
+        fut = self._loop.create_future()
+        fd = self.sock.fileno()
+
+        def ready() -> None:
+            if not fut.done():
+                fut.set_result(None)
+
+        rd, wr = bool(events & 1), bool(events & 4)
+        if rd:
+            self._loop.add_reader(fd, ready)
+        if wr:
+            self._loop.add_writer(fd, ready)
+        try:
+            await fut
+        finally:
+            if rd:
+                self._loop.remove_reader(fd)
+            if wr:
+                self._loop.remove_writer(fd)
+
+    async def handshake(self, timeout: float) -> None:
+        async def go() -> None:
+            while True:
+                try:
+                    w = self.tls.handshake_step()
+                except RuntimeError as e:
+                    raise RawHTTPError(str(e)) from e
+                if w == 0:
+                    return
+                await self._wait(w)
+        try:
+            await asyncio.wait_for(go(), timeout)
+        except asyncio.TimeoutError as e:
+            raise RawHTTPError("tls handshake timed out") from e
+
+    async def recv(self, n: int) -> bytes:
+        """Up to n bytes; b"" at end of stream."""
+        if self.tls is None:
+            return await self._loop.sock_recv(self.sock, n)
+        while True:
+            try:
+                r = self.tls.read_nb(n)
+            except RuntimeError as e:
+                raise RawHTTPError(str(e)) from e
+            if isinstance(r, bytes):
+                return r
+            await self._wait(r)
+
+    async def sendall(self, data: bytes) -> None:
+        if self.tls is None:
+            await self._loop.sock_sendall(self.sock, data)
+            return
+        mv = memoryview(data)
+        while mv:
+            try:
+                n, want = self.tls.write_nb(bytes(mv))
+            except RuntimeError as e:
+                raise RawHTTPError(str(e)) from e
+            if n:
+                mv = mv[n:]
+            else:
+                await self._wait(want)
+
+    def alive(self) -> bool:
+        """Idle pooled connection still usable (peer has not closed it)."""
+        if self.tls is not None:
+            try:
+                return self.tls.alive()
+            except RuntimeError:
+                return False
+        try:
+            self.sock.recv(1, socket.MSG_PEEK | socket.MSG_DONTWAIT)
+            return False         # EOF, or stray bytes: not reusable either way
+        except BlockingIOError:
+            return True          # nothing pending, still open
+        except OSError:
+            return False
+
+    def abort(self) -> None:
+        """Stop a pump running on this connection without closing the fd."""
+        if self.native is not None:
+            self.native.abort()
+        try:
+            self.sock.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
+
+    def close(self) -> None:
+        if self.sock.fileno() < 0:
+            return
+        if self.tls is not None:
+            try:
+                self.tls.shutdown_notify()
+            except RuntimeError:
+                pass
+        self.sock.close()
+
+
 @dataclass
 class Pool:
-    """Idle keep-alive sockets by (host, port)."""
+    """Idle keep-alive connections by (host, port, tls)."""
     max_idle: int = 16
     idle: dict = field(default_factory=dict)
 
-    async def connect(self, host: str, port: int, timeout: float = 30.0) -> tuple[socket.socket, bool]:
-        """(socket, reused).  A pooled socket the peer has closed is dropped."""
-        lst = self.idle.get((host, port))
+    async def connect(self, host: str, port: int, timeout: float = 30.0, tls=None,
+                      server_hostname: str | None = None) -> tuple[RawConn, bool]:
+        """(connection, reused).  ``tls``: a ``_relay.TlsContext`` (client) for
+        https.  A pooled connection the peer has closed is dropped."""
+        key = (host, port, id(tls) if tls is not None else 0)
+        lst = self.idle.get(key)
         while lst:
-            s = lst.pop()
-            if _alive(s):
-                return s, True
-            s.close()
+            c = lst.pop()
+            if c.alive():
+                return c, True
+            c.close()
         loop = asyncio.get_running_loop()
         infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
         err: Exception | None = None
@@ -111,34 +241,111 @@ class Pool:
             try:
                 s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 await asyncio.wait_for(loop.sock_connect(s, addr), timeout)
-                return s, False
             except (OSError, asyncio.TimeoutError) as e:
                 s.close()
                 err = e
+                continue
+            if tls is None:
+                c = RawConn(s)
+                c.pool_key = key
+                return c, False
+            relay = relay_module()
+            try:
+                t = relay.TlsConn(tls, s.fileno(), server_hostname or host, f"{host}:{port}")
+                c = RawConn(s, t)
+                await c.handshake(timeout)
+            except BaseException:
+                s.close()
+                raise
+            c.pool_key = key
+            return c, False
         raise RawHTTPError(f"connect {host}:{port}: {err}")
 
-    def release(self, host: str, port: int, s: socket.socket) -> None:
-        lst = self.idle.setdefault((host, port), [])
+    def release(self, host: str, port: int, c: RawConn) -> None:
+        key = getattr(c, "pool_key", None) or (host, port, 0)
+        lst = self.idle.setdefault(key, [])
         if len(lst) >= self.max_idle:
-            s.close()
+            c.close()
         else:
-            lst.append(s)
+            lst.append(c)
 
     def close(self) -> None:
         for lst in self.idle.values():
-            for s in lst:
-                s.close()
+            for c in lst:
+                c.close()
         self.idle.clear()
 
 
-def _alive(s: socket.socket) -> bool:
+_active_pumps = 0
+_active_lock = __import__("threading").Lock()
+
+
+def active_pumps() -> int:
+    """Relay pumps currently running in executor threads (tests / debugging)."""
+    return _active_pumps
+
+
+def _counted(fn, *args):
+    global _active_pumps
+    with _active_lock:
+        _active_pumps += 1
     try:
-        s.recv(1, socket.MSG_PEEK | socket.MSG_DONTWAIT)
-        return False         # EOF, or stray bytes: not reusable either way
-    except BlockingIOError:
-        return True          # nothing pending, still open
-    except OSError:
-        return False
+        return fn(*args)
+    finally:
+        with _active_lock:
+            _active_pumps -= 1
+
+
+async def run_pump(conn: RawConn, fn, *args):
+    """Run a relay pump ``fn(conn.native, *args)`` in an executor thread.
+
+    If the awaiting task is cancelled, the pump is aborted (sticky native flag
+    + socket shutdown, fd left open) and awaited to completion before the
+    cancellation propagates — so the caller's ``finally`` can never close a
+    socket or file the pump is still using (fd numbers are reused)."""
+    loop = asyncio.get_running_loop()
+    fut = loop.run_in_executor(None, _counted, fn, conn.native, *args)
+    try:
+        return await asyncio.shield(fut)
+    except asyncio.CancelledError:
+        conn.abort()
+        while not fut.done():
+            try:
+                await asyncio.shield(fut)
+            except asyncio.CancelledError:
+                continue
+            except Exception:  # noqa: BLE001 - the pump's own error no longer matters
+                break
+        raise
+
+
+_client_tls: dict = {}
+
+
+def client_tls_context(ca_file: str = "", verify: bool = True):
+    """Shared client ``_relay.TlsContext`` (one per CA setting, so session
+    tickets are reused across connections).  ``ca_file`` "" = the system
+    store; ``SSL_CERT_FILE`` is honoured, and ``TRITONDL_CA_FILE`` names an
+    extra trust file (e.g. a private MinIO CA)."""
+    relay = relay_module()
+    if relay is None:
+        return None
+    ca_file = ca_file or os.environ.get("TRITONDL_CA_FILE", "")
+    key = (ca_file, verify)
+    ctx = _client_tls.get(key)
+    if ctx is None:
+        ctx = _client_tls[key] = relay.TlsContext.client(ca_file=ca_file, verify=verify)
+    return ctx
+
+
+def register_client_ca(ca_pem: str):
+    """Client context trusting ``ca_pem`` (tests / fakes with a throwaway CA);
+    replaces the default context for this process."""
+    relay = relay_module()
+    ctx = relay.TlsContext.client(ca_pem=ca_pem)
+    _client_tls[("", True)] = ctx
+    _client_tls[(os.environ.get("TRITONDL_CA_FILE", ""), True)] = ctx
+    return ctx
 
 
 def request_head(method: str, target: str, headers: dict) -> bytes:
@@ -147,8 +354,13 @@ def request_head(method: str, target: str, headers: dict) -> bytes:
     return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
 
 
-async def read_head(s: socket.socket, timeout: float, max_size: int = 64 << 10) -> Head:
-    loop = asyncio.get_running_loop()
+async def _recv(s, n: int) -> bytes:
+    if isinstance(s, RawConn):
+        return await s.recv(n)
+    return await asyncio.get_running_loop().sock_recv(s, n)
+
+
+async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int = 64 << 10) -> Head:
     buf = b""
     while True:
         i = buf.find(b"\r\n\r\n")
@@ -157,7 +369,7 @@ async def read_head(s: socket.socket, timeout: float, max_size: int = 64 << 10) 
         if len(buf) > max_size:
             raise RawHTTPError("response head too large")
         try:
-            d = await asyncio.wait_for(loop.sock_recv(s, 256 << 10), timeout)
+            d = await asyncio.wait_for(_recv(s, 256 << 10), timeout)
         except asyncio.TimeoutError as e:
             raise RawHTTPError("timed out waiting for the response head") from e
         if not d:
@@ -178,17 +390,16 @@ async def read_head(s: socket.socket, timeout: float, max_size: int = 64 << 10) 
     return Head(int(code), reason, hdrs, buf[i + 4:], ver, keep)
 
 
-async def read_small_body(s: socket.socket, head: Head, timeout: float, limit: int = 16 << 20,
+async def read_small_body(s: "RawConn | socket.socket", head: Head, timeout: float, limit: int = 16 << 20,
                           method: str = "GET") -> bytes:
     """Whole body of a small response (Content-Length, chunked, or until
     close).  Marks ``head.keep_alive`` False when the connection can't be
     reused."""
-    loop = asyncio.get_running_loop()
     buf = bytearray(head.leftover)
 
     async def more() -> bool:
         try:
-            d = await asyncio.wait_for(loop.sock_recv(s, 256 << 10), timeout)
+            d = await asyncio.wait_for(_recv(s, 256 << 10), timeout)
         except asyncio.TimeoutError as e:
             raise RawHTTPError("timed out reading the response body") from e
         if not d:
