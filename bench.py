@@ -11,10 +11,16 @@ signing (verified by the fake S3), publishes ``api.Convert`` to
 ``v1.convert`` (broker-confirmed) and acks.  Broker, origin and S3 are
 local fakes, each in its own process; the payload is synthetic.
 
-Multi-GPU (torchrun, one rank per GPU): each rank is an independent worker
-with its own local backends — job-level data parallelism (competing-consumer
-workers) — so per-rank work is fixed: ``scaling="weak"``.
-``value`` = total jobs/s over all ranks (N·K / max-rank elapsed).
+Multi-GPU (torchrun, one rank per GPU): job-level data parallelism — the
+reference's competing consumers (``internal/rabbitmq/client.go:405-422``;
+SURVEY.md §2.3).  Rank 0 hosts ONE broker; every rank runs a worker that
+competes on the same ``v1.download-{0,1}`` queues, plus its own origin and S3
+node (sharded fakes: one single-process fake would cap the node, like one
+MinIO disk).  Rank 0 publishes N·K jobs and the timed region ends when N·K
+``v1.convert`` messages are back: ``value`` is the global ack rate (N·K /
+max-rank elapsed), per-rank work is fixed on average: ``scaling="weak"``.
+``--isolated`` restores private per-rank stacks; ``--tls`` runs origin and
+S3 over https (OpenSSL in the native data plane).
 
 The reference publishes no numbers → ``vs_baseline: null``.
 A secondary, untimed-for-headline figure reports the HIP batched piece-hash
@@ -80,6 +86,13 @@ def main() -> int:
                          "(-1: worker default, 0: open-ended probe)")
     ap.add_argument("--http-segments", type=int, default=0, help="max parallel Range streams (0: worker default)")
     ap.add_argument("--sign-threads", type=int, default=0, help="S3 chunk hashers per PUT (0: worker default)")
+    ap.add_argument("--tls", action="store_true", help="origin and S3 over https (self-signed CA)")
+    ap.add_argument("--payload", default="", choices=["", "streaming", "unsigned"],
+                    help="S3 payload mode ('' = aws-chunked over http, unsigned over https, like minio-go)")
+    ap.add_argument("--isolated", action="store_true",
+                    help="multi-rank: every rank gets a private broker (default: one shared broker, "
+                         "competing consumers)")
+    ap.add_argument("--dist-backend", default="", help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-level", default="warning")
     a = ap.parse_args()
 
@@ -90,15 +103,20 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    cuda = torch.cuda.is_available()
+    backend = a.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    cuda = torch.cuda.is_available() and backend == "nccl"
     if cuda:
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    ctl = None
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo")
+        dist.init_process_group(backend)
+        # control plane (endpoint exchange, phase barriers from a helper thread): gloo
+        ctl = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
+    shared = world > 1 and not a.isolated
 
     def barrier() -> None:
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=ctl)
         if cuda:
             torch.cuda.synchronize()
 
@@ -109,24 +127,59 @@ def main() -> int:
     file_size = int(a.file_mb * 1024 * 1024)
     stack = JobStack(file_size=file_size, concurrency=a.concurrency, prefetch=max(1, a.concurrency),
                      tag=f"r{rank}", http_probe_bytes=(a.probe_kb << 10) if a.probe_kb >= 0 else -1,
-                     http_segments=a.http_segments, sign_threads=a.sign_threads)
+                     http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
+                     payload_mode=a.payload)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
+
+    async def phase(n_per_rank: int) -> None:
+        """Shared mode: rank 0 publishes world*n jobs and waits for as many
+        v1.convert messages; every rank's worker competes for them until the
+        closing barrier (run off-loop so the workers keep working)."""
+        if rank == 0:
+            await stack.run_global(world * n_per_rank)
+        await loop.run_in_executor(None, lambda: dist.barrier(group=ctl))
+
     try:
-        loop.run_until_complete(stack.setup())
+        if shared:
+            mine = loop.run_until_complete(stack.start_backends(broker=rank == 0))
+            ca_pem = ""
+            if a.tls:
+                with open(mine["ca_file"]) as f:
+                    ca_pem = f.read()
+            gathered: list = [None] * world
+            dist.all_gather_object(gathered, {**mine, "ca_pem": ca_pem}, group=ctl)
+            endpoints = {"broker": gathered[0]["broker"], "origin": mine["origin"], "s3": mine["s3"]}
+            if a.tls:   # every rank trusts every rank's throwaway CA (origins are shared)
+                both = os.path.join(stack.workdir, "all-ca.pem")
+                with open(both, "w") as f:
+                    f.write("".join(g["ca_pem"] for g in gathered))
+                endpoints["ca_file"] = both
+            loop.run_until_complete(stack.setup(endpoints, origins=[g["origin"] for g in gathered],
+                                                producer=rank == 0))
+        else:
+            loop.run_until_complete(stack.setup())
         c = stack.cfg
         knobs = {"http_probe_bytes": c.http_probe_bytes, "http_segments": c.http_segments,
                  "s3_sign_threads": c.s3_sign_threads} if c is not None else {}
         if a.warmup:
-            loop.run_until_complete(stack.run_jobs(a.warmup))
+            if shared:
+                loop.run_until_complete(phase(a.warmup))
+            else:
+                loop.run_until_complete(stack.run_jobs(a.warmup))
+        base = len(stack.svc.results)  # type: ignore[union-attr]
         barrier()
         t0 = time.perf_counter()
-        loop.run_until_complete(stack.run_jobs(a.steps))
+        if shared:
+            loop.run_until_complete(phase(a.steps))
+        else:
+            loop.run_until_complete(stack.run_jobs(a.steps))
         if cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         barrier()
-        done = stack.svc.results[-a.steps:]  # type: ignore[union-attr]
+        done = stack.svc.results[base:]  # type: ignore[union-attr]
+        failed = len(stack.failures())
         lat = sorted(r.seconds for r in done)
         spans: dict[str, list[float]] = {}
         for r in done:
@@ -136,13 +189,21 @@ def main() -> int:
         loop.run_until_complete(stack.teardown())
         loop.close()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if cuda and world > 1 else "cpu")
+    t = torch.tensor([elapsed, float(failed)], dtype=torch.float64, device="cuda" if cuda and world > 1 else "cpu")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    max_elapsed = float(t.item())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)        # RCCL on the GPU node
+    max_elapsed = float(t[0].item())
+    if int(t[1].item()):
+        raise SystemExit(f"{int(t[1].item())} jobs failed on some rank")
+    per_rank = [len(done)]
+    if world > 1:
+        per_rank = [None] * world  # type: ignore[list-item]
+        dist.all_gather_object(per_rank, len(done), group=ctl)
     extra = {} if (a.no_gpu_probe or rank != 0) else _gpu_hash_probe()
     if rank == 0:
         jobs_per_sec = world * a.steps / max_elapsed
+        name = CONFIG_NAME if file_size == 10 << 20 else \
+            f"Single HTTP download job via local RabbitMQ, {file_size / 2**20:g} MiB file"
         res = {
             "metric": "jobs_per_sec",
             "value": round(jobs_per_sec, 3),
@@ -156,12 +217,16 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "uint8",
             "data": f"synthetic (deterministic pseudo-random {file_size / 2**20:g} MiB payload; "
-                    "local fake broker/origin/S3)",
-            "config": {"model": CONFIG_NAME if file_size == 10 << 20 else
-                       f"Single HTTP download job via local RabbitMQ, {file_size / 2**20:g} MiB file", "global_batch": world * a.concurrency, "seq_len": None,
+                    f"local fake broker/origin/S3{' over https' if a.tls else ''})",
+            "config": {"model": name, "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
+                       "topology": ("one shared broker, competing consumers; per-rank origin+S3 nodes"
+                                    if shared else "private broker/origin/S3 per rank"),
+                       "transport": "https (TLS 1.3, native OpenSSL data plane)" if a.tls else "http",
+                       "s3_payload": stack.payload_mode,
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
                        **knobs},
+            "jobs_per_rank": per_rank,
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
             "job_latency_ms_p50": round(lat[len(lat) // 2] * 1000, 2) if lat else None,
             "job_latency_ms_p90": round(lat[int(len(lat) * 0.9)] * 1000, 2) if lat else None,

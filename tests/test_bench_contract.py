@@ -57,3 +57,16 @@ def test_bench_two_ranks_torchrun_gloo():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 2
     # whole-job aggregate: 2 ranks x 3 steps over the slowest rank's time
     assert abs(d["value"] - 2 * 3 / (d["ms_per_step"] * 3 / 1000)) / d["value"] < 0.01
+    # one shared broker, competing consumers: both workers took jobs
+    assert d["config"]["topology"].startswith("one shared broker")
+    assert len(d["jobs_per_rank"]) == 2 and all(n > 0 for n in d["jobs_per_rank"]), d["jobs_per_rank"]
+    assert sum(d["jobs_per_rank"]) == 2 * 3
+
+
+def test_bench_tls_json():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--file-mb", "1",
+                        "--no-gpu-probe", "--tls"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_lines(r.stdout)[0]
+    assert d["config"]["transport"].startswith("https") and d["config"]["s3_payload"] == "unsigned"
+    assert d["value"] > 0

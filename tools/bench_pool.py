@@ -9,6 +9,11 @@ the jobs and counts the ``v1.convert`` messages.  Warm-up: one job per worker
 first, so every worker has connected and consumed before the clock starts.
 
     python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 1024   # 800 jobs
+    python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 10240 --nodes 4
+
+``--nodes K`` runs K origin and K S3 processes (CDN edges / MinIO nodes): job
+URLs round-robin over the origins and worker r uploads to S3 node r % K, so a
+single-process fake does not cap the node.  ONE broker either way.
 """
 
 from __future__ import annotations
@@ -33,6 +38,7 @@ async def main() -> int:
     ap.add_argument("--jobs-per-worker", type=int, default=100)
     ap.add_argument("--file-kb", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
+    ap.add_argument("--nodes", type=int, default=1, help="origin + S3 fake processes (sharded)")
     a = ap.parse_args()
     a.jobs = a.jobs or a.workers * a.jobs_per_worker
     from tritondl.amqp.codec import Properties
@@ -47,18 +53,24 @@ async def main() -> int:
     prod = None
     try:
         bk = await Backend("broker").start()
-        og = await Backend("origin").start()
-        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
-        backends = [bk, og, s3]
+        backends = [bk]
+        origins, s3s = [], []
+        for _ in range(max(1, a.nodes)):
+            og = await Backend("origin").start()
+            s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+            origins.append(og.info["url"])
+            s3s.append(s3.info["url"])
+            backends += [og, s3]
         env = {"RABBITMQ_ENDPOINT": bk.info["endpoint"], "RABBITMQ_USERNAME": "guest",
-               "RABBITMQ_PASSWORD": "guest", "S3_ENDPOINT": s3.info["url"], "AWS_ACCESS_KEY_ID": AK,
+               "RABBITMQ_PASSWORD": "guest", "AWS_ACCESS_KEY_ID": AK,
                "AWS_SECRET_ACCESS_KEY": SK, "PYTHONPATH": ROOT, "TRITONDL_RETRY_DELAY": "0",
                "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning", "TRITONDL_PROGRESS_LOG_INTERVAL": "0",
                "TRITONDL_CLEANUP": "1", "TRITONDL_CONCURRENCY": str(a.concurrency),
                "TRITONDL_PREFETCH": str(a.concurrency), "TRITONDL_GPU_VERIFY": "off"}
         ncpu = len(os.sched_getaffinity(0))
         pool = WorkerPool(plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)),
-                          env=env, cwd=work, grace=10)
+                          env=env, cwd=work, grace=10,
+                          worker_env=lambda r: {"S3_ENDPOINT": s3s[r % len(s3s)]})
         await pool.start()
         prod = await Connection.open(bk.info["url"], heartbeat=0)
         pch = await prod.channel()
@@ -90,7 +102,7 @@ async def main() -> int:
             for _ in range(n):
                 i = n_sub[0]
                 n_sub[0] += 1
-                url = f"{og.info['url']}/synthetic/{size}/clip-{i}.mkv"
+                url = f"{origins[i % len(origins)]}/synthetic/{size}/clip-{i}.mkv"
                 body = Download(created_at="now", media=Media(id=f"pool-{i}", name=f"clip {i}",
                                                               source=SourceType.HTTP, source_uri=url)).encode()
                 await pch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
@@ -109,7 +121,7 @@ async def main() -> int:
         dt = time.perf_counter() - t0
         print(json.dumps({"metric": "pool_jobs_per_sec", "value": round(a.jobs / dt, 2), "seconds": round(dt, 3),
                           "workers": a.workers, "jobs": a.jobs, "file_kb": a.file_kb,
-                          "concurrency_per_worker": a.concurrency,
+                          "concurrency_per_worker": a.concurrency, "fake_nodes": a.nodes,
                           "ingest_MB_per_sec": round(a.jobs * size / dt / 1e6, 1)}), flush=True)
     finally:
         if prod is not None:

@@ -2,10 +2,11 @@
 job via local RabbitMQ, 10 MB file", used by ``bench.py``, ``smoke()`` and
 the integration tests.
 
-Layout per worker (rank): the fake broker, HTTP origin and S3 each run in
-their OWN process (``tritondl.fakes.serve``) — as the real RabbitMQ / media
-server / MinIO would — and the worker (``Service``) runs in this process
-exactly as in production: AMQP consume from ``v1.download-{0,1}`` → HTTP
+Layout: the fake broker, HTTP origin and S3 each run in their OWN process
+(``tritondl.fakes.serve``) — as the real RabbitMQ / media server / MinIO
+would — and the worker (``Service``) runs in this process exactly as in
+production (multi-rank: one shared broker, per-rank origin + S3 nodes, see
+:class:`JobStack`): AMQP consume from ``v1.download-{0,1}`` → HTTP
 fetch into ``downloading/<id>/`` → select → SigV4 aws-chunked PUT to
 ``triton-staging/<id>/original/<b64>`` → publish ``v1.convert`` → ack.
 A producer connection publishes the ``api.Download`` jobs; completion is
@@ -74,7 +75,15 @@ class Backend:
 
 @dataclass
 class JobStack:
-    """Fakes + worker + producer for N synthetic jobs."""
+    """Fakes + worker + producer for N synthetic jobs.
+
+    Single-worker mode (``setup()``): this stack starts its own broker,
+    origin and S3.  Shared mode (multi-rank bench): rank 0 starts the ONE
+    broker every worker competes on (``start_backends(broker=True)``), each
+    rank starts its own origin and S3 node (sharded, like CDN edges / MinIO
+    nodes — a single-process fake would cap the node), the endpoints are
+    exchanged, and ``setup(endpoints, origins, producer=rank == 0)`` wires the
+    worker to them; only rank 0 publishes jobs and counts ``v1.convert``."""
 
     file_size: int = 10 * 1024 * 1024
     concurrency: int = 1
@@ -85,31 +94,76 @@ class JobStack:
     http_probe_bytes: int = -1       # -1: worker default (Config)
     http_segments: int = 0           # 0: worker default
     sign_threads: int = 0            # 0: worker default
+    tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
+    payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
     cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
     producer: Connection | None = None
+    origin_urls: list = field(default_factory=list)
     _n: int = 0
 
-    async def setup(self) -> None:
+    def _tls_files(self) -> tuple[str, str, str]:
+        """(ca_file, cert_file, key_file) of a throwaway PKI in the workdir."""
+        from .utils import rawhttp
+        assert self.workdir is not None
+        ca, cert, key = rawhttp.relay_module().make_test_pki(["127.0.0.1", "localhost"])
+        paths = []
+        for name, pem in (("ca.pem", ca), ("cert.pem", cert), ("key.pem", key)):
+            pth = os.path.join(self.workdir, name)
+            with open(pth, "w") as f:
+                f.write(pem)
+            paths.append(pth)
+        return paths[0], paths[1], paths[2]
+
+    async def start_backends(self, broker: bool = True) -> dict:
+        """Start this stack's fakes; returns their URLs (``broker`` only if asked)."""
         if self.workdir is None:
             self.workdir = tempfile.mkdtemp(prefix="tritondl-bench-")
+        out: dict = {}
         if self.inproc:
             from .fakes.broker import Broker
             from .fakes.s3 import FakeS3
             from .fakes.serve import SyntheticOrigin
-            b = await Broker().start()
-            o = await SyntheticOrigin().start()
-            s = await FakeS3(store="memory", access_key=AK, secret_key=SK).start()
-            self.backends = [b, o, s]
-            broker_url, origin_url, s3_url = b.url, f"http://{o.host}:{o.port}", s.endpoint
-        else:
+            tls = None
+            if self.tls:
+                ca_file, cert_f, key_f = self._tls_files()
+                with open(cert_f) as f1, open(key_f) as f2:
+                    tls = (f1.read(), f2.read())
+                out["ca_file"] = ca_file
+            if broker:
+                b = await Broker().start()
+                self.backends.append(b)
+                out["broker"] = b.url
+            o = await SyntheticOrigin(tls=tls).start()
+            s3 = await FakeS3(store="memory", access_key=AK, secret_key=SK, tls=tls).start()
+            self.backends += [o, s3]
+            out["origin"] = f"{'https' if tls else 'http'}://{o.host}:{o.port}"
+            out["s3"] = s3.endpoint
+            return out
+        tls_args: list[str] = []
+        if self.tls:
+            ca_file, cert_f, key_f = self._tls_files()
+            tls_args = ["--tls-cert", cert_f, "--tls-key", key_f]
+            out["ca_file"] = ca_file
+        if broker:
             bk = await Backend("broker").start()
-            og = await Backend("origin").start()
-            s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
-            self.backends = [bk, og, s3]
-            broker_url, origin_url, s3_url = bk.info["url"], og.info["url"], s3.info["url"]
-        self.origin_url = origin_url
+            self.backends.append(bk)
+            out["broker"] = bk.info["url"]
+        og = await Backend("origin", tls_args).start()
+        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK, *tls_args]).start()
+        self.backends += [og, s3]
+        out["origin"], out["s3"] = og.info["url"], s3.info["url"]
+        return out
+
+    async def setup(self, endpoints: dict | None = None, origins: list[str] | None = None,
+                    producer: bool = True) -> None:
+        if endpoints is None:
+            endpoints = await self.start_backends(broker=True)
+        if self.workdir is None:
+            self.workdir = tempfile.mkdtemp(prefix="tritondl-bench-")
+        broker_url, s3_url = endpoints["broker"], endpoints["s3"]
+        self.origin_urls = list(origins or [endpoints["origin"]])
         cfg = Config()
         cfg.download_dir = os.path.join(self.workdir, "downloading")
         cfg.concurrency = self.concurrency
@@ -119,6 +173,7 @@ class JobStack:
         cfg.max_retries = 0
         cfg.progress_log_interval_s = 0
         cfg.heartbeat_s = 0
+        cfg.ca_file = endpoints.get("ca_file", "")
         if self.http_probe_bytes >= 0:
             cfg.http_probe_bytes = self.http_probe_bytes
         if self.http_segments > 0:
@@ -126,16 +181,20 @@ class JobStack:
         if self.sign_threads > 0:
             cfg.s3_sign_threads = self.sign_threads
         self.cfg = cfg
+        mode = self.payload_mode or ("unsigned" if s3_url.startswith("https://") else "streaming")
+        self.payload_mode = mode
         amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=0, retry_delay=0)
-        up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode="streaming",
-                                           sign_threads=cfg.s3_sign_threads))
+        up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode=mode,
+                                           sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file))
         self.svc = Service(cfg, amqp=amqp, uploader=up)
         await self.svc.start()
+        self.converts: list[Convert] = []
+        if not producer:
+            return
         self.producer = await Connection.open(broker_url, heartbeat=0)
         self.pch = await self.producer.channel()
         await self.pch.confirm_select()
         self.convert_ch = await self.producer.channel()
-        self.converts: list[Convert] = []
 
         def on_convert(m) -> None:
             self.converts.append(Convert.decode(m.body))
@@ -149,7 +208,8 @@ class JobStack:
 
     def job_body(self, i: int) -> tuple[str, bytes]:
         mid = f"bench-{self.tag}-{i}"
-        url = f"{self.origin_url}/synthetic/{self.file_size}/movie-{i}.mkv"
+        origin = self.origin_urls[i % len(self.origin_urls)]
+        url = f"{origin}/synthetic/{self.file_size}/movie-{i}.mkv"
         d = Download(created_at="now", media=Media(id=mid, name=f"movie {i}", source=SourceType.HTTP,
                                                       source_uri=url))
         return mid, d.encode()
@@ -174,7 +234,7 @@ class JobStack:
             await asyncio.sleep(0.001)
 
     async def run_jobs(self, n: int) -> float:
-        """Submit n jobs and wait for all to finish; returns elapsed seconds."""
+        """Submit n jobs and wait for all to finish on THIS worker; returns elapsed seconds."""
         assert self.svc is not None
         base = len(self.svc.results)
         t0 = time.perf_counter()
@@ -185,6 +245,23 @@ class JobStack:
         if bad:
             raise RuntimeError(f"{len(bad)} jobs failed: {bad[0]}")
         return dt
+
+    async def run_global(self, n: int, timeout: float = 600) -> float:
+        """Producer side of shared mode: submit n jobs for ALL competing workers
+        and wait until n new ``v1.convert`` messages arrived (the global ack
+        rate's numerator)."""
+        base = len(self.converts)
+        t0 = time.perf_counter()
+        await self.submit(n)
+        while len(self.converts) < base + n:
+            if time.perf_counter() - t0 > timeout:
+                raise TimeoutError(f"only {len(self.converts) - base}/{n} converts")
+            await asyncio.sleep(0.001)
+        return time.perf_counter() - t0
+
+    def failures(self) -> list:
+        assert self.svc is not None
+        return [r for r in self.svc.results if not r.ok or r.bytes != self.file_size]
 
     async def teardown(self) -> None:
         if self.producer is not None:
@@ -215,7 +292,7 @@ def run_single_job_smoke(size: int = 1 << 20) -> None:
             c = st.converts[0]
             assert c.media is not None and c.media.id == "bench-smoke-0"
             from .fakes.serve import synthetic_bytes
-            s3 = st.backends[2]
+            s3 = st.backends[-1]
             from .s3.uploader import object_key
             got = s3.object_bytes("triton-staging", object_key(c.media.id, "movie-0.mkv"))
             assert hashlib.md5(got).digest() == hashlib.md5(synthetic_bytes(size)).digest()

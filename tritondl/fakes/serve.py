@@ -2,6 +2,7 @@
 not the fakes competing for its event loop).
 
     python -m tritondl.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
+                                   [--tls-cert PEM --tls-key PEM]   # origin / s3 over https
     python -m tritondl.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
 
 Prints ONE JSON line ``{"kind":..., "endpoint": ..., "url": ...}`` on stdout
@@ -47,7 +48,12 @@ class SyntheticOrigin(Origin):
 
 
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
-                 seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow") -> None:
+                 seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow",
+                 tls_cert: str | None = None, tls_key: str | None = None) -> None:
+    tls = None
+    if tls_cert and tls_key:
+        with open(tls_cert) as f1, open(tls_key) as f2:
+            tls = (f1.read(), f2.read())
     if kind == "seed":
         from ..fetch.bt.torrent import Torrent, TorrentConfig
         from .swarm import magnet_for, torrent_for
@@ -73,10 +79,11 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         srv = await Broker(port=port).start()
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.url}
     elif kind == "origin":
-        srv = await SyntheticOrigin(port=port).start()
-        info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}", "url": f"http://{srv.host}:{srv.port}"}
+        srv = await SyntheticOrigin(port=port, tls=tls).start()
+        info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}",
+                "url": f"{'https' if tls else 'http'}://{srv.host}:{srv.port}"}
     elif kind == "s3":
-        srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk).start()
+        srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk, tls=tls).start()
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.endpoint}
     else:
         raise SystemExit(f"unknown kind {kind}")
@@ -100,8 +107,11 @@ def main() -> None:
     ap.add_argument("--s3-store", default="discard", choices=["memory", "discard", "disk"])
     ap.add_argument("--access-key", default=None)
     ap.add_argument("--secret-key", default=None)
+    ap.add_argument("--tls-cert", default=None, help="origin/s3: serve https with this PEM certificate")
+    ap.add_argument("--tls-key", default=None)
     a = ap.parse_args()
-    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption))
+    asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption,
+                       a.tls_cert, a.tls_key))
 
 
 if __name__ == "__main__":

@@ -42,10 +42,13 @@ class WorkerPool:
     def __init__(self, specs: list[WorkerSpec], *, argv: list[str] | None = None, env: dict | None = None,
                  max_restarts: int = 5, restart_window: float = 60.0, grace: float = 30.0,
                  backoff_initial: float = 0.5, backoff_max: float = 30.0, cwd: str | None = None,
-                 module: str = "tritondl") -> None:
+                 module: str = "tritondl", worker_env=None) -> None:
+        """``worker_env(rank) -> dict``: extra env for one worker (e.g. its
+        nearest S3 node)."""
         self.workers = [_Worker(s) for s in specs]
         self.argv = argv or []
         self.env = env or {}
+        self.worker_env = worker_env
         self.max_restarts = max_restarts
         self.restart_window = restart_window
         self.grace = grace
@@ -61,6 +64,8 @@ class WorkerPool:
         env = dict(os.environ)
         env.update(self.env)
         env.update(w.spec.env())
+        if self.worker_env is not None:
+            env.update(self.worker_env(w.spec.rank))
         kw = {}
         if w.spec.cpus and hasattr(os, "sched_setaffinity"):
             cpus = set(w.spec.cpus)

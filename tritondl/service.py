@@ -60,7 +60,8 @@ from .utils.profiler import CPUProfiler
 def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
     http = HTTPDownloader(progress_interval=cfg.progress_interval_s, segments=cfg.http_segments,
-                          segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes)
+                          segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes,
+                          ca_file=cfg.ca_file)
     impls: list[ClientImpl] = []
     try:
         from .fetch.bt.client import TorrentDownloader
@@ -118,7 +119,7 @@ class Service:
                                               part_size=cfg.s3_part_size,
                                               multipart_threshold=cfg.s3_multipart_threshold,
                                               parallel_parts=cfg.s3_parallel_parts,
-                                              sign_threads=cfg.s3_sign_threads)
+                                              sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file)
         if self.amqp is None:
             if cfg.rabbitmq_endpoint_defaulted:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)

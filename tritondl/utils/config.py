@@ -88,6 +88,9 @@ class Config:
     minio_access_key: str = ""
     minio_secret_key: str = ""
 
+    # --- TLS trust (https origins / S3): "" = system store (SSL_CERT_FILE honoured) ---
+    ca_file: str = ""
+
     # --- observability ---
     metrics_addr: str = ""                      # "host:port" → /metrics
     extra: dict = field(default_factory=dict)
@@ -128,7 +131,7 @@ class Config:
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
-                "BT_ENCRYPTION": "bt_encryption"}
+                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file"}
         for k, a in ints.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, int(g("TRITONDL_" + k)))
