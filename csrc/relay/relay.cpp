@@ -126,6 +126,14 @@ PYBIND11_MODULE(_relay, m) {
              return py::make_tuple(static_cast<int64_t>(r), 0);
            },
            py::arg("data"), "(bytes written, poll events to wait for); retry unwritten bytes unchanged")
+      .def("flush_nb", [](TlsStream& t) {
+             short want = POLLOUT;
+             std::string err;
+             if (t.flush_nb(&want, &err)) return 0;
+             if (!err.empty()) throw std::runtime_error(err);
+             return static_cast<int>(want);
+           },
+           "send buffered ciphertext: 0 = all out, else the poll events to wait for")
       .def("pending", &TlsStream::pending)
       .def("alive", &TlsStream::alive)
       .def("shutdown_notify", &TlsStream::shutdown_notify)

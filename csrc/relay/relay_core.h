@@ -371,7 +371,25 @@ inline bool writev_all(Stream& io, std::vector<struct iovec>& iov, double idle_t
     }
     while (k < iov.size() && iov[k].iov_len == 0) ++k;
   }
-  return true;
+  // a TLS stream may still hold the last records' ciphertext
+  for (;;) {
+    short want = POLLOUT;
+    if (io.flush_nb(&want, err)) return true;
+    if (!err->empty()) return false;
+    if (stopped(io, flow)) {
+      *err = "cancelled";
+      return false;
+    }
+    if (since(last) > idle_timeout) {
+      *err = "send timeout";
+      return false;
+    }
+    if (wait_fd(io.fd(), want, 50) < 0) {
+      *err = "socket error while sending";
+      return false;
+    }
+    last = Clock::now();
+  }
 }
 
 inline bool send_all(Stream& io, const char* p, size_t n, double idle_timeout, const Flow* flow, std::string* err) {
@@ -520,7 +538,9 @@ inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, co
     if (splice_body(io, fd, off, want, r, flow, seg, seg_done0, idle_timeout) || !r.err.empty() || r.eof)
       return r;
   }
-  Buf buf(std::max<size_t>(buf_size, 64 << 10));
+  // TLS: decrypt into an L2-sized buffer so pwrite copies cache-hot bytes
+  Buf buf(io.plain() ? std::max<size_t>(buf_size, 64 << 10) : (256u << 10));
+  const size_t fill = io.plain() ? (1u << 20) : (256u << 10);
   auto last = Clock::now();
   while (r.received < want) {
     // fill the buffer with whatever is ready (TLS yields one record per read),
@@ -534,7 +554,7 @@ inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, co
       eof = true;
     } else {
       have = static_cast<size_t>(n);
-      while (have < cap && have < (1u << 20)) {
+      while (have < cap && have < fill) {
         short w = POLLIN;
         std::string e;
         const ssize_t m = io.recv_nb(buf.data() + have, cap - have, &w, &e);
@@ -590,7 +610,9 @@ struct ChunkSigner {
 
 inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
   SendResult r;
-  const uint64_t step = 4u << 20;
+  // sendfile moves 4 MiB per call; TLS encrypts from a user buffer, kept
+  // L2-sized so the pread'd bytes are still cache-hot when encrypted
+  const uint64_t step = io.plain() ? (4u << 20) : (256u << 10);
   auto last = Clock::now();
   Buf buf(io.plain() ? 0 : static_cast<size_t>(std::min<uint64_t>(step, std::max<uint64_t>(length, 1))));
   while (r.sent < length) {

@@ -74,6 +74,13 @@ class Stream {
   virtual ssize_t send_nb(const struct iovec* iov, int cnt, short* want, std::string* err) = 0;
   // true for a bare socket: the zero-copy kernel paths (splice, sendfile) apply
   virtual bool plain() const { return false; }
+  // Push out bytes a stream buffered internally (TLS ciphertext): true when
+  // nothing is pending; false with *want = POLLOUT (retry) or *err set.
+  virtual bool flush_nb(short* want, std::string* err) {
+    (void)want;
+    (void)err;
+    return true;
+  }
 
   void abort() { aborted_.store(true); }
   bool aborted() const { return aborted_.load(std::memory_order_relaxed); }
@@ -273,6 +280,13 @@ class TlsContext {
   friend class TlsStream;
 };
 
+// Write-side BIO: records are appended to the owning stream's out_ buffer
+// (no copy beyond the encryption output itself); flush_nb() sends from it.
+class TlsStream;
+namespace detail {
+BIO_METHOD* out_bio_method();
+}
+
 class TlsStream : public Stream {
  public:
   // `host`: server name for SNI + certificate verification (client side);
@@ -282,10 +296,20 @@ class TlsStream : public Stream {
     ssl_ = SSL_new(ctx_->ctx());
     if (!ssl_) throw std::runtime_error(ssl_errors("SSL_new"));
     SSL_set_ex_data(ssl_, TlsContext::ex_index(), this);
-    if (SSL_set_fd(ssl_, fd) != 1) {
+    // Reads come straight from the socket (with read-ahead); records are
+    // written into a memory BIO and sent in large batches (flush_nb): one
+    // send(2) per ~256 KiB of ciphertext instead of one per 16 KiB record.
+    BIO* rbio = BIO_new_socket(fd, BIO_NOCLOSE);
+    wbio_ = BIO_new(detail::out_bio_method());
+    if (!rbio || !wbio_) {
+      BIO_free(rbio);
+      BIO_free(wbio_);
       SSL_free(ssl_);
-      throw std::runtime_error(ssl_errors("SSL_set_fd"));
+      throw std::runtime_error(ssl_errors("BIO_new"));
     }
+    BIO_set_data(wbio_, this);
+    BIO_set_init(wbio_, 1);
+    SSL_set_bio(ssl_, rbio, wbio_);  // ssl_ owns both
     if (ctx_->is_server()) {
       SSL_set_accept_state(ssl_);
     } else {
@@ -322,10 +346,13 @@ class TlsStream : public Stream {
   // One non-blocking handshake step: 0 = done, POLLIN / POLLOUT = wait for
   // that, -1 = failed (*err says why, incl. the certificate verdict).
   int handshake_step(std::string* err) {
+    short fw = POLLOUT;
+    if (!flush_nb(&fw, err)) return err->empty() ? POLLOUT : -1;  // earlier flight still leaving
     ERR_clear_error();
     const int r = SSL_do_handshake(ssl_);
+    const int e = r == 1 ? SSL_ERROR_NONE : SSL_get_error(ssl_, r);
+    if (!flush_nb(&fw, err)) return err->empty() ? POLLOUT : -1;  // this flight: send before waiting
     if (r == 1) return 0;
-    const int e = SSL_get_error(ssl_, r);
     if (e == SSL_ERROR_WANT_READ) return POLLIN;
     if (e == SSL_ERROR_WANT_WRITE) return POLLOUT;
     std::string msg = ssl_errors("tls handshake");
@@ -354,8 +381,47 @@ class TlsStream : public Stream {
   ssize_t recv_nb(char* p, size_t n, short* want, std::string* err) override {
     ERR_clear_error();
     size_t got = 0;
-    if (SSL_read_ex(ssl_, p, n, &got) == 1) return static_cast<ssize_t>(got);
-    return fail(SSL_get_error(ssl_, 0), "tls recv", want, err);
+    const int ok = SSL_read_ex(ssl_, p, n, &got);
+    const int e = ok == 1 ? SSL_ERROR_NONE : SSL_get_error(ssl_, 0);
+    if (out_pending()) {  // reading can produce records to send (key update, alerts)
+      short w = POLLOUT;
+      std::string ferr;
+      flush_nb(&w, &ferr);
+    }
+    if (ok == 1) return static_cast<ssize_t>(got);
+    return fail(e, "tls recv", want, err);
+  }
+
+  size_t out_pending() const { return out_.size() - out_off_; }
+  void out_append(const char* p, size_t n) {
+    if (out_off_ && out_off_ == out_.size()) {
+      out_.clear();
+      out_off_ = 0;
+    }
+    out_.insert(out_.end(), p, p + n);
+  }
+
+  bool flush_nb(short* want, std::string* err) override {
+    for (;;) {
+      const size_t n = out_pending();
+      if (n == 0) {
+        out_.clear();
+        out_off_ = 0;
+        return true;
+      }
+      const ssize_t w = ::send(fd_, out_.data() + out_off_, n, MSG_NOSIGNAL | MSG_DONTWAIT);
+      if (w > 0) {
+        out_off_ += static_cast<size_t>(w);
+        continue;
+      }
+      if (w < 0 && errno == EINTR) continue;
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        *want = POLLOUT;
+        return false;
+      }
+      *err = errno_str("tls send");
+      return false;
+    }
   }
 
   ssize_t send_nb(const struct iovec* iov, int cnt, short* want, std::string* err) override {
@@ -379,10 +445,17 @@ class TlsStream : public Stream {
       len = stage_.size();
     }
     if (len == 0) return 0;
+    // bounded ciphertext backlog: flush what is pending before encrypting more
+    if (out_pending() >= kBacklog && !flush_nb(want, err)) {
+      if (!err->empty()) return IO_ERR;
+      if (out_pending() >= kBacklog) return IO_AGAIN;
+    }
     ERR_clear_error();
     size_t w = 0;
-    if (SSL_write_ex(ssl_, src, len, &w) == 1) return static_cast<ssize_t>(w);
-    return fail(SSL_get_error(ssl_, 0), "tls send", want, err);
+    if (SSL_write_ex(ssl_, src, len, &w) != 1) return fail(SSL_get_error(ssl_, 0), "tls send", want, err);
+    short fw = POLLOUT;
+    if (!flush_nb(&fw, err) && !err->empty()) return IO_ERR;  // a backlog left here goes out on the next call
+    return static_cast<ssize_t>(w);
   }
 
   // Decrypted bytes already buffered (readable without touching the socket).
@@ -405,6 +478,9 @@ class TlsStream : public Stream {
     ERR_clear_error();
     SSL_shutdown(ssl_);
     ERR_clear_error();
+    short w = POLLOUT;
+    std::string err;
+    flush_nb(&w, &err);
   }
 
   std::string version() const { return SSL_get_version(ssl_); }
@@ -442,14 +518,48 @@ class TlsStream : public Stream {
   }
 
   static constexpr size_t kDirect = 16 << 10;
-  static constexpr size_t kMaxWrite = 1 << 20;
+  static constexpr size_t kMaxWrite = 256 << 10;  // plaintext per SSL_write: ~16 records, one flush
   static constexpr size_t kStage = 256 << 10;
+  static constexpr size_t kBacklog = 1 << 20;     // unsent ciphertext held before the writer must wait
   std::shared_ptr<TlsContext> ctx_;
   SSL* ssl_ = nullptr;
+  BIO* wbio_ = nullptr;                           // owned by ssl_
+  std::vector<char> out_;                         // ciphertext not yet sent: [out_off_, size)
+  size_t out_off_ = 0;
   int fd_;
   std::string key_;
   std::vector<char> stage_;
 };
+
+namespace detail {
+inline int out_bio_write(BIO* b, const char* p, int n) {
+  if (n <= 0) return 0;
+  static_cast<TlsStream*>(BIO_get_data(b))->out_append(p, static_cast<size_t>(n));
+  return n;
+}
+inline long out_bio_ctrl(BIO* b, int cmd, long num, void* ptr) {
+  (void)num;
+  (void)ptr;
+  switch (cmd) {
+    case BIO_CTRL_FLUSH:
+      return 1;  // flushed for real by TlsStream::flush_nb
+    case BIO_CTRL_WPENDING:
+    case BIO_CTRL_PENDING:
+      return static_cast<long>(static_cast<TlsStream*>(BIO_get_data(b))->out_pending());
+    default:
+      return 0;
+  }
+}
+inline BIO_METHOD* out_bio_method() {
+  static BIO_METHOD* m = [] {
+    BIO_METHOD* x = BIO_meth_new(BIO_get_new_index() | BIO_TYPE_SOURCE_SINK, "tritondl tls out");
+    BIO_meth_set_write(x, out_bio_write);
+    BIO_meth_set_ctrl(x, out_bio_ctrl);
+    return x;
+  }();
+  return m;
+}
+}  // namespace detail
 
 inline int TlsContext::on_new_session(SSL* ssl, SSL_SESSION* sess) {
   auto* st = static_cast<TlsStream*>(SSL_get_ex_data(ssl, ex_index()));

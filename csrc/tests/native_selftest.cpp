@@ -245,6 +245,72 @@ static void test_relay(size_t size) {
   ::unlink(opath);
 }
 
+// The same pumps over TLS (OpenSSL streams, batched ciphertext flushes): a
+// handshake on two threads, then aws-chunked send/verify and plain
+// send/receive following a Flow, plus an abort of a pump waiting for bytes.
+static void test_tls_relay(size_t size) {
+  using namespace tritondl_relay;
+  std::mt19937 rng(5);
+  std::string data(size, '\0');
+  for (auto& c : data) c = static_cast<char>(rng());
+  char path[] = "/tmp/tdl_tlsXXXXXX";
+  const int wfd = ::mkstemp(path);
+  CHECK(wfd >= 0);
+  std::string e;
+  CHECK(pwrite_full(wfd, data.data(), size, 0, &e));
+  const int rfd = ::open(path, O_RDONLY);
+  int sv[2];
+  CHECK(::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  ::fcntl(sv[0], F_SETFL, O_NONBLOCK);
+  ::fcntl(sv[1], F_SETFL, O_NONBLOCK);
+  TestPki pki = make_test_pki({"127.0.0.1", "localhost"}, 1);
+  auto sctx = TlsContext::server(pki.cert_pem, pki.key_pem);
+  auto cctx = TlsContext::client(pki.ca_pem, "", true);
+  TlsStream cli(cctx, sv[0], "127.0.0.1", "selftest"), srv(sctx, sv[1], "", "");
+  std::string serr;
+  std::thread hs([&] { serr = srv.handshake(10.0); });
+  const std::string cerr = cli.handshake(10.0);
+  hs.join();
+  CHECK(cerr.empty() && serr.empty());
+  const std::string key(32, 'k'), amz = "20260101T000000Z", scope = "20260101/us-east-1/s3/aws4_request",
+                    seed(64, '0');
+  Flow flow({{0, static_cast<int64_t>(size), 0}});
+  std::thread adv([&] {
+    for (size_t off = 0; off < size; off += 300000) flow.advance(0, std::min(size, off + 300000));
+    flow.finish(size);
+  });
+  VerifyResult vr;
+  std::thread rcv([&] { vr = recv_verify_chunked(srv, chunked_length(size, 65536), "", 0, key, amz, scope, seed,
+                                                 true, 2, 10.0); });
+  SendResult sr = send_body(cli, "", rfd, 0, size, &flow, 1, key, amz, scope, seed, 65536, 2, 10.0);
+  adv.join();
+  rcv.join();
+  CHECK(sr.err.empty() && vr.err.empty() && vr.data == data);
+  char opath[] = "/tmp/tdl_tlsoutXXXXXX";
+  const int ofd = ::mkstemp(opath);
+  RecvResult rr;
+  std::thread r2([&] { rr = recv_body(srv, ofd, 0, static_cast<int64_t>(size), "", 0, nullptr, 0, 0, 10.0); });
+  SendResult ps = send_body(cli, "", rfd, 0, size, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
+  r2.join();
+  CHECK(ps.err.empty() && rr.err.empty() && rr.received == size);
+  std::string back(size, '\0');
+  CHECK(pread_full(ofd, &back[0], size, 0) == size && back == data);
+  // abort: a receive waiting for bytes that never come
+  RecvResult ra;
+  std::thread r3([&] { ra = recv_body(srv, -1, 0, 1 << 20, "", 0, nullptr, 0, 0, 10.0); });
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  srv.abort();
+  r3.join();
+  CHECK(ra.err == "cancelled");
+  ::close(sv[0]);
+  ::close(sv[1]);
+  ::close(wfd);
+  ::close(rfd);
+  ::close(ofd);
+  ::unlink(path);
+  ::unlink(opath);
+}
+
 int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
@@ -253,6 +319,7 @@ int main(int argc, char** argv) {
   test_merkle();
   test_relay(quick ? (1u << 20) + 777 : (8u << 20) + 777);
   test_relay(0);
+  test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
   if (failures) {

@@ -179,6 +179,14 @@ class RawConn:
                 mv = mv[n:]
             else:
                 await self._wait(want)
+        while True:                      # ciphertext the TLS layer still holds
+            try:
+                want = self.tls.flush_nb()
+            except RuntimeError as e:
+                raise RawHTTPError(str(e)) from e
+            if not want:
+                return
+            await self._wait(want)
 
     def alive(self) -> bool:
         """Idle pooled connection still usable (peer has not closed it)."""
