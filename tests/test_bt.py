@@ -416,3 +416,36 @@ def test_large_torrent_file_over_http_is_read_whole(tmp_path):
         assert data == pad
         await o.stop()
     run(main())
+
+
+def test_watch_files_fires_in_file_order_and_on_resume(tmp_path):
+    """Per-file completion (streamed uploads): watched files are fetched
+    first and complete in layout order; unwatched ones come last; on a
+    redelivered job the resume check fires every whole file at once."""
+    async def main():
+        src = tmp_path / "src" / "Pack"
+        make_payload(str(src), {"a.mkv": 3_000_000, "b.mkv": 3_000_000, "c.txt": 1_000_000, "d.mkv": 2_500_000})
+        info = torrent_for(str(src), 16384)
+        tr = await HTTPTracker().start()
+        seed = await Seeder(info, str(tmp_path / "src"), trackers=[tr.url]).start()
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        order = []
+        offered = []
+
+        def pick(paths):
+            offered.extend(paths)
+            return {p for p in paths if p.endswith(".mkv")}
+
+        await _dl().download(str(dst), Sink(), magnet_for(info, [tr.url]), pick_files=pick, on_file=order.append)
+        base = str(dst / "Pack")
+        assert sorted(offered) == sorted(os.path.join(base, n) for n in ("a.mkv", "b.mkv", "c.txt", "d.mkv"))
+        assert order == [os.path.join(base, n) for n in ("a.mkv", "b.mkv", "d.mkv")]
+        _check_tree(str(src), str(dst))
+        # redelivery: everything is on disk; the resume verify fires each watched file
+        again = []
+        await _dl().download(str(dst), Sink(), magnet_for(info, [tr.url]), pick_files=pick, on_file=again.append)
+        assert sorted(again) == sorted(order)
+        await seed.stop()
+        await tr.stop()
+    run(main())

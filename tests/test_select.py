@@ -88,3 +88,56 @@ def test_trailing_slash_root_is_cleaned(tmp_path):
     r = str(tmp_path)
     a = _touch(r, "x.mp4")
     assert dir_media(r + "/") == [a]
+
+
+# ---- predict_media: the torrent path's upload-before-walk prediction must be
+# exactly what the walk returns once the files exist (service streams uploads
+# per completed file and trusts it)
+
+_NAMES = ["a.mkv", "b.mp4", "c.nfo", "d.webm", "x.MKV", "e.mov", ".mkv"]
+_DIRS = ["season 1", "Show.S01", "Extras", "s2", "Season 3", "sample", "series"]
+
+
+def _layouts():
+    import random
+    rng = random.Random(1234)
+    for _ in range(300):
+        n = rng.randint(1, 6)
+        files = set()
+        single_tld = rng.random() < 0.6
+        tld = rng.choice(_DIRS)
+        for _k in range(n):
+            depth = rng.randint(0, 3)
+            comps = [rng.choice(_DIRS) for _d in range(depth)]
+            if single_tld:
+                comps = [tld] + comps
+            files.add("/".join(comps + [rng.choice(_NAMES)]))
+        yield sorted(files)
+
+
+def test_predict_media_matches_dir_media(tmp_path):
+    from tritondl.select import predict_media
+    for k, layout in enumerate(_layouts()):
+        root = tmp_path / f"case{k}"
+        root.mkdir()
+        paths = [os.path.join(str(root), rel) for rel in layout]
+        pred = predict_media(str(root), paths)        # before any file exists
+        for p in paths:
+            if any(q.startswith(p + "/") for q in paths):
+                break                                 # a name used as both file and dir: not a layout
+        else:
+            for rel in layout:
+                _touch(str(root), rel)
+            _touch(str(root), ".torrent.db")          # top-level plain files never matter
+            assert pred == set(dir_media(str(root))), layout
+
+
+def test_predict_media_refuses_foreign_directories(tmp_path):
+    from tritondl.select import predict_media
+    os.makedirs(tmp_path / "leftover")
+    assert predict_media(str(tmp_path), [str(tmp_path / "Show" / "season 1" / "e1.mkv")]) is None
+    # a directory the torrent itself creates is fine (resume of a redelivered job)
+    os.makedirs(tmp_path / "Show")
+    os.rmdir(tmp_path / "leftover")
+    assert predict_media(str(tmp_path), [str(tmp_path / "Show" / "season 1" / "e1.mkv")]) == \
+        {str(tmp_path / "Show" / "season 1" / "e1.mkv")}

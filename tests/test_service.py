@@ -349,3 +349,59 @@ def test_stream_upload_overlaps_and_fails_cleanly(tmp_path):
         assert object_key("s2", "dies.mkv") not in e.s3.buckets["triton-staging"]
         await e.down()
     run(main())
+
+
+def test_magnet_job_streams_each_file_as_it_completes(tmp_path):
+    """Torrent jobs upload every selected file as soon as its last piece is
+    verified (files fetched in order), not after the whole torrent: the first
+    file's upload must finish before the swarm download does."""
+    async def main():
+        e = await Env().up(tmp_path)
+        src = tmp_path / "seed" / "Show.S02"
+        sizes = {"season 2/e1.mkv": 2_000_000, "season 2/e2.mkv": 2_000_000, "season 2/e3.mkv": 8_000_000,
+                 "notes.txt": 1000}
+        make_payload(str(src), sizes)
+        info = torrent_for(str(src), 32768)
+        tr = await HTTPTracker().start()
+        seed = await Seeder(info, str(tmp_path / "seed"), trackers=[tr.url]).start()
+        e.submit(Media(id="tv-2", source_uri=magnet_for(info, [tr.url])))
+        res = await e.wait_results(1, timeout=60)
+        assert res[0].ok, res[0]
+        m = res[0].marks
+        # the first file's whole upload happened while the swarm was still downloading
+        assert m["first_file"] < m["first_upload"] < m["fetched"], m
+        keys = sorted(e.s3.buckets["triton-staging"])
+        assert keys == sorted(object_key("tv-2", f"e{k}.mkv") for k in (1, 2, 3))
+        for k in (1, 2, 3):
+            assert e.s3.object_bytes("triton-staging", object_key("tv-2", f"e{k}.mkv")) == \
+                (src / "season 2" / f"e{k}.mkv").read_bytes()
+        assert res[0].files == 3 and res[0].bytes == 12_000_000
+        await seed.stop()
+        await tr.stop()
+        await e.down()
+    run(main())
+
+
+def test_magnet_job_streamed_upload_failure_fails_job(tmp_path):
+    """An S3 failure of a streamed torrent file upload cancels the swarm
+    download and fails the job at stage ``upload`` (then dead-letters it)."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=0)
+        e.svc.uploader.client.max_retries = 0
+        src = tmp_path / "seed" / "Film"
+        make_payload(str(src), {"a.mkv": 1_500_000, "b.mkv": 1_500_000})
+        info = torrent_for(str(src), 32768)
+        tr = await HTTPTracker().start()
+        seed = await Seeder(info, str(tmp_path / "seed"), trackers=[tr.url]).start()
+        e.s3.create_bucket("triton-staging")
+        e.s3.fail_for(30.0)
+        e.submit(Media(id="f-1", source_uri=magnet_for(info, [tr.url])))
+        res = await e.wait_results(1, timeout=60)
+        assert not res[0].ok and res[0].stage == "upload", res[0]
+        await asyncio.sleep(0.1)
+        dead = _dlq(e.broker)
+        assert len(dead) == 1 and dead[0].props.headers["X-Failed-Stage"] == "upload"
+        await seed.stop()
+        await tr.stop()
+        await e.down()
+    run(main())

@@ -5,6 +5,14 @@ leecher (this process, the production TorrentDownloader) downloads it from a
 magnet with x.pe peers.  Prints one JSON line with MB/s.
 
     python tools/bench_bt.py --mb 1024 --seeds 4 [--utp] [--piece-kb 1024]
+
+``--job``: the whole worker job instead of the bare download — a multi-file
+season pack (``--files`` media files sharing ``--mb``) published as a magnet
+``v1.download`` job on a fake broker, run by the production ``Service``
+(torrent download → select → S3 multipart upload to a fake S3 → publish →
+ack), timed from publish to ack.  ``--stream both`` runs it with per-file
+streamed uploads off (the reference's order: upload after the whole torrent)
+and on, alternating, and prints one JSON line per run.
 """
 
 from __future__ import annotations
@@ -30,7 +38,13 @@ async def main() -> int:
     ap.add_argument("--utp", action="store_true", help="disable TCP dialing: uTP only")
     ap.add_argument("--profile", default="")
     ap.add_argument("--encryption", default="allow", help="MSE policy for seeders and leecher")
+    ap.add_argument("--job", action="store_true", help="full worker job (download+upload+publish+ack)")
+    ap.add_argument("--files", type=int, default=8, help="--job: media files in the pack")
+    ap.add_argument("--stream", default="both", choices=["on", "off", "both"])
+    ap.add_argument("--repeat", type=int, default=2)
     a = ap.parse_args()
+    if a.job:
+        return await job_bench(a)
     from tritondl.bench_job import Backend
     from tritondl.fakes.swarm import make_payload
     from tritondl.fetch.bt.client import TorrentDownloader
@@ -78,6 +92,79 @@ async def main() -> int:
     finally:
         for s in seeds:
             await s.stop()
+        shutil.rmtree(td, ignore_errors=True)
+    return 0
+
+
+async def job_bench(a) -> int:
+    from tritondl.amqp.client import Client
+    from tritondl.amqp.codec import Properties
+    from tritondl.amqp.connection import Connection
+    from tritondl.bench_job import AK, SK, Backend
+    from tritondl.fakes.swarm import make_payload
+    from tritondl.fetch.bt.client import TorrentDownloader
+    from tritondl.fetch.bt.torrent import TorrentConfig
+    from tritondl.fetch.registry import Dispatcher
+    from tritondl.models import Download, Media, SourceType
+    from tritondl.s3.client import S3Client
+    from tritondl.s3.credentials import Static
+    from tritondl.s3.uploader import Uploader
+    from tritondl.service import Service
+    from tritondl.utils.config import Config
+    from tritondl.utils.log import log
+    log.configure("warning", "")
+    td = tempfile.mkdtemp(prefix="tdl-btjob-", dir=os.environ.get("TMPDIR", "/tmp"))
+    backs = []
+    svc = None
+    prod = None
+    try:
+        pack = os.path.join(td, "src", "Show.S01")
+        per = (a.mb << 20) // a.files
+        make_payload(pack, {f"season 1/e{k + 1:02d}.mkv": per for k in range(a.files)} | {"info.nfo": 4096})
+        seeds = [await Backend("seed", ["--path", pack, "--piece-kb", str(a.piece_kb),
+                                        "--encryption", a.encryption]).start() for _ in range(a.seeds)]
+        broker = await Backend("broker").start()
+        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+        backs = seeds + [broker, s3]
+        magnet = seeds[0].info["url"] + "&" + "&".join(f"x.pe={s.info['endpoint']}" for s in seeds)
+        cfg = Config()
+        cfg.download_dir = os.path.join(td, "downloading")
+        cfg.cleanup, cfg.max_retries, cfg.retry_delay_s = True, 0, 0.0
+        cfg.progress_log_interval_s, cfg.heartbeat_s = 0, 0
+        bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
+                                             encryption=a.encryption), progress_interval=1.0, use_dht=False)
+        svc = Service(cfg, amqp=Client(broker.info["url"], heartbeat=0, retry_delay=0),
+                      dispatcher=Dispatcher(cfg.download_dir, [bt], 0),
+                      uploader=Uploader(cfg.bucket, S3Client(s3.info["url"], Static(AK, SK))))
+        await svc.start()
+        prod = await Connection.open(broker.info["url"], heartbeat=0)
+        ch = await prod.channel()
+        await ch.confirm_select()
+        modes = {"on": [True], "off": [False], "both": [False, True]}[a.stream]
+        for rep in range(a.repeat):
+            for on in modes:
+                cfg.stream_upload = on
+                n0 = len(svc.results)
+                body = Download(created_at="now", media=Media(id=f"pack-{rep}-{int(on)}", source=SourceType.TORRENT,
+                                                              source_uri=magnet)).encode()
+                t0 = time.perf_counter()
+                await ch.basic_publish("v1.download", "v1.download-0", body, Properties(delivery_mode=2))
+                while len(svc.results) == n0:
+                    await asyncio.sleep(0.002)
+                dt = time.perf_counter() - t0
+                r = svc.results[-1]
+                assert r.ok and r.files == a.files and r.bytes == per * a.files, r
+                print(json.dumps({"metric": "bt_job_seconds", "value": round(dt, 3), "stream_upload": on,
+                                  "mb": a.mb, "files": a.files, "seeds": a.seeds, "piece_kb": a.piece_kb,
+                                  "job_MB_per_sec": round(a.mb * 1.048576 / dt, 1),
+                                  "spans_ms": {k: round(v * 1000, 1) for k, v in r.marks.items()}}), flush=True)
+    finally:
+        if prod is not None:
+            await prod.close()
+        if svc is not None:
+            await svc.shutdown(grace=10)
+        for b in backs:
+            await b.stop()
         shutil.rmtree(td, ignore_errors=True)
     return 0
 

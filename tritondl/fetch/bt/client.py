@@ -46,6 +46,8 @@ def _parse_hostports(s: str) -> list[tuple[str, int]]:
 
 
 class TorrentDownloader:
+    streams_files = True          # download() accepts pick_files/on_file (per-file streamed uploads)
+
     def __init__(self, cfg: TorrentConfig | None = None, *, metadata_timeout: float = 600.0,
                  progress_interval: float = 1.0, use_dht: bool = True,
                  dht_bootstrap: list[tuple[str, int]] | None = None, extra_trackers: list[str] | None = None,
@@ -124,7 +126,11 @@ class TorrentDownloader:
         await t.start()
         return t, dht
 
-    async def download(self, base_dir: str, progress: ProgressSink, url: str) -> None:
+    async def download(self, base_dir: str, progress: ProgressSink, url: str, *,
+                       pick_files=None, on_file=None) -> None:
+        """``pick_files``/``on_file``: see :meth:`Torrent.watch_files` — the
+        service uses them to start each media file's upload as soon as that
+        file is whole."""
         t, dht = await self.open(base_dir, url)
         stop = asyncio.Event()
         rep: asyncio.Task | None = None
@@ -135,6 +141,8 @@ class TorrentDownloader:
             except asyncio.TimeoutError as e:
                 raise TorrentError("failed to get metadata") from e
             log.info("fetched torrent metadata")
+            if on_file is not None:
+                t.watch_files(pick_files, on_file)
             await t.download_all()
             total = t.info.total_length if t.info else 0
 

@@ -159,6 +159,12 @@ class Torrent:
         self._rare_t = 0.0
         self._rare_dirty = True
         self._finishers: set[asyncio.Task] = set()
+        # per-file completion (streamed uploads): see watch_files
+        self._file_cb = None                            # callable(path) for watched files
+        self._file_pick = None                          # callable([paths]) -> set of paths to watch
+        self._file_left: dict[int, int] = {}            # watched file index -> pieces still missing
+        self._piece_files: dict[int, list[int]] = {}    # piece -> watched files it covers
+        self._piece_rank: list[int] | None = None       # picker band per piece (lower first)
         self.peers: dict[tuple[str, int], _Peer] = {}
         self.known: set[tuple[str, int]] = set()
         self.connecting: set[tuple[str, int]] = set()
@@ -274,6 +280,7 @@ class Torrent:
         for i in have:
             self.have[i] = 1
         self.nhave = len(have)
+        self._init_file_tracking()
         self._downloading = True
         if self.nhave == self.info.num_pieces:
             self.complete.set()
@@ -281,6 +288,67 @@ class Torrent:
             self._send_have_state(p)
             self._update_interest(p)
             self._fill(p)
+
+    # ------------------------------------------------------------ per-file completion
+    def watch_files(self, pick, on_complete) -> None:
+        """Stream files out as they finish instead of after the whole torrent.
+
+        ``pick(paths)`` is called once storage is laid out with every file's
+        path and returns the subset to watch; ``on_complete(path)`` fires (on
+        the loop) when the last piece covering a watched file is verified and
+        written — at once for files the resume check already found whole.
+        Watched files also move to the front of the piece picker, in layout
+        order (rarest-first within each file), so they finish one by one.
+        The reference uploaded only after ``WaitAll`` (``torrent.go:104-113``
+        → ``downloader.go:122-133``); this lets the uploads overlap the swarm.
+        Must be called before :meth:`download_all`."""
+        self._file_pick, self._file_cb = pick, on_complete
+
+    def _init_file_tracking(self) -> None:
+        if self._file_cb is None or self.info is None or self.storage is None:
+            return
+        layout = self.storage.layout
+        picked = self._file_pick([p for p, _n in layout if p]) if self._file_pick else set()
+        pl = self.info.piece_length
+        n = self.info.num_pieces
+        rank = [len(layout)] * n
+        done: list[str] = []
+        for fi, (path, length) in enumerate(layout):
+            if not path or path not in picked:
+                continue
+            off = self.info.files[fi].offset
+            if length == 0:
+                done.append(path)
+                continue
+            first, last = off // pl, (off + length - 1) // pl
+            left = 0
+            for i in range(first, last + 1):
+                rank[i] = min(rank[i], fi)
+                if not self.have[i]:
+                    left += 1
+                    self._piece_files.setdefault(i, []).append(fi)
+            if left:
+                self._file_left[fi] = left
+            else:
+                done.append(path)
+        if picked:
+            self._piece_rank = rank
+            self._rare = None
+        for path in done:
+            self._file_cb(path)
+
+    def _note_piece(self, i: int) -> None:
+        fis = self._piece_files.pop(i, None)
+        if not fis:
+            return
+        assert self.storage is not None
+        for fi in fis:
+            left = self._file_left[fi] - 1
+            if left:
+                self._file_left[fi] = left
+            else:
+                del self._file_left[fi]
+                self._file_cb(self.storage.layout[fi][0])
 
     def bytes_completed(self) -> int:
         if self.info is None:
@@ -578,7 +646,12 @@ class Torrent:
                 self._rare_pos >= len(self._rare):
             idx = [i for i in range(len(self.have)) if not self.have[i]]
             random.shuffle(idx)
-            idx.sort(key=self.avail.__getitem__)
+            rank = self._piece_rank
+            if rank is None:
+                idx.sort(key=self.avail.__getitem__)
+            else:                          # watched files first, in order; rarest-first within
+                av = self.avail
+                idx.sort(key=lambda i: (rank[i], av[i]))
             self._rare, self._rare_t, self._rare_dirty, self._rare_pos = idx, now, False, 0
         return self._rare
 
@@ -730,6 +803,8 @@ class Torrent:
             if q.am_interested and q.have[i] and not self._wants(q):
                 q.am_interested = False
                 q.wire.send(pw.NOT_INTERESTED)
+        if self._piece_files:
+            self._note_piece(i)
         if self.nhave == self.info.num_pieces:
             self.complete.set()
         return True

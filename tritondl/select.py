@@ -79,5 +79,42 @@ def dir_media(path: str) -> list[str]:
     return files
 
 
+def predict_media(path: str, files: list[str]) -> set[str] | None:
+    """What :func:`dir_media` will return for ``files`` (absolute paths below
+    ``path``) once they exist — evaluated on the path strings alone, so a
+    torrent's media files can be uploaded as each completes.
+
+    Only directories change the rules (the sole-top-level-directory
+    allow-list entry), so the prediction is exact when every directory that
+    exists under ``path`` now is one the torrent itself creates; any other
+    top-level directory returns ``None`` (the caller must wait for the real
+    walk).  Plain files that are not in ``files`` never change the answer for
+    the files that are."""
+    root = go_join(path)
+    rels: list[list[str]] = []
+    for f in files:
+        p = go_join(f)
+        if not p.startswith(root.rstrip("/") + "/"):
+            return None
+        rels.append(p[len(root.rstrip("/")) + 1:].split("/"))
+    tops = {r[0] for r in rels if len(r) > 1}
+    try:
+        with os.scandir(path) as it:
+            present = {e.name for e in it if e.is_dir(follow_symlinks=False)}
+    except FileNotFoundError:
+        present = set()
+    if not present <= tops:
+        return None
+    allowed: tuple[str, ...] = ALLOWED_DIRS
+    if len(tops) == 1:
+        allowed = allowed + (next(iter(tops)),)
+    out: set[str] = set()
+    for r in rels:
+        full = go_join(root, *r)
+        if go_ext(full) in MEDIA_EXTS and all(_dir_allowed(c, allowed) for c in r[:-1]):
+            out.add(full)
+    return out
+
+
 # Reference-compatible alias: ``process.Dir``.
 Dir = dir_media

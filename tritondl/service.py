@@ -48,10 +48,10 @@ from .fetch.http import HTTPDownloader
 from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
 from .s3.uploader import UploadError, Uploader
-from .select import MEDIA_EXTS, dir_media
+from .select import MEDIA_EXTS, dir_media, predict_media
 from .utils import rawhttp
 from .utils.config import Config
-from .utils.gocompat import go_ext, go_time_string
+from .utils.gocompat import go_ext, go_join, go_time_string
 from .utils.log import log
 from .utils.metrics import Metrics, serve_metrics
 from .utils.profiler import CPUProfiler
@@ -216,7 +216,7 @@ class Service:
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="download")
             mark("download")
             stage = "select"
-            if streamed:
+            if streamed and len(streamed) == 1:
                 files = dir_media(dl_dir)      # single-file HTTP job dir: a few entries, no executor hop
             else:
                 files = await asyncio.get_running_loop().run_in_executor(None, dir_media, dl_dir)
@@ -276,6 +276,8 @@ class Service:
         running back to back.  Returns (job dir, {path: UploadResult})."""
         assert self.dispatcher is not None and self.uploader is not None
         impl = self.dispatcher.select(url)
+        if self.cfg.stream_upload and getattr(impl, "streams_files", False):
+            return await self._download_torrent(impl, media_id, url, marks, t0)
         if not (self.cfg.stream_upload and isinstance(impl, HTTPDownloader)):
             return await self.dispatcher.download(media_id, url), {}
         d = self.dispatcher.job_dir(media_id)
@@ -306,6 +308,70 @@ class Service:
         finally:
             if fd is not None:
                 os.close(fd)
+
+    async def _download_torrent(self, impl, media_id: str, url: str, marks: dict | None,
+                                t0: float) -> tuple[str, dict]:
+        """Torrent job with per-file streamed uploads: every file the selector
+        will pick starts its S3 upload the moment its last piece is verified
+        (the torrent fetches those files first, in order), so upload time
+        overlaps the rest of the swarm download instead of following it.  An
+        upload failure cancels the download.  Returns (job dir, {path:
+        UploadResult}) for the files already uploaded; anything the final
+        selector walk finds beyond them is uploaded afterwards as before."""
+        assert self.dispatcher is not None and self.uploader is not None
+        d = self.dispatcher.job_dir(media_id)
+        os.makedirs(d, mode=0o755, exist_ok=True)
+        uploads: dict[str, asyncio.Task] = {}
+        sem = asyncio.Semaphore(self.uploader.file_concurrency)
+        dl: asyncio.Task | None = None
+
+        def pick(paths: list[str]) -> set[str]:
+            got = predict_media(d, paths)
+            if got is None:
+                log.with_field("dir", d).debug("job dir has foreign directories; uploads wait for the download")
+                return set()
+            return got
+
+        async def upload_one(path: str):
+            async with sem:
+                res = await self.uploader.upload_files(media_id, d, [path])
+            if marks is not None and "first_upload" not in marks:
+                marks["first_upload"] = time.monotonic() - t0
+            return res[0]
+
+        def upload_failed(t: asyncio.Task) -> None:
+            if not t.cancelled() and t.exception() is not None and dl is not None and not dl.done():
+                dl.cancel()
+
+        def on_file(path: str) -> None:
+            path = go_join(path)
+            if path in uploads:
+                return
+            if marks is not None and not uploads:
+                marks["first_file"] = time.monotonic() - t0
+            t = asyncio.ensure_future(upload_one(path))
+            t.add_done_callback(upload_failed)
+            uploads[path] = t
+
+        dl = asyncio.ensure_future(impl.download(d, self.dispatcher.sink, url, pick_files=pick, on_file=on_file))
+        try:
+            try:
+                await dl
+            except asyncio.CancelledError:
+                failed = [t for t in uploads.values() if t.done() and not t.cancelled() and t.exception()]
+                if failed:
+                    raise failed[0].exception() from None
+                raise
+            if marks is not None:
+                marks["fetched"] = time.monotonic() - t0
+            done = await asyncio.gather(*uploads.values())
+            return d, dict(zip(uploads, done))
+        except BaseException:
+            dl.cancel()
+            for t in uploads.values():
+                t.cancel()
+            await asyncio.gather(dl, *uploads.values(), return_exceptions=True)
+            raise
 
     def _record(self, r: JobResult) -> JobResult:
         self.results.append(r)
