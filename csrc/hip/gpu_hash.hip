@@ -22,9 +22,18 @@
 //    full by two consecutive blocks while it is still L2-resident.
 //  * Host side: pinned double-buffered staging, one HIP stream per slot:
 //    parallel pread() of batch b+1 overlaps H2D + kernel + D2H of batch b.
+//  * Hybrid mode (cpu_threads > 0): the whole job is host->HBM bound
+//    (~45 GB/s of page-cache copies + PCIe), so the CPU's SHA-NI threads
+//    verify pieces from the BACK of the layout while the GPU pipeline claims
+//    staging chunks from the FRONT; they meet wherever the two rates put the
+//    boundary (no static split to mis-calibrate).  The GPU stops claiming
+//    once the CPU could finish the rest faster than one more kernel's
+//    per-lane latency, so the last window's kernel overlaps CPU work.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include "../hash/hash_core.h"  // OpenSSL SHA-NI path for the CPU half of hybrid verification
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -32,8 +41,10 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -373,7 +384,7 @@ class GpuHasher {
     std::string out(n * dl, '\0');
     {
       py::gil_scoped_release nogil;
-      run_windows(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, char*) {
+      run_gpu_only(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, char*) {
         copy_parallel(dst, src + off, len);
       }, [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>&) {
         std::memcpy(&out[first * dl], digests, count * dl);
@@ -382,90 +393,90 @@ class GpuHasher {
     return py::bytes(out);
   }
 
+  // Open a layout's files; spans carry stream offsets (kZeroSpan = padding).
+  static std::vector<Span> open_spans(const std::vector<std::pair<std::string, long long>>& files, long long& total) {
+    std::vector<Span> spans;
+    total = 0;
+    for (auto& f : files) {
+      if (f.second < 0) {
+        close_spans(spans);
+        throw std::invalid_argument("negative file length");
+      }
+      spans.push_back({f.first.empty() ? kZeroSpan : ::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
+      total += f.second;
+    }
+    return spans;
+  }
+  static void close_spans(std::vector<Span>& spans) {
+    for (auto& s : spans)
+      if (s.fd >= 0) ::close(s.fd);
+    spans.clear();
+  }
+
+  // (digests, complete) of every piece of a layout: GPU only, or hybrid with
+  // cpu_threads SHA-NI threads working from the other end.
+  void layout_digests(int alg, std::vector<Span>& spans, size_t piece_len, size_t total, size_t n, int cpu_threads,
+                      std::string& digests, std::string& complete) {
+    const int dl = digest_len(alg);
+    digests.assign(n * dl, '\0');
+    complete.assign(n, '\0');
+    py::gil_scoped_release nogil;
+    try {
+      if (cpu_threads > 0) {
+        hybrid_digest(alg, spans, piece_len, total, n, cpu_threads, digests, complete);
+      } else {
+        run_gpu_only(alg, piece_len, total, n,
+                     [&](uint8_t* dst, size_t off, size_t len, char* comp) {
+                       read_spans(spans, dst, off, len, piece_len, comp);
+                     },
+                     [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
+                       std::memcpy(&digests[first * dl], d, count * dl);
+                       for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
+                     });
+        last_gpu_pieces_ = n;
+      }
+    } catch (...) {
+      close_spans(spans);
+      throw;
+    }
+    close_spans(spans);
+  }
+
   // Verify a torrent's concatenated file layout against expected digests.
   py::bytes verify_files(const std::vector<std::pair<std::string, long long>>& files, size_t piece_len,
-                         const std::string& expected, const std::string& kind) {
+                         const std::string& expected, const std::string& kind, int cpu_threads) {
     const int alg = alg_id(kind);
     const int dl = digest_len(alg);
     if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
     if (expected.size() % dl) throw std::invalid_argument("expected digest blob has wrong size");
-    std::vector<Span> spans;
     long long total = 0;
-    for (auto& f : files) {
-      if (f.second < 0) throw std::invalid_argument("negative file length");
-      spans.push_back({f.first.empty() ? kZeroSpan : ::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
-      total += f.second;
-    }
-    auto close_all = [&] {
-      for (auto& s : spans)
-        if (s.fd >= 0) ::close(s.fd);
-    };
+    std::vector<Span> spans = open_spans(files, total);
     const size_t n = expected.size() / dl;
     const size_t need = total > 0 ? (static_cast<size_t>(total) + piece_len - 1) / piece_len : 0;
     if (n != need) {
-      close_all();
+      close_spans(spans);
       throw std::invalid_argument("piece count does not match total length");
     }
+    std::string digests, complete;
+    layout_digests(alg, spans, piece_len, static_cast<size_t>(total), n, cpu_threads, digests, complete);
     std::string ok(n, '\0');
-    {
-      py::gil_scoped_release nogil;
-      try {
-        run_windows(alg, piece_len, static_cast<size_t>(total), n,
-                    [&](uint8_t* dst, size_t off, size_t len, char* complete) {
-                      read_spans(spans, dst, off, len, piece_len, complete);
-                    },
-                    [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>& complete) {
-                      for (size_t k = 0; k < count; ++k)
-                        ok[first + k] = complete[k] &&
-                                        std::memcmp(digests + k * dl, expected.data() + (first + k) * dl, dl) == 0;
-                    });
-      } catch (...) {
-        close_all();
-        throw;
-      }
-    }
-    close_all();
+    for (size_t k = 0; k < n; ++k)
+      ok[k] = complete[k] && std::memcmp(digests.data() + k * dl, expected.data() + k * dl, dl) == 0;
     return py::bytes(ok);
   }
 
   // All piece digests of a file layout plus a per-piece "fully read" mask —
   // used at 16 KiB "pieces" for BitTorrent v2 merkle leaves (host reduces).
   py::tuple digest_files(const std::vector<std::pair<std::string, long long>>& files, size_t piece_len,
-                         const std::string& kind) {
+                         const std::string& kind, int cpu_threads) {
     const int alg = alg_id(kind);
-    const int dl = digest_len(alg);
     if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
-    std::vector<Span> spans;
     long long total = 0;
-    for (auto& f : files) {
-      if (f.second < 0) throw std::invalid_argument("negative file length");
-      spans.push_back({f.first.empty() ? kZeroSpan : ::open(f.first.c_str(), O_RDONLY | O_CLOEXEC), total, f.second});
-      total += f.second;
-    }
-    auto close_all = [&] {
-      for (auto& s : spans)
-        if (s.fd >= 0) ::close(s.fd);
-    };
+    std::vector<Span> spans = open_spans(files, total);
     const size_t n = total > 0 ? (static_cast<size_t>(total) + piece_len - 1) / piece_len : 0;
-    std::string digests(n * dl, '\0'), ok(n, '\0');
-    {
-      py::gil_scoped_release nogil;
-      try {
-        run_windows(alg, piece_len, static_cast<size_t>(total), n,
-                    [&](uint8_t* dst, size_t off, size_t len, char* complete) {
-                      read_spans(spans, dst, off, len, piece_len, complete);
-                    },
-                    [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& complete) {
-                      std::memcpy(&digests[first * dl], d, count * dl);
-                      for (size_t k = 0; k < count; ++k) ok[first + k] = complete[k];
-                    });
-      } catch (...) {
-        close_all();
-        throw;
-      }
-    }
-    close_all();
-    return py::make_tuple(py::bytes(digests), py::bytes(ok));
+    std::string digests, complete;
+    layout_digests(alg, spans, piece_len, static_cast<size_t>(total), n, cpu_threads, digests, complete);
+    return py::make_tuple(py::bytes(digests), py::bytes(complete));
   }
 
   size_t batch_bytes() const { return stage_req_; }
@@ -547,6 +558,40 @@ class GpuHasher {
     for (auto& th : ts) th.join();
   }
 
+  // Read stream bytes [ga, ge) of the layout into p (single thread); marks
+  // complete[k] = 0 for every piece k (relative to the piece at stream offset
+  // `base`) that could not be fully read.
+  static void read_range(const std::vector<Span>& spans, uint8_t* p, long long ga, long long ge, long long base,
+                         size_t piece_len, size_t np, char* complete) {
+    auto fail_range = [&](long long a, long long e) {  // stream offsets -> pieces
+      if (e <= a) return;
+      const size_t k0 = static_cast<size_t>(a - base) / piece_len;
+      const size_t k1 = (static_cast<size_t>(e - base) + piece_len - 1) / piece_len;
+      for (size_t k = k0; k < std::min(k1, np); ++k) complete[k] = 0;
+    };
+    long long cur = ga;
+    for (const Span& s : spans) {
+      if (s.start + s.length <= cur || s.start >= ge) continue;
+      const long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
+      const size_t want = static_cast<size_t>(re - ra);
+      uint8_t* q = p + (ra - ga);
+      size_t got = 0;
+      if (s.fd == kZeroSpan) {
+        std::memset(q, 0, want);
+        got = want;
+      } else if (s.fd >= 0) {
+        got = pread_full(s.fd, q, want, static_cast<off_t>(ra - s.start));
+      }
+      if (got != want) {
+        std::memset(q + got, 0, want - got);
+        fail_range(ra + static_cast<long long>(got), re);
+      }
+      cur = re;
+      if (cur >= ge) break;
+    }
+    fail_range(cur, ge);  // a gap nobody covers: incomplete
+  }
+
   // Read [off, off+len) (piece-aligned) of the concatenated layout into dst;
   // complete[k] is cleared for every piece k of this range not fully read.
   // Work is split into units of >= 1 MiB (whole pieces), so 16 KiB "pieces"
@@ -557,37 +602,11 @@ class GpuHasher {
     const size_t per_unit = std::max<size_t>(1, (1u << 20) / piece_len);
     const size_t nu = (np + per_unit - 1) / per_unit;
     std::atomic<size_t> next{0};
-    auto fail_range = [&](long long a, long long e) {  // stream offsets -> pieces of this window
-      if (e <= a) return;
-      const size_t k0 = static_cast<size_t>(a - static_cast<long long>(off)) / piece_len;
-      const size_t k1 = (static_cast<size_t>(e - static_cast<long long>(off)) + piece_len - 1) / piece_len;
-      for (size_t k = k0; k < std::min(k1, np); ++k) complete[k] = 0;
-    };
     auto work = [&] {
-      for (size_t u; (u = next.fetch_add(1)) < nu;) {
+      for (size_t u; (u = next.fetch_add(1)) < nu;) {  // units own disjoint pieces: no race on complete
         const size_t a = u * per_unit * piece_len, e = std::min(len, a + per_unit * piece_len);
-        const long long ga = static_cast<long long>(off + a), ge = static_cast<long long>(off + e);
-        long long cur = ga;
-        for (const Span& s : spans) {
-          if (s.start + s.length <= cur || s.start >= ge) continue;
-          const long long ra = std::max(cur, s.start), re = std::min(ge, s.start + s.length);
-          const size_t want = static_cast<size_t>(re - ra);
-          uint8_t* p = dst + (ra - static_cast<long long>(off));
-          size_t got = 0;
-          if (s.fd == kZeroSpan) {
-            std::memset(p, 0, want);
-            got = want;
-          } else if (s.fd >= 0) {
-            got = pread_full(s.fd, p, want, static_cast<off_t>(ra - s.start));
-          }
-          if (got != want) {
-            std::memset(p + got, 0, want - got);
-            fail_range(ra + static_cast<long long>(got), re);
-          }
-          cur = re;
-          if (cur >= ge) break;
-        }
-        fail_range(cur, ge);  // a gap nobody covers: incomplete (units own disjoint pieces: no race)
+        read_range(spans, dst + a, static_cast<long long>(off + a), static_cast<long long>(off + e),
+                   static_cast<long long>(off), piece_len, np, complete);
       }
     };
     std::vector<std::thread> ts;
@@ -597,16 +616,21 @@ class GpuHasher {
     for (auto& th : ts) th.join();
   }
 
-  template <class Fill, class Harvest>
-  void run_windows(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest) {
+  // Pipeline driver.  claim(max) hands out the next contiguous run of pieces
+  // [first, first+count) from the front of the layout (count 0 = no more);
+  // runs are packed into an HBM window until it is full or claims dry up,
+  // then one kernel hashes the window while the next one is being filled.
+  template <class Claim, class Fill, class Harvest>
+  void run_windows(int alg, size_t piece_len, size_t total, size_t n, size_t wbytes, Claim&& claim, Fill&& fill,
+                   Harvest&& harvest) {
     HIP_CHECK(hipSetDevice(device_));
     if (n == 0) return;
     const int dl = digest_len(alg);
-    const size_t wbytes = window_bytes_for(total, piece_len);
     last_window_ = wbytes;
-    const size_t per = wbytes / piece_len;                                   // pieces per window
-    const size_t stage = std::max<size_t>(1, stage_req_ / piece_len) * piece_len;  // piece-aligned staging
-    for (auto& st : stage_) ensure_stage(st, std::min(stage, wbytes));
+    const size_t per = std::min(n, wbytes / piece_len);                            // pieces per window
+    const size_t stage_p = std::max<size_t>(1, stage_req_ / piece_len);            // pieces per staging chunk
+    const size_t stage = stage_p * piece_len;
+    for (auto& st : stage_) ensure_stage(st, std::min(stage, per * piece_len));
     auto drain = [&](Window& w) {
       if (!w.pending) return;
       HIP_CHECK(hipEventSynchronize(w.done));
@@ -614,23 +638,32 @@ class GpuHasher {
       w.pending = false;
     };
     size_t widx = 0, sidx = 0;
-    for (size_t first = 0; first < n; first += per, ++widx) {
+    for (bool more = true; more; ++widx) {
       Window& w = win_[widx % 2];
       drain(w);  // its previous window (widx-2) must be hashed before we overwrite it
-      const size_t count = std::min(per, n - first);
-      const size_t woff = first * piece_len;
-      const size_t wlen = std::min(total - woff, count * piece_len);
-      ensure_window(w, count * piece_len, count * dl);
-      w.complete.assign(count, 1);
-      for (size_t off = 0; off < wlen; off += stage) {
+      ensure_window(w, per * piece_len, per * dl);
+      w.complete.assign(per, 1);
+      size_t count = 0, first = 0;
+      while (count < per) {
+        const auto got = claim(std::min(stage_p, per - count));
+        if (got.second == 0) {
+          more = false;
+          break;
+        }
+        if (count == 0) first = got.first;
+        if (got.first != first + count) throw std::logic_error("non-contiguous GPU claim");
         Stage& st = stage_[sidx++ % kStages];
         if (st.used) HIP_CHECK(hipEventSynchronize(st.free_ev));  // its previous H2D has landed
-        const size_t len = std::min(stage, wlen - off);
-        fill(st.h, woff + off, len, w.complete.data() + off / piece_len);
-        HIP_CHECK(hipMemcpyAsync(w.d + off, st.h, len, hipMemcpyHostToDevice, copy_stream_));
+        const size_t off = got.first * piece_len;
+        const size_t len = std::min(total - off, got.second * piece_len);
+        fill(st.h, off, len, w.complete.data() + count);
+        HIP_CHECK(hipMemcpyAsync(w.d + count * piece_len, st.h, len, hipMemcpyHostToDevice, copy_stream_));
         HIP_CHECK(hipEventRecord(st.free_ev, copy_stream_));
         st.used = true;
+        count += got.second;
       }
+      if (count == 0) break;
+      const size_t wlen = std::min(total - first * piece_len, count * piece_len);
       HIP_CHECK(hipEventRecord(w.copied, copy_stream_));
       HIP_CHECK(hipStreamWaitEvent(compute_stream_, w.copied, 0));
       launch_hash(alg, w.d, wlen, piece_len, static_cast<uint32_t>(count), w.d_out, compute_stream_);
@@ -644,6 +677,122 @@ class GpuHasher {
     drain(win_[(widx + 1) % 2]);
   }
 
+  // The whole layout front-to-back on the GPU (no CPU share).
+  template <class Fill, class Harvest>
+  void run_gpu_only(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest) {
+    size_t front = 0;
+    run_windows(alg, piece_len, total, n, window_bytes_for(total, piece_len),
+                [&](size_t mx) {
+                  const size_t c = std::min(mx, n - front);
+                  const size_t f = front;
+                  front += c;
+                  return std::make_pair(f, c);
+                },
+                fill, harvest);
+  }
+
+ public:
+  // Digest every piece of a file layout with the GPU pipeline claiming from
+  // the front and `cpu_threads` SHA-NI threads claiming >= 1 MiB units from
+  // the back.  Fills digests (n*dl) and complete (n) for all pieces.
+  void hybrid_digest(int alg, const std::vector<Span>& spans, size_t piece_len, size_t total, size_t n,
+                     int cpu_threads, std::string& digests, std::string& complete) {
+    const int dl = digest_len(alg);
+    const EVP_MD* md = alg == 1 ? tritondl_hash::sha1_md() : tritondl_hash::sha256_md();
+    std::mutex mu;
+    size_t front = 0, back = n;
+    std::atomic<unsigned long long> cpu_bytes{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    // one more GPU window costs at least the per-lane latency of one piece
+    // (one lane per piece, ~55 MB/s/lane measured) plus set-up
+    const double kernel_s = static_cast<double>(piece_len) / 55e6 + 1e-3;
+    constexpr double kCopyBps = 40e9;  // page cache -> pinned -> HBM, measured ~36-45 GB/s
+    const size_t unit = std::max<size_t>(1, (1u << 20) / piece_len);
+    std::exception_ptr cpu_err;
+    auto cpu_worker = [&] {
+      try {
+        std::vector<uint8_t> buf(unit * piece_len);
+        std::vector<char> ok(unit);
+        for (;;) {
+          size_t s, e;
+          {
+            std::lock_guard<std::mutex> g(mu);
+            if (back <= front) return;
+            e = back;
+            s = e - std::min(unit, back - front);
+            back = s;
+          }
+          const long long ga = static_cast<long long>(s * piece_len);
+          const long long ge = std::min(static_cast<long long>(total), static_cast<long long>(e * piece_len));
+          std::fill(ok.begin(), ok.end(), 1);
+          read_range(spans, buf.data(), ga, ge, ga, piece_len, e - s, ok.data());
+          for (size_t p = s; p < e; ++p) {
+            const size_t po = (p - s) * piece_len;
+            const size_t pl = std::min<size_t>(piece_len, static_cast<size_t>(ge - ga) - po);
+            const std::string d = tritondl_hash::one_shot(md, buf.data() + po, pl);
+            std::memcpy(&digests[p * dl], d.data(), dl);
+            complete[p] = ok[p - s];
+          }
+          cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!cpu_err) cpu_err = std::current_exception();
+        back = front;  // stop everyone
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int k = 0; k < cpu_threads; ++k) ts.emplace_back(cpu_worker);
+    size_t gpu_pieces = 0;
+    try {
+      // 1 GiB windows: kernels of earlier windows overlap later copies, so only
+      // the last window's latency is exposed — and the claim rule below hands
+      // that tail to the CPU threads
+      const size_t wb = std::max(piece_len, std::min<size_t>(window_bytes_for(total, piece_len), 1ull << 30));
+      run_windows(alg, piece_len, total, n, wb,
+                  [&](size_t mx) {
+                    std::lock_guard<std::mutex> g(mu);
+                    const size_t left = back - front;
+                    if (left == 0) return std::make_pair(front, size_t(0));
+                    if (cpu_threads > 0) {
+                      mx = std::min(mx, std::max<size_t>(unit, left / 2));  // leave the CPU its share near the end
+                      // take the chunk only if the GPU would finish it (copy + one
+                      // kernel latency) before the CPU threads could finish
+                      // everything that is left on their own
+                      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                      const double cpu_bps = el > 1e-3 ? cpu_bytes.load() / el : 0.0;
+                      const double chunk = static_cast<double>(std::min(mx, left)) * piece_len;
+                      if (cpu_bps > 0 && static_cast<double>(left) * piece_len / cpu_bps < chunk / kCopyBps + kernel_s)
+                        return std::make_pair(front, size_t(0));
+                    }
+                    const size_t c = std::min(mx, left);
+                    const size_t f = front;
+                    front += c;
+                    gpu_pieces += c;
+                    return std::make_pair(f, c);
+                  },
+                  [&](uint8_t* dst, size_t off, size_t len, char* comp) { read_spans(spans, dst, off, len, piece_len, comp); },
+                  [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
+                    std::memcpy(&digests[first * dl], d, count * dl);
+                    for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
+                  });
+    } catch (...) {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        back = front;
+      }
+      for (auto& th : ts) th.join();
+      throw;
+    }
+    for (auto& th : ts) th.join();
+    if (cpu_err) std::rethrow_exception(cpu_err);
+    last_gpu_pieces_ = gpu_pieces;
+  }
+
+  size_t last_gpu_pieces() const { return last_gpu_pieces_; }
+
+ private:
+  size_t last_gpu_pieces_ = 0;
   int device_;
   size_t stage_req_;
   int readers_;
@@ -687,9 +836,12 @@ PYBIND11_MODULE(_gpu_hash, m) {
            "a third of free HBM capped at 48 GiB)")
       .def("hash_buffer", &GpuHasher::hash_buffer, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"))
       .def("verify_files", &GpuHasher::verify_files, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
-           py::arg("kind") = "sha1")
+           py::arg("kind") = "sha1", py::arg("cpu_threads") = 0,
+           "one byte (0/1) per piece; cpu_threads > 0: hybrid (SHA-NI threads take pieces from the back)")
       .def("digest_files", &GpuHasher::digest_files, py::arg("files"), py::arg("piece_len"), py::arg("kind") = "sha256",
-           "(digests, fully_read_mask) of every piece of a file layout")
+           py::arg("cpu_threads") = 0, "(digests, fully_read_mask) of every piece of a file layout")
+      .def_property_readonly("last_gpu_pieces", &GpuHasher::last_gpu_pieces,
+                             "pieces the GPU hashed in the last verify/digest call (the rest: CPU threads)")
       .def("release", &GpuHasher::release)
       .def("window_bytes_for", &GpuHasher::window_bytes_for)
       .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)

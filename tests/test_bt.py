@@ -5,6 +5,7 @@ HTTP, resume from partial data, corrupt seeder)."""
 import asyncio
 import hashlib
 import os
+import shutil
 
 import pytest
 
@@ -448,4 +449,51 @@ def test_watch_files_fires_in_file_order_and_on_resume(tmp_path):
         assert sorted(again) == sorted(order)
         await seed.stop()
         await tr.stop()
+    run(main())
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu),
+                                    pytest.param("hybrid", marks=pytest.mark.gpu)])
+def test_redelivered_job_gpu_resume_refetches_only_the_corrupt_piece(tmp_path, device):
+    """Production resume path on the MI355X: a redelivered magnet job whose
+    files are already on disk (no completion DB) is batch re-verified by the
+    HIP pipeline inside FileStorage.verify_existing (TorrentDownloader with
+    verify_device=gpu|hybrid); one piece was corrupted on disk, and exactly
+    that piece — nothing else — is fetched from the swarm again."""
+    from tritondl.ops import hashing
+
+    async def main():
+        src = tmp_path / "src" / "Pack"
+        make_payload(str(src), {"e1.mkv": 3_000_000, "e2.mkv": 2_500_000})
+        piece = 65536
+        info = torrent_for(str(src), piece)
+        seed = await Seeder(info, str(tmp_path / "src")).start()
+        dst = tmp_path / "job"
+        shutil.copytree(src, dst / "Pack")               # the first delivery's data, no .torrent.db
+        bad = (3_000_000 + 700_000) // piece
+        with open(dst / "Pack" / "e2.mkv", "r+b") as f:
+            f.seek(700_000)
+            f.write(b"\xde\xad\xbe\xef")
+        calls = []
+        real = hashing.verify_pieces
+
+        def spy(files, piece_len, expected, kind="sha1", device="cpu", threads=0):
+            calls.append(device)
+            return real(files, piece_len, expected, kind, device=device, threads=threads)
+        hashing.verify_pieces = spy
+        try:
+            cfg = TorrentConfig(listen_host="127.0.0.1", verify_device=device, request_timeout=3)
+            d = TorrentDownloader(cfg, progress_interval=0.05, use_dht=False)
+            t, _dht = await d.open(str(dst), magnet_for(info) + f"&x.pe=127.0.0.1:{seed.torrent.port}")
+            await asyncio.wait_for(t.got_info.wait(), 20)
+            await t.download_all()
+            assert calls == [device]
+            assert t.nhave == info.num_pieces - 1 and not t.have[bad]
+            await asyncio.wait_for(t.complete.wait(), 30)
+            assert t.downloaded == info.piece_size(bad)      # one piece, fetched once
+            await t.close()
+        finally:
+            hashing.verify_pieces = real
+        _check_tree(str(src), str(dst))
+        await seed.stop()
     run(main())

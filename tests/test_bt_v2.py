@@ -246,7 +246,7 @@ def test_gpu_leaf_path_logic_emulated_on_host(tmp_path, monkeypatch):
     exp, widths, reals, known = info.v2_expectations()
 
     class FakeGpu:
-        def digest_files(self, files, pl, kind):
+        def digest_files(self, files, pl, kind, cpu_threads=0):
             blob = b"".join(bytes(n) if not p else open(p, "rb").read() for p, n in files)
             return hashing._host.piece_hashes(kind, blob, pl, 2), b"\x01" * (-(-len(blob) // pl))
     monkeypatch.setattr(hashing, "gpu_hasher", lambda *a, **k: FakeGpu())

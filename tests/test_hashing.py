@@ -165,14 +165,42 @@ def test_gpu_many_small_windows(tmp_path, window_pieces):
 
 def test_choose_device_cost_model(monkeypatch):
     monkeypatch.setattr(hashing, "gpu_available", lambda: True)
-    # many small pieces: GPU (lane-parallel) wins against a per-GPU host share
-    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=16) == "gpu"
+    # many small pieces: GPU (lane-parallel) wins against a per-GPU host share, and the
+    # 8 CPUs left beside its readers add their SHA-NI rate (hybrid)
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=16) == "hybrid"
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=9) == "gpu"
     # few huge pieces: one lane per piece starves the GPU
     assert hashing.choose_device(64, 16 << 20, 64 * (16 << 20), cpu_threads=16) == "cpu"
     assert hashing.choose_device(0, 16384, 0) == "cpu"
     monkeypatch.setattr(hashing, "gpu_available", lambda: False)
     assert hashing.choose_device(65536, 16384, 65536 * 16384) == "cpu"
     assert hashing.effective_cpus() >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("piece_len,cpu_threads", [(16384, 1), (32768, 3), (65536, 8), (1 << 20, 4)])
+def test_hybrid_verify_matches_host(tmp_path, piece_len, cpu_threads):
+    """GPU pipeline from the front + SHA-NI threads from the back: identical
+    results to the host verifier, whatever the meeting point — including a
+    corrupt piece and a truncated file."""
+    files, blob, exp = _make_torrent_layout(tmp_path, [3_000_000, 5, 0, 4_100_000, 12_345, 2_000_000], piece_len)
+    h = hashing.gpu_hasher(batch_bytes=1 << 20, window_bytes=max(1, (2 << 20) // piece_len) * piece_len)
+    n = len(exp) // 20
+    assert h.verify_files(files, piece_len, exp, "sha1", cpu_threads=cpu_threads) == b"\x01" * n
+    assert 0 <= h.last_gpu_pieces <= n
+    with open(files[3][0], "r+b") as f:
+        f.seek(1_000_000)
+        f.write(b"\xff\x00\xee")
+    os.truncate(files[5][0], 1_000_000)
+    host = hashing.verify_pieces(files, piece_len, exp, device="cpu")
+    assert 0 < sum(host) < n
+    assert h.verify_files(files, piece_len, exp, "sha1", cpu_threads=cpu_threads) == host
+    assert hashing.verify_pieces(files, piece_len, exp, device="hybrid") == host
+    # v2 leaves through the hybrid digest path
+    d_gpu, ok_gpu = h.digest_files(files, 16384, "sha256", cpu_threads=cpu_threads)
+    d_ref, ok_ref = h.digest_files(files, 16384, "sha256")
+    assert ok_gpu == ok_ref and all(
+        d_gpu[32 * k:32 * k + 32] == d_ref[32 * k:32 * k + 32] for k in range(len(ok_ref)) if ok_ref[k])
 
 
 def _padded_layout(tmp_path, piece_len):

@@ -59,7 +59,7 @@ async def main() -> int:
         o = await Origin().start()
         url = o.add("/job.torrent", torrent_file_bytes(info))
         for dev in a.device:
-            if dev == "gpu" and not hashing.gpu_available():
+            if dev in ("gpu", "hybrid") and not hashing.gpu_available():
                 continue
             for rep in range(a.reps):
                 # the same files, but no completion DB: the job must re-verify everything

@@ -49,10 +49,11 @@ TARGETS = {
     },
     "_gpu_hash": {
         "srcs": ["csrc/hip/gpu_hash.hip"],
+        "deps": ["csrc/hash/hash_core.h"],
         "cc": "hipcc",
         "flags": ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-fvisibility=hidden",
                   "-pthread", "-Wno-unused-result"],
-        "libs": [],
+        "libs": ["-lcrypto"],
     },
     "_relay": {
         "srcs": ["csrc/relay/relay.cpp"],

@@ -6,7 +6,10 @@ tools/build_native.py``) — there is no silent pure-Python fallback.
 
 GPU module ``tritondl._gpu_hash`` (HIP, gfx950) is used for batched piece
 verification when a device is present (``device="auto"``) or demanded
-(``device="gpu"``: raises if unavailable).
+(``device="gpu"``: raises if unavailable).  ``device="hybrid"`` runs the GPU
+pipeline and the host's SHA-NI threads on the same layout at once, from
+opposite ends (the GPU path is bound by host->HBM staging, not the kernel,
+so the idle CPU cores add throughput instead of waiting).
 """
 
 from __future__ import annotations
@@ -102,11 +105,15 @@ def gpu_available() -> bool:
         return False
 
 
-def gpu_hasher(device: int = 0, batch_bytes: int = 256 << 20, reader_threads: int = 8, window_bytes: int = 0):
+def gpu_hasher(device: int = 0, batch_bytes: int = 0, reader_threads: int = 0, window_bytes: int = 0):
     """Cached per-device :class:`GpuHasher`.  ``batch_bytes`` is the pinned
-    staging chunk; ``window_bytes`` the HBM window hashed per kernel launch
-    (0 = auto: a third of free HBM, capped at 48 GiB)."""
-    key = (device, max(batch_bytes, 1 << 20), window_bytes)
+    staging chunk (0: ``TRITONDL_GPU_STAGE_MB`` or 256 MiB); ``reader_threads``
+    the pread threads filling it (0: ``TRITONDL_GPU_READERS`` or
+    :data:`GPU_READERS`); ``window_bytes`` the HBM window hashed per kernel
+    launch (0 = auto: a third of free HBM, capped at 48 GiB)."""
+    batch_bytes = batch_bytes or (int(os.environ.get("TRITONDL_GPU_STAGE_MB", "256")) << 20)
+    reader_threads = reader_threads or int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS)))
+    key = (device, max(batch_bytes, 1 << 20), window_bytes, reader_threads)
     with _gpu_lock:
         h = _gpu_hashers.get(key)
         if h is None:
@@ -125,14 +132,27 @@ def warm_gpu(device: int = 0) -> bool:
     return True
 
 
+DEVICES = ("auto", "cpu", "gpu", "hybrid")
+GPU_READERS = 8            # pread threads feeding the GPU's pinned staging (gpu_hasher default)
+
+
 def _resolve(device: str) -> str:
     if device == "auto":
         return "gpu" if gpu_available() else "cpu"
-    if device == "gpu" and not gpu_available():
-        raise RuntimeError("GPU hashing requested but no HIP device / _gpu_hash extension available")
-    if device not in ("cpu", "gpu"):
-        raise ValueError(f"device must be auto|cpu|gpu, got {device!r}")
+    if device not in DEVICES:
+        raise ValueError(f"device must be one of {'|'.join(DEVICES)}, got {device!r}")
+    if device in ("gpu", "hybrid") and not gpu_available():
+        raise RuntimeError(f"{device} hashing requested but no HIP device / _gpu_hash extension available")
     return device
+
+
+def hybrid_cpu_threads(cpus: int | None = None) -> int:
+    """SHA-NI threads that work next to the GPU pipeline's readers
+    (``TRITONDL_HYBRID_CPU_THREADS`` overrides)."""
+    env = os.environ.get("TRITONDL_HYBRID_CPU_THREADS")
+    if env:
+        return max(1, int(env))
+    return max(1, (cpus or effective_cpus()) - int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS))))
 
 
 # Cost model for device="auto" batch verification, calibrated on MI355X with
@@ -161,12 +181,23 @@ def effective_cpus() -> int:
 
 
 def choose_device(n_pieces: int, piece_len: int, total: int, cpu_threads: int | None = None) -> str:
+    """cpu | gpu | hybrid for a batch verify, by the cost model above.  In
+    hybrid mode the CPU threads left next to the GPU readers add their rate
+    to the GPU's (the native claim rule also hands the GPU's last-kernel
+    latency tail to the CPU, so hybrid is never slower than its GPU part)."""
     if n_pieces == 0 or not gpu_available():
         return "cpu"
-    thr = max(1, min(cpu_threads or effective_cpus(), n_pieces))
+    cpus = cpu_threads or effective_cpus()
+    thr = max(1, min(cpus, n_pieces))
     t_gpu = total / GPU_COPY_BPS + piece_len / GPU_LANE_BPS + GPU_SETUP_S
     t_cpu = (total / CPU_THREAD_BPS + n_pieces * CPU_PIECE_S) / thr
-    return "gpu" if t_gpu < t_cpu else "cpu"
+    hthr = hybrid_cpu_threads(cpus)
+    cpu_bps = hthr * CPU_THREAD_BPS / (1 + CPU_PIECE_S * CPU_THREAD_BPS / piece_len)
+    t_hyb = max(total / (GPU_COPY_BPS + cpu_bps), piece_len / GPU_LANE_BPS) + GPU_SETUP_S
+    best = min(t_cpu, t_gpu, t_hyb)
+    if best == t_cpu:
+        return "cpu"
+    return "hybrid" if best == t_hyb and cpus - GPU_READERS >= 2 else "gpu"
 
 
 def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", threads: int = 0) -> bytes:
@@ -185,6 +216,8 @@ def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: by
     files = [(str(p), int(n)) for p, n in files]
     if dev == "gpu":
         return gpu_hasher().verify_files(files, piece_len, expected, kind)
+    if dev == "hybrid":
+        return gpu_hasher().verify_files(files, piece_len, expected, kind, cpu_threads=threads or hybrid_cpu_threads())
     return _host.verify_pieces(files, piece_len, expected, threads or effective_cpus(), kind)
 
 
@@ -201,8 +234,9 @@ def verify_pieces_v2(files: Sequence[tuple[str, int]], piece_len: int, expected:
     n = len(widths)
     kn = bytes(1 if k else 0 for k in (known if known is not None else [True] * n))
     thr = threads or effective_cpus()
-    if dev == "gpu":
-        leaves, leaf_ok = gpu_hasher().digest_files(files, 16384, "sha256")
+    if dev in ("gpu", "hybrid"):
+        leaves, leaf_ok = gpu_hasher().digest_files(files, 16384, "sha256",
+                                                    cpu_threads=hybrid_cpu_threads() if dev == "hybrid" else 0)
         leaves, leaf_ok = bytearray(leaves), bytearray(leaf_ok)
         # the kernel hashed whole 16 KiB blocks of the padded stream; a file's
         # short last leaf must hash only its real bytes: redo those (<= one per file)

@@ -69,7 +69,7 @@ class Config:
     bt_pex: bool = True
     bt_encryption: str = "allow"                # MSE/PE: disable | allow | prefer | require
     bt_bootstrap: str = "router.bittorrent.com:6881,dht.transmissionbt.com:6881"
-    gpu_verify: str = "auto"                    # auto|on|off (HIP batch piece hashing)
+    gpu_verify: str = "auto"                    # auto|on|off|hybrid (HIP batch piece hashing; hybrid = GPU + SHA-NI threads)
     gpu_warmup_timeout_s: float = 120.0         # start-up wait for the HIP hasher before consuming
 
     # --- upload (downloader.go:95, uploader.go) ---
@@ -195,7 +195,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     p.add_argument("--publish-topic", dest="publish_topic", default=None)
     p.add_argument("--metrics-addr", dest="metrics_addr", default=None)
     p.add_argument("--cleanup", dest="cleanup", action="store_true", default=None)
-    p.add_argument("--gpu-verify", dest="gpu_verify", choices=["auto", "on", "off"], default=None)
+    p.add_argument("--gpu-verify", dest="gpu_verify", choices=["auto", "on", "off", "hybrid"], default=None)
     return p
 
 
