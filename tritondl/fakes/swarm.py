@@ -110,24 +110,52 @@ class UDPTracker(asyncio.DatagramProtocol):
 
 
 class DHTNetwork:
-    def __init__(self, n: int = 4) -> None:
+    """``n`` in-process DHT nodes on loopback that all join through node 0
+    (the one bootstrap address), like a tiny mainline DHT.  ``ipv6`` makes
+    every node dual-stack (BEP 32) with node 0 reachable on ``::1`` too.
+    Joins run ``join_batch`` at a time; a second pass refreshes every node's
+    own neighbourhood so early joiners also learn about late ones."""
+
+    def __init__(self, n: int = 4, *, ipv6: bool = False, timeout: float = 2.0, join_batch: int = 16) -> None:
         self.n = n
+        self.ipv6 = ipv6
+        self.timeout = timeout
+        self.join_batch = join_batch
         self.nodes: list[DHTNode] = []
 
+    def _node(self, boot) -> DHTNode:
+        return DHTNode(host="127.0.0.1", bootstrap=boot, timeout=self.timeout,
+                       host6="::1" if self.ipv6 else None)
+
     async def start(self) -> "DHTNetwork":
-        first = await DHTNode(host="127.0.0.1").start()
+        first = await self._node(None).start()
         self.nodes = [first]
         for _ in range(self.n - 1):
-            nd = await DHTNode(host="127.0.0.1", bootstrap=[first.addr]).start()
-            self.nodes.append(nd)
-        for nd in self.nodes[1:]:
-            await nd.bootstrap()
-        await first.bootstrap()
+            self.nodes.append(await self._node(self.bootstrap).start())
+        rest = self.nodes[1:]
+        for i in range(0, len(rest), self.join_batch):
+            await asyncio.gather(*(nd.bootstrap() for nd in rest[i:i + self.join_batch]))
+        for i in range(0, len(self.nodes), self.join_batch):
+            await asyncio.gather(*(nd.bootstrap() for nd in self.nodes[i:i + self.join_batch]))
         return self
 
     @property
     def bootstrap(self) -> list[tuple[str, int]]:
-        return [self.nodes[0].addr]
+        out = [self.nodes[0].addr]
+        a6 = self.nodes[0].addr6
+        if a6 is not None:
+            out.append(a6)
+        return out
+
+    def kill(self, fraction: float, rng=None) -> list[DHTNode]:
+        """Stop a random ``fraction`` of the nodes (never the bootstrap node):
+        they vanish without a goodbye, as dead DHT peers do."""
+        import random
+        rng = rng or random.Random(0)
+        victims = rng.sample(self.nodes[1:], int(fraction * (len(self.nodes) - 1)))
+        for nd in victims:
+            nd.stop()
+        return victims
 
     def stop(self) -> None:
         for nd in self.nodes:

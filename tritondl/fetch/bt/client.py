@@ -40,6 +40,8 @@ def _parse_hostports(s: str) -> list[tuple[str, int]]:
         if not part:
             continue
         h, _, p = part.rpartition(":")
+        if h.startswith("[") and h.endswith("]"):
+            h = h[1:-1]                  # [v6 address]:port
         if h and p.isdigit():
             out.append((h, int(p)))
     return out
@@ -51,12 +53,15 @@ class TorrentDownloader:
     def __init__(self, cfg: TorrentConfig | None = None, *, metadata_timeout: float = 600.0,
                  progress_interval: float = 1.0, use_dht: bool = True,
                  dht_bootstrap: list[tuple[str, int]] | None = None, extra_trackers: list[str] | None = None,
-                 http_session: aiohttp.ClientSession | None = None) -> None:
+                 http_session: aiohttp.ClientSession | None = None, dht_ipv6: bool = False,
+                 dht_timeout: float = 2.0) -> None:
         self.cfg = cfg or TorrentConfig()
         self.metadata_timeout = metadata_timeout
         self.progress_interval = progress_interval
         self.use_dht = use_dht
         self.dht_bootstrap = dht_bootstrap or []
+        self.dht_ipv6 = dht_ipv6          # BEP 32: a second DHT socket + table on IPv6
+        self.dht_timeout = dht_timeout
         self.extra_trackers = extra_trackers or []
         self._http = http_session
 
@@ -65,7 +70,7 @@ class TorrentDownloader:
         tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, pex=c.bt_pex, encryption=c.bt_encryption,
                            verify_device={"on": "gpu", "off": "cpu"}.get(c.gpu_verify, c.gpu_verify))
         return cls(tc, metadata_timeout=c.metadata_timeout_s, progress_interval=c.progress_interval_s,
-                   use_dht=c.bt_dht, dht_bootstrap=_parse_hostports(c.bt_bootstrap))
+                   use_dht=c.bt_dht, dht_bootstrap=_parse_hostports(c.bt_bootstrap), dht_ipv6=c.bt_dht_ipv6)
 
     def register(self) -> ClientRegister:
         return ClientRegister(name="torrent", protocols=["magnet"], file_extensions=[".torrent"])
@@ -119,7 +124,9 @@ class TorrentDownloader:
             raise TorrentError(f"unsupported scheme '{u.scheme}'")
         dht = None
         if self.use_dht:
-            dht = await DHTNode(bootstrap=self.dht_bootstrap).start()
+            bind = "127.0.0.1" if self.cfg.listen_host == "127.0.0.1" else "0.0.0.0"
+            dht = await DHTNode(host=bind, bootstrap=self.dht_bootstrap, timeout=self.dht_timeout,
+                                host6=("::1" if bind == "127.0.0.1" else "::") if self.dht_ipv6 else None).start()
             asyncio.ensure_future(dht.bootstrap())
         t = Torrent(ih, base_dir, self.cfg, info=info, trackers=trackers, peers=peers, dht=dht, name_hint=name,
                     webseeds=webseeds)
