@@ -42,12 +42,17 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 namespace py = pybind11;
@@ -313,7 +318,76 @@ struct Span {
 };
 constexpr int kZeroSpan = -2;
 
-// Host pipeline: disk / host memory -> pinned staging (2 slots) -> HBM
+// Counts down the units of one staging fill; the first reader exception wins.
+struct Latch {
+  explicit Latch(size_t n) : left(n) {}
+  void done(std::exception_ptr e) {
+    std::lock_guard<std::mutex> g(m);
+    if (e && !err) err = e;
+    if (--left == 0) cv.notify_all();
+  }
+  void wait_quiet() {
+    std::unique_lock<std::mutex> g(m);
+    cv.wait(g, [&] { return left == 0; });
+  }
+  void wait() {
+    wait_quiet();
+    if (err) std::rethrow_exception(err);
+  }
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left;
+  std::exception_ptr err;
+};
+
+// Persistent pread/memcpy threads.  Fills of several staging slots are queued
+// back to back, so readers move straight on to slot k+1 while the DMA engine
+// drains slot k (the previous design spawned threads per slot and had every
+// reader wait at a per-slot barrier).
+class ReaderPool {
+ public:
+  explicit ReaderPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~ReaderPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+};
+
+// Host pipeline: disk / host memory -> pinned staging (a ring of kStages
+// slots filled by the reader pool, up to kStages-1 ahead of the DMA) -> HBM
 // window -> ONE kernel over every piece of the window -> digests.
 //
 // Why windows: the kernel's parallel axis is the piece (one lane each), so a
@@ -328,7 +402,8 @@ class GpuHasher {
       : device_(device),
         stage_req_(std::max<size_t>(stage_bytes, 1 << 20)),
         readers_(std::max(1, reader_threads)),
-        window_req_(window_bytes) {
+        window_req_(window_bytes),
+        pool_(new ReaderPool(std::max(1, reader_threads))) {
     HIP_CHECK(hipSetDevice(device_));
     HIP_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&compute_stream_, hipStreamNonBlocking));
@@ -339,6 +414,7 @@ class GpuHasher {
     }
   }
   ~GpuHasher() {
+    pool_.reset();
     hipSetDevice(device_);
     hipStreamSynchronize(copy_stream_);
     hipStreamSynchronize(compute_stream_);
@@ -385,7 +461,7 @@ class GpuHasher {
     {
       py::gil_scoped_release nogil;
       run_gpu_only(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, char*) {
-        copy_parallel(dst, src + off, len);
+        std::memcpy(dst, src + off, len);
       }, [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>&) {
         std::memcpy(&out[first * dl], digests, count * dl);
       });
@@ -426,9 +502,7 @@ class GpuHasher {
         hybrid_digest(alg, spans, piece_len, total, n, cpu_threads, digests, complete);
       } else {
         run_gpu_only(alg, piece_len, total, n,
-                     [&](uint8_t* dst, size_t off, size_t len, char* comp) {
-                       read_spans(spans, dst, off, len, piece_len, comp);
-                     },
+                     [&](uint8_t* dst, size_t off, size_t len, char* comp) { read_unit(spans, dst, off, len, piece_len, comp); },
                      [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
                        std::memcpy(&digests[first * dl], d, count * dl);
                        for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
@@ -494,7 +568,7 @@ class GpuHasher {
   }
 
  private:
-  static constexpr int kStages = 2;
+  static constexpr int kStages = 4;
   struct Stage {
     uint8_t* h = nullptr;
     size_t cap = 0;
@@ -541,23 +615,6 @@ class GpuHasher {
     }
   }
 
-  void copy_parallel(uint8_t* dst, const uint8_t* src, size_t len) {
-    const size_t kMin = 8 << 20;
-    int t = static_cast<int>(std::min<size_t>(readers_, std::max<size_t>(1, len / kMin)));
-    if (t <= 1) {
-      std::memcpy(dst, src, len);
-      return;
-    }
-    std::vector<std::thread> ts;
-    size_t chunk = (len + t - 1) / t;
-    for (int k = 0; k < t; ++k) {
-      size_t a = k * chunk, e = std::min(len, a + chunk);
-      if (a >= e) break;
-      ts.emplace_back([=] { std::memcpy(dst + a, src + a, e - a); });
-    }
-    for (auto& th : ts) th.join();
-  }
-
   // Read stream bytes [ga, ge) of the layout into p (single thread); marks
   // complete[k] = 0 for every piece k (relative to the piece at stream offset
   // `base`) that could not be fully read.
@@ -592,45 +649,85 @@ class GpuHasher {
     fail_range(cur, ge);  // a gap nobody covers: incomplete
   }
 
-  // Read [off, off+len) (piece-aligned) of the concatenated layout into dst;
-  // complete[k] is cleared for every piece k of this range not fully read.
-  // Work is split into units of >= 1 MiB (whole pieces), so 16 KiB "pieces"
-  // (v2 merkle leaves) still read with large preads.
-  void read_spans(const std::vector<Span>& spans, uint8_t* dst, size_t off, size_t len, size_t piece_len,
-                  char* complete) {
-    const size_t np = (len + piece_len - 1) / piece_len;
-    const size_t per_unit = std::max<size_t>(1, (1u << 20) / piece_len);
-    const size_t nu = (np + per_unit - 1) / per_unit;
-    std::atomic<size_t> next{0};
-    auto work = [&] {
-      for (size_t u; (u = next.fetch_add(1)) < nu;) {  // units own disjoint pieces: no race on complete
-        const size_t a = u * per_unit * piece_len, e = std::min(len, a + per_unit * piece_len);
-        read_range(spans, dst + a, static_cast<long long>(off + a), static_cast<long long>(off + e),
-                   static_cast<long long>(off), piece_len, np, complete);
-      }
-    };
-    std::vector<std::thread> ts;
-    const int t = static_cast<int>(std::min<size_t>(readers_, nu));
-    for (int k = 1; k < t; ++k) ts.emplace_back(work);
-    work();
-    for (auto& th : ts) th.join();
+  // One reader unit: stream bytes [off, off+len) (piece-aligned start) into dst.
+  static void read_unit(const std::vector<Span>& spans, uint8_t* dst, size_t off, size_t len, size_t piece_len,
+                        char* complete) {
+    read_range(spans, dst, static_cast<long long>(off), static_cast<long long>(off + len),
+               static_cast<long long>(off), piece_len, (len + piece_len - 1) / piece_len, complete);
+  }
+
+  // GPU-side timeline of the last call (trace on): H2D copies, kernels, D2H.
+  struct TraceRec {
+    const char* kind;
+    hipEvent_t a, b;
+    size_t bytes;
+  };
+  void trace_begin(hipStream_t s, const char* kind, size_t bytes) {
+    if (!trace_) return;
+    TraceRec r{kind, nullptr, nullptr, bytes};
+    HIP_CHECK(hipEventCreate(&r.a));
+    HIP_CHECK(hipEventCreate(&r.b));
+    HIP_CHECK(hipEventRecord(r.a, s));
+    trace_recs_.push_back(r);
+  }
+  void trace_end(hipStream_t s) {
+    if (trace_) HIP_CHECK(hipEventRecord(trace_recs_.back().b, s));
+  }
+  void trace_collect() {
+    timeline_.clear();
+    if (trace_recs_.empty()) return;
+    hipEvent_t t0 = trace_recs_.front().a;
+    for (auto& r : trace_recs_) {
+      float a = 0.f, b = 0.f;
+      hipEventElapsedTime(&a, t0, r.a);
+      hipEventElapsedTime(&b, t0, r.b);
+      timeline_.emplace_back(std::string(r.kind), a, b, r.bytes);
+    }
+    for (auto& r : trace_recs_) {
+      hipEventDestroy(r.a);
+      hipEventDestroy(r.b);
+    }
+    trace_recs_.clear();
   }
 
   // Pipeline driver.  claim(max) hands out the next contiguous run of pieces
   // [first, first+count) from the front of the layout (count 0 = no more);
   // runs are packed into an HBM window until it is full or claims dry up,
   // then one kernel hashes the window while the next one is being filled.
-  template <class Claim, class Fill, class Harvest>
-  void run_windows(int alg, size_t piece_len, size_t total, size_t n, size_t wbytes, Claim&& claim, Fill&& fill,
+  // Each claimed run goes to the next staging slot, is split into >= 1 MiB
+  // reader units for the pool, and is DMA'd to HBM as soon as its units are
+  // done — up to kStages-1 slots are being filled while one is in flight.
+  template <class Claim, class Unit, class Harvest>
+  void run_windows(int alg, size_t piece_len, size_t total, size_t n, size_t wbytes, Claim&& claim, Unit&& unit,
                    Harvest&& harvest) {
     HIP_CHECK(hipSetDevice(device_));
+    trace_recs_.clear();
+    timeline_.clear();
     if (n == 0) return;
     const int dl = digest_len(alg);
     last_window_ = wbytes;
-    const size_t per = std::min(n, wbytes / piece_len);                            // pieces per window
-    const size_t stage_p = std::max<size_t>(1, stage_req_ / piece_len);            // pieces per staging chunk
+    const size_t per = std::min(n, std::max<size_t>(1, wbytes / piece_len));      // pieces per window
+    const size_t stage_p = std::max<size_t>(1, stage_req_ / piece_len);            // pieces per staging slot
     const size_t stage = stage_p * piece_len;
     for (auto& st : stage_) ensure_stage(st, std::min(stage, per * piece_len));
+    const size_t unit_p = std::max<size_t>(1, (1u << 20) / piece_len);             // >= 1 MiB preads
+    struct Fill {
+      int slot;
+      size_t dst, len;
+      std::shared_ptr<Latch> latch;
+    };
+    std::deque<Fill> fills;
+    auto push_h2d = [&](Window& w) {  // oldest filled slot -> HBM
+      Fill f = fills.front();
+      fills.pop_front();
+      f.latch->wait();
+      Stage& st = stage_[f.slot];
+      trace_begin(copy_stream_, "h2d", f.len);
+      HIP_CHECK(hipMemcpyAsync(w.d + f.dst, st.h, f.len, hipMemcpyHostToDevice, copy_stream_));
+      trace_end(copy_stream_);
+      HIP_CHECK(hipEventRecord(st.free_ev, copy_stream_));
+      st.used = true;
+    };
     auto drain = [&](Window& w) {
       if (!w.pending) return;
       HIP_CHECK(hipEventSynchronize(w.done));
@@ -638,43 +735,81 @@ class GpuHasher {
       w.pending = false;
     };
     size_t widx = 0, sidx = 0;
-    for (bool more = true; more; ++widx) {
-      Window& w = win_[widx % 2];
-      drain(w);  // its previous window (widx-2) must be hashed before we overwrite it
-      ensure_window(w, per * piece_len, per * dl);
-      w.complete.assign(per, 1);
-      size_t count = 0, first = 0;
-      while (count < per) {
-        const auto got = claim(std::min(stage_p, per - count));
-        if (got.second == 0) {
-          more = false;
-          break;
+    try {
+      for (bool more = true; more; ++widx) {
+        Window& w = win_[widx % 2];
+        drain(w);  // its previous window (widx-2) must be hashed before we overwrite it
+        ensure_window(w, per * piece_len, per * dl);
+        w.complete.assign(per, 1);
+        size_t count = 0, first = 0;
+        while (count < per) {
+          const auto got = claim(std::min(stage_p, per - count));
+          if (got.second == 0) {
+            more = false;
+            break;
+          }
+          if (count == 0) first = got.first;
+          if (got.first != first + count) throw std::logic_error("non-contiguous GPU claim");
+          if (fills.size() == static_cast<size_t>(kStages)) push_h2d(w);
+          const int slot = static_cast<int>(sidx++ % kStages);
+          Stage& st = stage_[slot];
+          if (st.used) {
+            HIP_CHECK(hipEventSynchronize(st.free_ev));  // its previous H2D has landed
+            st.used = false;
+          }
+          const size_t off = got.first * piece_len;
+          const size_t len = std::min(total - off, got.second * piece_len);
+          const size_t nu = (got.second + unit_p - 1) / unit_p;
+          auto latch = std::make_shared<Latch>(nu);
+          uint8_t* h = st.h;
+          char* comp = w.complete.data() + count;
+          for (size_t u = 0; u < nu; ++u) {
+            const size_t a = u * unit_p * piece_len, e = std::min(len, a + unit_p * piece_len);
+            pool_->submit([&unit, latch, h, comp, off, a, e, u, unit_p] {
+              try {
+                unit(h + a, off + a, e - a, comp + u * unit_p);
+                latch->done(nullptr);
+              } catch (...) {
+                latch->done(std::current_exception());
+              }
+            });
+          }
+          fills.push_back({slot, count * piece_len, len, latch});
+          count += got.second;
         }
-        if (count == 0) first = got.first;
-        if (got.first != first + count) throw std::logic_error("non-contiguous GPU claim");
-        Stage& st = stage_[sidx++ % kStages];
-        if (st.used) HIP_CHECK(hipEventSynchronize(st.free_ev));  // its previous H2D has landed
-        const size_t off = got.first * piece_len;
-        const size_t len = std::min(total - off, got.second * piece_len);
-        fill(st.h, off, len, w.complete.data() + count);
-        HIP_CHECK(hipMemcpyAsync(w.d + count * piece_len, st.h, len, hipMemcpyHostToDevice, copy_stream_));
-        HIP_CHECK(hipEventRecord(st.free_ev, copy_stream_));
-        st.used = true;
-        count += got.second;
+        while (!fills.empty()) push_h2d(w);
+        if (count == 0) break;
+        const size_t wlen = std::min(total - first * piece_len, count * piece_len);
+        HIP_CHECK(hipEventRecord(w.copied, copy_stream_));
+        HIP_CHECK(hipStreamWaitEvent(compute_stream_, w.copied, 0));
+        trace_begin(compute_stream_, "kernel", wlen);
+        launch_hash(alg, w.d, wlen, piece_len, static_cast<uint32_t>(count), w.d_out, compute_stream_);
+        trace_end(compute_stream_);
+        trace_begin(compute_stream_, "d2h", count * dl);
+        HIP_CHECK(hipMemcpyAsync(w.h_out, w.d_out, count * dl, hipMemcpyDeviceToHost, compute_stream_));
+        trace_end(compute_stream_);
+        HIP_CHECK(hipEventRecord(w.done, compute_stream_));
+        w.first = first;
+        w.count = count;
+        w.pending = true;
       }
-      if (count == 0) break;
-      const size_t wlen = std::min(total - first * piece_len, count * piece_len);
-      HIP_CHECK(hipEventRecord(w.copied, copy_stream_));
-      HIP_CHECK(hipStreamWaitEvent(compute_stream_, w.copied, 0));
-      launch_hash(alg, w.d, wlen, piece_len, static_cast<uint32_t>(count), w.d_out, compute_stream_);
-      HIP_CHECK(hipMemcpyAsync(w.h_out, w.d_out, count * dl, hipMemcpyDeviceToHost, compute_stream_));
-      HIP_CHECK(hipEventRecord(w.done, compute_stream_));
-      w.first = first;
-      w.count = count;
-      w.pending = true;
+      drain(win_[widx % 2]);
+      drain(win_[(widx + 1) % 2]);
+    } catch (...) {
+      // queued reader units reference this frame: let every one finish first
+      for (auto& f : fills) f.latch->wait_quiet();
+      hipStreamSynchronize(copy_stream_);
+      hipStreamSynchronize(compute_stream_);
+      for (auto& st : stage_) st.used = false;
+      for (auto& w : win_) w.pending = false;
+      for (auto& r : trace_recs_) {
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+      }
+      trace_recs_.clear();
+      throw;
     }
-    drain(win_[widx % 2]);
-    drain(win_[(widx + 1) % 2]);
+    trace_collect();
   }
 
   // The whole layout front-to-back on the GPU (no CPU share).
@@ -771,7 +906,7 @@ class GpuHasher {
                     gpu_pieces += c;
                     return std::make_pair(f, c);
                   },
-                  [&](uint8_t* dst, size_t off, size_t len, char* comp) { read_spans(spans, dst, off, len, piece_len, comp); },
+                  [&](uint8_t* dst, size_t off, size_t len, char* comp) { read_unit(spans, dst, off, len, piece_len, comp); },
                   [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
                     std::memcpy(&digests[first * dl], d, count * dl);
                     for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
@@ -790,6 +925,9 @@ class GpuHasher {
   }
 
   size_t last_gpu_pieces() const { return last_gpu_pieces_; }
+  bool trace() const { return trace_; }
+  void set_trace(bool on) { trace_ = on; }
+  std::vector<std::tuple<std::string, float, float, size_t>> last_timeline() const { return timeline_; }
 
  private:
   size_t last_gpu_pieces_ = 0;
@@ -801,6 +939,10 @@ class GpuHasher {
   hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
   Stage stage_[kStages];
   Window win_[2];
+  std::unique_ptr<ReaderPool> pool_;
+  bool trace_ = false;
+  std::vector<TraceRec> trace_recs_;
+  std::vector<std::tuple<std::string, float, float, size_t>> timeline_;
 };
 
 int device_count() {
@@ -840,6 +982,10 @@ PYBIND11_MODULE(_gpu_hash, m) {
            "one byte (0/1) per piece; cpu_threads > 0: hybrid (SHA-NI threads take pieces from the back)")
       .def("digest_files", &GpuHasher::digest_files, py::arg("files"), py::arg("piece_len"), py::arg("kind") = "sha256",
            py::arg("cpu_threads") = 0, "(digests, fully_read_mask) of every piece of a file layout")
+      .def_property("trace", &GpuHasher::trace, &GpuHasher::set_trace,
+                    "record a GPU event timeline (H2D / kernel / D2H) of each call")
+      .def_property_readonly("last_timeline", &GpuHasher::last_timeline,
+                             "[(kind, start_ms, end_ms, bytes)] of the last call, relative to its first op")
       .def_property_readonly("last_gpu_pieces", &GpuHasher::last_gpu_pieces,
                              "pieces the GPU hashed in the last verify/digest call (the rest: CPU threads)")
       .def("release", &GpuHasher::release)

@@ -203,6 +203,34 @@ def test_hybrid_verify_matches_host(tmp_path, piece_len, cpu_threads):
         d_gpu[32 * k:32 * k + 32] == d_ref[32 * k:32 * k + 32] for k in range(len(ok_ref)) if ok_ref[k])
 
 
+@pytest.mark.gpu
+def test_gpu_pipeline_timeline_trace(tmp_path):
+    """The event timeline of a traced call accounts for every staged byte and
+    every window's kernel."""
+    piece_len = 16384
+    files, blob, exp = _make_torrent_layout(tmp_path, [9_000_000, 7_000_001], piece_len)
+    h = hashing.gpu_hasher(batch_bytes=1 << 20, window_bytes=4 << 20)
+    h.trace = True
+    try:
+        assert h.verify_files(files, piece_len, exp, "sha1") == b"\x01" * (len(exp) // 20)
+        tl = h.last_timeline
+    finally:
+        h.trace = False
+    assert sum(n for k, _a, _b, n in tl if k == "h2d") == len(blob)
+    kernels = [x for x in tl if x[0] == "kernel"]
+    assert len(kernels) == -(-len(blob) // (4 << 20))
+    assert all(0 <= a <= b for _k, a, b, _n in tl)
+    summ = hashing.timeline_summary(tl)
+    assert summ["h2d_count"] >= 16 and summ["kernels"] == len(kernels)
+
+
+def test_timeline_summary_math():
+    tl = [("h2d", 0.0, 1.0, 1000), ("h2d", 1.0, 2.0, 1000), ("kernel", 1.5, 3.0, 0), ("d2h", 3.0, 3.1, 20)]
+    s = hashing.timeline_summary(tl)
+    assert s["h2d_ms"] == 2.0 and s["kernel_ms"] == 1.5 and s["kernel_under_h2d_ms"] == 0.5
+    assert s["span_ms"] == 3.1 and s["h2d_GBps_busy"] == round(2000 / 2.0 / 1e6, 1)
+
+
 def _padded_layout(tmp_path, piece_len):
     """Files separated by BEP 47 padding spans (path "" = zeros, not on disk)."""
     a, b = os.urandom(40_000), os.urandom(70_001)

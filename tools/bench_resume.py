@@ -72,10 +72,19 @@ async def main() -> int:
                 t0 = time.perf_counter()
                 await d.download(os.path.join(td, "job"), lambda u, p: None, url)
                 dt = time.perf_counter() - t0
+                extra = {}
+                if dev in ("gpu", "hybrid", "auto") and hashing.gpu_available():
+                    h = hashing.gpu_hasher()
+                    if dev != "gpu":
+                        extra["gpu_share"] = round(h.last_gpu_pieces / max(1, info.num_pieces if info.pieces
+                                                                            else -(-info.total_length // 16384)), 3)
+                    if h.trace:
+                        extra["gpu_timeline"] = hashing.timeline_summary(h.last_timeline)
                 print(json.dumps({"metric": "resume_job_seconds", "device": dev, "run": "cold" if rep == 0 else "warm",
                                   "value": round(dt, 3), "GBps": round(info.total_length / dt / 1e9, 1),
                                   "bytes": info.total_length, "pieces": info.num_pieces,
-                                  "torrent_version": a.version, "make_torrent_s": round(t_make, 2)}), flush=True)
+                                  "torrent_version": a.version, "make_torrent_s": round(t_make, 2), **extra}),
+                      flush=True)
     finally:
         if o is not None:
             await o.stop()

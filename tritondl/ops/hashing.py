@@ -107,17 +107,18 @@ def gpu_available() -> bool:
 
 def gpu_hasher(device: int = 0, batch_bytes: int = 0, reader_threads: int = 0, window_bytes: int = 0):
     """Cached per-device :class:`GpuHasher`.  ``batch_bytes`` is the pinned
-    staging chunk (0: ``TRITONDL_GPU_STAGE_MB`` or 256 MiB); ``reader_threads``
+    staging slot, one of a ring of 4 (0: ``TRITONDL_GPU_STAGE_MB`` or 128 MiB); ``reader_threads``
     the pread threads filling it (0: ``TRITONDL_GPU_READERS`` or
     :data:`GPU_READERS`); ``window_bytes`` the HBM window hashed per kernel
     launch (0 = auto: a third of free HBM, capped at 48 GiB)."""
-    batch_bytes = batch_bytes or (int(os.environ.get("TRITONDL_GPU_STAGE_MB", "256")) << 20)
+    batch_bytes = batch_bytes or (int(os.environ.get("TRITONDL_GPU_STAGE_MB", "128")) << 20)
     reader_threads = reader_threads or int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS)))
     key = (device, max(batch_bytes, 1 << 20), window_bytes, reader_threads)
     with _gpu_lock:
         h = _gpu_hashers.get(key)
         if h is None:
             h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads, window_bytes)
+            h.trace = os.environ.get("TRITONDL_GPU_TRACE", "") == "1"
             _gpu_hashers[key] = h
         return h
 
@@ -134,6 +135,41 @@ def warm_gpu(device: int = 0) -> bool:
 
 DEVICES = ("auto", "cpu", "gpu", "hybrid")
 GPU_READERS = 8            # pread threads feeding the GPU's pinned staging (gpu_hasher default)
+
+
+def timeline_summary(tl) -> dict:
+    """Overlap of a :attr:`GpuHasher.last_timeline` (``trace`` on): busy time of
+    H2D copies and of kernels (interval unions), how much of the kernel time
+    ran under copies, and the copy engine's rate while busy."""
+    def union(iv):
+        out: list[list[float]] = []
+        for a, b in sorted(iv):
+            if out and a <= out[-1][1]:
+                out[-1][1] = max(out[-1][1], b)
+            else:
+                out.append([a, b])
+        return out
+
+    def inter(x, y):
+        i = j = 0
+        tot = 0.0
+        while i < len(x) and j < len(y):
+            a, b = max(x[i][0], y[j][0]), min(x[i][1], y[j][1])
+            tot += max(0.0, b - a)
+            if x[i][1] < y[j][1]:
+                i += 1
+            else:
+                j += 1
+        return tot
+    h2d = union([(a, b) for k, a, b, _n in tl if k == "h2d"])
+    ker = union([(a, b) for k, a, b, _n in tl if k == "kernel"])
+    nbytes = sum(n for k, _a, _b, n in tl if k == "h2d")
+    busy = sum(b - a for a, b in h2d)
+    span = max((b for _k, _a, b, _n in tl), default=0.0)
+    return {"h2d_ms": round(busy, 3), "h2d_count": sum(1 for x in tl if x[0] == "h2d"),
+            "kernel_ms": round(sum(b - a for a, b in ker), 3), "kernels": sum(1 for x in tl if x[0] == "kernel"),
+            "kernel_under_h2d_ms": round(inter(ker, h2d), 3), "span_ms": round(span, 3),
+            "h2d_GBps_busy": round(nbytes / busy / 1e6, 1) if busy else None}
 
 
 def _resolve(device: str) -> str:
