@@ -42,6 +42,8 @@ async def main() -> int:
     ap.add_argument("--files", type=int, default=8, help="--job: media files in the pack")
     ap.add_argument("--stream", default="both", choices=["on", "off", "both"])
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--s3-gbps", type=float, default=0.0,
+                    help="--job: cap the fake S3's ingest link (Gbit/s; 0 = loopback speed)")
     a = ap.parse_args()
     if a.job:
         return await job_bench(a)
@@ -124,7 +126,8 @@ async def job_bench(a) -> int:
         seeds = [await Backend("seed", ["--path", pack, "--piece-kb", str(a.piece_kb),
                                         "--encryption", a.encryption]).start() for _ in range(a.seeds)]
         broker = await Backend("broker").start()
-        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK,
+                                  "--rate-mbps", str(a.s3_gbps * 1000)]).start()
         backs = seeds + [broker, s3]
         magnet = seeds[0].info["url"] + "&" + "&".join(f"x.pe={s.info['endpoint']}" for s in seeds)
         cfg = Config()
@@ -155,6 +158,7 @@ async def job_bench(a) -> int:
                 r = svc.results[-1]
                 assert r.ok and r.files == a.files and r.bytes == per * a.files, r
                 print(json.dumps({"metric": "bt_job_seconds", "value": round(dt, 3), "stream_upload": on,
+                                  "s3_link_gbps": a.s3_gbps or None,
                                   "mb": a.mb, "files": a.files, "seeds": a.seeds, "piece_kb": a.piece_kb,
                                   "job_MB_per_sec": round(a.mb * 1.048576 / dt, 1),
                                   "spans_ms": {k: round(v * 1000, 1) for k, v in r.marks.items()}}), flush=True)

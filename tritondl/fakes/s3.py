@@ -75,6 +75,8 @@ class FakeS3:
         self.strict_parts = strict_parts
         self.bucket_regions: dict[str, str] = {}
         self._outage_until = 0.0
+        self.rate: float | None = None          # bytes/s of a shared ingest link (None: unlimited)
+        self._link_free = 0.0
         self.access_key, self.secret_key = access_key, secret_key
         self.region = region
         self.store = store
@@ -178,7 +180,18 @@ class FakeS3:
     async def _read_body(self, request: web.Request, auth, keep: bool = True):
         """Verified request body.  ``keep=False`` (object data in discard
         mode): aws-chunked bodies are verified without materialising the
-        decoded bytes and only their length is returned (as ``_Sized``)."""
+        decoded bytes and only their length is returned (as ``_Sized``).
+        With ``rate`` set, the reply waits until a shared link of that many
+        bytes/s would have carried the body (all requests queue on it)."""
+        n = request.body_length or 0                 # remaining bytes: read it before the body is consumed
+        body = await self._read_body_raw(request, auth, keep)
+        if self.rate:
+            now = time.monotonic()
+            self._link_free = max(now, self._link_free) + n / self.rate
+            await asyncio.sleep(self._link_free - now)
+        return body
+
+    async def _read_body_raw(self, request: web.Request, auth, keep: bool = True):
         phash = request.headers.get("x-amz-content-sha256", sigv4.UNSIGNED_PAYLOAD)
         relay = rawhttp.relay_module() if self.native else None
         if phash == sigv4.STREAMING_PAYLOAD:

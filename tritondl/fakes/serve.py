@@ -49,7 +49,7 @@ class SyntheticOrigin(Origin):
 
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
                  seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow",
-                 tls_cert: str | None = None, tls_key: str | None = None) -> None:
+                 tls_cert: str | None = None, tls_key: str | None = None, rate_mbps: float = 0.0) -> None:
     tls = None
     if tls_cert and tls_key:
         with open(tls_cert) as f1, open(tls_key) as f2:
@@ -84,6 +84,8 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
                 "url": f"{'https' if tls else 'http'}://{srv.host}:{srv.port}"}
     elif kind == "s3":
         srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk, tls=tls).start()
+        if rate_mbps:
+            srv.rate = rate_mbps * 1e6 / 8
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.endpoint}
     else:
         raise SystemExit(f"unknown kind {kind}")
@@ -109,9 +111,10 @@ def main() -> None:
     ap.add_argument("--secret-key", default=None)
     ap.add_argument("--tls-cert", default=None, help="origin/s3: serve https with this PEM certificate")
     ap.add_argument("--tls-key", default=None)
+    ap.add_argument("--rate-mbps", type=float, default=0.0, help="s3: cap ingest at this many Mbit/s (shared link)")
     a = ap.parse_args()
     asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption,
-                       a.tls_cert, a.tls_key))
+                       a.tls_cert, a.tls_key, a.rate_mbps))
 
 
 if __name__ == "__main__":

@@ -62,6 +62,8 @@ class TorrentConfig:
     webseed_conns: int = 4           # BEP 19: concurrent piece fetches per web seed
     encryption: str = "allow"        # MSE/PE policy: disable | allow | prefer | require (see .mse)
     layer_timeout: float = 120.0     # BEP 52: time to fetch piece layers of a v2 magnet
+    upnp: bool = False               # forward the listen port (TCP+UDP) via a UPnP gateway (see .portfwd)
+    upnp_ssdp: tuple | None = None   # SSDP target (default: the 239.255.255.250:1900 multicast group)
 
 
 @dataclass
@@ -178,6 +180,7 @@ class Torrent:
         self._server: asyncio.AbstractServer | None = None
         self.port = 0
         self.utp = None
+        self.portfwd = None
         self.uploaded = 0
         self.downloaded = 0
         self.closed = False
@@ -203,6 +206,10 @@ class Torrent:
             except OSError as e:
                 log.with_field("error", str(e)).warn("uTP disabled: cannot bind UDP port")
                 self.utp = None
+        if self.cfg.upnp:
+            from .portfwd import SSDP_ADDR, PortForwarder
+            self.portfwd = PortForwarder(self.port, ssdp_addr=self.cfg.upnp_ssdp or SSDP_ADDR)
+            self._spawn(self.portfwd.start())      # discovery runs in the background, never on the job path
         for p in self.static_peers:
             self.add_peer_addr(p)
         for url in self.trackers:
@@ -247,6 +254,9 @@ class Torrent:
             self.storage.close()
         if self.db is not None:
             self.db.close()
+        if self.portfwd is not None:
+            with contextlib.suppress(Exception):
+                await asyncio.wait_for(self.portfwd.close(), 5.0)
         if self._server is not None:
             with contextlib.suppress(Exception):
                 await self._server.wait_closed()
