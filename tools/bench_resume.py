@@ -58,6 +58,17 @@ async def main() -> int:
         t_make = time.perf_counter() - t0
         o = await Origin().start()
         url = o.add("/job.torrent", torrent_file_bytes(info))
+        spent = {"verify_s": 0.0}
+        for name in ("verify_pieces", "verify_pieces_v2"):
+            real = getattr(hashing, name)
+
+            def timed(*args, _real=real, **kw):
+                t = time.perf_counter()
+                try:
+                    return _real(*args, **kw)
+                finally:
+                    spent["verify_s"] += time.perf_counter() - t
+            setattr(hashing, name, timed)
         for dev in a.device:
             if dev in ("gpu", "hybrid") and not hashing.gpu_available():
                 continue
@@ -69,10 +80,11 @@ async def main() -> int:
                         os.remove(db + suffix)
                 d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device=dev), use_dht=False,
                                       progress_interval=1.0)
+                spent["verify_s"] = 0.0
                 t0 = time.perf_counter()
                 await d.download(os.path.join(td, "job"), lambda u, p: None, url)
                 dt = time.perf_counter() - t0
-                extra = {}
+                extra = {"verify_s": round(spent["verify_s"], 3)}
                 if dev in ("gpu", "hybrid", "auto") and hashing.gpu_available():
                     h = hashing.gpu_hasher()
                     if dev != "gpu":
