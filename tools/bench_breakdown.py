@@ -11,7 +11,7 @@ full job, and prints one JSON line per case:
 * ``job``     — the whole job (consume → fetch ‖ upload → publish → ack),
                 with the per-stage span medians the service records
 
-Usage: python tools/bench_breakdown.py [--file-mb 10] [--reps 20] [--payload streaming|unsigned]
+Usage: python tools/bench_breakdown.py [--file-mb 10] [--reps 20] [--payload streaming|unsigned] [--tls]
 """
 
 from __future__ import annotations
@@ -59,8 +59,8 @@ def _patch_defaults(cls, kw: str, value: int) -> None:
     cls.__init__ = init
 
 
-async def _fetch(origin: str, size: int, reps: int, work: str) -> dict:
-    dl = HTTPDownloader(progress_interval=0)
+async def _fetch(origin: str, size: int, reps: int, work: str, ca_file: str = "") -> dict:
+    dl = HTTPDownloader(progress_interval=0, ca_file=ca_file)
     sink = ProgressSink()
     ts = []
     try:
@@ -77,11 +77,12 @@ async def _fetch(origin: str, size: int, reps: int, work: str) -> dict:
 
 
 async def _upload(s3_url: str, size: int, reps: int, work: str, mode: str, make_bucket: bool = True,
-                  single: bool = False) -> dict:
+                  single: bool = False, ca_file: str = "") -> dict:
     p = os.path.join(work, "src.mkv")
     with open(p, "wb") as f:
         f.write(os.urandom(size))
-    c = S3Client(s3_url, Static(AK, SK), payload_mode=mode, **({"multipart_threshold": 1 << 62} if single else {}))
+    c = S3Client(s3_url, Static(AK, SK), payload_mode=mode, ca_file=ca_file,
+                 **({"multipart_threshold": 1 << 62} if single else {}))
     ts = []
     try:
         if make_bucket and not await c.bucket_exists("bd"):
@@ -158,9 +159,9 @@ def _trace_summary() -> dict:
     return {k: round(statistics.median(v) * 1e3, 3) for k, v in rel.items()}
 
 
-async def _job(size: int, reps: int) -> dict:
+async def _job(size: int, reps: int, tls: bool = False) -> dict:
     from tritondl.utils import rawhttp
-    st = JobStack(file_size=size)
+    st = JobStack(file_size=size, tls=tls)
     await st.setup()
     try:
         await st.run_jobs(3)
@@ -187,6 +188,7 @@ async def main() -> None:
     ap.add_argument("--http-bufsize", type=int, default=0, help="worker HTTP client read_bufsize (0 = default)")
     ap.add_argument("--s3-bufsize", type=int, default=0, help="fake S3 server read_bufsize (0 = default)")
     ap.add_argument("--io-block", type=int, default=0, help="S3 upload read/sign block (0 = default)")
+    ap.add_argument("--tls", action="store_true", help="origin and S3 over https (native TLS data plane)")
     a = ap.parse_args()
     if a.s3_bufsize:
         os.environ["TRITONDL_FAKE_S3_READ_BUFSIZE"] = str(a.s3_bufsize)
@@ -195,19 +197,23 @@ async def main() -> None:
     log.configure("error", "")
     size = int(a.file_mb * (1 << 20))
     work = tempfile.mkdtemp(prefix="tritondl-bd-")
-    og = await Backend("origin").start()
-    s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK]).start()
+    stack = JobStack(file_size=size, tls=a.tls, workdir=os.path.join(work, "stack"))
+    os.makedirs(stack.workdir)
+    eps = await stack.start_backends(broker=False)
+    ca = eps.get("ca_file", "")
+    payload = a.payload if not a.tls or a.payload != "streaming" else "unsigned"   # minio-go's https choice
     try:
-        out = {"file_bytes": size}
+        out = {"file_bytes": size, "tls": a.tls}
         out["sign"] = await asyncio.get_running_loop().run_in_executor(None, _sign, size, a.reps)
-        out["fetch"] = await _fetch(og.info["url"], size, a.reps, work)
-        out[f"upload_{a.payload}"] = await _upload(s3.info["url"], size, a.reps, work, a.payload)
-        out[f"upload_{a.payload}_nullsink"] = await _upload_null(size, a.reps, work, a.payload)
+        out["fetch"] = await _fetch(eps["origin"], size, a.reps, work, ca)
+        out[f"upload_{payload}"] = await _upload(eps["s3"], size, a.reps, work, payload, ca_file=ca)
+        if not a.tls:
+            out[f"upload_{payload}_nullsink"] = await _upload_null(size, a.reps, work, payload)
     finally:
-        await og.stop()
-        await s3.stop()
+        for b in stack.backends:
+            await b.stop()
         shutil.rmtree(work, ignore_errors=True)
-    out["job"] = await _job(size, a.reps)
+    out["job"] = await _job(size, a.reps, a.tls)
     out["knobs"] = {"http_bufsize": a.http_bufsize, "s3_bufsize": a.s3_bufsize, "io_block": a.io_block}
     print(json.dumps(out), flush=True)
 
