@@ -300,3 +300,44 @@ def test_failed_segment_stops_and_awaits_sibling_pumps(tmp_path):
         await h.close()
         await o.stop()
     run(main(), timeout=90)
+
+
+def test_striped_streams_pull_stripes_in_order(tmp_path):
+    """``stripe_bytes``: ``segments`` stream workers take fixed-size stripes in
+    file order over their keep-alive connections — the file is complete and
+    correct, every stripe is one Range request, the stripes are requested in
+    ascending order, and an interrupted striped download resumes."""
+    async def main():
+        o = await Origin().start()
+        pb, st = 256 * 1024, 300_000
+        h = _dl(segments=3, probe_bytes=pb, stripe_bytes=st, write_block=128 * 1024)
+        data = os.urandom(2_500_000)
+        url = o.add("/striped.mkv", data)
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "striped.mkv").read_bytes() == data
+        rngs = [r[2] for r in o.requests if r[0] == "GET"]
+        assert rngs[0] == f"bytes=0-{pb - 1}"
+        starts = [int(r.split("=")[1].split("-")[0]) for r in rngs[1:]]
+        want = list(range(pb, len(data), st))
+        assert sorted(starts) == want
+        # taken in file order: at most `segments` stripes are ever in flight out of turn
+        assert all(want.index(x) <= k + 2 for k, x in enumerate(starts)), starts
+        # HEAD-probe plan (open-ended probe) stripes files above the threshold too
+        plan = HTTPDownloader(segments=4, segment_threshold=1000, stripe_bytes=400)._plan(
+            __import__("tritondl.fetch.http", fromlist=["_Probe"])._Probe(
+                size=1900, ranges=True, etag="", last_modified="", filename="f", status=200))
+        assert plan == [[0, 400, 0], [400, 800, 0], [800, 1200, 0], [1200, 1600, 0], [1600, 1900, 0]]
+        # a cut mid-stripe fails the job; the next attempt resumes from the meta
+        url2 = o.add("/cut.mkv", data)
+        o.cut_after, o.cut_times, o.cut_match = 100_000, 1, f"bytes={pb + st}-"
+        h0 = _dl(segments=3, probe_bytes=pb, stripe_bytes=st, max_retries=0)
+        with pytest.raises(HTTPDownloadError):
+            await h0.download(str(tmp_path), Sink(), url2)
+        n = len(o.requests)
+        await h.download(str(tmp_path), Sink(), url2)
+        assert (tmp_path / "cut.mkv").read_bytes() == data
+        assert len(o.requests) - n < 1 + len(starts)          # resumed, not refetched from zero
+        await h0.close()
+        await h.close()
+        await o.stop()
+    run(main())

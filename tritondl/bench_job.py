@@ -93,6 +93,7 @@ class JobStack:
     tag: str = "r0"
     http_probe_bytes: int = -1       # -1: worker default (Config)
     http_segments: int = 0           # 0: worker default
+    http_stripe_bytes: int = -1      # -1: worker default
     sign_threads: int = 0            # 0: worker default
     tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
     payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
@@ -178,6 +179,8 @@ class JobStack:
             cfg.http_probe_bytes = self.http_probe_bytes
         if self.http_segments > 0:
             cfg.http_segments = self.http_segments
+        if self.http_stripe_bytes >= 0:
+            cfg.http_stripe_bytes = self.http_stripe_bytes
         if self.sign_threads > 0:
             cfg.s3_sign_threads = self.sign_threads
         self.cfg = cfg

@@ -19,7 +19,9 @@ Beyond the reference:
   on completion, so a crash never leaves a truncated file that looks done,
   and ``If-Range`` guards against resuming onto a changed origin object;
 * large files are fetched as ``segments`` concurrent Range streams written
-  with ``pwrite`` from worker threads (grab used one stream); with
+  with ``pwrite`` from worker threads (grab used one stream) — contiguous
+  slices, or with ``stripe_bytes`` in-order stripes pulled by ``segments``
+  stream workers so the upload-visible watermark advances steadily; with
   ``probe_bytes`` (opt-in: ``TRITONDL_HTTP_PROBE_BYTES``) the
   probe is ``GET bytes=0-(probe_bytes-1)`` and the rest of a bigger file is
   requested at once as parallel Range streams, so mid-size files are
@@ -129,8 +131,14 @@ class HTTPDownloader:
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
-                 ca_pem: str = "", ca_file: str = "") -> None:
+                 ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0) -> None:
         self.progress_interval = progress_interval
+        # >0: instead of `segments` contiguous slices, the file is cut into stripes of
+        # this size handed out IN ORDER to `segments` stream workers (each reuses its
+        # keep-alive connection).  All streams then advance through the file together,
+        # so the contiguous-bytes watermark -- which the streamed S3 upload follows --
+        # moves steadily instead of jumping when the last slice completes.
+        self.stripe_bytes = max(0, stripe_bytes)
         # >0: the GET probe asks for bytes=0-(probe_bytes-1); once its head names the
         # size, the rest of a bigger file is requested at once as up to `segments`
         # parallel Range streams (a file that fits stays one request).  0: open-ended
@@ -372,9 +380,19 @@ class HTTPDownloader:
 
         fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
-        tasks = [asyncio.ensure_future(self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
-                                                           first if i == 0 else None))
-                 for i in range(len(segs))]
+        if len(segs) <= self.segments:
+            tasks = [asyncio.ensure_future(self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
+                                                               first if i == 0 else None))
+                     for i in range(len(segs))]
+        else:
+            # stripes: `segments` stream workers take the next stripe in file order
+            order = iter(range(len(segs)))
+
+            async def worker() -> None:
+                for i in order:
+                    await self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
+                                              first if i == 0 else None)
+            tasks = [asyncio.ensure_future(worker()) for _ in range(self.segments)]
         try:
             await asyncio.gather(*tasks)
         except BaseException as e:
@@ -420,12 +438,18 @@ class HTTPDownloader:
             if p.first_end >= p.size:
                 return [[0, p.size, 0]]
             rest = p.size - p.first_end
+            if self.stripe_bytes:
+                st = self.stripe_bytes
+                return [[0, p.first_end, 0]] + [[a, min(p.size, a + st), 0] for a in range(p.first_end, p.size, st)]
             # the probe is one of the `segments` streams: at most segments-1 more
             k = max(1, min(max(1, self.segments - 1), -(-rest // p.first_end)))
             step = -(-rest // k)
             return [[0, p.first_end, 0]] + [[p.first_end + i * step, min(p.size, p.first_end + (i + 1) * step), 0]
                                             for i in range(k) if p.first_end + i * step < p.size]
         n = self.segments if (p.ranges and p.size >= self.segment_threshold) else 1
+        if n > 1 and self.stripe_bytes:
+            st = self.stripe_bytes
+            return [[a, min(p.size, a + st), 0] for a in range(0, p.size, st)]
         step = -(-p.size // n)
         return [[i * step, min(p.size, (i + 1) * step), 0] for i in range(n) if i * step < p.size] or [[0, 0, 0]]
 

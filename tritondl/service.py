@@ -61,7 +61,7 @@ def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
     http = HTTPDownloader(progress_interval=cfg.progress_interval_s, segments=cfg.http_segments,
                           segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes,
-                          ca_file=cfg.ca_file)
+                          ca_file=cfg.ca_file, stripe_bytes=cfg.http_stripe_bytes)
     impls: list[ClientImpl] = []
     try:
         from .fetch.bt.client import TorrentDownloader

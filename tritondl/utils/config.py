@@ -56,6 +56,7 @@ class Config:
     http_segments: int = 4                      # max parallel Range streams per HTTP file
     http_segment_threshold: int = 64 * 1024 * 1024   # open-ended probe only: segment files at least this big
     http_probe_bytes: int = 0                   # >0: GET probe = bytes=0-(N-1), the rest as parallel Range streams
+    http_stripe_bytes: int = 0                  # >0: parallel streams pull in-order stripes of this size
                                                 # (0 measured faster on the 10 MiB headline job: profiles/r01_probe)
 
     # --- download (downloader.go:81-93, torrent.go:67) ---
@@ -125,7 +126,8 @@ class Config:
                 "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
                 "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
                 "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
-                "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads"}
+                "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
+                "HTTP_STRIPE_BYTES": "http_stripe_bytes"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
