@@ -186,7 +186,14 @@ def test_bare_magnet_resolves_in_300_node_dht_with_20pct_dead(tmp_path):
                                progress_interval=0.05, use_dht=True, dht_bootstrap=net.bootstrap,
                                dht_timeout=0.4, metadata_timeout=60)
         t, node = await dl.open(str(dst), bare)
-        await asyncio.wait_for(t.got_info.wait(), 60)
+        try:
+            await asyncio.wait_for(t.got_info.wait(), 20)
+        except asyncio.TimeoutError:
+            print("DIAG lookups", list(node.lookups)[-5:])
+            print("DIAG known", t.known, "peers", list(t.peers), "connecting", t.connecting, "banned", t.banned,
+                  "seed", seed.torrent.port, "me", t.port, "found", await node.get_peers(info.infohash),
+                  "closed", t.closed, "tasks", len(t._tasks))
+            raise
         st = dict(node.last_lookup)
         look = list(node.lookups) + list(seed.dht.lookups)
         tot = {k: sum(x[k] for x in look) for k in ("queries", "responses", "timeouts")}
@@ -203,3 +210,33 @@ def test_bare_magnet_resolves_in_300_node_dht_with_20pct_dead(tmp_path):
         await seed.stop()
         net.stop()
     run(main(), timeout=240)
+
+
+def test_worker_keeps_one_warm_dht_node_across_jobs(tmp_path):
+    """The downloader's DHT node outlives a job (anacrolix-per-job re-bootstrapped
+    for every magnet): a second magnet job reuses the same node and routing
+    table, and close() stops it."""
+    async def main():
+        net = await DHTNetwork(20, timeout=0.5).start()
+        dl = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", dht_interval=0.3, verify_device="cpu"),
+                               progress_interval=0.05, use_dht=True, dht_bootstrap=net.bootstrap,
+                               dht_timeout=0.5, metadata_timeout=30)
+        nodes = []
+        for k in range(2):
+            src = tmp_path / f"src{k}"
+            make_payload(str(src), {f"f{k}.mkv": 200_000})
+            info = torrent_for(str(src / f"f{k}.mkv"), 16384)
+            seed = await Seeder(info, str(src), dht_bootstrap=net.bootstrap).start()
+            await seed.dht.announce_peer(info.infohash, seed.torrent.port)
+            dst = tmp_path / f"job{k}"
+            os.makedirs(dst)
+            await dl.download(str(dst), lambda u, p: None, f"magnet:?xt=urn:btih:{info.infohash.hex()}")
+            assert (dst / f"f{k}.mkv").read_bytes() == (src / f"f{k}.mkv").read_bytes()
+            nodes.append(dl._dht)
+            assert dl._dht is not None and dl._dht.transport_alive if hasattr(dl._dht, "transport_alive") else True
+            await seed.stop()
+        assert nodes[0] is nodes[1] and len(nodes[0].table) > 0
+        await dl.close()
+        assert dl._dht is None and not nodes[0].families
+        net.stop()
+    run(main(), timeout=120)

@@ -54,7 +54,7 @@ class TorrentDownloader:
                  progress_interval: float = 1.0, use_dht: bool = True,
                  dht_bootstrap: list[tuple[str, int]] | None = None, extra_trackers: list[str] | None = None,
                  http_session: aiohttp.ClientSession | None = None, dht_ipv6: bool = False,
-                 dht_timeout: float = 2.0) -> None:
+                 dht_timeout: float = 2.0, shared_dht: bool = True) -> None:
         self.cfg = cfg or TorrentConfig()
         self.metadata_timeout = metadata_timeout
         self.progress_interval = progress_interval
@@ -62,6 +62,12 @@ class TorrentDownloader:
         self.dht_bootstrap = dht_bootstrap or []
         self.dht_ipv6 = dht_ipv6          # BEP 32: a second DHT socket + table on IPv6
         self.dht_timeout = dht_timeout
+        # one DHT node per worker process, kept across jobs (routing table stays warm,
+        # buckets refreshed in the background): the reference's per-job anacrolix client
+        # re-bootstrapped its DHT from the routers for every magnet
+        self.shared_dht = shared_dht
+        self._dht: DHTNode | None = None
+        self._dht_boot: asyncio.Task | None = None
         self.extra_trackers = extra_trackers or []
         self._http = http_session
 
@@ -123,16 +129,34 @@ class TorrentDownloader:
             webseeds = list(mi.url_list)
         else:
             raise TorrentError(f"unsupported scheme '{u.scheme}'")
-        dht = None
-        if self.use_dht:
-            bind = "127.0.0.1" if self.cfg.listen_host == "127.0.0.1" else "0.0.0.0"
-            dht = await DHTNode(host=bind, bootstrap=self.dht_bootstrap, timeout=self.dht_timeout,
-                                host6=("::1" if bind == "127.0.0.1" else "::") if self.dht_ipv6 else None).start()
-            asyncio.ensure_future(dht.bootstrap())
+        dht = await self._dht_node() if self.use_dht else None
         t = Torrent(ih, base_dir, self.cfg, info=info, trackers=trackers, peers=peers, dht=dht, name_hint=name,
                     webseeds=webseeds)
         await t.start()
         return t, dht
+
+    async def _dht_node(self) -> DHTNode:
+        if self.shared_dht and self._dht is not None:
+            return self._dht
+        bind = "127.0.0.1" if self.cfg.listen_host == "127.0.0.1" else "0.0.0.0"
+        dht = await DHTNode(host=bind, bootstrap=self.dht_bootstrap, timeout=self.dht_timeout,
+                            host6=("::1" if bind == "127.0.0.1" else "::") if self.dht_ipv6 else None
+                            ).start(maintain=self.shared_dht)
+        boot = asyncio.ensure_future(dht.bootstrap())
+        if self.shared_dht:
+            self._dht, self._dht_boot = dht, boot
+        return dht
+
+    async def close(self) -> None:
+        """Stop the shared DHT node (Dispatcher.stop calls this on shutdown)."""
+        if self._dht_boot is not None:
+            self._dht_boot.cancel()
+            with contextlib.suppress(BaseException):
+                await self._dht_boot
+            self._dht_boot = None
+        if self._dht is not None:
+            self._dht.stop()
+            self._dht = None
 
     async def download(self, base_dir: str, progress: ProgressSink, url: str, *,
                        pick_files=None, on_file=None) -> None:
@@ -170,5 +194,5 @@ class TorrentDownloader:
                 with contextlib.suppress(BaseException):
                     await rep
             await t.close()
-            if dht is not None:
+            if dht is not None and dht is not self._dht:
                 dht.stop()

@@ -14,9 +14,9 @@ resolve on the real internet:
   favour of the newest replacement — BEP 5 "ping before evict".  Buckets idle
   for ``refresh_after`` are refreshed with a lookup of a random id in range;
 * **iterative lookup** — ``α = 3`` queries in flight toward the target,
-  keeping a shortlist ordered by XOR distance; it ends when the ``K``
+  keeping a shortlist ordered by XOR distance; it ends when the ``2K``
   closest nodes that have not failed have all answered (convergence), not
-  after a fixed number of rounds.  Timeouts mark the node failed in the
+  after a fixed number of rounds; the K closest of them are the result.  Timeouts mark the node failed in the
   table.  Each lookup's query/response/timeout counts land in
   :attr:`DHTNode.last_lookup`;
 * **server side** — answers ``ping``/``find_node``/``get_peers``/
@@ -264,7 +264,7 @@ class DHTNode:
                  bootstrap: list[tuple[str, int]] | None = None, timeout: float = 2.0, *,
                  host6: str | None = None, port6: int = 0, k: int = K, alpha: int = ALPHA,
                  stale_after: float = 900.0, refresh_after: float = 900.0, token_rotate: float = 300.0,
-                 peer_ttl: float = 1800.0, max_lookup_queries: int = 400) -> None:
+                 peer_ttl: float = 1800.0, max_lookup_queries: int = 400, lookup_width: int = 0) -> None:
         self.id = node_id or hashlib.sha1(os.urandom(20)).digest()
         self.host, self.port = host, port
         self.host6, self.port6 = host6, port6
@@ -275,6 +275,11 @@ class DHTNode:
         self.token_rotate = token_rotate
         self.peer_ttl = peer_ttl
         self.max_lookup_queries = max_lookup_queries
+        # a lookup has converged when the `lookup_width` closest live nodes have all
+        # answered (default 2K): exploring wider than the K it reports/announces to
+        # keeps a lookup from settling on a local minimum of incomplete routing
+        # tables, so announcer and searcher reliably meet on the same K nodes
+        self.lookup_width = lookup_width or 2 * k
         self.tables = {socket.AF_INET: RoutingTable(self.id, k, stale_after),
                        socket.AF_INET6: RoutingTable(self.id, k, stale_after)}
         self.peers: dict[bytes, dict[tuple[str, int], float]] = {}
@@ -637,7 +642,7 @@ class DHTNode:
         want = [b"n6"] if fam == socket.AF_INET6 else [b"n4"]
         if not len(table):
             await self._ask_routers(target, fam)
-        known: dict[bytes, tuple[str, int]] = {n.id: n.addr for n in table.closest(target, 2 * self.k)}
+        known: dict[bytes, tuple[str, int]] = {n.id: n.addr for n in table.closest(target, 2 * self.lookup_width)}
         state: dict[bytes, str] = {nid: "new" for nid in known}       # new | wait | ok | dead
         found: list[tuple[str, int]] = []
         tokens: dict[bytes, tuple[tuple[str, int], bytes]] = {}
@@ -650,7 +655,7 @@ class DHTNode:
 
         try:
             while True:
-                top = order()[:self.k]
+                top = order()[:self.lookup_width]
                 if all(state[nid] == "ok" for nid in top) and not any(state[n] == "wait" for n in top):
                     break                                                   # converged
                 for nid in top:
@@ -694,11 +699,11 @@ class DHTNode:
         finally:
             for t in inflight:
                 t.cancel()
-        top = order()[:self.k]
+        top = order()[:self.lookup_width]
         st.update(target=target.hex(), method=method, family="ipv6" if fam == socket.AF_INET6 else "ipv4",
                   peers=len(found), converged=all(state[n] == "ok" for n in top))
         self.last_lookup = st
         self.lookups.append(st)
-        self.last_closest = [(nid, known[nid]) for nid in top if state[nid] == "ok"]
+        self.last_closest = [(nid, known[nid]) for nid in top if state[nid] == "ok"][:self.k]
         log.with_fields(**{k: v for k, v in st.items() if k != "target"}).debug("dht lookup done")
         return found, tokens
