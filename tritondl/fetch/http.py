@@ -137,7 +137,10 @@ class HTTPDownloader:
         # this size handed out IN ORDER to `segments` stream workers (each reuses its
         # keep-alive connection).  All streams then advance through the file together,
         # so the contiguous-bytes watermark -- which the streamed S3 upload follows --
-        # moves steadily instead of jumping when the last slice completes.
+        # moves steadily instead of jumping when the last slice completes.  Opt-in
+        # (TRITONDL_HTTP_STRIPE_BYTES): on the 10 MiB headline job every extra Range
+        # request cost more than the smoother watermark won (http 219-225 vs 298 jobs/s,
+        # https 147-163 vs 175; profiles/r02_stripe_ab)
         self.stripe_bytes = max(0, stripe_bytes)
         # >0: the GET probe asks for bytes=0-(probe_bytes-1); once its head names the
         # size, the rest of a bigger file is requested at once as up to `segments`
