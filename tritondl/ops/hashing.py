@@ -105,12 +105,26 @@ def gpu_available() -> bool:
         return False
 
 
-def gpu_hasher(device: int = 0, batch_bytes: int = 0, reader_threads: int = 0, window_bytes: int = 0):
+def default_device() -> int:
+    """This worker's GPU: ``TRITONDL_GPU_DEVICE``, else torchrun's ``LOCAL_RANK``
+    (one worker per GPU), modulo the visible devices.  The supervised pool
+    (``parallel/pool.py``) pins each worker with ``HIP_VISIBLE_DEVICES``, so
+    there it is always 0."""
+    want = os.environ.get("TRITONDL_GPU_DEVICE") or os.environ.get("LOCAL_RANK") or "0"
+    try:
+        n = _load_gpu().device_count()
+    except Exception:  # noqa: BLE001 - no extension / no device: callers fail later, loudly
+        return 0
+    return int(want) % n if n > 0 else 0
+
+
+def gpu_hasher(device: int | None = None, batch_bytes: int = 0, reader_threads: int = 0, window_bytes: int = 0):
     """Cached per-device :class:`GpuHasher`.  ``batch_bytes`` is the pinned
     staging slot, one of a ring of 4 (0: ``TRITONDL_GPU_STAGE_MB`` or 128 MiB); ``reader_threads``
     the pread threads filling it (0: ``TRITONDL_GPU_READERS`` or
     :data:`GPU_READERS`); ``window_bytes`` the HBM window hashed per kernel
     launch (0 = auto: a third of free HBM, capped at 48 GiB)."""
+    device = default_device() if device is None else device
     batch_bytes = batch_bytes or (int(os.environ.get("TRITONDL_GPU_STAGE_MB", "128")) << 20)
     reader_threads = reader_threads or int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS)))
     key = (device, max(batch_bytes, 1 << 20), window_bytes, reader_threads)
@@ -123,7 +137,7 @@ def gpu_hasher(device: int = 0, batch_bytes: int = 0, reader_threads: int = 0, w
         return h
 
 
-def warm_gpu(device: int = 0) -> bool:
+def warm_gpu(device: int | None = None) -> bool:
     """Create the cached hasher and run one tiny batch (HIP context, code
     object, pinned staging) so the first resume-verify of a job does not pay
     the one-time setup.  Returns False when no GPU path is available."""
