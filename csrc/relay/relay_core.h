@@ -540,7 +540,10 @@ inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, co
   }
   // TLS: decrypt into an L2-sized buffer so pwrite copies cache-hot bytes
   Buf buf(io.plain() ? std::max<size_t>(buf_size, 64 << 10) : (256u << 10));
-  const size_t fill = io.plain() ? (1u << 20) : (256u << 10);
+  // with a follower (the S3 send pump hashes 64 KiB chunks as soon as the
+  // flow covers them) publish progress every 256 KiB, so the upload trails the
+  // download by a few chunks instead of a whole 1 MiB batch at the end
+  const size_t fill = io.plain() && !flow ? (1u << 20) : (256u << 10);
   auto last = Clock::now();
   while (r.received < want) {
     // fill the buffer with whatever is ready (TLS yields one record per read),
