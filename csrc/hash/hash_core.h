@@ -6,6 +6,11 @@
 
 #include <openssl/evp.h>
 #include <openssl/hmac.h>
+// The low-level SHA256_* API is deprecated in OpenSSL 3 but still exported; the
+// HMAC chain below needs plain copyable SHA-256 states (EVP contexts allocate on
+// every copy, and one-shot HMAC() re-fetches the MAC implementation per call).
+#define OPENSSL_SUPPRESS_DEPRECATED
+#include <openssl/sha.h>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -99,6 +104,98 @@ inline std::string hmac256(const std::string& key, const std::string& msg) {
     throw std::runtime_error("HMAC failed");
   return std::string(reinterpret_cast<char*>(out), len);
 }
+
+// HMAC-SHA256 with the key's inner/outer pad blocks absorbed once: each MAC
+// is a struct copy + the message blocks + one outer block (4.2 -> ~0.5 us per
+// aws-chunked chunk signature, which is a serial chain on the PUT's critical
+// path — 160 links per 10 MiB object).
+class HmacSha256 {
+ public:
+  explicit HmacSha256(const std::string& key) {
+    unsigned char k[64] = {0};
+    if (key.size() > 64) {
+      SHA256(reinterpret_cast<const unsigned char*>(key.data()), key.size(), k);
+    } else if (!key.empty()) {
+      std::memcpy(k, key.data(), key.size());
+    }
+    unsigned char ip[64], op[64];
+    for (int i = 0; i < 64; ++i) {
+      ip[i] = static_cast<unsigned char>(k[i] ^ 0x36);
+      op[i] = static_cast<unsigned char>(k[i] ^ 0x5c);
+    }
+    SHA256_Init(&inner_);
+    SHA256_Update(&inner_, ip, 64);
+    SHA256_Init(&outer_);
+    SHA256_Update(&outer_, op, 64);
+  }
+  void mac(const void* msg, size_t n, unsigned char out[32]) const {
+    SHA256_CTX c = inner_;
+    unsigned char ih[32];
+    SHA256_Update(&c, msg, n);
+    SHA256_Final(ih, &c);
+    c = outer_;
+    SHA256_Update(&c, ih, 32);
+    SHA256_Final(out, &c);
+  }
+
+ private:
+  SHA256_CTX inner_, outer_;
+};
+
+inline void hex_into(const unsigned char* d, size_t n, char* out) {
+  static const char* hx = "0123456789abcdef";
+  for (size_t i = 0; i < n; ++i) {
+    out[2 * i] = hx[d[i] >> 4];
+    out[2 * i + 1] = hx[d[i] & 15];
+  }
+}
+
+// aws-chunked (STREAMING-AWS4-HMAC-SHA256-PAYLOAD) signature chain.  The
+// string to sign is kept in one buffer whose previous-signature and
+// chunk-hash fields are overwritten in place:
+//   "AWS4-HMAC-SHA256-PAYLOAD\n" amzdate "\n" scope "\n" prev "\n" hex(sha256("")) "\n" hex(sha256(chunk))
+class SigChain {
+ public:
+  SigChain(const std::string& signing_key, const std::string& amzdate, const std::string& scope,
+           const std::string& seed)
+      : mac_(signing_key), head_("AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n") {
+    layout(seed);
+  }
+  // signature (hex) of the next chunk, given the hex SHA-256 of its data
+  const std::string& next(const char* chunk_hash_hex) {
+    std::memcpy(&buf_[hash_off_], chunk_hash_hex, 64);
+    unsigned char sig[32];
+    mac_.mac(buf_.data(), buf_.size(), sig);
+    char hx[64];
+    hex_into(sig, 32, hx);
+    if (prev_.size() != 64) {
+      layout(std::string(hx, 64));    // a seed of unusual length: every later link is 64 chars
+    } else {
+      std::memcpy(&prev_[0], hx, 64);
+      std::memcpy(&buf_[prev_off_], hx, 64);
+    }
+    return prev_;
+  }
+  const std::string& next(const std::string& chunk_hash_hex) {
+    if (chunk_hash_hex.size() != 64) throw std::invalid_argument("chunk hash must be 64 hex chars");
+    return next(chunk_hash_hex.data());
+  }
+  const std::string& prev() const { return prev_; }
+
+ private:
+  void layout(const std::string& prev) {
+    static const char empty[] = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855";
+    prev_ = prev;
+    buf_ = head_;
+    prev_off_ = buf_.size();
+    buf_ += prev + "\n" + empty + "\n";
+    hash_off_ = buf_.size();
+    buf_.append(64, '0');
+  }
+  HmacSha256 mac_;
+  std::string head_, buf_, prev_;
+  size_t prev_off_ = 0, hash_off_ = 0;
+};
 
 // pread that loops over short reads; returns bytes read (may be < n at EOF)
 inline size_t pread_full(int fd, char* dst, size_t n, off_t off) {
@@ -241,15 +338,10 @@ inline std::vector<std::string> chunk_signatures(const std::string& key, const s
                                                  bool include_final, int threads = 1) {
   if (chunk_size == 0) throw std::invalid_argument("chunk_size must be > 0");
   const std::vector<std::string> h = chunk_hashes(data, len, chunk_size, include_final, threads);
-  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
-  const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
+  SigChain chain(key, amzdate, scope, seed);
   std::vector<std::string> sigs;
   sigs.reserve(h.size());
-  std::string prev = seed;
-  for (const auto& hc : h) {
-    prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + hc));
-    sigs.push_back(prev);
-  }
+  for (const auto& hc : h) sigs.push_back(chain.next(hc));
   return sigs;
 }
 
@@ -308,10 +400,9 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
     *w++ = '\r';
     *w++ = '\n';
   });
-  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
-  const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
+  SigChain chain(key, amzdate, scope, prev);
   for (size_t i = 0; i < n; ++i) {
-    prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + h[i]));
+    prev = chain.next(h[i]);
     const size_t m = i < nfull ? std::min(chunk_size, len - i * chunk_size) : 0;
     std::memcpy(dst + frame[i] + hexlen(m) + 17, prev.data(), 64);
   }
@@ -365,12 +456,9 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
     h[i] = hex(one_shot(sha256_md(), f.n ? raw + f.off : "", f.n));
     if (decoded && f.n) std::memcpy(&(*decoded)[dst_off[i]], raw + f.off, f.n);
   });
-  const std::string empty_hash = hex(one_shot(sha256_md(), "", 0));
-  const std::string head = "AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n";
-  std::string prev = seed;
+  SigChain chain(key, amzdate, scope, seed);
   for (size_t i = 0; i < frames.size(); ++i) {
-    prev = hex(hmac256(key, head + prev + "\n" + empty_hash + "\n" + h[i]));
-    if (std::memcmp(prev.data(), frames[i].sig, 64) != 0) return "chunk signature mismatch";
+    if (std::memcmp(chain.next(h[i]).data(), frames[i].sig, 64) != 0) return "chunk signature mismatch";
   }
   return "";
 }

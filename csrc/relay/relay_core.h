@@ -599,16 +599,13 @@ struct SendResult {
 };
 
 struct ChunkSigner {
-  std::string key, head, empty_hash, prev;
+  tritondl_hash::SigChain chain;
+  std::string empty_hash;
   ChunkSigner(const std::string& k, const std::string& amzdate, const std::string& scope, const std::string& seed)
-      : key(k),
-        head("AWS4-HMAC-SHA256-PAYLOAD\n" + amzdate + "\n" + scope + "\n"),
-        empty_hash(tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), "", 0))),
-        prev(seed) {}
-  const std::string& next(const std::string& chunk_hash_hex) {
-    prev = tritondl_hash::hex(tritondl_hash::hmac256(key, head + prev + "\n" + empty_hash + "\n" + chunk_hash_hex));
-    return prev;
-  }
+      : chain(k, amzdate, scope, seed),
+        empty_hash(tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), "", 0))) {}
+  const std::string& next(const std::string& chunk_hash_hex) { return chain.next(chunk_hash_hex); }
+  const std::string& prev() const { return chain.prev(); }
 };
 
 inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
@@ -814,7 +811,7 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
     r.err = e;
     return r;
   }
-  r.last_sig = signer.prev;
+  r.last_sig = signer.prev();
   return r;
 }
 
