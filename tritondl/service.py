@@ -201,7 +201,8 @@ class Service:
             await self._dead_letter(msg, "decode", e)
             return self._record(JobResult(False, "decode", str(e)))
 
-        log.with_field("job", job.to_dict()).info("got message")
+        if log.enabled("info"):
+            log.with_field("job", job.to_dict()).info("got message")
         stage = "download"
         nbytes = 0
         marks: dict[str, float] = {}
@@ -236,7 +237,8 @@ class Service:
             await self.amqp.publish(self.cfg.publish_topic, conv.encode())
             mark("publish")
             stage = "ack"
-            log.with_field("job", job.to_dict()).info("finished processing")
+            if log.enabled("info"):
+                log.with_field("job", job.to_dict()).info("finished processing")
             await msg.ack()
             mark("ack")
         except asyncio.CancelledError:
@@ -263,8 +265,9 @@ class Service:
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
         self.metrics.observe("job_seconds", dt)
-        log.with_fields(media_id=job.media.id, bytes=nbytes,
-                        **{k: round(v * 1000, 3) for k, v in marks.items()}).debug("job spans (ms)")
+        if log.enabled("debug"):
+            log.with_fields(media_id=job.media.id, bytes=nbytes,
+                            **{k: round(v * 1000, 3) for k, v in marks.items()}).debug("job spans (ms)")
         return self._record(JobResult(True, "done", files=len(files), bytes=nbytes, seconds=dt, marks=marks))
 
     async def _download(self, media_id: str, url: str, marks: dict | None = None,

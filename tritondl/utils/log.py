@@ -94,6 +94,10 @@ class Logger:
     def with_error(self, err: BaseException) -> "Entry":
         return Entry(self, {"error": str(err)})
 
+    def enabled(self, level: str) -> bool:
+        """Would a record at ``level`` be emitted?  (Guards costly field building.)"""
+        return LEVELS[level] <= self.level
+
     # direct logging ----------------------------------------------------
     def debug(self, msg: str, *a: Any) -> None:
         Entry(self, {})._log("debug", msg, a, 3)
