@@ -341,3 +341,39 @@ def test_striped_streams_pull_stripes_in_order(tmp_path):
         await h.close()
         await o.stop()
     run(main())
+
+
+def test_redirects_followed_natively(tmp_path):
+    """301 -> 307 chains (absolute and relative Location) are followed on the
+    native path; the file is named after the FINAL URL (grab / Go http.Client
+    behaviour); later Range requests go straight to the final URL; a loop
+    stops after max_redirects."""
+    async def main():
+        from tritondl.fetch import http as H
+        o = await Origin().start()
+        data = os.urandom(1_500_000)
+        o.add("/cdn/real-name.mkv", data)
+        o.redirect("/b/hop2", "/cdn/real-name.mkv", 307)                 # relative
+        o.redirect("/a/watch", o.url("/b/hop2"), 301)                   # absolute
+        start = o.url("/a/watch") + "?id=7"
+        h = _dl(segments=3, probe_bytes=256 * 1024)
+        fell_back = []
+        orig_raw = h._raw_get
+
+        async def spy(url, headers):
+            r = await orig_raw(url, headers)
+            fell_back.append(r is None)
+            return r
+        h._raw_get = spy
+        await h.download(str(tmp_path), Sink(), start)
+        assert (tmp_path / "real-name.mkv").read_bytes() == data
+        assert fell_back and not any(fell_back)                        # never left the native path
+        paths = [r[1] for r in o.requests if r[0] == "GET"]
+        assert paths[:3] == ["/a/watch", "/b/hop2", "/cdn/real-name.mkv"]
+        assert all(p == "/cdn/real-name.mkv" for p in paths[3:]) and len(paths) > 3   # ranges skip the hops
+        o.redirect("/loop", "/loop")
+        with pytest.raises(H.HTTPDownloadError):
+            await _dl(max_retries=0).download(str(tmp_path), Sink(), o.url("/loop"))
+        await h.close()
+        await o.stop()
+    run(main())

@@ -70,12 +70,18 @@ class Origin:
         self.rate: float | None = None
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
+        self.redirects: dict[str, tuple[int, str]] = {}     # path -> (status, Location)
         self._server: web.Server | None = None
 
     def add(self, path: str, data: bytes | None = None, *, file: str | None = None,
             disposition: str | None = None) -> str:
         etag = '"' + (hashlib.md5(data).hexdigest() if data is not None else f"f{os.path.getmtime(file or '')}") + '"'
         self.blobs[path] = Blob(data, file, disposition, etag)
+        return self.url(path)
+
+    def redirect(self, path: str, location: str, status: int = 302) -> str:
+        """Answer ``path`` with a redirect to ``location`` (absolute or relative)."""
+        self.redirects[path] = (status, location)
         return self.url(path)
 
     def url(self, path: str) -> str:
@@ -98,6 +104,9 @@ class Origin:
         if self.fail > 0:
             self.fail -= 1
             return web.Response(status=500, text="injected")
+        rd = self.redirects.get(request.path)
+        if rd is not None:
+            return web.Response(status=rd[0], headers={"Location": rd[1]})
         blob = self.blobs.get(request.raw_path.split("?", 1)[0]) or self.blobs.get(request.path)
         if blob is None:
             return web.Response(status=404, text="not found")

@@ -30,8 +30,9 @@ Beyond the reference:
   parsed the connection (a plain socket, or an OpenSSL TLS session driven by
   the relay module) goes to the native receive pump (``csrc/relay``, GIL
   released), which writes the file and publishes progress on a native
-  ``Flow`` that the S3 send pump follows (redirects and chunked / encoded
-  bodies use aiohttp);
+  ``Flow`` that the S3 send pump follows; redirects are followed natively
+  (later Range requests go straight to the final URL); chunked / encoded
+  bodies use aiohttp;
 * when one segment fails, its siblings are cancelled and their pumps
   stopped and awaited before the file or any socket is closed (no write
   through a recycled fd number).
@@ -101,6 +102,7 @@ class _Probe:
     filename: str
     status: int
     first_end: int | None = None     # end (exclusive) of the GET probe's 206 body
+    final_url: str = ""              # after redirects: later Range requests go straight there
 
 
 def filename_from_disposition(cd: str | None) -> str:
@@ -131,8 +133,9 @@ class HTTPDownloader:
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
-                 ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0) -> None:
+                 ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10) -> None:
         self.progress_interval = progress_interval
+        self.max_redirects = max_redirects          # Go's http.Client default (grab uses it)
         # >0: instead of `segments` contiguous slices, the file is cut into stripes of
         # this size handed out IN ORDER to `segments` stream workers (each reuses its
         # keep-alive connection).  All streams then advance through the file together,
@@ -213,38 +216,54 @@ class HTTPDownloader:
         return await s.get(url, headers=headers, allow_redirects=True)
 
     async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":
-        u = URL(url)
-        secure = u.scheme == "https"
-        dport = 443 if secure else 80
-        host, port = u.raw_host or "", u.port or dport
-        target = u.raw_path_qs or "/"
-        hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
-        head = rawhttp.request_head("GET", target, hh)
-        tls = self._tls_ctx() if secure else None
-        if secure and tls is None:
-            return None
-        for _ in range(2):                    # a stale pooled keep-alive connection gets one fresh retry
-            try:
-                conn, reused = await self._raw.connect(host, port, timeout=30.0, tls=tls)
-            except (OSError, rawhttp.RawHTTPError) as e:
-                raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
-            try:
-                await asyncio.wait_for(conn.sendall(head), self.read_timeout)
-                h = await rawhttp.read_head(conn, self.read_timeout)
-            except (OSError, rawhttp.RawHTTPError) as e:
-                conn.close()
-                if reused:
-                    continue
-                raise aiohttp.ClientConnectionError(str(e)) from e
-            except BaseException:
-                conn.close()
-                raise
+        """Native GET.  Redirects (301/302/303/307/308, relative or absolute,
+        http <-> https) are followed here, up to ``max_redirects`` like Go's
+        http.Client under grab; the returned response's ``url`` is the final
+        one (file naming uses it, as grab does)."""
+        for _hop in range(self.max_redirects + 1):
+            u = URL(url)
+            secure = u.scheme == "https"
+            dport = 443 if secure else 80
+            host, port = u.raw_host or "", u.port or dport
+            target = u.raw_path_qs or "/"
+            hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
+            head = rawhttp.request_head("GET", target, hh)
+            tls = self._tls_ctx() if secure else None
+            if secure and tls is None:
+                return None
+            h = conn = None
+            for _ in range(2):                # a stale pooled keep-alive connection gets one fresh retry
+                try:
+                    conn, reused = await self._raw.connect(host, port, timeout=30.0, tls=tls)
+                except (OSError, rawhttp.RawHTTPError) as e:
+                    raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
+                try:
+                    await asyncio.wait_for(conn.sendall(head), self.read_timeout)
+                    h = await rawhttp.read_head(conn, self.read_timeout)
+                    break
+                except (OSError, rawhttp.RawHTTPError) as e:
+                    conn.close()
+                    if reused:
+                        continue
+                    raise aiohttp.ClientConnectionError(str(e)) from e
+                except BaseException:
+                    conn.close()
+                    raise
+            if h is None:
+                raise aiohttp.ClientConnectionError(f"GET {url}: connection reset")
+            loc = h.headers.get("Location")
+            if h.status in (301, 302, 303, 307, 308) and loc:
+                conn.close()                  # small redirect body: not worth draining for keep-alive
+                url = str(u.join(URL(loc)))
+                if not url.startswith(("http://", "https://")):
+                    return None
+                continue
             enc = h.headers.get("Content-Encoding", "identity").lower()
             if 300 <= h.status < 400 or h.chunked or enc not in ("", "identity"):
-                conn.close()                  # redirect / chunked / encoded body: aiohttp handles these
+                conn.close()                  # odd 3xx / chunked / encoded body: aiohttp handles these
                 return None
             return _RawResponse(self._raw, host, port, conn, h, url)
-        raise aiohttp.ClientConnectionError(f"GET {url}: connection reset")
+        raise HTTPDownloadError(f"GET {url}: stopped after {self.max_redirects} redirects")
 
     # ------------------------------------------------------------ probe
     async def _probe(self, url: str) -> _Probe:
@@ -305,6 +324,8 @@ class HTTPDownloader:
                 r.release()
                 raise HTTPDownloadError(f"GET {url}: bad Content-Range {r.headers.get('Content-Range')!r}")
             p.size, p.ranges, p.first_end = int(m.group(3)), True, int(m.group(2)) + 1
+        if str(r.url) != url:
+            p.final_url = str(r.url)
         return p, r
 
     def _probe_from(self, r: aiohttp.ClientResponse, url: str) -> _Probe:
@@ -383,8 +404,9 @@ class HTTPDownloader:
 
         fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
+        src = probe.final_url or url          # follow-up ranges skip the redirect hop(s)
         if len(segs) <= self.segments:
-            tasks = [asyncio.ensure_future(self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
+            tasks = [asyncio.ensure_future(self._fetch_segment(src, fd, i, segs, done, validator, probe, h,
                                                                first if i == 0 else None))
                      for i in range(len(segs))]
         else:
@@ -393,7 +415,7 @@ class HTTPDownloader:
 
             async def worker() -> None:
                 for i in order:
-                    await self._fetch_segment(url, fd, i, segs, done, validator, probe, h,
+                    await self._fetch_segment(src, fd, i, segs, done, validator, probe, h,
                                               first if i == 0 else None)
             tasks = [asyncio.ensure_future(worker()) for _ in range(self.segments)]
         try:
