@@ -172,6 +172,7 @@ def main() -> int:
                 loop.run_until_complete(stack.run_jobs(a.warmup))
         base = len(stack.svc.results)  # type: ignore[union-attr]
         barrier()
+        cpu0 = stack.cpu_seconds()
         t0 = time.perf_counter()
         if shared:
             loop.run_until_complete(phase(a.steps))
@@ -180,6 +181,7 @@ def main() -> int:
         if cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        cpu1 = stack.cpu_seconds()
         barrier()
         done = stack.svc.results[base:]  # type: ignore[union-attr]
         failed = len(stack.failures())
@@ -199,9 +201,13 @@ def main() -> int:
     if int(t[1].item()):
         raise SystemExit(f"{int(t[1].item())} jobs failed on some rank")
     per_rank = [len(done)]
+    cpu = {k: cpu1[k] - cpu0[k] for k in cpu0}
+    cpu_all = [cpu]
     if world > 1:
         per_rank = [None] * world  # type: ignore[list-item]
         dist.all_gather_object(per_rank, len(done), group=ctl)
+        cpu_all = [None] * world  # type: ignore[list-item]
+        dist.all_gather_object(cpu_all, cpu, group=ctl)
     extra = {} if (a.no_gpu_probe or rank != 0) else _gpu_hash_probe()
     if rank == 0:
         jobs_per_sec = world * a.steps / max_elapsed
@@ -235,6 +241,11 @@ def main() -> int:
             "job_latency_ms_p90": round(lat[int(len(lat) * 0.9)] * 1000, 2) if lat else None,
             # median ms from taking the job to the end of each stage (rank 0)
             "job_spans_ms_p50": {k: round(sorted(v)[len(v) // 2] * 1000, 2) for k, v in spans.items()},
+            # CPU cost per job over the timed region, all ranks (worker processes incl. their
+            # native pump threads; the out-of-process fakes separately): the node's CPU count
+            # divided by this bounds how far job-level data parallelism can scale
+            "cpu_ms_per_job": {k: round(sum(c[k] for c in cpu_all) / (world * a.steps) * 1000, 2)
+                               for k in ("worker", "fakes")},
         }
         res.update(extra)
         print(json.dumps(res), flush=True)

@@ -262,6 +262,24 @@ class JobStack:
             await asyncio.sleep(0.001)
         return time.perf_counter() - t0
 
+    def cpu_seconds(self) -> dict:
+        """CPU time (user+sys, s) so far of this worker process (all threads:
+        native pumps included) and of this stack's out-of-process fakes."""
+        import psutil
+        me = psutil.Process()
+        t = me.cpu_times()
+        out = {"worker": t.user + t.system, "fakes": 0.0}
+        for b in self.backends:
+            p = getattr(b, "proc", None)
+            if p is None:
+                continue
+            try:
+                ft = psutil.Process(p.pid).cpu_times()
+                out["fakes"] += ft.user + ft.system
+            except psutil.Error:
+                pass
+        return out
+
     def failures(self) -> list:
         assert self.svc is not None
         return [r for r in self.svc.results if not r.ok or r.bytes != self.file_size]
