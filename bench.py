@@ -245,7 +245,7 @@ def main() -> int:
             # native pump threads; the out-of-process fakes separately): the node's CPU count
             # divided by this bounds how far job-level data parallelism can scale
             "cpu_ms_per_job": {k: round(sum(c[k] for c in cpu_all) / (world * a.steps) * 1000, 2)
-                               for k in ("worker", "fakes")},
+                               for k in ("worker", "fakes", "broker")},
         }
         res.update(extra)
         print(json.dumps(res), flush=True)

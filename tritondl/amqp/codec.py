@@ -13,6 +13,7 @@ share one codec.
 
 from __future__ import annotations
 
+import asyncio
 import struct
 from dataclasses import dataclass, field
 from datetime import datetime, timezone
@@ -467,6 +468,48 @@ def content_frames(channel: int, m: Method, body: bytes, props: Properties, fram
     for i in range(0, len(body), chunk):
         out.append(frame(FRAME_BODY, channel, bytes(mv[i:i + chunk])))
     return out
+
+
+class FrameParser:
+    """Incremental frame splitter: ``feed`` raw socket bytes, get every complete
+    frame at once.  One ``read`` of up to 64 KiB usually holds several frames
+    (a delivery is method + header + body frames), so this replaces two
+    awaited ``readexactly`` calls per frame with one read per batch."""
+
+    def __init__(self, frame_max: int = 0) -> None:
+        self.frame_max = frame_max
+        self._buf = bytearray()
+
+    def feed(self, data: bytes) -> list[tuple[int, int, bytes]]:
+        buf = self._buf
+        buf += data
+        out: list[tuple[int, int, bytes]] = []
+        pos, n = 0, len(buf)
+        while n - pos >= 8:
+            ftype, ch, size = struct.unpack_from(">BHI", buf, pos)
+            if self.frame_max and size > self.frame_max:
+                raise FrameError(f"frame size {size} exceeds frame_max {self.frame_max}")
+            end = pos + 8 + size
+            if end > n:
+                break
+            if buf[end - 1] != FRAME_END:
+                raise FrameError("missing frame-end octet")
+            out.append((ftype, ch, bytes(buf[pos + 7:end - 1])))
+            pos = end
+        if pos:
+            del buf[:pos]
+        return out
+
+
+async def read_frames(reader, parser: FrameParser) -> list[tuple[int, int, bytes]]:
+    """At least one complete frame (all that one socket read delivered)."""
+    while True:
+        data = await reader.read(1 << 16)
+        if not data:
+            raise asyncio.IncompleteReadError(b"", None)
+        frames = parser.feed(data)
+        if frames:
+            return frames
 
 
 async def read_frame(reader, frame_max: int = 0) -> tuple[int, int, bytes]:

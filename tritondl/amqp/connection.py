@@ -126,6 +126,8 @@ class Connection:
         self._close_ok: asyncio.Future | None = None
         self._tasks: list[asyncio.Task] = []
         self._last_write = 0.0
+        self._wbuf: list[bytes] = []
+        self._flush_scheduled = False
         self._last_read = 0.0
         self._close_callbacks: list[Callable[[BaseException], Any]] = []
         self.blocked = asyncio.Event()
@@ -197,58 +199,79 @@ class Connection:
 
     # ------------------------------------------------------------- io
     def _write(self, data: bytes) -> None:
+        """Queue ``data``; everything queued during one event-loop iteration
+        leaves in one ``write`` (a job's ack + publish frames, a delivery's
+        method/header/body) instead of one syscall per frame."""
         if self._writer is None or self._writer.is_closing():
             raise ConnectionClosed(0, "socket closed")
-        self._writer.write(data)
+        self._wbuf.append(data)
+        if not self._flush_scheduled:
+            self._flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._flush)
         self._last_write = time.monotonic()
+
+    def _flush(self) -> None:
+        self._flush_scheduled = False
+        if not self._wbuf:
+            return
+        data = self._wbuf[0] if len(self._wbuf) == 1 else b"".join(self._wbuf)
+        self._wbuf.clear()
+        if self._writer is not None and not self._writer.is_closing():
+            self._writer.write(data)
 
     def _send_method(self, ch: int, m: Method) -> None:
         self._write(codec.method_frame(ch, m))
 
     async def drain(self) -> None:
+        self._flush()
         if self._writer is not None:
             await self._writer.drain()
 
     async def _read_loop(self) -> None:
         err: BaseException = ConnectionClosed(0, "connection lost")
         assert self._reader is not None
+        parser = codec.FrameParser()
         try:
-            while True:
-                ftype, ch, payload = await codec.read_frame(self._reader, self.frame_max if self.frame_max else 0)
-                self._last_read = time.monotonic()
-                if ftype == codec.FRAME_HEARTBEAT:
-                    continue
-                if ch == 0:
-                    if ftype != codec.FRAME_METHOD:
-                        raise codec.FrameError("non-method frame on channel 0")
-                    m = codec.decode_method(payload)
-                    if self._handshake_q is not None and m.name != "connection.close":
-                        self._handshake_q.put_nowait(m)
+            done = False
+            while not done:
+                for ftype, ch, payload in await codec.read_frames(self._reader, parser):
+                    parser.frame_max = self.frame_max or 0
+                    self._last_read = time.monotonic()
+                    if ftype == codec.FRAME_HEARTBEAT:
                         continue
-                    if m.name == "connection.close":
-                        try:
-                            self._send_method(0, Method("connection.close_ok"))
-                        except AMQPError:
-                            pass
-                        if self._handshake_q is not None:
+                    if ch == 0:
+                        if ftype != codec.FRAME_METHOD:
+                            raise codec.FrameError("non-method frame on channel 0")
+                        m = codec.decode_method(payload)
+                        if self._handshake_q is not None and m.name != "connection.close":
                             self._handshake_q.put_nowait(m)
-                        err = ConnectionClosed(m.reply_code, m.reply_text)
-                        break
-                    if m.name == "connection.close_ok":
-                        if self._close_ok and not self._close_ok.done():
-                            self._close_ok.set_result(True)
-                        err = ConnectionClosed(codec.REPLY_SUCCESS, "closed by client")
-                        break
-                    if m.name == "connection.blocked":
-                        self.unblocked.clear()
-                        self.blocked.set()
-                    elif m.name == "connection.unblocked":
-                        self.blocked.clear()
-                        self.unblocked.set()
-                    continue
-                chan = self._channels.get(ch)
-                if chan is not None:
-                    chan._on_frame(ftype, payload)
+                            continue
+                        if m.name == "connection.close":
+                            try:
+                                self._send_method(0, Method("connection.close_ok"))
+                            except AMQPError:
+                                pass
+                            if self._handshake_q is not None:
+                                self._handshake_q.put_nowait(m)
+                            err = ConnectionClosed(m.reply_code, m.reply_text)
+                            done = True
+                            break
+                        if m.name == "connection.close_ok":
+                            if self._close_ok and not self._close_ok.done():
+                                self._close_ok.set_result(True)
+                            err = ConnectionClosed(codec.REPLY_SUCCESS, "closed by client")
+                            done = True
+                            break
+                        if m.name == "connection.blocked":
+                            self.unblocked.clear()
+                            self.blocked.set()
+                        elif m.name == "connection.unblocked":
+                            self.blocked.clear()
+                            self.unblocked.set()
+                        continue
+                    chan = self._channels.get(ch)
+                    if chan is not None:
+                        chan._on_frame(ftype, payload)
         except (asyncio.IncompleteReadError, ConnectionError, OSError) as e:
             err = ConnectionClosed(0, f"connection lost: {e!r}")
         except asyncio.CancelledError:
@@ -286,6 +309,7 @@ class Connection:
         for ch in list(self._channels.values()):
             ch._on_closed(err if isinstance(err, AMQPError) else ConnectionClosed(0, str(err)))
         self._channels.clear()
+        self._flush()
         if self._writer is not None and not self._writer.is_closing():
             self._writer.close()
         me = asyncio.current_task()

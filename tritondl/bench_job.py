@@ -268,16 +268,18 @@ class JobStack:
         import psutil
         me = psutil.Process()
         t = me.cpu_times()
-        out = {"worker": t.user + t.system, "fakes": 0.0}
+        out = {"worker": t.user + t.system, "fakes": 0.0, "broker": 0.0}
         for b in self.backends:
             p = getattr(b, "proc", None)
             if p is None:
                 continue
             try:
                 ft = psutil.Process(p.pid).cpu_times()
-                out["fakes"] += ft.user + ft.system
             except psutil.Error:
-                pass
+                continue
+            out["fakes"] += ft.user + ft.system
+            if b.kind == "broker":
+                out["broker"] += ft.user + ft.system
         return out
 
     def failures(self) -> list:

@@ -133,10 +133,24 @@ class _ServerConn:
         self.closed = False
         self.client_properties: dict = {}
         self.user = ""
+        self._wbuf: list[bytes] = []
+        self._flush_scheduled = False
 
     def send(self, data: bytes) -> None:
+        """Corked: frames queued in one loop iteration go out in one write."""
         if not self.closed and not self.writer.is_closing():
-            self.writer.write(data)
+            self._wbuf.append(data)
+            if not self._flush_scheduled:
+                self._flush_scheduled = True
+                asyncio.get_running_loop().call_soon(self.flush)
+
+    def flush(self) -> None:
+        self._flush_scheduled = False
+        if self._wbuf:
+            data = self._wbuf[0] if len(self._wbuf) == 1 else b"".join(self._wbuf)
+            self._wbuf.clear()
+            if not self.writer.is_closing():
+                self.writer.write(data)
 
     def send_method(self, ch: int, m: Method) -> None:
         self.send(codec.method_frame(ch, m))
@@ -194,6 +208,8 @@ class Broker:
         for c in list(self.conns):
             if graceful:
                 c.send_method(0, Method("connection.close", {"reply_code": code, "reply_text": text}))
+            if graceful:
+                c.flush()
             self._teardown(c)
             try:
                 c.writer.transport.abort() if not graceful else c.writer.close()
@@ -248,29 +264,36 @@ class Broker:
                                                        "consumer_cancel_notify": True,
                                                        "connection.blocked": True, "per_consumer_qos": True}},
                 "mechanisms": b"PLAIN AMQPLAIN", "locales": b"en_US"}))
-            while True:
-                ftype, ch, payload = await codec.read_frame(reader)
-                try:
-                    self._on_frame(c, ftype, ch, payload)
-                except ConnError as e:
-                    c.send_method(0, Method("connection.close", {"reply_code": e.code, "reply_text": e.text[:255],
-                                                                 "class_id": e.cm[0], "method_id": e.cm[1]}))
-                    await writer.drain()
-                    break
-                except ChannelError as e:
-                    sc = c.channels.pop(ch, None)
-                    if sc is not None:
-                        self._close_channel(sc)
-                    c.send_method(ch, Method("channel.close", {"reply_code": e.code, "reply_text": e.text[:255],
-                                                               "class_id": e.cm[0], "method_id": e.cm[1]}))
-                if c.closed:
-                    break
+            parser = codec.FrameParser()
+            done = False
+            while not done:
+                for ftype, ch, payload in await codec.read_frames(reader, parser):
+                    try:
+                        self._on_frame(c, ftype, ch, payload)
+                    except ConnError as e:
+                        c.send_method(0, Method("connection.close", {"reply_code": e.code,
+                                                                     "reply_text": e.text[:255],
+                                                                     "class_id": e.cm[0], "method_id": e.cm[1]}))
+                        c.flush()
+                        await writer.drain()
+                        done = True
+                        break
+                    except ChannelError as e:
+                        sc = c.channels.pop(ch, None)
+                        if sc is not None:
+                            self._close_channel(sc)
+                        c.send_method(ch, Method("channel.close", {"reply_code": e.code, "reply_text": e.text[:255],
+                                                                   "class_id": e.cm[0], "method_id": e.cm[1]}))
+                    if c.closed:
+                        done = True
+                        break
                 await writer.drain()
         except (asyncio.IncompleteReadError, ConnectionError, OSError, codec.FrameError):
             pass
         finally:
             self._teardown(c)
             try:
+                c.flush()
                 writer.close()
             except Exception:
                 pass

@@ -113,6 +113,18 @@ def main() -> None:
     ap.add_argument("--tls-key", default=None)
     ap.add_argument("--rate-mbps", type=float, default=0.0, help="s3: cap ingest at this many Mbit/s (shared link)")
     a = ap.parse_args()
+    prof_path = os.environ.get("TRITONDL_FAKE_PROFILE")          # "<path>.<kind>" gets a cProfile dump
+    if prof_path:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb,
+                               a.encryption, a.tls_cert, a.tls_key, a.rate_mbps))
+        finally:
+            prof.disable()
+            prof.dump_stats(f"{prof_path}.{a.kind}")
+        return
     asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption,
                        a.tls_cert, a.tls_key, a.rate_mbps))
 
