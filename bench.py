@@ -85,6 +85,9 @@ def main() -> int:
                     help="HTTP GET probe size in KiB, the rest as parallel Range streams "
                          "(-1: worker default, 0: open-ended probe)")
     ap.add_argument("--http-segments", type=int, default=0, help="max parallel Range streams (0: worker default)")
+    ap.add_argument("--s3-part-mb", type=int, default=0, help="S3 multipart part size (0: worker default)")
+    ap.add_argument("--s3-multipart-mb", type=int, default=0,
+                    help="objects at least this big go multipart (0: worker default, 64 MiB like minio-go)")
     ap.add_argument("--stripe-kb", type=int, default=-1,
                     help="parallel streams pull in-order stripes of this size (-1: worker default, 0: off)")
     ap.add_argument("--sign-threads", type=int, default=0, help="S3 chunk hashers per PUT (0: worker default)")
@@ -131,6 +134,7 @@ def main() -> int:
                      tag=f"r{rank}", http_probe_bytes=(a.probe_kb << 10) if a.probe_kb >= 0 else -1,
                      http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
                      http_stripe_bytes=(a.stripe_kb << 10) if a.stripe_kb >= 0 else -1,
+                     s3_part_size=a.s3_part_mb << 20, s3_multipart_threshold=a.s3_multipart_mb << 20,
                      payload_mode=a.payload)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
@@ -163,8 +167,10 @@ def main() -> int:
         else:
             loop.run_until_complete(stack.setup())
         c = stack.cfg
-        knobs = {"http_probe_bytes": c.http_probe_bytes, "http_segments": c.http_segments,
-                 "http_stripe_bytes": c.http_stripe_bytes, "s3_sign_threads": c.s3_sign_threads} if c is not None else {}
+        knobs = ({"http_probe_bytes": c.http_probe_bytes, "http_segments": c.http_segments,
+                  "http_stripe_bytes": c.http_stripe_bytes, "s3_sign_threads": c.s3_sign_threads,
+                  "s3_part_size": c.s3_part_size, "s3_multipart_threshold": c.s3_multipart_threshold}
+                 if c is not None else {})
         if a.warmup:
             if shared:
                 loop.run_until_complete(phase(a.warmup))

@@ -94,6 +94,8 @@ class JobStack:
     http_probe_bytes: int = -1       # -1: worker default (Config)
     http_segments: int = 0           # 0: worker default
     http_stripe_bytes: int = -1      # -1: worker default
+    s3_part_size: int = 0            # 0: worker default
+    s3_multipart_threshold: int = 0  # 0: worker default
     sign_threads: int = 0            # 0: worker default
     tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
     payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
@@ -181,6 +183,10 @@ class JobStack:
             cfg.http_segments = self.http_segments
         if self.http_stripe_bytes >= 0:
             cfg.http_stripe_bytes = self.http_stripe_bytes
+        if self.s3_part_size > 0:
+            cfg.s3_part_size = self.s3_part_size
+        if self.s3_multipart_threshold > 0:
+            cfg.s3_multipart_threshold = self.s3_multipart_threshold
         if self.sign_threads > 0:
             cfg.s3_sign_threads = self.sign_threads
         self.cfg = cfg
@@ -188,7 +194,9 @@ class JobStack:
         self.payload_mode = mode
         amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=0, retry_delay=0)
         up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode=mode,
-                                           sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file))
+                                           sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file,
+                                           part_size=cfg.s3_part_size, multipart_threshold=cfg.s3_multipart_threshold,
+                                           parallel_parts=cfg.s3_parallel_parts))
         self.svc = Service(cfg, amqp=amqp, uploader=up)
         await self.svc.start()
         self.converts: list[Convert] = []
