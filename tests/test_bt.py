@@ -497,3 +497,27 @@ def test_redelivered_job_gpu_resume_refetches_only_the_corrupt_piece(tmp_path, d
         _check_tree(str(src), str(dst))
         await seed.stop()
     run(main())
+
+
+def test_torrent_disk_space_preflight(tmp_path, monkeypatch):
+    """Once the info dict is known the torrent checks it fits (minus what is
+    already on disk) before opening storage."""
+    from tritondl.utils import disk
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"big.mkv": 600_000})
+        info = torrent_for(str(src / "big.mkv"), 32768)
+        s = await Seeder(info, str(src)).start()
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        monkeypatch.setattr(disk, "free_bytes", lambda p: 500_000)
+        with pytest.raises(disk.DiskSpaceError, match="not enough disk space"):
+            await _dl().download(str(dst), Sink(), magnet_for(info, peers=[s.addr]))
+        assert not (dst / "big.mkv").exists()
+        # most of it already on disk (a redelivered job): only the rest must fit
+        (dst / "big.mkv").write_bytes((src / "big.mkv").read_bytes()[:300_000])
+        await _dl().download(str(dst), Sink(), magnet_for(info, peers=[s.addr]))
+        assert (dst / "big.mkv").read_bytes() == (src / "big.mkv").read_bytes()
+        await s.stop()
+    run(main())

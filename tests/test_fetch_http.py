@@ -377,3 +377,25 @@ def test_redirects_followed_natively(tmp_path):
         await h.close()
         await o.stop()
     run(main())
+
+
+def test_disk_space_preflight_fails_fast(tmp_path, monkeypatch):
+    """A download that cannot fit fails before writing anything (the reference
+    let grab fill the disk); a resumed download only needs what is missing."""
+    async def main():
+        from tritondl.utils import disk
+        o = await Origin().start()
+        data = os.urandom(400_000)
+        url = o.add("/big.mkv", data)
+        monkeypatch.setattr(disk, "free_bytes", lambda p: 300_000)
+        with pytest.raises(HTTPDownloadError, match="not enough disk space"):
+            await _dl().download(str(tmp_path), Sink(), url)
+        assert not (tmp_path / "big.mkv.part").exists()
+        monkeypatch.setattr(disk, "free_bytes", lambda p: 10**12)
+        h = _dl(disk_reserve=10**12 - 100_000)          # the reserve counts too
+        with pytest.raises(HTTPDownloadError, match="reserve"):
+            await h.download(str(tmp_path), Sink(), url)
+        await _dl().download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "big.mkv").read_bytes() == data
+        await o.stop()
+    run(main())

@@ -33,6 +33,7 @@ import struct
 import time
 from dataclasses import dataclass, field
 
+from ...utils.disk import check_space
 from ...utils.log import log
 from . import merkle, mse
 from . import peer as pw
@@ -64,6 +65,7 @@ class TorrentConfig:
     layer_timeout: float = 120.0     # BEP 52: time to fetch piece layers of a v2 magnet
     upnp: bool = False               # forward the listen port (TCP+UDP) via a UPnP gateway (see .portfwd)
     upnp_ssdp: tuple | None = None   # SSDP target (default: the 239.255.255.250:1900 multicast group)
+    disk_reserve: int = 0            # bytes to keep free on the job's filesystem (utils.disk preflight)
 
 
 @dataclass
@@ -277,6 +279,13 @@ class Torrent:
         """Open storage, verify existing data (resume), start fetching all pieces."""
         assert self.info is not None
         os.makedirs(self.base_dir, exist_ok=True)
+        # free-space preflight: what the layout still needs beyond the bytes on disk
+        have = 0
+        for p, n in self.info.file_paths(self.base_dir):
+            if p:
+                with contextlib.suppress(OSError):
+                    have += min(os.path.getsize(p), n)
+        check_space(self.base_dir, self.info.total_length - have, self.cfg.disk_reserve)
         self.db = CompletionDB(os.path.join(self.base_dir, ".torrent.db"))
         self.storage = FileStorage(self.base_dir, self.info, self.db)
         self.storage.open()

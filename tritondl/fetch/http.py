@@ -53,6 +53,7 @@ import aiohttp
 from yarl import URL
 
 from ..utils import rawhttp
+from ..utils.disk import DiskSpaceError, check_space
 from ..utils.log import log
 from .registry import ClientRegister, ProgressSink
 
@@ -133,8 +134,10 @@ class HTTPDownloader:
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
-                 ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10) -> None:
+                 ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
+                 disk_reserve: int = 0) -> None:
         self.progress_interval = progress_interval
+        self.disk_reserve = disk_reserve            # bytes to keep free (utils.disk preflight)
         self.max_redirects = max_redirects          # Go's http.Client default (grab uses it)
         # >0: instead of `segments` contiguous slices, the file is cut into stripes of
         # this size handed out IN ORDER to `segments` stream workers (each reuses its
@@ -372,7 +375,15 @@ class HTTPDownloader:
             if first is not None:                # resume uses ranged requests with If-Range
                 first.close()
                 first = None
-        else:
+        if probe.size:
+            have = sum(sg[2] for sg in segs) if resumable else 0
+            try:
+                check_space(base_dir, probe.size - have, self.disk_reserve)
+            except DiskSpaceError as e:
+                if first is not None:
+                    first.close()
+                raise HTTPDownloadError(str(e)) from e
+        if not resumable:
             fd = os.open(part, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
             try:
                 if probe.size:

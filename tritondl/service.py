@@ -61,7 +61,8 @@ def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
     http = HTTPDownloader(progress_interval=cfg.progress_interval_s, segments=cfg.http_segments,
                           segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes,
-                          ca_file=cfg.ca_file, stripe_bytes=cfg.http_stripe_bytes)
+                          ca_file=cfg.ca_file, stripe_bytes=cfg.http_stripe_bytes,
+                          disk_reserve=cfg.disk_reserve_bytes)
     impls: list[ClientImpl] = []
     try:
         from .fetch.bt.client import TorrentDownloader

@@ -67,6 +67,7 @@ class Config:
     dead_letter_topic: str = ""                 # "" => "<consume_topic>.dead"
     drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
     cleanup: bool = False                       # B15: off for parity
+    disk_reserve_bytes: int = 0                 # free-space preflight keeps this much free
     stream_upload: bool = True                  # overlap HTTP fetch with S3 upload
     http_segments: int = 4                      # max parallel Range streams per HTTP file
     http_segment_threshold: int = 64 * 1024 * 1024   # open-ended probe only: segment files at least this big
@@ -145,7 +146,7 @@ class Config:
                 "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
                 "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
                 "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
-                "HTTP_STRIPE_BYTES": "http_stripe_bytes"}
+                "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
