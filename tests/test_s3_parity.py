@@ -238,3 +238,72 @@ def test_multipart_upload_respects_limits_end_to_end(tmp_path):
         await c.close()
         await s3.stop()
     run(main())
+
+
+# --------------------------------------------------------------- resumable multipart
+
+def test_interrupted_multipart_upload_resumes_from_landed_parts(tmp_path):
+    """Beyond minio-go (which starts a failed multipart upload over): with a
+    state file the upload is kept open on failure, and the retry lists its
+    parts (paged), re-sends only parts S3 does not hold — a part whose local
+    bytes no longer match its ETag (MD5) is re-sent — and completes it."""
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk", store="memory").start()
+        s3.create_bucket("b")
+        s3.list_parts_page = 1                               # exercise ListParts paging
+        c = S3Client(s3.endpoint, Static("ak", "sk"), part_size=5 << 20, multipart_threshold=5 << 20,
+                     parallel_parts=1, max_retries=0)
+        data = bytearray(os.urandom((17 << 20) + 999))       # 4 parts
+        p = tmp_path / "show.mkv"
+        p.write_bytes(data)
+        state = str(p) + ".s3upload"
+        s3.fail_parts = {3}
+        with pytest.raises(S3Error):
+            await c.put_object("b", "k", str(p), resume_path=state)
+        assert os.path.exists(state) and len(s3.uploads) == 1          # kept open, not aborted
+        up = next(iter(s3.uploads.values()))
+        assert sorted(up.parts) == [1, 2]
+        # the local bytes of part 2 changed since (re-downloaded file): it must go again
+        data[(5 << 20) + 10] ^= 0xFF
+        p.write_bytes(data)
+        s3.fail_parts = set()
+        n0 = len(s3.requests)
+        await c.put_object("b", "k", str(p), resume_path=state)
+        sent = [r[1] for r in s3.requests[n0:] if r[0] == "PUT"]
+        assert sorted(int(x.split("partNumber=")[1].split("&")[0]) for x in sent) == [2, 3, 4]
+        assert s3.object_bytes("b", "k") == bytes(data)
+        assert not os.path.exists(state) and not s3.uploads
+        # without a state file a failure aborts the upload (minio-go behaviour)
+        s3.fail_parts = {2}
+        with pytest.raises(S3Error):
+            await c.put_object("b", "k2", str(p))
+        assert not s3.uploads
+        await c.close()
+        await s3.stop()
+    run(main())
+
+
+def test_stale_resume_state_starts_over(tmp_path):
+    """A state file whose upload the server no longer has (aborted by a
+    lifecycle rule) or that describes another object is ignored."""
+    import json
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk", store="memory").start()
+        s3.create_bucket("b")
+        c = S3Client(s3.endpoint, Static("ak", "sk"), part_size=5 << 20, multipart_threshold=5 << 20)
+        data = os.urandom((11 << 20) + 1)
+        p = tmp_path / "f.mkv"
+        p.write_bytes(data)
+        state = str(p) + ".s3upload"
+        with open(state, "w") as f:
+            json.dump({"bucket": "b", "key": "k", "size": len(data), "part_size": 5 << 20,
+                       "upload_id": "upload-does-not-exist"}, f)
+        await c.put_object("b", "k", str(p), resume_path=state)
+        assert s3.object_bytes("b", "k") == data and not os.path.exists(state)
+        with open(state, "w") as f:
+            json.dump({"bucket": "other", "key": "k", "size": 1, "part_size": 5, "upload_id": "x"}, f)
+        await c.put_object("b", "k", str(p), resume_path=state)
+        assert s3.object_bytes("b", "k") == data
+        await c.close()
+        await s3.stop()
+    run(main())

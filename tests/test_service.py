@@ -406,3 +406,29 @@ def test_magnet_job_streamed_upload_failure_fails_job(tmp_path):
         await tr.stop()
         await e.down()
     run(main())
+
+
+def test_failed_multipart_upload_resumes_on_retry(tmp_path):
+    """An S3 failure mid multipart upload fails the job; the retry (broker
+    delay queue) finds the file already downloaded and continues the kept
+    upload: parts that landed are not sent again."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=2)
+        c = e.svc.uploader.client
+        c.part_size, c.multipart_threshold, c.parallel_parts, c.max_retries = 5 << 20, 5 << 20, 1, 0
+        e.s3.store = "memory"
+        data = os.urandom((16 << 20) + 77)
+        url = e.origin.add("/season/pack.mkv", data)
+        e.s3.fail_parts = {3}
+        e.submit(Media(id="mp-1", source_uri=url))
+        res = await e.wait_results(1, timeout=60)
+        assert not res[0].ok and res[0].stage == "upload"
+        e.s3.fail_parts = set()
+        res = await e.wait_results(2, timeout=60)
+        assert res[1].ok, res[1]
+        parts = [int(r[1].split("partNumber=")[1].split("&")[0]) for r in e.s3.requests
+                 if r[0] == "PUT" and "partNumber=" in r[1]]
+        assert parts == [1, 2, 3, 3, 4], parts          # 1st try: 1, 2, (3 failed); retry: 3, 4
+        assert e.s3.object_bytes("triton-staging", object_key("mp-1", "pack.mkv")) == data
+        await e.down()
+    run(main())

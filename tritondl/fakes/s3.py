@@ -83,6 +83,8 @@ class FakeS3:
         self.root = root
         self.buckets: dict[str, dict[str, Obj]] = {}
         self.uploads: dict[str, Upload] = {}
+        self.list_parts_page = 1000
+        self.fail_parts: set[int] = set()       # fault injection: these part numbers get HTTP 500
         self._ids = itertools.count(1)
         self._fail = 0
         self._fail_status = 503
@@ -405,6 +407,9 @@ class FakeS3:
                 await request.read()
                 return _xml_err(404, "NoSuchUpload", "no such upload")
             pn = int(q.get("partNumber", "0") or 0)
+            if pn in self.fail_parts:
+                await request.read()
+                return _xml_err(500, "InternalError", "injected part failure")
             if self.strict_parts and not 1 <= pn <= 10000:
                 await request.read()
                 return _xml_err(400, "InvalidArgument", "Part number must be an integer between 1 and 10000")
@@ -463,6 +468,23 @@ class FakeS3:
         if m == "DELETE" and "uploadId" in q:
             self.uploads.pop(q["uploadId"], None)
             return web.Response(status=204)
+        if m == "GET" and "uploadId" in q:                   # ListParts, paged like S3 (max-parts, marker)
+            up = self.uploads.get(q["uploadId"])
+            if up is None or up.key != key:
+                return _xml_err(404, "NoSuchUpload", "The specified upload does not exist.")
+            marker = int(q.get("part-number-marker", "0") or 0)
+            maxp = int(q.get("max-parts", str(self.list_parts_page)) or self.list_parts_page)
+            nums = sorted(n for n in up.parts if n > marker)
+            page, more = nums[:maxp], len(nums) > maxp
+            xml = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>\"{up.parts[n].etag}\"</ETag>"
+                          f"<Size>{up.parts[n].size}</Size></Part>" for n in page)
+            body = (f"<ListPartsResult xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\"><Bucket>{bucket}</Bucket>"
+                    f"<Key>{_xml_escape(key)}</Key><UploadId>{q['uploadId']}</UploadId>"
+                    f"<PartNumberMarker>{marker}</PartNumberMarker>"
+                    f"<NextPartNumberMarker>{page[-1] if page else marker}</NextPartNumberMarker>"
+                    f"<MaxParts>{maxp}</MaxParts><IsTruncated>{'true' if more else 'false'}</IsTruncated>"
+                    f"{xml}</ListPartsResult>")
+            return web.Response(body=body.encode(), content_type="application/xml")
         if m in ("GET", "HEAD"):
             o = objs.get(key)
             if o is None:

@@ -26,6 +26,8 @@ minio-go library behaviours the reference relied on without naming them:
 from __future__ import annotations
 
 import asyncio
+import contextlib
+import json
 import os
 import re
 import xml.etree.ElementTree as ET
@@ -82,6 +84,14 @@ def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Err
         code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
                 resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
     return S3Error(status, code, msg, resource, region)
+
+
+def _save_json(path: str, obj: dict) -> None:
+    tmp = path + ".tmp"
+    with contextlib.suppress(OSError):
+        with open(tmp, "w") as f:
+            json.dump(obj, f)
+        os.replace(tmp, path)
 
 
 def plan_parts(size: int, part_size: int) -> tuple[int, int]:
@@ -367,8 +377,14 @@ class S3Client:
 
     # ------------------------------------------------------------ objects
     async def put_object(self, bucket: str, key: str, src: str | bytes | int, size: int | None = None,
-                         content_type: str = "application/octet-stream", wait_bytes=None, flow=None) -> str:
+                         content_type: str = "application/octet-stream", wait_bytes=None, flow=None,
+                         resume_path: str | None = None) -> str:
         """Upload a file path or fd (streamed) or bytes; returns the ETag.
+
+        ``resume_path``: a state file for multipart uploads — an interrupted
+        upload is kept open (not aborted) and a later call with the same
+        state continues it, re-sending only parts whose bytes S3 does not
+        already hold (checked by MD5 against the local file).
 
         ``wait_bytes(n)`` (optional coroutine) is awaited before bytes < n are
         read — lets the upload follow a file that is still being downloaded.
@@ -382,7 +398,7 @@ class S3Client:
             else:
                 size = os.path.getsize(src)
         if size > MAX_SINGLE_PUT or (size >= self.multipart_threshold and size > self.part_size):
-            return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes, flow)
+            return await self._put_multipart(bucket, key, src, size, content_type, wait_bytes, flow, resume_path)
         return await self._put_range(bucket, key, src, 0, size, {"content-type": content_type},
                                      wait_bytes=wait_bytes, flow=flow)
 
@@ -397,18 +413,80 @@ class S3Client:
         _st, rh, _b = await self._do("PUT", bucket, key, query=query, headers=headers, body_factory=factory)
         return rh.get("ETag", "").strip('"')
 
+    async def list_parts(self, bucket: str, key: str, upload_id: str) -> dict[int, tuple[str, int]]:
+        """ListParts (paged by ``part-number-marker``): {part number: (etag, size)}."""
+        out: dict[int, tuple[str, int]] = {}
+        marker = "0"
+        while True:
+            _st, _h, body = await self._do("GET", bucket, key, query={"uploadId": upload_id,
+                                                                       "part-number-marker": marker})
+            root = ET.fromstring(body)
+            for part in root.iter():
+                if part.tag.rsplit("}", 1)[-1] != "Part":
+                    continue
+                f = {c.tag.rsplit("}", 1)[-1]: (c.text or "") for c in part}
+                out[int(f["PartNumber"])] = (f.get("ETag", "").strip('"'), int(f.get("Size", "0") or 0))
+            trunc = (root.findtext(f"{S3_NS}IsTruncated") or root.findtext("IsTruncated") or "false")
+            marker = root.findtext(f"{S3_NS}NextPartNumberMarker") or root.findtext("NextPartNumberMarker") or ""
+            if trunc.lower() != "true" or not marker:
+                return out
+
+    async def _resume_parts(self, state_path: str, bucket: str, key: str, src, size: int, part_size: int,
+                            nparts: int) -> tuple[str, dict[int, str]]:
+        """(upload id, {part index: etag}) of an interrupted multipart upload of
+        this object that can be continued: same bucket/key/size/part size,
+        the upload still open on the server, and every reused part's ETag
+        equal to the MD5 of the local bytes it claims to hold."""
+        try:
+            with open(state_path) as f:
+                st = json.load(f)
+        except (OSError, ValueError):
+            return "", {}
+        if (st.get("bucket"), st.get("key"), st.get("size"), st.get("part_size")) != (bucket, key, size, part_size):
+            return "", {}
+        uid = st.get("upload_id") or ""
+        try:
+            listed = await self.list_parts(bucket, key, uid)
+        except S3Error as e:
+            log.with_fields(key=key, error=str(e)).info("interrupted multipart upload is gone; starting over")
+            return "", {}
+        path = src if isinstance(src, str) else f"/proc/self/fd/{src}" if isinstance(src, int) else None
+        want = {pn: tag for pn, (tag, sz) in listed.items()
+                if 1 <= pn <= nparts and sz == min(part_size, size - (pn - 1) * part_size) and len(tag) == 32}
+        if path is None or not want:
+            return uid, {}
+
+        def md5_of(pn: int) -> str:
+            off = (pn - 1) * part_size
+            return hashing.hash_file(path, ["md5"], off, min(part_size, size - off))["md5"].hex()
+        loop = asyncio.get_running_loop()
+        sums = await asyncio.gather(*(loop.run_in_executor(None, md5_of, pn) for pn in want))
+        ok = {pn - 1: tag for (pn, tag), got in zip(want.items(), sums) if got == tag}
+        log.with_fields(key=key, upload_id=uid, reused_parts=len(ok), of=nparts).info(
+            "resuming interrupted multipart upload")
+        return uid, ok
+
     async def _put_multipart(self, bucket: str, key: str, src: str | bytes | int, size: int, content_type: str,
-                             wait_bytes=None, flow=None) -> str:
+                             wait_bytes=None, flow=None, resume_path: str | None = None) -> str:
         plan_parts(size, self.part_size)           # refuse > 5 TiB before initiating
-        _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
-                                       headers={"content-type": content_type}, body=b"")
-        root = ET.fromstring(body)
-        upload_id = root.findtext(f"{S3_NS}UploadId") or root.findtext("UploadId") or ""
-        if not upload_id:
-            raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
         part_size, nparts = plan_parts(size, self.part_size)
+        upload_id, reused = ("", {})
+        if resume_path and not isinstance(src, (bytes, bytearray, memoryview)):
+            upload_id, reused = await self._resume_parts(resume_path, bucket, key, src, size, part_size, nparts)
+        if not upload_id:
+            _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
+                                           headers={"content-type": content_type}, body=b"")
+            root = ET.fromstring(body)
+            upload_id = root.findtext(f"{S3_NS}UploadId") or root.findtext("UploadId") or ""
+            if not upload_id:
+                raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
+        if resume_path:
+            _save_json(resume_path, {"bucket": bucket, "key": key, "size": size, "part_size": part_size,
+                                     "upload_id": upload_id})
         etags: list[str] = [""] * nparts
-        todo = _PartQueue(nparts, part_size, size, flow)
+        for i, tag in reused.items():
+            etags[i] = tag
+        todo = _PartQueue(nparts, part_size, size, flow, skip=reused)
 
         async def worker() -> None:
             while todo:
@@ -435,8 +513,19 @@ class S3Client:
             if b"<Error>" in rb:
                 raise _parse_error(200, rb, f"complete {key}")
             r = ET.fromstring(rb)
+            if resume_path:
+                with contextlib.suppress(OSError):
+                    os.remove(resume_path)
             return (r.findtext(f"{S3_NS}ETag") or r.findtext("ETag") or "").strip('"')
-        except BaseException:
+        except BaseException as e:
+            if resume_path and not isinstance(e, asyncio.CancelledError):
+                # keep the upload: a retry of this job continues from the parts that landed
+                # (stale uploads are the bucket lifecycle's AbortIncompleteMultipartUpload job)
+                log.with_fields(key=key, upload_id=upload_id).warn("multipart upload interrupted; kept for resume")
+                raise
+            if resume_path:
+                with contextlib.suppress(OSError):
+                    os.remove(resume_path)
             try:
                 await self._do("DELETE", bucket, key, query={"uploadId": upload_id}, expect=(204, 200),
                                retry=False)
@@ -581,10 +670,12 @@ class _PartQueue:
     costs O(runs + segments), not O(pending parts), so 10,000-part uploads stay
     cheap.  Without a flow (or once it finished) parts go in order."""
 
-    def __init__(self, nparts: int, part_size: int, size: int, flow=None) -> None:
+    def __init__(self, nparts: int, part_size: int, size: int, flow=None, skip=()) -> None:
         self.part_size, self.size, self.flow = part_size, size, flow
-        self._todo = list(range(nparts))          # ascending
-        self._runs = {0} if nparts else set()     # parts that start a run of pending parts
+        skip = set(skip)
+        self._todo = [p for p in range(nparts) if p not in skip]              # ascending
+        pending = set(self._todo)
+        self._runs = {p for p in self._todo if p - 1 not in pending}        # parts that start a run
 
     def __len__(self) -> int:
         return len(self._todo)

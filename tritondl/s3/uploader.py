@@ -51,6 +51,10 @@ class UploadError(Exception):
     pass
 
 
+# next to each local file: the state of its interrupted multipart upload (resume on redelivery)
+RESUME_SUFFIX = ".s3upload"
+
+
 class Uploader:
     def __init__(self, bucket: str, client: S3Client, *, file_concurrency: int = 2) -> None:
         self.heals = 0
@@ -115,7 +119,8 @@ class Uploader:
                 key = object_key(media_id, path)
                 log.info("starting upload of file '%s'", go_base(key))
                 try:
-                    etag = await self._healing(lambda: self.client.put_object(self.bucket, key, path, size))
+                    etag = await self._healing(lambda: self.client.put_object(
+                        self.bucket, key, path, size, resume_path=path + RESUME_SUFFIX))
                 except (S3Error, OSError) as e:
                     raise UploadError(f"failed to upload file {path}: {e}") from e
                 log.info("finished upload")
@@ -124,7 +129,7 @@ class Uploader:
         return list(await asyncio.gather(*(one(f) for f in files)))
 
     async def upload_stream(self, media_id: str, name: str, src: int | str, size: int, wait_bytes=None,
-                            flow=None) -> UploadResult:
+                            flow=None, resume_path: str | None = None) -> UploadResult:
         """Upload one file that may still be growing (``wait_bytes`` gates reads;
         ``flow`` is the download's native progress, followed without Python)."""
         await self.ensure_bucket()
@@ -132,7 +137,8 @@ class Uploader:
         log.info("starting upload of file '%s'", go_base(key))
         try:
             etag = await self._healing(lambda: self.client.put_object(self.bucket, key, src, size,
-                                                                      wait_bytes=wait_bytes, flow=flow))
+                                                                      wait_bytes=wait_bytes, flow=flow,
+                                                                      resume_path=resume_path))
         except (S3Error, OSError) as e:
             raise UploadError(f"failed to upload file {name}: {e}") from e
         log.info("finished upload")

@@ -47,7 +47,7 @@ from .amqp.client import Client, Delivery
 from .fetch.http import HTTPDownloader
 from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
-from .s3.uploader import UploadError, Uploader
+from .s3.uploader import RESUME_SUFFIX, UploadError, Uploader
 from .select import MEDIA_EXTS, dir_media, predict_media
 from .utils import rawhttp
 from .utils.config import Config
@@ -294,7 +294,8 @@ class Service:
         if h.size and go_ext(h.filename) in MEDIA_EXTS:
             fd = h.open_reader()
             up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes,
-                                                                   flow=h.flow))
+                                                                   flow=h.flow,
+                                                                   resume_path=h.dst + RESUME_SUFFIX))
         try:
             await h.wait()
             if marks is not None:
