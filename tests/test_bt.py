@@ -521,3 +521,23 @@ def test_torrent_disk_space_preflight(tmp_path, monkeypatch):
         assert (dst / "big.mkv").read_bytes() == (src / "big.mkv").read_bytes()
         await s.stop()
     run(main())
+
+
+def test_ipv6_peer_dials_dual_stack_listener(tmp_path):
+    """The listen port is also bound on IPv6 (peers from the IPv6 DHT / PEX
+    are announced with it); an IPv6 x.pe peer ([::1]:port, BEP 9) serves the
+    whole download."""
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"v6.mkv": 300_000})
+        info = torrent_for(str(src / "v6.mkv"), 16384)
+        s = await Seeder(info, str(src), listen_host6="::1").start()
+        uri = magnet_for(info, peers=[("::1", s.torrent.port)])
+        assert f"x.pe=[::1]:{s.torrent.port}" in uri
+        assert parse_magnet(uri).peers == [("::1", s.torrent.port)]
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        await _dl().download(str(dst), Sink(), uri)
+        assert (dst / "v6.mkv").read_bytes() == (src / "v6.mkv").read_bytes()
+        await s.stop()
+    run(main())

@@ -167,13 +167,14 @@ class Seeder:
 
     def __init__(self, info: Info, data_dir: str, *, trackers: list[str] | None = None,
                  dht_bootstrap: list[tuple[str, int]] | None = None, corrupt: bool = False,
-                 encryption: str = "allow") -> None:
+                 encryption: str = "allow", listen_host6: str | None = None) -> None:
         self.info = info
         self.data_dir = data_dir
         self.trackers = trackers or []
         self.dht_bootstrap = dht_bootstrap
         self.corrupt = corrupt
         self.encryption = encryption
+        self.listen_host6 = listen_host6
         self.torrent: Torrent | None = None
         self.dht: DHTNode | None = None
 
@@ -182,7 +183,7 @@ class Seeder:
             self.dht = await DHTNode(host="127.0.0.1", bootstrap=self.dht_bootstrap).start()
             await self.dht.bootstrap()
         cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, tracker_min_interval=1.0, dht_interval=1.0,
-                            verify_device="cpu", encryption=self.encryption)
+                            verify_device="cpu", encryption=self.encryption, listen_host6=self.listen_host6)
         t = Torrent(self.info.infohash, self.data_dir, cfg, info=self.info, trackers=self.trackers, dht=self.dht)
         await t.start()
         await t.download_all()

@@ -371,7 +371,7 @@ class Magnet:
         if self.display_name:
             parts.append("dn=" + quote(self.display_name))
         parts += ["tr=" + quote(t, safe="") for t in self.trackers]
-        parts += [f"x.pe={h}:{p}" for h, p in self.peers]
+        parts += [f"x.pe=[{h}]:{p}" if ":" in h else f"x.pe={h}:{p}" for h, p in self.peers]
         parts += ["ws=" + quote(w, safe="") for w in self.web_seeds]
         return "magnet:?" + "&".join(parts)
 

@@ -29,6 +29,7 @@ import hashlib
 import math
 import os
 import random
+import socket
 import struct
 import time
 from dataclasses import dataclass, field
@@ -66,6 +67,7 @@ class TorrentConfig:
     upnp: bool = False               # forward the listen port (TCP+UDP) via a UPnP gateway (see .portfwd)
     upnp_ssdp: tuple | None = None   # SSDP target (default: the 239.255.255.250:1900 multicast group)
     disk_reserve: int = 0            # bytes to keep free on the job's filesystem (utils.disk preflight)
+    listen_host6: str | None = None  # also accept peers on IPv6 (same port), e.g. "::"
 
 
 @dataclass
@@ -180,6 +182,7 @@ class Torrent:
         self._meta: dict[int, bytes] = {}
         self._tasks: set[asyncio.Task] = set()
         self._server: asyncio.AbstractServer | None = None
+        self._server6: asyncio.AbstractServer | None = None
         self.port = 0
         self.utp = None
         self.portfwd = None
@@ -200,6 +203,18 @@ class Torrent:
     async def start(self) -> None:
         self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
         self.port = self._server.sockets[0].getsockname()[1]
+        if self.cfg.listen_host6 is not None:
+            # dual stack like anacrolix: the same port on IPv6, so peers learnt from the
+            # IPv6 DHT / PEX (announced with this port) can dial in
+            try:
+                s6 = socket.socket(socket.AF_INET6, socket.SOCK_STREAM)
+                s6.setsockopt(socket.IPPROTO_IPV6, socket.IPV6_V6ONLY, 1)
+                s6.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                s6.bind((self.cfg.listen_host6, self.port))
+                self._server6 = await asyncio.start_server(self._on_inbound, sock=s6)
+            except OSError as e:
+                log.with_field("error", str(e)).debug("IPv6 listen socket unavailable")
+                self._server6 = None
         if self.cfg.utp:
             from .utp import UtpSocket
             try:  # uTP shares the TCP port number, as anacrolix/libutp do
@@ -240,6 +255,8 @@ class Torrent:
         self.closed = True
         if self._server is not None:
             self._server.close()
+        if self._server6 is not None:
+            self._server6.close()
         if self.utp is not None:
             self.utp.close()
         for p in list(self.peers.values()):
