@@ -1,0 +1,110 @@
+"""Native peer-wire data plane (csrc/btwire): block assembly into the shared
+piece store, request pipelining, choke/reject handling, end-game cancels."""
+
+import struct
+
+import pytest
+
+from tritondl import _btwire as W
+
+B = W.BLOCK
+
+
+def msgs(out: bytes):
+    """Split a peer-wire byte stream into (id, payload) messages."""
+    res, pos = [], 0
+    while pos < len(out):
+        (n,) = struct.unpack(">I", out[pos:pos + 4])
+        res.append((out[pos + 4], out[pos + 5:pos + 4 + n]))
+        pos += 4 + n
+    return res
+
+
+def piece_msg(i, off, data):
+    return struct.pack(">IBII", 9 + len(data), 7, i, off) + data
+
+
+def test_requests_pipeline_and_completion():
+    store = W.PieceStore(3, 4 * B, 10 * B + 100)          # pieces of 4, 4, 2(+100 B) blocks
+    assert [store.blocks(i) for i in range(3)] == [4, 4, 3] and store.piece_size(2) == 2 * B + 100
+    link = W.Link(store, pipeline=5)
+    link.assign(0)
+    link.assign(2)
+    assert link.pump() == b""                              # choked: nothing requested yet
+    ev, out = link.feed(b"\x00\x00\x00\x01\x01")         # UNCHOKE
+    assert list(ev) == [("unchoke",)]
+    reqs = [struct.unpack(">III", p) for mid, p in msgs(out) if mid == 6]
+    assert reqs == [(0, 0, B), (0, B, B), (0, 2 * B, B), (0, 3 * B, B), (2, 0, B)]
+    assert link.need_work() and link.outstanding == 5      # only 2 unrequested blocks queued behind the pipeline
+    data0 = bytes(range(256)) * (4 * B // 256)
+    stream = b"".join(piece_msg(0, k * B, data0[k * B:(k + 1) * B]) for k in range(4))
+    ev, out = link.feed(stream[:1000])                    # partial message: buffered
+    assert list(ev) == [] and link.buffered == 1000
+    ev, out = link.feed(stream[1000:])
+    assert list(ev) == [("piece", 0)]
+    assert store.take(0) == data0 and not store.active(0)
+    # the freed pipeline slots went to the rest of piece 2 (the tail block is short)
+    reqs = [struct.unpack(">III", p) for mid, p in msgs(out) if mid == 6]
+    assert reqs == [(2, B, B), (2, 2 * B, 100)]
+    assert link.downloaded == 4 * B
+
+
+def test_choke_lapses_and_reject_rerequests():
+    store = W.PieceStore(1, 4 * B, 4 * B)
+    link = W.Link(store, pipeline=4, fast=False)
+    link.assign(0)
+    link.peer_choking = False
+    assert len(msgs(link.pump())) == 4
+    ev, out = link.feed(b"\x00\x00\x00\x01\x00")         # CHOKE drops every pending request
+    assert list(ev) == [("choke",)] and link.outstanding == 0 and out == b""
+    ev, out = link.feed(b"\x00\x00\x00\x01\x01")
+    assert len([m for m in msgs(out) if m[0] == 6]) == 4     # all asked for again after UNCHOKE
+    fast = W.Link(W.PieceStore(1, 2 * B, 2 * B), pipeline=4, fast=True)
+    fast.assign(0)
+    fast.peer_choking = False
+    fast.pump()
+    ev, out = fast.feed(b"\x00\x00\x00\x01\x00")          # BEP 6: choke does not drop requests
+    assert fast.outstanding == 2
+    fast.peer_choking = False
+    rej = struct.pack(">IBIII", 13, 16, 0, B, B)             # ... an explicit REJECT does
+    ev, out = fast.feed(rej)
+    assert [struct.unpack(">III", p) for m, p in msgs(out) if m == 6] == [(0, B, B)]
+
+
+def test_endgame_two_links_share_the_store_and_cancel():
+    store = W.PieceStore(1, 2 * B, 2 * B)
+    a, b = W.Link(store, 8), W.Link(store, 8)
+    for l in (a, b):
+        l.assign(0)
+        l.peer_choking = False
+        assert len(msgs(l.pump())) == 2                    # both ask for both blocks (end game)
+    ev, _ = a.feed(piece_msg(0, 0, b"x" * B))
+    assert list(ev) == []
+    ev, _ = b.feed(piece_msg(0, B, b"y" * B))
+    assert list(ev) == [("piece", 0)]                      # completed by the second link's block
+    a.piece_done(0)
+    cancels = [struct.unpack(">III", p) for m, p in msgs(a.pump()) if m == 8]
+    assert sorted(cancels) == [(0, B, B)]                 # a still had block 1 outstanding
+    assert store.take(0) == b"x" * B + b"y" * B
+    ev, _ = a.feed(piece_msg(0, 0, b"z" * B))             # late duplicate: ignored
+    assert list(ev) == []
+
+
+def test_forwarded_messages_and_protocol_errors():
+    store = W.PieceStore(2, B, 2 * B)
+    link = W.Link(store, 4)
+    have = struct.pack(">IBI", 5, 4, 1)
+    ev, _ = link.feed(b"\x00\x00\x00\x00" + have)         # keep-alive + HAVE 1
+    assert list(ev) == [("msg", 4, b"\x00\x00\x00\x01")]
+    store.begin(0)
+    ev, _ = link.feed(piece_msg(0, 3, b"q" * B))           # misaligned block
+    assert ev[-1][0] == "bad"
+    link2 = W.Link(store, 4)
+    ev, _ = link2.feed(struct.pack(">I", 64 << 20))        # absurd length
+    assert ev[-1] == ("bad", "message too large")
+    link3 = W.Link(store, 4)
+    ev, _ = link3.feed(piece_msg(9, 0, b"q" * 10))
+    assert ev[-1][0] == "bad"
+    with pytest.raises(IndexError):
+        link3.assign(7)
+    assert store.partial_bytes == 0

@@ -39,6 +39,8 @@ async def main() -> int:
     ap.add_argument("--profile", default="")
     ap.add_argument("--encryption", default="allow", help="MSE policy for seeders and leecher")
     ap.add_argument("--job", action="store_true", help="full worker job (download+upload+publish+ack)")
+    ap.add_argument("--python-wire", action="store_true",
+                    help="leecher: per-block work in Python instead of the native csrc/btwire link")
     ap.add_argument("--files", type=int, default=8, help="--job: media files in the pack")
     ap.add_argument("--stream", default="both", choices=["on", "off", "both"])
     ap.add_argument("--repeat", type=int, default=2)
@@ -72,7 +74,7 @@ async def main() -> int:
         dst = os.path.join(td, "dst")
         os.makedirs(dst)
         d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
-                                            encryption=a.encryption),
+                                            encryption=a.encryption, native_wire=not a.python_wire),
                               progress_interval=1.0, use_dht=False)
         prof = None
         if a.profile:
@@ -90,7 +92,8 @@ async def main() -> int:
         print(json.dumps({"metric": "bt_ingest_MB_per_sec", "value": round(a.mb * 1.048576 / dt, 1),
                           "seconds": round(dt, 3), "mb": a.mb, "seeds": a.seeds, "piece_kb": a.piece_kb,
                           "transport": "utp" if a.utp else "tcp+utp",
-                          "encryption": a.encryption}), flush=True)
+                          "encryption": a.encryption, "wire": "python" if a.python_wire else "native"}),
+              flush=True)
     finally:
         for s in seeds:
             await s.stop()

@@ -5,6 +5,7 @@
 * ``tritondl/_gpu_hash*.so``   – hipcc --offload-arch=gfx950 (HIP kernels)
 * ``tritondl/_relay*.so``      – g++  (native fetch -> S3 data plane + OpenSSL TLS streams, pybind11)
 * ``tritondl/_utp*.so``        – g++  (uTP / LEDBAT transport, pybind11)
+* ``tritondl/_btwire*.so``     – g++  (BitTorrent peer-wire parser + block assembly, pybind11)
 
 Rebuilds only when a source is newer than its output.  ``--force`` rebuilds.
 Cross-compiles fine without a GPU (hipcc needs no device).
@@ -61,6 +62,12 @@ TARGETS = {
         "cc": "g++",
         "flags": ["-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread", "-Wall"],
         "libs": ["-lssl", "-lcrypto"],
+    },
+    "_btwire": {
+        "srcs": ["csrc/btwire/btwire.cpp"],
+        "cc": "g++",
+        "flags": ["-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread", "-Wall"],
+        "libs": [],
     },
     "_utp": {
         "srcs": ["csrc/utp/utp.cpp"],

@@ -125,6 +125,18 @@ class Wire:
                 return msgs
             await self._fill()
 
+    async def read_raw(self) -> bytes:
+        """The next chunk of the byte stream, unparsed (the native link parses
+        it): whatever the message parser had buffered first, else one read."""
+        if self._rbuf:
+            data = bytes(self._rbuf)
+            self._rbuf.clear()
+            return data
+        data = await self.reader.read(1 << 18)
+        if not data:
+            raise asyncio.IncompleteReadError(b"", None)
+        return data
+
     async def _fill(self) -> None:
         data = await self.reader.read(1 << 18)
         if not data:

@@ -43,6 +43,11 @@ from .metainfo import BLOCK, Info, MetainfoError
 from .storage import CompletionDB, FileStorage
 from .tracker import Announce, TrackerError, announce, new_peer_id
 
+try:  # native peer-wire data plane (csrc/btwire): block assembly + request pipelining
+    from ... import _btwire as _W  # type: ignore[attr-defined]
+except ImportError:  # pragma: no cover - the extension ships with every build
+    _W = None
+
 
 @dataclass
 class TorrentConfig:
@@ -68,6 +73,7 @@ class TorrentConfig:
     upnp_ssdp: tuple | None = None   # SSDP target (default: the 239.255.255.250:1900 multicast group)
     disk_reserve: int = 0            # bytes to keep free on the job's filesystem (utils.disk preflight)
     listen_host6: str | None = None  # also accept peers on IPv6 (same port), e.g. "::"
+    native_wire: bool = True         # per-block work in csrc/btwire (False: the pure-Python path)
 
 
 @dataclass
@@ -123,6 +129,7 @@ class _Peer:
         self.bad = 0
         self.downloaded = 0
         self.meta_requested = False
+        self.link = None                                    # _btwire.Link once the native data plane runs
 
     def set_have(self, i: int) -> bool:
         if 0 <= i < len(self.have) and not self.have[i]:
@@ -165,6 +172,8 @@ class Torrent:
         self._rare_t = 0.0
         self._rare_dirty = True
         self._finishers: set[asyncio.Task] = set()
+        self.store = None                               # _btwire.PieceStore (native data plane)
+        self.assigned: dict[int, set] = {}              # piece -> peer keys whose links fetch it
         # per-file completion (streamed uploads): see watch_files
         self._file_cb = None                            # callable(path) for watched files
         self._file_pick = None                          # callable([paths]) -> set of paths to watch
@@ -317,12 +326,147 @@ class Torrent:
             self.have[i] = 1
         self.nhave = len(have)
         self._init_file_tracking()
+        if self.cfg.native_wire and _W is not None and self.nhave < self.info.num_pieces:
+            self.store = _W.PieceStore(self.info.num_pieces, self.info.piece_length, self.info.total_length)
+            for p in list(self.peers.values()):
+                self._attach_link(p)
         self._downloading = True
         if self.nhave == self.info.num_pieces:
             self.complete.set()
         for p in list(self.peers.values()):
             self._send_have_state(p)
             self._update_interest(p)
+            self._fill(p)
+
+    # ------------------------------------------------------------ native data plane
+    def _attach_link(self, p: _Peer) -> None:
+        """Hand p's block traffic to a native link (csrc/btwire): from now on
+        its peer loop feeds raw bytes to the link, which assembles blocks into
+        the shared store and keeps requests pipelined over the pieces this
+        Torrent assigns it."""
+        if self.store is None or p.link is not None or p.wire.closed:
+            return
+        p.link = _W.Link(self.store, self.cfg.pipeline, p.hs.fast)
+        p.link.peer_choking = p.peer_choking
+
+    def in_flight(self, i: int) -> bool:
+        """Piece i is being fetched or verified (web seeds skip it)."""
+        return i in self.pieces or i in self.verifying or (self.store is not None and self.store.active(i))
+
+    def _unassign(self, p: _Peer, pieces=None) -> None:
+        link = p.link
+        if link is None:
+            return
+        for i in (link.assigned() if pieces is None else pieces):
+            link.drop(i)
+            s = self.assigned.get(i)
+            if s is not None:
+                s.discard(p.key)
+                if not s:
+                    del self.assigned[i]
+
+    def _pick_piece(self, p: _Peer) -> int | None:
+        """Next piece for p's link: a started piece nobody is fetching, else the
+        rarest (watched-file order first) unstarted piece it has, else (end
+        game) a piece other links are finishing."""
+        assert self.store is not None
+        have, store, assigned = self.have, self.store, self.assigned
+        for i in store.active_pieces():
+            if p.have[i] and not have[i] and not assigned.get(i) and i not in self.verifying:
+                return i
+        order = self._rarest_order()
+        pos = self._rare_pos
+        while pos < len(order) and (have[order[pos]] or store.active(order[pos]) or order[pos] in self.verifying):
+            pos += 1
+        self._rare_pos = pos
+        for k in range(pos, len(order)):
+            i = order[k]
+            if p.have[i] and not have[i] and not store.active(i) and i not in self.verifying \
+                    and i not in self.ws_busy:
+                return i
+        for i in store.active_pieces():
+            owners = assigned.get(i, ())
+            if p.have[i] and not have[i] and p.key not in owners and len(owners) < 3 and i not in self.verifying:
+                return i
+        return None
+
+    def _fill_native(self, p: _Peer) -> None:
+        link = p.link
+        if not p.peer_choking or p.hs.fast:
+            while link.need_work():
+                i = self._pick_piece(p)
+                if i is None:
+                    break
+                link.assign(i)
+                self.assigned.setdefault(i, set()).add(p.key)
+        out = link.pump()
+        if out:
+            p.wire.send_raw(out)
+
+    def _native_piece(self, src: _Peer, i: int) -> None:
+        """A link completed piece i: take its bytes, stop the other links
+        fetching it (end-game CANCELs), verify + write off-loop."""
+        assert self.store is not None
+        data = self.store.take(i)
+        for key in self.assigned.pop(i, set()):
+            q = self.peers.get(key)
+            if q is not None and q.link is not None:
+                q.link.piece_done(i)
+                if q is not src:
+                    out = q.link.pump()
+                    if out:
+                        q.wire.send_raw(out)
+        src.downloaded += len(data)
+        self.downloaded += len(data)
+        self.verifying.add(i)
+        t = asyncio.get_running_loop().create_task(self._finish_native(i, data, src))
+        self._finishers.add(t)
+        t.add_done_callback(self._finishers.discard)
+
+    async def _finish_native(self, i: int, data: bytes, src: _Peer) -> None:
+        try:
+            ok = await self.commit_piece(i, data)
+        finally:
+            self.verifying.discard(i)
+        if ok is False:
+            src.bad += 1
+            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
+            if src.bad >= self.cfg.max_bad_pieces:
+                self.banned.add(src.addr)
+                src.wire.close()
+            self._rare_dirty = True
+            for q in list(self.peers.values()):
+                if q.link is not None:
+                    self._fill(q)
+
+    async def _native_loop(self, p: _Peer) -> None:
+        data = await p.wire.read_raw()
+        p.last_recv = time.monotonic()
+        await self._native_feed(p, data)
+
+    async def _native_feed(self, p: _Peer, data: bytes) -> None:
+        link = p.link
+        ev, out = link.feed(data)
+        if out:
+            p.wire.send_raw(out)
+        for e in ev:
+            kind = e[0]
+            if kind == "msg":
+                await self._dispatch(p, e[1], e[2])
+            elif kind == "piece":
+                self._native_piece(p, e[1])
+            elif kind == "unchoke":
+                p.peer_choking = False
+            elif kind == "choke":
+                p.peer_choking = True
+                if not p.hs.fast:
+                    self._unassign(p)          # its pieces go back to the other links
+                    for q in list(self.peers.values()):
+                        if q is not p and q.link is not None:
+                            self._fill(q)
+            elif kind == "bad":
+                raise pw.PeerError(e[1])
+        if not self.closed and self.info is not None:
             self._fill(p)
 
     # ------------------------------------------------------------ per-file completion
@@ -391,6 +535,8 @@ class Torrent:
             return 0
         done = sum(self.info.piece_size(i) for i in range(self.info.num_pieces) if self.have[i])
         partial = sum(len(pc.received) * BLOCK for pc in self.pieces.values())
+        if self.store is not None:
+            partial += self.store.partial_bytes
         return min(done + partial, self.info.total_length)
 
     # ------------------------------------------------------------ discovery
@@ -548,6 +694,7 @@ class Torrent:
         if not inbound:
             p.listen_addr = addr
         self.peers[addr] = p
+        self._attach_link(p)
         try:
             if hs.extended:
                 p.wire.ext_handshake(len(self.info.raw) if self.info else None, self.port,
@@ -575,6 +722,12 @@ class Torrent:
             self.add_peer_addr(a)
 
     def _release(self, p: _Peer) -> None:
+        if p.link is not None:
+            self._unassign(p)
+            for q in list(self.peers.values()):
+                if q is not p:
+                    self._fill(q)
+            return
         for (i, off) in list(p.outstanding):
             pc = self.pieces.get(i)
             if pc is not None and pc.lapse(off // BLOCK, p.key):
@@ -600,12 +753,22 @@ class Torrent:
         last_drain = time.monotonic()
         p.last_recv = time.monotonic()
         while not self.closed:
-            msgs = await p.wire.read_batch()
-            p.last_recv = time.monotonic()
-            for m in msgs:
-                if m is None:
+            if p.link is not None:
+                await self._native_loop(p)
+            else:
+                msgs = await p.wire.read_batch()
+                p.last_recv = time.monotonic()
+                if p.link is not None:
+                    # the native link took over while this read was pending: these
+                    # messages (block replies to its requests included) are its input
+                    await self._native_feed(p, b"".join(
+                        struct.pack(">IB", len(m[1]) + 1, m[0]) + m[1] if m is not None else b"\0\0\0\0"
+                        for m in msgs))
                     continue
-                await self._dispatch(p, m[0], m[1])
+                for m in msgs:
+                    if m is None:
+                        continue
+                    await self._dispatch(p, m[0], m[1])
             now = time.monotonic()
             if now - last_drain > 0.5 or p.wire.writer.transport.get_write_buffer_size() > (4 << 20):
                 last_drain = now
@@ -631,9 +794,13 @@ class Torrent:
             pass
         elif mid == pw.UNCHOKE:
             p.peer_choking = False
+            if p.link is not None:          # parsed by Python just before the native link took over
+                p.link.peer_choking = False
             self._fill(p)
         elif mid == pw.CHOKE:
             p.peer_choking = True
+            if p.link is not None:
+                p.link.peer_choking = True
             if not p.hs.fast:
                 self._release(p)
         elif mid == pw.INTERESTED:
@@ -741,6 +908,10 @@ class Torrent:
         return None
 
     def _fill(self, p: _Peer) -> None:
+        if p.link is not None:
+            if self.info is not None and self._downloading and not p.wire.closed and not self.complete.is_set():
+                self._fill_native(p)
+            return
         if self.info is None or not self._downloading or p.peer_choking or p.wire.closed:
             return
         while len(p.outstanding) < self.cfg.pipeline:
@@ -867,6 +1038,15 @@ class Torrent:
                     p.wire.keepalive()
                 if now - getattr(p, "last_recv", now) > 300:
                     p.wire.close()  # silent for 5 minutes: drop
+                    continue
+                if p.link is not None:
+                    if p.link.outstanding and p.link.oldest_request_age() > self.cfg.request_timeout:
+                        p.link.lapse_all()
+                        self._unassign(p)
+                        p.peer_choking = p.link.peer_choking = True   # snubbed until it sends something
+                        for q in list(self.peers.values()):
+                            if q is not p:
+                                self._fill(q)
                     continue
                 stale = [k for k, t in p.outstanding.items() if now - t > self.cfg.request_timeout]
                 if stale and len(stale) == len(p.outstanding):

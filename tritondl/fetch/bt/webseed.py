@@ -76,7 +76,7 @@ class WebSeed:
         fallback = None
         for k in range(n):
             i = (self._cursor + k) % n
-            if t.have[i] or i in t.pieces or i in t.verifying or i in t.ws_busy:
+            if t.have[i] or t.in_flight(i) or i in t.ws_busy:
                 continue
             if t.avail[i] == 0:          # nobody in the swarm has it: ours
                 self._cursor = i + 1
