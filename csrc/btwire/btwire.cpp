@@ -27,6 +27,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -52,6 +53,49 @@ inline void put_be32(std::string& s, uint32_t v) {
 }
 inline uint64_t key(uint32_t piece, uint32_t block) { return (uint64_t(piece) << 32) | block; }
 
+// Recycled piece buffers: a 1 MiB bytes object per piece would be a fresh
+// mmap (256 page faults) plus a copy; a completed piece instead moves its
+// buffer into a Piece (buffer protocol, no copy) that hands it back here
+// when Python drops the last reference (after verify + write).
+struct Pool {
+  std::mutex mu;
+  std::vector<std::vector<uint8_t>> free;
+  size_t cap = 64;
+  std::vector<uint8_t> get(size_t n) {
+    std::vector<uint8_t> v;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (!free.empty()) {
+        v = std::move(free.back());
+        free.pop_back();
+      }
+    }
+    v.resize(n);  // zero-fills only growth; a recycled buffer keeps its bytes
+    return v;
+  }
+  void put(std::vector<uint8_t>&& v) {
+    std::lock_guard<std::mutex> g(mu);
+    if (free.size() < cap) free.push_back(std::move(v));
+  }
+};
+
+// A completed piece handed to Python: read-only bytes-like (memoryview(),
+// hashlib, os.pwrite accept it), buffer returned to the pool on release.
+class Piece {
+ public:
+  Piece(std::vector<uint8_t>&& d, std::shared_ptr<Pool> pool) : data_(std::move(d)), pool_(std::move(pool)) {}
+  ~Piece() {
+    if (pool_) pool_->put(std::move(data_));
+  }
+  Piece(const Piece&) = delete;
+  Piece& operator=(const Piece&) = delete;
+  const std::vector<uint8_t>& data() const { return data_; }
+
+ private:
+  std::vector<uint8_t> data_;
+  std::shared_ptr<Pool> pool_;
+};
+
 struct PieceBuf {
   std::vector<uint8_t> data;
   std::vector<uint8_t> got;
@@ -76,7 +120,7 @@ class PieceStore {
   bool begin(uint32_t i) {
     if (pieces_.count(i)) return false;
     PieceBuf& b = pieces_[i];
-    b.data.resize(piece_size(i));
+    b.data = pool_->get(piece_size(i));
     b.nblocks = blocks(i);
     b.got.assign(b.nblocks, 0);
     return true;
@@ -108,10 +152,10 @@ class PieceStore {
     bytes_ += n;
     return ++b.ngot == b.nblocks ? 1 : 0;
   }
-  py::bytes take(uint32_t i) {
+  std::unique_ptr<Piece> take(uint32_t i) {
     auto it = pieces_.find(i);
     if (it == pieces_.end()) throw std::out_of_range("piece not buffered");
-    py::bytes out(reinterpret_cast<const char*>(it->second.data.data()), it->second.data.size());
+    auto out = std::make_unique<Piece>(std::move(it->second.data), pool_);
     bytes_ -= it->second.nbytes;
     pieces_.erase(it);
     return out;
@@ -120,7 +164,12 @@ class PieceStore {
     auto it = pieces_.find(i);
     if (it == pieces_.end()) return;
     bytes_ -= it->second.nbytes;
+    pool_->put(std::move(it->second.data));
     pieces_.erase(it);
+  }
+  size_t pooled() {
+    std::lock_guard<std::mutex> g(pool_->mu);
+    return pool_->free.size();
   }
   std::vector<uint32_t> active_pieces() const {
     std::vector<uint32_t> v;
@@ -137,6 +186,7 @@ class PieceStore {
   uint64_t plen_, total_;
   uint64_t bytes_ = 0;
   std::unordered_map<uint32_t, PieceBuf> pieces_;
+  std::shared_ptr<Pool> pool_ = std::make_shared<Pool>();
 };
 
 class Link {
@@ -152,10 +202,41 @@ class Link {
     char* p = nullptr;
     Py_ssize_t n = 0;
     PyBytes_AsStringAndSize(data.ptr(), &p, &n);
-    buf_.insert(buf_.end(), reinterpret_cast<uint8_t*>(p), reinterpret_cast<uint8_t*>(p) + n);
+    reserve(size_t(n));
+    std::memcpy(buf_.data() + wpos_, p, size_t(n));
+    wpos_ += size_t(n);
+    return parse();
+  }
+
+  // Zero-copy receive (asyncio BufferedProtocol): the socket reads straight
+  // into the link's buffer, then feed_n(nbytes) parses what arrived.  The
+  // view stays valid until the next feed/feed_n call.
+  py::memoryview recv_buffer(size_t want) {
+    reserve(std::max<size_t>(want, 4096));
+    return py::memoryview::from_memory(buf_.data() + wpos_, py::ssize_t(buf_.size() - wpos_), false);
+  }
+  py::tuple feed_n(size_t n) {
+    if (n > buf_.size() - wpos_) throw std::out_of_range("feed_n past the receive buffer");
+    wpos_ += n;
+    return parse();
+  }
+
+ private:
+  // Room for n more bytes after wpos_: drop consumed bytes first (the kept
+  // tail is less than one message), grow only if still short.
+  void reserve(size_t n) {
+    if (rpos_) {
+      if (wpos_ > rpos_) std::memmove(buf_.data(), buf_.data() + rpos_, wpos_ - rpos_);
+      wpos_ -= rpos_;
+      rpos_ = 0;
+    }
+    if (buf_.size() - wpos_ < n) buf_.resize(wpos_ + n);
+  }
+
+  py::tuple parse() {
     py::list ev;
-    size_t pos = 0;
-    const size_t len = buf_.size();
+    size_t pos = rpos_;
+    const size_t len = wpos_;
     bool bad = false;
     while (len - pos >= 4) {
       const uint32_t ml = be32(&buf_[pos]);
@@ -206,10 +287,13 @@ class Link {
         ev.append(py::make_tuple("msg", int(id), py::bytes(reinterpret_cast<const char*>(pl), pn)));
       }
     }
-    buf_.erase(buf_.begin(), buf_.begin() + static_cast<std::ptrdiff_t>(pos));
+    rpos_ = pos;
+    if (rpos_ == wpos_) rpos_ = wpos_ = 0;
     std::string out = bad ? std::string() : requests();
     return py::make_tuple(ev, py::bytes(out));
   }
+
+ public:
 
   // Requests (and queued cancels) to send now.
   py::bytes pump() { return py::bytes(requests()); }
@@ -255,7 +339,7 @@ class Link {
   bool peer_choking() const { return peer_choking_; }
   void set_peer_choking(bool c) { peer_choking_ = c; }
   uint64_t downloaded() const { return downloaded_; }
-  size_t buffered() const { return buf_.size(); }
+  size_t buffered() const { return wpos_ - rpos_; }
 
  private:
   void unassign(uint32_t i, bool cancel) {
@@ -317,7 +401,8 @@ class Link {
   int pipeline_;
   bool fast_;
   bool peer_choking_ = true;
-  std::vector<uint8_t> buf_;
+  std::vector<uint8_t> buf_;                              // received bytes [rpos_, wpos_)
+  size_t rpos_ = 0, wpos_ = 0;
   std::vector<uint32_t> assigned_;
   std::unordered_map<uint32_t, uint32_t> cursor_;        // next never-requested block per assigned piece
   std::unordered_map<uint64_t, Clock::time_point> out_req_;
@@ -331,6 +416,15 @@ class Link {
 PYBIND11_MODULE(_btwire, m) {
   m.doc() = "tritondl BitTorrent peer-wire data plane (block assembly + request pipelining)";
   m.attr("BLOCK") = kBlock;
+  py::class_<Piece>(m, "Piece", py::buffer_protocol())
+      .def_buffer([](Piece& p) {
+        return py::buffer_info(const_cast<uint8_t*>(p.data().data()), 1, "B", 1, {py::ssize_t(p.data().size())},
+                               {py::ssize_t(1)}, true);
+      })
+      .def("__len__", [](const Piece& p) { return p.data().size(); })
+      .def("tobytes", [](const Piece& p) {
+        return py::bytes(reinterpret_cast<const char*>(p.data().data()), p.data().size());
+      });
   py::class_<PieceStore, std::shared_ptr<PieceStore>>(m, "PieceStore")
       .def(py::init<uint32_t, uint64_t, uint64_t>(), py::arg("num_pieces"), py::arg("piece_len"),
            py::arg("total_len"))
@@ -347,6 +441,7 @@ PYBIND11_MODULE(_btwire, m) {
         return s.put(i, off, reinterpret_cast<const uint8_t*>(p), size_t(n));
       })
       .def("take", &PieceStore::take)
+      .def_property_readonly("pooled", &PieceStore::pooled)
       .def("reset", &PieceStore::reset)
       .def("active_pieces", &PieceStore::active_pieces)
       .def_property_readonly("partial_bytes", &PieceStore::partial_bytes);
@@ -354,6 +449,8 @@ PYBIND11_MODULE(_btwire, m) {
       .def(py::init<std::shared_ptr<PieceStore>, int, bool>(), py::arg("store"), py::arg("pipeline") = 128,
            py::arg("fast") = false)
       .def("feed", &Link::feed)
+      .def("recv_buffer", &Link::recv_buffer, py::arg("want") = 262144)
+      .def("feed_n", &Link::feed_n)
       .def("pump", &Link::pump)
       .def("assign", &Link::assign)
       .def("piece_done", &Link::piece_done)

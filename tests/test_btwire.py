@@ -42,7 +42,7 @@ def test_requests_pipeline_and_completion():
     assert list(ev) == [] and link.buffered == 1000
     ev, out = link.feed(stream[1000:])
     assert list(ev) == [("piece", 0)]
-    assert store.take(0) == data0 and not store.active(0)
+    assert bytes(store.take(0)) == data0 and not store.active(0)
     # the freed pipeline slots went to the rest of piece 2 (the tail block is short)
     reqs = [struct.unpack(">III", p) for mid, p in msgs(out) if mid == 6]
     assert reqs == [(2, B, B), (2, 2 * B, 100)]
@@ -85,7 +85,7 @@ def test_endgame_two_links_share_the_store_and_cancel():
     a.piece_done(0)
     cancels = [struct.unpack(">III", p) for m, p in msgs(a.pump()) if m == 8]
     assert sorted(cancels) == [(0, B, B)]                 # a still had block 1 outstanding
-    assert store.take(0) == b"x" * B + b"y" * B
+    assert bytes(store.take(0)) == b"x" * B + b"y" * B
     ev, _ = a.feed(piece_msg(0, 0, b"z" * B))             # late duplicate: ignored
     assert list(ev) == []
 
@@ -108,3 +108,78 @@ def test_forwarded_messages_and_protocol_errors():
     with pytest.raises(IndexError):
         link3.assign(7)
     assert store.partial_bytes == 0
+
+
+def test_take_is_zero_copy_and_recycles_buffers():
+    store = W.PieceStore(4, 2 * B, 8 * B)
+    for i in range(2):
+        store.begin(i)
+        store.put(i, 0, bytes([i + 1]) * B)
+        store.put(i, B, bytes([i + 1]) * B)
+    p0 = store.take(0)
+    mv = memoryview(p0)
+    assert mv.readonly and len(mv) == 2 * B and len(p0) == 2 * B
+    assert mv[:4].tobytes() == b"\x01" * 4 and p0.tobytes() == b"\x01" * (2 * B)
+    assert store.pooled == 0
+    del p0
+    assert store.pooled == 0            # the memoryview still holds it
+    mv.release()
+    del mv
+    assert store.pooled == 1
+    store.begin(2)                      # reuses the recycled buffer
+    assert store.pooled == 0
+    store.reset(2)
+    assert store.pooled == 1
+
+
+def test_zero_copy_receive_buffer_keeps_partial_messages():
+    """recv_buffer/feed_n (the BufferedProtocol path): bytes written into the
+    view are parsed in place; a message split across reads is completed by
+    the next one even after the buffer compacts."""
+    store = W.PieceStore(1, 4 * B, 4 * B)
+    link = W.Link(store, pipeline=8)
+    link.assign(0)
+    link.peer_choking = False
+    link.pump()
+    data = bytes(range(256)) * (4 * B // 256)
+    stream = b"\x00\x00\x00\x00" + b"".join(piece_msg(0, k * B, data[k * B:(k + 1) * B]) for k in range(4)) \
+        + struct.pack(">IBI", 5, 4, 0)                    # keepalive, 4 blocks, HAVE 0
+    events, pos = [], 0
+    for cut in (3, 20000, 7, 30000, len(stream)):
+        chunk = stream[pos:min(cut + pos, len(stream))]
+        view = link.recv_buffer(1 << 16)
+        assert len(view) >= len(chunk) and not view.readonly
+        view[:len(chunk)] = chunk
+        ev, _out = link.feed_n(len(chunk))
+        events += list(ev)
+        pos += len(chunk)
+        if pos == len(stream):
+            break
+    assert events == [("piece", 0), ("msg", 4, b"\x00\x00\x00\x00")]
+    assert bytes(store.take(0)) == data and link.buffered == 0
+    with pytest.raises(IndexError):
+        link.feed_n(1 << 30)
+
+
+def test_download_uses_zero_copy_receive(tmp_path):
+    """A plain-TCP leecher switches its peer connections to LinkReader."""
+    import asyncio
+
+    from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+    from tritondl.fetch.bt.client import TorrentDownloader
+    from tritondl.fetch.bt.torrent import TorrentConfig
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 3_000_000})
+        info = torrent_for(str(src / "P"), 65536)
+        seed = await Seeder(info, str(src)).start()
+        d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1"), use_dht=False)
+        t, _ = await d.open(str(tmp_path / "dst"), magnet_for(info) + f"&x.pe=127.0.0.1:{seed.torrent.port}")
+        await asyncio.wait_for(t.got_info.wait(), 20)
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 30)
+        assert any(p.rx is not None for p in t.peers.values())
+        await t.close()
+        await seed.stop()
+    asyncio.run(main())

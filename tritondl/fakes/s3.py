@@ -85,6 +85,7 @@ class FakeS3:
         self.uploads: dict[str, Upload] = {}
         self.list_parts_page = 1000
         self.fail_parts: set[int] = set()       # fault injection: these part numbers get HTTP 500
+        self.fail_parts_once = False            # ... only the first time each is sent
         self._ids = itertools.count(1)
         self._fail = 0
         self._fail_status = 503
@@ -408,6 +409,8 @@ class FakeS3:
                 return _xml_err(404, "NoSuchUpload", "no such upload")
             pn = int(q.get("partNumber", "0") or 0)
             if pn in self.fail_parts:
+                if self.fail_parts_once:
+                    self.fail_parts.discard(pn)
                 await request.read()
                 return _xml_err(500, "InternalError", "injected part failure")
             if self.strict_parts and not 1 <= pn <= 10000:

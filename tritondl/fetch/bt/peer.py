@@ -137,6 +137,24 @@ class Wire:
             raise asyncio.IncompleteReadError(b"", None)
         return data
 
+    def take_over(self, link, on_data) -> tuple[LinkReader, bytes] | None:
+        """Switch a plain TCP connection to zero-copy native receive
+        (:class:`LinkReader`).  Returns (reader, bytes already buffered — the
+        caller feeds these first), or None where the transport cannot switch
+        (MSE-encrypted, uTP, closing): those keep :meth:`read_raw`.  Call only
+        while no read is pending."""
+        tr = self.writer.transport
+        buf = getattr(self.reader, "_buffer", None)
+        if type(self.reader) is not asyncio.StreamReader or type(tr).__name__ != "_SelectorSocketTransport" \
+                or buf is None or tr.is_closing() or self.reader.at_eof() or self.reader.exception() is not None:
+            return None
+        leftover = bytes(self._rbuf) + bytes(buf)
+        self._rbuf.clear()
+        buf.clear()
+        rx = LinkReader(tr, link, on_data)
+        tr.set_protocol(rx)
+        return rx, leftover
+
     async def _fill(self) -> None:
         data = await self.reader.read(1 << 18)
         if not data:
@@ -246,6 +264,93 @@ class Wire:
                 self.writer.close()
             except Exception:
                 pass
+
+
+class LinkReader(asyncio.BufferedProtocol):
+    """Zero-copy receive for a native link (csrc/btwire): installed on a plain
+    TCP transport in place of the StreamReader's protocol, so the socket reads
+    straight into the link's buffer (``recv_into``) and ``on_data(nbytes)``
+    parses it on the spot — no StreamReader buffer, no bytes objects, no task
+    wake-up per read.  Control messages the callback hands to :meth:`push`
+    queue up for the peer loop (:meth:`get`); write flow control and
+    connection loss are forwarded to the old protocol so the StreamWriter
+    keeps working."""
+
+    def __init__(self, transport: asyncio.Transport, link, on_data) -> None:
+        self._tr = transport
+        self._old = transport.get_protocol()
+        self._link = link
+        self._on_data = on_data
+        self._msgs: list[tuple[int, bytes]] = []
+        self._waiter: asyncio.Future | None = None
+        self._exc: BaseException | None = None
+        self._eof = False
+        self._paused = False
+
+    # -- transport callbacks --------------------------------------------------
+    def get_buffer(self, sizehint: int):
+        return self._link.recv_buffer(1 << 18)
+
+    def buffer_updated(self, nbytes: int) -> None:
+        try:
+            self._on_data(nbytes)
+        except Exception as e:  # a protocol violation: end the peer loop with it
+            self._fail(e)
+
+    def eof_received(self) -> bool:
+        self._eof = True
+        self._wake()
+        return False
+
+    def connection_lost(self, exc) -> None:
+        self._eof = True
+        if exc is not None and self._exc is None:
+            self._exc = exc
+        self._wake()
+        self._old.connection_lost(exc)
+
+    def pause_writing(self) -> None:
+        self._old.pause_writing()
+
+    def resume_writing(self) -> None:
+        self._old.resume_writing()
+
+    # -- peer-loop side -------------------------------------------------------
+    def push(self, mid: int, payload: bytes) -> None:
+        self._msgs.append((mid, payload))
+        if len(self._msgs) >= 1024 and not self._paused:   # the loop is behind: stop reading
+            self._paused = True
+            self._tr.pause_reading()
+        self._wake()
+
+    async def get(self) -> list[tuple[int, bytes]]:
+        """Control messages received since the last call (at least one)."""
+        while not self._msgs:
+            if self._exc is not None:
+                raise self._exc
+            if self._eof:
+                raise asyncio.IncompleteReadError(b"", None)
+            self._waiter = asyncio.get_running_loop().create_future()
+            try:
+                await self._waiter
+            finally:
+                self._waiter = None
+        msgs, self._msgs = self._msgs, []
+        if self._paused:
+            self._paused = False
+            self._tr.resume_reading()
+        return msgs
+
+    def _fail(self, e: BaseException) -> None:
+        if self._exc is None:
+            self._exc = e
+        self._wake()
+        self._tr.pause_reading()
+
+    def _wake(self) -> None:
+        w = self._waiter
+        if w is not None and not w.done():
+            w.set_result(None)
 
 
 def parse_ext_handshake(payload: bytes) -> ExtHandshake:

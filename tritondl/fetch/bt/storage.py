@@ -14,6 +14,7 @@ host, the threaded OpenSSL path otherwise.
 
 from __future__ import annotations
 
+import bisect
 import os
 import sqlite3
 import threading
@@ -86,15 +87,22 @@ class FileStorage:
             self._fds.clear()
 
     def _spans(self, gofs: int, length: int):
-        """Yield (file_index, offset_in_file, nbytes) covering [gofs, gofs+length)."""
+        """[(file_index, offset_in_file, nbytes)] covering [gofs, gofs+length);
+        bisects to the first file, so many-file torrents cost O(log files)."""
         end = gofs + length
-        for i, (p, n) in enumerate(self.layout):
-            fs = self.offsets[i]
+        out = []
+        offsets, layout = self.offsets, self.layout
+        for i in range(max(0, bisect.bisect_right(offsets, gofs) - 1), len(layout)):
+            fs = offsets[i]
+            if fs >= end:
+                break
+            n = layout[i][1]
             fe = fs + n
-            if fe <= gofs or fs >= end or n == 0:
+            if fe <= gofs or n == 0:
                 continue
             a, b = max(gofs, fs), min(end, fe)
-            yield i, a - fs, b - a
+            out.append((i, a - fs, b - a))
+        return out
 
     def write(self, piece: int, offset: int, data: bytes) -> None:
         gofs = piece * self.info.piece_length + offset
@@ -112,8 +120,12 @@ class FileStorage:
 
     def read(self, piece: int, offset: int, length: int) -> bytes:
         gofs = piece * self.info.piece_length + offset
+        spans = self._spans(gofs, length)
+        if len(spans) == 1 and spans[0][0] in self._fds:     # the common case: one file
+            i, fofs, n = spans[0]
+            return os.pread(self._fds[i], n, fofs)
         out = bytearray()
-        for i, fofs, n in self._spans(gofs, length):
+        for i, fofs, n in spans:
             out += os.pread(self._fds[i], n, fofs) if i in self._fds else bytes(n)
         return bytes(out)
 

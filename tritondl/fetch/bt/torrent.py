@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import functools
 import hashlib
 import math
 import os
@@ -130,6 +131,8 @@ class _Peer:
         self.downloaded = 0
         self.meta_requested = False
         self.link = None                                    # _btwire.Link once the native data plane runs
+        self.rx: pw.LinkReader | None = None                # zero-copy receive into the link (plain TCP)
+        self.rx_tried = False
 
     def set_have(self, i: int) -> bool:
         if 0 <= i < len(self.have) and not self.have[i]:
@@ -407,7 +410,7 @@ class Torrent:
         """A link completed piece i: take its bytes, stop the other links
         fetching it (end-game CANCELs), verify + write off-loop."""
         assert self.store is not None
-        data = self.store.take(i)
+        data = memoryview(self.store.take(i))     # pooled buffer, no copy
         for key in self.assigned.pop(i, set()):
             q = self.peers.get(key)
             if q is not None and q.link is not None:
@@ -423,7 +426,7 @@ class Torrent:
         self._finishers.add(t)
         t.add_done_callback(self._finishers.discard)
 
-    async def _finish_native(self, i: int, data: bytes, src: _Peer) -> None:
+    async def _finish_native(self, i: int, data: memoryview, src: _Peer) -> None:
         try:
             ok = await self.commit_piece(i, data)
         finally:
@@ -445,14 +448,25 @@ class Torrent:
         await self._native_feed(p, data)
 
     async def _native_feed(self, p: _Peer, data: bytes) -> None:
-        link = p.link
-        ev, out = link.feed(data)
+        msgs: list = []
+        self._native_events(p, *p.link.feed(data), msgs.append)
+        for m in msgs:
+            await self._dispatch(p, m[0], m[1])
+
+    def _native_recv(self, p: _Peer, nbytes: int) -> None:
+        """LinkReader callback: nbytes landed in p.link's buffer (zero-copy)."""
+        p.last_recv = time.monotonic()
+        self._native_events(p, *p.link.feed_n(nbytes), lambda m: p.rx.push(m[0], m[1]))
+
+    def _native_events(self, p: _Peer, ev, out: bytes, defer) -> None:
+        """Act on what a link parsed: pieces and choke state here and now;
+        other messages go to ``defer`` for the (async) dispatcher."""
         if out:
             p.wire.send_raw(out)
         for e in ev:
             kind = e[0]
             if kind == "msg":
-                await self._dispatch(p, e[1], e[2])
+                defer((e[1], e[2]))
             elif kind == "piece":
                 self._native_piece(p, e[1])
             elif kind == "unchoke":
@@ -754,7 +768,18 @@ class Torrent:
         p.last_recv = time.monotonic()
         while not self.closed:
             if p.link is not None:
-                await self._native_loop(p)
+                if p.rx is None and not p.rx_tried:
+                    p.rx_tried = True
+                    r = p.wire.take_over(p.link, functools.partial(self._native_recv, p))
+                    if r is not None:
+                        p.rx, leftover = r
+                        if leftover:
+                            await self._native_feed(p, leftover)
+                if p.rx is not None:
+                    for m in await p.rx.get():
+                        await self._dispatch(p, m[0], m[1])
+                else:
+                    await self._native_loop(p)
             else:
                 msgs = await p.wire.read_batch()
                 p.last_recv = time.monotonic()
