@@ -138,7 +138,8 @@ async def job_bench(a) -> int:
         cfg.cleanup, cfg.max_retries, cfg.retry_delay_s = True, 0, 0.0
         cfg.progress_log_interval_s, cfg.heartbeat_s = 0, 0
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
-                                             encryption=a.encryption), progress_interval=1.0, use_dht=False)
+                                             encryption=a.encryption, native_wire=not a.python_wire),
+                               progress_interval=1.0, use_dht=False)
         svc = Service(cfg, amqp=Client(broker.info["url"], heartbeat=0, retry_delay=0),
                       dispatcher=Dispatcher(cfg.download_dir, [bt], 0),
                       uploader=Uploader(cfg.bucket, S3Client(s3.info["url"], Static(AK, SK))))
@@ -161,7 +162,7 @@ async def job_bench(a) -> int:
                 r = svc.results[-1]
                 assert r.ok and r.files == a.files and r.bytes == per * a.files, r
                 print(json.dumps({"metric": "bt_job_seconds", "value": round(dt, 3), "stream_upload": on,
-                                  "s3_link_gbps": a.s3_gbps or None,
+                                  "s3_link_gbps": a.s3_gbps or None, "wire": "python" if a.python_wire else "native",
                                   "mb": a.mb, "files": a.files, "seeds": a.seeds, "piece_kb": a.piece_kb,
                                   "job_MB_per_sec": round(a.mb * 1.048576 / dt, 1),
                                   "spans_ms": {k: round(v * 1000, 1) for k, v in r.marks.items()}}), flush=True)

@@ -75,7 +75,8 @@ class TorrentDownloader:
     def from_config(cls, c, http=None) -> "TorrentDownloader":
         tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, pex=c.bt_pex, encryption=c.bt_encryption,
                            verify_device={"on": "gpu", "off": "cpu"}.get(c.gpu_verify, c.gpu_verify),
-                           upnp=c.bt_upnp, disk_reserve=c.disk_reserve_bytes,
+                           upnp=c.bt_upnp, native_wire=c.bt_native_wire,
+                           disk_reserve=c.disk_reserve_bytes,
                            listen_host6="::" if c.bt_dht_ipv6 else None)
         return cls(tc, metadata_timeout=c.metadata_timeout_s, progress_interval=c.progress_interval_s,
                    use_dht=c.bt_dht, dht_bootstrap=_parse_hostports(c.bt_bootstrap), dht_ipv6=c.bt_dht_ipv6)

@@ -83,6 +83,7 @@ class Config:
     bt_listen_port: int = 0                     # 0 = ephemeral
     bt_dht: bool = True
     bt_upnp: bool = True                        # UPnP IGD port forwarding of the listen port (anacrolix default)
+    bt_native_wire: bool = True                 # per-block peer-wire work in csrc/btwire (False: pure Python)
     bt_dht_ipv6: bool = True                    # BEP 32 dual-stack DHT (anacrolix default); IPv4-only if no IPv6
     bt_utp: bool = True
     bt_pex: bool = True
@@ -170,6 +171,7 @@ class Config:
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_dht_ipv6 = _env_bool(g("TRITONDL_BT_DHT_IPV6"), c.bt_dht_ipv6)
         c.bt_upnp = _env_bool(g("TRITONDL_BT_UPNP"), c.bt_upnp)
+        c.bt_native_wire = _env_bool(g("TRITONDL_BT_NATIVE_WIRE"), c.bt_native_wire)
         c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
         c.bt_pex = _env_bool(g("TRITONDL_BT_PEX"), c.bt_pex)
         if c.bt_encryption not in ("disable", "allow", "prefer", "require"):
