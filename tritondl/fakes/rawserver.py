@@ -290,6 +290,11 @@ class _Conn:
             await self.send(head)
             await self.loop.sock_sendfile(self.sock, _FdFile(resp.fd), resp.offset, resp.length)
             return
+        if self.raw.tls is None:
+            # the head leaves now, from the loop (one non-blocking send), so the
+            # client parses it while the pump thread is still being woken
+            await self.send(head)
+            head = b""
         _sent, _sig, err = await rawhttp.run_pump(self.raw, relay.send_body, head, resp.fd, resp.offset,
                                                   resp.length, None, 0)
         if err:

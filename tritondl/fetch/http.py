@@ -241,8 +241,9 @@ class HTTPDownloader:
                 except (OSError, rawhttp.RawHTTPError) as e:
                     raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
                 try:
-                    await asyncio.wait_for(conn.sendall(head), self.read_timeout)
+                    await conn.sendall(head, self.read_timeout)
                     h = await rawhttp.read_head(conn, self.read_timeout)
+                    rawhttp.trace("get_head")
                     break
                 except (OSError, rawhttp.RawHTTPError) as e:
                     conn.close()
@@ -416,7 +417,12 @@ class HTTPDownloader:
         fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
         src = probe.final_url or url          # follow-up ranges skip the redirect hop(s)
-        if len(segs) <= self.segments:
+        tasks: list[asyncio.Future] = []
+        if len(segs) == 1:
+            # one stream: run it inline, so its receive pump starts in this very
+            # step — ahead of the streamed upload's first step (which only waits)
+            fetch = self._fetch_segment(src, fd, 0, segs, done, validator, probe, h, first)
+        elif len(segs) <= self.segments:
             tasks = [asyncio.ensure_future(self._fetch_segment(src, fd, i, segs, done, validator, probe, h,
                                                                first if i == 0 else None))
                      for i in range(len(segs))]
@@ -430,7 +436,7 @@ class HTTPDownloader:
                                               first if i == 0 else None)
             tasks = [asyncio.ensure_future(worker()) for _ in range(self.segments)]
         try:
-            await asyncio.gather(*tasks)
+            await (asyncio.gather(*tasks) if tasks else fetch)
         except BaseException as e:
             # stop every sibling and WAIT for it: their native pumps write through
             # `fd` and read their own sockets, which must stay open until they return

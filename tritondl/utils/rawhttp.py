@@ -115,8 +115,10 @@ class RawConn:
     def fileno(self) -> int:
         return self.sock.fileno()
 
-    async def _wait(self, events: int) -> None:
-        """Wait until the socket is readable (POLLIN=1) / writable (POLLOUT=4)."""
+    async def _wait(self, events: int, timeout: float | None = None) -> None:
+        """Wait until the socket is readable (POLLIN=1) / writable (POLLOUT=4);
+        asyncio.TimeoutError after ``timeout`` seconds (a timer handle, not a
+        wait_for task: this sits on every request's critical path)."""
         fut = self._loop.create_future()
         fd = self.sock.fileno()
 
@@ -124,14 +126,21 @@ class RawConn:
             if not fut.done():
                 fut.set_result(None)
 
+        def expire() -> None:
+            if not fut.done():
+                fut.set_exception(asyncio.TimeoutError())
+
         rd, wr = bool(events & 1), bool(events & 4)
         if rd:
             self._loop.add_reader(fd, ready)
         if wr:
             self._loop.add_writer(fd, ready)
+        timer = self._loop.call_later(timeout, expire) if timeout is not None else None
         try:
             await fut
         finally:
+            if timer is not None:
+                timer.cancel()
             if rd:
                 self._loop.remove_reader(fd)
             if wr:
@@ -152,10 +161,16 @@ class RawConn:
         except asyncio.TimeoutError as e:
             raise RawHTTPError("tls handshake timed out") from e
 
-    async def recv(self, n: int) -> bytes:
-        """Up to n bytes; b"" at end of stream."""
+    async def recv(self, n: int, timeout: float | None = None) -> bytes:
+        """Up to n bytes; b"" at end of stream.  Tries the (non-blocking)
+        socket first and waits only if nothing is there yet; ``timeout``
+        bounds each wait (asyncio.TimeoutError)."""
         if self.tls is None:
-            return await self._loop.sock_recv(self.sock, n)
+            while True:
+                try:
+                    return self.sock.recv(n)
+                except (BlockingIOError, InterruptedError):
+                    await self._wait(1, timeout)
         while True:
             try:
                 r = self.tls.read_nb(n)
@@ -163,13 +178,23 @@ class RawConn:
                 raise RawHTTPError(str(e)) from e
             if isinstance(r, bytes):
                 return r
-            await self._wait(r)
+            await self._wait(r, timeout)
 
-    async def sendall(self, data: bytes) -> None:
-        if self.tls is None:
-            await self._loop.sock_sendall(self.sock, data)
-            return
+    async def sendall(self, data: bytes, timeout: float | None = None) -> None:
+        """Send everything; a request head normally leaves in one ``send``
+        with no event-loop round trip."""
         mv = memoryview(data)
+        if self.tls is None:
+            while mv:
+                try:
+                    k = self.sock.send(mv)
+                except (BlockingIOError, InterruptedError):
+                    k = 0
+                if k:
+                    mv = mv[k:]
+                else:
+                    await self._wait(4, timeout)
+            return
         while mv:
             try:
                 n, want = self.tls.write_nb(bytes(mv))
@@ -178,7 +203,7 @@ class RawConn:
             if n:
                 mv = mv[n:]
             else:
-                await self._wait(want)
+                await self._wait(want, timeout)
         while True:                      # ciphertext the TLS layer still holds
             try:
                 want = self.tls.flush_nb()
@@ -186,7 +211,7 @@ class RawConn:
                 raise RawHTTPError(str(e)) from e
             if not want:
                 return
-            await self._wait(want)
+            await self._wait(want, timeout)
 
     def alive(self) -> bool:
         """Idle pooled connection still usable (peer has not closed it)."""
@@ -362,10 +387,10 @@ def request_head(method: str, target: str, headers: dict) -> bytes:
     return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
 
 
-async def _recv(s, n: int) -> bytes:
+async def _recv(s, n: int, timeout: float) -> bytes:
     if isinstance(s, RawConn):
-        return await s.recv(n)
-    return await asyncio.get_running_loop().sock_recv(s, n)
+        return await s.recv(n, timeout)
+    return await asyncio.wait_for(asyncio.get_running_loop().sock_recv(s, n), timeout)
 
 
 async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int = 64 << 10) -> Head:
@@ -377,7 +402,7 @@ async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int 
         if len(buf) > max_size:
             raise RawHTTPError("response head too large")
         try:
-            d = await asyncio.wait_for(_recv(s, 256 << 10), timeout)
+            d = await _recv(s, 256 << 10, timeout)
         except asyncio.TimeoutError as e:
             raise RawHTTPError("timed out waiting for the response head") from e
         if not d:
@@ -407,7 +432,7 @@ async def read_small_body(s: "RawConn | socket.socket", head: Head, timeout: flo
 
     async def more() -> bool:
         try:
-            d = await asyncio.wait_for(_recv(s, 256 << 10), timeout)
+            d = await _recv(s, 256 << 10, timeout)
         except asyncio.TimeoutError as e:
             raise RawHTTPError("timed out reading the response body") from e
         if not d:
