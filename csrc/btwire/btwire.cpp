@@ -21,395 +21,44 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <algorithm>
-#include <chrono>
-#include <cstdint>
-#include <cstring>
-#include <deque>
-#include <memory>
-#include <mutex>
-#include <stdexcept>
-#include <string>
-#include <unordered_map>
-#include <unordered_set>
-#include <vector>
+#include "btwire_core.h"
 
 namespace py = pybind11;
+using namespace tritondl_btwire;
 
 namespace {
 
-constexpr uint32_t kBlock = 16384;
-constexpr uint8_t kChoke = 0, kUnchoke = 1, kPiece = 7, kRequest = 6, kCancel = 8, kReject = 16;
-constexpr uint32_t kMaxMsg = 2 * 1024 * 1024 + 13;
-
-using Clock = std::chrono::steady_clock;
-
-inline uint32_t be32(const uint8_t* p) {
-  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+// Events as the tuples Torrent._native_events expects.
+py::list to_py(const std::vector<Event>& ev) {
+  py::list out;
+  for (const Event& e : ev) {
+    switch (e.kind) {
+      case Event::kPieceDone: out.append(py::make_tuple("piece", e.piece)); break;
+      case Event::kMsg: out.append(py::make_tuple("msg", int(e.id), py::bytes(e.data))); break;
+      case Event::kChoked: out.append(py::make_tuple("choke")); break;
+      case Event::kUnchoked: out.append(py::make_tuple("unchoke")); break;
+      case Event::kBad: out.append(py::make_tuple("bad", e.data)); break;
+    }
+  }
+  return out;
 }
-inline void put_be32(std::string& s, uint32_t v) {
-  const char b[4] = {char(v >> 24), char(v >> 16), char(v >> 8), char(v)};
-  s.append(b, 4);
+
+py::tuple feed_bytes(Link& l, const py::bytes& data) {
+  char* p = nullptr;
+  Py_ssize_t n = 0;
+  PyBytes_AsStringAndSize(data.ptr(), &p, &n);
+  std::vector<Event> ev;
+  std::string out;
+  l.feed(reinterpret_cast<const uint8_t*>(p), size_t(n), &ev, &out);
+  return py::make_tuple(to_py(ev), py::bytes(out));
 }
-inline uint64_t key(uint32_t piece, uint32_t block) { return (uint64_t(piece) << 32) | block; }
 
-// Recycled piece buffers: a 1 MiB bytes object per piece would be a fresh
-// mmap (256 page faults) plus a copy; a completed piece instead moves its
-// buffer into a Piece (buffer protocol, no copy) that hands it back here
-// when Python drops the last reference (after verify + write).
-struct Pool {
-  std::mutex mu;
-  std::vector<std::vector<uint8_t>> free;
-  size_t cap = 64;
-  std::vector<uint8_t> get(size_t n) {
-    std::vector<uint8_t> v;
-    {
-      std::lock_guard<std::mutex> g(mu);
-      if (!free.empty()) {
-        v = std::move(free.back());
-        free.pop_back();
-      }
-    }
-    v.resize(n);  // zero-fills only growth; a recycled buffer keeps its bytes
-    return v;
-  }
-  void put(std::vector<uint8_t>&& v) {
-    std::lock_guard<std::mutex> g(mu);
-    if (free.size() < cap) free.push_back(std::move(v));
-  }
-};
-
-// A completed piece handed to Python: read-only bytes-like (memoryview(),
-// hashlib, os.pwrite accept it), buffer returned to the pool on release.
-class Piece {
- public:
-  Piece(std::vector<uint8_t>&& d, std::shared_ptr<Pool> pool) : data_(std::move(d)), pool_(std::move(pool)) {}
-  ~Piece() {
-    if (pool_) pool_->put(std::move(data_));
-  }
-  Piece(const Piece&) = delete;
-  Piece& operator=(const Piece&) = delete;
-  const std::vector<uint8_t>& data() const { return data_; }
-
- private:
-  std::vector<uint8_t> data_;
-  std::shared_ptr<Pool> pool_;
-};
-
-struct PieceBuf {
-  std::vector<uint8_t> data;
-  std::vector<uint8_t> got;
-  uint32_t nblocks = 0, ngot = 0;
-  uint64_t nbytes = 0;
-};
-
-class PieceStore {
- public:
-  PieceStore(uint32_t num_pieces, uint64_t piece_len, uint64_t total_len)
-      : n_(num_pieces), plen_(piece_len), total_(total_len) {
-    if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
-  }
-
-  uint64_t piece_size(uint32_t i) const {
-    if (i >= n_) throw std::out_of_range("piece index");
-    return i + 1 == n_ ? total_ - uint64_t(i) * plen_ : plen_;
-  }
-  uint32_t blocks(uint32_t i) const { return uint32_t((piece_size(i) + kBlock - 1) / kBlock); }
-
-  // Start buffering piece i (no-op if it already is).  Returns true if new.
-  bool begin(uint32_t i) {
-    if (pieces_.count(i)) return false;
-    PieceBuf& b = pieces_[i];
-    b.data = pool_->get(piece_size(i));
-    b.nblocks = blocks(i);
-    b.got.assign(b.nblocks, 0);
-    return true;
-  }
-  bool active(uint32_t i) const { return pieces_.count(i) != 0; }
-  bool has_block(uint32_t i, uint32_t b) const {
-    auto it = pieces_.find(i);
-    return it != pieces_.end() && b < it->second.nblocks && it->second.got[b];
-  }
-  uint32_t received(uint32_t i) const {
-    auto it = pieces_.find(i);
-    return it == pieces_.end() ? 0 : it->second.ngot;
-  }
-  // Copy one block in.  Returns 1 if it completed the piece, 0 if stored /
-  // duplicate / not wanted, -1 on bad geometry.
-  int put(uint32_t i, uint32_t off, const uint8_t* p, size_t n) {
-    auto it = pieces_.find(i);
-    if (it == pieces_.end()) return 0;
-    PieceBuf& b = it->second;
-    if (off % kBlock) return -1;
-    const uint32_t bi = off / kBlock;
-    if (bi >= b.nblocks) return -1;
-    const uint64_t want = std::min<uint64_t>(kBlock, b.data.size() - off);
-    if (n != want) return -1;
-    if (b.got[bi]) return 0;
-    std::memcpy(b.data.data() + off, p, n);
-    b.got[bi] = 1;
-    b.nbytes += n;
-    bytes_ += n;
-    return ++b.ngot == b.nblocks ? 1 : 0;
-  }
-  std::unique_ptr<Piece> take(uint32_t i) {
-    auto it = pieces_.find(i);
-    if (it == pieces_.end()) throw std::out_of_range("piece not buffered");
-    auto out = std::make_unique<Piece>(std::move(it->second.data), pool_);
-    bytes_ -= it->second.nbytes;
-    pieces_.erase(it);
-    return out;
-  }
-  void reset(uint32_t i) {
-    auto it = pieces_.find(i);
-    if (it == pieces_.end()) return;
-    bytes_ -= it->second.nbytes;
-    pool_->put(std::move(it->second.data));
-    pieces_.erase(it);
-  }
-  size_t pooled() {
-    std::lock_guard<std::mutex> g(pool_->mu);
-    return pool_->free.size();
-  }
-  std::vector<uint32_t> active_pieces() const {
-    std::vector<uint32_t> v;
-    v.reserve(pieces_.size());
-    for (auto& kv : pieces_) v.push_back(kv.first);
-    std::sort(v.begin(), v.end());
-    return v;
-  }
-  uint64_t partial_bytes() const { return bytes_; }   // bytes of not-yet-complete buffered pieces
-  uint32_t num_pieces() const { return n_; }
-
- private:
-  uint32_t n_;
-  uint64_t plen_, total_;
-  uint64_t bytes_ = 0;
-  std::unordered_map<uint32_t, PieceBuf> pieces_;
-  std::shared_ptr<Pool> pool_ = std::make_shared<Pool>();
-};
-
-class Link {
- public:
-  Link(std::shared_ptr<PieceStore> store, int pipeline, bool fast)
-      : store_(std::move(store)), pipeline_(std::max(1, pipeline)), fast_(fast) {}
-
-  // Parse `data`; returns (events, bytes to send).  events: ("piece", i) when a
-  // block from this link completed piece i; ("msg", id, payload) for every
-  // non-data message; ("choke",) / ("unchoke",) after handling them here;
-  // ("bad", reason) on a protocol violation (caller drops the peer).
-  py::tuple feed(const py::bytes& data) {
-    char* p = nullptr;
-    Py_ssize_t n = 0;
-    PyBytes_AsStringAndSize(data.ptr(), &p, &n);
-    reserve(size_t(n));
-    std::memcpy(buf_.data() + wpos_, p, size_t(n));
-    wpos_ += size_t(n);
-    return parse();
-  }
-
-  // Zero-copy receive (asyncio BufferedProtocol): the socket reads straight
-  // into the link's buffer, then feed_n(nbytes) parses what arrived.  The
-  // view stays valid until the next feed/feed_n call.
-  py::memoryview recv_buffer(size_t want) {
-    reserve(std::max<size_t>(want, 4096));
-    return py::memoryview::from_memory(buf_.data() + wpos_, py::ssize_t(buf_.size() - wpos_), false);
-  }
-  py::tuple feed_n(size_t n) {
-    if (n > buf_.size() - wpos_) throw std::out_of_range("feed_n past the receive buffer");
-    wpos_ += n;
-    return parse();
-  }
-
- private:
-  // Room for n more bytes after wpos_: drop consumed bytes first (the kept
-  // tail is less than one message), grow only if still short.
-  void reserve(size_t n) {
-    if (rpos_) {
-      if (wpos_ > rpos_) std::memmove(buf_.data(), buf_.data() + rpos_, wpos_ - rpos_);
-      wpos_ -= rpos_;
-      rpos_ = 0;
-    }
-    if (buf_.size() - wpos_ < n) buf_.resize(wpos_ + n);
-  }
-
-  py::tuple parse() {
-    py::list ev;
-    size_t pos = rpos_;
-    const size_t len = wpos_;
-    bool bad = false;
-    while (len - pos >= 4) {
-      const uint32_t ml = be32(&buf_[pos]);
-      if (ml > kMaxMsg) {
-        ev.append(py::make_tuple("bad", "message too large"));
-        bad = true;
-        break;
-      }
-      if (len - pos < 4 + size_t(ml)) break;
-      const uint8_t* m = &buf_[pos + 4];
-      pos += 4 + ml;
-      if (ml == 0) continue;  // keep-alive
-      const uint8_t id = m[0];
-      const uint8_t* pl = m + 1;
-      const size_t pn = ml - 1;
-      if (id == kPiece) {
-        if (pn < 8) {
-          ev.append(py::make_tuple("bad", "short piece message"));
-          bad = true;
-          break;
-        }
-        const uint32_t i = be32(pl), off = be32(pl + 4);
-        out_req_.erase(key(i, off / kBlock));
-        if (i >= store_->num_pieces()) {
-          ev.append(py::make_tuple("bad", "piece index out of range"));
-          bad = true;
-          break;
-        }
-        const int r = store_->put(i, off, pl + 8, pn - 8);
-        if (r < 0) {
-          ev.append(py::make_tuple("bad", "bad block geometry"));
-          bad = true;
-          break;
-        }
-        downloaded_ += pn - 8;
-        if (r == 1) ev.append(py::make_tuple("piece", i));
-      } else if (id == kChoke) {
-        peer_choking_ = true;
-        if (!fast_) lapse_all();  // BEP 3: a choke drops every pending request
-        ev.append(py::make_tuple("choke"));
-      } else if (id == kUnchoke) {
-        peer_choking_ = false;
-        ev.append(py::make_tuple("unchoke"));
-      } else if (id == kReject && pn >= 12) {
-        const uint32_t i = be32(pl), off = be32(pl + 4);
-        if (out_req_.erase(key(i, off / kBlock))) redo_.push_back(key(i, off / kBlock));
-      } else {
-        ev.append(py::make_tuple("msg", int(id), py::bytes(reinterpret_cast<const char*>(pl), pn)));
-      }
-    }
-    rpos_ = pos;
-    if (rpos_ == wpos_) rpos_ = wpos_ = 0;
-    std::string out = bad ? std::string() : requests();
-    return py::make_tuple(ev, py::bytes(out));
-  }
-
- public:
-
-  // Requests (and queued cancels) to send now.
-  py::bytes pump() { return py::bytes(requests()); }
-
-  void assign(uint32_t i) {
-    if (i >= store_->num_pieces()) throw std::out_of_range("piece index");
-    store_->begin(i);
-    if (std::find(assigned_.begin(), assigned_.end(), i) == assigned_.end()) {
-      assigned_.push_back(i);
-      cursor_[i] = 0;
-    }
-  }
-  // Another link (or a web seed) completed piece i: forget it, cancel what we asked for.
-  void piece_done(uint32_t i) {
-    unassign(i, true);
-  }
-  // Drop piece i without cancelling (e.g. failed verification: Python re-plans it).
-  void drop(uint32_t i) { unassign(i, false); }
-
-  // Room for more work: fewer unrequested-but-assigned blocks than the pipeline.
-  bool need_work() const {
-    size_t pending = redo_.size();
-    for (uint32_t i : assigned_) {
-      auto it = cursor_.find(i);
-      if (it != cursor_.end()) pending += store_->blocks(i) - std::min(store_->blocks(i), it->second);
-      if (pending >= size_t(pipeline_)) return false;
-    }
-    return true;
-  }
-  std::vector<uint32_t> assigned() const { return assigned_; }
-  size_t outstanding() const { return out_req_.size(); }
-  double oldest_request_age() const {
-    if (out_req_.empty()) return 0.0;
-    auto oldest = Clock::time_point::max();
-    for (auto& kv : out_req_) oldest = std::min(oldest, kv.second);
-    return std::chrono::duration<double>(Clock::now() - oldest).count();
-  }
-  // Everything this link had asked for goes back to the pool (timeout / snub).
-  void lapse_all() {
-    for (auto& kv : out_req_) redo_.push_back(kv.first);
-    out_req_.clear();
-  }
-  bool peer_choking() const { return peer_choking_; }
-  void set_peer_choking(bool c) { peer_choking_ = c; }
-  uint64_t downloaded() const { return downloaded_; }
-  size_t buffered() const { return wpos_ - rpos_; }
-
- private:
-  void unassign(uint32_t i, bool cancel) {
-    auto it = std::find(assigned_.begin(), assigned_.end(), i);
-    if (it != assigned_.end()) assigned_.erase(it);
-    cursor_.erase(i);
-    for (auto r = out_req_.begin(); r != out_req_.end();) {
-      if (uint32_t(r->first >> 32) == i) {
-        if (cancel) cancels_.push_back(r->first);
-        r = out_req_.erase(r);
-      } else {
-        ++r;
-      }
-    }
-    redo_.erase(std::remove_if(redo_.begin(), redo_.end(), [&](uint64_t k) { return uint32_t(k >> 32) == i; }),
-                redo_.end());
-  }
-
-  void msg3(std::string& out, uint8_t id, uint32_t i, uint32_t off, uint32_t n) {
-    put_be32(out, 13);
-    out.push_back(char(id));
-    put_be32(out, i);
-    put_be32(out, off);
-    put_be32(out, n);
-  }
-
-  std::string requests() {
-    std::string out;
-    for (uint64_t k : cancels_) {
-      const uint32_t i = uint32_t(k >> 32), b = uint32_t(k);
-      msg3(out, kCancel, i, b * kBlock, uint32_t(std::min<uint64_t>(kBlock, store_->piece_size(i) - uint64_t(b) * kBlock)));
-    }
-    cancels_.clear();
-    if (peer_choking_) return out;
-    const auto now = Clock::now();
-    auto issue = [&](uint32_t i, uint32_t b) {
-      out_req_[key(i, b)] = now;
-      msg3(out, kRequest, i, b * kBlock, uint32_t(std::min<uint64_t>(kBlock, store_->piece_size(i) - uint64_t(b) * kBlock)));
-    };
-    while (out_req_.size() < size_t(pipeline_) && !redo_.empty()) {
-      const uint64_t k = redo_.front();
-      redo_.pop_front();
-      const uint32_t i = uint32_t(k >> 32), b = uint32_t(k);
-      if (cursor_.count(i) && !store_->has_block(i, b) && !out_req_.count(k)) issue(i, b);
-    }
-    for (size_t a = 0; a < assigned_.size() && out_req_.size() < size_t(pipeline_); ++a) {
-      const uint32_t i = assigned_[a];
-      uint32_t& cur = cursor_[i];
-      const uint32_t nb = store_->blocks(i);
-      while (cur < nb && out_req_.size() < size_t(pipeline_)) {
-        const uint32_t b = cur++;
-        if (!store_->has_block(i, b) && !out_req_.count(key(i, b))) issue(i, b);
-      }
-    }
-    return out;
-  }
-
-  std::shared_ptr<PieceStore> store_;
-  int pipeline_;
-  bool fast_;
-  bool peer_choking_ = true;
-  std::vector<uint8_t> buf_;                              // received bytes [rpos_, wpos_)
-  size_t rpos_ = 0, wpos_ = 0;
-  std::vector<uint32_t> assigned_;
-  std::unordered_map<uint32_t, uint32_t> cursor_;        // next never-requested block per assigned piece
-  std::unordered_map<uint64_t, Clock::time_point> out_req_;
-  std::deque<uint64_t> redo_;                             // lapsed / rejected blocks to ask for again
-  std::vector<uint64_t> cancels_;
-  uint64_t downloaded_ = 0;
-};
+py::tuple feed_n(Link& l, size_t n) {
+  std::vector<Event> ev;
+  std::string out;
+  l.feed_n(n, &ev, &out);
+  return py::make_tuple(to_py(ev), py::bytes(out));
+}
 
 }  // namespace
 
@@ -448,10 +97,19 @@ PYBIND11_MODULE(_btwire, m) {
   py::class_<Link>(m, "Link")
       .def(py::init<std::shared_ptr<PieceStore>, int, bool>(), py::arg("store"), py::arg("pipeline") = 128,
            py::arg("fast") = false)
-      .def("feed", &Link::feed)
-      .def("recv_buffer", &Link::recv_buffer, py::arg("want") = 262144)
-      .def("feed_n", &Link::feed_n)
-      .def("pump", &Link::pump)
+      .def("feed", &feed_bytes,
+           "Parse bytes read from the peer; returns (events, bytes to send).  events: ('piece', i) when a "
+           "block from this link completed piece i; ('msg', id, payload) for every non-data message; "
+           "('choke',) / ('unchoke',) after handling them here; ('bad', reason) on a protocol violation.")
+      .def("recv_buffer",
+           [](Link& l, size_t want) {
+             auto span = l.recv_buffer(want);
+             return py::memoryview::from_memory(span.first, py::ssize_t(span.second), false);
+           },
+           py::arg("want") = 262144,
+           "Writable view of the receive buffer for recv_into (valid until the next feed/feed_n/recv_buffer).")
+      .def("feed_n", &feed_n, "Parse the n bytes just written into recv_buffer(); same result as feed().")
+      .def("pump", [](Link& l) { return py::bytes(l.pump()); })
       .def("assign", &Link::assign)
       .def("piece_done", &Link::piece_done)
       .def("drop", &Link::drop)

@@ -18,6 +18,7 @@
 #include "../hash/hash_core.h"
 #include "../relay/relay_core.h"
 #include "../utp/utp_engine.h"
+#include "../btwire/btwire_core.h"
 
 using namespace tritondl_hash;
 
@@ -311,6 +312,117 @@ static void test_tls_relay(size_t size) {
   ::unlink(opath);
 }
 
+// BitTorrent peer wire (csrc/btwire): a seeded swarm stream cut at random
+// points must assemble byte-exact pieces; mutated and random streams (it
+// parses untrusted peer input) must end in a kBad event or be absorbed,
+// never touch memory outside the buffers.
+static std::string bt_msg(uint8_t id, const std::string& payload) {
+  std::string m;
+  const uint32_t n = uint32_t(payload.size() + 1);
+  m.push_back(char(n >> 24));
+  m.push_back(char(n >> 16));
+  m.push_back(char(n >> 8));
+  m.push_back(char(n));
+  m.push_back(char(id));
+  return m + payload;
+}
+static std::string be32s(uint32_t v) {
+  return std::string{char(v >> 24), char(v >> 16), char(v >> 8), char(v)};
+}
+
+static void test_btwire(unsigned seed, int rounds) {
+  using namespace tritondl_btwire;
+  std::mt19937 rng(seed);
+  const uint32_t plen = 3 * kBlock, npieces = 5;
+  const uint64_t total = uint64_t(npieces - 1) * plen + kBlock + 100;
+  std::string content(total, 0);
+  for (auto& c : content) c = char(rng());
+  // well-formed stream, random cuts, interleaved control messages
+  {
+    auto store = std::make_shared<PieceStore>(npieces, plen, total);
+    Link link(store, 16, true);
+    for (uint32_t i = 0; i < npieces; ++i) link.assign(i);
+    std::string stream = bt_msg(kUnchoke, "");
+    for (uint32_t i = 0; i < npieces; ++i) {
+      const uint64_t ps = store->piece_size(i);
+      for (uint64_t off = 0; off < ps; off += kBlock) {
+        const uint64_t n = std::min<uint64_t>(kBlock, ps - off);
+        stream += bt_msg(kPiece, be32s(i) + be32s(uint32_t(off)) + content.substr(i * plen + off, n));
+        if (rng() % 3 == 0) stream += bt_msg(4, be32s(i));  // HAVE
+        if (rng() % 5 == 0) stream += std::string(4, '\0');  // keep-alive
+      }
+    }
+    std::vector<Event> ev;
+    std::string out;
+    size_t pos = 0;
+    while (pos < stream.size()) {
+      const size_t cut = std::min<size_t>(stream.size() - pos, 1 + rng() % 40000);
+      if (rng() % 2) {
+        auto span = link.recv_buffer(cut);
+        CHECK(span.second >= cut);
+        std::memcpy(span.first, stream.data() + pos, cut);
+        link.feed_n(cut, &ev, &out);
+      } else {
+        link.feed(reinterpret_cast<const uint8_t*>(stream.data() + pos), cut, &ev, &out);
+      }
+      pos += cut;
+    }
+    uint32_t done = 0;
+    for (const Event& e : ev) {
+      CHECK(e.kind != Event::kBad);
+      if (e.kind == Event::kPieceDone) {
+        auto piece = store->take(e.piece);
+        CHECK(std::memcmp(piece->data().data(), content.data() + e.piece * plen, piece->data().size()) == 0);
+        ++done;
+      }
+    }
+    CHECK(done == npieces && link.buffered() == 0);
+  }
+  // mutated / random streams
+  for (int r = 0; r < rounds; ++r) {
+    auto store = std::make_shared<PieceStore>(npieces, plen, total);
+    Link link(store, 1 + int(rng() % 64), rng() % 2);
+    for (uint32_t i = 0; i < npieces; ++i)
+      if (rng() % 2) link.assign(i);
+    std::string stream;
+    for (int k = 0; k < 30; ++k) {
+      const uint32_t i = rng() % (npieces + 2), off = (rng() % 5) * kBlock + (rng() % 7 == 0 ? 1 : 0);
+      switch (rng() % 6) {
+        case 0: stream += bt_msg(kPiece, be32s(i) + be32s(off) + std::string(rng() % 3 ? kBlock : rng() % 20000, 'x')); break;
+        case 1: stream += bt_msg(uint8_t(rng()), std::string(rng() % 64, char(rng()))); break;
+        case 2: stream += bt_msg(kReject, be32s(i) + be32s(off) + be32s(kBlock)); break;
+        case 3: stream += bt_msg(uint8_t(rng() % 2), ""); break;  // (un)choke
+        case 4: {
+          std::string junk(rng() % 300, 0);
+          for (auto& c : junk) c = char(rng());
+          stream += junk;
+          break;
+        }
+        default: stream += bt_msg(kPiece, std::string(rng() % 8, 'p')); break;  // short
+      }
+    }
+    for (int f = 0; f < 20 && !stream.empty(); ++f) stream[rng() % stream.size()] = char(rng());  // bit rot
+    std::vector<Event> ev;
+    std::string out;
+    size_t pos = 0;
+    bool bad = false;
+    while (pos < stream.size() && !bad) {
+      const size_t cut = std::min<size_t>(stream.size() - pos, 1 + rng() % 5000);
+      link.feed(reinterpret_cast<const uint8_t*>(stream.data() + pos), cut, &ev, &out);
+      for (const Event& e : ev) {
+        if (e.kind == Event::kBad) bad = true;
+        if (e.kind == Event::kPieceDone) store->take(e.piece);
+      }
+      ev.clear();
+      pos += cut;
+      if (rng() % 4 == 0) link.piece_done(rng() % npieces);
+      if (rng() % 4 == 0) link.lapse_all();
+      out = link.pump();
+    }
+    CHECK(store->partial_bytes() <= total);
+  }
+}
+
 int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
@@ -322,6 +434,7 @@ int main(int argc, char** argv) {
   test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
+  test_btwire(7, quick ? 300 : 3000);
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

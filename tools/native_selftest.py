@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Build and run csrc/tests/native_selftest.cpp (host C++ cores: hashing,
-aws-chunked signing, threaded piece verification, the relay pumps, uTP engine).
+aws-chunked signing, threaded piece verification, the relay pumps, uTP engine,
+the BitTorrent peer-wire parser with seeded fuzzing).
 
     python tools/native_selftest.py              # plain -O2 build
     python tools/native_selftest.py --sanitize   # ASan+UBSan build, then TSan build
