@@ -94,6 +94,28 @@ PYBIND11_MODULE(_btwire, m) {
       .def("reset", &PieceStore::reset)
       .def("active_pieces", &PieceStore::active_pieces)
       .def_property_readonly("partial_bytes", &PieceStore::partial_bytes);
+  py::class_<Source, std::shared_ptr<Source>>(m, "Source")
+      .def(py::init<uint32_t, uint64_t, uint64_t>(), py::arg("num_pieces"), py::arg("piece_len"),
+           py::arg("total_len"))
+      .def("add_file", &Source::add_file, py::arg("fd"), py::arg("start"), py::arg("length"),
+           "Next file of the stream (fd is dup()ed; -1 = padding, reads as zeros).")
+      .def("close", &Source::close)
+      .def("set_have", &Source::set_have)
+      .def("set_have_bits",
+           [](Source& s, const py::bytes& b) {
+             char* p = nullptr;
+             Py_ssize_t n = 0;
+             PyBytes_AsStringAndSize(b.ptr(), &p, &n);
+             s.set_have_bits(reinterpret_cast<const uint8_t*>(p), size_t(n));
+           },
+           "One byte per piece, nonzero = have.")
+      .def("has", &Source::has)
+      .def("read",
+           [](const Source& s, uint64_t gofs, size_t n) {
+             std::string out(n, '\0');
+             if (!s.read(gofs, &out[0], n)) throw std::runtime_error("short read");
+             return py::bytes(out);
+           });
   py::class_<Link>(m, "Link")
       .def(py::init<std::shared_ptr<PieceStore>, int, bool>(), py::arg("store"), py::arg("pipeline") = 128,
            py::arg("fast") = false)
@@ -120,5 +142,9 @@ PYBIND11_MODULE(_btwire, m) {
       .def_property_readonly("outstanding", &Link::outstanding)
       .def_property("peer_choking", &Link::peer_choking, &Link::set_peer_choking)
       .def_property_readonly("downloaded", &Link::downloaded)
+      .def("set_source", &Link::set_source)
+      .def_property("serving", &Link::serving, &Link::set_serving)
+      .def_property_readonly("uploaded", &Link::uploaded)
+      .def_property_readonly("serve_errors", &Link::serve_errors)
       .def_property_readonly("buffered", &Link::buffered);
 }

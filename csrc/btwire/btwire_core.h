@@ -17,12 +17,16 @@
 #include <utility>
 #include <vector>
 
+#include <cerrno>
+#include <unistd.h>
+
 namespace tritondl_btwire {
 
 
 constexpr uint32_t kBlock = 16384;
 constexpr uint8_t kChoke = 0, kUnchoke = 1, kPiece = 7, kRequest = 6, kCancel = 8, kReject = 16;
 constexpr uint32_t kMaxMsg = 2 * 1024 * 1024 + 13;
+constexpr uint32_t kMaxRequest = 128 * 1024;  // larger REQUESTs are refused (as libtorrent does)
 
 using Clock = std::chrono::steady_clock;
 
@@ -183,6 +187,87 @@ class PieceStore {
   std::shared_ptr<Pool> pool_ = std::make_shared<Pool>();
 };
 
+// Read side of a torrent's files, for answering REQUESTs without Python.
+// Holds its own dup()s of the storage fds (closing the storage cannot make a
+// link read a reused descriptor); close() ends serving before the job's
+// files go away.  BEP 47 padding files (fd -1) read as zeros.
+class Source {
+ public:
+  Source(uint32_t num_pieces, uint64_t piece_len, uint64_t total_len)
+      : n_(num_pieces), plen_(piece_len), total_(total_len), have_(num_pieces, 0) {
+    if (piece_len == 0) throw std::invalid_argument("piece_len must be > 0");
+  }
+  ~Source() { close(); }
+  Source(const Source&) = delete;
+  Source& operator=(const Source&) = delete;
+
+  // Files in stream order: [start, start + len) of the torrent's byte stream.
+  void add_file(int fd, uint64_t start, uint64_t len) {
+    if (!spans_.empty() && start < spans_.back().start) throw std::invalid_argument("files out of order");
+    const int own = fd >= 0 ? ::dup(fd) : -1;
+    if (fd >= 0 && own < 0) throw std::runtime_error("dup failed");
+    spans_.push_back({own, start, len});
+  }
+  void close() {
+    for (auto& s : spans_)
+      if (s.fd >= 0) ::close(s.fd);
+    spans_.clear();
+    closed_ = true;
+  }
+  void set_have(uint32_t i) {
+    if (i < n_) have_[i] = 1;
+  }
+  void set_have_bits(const uint8_t* bits, size_t n) {
+    for (size_t i = 0; i < n && i < n_; ++i) have_[i] = bits[i] ? 1 : 0;
+  }
+  bool has(uint32_t i) const { return !closed_ && i < n_ && have_[i]; }
+  uint32_t num_pieces() const { return n_; }
+  uint64_t piece_size(uint32_t i) const { return i + 1 == n_ ? total_ - uint64_t(i) * plen_ : plen_; }
+  uint64_t piece_len() const { return plen_; }
+
+  // Copy stream bytes [gofs, gofs + n) into dst; false on a short read.
+  bool read(uint64_t gofs, char* dst, size_t n) const {
+    if (closed_) return false;
+    const uint64_t end = gofs + n;
+    auto it = std::upper_bound(spans_.begin(), spans_.end(), gofs,
+                               [](uint64_t g, const Span& s) { return g < s.start; });
+    if (it != spans_.begin()) --it;
+    uint64_t pos = gofs;
+    for (; it != spans_.end() && pos < end; ++it) {
+      const uint64_t fe = it->start + it->len;
+      if (it->len == 0 || fe <= pos) continue;
+      if (it->start > pos) return false;  // hole in the layout
+      const uint64_t b = std::min(end, fe);
+      char* d = dst + (pos - gofs);
+      const size_t m = size_t(b - pos);
+      if (it->fd < 0) {
+        std::memset(d, 0, m);
+      } else {
+        size_t got = 0;
+        while (got < m) {
+          const ssize_t r = ::pread(it->fd, d + got, m - got, off_t(pos - it->start + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) return false;
+          got += size_t(r);
+        }
+      }
+      pos = b;
+    }
+    return pos == end;
+  }
+
+ private:
+  struct Span {
+    int fd;
+    uint64_t start, len;
+  };
+  uint32_t n_;
+  uint64_t plen_, total_;
+  std::vector<uint8_t> have_;
+  std::vector<Span> spans_;
+  bool closed_ = false;
+};
+
 class Link {
  public:
   Link(std::shared_ptr<PieceStore> store, int pipeline, bool fast)
@@ -274,6 +359,10 @@ class Link {
       } else if (id == kReject && pn >= 12) {
         const uint32_t i = be32(pl), off = be32(pl + 4);
         if (out_req_.erase(key(i, off / kBlock))) redo_.push_back(key(i, off / kBlock));
+      } else if (id == kRequest && source_ && pn >= 12) {
+        serve(be32(pl), be32(pl + 4), be32(pl + 8), out);
+      } else if (id == kCancel && source_ && pn >= 12) {
+        // every REQUEST was answered in the read that carried it: nothing to withdraw
       } else {
         ev->push_back(Event{Event::kMsg, 0, id, std::string(reinterpret_cast<const char*>(pl), pn)});
       }
@@ -335,6 +424,15 @@ class Link {
   uint64_t downloaded() const { return downloaded_; }
   size_t buffered() const { return wpos_ - rpos_; }
 
+  // Answer the peer's block REQUESTs from `src` (PIECE, or REJECT on a fast
+  // connection for what we cannot serve).  Without a source REQUEST and
+  // CANCEL reach Python as kMsg events.
+  void set_source(std::shared_ptr<Source> src) { source_ = std::move(src); }
+  bool serving() const { return serving_; }
+  void set_serving(bool s) { serving_ = s; }   // false: we choke this peer
+  uint64_t uploaded() const { return uploaded_; }
+  uint64_t serve_errors() const { return serve_errors_; }
+
  private:
   void unassign(uint32_t i, bool cancel) {
     auto it = std::find(assigned_.begin(), assigned_.end(), i);
@@ -350,6 +448,29 @@ class Link {
     }
     redo_.erase(std::remove_if(redo_.begin(), redo_.end(), [&](uint64_t k) { return uint32_t(k >> 32) == i; }),
                 redo_.end());
+  }
+
+  void serve(uint32_t i, uint32_t off, uint32_t n, std::string* out) {
+    bool ok = serving_ && source_->has(i) && n > 0 && n <= kMaxRequest &&
+              uint64_t(off) + n <= source_->piece_size(i);
+    if (ok) {
+      const size_t at = out->size();
+      out->resize(at + 13 + n);
+      char* h = &(*out)[at];
+      const uint32_t ml = 9 + n;
+      const char hdr[13] = {char(ml >> 24), char(ml >> 16), char(ml >> 8), char(ml), char(kPiece),
+                            char(i >> 24),  char(i >> 16),  char(i >> 8),  char(i),  char(off >> 24),
+                            char(off >> 16), char(off >> 8), char(off)};
+      std::memcpy(h, hdr, 13);
+      ok = source_->read(uint64_t(i) * source_->piece_len() + off, h + 13, n);
+      if (ok) {
+        uploaded_ += n;
+      } else {
+        out->resize(at);
+        ++serve_errors_;
+      }
+    }
+    if (!ok && fast_) msg3(*out, kReject, i, off, n);
   }
 
   void msg3(std::string& out, uint8_t id, uint32_t i, uint32_t off, uint32_t n) {
@@ -391,6 +512,9 @@ class Link {
   }
 
   std::shared_ptr<PieceStore> store_;
+  std::shared_ptr<Source> source_;
+  bool serving_ = true;
+  uint64_t uploaded_ = 0, serve_errors_ = 0;
   int pipeline_;
   bool fast_;
   bool peer_choking_ = true;

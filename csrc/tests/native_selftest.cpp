@@ -378,10 +378,34 @@ static void test_btwire(unsigned seed, int rounds) {
     }
     CHECK(done == npieces && link.buffered() == 0);
   }
+  // a source over the same content (serving REQUESTs), file + padding + file
+  char path[] = "/tmp/tritondl_btwire_XXXXXX";
+  const int sfd = ::mkstemp(path);
+  CHECK(sfd >= 0);
+  const uint64_t split = total / 2;
+  CHECK(::pwrite(sfd, content.data(), split, 0) == ssize_t(split));
+  auto src = std::make_shared<Source>(npieces, plen, total);
+  src->add_file(sfd, 0, split - 1000);
+  src->add_file(-1, split - 1000, 1000);
+  src->add_file(sfd, split, 0);
+  ::close(sfd);
+  ::unlink(path);
+  for (uint32_t i = 0; i < npieces; i += 2) src->set_have(i);
+  {
+    std::string out;
+    std::vector<Event> ev;
+    Link link(std::make_shared<PieceStore>(npieces, plen, total), 8, true);
+    link.set_source(src);
+    const std::string req = bt_msg(kRequest, be32s(0) + be32s(kBlock) + be32s(kBlock));
+    link.feed(reinterpret_cast<const uint8_t*>(req.data()), req.size(), &ev, &out);
+    CHECK(ev.empty() && out.size() == 13 + kBlock && out[4] == char(kPiece));
+    CHECK(std::memcmp(out.data() + 13, content.data() + kBlock, kBlock) == 0);
+  }
   // mutated / random streams
   for (int r = 0; r < rounds; ++r) {
     auto store = std::make_shared<PieceStore>(npieces, plen, total);
     Link link(store, 1 + int(rng() % 64), rng() % 2);
+    if (rng() % 2) link.set_source(src);
     for (uint32_t i = 0; i < npieces; ++i)
       if (rng() % 2) link.assign(i);
     std::string stream;
@@ -391,7 +415,14 @@ static void test_btwire(unsigned seed, int rounds) {
         case 0: stream += bt_msg(kPiece, be32s(i) + be32s(off) + std::string(rng() % 3 ? kBlock : rng() % 20000, 'x')); break;
         case 1: stream += bt_msg(uint8_t(rng()), std::string(rng() % 64, char(rng()))); break;
         case 2: stream += bt_msg(kReject, be32s(i) + be32s(off) + be32s(kBlock)); break;
-        case 3: stream += bt_msg(uint8_t(rng() % 2), ""); break;  // (un)choke
+        case 3:
+          if (rng() % 2) {
+            stream += bt_msg(uint8_t(rng() % 2), "");  // (un)choke
+          } else {
+            const uint32_t len = rng() % 3 ? kBlock : uint32_t(rng());
+            stream += bt_msg(kRequest, be32s(i) + be32s(uint32_t(rng() % (plen + 10))) + be32s(len));
+          }
+          break;
         case 4: {
           std::string junk(rng() % 300, 0);
           for (auto& c : junk) c = char(rng());

@@ -183,3 +183,52 @@ def test_download_uses_zero_copy_receive(tmp_path):
         await t.close()
         await seed.stop()
     asyncio.run(main())
+
+
+def test_link_serves_requests_from_source(tmp_path):
+    """REQUESTs are answered natively from the files (padding reads as zeros,
+    reads cross file boundaries); what cannot be served is REJECTed on a fast
+    connection; the source keeps its own fd dups and stops on close()."""
+    import os
+    a, b = os.urandom(3 * B + 100), os.urandom(2 * B)
+    pa, pb = tmp_path / "a", tmp_path / "b"
+    pa.write_bytes(a)
+    pb.write_bytes(b)
+    pad = 500                                      # BEP 47 padding between the files
+    stream = a + bytes(pad) + b
+    plen = 2 * B
+    n = (len(stream) + plen - 1) // plen
+    src = W.Source(n, plen, len(stream))
+    fa, fb = os.open(pa, os.O_RDONLY), os.open(pb, os.O_RDONLY)
+    src.add_file(fa, 0, len(a))
+    src.add_file(-1, len(a), pad)
+    src.add_file(fb, len(a) + pad, len(b))
+    os.close(fa)                                   # the source holds dups
+    os.close(fb)
+    src.set_have_bits(bytes([1] * (n - 1) + [0]))
+    link = W.Link(W.PieceStore(n, plen, len(stream)), pipeline=4, fast=True)
+    link.set_source(src)
+
+    def req(i, off, ln):
+        return struct.pack(">IBIII", 13, 6, i, off, ln)
+    ev, out = link.feed(req(1, B, B) + req(1, 0, 100) + req(n - 1, 0, 10) + req(0, 0, 200 * 1024) +
+                        struct.pack(">IBIII", 13, 8, 1, B, B))             # + a CANCEL: absorbed
+    assert list(ev) == []
+    got = msgs(out)
+    assert got[0] == (7, struct.pack(">II", 1, B) + stream[plen + B:plen + 2 * B])   # crosses a -> padding
+    assert got[1] == (7, struct.pack(">II", 1, 0) + stream[plen:plen + 100])
+    assert got[2] == (16, struct.pack(">III", n - 1, 0, 10))                  # not ours yet
+    assert got[3] == (16, struct.pack(">III", 0, 0, 200 * 1024))              # oversized
+    assert link.uploaded == B + 100
+    src.set_have(n - 1)
+    ev, out = link.feed(req(n - 1, 0, 10))
+    last = (n - 1) * plen
+    assert msgs(out) == [(7, struct.pack(">II", n - 1, 0) + stream[last:last + 10])]
+    link.serving = False                           # choked: refuse
+    assert msgs(link.feed(req(0, 0, 10))[1])[0][0] == 16
+    link.serving = True
+    src.close()
+    assert msgs(link.feed(req(0, 0, 10))[1])[0][0] == 16 and not src.has(0)
+    plain = W.Link(W.PieceStore(n, plen, len(stream)), pipeline=4, fast=False)
+    ev, out = plain.feed(req(0, 0, 10))            # no source: Python sees the REQUEST
+    assert list(ev) == [("msg", 6, struct.pack(">III", 0, 0, 10))] and out == b""

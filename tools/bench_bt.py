@@ -39,6 +39,8 @@ async def main() -> int:
     ap.add_argument("--profile", default="")
     ap.add_argument("--encryption", default="allow", help="MSE policy for seeders and leecher")
     ap.add_argument("--job", action="store_true", help="full worker job (download+upload+publish+ack)")
+    ap.add_argument("--python-seeders", action="store_true",
+                    help="seeders answer REQUESTs in Python instead of the native link")
     ap.add_argument("--python-wire", action="store_true",
                     help="leecher: per-block work in Python instead of the native csrc/btwire link")
     ap.add_argument("--files", type=int, default=8, help="--job: media files in the pack")
@@ -47,6 +49,8 @@ async def main() -> int:
     ap.add_argument("--s3-gbps", type=float, default=0.0,
                     help="--job: cap the fake S3's ingest link (Gbit/s; 0 = loopback speed)")
     a = ap.parse_args()
+    if a.python_seeders:
+        os.environ["TRITONDL_BT_NATIVE_WIRE"] = "0"     # read by the seeder processes (fakes/serve.py)
     if a.job:
         return await job_bench(a)
     from tritondl.bench_job import Backend
@@ -92,7 +96,8 @@ async def main() -> int:
         print(json.dumps({"metric": "bt_ingest_MB_per_sec", "value": round(a.mb * 1.048576 / dt, 1),
                           "seconds": round(dt, 3), "mb": a.mb, "seeds": a.seeds, "piece_kb": a.piece_kb,
                           "transport": "utp" if a.utp else "tcp+utp",
-                          "encryption": a.encryption, "wire": "python" if a.python_wire else "native"}),
+                          "encryption": a.encryption, "wire": "python" if a.python_wire else "native",
+                          "seeders": "python" if a.python_seeders else "native"}),
               flush=True)
     finally:
         for s in seeds:
@@ -163,6 +168,7 @@ async def job_bench(a) -> int:
                 assert r.ok and r.files == a.files and r.bytes == per * a.files, r
                 print(json.dumps({"metric": "bt_job_seconds", "value": round(dt, 3), "stream_upload": on,
                                   "s3_link_gbps": a.s3_gbps or None, "wire": "python" if a.python_wire else "native",
+                                  "seeders": "python" if a.python_seeders else "native",
                                   "mb": a.mb, "files": a.files, "seeds": a.seeds, "piece_kb": a.piece_kb,
                                   "job_MB_per_sec": round(a.mb * 1.048576 / dt, 1),
                                   "spans_ms": {k: round(v * 1000, 1) for k, v in r.marks.items()}}), flush=True)

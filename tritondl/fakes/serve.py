@@ -60,7 +60,8 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         assert seed_path, "--path required"
         info = torrent_for(seed_path, piece_kb << 10)
         cfg = TorrentConfig(listen_host="127.0.0.1", listen_port=port, seed=True, verify_device="cpu", utp=True,
-                            encryption=encryption)
+                            encryption=encryption,
+                            native_wire=os.environ.get("TRITONDL_BT_NATIVE_WIRE", "1") not in ("0", "false", "off"))
         srv = Torrent(info.infohash, os.path.dirname(os.path.abspath(seed_path)), cfg, info=info)
         await srv.start()
         await srv.download_all()

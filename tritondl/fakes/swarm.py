@@ -183,7 +183,8 @@ class Seeder:
             self.dht = await DHTNode(host="127.0.0.1", bootstrap=self.dht_bootstrap).start()
             await self.dht.bootstrap()
         cfg = TorrentConfig(listen_host="127.0.0.1", seed=True, tracker_min_interval=1.0, dht_interval=1.0,
-                            verify_device="cpu", encryption=self.encryption, listen_host6=self.listen_host6)
+                            verify_device="cpu", encryption=self.encryption, listen_host6=self.listen_host6,
+                            native_wire=not self.corrupt)   # corrupt: served by the patched Python path
         t = Torrent(self.info.infohash, self.data_dir, cfg, info=self.info, trackers=self.trackers, dht=self.dht)
         await t.start()
         await t.download_all()

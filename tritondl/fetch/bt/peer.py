@@ -285,7 +285,9 @@ class LinkReader(asyncio.BufferedProtocol):
         self._waiter: asyncio.Future | None = None
         self._exc: BaseException | None = None
         self._eof = False
-        self._paused = False
+        self._paused = False      # control messages queued up: the peer loop is behind
+        self._wpaused = False     # write buffer over the high-water mark
+        self._reading = True
 
     # -- transport callbacks --------------------------------------------------
     def get_buffer(self, sizehint: int):
@@ -310,17 +312,29 @@ class LinkReader(asyncio.BufferedProtocol):
         self._old.connection_lost(exc)
 
     def pause_writing(self) -> None:
+        # the link answers REQUESTs as it parses them: while the socket's send
+        # side is backed up, stop reading, so served blocks do not pile up
+        self._wpaused = True
+        self._update_reading()
         self._old.pause_writing()
 
     def resume_writing(self) -> None:
+        self._wpaused = False
+        self._update_reading()
         self._old.resume_writing()
+
+    def _update_reading(self) -> None:
+        want = not (self._paused or self._wpaused or self._exc is not None)
+        if want != self._reading and not self._tr.is_closing():
+            self._reading = want
+            (self._tr.resume_reading if want else self._tr.pause_reading)()
 
     # -- peer-loop side -------------------------------------------------------
     def push(self, mid: int, payload: bytes) -> None:
         self._msgs.append((mid, payload))
         if len(self._msgs) >= 1024 and not self._paused:   # the loop is behind: stop reading
             self._paused = True
-            self._tr.pause_reading()
+            self._update_reading()
         self._wake()
 
     async def get(self) -> list[tuple[int, bytes]]:
@@ -338,14 +352,14 @@ class LinkReader(asyncio.BufferedProtocol):
         msgs, self._msgs = self._msgs, []
         if self._paused:
             self._paused = False
-            self._tr.resume_reading()
+            self._update_reading()
         return msgs
 
     def _fail(self, e: BaseException) -> None:
         if self._exc is None:
             self._exc = e
         self._wake()
-        self._tr.pause_reading()
+        self._update_reading()
 
     def _wake(self) -> None:
         w = self._waiter

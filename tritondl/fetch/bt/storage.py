@@ -80,6 +80,10 @@ class FileStorage:
                 os.ftruncate(fd, n)
             self._fds[i] = fd
 
+    def fd(self, i: int) -> int:
+        """File i's descriptor, -1 for a padding file (never created)."""
+        return self._fds.get(i, -1)
+
     def close(self) -> None:
         with self._lock:
             for fd in self._fds.values():

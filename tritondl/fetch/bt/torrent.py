@@ -176,6 +176,7 @@ class Torrent:
         self._rare_dirty = True
         self._finishers: set[asyncio.Task] = set()
         self.store = None                               # _btwire.PieceStore (native data plane)
+        self.source = None                              # _btwire.Source: links serve REQUESTs from it
         self.assigned: dict[int, set] = {}              # piece -> peer keys whose links fetch it
         # per-file completion (streamed uploads): see watch_files
         self._file_cb = None                            # callable(path) for watched files
@@ -198,7 +199,7 @@ class Torrent:
         self.port = 0
         self.utp = None
         self.portfwd = None
-        self.uploaded = 0
+        self._uploaded = 0                              # Python-served bytes + links of dropped peers
         self.downloaded = 0
         self.closed = False
         self._wake = asyncio.Event()
@@ -281,6 +282,8 @@ class Torrent:
         for t in list(self._finishers):   # executor hash/write jobs must land before storage closes
             with contextlib.suppress(BaseException):
                 await t
+        if self.source is not None:
+            self.source.close()           # links stop serving before the job's files go away
         if self.storage is not None:
             self.storage.close()
         if self.db is not None:
@@ -329,8 +332,15 @@ class Torrent:
             self.have[i] = 1
         self.nhave = len(have)
         self._init_file_tracking()
-        if self.cfg.native_wire and _W is not None and self.nhave < self.info.num_pieces:
-            self.store = _W.PieceStore(self.info.num_pieces, self.info.piece_length, self.info.total_length)
+        if self.cfg.native_wire and _W is not None:
+            n, pl, total = self.info.num_pieces, self.info.piece_length, self.info.total_length
+            self.store = _W.PieceStore(n, pl, total)
+            # the links answer block REQUESTs from the files themselves (own fd dups)
+            self.source = _W.Source(n, pl, total)
+            st = self.storage
+            for fi, (_path, length) in enumerate(st.layout):
+                self.source.add_file(st.fd(fi), st.offsets[fi], length)
+            self.source.set_have_bits(bytes(self.have))
             for p in list(self.peers.values()):
                 self._attach_link(p)
         self._downloading = True
@@ -351,6 +361,8 @@ class Torrent:
             return
         p.link = _W.Link(self.store, self.cfg.pipeline, p.hs.fast)
         p.link.peer_choking = p.peer_choking
+        if self.source is not None:
+            p.link.set_source(self.source)
 
     def in_flight(self, i: int) -> bool:
         """Piece i is being fetched or verified (web seeds skip it)."""
@@ -721,10 +733,17 @@ class Torrent:
         finally:
             self._drop_peer(p)
 
+    @property
+    def uploaded(self) -> int:
+        """Bytes served to peers (tracker ``uploaded``), native links included."""
+        return self._uploaded + sum(p.link.uploaded for p in self.peers.values() if p.link is not None)
+
     def _drop_peer(self, p: _Peer) -> None:
         p.wire.close()
         if self.peers.get(p.key) is p:
             del self.peers[p.key]
+            if p.link is not None:
+                self._uploaded += p.link.uploaded
         if self.info is not None:
             for i in range(len(p.have)):
                 if p.have[i] and i < len(self.avail):
@@ -1030,6 +1049,8 @@ class Torrent:
             return True
         self.have[i] = 1
         self.nhave += 1
+        if self.source is not None:
+            self.source.set_have(i)
         for q in list(self.peers.values()):
             q.wire.have(i)
             if q.am_interested and q.have[i] and not self._wants(q):
@@ -1051,7 +1072,7 @@ class Torrent:
         # a 16 KiB pread from the page cache costs less than a thread hop
         data = self.storage.read(i, off, n)
         p.wire.piece(i, off, data)
-        self.uploaded += len(data)
+        self._uploaded += len(data)
 
     async def _timeout_loop(self) -> None:
         while not self.closed:
