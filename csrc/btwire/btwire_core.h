@@ -271,7 +271,7 @@ class Source {
 class Link {
  public:
   Link(std::shared_ptr<PieceStore> store, int pipeline, bool fast)
-      : store_(std::move(store)), pipeline_(std::max(1, pipeline)), fast_(fast) {}
+      : store_(std::move(store)), pipeline_(std::max(1, pipeline)), refill_(std::max(1, pipeline_ / 4)), fast_(fast) {}
 
   // Parse `n` more bytes of the stream.  Appends to *ev: kPieceDone when a
   // block from this link completed a piece; kMsg (id, payload) for every
@@ -489,6 +489,9 @@ class Link {
     }
     cancels_.clear();
     if (peer_choking_) return;
+    // refill in batches (a quarter of the pipeline): one small send per ~4
+    // received blocks instead of one per socket read; the pipeline stays >= 3/4 full
+    if (out_req_.size() + size_t(refill_) > size_t(pipeline_)) return;
     const auto now = Clock::now();
     auto issue = [&](uint32_t i, uint32_t b) {
       out_req_[key(i, b)] = now;
@@ -516,6 +519,7 @@ class Link {
   bool serving_ = true;
   uint64_t uploaded_ = 0, serve_errors_ = 0;
   int pipeline_;
+  int refill_;   // issue new requests only once this many slots are free
   bool fast_;
   bool peer_choking_ = true;
   std::vector<uint8_t> buf_;                              // received bytes [rpos_, wpos_)

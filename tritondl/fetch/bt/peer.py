@@ -291,7 +291,7 @@ class LinkReader(asyncio.BufferedProtocol):
 
     # -- transport callbacks --------------------------------------------------
     def get_buffer(self, sizehint: int):
-        return self._link.recv_buffer(1 << 18)
+        return self._link.recv_buffer(1 << 20)
 
     def buffer_updated(self, nbytes: int) -> None:
         try:
