@@ -38,7 +38,6 @@
 #include <climits>
 #include <condition_variable>
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -520,114 +519,6 @@ inline bool splice_body(Stream& io, int fd, uint64_t off, uint64_t want, RecvRes
   return ok;  // false: caller continues with recv + pwrite
 }
 
-// Overlapped receive: this thread fills a ring of buffers from the socket
-// while a writer thread pwrites the filled ones in order and publishes the
-// flow, so the two copies of every byte (socket -> buffer, buffer -> page
-// cache) run on two cores instead of back to back.  The writer is joined
-// before returning: nothing touches `fd` after the pump returns.
-inline bool overlap_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("TRITONDL_RELAY_OVERLAP");
-    return !(e && (std::string(e) == "0" || std::string(e) == "off"));
-  }();
-  return on;
-}
-
-inline void recv_overlapped(Stream& io, int fd, uint64_t off, uint64_t want, int64_t length, RecvResult& r,
-                            Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout, size_t fill) {
-  constexpr int K = 4;
-  Buf ring(K * fill);
-  size_t len[K] = {0, 0, 0, 0};
-  bool full[K] = {false, false, false, false};
-  std::mutex mu;
-  std::condition_variable cv_full, cv_free;
-  bool done = false;
-  std::string werr;
-  const uint64_t start = r.received;
-  std::thread writer([&] {
-    uint64_t pos = start;
-    for (int k = 0;; k = (k + 1) % K) {
-      size_t n;
-      {
-        std::unique_lock<std::mutex> l(mu);
-        cv_full.wait(l, [&] { return full[k] || done; });
-        if (!full[k]) return;  // done and drained
-        n = len[k];
-      }
-      std::string e;
-      if (!pwrite_full(fd, ring.data() + size_t(k) * fill, n, off + pos, &e)) {
-        std::lock_guard<std::mutex> l(mu);
-        werr = e;
-        full[k] = false;
-        cv_free.notify_all();
-        return;
-      }
-      pos += n;
-      if (flow) flow->advance(seg, seg_done0 + pos);
-      {
-        std::lock_guard<std::mutex> l(mu);
-        full[k] = false;
-      }
-      cv_free.notify_one();
-    }
-  });
-  auto last = Clock::now();
-  for (int k = 0; r.received < want; k = (k + 1) % K) {
-    {
-      std::unique_lock<std::mutex> l(mu);
-      cv_free.wait(l, [&] { return !full[k] || !werr.empty(); });
-      if (!werr.empty()) break;
-    }
-    char* b = ring.data() + size_t(k) * fill;
-    const size_t cap = static_cast<size_t>(std::min<uint64_t>(fill, want - r.received));
-    size_t have = 0;
-    bool eof = false;
-    const ssize_t n = recv_wait(io, b, cap, &last, idle_timeout, flow, &r.err);
-    if (n < 0) break;
-    if (n == 0) {
-      eof = true;
-    } else {
-      have = static_cast<size_t>(n);
-      while (have < cap) {
-        short w = POLLIN;
-        std::string e;
-        const ssize_t m = io.recv_nb(b + have, cap - have, &w, &e);
-        if (m > 0) {
-          have += static_cast<size_t>(m);
-          continue;
-        }
-        if (m == 0) eof = true;
-        if (m == IO_ERR) r.err = e;
-        break;
-      }
-    }
-    if (have) {
-      {
-        std::lock_guard<std::mutex> l(mu);
-        len[k] = have;
-        full[k] = true;
-      }
-      cv_full.notify_one();
-      r.received += have;
-    }
-    if (!r.err.empty()) break;
-    if (eof) {
-      r.eof = true;
-      if (length >= 0 && r.received < want) r.err = "connection closed early";
-      break;
-    }
-  }
-  {
-    std::lock_guard<std::mutex> l(mu);
-    done = true;
-  }
-  cv_full.notify_all();
-  writer.join();
-  if (!werr.empty()) {
-    if (r.err.empty()) r.err = werr;
-  }
-}
-
 inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
                             Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout,
                             size_t buf_size = 4u << 20, bool use_splice = true) {
@@ -647,16 +538,12 @@ inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, co
     if (splice_body(io, fd, off, want, r, flow, seg, seg_done0, idle_timeout) || !r.err.empty() || r.eof)
       return r;
   }
+  // TLS: decrypt into an L2-sized buffer so pwrite copies cache-hot bytes
+  Buf buf(io.plain() ? std::max<size_t>(buf_size, 64 << 10) : (256u << 10));
   // with a follower (the S3 send pump hashes 64 KiB chunks as soon as the
   // flow covers them) publish progress every 256 KiB, so the upload trails the
   // download by a few chunks instead of a whole 1 MiB batch at the end
   const size_t fill = io.plain() && !flow ? (1u << 20) : (256u << 10);
-  if (fd >= 0 && want - r.received >= (2u << 20) && overlap_enabled()) {
-    recv_overlapped(io, fd, off, want, length, r, flow, seg, seg_done0, idle_timeout, fill);
-    return r;
-  }
-  // TLS: decrypt into an L2-sized buffer so pwrite copies cache-hot bytes
-  Buf buf(io.plain() ? std::max<size_t>(buf_size, 64 << 10) : (256u << 10));
   auto last = Clock::now();
   while (r.received < want) {
     // fill the buffer with whatever is ready (TLS yields one record per read),
