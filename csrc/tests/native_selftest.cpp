@@ -237,6 +237,18 @@ static void test_relay(size_t size) {
   CHECK(ps.err.empty() && rr.err.empty() && rr.received == size && f2.watermark() == size);
   std::string back(size, '\0');
   CHECK(pread_full(ofd, &back[0], size, 0) == size && back == data);
+  // the same without splice: recv + pwrite
+  if (size >= 2) {
+    CHECK(::ftruncate(ofd, 0) == 0);
+    Flow f3({{0, static_cast<int64_t>(size), 0}});
+    std::thread rcv2([&] { rr = recv_body(s1, ofd, 0, static_cast<int64_t>(size), "xy", 2, &f3, 0, 0, 10.0,
+                                          4u << 20, false); });
+    ps = send_body(s0, "", rfd, 2, size - 2, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
+    rcv2.join();
+    CHECK(ps.err.empty() && rr.err.empty() && rr.received == size && f3.watermark() == size);
+    back.assign(size, '\0');
+    CHECK(pread_full(ofd, &back[0], size, 0) == size && back.substr(2) == data.substr(2) && back.substr(0, 2) == "xy");
+  }
   ::close(sv[0]);
   ::close(sv[1]);
   ::close(wfd);
@@ -460,7 +472,7 @@ int main(int argc, char** argv) {
   test_aws_chunked();
   test_pieces_and_verify();
   test_merkle();
-  test_relay(quick ? (1u << 20) + 777 : (8u << 20) + 777);
+  test_relay(quick ? (3u << 20) + 777 : (8u << 20) + 777);
   test_relay(0);
   test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
