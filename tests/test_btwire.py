@@ -232,3 +232,57 @@ def test_link_serves_requests_from_source(tmp_path):
     plain = W.Link(W.PieceStore(n, plen, len(stream)), pipeline=4, fast=False)
     ev, out = plain.feed(req(0, 0, 10))            # no source: Python sees the REQUEST
     assert list(ev) == [("msg", 6, struct.pack(">III", 0, 0, 10))] and out == b""
+
+
+def test_malformed_block_from_a_scripted_peer_drops_it(tmp_path):
+    """End to end on the zero-copy path: a scripted seed answers the first
+    REQUEST properly, then sends a PIECE of the wrong length; the native
+    link flags it, the Torrent drops that connection (the peer sees EOF)
+    and keeps the good block."""
+    import asyncio
+
+    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl.fetch.bt import peer as pw
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 4 * B})
+        info = torrent_for(str(src / "P"), 2 * B)
+        payload = (src / "P" / "a.bin").read_bytes()
+        seen: dict = {"eof": asyncio.Event(), "requests": []}
+
+        async def scripted(r: asyncio.StreamReader, w: asyncio.StreamWriter) -> None:
+            await pw.read_handshake(r)
+            w.write(pw.encode_handshake(info.infohash, b"-SCRIPT-" + bytes(12)))
+            w.write(struct.pack(">IB", 1, pw.HAVE_ALL) + struct.pack(">IB", 1, pw.UNCHOKE))
+            try:
+                while True:
+                    (n,) = struct.unpack(">I", await r.readexactly(4))
+                    body = await r.readexactly(n) if n else b""
+                    if body[:1] != bytes([pw.REQUEST]):
+                        continue
+                    i, off, ln = struct.unpack(">III", body[1:13])
+                    seen["requests"].append((i, off, ln))
+                    data = payload[i * 2 * B + off:i * 2 * B + off + ln]
+                    if len(seen["requests"]) == 2:
+                        data = data[:-1]                    # short block: a protocol violation
+                    w.write(struct.pack(">IBII", 9 + len(data), pw.PIECE, i, off) + data)
+                    await w.drain()
+            except (asyncio.IncompleteReadError, ConnectionError):
+                seen["eof"].set()
+
+        srv = await asyncio.start_server(scripted, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        cfg = TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=False, encryption="disable")
+        t = Torrent(info.infohash, str(tmp_path / "dst"), cfg, info=info)
+        await t.start()
+        await t.download_all()
+        t.add_peer_addr(("127.0.0.1", port))
+        await asyncio.wait_for(seen["eof"].wait(), 10)
+        assert len(seen["requests"]) >= 2
+        assert t.store is not None and t.store.partial_bytes >= B     # the good block stayed
+        assert ("127.0.0.1", port) not in t.peers
+        await t.close()
+        srv.close()
+    asyncio.run(main())
