@@ -55,7 +55,8 @@ inline uint64_t key(uint32_t piece, uint32_t block) { return (uint64_t(piece) <<
 struct Pool {
   std::mutex mu;
   std::vector<std::vector<uint8_t>> free;
-  size_t cap = 64;
+  size_t cached = 0;                       // bytes held in `free`
+  size_t cap_bytes = size_t(256) << 20;    // 16 x 16 MiB pieces, 256 x 1 MiB
   std::vector<uint8_t> get(size_t n) {
     std::vector<uint8_t> v;
     {
@@ -63,6 +64,7 @@ struct Pool {
       if (!free.empty()) {
         v = std::move(free.back());
         free.pop_back();
+        cached -= v.capacity();
       }
     }
     v.resize(n);  // zero-fills only growth; a recycled buffer keeps its bytes
@@ -70,7 +72,10 @@ struct Pool {
   }
   void put(std::vector<uint8_t>&& v) {
     std::lock_guard<std::mutex> g(mu);
-    if (free.size() < cap) free.push_back(std::move(v));
+    if (cached + v.capacity() <= cap_bytes) {
+      cached += v.capacity();
+      free.push_back(std::move(v));
+    }
   }
 };
 
