@@ -286,3 +286,49 @@ def test_malformed_block_from_a_scripted_peer_drops_it(tmp_path):
         await t.close()
         srv.close()
     asyncio.run(main())
+
+
+def test_take_over_resumes_a_transport_the_stream_reader_paused():
+    """A StreamReader pauses its transport when its buffer passes the limit;
+    switching to LinkReader must hand over those bytes AND resume reading,
+    or the connection would stall forever."""
+    import asyncio
+
+    from tritondl.fetch.bt import peer as pw
+
+    async def main():
+        got = bytearray()
+        done = asyncio.Event()
+
+        async def serve(r, w):
+            w.write(b"\x00\x00\x00\x00" * 100_000)              # 400 KB of keep-alives
+            await w.drain()
+            w.write(struct.pack(">IB", 5, 4) + struct.pack(">I", 7))   # then a HAVE
+            await w.drain()
+            await done.wait()
+            w.close()
+
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        r, w = await asyncio.open_connection("127.0.0.1", srv.sockets[0].getsockname()[1], limit=1 << 16)
+        await asyncio.sleep(0.2)                                 # buffer fills past 2*limit: paused
+        assert not w.transport.is_reading()
+        wire = pw.Wire(r, w)
+        link = W.Link(W.PieceStore(1, B, B), 4, False)
+        msgs = []
+
+        def on_data(n):
+            ev, _out = link.feed_n(n)
+            for e in ev:
+                if e[0] == "msg":
+                    msgs.append(e)
+            if msgs:
+                done.set()
+        rx, leftover = wire.take_over(link, on_data)
+        assert leftover and w.transport.is_reading()
+        ev, _out = link.feed(leftover)
+        msgs += [e for e in ev if e[0] == "msg"]
+        await asyncio.wait_for(done.wait(), 5)
+        assert msgs == [("msg", 4, struct.pack(">I", 7))]
+        w.close()
+        srv.close()
+    asyncio.run(main())

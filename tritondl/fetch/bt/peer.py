@@ -153,6 +153,10 @@ class Wire:
         buf.clear()
         rx = LinkReader(tr, link, on_data)
         tr.set_protocol(rx)
+        if not tr.is_reading():
+            # the StreamReader had paused the transport (its buffer was over the
+            # limit); that buffer is now the caller's `leftover`: read on
+            tr.resume_reading()
         return rx, leftover
 
     async def _fill(self) -> None:
