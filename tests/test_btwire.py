@@ -332,3 +332,92 @@ def test_take_over_resumes_a_transport_the_stream_reader_paused():
         w.close()
         srv.close()
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("fast", [True, False])
+def test_download_completes_against_chaotic_scripted_peers(tmp_path, fast, native):
+    """Native links under churn: scripted seeds that randomly choke/unchoke
+    (dropping queued requests), REJECT (fast), ignore requests, and hang up
+    mid-stream.  The leecher must still finish with byte-exact data."""
+    import asyncio
+    import random
+
+    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl.fetch.bt import peer as pw
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 3_000_000 + 123})
+        info = torrent_for(str(src / "P"), 32 * 1024)
+        payload = (src / "P" / "a.bin").read_bytes()
+        rng = random.Random(1234 + fast)
+        reserved = bytearray(8)
+        if fast:
+            reserved[7] |= 0x04
+
+        async def chaotic(r: asyncio.StreamReader, w: asyncio.StreamWriter) -> None:
+            try:
+                await pw.read_handshake(r)
+                w.write(pw.encode_handshake(info.infohash, b"-CHAOS-" + bytes(13), bytes(reserved)))
+                w.write(struct.pack(">IB", 1, pw.HAVE_ALL) if fast else
+                        struct.pack(">IB", 1 + len(pw.set_to_bits([True] * info.num_pieces, info.num_pieces)),
+                                    pw.BITFIELD) + pw.set_to_bits([True] * info.num_pieces, info.num_pieces))
+                choked = True
+                budget = rng.randint(20, 200)              # blocks before hanging up
+                while budget > 0:
+                    if choked and rng.random() < 0.5:
+                        w.write(struct.pack(">IB", 1, pw.UNCHOKE))
+                        choked = False
+                    (n,) = struct.unpack(">I", await asyncio.wait_for(r.readexactly(4), 5))
+                    body = await r.readexactly(n) if n else b""
+                    if body[:1] != bytes([pw.REQUEST]):
+                        continue
+                    i, off, ln = struct.unpack(">III", body[1:13])
+                    x = rng.random()
+                    if choked or x < 0.05:
+                        if fast:
+                            w.write(struct.pack(">IBIII", 13, pw.REJECT, i, off, ln))
+                        continue                             # non-fast: silently dropped
+                    if x < 0.08:
+                        w.write(struct.pack(">IB", 1, pw.CHOKE))
+                        choked = True
+                        continue
+                    if x < 0.10:
+                        continue                             # ignored: the timeout path re-asks
+                    data = payload[i * info.piece_length + off:i * info.piece_length + off + ln]
+                    w.write(struct.pack(">IBII", 9 + len(data), pw.PIECE, i, off) + data)
+                    budget -= 1
+                    await w.drain()
+            except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError):
+                pass
+            finally:
+                w.close()
+
+        servers = [await asyncio.start_server(chaotic, "127.0.0.1", 0) for _ in range(3)]
+        addrs = [("127.0.0.1", s.sockets[0].getsockname()[1]) for s in servers]
+        cfg = TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=False, request_timeout=1.0,
+                            pipeline=16, native_wire=native)
+        t = Torrent(info.infohash, str(tmp_path / "dst"), cfg, info=info, peers=addrs)
+        await t.start()
+        await t.download_all()
+
+        async def redial():                                  # scripted seeds hang up: keep dialing them
+            while not t.complete.is_set():
+                for a in addrs:
+                    t.banned.discard(a)
+                    t.add_peer_addr(a)
+                await asyncio.sleep(0.1)
+        dialer = asyncio.ensure_future(redial())
+        try:
+            await asyncio.wait_for(t.complete.wait(), 60)
+        finally:
+            dialer.cancel()
+        assert t.store is None or t.store.partial_bytes == 0
+        with open(tmp_path / "dst" / "P" / "a.bin", "rb") as f:
+            assert f.read() == payload
+        await t.close()
+        for s in servers:
+            s.close()
+    asyncio.run(main())
