@@ -299,3 +299,25 @@ def test_bep3_http_tracker_query_against_a_scripted_peer():
         assert (q["port"], q["uploaded"], q["downloaded"], q["left"], q["compact"], q["event"]) == \
             ("51413", "0", "10", "99", "1", "started")
     run(main())
+
+
+def test_bep40_canonical_peer_priority_examples():
+    """BEP 40's worked examples, CRC-32C's check value, and symmetry."""
+    from tritondl.fetch.bt.bep40 import crc32c, priority
+    assert crc32c(b"123456789") == 0xE3069283
+    assert priority(("123.213.32.10", 0), ("98.76.54.32", 0)) == 0xEC2D7224
+    assert priority(("123.213.32.10", 0), ("123.213.32.234", 0)) == 0x99568189
+    a, b = ("10.0.0.1", 6881), ("10.0.0.1", 51413)          # same IP: ports decide
+    assert priority(a, b) == priority(b, a) == crc32c(bytes.fromhex("1ae1c8d5"))
+    assert priority(("2001:db8::1", 1), ("2001:db8:1::2", 2)) == priority(("2001:db8:1::2", 2), ("2001:db8::1", 1))
+
+
+def test_topup_dials_highest_bep40_priority_first(tmp_path):
+    from tritondl.fetch.bt.bep40 import priority
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+    t = Torrent(b"\x01" * 20, str(tmp_path), TorrentConfig(announce_host="123.213.32.10"))
+    t.port = 6881
+    t.known = {("98.76.54.32", 1), ("123.213.32.234", 2), ("8.8.8.8", 3), ("1.2.3.4", 4)}
+    best = t._best_candidates(2)
+    ranked = sorted(t.known, key=lambda a: priority(("123.213.32.10", 6881), a), reverse=True)
+    assert best == ranked[:2]

@@ -27,6 +27,7 @@ import asyncio
 import contextlib
 import functools
 import hashlib
+import heapq
 import math
 import os
 import random
@@ -37,7 +38,7 @@ from dataclasses import dataclass, field
 
 from ...utils.disk import check_space
 from ...utils.log import log
-from . import merkle, mse
+from . import bep40, merkle, mse
 from . import peer as pw
 from .dht import DHTNode
 from .metainfo import BLOCK, Info, MetainfoError
@@ -176,6 +177,8 @@ class Torrent:
         self._rare_dirty = True
         self._finishers: set[asyncio.Task] = set()
         self.store = None                               # _btwire.PieceStore (native data plane)
+        self._my_ip: str | None = None                  # learned from our first connection
+        self._prio: dict[tuple[str, int], int] = {}     # BEP 40 priority cache
         self.source = None                              # _btwire.Source: links serve REQUESTs from it
         self.assigned: dict[int, set] = {}              # piece -> peer keys whose links fetch it
         # per-file completion (streamed uploads): see watch_files
@@ -566,6 +569,18 @@ class Torrent:
         return min(done + partial, self.info.total_length)
 
     # ------------------------------------------------------------ discovery
+    def add_peer_addrs(self, addrs) -> None:
+        """A batch from a tracker / the DHT: all become known, and the free
+        connection slots go to the highest BEP 40 priority ones."""
+        for a in addrs:
+            if not self.closed and a not in self.banned and a[1] > 0 and \
+                    not (a[1] == self.port and a[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host)):
+                self.known.add(a)
+        free = self.cfg.max_peers - len(self.peers) - len(self.connecting)
+        if free > 0:
+            for a in self._best_candidates(free):
+                self.add_peer_addr(a)
+
     def add_peer_addr(self, addr: tuple[str, int]) -> None:
         if self.closed or addr in self.banned or addr[1] <= 0:
             return
@@ -586,8 +601,7 @@ class Torrent:
             interval = self.cfg.tracker_min_interval
             try:
                 res = await announce(url, a)
-                for p in res.peers:
-                    self.add_peer_addr(p)
+                self.add_peer_addrs(res.peers)
                 interval = max(self.cfg.tracker_min_interval, min(res.interval, 1800))
                 event = ""
             except (TrackerError, OSError) as e:
@@ -617,8 +631,7 @@ class Torrent:
             if self.private:
                 return                   # BEP 27: private torrents use their trackers only
             try:
-                for p in await self.dht.get_peers(self.infohash):
-                    self.add_peer_addr(p)
+                self.add_peer_addrs(await self.dht.get_peers(self.infohash))
                 await self.dht.announce_peer(self.infohash, self.port)
             except Exception as e:  # noqa: BLE001 - discovery is best-effort
                 log.with_field("error", str(e)).debug("dht lookup failed")
@@ -716,6 +729,9 @@ class Torrent:
             writer.close()
             return
         n = self.info.num_pieces if self.info else 0
+        if self._my_ip is None:           # our address as peers see it (BEP 40 priorities)
+            sn = writer.get_extra_info("sockname")
+            self._my_ip = self.cfg.announce_host or (sn[0] if sn else None)
         p = _Peer(pw.Wire(reader, writer), addr, hs, n)
         if not inbound:
             p.listen_addr = addr
@@ -750,9 +766,23 @@ class Torrent:
                     self.avail[i] -= 1
                     self._rare_dirty = True
         self._release(p)
-        # top up from known addresses
-        for a in list(self.known - set(self.peers) - self.connecting - self.banned)[:4]:
+        # top up from known addresses, highest BEP 40 priority first (as anacrolix dials)
+        for a in self._best_candidates(4):
             self.add_peer_addr(a)
+
+    def _best_candidates(self, k: int) -> list[tuple[str, int]]:
+        cands = self.known - set(self.peers) - self.connecting - self.banned
+        if not cands:
+            return []
+        mine = (self._my_ip or self.cfg.announce_host or "0.0.0.0", self.port)
+        prio = self._prio
+
+        def key(a: tuple[str, int]) -> int:
+            v = prio.get(a)
+            if v is None:
+                v = prio[a] = bep40.priority(mine, a)
+            return v
+        return heapq.nlargest(k, cands, key=key)
 
     def _release(self, p: _Peer) -> None:
         if p.link is not None:
