@@ -25,7 +25,7 @@ from tritondl.utils.backoff import ExponentialBackoff
 from tritondl.utils.config import Config
 
 
-@pytest.mark.parametrize("seed", [1234, 7])
+@pytest.mark.parametrize("seed", [1234, 7, 99, 2024, 31337])
 def test_chaos_soak_every_job_lands(tmp_path, seed):
     rng = random.Random(seed)
     n_jobs = 60
