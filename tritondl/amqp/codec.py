@@ -332,7 +332,86 @@ def decode_table(buf: bytes) -> dict:
 # ---------------------------------------------------------------- methods
 
 
+_S_HH = struct.Struct(">HH")
+_S_ACK = struct.Struct(">HHQB")          # basic.ack / basic.nack: ids, delivery-tag, bits
+_S_Q = struct.Struct(">Q")
+_S_HHH = struct.Struct(">HHH")
+
+
+def _ss_fast(s: str | bytes) -> bytes:
+    b = s.encode() if isinstance(s, str) else s
+    if len(b) > 255:
+        raise AMQPError("shortstr too long")
+    return bytes((len(b),)) + b
+
+
+# Hand-packed encoders for the per-message methods (the table-driven path
+# below costs ~10 Python operations per field): same bytes, pinned against
+# the generic encoder in tests/test_amqp.py.
+_FAST_ENC = {
+    "basic.ack": lambda a: _S_ACK.pack(60, 80, a.get("delivery_tag", 0), 1 if a.get("multiple") else 0),
+    "basic.nack": lambda a: _S_ACK.pack(60, 120, a.get("delivery_tag", 0),
+                                        (1 if a.get("multiple") else 0) | (2 if a.get("requeue") else 0)),
+    "basic.deliver": lambda a: (_S_HH.pack(60, 60) + _ss_fast(a.get("consumer_tag", "")) +
+                                _S_Q.pack(a.get("delivery_tag", 0)) + (b"\x01" if a.get("redelivered") else b"\x00") +
+                                _ss_fast(a.get("exchange", "")) + _ss_fast(a.get("routing_key", ""))),
+    "basic.publish": lambda a: (_S_HHH.pack(60, 40, a.get("ticket", 0)) + _ss_fast(a.get("exchange", "")) +
+                                _ss_fast(a.get("routing_key", "")) +
+                                bytes(((1 if a.get("mandatory") else 0) | (2 if a.get("immediate") else 0),))),
+}
+
+
+def _fast_decode(cid: int, mid: int, payload: bytes) -> Method | None:
+    """Hot methods without the table-driven reader; None: use the generic path."""
+    if cid != 60:
+        return None
+    try:
+        if mid == 80 and len(payload) == 13:
+            tag, bits = struct.unpack_from(">QB", payload, 4)
+            return Method("basic.ack", {"delivery_tag": tag, "multiple": bool(bits & 1)})
+        if mid == 120 and len(payload) == 13:
+            tag, bits = struct.unpack_from(">QB", payload, 4)
+            return Method("basic.nack", {"delivery_tag": tag, "multiple": bool(bits & 1), "requeue": bool(bits & 2)})
+        if mid == 60:
+            pos = 4
+            n = payload[pos]
+            ctag = payload[pos + 1:pos + 1 + n].decode("utf-8", "surrogateescape")
+            pos += 1 + n
+            (tag,) = struct.unpack_from(">Q", payload, pos)
+            red = bool(payload[pos + 8] & 1)
+            pos += 9
+            n = payload[pos]
+            ex = payload[pos + 1:pos + 1 + n].decode("utf-8", "surrogateescape")
+            pos += 1 + n
+            n = payload[pos]
+            rk = payload[pos + 1:pos + 1 + n]
+            if pos + 1 + n != len(payload):
+                return None
+            return Method("basic.deliver", {"consumer_tag": ctag, "delivery_tag": tag, "redelivered": red,
+                                            "exchange": ex, "routing_key": rk.decode("utf-8", "surrogateescape")})
+        if mid == 40:
+            (ticket,) = struct.unpack_from(">H", payload, 4)
+            pos = 6
+            n = payload[pos]
+            ex = payload[pos + 1:pos + 1 + n].decode("utf-8", "surrogateescape")
+            pos += 1 + n
+            n = payload[pos]
+            rk = payload[pos + 1:pos + 1 + n].decode("utf-8", "surrogateescape")
+            pos += 1 + n
+            if pos + 1 != len(payload):
+                return None
+            bits = payload[pos]
+            return Method("basic.publish", {"ticket": ticket, "exchange": ex, "routing_key": rk,
+                                            "mandatory": bool(bits & 1), "immediate": bool(bits & 2)})
+    except (IndexError, struct.error):
+        return None                     # malformed: the generic path raises the proper FrameError
+    return None
+
+
 def encode_method(m: Method) -> bytes:
+    f = _FAST_ENC.get(m.name)
+    if f is not None:
+        return f(m.args)
     cid, mid = BY_NAME[m.name]
     out = bytearray(struct.pack(">HH", cid, mid))
     bits: list[bool] = []
@@ -373,6 +452,11 @@ def encode_method(m: Method) -> bytes:
 
 
 def decode_method(payload: bytes) -> Method:
+    if len(payload) >= 4:
+        cid, mid = _S_HH.unpack_from(payload)
+        m = _fast_decode(cid, mid, payload)
+        if m is not None:
+            return m
     r = _Reader(payload)
     cid, mid = r.unpack(">HH")
     spec = METHODS.get((cid, mid))
@@ -449,8 +533,11 @@ def decode_header(payload: bytes) -> tuple[int, int, Properties]:
 # ------------------------------------------------------------------ frames
 
 
+_S_FRAME = struct.Struct(">BHI")
+
+
 def frame(ftype: int, channel: int, payload: bytes) -> bytes:
-    return struct.pack(">BHI", ftype, channel, len(payload)) + payload + b"\xce"
+    return b"".join((_S_FRAME.pack(ftype, channel, len(payload)), payload, b"\xce"))
 
 
 def method_frame(channel: int, m: Method) -> bytes:

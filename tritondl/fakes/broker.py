@@ -156,6 +156,45 @@ class _ServerConn:
         self.send(codec.method_frame(ch, m))
 
 
+class _FrameProtocol(asyncio.Protocol):
+    """A broker connection after the protocol header: every read is parsed
+    and handled synchronously in the transport callback.  Write flow control
+    and connection loss are forwarded to the StreamWriter's protocol."""
+
+    def __init__(self, broker: "Broker", c: _ServerConn, transport: asyncio.Transport) -> None:
+        self.broker, self.c, self.tr = broker, c, transport
+        self.old = transport.get_protocol()
+        self.parser = codec.FrameParser()
+        self.done: asyncio.Future = asyncio.get_running_loop().create_future()
+
+    def data_received(self, data: bytes) -> None:
+        if self.done.done():
+            return
+        try:
+            ok = self.broker._frames(self.c, self.parser.feed(data))
+        except codec.FrameError:
+            ok = False
+        if not ok:
+            self.tr.pause_reading()
+            self.done.set_result(None)
+
+    def eof_received(self) -> bool:
+        if not self.done.done():
+            self.done.set_result(None)
+        return False
+
+    def connection_lost(self, exc) -> None:
+        if not self.done.done():
+            self.done.set_result(None)
+        self.old.connection_lost(exc)
+
+    def pause_writing(self) -> None:
+        self.old.pause_writing()
+
+    def resume_writing(self) -> None:
+        self.old.resume_writing()
+
+
 class Broker:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, *, username: str | None = None,
                  password: str | None = None, heartbeat: int = 0, frame_max: int = codec.DEFAULT_FRAME_MAX) -> None:
@@ -264,30 +303,19 @@ class Broker:
                                                        "consumer_cancel_notify": True,
                                                        "connection.blocked": True, "per_consumer_qos": True}},
                 "mechanisms": b"PLAIN AMQPLAIN", "locales": b"en_US"}))
-            parser = codec.FrameParser()
-            done = False
-            while not done:
-                for ftype, ch, payload in await codec.read_frames(reader, parser):
-                    try:
-                        self._on_frame(c, ftype, ch, payload)
-                    except ConnError as e:
-                        c.send_method(0, Method("connection.close", {"reply_code": e.code,
-                                                                     "reply_text": e.text[:255],
-                                                                     "class_id": e.cm[0], "method_id": e.cm[1]}))
-                        c.flush()
-                        await writer.drain()
-                        done = True
-                        break
-                    except ChannelError as e:
-                        sc = c.channels.pop(ch, None)
-                        if sc is not None:
-                            self._close_channel(sc)
-                        c.send_method(ch, Method("channel.close", {"reply_code": e.code, "reply_text": e.text[:255],
-                                                                   "class_id": e.cm[0], "method_id": e.cm[1]}))
-                    if c.closed:
-                        done = True
-                        break
-                await writer.drain()
+            # from here on frames are handled inside the transport's read callback
+            # (no StreamReader buffer, no task wake-up per read): the broker's cost
+            # per message is what bounds a node of competing workers
+            proto = _FrameProtocol(self, c, writer.transport)
+            leftover = bytes(getattr(reader, "_buffer", b""))
+            if hasattr(reader, "_buffer"):
+                reader._buffer.clear()
+            writer.transport.set_protocol(proto)
+            if not writer.transport.is_reading():
+                writer.transport.resume_reading()
+            if leftover:
+                proto.data_received(leftover)
+            await proto.done
         except (asyncio.IncompleteReadError, ConnectionError, OSError, codec.FrameError):
             pass
         finally:
@@ -297,6 +325,27 @@ class Broker:
                 writer.close()
             except Exception:
                 pass
+
+    def _frames(self, c: _ServerConn, frames) -> bool:
+        """Handle parsed frames; False once the connection is to be closed."""
+        for ftype, ch, payload in frames:
+            try:
+                self._on_frame(c, ftype, ch, payload)
+            except ConnError as e:
+                c.send_method(0, Method("connection.close", {"reply_code": e.code,
+                                                             "reply_text": e.text[:255],
+                                                             "class_id": e.cm[0], "method_id": e.cm[1]}))
+                c.flush()
+                return False
+            except ChannelError as e:
+                sc = c.channels.pop(ch, None)
+                if sc is not None:
+                    self._close_channel(sc)
+                c.send_method(ch, Method("channel.close", {"reply_code": e.code, "reply_text": e.text[:255],
+                                                           "class_id": e.cm[0], "method_id": e.cm[1]}))
+            if c.closed:
+                return False
+        return True
 
     def _teardown(self, c: _ServerConn) -> None:
         if c in self.conns:
