@@ -226,14 +226,25 @@ class JobStack:
         return mid, d.encode()
 
     async def submit(self, n: int) -> list[str]:
+        """Publish n jobs with confirms pipelined (up to 256 outstanding), so
+        the producer costs one broker round trip per batch, not per job."""
         ids = []
+        pending: list[asyncio.Future] = []
         for _ in range(n):
             i = self._n
             self._n += 1
             mid, body = self.job_body(i)
-            await self.pch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
-                                         Properties(delivery_mode=2, content_type="application/octet-stream"))
+            fut = await self.pch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
+                                               Properties(delivery_mode=2, content_type="application/octet-stream"),
+                                               wait_confirm=False)
+            if fut is not None:
+                pending.append(fut)
+            if len(pending) >= 256:
+                await asyncio.gather(*pending)
+                pending.clear()
             ids.append(mid)
+        if pending:
+            await asyncio.gather(*pending)
         return ids
 
     async def wait_done(self, total: int, timeout: float = 600) -> None:
