@@ -29,6 +29,8 @@
 #include <utility>
 #include <vector>
 
+#include "sha256x2.h"
+
 namespace tritondl_hash {
 
 // OpenSSL 3: sha256_md() & co. are legacy handles, and every
@@ -83,6 +85,36 @@ inline std::string one_shot(const EVP_MD* md, const void* p, size_t n) {
   MdCtx c(md);
   c.update(p, n);
   return c.final();
+}
+
+// SHA-256 of one / two buffers into raw 32-byte digests: SHA-NI (two
+// messages in lockstep, sha256x2.h) when the CPU has it, else OpenSSL.
+inline void sha256_raw(const void* p, size_t n, unsigned char out[32]) {
+  if (sha2x::cpu_has_sha_ni()) {
+    sha2x::sha256_x1(p, n, out);
+    return;
+  }
+  unsigned int len = 32;
+  EVP_Digest(n ? p : "", n, out, &len, sha256_md(), nullptr);
+}
+inline void sha256_pair(const void* a, size_t na, const void* b, size_t nb, unsigned char oa[32],
+                        unsigned char ob[32]) {
+  if (sha2x::cpu_has_sha_ni()) {
+    sha2x::sha256_x2(a, na, b, nb, oa, ob);
+    return;
+  }
+  sha256_raw(a, na, oa);
+  sha256_raw(b, nb, ob);
+}
+
+inline std::string hex_raw(const unsigned char* d, size_t n) {
+  static const char* hx = "0123456789abcdef";
+  std::string out(n * 2, '0');
+  for (size_t i = 0; i < n; ++i) {
+    out[2 * i] = hx[d[i] >> 4];
+    out[2 * i + 1] = hx[d[i] & 15];
+  }
+  return out;
 }
 
 inline std::string hex(const std::string& d) {
@@ -324,10 +356,23 @@ inline std::vector<std::string> chunk_hashes(const char* data, size_t len, size_
   const size_t per_thread = (1u << 20) / chunk_size + 1;  // >= ~1 MiB of hashing per thread
   const int t = threads <= 0 ? default_threads() : threads;
   const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, nfull / per_thread)));
-  parallel_for(n, used, [&](size_t i) {
-    const size_t off = i * chunk_size;
-    const size_t m = off < len ? std::min(chunk_size, len - off) : 0;
-    h[i] = hex(one_shot(sha256_md(), m ? data + off : "", m));
+  // chunks in pairs: SHA-NI hashes both in lockstep
+  parallel_for((n + 1) / 2, used, [&](size_t k) {
+    unsigned char d[2][32];
+    const char* p[2];
+    size_t m[2];
+    const size_t cnt = std::min<size_t>(2, n - 2 * k);
+    for (size_t j = 0; j < cnt; ++j) {
+      const size_t off = (2 * k + j) * chunk_size;
+      m[j] = off < len ? std::min(chunk_size, len - off) : 0;
+      p[j] = m[j] ? data + off : "";
+    }
+    if (cnt == 2) {
+      sha256_pair(p[0], m[0], p[1], m[1], d[0], d[1]);
+    } else {
+      sha256_raw(p[0], m[0], d[0]);
+    }
+    for (size_t j = 0; j < cnt; ++j) h[2 * k + j] = hex_raw(d[j], 32);
   });
   return h;
 }
@@ -382,10 +427,7 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
   const size_t per_thread = (1u << 20) / chunk_size + 1;
   const int t = threads <= 0 ? default_threads() : threads;
   const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, nfull / per_thread)));
-  parallel_for(n, used, [&](size_t i) {
-    const size_t m = i < nfull ? std::min(chunk_size, len - i * chunk_size) : 0;
-    const char* p = m ? data + i * chunk_size : "";
-    h[i] = hex(one_shot(sha256_md(), p, m));
+  auto write_frame = [&](size_t i, const char* p, size_t m) {
     char hx[32];
     const int hl = std::snprintf(hx, sizeof hx, "%zx", m);
     char* w = dst + frame[i];
@@ -399,6 +441,26 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
     w += m;
     *w++ = '\r';
     *w++ = '\n';
+  };
+  parallel_for((n + 1) / 2, used, [&](size_t k) {  // chunk pairs: SHA-NI hashes both in lockstep
+    const size_t cnt = std::min<size_t>(2, n - 2 * k);
+    const char* p[2];
+    size_t m[2];
+    unsigned char d[2][32];
+    for (size_t j = 0; j < cnt; ++j) {
+      const size_t i = 2 * k + j;
+      m[j] = i < nfull ? std::min(chunk_size, len - i * chunk_size) : 0;
+      p[j] = m[j] ? data + i * chunk_size : "";
+    }
+    if (cnt == 2) {
+      sha256_pair(p[0], m[0], p[1], m[1], d[0], d[1]);
+    } else {
+      sha256_raw(p[0], m[0], d[0]);
+    }
+    for (size_t j = 0; j < cnt; ++j) {
+      h[2 * k + j] = hex_raw(d[j], 32);
+      write_frame(2 * k + j, p[j], m[j]);
+    }
   });
   SigChain chain(key, amzdate, scope, prev);
   for (size_t i = 0; i < n; ++i) {
@@ -451,10 +513,21 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
   if (decoded) decoded->assign(total, '\0');
   std::vector<size_t> dst_off(frames.size() + 1, 0);
   for (size_t i = 0; i < frames.size(); ++i) dst_off[i + 1] = dst_off[i] + frames[i].n;
-  parallel_for(frames.size(), used, [&](size_t i) {
-    const Frame& f = frames[i];
-    h[i] = hex(one_shot(sha256_md(), f.n ? raw + f.off : "", f.n));
-    if (decoded && f.n) std::memcpy(&(*decoded)[dst_off[i]], raw + f.off, f.n);
+  const size_t nf = frames.size();
+  parallel_for((nf + 1) / 2, used, [&](size_t k) {  // frame pairs: SHA-NI lockstep
+    const size_t i = 2 * k;
+    const Frame& a = frames[i];
+    unsigned char d[2][32];
+    if (i + 1 < nf) {
+      const Frame& b = frames[i + 1];
+      sha256_pair(raw + a.off, a.n, raw + b.off, b.n, d[0], d[1]);
+      h[i + 1] = hex_raw(d[1], 32);
+      if (decoded && b.n) std::memcpy(&(*decoded)[dst_off[i + 1]], raw + b.off, b.n);
+    } else {
+      sha256_raw(raw + a.off, a.n, d[0]);
+    }
+    h[i] = hex_raw(d[0], 32);
+    if (decoded && a.n) std::memcpy(&(*decoded)[dst_off[i]], raw + a.off, a.n);
   });
   SigChain chain(key, amzdate, scope, seed);
   for (size_t i = 0; i < frames.size(); ++i) {

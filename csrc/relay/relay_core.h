@@ -699,20 +699,26 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
     cv_free.notify_all();
   };
 
+  // Each hasher takes two consecutive chunks: SHA-NI hashes them in lockstep
+  // (sha256x2.h).  Both ring slots must be free (K >= 2 whenever n >= 2), and
+  // the chunk the sender waits for always belongs to a pair whose slots are.
   auto hasher = [&] {
     for (;;) {
-      const size_t i = next.fetch_add(1);
+      const size_t i = next.fetch_add(2);
       if (i >= n) return;
-      const size_t slot = i % K;
+      const size_t cnt = std::min<size_t>(2, n - i);
+      const size_t last = i + cnt - 1;
       {
         std::unique_lock<std::mutex> l(mu);
-        cv_free.wait(l, [&] { return abort.load() || static_cast<int64_t>(i) < sent_chunks + static_cast<int64_t>(K); });
+        cv_free.wait(l, [&] { return abort.load() || static_cast<int64_t>(last) < sent_chunks + static_cast<int64_t>(K); });
         if (abort.load()) return;
       }
       const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
-      const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(i) * chunk));
+      size_t m[2] = {0, 0};
+      for (size_t j = 0; j < cnt; ++j)
+        m[j] = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(i + j) * chunk));
       if (flow) {
-        const int w = flow->wait_covered(a, a + m, idle_timeout, &abort);
+        const int w = flow->wait_covered(a, a + m[0] + m[1], idle_timeout, &abort);
         if (w) {
           if (!abort.load())
             set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
@@ -720,22 +726,32 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
           return;
         }
       }
-      char* dst = ring.data() + slot * chunk;
-      if (tritondl_hash::pread_full(fd, dst, m, static_cast<off_t>(a)) != m) {
-        set_err("source file shorter than expected");
-        return;
+      char* dst[2];
+      for (size_t j = 0; j < cnt; ++j) {
+        dst[j] = ring.data() + ((i + j) % K) * chunk;
+        if (tritondl_hash::pread_full(fd, dst[j], m[j], static_cast<off_t>(a + j * chunk)) != m[j]) {
+          set_err("source file shorter than expected");
+          return;
+        }
       }
-      std::string h = tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), dst, m));
+      unsigned char d[2][32];
+      if (cnt == 2) {
+        tritondl_hash::sha256_pair(dst[0], m[0], dst[1], m[1], d[0], d[1]);
+      } else {
+        tritondl_hash::sha256_raw(dst[0], m[0], d[0]);
+      }
       {
         std::lock_guard<std::mutex> l(mu);
-        hashes[slot] = std::move(h);
-        ready[slot] = static_cast<int64_t>(i);
+        for (size_t j = 0; j < cnt; ++j) {
+          hashes[(i + j) % K] = tritondl_hash::hex_raw(d[j], 32);
+          ready[(i + j) % K] = static_cast<int64_t>(i + j);
+        }
       }
       cv_ready.notify_all();
     }
   };
 
-  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, n)));
+  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + 1) / 2)));
   std::vector<std::thread> pool;
   if (n) {
     pool.reserve(static_cast<size_t>(nthreads));
@@ -960,9 +976,20 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
       std::vector<size_t> doff(frames.size() + 1, 0);
       for (size_t i = 0; i < frames.size(); ++i) doff[i + 1] = doff[i] + frames[i].n;
       const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, doff.back() >> 20)));
-      tritondl_hash::parallel_for(frames.size(), used, [&](size_t i) {
+      const size_t nf = frames.size();
+      tritondl_hash::parallel_for((nf + 1) / 2, used, [&](size_t k) {  // frame pairs: SHA-NI lockstep
+        const size_t i = 2 * k;
+        unsigned char d[2][32];
         const RawFrame& f = frames[i];
-        h[i] = tritondl_hash::hex(tritondl_hash::one_shot(tritondl_hash::sha256_md(), f.n ? raw + f.off : "", f.n));
+        if (i + 1 < nf) {
+          const RawFrame& g = frames[i + 1];
+          tritondl_hash::sha256_pair(raw + f.off, f.n, raw + g.off, g.n, d[0], d[1]);
+          h[i + 1] = tritondl_hash::hex_raw(d[1], 32);
+          if (keep && g.n) std::memcpy(&r.data[dbase + doff[i + 1]], raw + g.off, g.n);
+        } else {
+          tritondl_hash::sha256_raw(raw + f.off, f.n, d[0]);
+        }
+        h[i] = tritondl_hash::hex_raw(d[0], 32);
         if (keep && f.n) std::memcpy(&r.data[dbase + doff[i]], raw + f.off, f.n);
       });
       for (size_t i = 0; i < frames.size(); ++i) {
@@ -1013,17 +1040,26 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
   std::atomic<size_t> next{0};
   bool final_seen = false;
 
+  // frames in pairs (SHA-NI lockstep): a hasher waits until both of its
+  // frames are published, or takes the last one alone once parsing is done
   auto hasher = [&] {
     for (;;) {
-      const size_t j = next.fetch_add(1);
+      const size_t j = next.fetch_add(2);
+      size_t cnt;
       {
         std::unique_lock<std::mutex> l(mu);
-        cv_pub.wait(l, [&] { return stop || j < published || parse_done; });
+        cv_pub.wait(l, [&] { return stop || j + 1 < published || parse_done; });
         if (stop || j >= published) return;
+        cnt = j + 1 < published ? 2 : 1;
       }
       StreamFrame& f = frame(j);
-      unsigned int len = 32;
-      EVP_Digest(f.n ? raw + f.off : "", f.n, f.h, &len, tritondl_hash::sha256_md(), nullptr);
+      if (cnt == 2) {
+        StreamFrame& g = frame(j + 1);
+        tritondl_hash::sha256_pair(raw + f.off, f.n, raw + g.off, g.n, f.h, g.h);
+        g.ready.store(1, std::memory_order_release);
+      } else {
+        tritondl_hash::sha256_raw(raw + f.off, f.n, f.h);
+      }
       f.ready.store(1, std::memory_order_release);
       {
         std::lock_guard<std::mutex> l(mu);  // pairs with the checker's wait

@@ -5,6 +5,7 @@
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <string>
 #include <vector>
@@ -43,6 +44,25 @@ static std::string signing_key(const std::string& secret, const std::string& dat
   k = hmac256(k, "us-east-1");
   k = hmac256(k, "s3");
   return hmac256(k, "aws4_request");
+}
+
+// Two-stream SHA-NI SHA-256 (sha256x2.h) against OpenSSL: random lengths
+// around the block and padding boundaries, equal and unequal pairs.
+static void test_sha256_pair() {
+  std::mt19937 rng(11);
+  std::string a(200000, '\0'), b(200000, '\0');
+  for (auto& c : a) c = char(rng());
+  for (auto& c : b) c = char(rng());
+  for (int it = 0; it < 400; ++it) {
+    const size_t na = it < 200 ? size_t(it) : rng() % a.size();
+    const size_t nb = rng() % 3 ? na : rng() % b.size();
+    unsigned char oa[32], ob[32], r1[32];
+    sha256_pair(a.data(), na, b.data(), nb, oa, ob);
+    sha256_raw(a.data(), na, r1);
+    CHECK(std::string(reinterpret_cast<char*>(oa), 32) == one_shot(sha256_md(), a.data(), na));
+    CHECK(std::string(reinterpret_cast<char*>(ob), 32) == one_shot(sha256_md(), b.data(), nb));
+    CHECK(std::memcmp(oa, r1, 32) == 0);
+  }
 }
 
 static void test_aws_chunked() {
@@ -469,6 +489,7 @@ static void test_btwire(unsigned seed, int rounds) {
 int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
+  test_sha256_pair();
   test_aws_chunked();
   test_pieces_and_verify();
   test_merkle();
