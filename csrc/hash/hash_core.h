@@ -29,7 +29,7 @@
 #include <utility>
 #include <vector>
 
-#include "sha256x2.h"
+#include "sha_ni.h"
 
 namespace tritondl_hash {
 
@@ -88,7 +88,7 @@ inline std::string one_shot(const EVP_MD* md, const void* p, size_t n) {
 }
 
 // SHA-256 of one / two buffers into raw 32-byte digests: SHA-NI (two
-// messages in lockstep, sha256x2.h) when the CPU has it, else OpenSSL.
+// messages in lockstep, sha_ni.h) when the CPU has it, else OpenSSL.
 inline void sha256_raw(const void* p, size_t n, unsigned char out[32]) {
   if (sha2x::cpu_has_sha_ni()) {
     sha2x::sha256_x1(p, n, out);
@@ -105,6 +105,26 @@ inline void sha256_pair(const void* a, size_t na, const void* b, size_t nb, unsi
   }
   sha256_raw(a, na, oa);
   sha256_raw(b, nb, ob);
+}
+
+// Raw digest with an EVP algorithm; SHA-1 / SHA-256 take the SHA-NI path.
+inline void md_raw(const EVP_MD* md, const void* p, size_t n, unsigned char* out) {
+  if (sha2x::cpu_has_sha_ni()) {
+    if (md == sha256_md()) return sha2x::sha256_x1(p, n, out);
+    if (md == sha1_md()) return sha2x::sha1_x1(p, n, out);
+  }
+  unsigned int len = 0;
+  EVP_Digest(n ? p : "", n, out, &len, md, nullptr);
+}
+// Two messages: in lockstep on SHA-NI (SHA-1 / SHA-256), else one by one.
+inline void md_pair(const EVP_MD* md, const void* a, size_t na, const void* b, size_t nb, unsigned char* oa,
+                    unsigned char* ob) {
+  if (sha2x::cpu_has_sha_ni()) {
+    if (md == sha256_md()) return sha2x::sha256_x2(a, na, b, nb, oa, ob);
+    if (md == sha1_md()) return sha2x::sha1_x2(a, na, b, nb, oa, ob);
+  }
+  md_raw(md, a, na, oa);
+  md_raw(md, b, nb, ob);
 }
 
 inline std::string hex_raw(const unsigned char* d, size_t n) {
@@ -271,10 +291,17 @@ inline std::string piece_hashes(const EVP_MD* md, const char* data, size_t len, 
   const size_t n = (len + piece_len - 1) / piece_len;
   const size_t dl = static_cast<size_t>(EVP_MD_size(md));
   std::string out(n * dl, '\0');
-  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t i) {
-    const size_t off = i * piece_len;
-    const std::string d = one_shot(md, data + off, std::min(piece_len, len - off));
-    std::memcpy(&out[i * dl], d.data(), dl);
+  parallel_for((n + 1) / 2, threads <= 0 ? default_threads() : threads, [&](size_t k) {  // pairs: SHA-NI lockstep
+    const size_t i = 2 * k, a = i * piece_len, na = std::min(piece_len, len - a);
+    unsigned char d0[EVP_MAX_MD_SIZE], d1[EVP_MAX_MD_SIZE];
+    if (i + 1 < n) {
+      const size_t b = a + piece_len, nb = std::min(piece_len, len - b);
+      md_pair(md, data + a, na, data + b, nb, d0, d1);
+      std::memcpy(&out[(i + 1) * dl], d1, dl);
+    } else {
+      md_raw(md, data + a, na, d0);
+    }
+    std::memcpy(&out[i * dl], d0, dl);
   });
   return out;
 }
@@ -306,10 +333,12 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
   std::vector<int> fds(spans.size(), -1);
   for (size_t i = 0; i < spans.size(); ++i)
     if (!spans[i].path.empty()) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
-  parallel_for(n, threads <= 0 ? default_threads() : threads, [&](size_t p) {
+  // read piece p of the layout into buf (sized to the piece); false if a
+  // file is missing or short
+  auto load = [&](size_t p, std::vector<char>& buf) -> bool {
     const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
     const long long plen = std::min<long long>(static_cast<long long>(piece_len), total - pstart);
-    std::vector<char> buf(static_cast<size_t>(plen));
+    buf.resize(static_cast<size_t>(plen));
     long long filled = 0;
     size_t lo = 0, hi = spans.size();  // last span starting at or before pstart
     while (hi - lo > 1) {
@@ -327,13 +356,27 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
         filled += static_cast<long long>(want);
         continue;
       }
-      if (a != pstart + filled || fds[s] < 0) return;
-      if (pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) return;
+      if (a != pstart + filled || fds[s] < 0) return false;
+      if (pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) return false;
       filled += static_cast<long long>(want);
     }
-    if (filled != plen) return;
-    const std::string d = one_shot(md, buf.data(), buf.size());
-    if (std::memcmp(d.data(), expected.data() + p * dl, dl) == 0) ok[p] = 1;
+    return filled == plen;
+  };
+  // pieces in pairs: SHA-NI hashes both in lockstep (md_pair)
+  parallel_for((n + 1) / 2, threads <= 0 ? default_threads() : threads, [&](size_t k) {
+    std::vector<char> b0, b1;
+    const size_t p = 2 * k;
+    const bool l0 = load(p, b0), l1 = p + 1 < n && load(p + 1, b1);
+    unsigned char d0[EVP_MAX_MD_SIZE], d1[EVP_MAX_MD_SIZE];
+    if (l0 && l1) {
+      md_pair(md, b0.data(), b0.size(), b1.data(), b1.size(), d0, d1);
+    } else if (l0) {
+      md_raw(md, b0.data(), b0.size(), d0);
+    } else if (l1) {
+      md_raw(md, b1.data(), b1.size(), d1);
+    }
+    if (l0 && std::memcmp(d0, expected.data() + p * dl, dl) == 0) ok[p] = 1;
+    if (l1 && std::memcmp(d1, expected.data() + (p + 1) * dl, dl) == 0) ok[p + 1] = 1;
   });
   for (int fd : fds)
     if (fd >= 0) ::close(fd);

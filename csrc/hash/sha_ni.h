@@ -1,10 +1,11 @@
-// Two-stream SHA-256 with the x86 SHA extensions (SHA-NI).
+// Two-stream SHA-256 and SHA-1 with the x86 SHA extensions (SHA-NI).
 //
 // SHA-256 is a serial chain inside one message, and each sha256rnds2 waits
 // on the previous one (3-4 cycles of latency on Zen / Intel cores that can
 // issue one every 1-2 cycles).  Hashing TWO independent messages in
 // lockstep fills those latency slots.  aws-chunked uploads have exactly
-// that shape: every 64 KiB chunk is hashed on its own.  The result is ~1.6-2x
+// that shape: every 64 KiB chunk is hashed on its own.  BitTorrent v1
+// verification does too (every piece is its own SHA-1).  The result is ~1.6-2x
 // the single-stream rate per core (tools/bench_sha.py).  Used by the relay
 // send pump, the streamed verifier and the chunk encoders; falls back to
 // OpenSSL where the CPU has no SHA-NI.
@@ -187,6 +188,133 @@ inline void sha256_x2(const void* da, size_t na, const void* db, size_t nb, uint
   }
   digest_out(sa, oa);
   digest_out(sb, ob);
+}
+
+// ------------------------------------------------------------------ SHA-1
+// Same scheme for SHA-1 (sha1rnds4 / sha1nexte / sha1msg1 / sha1msg2):
+// BitTorrent v1 piece verification on the host (resume, hybrid GPU+CPU).
+
+struct Lane1 {
+  __m128i abcd, e[2], m[4];
+};
+
+#define TDL_SHA_TARGET __attribute__((target("sha,sse4.1,ssse3"), always_inline))
+
+// Rounds 4g .. 4g+3 (g compile-time after unrolling).  The E register
+// alternates between e[0] and e[1] every group.
+TDL_SHA_TARGET inline void group1(Lane1& l, int g, const uint8_t* p, __m128i mask) {
+  __m128i& cur = l.m[g & 3];
+  if (g < 4) cur = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * g)), mask);
+  __m128i& ec = l.e[g & 1];
+  __m128i& en = l.e[(g + 1) & 1];
+  if (g == 0) {
+    ec = _mm_add_epi32(ec, cur);
+  } else {
+    ec = _mm_sha1nexte_epu32(ec, cur);
+  }
+  en = l.abcd;
+  if (g >= 3 && g <= 18) l.m[(g + 1) & 3] = _mm_sha1msg2_epu32(l.m[(g + 1) & 3], cur);
+  switch (g / 5) {  // the round function index must be an immediate
+    case 0: l.abcd = _mm_sha1rnds4_epu32(l.abcd, ec, 0); break;
+    case 1: l.abcd = _mm_sha1rnds4_epu32(l.abcd, ec, 1); break;
+    case 2: l.abcd = _mm_sha1rnds4_epu32(l.abcd, ec, 2); break;
+    default: l.abcd = _mm_sha1rnds4_epu32(l.abcd, ec, 3); break;
+  }
+  if (g >= 1 && g <= 16) l.m[(g + 3) & 3] = _mm_sha1msg1_epu32(l.m[(g + 3) & 3], cur);
+  if (g >= 2 && g <= 17) l.m[(g + 2) & 3] = _mm_xor_si128(l.m[(g + 2) & 3], cur);
+}
+
+__attribute__((target("sha,sse4.1,ssse3"))) inline void sha1_blocks_x1(uint32_t st[5], const uint8_t* p, size_t n) {
+  const __m128i mask = _mm_set_epi64x(0x0001020304050607ULL, 0x08090a0b0c0d0e0fULL);
+  Lane1 a;
+  a.abcd = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(st)), 0x1B);
+  a.e[0] = _mm_set_epi32(int(st[4]), 0, 0, 0);
+  for (; n; --n, p += 64) {
+    const __m128i abcd0 = a.abcd, e0 = a.e[0];
+#pragma GCC unroll 20
+    for (int g = 0; g < 20; ++g) group1(a, g, p, mask);
+    a.e[0] = _mm_sha1nexte_epu32(a.e[0], e0);
+    a.abcd = _mm_add_epi32(a.abcd, abcd0);
+  }
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(st), _mm_shuffle_epi32(a.abcd, 0x1B));
+  st[4] = uint32_t(_mm_extract_epi32(a.e[0], 3));
+}
+
+__attribute__((target("sha,sse4.1,ssse3"))) inline void sha1_blocks_x2(uint32_t sa[5], uint32_t sb[5],
+                                                                      const uint8_t* pa, const uint8_t* pb,
+                                                                      size_t n) {
+  const __m128i mask = _mm_set_epi64x(0x0001020304050607ULL, 0x08090a0b0c0d0e0fULL);
+  Lane1 a, b;
+  a.abcd = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(sa)), 0x1B);
+  a.e[0] = _mm_set_epi32(int(sa[4]), 0, 0, 0);
+  b.abcd = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(sb)), 0x1B);
+  b.e[0] = _mm_set_epi32(int(sb[4]), 0, 0, 0);
+  for (; n; --n, pa += 64, pb += 64) {
+    const __m128i a0 = a.abcd, ae = a.e[0], b0 = b.abcd, be = b.e[0];
+#pragma GCC unroll 20
+    for (int g = 0; g < 20; ++g) {
+      group1(a, g, pa, mask);
+      group1(b, g, pb, mask);
+    }
+    a.e[0] = _mm_sha1nexte_epu32(a.e[0], ae);
+    a.abcd = _mm_add_epi32(a.abcd, a0);
+    b.e[0] = _mm_sha1nexte_epu32(b.e[0], be);
+    b.abcd = _mm_add_epi32(b.abcd, b0);
+  }
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(sa), _mm_shuffle_epi32(a.abcd, 0x1B));
+  sa[4] = uint32_t(_mm_extract_epi32(a.e[0], 3));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(sb), _mm_shuffle_epi32(b.abcd, 0x1B));
+  sb[4] = uint32_t(_mm_extract_epi32(b.e[0], 3));
+}
+
+#undef TDL_SHA_TARGET
+
+static const uint32_t kH1[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+
+inline void sha1_out(const uint32_t st[5], uint8_t out[20]) {
+  for (int i = 0; i < 5; ++i) {
+    out[4 * i] = uint8_t(st[i] >> 24);
+    out[4 * i + 1] = uint8_t(st[i] >> 16);
+    out[4 * i + 2] = uint8_t(st[i] >> 8);
+    out[4 * i + 3] = uint8_t(st[i]);
+  }
+}
+
+// SHA-1 of one message (SHA-NI required).
+inline void sha1_x1(const void* data, size_t n, uint8_t out[20]) {
+  uint32_t st[5];
+  std::memcpy(st, kH1, sizeof st);
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  const size_t full = n / 64;
+  if (full) sha1_blocks_x1(st, p, full);
+  uint8_t tail[128];
+  const size_t nb = pad_tail(tail, p + full * 64, n - full * 64, n);  // same padding as SHA-256
+  sha1_blocks_x1(st, tail, nb);
+  sha1_out(st, out);
+}
+
+// SHA-1 of two messages in lockstep (SHA-NI required).
+inline void sha1_x2(const void* da, size_t na, const void* db, size_t nb, uint8_t oa[20], uint8_t ob[20]) {
+  uint32_t sa[5], sb[5];
+  std::memcpy(sa, kH1, sizeof sa);
+  std::memcpy(sb, kH1, sizeof sb);
+  const uint8_t* pa = static_cast<const uint8_t*>(da);
+  const uint8_t* pb = static_cast<const uint8_t*>(db);
+  const size_t fa = na / 64, fb = nb / 64, both = fa < fb ? fa : fb;
+  if (both) sha1_blocks_x2(sa, sb, pa, pb, both);
+  if (fa > both) sha1_blocks_x1(sa, pa + both * 64, fa - both);
+  if (fb > both) sha1_blocks_x1(sb, pb + both * 64, fb - both);
+  uint8_t ta[128], tb[128];
+  const size_t ka = pad_tail(ta, pa + fa * 64, na - fa * 64, na);
+  const size_t kb = pad_tail(tb, pb + fb * 64, nb - fb * 64, nb);
+  if (ka == kb) {
+    sha1_blocks_x2(sa, sb, ta, tb, ka);
+  } else {
+    sha1_blocks_x1(sa, ta, ka);
+    sha1_blocks_x1(sb, tb, kb);
+  }
+  sha1_out(sa, oa);
+  sha1_out(sb, ob);
 }
 
 }  // namespace sha2x

@@ -700,7 +700,7 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
   };
 
   // Each hasher takes two consecutive chunks: SHA-NI hashes them in lockstep
-  // (sha256x2.h).  Both ring slots must be free (K >= 2 whenever n >= 2), and
+  // (sha_ni.h).  Both ring slots must be free (K >= 2 whenever n >= 2), and
   // the chunk the sender waits for always belongs to a pair whose slots are.
   auto hasher = [&] {
     for (;;) {

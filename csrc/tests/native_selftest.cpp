@@ -46,7 +46,7 @@ static std::string signing_key(const std::string& secret, const std::string& dat
   return hmac256(k, "aws4_request");
 }
 
-// Two-stream SHA-NI SHA-256 (sha256x2.h) against OpenSSL: random lengths
+// Two-stream SHA-NI SHA-256 and SHA-1 (sha_ni.h) against OpenSSL: random lengths
 // around the block and padding boundaries, equal and unequal pairs.
 static void test_sha256_pair() {
   std::mt19937 rng(11);
@@ -62,6 +62,12 @@ static void test_sha256_pair() {
     CHECK(std::string(reinterpret_cast<char*>(oa), 32) == one_shot(sha256_md(), a.data(), na));
     CHECK(std::string(reinterpret_cast<char*>(ob), 32) == one_shot(sha256_md(), b.data(), nb));
     CHECK(std::memcmp(oa, r1, 32) == 0);
+    unsigned char s1a[20], s1b[20], s1[20];
+    md_pair(sha1_md(), a.data(), na, b.data(), nb, s1a, s1b);
+    md_raw(sha1_md(), a.data(), na, s1);
+    CHECK(std::string(reinterpret_cast<char*>(s1a), 20) == one_shot(sha1_md(), a.data(), na));
+    CHECK(std::string(reinterpret_cast<char*>(s1b), 20) == one_shot(sha1_md(), b.data(), nb));
+    CHECK(std::memcmp(s1a, s1, 20) == 0);
   }
 }
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """SHA-256 throughput of the aws-chunked hot loop: OpenSSL vs the two-stream
-SHA-NI path (csrc/hash/sha256x2.h).
+SHA-NI path (csrc/hash/sha_ni.h).
 
 Runs ``hashing.chunk_signatures`` over a buffer of 64 KiB chunks on 1 and
 N threads in two child processes, one with ``TRITONDL_SHA_NI=0`` (OpenSSL
