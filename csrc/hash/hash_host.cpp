@@ -254,6 +254,8 @@ PYBIND11_MODULE(_hash_host, m) {
   m.def("verify_pieces", &py_verify_pieces, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
         py::arg("threads") = 0, py::arg("kind") = "sha1");
   m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) { return py::bytes(hmac256(k, msg)); });
+  m.def("sha_ni", &sha2x::cpu_has_sha_ni,
+        "SHA-1/SHA-256 run on the two-stream SHA-NI path (False: OpenSSL; TRITONDL_SHA_NI=0 forces that)");
   m.def("chunk_signatures", &py_chunk_signatures, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
         py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true,
         py::arg("threads") = 1);

@@ -206,14 +206,16 @@ def hybrid_cpu_threads(cpus: int | None = None) -> int:
 
 
 # Cost model for device="auto" batch verification, calibrated on MI355X with
-# the box's 16-CPU share (profiles/r01_hash_v3_windows): the GPU path is
-# bounded by host->HBM copies (~45 GB/s) plus, because the kernel runs one lane
-# per piece, the per-lane SHA-1 rate (~55 MB/s) for one piece; the host path
-# runs ~1.5 GB/s per SHA-NI thread plus ~15 us of per-piece overhead.
+# the box's 16-CPU share (profiles/r01_hash_v3_windows, profiles/r02_sha1_ab):
+# the GPU path is bounded by host->HBM copies (~45 GB/s) plus, because the
+# kernel runs one lane per piece, the per-lane SHA-1 rate (~55 MB/s) for one
+# piece; the host path runs ~1.5 GB/s per thread through OpenSSL, ~3 GB/s
+# with the two-stream SHA-NI pairs (8 GiB v1 resume on 16 threads: 35 -> 55
+# GB/s), plus ~15 us of per-piece overhead.
 GPU_COPY_BPS = 45e9
 GPU_LANE_BPS = 55e6
 GPU_SETUP_S = 5e-3
-CPU_THREAD_BPS = 1.5e9
+CPU_THREAD_BPS = 3.0e9 if getattr(_host, "sha_ni", lambda: False)() else 1.5e9
 CPU_PIECE_S = 15e-6
 
 
