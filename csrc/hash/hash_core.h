@@ -589,17 +589,23 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
 constexpr size_t kMerkleLeaf = 16384;
 
 inline void merkle_reduce(std::vector<unsigned char>& row, size_t width) {
-  // row holds `width` 32-byte nodes; reduce in place to row[0..32)
-  const EVP_MD* md = sha256_md();
-  MdCtx ctx(md);
+  // row holds `width` 32-byte nodes; reduce in place to row[0..32).  Node
+  // pairs are hashed two at a time (SHA-NI lockstep); writing node k only
+  // touches bytes [32k, 32k+32), which nodes >= k have already been read from.
+  unsigned char h[2][32];
   while (width > 1) {
-    for (size_t k = 0; k < width / 2; ++k) {
-      unsigned int outl = 0;
-      if (EVP_DigestInit_ex(ctx.ctx, md, nullptr) != 1 || EVP_DigestUpdate(ctx.ctx, row.data() + 64 * k, 64) != 1 ||
-          EVP_DigestFinal_ex(ctx.ctx, row.data() + 32 * k, &outl) != 1)
-        throw std::runtime_error("EVP failed in merkle_reduce");
+    const size_t half = width / 2;
+    size_t k = 0;
+    for (; k + 1 < half; k += 2) {
+      sha256_pair(row.data() + 64 * k, 64, row.data() + 64 * (k + 1), 64, h[0], h[1]);
+      std::memcpy(row.data() + 32 * k, h[0], 32);
+      std::memcpy(row.data() + 32 * (k + 1), h[1], 32);
     }
-    width /= 2;
+    if (k < half) {
+      sha256_raw(row.data() + 64 * k, 64, h[0]);
+      std::memcpy(row.data() + 32 * k, h[0], 32);
+    }
+    width = half;
   }
 }
 
@@ -683,11 +689,16 @@ inline std::string merkle_verify(const std::vector<std::pair<std::string, long l
     const size_t width = static_cast<size_t>(widths[p]);
     if (width == 0 || (width & (width - 1)) || nl > width) return;
     std::vector<unsigned char> row(32 * width, 0);
-    for (size_t k = 0; k < nl; ++k) {
+    for (size_t k = 0; k < nl; k += 2) {  // leaves in pairs (SHA-NI lockstep)
       const size_t off = k * kMerkleLeaf;
       const size_t len = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off);
-      const std::string d = one_shot(md, buf.data() + off, len);
-      std::memcpy(row.data() + 32 * k, d.data(), 32);
+      if (k + 1 < nl) {
+        const size_t len2 = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off - kMerkleLeaf);
+        md_pair(md, buf.data() + off, len, buf.data() + off + kMerkleLeaf, len2, row.data() + 32 * k,
+                row.data() + 32 * (k + 1));
+      } else {
+        md_raw(md, buf.data() + off, len, row.data() + 32 * k);
+      }
     }
     merkle_reduce(row, width);
     ok[p] = std::memcmp(row.data(), expected.data() + 32 * p, 32) == 0;
