@@ -36,6 +36,7 @@ import struct
 import time
 from dataclasses import dataclass, field
 
+from ...ops import hashing
 from ...utils.disk import check_space
 from ...utils.log import log
 from . import bep40, merkle, mse
@@ -180,6 +181,8 @@ class Torrent:
         self._my_ip: str | None = None                  # learned from our first connection
         self._prio: dict[tuple[str, int], int] = {}     # BEP 40 priority cache
         self.source = None                              # _btwire.Source: links serve REQUESTs from it
+        self._vq: list = []                             # (piece, data, peer) awaiting a verify partner
+        self._vflush = False
         self.assigned: dict[int, set] = {}              # piece -> peer keys whose links fetch it
         # per-file completion (streamed uploads): see watch_files
         self._file_cb = None                            # callable(path) for watched files
@@ -437,9 +440,56 @@ class Torrent:
         src.downloaded += len(data)
         self.downloaded += len(data)
         self.verifying.add(i)
+        if self.info is not None and self.info.pieces:
+            # v1 / hybrid: pieces are verified two at a time (SHA-1 in SHA-NI
+            # lockstep, one executor hop per pair); a lone piece goes at the
+            # end of this loop iteration if no partner turned up by then
+            self._vq.append((i, data, src))
+            if len(self._vq) >= 2:
+                self._submit_verify()
+            elif not self._vflush:
+                self._vflush = True
+                asyncio.get_running_loop().call_soon(self._submit_verify)
+            return
         t = asyncio.get_running_loop().create_task(self._finish_native(i, data, src))
         self._finishers.add(t)
         t.add_done_callback(self._finishers.discard)
+
+    def _submit_verify(self) -> None:
+        self._vflush = False
+        if self.closed:                   # close() is draining: no writes may start now
+            for i, _d, _s in self._vq:
+                self.verifying.discard(i)
+            self._vq.clear()
+            return
+        while self._vq:
+            batch, self._vq = self._vq[:2], self._vq[2:]
+            t = asyncio.get_running_loop().create_task(self._verify_batch(batch))
+            self._finishers.add(t)
+            t.add_done_callback(self._finishers.discard)
+
+    async def _verify_batch(self, batch: list) -> None:
+        assert self.info is not None and self.storage is not None
+        info, st = self.info, self.storage
+
+        def work() -> bytes:
+            exp = b"".join(info.piece_hash(i) for i, _d, _s in batch)
+            ok = hashing.verify_buffers("sha1", [d for _i, d, _s in batch], exp, 1)
+            for (i, d, _s), good in zip(batch, ok):
+                if good:
+                    st.write(i, 0, d)
+                    st.mark(i, True)
+            return ok
+        try:
+            ok = await asyncio.get_running_loop().run_in_executor(None, work)
+        finally:
+            for i, _d, _s in batch:
+                self.verifying.discard(i)
+        for (i, _d, s), good in zip(batch, ok):
+            if good:
+                self._record_piece(i)
+            else:
+                self._bad_piece(i, s)
 
     async def _finish_native(self, i: int, data: memoryview, src: _Peer) -> None:
         try:
@@ -447,15 +497,20 @@ class Torrent:
         finally:
             self.verifying.discard(i)
         if ok is False:
-            src.bad += 1
-            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
-            if src.bad >= self.cfg.max_bad_pieces:
-                self.banned.add(src.addr)
-                src.wire.close()
-            self._rare_dirty = True
-            for q in list(self.peers.values()):
-                if q.link is not None:
-                    self._fill(q)
+            self._bad_piece(i, src)
+
+    def _bad_piece(self, i: int, src: _Peer) -> None:
+        """Piece i from src failed its hash: count it against src (ban at the
+        limit) and let the links fetch it again."""
+        src.bad += 1
+        log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
+        if src.bad >= self.cfg.max_bad_pieces:
+            self.banned.add(src.addr)
+            src.wire.close()
+        self._rare_dirty = True
+        for q in list(self.peers.values()):
+            if q.link is not None:
+                self._fill(q)
 
     async def _native_loop(self, p: _Peer) -> None:
         data = await p.wire.read_raw()
@@ -1075,8 +1130,15 @@ class Torrent:
             self.verifying.discard(i)
         if not ok:
             return ok
+        self._record_piece(i)
+        return True
+
+    def _record_piece(self, i: int) -> None:
+        """Piece i is verified and written: mark it, announce it, update
+        interest, per-file completion and the torrent's completion."""
+        assert self.info is not None
         if self.have[i]:
-            return True
+            return
         self.have[i] = 1
         self.nhave += 1
         if self.source is not None:
@@ -1090,7 +1152,6 @@ class Torrent:
             self._note_piece(i)
         if self.nhave == self.info.num_pieces:
             self.complete.set()
-        return True
 
     def _on_request(self, p: _Peer, pl: bytes) -> None:
         i, off, n = struct.unpack(">III", pl[:12])

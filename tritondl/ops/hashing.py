@@ -260,6 +260,13 @@ def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", 
     return _host.piece_hashes(kind, data, piece_len, threads or effective_cpus())
 
 
+def verify_buffers(kind: str, buffers: Sequence, expected: bytes, threads: int = 0) -> bytes:
+    """Verify in-memory pieces (any buffer objects) against concatenated
+    digests on the host: SHA-NI pairs on ``threads`` threads, GIL released.
+    One byte (0/1) per buffer."""
+    return _host.verify_buffers(kind, list(buffers), expected, threads)
+
+
 def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: bytes, kind: str = "sha1",
                   device: str = "cpu", threads: int = 0) -> bytes:
     """Verify the torrent layout ``files`` [(path, length), ...] against
