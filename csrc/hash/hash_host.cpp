@@ -251,6 +251,38 @@ PYBIND11_MODULE(_hash_host, m) {
         py::arg("length") = -1, py::arg("bufsize") = 1 << 20);
   m.def("piece_hashes", &py_piece_hashes, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"),
         py::arg("threads") = 0);
+  m.def(
+      "verify_buffers",
+      [](const std::string& kind, const std::vector<py::buffer>& bufs, const py::bytes& expected, int threads) {
+        const EVP_MD* md = md_for(kind);
+        const size_t dl = static_cast<size_t>(EVP_MD_size(md));
+        const std::string exp = expected;
+        if (exp.size() != dl * bufs.size()) throw std::invalid_argument("expected digest blob has wrong size");
+        std::vector<py::buffer_info> keep(bufs.size());
+        std::vector<BufView> v;
+        v.reserve(bufs.size());
+        for (size_t i = 0; i < bufs.size(); ++i) v.push_back(view_of(bufs[i], keep[i]));
+        std::string ok(bufs.size(), '\0');
+        {
+          py::gil_scoped_release nogil;
+          const size_t n = v.size(), pairs = (n + 1) / 2;
+          parallel_for(pairs, static_cast<int>(std::min<size_t>(pairs, threads <= 0 ? default_threads() : threads)),
+                       [&](size_t k) {
+                         unsigned char d[2][EVP_MAX_MD_SIZE];
+                         const size_t i = 2 * k;
+                         if (i + 1 < n) {
+                           md_pair(md, v[i].ptr, v[i].len, v[i + 1].ptr, v[i + 1].len, d[0], d[1]);
+                           ok[i + 1] = std::memcmp(d[1], exp.data() + (i + 1) * dl, dl) == 0;
+                         } else {
+                           md_raw(md, v[i].ptr, v[i].len, d[0]);
+                         }
+                         ok[i] = std::memcmp(d[0], exp.data() + i * dl, dl) == 0;
+                       });
+        }
+        return py::bytes(ok);
+      },
+      py::arg("kind"), py::arg("buffers"), py::arg("expected"), py::arg("threads") = 0,
+      "Verify in-memory pieces against concatenated digests (pairs on SHA-NI, GIL released); one byte (0/1) each.");
   m.def("verify_pieces", &py_verify_pieces, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
         py::arg("threads") = 0, py::arg("kind") = "sha1");
   m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) { return py::bytes(hmac256(k, msg)); });
