@@ -252,6 +252,33 @@ PYBIND11_MODULE(_hash_host, m) {
   m.def("piece_hashes", &py_piece_hashes, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"),
         py::arg("threads") = 0);
   m.def(
+      "merkle_root",
+      [](const py::buffer& data, size_t width) {
+        py::buffer_info bi;
+        BufView v = view_of(data, bi);
+        const size_t nl = (v.len + kMerkleLeaf - 1) / kMerkleLeaf;
+        if (width == 0 || (width & (width - 1)) || nl > width)
+          throw std::invalid_argument("width must be a power of two >= the leaf count");
+        std::vector<unsigned char> row(32 * width, 0);
+        {
+          py::gil_scoped_release nogil;
+          for (size_t k = 0; k < nl; k += 2) {  // leaves in SHA-NI pairs
+            const size_t off = k * kMerkleLeaf, len = std::min(kMerkleLeaf, v.len - off);
+            if (k + 1 < nl) {
+              const size_t len2 = std::min(kMerkleLeaf, v.len - off - kMerkleLeaf);
+              sha256_pair(v.ptr + off, len, v.ptr + off + kMerkleLeaf, len2, row.data() + 32 * k,
+                          row.data() + 32 * (k + 1));
+            } else {
+              sha256_raw(v.ptr + off, len, row.data() + 32 * k);
+            }
+          }
+          merkle_reduce(row, width);
+        }
+        return py::bytes(reinterpret_cast<const char*>(row.data()), 32);
+      },
+      py::arg("data"), py::arg("width"),
+      "BEP 52 merkle root of one piece's data: SHA-256 leaves of 16 KiB, zero-padded to `width`, reduced.");
+  m.def(
       "verify_buffers",
       [](const std::string& kind, const std::vector<py::buffer>& bufs, const py::bytes& expected, int threads) {
         const EVP_MD* md = md_for(kind);

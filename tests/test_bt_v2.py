@@ -253,3 +253,19 @@ def test_gpu_leaf_path_logic_emulated_on_host(tmp_path, monkeypatch):
     monkeypatch.setattr(hashing, "_resolve", lambda d: d)
     ok = hashing.verify_pieces_v2(layout, info.piece_length, exp, widths, reals, known, device="gpu")
     assert ok == b"\x01" * info.num_pieces
+
+
+def test_native_merkle_root_matches_the_spec():
+    """hashing.merkle_root (C++, SHA-NI pairs) == merkle.piece_root (spec)
+    for lengths around leaf boundaries and padded widths."""
+    import os as _os
+    from tritondl.fetch.bt import merkle as mk
+    from tritondl.ops import hashing
+    for n in (1, 100, 16384, 16385, 3 * 16384, 3 * 16384 + 7, 64 * 16384):
+        data = _os.urandom(n)
+        nl = (n + 16383) // 16384
+        for width in {mk.next_pow2(nl), 2 * mk.next_pow2(nl), 64}:
+            if width >= nl:
+                assert hashing.merkle_root(data, width) == mk.piece_root(data, width)
+    with pytest.raises(ValueError):
+        hashing.merkle_root(b"x" * 40000, 2)          # 3 leaves do not fit 2

@@ -25,6 +25,11 @@ from urllib.parse import parse_qs, quote, unquote, urlparse
 from . import bencode, merkle
 from .bencode import BencodeError
 
+try:  # native piece roots (SHA-NI pairs, GIL released); merkle.piece_root is the executable spec
+    from ...ops.hashing import merkle_root as _merkle_root
+except ImportError:  # pragma: no cover - host extension not built
+    _merkle_root = merkle.piece_root
+
 BLOCK = 16 * 1024  # request/metadata block size
 
 
@@ -154,7 +159,7 @@ class Info:
         exp, width, real = self.v2_piece(i)
         if exp is None:
             return None
-        return merkle.piece_root(memoryview(data)[:real], width) == exp
+        return _merkle_root(memoryview(data)[:real], width) == exp
 
     def matches(self, infohash: bytes) -> bool:
         return infohash in (self.infohash, self.infohash_v2, self.infohash_v2[:20]) and len(infohash) in (20, 32)

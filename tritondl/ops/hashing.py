@@ -260,6 +260,12 @@ def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", 
     return _host.piece_hashes(kind, data, piece_len, threads or effective_cpus())
 
 
+def merkle_root(data, width: int) -> bytes:
+    """BEP 52 root of one piece's data over a ``width``-leaf tree, native
+    (SHA-NI pairs, GIL released); ``fetch.bt.merkle.piece_root`` is the spec."""
+    return _host.merkle_root(data, width)
+
+
 def verify_buffers(kind: str, buffers: Sequence, expected: bytes, threads: int = 0) -> bytes:
     """Verify in-memory pieces (any buffer objects) against concatenated
     digests on the host: SHA-NI pairs on ``threads`` threads, GIL released.
