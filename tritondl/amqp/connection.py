@@ -109,6 +109,34 @@ def parse_url(url: str) -> URLParams:
     return p
 
 
+class _FrameProtocol(asyncio.Protocol):
+    """Reads of an open AMQP connection, handled in the transport callback
+    (``Connection._on_data``).  Write flow control and connection loss go to
+    the StreamWriter's protocol too, so ``drain`` and ``close`` keep working."""
+
+    def __init__(self, conn: "Connection", transport: asyncio.Transport) -> None:
+        self.conn = conn
+        self.old = transport.get_protocol()
+        self.parser = codec.FrameParser()
+
+    def data_received(self, data: bytes) -> None:
+        self.conn._on_data(self.parser, data)
+
+    def eof_received(self) -> bool:
+        self.conn._abort(ConnectionClosed(0, "connection lost: EOF"))
+        return False
+
+    def connection_lost(self, exc) -> None:
+        self.conn._abort(ConnectionClosed(0, f"connection lost: {exc!r}" if exc else "connection lost"))
+        self.old.connection_lost(exc)
+
+    def pause_writing(self) -> None:
+        self.old.pause_writing()
+
+    def resume_writing(self) -> None:
+        self.old.resume_writing()
+
+
 class Connection:
     def __init__(self, params: URLParams, heartbeat: int = 30, frame_max: int = codec.DEFAULT_FRAME_MAX,
                  channel_max: int = 2047, client_properties: dict | None = None) -> None:
@@ -151,7 +179,11 @@ class Connection:
         self._closed = loop.create_future()
         self._handshake_q = asyncio.Queue()
         self._write(codec.PROTOCOL_HEADER)
-        self._tasks.append(asyncio.ensure_future(self._read_loop()))
+        proto = _FrameProtocol(self, self._writer.transport)
+        buffered = bytes(getattr(self._reader, "_buffer", b""))
+        self._writer.transport.set_protocol(proto)
+        if buffered:
+            proto.data_received(buffered)
         try:
             start = await self._hs_expect("connection.start")
             self.server_properties = start.server_properties
@@ -227,55 +259,53 @@ class Connection:
         if self._writer is not None:
             await self._writer.drain()
 
-    async def _read_loop(self) -> None:
-        err: BaseException = ConnectionClosed(0, "connection lost")
-        assert self._reader is not None
-        parser = codec.FrameParser()
+    def _on_frames(self, frames) -> BaseException | None:
+        """Dispatch parsed frames; returns the error that ends the connection
+        (connection.close from the server, close-ok after ours), else None."""
+        for ftype, ch, payload in frames:
+            if ftype == codec.FRAME_HEARTBEAT:
+                continue
+            if ch == 0:
+                if ftype != codec.FRAME_METHOD:
+                    raise codec.FrameError("non-method frame on channel 0")
+                m = codec.decode_method(payload)
+                if self._handshake_q is not None and m.name != "connection.close":
+                    self._handshake_q.put_nowait(m)
+                    continue
+                if m.name == "connection.close":
+                    try:
+                        self._send_method(0, Method("connection.close_ok"))
+                    except AMQPError:
+                        pass
+                    if self._handshake_q is not None:
+                        self._handshake_q.put_nowait(m)
+                    return ConnectionClosed(m.reply_code, m.reply_text)
+                if m.name == "connection.close_ok":
+                    if self._close_ok and not self._close_ok.done():
+                        self._close_ok.set_result(True)
+                    return ConnectionClosed(codec.REPLY_SUCCESS, "closed by client")
+                if m.name == "connection.blocked":
+                    self.unblocked.clear()
+                    self.blocked.set()
+                elif m.name == "connection.unblocked":
+                    self.blocked.clear()
+                    self.unblocked.set()
+                continue
+            chan = self._channels.get(ch)
+            if chan is not None:
+                chan._on_frame(ftype, payload)
+        return None
+
+    def _on_data(self, parser: codec.FrameParser, data: bytes) -> None:
+        """Transport callback: parse and dispatch everything this read
+        delivered, synchronously (no reader task to wake per read)."""
+        if self._closed is None or self._closed.done():
+            return
+        self._last_read = time.monotonic()
+        err: BaseException | None
         try:
-            done = False
-            while not done:
-                for ftype, ch, payload in await codec.read_frames(self._reader, parser):
-                    parser.frame_max = self.frame_max or 0
-                    self._last_read = time.monotonic()
-                    if ftype == codec.FRAME_HEARTBEAT:
-                        continue
-                    if ch == 0:
-                        if ftype != codec.FRAME_METHOD:
-                            raise codec.FrameError("non-method frame on channel 0")
-                        m = codec.decode_method(payload)
-                        if self._handshake_q is not None and m.name != "connection.close":
-                            self._handshake_q.put_nowait(m)
-                            continue
-                        if m.name == "connection.close":
-                            try:
-                                self._send_method(0, Method("connection.close_ok"))
-                            except AMQPError:
-                                pass
-                            if self._handshake_q is not None:
-                                self._handshake_q.put_nowait(m)
-                            err = ConnectionClosed(m.reply_code, m.reply_text)
-                            done = True
-                            break
-                        if m.name == "connection.close_ok":
-                            if self._close_ok and not self._close_ok.done():
-                                self._close_ok.set_result(True)
-                            err = ConnectionClosed(codec.REPLY_SUCCESS, "closed by client")
-                            done = True
-                            break
-                        if m.name == "connection.blocked":
-                            self.unblocked.clear()
-                            self.blocked.set()
-                        elif m.name == "connection.unblocked":
-                            self.blocked.clear()
-                            self.unblocked.set()
-                        continue
-                    chan = self._channels.get(ch)
-                    if chan is not None:
-                        chan._on_frame(ftype, payload)
-        except (asyncio.IncompleteReadError, ConnectionError, OSError) as e:
-            err = ConnectionClosed(0, f"connection lost: {e!r}")
-        except asyncio.CancelledError:
-            err = ConnectionClosed(0, "reader cancelled")
+            parser.frame_max = self.frame_max or 0
+            err = self._on_frames(parser.feed(data))
         except AMQPError as e:
             err = e
             try:
@@ -283,7 +313,8 @@ class Connection:
                                                                 "reply_text": str(e)[:200]}))
             except AMQPError:
                 pass
-        self._abort(err)
+        if err is not None:
+            self._abort(err)
 
     async def _heartbeat_loop(self) -> None:
         hb = self.heartbeat
