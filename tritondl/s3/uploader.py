@@ -65,7 +65,7 @@ class Uploader:
 
     @classmethod
     def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "",
-                 part_size: int = 64 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
+                 part_size: int = 16 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
                  env=None, sign_threads: int = 4, ca_file: str = "") -> "Uploader":
         ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
         Endpoint.parse(ep)                       # ValueError on an endpoint minio-go would refuse
