@@ -120,12 +120,21 @@ def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
         async def no_tcp(self, addr):
             raise OSError("tcp disabled for this test")
         monkeypatch.setattr(Torrent, "_dial_tcp", no_tcp)
+        from tritondl.fetch.bt import peer as pw
+        delivered = []
+        orig = pw.UtpLinkReader.deliver
+
+        def spy(self, data):
+            delivered.append(len(data))
+            return orig(self, data)
+        monkeypatch.setattr(pw.UtpLinkReader, "deliver", spy)   # the native link is fed straight from the engine
         dst = tmp_path / "job"
         os.makedirs(dst)
         dl = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", utp=True, verify_device="cpu"),
                                progress_interval=0.05, use_dht=False)
         await dl.download(str(dst), lambda u, p: None, magnet_for(info, peers=[("127.0.0.1", st.port)]))
         assert (dst / "film.mkv").read_bytes() == (src / "film.mkv").read_bytes()
+        assert sum(delivered) > 1_000_000
         await st.close()
     asyncio.run(asyncio.wait_for(main(), 60))
 

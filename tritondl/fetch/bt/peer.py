@@ -137,16 +137,28 @@ class Wire:
             raise asyncio.IncompleteReadError(b"", None)
         return data
 
-    def take_over(self, link, on_data) -> tuple[LinkReader, bytes] | None:
-        """Switch a plain TCP connection to zero-copy native receive
-        (:class:`LinkReader`).  Returns (reader, bytes already buffered — the
-        caller feeds these first), or None where the transport cannot switch
-        (MSE-encrypted, uTP, closing): those keep :meth:`read_raw`.  Call only
-        while no read is pending."""
+    def take_over(self, link, on_data, on_bytes=None) -> tuple[LinkReader, bytes] | None:
+        """Switch a connection's receive side to the native link.  Plain TCP
+        gets zero-copy receive (:class:`LinkReader`: ``on_data(nbytes)`` after
+        the kernel wrote into the link's buffer); a uTP stream hands the
+        engine's bytes straight to ``on_bytes(data)`` (:class:`UtpLinkReader`).
+        Returns (reader, bytes already buffered — the caller feeds these
+        first), or None (MSE-encrypted, closing): those keep :meth:`read_raw`.
+        Call only while no read is pending."""
         tr = self.writer.transport
         buf = getattr(self.reader, "_buffer", None)
-        if type(self.reader) is not asyncio.StreamReader or type(tr).__name__ != "_SelectorSocketTransport" \
-                or buf is None or tr.is_closing() or self.reader.at_eof() or self.reader.exception() is not None:
+        if type(self.reader) is not asyncio.StreamReader or buf is None or tr.is_closing() \
+                or self.reader.at_eof() or self.reader.exception() is not None:
+            return None
+        stream = getattr(tr, "stream", None)
+        if type(tr).__name__ == "_UtpTransport" and stream is not None and on_bytes is not None:
+            leftover = bytes(self._rbuf) + bytes(buf)
+            self._rbuf.clear()
+            buf.clear()
+            urx = UtpLinkReader(tr, link, on_bytes)
+            stream.sink, stream.sink_eof = urx.deliver, urx.eof
+            return urx, leftover
+        if type(tr).__name__ != "_SelectorSocketTransport":
             return None
         leftover = bytes(self._rbuf) + bytes(buf)
         self._rbuf.clear()
@@ -369,6 +381,37 @@ class LinkReader(asyncio.BufferedProtocol):
         w = self._waiter
         if w is not None and not w.done():
             w.set_result(None)
+
+
+class UtpLinkReader(LinkReader):
+    """:class:`LinkReader` for a uTP stream: the uTP engine's delivered bytes
+    come in through :meth:`deliver` (the stream's sink) instead of a socket
+    read callback; no transport protocol is swapped and reading is never
+    paused (the engine's receive window does the flow control)."""
+
+    def __init__(self, transport: asyncio.Transport, link, on_bytes) -> None:
+        self._tr = transport
+        self._old = None
+        self._link = link
+        self._on_data = on_bytes
+        self._msgs = []
+        self._waiter = None
+        self._exc = None
+        self._eof = False
+        self._paused = False
+        self._wpaused = False
+        self._reading = True
+
+    def deliver(self, data: bytes) -> None:
+        if self._exc is None:
+            self.buffer_updated(data)          # on_bytes(data), errors end the loop
+
+    def eof(self) -> None:
+        self._eof = True
+        self._wake()
+
+    def _update_reading(self) -> None:
+        pass
 
 
 def parse_ext_handshake(payload: bytes) -> ExtHandshake:

@@ -528,6 +528,11 @@ class Torrent:
         p.last_recv = time.monotonic()
         self._native_events(p, *p.link.feed_n(nbytes), lambda m: p.rx.push(m[0], m[1]))
 
+    def _native_recv_bytes(self, p: _Peer, data: bytes) -> None:
+        """UtpLinkReader callback: bytes the uTP engine delivered for p."""
+        p.last_recv = time.monotonic()
+        self._native_events(p, *p.link.feed(data), lambda m: p.rx.push(m[0], m[1]))
+
     def _native_events(self, p: _Peer, ev, out: bytes, defer) -> None:
         """Act on what a link parsed: pieces and choke state here and now;
         other messages go to ``defer`` for the (async) dispatcher."""
@@ -874,7 +879,8 @@ class Torrent:
             if p.link is not None:
                 if p.rx is None and not p.rx_tried:
                     p.rx_tried = True
-                    r = p.wire.take_over(p.link, functools.partial(self._native_recv, p))
+                    r = p.wire.take_over(p.link, functools.partial(self._native_recv, p),
+                                         functools.partial(self._native_recv_bytes, p))
                     if r is not None:
                         p.rx, leftover = r
                         if leftover:

@@ -15,6 +15,7 @@ import asyncio
 import contextlib
 import socket
 import time
+from typing import Callable
 
 try:
     from ... import _utp  # type: ignore[attr-defined]
@@ -123,11 +124,16 @@ class _Stream:
         self.reader = asyncio.StreamReader(limit=1 << 22)
         self.protocol = asyncio.StreamReaderProtocol(self.reader)
         self.transport = _UtpTransport(sock, cid, peer)
+        self.transport.stream = self
         self.transport.set_protocol(self.protocol)
         self.protocol.connection_made(self.transport)
         self.writer = asyncio.StreamWriter(self.transport, self.protocol, self.reader, loop)
         self.connected = asyncio.Event()
         self.eof = False
+        # a native link's receive hook (peer.Wire.take_over): when set, bytes
+        # the engine delivers go straight to it instead of the StreamReader
+        self.sink: Callable[[bytes], None] | None = None
+        self.sink_eof: Callable[[], None] | None = None
 
 
 class UtpSocket:
@@ -170,6 +176,8 @@ class UtpSocket:
             if not s.eof:
                 s.eof = True
                 s.reader.feed_eof()
+                if s.sink_eof is not None:
+                    s.sink_eof()
         self._flush()
         if self._ticker is not None:
             self._ticker.cancel()
@@ -222,12 +230,17 @@ class UtpSocket:
             s.connected.set()
         data = self.engine.read(cid)
         if data:
-            s.reader.feed_data(data)
+            if s.sink is not None:
+                s.sink(data)
+            else:
+                s.reader.feed_data(data)
         if not s.eof and (self.engine.eof(cid) or st == _utp.RESET):
             s.eof = True
             if st == _utp.RESET and not s.connected.is_set():
                 s.connected.set()
             s.reader.feed_eof()
+            if s.sink_eof is not None:
+                s.sink_eof()
         s.transport._push()
 
     def _flush(self) -> None:
