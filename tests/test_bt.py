@@ -541,3 +541,49 @@ def test_ipv6_peer_dials_dual_stack_listener(tmp_path):
         assert (dst / "v6.mkv").read_bytes() == (src / "v6.mkv").read_bytes()
         await s.stop()
     run(main())
+
+
+def test_interest_counters_track_the_bitmaps(tmp_path):
+    """p.wants (O(1) 'does p have a piece we lack') stays equal to the bitmap
+    computation through HAVE/BITFIELD, our own completions and a resume jump."""
+    import random
+    from tritondl.fetch.bt import peer as pw
+    from tritondl.fetch.bt.torrent import Torrent, _Peer
+
+    class StubWire:
+        closed = False
+
+        def __getattr__(self, _name):
+            return lambda *a, **k: None
+
+    src = tmp_path / "src"
+    make_payload(str(src), {"a.bin": 40 * 16384})
+    info = torrent_for(str(src / "a.bin"), 16384)
+    t = Torrent(info.infohash, str(tmp_path / "dst"), TorrentConfig(native_wire=False), info=info)
+    t._downloading = True
+    rng = random.Random(9)
+    n = info.num_pieces
+    peers = []
+    for k in range(4):
+        p = _Peer(StubWire(), ("10.0.0.%d" % k, 1), pw.Handshake(bytes(8), info.infohash, bytes(20)), n)
+        t.peers[p.key] = p
+        peers.append(p)
+
+    def truth(p):
+        return (int.from_bytes(p.have, "little") & ~int.from_bytes(t.have, "little")).bit_count()
+    for step in range(300):
+        r = rng.random()
+        if r < 0.6:
+            t._peer_has(rng.choice(peers), [rng.randrange(n) for _ in range(rng.randint(1, 5))])
+        elif r < 0.95:
+            i = rng.randrange(n)
+            if not t.have[i]:
+                t._record_piece(i)
+        else:                                             # resume-style jump of our bitmap
+            for i in rng.sample(range(n), 5):
+                if not t.have[i]:
+                    t.have[i] = 1
+                    t.nhave += 1
+            t._recount_wants()
+        for p in peers:
+            assert p.wants == truth(p), step

@@ -415,6 +415,9 @@ def test_download_completes_against_chaotic_scripted_peers(tmp_path, fast, nativ
         finally:
             dialer.cancel()
         assert t.store is None or t.store.partial_bytes == 0
+        mine = ~int.from_bytes(t.have, "little")
+        for q in t.peers.values():                       # O(1) interest counters == the bitmap truth
+            assert q.wants == (int.from_bytes(q.have, "little") & mine).bit_count() == 0
         with open(tmp_path / "dst" / "P" / "a.bin", "rb") as f:
             assert f.read() == payload
         await t.close()

@@ -130,6 +130,7 @@ class _Peer:
         self.listen_addr: tuple[str, int] | None = None   # where others can dial it (PEX)
         self.pex_sent: set[tuple[str, int]] = set()
         self.bad = 0
+        self.wants = 0                                      # pieces it has that we lack
         self.downloaded = 0
         self.meta_requested = False
         self.link = None                                    # _btwire.Link once the native data plane runs
@@ -311,6 +312,7 @@ class Torrent:
         self.avail = [0] * n
         for p in self.peers.values():
             p.have = bytearray(n) if len(p.have) != n else p.have
+        self._recount_wants()
         self.got_info.set()
 
     async def download_all(self) -> None:
@@ -337,6 +339,7 @@ class Torrent:
         for i in have:
             self.have[i] = 1
         self.nhave = len(have)
+        self._recount_wants()
         self._init_file_tracking()
         if self.cfg.native_wire and _W is not None:
             n, pl, total = self.info.num_pieces, self.info.piece_length, self.info.total_length
@@ -958,16 +961,25 @@ class Torrent:
     def _peer_has(self, p: _Peer, idxs) -> None:
         if self.info is None:
             return
+        have = self.have
         for i in idxs:
             if p.set_have(i):
                 self.avail[i] += 1
                 self._rare_dirty = True
+                if not have[i]:
+                    p.wants += 1
         self._update_interest(p)
         self._fill(p)
 
     def _wants(self, p: _Peer) -> bool:
-        """Does p have any piece we lack?  (bitwise over the whole bitmap, in C)"""
-        return bool(int.from_bytes(p.have, "little") & ~int.from_bytes(self.have, "little"))
+        """Does p have any piece we lack?  O(1): p.wants counts them, kept by
+        _peer_has / _record_piece and recounted when our bitmap jumps (resume)."""
+        return p.wants > 0
+
+    def _recount_wants(self) -> None:
+        mine = ~int.from_bytes(self.have, "little")
+        for p in self.peers.values():
+            p.wants = (int.from_bytes(p.have, "little") & mine).bit_count() if len(p.have) == len(self.have) else 0
 
     def _update_interest(self, p: _Peer) -> None:
         if self.info is None or not self._downloading:
@@ -1151,6 +1163,8 @@ class Torrent:
             self.source.set_have(i)
         for q in list(self.peers.values()):
             q.wire.have(i)
+            if q.have[i]:
+                q.wants -= 1
             if q.am_interested and q.have[i] and not self._wants(q):
                 q.am_interested = False
                 q.wire.send(pw.NOT_INTERESTED)
