@@ -145,6 +145,8 @@ PYBIND11_MODULE(_btwire, m) {
       .def("set_source", &Link::set_source)
       .def_property("serving", &Link::serving, &Link::set_serving)
       .def_property_readonly("uploaded", &Link::uploaded)
+      .def_property_readonly("stalled", &Link::stalled,
+                             "the last feed hit the serve budget; feed_n(0) / feed(b'') parses the rest")
       .def_property_readonly("serve_errors", &Link::serve_errors)
       .def_property_readonly("buffered", &Link::buffered);
 }

@@ -319,7 +319,15 @@ class Link {
     size_t pos = rpos_;
     const size_t len = wpos_;
     bool bad = false;
+    stalled_ = false;
     while (len - pos >= 4) {
+      if (source_ && out->size() >= serve_budget_) {
+        // enough PIECE replies for one write: leave the rest parsed later
+        // (feed_n(0) once the socket drains), so a peer that pipelines
+        // thousands of REQUESTs cannot make one read queue unbounded output
+        stalled_ = true;
+        break;
+      }
       const uint32_t ml = be32(&buf_[pos]);
       if (ml > kMaxMsg) {
         ev->push_back(Event::bad("message too large"));
@@ -436,6 +444,8 @@ class Link {
   bool serving() const { return serving_; }
   void set_serving(bool s) { serving_ = s; }   // false: we choke this peer
   uint64_t uploaded() const { return uploaded_; }
+  // The last feed stopped at the serve budget with messages left unparsed.
+  bool stalled() const { return stalled_; }
   uint64_t serve_errors() const { return serve_errors_; }
 
  private:
@@ -522,6 +532,8 @@ class Link {
   std::shared_ptr<PieceStore> store_;
   std::shared_ptr<Source> source_;
   bool serving_ = true;
+  bool stalled_ = false;
+  size_t serve_budget_ = size_t(2) << 20;  // PIECE reply bytes per feed call
   uint64_t uploaded_ = 0, serve_errors_ = 0;
   int pipeline_;
   int refill_;   // issue new requests only once this many slots are free

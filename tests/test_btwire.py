@@ -424,3 +424,80 @@ def test_download_completes_against_chaotic_scripted_peers(tmp_path, fast, nativ
         for s in servers:
             s.close()
     asyncio.run(main())
+
+
+def test_native_serving_backpressure_bounds_the_write_buffer(tmp_path):
+    """A peer that pipelines thousands of REQUESTs but does not read: the
+    seeder's link answers as it parses, the transport signals pause_writing
+    and LinkReader stops reading, so the seeder's write buffer stays bounded;
+    once the peer reads, every request is answered with the right bytes."""
+    import asyncio
+
+    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl.fetch.bt import peer as pw
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 8 << 20})
+        info = torrent_for(str(src / "P"), 1 << 20)
+        payload = (src / "P" / "a.bin").read_bytes()
+        seed = Torrent(info.infohash, str(src), TorrentConfig(listen_host="127.0.0.1", seed=True, verify_device="cpu",
+                                                              utp=False, encryption="disable"), info=info)
+        await seed.start()
+        await seed.download_all()
+        r, w = await asyncio.open_connection("127.0.0.1", seed.port)
+        w.transport.set_write_buffer_limits(1 << 20)
+        sock = w.get_extra_info("socket")
+        import socket as _s
+        sock.setsockopt(_s.SOL_SOCKET, _s.SO_RCVBUF, 64 << 10)   # keep the kernel's share small
+        w.write(pw.encode_handshake(info.infohash, b"-BPTEST-" + bytes(12)))
+        await pw.read_handshake(r)
+        reqs = [(i, off) for _rep in range(4) for i in range(8) for off in range(0, 1 << 20, B)]
+        w.write(b"".join(struct.pack(">IBIII", 13, pw.REQUEST, i, off, B) for i, off in reqs))
+        await w.drain()
+        await asyncio.sleep(0.5)                                # seeder answers until its socket backs up
+        (peer,) = list(seed.peers.values())
+        assert peer.rx is not None
+        buffered = peer.wire.writer.transport.get_write_buffer_size()
+        assert buffered < (24 << 20), buffered                  # 32 MiB were requested
+        got = 0
+        while got < len(reqs):                                   # now read everything back
+            (n,) = struct.unpack(">I", await asyncio.wait_for(r.readexactly(4), 10))
+            body = await r.readexactly(n)
+            if body[:1] != bytes([pw.PIECE]):
+                continue
+            i, off = struct.unpack(">II", body[1:9])
+            assert body[9:] == payload[i * (1 << 20) + off:i * (1 << 20) + off + B]
+            got += 1
+        w.close()
+        await seed.close()
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_link_serve_budget_stalls_and_resumes(tmp_path):
+    """One feed answers at most ~2 MiB of PIECEs; the rest of the REQUESTs
+    stay buffered (stalled) until feed(b"") is called again."""
+    import os
+    data = os.urandom(4 << 20)
+    (tmp_path / "f").write_bytes(data)
+    src = W.Source(4, 1 << 20, len(data))
+    fd = os.open(tmp_path / "f", os.O_RDONLY)
+    src.add_file(fd, 0, len(data))
+    os.close(fd)
+    src.set_have_bits(b"\x01" * 4)
+    link = W.Link(W.PieceStore(4, 1 << 20, len(data)), pipeline=4, fast=True)
+    link.set_source(src)
+    reqs = [(i, off) for i in range(4) for off in range(0, 1 << 20, B)]
+    _ev, out = link.feed(b"".join(struct.pack(">IBIII", 13, 6, i, off, B) for i, off in reqs))
+    served = msgs(out)
+    assert link.stalled and (2 << 20) <= len(out) < (2 << 20) + B + 64
+    rounds = 1
+    while link.stalled:
+        _ev, out = link.feed(b"")
+        served += msgs(out)
+        rounds += 1
+    assert rounds == 2 and len(served) == len(reqs) and link.buffered == 0
+    for (mid, pl), (i, off) in zip(served, reqs):
+        assert mid == 7 and pl[:8] == struct.pack(">II", i, off)
+        assert pl[8:] == data[i * (1 << 20) + off:i * (1 << 20) + off + B]

@@ -156,6 +156,8 @@ class Wire:
             self._rbuf.clear()
             buf.clear()
             urx = UtpLinkReader(tr, link, on_bytes)
+            urx._old = tr.get_protocol()
+            tr.set_protocol(urx)                 # its pause/resume_writing reach the reader (serve budget)
             stream.sink, stream.sink_eof = urx.deliver, urx.eof
             return urx, leftover
         if type(tr).__name__ != "_SelectorSocketTransport":
@@ -304,16 +306,30 @@ class LinkReader(asyncio.BufferedProtocol):
         self._paused = False      # control messages queued up: the peer loop is behind
         self._wpaused = False     # write buffer over the high-water mark
         self._reading = True
+        self._kick_scheduled = False
+        self._empty = 0           # what _on_data gets to parse what is already buffered
 
     # -- transport callbacks --------------------------------------------------
     def get_buffer(self, sizehint: int):
         return self._link.recv_buffer(1 << 20)
 
-    def buffer_updated(self, nbytes: int) -> None:
+    def buffer_updated(self, nbytes) -> None:
         try:
             self._on_data(nbytes)
         except Exception as e:  # a protocol violation: end the peer loop with it
             self._fail(e)
+            return
+        if self._link.stalled and not self._kick_scheduled:
+            # the link stopped at its serve budget: parse the rest once the
+            # replies are on their way (now, or when the socket drains)
+            self._kick_scheduled = True
+            if not self._wpaused:
+                asyncio.get_running_loop().call_soon(self._kick)
+
+    def _kick(self) -> None:
+        self._kick_scheduled = False
+        if self._exc is None and not self._tr.is_closing():
+            self.buffer_updated(self._empty)
 
     def eof_received(self) -> bool:
         self._eof = True
@@ -338,6 +354,8 @@ class LinkReader(asyncio.BufferedProtocol):
         self._wpaused = False
         self._update_reading()
         self._old.resume_writing()
+        if self._kick_scheduled:
+            asyncio.get_running_loop().call_soon(self._kick)
 
     def _update_reading(self) -> None:
         want = not (self._paused or self._wpaused or self._exc is not None)
@@ -401,6 +419,8 @@ class UtpLinkReader(LinkReader):
         self._paused = False
         self._wpaused = False
         self._reading = True
+        self._kick_scheduled = False
+        self._empty = b""
 
     def deliver(self, data: bytes) -> None:
         if self._exc is None:

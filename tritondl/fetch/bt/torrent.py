@@ -521,10 +521,15 @@ class Torrent:
         await self._native_feed(p, data)
 
     async def _native_feed(self, p: _Peer, data: bytes) -> None:
-        msgs: list = []
-        self._native_events(p, *p.link.feed(data), msgs.append)
-        for m in msgs:
-            await self._dispatch(p, m[0], m[1])
+        while True:
+            msgs: list = []
+            self._native_events(p, *p.link.feed(data), msgs.append)
+            for m in msgs:
+                await self._dispatch(p, m[0], m[1])
+            if not p.link.stalled or p.wire.closed or self.closed:
+                return
+            await p.wire.drain()      # served up to the budget: let it drain, then parse the rest
+            data = b""
 
     def _native_recv(self, p: _Peer, nbytes: int) -> None:
         """LinkReader callback: nbytes landed in p.link's buffer (zero-copy)."""
