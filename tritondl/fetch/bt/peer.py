@@ -156,7 +156,6 @@ class Wire:
             self._rbuf.clear()
             buf.clear()
             urx = UtpLinkReader(tr, link, on_bytes)
-            urx._old = tr.get_protocol()
             tr.set_protocol(urx)                 # its pause/resume_writing reach the reader (serve budget)
             stream.sink, stream.sink_eof = urx.deliver, urx.eof
             return urx, leftover
@@ -404,23 +403,13 @@ class LinkReader(asyncio.BufferedProtocol):
 class UtpLinkReader(LinkReader):
     """:class:`LinkReader` for a uTP stream: the uTP engine's delivered bytes
     come in through :meth:`deliver` (the stream's sink) instead of a socket
-    read callback; no transport protocol is swapped and reading is never
-    paused (the engine's receive window does the flow control)."""
+    read callback, and reading is never paused (the engine's receive window
+    does the flow control).  The reader is still installed as the transport's
+    protocol, so write-pause signals reach the serve budget."""
 
     def __init__(self, transport: asyncio.Transport, link, on_bytes) -> None:
-        self._tr = transport
-        self._old = None
-        self._link = link
-        self._on_data = on_bytes
-        self._msgs = []
-        self._waiter = None
-        self._exc = None
-        self._eof = False
-        self._paused = False
-        self._wpaused = False
-        self._reading = True
-        self._kick_scheduled = False
-        self._empty = b""
+        super().__init__(transport, link, on_bytes)
+        self._empty = b""           # on_bytes(b"") parses what the link already holds
 
     def deliver(self, data: bytes) -> None:
         if self._exc is None:
