@@ -501,3 +501,44 @@ def test_link_serve_budget_stalls_and_resumes(tmp_path):
     for (mid, pl), (i, off) in zip(served, reqs):
         assert mid == 7 and pl[:8] == struct.pack(">II", i, off)
         assert pl[8:] == data[i * (1 << 20) + off:i * (1 << 20) + off + B]
+
+
+def test_seeding_falls_back_to_python_when_the_native_source_fails(tmp_path, monkeypatch):
+    """If the serving Source cannot be built (e.g. no descriptors left for the
+    fd dups), the Torrent keeps its native links but answers REQUESTs in
+    Python; a download from it still completes."""
+    import asyncio
+    import types
+
+    from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+    from tritondl.fetch.bt import torrent as tmod
+    from tritondl.fetch.bt.client import TorrentDownloader
+    from tritondl.fetch.bt.torrent import TorrentConfig
+
+    class NoFds:
+        def __init__(self, *a):
+            pass
+
+        def add_file(self, *a):
+            raise RuntimeError("dup failed")
+
+        def close(self):
+            pass
+    shim = types.SimpleNamespace(PieceStore=W.PieceStore, Link=W.Link, Source=NoFds)
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 2_000_000})
+        info = torrent_for(str(src / "P"), 65536)
+        monkeypatch.setattr(tmod, "_W", shim)
+        seed = await Seeder(info, str(src)).start()
+        assert seed.torrent.source is None and seed.torrent.store is not None
+        d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1"), use_dht=False)
+        t, _ = await d.open(str(tmp_path / "dst"), magnet_for(info) + f"&x.pe=127.0.0.1:{seed.torrent.port}")
+        await asyncio.wait_for(t.got_info.wait(), 20)
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 30)
+        assert (tmp_path / "dst" / "P" / "a.bin").read_bytes() == (src / "P" / "a.bin").read_bytes()
+        await t.close()
+        await seed.stop()
+    asyncio.run(main())

@@ -345,11 +345,16 @@ class Torrent:
             n, pl, total = self.info.num_pieces, self.info.piece_length, self.info.total_length
             self.store = _W.PieceStore(n, pl, total)
             # the links answer block REQUESTs from the files themselves (own fd dups)
-            self.source = _W.Source(n, pl, total)
+            src = _W.Source(n, pl, total)
             st = self.storage
-            for fi, (_path, length) in enumerate(st.layout):
-                self.source.add_file(st.fd(fi), st.offsets[fi], length)
-            self.source.set_have_bits(bytes(self.have))
+            try:
+                for fi, (_path, length) in enumerate(st.layout):
+                    src.add_file(st.fd(fi), st.offsets[fi], length)
+                src.set_have_bits(bytes(self.have))
+                self.source = src
+            except RuntimeError as e:            # e.g. out of descriptors: serve from Python instead
+                src.close()
+                log.with_field("error", str(e)).warn("native serving unavailable; requests answered in Python")
             for p in list(self.peers.values()):
                 self._attach_link(p)
         self._downloading = True

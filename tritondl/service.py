@@ -452,9 +452,26 @@ class Service:
         await self.shutdown()
 
 
+def raise_nofile_limit() -> int:
+    """Lift the soft open-files limit to the hard one (as the Go runtime does
+    at start-up since 1.19): a multi-file torrent holds one descriptor per
+    file for storage and one for the native serving source, next to the
+    job's sockets.  Returns the soft limit now in force."""
+    try:
+        import resource
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        want = hard if hard != resource.RLIM_INFINITY else max(soft, 1 << 20)
+        if soft < want:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (want, hard))
+        return resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    except (ImportError, ValueError, OSError):
+        return -1
+
+
 def main(argv: list[str] | None = None) -> int:
     cfg = Config.from_env(argv=list(sys.argv[1:] if argv is None else argv))
     log.configure(cfg.log_level, cfg.log_format)
+    raise_nofile_limit()
     prof = CPUProfiler(cfg.cpuprofile)
     prof.start()
     try:
