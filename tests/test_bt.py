@@ -587,3 +587,32 @@ def test_interest_counters_track_the_bitmaps(tmp_path):
             t._recount_wants()
         for p in peers:
             assert p.wants == truth(p), step
+
+
+def test_storage_write_error_fails_the_job_instead_of_hanging(tmp_path, monkeypatch):
+    """A piece that cannot be written (disk full) ends the download with
+    TorrentError; the reference would block in WaitAll forever."""
+    import errno
+
+    from tritondl.fetch.bt.storage import FileStorage
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"a.mkv": 1_000_000})
+        info = torrent_for(str(src / "a.mkv"), 65536)
+        seed = await Seeder(info, str(src)).start()
+        real = FileStorage.write
+        calls = {"n": 0}
+
+        def flaky(self, piece, offset, data):
+            calls["n"] += 1
+            if calls["n"] > 3:
+                raise OSError(errno.ENOSPC, "No space left on device")
+            return real(self, piece, offset, data)
+        monkeypatch.setattr(FileStorage, "write", flaky)
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        with pytest.raises(TorrentError, match="storage failed"):
+            await asyncio.wait_for(_dl().download(str(dst), lambda u, p: None, magnet_for(info, peers=[seed.addr])), 30)
+        await seed.stop()
+    run(main())

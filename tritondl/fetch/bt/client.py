@@ -187,7 +187,15 @@ class TorrentDownloader:
 
             rep = asyncio.ensure_future(reporter())
             log.info("waiting for torrent download")
-            await t.complete.wait()
+            done = asyncio.ensure_future(t.complete.wait())
+            bad = asyncio.ensure_future(t.failed.wait())
+            try:
+                await asyncio.wait({done, bad}, return_when=asyncio.FIRST_COMPLETED)
+            finally:
+                for f in (done, bad):
+                    f.cancel()
+            if not t.complete.is_set():
+                raise TorrentError(f"torrent storage failed: {t.fatal}")
             progress(url, 100)
         finally:
             stop.set()

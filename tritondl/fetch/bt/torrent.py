@@ -182,6 +182,8 @@ class Torrent:
         self._my_ip: str | None = None                  # learned from our first connection
         self._prio: dict[tuple[str, int], int] = {}     # BEP 40 priority cache
         self.source = None                              # _btwire.Source: links serve REQUESTs from it
+        self.fatal: BaseException | None = None         # storage error that ends the download
+        self.failed = asyncio.Event()
         self._vq: list = []                             # (piece, data, peer) awaiting a verify partner
         self._vflush = False
         self.assigned: dict[int, set] = {}              # piece -> peer keys whose links fetch it
@@ -490,6 +492,9 @@ class Torrent:
             return ok
         try:
             ok = await asyncio.get_running_loop().run_in_executor(None, work)
+        except OSError as e:                  # the piece could not be written: the job cannot finish
+            self._fatal(e)
+            return
         finally:
             for i, _d, _s in batch:
                 self.verifying.discard(i)
@@ -506,6 +511,14 @@ class Torrent:
             self.verifying.discard(i)
         if ok is False:
             self._bad_piece(i, src)
+
+    def _fatal(self, e: BaseException) -> None:
+        """A storage error (disk full, I/O error): record it and wake whoever
+        waits on ``failed`` — the job fails instead of waiting forever."""
+        if self.fatal is None:
+            self.fatal = e
+            log.with_field("error", str(e)).error("torrent storage failed")
+        self.failed.set()
 
     def _bad_piece(self, i: int, src: _Peer) -> None:
         """Piece i from src failed its hash: count it against src (ban at the
@@ -1154,6 +1167,9 @@ class Torrent:
         self.verifying.add(i)
         try:
             ok = await loop.run_in_executor(None, verify_and_write)
+        except OSError as e:
+            self._fatal(e)
+            return None
         finally:
             self.verifying.discard(i)
         if not ok:
