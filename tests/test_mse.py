@@ -32,7 +32,7 @@ async def _pair(provide, allow_plain=True):
     async def on_conn(r, w):
         try:
             first = await r.readexactly(20)
-            rr, ww, sel = await mse.respond(r, w, first, skey, allow_plain=allow_plain)
+            rr, ww, sel = await mse.respond(r, w, first, skey, allow_plain=allow_plain, timeout=2.0)
             got["ia"] = await rr.readexactly(5)
             got["sel"] = sel
             ww.write(b"pong" * 1000)
@@ -46,7 +46,7 @@ async def _pair(provide, allow_plain=True):
     port = srv.sockets[0].getsockname()[1]
     r, w = await asyncio.open_connection("127.0.0.1", port)
     try:
-        rr, ww, sel = await mse.initiate(r, w, skey, b"hello", provide)
+        rr, ww, sel = await mse.initiate(r, w, skey, b"hello", provide, timeout=2.0)
         ww.write(b"world!")
         assert await rr.readexactly(4000) == b"pong" * 1000
         await asyncio.wait_for(done.wait(), 5)
