@@ -310,7 +310,10 @@ def test_take_over_resumes_a_transport_the_stream_reader_paused():
 
         srv = await asyncio.start_server(serve, "127.0.0.1", 0)
         r, w = await asyncio.open_connection("127.0.0.1", srv.sockets[0].getsockname()[1], limit=1 << 16)
-        await asyncio.sleep(0.2)                                 # buffer fills past 2*limit: paused
+        for _ in range(250):                                     # buffer fills past 2*limit: paused
+            if not w.transport.is_reading():
+                break
+            await asyncio.sleep(0.02)
         assert not w.transport.is_reading()
         wire = pw.Wire(r, w)
         link = W.Link(W.PieceStore(1, B, B), 4, False)
