@@ -460,6 +460,11 @@ def test_native_serving_backpressure_bounds_the_write_buffer(tmp_path):
         w.write(b"".join(struct.pack(">IBIII", 13, pw.REQUEST, i, off, B) for i, off in reqs))
         await w.drain()
         await asyncio.sleep(0.5)                                # seeder answers until its socket backs up
+        for _ in range(250):
+            peers = list(seed.peers.values())
+            if peers and peers[0].rx is not None:
+                break
+            await asyncio.sleep(0.02)
         (peer,) = list(seed.peers.values())
         assert peer.rx is not None
         buffered = peer.wire.writer.transport.get_write_buffer_size()
