@@ -9,7 +9,7 @@ PYTEST     := $(PYTHON) -m pytest
 
 all: build
 
-## build the in-tree native extensions (host C++, uTP, HIP gfx950 kernels)
+## build the in-tree native extensions (host C++ hashing + relay, BT peer wire, uTP, HIP gfx950 kernels)
 build:
 	PYTORCH_ROCM_ARCH=$(ROCM_ARCH) $(PYTHON) tools/build_native.py -v
 
