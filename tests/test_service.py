@@ -430,3 +430,34 @@ def test_failed_multipart_upload_resumes_on_retry(tmp_path):
         assert e.s3.object_bytes("triton-staging", object_key("mp-1", "pack.mkv")) == data
         await e.down()
     run(main())
+
+
+def test_wait_finished_wakes_on_result_and_times_out():
+    """Service.wait_finished is woken by the recorded result itself (the
+    bench harness waits on it instead of polling the workers' loop); the
+    count keeps growing when the recent-results list is trimmed."""
+    from tritondl.service import JobResult
+
+    async def main():
+        svc = Service(Config(bucket="b", s3_endpoint="http://127.0.0.1:1"))
+        w = asyncio.ensure_future(svc.wait_finished(2, timeout=5))
+        await asyncio.sleep(0)
+        svc._record(JobResult(True, "done"))
+        await asyncio.sleep(0)
+        assert not w.done()
+        svc._record(JobResult(True, "done"))
+        await asyncio.wait_for(w, 1)
+        assert svc.jobs_finished == 2 and not svc._finish_waiters
+        await svc.wait_finished(1)                     # already reached: returns at once
+        for _ in range(10001):
+            svc._record(JobResult(True, "done"))
+        assert len(svc.results) < svc.jobs_finished == 10003
+        try:
+            await svc.wait_finished(10004, timeout=0.05)
+        except TimeoutError as e:
+            assert "10003/10004" in str(e)
+        else:
+            raise AssertionError("no timeout")
+        assert not svc._finish_waiters
+
+    asyncio.run(main())

@@ -2,7 +2,7 @@
 # Round-2 closing measurements: GPU tests, smoke, headline x3 (http), https,
 # 8-worker pool, 2/4-rank shared broker (gloo), BT ingest + pack job, resume.
 set -o pipefail
-OUT=gpurun_out/r02_final
+OUT=${OUT:-gpurun_out/r02_final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&

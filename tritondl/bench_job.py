@@ -200,6 +200,7 @@ class JobStack:
         self.svc = Service(cfg, amqp=amqp, uploader=up)
         await self.svc.start()
         self.converts: list[Convert] = []
+        self._convert_waiter: tuple[int, asyncio.Future] | None = None
         if not producer:
             return
         self.producer = await Connection.open(broker_url, heartbeat=0)
@@ -210,6 +211,9 @@ class JobStack:
         def on_convert(m) -> None:
             self.converts.append(Convert.decode(m.body))
             asyncio.ensure_future(m.ack())
+            w = self._convert_waiter
+            if w is not None and len(self.converts) >= w[0] and not w[1].done():
+                w[1].set_result(None)
 
         # the worker declared v1.convert-{0,1} on its first publish; declare them here too
         for i in range(2):
@@ -248,20 +252,18 @@ class JobStack:
         return ids
 
     async def wait_done(self, total: int, timeout: float = 600) -> None:
+        """Wait (event-driven: no polling on the workers' loop) until the
+        worker has finished ``total`` jobs in all."""
         assert self.svc is not None
-        t0 = time.monotonic()
-        while len(self.svc.results) < total:
-            if time.monotonic() - t0 > timeout:
-                raise TimeoutError(f"only {len(self.svc.results)}/{total} jobs finished")
-            await asyncio.sleep(0.001)
+        await self.svc.wait_finished(total, timeout)
 
     async def run_jobs(self, n: int) -> float:
         """Submit n jobs and wait for all to finish on THIS worker; returns elapsed seconds."""
         assert self.svc is not None
-        base = len(self.svc.results)
+        base, start = len(self.svc.results), self.svc.jobs_finished
         t0 = time.perf_counter()
         await self.submit(n)
-        await self.wait_done(base + n)
+        await self.wait_done(start + n)
         dt = time.perf_counter() - t0
         bad = [r for r in self.svc.results[base:] if not r.ok or r.bytes != self.file_size]
         if bad:
@@ -274,11 +276,16 @@ class JobStack:
         rate's numerator)."""
         base = len(self.converts)
         t0 = time.perf_counter()
-        await self.submit(n)
-        while len(self.converts) < base + n:
-            if time.perf_counter() - t0 > timeout:
-                raise TimeoutError(f"only {len(self.converts) - base}/{n} converts")
-            await asyncio.sleep(0.001)
+        fut = asyncio.get_running_loop().create_future()
+        self._convert_waiter = (base + n, fut)
+        try:
+            await self.submit(n)
+            if len(self.converts) < base + n:
+                await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            raise TimeoutError(f"only {len(self.converts) - base}/{n} converts") from None
+        finally:
+            self._convert_waiter = None
         return time.perf_counter() - t0
 
     def cpu_seconds(self) -> dict:

@@ -107,7 +107,23 @@ class Service:
         self._inflight = 0
         self._metrics_runner = None
         self._cleanups: set[asyncio.Future] = set()
-        self.results: list[JobResult] = []
+        self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
+        self.jobs_finished = 0                     # monotonic count of results recorded
+        self._finish_waiters: list[tuple[int, asyncio.Future]] = []
+
+    async def wait_finished(self, total: int, timeout: float | None = None) -> None:
+        """Wait until ``jobs_finished >= total`` (woken by the result itself,
+        no polling of the event loop the jobs run on)."""
+        if self.jobs_finished >= total:
+            return
+        fut = asyncio.get_running_loop().create_future()
+        self._finish_waiters.append((total, fut))
+        try:
+            await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            raise TimeoutError(f"only {self.jobs_finished}/{total} jobs finished") from None
+        finally:
+            self._finish_waiters = [w for w in self._finish_waiters if w[1] is not fut]
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
@@ -382,6 +398,10 @@ class Service:
         self.results.append(r)
         if len(self.results) > 10000:
             del self.results[:5000]
+        self.jobs_finished += 1
+        for total, fut in self._finish_waiters:
+            if total <= self.jobs_finished and not fut.done():
+                fut.set_result(None)
         return r
 
     async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> None:
