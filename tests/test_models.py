@@ -82,3 +82,32 @@ def test_go_time_string_format():
     assert zone[0] in "+-" and len(zone) == 5
     assert mono == "m=+1.500000000"
     assert go_time_string(now_ns=1_600_000_000_000_000_000, mono_ns=0).split(" ")[1].count(".") == 0
+
+
+def test_field_numbers_operator_override():
+    """TRITONDL_MEDIA_FIELDS / TRITONDL_ENVELOPE_FIELDS remap the reconstructed
+    field numbers (parity unpinned): a message written with another numbering
+    decodes once the operator supplies it; media bytes still pass verbatim."""
+    import pytest
+
+    from tritondl.models import messages
+    # the producer's schema: source_uri=3, creator=7 (swapped), createdAt=4, media=5
+    media = (wire.enc_string(1, "m1") + wire.enc_string(3, "http://h/a.mkv") + wire.enc_varint_field(7, 1))
+    body = wire.enc_string(4, "t0") + wire.enc_bytes_always(5, media)
+    try:
+        d = Download.decode(body)
+        assert d.media is None and d.created_at == ""          # default numbering cannot read it
+        messages.configure_fields("source_uri=3,creator=7", "created_at=4,media=5")
+        d = Download.decode(body)
+        assert (d.created_at, d.media.id, d.media.source_uri, d.media.creator) == ("t0", "m1", "http://h/a.mkv", 1)
+        c = Convert.from_download(d, "now").encode()
+        assert wire.enc_bytes_always(5, media) in c and c.startswith(wire.enc_string(4, "now"))
+        assert Media.decode(Media(id="x", source_uri="u", creator=1).encode()).source_uri == "u"
+        for bad in ("nope=3", "id=0", "id=19000", "id=x", "id=2"):   # unknown, invalid, reserved, duplicate
+            with pytest.raises(ValueError):
+                messages.configure_fields(bad)
+        with pytest.raises(ValueError):
+            messages.configure_fields("", "media=1")
+    finally:
+        messages.configure_fields()
+    assert messages._MEDIA_STR[7] == "source_uri" and messages._ENV_FIELDS == {"created_at": 1, "media": 2}

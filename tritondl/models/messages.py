@@ -5,16 +5,22 @@ Used fields (reference): ``Download.Media.Id``, ``Download.Media.SourceURI``
 and ``Convert.Media = job.Media`` (``:136-139``); gogo ``proto.Marshal`` /
 ``Unmarshal`` (``:106,141``).
 
-TODO verify against tritonmedia.go v1.0.2 api.proto — the field numbers
-below are our best reconstruction (not available offline).  Robustness by
-construction: every message keeps its unknown fields and the raw bytes of
-``media`` so that ``Convert.media`` is re-emitted exactly as received.
+Parity unpinned: the field numbers below are a reconstruction of
+tritonmedia.go v1.0.2 ``api.proto`` (the schema is not vendored and not
+available offline, ``go.sum:272-273``).  Two safeguards: every message keeps
+its unknown fields and the raw bytes of ``media``, so ``Convert.media`` is
+re-emitted exactly as received; and the numbers are operator-overridable
+without a rebuild (``TRITONDL_MEDIA_FIELDS="id=1,source_uri=7"``,
+``TRITONDL_ENVELOPE_FIELDS="created_at=1,media=2"``; see
+:func:`configure_fields`).
 """
 
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 from enum import IntEnum
+
+import os
 
 from . import wire
 
@@ -55,6 +61,47 @@ class MediaStatus(IntEnum):
 
 _MEDIA_STR = {1: "id", 2: "name", 4: "creator_id", 7: "source_uri", 9: "metadata_id"}
 _MEDIA_INT = {3: "creator", 5: "type", 6: "source", 8: "metadata", 10: "status"}
+_ENV_FIELDS = {"created_at": 1, "media": 2}         # api.Download / api.Convert
+_DEFAULT_MEDIA = ({**_MEDIA_STR}, {**_MEDIA_INT})
+
+
+def _parse_spec(spec: str, names: set[str], what: str) -> dict[str, int]:
+    out: dict[str, int] = {}
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        name, sep, num = item.partition("=")
+        name = name.strip()
+        if not sep or name not in names:
+            raise ValueError(f"{what}: unknown field {name!r} (known: {', '.join(sorted(names))})")
+        try:
+            n = int(num)
+        except ValueError:
+            raise ValueError(f"{what}: field number for {name!r} is not an integer: {num!r}") from None
+        if not 1 <= n < (1 << 29) or 19000 <= n <= 19999:
+            raise ValueError(f"{what}: {n} is not a valid protobuf field number")
+        out[name] = n
+    return out
+
+
+def configure_fields(media: str = "", envelope: str = "") -> None:
+    """Override protobuf field numbers (``"name=N,..."``) for ``api.Media``
+    and the ``api.Download``/``api.Convert`` envelope; names not listed keep
+    their reconstructed number.  Numbers must stay unique per message.  Called
+    at import with ``TRITONDL_MEDIA_FIELDS`` / ``TRITONDL_ENVELOPE_FIELDS``;
+    ``configure_fields()`` restores the defaults."""
+    dstr, dint = _DEFAULT_MEDIA
+    by_name = {v: k for k, v in {**dstr, **dint}.items()}
+    by_name.update(_parse_spec(media, set(by_name), "TRITONDL_MEDIA_FIELDS"))
+    if len(set(by_name.values())) != len(by_name):
+        raise ValueError(f"TRITONDL_MEDIA_FIELDS: duplicate field numbers in {by_name}")
+    env = {"created_at": 1, "media": 2}
+    env.update(_parse_spec(envelope, set(env), "TRITONDL_ENVELOPE_FIELDS"))
+    if env["created_at"] == env["media"]:
+        raise ValueError("TRITONDL_ENVELOPE_FIELDS: created_at and media share a number")
+    _MEDIA_STR.clear()
+    _MEDIA_STR.update({by_name[name]: name for name in dstr.values()})
+    _MEDIA_INT.clear()
+    _MEDIA_INT.update({by_name[name]: name for name in dint.values()})
+    _ENV_FIELDS.update(env)
 
 
 @dataclass
@@ -93,7 +140,7 @@ class Media:
 
     def encode(self) -> bytes:
         out = bytearray()
-        for fn in range(1, 11):
+        for fn in sorted((*_MEDIA_STR, *_MEDIA_INT)):
             if fn in _MEDIA_STR:
                 out += wire.enc_string(fn, getattr(self, _MEDIA_STR[fn]))
             else:
@@ -123,13 +170,14 @@ class _Envelope:
     def decode(cls, buf: bytes):
         m = cls()
         unk = bytearray()
+        f_created, f_media = _ENV_FIELDS["created_at"], _ENV_FIELDS["media"]
         for fn, wt, val, raw in wire.iter_fields(buf):
-            if fn == 1 and wt == wire.LEN:
+            if fn == f_created and wt == wire.LEN:
                 try:
                     m.created_at = val.decode("utf-8")  # type: ignore[union-attr]
                 except UnicodeDecodeError as e:
                     raise wire.DecodeError("invalid utf-8 in createdAt") from e
-            elif fn == 2 and wt == wire.LEN:
+            elif fn == f_media and wt == wire.LEN:
                 # proto3 merge semantics for repeated occurrences: concatenate
                 m.media_raw = (m.media_raw or b"") + val  # type: ignore[operator]
                 m.media = Media.decode(m.media_raw)
@@ -139,11 +187,12 @@ class _Envelope:
         return m
 
     def encode(self) -> bytes:
-        out = bytearray(wire.enc_string(1, self.created_at))
+        f_created, f_media = _ENV_FIELDS["created_at"], _ENV_FIELDS["media"]
+        out = bytearray(wire.enc_string(f_created, self.created_at))
         if self.media_raw is not None:
-            out += wire.enc_bytes_always(2, self.media_raw)
+            out += wire.enc_bytes_always(f_media, self.media_raw)
         elif self.media is not None:
-            out += wire.enc_bytes_always(2, self.media.encode())
+            out += wire.enc_bytes_always(f_media, self.media.encode())
         out += self.unknown
         return bytes(out)
 
@@ -164,3 +213,6 @@ class Convert(_Envelope):
         c.media = job.media
         c.media_raw = job.media_raw
         return c
+
+
+configure_fields(os.environ.get("TRITONDL_MEDIA_FIELDS", ""), os.environ.get("TRITONDL_ENVELOPE_FIELDS", ""))
