@@ -156,13 +156,12 @@ async def job_bench(a) -> int:
         for rep in range(a.repeat):
             for on in modes:
                 cfg.stream_upload = on
-                n0 = len(svc.results)
+                n0 = svc.jobs_finished
                 body = Download(created_at="now", media=Media(id=f"pack-{rep}-{int(on)}", source=SourceType.TORRENT,
                                                               source_uri=magnet)).encode()
                 t0 = time.perf_counter()
                 await ch.basic_publish("v1.download", "v1.download-0", body, Properties(delivery_mode=2))
-                while len(svc.results) == n0:
-                    await asyncio.sleep(0.002)
+                await svc.wait_finished(n0 + 1, timeout=600)
                 dt = time.perf_counter() - t0
                 r = svc.results[-1]
                 assert r.ok and r.files == a.files and r.bytes == per * a.files, r
