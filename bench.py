@@ -176,7 +176,7 @@ def main() -> int:
                 loop.run_until_complete(phase(a.warmup))
             else:
                 loop.run_until_complete(stack.run_jobs(a.warmup))
-        base = len(stack.svc.results)  # type: ignore[union-attr]
+        start = stack.svc.jobs_finished  # type: ignore[union-attr]
         barrier()
         cpu0 = stack.cpu_seconds()
         t0 = time.perf_counter()
@@ -189,7 +189,9 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         cpu1 = stack.cpu_seconds()
         barrier()
-        done = stack.svc.results[base:]  # type: ignore[union-attr]
+        n_done = stack.svc.jobs_finished - start  # type: ignore[union-attr]
+        # latency/span stats over the recent-results window (trimmed past 10,000)
+        done = stack.svc.results[-n_done:] if n_done else []  # type: ignore[union-attr]
         failed = len(stack.failures())
         lat = sorted(r.seconds for r in done)
         spans: dict[str, list[float]] = {}
@@ -206,12 +208,12 @@ def main() -> int:
     max_elapsed = float(t[0].item())
     if int(t[1].item()):
         raise SystemExit(f"{int(t[1].item())} jobs failed on some rank")
-    per_rank = [len(done)]
+    per_rank = [n_done]
     cpu = {k: cpu1[k] - cpu0[k] for k in cpu0}
     cpu_all = [cpu]
     if world > 1:
         per_rank = [None] * world  # type: ignore[list-item]
-        dist.all_gather_object(per_rank, len(done), group=ctl)
+        dist.all_gather_object(per_rank, n_done, group=ctl)
         cpu_all = [None] * world  # type: ignore[list-item]
         dist.all_gather_object(cpu_all, cpu, group=ctl)
     extra = {} if (a.no_gpu_probe or rank != 0) else _gpu_hash_probe()
