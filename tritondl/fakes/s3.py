@@ -69,8 +69,10 @@ def _xml_err(status: int, code: str, msg: str, region: str = "") -> web.Response
 class FakeS3:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, *, access_key: str | None = None,
                  secret_key: str | None = None, region: str = "us-east-1", store: str = "memory",
-                 root: str | None = None, tls: tuple[str, str] | None = None, strict_parts: bool = True) -> None:
+                 root: str | None = None, tls: tuple[str, str] | None = None, strict_parts: bool = True,
+                 names: tuple[str, ...] = ()) -> None:
         self.host, self.port = host, port
+        self.names = set(names)        # other names of the service endpoint (path-style, not a bucket)
         self.tls = tls
         self.strict_parts = strict_parts
         self.bucket_regions: dict[str, str] = {}
@@ -138,7 +140,7 @@ class FakeS3:
         raw = request.raw_path.split("?", 1)[0]
         host = request.headers.get("Host", "").split(":")[0]
         if host.count(".") and not re.match(r"^\d+\.\d+\.\d+\.\d+$", host) and host not in ("localhost",) \
-                and not host.startswith(self.host):
+                and not host.startswith(self.host) and host not in self.names:
             bucket = host.split(".", 1)[0]
             return bucket, unquote(raw[1:])
         parts = raw[1:].split("/", 1)

@@ -74,6 +74,7 @@ class TorrentDownloader:
     @classmethod
     def from_config(cls, c, http=None) -> "TorrentDownloader":
         tc = TorrentConfig(listen_port=c.bt_listen_port, utp=c.bt_utp, pex=c.bt_pex, encryption=c.bt_encryption,
+                           established_conns=c.bt_established_conns, half_open_conns=c.bt_half_open_conns,
                            verify_device={"on": "gpu", "off": "cpu"}.get(c.gpu_verify, c.gpu_verify),
                            upnp=c.bt_upnp, native_wire=c.bt_native_wire,
                            disk_reserve=c.disk_reserve_bytes,
@@ -85,10 +86,17 @@ class TorrentDownloader:
         return ClientRegister(name="torrent", protocols=["magnet"], file_extensions=[".torrent"])
 
     async def _fetch_torrent_file(self, url: str) -> bytes:
+        from ...utils import proxy as _proxy
         own = self._http is None
         s = self._http or aiohttp.ClientSession()
         try:
-            async with s.get(url, timeout=aiohttp.ClientTimeout(total=120)) as r:
+            # a .torrent URL is an ordinary web fetch: it honours the egress proxy
+            # (HTTP_PROXY / HTTPS_PROXY / NO_PROXY) like the HTTP downloader
+            try:
+                kw, extra = _proxy.aiohttp_kwargs(_proxy.proxy_for(url), url.startswith("https:"))
+            except (_proxy.ProxyConfigError, ValueError) as e:
+                raise TorrentError(f"failed to fetch torrent file: {e}") from e
+            async with s.get(url, timeout=aiohttp.ClientTimeout(total=120), headers=extra, **kw) as r:
                 if r.status != 200:
                     raise TorrentError(f"failed to fetch torrent file: HTTP {r.status}")
                 cap = 64 * 1024 * 1024          # v2 piece layers make big torrents large

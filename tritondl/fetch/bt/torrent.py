@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import errno
 import functools
 import hashlib
 import heapq
@@ -54,10 +55,14 @@ except ImportError:  # pragma: no cover - the extension ships with every build
 
 @dataclass
 class TorrentConfig:
-    max_peers: int = 60
+    # anacrolix NewDefaultClientConfig (torrent.go:40): EstablishedConnsPerTorrent 50,
+    # HalfOpenConnsPerTorrent 25 — peers with a finished handshake, and dials in flight
+    established_conns: int = 50
+    half_open_conns: int = 25
     pipeline: int = 128
     listen_host: str = "0.0.0.0"
-    listen_port: int = 0
+    listen_port: int = 0             # 0 = ephemeral (the worker's Config passes anacrolix's 42069)
+    listen_port_fallback: bool = True  # listen_port busy (another torrent / worker has it): use an ephemeral one
     announce_host: str | None = None
     seed: bool = False
     request_timeout: float = 20.0
@@ -223,7 +228,16 @@ class Torrent:
         return t
 
     async def start(self) -> None:
-        self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
+        try:
+            self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
+        except OSError as e:
+            # anacrolix fails NewClient on a busy port; here one worker process can run
+            # several torrents (and a node several workers), so the later ones take an
+            # ephemeral port instead (announced to trackers / the DHT as usual)
+            if not (self.cfg.listen_port and self.cfg.listen_port_fallback and e.errno == errno.EADDRINUSE):
+                raise
+            log.with_fields(port=self.cfg.listen_port).info("bittorrent listen port busy; using an ephemeral port")
+            self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, 0)
         self.port = self._server.sockets[0].getsockname()[1]
         if self.cfg.listen_host6 is not None:
             # dual stack like anacrolix: the same port on IPv6, so peers learnt from the
@@ -662,7 +676,7 @@ class Torrent:
             if not self.closed and a not in self.banned and a[1] > 0 and \
                     not (a[1] == self.port and a[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host)):
                 self.known.add(a)
-        free = self.cfg.max_peers - len(self.peers) - len(self.connecting)
+        free = self._dial_slots()
         if free > 0:
             for a in self._best_candidates(free):
                 self.add_peer_addr(a)
@@ -675,9 +689,16 @@ class Torrent:
         if addr[1] == self.port and addr[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host):
             return
         self.known.add(addr)
-        if len(self.peers) + len(self.connecting) < self.cfg.max_peers:
+        if self._dial_slots() > 0:
             self.connecting.add(addr)
             self._spawn(self._connect(addr))
+
+    def _dial_slots(self) -> int:
+        """Dials that may start now: half-open connections are capped at
+        ``half_open_conns`` and established + half-open at ``established_conns``
+        (anacrolix ``HalfOpenConnsPerTorrent`` / ``EstablishedConnsPerTorrent``)."""
+        return min(self.cfg.half_open_conns - len(self.connecting),
+                   self.cfg.established_conns - len(self.peers) - len(self.connecting))
 
     async def _tracker_loop(self, url: str) -> None:
         event = "started"
@@ -811,7 +832,8 @@ class Torrent:
         await self._run_peer(reader, writer, addr, hs, inbound=True)
 
     async def _run_peer(self, reader, writer, addr, hs: pw.Handshake, inbound: bool = True) -> None:
-        if not self._accepts(hs.infohash) or hs.peer_id == self.peer_id or addr in self.peers or self.closed:
+        if not self._accepts(hs.infohash) or hs.peer_id == self.peer_id or addr in self.peers or self.closed or \
+                (inbound and len(self.peers) >= self.cfg.established_conns):
             writer.close()
             return
         n = self.info.num_pieces if self.info else 0

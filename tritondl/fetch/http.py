@@ -52,6 +52,7 @@ from urllib.parse import unquote, urlparse
 import aiohttp
 from yarl import URL
 
+from ..utils import proxy as _proxy
 from ..utils import rawhttp
 from ..utils.disk import DiskSpaceError, check_space
 from ..utils.log import log
@@ -135,8 +136,10 @@ class HTTPDownloader:
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
                  ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
-                 disk_reserve: int = 0) -> None:
+                 disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None) -> None:
         self.progress_interval = progress_interval
+        # egress proxy (HTTP_PROXY / HTTPS_PROXY / NO_PROXY, Go semantics); None = the environment
+        self.proxies = proxies
         self.disk_reserve = disk_reserve            # bytes to keep free (utils.disk preflight)
         self.max_redirects = max_redirects          # Go's http.Client default (grab uses it)
         # >0: instead of `segments` contiguous slices, the file is cut into stripes of
@@ -208,6 +211,33 @@ class HTTPDownloader:
             return None
         return rawhttp.relay_module()
 
+    def _proxy(self, url: str) -> "_proxy.ProxyURL | None":
+        """The egress proxy for ``url`` (grab's transport: ``ProxyFromEnvironment``)."""
+        try:
+            return (self.proxies or _proxy.from_environment()).proxy_for(url)
+        except _proxy.ProxyConfigError as e:
+            raise HTTPDownloadError(f"GET {url}: {e}") from e
+
+    def _aio_proxy(self, url: str, headers: dict) -> dict:
+        """aiohttp request kwargs (``headers`` included) routing ``url``
+        through its proxy."""
+        try:
+            kw, extra = _proxy.aiohttp_kwargs(self._proxy(url), url.startswith("https:"))
+        except ValueError as e:
+            raise _FatalHTTPError(f"GET {url}: {e}") from e
+        return {**kw, "headers": {**headers, **extra}}
+
+    async def _aio_get(self, url: str, headers: dict):
+        """aiohttp GET through the egress proxy; a proxy that refuses us
+        (407/403 on CONNECT) fails the job instead of being retried."""
+        s = await self._sess()
+        try:
+            return await s.get(url, allow_redirects=True, **self._aio_proxy(url, headers))
+        except aiohttp.ClientHttpProxyError as e:
+            if e.status in (401, 403, 407):
+                raise _FatalHTTPError(f"GET {url}: proxy refused the tunnel: {e.status} {e.message}") from e
+            raise
+
     async def _open(self, url: str, headers: dict):
         """GET ``url``: a :class:`_RawResponse` on the native path (plain
         http, identity body, no redirect), else an open aiohttp response."""
@@ -215,8 +245,11 @@ class HTTPDownloader:
             r = await self._raw_get(url, headers)
             if r is not None:
                 return r
-        s = await self._sess()
-        return await s.get(url, headers=headers, allow_redirects=True)
+        r = await self._aio_get(url, headers)
+        if r.status == 407:
+            r.release()
+            raise _FatalHTTPError(f"GET {url}: proxy authentication required (407)")
+        return r
 
     async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":
         """Native GET.  Redirects (301/302/303/307/308, relative or absolute,
@@ -228,8 +261,12 @@ class HTTPDownloader:
             secure = u.scheme == "https"
             dport = 443 if secure else 80
             host, port = u.raw_host or "", u.port or dport
-            target = u.raw_path_qs or "/"
-            hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers}
+            px = self._proxy(url)
+            if not rawhttp.native_proxy_ok(px, secure):
+                return None
+            target = rawhttp.request_target(u, px, secure)
+            hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers,
+                  **rawhttp.proxy_auth_header(px)}
             head = rawhttp.request_head("GET", target, hh)
             tls = self._tls_ctx() if secure else None
             if secure and tls is None:
@@ -237,7 +274,11 @@ class HTTPDownloader:
             h = conn = None
             for _ in range(2):                # a stale pooled keep-alive connection gets one fresh retry
                 try:
-                    conn, reused = await self._raw.connect(host, port, timeout=30.0, tls=tls)
+                    conn, reused = await self._raw.connect(
+                        host, port, timeout=30.0, tls=tls, proxy=px,
+                        proxy_tls=self._tls_ctx() if px is not None and px.scheme == "https" else None)
+                except rawhttp.ProxyRefused as e:
+                    raise _FatalHTTPError(f"GET {url}: {e}") from e
                 except (OSError, rawhttp.RawHTTPError) as e:
                     raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
                 try:
@@ -255,6 +296,10 @@ class HTTPDownloader:
                     raise
             if h is None:
                 raise aiohttp.ClientConnectionError(f"GET {url}: connection reset")
+            if h.status == 407 and rawhttp.absolute_form(px):
+                conn.close()
+                raise _FatalHTTPError(f"GET {url}: proxy {px.redacted()} requires authentication: "
+                                      f"407 {h.reason}")
             loc = h.headers.get("Location")
             if h.status in (301, 302, 303, 307, 308) and loc:
                 conn.close()                  # small redirect body: not worth draining for keep-alive
@@ -273,13 +318,15 @@ class HTTPDownloader:
     async def _probe(self, url: str) -> _Probe:
         s = await self._sess()
         try:
-            async with s.head(url, headers=self.headers, allow_redirects=True) as r:
+            async with s.head(url, allow_redirects=True, **self._aio_proxy(url, self.headers)) as r:
                 if r.status < 400:
                     return self._probe_from(r, url)
         except aiohttp.ClientError:
             pass
         # HEAD unsupported: probe with a 1-byte ranged GET
-        async with s.get(url, headers={**self.headers, "Range": "bytes=0-0"}, allow_redirects=True) as r:
+        async with await self._aio_get(url, {**self.headers, "Range": "bytes=0-0"}) as r:
+            if r.status == 407:
+                raise _FatalHTTPError(f"GET {url}: proxy authentication required (407)")
             if r.status >= 400:
                 raise HTTPDownloadError(f"GET {url}: HTTP {r.status}")
             p = self._probe_from(r, url)
@@ -459,6 +506,7 @@ class HTTPDownloader:
         if probe.size is None:
             os.truncate(h.part, total)
         os.replace(h.part, h.dst)
+        _set_remote_time(h.dst, probe.last_modified)
         try:
             os.remove(meta_path)
         except FileNotFoundError:
@@ -745,6 +793,19 @@ class DownloadHandle:
             self.flow.cancel()             # stops native pumps blocked on this download
         if self.task is not None and not self.task.done():
             self.task.cancel()
+
+
+def _set_remote_time(path: str, last_modified: str) -> None:
+    """grab's ``setLastModified`` (``IgnoreRemoteTime`` is false by default):
+    a parseable ``Last-Modified`` becomes the file's atime and mtime."""
+    if not last_modified:
+        return
+    from email.utils import parsedate_to_datetime
+    try:
+        t = parsedate_to_datetime(last_modified).timestamp()
+        os.utime(path, (t, t))
+    except (TypeError, ValueError, OverflowError, OSError):
+        pass
 
 
 def _pwritev_all(fd: int, bufs: list[bytes], pos: int) -> None:

@@ -26,8 +26,9 @@ class WorkerSpec:
     bt_listen_port: int = 0
 
     def env(self) -> dict[str, str]:
-        e = {"RANK": str(self.rank), "LOCAL_RANK": str(self.local_rank), "WORLD_SIZE": str(self.world_size),
-             "TRITONDL_BT_LISTEN_PORT": str(self.bt_listen_port)}
+        e = {"RANK": str(self.rank), "LOCAL_RANK": str(self.local_rank), "WORLD_SIZE": str(self.world_size)}
+        if self.bt_listen_port:         # else the worker default (42069, busy → ephemeral)
+            e["TRITONDL_BT_LISTEN_PORT"] = str(self.bt_listen_port)
         if self.gpu is not None:
             e["HIP_VISIBLE_DEVICES"] = str(self.gpu)
         else:

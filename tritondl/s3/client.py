@@ -41,6 +41,7 @@ from yarl import URL
 
 from ..ops import hashing
 from ..utils.backoff import ExponentialBackoff
+from ..utils import proxy as _proxy
 from ..utils import rawhttp
 from ..utils.log import log
 from . import sigv4
@@ -84,6 +85,13 @@ def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Err
         code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
                 resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
     return S3Error(status, code, msg, resource, region)
+
+
+def _proxy_auth_error(px, resource: str, status: int = 407, detail: str = "") -> S3Error:
+    """A proxy that refuses this client: not retried (another try cannot pass)."""
+    who = px.redacted() if px is not None else "the proxy"
+    return S3Error(status, "ProxyAuthenticationRequired" if status == 407 else "ProxyRefused",
+                   detail or f"{who} refused the request ({status})", resource)
 
 
 def _save_json(path: str, obj: dict) -> None:
@@ -159,8 +167,11 @@ class S3Client:
                  lookup: str = "auto", payload_mode: str = "auto", part_size: int = 64 << 20,
                  multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
                  io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
-                 native: bool = True, sign_threads: int = 4, ca_pem: str = "", ca_file: str = "") -> None:
+                 native: bool = True, sign_threads: int = 4, ca_pem: str = "", ca_file: str = "",
+                 proxies: "_proxy.ProxyConfig | None" = None) -> None:
         self.ep = Endpoint.parse(endpoint) if isinstance(endpoint, str) else endpoint
+        # egress proxy (minio-go's DefaultTransport: ProxyFromEnvironment); None = the environment
+        self.proxies = proxies
         self.creds = creds or default_chain()
         self.region = region            # "" = discover each bucket's region (minio-go without Region)
         self._regions: dict[str, str] = {}
@@ -189,9 +200,10 @@ class S3Client:
         ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
         return ctx
 
-    def _tls_ctx(self):
-        """Native client TLS context for the relay pumps (None for plain http)."""
-        if not self.ep.secure:
+    def _tls_ctx(self, force: bool = False):
+        """Native client TLS context for the relay pumps (None for plain http
+        unless ``force``: an https proxy in front of a plain endpoint)."""
+        if not (self.ep.secure or force):
             return None
         if self._ntls is None:
             relay = rawhttp.relay_module()
@@ -244,6 +256,24 @@ class S3Client:
 
     def _creds(self) -> Value:
         return self.creds.retrieve()
+
+    def _proxy(self, host: str) -> "_proxy.ProxyURL | None":
+        """The egress proxy for requests to ``host`` (the endpoint, or a
+        virtual-host bucket name under it), chosen as Go's
+        ``ProxyFromEnvironment`` chooses it for minio-go's request URL."""
+        url = f"{'https' if self.ep.secure else 'http'}://{host}/"
+        try:
+            return (self.proxies or _proxy.from_environment()).proxy_for(url)
+        except _proxy.ProxyConfigError as e:
+            raise S3Error(0, "ProxyConfig", str(e), host) from e
+
+    def _aio_proxy(self, host: str, headers: dict) -> dict:
+        """aiohttp request kwargs (``headers`` included) through the proxy of ``host``."""
+        try:
+            kw, extra = _proxy.aiohttp_kwargs(self._proxy(host), self.ep.secure)
+        except ValueError as e:
+            raise S3Error(0, "ProxyUnsupported", str(e), host) from e
+        return {**kw, "headers": {**headers, **extra}}
 
     # ------------------------------------------------------------ regions
     async def bucket_region(self, bucket: str) -> str:
@@ -333,11 +363,13 @@ class S3Client:
             try:
                 sess = await self._sess()
                 payload = data.stream() if hasattr(data, "stream") else data
-                async with sess.request(method, url, headers=send_headers, data=payload,
-                                        skip_auto_headers=("Content-Type",), allow_redirects=False) as r:
+                async with sess.request(method, url, data=payload, skip_auto_headers=("Content-Type",),
+                                        allow_redirects=False, **self._aio_proxy(host, send_headers)) as r:
                     rbody = await r.read()
                     if r.status in expect:
                         return r.status, CIMultiDict(r.headers), rbody
+                    if r.status == 407:
+                        raise _proxy_auth_error(self._proxy(host), f"{method} {path}")
                     err = _parse_error(r.status, rbody, f"{method} {path}", r.headers)
                     if region is None and region_hops < 2 and self._learn_region(bucket, err, sreg):
                         region_hops += 1
@@ -345,6 +377,12 @@ class S3Client:
                         continue
                     if r.status < 500 or not retry or attempt > self.max_retries:
                         raise err
+            except aiohttp.ClientHttpProxyError as e:
+                if e.status in (401, 403, 407):
+                    raise _proxy_auth_error(self._proxy(host), f"{method} {path}", e.status) from e
+                if not retry or attempt > self.max_retries:
+                    raise S3Error(0, "ProxyError", str(e), f"{method} {path}") from e
+                err = e  # type: ignore[assignment]
             except (aiohttp.ClientError, asyncio.TimeoutError, ConnectionError) as e:
                 if not retry or attempt > self.max_retries:
                     raise S3Error(0, "ConnectionError", str(e), f"{method} {path}") from e
@@ -406,6 +444,9 @@ class S3Client:
                          headers: dict, query: dict | None = None, wait_bytes=None, flow=None) -> str:
         mode = self._payload_mode()
         relay = rawhttp.relay_module() if self.native else None
+        if relay is not None and not rawhttp.native_proxy_ok(self._proxy(self._target(bucket, key)[0]),
+                                                             self.ep.secure):
+            relay = None                     # TLS inside an https proxy: aiohttp
         if relay is not None and mode in ("streaming", "unsigned") and \
                 not isinstance(src, (bytes, bytearray, memoryview)) and (flow is not None or wait_bytes is None):
             return await self._put_native(relay, bucket, key, src, offset, length, headers, query, mode, flow)
@@ -574,13 +615,22 @@ class S3Client:
                                         cred.secret_access_key, sreg, amzdate, path_is_encoded=True)
                     hdrs["authorization"] = signed.authorization
                 target = path + (("?" + sigv4.canonical_query(query)) if query else "")
-                send = {"Host": host, **{k: v for k, v in hdrs.items() if k != "host"}}
+                px = self._proxy(host)
+                if rawhttp.absolute_form(px) and not self.ep.secure:
+                    target = f"http://{host}{target}"
+                send = {"Host": host, **{k: v for k, v in hdrs.items() if k != "host"},
+                        **rawhttp.proxy_auth_header(px)}
                 head = rawhttp.request_head("PUT", target, send)
                 chost, cport = rawhttp.split_host(host, 443 if self.ep.secure else 80)
                 err: Exception | None = None
                 conn = None
                 try:
-                    conn, reused = await self._raw.connect(chost, cport, tls=self._tls_ctx())
+                    try:
+                        conn, reused = await self._raw.connect(
+                            chost, cport, tls=self._tls_ctx(), proxy=px,
+                            proxy_tls=self._tls_ctx(True) if px is not None and px.scheme == "https" else None)
+                    except rawhttp.ProxyRefused as e:
+                        raise _proxy_auth_error(px, f"PUT {path}", e.status or 407, str(e)) from e
                     rawhttp.trace("put_pump_start")
                     sent, _last, perr = await rawhttp.run_pump(
                         conn, relay.send_body, head, fd, offset, length, flow,
@@ -605,6 +655,8 @@ class S3Client:
                             self._raw.release(chost, cport, conn)
                             conn = None
                         return resp.headers.get("ETag", "").strip('"')
+                    if resp.status == 407 and px is not None:
+                        raise _proxy_auth_error(px, f"PUT {path}")
                     err = _parse_error(resp.status, body, f"PUT {path}", resp.headers)
                     if region_hops < 2 and self._learn_region(bucket, err, sreg):
                         region_hops += 1

@@ -50,7 +50,7 @@ class Config:
     rabbitmq_username: str = ""
     rabbitmq_password: str = ""
     rabbitmq_vhost: str = "/"
-    heartbeat_s: int = 30
+    heartbeat_s: int = 10                       # streadway amqp.Dial's defaultHeartbeat (client.go:309)
 
     # --- topology (hard-coded in the reference) ---
     consume_topic: str = "v1.download"          # downloader.go:68
@@ -80,15 +80,24 @@ class Config:
     progress_interval_s: float = 1.0            # http.go:45, torrent.go:83
     progress_log_interval_s: float = 5.0        # downloader.go:115
     metadata_timeout_s: float = 600.0           # torrent.go:67
-    bt_listen_port: int = 0                     # 0 = ephemeral
+    # anacrolix NewDefaultClientConfig defaults (torrent.go:40): ListenPort 42069 (busy →
+    # an ephemeral port, see TorrentConfig.listen_port_fallback; 0 = always ephemeral),
+    # EstablishedConnsPerTorrent 50, HalfOpenConnsPerTorrent 25
+    bt_listen_port: int = 42069
+    bt_established_conns: int = 50
+    bt_half_open_conns: int = 25
     bt_dht: bool = True
     bt_upnp: bool = True                        # UPnP IGD port forwarding of the listen port (anacrolix default)
     bt_native_wire: bool = True                 # per-block peer-wire work in csrc/btwire (False: pure Python)
     bt_dht_ipv6: bool = True                    # BEP 32 dual-stack DHT (anacrolix default); IPv4-only if no IPv6
     bt_utp: bool = True
     bt_pex: bool = True
-    bt_encryption: str = "allow"                # MSE/PE: disable | allow | prefer | require
-    bt_bootstrap: str = "router.bittorrent.com:6881,dht.transmissionbt.com:6881"
+    # MSE/PE: disable | allow | prefer | require; anacrolix HeaderObfuscationPolicy{Preferred: true,
+    # RequirePreferred: false} = "prefer" (obfuscated first, plaintext accepted)
+    bt_encryption: str = "prefer"
+    # dht.GlobalBootstrapAddrs (anacrolix/dht v2), in its order
+    bt_bootstrap: str = ("router.utorrent.com:6881,router.bittorrent.com:6881,dht.transmissionbt.com:6881,"
+                         "dht.aelitis.com:6881,router.silotis.us:6881,dht.libtorrent.org:25401")
     gpu_verify: str = "auto"                    # auto|on|off|hybrid (HIP batch piece hashing; hybrid = GPU + SHA-NI threads)
     gpu_warmup_timeout_s: float = 120.0         # start-up wait for the HIP hasher before consuming
 
@@ -151,7 +160,8 @@ class Config:
                 "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
                 "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
                 "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
-                "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes"}
+                "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
+                "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",

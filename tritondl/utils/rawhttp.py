@@ -62,6 +62,40 @@ class RawHTTPError(ConnectionError):
     pass
 
 
+class ProxyError(RawHTTPError):
+    """The egress proxy could not be reached or could not open the tunnel
+    (transient: 502/503/504 from CONNECT, a connect failure)."""
+
+
+class ProxyRefused(ProxyError):
+    """The proxy refused this client (407 / 403 on CONNECT, SOCKS auth or rule
+    refusal): retrying cannot help, so callers fail the job at once."""
+
+    def __init__(self, msg: str, status: int = 0) -> None:
+        super().__init__(msg)
+        self.status = status
+
+
+def absolute_form(proxy) -> bool:
+    """Requests go to an http(s) proxy in absolute form (``GET http://h/p``)
+    for plain-http targets; https targets and socks5 use a tunnel."""
+    return proxy is not None and proxy.scheme in ("http", "https")
+
+
+def request_target(url, proxy, secure: bool) -> str:
+    """Request-line target of ``url`` (a yarl URL): origin form, or absolute
+    form when it goes through an http(s) proxy without a tunnel."""
+    if not secure and absolute_form(proxy):
+        return str(url.with_fragment(None))
+    return url.raw_path_qs or "/"
+
+
+def native_proxy_ok(proxy, secure: bool) -> bool:
+    """False for TLS inside TLS (an https target through an https proxy),
+    which the native streams do not do; callers use aiohttp then."""
+    return not (secure and proxy is not None and proxy.scheme == "https")
+
+
 @dataclass
 class Head:
     status: int
@@ -250,49 +284,75 @@ class RawConn:
 
 @dataclass
 class Pool:
-    """Idle keep-alive connections by (host, port, tls)."""
+    """Idle keep-alive connections by (host, port, tls) — or, through an
+    egress proxy, by (proxy) for absolute-form requests and by (proxy,
+    host, port, tls) for tunnels."""
     max_idle: int = 16
     idle: dict = field(default_factory=dict)
 
     async def connect(self, host: str, port: int, timeout: float = 30.0, tls=None,
-                      server_hostname: str | None = None) -> tuple[RawConn, bool]:
+                      server_hostname: str | None = None, proxy=None, proxy_tls=None) -> tuple[RawConn, bool]:
         """(connection, reused).  ``tls``: a ``_relay.TlsContext`` (client) for
-        https.  A pooled connection the peer has closed is dropped."""
-        key = (host, port, id(tls) if tls is not None else 0)
+        https.  A pooled connection the peer has closed is dropped.
+
+        ``proxy`` (a :class:`~tritondl.utils.proxy.ProxyURL`): for a plain-http
+        target through an http(s) proxy the connection goes to the proxy (the
+        caller sends absolute-form requests with :func:`proxy_auth_header`);
+        for an https target the proxy is asked to ``CONNECT host:port`` and
+        TLS runs inside the tunnel; ``socks5`` opens a SOCKS tunnel either way.
+        ``proxy_tls``: the client context for an ``https://`` proxy (Go uses
+        the transport's TLS config, i.e. the same trust as for targets;
+        default: the shared system-store context).
+        """
+        tid = id(tls) if tls is not None else 0
+        if proxy is None:
+            key: tuple = (host, port, tid)
+        elif tls is None and absolute_form(proxy):
+            key = ("proxy",) + proxy.key
+        else:
+            key = ("tunnel",) + proxy.key + (host, port, tid)
         lst = self.idle.get(key)
         while lst:
             c = lst.pop()
             if c.alive():
                 return c, True
             c.close()
-        loop = asyncio.get_running_loop()
-        infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
-        err: Exception | None = None
-        for fam, typ, proto, _cn, addr in infos:
-            s = socket.socket(fam, typ, proto)
-            s.setblocking(False)
+        if proxy is None:
+            s = await _dial(host, port, timeout)
+        else:
             try:
-                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                await asyncio.wait_for(loop.sock_connect(s, addr), timeout)
-            except (OSError, asyncio.TimeoutError) as e:
-                s.close()
-                err = e
-                continue
+                s = await _dial(proxy.host, proxy.port, timeout)
+            except RawHTTPError as e:
+                raise ProxyError(f"proxyconnect tcp: {proxy.redacted()}: {e}") from e
+        try:
+            if proxy is not None and proxy.scheme == "https":
+                if tls is not None:
+                    raise ProxyError("TLS inside an https proxy tunnel is not supported natively")
+                c = RawConn(s, relay_module().TlsConn(proxy_tls or client_tls_context(), s.fileno(), proxy.host,
+                                                     f"{proxy.host}:{proxy.port}"))
+                await c.handshake(timeout)
+                c.pool_key = key
+                return c, False
+            if proxy is not None and proxy.scheme == "socks5":
+                await _socks5_connect(RawConn(s), proxy, host, port, timeout)
+            elif proxy is not None and tls is not None:
+                await _http_connect(RawConn(s), proxy, host, port, timeout)
             if tls is None:
                 c = RawConn(s)
                 c.pool_key = key
                 return c, False
-            relay = relay_module()
-            try:
-                t = relay.TlsConn(tls, s.fileno(), server_hostname or host, f"{host}:{port}")
-                c = RawConn(s, t)
-                await c.handshake(timeout)
-            except BaseException:
-                s.close()
-                raise
-            c.pool_key = key
-            return c, False
-        raise RawHTTPError(f"connect {host}:{port}: {err}")
+            t = relay_module().TlsConn(tls, s.fileno(), server_hostname or host, f"{host}:{port}")
+            c = RawConn(s, t)
+            await c.handshake(timeout)
+        except asyncio.TimeoutError as e:
+            s.close()
+            raise (ProxyError if proxy is not None else RawHTTPError)(
+                f"connect {_hostport(host, port)}: timed out") from e
+        except BaseException:
+            s.close()
+            raise
+        c.pool_key = key
+        return c, False
 
     def release(self, host: str, port: int, c: RawConn) -> None:
         key = getattr(c, "pool_key", None) or (host, port, 0)
@@ -307,6 +367,122 @@ class Pool:
             for c in lst:
                 c.close()
         self.idle.clear()
+
+
+async def _dial(host: str, port: int, timeout: float) -> socket.socket:
+    """A connected non-blocking TCP socket (first address that answers)."""
+    loop = asyncio.get_running_loop()
+    try:
+        infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
+    except OSError as e:
+        raise RawHTTPError(f"connect {host}:{port}: {e}") from e
+    err: Exception | None = None
+    for fam, typ, proto, _cn, addr in infos:
+        s = socket.socket(fam, typ, proto)
+        s.setblocking(False)
+        try:
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            await asyncio.wait_for(loop.sock_connect(s, addr), timeout)
+        except (OSError, asyncio.TimeoutError) as e:
+            s.close()
+            err = e
+            continue
+        except BaseException:
+            s.close()
+            raise
+        return s
+    raise RawHTTPError(f"connect {host}:{port}: {err}")
+
+
+def _hostport(host: str, port: int) -> str:
+    return f"[{host}]:{port}" if ":" in host else f"{host}:{port}"
+
+
+def proxy_auth_header(proxy) -> dict:
+    """``{"Proxy-Authorization": ...}`` for absolute-form requests through an
+    http(s) proxy with credentials, else {}."""
+    if not absolute_form(proxy):
+        return {}
+    a = proxy.authorization()
+    return {"Proxy-Authorization": a} if a else {}
+
+
+async def _http_connect(c: RawConn, proxy, host: str, port: int, timeout: float) -> None:
+    """``CONNECT host:port`` through an http proxy (Go's Transport: any
+    status but 200 fails the dial with the status text)."""
+    hp = _hostport(host, port)
+    hdrs = {"Host": hp}
+    if proxy.authorization():
+        hdrs["Proxy-Authorization"] = proxy.authorization()
+    await c.sendall(request_head("CONNECT", hp, hdrs), timeout)
+    try:
+        h = await read_head(c, timeout)
+    except RawHTTPError as e:
+        raise ProxyError(f"proxy {proxy.redacted()}: CONNECT {hp}: {e}") from e
+    if h.status != 200:
+        msg = f"proxy {proxy.redacted()} refused CONNECT {hp}: {h.status} {h.reason}"
+        if h.status in (401, 403, 407):
+            raise ProxyRefused(msg, h.status)
+        raise ProxyError(msg)
+    if h.leftover:
+        raise ProxyError(f"proxy {proxy.redacted()}: data after the CONNECT reply")
+
+
+async def _recv_exact(c: RawConn, n: int, timeout: float) -> bytes:
+    buf = b""
+    while len(buf) < n:
+        d = await c.recv(n - len(buf), timeout)
+        if not d:
+            raise ProxyError("socks5 proxy closed the connection")
+        buf += d
+    return buf
+
+
+_SOCKS_REPLIES = {1: "general failure", 2: "connection not allowed by ruleset", 3: "network unreachable",
+                  4: "host unreachable", 5: "connection refused", 6: "TTL expired", 7: "command not supported",
+                  8: "address type not supported"}
+
+
+async def _socks5_connect(c: RawConn, proxy, host: str, port: int, timeout: float) -> None:
+    """RFC 1928 CONNECT (RFC 1929 username/password when the proxy URL has
+    userinfo — the methods Go's socks dialer offers); the target name is
+    resolved by the proxy unless it is an IP literal."""
+    import ipaddress
+    import struct
+    methods = b"\x00\x02" if proxy.username is not None else b"\x00"
+    try:
+        await c.sendall(b"\x05" + bytes([len(methods)]) + methods, timeout)
+        ver, meth = await _recv_exact(c, 2, timeout)
+        if ver != 5:
+            raise ProxyError(f"socks5 proxy {proxy.redacted()}: unexpected protocol version {ver}")
+        if meth == 0xFF:
+            raise ProxyRefused(f"socks5 proxy {proxy.redacted()}: no acceptable authentication methods")
+        if meth == 2:
+            u, p = (proxy.username or "").encode(), (proxy.password or "").encode()
+            await c.sendall(b"\x01" + bytes([len(u)]) + u + bytes([len(p)]) + p, timeout)
+            _v, st = await _recv_exact(c, 2, timeout)
+            if st != 0:
+                raise ProxyRefused(f"socks5 proxy {proxy.redacted()}: username/password authentication failed")
+        elif meth != 0:
+            raise ProxyError(f"socks5 proxy {proxy.redacted()}: unsupported method {meth}")
+        try:
+            ip = ipaddress.ip_address(host)
+            addr = (b"\x01" if ip.version == 4 else b"\x04") + ip.packed
+        except ValueError:
+            name = host.encode("idna")
+            addr = b"\x03" + bytes([len(name)]) + name
+        await c.sendall(b"\x05\x01\x00" + addr + struct.pack(">H", port), timeout)
+        _v, rep, _r, atyp = await _recv_exact(c, 4, timeout)
+        if rep != 0:
+            msg = f"socks5 proxy {proxy.redacted()}: connect {_hostport(host, port)}: " \
+                  f"{_SOCKS_REPLIES.get(rep, f'reply {rep}')}"
+            raise (ProxyRefused(msg) if rep == 2 else ProxyError(msg))
+        alen = {1: 4, 4: 16}.get(atyp)
+        if alen is None:
+            alen = (await _recv_exact(c, 1, timeout))[0]
+        await _recv_exact(c, alen + 2, timeout)
+    except asyncio.TimeoutError as e:
+        raise ProxyError(f"socks5 proxy {proxy.redacted()}: handshake timed out") from e
 
 
 _active_pumps = 0
