@@ -142,6 +142,7 @@ PYBIND11_MODULE(_btwire, m) {
       .def_property_readonly("outstanding", &Link::outstanding)
       .def_property("peer_choking", &Link::peer_choking, &Link::set_peer_choking)
       .def_property_readonly("downloaded", &Link::downloaded)
+      .def_property_readonly("wasted", &Link::wasted, "bytes of unrequested PIECE messages (dropped)")
       .def("set_source", &Link::set_source)
       .def_property("serving", &Link::serving, &Link::set_serving)
       .def_property_readonly("uploaded", &Link::uploaded)

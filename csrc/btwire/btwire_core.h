@@ -14,6 +14,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -348,11 +349,23 @@ class Link {
           break;
         }
         const uint32_t i = be32(pl), off = be32(pl + 4);
-        out_req_.erase(key(i, off / kBlock));
         if (i >= store_->num_pieces()) {
           ev->push_back(Event::bad("piece index out of range"));
           bad = true;
           break;
+        }
+        if (off % kBlock) {
+          ev->push_back(Event::bad("bad block geometry"));
+          bad = true;
+          break;
+        }
+        const uint64_t k = key(i, off / kBlock);
+        if (!out_req_.erase(k) && !recent_.erase(k)) {
+          // never asked of this link (nor recently withdrawn from it): a peer
+          // pushing blocks could poison pieces other links are filling, and
+          // the hash failure would be blamed on whoever completed the piece
+          wasted_ += pn - 8;
+          continue;
         }
         const int r = store_->put(i, off, pl + 8, pn - 8);
         if (r < 0) {
@@ -372,6 +385,7 @@ class Link {
       } else if (id == kReject && pn >= 12) {
         const uint32_t i = be32(pl), off = be32(pl + 4);
         if (out_req_.erase(key(i, off / kBlock))) redo_.push_back(key(i, off / kBlock));
+        recent_.erase(key(i, off / kBlock));
       } else if (id == kRequest && source_ && pn >= 12) {
         serve(be32(pl), be32(pl + 4), be32(pl + 8), out);
       } else if (id == kCancel && source_ && pn >= 12) {
@@ -429,9 +443,14 @@ class Link {
   }
   // Everything this link had asked for goes back to the pool (timeout / snub).
   void lapse_all() {
-    for (auto& kv : out_req_) redo_.push_back(kv.first);
+    for (auto& kv : out_req_) {
+      redo_.push_back(kv.first);
+      withdrew(kv.first);
+    }
     out_req_.clear();
   }
+  // Bytes of PIECE messages this link never requested (dropped, not stored).
+  uint64_t wasted() const { return wasted_; }
   bool peer_choking() const { return peer_choking_; }
   void set_peer_choking(bool c) { peer_choking_ = c; }
   uint64_t downloaded() const { return downloaded_; }
@@ -456,6 +475,7 @@ class Link {
     for (auto r = out_req_.begin(); r != out_req_.end();) {
       if (uint32_t(r->first >> 32) == i) {
         if (cancel) cancels_.push_back(r->first);
+        withdrew(r->first);
         r = out_req_.erase(r);
       } else {
         ++r;
@@ -486,6 +506,17 @@ class Link {
       }
     }
     if (!ok && fast_) msg3(*out, kReject, i, off, n);
+  }
+
+  // A request taken back (lapsed, or cancelled because another link finished
+  // the piece): the block may still be in flight, so it stays acceptable.
+  // Bounded FIFO, so a peer cannot grow it.
+  void withdrew(uint64_t k) {
+    if (recent_.insert(k).second) recent_fifo_.push_back(k);
+    while (recent_fifo_.size() > kRecent) {
+      recent_.erase(recent_fifo_.front());
+      recent_fifo_.pop_front();
+    }
   }
 
   void msg3(std::string& out, uint8_t id, uint32_t i, uint32_t off, uint32_t n) {
@@ -546,7 +577,10 @@ class Link {
   std::unordered_map<uint64_t, Clock::time_point> out_req_;
   std::deque<uint64_t> redo_;                             // lapsed / rejected blocks to ask for again
   std::vector<uint64_t> cancels_;
-  uint64_t downloaded_ = 0;
+  static constexpr size_t kRecent = 2048;
+  std::unordered_set<uint64_t> recent_;                   // withdrawn requests still acceptable
+  std::deque<uint64_t> recent_fifo_;                      // their order, for the bound
+  uint64_t downloaded_ = 0, wasted_ = 0;
 };
 
 }  // namespace tritondl_btwire

@@ -380,30 +380,39 @@ static void test_btwire(unsigned seed, int rounds) {
     auto store = std::make_shared<PieceStore>(npieces, plen, total);
     Link link(store, 16, true);
     for (uint32_t i = 0; i < npieces; ++i) link.assign(i);
+    // a well-behaved peer: it answers exactly the REQUESTs the link sends
+    // (unrequested blocks are dropped by design), with HAVEs and keep-alives
+    // mixed in, and the stream arrives in random cuts through both receive paths
     std::string stream = bt_msg(kUnchoke, "");
-    for (uint32_t i = 0; i < npieces; ++i) {
-      const uint64_t ps = store->piece_size(i);
-      for (uint64_t off = 0; off < ps; off += kBlock) {
-        const uint64_t n = std::min<uint64_t>(kBlock, ps - off);
-        stream += bt_msg(kPiece, be32s(i) + be32s(uint32_t(off)) + content.substr(i * plen + off, n));
-        if (rng() % 3 == 0) stream += bt_msg(4, be32s(i));  // HAVE
-        if (rng() % 5 == 0) stream += std::string(4, '\0');  // keep-alive
-      }
-    }
     std::vector<Event> ev;
     std::string out;
-    size_t pos = 0;
-    while (pos < stream.size()) {
-      const size_t cut = std::min<size_t>(stream.size() - pos, 1 + rng() % 40000);
+    auto answer = [&](const std::string& o) {
+      size_t p = 0;
+      while (p + 4 <= o.size()) {
+        const uint32_t ml = be32(reinterpret_cast<const uint8_t*>(o.data() + p));
+        if (ml == 13 && uint8_t(o[p + 4]) == kRequest) {
+          const uint8_t* q = reinterpret_cast<const uint8_t*>(o.data() + p + 5);
+          const uint32_t i = be32(q), off = be32(q + 4), n = be32(q + 8);
+          stream += bt_msg(kPiece, be32s(i) + be32s(off) + content.substr(i * plen + off, n));
+          if (rng() % 3 == 0) stream += bt_msg(4, be32s(i));  // HAVE
+          if (rng() % 5 == 0) stream += std::string(4, '\0');  // keep-alive
+        }
+        p += 4 + ml;
+      }
+    };
+    while (!stream.empty()) {
+      const size_t cut = std::min<size_t>(stream.size(), 1 + rng() % 40000);
       if (rng() % 2) {
         auto span = link.recv_buffer(cut);
         CHECK(span.second >= cut);
-        std::memcpy(span.first, stream.data() + pos, cut);
+        std::memcpy(span.first, stream.data(), cut);
         link.feed_n(cut, &ev, &out);
       } else {
-        link.feed(reinterpret_cast<const uint8_t*>(stream.data() + pos), cut, &ev, &out);
+        link.feed(reinterpret_cast<const uint8_t*>(stream.data()), cut, &ev, &out);
       }
-      pos += cut;
+      stream.erase(0, cut);
+      answer(out);
+      out.clear();
     }
     uint32_t done = 0;
     for (const Event& e : ev) {

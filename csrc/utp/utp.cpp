@@ -257,6 +257,7 @@ PYBIND11_MODULE(_utp, m) {
         d["retransmits"] = s.retransmits;
         d["timeouts"] = s.timeouts;
         d["fast_retransmits"] = s.fast_retransmits;
+        d["window_full_drops"] = s.window_full_drops;
         d["addr"] = s.addr;
         return d;
       })

@@ -157,6 +157,7 @@ struct Conn {
   bool in_batch = false;                // touched in the current receive batch
   // stats
   uint64_t bytes_sent = 0, bytes_recv = 0, retransmits = 0, timeouts = 0, fast_retransmits = 0;
+  uint64_t window_full_drops = 0;       // in-order packets dropped: the app's unread bytes filled the window
 };
 
 class Engine {
@@ -310,7 +311,11 @@ class Engine {
   std::string read(int id) {
     Conn* c = get(id);
     std::string out;
-    if (c) out.swap(c->inbuf);
+    if (!c) return out;
+    // a read that reopens a window we had advertised as (nearly) closed sends a
+    // window update at the next flush, so the sender does not wait for a timeout
+    if (c->inbuf.size() + 2 * kMss > kRecvWindow) c->need_ack = true;
+    out.swap(c->inbuf);
     return out;
   }
 
@@ -415,6 +420,7 @@ class Engine {
     double cwnd = 0;
     uint32_t inflight = 0, our_delay_us = 0;
     uint64_t bytes_sent = 0, bytes_recv = 0, retransmits = 0, timeouts = 0, fast_retransmits = 0;
+    uint64_t window_full_drops = 0;
     std::string addr;
   };
 
@@ -433,6 +439,7 @@ class Engine {
     s.retransmits = c->retransmits;
     s.timeouts = c->timeouts;
     s.fast_retransmits = c->fast_retransmits;
+    s.window_full_drops = c->window_full_drops;
     s.addr = c->addr;
     return s;
   }
@@ -635,6 +642,14 @@ class Engine {
       return;
     }
     if (!fin) {
+      if (c.inbuf.size() + payload_n > kRecvWindow + kMss) {
+        // the app stopped reading (it is backed up) and the window we advertised
+        // is used up: drop the packet unacked; the sender retries after the window
+        // update that the next read() sends.  The bytes held for a paused reader
+        // therefore stay bounded by the window.
+        c.window_full_drops++;
+        return;
+      }
       c.inbuf.append(payload, payload_n);
       c.bytes_recv += payload_n;
     }

@@ -90,6 +90,30 @@ def test_endgame_two_links_share_the_store_and_cancel():
     assert list(ev) == []
 
 
+def test_unrequested_blocks_are_dropped_not_stored():
+    """A peer pushing blocks nobody asked it for cannot write into pieces other
+    links are filling; blocks of requests withdrawn lately (lapsed, or
+    cancelled because another link finished the piece) are still taken."""
+    store = W.PieceStore(2, 2 * B, 4 * B)
+    honest, pusher = W.Link(store, 2), W.Link(store, 2)
+    honest.assign(0)
+    honest.peer_choking = False
+    assert len(msgs(honest.pump())) == 2                   # honest asked for piece 0's two blocks
+    ev, _ = pusher.feed(piece_msg(0, 0, b"E" * B) + piece_msg(0, B, b"E" * B))
+    assert list(ev) == [] and pusher.wasted == 2 * B and store.received(0) == 0
+    ev, _ = honest.feed(piece_msg(0, 0, b"g" * B) + piece_msg(0, B, b"g" * B))
+    assert list(ev) == [("piece", 0)] and bytes(store.take(0)) == b"g" * 2 * B
+    late = W.Link(store, 4, False)
+    late.assign(1)
+    late.peer_choking = False
+    late.pump()
+    late.feed(b"\x00\x00\x00\x01\x00")                     # CHOKE: both requests lapse
+    ev, _ = late.feed(piece_msg(1, 0, b"a" * B))           # ... but a block already in flight is kept
+    assert late.wasted == 0 and store.received(1) == 1
+    ev, _ = late.feed(piece_msg(1, 0, b"a" * B))           # the same block again: not asked any more
+    assert late.wasted == B
+
+
 def test_forwarded_messages_and_protocol_errors():
     store = W.PieceStore(2, B, 2 * B)
     link = W.Link(store, 4)
@@ -481,6 +505,67 @@ def test_native_serving_backpressure_bounds_the_write_buffer(tmp_path):
         w.close()
         await seed.close()
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_native_serving_backpressure_over_utp(tmp_path):
+    """The same over uTP: the seeder's uTP reader stops taking bytes while its
+    send side is backed up (they stay in the engine, whose advertised window
+    closes), so the served replies stay bounded; the leecher's own reader is
+    flow-controlled the same way (pause_reading on the uTP transport)."""
+    import asyncio
+
+    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl.fetch.bt import peer as pw
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+    from tritondl.fetch.bt.utp import UtpSocket
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src / "P"), {"a.bin": 8 << 20})
+        info = torrent_for(str(src / "P"), 1 << 20)
+        payload = (src / "P" / "a.bin").read_bytes()
+        seed = Torrent(info.infohash, str(src), TorrentConfig(listen_host="127.0.0.1", seed=True, verify_device="cpu",
+                                                              utp=True, encryption="disable"), info=info)
+        await seed.start()
+        await seed.download_all()
+        cli = await UtpSocket().start("127.0.0.1", 0)
+        r, w = await cli.connect("127.0.0.1", seed.port)
+        w.write(pw.encode_handshake(info.infohash, b"-BPTEST-" + bytes(12)))
+        await pw.read_handshake(r)
+        w.transport.pause_reading()                            # the leecher stops reading: its window closes
+        reqs = [(i, off) for _rep in range(4) for i in range(8) for off in range(0, 1 << 20, B)]
+        for _ in range(250):
+            peers = list(seed.peers.values())
+            if peers and peers[0].rx is not None:
+                break
+            await asyncio.sleep(0.02)
+        (peer,) = list(seed.peers.values())
+        assert peer.rx is not None
+        # the REQUESTs trickle in (keep-alives in between): every delivery is a new
+        # chance to serve, so only a paused reader keeps the replies bounded
+        for k in range(0, len(reqs), 64):
+            w.write(b"".join(struct.pack(">IBIII", 13, pw.REQUEST, i, off, B) for i, off in reqs[k:k + 64]))
+            w.write(b"\x00\x00\x00\x00")
+            await asyncio.sleep(0.01)
+        await asyncio.sleep(0.5)
+        buffered = peer.wire.writer.transport.get_write_buffer_size()
+        assert buffered < (16 << 20), buffered                  # 32 MiB were requested
+        assert peer.link.uploaded < (24 << 20)                  # the rest waits, unparsed, in the engine
+        assert len(r._buffer) < (2 << 20)                       # the paused leecher holds ~ one window
+        w.transport.resume_reading()
+        got = 0
+        while got < len(reqs):                                   # now read everything back
+            (n,) = struct.unpack(">I", await asyncio.wait_for(r.readexactly(4), 20))
+            body = await asyncio.wait_for(r.readexactly(n), 20)
+            if body[:1] != bytes([pw.PIECE]):
+                continue
+            i, off = struct.unpack(">II", body[1:9])
+            assert body[9:] == payload[i * (1 << 20) + off:i * (1 << 20) + off + B]
+            got += 1
+        w.close()
+        cli.close()
+        await seed.close()
+    asyncio.run(asyncio.wait_for(main(), 90))
 
 
 def test_link_serve_budget_stalls_and_resumes(tmp_path):

@@ -240,3 +240,23 @@ def test_worker_keeps_one_warm_dht_node_across_jobs(tmp_path):
         assert dl._dht is None and not nodes[0].families
         net.stop()
     run(main(), timeout=120)
+
+
+def test_announce_store_is_bounded_and_purged():
+    """A long-running worker's DHT server: announces for ever more info-hashes
+    evict the least recently announced one (libtorrent dht_max_torrents), and
+    the maintenance purge drops expired peers and emptied info-hashes."""
+    import time as _time
+    n = D.DHTNode(max_torrents=3, max_peers_per_torrent=2, peer_ttl=0.05)
+    ih = [bytes([i]) * 20 for i in range(5)]
+    for h in ih[:3]:
+        n._store_peer(h, ("10.0.0.1", 1))
+    n._store_peer(ih[0], ("10.0.0.2", 2))          # re-announced: now the most recent
+    n._store_peer(ih[3], ("10.0.0.3", 3))          # evicts ih[1], the least recent
+    assert list(n.peers) == [ih[2], ih[0], ih[3]]
+    for p in range(5):
+        n._store_peer(ih[3], ("10.0.1.1", 100 + p))
+    assert list(n.peers[ih[3]]) == [("10.0.1.1", 103), ("10.0.1.1", 104)]
+    _time.sleep(0.06)
+    n._store_peer(ih[4], ("10.0.0.9", 9))          # evicts ih[2]; fresh
+    assert n.purge_peers() == 2 and list(n.peers) == [ih[4]]

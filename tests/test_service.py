@@ -173,6 +173,41 @@ def test_failed_job_retried_then_dead_lettered(tmp_path):
     run(main())
 
 
+def test_failed_retry_publish_still_settles_the_delivery(tmp_path, monkeypatch):
+    """A retry that cannot be scheduled (e.g. the delay queue's declare is
+    refused) falls back to the dead-letter queue; if that publish fails too,
+    the delivery is nacked with requeue.  Either way the prefetch-1 slot is
+    freed, so the consumer never stalls."""
+    from tritondl.amqp import client as amqp_client
+
+    async def no_retry(self, delay=None):
+        raise RuntimeError("PRECONDITION_FAILED - inequivalent arg 'x-message-ttl'")
+    monkeypatch.setattr(amqp_client.Delivery, "retry", no_retry)
+    real_publish = amqp_client.Client.publish
+    fails = {"n": 1}
+
+    async def flaky_publish(self, topic, body, *a, **kw):
+        if topic.endswith(".dead") and fails["n"]:
+            fails["n"] -= 1
+            raise RuntimeError("publish nacked")
+        return await real_publish(self, topic, body, *a, **kw)
+    monkeypatch.setattr(amqp_client.Client, "publish", flaky_publish)
+
+    async def main():
+        e = await Env().up(tmp_path, max_retries=3)
+        e.submit(Media(id="x", source_uri="ftp://h/a.zip"))
+        res = await e.wait_results(2)               # requeued once, handled again
+        assert [r.ok for r in res] == [False, False]
+        await asyncio.sleep(0.05)
+        dead = _dlq(e.broker)
+        assert len(dead) == 1 and e.broker.unacked_count() == 0
+        assert e.svc.metrics.get("jobs_requeued") == 1
+        e.submit(Media(id="y", source_uri="ftp://h/b.zip"))   # the consumer still takes jobs
+        await e.wait_results(3)
+        await e.down()
+    run(main())
+
+
 def test_unsupported_scheme_dead_lettered(tmp_path):
     async def main():
         e = await Env().up(tmp_path, max_retries=0)

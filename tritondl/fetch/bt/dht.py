@@ -264,8 +264,15 @@ class DHTNode:
                  bootstrap: list[tuple[str, int]] | None = None, timeout: float = 2.0, *,
                  host6: str | None = None, port6: int = 0, k: int = K, alpha: int = ALPHA,
                  stale_after: float = 900.0, refresh_after: float = 900.0, token_rotate: float = 300.0,
-                 peer_ttl: float = 1800.0, max_lookup_queries: int = 400, lookup_width: int = 0) -> None:
+                 peer_ttl: float = 1800.0, max_lookup_queries: int = 400, lookup_width: int = 0,
+                 max_torrents: int = 2000, max_peers_per_torrent: int = 2000) -> None:
         self.id = node_id or hashlib.sha1(os.urandom(20)).digest()
+        # announce_peer store bounds (libtorrent dht_max_torrents / dht_max_peers): the
+        # least recently announced info-hash is evicted first, and expired peers and
+        # empty info-hashes are purged by the maintenance loop, so a long-running
+        # worker's DHT memory stays bounded whatever announces it receives
+        self.max_torrents = max_torrents
+        self.max_peers_per_torrent = max_peers_per_torrent
         self.host, self.port = host, port
         self.host6, self.port6 = host6, port6
         self.bootstrap_nodes = list(bootstrap or [])
@@ -485,14 +492,43 @@ class DHTNode:
             if not isinstance(port, int) or not 0 < port < 65536:
                 self._send({b"t": t, b"y": b"e", b"e": [203, b"bad port"]}, addr)
                 return
-            store = self.peers.setdefault(ih, {})
-            store[(_norm_host(addr[0]), int(port))] = time.monotonic()
-            if len(store) > 2000:
-                del store[min(store, key=store.__getitem__)]
+            self._store_peer(ih, (_norm_host(addr[0]), int(port)))
         else:
             self._send({b"t": t, b"y": b"e", b"e": [204, b"method unknown"]}, addr)
             return
         self._send({b"t": t, b"y": b"r", b"r": r}, addr)
+
+    def _store_peer(self, ih: bytes, peer: tuple[str, int]) -> None:
+        """Record an announce.  ``self.peers`` is kept in announce order (an
+        info-hash moves to the end on every announce), so the first key is the
+        least recently announced one — evicted when the store is full."""
+        store = self.peers.pop(ih, None)
+        if store is None:
+            store = {}
+            while len(self.peers) >= self.max_torrents:
+                del self.peers[next(iter(self.peers))]
+        self.peers[ih] = store
+        store.pop(peer, None)
+        store[peer] = time.monotonic()          # dict order == announce order
+        while len(store) > self.max_peers_per_torrent:
+            del store[next(iter(store))]
+
+    def purge_peers(self) -> int:
+        """Drop expired announces and info-hashes left with none; returns how
+        many info-hashes were removed."""
+        cutoff = time.monotonic() - self.peer_ttl
+        gone = 0
+        for ih in list(self.peers):
+            store = self.peers[ih]
+            while store:
+                first = next(iter(store))
+                if store[first] >= cutoff:
+                    break                       # announce order: the rest are newer
+                del store[first]
+            if not store:
+                del self.peers[ih]
+                gone += 1
+        return gone
 
     def _live_peers(self, ih: bytes) -> list[tuple[str, int]]:
         store = self.peers.get(ih)
@@ -596,6 +632,7 @@ class DHTNode:
         period = max(1.0, min(60.0, self.refresh_after / 4))
         while True:
             await asyncio.sleep(period)
+            self.purge_peers()
             try:
                 await self.refresh()
             except Exception as e:  # noqa: BLE001 - maintenance must not die

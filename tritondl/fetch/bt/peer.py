@@ -403,9 +403,10 @@ class LinkReader(asyncio.BufferedProtocol):
 class UtpLinkReader(LinkReader):
     """:class:`LinkReader` for a uTP stream: the uTP engine's delivered bytes
     come in through :meth:`deliver` (the stream's sink) instead of a socket
-    read callback, and reading is never paused (the engine's receive window
-    does the flow control).  The reader is still installed as the transport's
-    protocol, so write-pause signals reach the serve budget."""
+    read callback.  Pausing works as on TCP: while the send side is backed up
+    (or the peer loop is behind) the transport stops handing over bytes, they
+    stay in the engine and its advertised receive window closes — so a peer
+    pipelining REQUESTs cannot make the served PIECE replies pile up."""
 
     def __init__(self, transport: asyncio.Transport, link, on_bytes) -> None:
         super().__init__(transport, link, on_bytes)
@@ -418,9 +419,6 @@ class UtpLinkReader(LinkReader):
     def eof(self) -> None:
         self._eof = True
         self._wake()
-
-    def _update_reading(self) -> None:
-        pass
 
 
 def parse_ext_handshake(payload: bytes) -> ExtHandshake:

@@ -141,6 +141,15 @@ class _Peer:
         self.link = None                                    # _btwire.Link once the native data plane runs
         self.rx: pw.LinkReader | None = None                # zero-copy receive into the link (plain TCP)
         self.rx_tried = False
+        # requests withdrawn (lapsed / cancelled) lately: a block that answers one is
+        # still accepted; a block matching neither this nor `outstanding` is dropped
+        self.recent: dict[tuple[int, int], int] = {}
+        self.wasted = 0
+
+    def withdrew(self, k: tuple[int, int]) -> None:
+        self.recent[k] = 1
+        if len(self.recent) > 1024:
+            del self.recent[next(iter(self.recent))]
 
     def set_have(self, i: int) -> bool:
         if 0 <= i < len(self.have) and not self.have[i]:
@@ -215,6 +224,7 @@ class Torrent:
         self.portfwd = None
         self._uploaded = 0                              # Python-served bytes + links of dropped peers
         self.downloaded = 0
+        self.wasted = 0                                 # unrequested block bytes dropped (Python wire)
         self.closed = False
         self._wake = asyncio.Event()
         if info is not None:
@@ -1117,7 +1127,8 @@ class Torrent:
             p.wire.request(i, off, n)
 
     def _unrequest(self, p: _Peer, i: int, off: int) -> None:
-        p.outstanding.pop((i, off), None)
+        if p.outstanding.pop((i, off), None) is not None:
+            p.withdrew((i, off))
         pc = self.pieces.get(i)
         if pc is not None and pc.lapse(off // BLOCK, p.key):
             self.open_pieces[i] = pc
@@ -1125,7 +1136,13 @@ class Torrent:
     async def _on_block(self, p: _Peer, pl: bytes) -> None:
         i, off = struct.unpack(">II", pl[:8])
         data = pl[8:]
-        p.outstanding.pop((i, off), None)
+        if p.outstanding.pop((i, off), None) is None and not p.recent.pop((i, off), 0):
+            # never asked of this peer (nor recently withdrawn): a peer pushing blocks
+            # could poison pieces other peers are filling, so the bytes are dropped
+            p.wasted += len(data)
+            self.wasted += len(data)
+            self._fill(p)
+            return
         pc = self.pieces.get(i)
         if pc is None or self.info is None or self.have[i]:
             self._fill(p)
@@ -1143,6 +1160,7 @@ class Torrent:
                 q = self.peers.get(other)
                 if q is not None and q is not p and (i, off) in q.outstanding:
                     q.outstanding.pop((i, off), None)
+                    q.withdrew((i, off))
                     q.wire.cancel(i, off, len(data))
         else:
             pc.requested.pop(b, None)

@@ -94,6 +94,21 @@ class _UtpTransport(asyncio.Transport):
                 self._paused = False
                 self._protocol.resume_writing()
 
+    def pause_reading(self) -> None:
+        """Leave delivered bytes in the engine: its advertised receive window
+        closes as they pile up, so the peer stops sending (real backpressure,
+        not an unbounded buffer on our side)."""
+        self.stream.paused = True
+
+    def resume_reading(self) -> None:
+        if self.stream.paused:
+            self.stream.paused = False
+            self.sock._service(self.cid)       # hand over what waited (and reopen the window)
+            self.sock._flush()
+
+    def is_reading(self) -> bool:
+        return not self.stream.paused
+
     def can_write_eof(self) -> bool:
         return False
 
@@ -134,6 +149,7 @@ class _Stream:
         # the engine delivers go straight to it instead of the StreamReader
         self.sink: Callable[[bytes], None] | None = None
         self.sink_eof: Callable[[], None] | None = None
+        self.paused = False        # the reader is backed up: bytes stay in the engine
 
 
 class UtpSocket:
@@ -228,6 +244,9 @@ class UtpSocket:
         st = self.engine.state(cid)
         if st >= _utp.CONNECTED and not s.connected.is_set() and st != _utp.RESET:
             s.connected.set()
+        if s.paused and st != _utp.RESET:
+            s.transport._push()           # keep sending; receive resumes on resume_reading()
+            return
         data = self.engine.read(cid)
         if data:
             if s.sink is not None:

@@ -416,13 +416,15 @@ class Service:
                 self.metrics.inc("jobs_retried")
                 return
         except Exception as e:  # noqa: BLE001
-            log.with_field("error", str(e)).error("failed to schedule retry; broker will redeliver")
-            return
+            # e.g. the delay queue's declare refused (PRECONDITION_FAILED): the
+            # delivery must still be settled, or a prefetch-1 consumer stalls (B4)
+            log.with_field("error", str(e)).error("failed to schedule retry; dead-lettering the job")
         await self._dead_letter(msg, stage, err)
 
     async def _dead_letter(self, msg: Delivery, stage: str, err: Exception) -> None:
         """Publish the job (confirmed) to the durable dead-letter topic, then ack.
-        On any failure the delivery stays unacked, so the broker keeps it."""
+        If that fails the delivery is nacked with requeue, so it is always
+        settled (the broker keeps the job either way)."""
         assert self.amqp is not None
         try:
             if self.cfg.drop_failed:
@@ -437,7 +439,12 @@ class Service:
             log.with_fields(topic=self.cfg.dlq_topic, stage=stage).warn("job dead-lettered")
             self.metrics.inc("jobs_dead_lettered")
         except Exception as e:  # noqa: BLE001
-            log.with_field("error", str(e)).error("failed to dead-letter job; broker will redeliver")
+            log.with_field("error", str(e)).error("failed to dead-letter job; requeueing it")
+            try:
+                await msg.nack(requeue=True)
+                self.metrics.inc("jobs_requeued")
+            except Exception as e2:  # noqa: BLE001 - channel gone: the broker redelivers it anyway
+                log.with_field("error", str(e2)).error("failed to requeue job; broker will redeliver")
 
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
