@@ -150,22 +150,24 @@ PYBIND11_MODULE(_relay, m) {
   m.def("recv_body",
         [](const py::object& sock, int fd, uint64_t off, int64_t length, const py::bytes& prefix,
            std::shared_ptr<Flow> flow, size_t seg, uint64_t seg_done0, double idle_timeout, size_t buf_size,
-           bool use_splice) {
+           bool use_splice, bool chunked) -> py::tuple {
           std::string pre = prefix;
           StreamArg io = as_stream(sock);
           RecvResult r;
           {
             py::gil_scoped_release nogil;
             r = recv_body(*io.s, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0, idle_timeout,
-                          buf_size, use_splice);
+                          buf_size, use_splice, chunked);
           }
+          if (chunked) return py::make_tuple(r.received, r.eof, r.err, r.ended && !r.extra);
           return py::make_tuple(r.received, r.eof, r.err);
         },
         py::arg("sock"), py::arg("fd"), py::arg("offset"), py::arg("length"), py::arg("prefix"), py::arg("flow"),
         py::arg("seg") = 0, py::arg("seg_done0") = 0, py::arg("idle_timeout") = 120.0,
-        py::arg("buf_size") = 4u << 20, py::arg("splice") = true,
+        py::arg("buf_size") = 4u << 20, py::arg("splice") = true, py::arg("chunked") = false,
         "Stream a body into fd at offset (plain sockets: splice socket->pipe->file when possible, else "
-        "recv+pwrite); returns (received, eof, error).");
+        "recv+pwrite); returns (received, eof, error).  chunked=True decodes a chunked transfer coding "
+        "and returns (received, eof, error, reusable).");
 
   m.def("send_body",
         [](const py::object& sock, const py::bytes& head, int fd, uint64_t off, uint64_t length,

@@ -431,8 +431,118 @@ inline ssize_t recv_wait(Stream& io, char* p, size_t n, Clock::time_point* last,
 // length < 0: until EOF.  Progress: flow->advance(seg, seg_done0 + received).
 struct RecvResult {
   uint64_t received = 0;
-  bool eof = false;  // peer closed (normal end for length < 0)
+  bool eof = false;    // peer closed (normal end for length < 0)
+  bool ended = false;  // chunked: the last chunk and its trailers were read
+  bool extra = false;  // chunked: bytes arrived after the body (connection not reusable)
   std::string err;
+};
+
+// Incremental decoder of an HTTP/1.1 chunked body (RFC 9112 §7.1):
+//   chunk = hex-size [; ext] CRLF data CRLF ... 0 [; ext] CRLF *(trailer CRLF) CRLF
+// decode() works in place: the data bytes of buf[0, n) are moved to the front
+// of buf (the framing between them is overwritten; dst <= src always), so one
+// pwrite stores what a whole receive buffer carried.
+class ChunkedDecoder {
+ public:
+  // Consumes buf[0, n); returns bytes consumed (< n only once the body ended).
+  // *data_n = data bytes now at buf[0, *data_n).  Malformed framing sets *err.
+  size_t decode(char* buf, size_t n, size_t* data_n, std::string* err) {
+    size_t i = 0, w = 0;
+    while (i < n && phase_ != kDone) {
+      const char c = buf[i];
+      switch (phase_) {
+        case kSize: {
+          const int v = hexval(c);
+          if (v >= 0) {
+            if (++digits_ > 15) return fail(err, "chunk size too large", data_n, w);
+            size_ = (size_ << 4) | uint64_t(v);
+          } else if (digits_ && (c == ';' || c == ' ' || c == '\t')) {
+            phase_ = kExt;
+          } else if (digits_ && c == '\r') {
+            phase_ = kSizeLF;
+          } else {
+            return fail(err, "malformed chunk size line", data_n, w);
+          }
+          ++i;
+          break;
+        }
+        case kExt:  // chunk extensions are ignored (bounded)
+          if (c == '\r') phase_ = kSizeLF;
+          else if (++ext_ > 4096) return fail(err, "chunk extension too long", data_n, w);
+          ++i;
+          break;
+        case kSizeLF:
+          if (c != '\n') return fail(err, "malformed chunk size line", data_n, w);
+          ++i;
+          if (size_ == 0) {
+            phase_ = kTrailer;
+            line_ = 0;
+          } else {
+            phase_ = kData;
+            left_ = size_;
+          }
+          break;
+        case kData: {
+          const size_t m = size_t(std::min<uint64_t>(left_, n - i));
+          if (w != i) std::memmove(buf + w, buf + i, m);
+          w += m;
+          i += m;
+          left_ -= m;
+          if (left_ == 0) phase_ = kDataCR;
+          break;
+        }
+        case kDataCR:
+          if (c != '\r') return fail(err, "chunk data not followed by CRLF", data_n, w);
+          phase_ = kDataLF;
+          ++i;
+          break;
+        case kDataLF:
+          if (c != '\n') return fail(err, "chunk data not followed by CRLF", data_n, w);
+          phase_ = kSize;
+          size_ = 0;
+          digits_ = 0;
+          ext_ = 0;
+          ++i;
+          break;
+        case kTrailer:  // trailer fields (ignored), then the empty line
+          if (c == '\r') phase_ = kTrailerLF;
+          else ++line_;
+          if (++trailer_ > (64u << 10)) return fail(err, "chunked trailer too large", data_n, w);
+          ++i;
+          break;
+        case kTrailerLF:
+          if (c != '\n') return fail(err, "malformed chunked trailer", data_n, w);
+          ++i;
+          if (line_ == 0) phase_ = kDone;
+          line_ = 0;
+          if (phase_ != kDone) phase_ = kTrailer;
+          break;
+        case kDone:
+          break;
+      }
+    }
+    *data_n = w;
+    return i;
+  }
+  bool done() const { return phase_ == kDone; }
+
+ private:
+  enum Phase { kSize, kExt, kSizeLF, kData, kDataCR, kDataLF, kTrailer, kTrailerLF, kDone };
+  static int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  static size_t fail(std::string* err, const char* why, size_t* data_n, size_t w) {
+    *err = why;
+    *data_n = w;
+    return 0;
+  }
+  Phase phase_ = kSize;
+  uint64_t size_ = 0, left_ = 0;
+  int digits_ = 0;
+  size_t ext_ = 0, line_ = 0, trailer_ = 0;
 };
 
 // Zero-user-copy receive: socket -> pipe (page references move) -> file
@@ -519,14 +629,68 @@ inline bool splice_body(Stream& io, int fd, uint64_t off, uint64_t want, RecvRes
   return ok;  // false: caller continues with recv + pwrite
 }
 
+// recv_chunked: the chunked-transfer form of recv_body.  Decoded bytes go to
+// the file at off + received; `length` >= 0 caps them (a longer body is an
+// error).  Ends at the last chunk, so the connection stays reusable.
+inline RecvResult recv_chunked(Stream& io, int fd, uint64_t off, int64_t length, const char* prefix,
+                               size_t prefix_len, Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout) {
+  RecvResult r;
+  ChunkedDecoder dec;
+  Buf buf(256u << 10);
+  auto last = Clock::now();
+  // one decode + write step over buf[0, have)
+  auto step = [&](size_t have) -> bool {
+    size_t data_n = 0;
+    const size_t used = dec.decode(buf.data(), have, &data_n, &r.err);
+    if (!r.err.empty()) return false;
+    bool capped = false;
+    if (length >= 0 && r.received + data_n >= uint64_t(length)) {
+      // the segment ends here (the probe's stream runs on into the next
+      // segment's bytes): keep what belongs to it and drop the connection
+      capped = r.received + data_n > uint64_t(length) || !dec.done();
+      data_n = size_t(uint64_t(length) - r.received);
+    }
+    if (data_n) {
+      if (fd >= 0 && !pwrite_full(fd, buf.data(), data_n, off + r.received, &r.err)) return false;
+      r.received += data_n;
+      if (flow) flow->advance(seg, seg_done0 + r.received);
+    }
+    if (capped) {
+      r.ended = r.extra = true;
+    } else if (dec.done()) {
+      r.ended = true;
+      r.extra = used < have;
+    }
+    return true;
+  };
+  for (size_t p = 0; p < prefix_len && !r.ended;) {
+    const size_t m = std::min(prefix_len - p, buf.size());
+    std::memcpy(buf.data(), prefix + p, m);
+    if (!step(m)) return r;
+    p += m;
+  }
+  while (!r.ended) {
+    const ssize_t n = recv_wait(io, buf.data(), buf.size(), &last, idle_timeout, flow, &r.err);
+    if (n < 0) return r;
+    if (n == 0) {
+      r.eof = true;
+      r.err = "connection closed inside a chunked body";
+      return r;
+    }
+    if (!step(size_t(n))) return r;
+  }
+  return r;
+}
+
 inline RecvResult recv_body(Stream& io, int fd, uint64_t off, int64_t length, const char* prefix, size_t prefix_len,
                             Flow* flow, size_t seg, uint64_t seg_done0, double idle_timeout,
-                            size_t buf_size = 4u << 20, bool use_splice = true) {
+                            size_t buf_size = 4u << 20, bool use_splice = true, bool chunked = false) {
   RecvResult r;
   if (stopped(io, flow)) {  // before touching the file: a cancelled segment writes nothing
     r.err = "cancelled";
     return r;
   }
+  if (chunked) return recv_chunked(io, fd, off, length, prefix, prefix_len, flow, seg, seg_done0, idle_timeout);
   const uint64_t want = length < 0 ? UINT64_MAX : static_cast<uint64_t>(length);
   if (prefix_len) {
     const size_t n = static_cast<size_t>(std::min<uint64_t>(prefix_len, want));

@@ -399,3 +399,101 @@ def test_disk_space_preflight_fails_fast(tmp_path, monkeypatch):
         assert (tmp_path / "big.mkv").read_bytes() == data
         await o.stop()
     run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_chunked_origin_fetched_once(tmp_path, native):
+    """A chunked response (no length, no ranges; chunk extensions and a
+    trailer) is decoded by the native receive pump — one GET, no second
+    request through aiohttp — and the keep-alive connection is reused."""
+    from tritondl.utils import rawhttp
+
+    async def main():
+        o = await Origin().start()
+        o.chunked = True
+        data = os.urandom(2_345_678)
+        url = o.add("/live/feed.mkv", data)
+        h = _dl(native=native, segments=4)
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "feed.mkv").read_bytes() == data
+        assert [r[0] for r in o.requests] == ["GET"]                       # exactly one GET
+        if native:
+            assert sum(len(v) for v in h._raw.idle.values()) == 1          # read to its end: pooled
+        os.remove(tmp_path / "feed.mkv")
+        await h.download(str(tmp_path), Sink(), url)                      # again, on the pooled connection
+        assert (tmp_path / "feed.mkv").read_bytes() == data and len(o.requests) == 2
+        await h.close()
+        await o.stop()
+    assert rawhttp.relay_module() is not None
+    run(main())
+
+
+def test_chunked_decoder_rejects_bad_framing(tmp_path):
+    """Malformed chunk framing fails the pump with a clear error."""
+    import socket
+
+    from tritondl.utils import rawhttp
+    relay = rawhttp.relay_module()
+    good = b"5;x=y\r\nhello\r\n1\r\n \r\n0\r\nT: v\r\n\r\n"
+    fd = os.open(tmp_path / "out", os.O_RDWR | os.O_CREAT, 0o644)
+    try:
+        for body, want in ((good, ""), (b"zz\r\n", "chunk size"), (b"3\r\nabcX\r\n", "CRLF"),
+                           (b"3\r\nabc\r\n", "closed inside")):
+            a, b = socket.socketpair()
+            a.sendall(body)
+            a.close()
+            got, _eof, err, reusable = relay.recv_body(b.fileno(), fd, 0, -1, b"", None, chunked=True)
+            b.close()
+            assert (want in err) if want else err == "", (body, err)
+            if not want:
+                assert got == 6 and reusable and os.pread(fd, 6, 0) == b"hello "
+        a, b = socket.socketpair()                    # a cap (the segment's end) stops early, not reusable
+        a.sendall(good)
+        got, _eof, err, reusable = relay.recv_body(b.fileno(), fd, 0, 3, b"", None, chunked=True)
+        a.close()
+        b.close()
+        assert (got, err, reusable) == (3, "", False)
+    finally:
+        os.close(fd)
+
+
+def test_cancelled_fallback_download_writes_nothing_after_close(tmp_path, monkeypatch):
+    """The aiohttp data path (no native relay) writes through executor threads:
+    cancelling a download with several segments in flight must wait for every
+    write before the file's descriptor is closed — a sentinel file opened
+    right after (taking the freed descriptor number) stays untouched."""
+    import time as _time
+
+    from tritondl.fetch import http as H
+    real = H._pwritev_all
+    writing = []
+
+    def slow_write(fd, bufs, pos):
+        writing.append(fd)
+        _time.sleep(0.3)                              # a slow disk: the write outlives the cancel
+        real(fd, bufs, pos)
+    monkeypatch.setattr(H, "_pwritev_all", slow_write)
+
+    async def main():
+        o = await Origin().start()
+        o.rate = 8e6
+        data = os.urandom(8 << 20)
+        url = o.add("/big.mkv", data)
+        h = _dl(native=False, segments=4, segment_threshold=1 << 20, write_block=64 << 10)
+        dh = await h.start(str(tmp_path), Sink(), url)
+        for _ in range(200):
+            if writing:
+                break
+            await asyncio.sleep(0.01)
+        assert writing
+        dh.cancel()
+        with pytest.raises(BaseException):
+            await dh.wait()
+        sentinels = [os.open(tmp_path / f"sentinel{k}", os.O_RDWR | os.O_CREAT, 0o644) for k in range(8)]
+        await asyncio.sleep(0.8)                      # any write still in flight would land now
+        for fd in sentinels:
+            assert os.fstat(fd).st_size == 0
+            os.close(fd)
+        await h.close()
+        await o.stop()
+    run(main())

@@ -67,6 +67,7 @@ class Origin:
         self.cut_times = 0
         self.cut_match: str | None = None       # only cut requests whose Range header starts with this
         self.fail = 0
+        self.chunked = False                    # GET bodies with Transfer-Encoding: chunked (no ranges)
         self.rate: float | None = None
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
@@ -123,6 +124,8 @@ class Origin:
             return web.Response(status=200, headers=hdrs)
         if request.method != "GET":
             return web.Response(status=405)
+        if self.chunked:
+            return await self._chunked(request, blob, hdrs)
         start, end, status = 0, size, 200
         rng = request.headers.get("Range")
         if rng and self.ranges:
@@ -162,4 +165,25 @@ class Origin:
             if self.rate:
                 await asyncio.sleep(n / self.rate)
         await resp.write_eof()
+        return resp
+
+    async def _chunked(self, request: web.Request, blob: Blob, hdrs: dict) -> web.StreamResponse:
+        """The whole object with ``Transfer-Encoding: chunked`` (no length, no
+        ranges — a dynamic origin): chunks of varying size, some with chunk
+        extensions, and a trailer field; ``rate`` paces it."""
+        import random
+        hdrs = {k: v for k, v in hdrs.items() if k != "Accept-Ranges"}
+        hdrs["Transfer-Encoding"] = "chunked"
+        resp = web.StreamResponse(status=200, headers=hdrs)
+        await resp.prepare(request)
+        rng = random.Random(len(self.requests))
+        pos, size = 0, blob.size()
+        while pos < size:
+            n = min(size - pos, rng.choice((1, 7, 4096, 65536, 300_000)))
+            ext = ";name=value" if rng.random() < 0.3 else ""
+            await resp.write(f"{n:x}{ext}\r\n".encode() + blob.read(pos, pos + n) + b"\r\n")
+            pos += n
+            if self.rate:
+                await asyncio.sleep(n / self.rate)
+        await resp.write(b"0\r\nX-Checksum: none\r\n\r\n")
         return resp

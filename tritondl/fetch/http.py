@@ -31,8 +31,13 @@ Beyond the reference:
   the relay module) goes to the native receive pump (``csrc/relay``, GIL
   released), which writes the file and publishes progress on a native
   ``Flow`` that the S3 send pump follows; redirects are followed natively
-  (later Range requests go straight to the final URL); chunked / encoded
-  bodies use aiohttp;
+  (later Range requests go straight to the final URL); chunked bodies are
+  decoded by the pump (one GET, connection reused), content-coded bodies are
+  stored as sent, as the aiohttp path does; aiohttp remains for odd 3xx
+  replies, TLS through an https proxy, and builds without the relay module;
+* the egress proxy of ``HTTP_PROXY`` / ``HTTPS_PROXY`` / ``NO_PROXY`` is used
+  with Go's rules (:mod:`tritondl.utils.proxy`), as grab's transport did;
+* the file's mtime is set from ``Last-Modified``, as grab does;
 * when one segment fails, its siblings are cancelled and their pumps
   stopped and awaited before the file or any socket is closed (no write
   through a recycled fd number).
@@ -307,10 +312,11 @@ class HTTPDownloader:
                 if not url.startswith(("http://", "https://")):
                     return None
                 continue
-            enc = h.headers.get("Content-Encoding", "identity").lower()
-            if 300 <= h.status < 400 or h.chunked or enc not in ("", "identity"):
-                conn.close()                  # odd 3xx / chunked / encoded body: aiohttp handles these
+            if 300 <= h.status < 400:
+                conn.close()                  # odd 3xx (300, 304, ...): aiohttp handles these
                 return None
+            # chunked bodies are decoded by the native pump; a content-coded body is
+            # stored as sent, like the aiohttp path (auto_decompress=False) stores it
             return _RawResponse(self._raw, host, port, conn, h, url)
         raise HTTPDownloadError(f"GET {url}: stopped after {self.max_redirects} redirects")
 
@@ -635,7 +641,7 @@ class HTTPDownloader:
                 bufs.append(chunk)
                 nbuf += len(chunk)
             if nbuf >= self.write_block or (limit >= 0 and (wpos - pos) + nbuf >= limit):
-                await loop.run_in_executor(None, _pwritev_all, fd, bufs, wpos)
+                await rawhttp.run_settled(loop, _pwritev_all, fd, bufs, wpos)
                 wpos += nbuf
                 done[i] += nbuf
                 bufs, nbuf = [], 0
@@ -645,7 +651,7 @@ class HTTPDownloader:
                     if segs[i][1] < 0 or len(segs) > 1:
                         break               # more body follows (next segment's bytes): stop here
         if bufs:
-            await loop.run_in_executor(None, _pwritev_all, fd, bufs, wpos)
+            await rawhttp.run_settled(loop, _pwritev_all, fd, bufs, wpos)
             wpos += nbuf
             done[i] += nbuf
             if h is not None:
@@ -666,10 +672,13 @@ class HTTPDownloader:
             n = cl if cl is not None else -1
         prefix, r.leftover = r.leftover, b""
         flow = h.flow if h is not None else None
+        chunked = r.head.chunked
         rawhttp.trace("get_pump_start")
-        got, eof, err = await rawhttp.run_pump(
-            r.sock, relay.recv_body, fd, pos, n, prefix, flow, i, done[i], self.read_timeout, 4 << 20, self.splice)
+        res = await rawhttp.run_pump(
+            r.sock, relay.recv_body, fd, pos, n, prefix, flow, i, done[i], self.read_timeout, 4 << 20,
+            self.splice, chunked)
         rawhttp.trace("get_pump_end")
+        got, eof, err = res[:3]
         done[i] += got
         if h is not None:
             h._advance(i, done[i])
@@ -678,9 +687,12 @@ class HTTPDownloader:
             if err == "cancelled" or (flow is not None and flow.cancelled):
                 raise _FatalHTTPError(f"segment {i}: cancelled")
             raise HTTPDownloadError(err)
-        r.complete = (n < 0 and eof) or (cl is not None and n == cl and len(prefix) <= cl)
-        if n < 0:
-            r.head.keep_alive = False             # close-delimited body
+        if chunked:
+            r.complete = bool(res[3])             # last chunk read, nothing after it: reusable
+        else:
+            r.complete = (n < 0 and eof) or (cl is not None and n == cl and len(prefix) <= cl)
+            if n < 0:
+                r.head.keep_alive = False         # close-delimited body
         if end >= 0 and segs[i][0] + done[i] < end:
             raise HTTPDownloadError("connection closed early")
 

@@ -528,6 +528,26 @@ async def run_pump(conn: RawConn, fn, *args):
         raise
 
 
+async def run_settled(loop, fn, *args):
+    """``fn(*args)`` in an executor thread, awaited to completion even if the
+    caller is cancelled (the cancellation is re-raised once it returned).
+    For blocking I/O on a descriptor the caller closes afterwards: a write
+    still running in the thread when the fd is closed and its number reused
+    would land in whatever file took the number."""
+    fut = loop.run_in_executor(None, fn, *args)
+    try:
+        return await asyncio.shield(fut)
+    except asyncio.CancelledError:
+        while not fut.done():
+            try:
+                await asyncio.shield(fut)
+            except asyncio.CancelledError:
+                continue
+            except Exception:  # noqa: BLE001 - the write's own error no longer matters
+                break
+        raise
+
+
 _client_tls: dict = {}
 
 
