@@ -99,6 +99,9 @@ def main() -> int:
                          "competing consumers)")
     ap.add_argument("--dist-backend", default="", help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-level", default="warning")
+    ap.add_argument("--cpuprofile", default="",
+                    help="sampled whole-process CPU profile of the timed region (pprof + .txt summary; "
+                         "rank r writes PATH.r<r> when N > 1)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -177,7 +180,13 @@ def main() -> int:
             else:
                 loop.run_until_complete(stack.run_jobs(a.warmup))
         start = stack.svc.jobs_finished  # type: ignore[union-attr]
+        prof = None
+        if a.cpuprofile:
+            from tritondl.utils.profiler import CPUProfiler
+            prof = CPUProfiler(a.cpuprofile if world == 1 else f"{a.cpuprofile}.r{rank}")
         barrier()
+        if prof is not None:
+            prof.start()
         cpu0 = stack.cpu_seconds()
         t0 = time.perf_counter()
         if shared:
@@ -188,6 +197,8 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         cpu1 = stack.cpu_seconds()
+        if prof is not None:
+            prof.stop()
         barrier()
         n_done = stack.svc.jobs_finished - start  # type: ignore[union-attr]
         # latency/span stats over the recent-results window (trimmed past 10,000)

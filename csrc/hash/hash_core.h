@@ -17,6 +17,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cctype>
 #include <cerrno>
 #include <cstdlib>
@@ -26,6 +29,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <pthread.h>
 #include <utility>
 #include <vector>
 
@@ -264,6 +268,95 @@ inline size_t pread_full(int fd, char* dst, size_t n, off_t off) {
   return got;
 }
 
+// Name the calling thread (<= 15 chars) so per-thread CPU accounting
+// (-cpuprofile, top -H, /proc/<pid>/task/*/comm) can tell the pools apart.
+inline void name_thread(const char* name) { pthread_setname_np(pthread_self(), name); }
+
+// Process-wide pool of parked worker threads.  A worker ran its hasher pools
+// on fresh std::threads per call — per 10 MiB job that was 8 thread creations
+// and joins for the PUT's chunk hashers alone — and threads that exited
+// within a profiler tick were invisible to per-thread CPU accounting.
+// Tasks may block (on a ring slot, on download progress), so the pool never
+// queues a task behind a busy worker: it starts another thread instead, and
+// keeps at most `max_idle` parked.  Each task names its thread while it runs.
+class TaskPool {
+ public:
+  struct Group {
+    std::mutex mu;
+    std::condition_variable cv;
+    int left = 0;
+    void wait() {
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return left == 0; });
+    }
+  };
+
+  static TaskPool& get() {
+    static TaskPool* p = new TaskPool();  // never destroyed: threads stay parked until exit
+    return *p;
+  }
+
+  // Run `fn` on `copies` threads at once; the returned group's wait() joins them.
+  std::shared_ptr<Group> run(int copies, std::function<void()> fn, const char* name) {
+    auto g = std::make_shared<Group>();
+    g->left = copies;
+    auto shared_fn = std::make_shared<std::function<void()>>(std::move(fn));
+    std::lock_guard<std::mutex> l(mu_);
+    for (int k = 0; k < copies; ++k) q_.push_back(Task{shared_fn, g, name});
+    const size_t want = q_.size();
+    while (idle_ < want) {
+      ++idle_;  // counted idle until it takes a task
+      ++threads_;
+      std::thread([this] { loop(); }).detach();
+    }
+    cv_.notify_all();
+    return g;
+  }
+  size_t threads() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return threads_;
+  }
+
+ private:
+  struct Task {
+    std::shared_ptr<std::function<void()>> fn;
+    std::shared_ptr<Group> g;
+    const char* name;
+  };
+  static constexpr size_t max_idle = 64;
+
+  void loop() {
+    std::unique_lock<std::mutex> l(mu_);
+    for (;;) {
+      cv_.wait(l, [&] { return !q_.empty(); });
+      Task t = std::move(q_.front());
+      q_.erase(q_.begin());
+      --idle_;
+      l.unlock();
+      name_thread(t.name);
+      (*t.fn)();
+      {
+        std::lock_guard<std::mutex> gl(t.g->mu);
+        if (--t.g->left == 0) t.g->cv.notify_all();
+      }
+      // keeps the task's name while parked: CPU accounting that samples names
+      // (-cpuprofile) charges the work just done to that task kind
+      t = Task{};
+      l.lock();
+      if (idle_ >= max_idle) {
+        --threads_;
+        return;
+      }
+      ++idle_;
+    }
+  }
+
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Task> q_;
+  size_t idle_ = 0, threads_ = 0;
+};
+
 template <class F>
 void parallel_for(size_t n, int threads, F&& fn) {
   if (threads <= 1 || n <= 1) {
@@ -271,13 +364,10 @@ void parallel_for(size_t n, int threads, F&& fn) {
     return;
   }
   std::atomic<size_t> next{0};
-  std::vector<std::thread> ts;
   int t = static_cast<int>(std::min<size_t>(static_cast<size_t>(threads), n));
-  for (int k = 0; k < t; ++k)
-    ts.emplace_back([&] {
-      for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
-    });
-  for (auto& th : ts) th.join();
+  TaskPool::get().run(t, [&] {
+    for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
+  }, "tdl-hash")->wait();
 }
 
 inline int default_threads() {

@@ -347,7 +347,10 @@ struct Latch {
 class ReaderPool {
  public:
   explicit ReaderPool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] {
+      tritondl_hash::name_thread("tdl-gpu-read");
+      loop();
+    });
   }
   ~ReaderPool() {
     {
@@ -884,7 +887,10 @@ class GpuHasher {
       }
     };
     std::vector<std::thread> ts;
-    for (int k = 0; k < cpu_threads; ++k) ts.emplace_back(cpu_worker);
+    for (int k = 0; k < cpu_threads; ++k) ts.emplace_back([&] {
+      tritondl_hash::name_thread("tdl-hybrid-cpu");
+      cpu_worker();
+    });
     size_t gpu_pieces = 0;
     try {
       // 1 GiB windows: kernels of earlier windows overlap later copies, so only

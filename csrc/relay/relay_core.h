@@ -916,11 +916,8 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
   };
 
   const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + 1) / 2)));
-  std::vector<std::thread> pool;
-  if (n) {
-    pool.reserve(static_cast<size_t>(nthreads));
-    for (int t = 0; t < nthreads; ++t) pool.emplace_back(hasher);
-  }
+  std::shared_ptr<tritondl_hash::TaskPool::Group> pool;  // parked pool threads, not fresh ones per PUT
+  if (n) pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, "tdl-sha256");
 
   std::vector<std::string> heads;
   std::vector<struct iovec> iov;
@@ -983,7 +980,7 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
     cv_free.notify_all();
     cv_ready.notify_all();
   }
-  for (auto& t : pool) t.join();
+  if (pool) pool->wait();
   if (!r.err.empty()) return r;
   const std::string fin = "0;chunk-signature=" + signer.next(signer.empty_hash) + "\r\n\r\n";
   std::string e;
@@ -1135,6 +1132,7 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
     if (keep) r.data.resize(dbase + wtotal);
     Buf* wb = &buf[cur];
     verifier = std::thread([&, wb, frames = std::move(frames), dbase] {
+      tritondl_hash::name_thread("tdl-verify");
       const char* raw = wb->data();
       std::vector<std::string> h(frames.size());
       std::vector<size_t> doff(frames.size() + 1, 0);
@@ -1232,8 +1230,7 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
     }
   };
   const int nthreads = std::max(1, threads <= 0 ? 4 : threads);
-  std::vector<std::thread> pool;
-  for (int t = 0; t < nthreads; ++t) pool.emplace_back(hasher);
+  auto pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, "tdl-s3verify");
 
   ChunkSigner signer(key, amzdate, scope, seed);
   size_t checked = 0;
@@ -1319,7 +1316,7 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
     stop = true;
   }
   cv_pub.notify_all();
-  for (auto& t : pool) t.join();
+  pool->wait();
   if (r.err.empty() && !sig_ok) r.err = "chunk signature mismatch";
   if (r.err.empty() && (!final_seen || parsed != raw_len || have != raw_len)) r.err = "trailing bytes after final chunk";
   if (r.err.empty() && keep) {
