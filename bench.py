@@ -42,8 +42,11 @@ sys.path.insert(0, ROOT)
 CONFIG_NAME = "Single HTTP download job via local RabbitMQ, 10 MB file"
 
 
-def _gpu_hash_probe(total_mb: int = 256) -> dict:
-    """Secondary metric: HIP SHA-1 piece kernel on device-resident data."""
+def _gpu_hash_probe(total_mb: int = 4096) -> dict:
+    """Secondary metric: HIP SHA-1 piece kernel on device-resident data.  One
+    lane hashes one piece, so the buffer is sized for the 256 KiB figure to
+    fill the device: 4 GiB = 16,384 pieces (262,144 at 16 KiB); the lane
+    count is reported with each rate."""
     try:
         import torch
 
@@ -68,6 +71,9 @@ def _gpu_hash_probe(total_mb: int = 256) -> dict:
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / reps
             out[f"gpu_sha1_piece{pk}k_GBps"] = round(total / dt / 1e9, 1)
+            out[f"gpu_sha1_piece{pk}k_lanes"] = n
+        del dev
+        torch.cuda.empty_cache()
         return out
     except Exception as e:  # secondary figure only
         return {"gpu_probe_error": str(e)[:200]}
@@ -261,11 +267,17 @@ def main() -> int:
             # median ms from taking the job to the end of each stage (rank 0)
             "job_spans_ms_p50": {k: round(sorted(v)[len(v) // 2] * 1000, 2) for k, v in spans.items()},
             # CPU cost per job over the timed region, all ranks (worker processes incl. their
-            # native pump threads; the out-of-process fakes separately): the node's CPU count
-            # divided by this bounds how far job-level data parallelism can scale
-            "cpu_ms_per_job": {k: round(sum(c[k] for c in cpu_all) / (world * a.steps) * 1000, 2)
-                               for k in ("worker", "fakes", "broker")},
+            # native pump threads, from getrusage; the out-of-process fakes, producer included,
+            # separately): the node's CPU count divided by this bounds how far job-level data
+            # parallelism can scale.  null when the timed region is too short to mean much
+            "cpu_ms_per_job": ({k: round(sum(c[k] for c in cpu_all) / (world * a.steps) * 1000, 3)
+                                for k in ("worker", "fakes", "broker")} if max_elapsed >= 0.5 else None),
+            # the one fake broker serves every rank: the share of a core it used.  Above
+            # 0.5 the harness, not the workers, may be what limits the run
+            "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3) if max_elapsed >= 0.5 else None,
         }
+        if res["broker_core_share"] is not None and res["broker_core_share"] > 0.5:
+            res["harness_bound"] = True
         res.update(extra)
         print(json.dumps(res), flush=True)
     if world > 1:

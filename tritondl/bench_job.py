@@ -40,15 +40,17 @@ AK, SK = "benchaccess", "benchsecret"
 
 
 class Backend:
-    def __init__(self, kind: str, extra: list[str] | None = None) -> None:
+    def __init__(self, kind: str, extra: list[str] | None = None, module: str = "tritondl.fakes.serve") -> None:
         self.kind = kind
         self.extra = extra or []
+        self.module = module
         self.proc: asyncio.subprocess.Process | None = None
         self.info: dict = {}
 
     async def start(self) -> "Backend":
+        args = [self.kind] if self.module == "tritondl.fakes.serve" else []
         self.proc = await asyncio.create_subprocess_exec(
-            sys.executable, "-m", "tritondl.fakes.serve", self.kind, *self.extra,
+            sys.executable, "-m", self.module, *args, *self.extra,
             stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert self.proc.stdout is not None
@@ -57,6 +59,19 @@ class Backend:
             raise RuntimeError(f"fake {self.kind} failed to start")
         self.info = json.loads(line)
         return self
+
+    async def request(self, msg: dict, timeout: float = 900) -> dict:
+        """One JSON command on stdin, one JSON reply on stdout (the producer)."""
+        assert self.proc is not None and self.proc.stdin is not None and self.proc.stdout is not None
+        self.proc.stdin.write((json.dumps(msg) + "\n").encode())
+        await self.proc.stdin.drain()
+        line = await asyncio.wait_for(self.proc.stdout.readline(), timeout)
+        if not line:
+            raise RuntimeError(f"{self.kind} process exited")
+        out = json.loads(line)
+        if "error" in out:
+            raise RuntimeError(f"{self.kind}: {out['error']}")
+        return out
 
     async def stop(self) -> None:
         p = self.proc
@@ -102,7 +117,10 @@ class JobStack:
     cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
-    producer: Connection | None = None
+    producer: Connection | None = None               # in-process producer (inproc stacks: smoke, tests)
+    producer_proc: Backend | None = None             # the producer / convert counter process (benches)
+    broker_pid: int = 0
+    last_run: dict = field(default_factory=dict)     # the producer's report of the last run
     origin_urls: list = field(default_factory=list)
     _n: int = 0
 
@@ -153,6 +171,7 @@ class JobStack:
             bk = await Backend("broker").start()
             self.backends.append(bk)
             out["broker"] = bk.info["url"]
+            self.broker_pid = bk.proc.pid if bk.proc is not None else 0
         og = await Backend("origin", tls_args).start()
         s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK, *tls_args]).start()
         self.backends += [og, s3]
@@ -202,6 +221,13 @@ class JobStack:
         self.converts: list[Convert] = []
         self._convert_waiter: tuple[int, asyncio.Future] | None = None
         if not producer:
+            return
+        if not self.inproc:
+            # the producing / converting services run in a process of their own, off
+            # this worker's event loop (bench_producer.py)
+            self.producer_proc = await Backend("producer", [
+                "--broker", broker_url, "--origins", ",".join(self.origin_urls), "--size", str(self.file_size),
+                "--tag", self.tag, "--broker-pid", str(self.broker_pid)], module="tritondl.bench_producer").start()
             return
         self.producer = await Connection.open(broker_url, heartbeat=0)
         self.pch = await self.producer.channel()
@@ -262,7 +288,10 @@ class JobStack:
         assert self.svc is not None
         base, start = len(self.svc.results), self.svc.jobs_finished
         t0 = time.perf_counter()
-        await self.submit(n)
+        if self.producer_proc is not None:
+            self.last_run = await self.producer_proc.request({"cmd": "run", "n": n})
+        else:
+            await self.submit(n)
         await self.wait_done(start + n)
         dt = time.perf_counter() - t0
         bad = [r for r in self.svc.results[base:] if not r.ok or r.bytes != self.file_size]
@@ -274,6 +303,10 @@ class JobStack:
         """Producer side of shared mode: submit n jobs for ALL competing workers
         and wait until n new ``v1.convert`` messages arrived (the global ack
         rate's numerator)."""
+        if self.producer_proc is not None:
+            t0 = time.perf_counter()
+            self.last_run = await self.producer_proc.request({"cmd": "run", "n": n, "timeout": timeout})
+            return time.perf_counter() - t0
         base = len(self.converts)
         t0 = time.perf_counter()
         fut = asyncio.get_running_loop().create_future()
@@ -290,12 +323,14 @@ class JobStack:
 
     def cpu_seconds(self) -> dict:
         """CPU time (user+sys, s) so far of this worker process (all threads:
-        native pumps included) and of this stack's out-of-process fakes."""
+        native pumps included; getrusage, microsecond resolution) and of this
+        stack's out-of-process fakes (producer included)."""
+        import resource
+
         import psutil
-        me = psutil.Process()
-        t = me.cpu_times()
-        out = {"worker": t.user + t.system, "fakes": 0.0, "broker": 0.0}
-        for b in self.backends:
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        out = {"worker": ru.ru_utime + ru.ru_stime, "fakes": 0.0, "broker": 0.0}
+        for b in self.backends + ([self.producer_proc] if self.producer_proc is not None else []):
             p = getattr(b, "proc", None)
             if p is None:
                 continue
@@ -316,6 +351,9 @@ class JobStack:
         if self.producer is not None:
             with contextlib.suppress(Exception):
                 await self.producer.close()
+        if self.producer_proc is not None:
+            with contextlib.suppress(Exception):
+                await self.producer_proc.stop()
         if self.svc is not None:
             await self.svc.shutdown(grace=10)
         for b in self.backends:
