@@ -25,12 +25,16 @@
 
 #include <fcntl.h>
 #include <poll.h>
+#include <sys/mman.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdlib>
 #include <cctype>
 #include <atomic>
 #include <cerrno>
@@ -992,13 +996,239 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
   return r;
 }
 
+// send() on a plain non-blocking socket until done; MSG_MORE holds a short
+// header back so it leaves in the same segment as the payload that follows.
+inline bool send_more(Stream& io, const char* p, size_t n, double idle_timeout, const Flow* flow, std::string* err) {
+  const int sock = io.fd();
+  auto last = Clock::now();
+  while (n) {
+    const ssize_t w = ::send(sock, p, n, MSG_MORE | MSG_NOSIGNAL);
+    if (w > 0) {
+      p += w;
+      n -= static_cast<size_t>(w);
+      last = Clock::now();
+      continue;
+    }
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK) {
+      *err = errno_str("send");
+      return false;
+    }
+    if (stopped(io, flow)) {
+      *err = "cancelled";
+      return false;
+    }
+    if (since(last) > idle_timeout || wait_fd(sock, POLLOUT, 50) < 0) {
+      *err = "send timeout";
+      return false;
+    }
+  }
+  return true;
+}
+
+// sendfile [o, o + n) of fd to a plain socket (page cache -> socket).
+inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle_timeout, const Flow* flow,
+                         std::string* err) {
+  const int sock = io.fd();
+  auto last = Clock::now();
+  uint64_t k = 0;
+  while (k < n) {
+    off_t pos = static_cast<off_t>(o + k);
+    const ssize_t w = ::sendfile(sock, fd, &pos, static_cast<size_t>(n - k));
+    if (w > 0) {
+      k += static_cast<uint64_t>(w);
+      last = Clock::now();
+      continue;
+    }
+    if (w == 0) {
+      *err = "source file shorter than expected";
+      return false;
+    }
+    if (errno == EINTR) continue;
+    if (errno != EAGAIN && errno != EWOULDBLOCK) {
+      *err = errno_str("sendfile");
+      return false;
+    }
+    if (stopped(io, flow)) {
+      *err = "cancelled";
+      return false;
+    }
+    if (since(last) > idle_timeout || wait_fd(sock, POLLOUT, 50) < 0) {
+      *err = "send timeout";
+      return false;
+    }
+  }
+  return true;
+}
+
+// send_chunked_zc: the aws-chunked body over a PLAIN socket with no payload
+// copy through user space.  send_chunked reads every chunk into a ring
+// (pread: one 10 MiB copy per 10 MiB job) and writev's the ring into the
+// socket (a second one).  Here:
+//   * chunk SHA-256s are computed straight from a read-only MAP_SHARED mapping
+//     of the file (the download's page cache), when the file already spans the
+//     range (it is pre-sized when the length is known); otherwise from a
+//     per-task pread scratch;
+//   * each frame's payload leaves with sendfile (page cache -> socket), and
+//     only the ~90-byte chunk header is written from user space, with MSG_MORE
+//     so it shares a segment with the payload after it.
+// Hashers run ahead of the sender as far as the download allows (a digest is
+// 32 bytes, so there is no ring to bound them).  TLS streams keep
+// send_chunked: the record layer needs the bytes in user space anyway.
+inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow,
+                                  ChunkSigner& signer, size_t chunk, int threads, double idle_timeout) {
+  SendResult r;
+  if (chunk == 0) {
+    r.err = "chunk size must be > 0";
+    return r;
+  }
+  const size_t n = static_cast<size_t>((length + chunk - 1) / chunk);
+  std::vector<std::array<unsigned char, 32>> dig(n);
+  std::vector<uint8_t> ready(n, 0);
+  std::mutex mu;
+  std::condition_variable cv_ready;
+  std::atomic<bool> abort{false};
+  std::string worker_err;
+  std::atomic<size_t> next{0};
+
+  // the mapping: only over bytes the file already holds (a read past EOF of a
+  // mapping is SIGBUS, a pread past EOF is a short read)
+  const char* map = nullptr;
+  size_t map_len = 0;
+  uint64_t base = 0;
+  struct stat st;
+  if (length && ::fstat(fd, &st) == 0 && static_cast<uint64_t>(st.st_size) >= off + length) {
+    const uint64_t page = static_cast<uint64_t>(::sysconf(_SC_PAGESIZE));
+    base = off & ~(page - 1);
+    map_len = static_cast<size_t>(off + length - base);
+    void* m = ::mmap(nullptr, map_len, PROT_READ, MAP_SHARED, fd, static_cast<off_t>(base));
+    if (m != MAP_FAILED) {
+      map = static_cast<const char*>(m);
+      ::madvise(m, map_len, MADV_SEQUENTIAL);
+    }
+  }
+
+  auto set_err = [&](const std::string& e) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      if (worker_err.empty()) worker_err = e;
+      abort.store(true);
+    }
+    cv_ready.notify_all();
+  };
+  auto hasher = [&] {
+    std::vector<char> scratch(map ? 0 : 2 * chunk);
+    for (;;) {
+      const size_t i = next.fetch_add(2);
+      if (i >= n || abort.load()) return;
+      const size_t cnt = std::min<size_t>(2, n - i);
+      const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
+      size_t m[2] = {0, 0};
+      for (size_t j = 0; j < cnt; ++j)
+        m[j] = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(i + j) * chunk));
+      if (flow) {
+        const int w = flow->wait_covered(a, a + m[0] + m[1], idle_timeout, &abort);
+        if (w) {
+          if (!abort.load())
+            set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
+                                                                       : "source transfer failed: " + flow->error());
+          return;
+        }
+      }
+      const char* src[2];
+      for (size_t j = 0; j < cnt; ++j) {
+        if (map) {
+          src[j] = map + (a + j * chunk - base);
+        } else {
+          char* d = scratch.data() + j * chunk;
+          if (tritondl_hash::pread_full(fd, d, m[j], static_cast<off_t>(a + j * chunk)) != m[j]) {
+            set_err("source file shorter than expected");
+            return;
+          }
+          src[j] = d;
+        }
+      }
+      if (cnt == 2) {
+        tritondl_hash::sha256_pair(src[0], m[0], src[1], m[1], dig[i].data(), dig[i + 1].data());
+      } else {
+        tritondl_hash::sha256_raw(src[0], m[0], dig[i].data());
+      }
+      {
+        std::lock_guard<std::mutex> l(mu);
+        for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
+      }
+      cv_ready.notify_all();
+    }
+  };
+  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + 1) / 2)));
+  std::shared_ptr<tritondl_hash::TaskPool::Group> pool;
+  if (n) pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, "tdl-sha256");
+
+  std::string head;
+  char hx[32];
+  for (size_t c = 0; c < n && r.err.empty(); ++c) {
+    {
+      std::unique_lock<std::mutex> l(mu);
+      while (!abort.load() && !ready[c]) {
+        if (io.aborted()) {  // the hashers may sit in a flow wait: stop them too
+          if (worker_err.empty()) worker_err = "cancelled";
+          abort.store(true);
+          break;
+        }
+        cv_wait_ms(cv_ready, l, 20);
+      }
+      if (abort.load()) {
+        r.err = worker_err;
+        break;
+      }
+    }
+    const uint64_t a = off + static_cast<uint64_t>(c) * chunk;
+    const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(c) * chunk));
+    std::snprintf(hx, sizeof hx, "%zx", m);
+    head.assign(c ? "\r\n" : "");
+    head += hx;
+    head += ";chunk-signature=";
+    head += signer.next(tritondl_hash::hex_raw(dig[c].data(), 32));
+    head += "\r\n";
+    if (!send_more(io, head.data(), head.size(), idle_timeout, flow, &r.err)) break;
+    if (!sendfile_all(io, fd, a, m, idle_timeout, flow, &r.err)) break;
+    r.sent += m;
+  }
+  if (!r.err.empty()) set_err(r.err);
+  if (pool) pool->wait();
+  if (map) ::munmap(const_cast<char*>(map), map_len);
+  if (!r.err.empty()) return r;
+  const std::string fin = std::string(n ? "\r\n" : "") + "0;chunk-signature=" + signer.next(signer.empty_hash) +
+                          "\r\n\r\n";
+  if (!send_all(io, fin.data(), fin.size(), idle_timeout, flow, &r.err)) return r;
+  r.last_sig = signer.prev();
+  return r;
+}
+
+// Zero-copy chunked sends for plain sockets (TRITONDL_RELAY_ZC=0: the ring path).
+inline bool zc_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("TRITONDL_RELAY_ZC");
+    return !(v && (std::strcmp(v, "0") == 0 || std::strcmp(v, "off") == 0 || std::strcmp(v, "false") == 0));
+  }();
+  return on;
+}
+
 inline SendResult send_body(Stream& io, const std::string& head, int fd, uint64_t off, uint64_t length, Flow* flow,
                             int mode, const std::string& key, const std::string& amzdate, const std::string& scope,
                             const std::string& seed, size_t chunk, int threads, double idle_timeout) {
   SendResult r;
-  if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
-  if (mode == 0) return send_plain(io, fd, off, length, flow, idle_timeout);
+  if (mode == 0) {
+    if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
+    return send_plain(io, fd, off, length, flow, idle_timeout);
+  }
   ChunkSigner signer(key, amzdate, scope, seed);
+  if (io.plain() && zc_enabled()) {
+    // the request head goes out with MSG_MORE too: it shares the first segment
+    if (!send_more(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
+    return send_chunked_zc(io, fd, off, length, flow, signer, chunk, threads, idle_timeout);
+  }
+  if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
   return send_chunked(io, fd, off, length, flow, signer, chunk, threads, idle_timeout);
 }
 

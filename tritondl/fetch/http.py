@@ -176,6 +176,8 @@ class HTTPDownloader:
         # (3.6 vs 5.9 ms per 10 MiB) but slower on the MI355X box's overlayfs with 4 concurrent
         # range streams (1 GiB fetch 154 vs 85 ms), so opt-in: TRITONDL_RELAY_SPLICE=1
         self.splice = os.environ.get("TRITONDL_RELAY_SPLICE", "0").lower() in ("1", "on", "true", "yes")
+        # receive buffer of the native pump (socket -> buffer -> pwrite)
+        self.recv_buf = int(os.environ.get("TRITONDL_RELAY_RECV_BUF", "") or (4 << 20))
         self._raw = rawhttp.Pool()
         # https trust: a private CA (PEM text / file), else the system store
         self.ca_pem, self.ca_file = ca_pem, ca_file or os.environ.get("TRITONDL_CA_FILE", "")
@@ -675,7 +677,7 @@ class HTTPDownloader:
         chunked = r.head.chunked
         rawhttp.trace("get_pump_start")
         res = await rawhttp.run_pump(
-            r.sock, relay.recv_body, fd, pos, n, prefix, flow, i, done[i], self.read_timeout, 4 << 20,
+            r.sock, relay.recv_body, fd, pos, n, prefix, flow, i, done[i], self.read_timeout, self.recv_buf,
             self.splice, chunked)
         rawhttp.trace("get_pump_end")
         got, eof, err = res[:3]
