@@ -322,6 +322,8 @@ PYBIND11_MODULE(_hash_host, m) {
         py::arg("prev_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("final") = false,
         py::arg("threads") = 1);
   m.def("default_threads", &default_threads);
+  m.def("pool_threads", [] { return TaskPool::get().threads(); },
+        "threads of the process-wide native task pool (parked + busy)");
   m.def("aws_chunk_decode", &py_aws_chunk_decode, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
         py::arg("seed_signature"), py::arg("raw"), py::arg("threads") = 1, py::arg("want_data") = true,
         py::arg("require_final") = true,

@@ -208,4 +208,6 @@ PYBIND11_MODULE(_relay, m) {
         "Receive + verify an aws-chunked body; returns (decoded_len, error, data_or_None).");
 
   m.def("chunked_length", &chunked_length, py::arg("length"), py::arg("chunk") = 64 << 10);
+  m.def("pool_threads", [] { return tritondl_hash::TaskPool::get().threads(); },
+        "threads of this module's native task pool (chunk hashers; parked + busy)");
 }

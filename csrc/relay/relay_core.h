@@ -82,13 +82,23 @@ class Flow {
 
   explicit Flow(std::vector<Seg> segs) : segs_(std::move(segs)) {}
 
+  // Wakes waiters only when one of their ranges became covered: the upload's
+  // chunk hashers wait for ranges ahead of the receive frontier, and waking
+  // all of them on every 256 KiB of progress was a thundering herd of
+  // futex wake-ups (8 hashers x ~40 advances per 10 MiB job).
   void advance(size_t seg, uint64_t done) {
+    bool wake = false;
     {
       std::lock_guard<std::mutex> l(mu_);
       if (seg >= segs_.size()) return;
       if (done > segs_[seg].done) segs_[seg].done = done;
+      for (const auto& w : waiters_)
+        if (covered_locked(w.first, w.second)) {
+          wake = true;
+          break;
+        }
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
   }
   // All bytes below `total` are on disk (also resolves open-ended segments).
   void finish(uint64_t total) {
@@ -198,17 +208,22 @@ class Flow {
   // 3 = the download finished short of b.
   int wait_covered(uint64_t a, uint64_t b, double timeout_s, const std::atomic<bool>* abort = nullptr) {
     std::unique_lock<std::mutex> l(mu_);
+    if (covered_locked(a, b)) return 0;
     const auto deadline = Clock::now() + std::chrono::duration_cast<Clock::duration>(
                                              std::chrono::duration<double>(std::max(0.0, timeout_s)));
+    waiters_.emplace_back(a, b);  // advance() wakes us once this range is covered
+    int rc;
     for (;;) {
-      if (covered_locked(a, b)) return 0;
-      if (failed_) return 1;
-      if (finished_) return 3;
-      if (abort && abort->load()) return 1;
-      if (Clock::now() >= deadline) return 2;
+      if (covered_locked(a, b)) { rc = 0; break; }
+      if (failed_) { rc = 1; break; }
+      if (finished_) { rc = 3; break; }
+      if (abort && abort->load()) { rc = 1; break; }
+      if (Clock::now() >= deadline) { rc = 2; break; }
       // short slices so an aborting caller (the upload pump's sender) is seen promptly
       cv_wait_ms(cv_, l, 20);
     }
+    waiters_.erase(std::find(waiters_.begin(), waiters_.end(), std::make_pair(a, b)));
+    return rc;
   }
 
  private:
@@ -239,6 +254,7 @@ class Flow {
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::vector<Seg> segs_;
+  std::vector<std::pair<uint64_t, uint64_t>> waiters_;  // ranges wait_covered() is blocked on
   bool finished_ = false;
   uint64_t total_ = 0;
   bool failed_ = false;

@@ -1,0 +1,29 @@
+"""Resource-leak soak, reduced for the CPU suite (the full run —
+5,000 headline jobs + 100 magnet jobs — is ``tools/box/r03_soak.sh``, log in
+profiles/).  One worker runs HTTP jobs, magnet jobs and failing jobs that
+are retried and dead-lettered; after warm-up its descriptors, threads,
+asyncio tasks and native pool threads must stay flat (reference job loop:
+``cmd/downloader/downloader.go:103-155`` runs for the process lifetime)."""
+
+import asyncio
+
+from tritondl.soak import run_soak
+from tritondl.utils.log import log
+
+
+def test_worker_resources_stay_flat(tmp_path):
+    log.configure("error", "")
+    res = asyncio.run(asyncio.wait_for(
+        run_soak(jobs=360, torrent_jobs=6, fail_every=30, sample_every=60, file_size=256 << 10, torrent_mb=1,
+                 warmup=120, workdir=str(tmp_path)), 300))
+    assert res["attempts"] == 360 + res["failing_jobs"] * 2
+    assert res["ok_attempts"] == 360 - res["failing_jobs"]          # every non-failing job succeeded
+    assert res["torrent_jobs"] == 6 and res["failing_jobs"] == 12
+    d = res["drift"]
+    assert d["fds"]["to"] <= d["fds"]["from"] + 3, d
+    assert d["os_threads"]["to"] <= d["os_threads"]["from"] + 4, d
+    assert d["py_threads"]["to"] <= d["py_threads"]["from"] + 2, d
+    assert d["tasks"]["to"] <= d["tasks"]["from"] + 3, d
+    if "pool_threads" in d:
+        assert d["pool_threads"]["max"] <= 16, d                     # parked hashers, not one per job
+    assert d["rss_drift_pct"] < 15, d
