@@ -105,6 +105,8 @@ def main() -> int:
                          "competing consumers)")
     ap.add_argument("--dist-backend", default="", help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-level", default="warning")
+    ap.add_argument("--s3-hash-device", default="cpu", choices=["cpu", "gpu"],
+                    help="aws-chunked chunk SHA-256s on SHA-NI (default) or the HIP kernel")
     ap.add_argument("--cpuprofile", default="",
                     help="sampled whole-process CPU profile of the timed region (pprof + .txt summary; "
                          "rank r writes PATH.r<r> when N > 1)")
@@ -144,7 +146,7 @@ def main() -> int:
                      http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
                      http_stripe_bytes=(a.stripe_kb << 10) if a.stripe_kb >= 0 else -1,
                      s3_part_size=a.s3_part_mb << 20, s3_multipart_threshold=a.s3_multipart_mb << 20,
-                     payload_mode=a.payload)
+                     payload_mode=a.payload, hash_device=a.s3_hash_device)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 
@@ -257,7 +259,7 @@ def main() -> int:
                        "topology": ("one shared broker, competing consumers; per-rank origin+S3 nodes"
                                     if shared else "private broker/origin/S3 per rank"),
                        "transport": "https (TLS 1.3, native OpenSSL data plane)" if a.tls else "http",
-                       "s3_payload": stack.payload_mode,
+                       "s3_payload": stack.payload_mode, "s3_hash_device": a.s3_hash_device,
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
                        **knobs},
             "jobs_per_rank": per_rank,

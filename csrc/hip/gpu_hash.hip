@@ -33,6 +33,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../hash/gpu_chunk_api.h"
 #include "../hash/hash_core.h"  // OpenSSL SHA-NI path for the CPU half of hybrid verification
 
 #include <fcntl.h>
@@ -964,11 +965,112 @@ int device_count() {
   return n;
 }
 
+// ------------------------------------------------------------ S3 chunk hashing
+// The aws-chunked streaming signature needs the SHA-256 of every 64 KiB chunk
+// of an upload; on a CPU-bound node that is half of a worker's CPU.  Each
+// calling thread (the relay's parked hasher tasks) owns a stream, a
+// blocking-sync event and pinned + device staging that grow to the largest
+// batch seen.  One call = copy into pinned staging, H2D, one kernel (a lane
+// per chunk), D2H of the digests, then the thread SLEEPS on the event (no
+// spin-wait: that would burn the CPU this offload exists to save).
+struct ChunkCtx {
+  hipStream_t s = nullptr;
+  hipEvent_t ev = nullptr;
+  uint8_t* pin = nullptr;
+  uint8_t* dev = nullptr;
+  uint32_t* dout = nullptr;
+  uint8_t* pout = nullptr;
+  size_t cap = 0, ocap = 0;
+  ~ChunkCtx() {
+    if (pin) (void)hipHostFree(pin);
+    if (pout) (void)hipHostFree(pout);
+    if (dev) (void)hipFree(dev);
+    if (dout) (void)hipFree(dout);
+    if (ev) (void)hipEventDestroy(ev);
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+std::atomic<int> g_chunk_device{0};
+
+int sha256_chunks_impl(const void* src, size_t len, size_t chunk, unsigned char* out, char* err, size_t errlen) {
+  static thread_local std::unique_ptr<ChunkCtx> tls;
+  try {
+    if (chunk == 0 || len == 0) throw std::invalid_argument("empty chunk batch");
+    const size_t n = (len + chunk - 1) / chunk;
+    if (!tls) {
+      auto c = std::make_unique<ChunkCtx>();
+      HIP_CHECK(hipSetDevice(g_chunk_device.load()));
+      HIP_CHECK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&c->ev, hipEventBlockingSync | hipEventDisableTiming));
+      tls = std::move(c);
+    }
+    ChunkCtx& c = *tls;
+    if (c.cap < len) {
+      if (c.pin) HIP_CHECK(hipHostFree(c.pin));
+      if (c.dev) HIP_CHECK(hipFree(c.dev));
+      c.pin = nullptr;
+      c.dev = nullptr;
+      c.cap = 0;
+      const size_t cap = std::max<size_t>(len, 4u << 20);
+      HIP_CHECK(hipHostMalloc(&c.pin, cap, hipHostMallocDefault));
+      HIP_CHECK(hipMalloc(&c.dev, cap));
+      c.cap = cap;
+    }
+    if (c.ocap < n * 32) {
+      if (c.pout) HIP_CHECK(hipHostFree(c.pout));
+      if (c.dout) HIP_CHECK(hipFree(c.dout));
+      c.pout = nullptr;
+      c.dout = nullptr;
+      c.ocap = 0;
+      const size_t ocap = std::max<size_t>(n * 32, 8192);
+      HIP_CHECK(hipHostMalloc(&c.pout, ocap, hipHostMallocDefault));
+      HIP_CHECK(hipMalloc(&c.dout, ocap));
+      c.ocap = ocap;
+    }
+    std::memcpy(c.pin, src, len);  // page cache mapping -> pinned (the DMA needs pinned pages)
+    HIP_CHECK(hipMemcpyAsync(c.dev, c.pin, len, hipMemcpyHostToDevice, c.s));
+    launch_hash(256, c.dev, len, chunk, static_cast<uint32_t>(n), c.dout, c.s, 64);
+    HIP_CHECK(hipMemcpyAsync(c.pout, c.dout, n * 32, hipMemcpyDeviceToHost, c.s));
+    HIP_CHECK(hipEventRecord(c.ev, c.s));
+    HIP_CHECK(hipEventSynchronize(c.ev));
+    std::memcpy(out, c.pout, n * 32);
+    return 0;
+  } catch (const std::exception& e) {
+    if (err && errlen) std::snprintf(err, errlen, "%s", e.what());
+    return -1;
+  }
+}
+
+TdlGpuChunkApi g_chunk_api{1, &sha256_chunks_impl};
+
 }  // namespace
 
 PYBIND11_MODULE(_gpu_hash, m) {
   m.doc() = "tritondl HIP (gfx950) batched SHA-1/SHA-256 piece hashing";
   m.def("device_count", &device_count);
+  m.def("chunk_api", [](int device) {
+          g_chunk_device.store(device);
+          return py::capsule(&g_chunk_api, TDL_GPU_CHUNK_API_NAME);
+        },
+        py::arg("device") = 0,
+        "PyCapsule with the C table the relay's S3 send pump uses to hash aws-chunked chunks on the GPU");
+  m.def(
+      "sha256_chunks",
+      [](const py::buffer& buf, size_t chunk) {
+        py::buffer_info bi = buf.request();
+        const size_t len = static_cast<size_t>(bi.size * bi.itemsize);
+        std::string out(((len + chunk - 1) / chunk) * 32, '\0');
+        char err[256] = {0};
+        int rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = sha256_chunks_impl(bi.ptr, len, chunk, reinterpret_cast<unsigned char*>(&out[0]), err, sizeof err);
+        }
+        if (rc) throw std::runtime_error(err);
+        return py::bytes(out);
+      },
+      py::arg("buffer"), py::arg("chunk"), "the chunk_api call from Python (tests): concatenated 32-byte digests");
   m.def(
       "hash_device",
       [](const std::string& kind, uintptr_t data_ptr, uint64_t total, uint64_t piece_len, uintptr_t out_ptr,

@@ -172,21 +172,30 @@ PYBIND11_MODULE(_relay, m) {
   m.def("send_body",
         [](const py::object& sock, const py::bytes& head, int fd, uint64_t off, uint64_t length,
            std::shared_ptr<Flow> flow, int mode, const py::bytes& key, const std::string& amzdate,
-           const std::string& scope, const std::string& seed, size_t chunk, int threads, double idle_timeout) {
+           const std::string& scope, const std::string& seed, size_t chunk, int threads, double idle_timeout,
+           const py::object& gpu) {
           std::string h = head, k = key;
           StreamArg io = as_stream(sock);
+          const TdlGpuChunkApi* api = nullptr;
+          if (!gpu.is_none()) {
+            api = static_cast<const TdlGpuChunkApi*>(PyCapsule_GetPointer(gpu.ptr(), TDL_GPU_CHUNK_API_NAME));
+            if (!api) throw py::error_already_set();
+            if (api->version != 1) throw std::invalid_argument("unsupported GPU chunk API version");
+          }
           SendResult r;
           {
             py::gil_scoped_release nogil;
             r = send_body(*io.s, h, fd, off, length, flow.get(), mode, k, amzdate, scope, seed, chunk, threads,
-                          idle_timeout);
+                          idle_timeout, api);
           }
           return py::make_tuple(r.sent, r.last_sig, r.err);
         },
         py::arg("sock"), py::arg("head"), py::arg("fd"), py::arg("offset"), py::arg("length"), py::arg("flow"),
         py::arg("mode"), py::arg("signing_key") = py::bytes(), py::arg("amzdate") = "", py::arg("scope") = "",
         py::arg("seed") = "", py::arg("chunk") = 64 << 10, py::arg("threads") = 4, py::arg("idle_timeout") = 300.0,
-        "Send head + body (mode 0 plain / 1 aws-chunked); returns (payload_sent, last_signature, error).");
+        py::arg("gpu") = py::none(),
+        "Send head + body (mode 0 plain / 1 aws-chunked); returns (payload_sent, last_signature, error).  "
+        "gpu: _gpu_hash.chunk_api() to hash the aws-chunked chunks on the GPU (plain sockets).");
 
   m.def("recv_verify_chunked",
         [](const py::object& sock, uint64_t raw_len, const py::bytes& prefix, const py::bytes& key,

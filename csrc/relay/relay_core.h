@@ -50,6 +50,7 @@
 #include <utility>
 #include <vector>
 
+#include "../hash/gpu_chunk_api.h"
 #include "../hash/hash_core.h"
 #include "stream.h"
 
@@ -1091,8 +1092,14 @@ inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle
 // Hashers run ahead of the sender as far as the download allows (a digest is
 // 32 bytes, so there is no ring to bound them).  TLS streams keep
 // send_chunked: the record layer needs the bytes in user space anyway.
+//
+// With `gpu` (the HIP module's chunk API, pool mode on a CPU-bound node) each
+// hasher task claims `gpu_batch` consecutive chunks and hashes them on the
+// GPU in one call (a lane per chunk) instead of pairs on SHA-NI; a batch the
+// GPU call fails on is hashed on the CPU.
 inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow,
-                                  ChunkSigner& signer, size_t chunk, int threads, double idle_timeout) {
+                                  ChunkSigner& signer, size_t chunk, int threads, double idle_timeout,
+                                  const TdlGpuChunkApi* gpu = nullptr, size_t gpu_batch = 32) {
   SendResult r;
   if (chunk == 0) {
     r.err = "chunk size must be > 0";
@@ -1132,11 +1139,44 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     }
     cv_ready.notify_all();
   };
+  const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : 2;  // chunks per claim
   auto hasher = [&] {
-    std::vector<char> scratch(map ? 0 : 2 * chunk);
+    std::vector<char> scratch(map ? 0 : per * chunk);
     for (;;) {
-      const size_t i = next.fetch_add(2);
+      const size_t i = next.fetch_add(per);
       if (i >= n || abort.load()) return;
+      if (gpu) {
+        const size_t cnt = std::min(per, n - i);
+        const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
+        const size_t len = static_cast<size_t>(std::min<uint64_t>(cnt * chunk, off + length - a));
+        if (flow) {
+          const int w = flow->wait_covered(a, a + len, idle_timeout, &abort);
+          if (w) {
+            if (!abort.load())
+              set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
+                                                                         : "source transfer failed: " + flow->error());
+            return;
+          }
+        }
+        const char* src = map ? map + (a - base) : scratch.data();
+        if (!map && tritondl_hash::pread_full(fd, scratch.data(), len, static_cast<off_t>(a)) != len) {
+          set_err("source file shorter than expected");
+          return;
+        }
+        char gerr[256] = {0};
+        if (gpu->sha256_chunks(src, len, chunk, dig[i].data(), gerr, sizeof gerr) != 0) {
+          for (size_t j = 0; j < cnt; ++j) {  // the GPU failed this batch: SHA-NI instead
+            const size_t mj = std::min<size_t>(chunk, len - j * chunk);
+            tritondl_hash::sha256_raw(src + j * chunk, mj, dig[i + j].data());
+          }
+        }
+        {
+          std::lock_guard<std::mutex> l(mu);
+          for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
+        }
+        cv_ready.notify_all();
+        continue;
+      }
       const size_t cnt = std::min<size_t>(2, n - i);
       const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
       size_t m[2] = {0, 0};
@@ -1176,9 +1216,10 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
       cv_ready.notify_all();
     }
   };
-  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + 1) / 2)));
+  const int nthreads = static_cast<int>(
+      std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + per - 1) / per)));
   std::shared_ptr<tritondl_hash::TaskPool::Group> pool;
-  if (n) pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, "tdl-sha256");
+  if (n) pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, gpu ? "tdl-gpu-sha256" : "tdl-sha256");
 
   std::string head;
   char hx[32];
@@ -1232,17 +1273,18 @@ inline bool zc_enabled() {
 
 inline SendResult send_body(Stream& io, const std::string& head, int fd, uint64_t off, uint64_t length, Flow* flow,
                             int mode, const std::string& key, const std::string& amzdate, const std::string& scope,
-                            const std::string& seed, size_t chunk, int threads, double idle_timeout) {
+                            const std::string& seed, size_t chunk, int threads, double idle_timeout,
+                            const TdlGpuChunkApi* gpu = nullptr) {
   SendResult r;
   if (mode == 0) {
     if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
     return send_plain(io, fd, off, length, flow, idle_timeout);
   }
   ChunkSigner signer(key, amzdate, scope, seed);
-  if (io.plain() && zc_enabled()) {
+  if (io.plain() && (zc_enabled() || gpu)) {
     // the request head goes out with MSG_MORE too: it shares the first segment
     if (!send_more(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
-    return send_chunked_zc(io, fd, off, length, flow, signer, chunk, threads, idle_timeout);
+    return send_chunked_zc(io, fd, off, length, flow, signer, chunk, threads, idle_timeout, gpu);
   }
   if (!send_all(io, head.data(), head.size(), idle_timeout, flow, &r.err)) return r;
   return send_chunked(io, fd, off, length, flow, signer, chunk, threads, idle_timeout);

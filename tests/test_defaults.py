@@ -105,3 +105,11 @@ def test_last_modified_becomes_mtime(tmp_path):
         await h.close()
         await o.stop()
     run(main())
+
+
+def test_s3_hash_device_knob():
+    import pytest as _p
+    assert Config().s3_hash_device == "cpu"
+    assert Config.from_env({"TRITONDL_S3_HASH_DEVICE": "gpu"}).s3_hash_device == "gpu"
+    with _p.raises(ValueError):
+        Config.from_env({"TRITONDL_S3_HASH_DEVICE": "tpu"})

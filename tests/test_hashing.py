@@ -250,3 +250,39 @@ def test_verify_pieces_padding_spans_host(tmp_path):
 def test_verify_pieces_padding_spans_gpu(tmp_path):
     files, exp = _padded_layout(tmp_path, 16384)
     assert all(hashing.verify_pieces(files, 16384, exp, device="gpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [65536, 65536 * 32, 65536 * 32 + 777, 100, 5 * 65536 - 1])
+def test_gpu_chunk_api_matches_hashlib(size):
+    """The C table the S3 send pump calls (``_gpu_hash.chunk_api``), driven
+    from Python: one 32-byte SHA-256 per 64 KiB aws chunk, the last short."""
+    mod = hashing.gpu_module()
+    data = os.urandom(size)
+    got = mod.sha256_chunks(data, 65536)
+    want = b"".join(hashlib.sha256(data[i:i + 65536]).digest() for i in range(0, size, 65536))
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_s3_put_with_gpu_chunk_hashing(tmp_path):
+    """A streaming-signed PUT whose chunk SHA-256s come from the GPU: the
+    fake S3 verifies every chunk signature, so a wrong digest fails the PUT."""
+    import asyncio
+
+    from tritondl.fakes.s3 import FakeS3
+    from tritondl.s3.client import S3Client
+    from tritondl.s3.credentials import Static
+
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk").start()
+        data = os.urandom((10 << 20) + 12345)
+        p = tmp_path / "obj"
+        p.write_bytes(data)
+        c = S3Client(s3.endpoint, Static("ak", "sk"), payload_mode="streaming", hash_device="gpu")
+        await c.make_bucket("b")
+        await c.put_object("b", "k", str(p))
+        assert s3.object_bytes("b", "k") == data
+        await c.close()
+        await s3.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))

@@ -39,6 +39,8 @@ async def main() -> int:
     ap.add_argument("--file-kb", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     ap.add_argument("--nodes", type=int, default=1, help="origin + S3 fake processes (sharded)")
+    ap.add_argument("--s3-hash-device", default="cpu", choices=["cpu", "gpu"],
+                    help="workers hash aws-chunked chunks on SHA-NI or the HIP kernel")
     a = ap.parse_args()
     a.jobs = a.jobs or a.workers * a.jobs_per_worker
     from tritondl.amqp.codec import Properties
@@ -66,7 +68,8 @@ async def main() -> int:
                "AWS_SECRET_ACCESS_KEY": SK, "PYTHONPATH": ROOT, "TRITONDL_RETRY_DELAY": "0",
                "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning", "TRITONDL_PROGRESS_LOG_INTERVAL": "0",
                "TRITONDL_CLEANUP": "1", "TRITONDL_CONCURRENCY": str(a.concurrency),
-               "TRITONDL_PREFETCH": str(a.concurrency), "TRITONDL_GPU_VERIFY": "off"}
+               "TRITONDL_PREFETCH": str(a.concurrency), "TRITONDL_GPU_VERIFY": "off",
+               "TRITONDL_S3_HASH_DEVICE": a.s3_hash_device}
         ncpu = len(os.sched_getaffinity(0))
         pool = WorkerPool(plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)),
                           env=env, cwd=work, grace=10,

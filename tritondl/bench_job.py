@@ -114,6 +114,7 @@ class JobStack:
     sign_threads: int = 0            # 0: worker default
     tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
     payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
+    hash_device: str = "cpu"         # aws-chunked chunk SHA-256s: cpu (SHA-NI) | gpu (HIP)
     cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
@@ -215,7 +216,7 @@ class JobStack:
         up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode=mode,
                                            sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file,
                                            part_size=cfg.s3_part_size, multipart_threshold=cfg.s3_multipart_threshold,
-                                           parallel_parts=cfg.s3_parallel_parts))
+                                           parallel_parts=cfg.s3_parallel_parts, hash_device=self.hash_device))
         self.svc = Service(cfg, amqp=amqp, uploader=up)
         await self.svc.start()
         self.converts: list[Convert] = []

@@ -168,8 +168,14 @@ class S3Client:
                  multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
                  io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  native: bool = True, sign_threads: int = 4, ca_pem: str = "", ca_file: str = "",
-                 proxies: "_proxy.ProxyConfig | None" = None) -> None:
+                 proxies: "_proxy.ProxyConfig | None" = None, hash_device: str = "cpu") -> None:
         self.ep = Endpoint.parse(endpoint) if isinstance(endpoint, str) else endpoint
+        # "gpu": aws-chunked chunk SHA-256s on the HIP kernel (plain-http native PUTs);
+        # fails loudly at the first PUT if the GPU module or a device is missing
+        if hash_device not in ("cpu", "gpu"):
+            raise ValueError(f"hash_device must be cpu|gpu, got {hash_device!r}")
+        self.hash_device = hash_device
+        self._gpu_api = None
         # egress proxy (minio-go's DefaultTransport: ProxyFromEnvironment); None = the environment
         self.proxies = proxies
         self.creds = creds or default_chain()
@@ -256,6 +262,21 @@ class S3Client:
 
     def _creds(self) -> Value:
         return self.creds.retrieve()
+
+    def _chunk_gpu(self):
+        """The HIP chunk-hashing API for the send pump (``hash_device="gpu"``)."""
+        if self.hash_device != "gpu":
+            return None
+        if self._gpu_api is None:
+            try:
+                mod = hashing.gpu_module()
+                ok = mod.device_count() > 0
+            except Exception:  # noqa: BLE001 - reported below
+                ok = False
+            if not ok:
+                raise S3Error(0, "GPUUnavailable", "TRITONDL_S3_HASH_DEVICE=gpu but no HIP device / _gpu_hash module")
+            self._gpu_api = mod.chunk_api(hashing.default_device())
+        return self._gpu_api
 
     def _proxy(self, host: str) -> "_proxy.ProxyURL | None":
         """The egress proxy for requests to ``host`` (the endpoint, or a
@@ -636,7 +657,7 @@ class S3Client:
                         conn, relay.send_body, head, fd, offset, length, flow,
                         1 if m == "streaming" else 0, signed.key if signed else b"", amzdate,
                         signed.scope if signed else "", signed.signature if signed else "", sigv4.STREAM_CHUNK,
-                        self.sign_threads, 300.0)
+                        self.sign_threads, 300.0, self._chunk_gpu() if m == "streaming" else None)
                     if perr and ("source" in perr or perr == "cancelled"):
                         raise S3Error(0, "SourceFailed", perr, f"PUT {path}")
                     try:

@@ -66,12 +66,12 @@ class Uploader:
     @classmethod
     def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "",
                  part_size: int = 16 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
-                 env=None, sign_threads: int = 4, ca_file: str = "") -> "Uploader":
+                 env=None, sign_threads: int = 4, ca_file: str = "", hash_device: str = "cpu") -> "Uploader":
         ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
         Endpoint.parse(ep)                       # ValueError on an endpoint minio-go would refuse
         client = S3Client(ep, default_chain(env), region=region, part_size=part_size,
                           multipart_threshold=multipart_threshold, parallel_parts=parallel_parts,
-                          sign_threads=sign_threads, ca_file=ca_file)
+                          sign_threads=sign_threads, ca_file=ca_file, hash_device=hash_device)
         return cls(bucket, client)
 
     async def ensure_bucket(self) -> None:

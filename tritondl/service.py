@@ -136,7 +136,8 @@ class Service:
                                               part_size=cfg.s3_part_size,
                                               multipart_threshold=cfg.s3_multipart_threshold,
                                               parallel_parts=cfg.s3_parallel_parts,
-                                              sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file)
+                                              sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file,
+                                              hash_device=cfg.s3_hash_device)
         if self.amqp is None:
             if cfg.rabbitmq_endpoint_defaulted:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)

@@ -118,6 +118,10 @@ class Config:
     # job's critical path (box A/B, 10 MiB job: 4 -> 245-270, 6 -> 295, 8 -> 307 jobs/s;
     # profiles/r02_fill_ab); half the CPUs this process may use, 2..8
     s3_sign_threads: int = field(default_factory=lambda: _default_sign_threads())
+    # where the aws-chunked chunk SHA-256s run: "cpu" (SHA-NI; lowest per-job latency) or
+    # "gpu" (the HIP piece kernel, a lane per 64 KiB chunk: ~2.6 ms per batch, so it
+    # pays only when the node is CPU-bound, e.g. many workers per CPU share)
+    s3_hash_device: str = "cpu"
     aws_access_key_id: str = ""
     aws_secret_access_key: str = ""
     aws_session_token: str = ""
@@ -169,7 +173,7 @@ class Config:
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
-                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file"}
+                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file", "S3_HASH_DEVICE": "s3_hash_device"}
         for k, a in ints.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, int(g("TRITONDL_" + k)))
@@ -188,6 +192,8 @@ class Config:
         c.bt_native_wire = _env_bool(g("TRITONDL_BT_NATIVE_WIRE"), c.bt_native_wire)
         c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
         c.bt_pex = _env_bool(g("TRITONDL_BT_PEX"), c.bt_pex)
+        if c.s3_hash_device not in ("cpu", "gpu"):
+            raise ValueError(f"TRITONDL_S3_HASH_DEVICE must be cpu|gpu, got {c.s3_hash_device!r}")
         if c.bt_encryption not in ("disable", "allow", "prefer", "require"):
             raise ValueError(f"TRITONDL_BT_ENCRYPTION must be disable|allow|prefer|require, got {c.bt_encryption!r}")
         if argv is not None:
