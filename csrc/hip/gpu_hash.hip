@@ -1002,7 +1002,7 @@ int sha256_chunks_impl(const void* src, size_t len, size_t chunk, unsigned char*
       auto c = std::make_unique<ChunkCtx>();
       HIP_CHECK(hipSetDevice(g_chunk_device.load()));
       HIP_CHECK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
-      HIP_CHECK(hipEventCreateWithFlags(&c->ev, hipEventBlockingSync | hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming));
       tls = std::move(c);
     }
     ChunkCtx& c = *tls;
@@ -1032,8 +1032,20 @@ int sha256_chunks_impl(const void* src, size_t len, size_t chunk, unsigned char*
     HIP_CHECK(hipMemcpyAsync(c.dev, c.pin, len, hipMemcpyHostToDevice, c.s));
     launch_hash(256, c.dev, len, chunk, static_cast<uint32_t>(n), c.dout, c.s, 64);
     HIP_CHECK(hipMemcpyAsync(c.pout, c.dout, n * 32, hipMemcpyDeviceToHost, c.s));
+    // Completion: the thread sleeps between event queries.  Both HIP blocking
+    // mechanisms cost more CPU than the SHA-NI hashing this replaces
+    // (profiles/r03_gpu_sha_ab): hipEventSynchronize, even on a
+    // hipEventBlockingSync event, polled (~20 ms of CPU per 10 MiB job over
+    // the hasher threads); hipLaunchHostFunc's runtime thread cost ~6.5 ms.
+    // The kernel of a 64 KiB-chunk batch runs ~2.6 ms, so 250 us sleeps add
+    // little latency and almost no CPU.
     HIP_CHECK(hipEventRecord(c.ev, c.s));
-    HIP_CHECK(hipEventSynchronize(c.ev));
+    for (;;) {
+      const hipError_t q = hipEventQuery(c.ev);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) HIP_CHECK(q);
+      std::this_thread::sleep_for(std::chrono::microseconds(250));
+    }
     std::memcpy(out, c.pout, n * 32);
     return 0;
   } catch (const std::exception& e) {

@@ -1096,10 +1096,13 @@ inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle
 // With `gpu` (the HIP module's chunk API, pool mode on a CPU-bound node) each
 // hasher task claims `gpu_batch` consecutive chunks and hashes them on the
 // GPU in one call (a lane per chunk) instead of pairs on SHA-NI; a batch the
-// GPU call fails on is hashed on the CPU.
+// GPU call fails on is hashed on the CPU.  One kernel per 16 MiB: a lane's
+// 64 KiB chain takes ~2.6 ms whatever the lane count, and kernels from
+// several streams of one process were measured to serialize (5 x 2 MiB
+// batches per 10 MiB job cost ~9 ms per job, one 10 MiB batch ~3 ms).
 inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow,
                                   ChunkSigner& signer, size_t chunk, int threads, double idle_timeout,
-                                  const TdlGpuChunkApi* gpu = nullptr, size_t gpu_batch = 32) {
+                                  const TdlGpuChunkApi* gpu = nullptr, size_t gpu_batch = 256) {
   SendResult r;
   if (chunk == 0) {
     r.err = "chunk size must be > 0";

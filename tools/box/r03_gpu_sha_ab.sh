@@ -15,7 +15,7 @@ for rep in 1 2; do
   timeout -k 10 300 python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 10240 --nodes 4 --s3-hash-device gpu > $OUT/pool_gpu$rep.log 2>&1 || exit $?
 done
 timeout -k 10 200 python bench.py --steps 200 --warmup 10 --no-gpu-probe --s3-hash-device gpu --cpuprofile $OUT/gpu.prof > $OUT/head_gpu_prof.log 2>&1 &&
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/rocprof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 5 --no-gpu-probe --s3-hash-device gpu > $GRAFT_REPO_ROOT/$OUT/rocprof.log 2>&1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/rocprof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 5 --no-gpu-probe --s3-hash-device gpu > $GRAFT_REPO_ROOT/$OUT/rocprof.log 2>&1
 rc=$?
 cd $GRAFT_REPO_ROOT
 tail -2 $OUT/pytest_gpu.log
