@@ -326,6 +326,39 @@ def test_concurrency_overlaps_jobs(tmp_path):
     run(main())
 
 
+def test_same_job_twice_runs_one_at_a_time(tmp_path):
+    """Two deliveries of one media id at once (a redelivery while the first
+    still runs): the second waits for the first instead of truncating the
+    file it is uploading from, then finds it complete and re-uploads it."""
+    import fcntl
+
+    async def main():
+        e = await Env().up(tmp_path, concurrency=2, prefetch=2)
+        e.origin.rate = 4_000_000
+        data = os.urandom(1_000_000)
+        url = e.origin.add("/same.mkv", data)
+        e.submit(Media(id="dup", source_uri=url), i=0)
+        e.submit(Media(id="dup", source_uri=url), i=1)
+        res = await e.wait_results(2)
+        assert all(r.ok for r in res), res
+        assert e.s3.object_bytes("triton-staging", object_key("dup", "same.mkv")) == data
+        assert [m[0] for m in e.origin.requests].count("GET") == 2   # the second one: probe, file complete
+        # another worker process holding the job dir's lock blocks a delivery until released
+        d = tmp_path / "downloading" / "held"
+        d.mkdir(parents=True)
+        fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
+        fcntl.flock(fd, fcntl.LOCK_EX)
+        url2 = e.origin.add("/held.mkv", b"h" * 1000)
+        e.submit(Media(id="held", source_uri=url2), i=0)
+        await asyncio.sleep(0.3)
+        assert len(e.svc.results) == 2                                # still waiting on the lock
+        os.close(fd)
+        res = await e.wait_results(3)
+        assert res[-1].ok
+        await e.down()
+    run(main())
+
+
 def test_cli_runs_and_writes_cpuprofile(tmp_path):
     async def backends():
         b = await Broker().start()

@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import fcntl
 import os
 import shutil
 import signal
@@ -110,6 +111,46 @@ class Service:
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
         self.jobs_finished = 0                     # monotonic count of results recorded
         self._finish_waiters: list[tuple[int, asyncio.Future]] = []
+        self._id_locks: dict[str, list] = {}       # media id -> [asyncio.Lock, users]
+
+    @contextlib.asynccontextmanager
+    async def _job_lock(self, media_id: str):
+        """One job per media id at a time, in this process (an asyncio lock)
+        and across the workers sharing ``downloading/`` (``flock`` on the job
+        dir).  A job redelivered while its first delivery still runs —
+        another worker whose channel died mid-job, or concurrency > 1 — would
+        otherwise truncate and rewrite the very file the first delivery is
+        uploading from (and the send pump maps that file).  The second
+        delivery waits, then finds the file complete and re-uploads it
+        (at-least-once, as the reference)."""
+        ent = self._id_locks.setdefault(media_id, [asyncio.Lock(), 0])
+        ent[1] += 1
+        fd = -1
+        try:
+            async with ent[0]:
+                try:
+                    d = self.dispatcher.job_dir(media_id) if self.dispatcher is not None else ""
+                except ValueError:
+                    d = ""                          # invalid id: the job fails in its download stage
+                if d:
+                    try:
+                        os.makedirs(d, mode=0o755, exist_ok=True)
+                        fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
+                        try:
+                            fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                        except BlockingIOError:
+                            log.with_field("media_id", media_id).warn(
+                                "job already running in another worker; waiting for it")
+                            await asyncio.get_running_loop().run_in_executor(None, fcntl.flock, fd, fcntl.LOCK_EX)
+                    except OSError as e:
+                        log.with_fields(media_id=media_id, error=str(e)).warn("job lock unavailable")
+                yield
+        finally:
+            if fd >= 0:
+                os.close(fd)                        # releases the flock
+            ent[1] -= 1
+            if ent[1] == 0:
+                self._id_locks.pop(media_id, None)
 
     async def wait_finished(self, total: int, timeout: float | None = None) -> None:
         """Wait until ``jobs_finished >= total`` (woken by the result itself,
@@ -221,6 +262,10 @@ class Service:
 
         if log.enabled("info"):
             log.with_field("job", job.to_dict()).info("got message")
+        async with self._job_lock(job.media.id):
+            return await self._run_job(msg, job, t0)
+
+    async def _run_job(self, msg: Delivery, job: Download, t0: float) -> JobResult:
         stage = "download"
         nbytes = 0
         marks: dict[str, float] = {}
