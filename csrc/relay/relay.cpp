@@ -1,8 +1,10 @@
 // pybind11 bindings for the native fetch -> S3 data plane (relay_core.h,
-// stream.h).  Every pump releases the GIL for its whole run; Python awaits it
-// from an executor thread while the event loop keeps serving the control
-// plane.  Pumps take a stream: a `Sock` / `TlsConn` object (abortable), or a
-// bare socket fd (int).
+// stream.h).  A pump runs either inside the call with the GIL released
+// (recv_body / send_body, for executor threads and tests) or on the native
+// task pool (start_recv_body / start_send_body), reporting to a
+// CompletionPort whose eventfd the event loop watches — the worker's path.
+// Pumps take a stream: a `Sock` / `TlsConn` object (abortable), or a bare
+// socket fd (int).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -31,6 +33,25 @@ StreamArg as_stream(const py::object& o) {
     a.s = a.tmp.get();
   }
   return a;
+}
+
+// The same for a pump that outlives the call (start_*): always shared.
+std::shared_ptr<Stream> stream_ptr(const py::object& o) {
+  if (py::isinstance<Stream>(o)) return o.cast<std::shared_ptr<Stream>>();
+  return std::make_shared<PlainStream>(o.cast<int>());
+}
+
+const TdlGpuChunkApi* gpu_api(const py::object& gpu) {
+  if (gpu.is_none()) return nullptr;
+  auto api = static_cast<const TdlGpuChunkApi*>(PyCapsule_GetPointer(gpu.ptr(), TDL_GPU_CHUNK_API_NAME));
+  if (!api) throw py::error_already_set();
+  if (api->version != 1) throw std::invalid_argument("unsupported GPU chunk API version");
+  return api;
+}
+
+py::tuple recv_tuple(const RecvResult& r, bool chunked) {
+  if (chunked) return py::make_tuple(r.received, r.eof, r.err, r.ended && !r.extra);
+  return py::make_tuple(r.received, r.eof, r.err);
 }
 
 }  // namespace
@@ -159,8 +180,7 @@ PYBIND11_MODULE(_relay, m) {
             r = recv_body(*io.s, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0, idle_timeout,
                           buf_size, use_splice, chunked);
           }
-          if (chunked) return py::make_tuple(r.received, r.eof, r.err, r.ended && !r.extra);
-          return py::make_tuple(r.received, r.eof, r.err);
+          return recv_tuple(r, chunked);
         },
         py::arg("sock"), py::arg("fd"), py::arg("offset"), py::arg("length"), py::arg("prefix"), py::arg("flow"),
         py::arg("seg") = 0, py::arg("seg_done0") = 0, py::arg("idle_timeout") = 120.0,
@@ -176,12 +196,7 @@ PYBIND11_MODULE(_relay, m) {
            const py::object& gpu) {
           std::string h = head, k = key;
           StreamArg io = as_stream(sock);
-          const TdlGpuChunkApi* api = nullptr;
-          if (!gpu.is_none()) {
-            api = static_cast<const TdlGpuChunkApi*>(PyCapsule_GetPointer(gpu.ptr(), TDL_GPU_CHUNK_API_NAME));
-            if (!api) throw py::error_already_set();
-            if (api->version != 1) throw std::invalid_argument("unsupported GPU chunk API version");
-          }
+          const TdlGpuChunkApi* api = gpu_api(gpu);
           SendResult r;
           {
             py::gil_scoped_release nogil;
@@ -196,6 +211,67 @@ PYBIND11_MODULE(_relay, m) {
         py::arg("gpu") = py::none(),
         "Send head + body (mode 0 plain / 1 aws-chunked); returns (payload_sent, last_signature, error).  "
         "gpu: _gpu_hash.chunk_api() to hash the aws-chunked chunks on the GPU (plain sockets).");
+
+  py::class_<CompletionPort, std::shared_ptr<CompletionPort>>(m, "CompletionPort")
+      .def(py::init<>())
+      .def("fileno", &CompletionPort::fd, "eventfd, readable while finished pumps wait to be reaped")
+      .def_property_readonly("inflight", &CompletionPort::inflight)
+      .def("wait", [](const CompletionPort& p, int timeout_ms) {
+             py::gil_scoped_release nogil;
+             return p.wait(timeout_ms);
+           },
+           py::arg("timeout_ms"))
+      .def("reap", [](CompletionPort& p) {
+             py::list out;
+             for (const CompletionPort::Done& d : p.reap())
+               out.append(py::make_tuple(d.id, d.kind == 1 ? recv_tuple(d.rr, d.chunked)
+                                                           : py::make_tuple(d.sr.sent, d.sr.last_sig, d.sr.err)));
+             return out;
+           },
+           "[(id, result), ...] of every pump finished since the last call; result as recv_body / send_body");
+
+  m.def("start_recv_body",
+        [](std::shared_ptr<CompletionPort> port, uint64_t id, const py::object& sock, int fd, uint64_t off,
+           int64_t length, const py::bytes& prefix, std::shared_ptr<Flow> flow, size_t seg, uint64_t seg_done0,
+           double idle_timeout, size_t buf_size, bool use_splice, bool chunked) {
+          std::string pre = prefix;
+          std::shared_ptr<Stream> io = stream_ptr(sock);
+          start_pump(
+              std::move(port), id, 1, chunked,
+              [io, pre, fd, off, length, flow, seg, seg_done0, idle_timeout, buf_size, use_splice,
+               chunked](CompletionPort::Done& d) {
+                d.rr = recv_body(*io, fd, off, length, pre.data(), pre.size(), flow.get(), seg, seg_done0,
+                                 idle_timeout, buf_size, use_splice, chunked);
+              },
+              "tdl-recv");
+        },
+        py::arg("port"), py::arg("id"), py::arg("sock"), py::arg("fd"), py::arg("offset"), py::arg("length"),
+        py::arg("prefix"), py::arg("flow"), py::arg("seg") = 0, py::arg("seg_done0") = 0,
+        py::arg("idle_timeout") = 120.0, py::arg("buf_size") = 4u << 20, py::arg("splice") = true,
+        py::arg("chunked") = false, "recv_body on the native task pool; the result is reaped from `port`.");
+
+  m.def("start_send_body",
+        [](std::shared_ptr<CompletionPort> port, uint64_t id, const py::object& sock, const py::bytes& head, int fd,
+           uint64_t off, uint64_t length, std::shared_ptr<Flow> flow, int mode, const py::bytes& key,
+           const std::string& amzdate, const std::string& scope, const std::string& seed, size_t chunk, int threads,
+           double idle_timeout, const py::object& gpu) {
+          std::string h = head, k = key;
+          std::shared_ptr<Stream> io = stream_ptr(sock);
+          const TdlGpuChunkApi* api = gpu_api(gpu);
+          start_pump(
+              std::move(port), id, 2, false,
+              [io, h, fd, off, length, flow, mode, k, amzdate, scope, seed, chunk, threads, idle_timeout,
+               api](CompletionPort::Done& d) {
+                d.sr = send_body(*io, h, fd, off, length, flow.get(), mode, k, amzdate, scope, seed, chunk, threads,
+                                 idle_timeout, api);
+              },
+              "tdl-send");
+        },
+        py::arg("port"), py::arg("id"), py::arg("sock"), py::arg("head"), py::arg("fd"), py::arg("offset"),
+        py::arg("length"), py::arg("flow"), py::arg("mode"), py::arg("signing_key") = py::bytes(),
+        py::arg("amzdate") = "", py::arg("scope") = "", py::arg("seed") = "", py::arg("chunk") = 64 << 10,
+        py::arg("threads") = 4, py::arg("idle_timeout") = 300.0, py::arg("gpu") = py::none(),
+        "send_body on the native task pool; the result is reaped from `port`.");
 
   m.def("recv_verify_chunked",
         [](const py::object& sock, uint64_t raw_len, const py::bytes& prefix, const py::bytes& key,

@@ -25,6 +25,7 @@
 
 #include <fcntl.h>
 #include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/mman.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
@@ -83,40 +84,35 @@ class Flow {
 
   explicit Flow(std::vector<Seg> segs) : segs_(std::move(segs)) {}
 
-  // Wakes waiters only when one of their ranges became covered: the upload's
-  // chunk hashers wait for ranges ahead of the receive frontier, and waking
-  // all of them on every 256 KiB of progress was a thundering herd of
-  // futex wake-ups (8 hashers x ~40 advances per 10 MiB job).
+  // Wakes exactly the waiters whose range became covered: the upload's chunk
+  // hashers wait for ranges ahead of the receive frontier, and waking all of
+  // them on every 256 KiB of progress was a thundering herd of futex
+  // wake-ups (4 hashers x ~40 advances per 10 MiB job, most going straight
+  // back to sleep).  Each waiter owns its condition variable; the notify
+  // happens under the lock, so a waiter that timed out and left cannot be
+  // notified after it is gone.
   void advance(size_t seg, uint64_t done) {
-    bool wake = false;
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      if (seg >= segs_.size()) return;
-      if (done > segs_[seg].done) segs_[seg].done = done;
-      for (const auto& w : waiters_)
-        if (covered_locked(w.first, w.second)) {
-          wake = true;
-          break;
-        }
-    }
-    if (wake) cv_.notify_all();
+    std::lock_guard<std::mutex> l(mu_);
+    if (seg >= segs_.size()) return;
+    if (done > segs_[seg].done) segs_[seg].done = done;
+    for (Waiter* w : waiters_)
+      if (!w->woken && covered_locked(w->a, w->b)) {
+        w->woken = true;
+        w->cv.notify_one();
+      }
   }
   // All bytes below `total` are on disk (also resolves open-ended segments).
   void finish(uint64_t total) {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      finished_ = true;
-      total_ = total;
-    }
-    cv_.notify_all();
+    std::lock_guard<std::mutex> l(mu_);
+    finished_ = true;
+    total_ = total;
+    wake_all_locked();
   }
   void fail(const std::string& why) {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      if (!failed_) err_ = why;
-      failed_ = true;
-    }
-    cv_.notify_all();
+    std::lock_guard<std::mutex> l(mu_);
+    if (!failed_) err_ = why;
+    failed_ = true;
+    wake_all_locked();
   }
   void cancel() {
     cancel_.store(true);
@@ -212,7 +208,8 @@ class Flow {
     if (covered_locked(a, b)) return 0;
     const auto deadline = Clock::now() + std::chrono::duration_cast<Clock::duration>(
                                              std::chrono::duration<double>(std::max(0.0, timeout_s)));
-    waiters_.emplace_back(a, b);  // advance() wakes us once this range is covered
+    Waiter me{a, b};
+    waiters_.push_back(&me);  // advance() wakes us once this range is covered
     int rc;
     for (;;) {
       if (covered_locked(a, b)) { rc = 0; break; }
@@ -221,13 +218,25 @@ class Flow {
       if (abort && abort->load()) { rc = 1; break; }
       if (Clock::now() >= deadline) { rc = 2; break; }
       // short slices so an aborting caller (the upload pump's sender) is seen promptly
-      cv_wait_ms(cv_, l, 20);
+      cv_wait_ms(me.cv, l, 20);
     }
-    waiters_.erase(std::find(waiters_.begin(), waiters_.end(), std::make_pair(a, b)));
+    waiters_.erase(std::find(waiters_.begin(), waiters_.end(), &me));
     return rc;
   }
 
  private:
+  struct Waiter {
+    uint64_t a, b;
+    std::condition_variable cv;
+    bool woken = false;
+    Waiter(uint64_t a_, uint64_t b_) : a(a_), b(b_) {}
+  };
+  void wake_all_locked() {
+    for (Waiter* w : waiters_) {
+      w->woken = true;
+      w->cv.notify_one();
+    }
+  }
   uint64_t watermark_locked() const {
     if (finished_) return total_;
     uint64_t w = 0;
@@ -253,9 +262,8 @@ class Flow {
   }
 
   mutable std::mutex mu_;
-  std::condition_variable cv_;
   std::vector<Seg> segs_;
-  std::vector<std::pair<uint64_t, uint64_t>> waiters_;  // ranges wait_covered() is blocked on
+  std::vector<Waiter*> waiters_;  // wait_covered() calls blocked on a range (their frames own them)
   bool finished_ = false;
   uint64_t total_ = 0;
   bool failed_ = false;
@@ -1142,6 +1150,15 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     }
     cv_ready.notify_all();
   };
+  // the sender sleeps on one chunk at a time: a hasher wakes it only when it
+  // just finished that chunk (not on every pair, most of which it is not
+  // waiting for yet)
+  size_t sender_wants = SIZE_MAX;
+  auto publish = [&](size_t i, size_t cnt) {
+    std::lock_guard<std::mutex> l(mu);
+    for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
+    if (sender_wants >= i && sender_wants < i + cnt) cv_ready.notify_one();
+  };
   const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : 2;  // chunks per claim
   auto hasher = [&] {
     std::vector<char> scratch(map ? 0 : per * chunk);
@@ -1173,11 +1190,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
             tritondl_hash::sha256_raw(src + j * chunk, mj, dig[i + j].data());
           }
         }
-        {
-          std::lock_guard<std::mutex> l(mu);
-          for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
-        }
-        cv_ready.notify_all();
+        publish(i, cnt);
         continue;
       }
       const size_t cnt = std::min<size_t>(2, n - i);
@@ -1212,11 +1225,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
       } else {
         tritondl_hash::sha256_raw(src[0], m[0], dig[i].data());
       }
-      {
-        std::lock_guard<std::mutex> l(mu);
-        for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
-      }
-      cv_ready.notify_all();
+      publish(i, cnt);
     }
   };
   const int nthreads = static_cast<int>(
@@ -1229,6 +1238,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
   for (size_t c = 0; c < n && r.err.empty(); ++c) {
     {
       std::unique_lock<std::mutex> l(mu);
+      sender_wants = c;
       while (!abort.load() && !ready[c]) {
         if (io.aborted()) {  // the hashers may sit in a flow wait: stop them too
           if (worker_err.empty()) worker_err = "cancelled";
@@ -1237,6 +1247,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
         }
         cv_wait_ms(cv_ready, l, 20);
       }
+      sender_wants = SIZE_MAX;
       if (abort.load()) {
         r.err = worker_err;
         break;
@@ -1632,6 +1643,102 @@ inline VerifyResult recv_verify_chunked(Stream& io, uint64_t raw_len, const char
 // Exact on-the-wire size of an aws-chunked body of `len` payload bytes.
 inline uint64_t chunked_length(uint64_t len, uint64_t chunk) {
   return tritondl_hash::aws_chunk_encoded_size(static_cast<size_t>(len), static_cast<size_t>(chunk), true);
+}
+
+// ---------------------------------------------------------------------------
+// CompletionPort: pumps started on the native task pool report back to ONE
+// event loop through an eventfd, instead of running inside an interpreter
+// executor thread.  An executor hop costs a Python thread wake-up, two GIL
+// hand-offs, a future callback and the loop's self-pipe write (~30-70 µs of
+// CPU); here the pump thread never touches the interpreter, and the loop's
+// reader drains every finished pump per wake-up.  The eventfd is written
+// only when the queue goes from empty to non-empty (the reader takes the
+// whole queue under the same lock), so a burst of completions costs one
+// wake-up.
+class CompletionPort {
+ public:
+  struct Done {
+    uint64_t id = 0;
+    int kind = 0;  // 1 = recv_body, 2 = send_body
+    bool chunked = false;
+    RecvResult rr;
+    SendResult sr;
+  };
+
+  CompletionPort() : efd_(::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)) {
+    if (efd_ < 0) throw std::runtime_error(errno_str("eventfd"));
+  }
+  ~CompletionPort() { ::close(efd_); }
+  CompletionPort(const CompletionPort&) = delete;
+  CompletionPort& operator=(const CompletionPort&) = delete;
+
+  int fd() const { return efd_; }
+  size_t inflight() const { return inflight_.load(); }
+
+  void started() { inflight_.fetch_add(1); }
+  void post(Done&& d) {
+    bool was_empty;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      was_empty = q_.empty();
+      q_.push_back(std::move(d));
+      inflight_.fetch_sub(1);
+    }
+    if (was_empty) {
+      const uint64_t one = 1;
+      ssize_t w;
+      do w = ::write(efd_, &one, sizeof one);
+      while (w < 0 && errno == EINTR);
+    }
+  }
+  // Everything finished so far (clears the eventfd first, so a post racing
+  // with this call re-arms it or lands in this batch).
+  std::vector<Done> reap() {
+    uint64_t v;
+    while (::read(efd_, &v, sizeof v) < 0 && errno == EINTR) {
+    }
+    std::vector<Done> out;
+    std::lock_guard<std::mutex> l(mu_);
+    out.swap(q_);
+    return out;
+  }
+  // Blocks until something is queued or timeout_ms passed (tests / the self-test).
+  bool wait(int timeout_ms) const {
+    pollfd p{efd_, POLLIN, 0};
+    return ::poll(&p, 1, timeout_ms) > 0;
+  }
+
+ private:
+  int efd_;
+  std::atomic<size_t> inflight_{0};
+  std::mutex mu_;
+  std::vector<Done> q_;
+};
+
+// Start a pump on the task pool; `done` is posted to `port` when it returns.
+// The closure owns everything the pump touches (stream and flow by
+// shared_ptr), so the caller may drop its references at once; the file
+// descriptors stay the caller's, who must not close them before the
+// completion (rawhttp.run_pump awaits it even when cancelled).
+template <class Pump>
+inline void start_pump(std::shared_ptr<CompletionPort> port, uint64_t id, int kind, bool chunked, Pump pump,
+                       const char* name) {
+  port->started();
+  tritondl_hash::TaskPool::get().run(
+      1,
+      [port, id, kind, chunked, pump]() mutable {
+        CompletionPort::Done d;
+        d.id = id;
+        d.kind = kind;
+        d.chunked = chunked;
+        try {
+          pump(d);
+        } catch (const std::exception& e) {
+          (kind == 1 ? d.rr.err : d.sr.err) = std::string("native pump failed: ") + e.what();
+        }
+        port->post(std::move(d));
+      },
+      name);
 }
 
 }  // namespace tritondl_relay

@@ -284,6 +284,58 @@ static void test_relay(size_t size) {
   ::unlink(opath);
 }
 
+// Pumps started on the task pool and reaped from a CompletionPort (the
+// worker's path): a receive pump and an aws-chunked send following a Flow
+// that a writer thread advances, with the verifier on a plain thread.
+static void test_port(size_t size) {
+  using namespace tritondl_relay;
+  std::mt19937 rng(23);
+  std::string data(size, '\0');
+  for (auto& c : data) c = static_cast<char>(rng());
+  char path[] = "/tmp/tdl_portXXXXXX";
+  const int wfd = ::mkstemp(path);
+  CHECK(wfd >= 0);
+  CHECK(::ftruncate(wfd, static_cast<off_t>(size)) == 0);
+  int a[2], b[2];
+  CHECK(::socketpair(AF_UNIX, SOCK_STREAM, 0, a) == 0 && ::socketpair(AF_UNIX, SOCK_STREAM, 0, b) == 0);
+  for (int fd : {a[0], a[1], b[0], b[1]}) ::fcntl(fd, F_SETFL, O_NONBLOCK);
+  auto port = std::make_shared<CompletionPort>();
+  auto flow = std::make_shared<Flow>(std::vector<Flow::Seg>{{0, static_cast<int64_t>(size), 0}});
+  auto in = std::make_shared<PlainStream>(a[1]);
+  auto out = std::make_shared<PlainStream>(b[0]);
+  const std::string key(32, 'k'), amz = "20260101T000000Z", scope = "20260101/us-east-1/s3/aws4_request",
+                    seed(64, '0');
+  // origin -> a[0]; the receive pump lands a[1] in the file and advances the flow
+  start_pump(port, 1, 1, false, [=](CompletionPort::Done& d) {
+    d.rr = recv_body(*in, wfd, 0, static_cast<int64_t>(size), "", 0, flow.get(), 0, 0, 10.0, 1u << 20, false);
+  }, "tdl-recv");
+  start_pump(port, 2, 2, false, [=](CompletionPort::Done& d) {
+    d.sr = send_body(*out, "", wfd, 0, size, flow.get(), 1, key, amz, scope, seed, 65536, 3, 10.0);
+  }, "tdl-send");
+  VerifyResult vr;
+  PlainStream sink(b[1]);
+  std::thread verifier([&] {
+    vr = recv_verify_chunked(sink, chunked_length(size, 65536), "", 0, key, amz, scope, seed, true, 2, 10.0);
+  });
+  std::string e;
+  PlainStream src(a[0]);
+  CHECK(send_all(src, data.data(), data.size(), 10.0, nullptr, &e));
+  std::vector<CompletionPort::Done> done;
+  while (done.size() < 2) {
+    CHECK(port->wait(10000));
+    for (auto& d : port->reap()) done.push_back(std::move(d));
+  }
+  verifier.join();
+  CHECK(port->inflight() == 0);
+  for (const auto& d : done) {
+    if (d.id == 1) CHECK(d.kind == 1 && d.rr.err.empty() && d.rr.received == size);
+    if (d.id == 2) CHECK(d.kind == 2 && d.sr.err.empty() && d.sr.sent == size);
+  }
+  CHECK(vr.err.empty() && vr.data == data);
+  for (int fd : {a[0], a[1], b[0], b[1], wfd}) ::close(fd);
+  ::unlink(path);
+}
+
 // The same pumps over TLS (OpenSSL streams, batched ciphertext flushes): a
 // handshake on two threads, then aws-chunked send/verify and plain
 // send/receive following a Flow, plus an abort of a pump waiting for bytes.
@@ -561,6 +613,7 @@ int main(int argc, char** argv) {
   test_merkle();
   test_relay(quick ? (3u << 20) + 777 : (8u << 20) + 777);
   test_relay(0);
+  test_port(quick ? (2u << 20) + 99 : (6u << 20) + 99);
   test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);

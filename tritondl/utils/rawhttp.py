@@ -22,6 +22,7 @@ from __future__ import annotations
 import asyncio
 import os
 import socket
+import weakref
 from dataclasses import dataclass, field
 
 from multidict import CIMultiDict
@@ -505,15 +506,81 @@ def _counted(fn, *args):
             _active_pumps -= 1
 
 
+class _Port:
+    """One event loop's ``_relay.CompletionPort``: relay pumps run on the
+    native task pool and finish into it; the loop's reader on the port's
+    eventfd resolves their futures (every pump finished since the last wake
+    in one pass).  No interpreter thread is involved, unlike an executor
+    hop (a Python thread wake-up, two GIL hand-offs and the loop's self-pipe
+    per pump)."""
+
+    def __init__(self, loop, relay) -> None:
+        self.port = relay.CompletionPort()
+        self.futs: dict[int, asyncio.Future] = {}
+        self.next_id = 0
+        self.start = {relay.recv_body: relay.start_recv_body, relay.send_body: relay.start_send_body}
+        loop.add_reader(self.port.fileno(), self._drain)
+
+    def _drain(self) -> None:
+        global _active_pumps
+        for pid, res in self.port.reap():
+            fut = self.futs.pop(pid, None)
+            with _active_lock:
+                _active_pumps -= 1
+            if fut is not None and not fut.done():
+                fut.set_result(res)
+
+    def submit(self, loop, fn, native, args) -> "asyncio.Future | None":
+        start = self.start.get(fn)
+        if start is None:
+            return None
+        global _active_pumps
+        self.next_id += 1
+        pid = self.next_id
+        fut = loop.create_future()
+        with _active_lock:
+            _active_pumps += 1
+        try:
+            start(self.port, pid, native, *args)
+        except BaseException:
+            with _active_lock:
+                _active_pumps -= 1
+            raise
+        self.futs[pid] = fut
+        return fut
+
+
+_ports: weakref.WeakKeyDictionary = weakref.WeakKeyDictionary()
+
+
+def _native_pumps() -> bool:
+    return os.environ.get("TRITONDL_RELAY_PORT", "1").lower() not in ("0", "off", "false", "no")
+
+
+def _port(loop) -> "_Port | None":
+    p = _ports.get(loop)
+    if p is None:
+        relay = relay_module()
+        if relay is None or not hasattr(relay, "CompletionPort") or not _native_pumps():
+            return None
+        p = _ports[loop] = _Port(loop, relay)
+    return p
+
+
 async def run_pump(conn: RawConn, fn, *args):
-    """Run a relay pump ``fn(conn.native, *args)`` in an executor thread.
+    """Run a relay pump ``fn(conn.native, *args)``: ``recv_body`` /
+    ``send_body`` on the native task pool through the loop's completion port
+    (``TRITONDL_RELAY_PORT=0``: an executor thread, as for any other ``fn``).
 
     If the awaiting task is cancelled, the pump is aborted (sticky native flag
     + socket shutdown, fd left open) and awaited to completion before the
     cancellation propagates — so the caller's ``finally`` can never close a
     socket or file the pump is still using (fd numbers are reused)."""
     loop = asyncio.get_running_loop()
-    fut = loop.run_in_executor(None, _counted, fn, conn.native, *args)
+    port = _port(loop)
+    fut = port.submit(loop, fn, conn.native, args) if port is not None else None
+    if fut is None:
+        fut = loop.run_in_executor(None, _counted, fn, conn.native, *args)
     try:
         return await asyncio.shield(fut)
     except asyncio.CancelledError:
