@@ -1,8 +1,9 @@
 #!/bin/bash
-# Relay A/B in one session, alternated: "old" = ab/_relay_a.so (pumps on
-# executor threads, every hasher woken per flow advance), "flow" = the new
-# build with TRITONDL_RELAY_PORT=0 (targeted flow/sender wake-ups only),
-# "port" = the new build, pumps on the native pool reaped via an eventfd.
+# Relay A/B in one session, alternated:
+#   old    ab/_relay_a.so: pumps on executor threads, every hasher woken per flow advance
+#   flow   new build, TRITONDL_RELAY_PORT=0, no hasher cap: targeted wake-ups only
+#   port   new build, no hasher cap: + pumps on the native pool, reaped via an eventfd
+#   cap    new build defaults: + 2 hashers while the PUT follows a download
 set -o pipefail
 OUT=${OUT:-gpurun_out/r03_port_ab}
 mkdir -p $OUT
@@ -20,14 +21,15 @@ pool() {
     > $OUT/pool_$name.log 2>&1 || return $?
 }
 for rep in 1 2 3; do
-  use a && head old$rep && use b && head flow$rep TRITONDL_RELAY_PORT=0 && head port$rep TRITONDL_RELAY_PORT=1 || exit $?
+  use a && head old$rep && use b && head flow$rep TRITONDL_RELAY_PORT=0 TRITONDL_RELAY_FOLLOW_HASHERS=0 &&
+    head port$rep TRITONDL_RELAY_FOLLOW_HASHERS=0 && head cap$rep || exit $?
 done
 for rep in 1 2; do
-  use a && pool old$rep && use b && pool flow$rep TRITONDL_RELAY_PORT=0 && pool port$rep TRITONDL_RELAY_PORT=1 || exit $?
+  use a && pool old$rep && use b && pool port$rep TRITONDL_RELAY_FOLLOW_HASHERS=0 && pool cap$rep || exit $?
 done
 for f in $OUT/head_*.log $OUT/pool_*.log; do
   n=$(basename $f .log)
   echo "$n $(grep -o '"value": [0-9.]*' $f | head -1) $(grep -o '"cpu_ms_per_job[^}]*' $f) $(grep -o '"job_latency_ms_p50": [0-9.]*' $f)"
-  [ -f $OUT/${n#head_}.prof.txt ] && grep -A5 'cpu by thread class' $OUT/${n#head_}.prof.txt | tail -5
+  [ -f $OUT/${n#head_}.prof.txt ] && grep -A6 'cpu by thread class' $OUT/${n#head_}.prof.txt | tail -6
 done
 exit 0
