@@ -309,7 +309,10 @@ class TaskPool {
       ++threads_;
       std::thread([this] { loop(); }).detach();
     }
-    cv_.notify_all();
+    // one parked thread per task: notify_all woke every parked thread (a
+    // dozen once pumps and hashers share the pool) to fight over mu_ for
+    // one or two tasks
+    for (int k = 0; k < copies; ++k) cv_.notify_one();
     return g;
   }
   size_t threads() const {
@@ -326,6 +329,7 @@ class TaskPool {
   static constexpr size_t max_idle = 64;
 
   void loop() {
+    const char* named = nullptr;
     std::unique_lock<std::mutex> l(mu_);
     for (;;) {
       cv_.wait(l, [&] { return !q_.empty(); });
@@ -333,7 +337,10 @@ class TaskPool {
       q_.erase(q_.begin());
       --idle_;
       l.unlock();
-      name_thread(t.name);
+      if (t.name != named) {  // pthread_setname_np is a write to /proc: only on a change of task kind
+        name_thread(t.name);
+        named = t.name;
+      }
       (*t.fn)();
       {
         std::lock_guard<std::mutex> gl(t.g->mu);

@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 SO=tritondl/_relay.cpython-310-x86_64-linux-gnu.so
 use() { cp ab/_relay_$1.so $SO || exit 1; }
-head() {  # name env...
+hd() {  # name env...
   local name=$1; shift
   env "$@" timeout -k 10 200 python bench.py --steps 300 --warmup 10 --no-gpu-probe --cpuprofile $OUT/$name.prof \
     > $OUT/head_$name.log 2>&1 || return $?
@@ -21,8 +21,8 @@ pool() {
     > $OUT/pool_$name.log 2>&1 || return $?
 }
 for rep in 1 2 3; do
-  use a && head old$rep && use b && head flow$rep TRITONDL_RELAY_PORT=0 TRITONDL_RELAY_FOLLOW_HASHERS=0 &&
-    head port$rep TRITONDL_RELAY_FOLLOW_HASHERS=0 && head cap$rep || exit $?
+  use a && hd old$rep && use b && hd flow$rep TRITONDL_RELAY_PORT=0 TRITONDL_RELAY_FOLLOW_HASHERS=0 &&
+    hd port$rep TRITONDL_RELAY_FOLLOW_HASHERS=0 && hd cap$rep || exit $?
 done
 for rep in 1 2; do
   use a && pool old$rep && use b && pool port$rep TRITONDL_RELAY_FOLLOW_HASHERS=0 && pool cap$rep || exit $?
