@@ -1086,22 +1086,6 @@ inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle
   return true;
 }
 
-// Hashers for a PUT that follows a download still landing: they cannot hash
-// faster than the bytes arrive, and two SHA-NI cores (~7 GB/s) outrun the
-// receive pump, so more only wait and wake (measured +0.6 ms of CPU per
-// 10 MiB job for 4 vs 2, profiles/r03_cost/SUMMARY.md).  A PUT of a file
-// already on disk keeps the configured count.  TRITONDL_RELAY_FOLLOW_HASHERS
-// overrides (0 = no cap).
-inline int follow_hashers() {
-  static const int n = [] {
-    const char* v = std::getenv("TRITONDL_RELAY_FOLLOW_HASHERS");
-    if (!v || !*v) return 2;
-    const int k = std::atoi(v);
-    return k <= 0 ? INT_MAX : k;
-  }();
-  return n;
-}
-
 // send_chunked_zc: the aws-chunked body over a PLAIN socket with no payload
 // copy through user space.  send_chunked reads every chunk into a ring
 // (pread: one 10 MiB copy per 10 MiB job) and writev's the ring into the
@@ -1244,9 +1228,8 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
       publish(i, cnt);
     }
   };
-  int want = threads <= 0 ? 4 : threads;
-  if (!gpu && flow && !flow->finished()) want = std::min(want, follow_hashers());
-  const int nthreads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, (n + per - 1) / per)));
+  const int nthreads = static_cast<int>(
+      std::max<size_t>(1, std::min<size_t>(threads <= 0 ? 4 : threads, (n + per - 1) / per)));
   std::shared_ptr<tritondl_hash::TaskPool::Group> pool;
   if (n) pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, gpu ? "tdl-gpu-sha256" : "tdl-sha256");
 

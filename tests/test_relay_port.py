@@ -61,9 +61,11 @@ def test_port_results_keep_the_chunked_form(tmp_path):
         b.close()
 
 
-def test_run_pump_uses_the_port_and_cancel_waits_for_the_pump(tmp_path):
+def test_run_pump_uses_the_port_and_cancel_waits_for_the_pump(tmp_path, monkeypatch):
     """A cancelled run_pump aborts the native pump and returns only once it
     finished, so the caller may close the fd right after."""
+    monkeypatch.setenv("TRITONDL_RELAY_PORT", "1")
+
     async def main():
         a, b = socket.socketpair()
         b.setblocking(False)
@@ -91,8 +93,8 @@ def test_run_pump_uses_the_port_and_cancel_waits_for_the_pump(tmp_path):
     asyncio.run(asyncio.wait_for(main(), 30))
 
 
-def test_run_pump_executor_fallback(tmp_path, monkeypatch):
-    monkeypatch.setenv("TRITONDL_RELAY_PORT", "0")
+def test_run_pump_executor_by_default(tmp_path, monkeypatch):
+    monkeypatch.delenv("TRITONDL_RELAY_PORT", raising=False)
 
     async def main():
         a, b = socket.socketpair()

@@ -554,7 +554,10 @@ _ports: weakref.WeakKeyDictionary = weakref.WeakKeyDictionary()
 
 
 def _native_pumps() -> bool:
-    return os.environ.get("TRITONDL_RELAY_PORT", "1").lower() not in ("0", "off", "false", "no")
+    # opt-in: in isolation a port-started send pump is ~8 % faster than one on
+    # an executor thread (profiles/r03_port_ab/upab), but whole headline jobs
+    # measured slower on the box with it (profiles/r03_port_ab/SUMMARY.md)
+    return os.environ.get("TRITONDL_RELAY_PORT", "0").lower() in ("1", "on", "true", "yes")
 
 
 def _port(loop) -> "_Port | None":
@@ -568,9 +571,9 @@ def _port(loop) -> "_Port | None":
 
 
 async def run_pump(conn: RawConn, fn, *args):
-    """Run a relay pump ``fn(conn.native, *args)``: ``recv_body`` /
-    ``send_body`` on the native task pool through the loop's completion port
-    (``TRITONDL_RELAY_PORT=0``: an executor thread, as for any other ``fn``).
+    """Run a relay pump ``fn(conn.native, *args)`` in an executor thread, or
+    with ``TRITONDL_RELAY_PORT=1`` (``recv_body`` / ``send_body``) on the
+    native task pool through the loop's completion port.
 
     If the awaiting task is cancelled, the pump is aborted (sticky native flag
     + socket shutdown, fd left open) and awaited to completion before the
