@@ -14,8 +14,10 @@ HMAC/SHA-256 of chunk chains run in the native C++ module (OpenSSL SHA-NI).
 from __future__ import annotations
 
 import datetime as _dt
+import functools
 import hashlib
 import hmac
+import re
 from dataclasses import dataclass
 from urllib.parse import quote
 
@@ -29,8 +31,15 @@ STREAM_CHUNK = 64 * 1024
 SIGN_THREADS = 4
 
 
+_PLAIN = re.compile(r"[A-Za-z0-9\-_.~]*")
+_PLAIN_PATH = re.compile(r"[A-Za-z0-9\-_.~/]*")
+
+
 def uri_encode(s: str, encode_slash: bool = True) -> str:
-    """AWS UriEncode: unreserved = A-Za-z0-9-._~ ; uppercase hex escapes."""
+    """AWS UriEncode: unreserved = A-Za-z0-9-._~ ; uppercase hex escapes.
+    Strings with nothing to escape (most object keys) skip ``quote``."""
+    if (_PLAIN if encode_slash else _PLAIN_PATH).fullmatch(s):
+        return s
     return quote(s, safe="-_.~" if encode_slash else "-_.~/")
 
 
@@ -46,7 +55,10 @@ def _trim(v: str) -> str:
     return " ".join(str(v).strip().split())
 
 
+@functools.lru_cache(maxsize=16)
 def signing_key(secret: str, date: str, region: str, service: str = "s3") -> bytes:
+    """The derived key changes once a day per credential and region (four
+    HMACs per request otherwise), so it is cached."""
     k = hmac.new(("AWS4" + secret).encode(), date.encode(), hashlib.sha256).digest()
     k = hmac.new(k, region.encode(), hashlib.sha256).digest()
     k = hmac.new(k, service.encode(), hashlib.sha256).digest()
