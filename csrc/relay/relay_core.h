@@ -1159,11 +1159,28 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     for (size_t j = 0; j < cnt; ++j) ready[i + j] = 1;
     if (sender_wants >= i && sender_wants < i + cnt) cv_ready.notify_one();
   };
-  const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : 2;  // chunks per claim
+  // Chunks per claim: 16 for the 16-lane AVX-512 kernel, else an SHA-NI
+  // pair.  The last 32 chunks always go in pairs: a 16-chunk claim cannot
+  // start before its last byte lands, so near the end of a download it would
+  // leave 1 MiB to hash on one core after the transfer; pairs spread that
+  // over the hashers.
+  const size_t wide = gpu ? 0 : tritondl_hash::sha256_claim();
+  const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : wide;
+  auto claim = [&](size_t* take) {
+    if (gpu || wide <= 2) {
+      *take = per;
+      return next.fetch_add(per);
+    }
+    size_t i = next.load();
+    do *take = i + wide + 32 <= n ? wide : 2;
+    while (!next.compare_exchange_weak(i, i + *take));
+    return i;
+  };
   auto hasher = [&] {
     std::vector<char> scratch(map ? 0 : per * chunk);
     for (;;) {
-      const size_t i = next.fetch_add(per);
+      size_t take = 0;
+      const size_t i = claim(&take);
       if (i >= n || abort.load()) return;
       if (gpu) {
         const size_t cnt = std::min(per, n - i);
@@ -1193,13 +1210,16 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
         publish(i, cnt);
         continue;
       }
-      const size_t cnt = std::min<size_t>(2, n - i);
+      const size_t cnt = std::min(take, n - i);
       const uint64_t a = off + static_cast<uint64_t>(i) * chunk;
-      size_t m[2] = {0, 0};
-      for (size_t j = 0; j < cnt; ++j)
+      size_t m[16] = {0};
+      uint64_t span = 0;
+      for (size_t j = 0; j < cnt; ++j) {
         m[j] = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(i + j) * chunk));
+        span += m[j];
+      }
       if (flow) {
-        const int w = flow->wait_covered(a, a + m[0] + m[1], idle_timeout, &abort);
+        const int w = flow->wait_covered(a, a + span, idle_timeout, &abort);
         if (w) {
           if (!abort.load())
             set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
@@ -1207,7 +1227,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
           return;
         }
       }
-      const char* src[2];
+      const void* src[16];
       for (size_t j = 0; j < cnt; ++j) {
         if (map) {
           src[j] = map + (a + j * chunk - base);
@@ -1220,11 +1240,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
           src[j] = d;
         }
       }
-      if (cnt == 2) {
-        tritondl_hash::sha256_pair(src[0], m[0], src[1], m[1], dig[i].data(), dig[i + 1].data());
-      } else {
-        tritondl_hash::sha256_raw(src[0], m[0], dig[i].data());
-      }
+      tritondl_hash::sha256_batch(src, m, cnt, dig[i].data());
       publish(i, cnt);
     }
   };
@@ -1501,30 +1517,41 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
   std::condition_variable cv_pub, cv_ready;
   size_t published = 0;  // guarded by mu
   bool parse_done = false, stop = false;
-  std::atomic<size_t> next{0};
   bool final_seen = false;
 
-  // frames in pairs (SHA-NI lockstep): a hasher waits until both of its
-  // frames are published, or takes the last one alone once parsing is done
+  // Frames are claimed in pairs (SHA-NI lockstep) as they are published, or
+  // 16 at a time for the AVX-512 kernel once the hashers have fallen behind
+  // (a backlog of >= 32 frames): then throughput is what counts, while
+  // hashers keeping up with the receiver stay on pairs, so the last frame's
+  // hash still lands right after its bytes.
+  size_t claimed = 0;  // guarded by mu
+  const size_t wide = tritondl_hash::sha256_claim();
   auto hasher = [&] {
     for (;;) {
-      const size_t j = next.fetch_add(2);
-      size_t cnt;
+      size_t j, cnt;
       {
         std::unique_lock<std::mutex> l(mu);
-        cv_pub.wait(l, [&] { return stop || j + 1 < published || parse_done; });
-        if (stop || j >= published) return;
-        cnt = j + 1 < published ? 2 : 1;
+        cv_pub.wait(l, [&] { return stop || parse_done || published >= claimed + 2; });
+        if (stop || published == claimed) return;  // (parse done: nothing left)
+        const size_t avail = published - claimed;
+        cnt = wide > 2 && avail >= 2 * wide ? wide : std::min<size_t>(2, avail);
+        j = claimed;
+        claimed += cnt;
       }
-      StreamFrame& f = frame(j);
-      if (cnt == 2) {
-        StreamFrame& g = frame(j + 1);
-        tritondl_hash::sha256_pair(raw + f.off, f.n, raw + g.off, g.n, f.h, g.h);
-        g.ready.store(1, std::memory_order_release);
-      } else {
-        tritondl_hash::sha256_raw(raw + f.off, f.n, f.h);
+      const void* p[16];
+      size_t n[16];
+      unsigned char d[16 * 32];
+      for (size_t k = 0; k < cnt; ++k) {
+        const StreamFrame& f = frame(j + k);
+        p[k] = raw + f.off;
+        n[k] = f.n;
       }
-      f.ready.store(1, std::memory_order_release);
+      tritondl_hash::sha256_batch(p, n, cnt, d);
+      for (size_t k = 0; k < cnt; ++k) {
+        StreamFrame& f = frame(j + k);
+        std::memcpy(f.h, d + 32 * k, 32);
+        f.ready.store(1, std::memory_order_release);
+      }
       {
         std::lock_guard<std::mutex> l(mu);  // pairs with the checker's wait
       }

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../hash/hash_core.h"
+#include "../hash/sha256_mb.h"
 
 namespace {
 
@@ -105,9 +106,21 @@ void report(const char* name, const Stat& s) {
   std::fflush(stdout);
 }
 
+void hash_x16(const char* p, size_t len) {
+  unsigned char d[16 * 32];
+  const size_t n = len / kChunk;
+  size_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    const void* m[16];
+    for (int j = 0; j < 16; ++j) m[j] = p + (i + j) * kChunk;
+    tritondl_hash::sha16::sha256_x16(m, kChunk, d);
+  }
+  if (i < n) hash_pairs(p + i * kChunk, len - i * kChunk);
+}
+
 void probe_sha_hot(int reps) {
   std::vector<char> b(kLen, 'x');
-  Stat s;
+  Stat s, s16;
   hash_pairs(b.data(), kLen);
   for (int r = 0; r < reps; ++r) {
     const double c = thread_ms(), w = wall_ms();
@@ -115,6 +128,14 @@ void probe_sha_hot(int reps) {
     s.add(thread_ms() - c, wall_ms() - w);
   }
   report("sha_hot", s);
+  if (!tritondl_hash::sha16::cpu_has_avx512()) return;
+  hash_x16(b.data(), kLen);
+  for (int r = 0; r < reps; ++r) {
+    const double c = thread_ms(), w = wall_ms();
+    hash_x16(b.data(), kLen);
+    s16.add(thread_ms() - c, wall_ms() - w);
+  }
+  report("sha_hot_x16", s16);
 }
 
 void probe_file(int reps) {

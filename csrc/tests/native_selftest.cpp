@@ -71,6 +71,30 @@ static void test_sha256_pair() {
   }
 }
 
+// 16-lane AVX-512 SHA-256 (sha256_mb.h) and the batch dispatcher against
+// OpenSSL: every length class of the padding (0, < 56, 56..63, whole
+// blocks, 64 KiB chunks), equal-length runs of 16 and mixed batches that
+// fall back to pairs part-way.
+static void test_sha256_batch() {
+  std::mt19937 rng(29);
+  std::string buf(40 * 70000, '\0');
+  for (auto& c : buf) c = char(rng());
+  for (int it = 0; it < 60; ++it) {
+    const size_t n = it < 20 ? 16 : 1 + rng() % 40;
+    const size_t base = it < 12 ? size_t(it * 7) : it < 20 ? size_t(65536) : 1 + rng() % 70000;
+    std::vector<const void*> p(n);
+    std::vector<size_t> len(n);
+    for (size_t i = 0; i < n; ++i) {
+      p[i] = buf.data() + (rng() % 64) + i * 70000;
+      len[i] = (it % 3 == 2 && i == n / 2) ? base / 2 : base;  // one odd length breaks a run
+    }
+    std::vector<unsigned char> out(32 * n);
+    sha256_batch(p.data(), len.data(), n, out.data());
+    for (size_t i = 0; i < n; ++i)
+      CHECK(std::string(reinterpret_cast<char*>(&out[32 * i]), 32) == one_shot(sha256_md(), p[i], len[i]));
+  }
+}
+
 static void test_aws_chunked() {
   // AWS S3 SigV4 streaming example: 66560 bytes of 'a', 64 KiB chunks
   const std::string key = signing_key("wJalrXUtnFEMI/K7MDENG/bPxRfiCYEXAMPLEKEY", "20130524");
@@ -608,6 +632,7 @@ int main(int argc, char** argv) {
   bool quick = argc > 1 && std::string(argv[1]) == "--quick";
   test_vectors();
   test_sha256_pair();
+  test_sha256_batch();
   test_aws_chunked();
   test_pieces_and_verify();
   test_merkle();
