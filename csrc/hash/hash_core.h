@@ -517,23 +517,19 @@ inline std::vector<std::string> chunk_hashes(const char* data, size_t len, size_
   const size_t per_thread = (1u << 20) / chunk_size + 1;  // >= ~1 MiB of hashing per thread
   const int t = threads <= 0 ? default_threads() : threads;
   const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, nfull / per_thread)));
-  // chunks in pairs: SHA-NI hashes both in lockstep
-  parallel_for((n + 1) / 2, used, [&](size_t k) {
-    unsigned char d[2][32];
-    const char* p[2];
-    size_t m[2];
-    const size_t cnt = std::min<size_t>(2, n - 2 * k);
+  // chunks in groups of 16 (the AVX-512 kernel; SHA-NI pairs without it)
+  parallel_for((n + 15) / 16, used, [&](size_t k) {
+    unsigned char d[16 * 32];
+    const void* p[16];
+    size_t m[16];
+    const size_t cnt = std::min<size_t>(16, n - 16 * k);
     for (size_t j = 0; j < cnt; ++j) {
-      const size_t off = (2 * k + j) * chunk_size;
+      const size_t off = (16 * k + j) * chunk_size;
       m[j] = off < len ? std::min(chunk_size, len - off) : 0;
       p[j] = m[j] ? data + off : "";
     }
-    if (cnt == 2) {
-      sha256_pair(p[0], m[0], p[1], m[1], d[0], d[1]);
-    } else {
-      sha256_raw(p[0], m[0], d[0]);
-    }
-    for (size_t j = 0; j < cnt; ++j) h[2 * k + j] = hex_raw(d[j], 32);
+    sha256_batch(p, m, cnt, d);
+    for (size_t j = 0; j < cnt; ++j) h[16 * k + j] = hex_raw(d + 32 * j, 32);
   });
   return h;
 }
@@ -603,24 +599,20 @@ inline std::string aws_chunk_encode(const std::string& key, const std::string& a
     *w++ = '\r';
     *w++ = '\n';
   };
-  parallel_for((n + 1) / 2, used, [&](size_t k) {  // chunk pairs: SHA-NI hashes both in lockstep
-    const size_t cnt = std::min<size_t>(2, n - 2 * k);
-    const char* p[2];
-    size_t m[2];
-    unsigned char d[2][32];
+  parallel_for((n + 15) / 16, used, [&](size_t k) {  // groups of 16 chunks (sha256_batch)
+    const size_t cnt = std::min<size_t>(16, n - 16 * k);
+    const void* p[16];
+    size_t m[16];
+    unsigned char d[16 * 32];
     for (size_t j = 0; j < cnt; ++j) {
-      const size_t i = 2 * k + j;
+      const size_t i = 16 * k + j;
       m[j] = i < nfull ? std::min(chunk_size, len - i * chunk_size) : 0;
       p[j] = m[j] ? data + i * chunk_size : "";
     }
-    if (cnt == 2) {
-      sha256_pair(p[0], m[0], p[1], m[1], d[0], d[1]);
-    } else {
-      sha256_raw(p[0], m[0], d[0]);
-    }
+    sha256_batch(p, m, cnt, d);
     for (size_t j = 0; j < cnt; ++j) {
-      h[2 * k + j] = hex_raw(d[j], 32);
-      write_frame(2 * k + j, p[j], m[j]);
+      h[16 * k + j] = hex_raw(d + 32 * j, 32);
+      write_frame(16 * k + j, static_cast<const char*>(p[j]), m[j]);
     }
   });
   SigChain chain(key, amzdate, scope, prev);
@@ -675,20 +667,21 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
   std::vector<size_t> dst_off(frames.size() + 1, 0);
   for (size_t i = 0; i < frames.size(); ++i) dst_off[i + 1] = dst_off[i] + frames[i].n;
   const size_t nf = frames.size();
-  parallel_for((nf + 1) / 2, used, [&](size_t k) {  // frame pairs: SHA-NI lockstep
-    const size_t i = 2 * k;
-    const Frame& a = frames[i];
-    unsigned char d[2][32];
-    if (i + 1 < nf) {
-      const Frame& b = frames[i + 1];
-      sha256_pair(raw + a.off, a.n, raw + b.off, b.n, d[0], d[1]);
-      h[i + 1] = hex_raw(d[1], 32);
-      if (decoded && b.n) std::memcpy(&(*decoded)[dst_off[i + 1]], raw + b.off, b.n);
-    } else {
-      sha256_raw(raw + a.off, a.n, d[0]);
+  parallel_for((nf + 15) / 16, used, [&](size_t k) {  // groups of 16 frames (sha256_batch)
+    const size_t i0 = 16 * k, cnt = std::min<size_t>(16, nf - i0);
+    const void* p[16];
+    size_t m[16];
+    unsigned char d[16 * 32];
+    for (size_t j = 0; j < cnt; ++j) {
+      p[j] = raw + frames[i0 + j].off;
+      m[j] = frames[i0 + j].n;
     }
-    h[i] = hex_raw(d[0], 32);
-    if (decoded && a.n) std::memcpy(&(*decoded)[dst_off[i]], raw + a.off, a.n);
+    sha256_batch(p, m, cnt, d);
+    for (size_t j = 0; j < cnt; ++j) {
+      const Frame& a = frames[i0 + j];
+      h[i0 + j] = hex_raw(d + 32 * j, 32);
+      if (decoded && a.n) std::memcpy(&(*decoded)[dst_off[i0 + j]], raw + a.off, a.n);
+    }
   });
   SigChain chain(key, amzdate, scope, seed);
   for (size_t i = 0; i < frames.size(); ++i) {
@@ -707,21 +700,23 @@ inline std::string aws_chunk_decode(const std::string& key, const std::string& a
 constexpr size_t kMerkleLeaf = 16384;
 
 inline void merkle_reduce(std::vector<unsigned char>& row, size_t width) {
-  // row holds `width` 32-byte nodes; reduce in place to row[0..32).  Node
-  // pairs are hashed two at a time (SHA-NI lockstep); writing node k only
-  // touches bytes [32k, 32k+32), which nodes >= k have already been read from.
-  unsigned char h[2][32];
+  // row holds `width` 32-byte nodes; reduce in place to row[0..32).  Parent
+  // nodes are hashed 16 at a time (sha256_batch: the AVX-512 kernel, or
+  // SHA-NI pairs); a group's outputs land in [32k, 32k+512) only after all
+  // of its inputs [64k, 64k+1024) were read, and later groups read above that.
+  unsigned char h[16 * 32];
+  const void* p[16];
+  size_t m[16];
   while (width > 1) {
     const size_t half = width / 2;
-    size_t k = 0;
-    for (; k + 1 < half; k += 2) {
-      sha256_pair(row.data() + 64 * k, 64, row.data() + 64 * (k + 1), 64, h[0], h[1]);
-      std::memcpy(row.data() + 32 * k, h[0], 32);
-      std::memcpy(row.data() + 32 * (k + 1), h[1], 32);
-    }
-    if (k < half) {
-      sha256_raw(row.data() + 64 * k, 64, h[0]);
-      std::memcpy(row.data() + 32 * k, h[0], 32);
+    for (size_t k = 0; k < half; k += 16) {
+      const size_t cnt = std::min<size_t>(16, half - k);
+      for (size_t j = 0; j < cnt; ++j) {
+        p[j] = row.data() + 64 * (k + j);
+        m[j] = 64;
+      }
+      sha256_batch(p, m, cnt, h);
+      std::memcpy(row.data() + 32 * k, h, 32 * cnt);
     }
     width = half;
   }
@@ -807,15 +802,19 @@ inline std::string merkle_verify(const std::vector<std::pair<std::string, long l
     const size_t width = static_cast<size_t>(widths[p]);
     if (width == 0 || (width & (width - 1)) || nl > width) return;
     std::vector<unsigned char> row(32 * width, 0);
-    for (size_t k = 0; k < nl; k += 2) {  // leaves in pairs (SHA-NI lockstep)
-      const size_t off = k * kMerkleLeaf;
-      const size_t len = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off);
-      if (k + 1 < nl) {
-        const size_t len2 = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off - kMerkleLeaf);
-        md_pair(md, buf.data() + off, len, buf.data() + off + kMerkleLeaf, len2, row.data() + 32 * k,
-                row.data() + 32 * (k + 1));
+    for (size_t k = 0; k < nl; k += 16) {  // leaves 16 at a time (sha256_batch)
+      const size_t cnt = std::min<size_t>(16, nl - k);
+      const void* lp[16];
+      size_t ll[16];
+      for (size_t j = 0; j < cnt; ++j) {
+        const size_t off = (k + j) * kMerkleLeaf;
+        lp[j] = buf.data() + off;
+        ll[j] = std::min(kMerkleLeaf, static_cast<size_t>(plen) - off);
+      }
+      if (md == sha256_md()) {
+        sha256_batch(lp, ll, cnt, row.data() + 32 * k);
       } else {
-        md_raw(md, buf.data() + off, len, row.data() + 32 * k);
+        for (size_t j = 0; j < cnt; ++j) md_raw(md, lp[j], ll[j], row.data() + 32 * (k + j));
       }
     }
     merkle_reduce(row, width);

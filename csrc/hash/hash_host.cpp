@@ -262,15 +262,16 @@ PYBIND11_MODULE(_hash_host, m) {
         std::vector<unsigned char> row(32 * width, 0);
         {
           py::gil_scoped_release nogil;
-          for (size_t k = 0; k < nl; k += 2) {  // leaves in SHA-NI pairs
-            const size_t off = k * kMerkleLeaf, len = std::min(kMerkleLeaf, v.len - off);
-            if (k + 1 < nl) {
-              const size_t len2 = std::min(kMerkleLeaf, v.len - off - kMerkleLeaf);
-              sha256_pair(v.ptr + off, len, v.ptr + off + kMerkleLeaf, len2, row.data() + 32 * k,
-                          row.data() + 32 * (k + 1));
-            } else {
-              sha256_raw(v.ptr + off, len, row.data() + 32 * k);
+          for (size_t k = 0; k < nl; k += 16) {  // leaves 16 at a time (sha256_batch)
+            const size_t cnt = std::min<size_t>(16, nl - k);
+            const void* lp[16];
+            size_t ll[16];
+            for (size_t j = 0; j < cnt; ++j) {
+              const size_t off = (k + j) * kMerkleLeaf;
+              lp[j] = v.ptr + off;
+              ll[j] = std::min(kMerkleLeaf, v.len - off);
             }
+            sha256_batch(lp, ll, cnt, row.data() + 32 * k);
           }
           merkle_reduce(row, width);
         }
