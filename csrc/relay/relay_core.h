@@ -1086,6 +1086,18 @@ inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle
   return true;
 }
 
+// Leading chunks of a PUT that follows a download hashed in pairs before the
+// 16-wide claims start: the sender cannot send chunk 0 before its digest,
+// and a 16-chunk claim's digests come ~0.2 ms after its last byte lands
+// (one 64 KiB chain per lane).  TRITONDL_SHA_MB_HEAD overrides (chunks).
+inline size_t zc_head_pairs() {
+  static const size_t n = [] {
+    const char* v = std::getenv("TRITONDL_SHA_MB_HEAD");
+    return v && *v ? static_cast<size_t>(std::strtoul(v, nullptr, 10)) : size_t(32);
+  }();
+  return n;
+}
+
 // send_chunked_zc: the aws-chunked body over a PLAIN socket with no payload
 // copy through user space.  send_chunked reads every chunk into a ring
 // (pread: one 10 MiB copy per 10 MiB job) and writev's the ring into the
@@ -1166,13 +1178,14 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
   // over the hashers.
   const size_t wide = gpu ? 0 : tritondl_hash::sha256_claim();
   const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : wide;
+  const size_t head = flow ? zc_head_pairs() : 0;
   auto claim = [&](size_t* take) {
     if (gpu || wide <= 2) {
       *take = per;
       return next.fetch_add(per);
     }
     size_t i = next.load();
-    do *take = i + wide + 32 <= n ? wide : 2;
+    do *take = i >= head && i + wide + 32 <= n ? wide : 2;
     while (!next.compare_exchange_weak(i, i + *take));
     return i;
   };
