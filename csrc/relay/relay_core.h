@@ -1178,14 +1178,14 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
   // over the hashers.
   const size_t wide = gpu ? 0 : tritondl_hash::sha256_claim();
   const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : wide;
-  const size_t head = flow ? zc_head_pairs() : 0;
+  const size_t lead = flow ? zc_head_pairs() : 0;
   auto claim = [&](size_t* take) {
     if (gpu || wide <= 2) {
       *take = per;
       return next.fetch_add(per);
     }
     size_t i = next.load();
-    do *take = i >= head && i + wide + 32 <= n ? wide : 2;
+    do *take = i >= lead && i + wide + 32 <= n ? wide : 2;
     while (!next.compare_exchange_weak(i, i + *take));
     return i;
   };
