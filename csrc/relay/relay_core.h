@@ -1089,9 +1089,11 @@ inline bool sendfile_all(Stream& io, int fd, uint64_t o, uint64_t n, double idle
 // Where a PUT that follows a download hashes in SHA-NI pairs instead of
 // 16-wide claims: a 16-chunk claim's digests come ~0.2 ms after its last
 // byte lands (one 64 KiB chain per lane), and the sender, which sends in
-// order, trails the download by that much.  Pairs over the first `head` and
-// the last `tail` chunks let it start early and catch up before the end.
-// TRITONDL_SHA_MB_HEAD / TRITONDL_SHA_MB_TAIL override (chunks).
+// order, trails the download by that much.  Pairs over the first `head`
+// (default 0) and the last `tail` (default 32) chunks let it start early
+// and catch up before the end; wider pair regions measured no better
+// (profiles/r03_mb_ab/SUMMARY.md).  TRITONDL_SHA_MB_HEAD /
+// TRITONDL_SHA_MB_TAIL override (chunks).
 inline size_t zc_env_chunks(const char* name, size_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? static_cast<size_t>(std::strtoul(v, nullptr, 10)) : dflt;
@@ -1101,7 +1103,7 @@ inline size_t zc_head_pairs() {
   return n;
 }
 inline size_t zc_tail_pairs() {
-  static const size_t n = zc_env_chunks("TRITONDL_SHA_MB_TAIL", 64);
+  static const size_t n = zc_env_chunks("TRITONDL_SHA_MB_TAIL", 32);
   return n;
 }
 
@@ -1179,13 +1181,13 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     if (sender_wants >= i && sender_wants < i + cnt) cv_ready.notify_one();
   };
   // Chunks per claim: 16 for the 16-lane AVX-512 kernel, else an SHA-NI
-  // pair.  The last chunks always go in pairs (zc_tail_pairs; 32 for a file
-  // already on disk): a 16-chunk claim cannot start before its last byte
-  // lands, so near the end of a download it would leave 1 MiB to hash on
-  // one core after the transfer; pairs spread that over the hashers.
+  // pair.  The last 32 chunks always go in pairs (zc_tail_pairs): a 16-chunk
+  // claim cannot start before its last byte lands, so near the end of a
+  // download it would leave 1 MiB to hash on one core after the transfer;
+  // pairs spread that over the hashers.
   const size_t wide = gpu ? 0 : tritondl_hash::sha256_claim();
   const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : wide;
-  const size_t lead = flow ? zc_head_pairs() : 0, trail = flow ? zc_tail_pairs() : 32;
+  const size_t lead = flow ? zc_head_pairs() : 0, trail = zc_tail_pairs();
   auto claim = [&](size_t* take) {
     if (gpu || wide <= 2) {
       *take = per;
