@@ -246,6 +246,31 @@ void probe_sock(int reps, size_t buf_size, const char* rname, bool report_send) 
     std::vector<char> buf(buf_size);
     const size_t total = kLen + (kLen / kChunk) * 96;
     size_t got = 0, written = 0;
+    if (buf_size == 0) {  // splice: socket -> pipe (page refs) -> file (one copy)
+      int p[2];
+      if (::pipe2(p, O_CLOEXEC) != 0) perror("pipe2");
+      ::fcntl(p[1], F_SETPIPE_SZ, 1 << 20);
+      while (got < total) {
+        const ssize_t n = ::splice(b, nullptr, p[1], nullptr, std::min<size_t>(1u << 20, total - got), SPLICE_F_MOVE);
+        if (n <= 0) {
+          perror("splice in");
+          break;
+        }
+        size_t left = static_cast<size_t>(n);
+        while (left) {
+          loff_t o = static_cast<loff_t>(got);
+          const ssize_t m = ::splice(p[0], nullptr, dfd, &o, left, SPLICE_F_MOVE);
+          if (m <= 0) {
+            perror("splice out");
+            break;
+          }
+          left -= static_cast<size_t>(m);
+          got += static_cast<size_t>(m);
+        }
+      }
+      ::close(p[0]);
+      ::close(p[1]);
+    }
     while (got < total) {
       const ssize_t n = ::recv(b, buf.data(), std::min(buf.size(), total - got), 0);
       if (n <= 0) {
@@ -292,5 +317,6 @@ int main(int argc, char** argv) {
   probe_file(reps);
   probe_sock(reps, 4u << 20, "recv_pwrite", true);
   probe_sock(reps, 256u << 10, "recv_small", false);
+  probe_sock(reps, 0, "splice_file", false);
   return 0;
 }
