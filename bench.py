@@ -195,6 +195,13 @@ def main() -> int:
         barrier()
         if prof is not None:
             prof.start()
+        # diagnostic: deterministic profile of the event-loop thread's own CPU
+        # (thread_time clock) over the timed jobs only
+        loop_prof = None
+        if os.environ.get("TRITONDL_BENCH_LOOP_PROFILE"):
+            import cProfile
+            loop_prof = cProfile.Profile(time.thread_time)
+            loop_prof.enable()
         cpu0 = stack.cpu_seconds()
         t0 = time.perf_counter()
         if shared:
@@ -205,6 +212,9 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         cpu1 = stack.cpu_seconds()
+        if loop_prof is not None:
+            loop_prof.disable()
+            loop_prof.dump_stats(os.environ["TRITONDL_BENCH_LOOP_PROFILE"])
         if prof is not None:
             prof.stop()
         barrier()

@@ -112,6 +112,7 @@ class Service:
         self.jobs_finished = 0                     # monotonic count of results recorded
         self._finish_waiters: list[tuple[int, asyncio.Future]] = []
         self._id_locks: dict[str, list] = {}       # media id -> [asyncio.Lock, users]
+        self._locked_dirs: set[str] = set()        # job dirs _job_lock created for running jobs
 
     @contextlib.asynccontextmanager
     async def _job_lock(self, media_id: str):
@@ -126,6 +127,7 @@ class Service:
         ent = self._id_locks.setdefault(media_id, [asyncio.Lock(), 0])
         ent[1] += 1
         fd = -1
+        d = ""
         try:
             async with ent[0]:
                 try:
@@ -135,6 +137,7 @@ class Service:
                 if d:
                     try:
                         os.makedirs(d, mode=0o755, exist_ok=True)
+                        self._locked_dirs.add(d)
                         fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
                         try:
                             fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
@@ -146,6 +149,7 @@ class Service:
                         log.with_fields(media_id=media_id, error=str(e)).warn("job lock unavailable")
                 yield
         finally:
+            self._locked_dirs.discard(d)
             if fd >= 0:
                 os.close(fd)                        # releases the flock
             ent[1] -= 1
@@ -347,7 +351,8 @@ class Service:
         if not (self.cfg.stream_upload and isinstance(impl, HTTPDownloader)):
             return await self.dispatcher.download(media_id, url), {}
         d = self.dispatcher.job_dir(media_id)
-        os.makedirs(d, mode=0o755, exist_ok=True)
+        if d not in self._locked_dirs:          # _job_lock made (and locked) it already
+            os.makedirs(d, mode=0o755, exist_ok=True)
         h = await impl.start(d, self.dispatcher.sink, url)
         if marks is not None:
             marks["probe"] = time.monotonic() - t0

@@ -249,6 +249,8 @@ class ProxyConfig:
     def proxy_for(self, url: str) -> ProxyURL | None:
         """The proxy for ``url`` (None = dial directly).  Raises
         :class:`ProxyConfigError` where Go's ``proxyForURL`` errors."""
+        if self.http_proxy is None and self.https_proxy is None:
+            return None                 # the common case: no proxy at all, nothing to parse
         u = urlsplit(url)
         scheme = u.scheme.lower()
         if scheme == "https":
