@@ -33,6 +33,7 @@
 #include <utility>
 #include <vector>
 
+#include "sha1_mb.h"
 #include "sha256_mb.h"
 #include "sha_ni.h"
 
@@ -150,6 +151,30 @@ inline void md_pair(const EVP_MD* md, const void* a, size_t na, const void* b, s
   }
   md_raw(md, a, na, oa);
   md_raw(md, b, nb, ob);
+}
+
+// Digests of n messages into out + i*digest_size: runs of 16 equal-length
+// messages take the 16-lane AVX-512 kernels (SHA-1 and SHA-256), the rest
+// SHA-NI pairs; other algorithms one by one.
+inline void md_batch(const EVP_MD* md, const void* const* p, const size_t* len, size_t n, unsigned char* out) {
+  if (md == sha256_md()) return sha256_batch(p, len, n, out);
+  const size_t dl = static_cast<size_t>(EVP_MD_size(md));
+  size_t i = 0;
+  if (md == sha1_md() && n >= 16 && sha16::cpu_has_avx512()) {
+    while (i + 16 <= n) {
+      bool same = true;
+      for (size_t j = 1; j < 16 && same; ++j) same = len[i + j] == len[i];
+      if (!same) break;
+      sha16::sha1_x16(p + i, len[i], out + dl * i);
+      i += 16;
+    }
+  }
+  for (; i + 1 < n; i += 2) md_pair(md, p[i], len[i], p[i + 1], len[i + 1], out + dl * i, out + dl * (i + 1));
+  if (i < n) md_raw(md, p[i], len[i], out + dl * i);
+}
+// Messages per claim that keep the widest kernel for `md` fed.
+inline size_t md_claim(const EVP_MD* md) {
+  return (md == sha1_md() || md == sha256_md()) && sha16::cpu_has_avx512() ? 16 : 2;
 }
 
 inline std::string hex_raw(const unsigned char* d, size_t n) {
@@ -409,17 +434,17 @@ inline std::string piece_hashes(const EVP_MD* md, const char* data, size_t len, 
   const size_t n = (len + piece_len - 1) / piece_len;
   const size_t dl = static_cast<size_t>(EVP_MD_size(md));
   std::string out(n * dl, '\0');
-  parallel_for((n + 1) / 2, threads <= 0 ? default_threads() : threads, [&](size_t k) {  // pairs: SHA-NI lockstep
-    const size_t i = 2 * k, a = i * piece_len, na = std::min(piece_len, len - a);
-    unsigned char d0[EVP_MAX_MD_SIZE], d1[EVP_MAX_MD_SIZE];
-    if (i + 1 < n) {
-      const size_t b = a + piece_len, nb = std::min(piece_len, len - b);
-      md_pair(md, data + a, na, data + b, nb, d0, d1);
-      std::memcpy(&out[(i + 1) * dl], d1, dl);
-    } else {
-      md_raw(md, data + a, na, d0);
+  const size_t g = md_claim(md);  // pieces per task: 16 for the AVX-512 kernels, else a SHA-NI pair
+  parallel_for((n + g - 1) / g, threads <= 0 ? default_threads() : threads, [&](size_t k) {
+    const size_t i0 = k * g, cnt = std::min(g, n - i0);
+    const void* p[16];
+    size_t m[16];
+    for (size_t j = 0; j < cnt; ++j) {
+      const size_t a = (i0 + j) * piece_len;
+      p[j] = data + a;
+      m[j] = std::min(piece_len, len - a);
     }
-    std::memcpy(&out[i * dl], d0, dl);
+    md_batch(md, p, m, cnt, reinterpret_cast<unsigned char*>(&out[i0 * dl]));
   });
   return out;
 }
@@ -480,21 +505,24 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
     }
     return filled == plen;
   };
-  // pieces in pairs: SHA-NI hashes both in lockstep (md_pair)
-  parallel_for((n + 1) / 2, threads <= 0 ? default_threads() : threads, [&](size_t k) {
-    std::vector<char> b0, b1;
-    const size_t p = 2 * k;
-    const bool l0 = load(p, b0), l1 = p + 1 < n && load(p + 1, b1);
-    unsigned char d0[EVP_MAX_MD_SIZE], d1[EVP_MAX_MD_SIZE];
-    if (l0 && l1) {
-      md_pair(md, b0.data(), b0.size(), b1.data(), b1.size(), d0, d1);
-    } else if (l0) {
-      md_raw(md, b0.data(), b0.size(), d0);
-    } else if (l1) {
-      md_raw(md, b1.data(), b1.size(), d1);
+  // Pieces per task: 16 for the AVX-512 kernels (up to 4 MiB pieces: a task
+  // holds its pieces in memory), else a SHA-NI pair.
+  const size_t g = piece_len <= (4u << 20) ? md_claim(md) : 2;
+  parallel_for((n + g - 1) / g, threads <= 0 ? default_threads() : threads, [&](size_t k) {
+    const size_t p0 = k * g, cnt = std::min(g, n - p0);
+    std::vector<std::vector<char>> bufs(cnt);
+    const void* p[16];
+    size_t m[16], idx[16], got = 0;
+    for (size_t j = 0; j < cnt; ++j) {
+      if (!load(p0 + j, bufs[j])) continue;  // missing / short: stays 0
+      p[got] = bufs[j].data();
+      m[got] = bufs[j].size();
+      idx[got++] = p0 + j;
     }
-    if (l0 && std::memcmp(d0, expected.data() + p * dl, dl) == 0) ok[p] = 1;
-    if (l1 && std::memcmp(d1, expected.data() + (p + 1) * dl, dl) == 0) ok[p + 1] = 1;
+    unsigned char d[16 * EVP_MAX_MD_SIZE];
+    md_batch(md, p, m, got, d);
+    for (size_t j = 0; j < got; ++j)
+      if (std::memcmp(d + j * dl, expected.data() + idx[j] * dl, dl) == 0) ok[idx[j]] = 1;
   });
   for (int fd : fds)
     if (fd >= 0) ::close(fd);

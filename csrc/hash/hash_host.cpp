@@ -293,18 +293,21 @@ PYBIND11_MODULE(_hash_host, m) {
         std::string ok(bufs.size(), '\0');
         {
           py::gil_scoped_release nogil;
-          const size_t n = v.size(), pairs = (n + 1) / 2;
-          parallel_for(pairs, static_cast<int>(std::min<size_t>(pairs, threads <= 0 ? default_threads() : threads)),
+          // groups of 16 buffers for the AVX-512 kernels, else SHA-NI pairs (md_batch)
+          const size_t n = v.size(), g = md_claim(md), groups = (n + g - 1) / g;
+          parallel_for(groups, static_cast<int>(std::min<size_t>(groups, threads <= 0 ? default_threads() : threads)),
                        [&](size_t k) {
-                         unsigned char d[2][EVP_MAX_MD_SIZE];
-                         const size_t i = 2 * k;
-                         if (i + 1 < n) {
-                           md_pair(md, v[i].ptr, v[i].len, v[i + 1].ptr, v[i + 1].len, d[0], d[1]);
-                           ok[i + 1] = std::memcmp(d[1], exp.data() + (i + 1) * dl, dl) == 0;
-                         } else {
-                           md_raw(md, v[i].ptr, v[i].len, d[0]);
+                         const size_t i0 = k * g, cnt = std::min(g, n - i0);
+                         const void* p[16];
+                         size_t m[16];
+                         for (size_t j = 0; j < cnt; ++j) {
+                           p[j] = v[i0 + j].ptr;
+                           m[j] = v[i0 + j].len;
                          }
-                         ok[i] = std::memcmp(d[0], exp.data() + i * dl, dl) == 0;
+                         unsigned char d[16 * EVP_MAX_MD_SIZE];
+                         md_batch(md, p, m, cnt, d);
+                         for (size_t j = 0; j < cnt; ++j)
+                           ok[i0 + j] = std::memcmp(d + j * dl, exp.data() + (i0 + j) * dl, dl) == 0;
                        });
         }
         return py::bytes(ok);

@@ -846,7 +846,10 @@ class GpuHasher {
     // (one lane per piece, ~55 MB/s/lane measured) plus set-up
     const double kernel_s = static_cast<double>(piece_len) / 55e6 + 1e-3;
     constexpr double kCopyBps = 40e9;  // page cache -> pinned -> HBM, measured ~36-45 GB/s
-    const size_t unit = std::max<size_t>(2, (1u << 20) / piece_len);  // >= 2: pieces hashed in pairs
+    // pieces per CPU claim: >= 16 for the host's 16-lane AVX-512 kernels
+    // (pieces up to 4 MiB), else >= 2 for SHA-NI pairs
+    const size_t wide = piece_len <= (4u << 20) ? tritondl_hash::md_claim(md) : 2;
+    const size_t unit = std::max<size_t>(wide, (1u << 20) / piece_len);
     std::exception_ptr cpu_err;
     auto cpu_worker = [&] {
       try {
@@ -865,19 +868,17 @@ class GpuHasher {
           const long long ge = std::min(static_cast<long long>(total), static_cast<long long>(e * piece_len));
           std::fill(ok.begin(), ok.end(), 1);
           read_range(spans, buf.data(), ga, ge, ga, piece_len, e - s, ok.data());
-          for (size_t p = s; p < e; p += 2) {  // SHA-NI: two pieces in lockstep
-            const size_t po = (p - s) * piece_len;
-            const size_t pl = std::min<size_t>(piece_len, static_cast<size_t>(ge - ga) - po);
-            if (p + 1 < e) {
-              const size_t pl2 = std::min<size_t>(piece_len, static_cast<size_t>(ge - ga) - po - piece_len);
-              tritondl_hash::md_pair(md, buf.data() + po, pl, buf.data() + po + piece_len, pl2,
-                                     reinterpret_cast<unsigned char*>(&digests[p * dl]),
-                                     reinterpret_cast<unsigned char*>(&digests[(p + 1) * dl]));
-              complete[p + 1] = ok[p + 1 - s];
-            } else {
-              tritondl_hash::md_raw(md, buf.data() + po, pl, reinterpret_cast<unsigned char*>(&digests[p * dl]));
+          for (size_t p = s; p < e; p += 16) {  // 16-lane AVX-512 groups, else SHA-NI pairs (md_batch)
+            const size_t cnt = std::min<size_t>(16, e - p);
+            const void* src[16];
+            size_t len[16];
+            for (size_t j = 0; j < cnt; ++j) {
+              const size_t po = (p + j - s) * piece_len;
+              src[j] = buf.data() + po;
+              len[j] = std::min<size_t>(piece_len, static_cast<size_t>(ge - ga) - po);
             }
-            complete[p] = ok[p - s];
+            tritondl_hash::md_batch(md, src, len, cnt, reinterpret_cast<unsigned char*>(&digests[p * dl]));
+            for (size_t j = 0; j < cnt; ++j) complete[p + j] = ok[p + j - s];
           }
           cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
         }

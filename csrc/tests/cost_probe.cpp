@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../hash/hash_core.h"
+#include "../hash/sha1_mb.h"
 #include "../hash/sha256_mb.h"
 
 namespace {
@@ -136,6 +137,28 @@ void probe_sha_hot(int reps) {
     s16.add(thread_ms() - c, wall_ms() - w);
   }
   report("sha_hot_x16", s16);
+  // SHA-1 of 1 MiB pieces (BitTorrent v1), 16 at a time vs SHA-NI pairs
+  Stat p2, p16;
+  for (int r = 0; r < reps; ++r) {
+    const void* m[16];
+    size_t l[16];
+    for (int j = 0; j < 10; ++j) {
+      m[j] = b.data() + (size_t(j) << 20);
+      l[j] = 1u << 20;
+    }
+    unsigned char d[16 * 20];
+    double c = thread_ms(), w = wall_ms();
+    for (int j = 0; j < 10; j += 2) tritondl_hash::sha2x::sha1_x2(m[j], l[j], m[j + 1], l[j + 1], d, d + 20);
+    p2.add(thread_ms() - c, wall_ms() - w);
+    const void* m16[16];
+    for (int j = 0; j < 16; ++j) m16[j] = b.data() + (size_t(j % 10) << 20);
+    c = thread_ms();
+    w = wall_ms();
+    tritondl_hash::sha16::sha1_x16(m16, 1u << 20, d);
+    p16.add((thread_ms() - c) * 10 / 16, (wall_ms() - w) * 10 / 16);  // per 10 MiB
+  }
+  report("sha1_pieces_pairs", p2);
+  report("sha1_pieces_x16", p16);
 }
 
 void probe_file(int reps) {

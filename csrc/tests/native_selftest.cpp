@@ -71,7 +71,7 @@ static void test_sha256_pair() {
   }
 }
 
-// 16-lane AVX-512 SHA-256 (sha256_mb.h) and the batch dispatcher against
+// 16-lane AVX-512 SHA-256 / SHA-1 (sha256_mb.h, sha1_mb.h) and the batch dispatchers against
 // OpenSSL: every length class of the padding (0, < 56, 56..63, whole
 // blocks, 64 KiB chunks), equal-length runs of 16 and mixed batches that
 // fall back to pairs part-way.
@@ -88,10 +88,13 @@ static void test_sha256_batch() {
       p[i] = buf.data() + (rng() % 64) + i * 70000;
       len[i] = (it % 3 == 2 && i == n / 2) ? base / 2 : base;  // one odd length breaks a run
     }
-    std::vector<unsigned char> out(32 * n);
+    std::vector<unsigned char> out(32 * n), out1(20 * n);
     sha256_batch(p.data(), len.data(), n, out.data());
-    for (size_t i = 0; i < n; ++i)
+    md_batch(sha1_md(), p.data(), len.data(), n, out1.data());  // 16-lane SHA-1 (sha1_mb.h)
+    for (size_t i = 0; i < n; ++i) {
       CHECK(std::string(reinterpret_cast<char*>(&out[32 * i]), 32) == one_shot(sha256_md(), p[i], len[i]));
+      CHECK(std::string(reinterpret_cast<char*>(&out1[20 * i]), 20) == one_shot(sha1_md(), p[i], len[i]));
+    }
   }
 }
 
