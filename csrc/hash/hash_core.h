@@ -476,12 +476,9 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
   std::vector<int> fds(spans.size(), -1);
   for (size_t i = 0; i < spans.size(); ++i)
     if (!spans[i].path.empty()) fds[i] = ::open(spans[i].path.c_str(), O_RDONLY | O_CLOEXEC);
-  // read piece p of the layout into buf (sized to the piece); false if a
-  // file is missing or short
-  auto load = [&](size_t p, std::vector<char>& buf) -> bool {
-    const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
-    const long long plen = std::min<long long>(static_cast<long long>(piece_len), total - pstart);
-    buf.resize(static_cast<size_t>(plen));
+  // read [pstart, pstart + plen) of the layout into dst; false if a file is
+  // missing or short
+  auto read_at = [&](long long pstart, long long plen, char* dst) -> bool {
     long long filled = 0;
     size_t lo = 0, hi = spans.size();  // last span starting at or before pstart
     while (hi - lo > 1) {
@@ -495,21 +492,58 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
       if (e <= a) continue;
       const size_t want = static_cast<size_t>(e - a);
       if (a == pstart + filled && spans[s].path.empty()) {  // BEP 47 padding file: zeros, not on disk
-        std::memset(buf.data() + filled, 0, want);
+        std::memset(dst + filled, 0, want);
         filled += static_cast<long long>(want);
         continue;
       }
       if (a != pstart + filled || fds[s] < 0) return false;
-      if (pread_full(fds[s], buf.data() + filled, want, static_cast<off_t>(a - fstart)) != want) return false;
+      if (pread_full(fds[s], dst + filled, want, static_cast<off_t>(a - fstart)) != want) return false;
       filled += static_cast<long long>(want);
     }
     return filled == plen;
   };
-  // Pieces per task: 16 for the AVX-512 kernels (up to 4 MiB pieces: a task
-  // holds its pieces in memory), else a SHA-NI pair.
-  const size_t g = piece_len <= (4u << 20) ? md_claim(md) : 2;
+  // piece p into buf (sized to the piece)
+  auto load = [&](size_t p, std::vector<char>& buf) -> bool {
+    const long long pstart = static_cast<long long>(p) * static_cast<long long>(piece_len);
+    const long long plen = std::min<long long>(static_cast<long long>(piece_len), total - pstart);
+    buf.resize(static_cast<size_t>(plen));
+    return read_at(pstart, plen, buf.data());
+  };
+  // SHA-1 pieces go 16 at a time through the AVX-512 kernel, streamed: each
+  // lane's next 64 KiB is read into a 1 MiB staging area that stays in the
+  // core's L2, hashed, and the area reused.  Loading 16 whole pieces first
+  // (16 MiB per task) hashed from DRAM and halved host throughput.  The
+  // rest, and the torrent's last (short) piece, go in SHA-NI pairs.
+  constexpr size_t kStage = 64u << 10;
+  const bool wide = md == sha1_md() && sha16::cpu_has_avx512() && piece_len % 64 == 0 &&
+                    (piece_len <= kStage || piece_len % kStage == 0);
+  const size_t g = wide ? 16 : 2;
   parallel_for((n + g - 1) / g, threads <= 0 ? default_threads() : threads, [&](size_t k) {
     const size_t p0 = k * g, cnt = std::min(g, n - p0);
+    if (cnt == 16 && static_cast<long long>((p0 + 16) * piece_len) <= total) {
+      const size_t step = std::min(piece_len, kStage);
+      std::unique_ptr<char[]> stage(new char[16 * step]);
+      const void* lane[16];
+      bool lane_ok[16];
+      for (size_t j = 0; j < 16; ++j) {
+        lane[j] = stage.get() + j * step;
+        lane_ok[j] = true;
+      }
+      sha16::Sha1x16 st;
+      sha16::sha1_x16_init(&st);
+      for (size_t off = 0; off < piece_len; off += step) {
+        for (size_t j = 0; j < 16; ++j)
+          if (lane_ok[j] && !read_at(static_cast<long long>((p0 + j) * piece_len + off), static_cast<long long>(step),
+                                     stage.get() + j * step))
+            lane_ok[j] = false;  // its digest is discarded; the lane keeps hashing whatever is staged
+        sha16::sha1_x16_update(&st, lane, step / 64);
+      }
+      unsigned char d[16 * 20];
+      sha16::sha1_x16_finish(&st, lane, piece_len, d);  // piece_len % 64 == 0: no data in the tail
+      for (size_t j = 0; j < 16; ++j)
+        if (lane_ok[j] && std::memcmp(d + 20 * j, expected.data() + (p0 + j) * dl, dl) == 0) ok[p0 + j] = 1;
+      return;
+    }
     std::vector<std::vector<char>> bufs(cnt);
     const void* p[16];
     size_t m[16], idx[16], got = 0;

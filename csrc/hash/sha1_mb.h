@@ -73,32 +73,57 @@ TDL_MB1_TARGET inline void sha1_compress(__m512i s[5], const uint8_t* const p[16
   }
 }
 
-// SHA-1 of 16 messages of `len` bytes each: out + 20*j = digest of msg[j].
-TDL_MB1_TARGET inline void sha1_x16(const void* const msg[16], size_t len, unsigned char* out) {
-  static const uint32_t h0[5] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0};
+// Incremental form, for messages that do not fit a core's cache at once
+// (resume verification streams 16 pieces through a 1 MiB staging area):
+// init, any number of update() calls of whole 64-byte blocks, finish() with
+// the remaining < 64 bytes of each lane and the total length.
+struct Sha1x16 {
   __m512i s[5];
-  for (int i = 0; i < 5; ++i) s[i] = _mm512_set1_epi32(static_cast<int>(h0[i]));
+};
+TDL_MB1_TARGET inline void sha1_x16_init(Sha1x16* st) {
+  static const uint32_t h0[5] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0};
+  for (int i = 0; i < 5; ++i) st->s[i] = _mm512_set1_epi32(static_cast<int>(h0[i]));
+}
+TDL_MB1_TARGET inline void sha1_x16_update(Sha1x16* st, const void* const msg[16], size_t nblocks) {
   const uint8_t* p[16];
   for (int j = 0; j < 16; ++j) p[j] = static_cast<const uint8_t*>(msg[j]);
+  sha1_compress(st->s, p, nblocks);
+}
+TDL_MB1_TARGET inline void sha1_x16_finish(Sha1x16* st, const void* const rest[16], size_t total,
+                                           unsigned char* out);
+
+// SHA-1 of 16 messages of `len` bytes each: out + 20*j = digest of msg[j].
+TDL_MB1_TARGET inline void sha1_x16(const void* const msg[16], size_t len, unsigned char* out) {
+  Sha1x16 st;
+  sha1_x16_init(&st);
   const size_t full = len / 64;
-  sha1_compress(s, p, full);
-  const size_t rem = len % 64;
+  sha1_x16_update(&st, msg, full);
+  const void* rest[16];
+  for (int j = 0; j < 16; ++j) rest[j] = static_cast<const uint8_t*>(msg[j]) + full * 64;
+  sha1_x16_finish(&st, rest, len, out);
+}
+
+// rest[j]: the last total % 64 bytes of lane j
+TDL_MB1_TARGET inline void sha1_x16_finish(Sha1x16* st, const void* const rest[16], size_t total,
+                                           unsigned char* out) {
+  const size_t rem = total % 64;
   const size_t tail_blocks = rem < 56 ? 1 : 2;
   alignas(64) uint8_t tail[16][128];
-  const uint64_t bits = static_cast<uint64_t>(len) * 8;
+  const uint8_t* p[16];
+  const uint64_t bits = static_cast<uint64_t>(total) * 8;
   for (int j = 0; j < 16; ++j) {
     std::memset(tail[j], 0, sizeof tail[j]);
-    if (rem) std::memcpy(tail[j], p[j] + full * 64, rem);
+    if (rem) std::memcpy(tail[j], rest[j], rem);
     tail[j][rem] = 0x80;
     for (int k = 0; k < 8; ++k) tail[j][tail_blocks * 64 - 1 - k] = static_cast<uint8_t>(bits >> (8 * k));
     p[j] = tail[j];
   }
-  sha1_compress(s, p, tail_blocks);
-  alignas(64) uint32_t st[5][16];
-  for (int i = 0; i < 5; ++i) _mm512_store_si512(st[i], s[i]);
+  sha1_compress(st->s, p, tail_blocks);
+  alignas(64) uint32_t words[5][16];
+  for (int i = 0; i < 5; ++i) _mm512_store_si512(words[i], st->s[i]);
   for (int j = 0; j < 16; ++j)
     for (int i = 0; i < 5; ++i) {
-      const uint32_t v = st[i][j];
+      const uint32_t v = words[i][j];
       unsigned char* o = out + 20 * j + 4 * i;
       o[0] = static_cast<unsigned char>(v >> 24);
       o[1] = static_cast<unsigned char>(v >> 16);

@@ -141,6 +141,15 @@ static void test_pieces_and_verify() {
   std::vector<std::pair<std::string, long long>> files = {{a, (long long)cut}, {b, (long long)(blob.size() - cut)}};
   std::string ok = verify_pieces(files, pl, ph, 8, EVP_sha1());
   CHECK(ok == std::string(ok.size(), '\1'));
+  // sha1_md(): 16-piece groups streamed through the AVX-512 kernel (pieces of
+  // 32 KiB, so one stage per piece; and 128 KiB pieces, two stages each)
+  CHECK(verify_pieces(files, pl, ph, 8, sha1_md()) == std::string(ok.size(), '\1'));
+  const std::string ph128 = piece_hashes(sha1_md(), blob.data(), blob.size(), 131072, 4);
+  CHECK(ph128.size() == 8 * 20);
+  {
+    std::vector<std::pair<std::string, long long>> one = {{a, (long long)cut}, {b, (long long)(blob.size() - cut)}};
+    CHECK(verify_pieces(one, 131072, ph128, 4, sha1_md()) == std::string(8, '\1'));
+  }
   // corrupt one byte inside piece 20
   FILE* fc = std::fopen(b.c_str(), "r+b");
   std::fseek(fc, 20 * pl - cut + 5, SEEK_SET);
@@ -150,9 +159,12 @@ static void test_pieces_and_verify() {
   int bad = 0;
   for (char ch : ok) bad += ch == 0;
   CHECK(bad == 1 && ok[20] == 0);
+  const std::string ok16 = verify_pieces(files, pl, ph, 8, sha1_md());
+  CHECK(ok16 == ok);
   std::remove(a.c_str());
   ok = verify_pieces(files, pl, ph, 8, EVP_sha1());  // missing file -> its pieces fail, no crash
   CHECK(ok[0] == 0);
+  CHECK(verify_pieces(files, pl, ph, 8, sha1_md()) == ok);
   std::remove(b.c_str());
   rmdir(dir);
 }
