@@ -319,6 +319,9 @@ PYBIND11_MODULE(_hash_host, m) {
   m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) { return py::bytes(hmac256(k, msg)); });
   m.def("sha_ni", &sha2x::cpu_has_sha_ni,
         "SHA-1/SHA-256 run on the two-stream SHA-NI path (False: OpenSSL; TRITONDL_SHA_NI=0 forces that)");
+  m.def("sha_mb", &sha16::cpu_has_avx512,
+        "batches of 16 equal-length SHA-1/SHA-256 messages run on the 16-lane AVX-512 kernels "
+        "(TRITONDL_SHA_MB=0 turns them off)");
   m.def("chunk_signatures", &py_chunk_signatures, py::arg("signing_key"), py::arg("amzdate"), py::arg("scope"),
         py::arg("seed_signature"), py::arg("data"), py::arg("chunk_size"), py::arg("include_final") = true,
         py::arg("threads") = 1);

@@ -211,11 +211,13 @@ def hybrid_cpu_threads(cpus: int | None = None) -> int:
 # kernel runs one lane per piece, the per-lane SHA-1 rate (~55 MB/s) for one
 # piece; the host path runs ~1.5 GB/s per thread through OpenSSL, ~3 GB/s
 # with the two-stream SHA-NI pairs (8 GiB v1 resume on 16 threads: 35 -> 55
-# GB/s), plus ~15 us of per-piece overhead.
+# GB/s), ~4.4 GB/s with the 16-lane AVX-512 SHA-1 (70 GB/s on 16 threads,
+# profiles/r03_sha1_mb), plus ~15 us of per-piece overhead.
 GPU_COPY_BPS = 45e9
 GPU_LANE_BPS = 55e6
 GPU_SETUP_S = 5e-3
-CPU_THREAD_BPS = 3.0e9 if getattr(_host, "sha_ni", lambda: False)() else 1.5e9
+CPU_THREAD_BPS = (4.4e9 if getattr(_host, "sha_mb", lambda: False)() else
+                  3.0e9 if getattr(_host, "sha_ni", lambda: False)() else 1.5e9)
 CPU_PIECE_S = 15e-6
 
 
