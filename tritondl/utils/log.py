@@ -99,11 +99,15 @@ class Logger:
         return LEVELS[level] <= self.level
 
     # direct logging ----------------------------------------------------
+    # debug/info are called on every job: a disabled level returns before
+    # building an entry or formatting the message
     def debug(self, msg: str, *a: Any) -> None:
-        Entry(self, {})._log("debug", msg, a, 3)
+        if LEVELS["debug"] <= self.level:
+            Entry(self, {})._log("debug", msg, a, 3)
 
     def info(self, msg: str, *a: Any) -> None:
-        Entry(self, {})._log("info", msg, a, 3)
+        if LEVELS["info"] <= self.level:
+            Entry(self, {})._log("info", msg, a, 3)
 
     def warn(self, msg: str, *a: Any) -> None:
         Entry(self, {})._log("warning", msg, a, 3)
@@ -164,6 +168,8 @@ class Entry:
         return Entry(self.logger, d)
 
     def _log(self, level: str, msg: str, args: tuple, depth: int) -> None:
+        if LEVELS[level] > self.logger.level:
+            return
         if args:
             msg = msg % args
         self.logger._emit(level, msg, self.fields, depth + 1)
