@@ -82,6 +82,33 @@ def test_verify_pieces_host(tmp_path, device):
     assert ok[0] == 0 and ok[1] == 0
 
 
+def test_sixteen_lane_batches_match_hashlib(tmp_path):
+    """Groups of 16 equal-length messages take the 16-lane AVX-512 kernels
+    (csrc/hash/sha1_mb.h, sha256_mb.h) where the CPU has them: piece hashes,
+    buffer verification and streamed resume verification (37 pieces: two
+    full groups of 16 plus a tail in SHA-NI pairs) must equal hashlib."""
+    from tritondl.ops.hashing import _host
+    piece_len = 65536
+    data = os.urandom(piece_len * 36 + 999)
+    for kind in ("sha1", "sha256"):
+        assert hashing.piece_hashes(data, piece_len, kind, threads=4) == _ref_pieces(data, piece_len, kind)
+    bufs = [data[i:i + piece_len] for i in range(0, len(data), piece_len)]
+    exp = _ref_pieces(data, piece_len, "sha1")
+    bad = bytearray(exp)
+    bad[20 * 17] ^= 1                                   # piece 17 (second group) must fail alone
+    ok = _host.verify_buffers("sha1", bufs, bytes(bad), 4)
+    assert [i for i, v in enumerate(ok) if not v] == [17]
+    files, blob, exp2 = _make_torrent_layout(tmp_path, [piece_len * 20 + 5, piece_len * 16 - 5, 999], piece_len)
+    assert hashing.verify_pieces(files, piece_len, exp2, device="cpu") == b"\x01" * (len(exp2) // 20)
+    with open(files[1][0], "r+b") as f:               # a byte inside piece 30 (a streamed 16-piece group)
+        f.seek(piece_len * 10)
+        b = f.read(1)
+        f.seek(piece_len * 10)
+        f.write(bytes([b[0] ^ 0xFF]))
+    ok = hashing.verify_pieces(files, piece_len, exp2, device="cpu")
+    assert [i for i, v in enumerate(ok) if not v] == [(piece_len * 20 + 5 + piece_len * 10) // piece_len]
+
+
 def test_chunk_signature_chain_matches_python():
     import hmac
     key = os.urandom(32)
