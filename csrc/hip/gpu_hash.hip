@@ -847,8 +847,9 @@ class GpuHasher {
     const double kernel_s = static_cast<double>(piece_len) / 55e6 + 1e-3;
     constexpr double kCopyBps = 40e9;  // page cache -> pinned -> HBM, measured ~36-45 GB/s
     // pieces per CPU claim: >= 16 for the host's 16-lane AVX-512 kernels
-    // (pieces up to 4 MiB), else >= 2 for SHA-NI pairs
-    const size_t wide = piece_len <= (4u << 20) ? tritondl_hash::md_claim(md) : 2;
+    // (pieces up to 1 MiB: a claim's buffer is 16 pieces per CPU thread),
+    // else >= 2 for SHA-NI pairs
+    const size_t wide = piece_len <= (1u << 20) ? tritondl_hash::md_claim(md) : 2;
     const size_t unit = std::max<size_t>(wide, (1u << 20) / piece_len);
     std::exception_ptr cpu_err;
     auto cpu_worker = [&] {
