@@ -544,19 +544,24 @@ inline std::string verify_pieces(const std::vector<std::pair<std::string, long l
         if (lane_ok[j] && std::memcmp(d + 20 * j, expected.data() + (p0 + j) * dl, dl) == 0) ok[p0 + j] = 1;
       return;
     }
-    std::vector<std::vector<char>> bufs(cnt);
-    const void* p[16];
-    size_t m[16], idx[16], got = 0;
-    for (size_t j = 0; j < cnt; ++j) {
-      if (!load(p0 + j, bufs[j])) continue;  // missing / short: stays 0
-      p[got] = bufs[j].data();
-      m[got] = bufs[j].size();
-      idx[got++] = p0 + j;
+    // whole pieces, two at a time (a SHA-NI pair), so a task never holds
+    // more than two pieces in memory
+    std::vector<char> bufs[2];
+    for (size_t j0 = 0; j0 < cnt; j0 += 2) {
+      const void* p[2];
+      size_t m[2], idx[2], got = 0;
+      for (size_t j = j0; j < std::min(cnt, j0 + 2); ++j) {
+        if (!load(p0 + j, bufs[got])) continue;  // missing / short: stays 0
+        p[got] = bufs[got].data();
+        m[got] = bufs[got].size();
+        idx[got] = p0 + j;
+        ++got;
+      }
+      unsigned char d[2 * EVP_MAX_MD_SIZE];
+      md_batch(md, p, m, got, d);
+      for (size_t j = 0; j < got; ++j)
+        if (std::memcmp(d + j * dl, expected.data() + idx[j] * dl, dl) == 0) ok[idx[j]] = 1;
     }
-    unsigned char d[16 * EVP_MAX_MD_SIZE];
-    md_batch(md, p, m, got, d);
-    for (size_t j = 0; j < got; ++j)
-      if (std::memcmp(d + j * dl, expected.data() + idx[j] * dl, dl) == 0) ok[idx[j]] = 1;
   });
   for (int fd : fds)
     if (fd >= 0) ::close(fd);
