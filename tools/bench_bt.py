@@ -37,6 +37,7 @@ async def main() -> int:
     ap.add_argument("--piece-kb", type=int, default=1024)
     ap.add_argument("--utp", action="store_true", help="disable TCP dialing: uTP only")
     ap.add_argument("--profile", default="")
+    ap.add_argument("--cpuprofile", default="", help="whole-process sampling profile (pprof + .txt) of the download")
     ap.add_argument("--encryption", default="allow", help="MSE policy for seeders and leecher")
     ap.add_argument("--job", action="store_true", help="full worker job (download+upload+publish+ack)")
     ap.add_argument("--python-seeders", action="store_true",
@@ -80,17 +81,23 @@ async def main() -> int:
         d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
                                             encryption=a.encryption, native_wire=not a.python_wire),
                               progress_interval=1.0, use_dht=False)
-        prof = None
+        prof = sprof = None
         if a.profile:
             import cProfile
             prof = cProfile.Profile()
             prof.enable()
+        if a.cpuprofile:
+            from tritondl.utils.profiler import CPUProfiler
+            sprof = CPUProfiler(a.cpuprofile)
+            sprof.start()
         t0 = time.perf_counter()
         await d.download(dst, lambda u, p: None, magnet)
         dt = time.perf_counter() - t0
         if prof:
             prof.disable()
             prof.dump_stats(a.profile)
+        if sprof:
+            sprof.stop()                                 # writes PATH and PATH.txt
         assert parse_magnet(magnet).infohash.hex() == seeds[0].info["infohash"]
         assert os.path.getsize(os.path.join(dst, "movie.mkv")) == a.mb << 20
         print(json.dumps({"metric": "bt_ingest_MB_per_sec", "value": round(a.mb * 1.048576 / dt, 1),
