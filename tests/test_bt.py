@@ -616,3 +616,28 @@ def test_storage_write_error_fails_the_job_instead_of_hanging(tmp_path, monkeypa
             await asyncio.wait_for(_dl().download(str(dst), lambda u, p: None, magnet_for(info, peers=[seed.addr])), 30)
         await seed.stop()
     run(main())
+
+
+def test_completion_db_batches_marks_and_flushes_on_read_and_close(tmp_path):
+    """Piece marks are committed in batches (one WAL transaction per batch,
+    not per piece) but every read and close sees them all."""
+    from tritondl.fetch.bt.storage import CompletionDB
+    import sqlite3
+    p = str(tmp_path / ".torrent.db")
+    db = CompletionDB(p, batch=8, max_delay_s=3600)
+    ih = b"\x11" * 20
+    for i in range(5):
+        db.set(ih, i, True)
+    other = sqlite3.connect(p)
+    assert other.execute("SELECT COUNT(*) FROM piece_completion").fetchone()[0] == 0   # still pending
+    for i in range(5, 9):
+        db.set(ih, i, True)                      # the 8th mark commits the batch
+    assert other.execute("SELECT COUNT(*) FROM piece_completion").fetchone()[0] == 8
+    db.set(ih, 3, False)
+    db.set(ih, 20, True)
+    assert db.get(ih) == set(range(9)) - {3} | {20}                  # a read flushes first
+    db.set(ih, 21, True)
+    db.close()                                                        # close flushes
+    assert {r[0] for r in other.execute("SELECT idx FROM piece_completion WHERE complete=1")} == \
+        set(range(9)) - {3} | {20, 21}
+    other.close()

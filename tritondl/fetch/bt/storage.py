@@ -18,6 +18,7 @@ import bisect
 import os
 import sqlite3
 import threading
+import time
 
 from ...ops import hashing
 from ...utils.log import log
@@ -27,9 +28,20 @@ DB_NAME = ".torrent.db"
 
 
 class CompletionDB:
-    def __init__(self, path: str) -> None:
+    """Piece-completion marks.  Marks are committed in batches (every
+    ``batch`` marks or ``max_delay_s``, and on every read and close): one
+    autocommitted INSERT per verified piece was a WAL transaction per piece,
+    ~0.1-0.25 ms each, i.e. most of a core at 5 GB/s of 1 MiB pieces.  A crash
+    can only forget the newest marks, which resume re-verification recovers
+    (the same guarantee synchronous=NORMAL already gave)."""
+
+    def __init__(self, path: str, batch: int = 128, max_delay_s: float = 0.25) -> None:
         self.path = path
         self._lock = threading.Lock()
+        self.batch = batch
+        self.max_delay_s = max_delay_s
+        self._pending: dict[tuple[bytes, int], int] = {}
+        self._last_flush = time.monotonic()
         self.conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
         self.conn.execute("PRAGMA journal_mode=WAL")
         # WAL + NORMAL: no fsync per piece mark; a crash can only forget the
@@ -38,25 +50,44 @@ class CompletionDB:
         self.conn.execute("CREATE TABLE IF NOT EXISTS piece_completion (infohash BLOB NOT NULL, "
                           "idx INTEGER NOT NULL, complete INTEGER NOT NULL, PRIMARY KEY (infohash, idx))")
 
+    def _write_locked(self, rows) -> None:
+        self.conn.execute("BEGIN")
+        self.conn.executemany("INSERT OR REPLACE INTO piece_completion VALUES (?,?,?)", rows)
+        self.conn.execute("COMMIT")
+
+    def _flush_locked(self) -> None:
+        if self._pending:
+            rows = [(ih, i, c) for (ih, i), c in self._pending.items()]
+            self._pending.clear()
+            self._write_locked(rows)
+        self._last_flush = time.monotonic()
+
+    def flush(self) -> None:
+        with self._lock:
+            self._flush_locked()
+
     def get(self, infohash: bytes) -> set[int]:
         with self._lock:
+            self._flush_locked()
             rows = self.conn.execute("SELECT idx FROM piece_completion WHERE infohash=? AND complete=1",
                                      (infohash,)).fetchall()
         return {r[0] for r in rows}
 
     def set(self, infohash: bytes, idx: int, complete: bool) -> None:
         with self._lock:
-            self.conn.execute("INSERT OR REPLACE INTO piece_completion VALUES (?,?,?)", (infohash, idx, int(complete)))
+            self._pending[(infohash, idx)] = int(complete)
+            if len(self._pending) >= self.batch or time.monotonic() - self._last_flush >= self.max_delay_s:
+                self._flush_locked()
 
     def set_many(self, infohash: bytes, states: dict[int, bool]) -> None:
         with self._lock:
-            self.conn.execute("BEGIN")
-            self.conn.executemany("INSERT OR REPLACE INTO piece_completion VALUES (?,?,?)",
-                                  [(infohash, i, int(c)) for i, c in states.items()])
-            self.conn.execute("COMMIT")
+            for i, c in states.items():
+                self._pending[(infohash, i)] = int(c)
+            self._flush_locked()
 
     def close(self) -> None:
         with self._lock:
+            self._flush_locked()
             self.conn.close()
 
 
