@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../hash/hash_core.h"
+#include "../relay/relay_core.h"
 #include "../hash/sha1_mb.h"
 #include "../hash/sha256_mb.h"
 
@@ -326,6 +327,61 @@ void probe_sock(int reps, size_t buf_size, const char* rname, bool report_send) 
   if (report_send) report("sendfile", ss);
 }
 
+// TLS 1.3 over loopback TCP (AES-128-GCM, the worker's default): thread CPU
+// of the receiving pump (recv_body: SSL_read + pwrite) and of the sending
+// pump (send_body unsigned: pread + SSL_write) for 10 MiB, next to the AES
+// floor (openssl speed on the box: ~6.9 GB/s per core)
+void probe_tls(int reps) {
+  using namespace tritondl_relay;
+  std::vector<char> src(1u << 20, 'z');
+  const std::string spath = fresh_path();
+  const int sfd = write_file(spath, src);
+  TestPki pki = make_test_pki({"127.0.0.1"}, 1);
+  auto sctx = TlsContext::server(pki.cert_pem, pki.key_pem);
+  auto cctx = TlsContext::client(pki.ca_pem, "", true);
+  Stat rs, ss;
+  for (int r = 0; r < reps; ++r) {
+    int a, b;
+    sock_pair(&a, &b);
+    ::fcntl(a, F_SETFL, O_NONBLOCK);
+    ::fcntl(b, F_SETFL, O_NONBLOCK);
+    TlsStream srv(sctx, a, "", ""), cli(cctx, b, "127.0.0.1", "probe");
+    std::string serr;
+    std::thread hs([&] { serr = srv.handshake(10.0); });
+    const std::string cerr = cli.handshake(10.0);
+    hs.join();
+    if (!cerr.empty() || !serr.empty()) {
+      std::fprintf(stderr, "tls handshake: %s %s\n", cerr.c_str(), serr.c_str());
+      std::exit(1);
+    }
+    const std::string dpath = fresh_path();
+    const int dfd = ::open(dpath.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+    if (::ftruncate(dfd, kLen) != 0) perror("ftruncate");
+    double scpu = 0, swall = 0;
+    std::thread sender([&] {
+      const double c = thread_ms(), w = wall_ms();
+      SendResult sr = send_body(srv, "", sfd, 0, kLen, nullptr, 0, "", "", "", "", 65536, 1, 10.0);
+      if (!sr.err.empty()) std::fprintf(stderr, "tls send: %s\n", sr.err.c_str());
+      scpu = thread_ms() - c;
+      swall = wall_ms() - w;
+    });
+    const double c = thread_ms(), w = wall_ms();
+    RecvResult rr = recv_body(cli, dfd, 0, static_cast<int64_t>(kLen), "", 0, nullptr, 0, 0, 10.0);
+    rs.add(thread_ms() - c, wall_ms() - w);
+    sender.join();
+    ss.add(scpu, swall);
+    if (!rr.err.empty() || rr.received != kLen) std::fprintf(stderr, "tls recv: %s\n", rr.err.c_str());
+    ::close(dfd);
+    ::unlink(dpath.c_str());
+    ::close(a);
+    ::close(b);
+  }
+  ::close(sfd);
+  ::unlink(spath.c_str());
+  report("tls_recv_pwrite", rs);
+  report("tls_pread_send", ss);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -341,5 +397,6 @@ int main(int argc, char** argv) {
   probe_sock(reps, 4u << 20, "recv_pwrite", true);
   probe_sock(reps, 256u << 10, "recv_small", false);
   probe_sock(reps, 0, "splice_file", false);
+  probe_tls(reps);
   return 0;
 }
