@@ -118,7 +118,7 @@ static void test_aws_chunked() {
 
 static void test_pieces_and_verify() {
   std::mt19937 rng(7);
-  std::string blob(1 << 20, '\0');
+  std::string blob(4 << 20, '\0');
   for (auto& ch : blob) ch = static_cast<char>(rng());
   const size_t pl = 32768;
   std::string ph = piece_hashes(EVP_sha1(), blob.data(), blob.size(), pl, 4);
@@ -145,10 +145,10 @@ static void test_pieces_and_verify() {
   // 32 KiB, so one stage per piece; and 128 KiB pieces, two stages each)
   CHECK(verify_pieces(files, pl, ph, 8, sha1_md()) == std::string(ok.size(), '\1'));
   const std::string ph128 = piece_hashes(sha1_md(), blob.data(), blob.size(), 131072, 4);
-  CHECK(ph128.size() == 8 * 20);
+  CHECK(ph128.size() == 32 * 20);
   {
     std::vector<std::pair<std::string, long long>> one = {{a, (long long)cut}, {b, (long long)(blob.size() - cut)}};
-    CHECK(verify_pieces(one, 131072, ph128, 4, sha1_md()) == std::string(8, '\1'));
+    CHECK(verify_pieces(one, 131072, ph128, 4, sha1_md()) == std::string(32, '\1'));
   }
   // corrupt one byte inside piece 20
   FILE* fc = std::fopen(b.c_str(), "r+b");
@@ -321,6 +321,34 @@ static void test_relay(size_t size) {
   ::close(ofd);
   ::unlink(path);
   ::unlink(opath);
+}
+
+// The streamed S3 verifier with its whole body already in hand (the prefix):
+// every frame is published at once, so the hashers start far behind and
+// claim 16 frames at a time (the AVX-512 path); a flipped payload byte in
+// one frame must still fail the signature chain.
+static void test_verify_backlog() {
+  using namespace tritondl_relay;
+  const size_t size = (3u << 20) + 77;
+  std::mt19937 rng(31);
+  std::string data(size, '\0');
+  for (auto& c : data) c = static_cast<char>(rng());
+  const std::string key(32, 'k'), amz = "20260101T000000Z", scope = "20260101/us-east-1/s3/aws4_request",
+                    seed(64, '0');
+  std::string raw(tritondl_hash::aws_chunk_encoded_size(size, 65536, true), '\0');
+  tritondl_hash::aws_chunk_encode(key, amz, scope, seed, data.data(), size, 65536, true, &raw[0], 2);
+  int sv[2];
+  CHECK(::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  ::fcntl(sv[1], F_SETFL, O_NONBLOCK);
+  PlainStream s1(sv[1]);
+  VerifyResult vr = recv_verify_chunked(s1, raw.size(), raw.data(), raw.size(), key, amz, scope, seed, true, 2, 10.0);
+  CHECK(vr.err.empty() && vr.data == data);
+  std::string bad = raw;
+  bad[20 * (65536 + 87) + 1000] ^= 1;  // inside frame 20's payload
+  vr = recv_verify_chunked(s1, bad.size(), bad.data(), bad.size(), key, amz, scope, seed, false, 2, 10.0);
+  CHECK(vr.err == "chunk signature mismatch");
+  ::close(sv[0]);
+  ::close(sv[1]);
 }
 
 // Pumps started on the task pool and reaped from a CompletionPort (the
@@ -654,6 +682,7 @@ int main(int argc, char** argv) {
   test_relay(quick ? (3u << 20) + 777 : (8u << 20) + 777);
   test_relay(0);
   test_port(quick ? (2u << 20) + 99 : (6u << 20) + 99);
+  test_verify_backlog();
   test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
