@@ -52,6 +52,12 @@ try:  # native peer-wire data plane (csrc/btwire): block assembly + request pipe
 except ImportError:  # pragma: no cover - the extension ships with every build
     _W = None
 
+# Live v1 verification: completed pieces per executor hop.  16 when the host
+# has the 16-lane AVX-512 SHA-1 (hash_core.h md_batch; a partial group waits
+# at most VERIFY_WAIT_S for partners), else an SHA-NI pair.
+VERIFY_GROUP = 16 if hashing.sha_mb() else 2
+VERIFY_WAIT_S = 0.003
+
 
 @dataclass
 class TorrentConfig:
@@ -475,15 +481,20 @@ class Torrent:
         self.downloaded += len(data)
         self.verifying.add(i)
         if self.info is not None and self.info.pieces:
-            # v1 / hybrid: pieces are verified two at a time (SHA-1 in SHA-NI
-            # lockstep, one executor hop per pair); a lone piece goes at the
-            # end of this loop iteration if no partner turned up by then
+            # v1 / hybrid: pieces are verified in groups, one executor hop per
+            # group: 16 for the host's 16-lane AVX-512 SHA-1 (flushed after
+            # VERIFY_WAIT_S if fewer arrive), else pairs in SHA-NI lockstep
+            # (a lone piece goes at the end of this loop iteration)
             self._vq.append((i, data, src))
-            if len(self._vq) >= 2:
+            if len(self._vq) >= VERIFY_GROUP:
                 self._submit_verify()
             elif not self._vflush:
                 self._vflush = True
-                asyncio.get_running_loop().call_soon(self._submit_verify)
+                loop = asyncio.get_running_loop()
+                if VERIFY_GROUP > 2:
+                    loop.call_later(VERIFY_WAIT_S, self._submit_verify)
+                else:
+                    loop.call_soon(self._submit_verify)
             return
         t = asyncio.get_running_loop().create_task(self._finish_native(i, data, src))
         self._finishers.add(t)
@@ -497,7 +508,7 @@ class Torrent:
             self._vq.clear()
             return
         while self._vq:
-            batch, self._vq = self._vq[:2], self._vq[2:]
+            batch, self._vq = self._vq[:VERIFY_GROUP], self._vq[VERIFY_GROUP:]
             t = asyncio.get_running_loop().create_task(self._verify_batch(batch))
             self._finishers.add(t)
             t.add_done_callback(self._finishers.discard)

@@ -43,6 +43,12 @@ def hmac_sha256(key: bytes, msg: bytes) -> bytes:
     return _host.hmac_sha256(key, msg)
 
 
+def sha_mb() -> bool:
+    """Groups of 16 equal-length SHA-1/SHA-256 messages run on the host's
+    16-lane AVX-512 kernels (csrc/hash/sha1_mb.h, sha256_mb.h)."""
+    return bool(getattr(_host, "sha_mb", lambda: False)())
+
+
 def chunk_signatures(signing_key: bytes, amzdate: str, scope: str, seed_signature: str, data,
                      chunk_size: int, include_final: bool = True, threads: int = 1) -> list[str]:
     """aws-chunked signature chain over ``data`` (one per ``chunk_size`` chunk,
@@ -216,7 +222,7 @@ def hybrid_cpu_threads(cpus: int | None = None) -> int:
 GPU_COPY_BPS = 45e9
 GPU_LANE_BPS = 55e6
 GPU_SETUP_S = 5e-3
-CPU_THREAD_BPS = (4.4e9 if getattr(_host, "sha_mb", lambda: False)() else
+CPU_THREAD_BPS = (4.4e9 if sha_mb() else
                   3.0e9 if getattr(_host, "sha_ni", lambda: False)() else 1.5e9)
 CPU_PIECE_S = 15e-6
 
