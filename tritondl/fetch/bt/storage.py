@@ -190,7 +190,7 @@ class FileStorage:
             # independent, so the GPU sees total/16 KiB lanes whatever the piece size
             exp, widths, reals, known = self.info.v2_expectations()
             if device == "auto":
-                dev = hashing.choose_device(-(-self.info.total_length // 16384), 16384, self.info.total_length)
+                dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length, lane_len=16384)
             ok = hashing.verify_pieces_v2(self.layout, self.info.piece_length, exp, widths, reals, known,
                                           device=dev)
         have = {i for i, v in enumerate(ok) if v}

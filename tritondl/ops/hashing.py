@@ -240,20 +240,25 @@ def effective_cpus() -> int:
     return max(1, n)
 
 
-def choose_device(n_pieces: int, piece_len: int, total: int, cpu_threads: int | None = None) -> str:
+def choose_device(n_pieces: int, piece_len: int, total: int, cpu_threads: int | None = None,
+                  lane_len: int | None = None) -> str:
     """cpu | gpu | hybrid for a batch verify, by the cost model above.  In
     hybrid mode the CPU threads left next to the GPU readers add their rate
     to the GPU's (the native claim rule also hands the GPU's last-kernel
-    latency tail to the CPU, so hybrid is never slower than its GPU part)."""
+    latency tail to the CPU, so hybrid is never slower than its GPU part).
+    ``lane_len``: bytes one GPU lane hashes serially (default ``piece_len``;
+    16 KiB for BEP 52 merkle leaves, where the host still reads whole
+    pieces, so its per-piece overhead counts ``n_pieces`` pieces)."""
     if n_pieces == 0 or not gpu_available():
         return "cpu"
+    lane = lane_len or piece_len
     cpus = cpu_threads or effective_cpus()
     thr = max(1, min(cpus, n_pieces))
-    t_gpu = total / GPU_COPY_BPS + piece_len / GPU_LANE_BPS + GPU_SETUP_S
+    t_gpu = total / GPU_COPY_BPS + lane / GPU_LANE_BPS + GPU_SETUP_S
     t_cpu = (total / CPU_THREAD_BPS + n_pieces * CPU_PIECE_S) / thr
     hthr = hybrid_cpu_threads(cpus)
     cpu_bps = hthr * CPU_THREAD_BPS / (1 + CPU_PIECE_S * CPU_THREAD_BPS / piece_len)
-    t_hyb = max(total / (GPU_COPY_BPS + cpu_bps), piece_len / GPU_LANE_BPS) + GPU_SETUP_S
+    t_hyb = max(total / (GPU_COPY_BPS + cpu_bps), lane / GPU_LANE_BPS) + GPU_SETUP_S
     best = min(t_cpu, t_gpu, t_hyb)
     if best == t_cpu:
         return "cpu"
