@@ -39,8 +39,9 @@ TDL_MB1_TARGET inline void sha1_compress(__m512i s[5], const uint8_t* const p[16
 #define TDL_MB1_ROUND(wt, fimm, k)                                                                     \
   do {                                                                                                 \
     const __m512i f_ = _mm512_ternarylogic_epi32(b, c, d, fimm);                                        \
-    const __m512i tmp_ = _mm512_add_epi32(_mm512_add_epi32(_mm512_rol_epi32(a, 5), f_),                 \
-                                          _mm512_add_epi32(e, _mm512_add_epi32(wt, k)));               \
+    /* rotl5(a) joins last: the new a is two ops deep in a (latency-bound chain) */                    \
+    const __m512i tmp_ = _mm512_add_epi32(_mm512_rol_epi32(a, 5),                                     \
+                                          _mm512_add_epi32(f_, _mm512_add_epi32(e, _mm512_add_epi32(wt, k)))); \
     e = d;                                                                                             \
     d = c;                                                                                             \
     c = _mm512_rol_epi32(b, 30);                                                                       \

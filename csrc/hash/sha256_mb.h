@@ -90,20 +90,25 @@ TDL_MB_TARGET inline void compress(__m512i s[8], const uint8_t* const p[16], siz
     __m512i w[16];
     load_transposed(p, blk * 64, w);
     __m512i a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+// The round is latency-bound (each op waits on the previous round's e / a),
+// so the sums are associated to keep the chains short: h + W + K and
+// d + (h + W + K) do not depend on this round's e and are ready early;
+// new e = ((d + hwk) + Ch) + Σ1 is three ops deep from e, and new
+// a = ((hwk + Ch) + Σ1) + (Σ0 + Maj) four (instead of five for both).
 #define TDL_MB_ROUND(t, wt)                                                                              \
   do {                                                                                                   \
+    const __m512i hwk = _mm512_add_epi32(h, _mm512_add_epi32(                                            \
+                                                wt, _mm512_set1_epi32(static_cast<int>(sha2x::kK[t])))); \
+    const __m512i dhwk = _mm512_add_epi32(d, hwk);                                                       \
     const __m512i s1 = xor3(_mm512_ror_epi32(e, 6), _mm512_ror_epi32(e, 11), _mm512_ror_epi32(e, 25));  \
     const __m512i ch = _mm512_ternarylogic_epi32(e, f, g, 0xca);                                         \
-    const __m512i t1 = _mm512_add_epi32(_mm512_add_epi32(h, s1),                                         \
-                                        _mm512_add_epi32(ch, _mm512_add_epi32(                           \
-                                                                 wt, _mm512_set1_epi32(                  \
-                                                                         static_cast<int>(sha2x::kK[t])))));\
     const __m512i s0 = xor3(_mm512_ror_epi32(a, 2), _mm512_ror_epi32(a, 13), _mm512_ror_epi32(a, 22));  \
     const __m512i mj = _mm512_ternarylogic_epi32(a, b, c, 0xe8);                                         \
+    const __m512i t1 = _mm512_add_epi32(_mm512_add_epi32(hwk, ch), s1);                                  \
     h = g;                                                                                               \
     g = f;                                                                                               \
     f = e;                                                                                               \
-    e = _mm512_add_epi32(d, t1);                                                                         \
+    e = _mm512_add_epi32(_mm512_add_epi32(dhwk, ch), s1);                                                \
     d = c;                                                                                               \
     c = b;                                                                                               \
     b = a;                                                                                               \
