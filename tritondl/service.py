@@ -37,9 +37,11 @@ import asyncio
 import contextlib
 import fcntl
 import os
+import queue
 import shutil
 import signal
 import sys
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
@@ -95,6 +97,42 @@ def _warm_gpu_quietly() -> bool:
         return False
 
 
+class _Reaper:
+    """Deletes finished job dirs on one daemon thread.  A queue put per job
+    replaces an executor submit + future + loop callback per job; the
+    deletion itself (mostly the kernel freeing the file's page cache) stays
+    off the event loop.  ``drain`` returns once everything queued before it
+    is gone (shutdown)."""
+
+    def __init__(self) -> None:
+        self._q: queue.SimpleQueue = queue.SimpleQueue()
+        self._thread: threading.Thread | None = None
+        self._lock = threading.Lock()
+
+    def submit(self, path: str) -> None:
+        if self._thread is None:
+            with self._lock:
+                if self._thread is None:
+                    self._thread = threading.Thread(target=self._run, name="tdl-reaper", daemon=True)
+                    self._thread.start()
+        self._q.put(path)
+
+    def _run(self) -> None:
+        while True:
+            item = self._q.get()
+            if isinstance(item, threading.Event):
+                item.set()
+            else:
+                shutil.rmtree(item, ignore_errors=True)
+
+    def drain(self, timeout: float = 60.0) -> bool:
+        if self._thread is None:
+            return True
+        done = threading.Event()
+        self._q.put(done)
+        return done.wait(timeout)
+
+
 class Service:
     def __init__(self, cfg: Config, *, amqp: Client | None = None, dispatcher: Dispatcher | None = None,
                  uploader: Uploader | None = None, metrics: Metrics | None = None) -> None:
@@ -107,7 +145,7 @@ class Service:
         self._stop = asyncio.Event()
         self._inflight = 0
         self._metrics_runner = None
-        self._cleanups: set[asyncio.Future] = set()
+        self._reaper = _Reaper()                    # deletes finished job dirs off the loop
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
         self.jobs_finished = 0                     # monotonic count of results recorded
         self._finish_waiters: list[tuple[int, asyncio.Future]] = []
@@ -325,9 +363,7 @@ class Service:
                 os.rename(dl_dir, trash)
             except OSError:
                 trash = dl_dir
-            c = asyncio.get_running_loop().run_in_executor(None, shutil.rmtree, trash, True)
-            self._cleanups.add(c)
-            c.add_done_callback(self._cleanups.discard)
+            self._reaper.submit(trash)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -507,8 +543,7 @@ class Service:
             for t in pending:
                 with contextlib.suppress(BaseException):
                     await t
-        if self._cleanups:
-            await asyncio.gather(*self._cleanups, return_exceptions=True)
+        await asyncio.get_running_loop().run_in_executor(None, self._reaper.drain)
         if self.dispatcher is not None:
             await self.dispatcher.stop()
         if self.uploader is not None:
