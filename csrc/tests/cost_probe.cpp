@@ -12,6 +12,9 @@
 //   recv_small       the same with a 256 KiB receive buffer
 //   sendfile         the sender side: sendfile 64 KiB frames (MSG_MORE heads)
 //   unlink           removing the job file
+//   pwrite_reuse     the download's writes into a recycled file (the previous
+//                    job's, renamed into place and resized): cached pages are
+//                    overwritten, none allocated, none freed by an unlink
 //
 // Build + run: python tools/cost_probe.py [--dir DIR] [--reps N]
 #include <fcntl.h>
@@ -384,6 +387,33 @@ void probe_tls(int reps) {
 
 }  // namespace
 
+// what the service's spare-file recycling does per job: rename the finished
+// file into the next job's place, size it, overwrite it
+void probe_reuse(int reps) {
+  std::vector<char> src(1u << 20);
+  for (size_t i = 0; i < src.size(); ++i) src[i] = static_cast<char>(i * 7u);
+  Stat pw;
+  std::string cur = fresh_path();
+  ::close(write_file(cur, src));
+  for (int r = 0; r < 4 * reps; ++r) {
+    const std::string next = fresh_path();
+    const double c = thread_ms(), w = wall_ms();
+    if (::rename(cur.c_str(), next.c_str()) != 0) perror("rename");
+    const int fd = ::open(next.c_str(), O_WRONLY | O_CLOEXEC);
+    if (fd < 0 || ::ftruncate(fd, kLen) != 0) perror("reuse open");
+    for (size_t o = 0; o < kLen; o += 256u << 10) {
+      const size_t m = std::min<size_t>(256u << 10, kLen - o);
+      if (::pwrite(fd, src.data() + (o % (1u << 20)), m, static_cast<off_t>(o)) != static_cast<ssize_t>(m))
+        perror("pwrite");
+    }
+    pw.add(thread_ms() - c, wall_ms() - w);
+    ::close(fd);
+    cur = next;
+  }
+  ::unlink(cur.c_str());
+  report("pwrite_reuse", pw);
+}
+
 int main(int argc, char** argv) {
   int reps = 30;
   for (int i = 1; i + 1 < argc; i += 2) {
@@ -394,6 +424,7 @@ int main(int argc, char** argv) {
               g_dir.c_str(), kLen);
   probe_sha_hot(reps);
   probe_file(reps);
+  probe_reuse(reps);
   probe_sock(reps, 4u << 20, "recv_pwrite", true);
   probe_sock(reps, 256u << 10, "recv_small", false);
   probe_sock(reps, 0, "splice_file", false);

@@ -37,11 +37,9 @@ import asyncio
 import contextlib
 import fcntl
 import os
-import queue
 import shutil
 import signal
 import sys
-import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
@@ -52,7 +50,7 @@ from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
 from .s3.uploader import RESUME_SUFFIX, UploadError, Uploader
 from .select import MEDIA_EXTS, dir_media, predict_media
-from .utils import rawhttp, spares
+from .utils import rawhttp
 from .utils.config import Config
 from .utils.gocompat import go_ext, go_join, go_time_string
 from .utils.log import log
@@ -97,50 +95,6 @@ def _warm_gpu_quietly() -> bool:
         return False
 
 
-class _Reaper:
-    """Deletes finished job dirs on one daemon thread.  A queue put per job
-    replaces an executor submit + future + loop callback per job; the
-    deletion itself (mostly the kernel freeing the file's page cache) stays
-    off the event loop.  ``drain`` returns once everything queued before it
-    is gone (shutdown).  With a spare pool, each dir's largest file is offered
-    to it first (utils/spares.py)."""
-
-    def __init__(self) -> None:
-        self._q: queue.SimpleQueue = queue.SimpleQueue()
-        self._thread: threading.Thread | None = None
-        self._lock = threading.Lock()
-        self.pool: spares.SparePool | None = None
-
-    def submit(self, path: str) -> None:
-        if self._thread is None:
-            with self._lock:
-                if self._thread is None:
-                    self._thread = threading.Thread(target=self._run, name="tdl-reaper", daemon=True)
-                    self._thread.start()
-        self._q.put(path)
-
-    def _run(self) -> None:
-        while True:
-            item = self._q.get()
-            if isinstance(item, threading.Event):
-                item.set()
-                continue
-            pool = self.pool
-            if pool is not None:
-                try:
-                    pool.offer_dir(item)
-                except OSError:
-                    pass
-            shutil.rmtree(item, ignore_errors=True)
-
-    def drain(self, timeout: float = 60.0) -> bool:
-        if self._thread is None:
-            return True
-        done = threading.Event()
-        self._q.put(done)
-        return done.wait(timeout)
-
-
 class Service:
     def __init__(self, cfg: Config, *, amqp: Client | None = None, dispatcher: Dispatcher | None = None,
                  uploader: Uploader | None = None, metrics: Metrics | None = None) -> None:
@@ -153,7 +107,7 @@ class Service:
         self._stop = asyncio.Event()
         self._inflight = 0
         self._metrics_runner = None
-        self._reaper = _Reaper()                    # deletes finished job dirs off the loop
+        self._cleanups: set[asyncio.Future] = set()
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
         self.jobs_finished = 0                     # monotonic count of results recorded
         self._finish_waiters: list[tuple[int, asyncio.Future]] = []
@@ -244,12 +198,6 @@ class Service:
         if self.dispatcher is None:
             self.dispatcher = Dispatcher(cfg.download_dir, default_impls(cfg), cfg.progress_log_interval_s)
         self.dispatcher.start()
-        if cfg.cleanup and cfg.recycle_bytes > 0:
-            base = self.dispatcher.base_dir
-            for stale in spares.stale_pools(base):
-                self._reaper.submit(stale)
-            self._reaper.pool = spares.register(spares.SparePool(
-                base, max_bytes=cfg.recycle_bytes, max_files=max(2, cfg.concurrency + 1)))
         if cfg.gpu_verify != "off":
             # HIP context + hasher set-up off the job path (first torrent resume would pay it).
             # Finished before consuming: importing torch holds the GIL for ~1-2 s, which would
@@ -377,7 +325,9 @@ class Service:
                 os.rename(dl_dir, trash)
             except OSError:
                 trash = dl_dir
-            self._reaper.submit(trash)
+            c = asyncio.get_running_loop().run_in_executor(None, shutil.rmtree, trash, True)
+            self._cleanups.add(c)
+            c.add_done_callback(self._cleanups.discard)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -557,13 +507,8 @@ class Service:
             for t in pending:
                 with contextlib.suppress(BaseException):
                     await t
-        pool, self._reaper.pool = self._reaper.pool, None
-        if pool is not None:
-            spares.unregister(pool)
-            self._reaper.submit(pool.root)
-        await asyncio.get_running_loop().run_in_executor(None, self._reaper.drain)
-        if pool is not None:
-            pool.clear()                    # whatever was offered while the rmtree was queued
+        if self._cleanups:
+            await asyncio.gather(*self._cleanups, return_exceptions=True)
         if self.dispatcher is not None:
             await self.dispatcher.stop()
         if self.uploader is not None:

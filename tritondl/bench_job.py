@@ -192,6 +192,8 @@ class JobStack:
         cfg.concurrency = self.concurrency
         cfg.prefetch = self.prefetch
         cfg.cleanup = True          # keep disk bounded across thousands of bench jobs
+        # spare-file recycling (utils/spares.py) is on with cleanup; 0 = the A/B switch
+        cfg.recycle_bytes = int(os.environ.get("TRITONDL_RECYCLE_BYTES", cfg.recycle_bytes))
         cfg.retry_delay_s = 0.0
         cfg.max_retries = 0
         cfg.progress_log_interval_s = 0

@@ -58,7 +58,7 @@ import aiohttp
 from yarl import URL
 
 from ..utils import proxy as _proxy
-from ..utils import rawhttp
+from ..utils import rawhttp, spares
 from ..utils.disk import DiskSpaceError, check_space
 from ..utils.log import log
 from .registry import ClientRegister, ProgressSink
@@ -440,7 +440,13 @@ class HTTPDownloader:
                     first.close()
                 raise HTTPDownloadError(str(e)) from e
         if not resumable:
-            fd = os.open(part, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            # a spare (a finished job's file, --cleanup only) is overwritten in place:
+            # its page cache is reused instead of freed and allocated again (utils/spares.py)
+            pool = spares.pool_for(base_dir) if probe.size else None
+            if pool is not None and pool.take(part):
+                fd = os.open(part, os.O_WRONLY)
+            else:
+                fd = os.open(part, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
             try:
                 if probe.size:
                     os.ftruncate(fd, probe.size)

@@ -71,6 +71,10 @@ class Config:
     dead_letter_topic: str = ""                 # "" => "<consume_topic>.dead"
     drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
     cleanup: bool = False                       # B15: off for parity
+    # with cleanup: keep up to this many bytes of finished job files as spares that new
+    # downloads are renamed into and overwrite, instead of freeing and re-allocating
+    # their page cache per job (utils/spares.py; 0 = delete every file)
+    recycle_bytes: int = 1 << 30
     disk_reserve_bytes: int = 0                 # free-space preflight keeps this much free
     stream_upload: bool = True                  # overlap HTTP fetch with S3 upload
     http_segments: int = 4                      # max parallel Range streams per HTTP file
@@ -169,7 +173,8 @@ class Config:
                 "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
                 "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
                 "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
-                "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns"}
+                "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
+                "RECYCLE_BYTES": "recycle_bytes"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
