@@ -192,6 +192,7 @@ def main() -> int:
         if a.cpuprofile:
             from tritondl.utils.profiler import CPUProfiler
             prof = CPUProfiler(a.cpuprofile if world == 1 else f"{a.cpuprofile}.r{rank}")
+        stack.cpu_seconds()              # first call imports psutil: keep it out of the profiled window
         barrier()
         if prof is not None:
             prof.start()
