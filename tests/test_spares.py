@@ -63,6 +63,9 @@ def test_pool_bounds_and_lifo(tmp_path):
         os.symlink(big, jd / "link.mkv")
         pool.offer_dir(str(jd))
         assert not os.path.exists(big) and pool.take(str(job / "w.part"))
+        # release(): a download short of disk space deletes the spares first
+        assert pool.offer(_file(tmp_path / "d", 2 << 20)) and pool.release() == 2 << 20
+        assert os.listdir(pool.root) == [] and not pool.take(str(job / "v.part"))
     finally:
         spares.unregister(pool)
         pool.clear()
@@ -134,3 +137,37 @@ def test_recycled_files_never_leak_previous_bytes(tmp_path):
         assert not [n for n in os.listdir(cfg.download_dir) if n.startswith(spares.PREFIX)]
         assert spares.pool_for(os.path.join(cfg.download_dir, "x")) is None
     asyncio.run(asyncio.wait_for(main(), 120))
+
+
+def test_download_short_of_space_deletes_spares_first(tmp_path, monkeypatch):
+    import tritondl.fetch.http as fh
+    from tritondl.utils.disk import DiskSpaceError
+
+    base = tmp_path / "dl"
+    (base / "job").mkdir(parents=True)
+    pool = spares.register(spares.SparePool(str(base)))
+    checks = []
+
+    def check_space(path, need, reserve=0):
+        checks.append(len(pool._files))
+        if pool._files:                    # the spares are what fills the disk
+            raise DiskSpaceError("no space")
+    monkeypatch.setattr(fh, "check_space", check_space)
+    data = random.Random(1).randbytes(3 << 20)
+
+    async def main():
+        origin = await Origin().start()
+        try:
+            url = origin.add("/m/a.mkv", data)
+            assert pool.offer(_file(tmp_path / "old", 2 << 20, b"o"))
+            await HTTPDownloader(progress_interval=0.05).download(str(base / "job"), lambda *a: None, url)
+        finally:
+            await origin.stop()
+    try:
+        asyncio.run(asyncio.wait_for(main(), 60))
+        with open(base / "job" / "a.mkv", "rb") as f:
+            assert f.read() == data
+        assert checks == [1, 0] and pool.taken == 0 and os.listdir(pool.root) == []
+    finally:
+        spares.unregister(pool)
+        pool.clear()

@@ -434,7 +434,13 @@ class HTTPDownloader:
         if probe.size:
             have = sum(sg[2] for sg in segs) if resumable else 0
             try:
-                check_space(base_dir, probe.size - have, self.disk_reserve)
+                try:
+                    check_space(base_dir, probe.size - have, self.disk_reserve)
+                except DiskSpaceError:
+                    pool = spares.pool_for(base_dir)
+                    if pool is None or not pool.release():
+                        raise
+                    check_space(base_dir, probe.size - have, self.disk_reserve)   # spares deleted: again
             except DiskSpaceError as e:
                 if first is not None:
                     first.close()

@@ -37,11 +37,12 @@ _lock = threading.Lock()
 
 class SparePool:
     def __init__(self, base_dir: str, max_bytes: int = 1 << 30, max_files: int = 4,
-                 max_file_bytes: int = 256 << 20, min_file_bytes: int = 1 << 20) -> None:
+                 max_file_bytes: int | None = None, min_file_bytes: int = 1 << 20) -> None:
         self.base_dir = os.path.abspath(base_dir)
         self.root = os.path.join(self.base_dir, f"{PREFIX}{os.getpid()}")
         self.max_bytes, self.max_files = max_bytes, max_files
-        self.max_file_bytes, self.min_file_bytes = max_file_bytes, min_file_bytes
+        self.max_file_bytes = max_bytes if max_file_bytes is None else max_file_bytes
+        self.min_file_bytes = min_file_bytes
         self._files: list[tuple[str, int]] = []    # (path, size), most recent last
         self._bytes = 0
         self._seq = 0
@@ -104,6 +105,18 @@ class SparePool:
                 self.taken += 1
                 return True
         return False
+
+    def release(self) -> int:
+        """Delete every spare (a download needs their disk space); returns
+        the bytes freed."""
+        with self._mu:
+            files, self._files, self._bytes = self._files, [], 0
+        for path, _size in files:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+        return sum(size for _p, size in files)
 
     def clear(self) -> None:
         with self._mu:
