@@ -171,3 +171,4 @@ def test_download_short_of_space_deletes_spares_first(tmp_path, monkeypatch):
     finally:
         spares.unregister(pool)
         pool.clear()
+

@@ -148,6 +148,7 @@ async def job_bench(a) -> int:
         cfg = Config()
         cfg.download_dir = os.path.join(td, "downloading")
         cfg.cleanup, cfg.max_retries, cfg.retry_delay_s = True, 0, 0.0
+        cfg.recycle_bytes = int(os.environ.get("TRITONDL_RECYCLE_BYTES", cfg.recycle_bytes))
         cfg.progress_log_interval_s, cfg.heartbeat_s = 0, 0
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
                                              encryption=a.encryption, native_wire=not a.python_wire),

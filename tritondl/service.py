@@ -249,7 +249,7 @@ class Service:
             for stale in spares.stale_pools(base):
                 self._reaper.submit(stale)
             self._reaper.pool = spares.register(spares.SparePool(
-                base, max_bytes=cfg.recycle_bytes, max_files=max(2, cfg.concurrency + 1)))
+                base, max_bytes=cfg.recycle_bytes, max_files=64))
         if cfg.gpu_verify != "off":
             # HIP context + hasher set-up off the job path (first torrent resume would pay it).
             # Finished before consuming: importing torch holds the GIL for ~1-2 s, which would

@@ -7,15 +7,19 @@ that is ~0.25 ms for the unlink plus ~0.7 ms of page allocation inside the
 receive pump's pwrites, against ~0.3 ms to overwrite pages that are already
 there (``tools/cost_probe.py`` ``unlink`` / ``pwrite_new`` / ``pwrite_reuse``).
 
-So the reaper offers each finished job's largest file to a small per-process
-pool (``<download_dir>/.tritondl-spare-<pid>/``) instead of deleting it, and
-the HTTP downloader, starting a fresh (non-resumed) ``.part`` file, renames a
-spare into place and resizes it instead of creating one.  Bytes the new
-download has not written yet are the previous job's; nothing reads them:
+So the reaper offers a finished job's files (largest first) to a small
+per-process pool (``<download_dir>/.tritondl-spare-<pid>/``) instead of
+deleting them, and the HTTP downloader, starting a fresh (non-resumed)
+``.part`` file, renames a spare into place and resizes it instead of
+creating one.  Bytes the new download has not written yet are the previous
+job's; nothing reads them:
 
 * the streamed upload only reads ranges the receive pumps have published;
 * resume trusts only the segment counts saved in ``.part.meta``;
 * the ``.part`` becomes the destination only after every byte arrived.
+
+Torrent storage does not take spares: the 1 GiB pack job measured no
+faster with them (``profiles/r03_recycle_bt/``).
 
 The pool is bounded (files, total bytes, bytes per file), lives on the
 download filesystem (a rename, never a copy), is deleted on shutdown, and
@@ -74,9 +78,10 @@ class SparePool:
             self.offered += 1
             return True
 
-    def offer_dir(self, path: str) -> None:
-        """Offer the largest regular file under the job dir ``path``."""
-        best, best_size = "", 0
+    def offer_dir(self, path: str) -> int:
+        """Offer the regular files under the job dir ``path``, largest first,
+        until the pool is full; returns how many it kept."""
+        found = []
         for dirpath, _dirs, names in os.walk(path):
             for n in names:
                 p = os.path.join(dirpath, n)
@@ -84,10 +89,15 @@ class SparePool:
                     s = os.stat(p, follow_symlinks=False)
                 except OSError:
                     continue
-                if s.st_size > best_size and os.path.isfile(p) and not os.path.islink(p):
-                    best, best_size = p, s.st_size
-        if best:
-            self.offer(best)
+                if self.min_file_bytes <= s.st_size <= self.max_file_bytes and os.path.isfile(p) \
+                        and not os.path.islink(p):
+                    found.append((s.st_size, p))
+        kept = 0
+        for _size, p in sorted(found, reverse=True):
+            if not self.offer(p):
+                break
+            kept += 1
+        return kept
 
     # ---------------------------------------------------------------- downloader side
     def take(self, dst: str) -> bool:
