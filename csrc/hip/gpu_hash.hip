@@ -20,8 +20,13 @@
 //    latency hides under ~1.5k cycles of ALU work.  Lanes stride by
 //    piece_len, so each wave-load touches 64 lines; every line is consumed in
 //    full by two consecutive blocks while it is still L2-resident.
-//  * Host side: pinned double-buffered staging, one HIP stream per slot:
-//    parallel pread() of batch b+1 overlaps H2D + kernel + D2H of batch b.
+//  * Host side: runs whose bytes sit in one fully present, page-cache
+//    resident file are DMA'd to HBM straight from the file's page cache: the
+//    read-only file mapping is registered with hipHostRegister in 64 MiB
+//    blocks (~2-7 ms per GiB, then 57.6 GB/s, the same as from pinned
+//    memory; profiles/r03_reg_probe).  Everything else (cold pages, runs
+//    straddling files, BEP 47 padding, short files) goes through a ring of
+//    pinned staging slots filled by a pread() reader pool.
 //  * Hybrid mode (cpu_threads > 0): the whole job is host->HBM bound
 //    (~45 GB/s of page-cache copies + PCIe), so the CPU's SHA-NI threads
 //    verify pieces from the BACK of the layout while the GPU pipeline claims
@@ -37,6 +42,8 @@
 #include "../hash/hash_core.h"  // OpenSSL SHA-NI path for the CPU half of hybrid verification
 
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -45,9 +52,11 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -390,6 +399,148 @@ class ReaderPool {
   bool stop_ = false;
 };
 
+// Page cache -> HBM with no CPU copy.  A run of pieces that lies inside one
+// file that is fully present and resident in the page cache is copied by the
+// DMA engine straight from the file's read-only mapping, registered with
+// hipHostRegister in kBlock-sized blocks (a run may span two; each copy
+// stays inside one registration).  Blocks are reference-counted by the HBM
+// windows whose copies use them and unregistered once those windows are
+// hashed, so at most about two windows' worth of page cache is pinned.
+// TRITONDL_GPU_DIRECT=0 turns it off (everything through pinned staging).
+class DirectSource {
+ public:
+  explicit DirectSource(const std::vector<Span>& spans) : spans_(spans), maps_(spans.size()) {
+    const char* env = std::getenv("TRITONDL_GPU_DIRECT");
+    on_ = !(env && (env[0] == '0' || env[0] == 'n' || env[0] == 'o'));
+    const long pg = ::sysconf(_SC_PAGESIZE);
+    page_ = pg > 0 ? static_cast<size_t>(pg) : 4096;
+    const char* mb = std::getenv("TRITONDL_GPU_DIRECT_BLOCK_MB");
+    if (mb && std::atol(mb) > 0) kBlock = static_cast<size_t>(std::atol(mb)) << 20;
+    const char* keep = std::getenv("TRITONDL_GPU_DIRECT_KEEP");
+    keep_ = keep && keep[0] == '1';
+  }
+  ~DirectSource() { release_all(); }
+  DirectSource(const DirectSource&) = delete;
+  DirectSource& operator=(const DirectSource&) = delete;
+
+  bool on() const { return on_; }
+  size_t bytes() const { return bytes_; }
+
+  // Can layout bytes [off, off+len) go direct?  Registers the blocks they
+  // need; false leaves the run to the staging path.
+  bool prepare(size_t off, size_t len) {
+    if (!on_ || len == 0) return false;
+    const int i = span_of(off, len);
+    if (i < 0) return false;
+    Map& m = mapping(i);
+    if (!m.base) return false;
+    const size_t fo = off - static_cast<size_t>(spans_[i].start);
+    const size_t a = fo / page_ * page_;
+    const size_t np = (fo + len - a + page_ - 1) / page_;
+    resident_.resize(np);
+    if (::mincore(m.base + a, np * page_, resident_.data()) != 0) return false;
+    for (unsigned char r : resident_)
+      if (!(r & 1)) return false;  // cold pages: parallel preads beat one faulting thread
+    for (size_t b = fo / kBlock; b <= (fo + len - 1) / kBlock; ++b) {
+      const uint64_t key = (static_cast<uint64_t>(i) << 32) | b;
+      if (regs_.count(key)) continue;
+      uint8_t* p = m.base + b * kBlock;
+      const size_t rl = std::min(kBlock, m.len - b * kBlock);
+      if (hipHostRegister(p, rl, hipHostRegisterReadOnly) != hipSuccess) {
+        (void)hipGetLastError();
+        on_ = false;  // not supported here: stop trying for this call
+        return false;
+      }
+      regs_.emplace(key, Reg{p, 0});
+    }
+    return true;
+  }
+
+  // Enqueue the H2D copies of a prepared run on `s`; `used` collects the
+  // blocks the copies read (released by unref once they completed).
+  void enqueue(uint8_t* dst, size_t off, size_t len, hipStream_t s, std::vector<uint64_t>& used) {
+    const int i = span_of(off, len);
+    const Map& m = maps_[i];
+    const size_t fo = off - static_cast<size_t>(spans_[i].start);
+    for (size_t b = fo / kBlock; b <= (fo + len - 1) / kBlock; ++b) {
+      const size_t sa = std::max(fo, b * kBlock), se = std::min(fo + len, (b + 1) * kBlock);
+      const uint64_t key = (static_cast<uint64_t>(i) << 32) | b;
+      HIP_CHECK(hipMemcpyAsync(dst + (sa - fo), m.base + sa, se - sa, hipMemcpyHostToDevice, s));
+      ++regs_.at(key).refs;
+      used.push_back(key);
+    }
+    bytes_ += len;
+  }
+
+  // The copies that used these blocks have completed.
+  void unref(std::vector<uint64_t>& used) {
+    if (keep_) {  // unregister everything at the end of the call instead
+      used.clear();
+      return;
+    }
+    for (uint64_t key : used) {
+      auto it = regs_.find(key);
+      if (it == regs_.end()) continue;
+      if (--it->second.refs <= 0) {
+        (void)hipHostUnregister(it->second.p);
+        regs_.erase(it);
+      }
+    }
+    used.clear();
+  }
+
+  // Every copy has completed (or the streams were synchronised after an error).
+  void release_all() {
+    for (auto& kv : regs_) (void)hipHostUnregister(kv.second.p);
+    regs_.clear();
+    for (auto& m : maps_)
+      if (m.base) ::munmap(m.base, m.len);
+    maps_.assign(maps_.size(), Map{});
+  }
+
+ private:
+  struct Map {
+    uint8_t* base = nullptr;
+    size_t len = 0;  // mapped bytes (file length rounded up to a page)
+    bool tried = false;
+  };
+  struct Reg {
+    uint8_t* p;
+    int refs;
+  };
+  int span_of(size_t off, size_t len) const {
+    for (size_t k = 0; k < spans_.size(); ++k) {
+      const Span& sp = spans_[k];
+      const size_t a = static_cast<size_t>(sp.start), e = a + static_cast<size_t>(sp.length);
+      if (off >= a && off < e) return (sp.fd >= 0 && off + len <= e) ? static_cast<int>(k) : -1;
+    }
+    return -1;
+  }
+  Map& mapping(int i) {
+    Map& m = maps_[i];
+    if (m.tried) return m;
+    m.tried = true;
+    const Span& sp = spans_[i];
+    struct stat st {};
+    if (sp.length <= 0 || ::fstat(sp.fd, &st) != 0 || st.st_size < sp.length) return m;  // short file: staging
+    const size_t len = (static_cast<size_t>(sp.length) + page_ - 1) / page_ * page_;
+    void* p = ::mmap(nullptr, len, PROT_READ, MAP_SHARED, sp.fd, 0);
+    if (p == MAP_FAILED) return m;
+    m.base = static_cast<uint8_t*>(p);
+    m.len = len;
+    return m;
+  }
+  size_t kBlock = 64u << 20;
+  bool keep_ = false;
+  const std::vector<Span>& spans_;
+  std::vector<Map> maps_;
+  std::map<uint64_t, Reg> regs_;
+  std::vector<unsigned char> resident_;
+  size_t page_ = 4096;
+  size_t bytes_ = 0;
+  bool on_ = true;
+};
+
 // Host pipeline: disk / host memory -> pinned staging (a ring of kStages
 // slots filled by the reader pool, up to kStages-1 ahead of the DMA) -> HBM
 // window -> ONE kernel over every piece of the window -> digests.
@@ -502,17 +653,20 @@ class GpuHasher {
     complete.assign(n, '\0');
     py::gil_scoped_release nogil;
     try {
+      DirectSource ds(spans);  // unmapped before the spans' fds close
       if (cpu_threads > 0) {
-        hybrid_digest(alg, spans, piece_len, total, n, cpu_threads, digests, complete);
+        hybrid_digest(alg, spans, piece_len, total, n, cpu_threads, digests, complete, &ds);
       } else {
         run_gpu_only(alg, piece_len, total, n,
                      [&](uint8_t* dst, size_t off, size_t len, char* comp) { read_unit(spans, dst, off, len, piece_len, comp); },
                      [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
                        std::memcpy(&digests[first * dl], d, count * dl);
                        for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
-                     });
+                     },
+                     &ds);
         last_gpu_pieces_ = n;
       }
+      last_direct_bytes_ = ds.bytes();
     } catch (...) {
       close_spans(spans);
       throw;
@@ -589,6 +743,7 @@ class GpuHasher {
     bool pending = false;
     size_t first = 0, count = 0;
     std::vector<char> complete;
+    std::vector<uint64_t> regs;  // DirectSource blocks its copies read
   };
 
   void ensure_stage(Stage& st, size_t bytes) {
@@ -703,7 +858,7 @@ class GpuHasher {
   // done — up to kStages-1 slots are being filled while one is in flight.
   template <class Claim, class Unit, class Harvest>
   void run_windows(int alg, size_t piece_len, size_t total, size_t n, size_t wbytes, Claim&& claim, Unit&& unit,
-                   Harvest&& harvest) {
+                   Harvest&& harvest, DirectSource* ds = nullptr) {
     HIP_CHECK(hipSetDevice(device_));
     trace_recs_.clear();
     timeline_.clear();
@@ -736,6 +891,7 @@ class GpuHasher {
       if (!w.pending) return;
       HIP_CHECK(hipEventSynchronize(w.done));
       harvest(w.first, w.count, w.h_out, w.complete);
+      if (ds) ds->unref(w.regs);  // its copies have landed (the kernel waited for them)
       w.pending = false;
     };
     size_t widx = 0, sidx = 0;
@@ -754,6 +910,17 @@ class GpuHasher {
           }
           if (count == 0) first = got.first;
           if (got.first != first + count) throw std::logic_error("non-contiguous GPU claim");
+          {
+            const size_t off = got.first * piece_len;
+            const size_t len = std::min(total - off, got.second * piece_len);
+            if (ds && ds->prepare(off, len)) {  // page cache -> HBM, no staging copy
+              trace_begin(copy_stream_, "h2d_direct", len);
+              ds->enqueue(w.d + count * piece_len, off, len, copy_stream_, w.regs);
+              trace_end(copy_stream_);
+              count += got.second;
+              continue;
+            }
+          }
           if (fills.size() == static_cast<size_t>(kStages)) push_h2d(w);
           const int slot = static_cast<int>(sidx++ % kStages);
           Stage& st = stage_[slot];
@@ -805,7 +972,10 @@ class GpuHasher {
       hipStreamSynchronize(copy_stream_);
       hipStreamSynchronize(compute_stream_);
       for (auto& st : stage_) st.used = false;
-      for (auto& w : win_) w.pending = false;
+      for (auto& w : win_) {
+        w.pending = false;
+        if (ds) ds->unref(w.regs);
+      }
       for (auto& r : trace_recs_) {
         hipEventDestroy(r.a);
         hipEventDestroy(r.b);
@@ -818,7 +988,8 @@ class GpuHasher {
 
   // The whole layout front-to-back on the GPU (no CPU share).
   template <class Fill, class Harvest>
-  void run_gpu_only(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest) {
+  void run_gpu_only(int alg, size_t piece_len, size_t total, size_t n, Fill&& fill, Harvest&& harvest,
+                    DirectSource* ds = nullptr) {
     size_t front = 0;
     run_windows(alg, piece_len, total, n, window_bytes_for(total, piece_len),
                 [&](size_t mx) {
@@ -827,7 +998,7 @@ class GpuHasher {
                   front += c;
                   return std::make_pair(f, c);
                 },
-                fill, harvest);
+                fill, harvest, ds);
   }
 
  public:
@@ -835,7 +1006,7 @@ class GpuHasher {
   // the front and `cpu_threads` SHA-NI threads claiming >= 1 MiB units from
   // the back.  Fills digests (n*dl) and complete (n) for all pieces.
   void hybrid_digest(int alg, const std::vector<Span>& spans, size_t piece_len, size_t total, size_t n,
-                     int cpu_threads, std::string& digests, std::string& complete) {
+                     int cpu_threads, std::string& digests, std::string& complete, DirectSource* ds = nullptr) {
     const int dl = digest_len(alg);
     const EVP_MD* md = alg == 1 ? tritondl_hash::sha1_md() : tritondl_hash::sha256_md();
     std::mutex mu;
@@ -845,7 +1016,8 @@ class GpuHasher {
     // one more GPU window costs at least the per-lane latency of one piece
     // (one lane per piece, ~55 MB/s/lane measured) plus set-up
     const double kernel_s = static_cast<double>(piece_len) / 55e6 + 1e-3;
-    constexpr double kCopyBps = 40e9;  // page cache -> pinned -> HBM, measured ~36-45 GB/s
+    // page cache -> HBM: ~57 GB/s direct (registered mapping), ~36-45 GB/s through pinned staging
+    const double kCopyBps = ds && ds->on() ? 55e9 : 40e9;
     // pieces per CPU claim: >= 16 for the host's 16-lane AVX-512 kernels
     // (pieces up to 1 MiB: a claim's buffer is 16 pieces per CPU thread),
     // else >= 2 for SHA-NI pairs
@@ -926,7 +1098,8 @@ class GpuHasher {
                   [&](size_t first, size_t count, const uint8_t* d, const std::vector<char>& comp) {
                     std::memcpy(&digests[first * dl], d, count * dl);
                     for (size_t k = 0; k < count; ++k) complete[first + k] = comp[k];
-                  });
+                  },
+                  ds);
     } catch (...) {
       {
         std::lock_guard<std::mutex> g(mu);
@@ -941,12 +1114,14 @@ class GpuHasher {
   }
 
   size_t last_gpu_pieces() const { return last_gpu_pieces_; }
+  size_t last_direct_bytes() const { return last_direct_bytes_; }
   bool trace() const { return trace_; }
   void set_trace(bool on) { trace_ = on; }
   std::vector<std::tuple<std::string, float, float, size_t>> last_timeline() const { return timeline_; }
 
  private:
   size_t last_gpu_pieces_ = 0;
+  size_t last_direct_bytes_ = 0;
   int device_;
   size_t stage_req_;
   int readers_;
@@ -1117,6 +1292,8 @@ PYBIND11_MODULE(_gpu_hash, m) {
                              "[(kind, start_ms, end_ms, bytes)] of the last call, relative to its first op")
       .def_property_readonly("last_gpu_pieces", &GpuHasher::last_gpu_pieces,
                              "pieces the GPU hashed in the last verify/digest call (the rest: CPU threads)")
+      .def_property_readonly("last_direct_bytes", &GpuHasher::last_direct_bytes,
+                             "bytes of the last verify/digest call DMA'd straight from the page cache")
       .def("release", &GpuHasher::release)
       .def("window_bytes_for", &GpuHasher::window_bytes_for)
       .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)

@@ -193,7 +193,14 @@ def test_gpu_many_small_windows(tmp_path, window_pieces):
 def test_choose_device_cost_model(monkeypatch):
     monkeypatch.setattr(hashing, "gpu_available", lambda: True)
     # many small pieces: GPU (lane-parallel) wins against a per-GPU host share, and the
-    # 8 CPUs left beside its readers add their SHA-NI rate (hybrid)
+    # CPUs left beside it add their hashing rate (hybrid): all but one when its copies
+    # come straight from the page cache, the ones the staging readers leave otherwise
+    monkeypatch.setenv("TRITONDL_GPU_DIRECT", "1")
+    assert hashing.hybrid_cpu_threads(16) == 15
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=9) == "hybrid"
+    assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=2) == "gpu"
+    monkeypatch.setenv("TRITONDL_GPU_DIRECT", "0")
+    assert hashing.hybrid_cpu_threads(16) == 16 - hashing.GPU_READERS
     assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=16) == "hybrid"
     assert hashing.choose_device(65536, 16384, 65536 * 16384, cpu_threads=9) == "gpu"
     # few huge pieces: one lane per piece starves the GPU
@@ -243,12 +250,42 @@ def test_gpu_pipeline_timeline_trace(tmp_path):
         tl = h.last_timeline
     finally:
         h.trace = False
-    assert sum(n for k, _a, _b, n in tl if k == "h2d") == len(blob)
+    assert sum(n for k, _a, _b, n in tl if k.startswith("h2d")) == len(blob)     # staged + direct
     kernels = [x for x in tl if x[0] == "kernel"]
     assert len(kernels) == -(-len(blob) // (4 << 20))
     assert all(0 <= a <= b for _k, a, b, _n in tl)
     summ = hashing.timeline_summary(tl)
     assert summ["h2d_count"] >= 16 and summ["kernels"] == len(kernels)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu_threads", [0, 3])
+def test_gpu_direct_from_page_cache(tmp_path, monkeypatch, cpu_threads):
+    """Runs inside one fully present, resident file are DMA'd straight from the
+    page cache (registered read-only mappings); runs straddling files, padding
+    and short files go through staging.  Same verdicts either way, and the
+    same as with the direct path switched off."""
+    piece_len = 65536
+    # 5 MiB + a 3-byte file + 4 MiB: pieces straddle the file boundaries
+    files, blob, exp = _make_torrent_layout(tmp_path, [5_000_000, 3, 4_200_000, 2_000_000], piece_len)
+    n = len(exp) // 20
+    h = hashing.gpu_hasher(batch_bytes=1 << 20, window_bytes=2 << 20)
+    monkeypatch.setenv("TRITONDL_GPU_DIRECT", "1")
+    assert h.verify_files(files, piece_len, exp, "sha1", cpu_threads=cpu_threads) == b"\x01" * n
+    direct = h.last_direct_bytes
+    if cpu_threads == 0:
+        assert direct > len(blob) // 2          # the GPU saw every piece; most runs are in one file
+    assert direct <= len(blob)
+    with open(files[2][0], "r+b") as f:      # corrupt a piece inside a file
+        f.seek(1_000_000)
+        f.write(b"\xff\x00\xee")
+    os.truncate(files[3][0], 1_000_000)       # a short file: its runs take the staging path
+    host = hashing.verify_pieces(files, piece_len, exp, device="cpu")
+    assert 0 < sum(host) < n
+    assert h.verify_files(files, piece_len, exp, "sha1", cpu_threads=cpu_threads) == host
+    monkeypatch.setenv("TRITONDL_GPU_DIRECT", "0")
+    assert h.verify_files(files, piece_len, exp, "sha1", cpu_threads=cpu_threads) == host
+    assert h.last_direct_bytes == 0
 
 
 def test_timeline_summary_math():

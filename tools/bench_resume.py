@@ -32,6 +32,7 @@ async def main() -> int:
     ap.add_argument("--version", type=int, default=2, choices=[1, 2, 3])
     ap.add_argument("--device", nargs="*", default=["cpu", "gpu"])
     ap.add_argument("--reps", type=int, default=2, help="runs per device; the first GPU run pays HIP set-up")
+    ap.add_argument("--trace", action="store_true", help="GPU event timeline summary per run")
     a = ap.parse_args()
     import numpy as np
 
@@ -78,6 +79,8 @@ async def main() -> int:
                 for suffix in ("", "-wal", "-shm"):
                     if os.path.exists(db + suffix):
                         os.remove(db + suffix)
+                if a.trace and dev in ("gpu", "hybrid"):
+                    hashing.gpu_hasher().trace = True
                 d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device=dev), use_dht=False,
                                       progress_interval=1.0)
                 spent["verify_s"] = 0.0
@@ -90,6 +93,7 @@ async def main() -> int:
                     if dev != "gpu":
                         extra["gpu_share"] = round(h.last_gpu_pieces / max(1, info.num_pieces if info.pieces
                                                                             else -(-info.total_length // 16384)), 3)
+                    extra["direct_share"] = round(h.last_direct_bytes / max(1, info.total_length), 3)
                     if h.trace:
                         extra["gpu_timeline"] = hashing.timeline_summary(h.last_timeline)
                 print(json.dumps({"metric": "resume_job_seconds", "device": dev, "run": "cold" if rep == 0 else "warm",

@@ -181,12 +181,13 @@ def timeline_summary(tl) -> dict:
             else:
                 j += 1
         return tot
-    h2d = union([(a, b) for k, a, b, _n in tl if k == "h2d"])
+    h2d = union([(a, b) for k, a, b, _n in tl if k.startswith("h2d")])        # staged + direct copies
     ker = union([(a, b) for k, a, b, _n in tl if k == "kernel"])
-    nbytes = sum(n for k, _a, _b, n in tl if k == "h2d")
+    nbytes = sum(n for k, _a, _b, n in tl if k.startswith("h2d"))
     busy = sum(b - a for a, b in h2d)
     span = max((b for _k, _a, b, _n in tl), default=0.0)
-    return {"h2d_ms": round(busy, 3), "h2d_count": sum(1 for x in tl if x[0] == "h2d"),
+    return {"h2d_ms": round(busy, 3), "h2d_count": sum(1 for x in tl if x[0].startswith("h2d")),
+            "h2d_direct_count": sum(1 for x in tl if x[0] == "h2d_direct"),
             "kernel_ms": round(sum(b - a for a, b in ker), 3), "kernels": sum(1 for x in tl if x[0] == "kernel"),
             "kernel_under_h2d_ms": round(inter(ker, h2d), 3), "span_ms": round(span, 3),
             "h2d_GBps_busy": round(nbytes / busy / 1e6, 1) if busy else None}
@@ -202,13 +203,25 @@ def _resolve(device: str) -> str:
     return device
 
 
+def gpu_direct() -> bool:
+    """Resident file data is DMA'd to HBM straight from the page cache
+    (registered read-only mappings, no reader threads); ``TRITONDL_GPU_DIRECT=0``
+    sends everything through the pinned staging ring."""
+    return os.environ.get("TRITONDL_GPU_DIRECT", "1")[:1] not in ("0", "n", "o")
+
+
 def hybrid_cpu_threads(cpus: int | None = None) -> int:
-    """SHA-NI threads that work next to the GPU pipeline's readers
-    (``TRITONDL_HYBRID_CPU_THREADS`` overrides)."""
+    """Host hashing threads that work next to the GPU pipeline
+    (``TRITONDL_HYBRID_CPU_THREADS`` overrides): every CPU but the one driving
+    the GPU when its copies come straight from the page cache, else the CPUs
+    left by the staging readers."""
     env = os.environ.get("TRITONDL_HYBRID_CPU_THREADS")
     if env:
         return max(1, int(env))
-    return max(1, (cpus or effective_cpus()) - int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS))))
+    n = cpus or effective_cpus()
+    if gpu_direct():
+        return max(1, n - 1)
+    return max(1, n - int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS))))
 
 
 # Cost model for device="auto" batch verification, calibrated on MI355X with
@@ -219,7 +232,7 @@ def hybrid_cpu_threads(cpus: int | None = None) -> int:
 # with the two-stream SHA-NI pairs (8 GiB v1 resume on 16 threads: 35 -> 55
 # GB/s), ~4.4 GB/s with the 16-lane AVX-512 SHA-1 (70 GB/s on 16 threads,
 # profiles/r03_sha1_mb), plus ~15 us of per-piece overhead.
-GPU_COPY_BPS = 45e9
+GPU_COPY_BPS = 55e9 if gpu_direct() else 45e9   # direct from the page cache: 57.6 GB/s (profiles/r03_reg_probe)
 GPU_LANE_BPS = 55e6
 GPU_SETUP_S = 5e-3
 CPU_THREAD_BPS = (4.4e9 if sha_mb() else
@@ -262,7 +275,7 @@ def choose_device(n_pieces: int, piece_len: int, total: int, cpu_threads: int | 
     best = min(t_cpu, t_gpu, t_hyb)
     if best == t_cpu:
         return "cpu"
-    return "hybrid" if best == t_hyb and cpus - GPU_READERS >= 2 else "gpu"
+    return "hybrid" if best == t_hyb and hthr >= 2 else "gpu"
 
 
 def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", threads: int = 0) -> bytes:
