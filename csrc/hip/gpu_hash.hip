@@ -22,7 +22,7 @@
 //    full by two consecutive blocks while it is still L2-resident.
 //  * Host side: runs whose bytes sit in one fully present, page-cache
 //    resident file are DMA'd to HBM straight from the file's page cache: the
-//    read-only file mapping is registered with hipHostRegister in 64 MiB
+//    read-only file mapping is registered with hipHostRegister in 256 MiB
 //    blocks (~2-7 ms per GiB, then 57.6 GB/s, the same as from pinned
 //    memory; profiles/r03_reg_probe).  Everything else (cold pages, runs
 //    straddling files, BEP 47 padding, short files) goes through a ring of
@@ -402,7 +402,7 @@ class ReaderPool {
 // Page cache -> HBM with no CPU copy.  A run of pieces that lies inside one
 // file that is fully present and resident in the page cache is copied by the
 // DMA engine straight from the file's read-only mapping, registered with
-// hipHostRegister in kBlock-sized blocks (a run may span two; each copy
+// hipHostRegister in kBlock-sized blocks (256 MiB; a run may span two; each copy
 // stays inside one registration).  Blocks are reference-counted by the HBM
 // windows whose copies use them and unregistered once those windows are
 // hashed, so at most about two windows' worth of page cache is pinned.
@@ -530,7 +530,7 @@ class DirectSource {
     m.len = len;
     return m;
   }
-  size_t kBlock = 64u << 20;
+  size_t kBlock = 256u << 20;  // TRITONDL_GPU_DIRECT_BLOCK_MB; 64-1024 measured alike (profiles/r03_direct_knobs)
   bool keep_ = false;
   const std::vector<Span>& spans_;
   std::vector<Map> maps_;
