@@ -27,6 +27,32 @@ def test_plan_shapes():
     assert [w.rank for w in r] == [2, 3] and r[1].bt_listen_port == 7001 and r[0].world_size == 4
 
 
+def test_cpusets_follow_l3_domains(tmp_path):
+    """Zen-style topology: 2 CCDs of 4 cores + SMT siblings 8..15.  Sets are
+    packed into one L3 domain, one disjoint set per index."""
+    from tritondl.parallel import topology as t
+    assert t.parse_cpulist("0-3,8, 10-11") == [0, 1, 2, 3, 8, 10, 11]
+    for c in range(16):
+        d = tmp_path / f"cpu{c}" / "cache" / "index3"
+        d.mkdir(parents=True)
+        (d / "shared_cpu_list").write_text("0-3,8-11\n" if c % 8 < 4 else "4-7,12-15\n")
+    doms = t.l3_domains(list(range(16)), sysfs=str(tmp_path))
+    assert doms == [[0, 1, 2, 3, 8, 9, 10, 11], [4, 5, 6, 7, 12, 13, 14, 15]]
+    # restricted affinity keeps only the allowed CPUs of each domain
+    assert t.l3_domains([1, 2, 5, 9], sysfs=str(tmp_path)) == [[1, 2, 9], [5]]
+    # no cache topology: one group
+    assert t.l3_domains([0, 1], sysfs=str(tmp_path / "missing")) == [[0, 1]]
+    orig = t.l3_domains
+    try:
+        t.l3_domains = lambda allowed=None: doms
+        assert t.compact_cpuset(8) == [0, 1, 2, 3, 8, 9, 10, 11]
+        assert t.compact_cpuset(8, 1) == [4, 5, 6, 7, 12, 13, 14, 15]
+        assert t.compact_cpuset(4, 3) == [12, 13, 14, 15]
+        assert len(t.compact_cpuset(64)) == 16
+    finally:
+        t.l3_domains = orig
+
+
 def test_pool_competing_consumers_and_restart(tmp_path):
     async def main():
         b = await Broker().start()

@@ -68,3 +68,62 @@ def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | Non
         out.append(WorkerSpec(node_rank * workers + i, i, world, gpu, cset,
                               (base_port + i) if base_port else 0))
     return out
+
+
+# ---------------------------------------------------------------- CPU sets
+
+def parse_cpulist(s: str) -> list[int]:
+    """Linux cpulist syntax (``0-7,128-135``, as in ``shared_cpu_list``)."""
+    out: list[int] = []
+    for part in s.replace(" ", "").split(","):
+        if not part:
+            continue
+        if "-" in part:
+            lo, hi = part.split("-", 1)
+            out.extend(range(int(lo), int(hi) + 1))
+        else:
+            out.append(int(part))
+    return sorted(set(out))
+
+
+def l3_domains(allowed: list[int] | None = None, sysfs: str = "/sys/devices/system/cpu") -> list[list[int]]:
+    """CPUs grouped by shared last-level cache (one group per Zen CCD),
+    restricted to ``allowed`` (default: this process's affinity), ordered by
+    their lowest CPU.  One group with every allowed CPU if sysfs has no
+    cache topology."""
+    if allowed is None:
+        allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+            list(range(os.cpu_count() or 1))
+    ok = set(allowed)
+    groups: dict[tuple[int, ...], list[int]] = {}
+    for c in allowed:
+        try:
+            with open(f"{sysfs}/cpu{c}/cache/index3/shared_cpu_list") as f:
+                key = tuple(x for x in parse_cpulist(f.read().strip()) if x in ok)
+        except (OSError, ValueError):
+            return [sorted(ok)]
+        groups.setdefault(key or (c,), []).append(c)
+    return sorted((sorted(g) for g in groups.values()), key=lambda g: g[0])
+
+
+def cpu_quota() -> float | None:
+    """CPUs' worth of time the cgroup allows (``cpu.max``), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        return None
+
+
+def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> list[int]:
+    """``n`` CPUs packed into as few last-level-cache domains as possible;
+    ``index`` selects the index-th such set (one per rank), wrapping round.
+    Keeps a process's threads — and the data they hand each other — on one
+    CCD's L3 instead of spread over the socket."""
+    doms = l3_domains(allowed)
+    flat = [c for d in doms for c in d]
+    if n <= 0 or n >= len(flat):
+        return flat
+    start = (index * n) % len(flat)
+    return (flat + flat)[start:start + n]
