@@ -106,3 +106,22 @@ def test_pool_competing_consumers_and_restart(tmp_path):
         await o.stop()
         await b.stop()
     asyncio.run(asyncio.wait_for(main(), 120))
+
+
+def test_pin_spec_and_config():
+    """``TRITONDL_CPUS`` / ``bench.py --cpus``: empty or "none" leaves the
+    affinity alone; a cpulist or auto[:N] pins the calling process."""
+    from tritondl.parallel import topology as t
+    from tritondl.utils.config import Config
+    assert Config.from_env({"TRITONDL_CPUS": "auto:4"}).cpus == "auto:4"
+    assert Config.from_env({}).cpus == ""
+    before = os.sched_getaffinity(0)
+    try:
+        assert t.pin("") == [] and t.pin("none") == [] and os.sched_getaffinity(0) == before
+        first = min(before)
+        assert t.pin(str(first)) == [first] and os.sched_getaffinity(0) == {first}
+        os.sched_setaffinity(0, before)
+        got = t.pin("auto:2")
+        assert len(got) == min(2, len(before)) and os.sched_getaffinity(0) == set(got)
+    finally:
+        os.sched_setaffinity(0, before)

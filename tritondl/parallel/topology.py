@@ -52,8 +52,9 @@ def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | Non
          cpus_per_worker: int = 2, base_port: int = 0, node_rank: int = 0, nnodes: int = 1) -> list[WorkerSpec]:
     gpus = detect_gpus() if gpus is None else gpus
     if cpus is None:
-        avail = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
-            list(range(os.cpu_count() or 1))
+        # ordered by last-level-cache domain, so each worker's slice (its receive
+        # pump, hashers and send pump hand a job's bytes to each other) shares an L3
+        avail = [c for d in l3_domains() for c in d]
         cpus = len(avail)
     else:
         avail = list(range(cpus))
@@ -127,3 +128,25 @@ def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> 
         return flat
     start = (index * n) % len(flat)
     return (flat + flat)[start:start + n]
+
+
+def pin(spec: str, index: int = 0) -> list[int]:
+    """Pin the calling process (and every thread and child it starts later)
+    to ``spec``: a cpulist, or ``auto[:N]`` = :func:`compact_cpuset` of N CPUs
+    (default: the cgroup quota rounded up, 16 without one), the ``index``-th
+    such set.  Returns the CPUs, or [] when ``spec`` is empty or pinning is
+    unavailable."""
+    spec = spec.strip()
+    if not spec or spec == "none" or not hasattr(os, "sched_setaffinity"):
+        return []
+    if spec.startswith("auto"):
+        if ":" in spec:
+            n = int(spec.split(":", 1)[1])
+        else:
+            q = cpu_quota()
+            n = int(-(-q // 1)) if q else 16
+        cpus = compact_cpuset(n, index)
+    else:
+        cpus = parse_cpulist(spec)
+    os.sched_setaffinity(0, cpus)
+    return cpus

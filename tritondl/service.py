@@ -605,6 +605,11 @@ def main(argv: list[str] | None = None) -> int:
     cfg = Config.from_env(argv=list(sys.argv[1:] if argv is None else argv))
     log.configure(cfg.log_level, cfg.log_format)
     raise_nofile_limit()
+    if cfg.cpus:
+        from .parallel.topology import pin
+        cpus = pin(cfg.cpus, int(os.environ.get("LOCAL_RANK", "0") or 0))
+        if cpus:
+            log.with_field("cpus", len(cpus)).info("pinned to %d..%d", cpus[0], cpus[-1])
     prof = CPUProfiler(cfg.cpuprofile)
     prof.start()
     try:

@@ -139,6 +139,13 @@ class Config:
     # --- TLS trust (https origins / S3): "" = system store (SSL_CERT_FILE honoured) ---
     ca_file: str = ""
 
+    # --- placement ---
+    # CPU set the worker pins itself to at start-up: a cpulist ("0-7,128-135"),
+    # "auto[:N]" (N CPUs, default the cgroup quota, packed into the fewest L3
+    # domains) or "" (no pinning).  One CCD keeps a job's bytes in its L3 as
+    # they pass receive pump -> hashers -> send pump (profiles/r03_pin_ab/)
+    cpus: str = ""
+
     # --- observability ---
     metrics_addr: str = ""                      # "host:port" → /metrics
     extra: dict = field(default_factory=dict)
@@ -182,7 +189,8 @@ class Config:
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
-                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file", "S3_HASH_DEVICE": "s3_hash_device"}
+                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file", "S3_HASH_DEVICE": "s3_hash_device",
+                "CPUS": "cpus"}
         for k, a in ints.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, int(g("TRITONDL_" + k)))
