@@ -119,16 +119,24 @@ def main() -> int:
                          "rank r writes PATH.r<r> when N > 1)")
     ap.add_argument("--cpus", default="auto",
                     help="pin this rank (worker, fakes, pump threads) to a CPU set: a cpulist like 0-15, "
-                         "or auto[:N] = N CPUs (default: the cgroup quota) packed into the fewest L3 "
-                         "domains, a disjoint set per rank; 'none' = no pinning.  Default auto: on the "
+                         "auto = one whole L3 domain (CCD + SMT siblings) per rank, auto:N = N CPUs "
+                         "packed into the fewest L3 domains; 'none' = no pinning.  Default auto: on the "
                          "16-CPU box share one CCD measured 323-336 vs 222-279 jobs/s unpinned, "
                          "profiles/r03_pin_ab/)")
+    ap.add_argument("--fake-cpus", default="",
+                    help="pin the fake broker/origin/S3/producer processes elsewhere: a cpulist, or auto = "
+                         "the CPU set after the last rank's ('' = same set as the rank)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     pinned = _pin(a.cpus, local_rank)
+    if a.fake_cpus:
+        from tritondl.parallel import topology
+        fc = (topology.compact_cpuset(len(pinned) or 16, world + local_rank) if a.fake_cpus == "auto"
+              else topology.parse_cpulist(a.fake_cpus))
+        os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, fc))
 
     import torch
     import torch.distributed as dist
@@ -286,6 +294,7 @@ def main() -> int:
                        "transport": "https (TLS 1.3, native OpenSSL data plane)" if a.tls else "http",
                        "s3_payload": stack.payload_mode, "s3_hash_device": a.s3_hash_device,
                        "cpus": (f"{len(pinned)} pinned ({pinned[0]}..{pinned[-1]})" if pinned else "unpinned"),
+                       "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
                        **knobs},
             "jobs_per_rank": per_rank,

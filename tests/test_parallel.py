@@ -125,3 +125,19 @@ def test_pin_spec_and_config():
         assert len(got) == min(2, len(before)) and os.sched_getaffinity(0) == set(got)
     finally:
         os.sched_setaffinity(0, before)
+
+
+def test_pin_auto_takes_whole_l3_domain(monkeypatch):
+    from tritondl.parallel import topology as t
+    cpus = sorted(os.sched_getaffinity(0))
+    doms = [cpus[:1], cpus[1:]] if len(cpus) > 1 else [cpus]
+    monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
+    before = os.sched_getaffinity(0)
+    try:
+        assert t.pin("auto", 0) == doms[0]
+        os.sched_setaffinity(0, before)
+        assert t.pin("auto", 1) == doms[1 % len(doms)]
+        os.sched_setaffinity(0, before)
+        assert t.pin("auto", 2) == doms[2 % len(doms)]       # ranks wrap round the domains
+    finally:
+        os.sched_setaffinity(0, before)

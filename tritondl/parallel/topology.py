@@ -132,20 +132,20 @@ def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> 
 
 def pin(spec: str, index: int = 0) -> list[int]:
     """Pin the calling process (and every thread and child it starts later)
-    to ``spec``: a cpulist, or ``auto[:N]`` = :func:`compact_cpuset` of N CPUs
-    (default: the cgroup quota rounded up, 16 without one), the ``index``-th
-    such set.  Returns the CPUs, or [] when ``spec`` is empty or pinning is
-    unavailable."""
+    to ``spec``: a cpulist; ``auto`` = the ``index``-th whole last-level-cache
+    domain (one CCD with its SMT siblings per worker: on the box that beat 8
+    cores without siblings and two CCDs, ``profiles/r03_pin_ab/``);
+    ``auto:N`` = the ``index``-th :func:`compact_cpuset` of N CPUs.  Returns
+    the CPUs, or [] when ``spec`` is empty/"none" or pinning is unavailable."""
     spec = spec.strip()
     if not spec or spec == "none" or not hasattr(os, "sched_setaffinity"):
         return []
     if spec.startswith("auto"):
         if ":" in spec:
-            n = int(spec.split(":", 1)[1])
+            cpus = compact_cpuset(int(spec.split(":", 1)[1]), index)
         else:
-            q = cpu_quota()
-            n = int(-(-q // 1)) if q else 16
-        cpus = compact_cpuset(n, index)
+            doms = l3_domains()
+            cpus = doms[index % len(doms)]
     else:
         cpus = parse_cpulist(spec)
     os.sched_setaffinity(0, cpus)
