@@ -125,18 +125,21 @@ def main() -> int:
                          "profiles/r03_pin_ab/)")
     ap.add_argument("--fake-cpus", default="",
                     help="pin the fake broker/origin/S3/producer processes elsewhere: a cpulist, or auto = "
-                         "the CPU set after the last rank's ('' = same set as the rank)")
+                         "the L3 domain after the last rank's ('' = same set as the rank)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    pinned = _pin(a.cpus, local_rank)
-    if a.fake_cpus:
+    if a.fake_cpus:          # before pinning: afterwards only the rank's own CPUs are visible
         from tritondl.parallel import topology
-        fc = (topology.compact_cpuset(len(pinned) or 16, world + local_rank) if a.fake_cpus == "auto"
-              else topology.parse_cpulist(a.fake_cpus))
+        if a.fake_cpus == "auto":
+            doms = topology.l3_domains()
+            fc = doms[(world + local_rank) % len(doms)]
+        else:
+            fc = topology.parse_cpulist(a.fake_cpus)
         os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, fc))
+    pinned = _pin(a.cpus, local_rank)
 
     import torch
     import torch.distributed as dist

@@ -66,9 +66,12 @@ def test_profile_attributes_python_and_native_threads(tmp_path):
     t0 = time.monotonic()
     while time.monotonic() - t0 < 0.8:               # native SHA-1 pool threads (tdl-hash)
         hashing.piece_hashes(data, 1 << 20, "sha1", "cpu", threads=4)
+    # stop while the burner still runs: a thread that ends between ticks takes its CPU
+    # since the last tick with it, and on a loaded CI host the profiler thread may get
+    # only a few ticks in (it needs the GIL the burner holds)
+    p.stop()
     stop.set()
     t.join()
-    p.stop()
     raw = gzip.decompress(path.read_bytes())
     fields = _fields(raw)
     strings = [v.decode() for num, wt, v in fields if num == 6]
