@@ -141,3 +141,12 @@ def test_pin_auto_takes_whole_l3_domain(monkeypatch):
         assert t.pin("auto", 2) == doms[2 % len(doms)]       # ranks wrap round the domains
     finally:
         os.sched_setaffinity(0, before)
+
+
+def test_plan_gives_each_worker_an_l3_domain(monkeypatch):
+    from tritondl.parallel import topology as t
+    doms = [[0, 1, 8, 9], [2, 3, 10, 11], [4, 5, 12, 13], [6, 7, 14, 15]]
+    monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
+    assert [w.cpus for w in t.plan(3, gpus=0)] == doms[:3]
+    # more workers than domains: consecutive slices of the L3-ordered CPUs
+    assert [w.cpus for w in t.plan(8, gpus=0)][:2] == [[0, 1], [8, 9]]

@@ -39,6 +39,8 @@ async def main() -> int:
     ap.add_argument("--file-kb", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     ap.add_argument("--nodes", type=int, default=1, help="origin + S3 fake processes (sharded)")
+    ap.add_argument("--placement", default="l3", choices=["l3", "slice"],
+                    help="worker CPU sets: one L3 domain each (default) or consecutive CPU-id slices")
     ap.add_argument("--s3-hash-device", default="cpu", choices=["cpu", "gpu"],
                     help="workers hash aws-chunked chunks on SHA-NI or the HIP kernel")
     a = ap.parse_args()
@@ -71,7 +73,10 @@ async def main() -> int:
                "TRITONDL_PREFETCH": str(a.concurrency), "TRITONDL_GPU_VERIFY": "off",
                "TRITONDL_S3_HASH_DEVICE": a.s3_hash_device}
         ncpu = len(os.sched_getaffinity(0))
-        pool = WorkerPool(plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)),
+        # --placement l3: one CCD per worker (topology.plan); slice: consecutive CPU ids
+        specs = (plan(a.workers, gpus=0) if a.placement == "l3" else
+                 plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)))
+        pool = WorkerPool(specs,
                           env=env, cwd=work, grace=10,
                           worker_env=lambda r: {"S3_ENDPOINT": s3s[r % len(s3s)]})
         await pool.start()
@@ -123,7 +128,7 @@ async def main() -> int:
         await asyncio.wait_for(got.wait(), 600)
         dt = time.perf_counter() - t0
         print(json.dumps({"metric": "pool_jobs_per_sec", "value": round(a.jobs / dt, 2), "seconds": round(dt, 3),
-                          "workers": a.workers, "jobs": a.jobs, "file_kb": a.file_kb,
+                          "workers": a.workers, "placement": a.placement, "jobs": a.jobs, "file_kb": a.file_kb,
                           "concurrency_per_worker": a.concurrency, "fake_nodes": a.nodes,
                           "ingest_MB_per_sec": round(a.jobs * size / dt / 1e6, 1)}), flush=True)
     finally:

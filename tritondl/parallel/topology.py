@@ -51,10 +51,12 @@ def detect_gpus() -> int:
 def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | None = None,
          cpus_per_worker: int = 2, base_port: int = 0, node_rank: int = 0, nnodes: int = 1) -> list[WorkerSpec]:
     gpus = detect_gpus() if gpus is None else gpus
+    doms: list[list[int]] = []
     if cpus is None:
         # ordered by last-level-cache domain, so each worker's slice (its receive
         # pump, hashers and send pump hand a job's bytes to each other) shares an L3
-        avail = [c for d in l3_domains() for c in d]
+        doms = l3_domains()
+        avail = [c for d in doms for c in d]
         cpus = len(avail)
     else:
         avail = list(range(cpus))
@@ -63,9 +65,15 @@ def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | Non
     world = workers * nnodes
     out = []
     per = max(1, cpus // workers)
+    # one whole L3 domain (CCD + SMT siblings) per worker when there are enough:
+    # a single worker measured faster on one CCD than on two (profiles/r03_pin_ab/)
+    by_domain = len(doms) > 1 and len(doms) >= workers
     for i in range(workers):
         gpu = (i % gpus) if gpus > 0 else None
-        cset = avail[i * per:(i + 1) * per] if cpus >= workers else []
+        if by_domain:
+            cset = doms[i]
+        else:
+            cset = avail[i * per:(i + 1) * per] if cpus >= workers else []
         out.append(WorkerSpec(node_rank * workers + i, i, world, gpu, cset,
                               (base_port + i) if base_port else 0))
     return out
