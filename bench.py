@@ -79,11 +79,31 @@ def _gpu_hash_probe(total_mb: int = 4096) -> dict:
         return {"gpu_probe_error": str(e)[:200]}
 
 
-def _pin(spec: str, local_rank: int) -> list[int]:
-    """Set this process's CPU affinity (inherited by the fakes it spawns and
-    every native thread) before anything starts."""
+def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_size: int) -> list[int]:
+    """Pin this rank's process (inherited by every native thread and by the
+    fakes it spawns) before anything starts, and choose the fakes' set.
+
+    ``auto``: each rank gets whole L3 domains, one for small jobs and two for
+    jobs of 256 MiB and up (a 1 GiB job's ~9 CPUs of pump and hashing work
+    does not fit one CCD: 7.7-8.4 jobs/s on one, 9.8-12.3 on two,
+    ``profiles/r03_place_ab2/``); the fakes, which stand in for remote
+    endpoints, get the next domain after all ranks' (``--fake-cpus auto``)."""
     from tritondl.parallel import topology
-    return topology.pin(spec, local_rank)
+    fc: list[int] = []
+    pinned: list[int] = []
+    doms = topology.l3_domains()            # before pinning: afterwards only our own CPUs show
+    k = 2 if file_size >= 256 << 20 else 1
+    if fake_cpus not in ("", "same") and cpus not in ("", "none"):
+        fc = (doms[(local_world * k + local_rank) % len(doms)] if fake_cpus == "auto"
+              else topology.parse_cpulist(fake_cpus))
+    if cpus == "auto":
+        pinned = sorted({c for j in range(k) for c in doms[(local_rank * k + j) % len(doms)]})
+        os.sched_setaffinity(0, pinned)
+    elif cpus not in ("", "none"):
+        pinned = topology.pin(cpus, local_rank)
+    if fc:
+        os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, fc))
+    return pinned
 
 
 def main() -> int:
@@ -119,27 +139,22 @@ def main() -> int:
                          "rank r writes PATH.r<r> when N > 1)")
     ap.add_argument("--cpus", default="auto",
                     help="pin this rank (worker, fakes, pump threads) to a CPU set: a cpulist like 0-15, "
-                         "auto = one whole L3 domain (CCD + SMT siblings) per rank, auto:N = N CPUs "
+                         "auto = whole L3 domains (CCD + SMT siblings) per rank: one, or two for files "
+                         "of 256 MiB and up; auto:N = N CPUs "
                          "packed into the fewest L3 domains; 'none' = no pinning.  Default auto: on the "
                          "16-CPU box share one CCD measured 323-336 vs 222-279 jobs/s unpinned, "
                          "profiles/r03_pin_ab/)")
-    ap.add_argument("--fake-cpus", default="",
-                    help="pin the fake broker/origin/S3/producer processes elsewhere: a cpulist, or auto = "
-                         "the L3 domain after the last rank's ('' = same set as the rank)")
+    ap.add_argument("--fake-cpus", default="auto",
+                    help="pin the fake broker/origin/S3/producer processes (remote endpoints in "
+                         "production) elsewhere: a cpulist, auto = the L3 domain after the last rank's, "
+                         "'same' = the rank's own set")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.fake_cpus:          # before pinning: afterwards only the rank's own CPUs are visible
-        from tritondl.parallel import topology
-        if a.fake_cpus == "auto":
-            doms = topology.l3_domains()
-            fc = doms[(world + local_rank) % len(doms)]
-        else:
-            fc = topology.parse_cpulist(a.fake_cpus)
-        os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, fc))
-    pinned = _pin(a.cpus, local_rank)
+    pinned = _place(a.cpus, a.fake_cpus, local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                    int(a.file_mb * 1024 * 1024))
 
     import torch
     import torch.distributed as dist
