@@ -189,7 +189,14 @@ async def main() -> None:
     ap.add_argument("--s3-bufsize", type=int, default=0, help="fake S3 server read_bufsize (0 = default)")
     ap.add_argument("--io-block", type=int, default=0, help="S3 upload read/sign block (0 = default)")
     ap.add_argument("--tls", action="store_true", help="origin and S3 over https (native TLS data plane)")
+    ap.add_argument("--cpus", default="auto", choices=["auto", "none"],
+                    help="auto: this process on one L3 domain and the fakes on the next, as bench.py")
     a = ap.parse_args()
+    if a.cpus == "auto":
+        from tritondl.parallel import topology
+        doms = topology.l3_domains()
+        os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, doms[1 % len(doms)]))
+        os.sched_setaffinity(0, doms[0])
     if a.s3_bufsize:
         os.environ["TRITONDL_FAKE_S3_READ_BUFSIZE"] = str(a.s3_bufsize)
     _patch_defaults(HTTPDownloader, "read_bufsize", a.http_bufsize)
