@@ -150,3 +150,13 @@ def test_plan_gives_each_worker_an_l3_domain(monkeypatch):
     assert [w.cpus for w in t.plan(3, gpus=0)] == doms[:3]
     # more workers than domains: consecutive slices of the L3-ordered CPUs
     assert [w.cpus for w in t.plan(8, gpus=0)][:2] == [[0, 1], [8, 9]]
+
+
+def test_worker_bad_cpus_is_fatal(monkeypatch):
+    """A malformed TRITONDL_CPUS stops the worker at start-up (exit 1), before
+    it connects anywhere."""
+    from tritondl import service
+    monkeypatch.setenv("TRITONDL_CPUS", "0-x")
+    assert service.main([]) == 1
+    monkeypatch.setenv("TRITONDL_CPUS", "99999")     # not a CPU of this machine
+    assert service.main([]) == 1

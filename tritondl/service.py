@@ -607,7 +607,11 @@ def main(argv: list[str] | None = None) -> int:
     raise_nofile_limit()
     if cfg.cpus:
         from .parallel.topology import pin
-        cpus = pin(cfg.cpus, int(os.environ.get("LOCAL_RANK", "0") or 0))
+        try:
+            cpus = pin(cfg.cpus, int(os.environ.get("LOCAL_RANK", "0") or 0))
+        except (ValueError, OSError) as e:      # a bad cpulist is fatal configuration
+            log.error("fatal: TRITONDL_CPUS=%r: %s", cfg.cpus, e)
+            return 1
         if cpus:
             log.with_field("cpus", len(cpus)).info("pinned to %d..%d", cpus[0], cpus[-1])
     prof = CPUProfiler(cfg.cpuprofile)
