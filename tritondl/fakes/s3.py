@@ -93,6 +93,8 @@ class FakeS3:
         self._fail_status = 503
         self.requests: list[tuple[str, str]] = []
         self.bytes_received = 0
+        # native aws-chunked verifier threads per PUT (stands in for a remote S3's capacity)
+        self.verify_threads = int(os.environ.get("TRITONDL_FAKE_S3_VERIFY_THREADS", "4"))
         self._server: web.Server | None = None
         self.native = True
 
@@ -229,7 +231,8 @@ class FakeS3:
         raw_len = request.body_length
         stream, pre = request.take_body()
         n, err, data = await asyncio.get_running_loop().run_in_executor(
-            None, relay.recv_verify_chunked, stream, raw_len, pre, key, amzdate, scope, seed, keep, 4, 300.0)
+            None, relay.recv_verify_chunked, stream, raw_len, pre, key, amzdate, scope, seed, keep,
+            self.verify_threads, 300.0)
         self.bytes_received += raw_len
         if err:
             if "closed" in err or "timeout" in err or "socket" in err or "recv" in err:
