@@ -42,6 +42,9 @@ def test_bench_single_process_json():
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["config"]["model"].startswith("Single HTTP download job") and d["config"]["parallelism"] == "dp1"
     assert abs(d["value"] - 4 / (d["ms_per_step"] * 4 / 1000)) / d["value"] < 0.01
+    # the placement is part of the reported config (default: pinned to an L3 domain)
+    assert d["config"]["cpus"].endswith(")") and "pinned" in d["config"]["cpus"]
+    assert d["config"]["fake_cpus"]
 
 
 def test_bench_two_ranks_torchrun_gloo():
