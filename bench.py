@@ -87,17 +87,23 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
     jobs of 256 MiB and up (a 1 GiB job's ~9 CPUs of pump and hashing work
     does not fit one CCD: 7.7-8.4 jobs/s on one, 9.8-12.3 on two,
     ``profiles/r03_place_ab2/``); the fakes, which stand in for remote
-    endpoints, get the next domain after all ranks' (``--fake-cpus auto``)."""
+    endpoints, get the domain right after their rank's (``--fake-cpus auto``),
+    so on a 16-CCD node 8 ranks and their fakes pair up on the same socket."""
     from tritondl.parallel import topology
     fc: list[int] = []
     pinned: list[int] = []
     doms = topology.l3_domains()            # before pinning: afterwards only our own CPUs show
     k = 2 if file_size >= 256 << 20 else 1
+    # with room for it, rank r takes domains [r(k+1), r(k+1)+k) and its fakes the next one:
+    # neighbours in L3 order share a socket, and ranks spread over both sockets as
+    # their GPUs do; otherwise the ranks come first and the fakes after them all
+    packed = len(doms) >= (k + 1) * local_world
+    first = local_rank * (k + 1) if packed else local_rank * k
     if fake_cpus not in ("", "same") and cpus not in ("", "none"):
-        fc = (doms[(local_world * k + local_rank) % len(doms)] if fake_cpus == "auto"
-              else topology.parse_cpulist(fake_cpus))
+        fc = (doms[(first + k if packed else local_world * k + local_rank) % len(doms)]
+              if fake_cpus == "auto" else topology.parse_cpulist(fake_cpus))
     if cpus == "auto":
-        pinned = sorted({c for j in range(k) for c in doms[(local_rank * k + j) % len(doms)]})
+        pinned = sorted({c for j in range(k) for c in doms[(first + j) % len(doms)]})
         os.sched_setaffinity(0, pinned)
     elif cpus not in ("", "none"):
         pinned = topology.pin(cpus, local_rank)
