@@ -49,17 +49,12 @@ class Backend:
 
     async def start(self) -> "Backend":
         args = [self.kind] if self.module == "tritondl.fakes.serve" else []
-        kw: dict = {}
-        fake_cpus = os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "")
-        if fake_cpus and hasattr(os, "sched_setaffinity"):
-            # the fakes stand in for remote endpoints: optionally keep them off the worker's CPUs
-            from .parallel.topology import parse_cpulist
-            cpus = parse_cpulist(fake_cpus)
-            kw["preexec_fn"] = lambda: os.sched_setaffinity(0, cpus)
+        # (TRITONDL_BENCH_FAKE_CPUS, if set, is inherited: the child pins itself first
+        # thing, topology.pin_from_env — no preexec_fn in a process that has threads)
         self.proc = await asyncio.create_subprocess_exec(
             sys.executable, "-m", self.module, *args, *self.extra,
             stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
-            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), **kw)
+            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert self.proc.stdout is not None
         line = await asyncio.wait_for(self.proc.stdout.readline(), 120)
         if not line:

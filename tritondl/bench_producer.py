@@ -159,6 +159,8 @@ async def _amain(a: argparse.Namespace) -> None:
 
 
 def main() -> None:
+    from tritondl.parallel.topology import pin_from_env
+    pin_from_env()
     ap = argparse.ArgumentParser()
     ap.add_argument("--broker", required=True)
     ap.add_argument("--origins", required=True, help="comma-separated origin base URLs (jobs round-robin)")

@@ -101,6 +101,8 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
 
 
 def main() -> None:
+    from tritondl.parallel.topology import pin_from_env
+    pin_from_env()
     ap = argparse.ArgumentParser()
     ap.add_argument("kind", choices=["broker", "origin", "s3", "seed"])
     ap.add_argument("--path", default=None, help="seed: file or directory to seed")

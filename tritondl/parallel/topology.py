@@ -158,3 +158,14 @@ def pin(spec: str, index: int = 0) -> list[int]:
         cpus = parse_cpulist(spec)
     os.sched_setaffinity(0, cpus)
     return cpus
+
+
+def pin_from_env(var: str = "TRITONDL_BENCH_FAKE_CPUS") -> list[int]:
+    """Bench fakes (broker, origin, S3, producer) call this first thing: the
+    bench puts them on their own L3 domain, standing in for remote endpoints."""
+    spec = os.environ.get(var, "")
+    if not spec or not hasattr(os, "sched_setaffinity"):
+        return []
+    cpus = parse_cpulist(spec)
+    os.sched_setaffinity(0, cpus)
+    return cpus
