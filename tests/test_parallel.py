@@ -139,6 +139,11 @@ def test_pin_auto_takes_whole_l3_domain(monkeypatch):
         assert t.pin("auto", 1) == doms[1 % len(doms)]
         os.sched_setaffinity(0, before)
         assert t.pin("auto", 2) == doms[2 % len(doms)]       # ranks wrap round the domains
+        os.sched_setaffinity(0, before)
+        four = [[c] for c in cpus[:4]] if len(cpus) >= 4 else None
+        if four:
+            monkeypatch.setattr(t, "l3_domains", lambda allowed=None: four)
+            assert t.pin("auto", 1, count=2) == four[2]          # 2 workers on 4 domains: 0 and 2
     finally:
         os.sched_setaffinity(0, before)
 
@@ -147,7 +152,8 @@ def test_plan_gives_each_worker_an_l3_domain(monkeypatch):
     from tritondl.parallel import topology as t
     doms = [[0, 1, 8, 9], [2, 3, 10, 11], [4, 5, 12, 13], [6, 7, 14, 15]]
     monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
-    assert [w.cpus for w in t.plan(3, gpus=0)] == doms[:3]
+    assert [w.cpus for w in t.plan(2, gpus=0)] == [doms[0], doms[2]]     # spread, like the GPUs
+    assert [w.cpus for w in t.plan(4, gpus=0)] == doms
     # more workers than domains: consecutive slices of the L3-ordered CPUs
     assert [w.cpus for w in t.plan(8, gpus=0)][:2] == [[0, 1], [8, 9]]
 

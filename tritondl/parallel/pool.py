@@ -66,12 +66,12 @@ class WorkerPool:
         env.update(w.spec.env())
         if self.worker_env is not None:
             env.update(self.worker_env(w.spec.rank))
-        kw = {}
-        if w.spec.cpus and hasattr(os, "sched_setaffinity"):
-            cpus = set(w.spec.cpus)
-            kw["preexec_fn"] = lambda: os.sched_setaffinity(0, cpus)
+        if w.spec.cpus and "TRITONDL_CPUS" not in self.env:
+            # the worker pins itself first thing (service.main, TRITONDL_CPUS): no
+            # preexec_fn in this threaded supervisor
+            env["TRITONDL_CPUS"] = ",".join(map(str, w.spec.cpus))
         w.proc = await asyncio.create_subprocess_exec(sys.executable, "-m", self.module, *self.argv, env=env,
-                                                      cwd=self.cwd, **kw)
+                                                      cwd=self.cwd)
         w.started_at = time.monotonic()
         log.with_fields(rank=w.spec.rank, pid=w.proc.pid, gpu=w.spec.gpu).info("worker started")
 

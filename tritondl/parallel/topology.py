@@ -68,10 +68,11 @@ def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | Non
     # one whole L3 domain (CCD + SMT siblings) per worker when there are enough:
     # a single worker measured faster on one CCD than on two (profiles/r03_pin_ab/)
     by_domain = len(doms) > 1 and len(doms) >= workers
+    stride = max(1, len(doms) // max(1, workers))   # spread over both sockets, as the GPUs are
     for i in range(workers):
         gpu = (i % gpus) if gpus > 0 else None
         if by_domain:
-            cset = doms[i]
+            cset = doms[i * stride]
         else:
             cset = avail[i * per:(i + 1) * per] if cpus >= workers else []
         out.append(WorkerSpec(node_rank * workers + i, i, world, gpu, cset,
@@ -138,10 +139,10 @@ def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> 
     return (flat + flat)[start:start + n]
 
 
-def pin(spec: str, index: int = 0) -> list[int]:
+def pin(spec: str, index: int = 0, count: int = 1) -> list[int]:
     """Pin the calling process (and every thread and child it starts later)
-    to ``spec``: a cpulist; ``auto`` = the ``index``-th whole last-level-cache
-    domain (one CCD with its SMT siblings per worker: on the box that beat 8
+    to ``spec``: a cpulist; ``auto`` = the ``index``-th of ``count`` whole
+    last-level-cache domains spaced evenly over the node (one CCD with its SMT siblings per worker: on the box that beat 8
     cores without siblings and two CCDs, ``profiles/r03_pin_ab/``);
     ``auto:N`` = the ``index``-th :func:`compact_cpuset` of N CPUs.  Returns
     the CPUs, or [] when ``spec`` is empty/"none" or pinning is unavailable."""
@@ -153,7 +154,10 @@ def pin(spec: str, index: int = 0) -> list[int]:
             cpus = compact_cpuset(int(spec.split(":", 1)[1]), index)
         else:
             doms = l3_domains()
-            cpus = doms[index % len(doms)]
+            # ``count`` workers on this node (LOCAL_WORLD_SIZE) spread over all the
+            # domains, so half of 8 GPU workers land on each socket with their GPUs
+            stride = max(1, len(doms) // max(1, count, index + 1))
+            cpus = doms[(index * stride) % len(doms)]
     else:
         cpus = parse_cpulist(spec)
     os.sched_setaffinity(0, cpus)

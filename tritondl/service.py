@@ -608,7 +608,8 @@ def main(argv: list[str] | None = None) -> int:
     if cfg.cpus:
         from .parallel.topology import pin
         try:
-            cpus = pin(cfg.cpus, int(os.environ.get("LOCAL_RANK", "0") or 0))
+            cpus = pin(cfg.cpus, int(os.environ.get("LOCAL_RANK", "0") or 0),
+                       int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
         except (ValueError, OSError) as e:      # a bad cpulist is fatal configuration
             log.error("fatal: TRITONDL_CPUS=%r: %s", cfg.cpus, e)
             return 1
