@@ -33,7 +33,12 @@ async def main() -> int:
     ap.add_argument("--device", nargs="*", default=["cpu", "gpu"])
     ap.add_argument("--reps", type=int, default=2, help="runs per device; the first GPU run pays HIP set-up")
     ap.add_argument("--trace", action="store_true", help="GPU event timeline summary per run")
+    ap.add_argument("--cpus", default="", help="pin the run (file writes, so page-cache placement, and hashing "
+                                               "threads) to this cpulist")
     a = ap.parse_args()
+    if a.cpus:
+        from tritondl.parallel.topology import parse_cpulist
+        os.sched_setaffinity(0, parse_cpulist(a.cpus))
     import numpy as np
 
     from tritondl.fakes.origin import Origin
@@ -105,6 +110,9 @@ async def main() -> int:
         if o is not None:
             await o.stop()
         shutil.rmtree(td, ignore_errors=True)
+    if a.cpus and any(d != "cpu" for d in a.device):
+        from tritondl.parallel.topology import gpu_numa_node
+        print(json.dumps({"cpus": a.cpus, "gpu_numa_node": gpu_numa_node(0)}), flush=True)
     return 0
 
 

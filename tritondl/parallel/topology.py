@@ -173,3 +173,19 @@ def pin_from_env(var: str = "TRITONDL_BENCH_FAKE_CPUS") -> list[int]:
     cpus = parse_cpulist(spec)
     os.sched_setaffinity(0, cpus)
     return cpus
+
+
+def gpu_numa_node(device: int = 0) -> int | None:
+    """NUMA node of a visible HIP device (its PCI function's ``numa_node``),
+    or None if unknown.  Initialises the HIP runtime (torch)."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(device)
+        dom, bus, dev = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        if bus is None or dev is None:
+            return None
+        with open(f"/sys/bus/pci/devices/{int(dom or 0):04x}:{int(bus):02x}:{int(dev):02x}.0/numa_node") as f:
+            n = int(f.read().strip())
+        return n if n >= 0 else None
+    except Exception:  # noqa: BLE001 - diagnostics only
+        return None
