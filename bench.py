@@ -159,8 +159,13 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    pinned = _place(a.cpus, a.fake_cpus, local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
-                    int(a.file_mb * 1024 * 1024))
+    try:
+        pinned = _place(a.cpus, a.fake_cpus, local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                        int(a.file_mb * 1024 * 1024))
+    except (OSError, ValueError, IndexError) as e:     # placement is an optimisation: run unpinned
+        print(f"bench: CPU placement skipped ({e})", file=sys.stderr, flush=True)
+        os.environ.pop("TRITONDL_BENCH_FAKE_CPUS", None)
+        pinned = []
 
     import torch
     import torch.distributed as dist
