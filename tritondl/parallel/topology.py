@@ -170,8 +170,11 @@ def pin_from_env(var: str = "TRITONDL_BENCH_FAKE_CPUS") -> list[int]:
     spec = os.environ.get(var, "")
     if not spec or not hasattr(os, "sched_setaffinity"):
         return []
-    cpus = parse_cpulist(spec)
-    os.sched_setaffinity(0, cpus)
+    try:
+        cpus = parse_cpulist(spec)
+        os.sched_setaffinity(0, cpus)
+    except (OSError, ValueError):      # placement is an optimisation: run where we are
+        return []
     return cpus
 
 
