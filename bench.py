@@ -88,11 +88,18 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
     does not fit one CCD: 7.7-8.4 jobs/s on one, 9.8-12.3 on two,
     ``profiles/r03_place_ab2/``); the fakes, which stand in for remote
     endpoints, get the domain right after their rank's (``--fake-cpus auto``),
-    so on a 16-CCD node 8 ranks and their fakes pair up on the same socket."""
+    so on an idle 16-CCD node 8 ranks and their fakes pair up on the same
+    socket.  Domains are taken idle-first (sampled once per launch by local
+    rank 0): a shared host's busy CCDs go last."""
     from tritondl.parallel import topology
     fc: list[int] = []
     pinned: list[int] = []
-    doms = topology.l3_domains()            # before pinning: afterwards only our own CPUs show
+    # before pinning (afterwards only our own CPUs show), and idle-first: on a host
+    # shared with other tenants a fixed CCD 0..n can be one they keep busy
+    # (profiles/r03_final4/: ranks on CCDs 2-5 did 125-168 jobs against 208-256)
+    tag = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
+    doms, busy = (topology.shared_idle_order(local_rank, local_world, tag) if cpus == "auto"
+                  else (topology.l3_domains(), []))
     k = 2 if file_size >= 256 << 20 else 1
     # with room for it, rank r takes domains [r(k+1), r(k+1)+k) and its fakes the next one:
     # neighbours in L3 order share a socket, and ranks spread over both sockets as
@@ -105,6 +112,8 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
     if cpus == "auto":
         pinned = sorted({c for j in range(k) for c in doms[(first + j) % len(doms)]})
         os.sched_setaffinity(0, pinned)
+        if busy:
+            os.environ["TRITONDL_BENCH_DOMAIN_BUSY"] = f"{busy[first % len(busy)]:.2f}"
     elif cpus not in ("", "none"):
         pinned = topology.pin(cpus, local_rank)
     if fc:
@@ -324,6 +333,7 @@ def main() -> int:
                        "s3_payload": stack.payload_mode, "s3_hash_device": a.s3_hash_device,
                        "cpus": (f"{len(pinned)} pinned ({pinned[0]}..{pinned[-1]})" if pinned else "unpinned"),
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
+                       "cpus_busy_before": os.environ.get("TRITONDL_BENCH_DOMAIN_BUSY", ""),
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
                        **knobs},
             "jobs_per_rank": per_rank,

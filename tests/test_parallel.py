@@ -166,3 +166,23 @@ def test_worker_bad_cpus_is_fatal(monkeypatch):
     assert service.main([]) == 1
     monkeypatch.setenv("TRITONDL_CPUS", "99999")     # not a CPU of this machine
     assert service.main([]) == 1
+
+
+def test_idle_first_order_shared_by_local_ranks(tmp_path, monkeypatch):
+    """bench --cpus auto: local rank 0 samples the domains' load once and
+    publishes an idle-first order; another local rank reads the same order
+    even though its own sample would differ."""
+    import tempfile
+    from tritondl.parallel import topology as t
+    doms = [[0], [1], [2], [3]]
+    assert t.idle_first(doms, [0.0, 0.5, 0.02, 0.3]) == [[0], [2], [3], [1]]
+    assert t.idle_first(doms, [0.0] * 4) == doms                 # idle host: topology order
+    monkeypatch.setattr(tempfile, "gettempdir", lambda: str(tmp_path))
+    monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
+    monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.9, 0.0, 0.0, 0.4])
+    o0, b0 = t.shared_idle_order(0, 2, "tagA")
+    assert o0 == [[1], [2], [3], [0]] and b0 == [0.0, 0.0, 0.4, 0.9]
+    monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.0, 0.9, 0.9, 0.9])
+    o1, _ = t.shared_idle_order(1, 2, "tagA")
+    assert o1 == o0
+    assert t._cpu_ticks()                                          # /proc/stat parses here

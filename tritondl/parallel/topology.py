@@ -192,3 +192,81 @@ def gpu_numa_node(device: int = 0) -> int | None:
         return n if n >= 0 else None
     except Exception:  # noqa: BLE001 - diagnostics only
         return None
+
+
+def _cpu_ticks() -> dict[int, tuple[int, int]]:
+    """Per-CPU (busy, total) jiffies from /proc/stat."""
+    out: dict[int, tuple[int, int]] = {}
+    with open("/proc/stat") as f:
+        for line in f:
+            if not line.startswith("cpu") or line.startswith("cpu "):
+                continue
+            parts = line.split()
+            v = [int(x) for x in parts[1:]]
+            idle = v[3] + (v[4] if len(v) > 4 else 0)          # idle + iowait
+            tot = sum(v[:8])                                      # guest time is inside user
+            out[int(parts[0][3:])] = (tot - idle, tot)
+    return out
+
+
+def domain_busy(doms: list[list[int]], interval: float = 0.2) -> list[float]:
+    """Fraction of each domain's CPU time spent busy over ``interval``
+    seconds (other tenants of a shared host included).  Zeros if /proc/stat
+    is unreadable."""
+    import time
+    try:
+        a = _cpu_ticks()
+        time.sleep(interval)
+        b = _cpu_ticks()
+    except (OSError, ValueError, IndexError):
+        return [0.0] * len(doms)
+    out = []
+    for d in doms:
+        busy = sum(b[c][0] - a[c][0] for c in d if c in a and c in b)
+        tot = sum(b[c][1] - a[c][1] for c in d if c in a and c in b)
+        out.append(busy / tot if tot > 0 else 0.0)
+    return out
+
+
+def idle_first(doms: list[list[int]], busy: list[float]) -> list[list[int]]:
+    """Domains ordered by load in 10 % steps, L3 order within a step: an
+    idle host keeps the topology order (neighbours share a socket), a shared
+    one sends our ranks past the CCDs another tenant keeps busy."""
+    order = sorted(range(len(doms)), key=lambda i: (round(busy[i] * 10), i))
+    return [doms[i] for i in order]
+
+
+def shared_idle_order(local_rank: int, local_world: int, tag: str, timeout: float = 10.0) -> tuple[list, list]:
+    """(domains idle-first, their busy fractions), sampled ONCE per launch:
+    local rank 0 samples and publishes the order in a small file named by
+    ``tag`` (e.g. the launcher's pid and port); the other local ranks read it,
+    so every rank places itself against the same ranking.  A rank that
+    cannot read it in ``timeout`` samples for itself."""
+    import json
+    import tempfile
+    import time
+    doms = l3_domains()
+    if len(doms) <= 1:
+        return doms, [0.0] * len(doms)
+    path = os.path.join(tempfile.gettempdir(), f"tritondl-place-{tag}.json")
+    if local_rank == 0 or local_world <= 1:
+        busy = domain_busy(doms)
+        order = sorted(range(len(doms)), key=lambda i: (round(busy[i] * 10), i))
+        if local_world > 1:
+            tmp = f"{path}.{os.getpid()}"
+            with open(tmp, "w") as f:
+                json.dump({"t": time.time(), "doms": doms, "order": order, "busy": busy}, f)
+            os.replace(tmp, path)
+        return [doms[i] for i in order], [busy[i] for i in order]
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if time.time() - d["t"] < 120 and d["doms"] == doms:
+                return [doms[i] for i in d["order"]], [d["busy"][i] for i in d["order"]]
+        except (OSError, ValueError, KeyError):
+            pass
+        time.sleep(0.05)
+    busy = domain_busy(doms)
+    return idle_first(doms, busy), sorted(busy, key=lambda b: round(b * 10))
