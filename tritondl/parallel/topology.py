@@ -142,8 +142,9 @@ def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> 
 def pin(spec: str, index: int = 0, count: int = 1) -> list[int]:
     """Pin the calling process (and every thread and child it starts later)
     to ``spec``: a cpulist; ``auto`` = the ``index``-th of ``count`` whole
-    last-level-cache domains spaced evenly over the node (one CCD with its SMT siblings per worker: on the box that beat 8
-    cores without siblings and two CCDs, ``profiles/r03_pin_ab/``);
+    last-level-cache domains spaced evenly over the node (one CCD with its
+    SMT siblings per worker: on the box that beat 8 cores without siblings
+    and two CCDs, ``profiles/r03_pin_ab/``);
     ``auto:N`` = the ``index``-th :func:`compact_cpuset` of N CPUs.  Returns
     the CPUs, or [] when ``spec`` is empty/"none" or pinning is unavailable."""
     spec = spec.strip()
