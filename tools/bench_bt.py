@@ -49,7 +49,14 @@ async def main() -> int:
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--s3-gbps", type=float, default=0.0,
                     help="--job: cap the fake S3's ingest link (Gbit/s; 0 = loopback speed)")
+    ap.add_argument("--cpus", default="", help="pin the leecher (worker) to this cpulist")
+    ap.add_argument("--fake-cpus", default="", help="pin the seeder (and fake S3) processes to this cpulist")
     a = ap.parse_args()
+    if a.fake_cpus:
+        os.environ["TRITONDL_BENCH_FAKE_CPUS"] = a.fake_cpus   # the fakes pin themselves (topology.pin_from_env)
+    if a.cpus:
+        from tritondl.parallel.topology import parse_cpulist
+        os.sched_setaffinity(0, parse_cpulist(a.cpus))
     if a.python_seeders:
         os.environ["TRITONDL_BT_NATIVE_WIRE"] = "0"     # read by the seeder processes (fakes/serve.py)
     if a.job:
