@@ -181,7 +181,15 @@ def main() -> int:
     ap.add_argument("--file-kb", type=int, default=10240)
     ap.add_argument("--torrent-mb", type=int, default=8)
     ap.add_argument("--out", default="")
+    ap.add_argument("--cpus", default="", help="pin the worker like TRITONDL_CPUS (cpulist or auto); the fakes "
+                                               "go to the next L3 domain with auto")
     a = ap.parse_args()
+    if a.cpus:
+        from .parallel import topology
+        if a.cpus == "auto":
+            doms = topology.l3_domains()
+            os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, doms[1 % len(doms)]))
+        topology.pin(a.cpus)
     from .utils.log import log
     log.configure("warning", "")
     fh = open(a.out, "w") if a.out else None
