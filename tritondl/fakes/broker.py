@@ -16,6 +16,13 @@ Implements the RabbitMQ semantics the worker depends on:
   ``expiration``, expired at the queue head like RabbitMQ) — the delayed
   retry queues of :mod:`tritondl.amqp.client` are built on that;
 * ``basic.get``, ``basic.cancel``, publisher confirms, ``mandatory`` returns;
+* per-user permissions (:meth:`add_user`): RabbitMQ's configure / write /
+  read regexes per resource, checked where RabbitMQ checks them
+  (``rabbit_channel``): declare/delete need *configure* on the entity,
+  publish needs *write* on the exchange (``amq.default`` for ""), bind needs
+  *write* on the queue and *read* on the exchange, consume/get/purge need
+  *read* on the queue, and a queue with ``x-dead-letter-exchange`` needs
+  *write* on that exchange.  A refusal is a 403 channel error;
 * fault injection: :meth:`drop_connections`, :meth:`set_blocked`,
   :meth:`fail_next_publishes` (nack), accept-delay.
 """
@@ -25,6 +32,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import itertools
+import re
 import time
 from dataclasses import dataclass, field
 from typing import Any
@@ -66,6 +74,20 @@ class Queue:
     rr: int = 0
     owner: Any = None
     delivered_total: int = 0
+
+
+@dataclass
+class Perms:
+    """One user's RabbitMQ permissions in the (single) vhost: a regex per
+    access kind, matched with search semantics like RabbitMQ's ``re:run``;
+    "" matches nothing (RabbitMQ stores it as ``^$``)."""
+    configure: str = ".*"
+    write: str = ".*"
+    read: str = ".*"
+
+    def allows(self, kind: str, name: str) -> bool:
+        pat = getattr(self, kind)
+        return pat != "" and re.search(pat, name) is not None
 
 
 class _Consumer:
@@ -133,6 +155,7 @@ class _ServerConn:
         self.closed = False
         self.client_properties: dict = {}
         self.user = ""
+        self.perms: Perms | None = None            # None: every resource allowed
         self._wbuf: list[bytes] = []
         self._flush_scheduled = False
 
@@ -217,6 +240,24 @@ class Broker:
         self.fail_publishes = 0
         self.published: list[QMsg] = []
         self.stats = collections.Counter()
+        self.users: dict[str, tuple[str, Perms]] = {}
+        self.refusals: list[tuple[str, str, str, str]] = []   # (user, kind, resource type, name)
+
+    def add_user(self, user: str, password: str, *, configure: str = ".*", write: str = ".*",
+                 read: str = ".*") -> None:
+        """A login with its own permission regexes (``rabbitmqctl set_permissions``)."""
+        self.users[user] = (password, Perms(configure, write, read))
+
+    def _check(self, c: "_ServerConn", kind: str, rtype: str, name: str, m: Method) -> None:
+        if c.perms is None:
+            return
+        rname = "amq.default" if rtype == "exchange" and name == "" else name
+        if not c.perms.allows(kind, rname):
+            self.refusals.append((c.user, kind, rtype, rname))
+            self.stats["refused"] += 1
+            raise ChannelError(codec.ACCESS_REFUSED,
+                               f"ACCESS_REFUSED - {kind} access to {rtype} '{rname}' in vhost '/' "
+                               f"refused for user '{c.user}'", m.ids)
 
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> "Broker":
@@ -282,6 +323,17 @@ class Broker:
         out = list(q.messages)
         q.messages.clear()
         return out
+
+    def declare(self, topic: str, shards: int = 2, *, queue_args: dict | None = None) -> None:
+        """Pre-declare a durable direct exchange ``topic`` with shard queues
+        ``topic-0..`` bound by name, as another service (e.g. the converter)
+        would — with its own queue arguments (``{"x-queue-type": "quorum"}``)."""
+        ex = self.exchanges.setdefault(topic, Exchange(topic, "direct", True))
+        for i in range(shards):
+            q = f"{topic}-{i}"
+            self.queues.setdefault(q, Queue(q, True, arguments=dict(queue_args or {})))
+            if (q, q, {}) not in ex.bindings:
+                ex.bindings.append((q, q, {}))
 
     def inject(self, exchange: str, routing_key: str, body: bytes, props: Properties | None = None) -> int:
         """Publish from outside any connection (test producer). Returns #queues routed."""
@@ -430,7 +482,12 @@ class Broker:
             else:  # AMQPLAIN: a field table without its length prefix
                 t = codec._Reader(struct_pack_len(resp)).table()
                 user, pw = str(t.get("LOGIN", "")), str(t.get("PASSWORD", ""))
-            if self.username is not None and (user != self.username or pw != (self.password or "")):
+            if user in self.users:
+                if pw != self.users[user][0]:
+                    raise ConnError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - Login was refused", m.ids)
+                c.perms = self.users[user][1]
+            elif (self.username is not None and (user != self.username or pw != (self.password or ""))) or \
+                    (self.users and self.username is None):
                 raise ConnError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - Login was refused", m.ids)
             c.user = user
             c.send_method(0, Method("connection.tune", {"channel_max": 2047, "frame_max": self.frame_max,
@@ -468,20 +525,31 @@ class Broker:
                 ch.prefetch_consumer = a["prefetch_count"]
             ok("basic.qos_ok")
         elif n == "exchange.declare":
+            if not a["passive"]:
+                self._check(c, "configure", "exchange", a["exchange"], m)
             self._exchange_declare(m)
             if not a["nowait"]:
                 ok("exchange.declare_ok")
         elif n == "exchange.delete":
+            self._check(c, "configure", "exchange", a["exchange"], m)
             if a["exchange"] not in self.exchanges:
                 raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{a['exchange']}'", m.ids)
             self.exchanges.pop(a["exchange"])
             if not a["nowait"]:
                 ok("exchange.delete_ok")
         elif n == "queue.declare":
+            if not a["passive"]:
+                self._check(c, "configure", "queue", a["queue"], m)
+                dlx = (a["arguments"] or {}).get("x-dead-letter-exchange")
+                if isinstance(dlx, str):
+                    self._check(c, "read", "queue", a["queue"], m)
+                    self._check(c, "write", "exchange", dlx, m)
             q = self._queue_declare(c, m)
             if not a["nowait"]:
                 ok("queue.declare_ok", queue=q.name, message_count=len(q.messages), consumer_count=len(q.consumers))
         elif n == "queue.bind":
+            self._check(c, "write", "queue", a["queue"], m)
+            self._check(c, "read", "exchange", a["exchange"], m)
             q = self._get_queue(a["queue"], m)
             ex = self.exchanges.get(a["exchange"])
             if ex is None:
@@ -492,17 +560,21 @@ class Broker:
             if not a["nowait"]:
                 ok("queue.bind_ok")
         elif n == "queue.unbind":
+            self._check(c, "write", "queue", a["queue"], m)
+            self._check(c, "read", "exchange", a["exchange"], m)
             ex = self.exchanges.get(a["exchange"])
             if ex is not None:
                 ex.bindings = [b for b in ex.bindings if not (b[0] == a["queue"] and b[1] == a["routing_key"])]
             ok("queue.unbind_ok")
         elif n == "queue.purge":
+            self._check(c, "read", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
             cnt = len(q.messages)
             q.messages.clear()
             if not a["nowait"]:
                 ok("queue.purge_ok", message_count=cnt)
         elif n == "queue.delete":
+            self._check(c, "configure", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
             cnt = len(q.messages)
             for cons in list(q.consumers):
@@ -514,6 +586,7 @@ class Broker:
             if not a["nowait"]:
                 ok("queue.delete_ok", message_count=cnt)
         elif n == "basic.consume":
+            self._check(c, "read", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
             if a["exclusive"] and q.consumers:
                 raise ChannelError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - queue in use", m.ids)
@@ -535,6 +608,7 @@ class Broker:
         elif n in ("basic.ack", "basic.nack", "basic.reject"):
             self._settle(ch, m)
         elif n == "basic.get":
+            self._check(c, "read", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
             if not q.messages:
                 ok("basic.get_empty")
@@ -653,6 +727,7 @@ class Broker:
         self.stats["published"] += 1
         if ch.confirm:
             ch.pub_seq += 1
+        self._check(c, "write", "exchange", m.exchange, m)   # before the lookup, as rabbit_channel
         if m.exchange not in self.exchanges:
             raise ChannelError(codec.NOT_FOUND, f"NOT_FOUND - no exchange '{m.exchange}'", (60, 40))
         if ch.confirm and self.fail_publishes > 0:

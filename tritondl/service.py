@@ -76,6 +76,10 @@ def default_impls(cfg: Config) -> list[ClientImpl]:
     return impls
 
 
+class JobBusy(Exception):
+    """Another worker has held this job's dir for longer than ``job_lock_wait_s``."""
+
+
 @dataclass
 class JobResult:
     ok: bool
@@ -168,8 +172,8 @@ class Service:
         another worker whose channel died mid-job, or concurrency > 1 — would
         otherwise truncate and rewrite the very file the first delivery is
         uploading from (and the send pump maps that file).  The second
-        delivery waits, then finds the file complete and re-uploads it
-        (at-least-once, as the reference)."""
+        delivery waits (see :meth:`_lock_dir`), then finds the file complete
+        and re-uploads it (at-least-once, as the reference)."""
         ent = self._id_locks.setdefault(media_id, [asyncio.Lock(), 0])
         ent[1] += 1
         fd = -1
@@ -182,15 +186,8 @@ class Service:
                     d = ""                          # invalid id: the job fails in its download stage
                 if d:
                     try:
-                        os.makedirs(d, mode=0o755, exist_ok=True)
+                        fd = await self._lock_dir(d, media_id)
                         self._locked_dirs.add(d)
-                        fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
-                        try:
-                            fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
-                        except BlockingIOError:
-                            log.with_field("media_id", media_id).warn(
-                                "job already running in another worker; waiting for it")
-                            await asyncio.get_running_loop().run_in_executor(None, fcntl.flock, fd, fcntl.LOCK_EX)
                     except OSError as e:
                         log.with_fields(media_id=media_id, error=str(e)).warn("job lock unavailable")
                 yield
@@ -201,6 +198,54 @@ class Service:
             ent[1] -= 1
             if ent[1] == 0:
                 self._id_locks.pop(media_id, None)
+
+    async def _lock_dir(self, d: str, media_id: str) -> int:
+        """Create ``d`` and ``flock`` it; returns the locked fd.
+
+        The wait for another process's lock is a poll (``LOCK_NB`` + an
+        asyncio backoff up to 0.5 s), never a blocking ``flock`` in an
+        executor thread: cancellation (SIGTERM) ends it at once, and no
+        thread is left blocked past shutdown.  After ``job_lock_wait_s``, or
+        once shutdown has begun, it raises :class:`JobBusy` and the delivery
+        goes back to the broker.
+        The lock must be on the dir that is still at ``d``: with cleanup the
+        holder renames its dir away when it finishes, so a lock won on an fd
+        opened before that rename is on the old inode — checked by comparing
+        ``fstat(fd)`` with ``stat(d)``, and retried on a fresh dir."""
+        deadline = time.monotonic() + max(0.0, self.cfg.job_lock_wait_s)
+        pause = 0.005
+        warned = False
+        while True:
+            os.makedirs(d, mode=0o755, exist_ok=True)
+            try:
+                fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
+            except FileNotFoundError:
+                continue                            # renamed away between makedirs and open
+            try:
+                fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+            except BlockingIOError:
+                os.close(fd)
+                if not warned:
+                    warned = True
+                    log.with_field("media_id", media_id).warn("job already running in another worker; waiting for it")
+                if time.monotonic() >= deadline:
+                    raise JobBusy(f"job dir {d} held by another worker for {self.cfg.job_lock_wait_s:.0f}s") \
+                        from None
+                if self._stop.is_set():
+                    raise JobBusy(f"job dir {d} held by another worker at shutdown") from None
+                await asyncio.sleep(pause)
+                pause = min(pause * 2, 0.5)
+                continue
+            except BaseException:
+                os.close(fd)
+                raise
+            try:
+                same = os.path.samestat(os.fstat(fd), os.stat(d))
+            except FileNotFoundError:
+                same = False
+            if same:
+                return fd
+            os.close(fd)                            # locked a dir that was renamed away: go again
 
     async def wait_finished(self, total: int, timeout: float | None = None) -> None:
         """Wait until ``jobs_finished >= total`` (woken by the result itself,
@@ -234,7 +279,9 @@ class Service:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)
             log.info("connecting to rabbitmq ...")
             self.amqp = Client(cfg.rabbitmq_url(), prefetch=cfg.prefetch, num_shard_queues=cfg.num_shard_queues,
-                               heartbeat=cfg.heartbeat_s, retry_delay=cfg.retry_delay_s)
+                               heartbeat=cfg.heartbeat_s, retry_delay=cfg.retry_delay_s,
+                               declare_publish=cfg.declare_publish,
+                               declare_publish_queues=cfg.declare_publish_queues)
             await self.amqp.connect()
             log.info("connected")
         else:
@@ -318,8 +365,20 @@ class Service:
 
         if log.enabled("info"):
             log.with_field("job", job.to_dict()).info("got message")
-        async with self._job_lock(job.media.id):
-            return await self._run_job(msg, job, t0)
+        try:
+            async with self._job_lock(job.media.id):
+                return await self._run_job(msg, job, t0)
+        except JobBusy as e:
+            # not the job's failure: hand it back without spending a retry
+            log.with_field("media_id", job.media.id).warn("%s; handing the delivery back", e)
+            self.metrics.inc("jobs", status="busy")
+            try:
+                await msg.retry(max(self.cfg.retry_delay_s, 1.0), increment=0)
+            except Exception as e2:  # noqa: BLE001
+                log.with_field("error", str(e2)).error("failed to hand a busy job back; parking it")
+                if not (msg.settled or msg.stale):
+                    self.amqp.park(msg, msg.retry_props(0), self.cfg.retry_delay_max_s)
+            return self._record(JobResult(False, "lock", str(e), seconds=time.monotonic() - t0))
 
     async def _run_job(self, msg: Delivery, job: Download, t0: float) -> JobResult:
         stage = "download"
@@ -401,7 +460,7 @@ class Service:
         if not (self.cfg.stream_upload and isinstance(impl, HTTPDownloader)):
             return await self.dispatcher.download(media_id, url), {}
         d = self.dispatcher.job_dir(media_id)
-        if d not in self._locked_dirs:          # _job_lock made (and locked) it already
+        if d not in self._locked_dirs:          # _job_lock made, locked and checked it already
             os.makedirs(d, mode=0o755, exist_ok=True)
         h = await impl.start(d, self.dispatcher.sink, url)
         if marks is not None:
@@ -507,25 +566,31 @@ class Service:
 
     async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> None:
         """B4 fix: retry with X-Retries+1 through a broker delay queue (the slot
-        is free at once), dead-letter after ``max_retries``."""
+        is free at once; parked in-process if the broker refuses the delay
+        queue), dead-letter after ``max_retries``."""
         assert self.amqp is not None
         try:
             if msg.metadata.retries < self.cfg.max_retries:
                 d = self.cfg.retry_delay_for(msg.metadata.retries)
                 log.with_fields(retries=msg.metadata.retries + 1, delay_s=d).warn("scheduling job retry")
-                await msg.retry(d)
+                how = await msg.retry(d)
                 self.metrics.inc("jobs_retried")
+                if how == "parked":
+                    self.metrics.inc("jobs_parked")
                 return
         except Exception as e:  # noqa: BLE001
-            # e.g. the delay queue's declare refused (PRECONDITION_FAILED): the
-            # delivery must still be settled, or a prefetch-1 consumer stalls (B4)
+            # the retry publish itself failed: the delivery must still be settled, or a
+            # prefetch-1 consumer stalls (B4)
             log.with_field("error", str(e)).error("failed to schedule retry; dead-lettering the job")
         await self._dead_letter(msg, stage, err)
 
     async def _dead_letter(self, msg: Delivery, stage: str, err: Exception) -> None:
         """Publish the job (confirmed) to the durable dead-letter topic, then ack.
-        If that fails the delivery is nacked with requeue, so it is always
-        settled (the broker keeps the job either way)."""
+        If the dead-letter topic cannot be reached (a user that may neither
+        declare nor write it), the job is parked: re-published to its own
+        queue with ``X-Retries+1`` after ``retry_delay_max_s`` — the
+        reference's ``Error()`` at the longest delay, never a nack-requeue
+        loop, and never dropped."""
         assert self.amqp is not None
         try:
             if self.cfg.drop_failed:
@@ -535,17 +600,17 @@ class Service:
             hdrs = dict(msg.msg.properties.headers or {})
             hdrs.update({"X-Retries": msg.metadata.retries, "X-Failed-Stage": stage, "X-Error": str(err)[:512],
                          "X-Original-Routing-Key": msg.routing_key})
-            await self.amqp.publish(self.cfg.dlq_topic, msg.body, headers=hdrs)
+            await self.amqp.publish(self.cfg.dlq_topic, msg.body, headers=hdrs, max_attempts=3)
             await msg.ack()
             log.with_fields(topic=self.cfg.dlq_topic, stage=stage).warn("job dead-lettered")
             self.metrics.inc("jobs_dead_lettered")
         except Exception as e:  # noqa: BLE001
-            log.with_field("error", str(e)).error("failed to dead-letter job; requeueing it")
-            try:
-                await msg.nack(requeue=True)
-                self.metrics.inc("jobs_requeued")
-            except Exception as e2:  # noqa: BLE001 - channel gone: the broker redelivers it anyway
-                log.with_field("error", str(e2)).error("failed to requeue job; broker will redeliver")
+            if msg.settled or msg.stale:
+                return                      # its channel is gone: the broker redelivers it anyway
+            log.with_fields(error=str(e), delay_s=self.cfg.retry_delay_max_s).error(
+                "failed to dead-letter job; parking it")
+            self.amqp.park(msg, msg.retry_props(), self.cfg.retry_delay_max_s)
+            self.metrics.inc("jobs_parked")
 
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")

@@ -61,6 +61,11 @@ class Config:
     publish_topic: str = "v1.convert"           # downloader.go:147
     num_shard_queues: int = 2                   # client.go:108
     prefetch: int = 1                           # downloader.go:62
+    # publish-side topology (the reference declared none, client.go:224): declare the
+    # publish exchange (and its shard queues) before the first publish, best-effort —
+    # a 403/406 means someone else owns it and the worker publishes without declaring
+    declare_publish: bool = True
+    declare_publish_queues: bool = True
 
     # --- job processing ---
     concurrency: int = 1                        # one job loop (downloader.go:103)
@@ -70,6 +75,9 @@ class Config:
     retry_delay_max_s: float = 300.0            # cap on one retry delay
     dead_letter_topic: str = ""                 # "" => "<consume_topic>.dead"
     drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
+    # a delivery whose job dir another worker holds waits this long, then goes back to
+    # the broker (same X-Retries) instead of pinning the job slot
+    job_lock_wait_s: float = 60.0
     cleanup: bool = False                       # B15: off for parity
     # with cleanup: keep up to this many bytes of finished job files as spares that new
     # downloads are renamed into and overwrite, instead of freeing and re-allocating
@@ -187,7 +195,7 @@ class Config:
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
-                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s"}
+                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s"}
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -204,6 +212,8 @@ class Config:
                 setattr(c, a, g("TRITONDL_" + k))
         c.cleanup = _env_bool(g("TRITONDL_CLEANUP"), c.cleanup)
         c.drop_failed = _env_bool(g("TRITONDL_DROP_FAILED"), c.drop_failed)
+        c.declare_publish = _env_bool(g("TRITONDL_DECLARE_PUBLISH"), c.declare_publish)
+        c.declare_publish_queues = _env_bool(g("TRITONDL_DECLARE_PUBLISH_QUEUES"), c.declare_publish_queues)
         c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_dht_ipv6 = _env_bool(g("TRITONDL_BT_DHT_IPV6"), c.bt_dht_ipv6)
