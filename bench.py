@@ -22,6 +22,15 @@ max-rank elapsed), per-rank work is fixed on average: ``scaling="weak"``.
 ``--isolated`` restores private per-rank stacks; ``--tls`` runs origin and
 S3 over https (OpenSSL in the native data plane).
 
+Every job fetches its own payload variant and the S3 fake refuses a PUT
+whose content is not that variant's (64 KiB-leaf SHA-256 list, computed
+natively while the chunk signatures are verified): a worker uploading
+stale or torn bytes fails the run.  ``config`` states the cleanup mode
+(the reference never deletes a job dir, B15) and the spare-file recycling
+budget; ``diag`` carries what explains a slow run (per-job latency spread,
+CCD load at launch, CPU clocks, faults and context switches per job,
+whether this was the lease's first run).
+
 The reference publishes no numbers → ``vs_baseline: null``.
 A secondary, untimed-for-headline figure reports the HIP batched piece-hash
 kernel (torrent resume verification) on this GPU.
@@ -79,6 +88,58 @@ def _gpu_hash_probe(total_mb: int = 4096) -> dict:
         return {"gpu_probe_error": str(e)[:200]}
 
 
+_PLACEMENT: dict = {}
+
+
+def _cpu_mhz(cpus: list[int]) -> dict | None:
+    """Current clock of the given CPUs (cpufreq, else /proc/cpuinfo): min/mean/max MHz."""
+    vals: list[float] = []
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cpufreq/scaling_cur_freq") as f:
+                vals.append(int(f.read()) / 1000.0)
+        except (OSError, ValueError):
+            vals = []
+            break
+    if not vals:
+        try:
+            mhz: dict[int, float] = {}
+            cur = -1
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("processor"):
+                        cur = int(line.split(":")[1])
+                    elif line.startswith("cpu MHz") and cur >= 0:
+                        mhz[cur] = float(line.split(":")[1])
+            vals = [mhz[c] for c in cpus if c in mhz]
+        except (OSError, ValueError):
+            return None
+    if not vals:
+        return None
+    return {"min": round(min(vals)), "mean": round(sum(vals) / len(vals)), "max": round(max(vals)), "n": len(vals)}
+
+
+def _lease_state() -> dict:
+    """Was this the first bench on this host since it booted / was leased?  A
+    marker in /tmp (fresh on every gpurun box) says; uptime and load help."""
+    import tempfile
+    marker = os.path.join(tempfile.gettempdir(), "tritondl-bench-ran")
+    fresh = not os.path.exists(marker)
+    try:
+        with open(marker, "a") as f:
+            f.write(f"{time.time()}\n")
+    except OSError:
+        pass
+    out: dict = {"lease_fresh": fresh}
+    try:
+        with open("/proc/uptime") as f:
+            out["host_uptime_s"] = round(float(f.read().split()[0]))
+        out["loadavg"] = [round(x, 2) for x in os.getloadavg()]
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_size: int) -> list[int]:
     """Pin this rank's process (inherited by every native thread and by the
     fakes it spawns) before anything starts, and choose the fakes' set.
@@ -114,6 +175,11 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
         os.sched_setaffinity(0, pinned)
         if busy:
             os.environ["TRITONDL_BENCH_DOMAIN_BUSY"] = f"{busy[first % len(busy)]:.2f}"
+            # every L3 domain's busy share at launch, in topology order (first CPU: share)
+            chosen = {doms[(first + j) % len(doms)][0] for j in range(k)}
+            _PLACEMENT["ccd_busy_at_launch"] = {str(d[0]): round(b, 3) for d, b in
+                                                 sorted(zip(doms, busy), key=lambda x: x[0][0])}
+            _PLACEMENT["chosen_ccds"] = sorted(chosen)
     elif cpus not in ("", "none"):
         pinned = topology.pin(cpus, local_rank)
     if fc:
@@ -159,11 +225,21 @@ def main() -> int:
                          "packed into the fewest L3 domains; 'none' = no pinning.  Default auto: on the "
                          "16-CPU box share one CCD measured 323-336 vs 222-279 jobs/s unpinned, "
                          "profiles/r03_pin_ab/)")
+    ap.add_argument("--cleanup", default="on", choices=["on", "off"],
+                    help="on: each settled job's dir is deleted (its file kept as a spare the next download "
+                         "is renamed into, up to --recycle-mb); off: the reference, which never deletes (B15)")
+    ap.add_argument("--recycle-mb", type=int, default=-1, help="spare-file budget with cleanup on (-1: worker "
+                                                               "default, 0: delete every file)")
+    ap.add_argument("--variants", type=int, default=-1,
+                    help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
+    ap.add_argument("--no-content-check", action="store_true",
+                    help="S3 does not compare PUT content with the origin's payload")
     ap.add_argument("--fake-cpus", default="auto",
                     help="pin the fake broker/origin/S3/producer processes (remote endpoints in "
                          "production) elsewhere: a cpulist, auto = the L3 domain after the last rank's, "
                          "'same' = the rank's own set")
     a = ap.parse_args()
+    lease = _lease_state()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,7 +282,9 @@ def main() -> int:
                      http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
                      http_stripe_bytes=(a.stripe_kb << 10) if a.stripe_kb >= 0 else -1,
                      s3_part_size=a.s3_part_mb << 20, s3_multipart_threshold=a.s3_multipart_mb << 20,
-                     payload_mode=a.payload, hash_device=a.s3_hash_device)
+                     payload_mode=a.payload, hash_device=a.s3_hash_device, cleanup=a.cleanup == "on",
+                     recycle_bytes=(a.recycle_mb << 20) if a.recycle_mb >= 0 else -1, variants=a.variants,
+                     content_check=not a.no_content_check)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 
@@ -253,6 +331,8 @@ def main() -> int:
             from tritondl.utils.profiler import CPUProfiler
             prof = CPUProfiler(a.cpuprofile if world == 1 else f"{a.cpuprofile}.r{rank}")
         stack.cpu_seconds()              # first call imports psutil: keep it out of the profiled window
+        import resource
+        mhz0 = _cpu_mhz(pinned) if pinned else None
         barrier()
         if prof is not None:
             prof.start()
@@ -264,6 +344,7 @@ def main() -> int:
             loop_prof = cProfile.Profile(time.thread_time)
             loop_prof.enable()
         cpu0 = stack.cpu_seconds()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         if shared:
             loop.run_until_complete(phase(a.steps))
@@ -272,7 +353,9 @@ def main() -> int:
         if cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
         cpu1 = stack.cpu_seconds()
+        mhz1 = _cpu_mhz(pinned) if pinned else None
         if loop_prof is not None:
             loop_prof.disable()
             loop_prof.dump_stats(os.environ["TRITONDL_BENCH_LOOP_PROFILE"])
@@ -284,6 +367,18 @@ def main() -> int:
         done = stack.svc.results[-n_done:] if n_done else []  # type: ignore[union-attr]
         failed = len(stack.failures())
         lat = sorted(r.seconds for r in done)
+        n_div = max(1, n_done)
+        diag = {**lease, **_PLACEMENT,
+                "job_latency_ms": ({"min": round(lat[0] * 1000, 2), "max": round(lat[-1] * 1000, 2),
+                                    "first": round(done[0].seconds * 1000, 2),
+                                    "last": round(done[-1].seconds * 1000, 2)} if done else None),
+                "cpu_mhz_pinned": {"start": mhz0, "end": mhz1},
+                # worker process (this rank), per timed job
+                "minflt_per_job": round((ru1.ru_minflt - ru0.ru_minflt) / n_div, 1),
+                "majflt_per_job": round((ru1.ru_majflt - ru0.ru_majflt) / n_div, 2),
+                "nvcsw_per_job": round((ru1.ru_nvcsw - ru0.ru_nvcsw) / n_div, 1),
+                "nivcsw_per_job": round((ru1.ru_nivcsw - ru0.ru_nivcsw) / n_div, 1),
+                "s3_content_checked": bool(stack.content_check and stack.resolved_variants())}
         spans: dict[str, list[float]] = {}
         for r in done:
             for k, v in r.marks.items():
@@ -323,7 +418,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8",
-            "data": f"synthetic (deterministic pseudo-random {file_size / 2**20:g} MiB payload; "
+            "data": f"synthetic ({stack.resolved_variants() or 1} distinct deterministic pseudo-random "
+                    f"{file_size / 2**20:g} MiB payloads, one per job in rotation, S3 content-checked; "
                     f"local fake broker/origin/S3{' over https' if a.tls else ''})",
             "config": {"model": name, "global_batch": world * a.concurrency, "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
@@ -335,6 +431,9 @@ def main() -> int:
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
                        "cpus_busy_before": os.environ.get("TRITONDL_BENCH_DOMAIN_BUSY", ""),
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
+                       "cleanup": stack.cleanup,
+                       "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
+                       "payload_variants": stack.resolved_variants(),
                        **knobs},
             "jobs_per_rank": per_rank,
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
@@ -351,6 +450,7 @@ def main() -> int:
             # the one fake broker serves every rank: the share of a core it used.  Above
             # 0.5 the harness, not the workers, may be what limits the run
             "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3) if max_elapsed >= 0.5 else None,
+            "diag": diag,
         }
         if res["broker_core_share"] is not None and res["broker_core_share"] > 0.5:
             res["harness_bound"] = True

@@ -285,12 +285,15 @@ PYBIND11_MODULE(_relay, m) {
             r = recv_verify_chunked(*io.s, raw_len, pre.data(), pre.size(), k, amzdate, scope, seed, keep, threads,
                                     idle_timeout);
           }
-          return py::make_tuple(r.decoded, r.err, keep ? py::object(py::bytes(r.data)) : py::object(py::none()));
+          return py::make_tuple(r.decoded, r.err, keep ? py::object(py::bytes(r.data)) : py::object(py::none()),
+                                py::bytes(r.leaf_hashes));
         },
         py::arg("sock"), py::arg("raw_len"), py::arg("prefix"), py::arg("signing_key"), py::arg("amzdate"),
         py::arg("scope"), py::arg("seed"), py::arg("keep") = false, py::arg("threads") = 4,
         py::arg("idle_timeout") = 300.0,
-        "Receive + verify an aws-chunked body; returns (decoded_len, error, data_or_None).");
+        "Receive + verify an aws-chunked body; returns (decoded_len, error, data_or_None, leaf_hashes): "
+        "leaf_hashes = the payload SHA-256s of its 64 KiB leaves, concatenated (b'' unless every frame "
+        "but the last is one 64 KiB leaf).");
 
   m.def("chunked_length", &chunked_length, py::arg("length"), py::arg("chunk") = 64 << 10);
   m.def("pool_threads", [] { return tritondl_hash::TaskPool::get().threads(); },

@@ -1352,7 +1352,24 @@ struct VerifyResult {
   uint64_t decoded = 0;
   std::string err;
   std::string data;  // decoded payload when keep
+  // content fingerprint of the decoded payload, free from the chunk
+  // verification: the payload SHA-256s of its 64 KiB leaves, concatenated
+  // (32 bytes per leaf).  Only when every frame but the last carries exactly
+  // one 64 KiB leaf (the client's chunking); empty otherwise.  Leaf lists of
+  // consecutive multipart parts concatenate to the whole object's
+  std::string leaf_hashes;
 };
+
+constexpr size_t kLeafBytes = 64u << 10;
+
+// leaf_hashes from the frames' payload SHA-256s (raw, 32 bytes each, in
+// order; zero-length frames excluded by the caller), if the frames are leaves
+inline std::string leaf_hashes_of(std::string hashes, const std::vector<size_t>& sizes) {
+  for (size_t i = 0; i + 1 < sizes.size(); ++i)
+    if (sizes[i] != kLeafBytes) return std::string();
+  if (!sizes.empty() && (sizes.back() == 0 || sizes.back() > kLeafBytes)) return std::string();
+  return hashes;
+}
 
 struct RawFrame {
   size_t off, n;  // payload offset in its window buffer, payload length
@@ -1414,6 +1431,8 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
   std::string verr;  // verifier error (read after join)
   bool final_seen = false;
   const int t = threads <= 0 ? 4 : threads;
+  std::string leaf_hashes;          // raw payload SHA-256s of the non-empty frames, in order
+  std::vector<size_t> leaf_sizes;   // (appended by one verifier thread at a time)
 
   auto join = [&] {
     if (verifier.joinable()) verifier.join();
@@ -1475,6 +1494,7 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
       tritondl_hash::name_thread("tdl-verify");
       const char* raw = wb->data();
       std::vector<std::string> h(frames.size());
+      std::string rawh(32 * frames.size(), '\0');
       std::vector<size_t> doff(frames.size() + 1, 0);
       for (size_t i = 0; i < frames.size(); ++i) doff[i + 1] = doff[i] + frames[i].n;
       const int used = static_cast<int>(std::min<size_t>(static_cast<size_t>(t), std::max<size_t>(1, doff.back() >> 20)));
@@ -1487,17 +1507,23 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
           const RawFrame& g = frames[i + 1];
           tritondl_hash::sha256_pair(raw + f.off, f.n, raw + g.off, g.n, d[0], d[1]);
           h[i + 1] = tritondl_hash::hex_raw(d[1], 32);
+          std::memcpy(&rawh[32 * (i + 1)], d[1], 32);
           if (keep && g.n) std::memcpy(&r.data[dbase + doff[i + 1]], raw + g.off, g.n);
         } else {
           tritondl_hash::sha256_raw(raw + f.off, f.n, d[0]);
         }
         h[i] = tritondl_hash::hex_raw(d[0], 32);
+        std::memcpy(&rawh[32 * i], d[0], 32);
         if (keep && f.n) std::memcpy(&r.data[dbase + doff[i]], raw + f.off, f.n);
       });
       for (size_t i = 0; i < frames.size(); ++i) {
         if (std::memcmp(signer.next(h[i]).data(), raw + frames[i].sig, 64) != 0) {
           verr = "chunk signature mismatch";
           return;
+        }
+        if (frames[i].n) {
+          leaf_hashes.append(rawh, 32 * i, 32);
+          leaf_sizes.push_back(frames[i].n);
         }
       }
     });
@@ -1507,6 +1533,7 @@ inline VerifyResult recv_verify_windowed(Stream& io, uint64_t raw_len, const cha
   join();
   if (r.err.empty() && !verr.empty()) r.err = verr;
   if (r.err.empty() && (have != 0 || received != raw_len)) r.err = "trailing bytes after final chunk";
+  if (r.err.empty()) r.leaf_hashes = leaf_hashes_of(std::move(leaf_hashes), leaf_sizes);
   return r;
 }
 
@@ -1670,6 +1697,18 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
   pool->wait();
   if (r.err.empty() && !sig_ok) r.err = "chunk signature mismatch";
   if (r.err.empty() && (!final_seen || parsed != raw_len || have != raw_len)) r.err = "trailing bytes after final chunk";
+  if (r.err.empty()) {
+    std::string hs;
+    std::vector<size_t> sizes;
+    hs.reserve(32 * published);
+    sizes.reserve(published);
+    for (size_t j = 0; j < published; ++j) {
+      if (!frame(j).n) continue;
+      hs.append(reinterpret_cast<const char*>(frame(j).h), 32);
+      sizes.push_back(frame(j).n);
+    }
+    r.leaf_hashes = leaf_hashes_of(std::move(hs), sizes);
+  }
   if (r.err.empty() && keep) {
     r.data.resize(static_cast<size_t>(r.decoded));
     size_t o = 0;

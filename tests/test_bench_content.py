@@ -1,0 +1,133 @@
+"""The headline bench sees wrong bytes (VERDICT r03 Weak #2).
+
+Jobs rotate through distinct payload variants and the S3 fake checks each
+PUT's 64 KiB-leaf SHA-256 list against the origin's variant — from the hashes
+the native chunk verifier computes anyway (``csrc/relay/relay_core.h``).
+A deliberately broken download watermark (the streamed upload told the whole
+file is on disk when it is not) must fail the run; the reference's upload
+(``internal/uploader/uploader.go:89``) streams the finished file, which is
+what the watermark stands in for."""
+
+import asyncio
+import hashlib
+import os
+import socket
+
+import pytest
+
+from tritondl.bench_job import JobStack
+from tritondl.fakes import payload
+from tritondl.fetch.http import HTTPDownloader
+from tritondl.utils import rawhttp
+
+
+def run(coro, timeout=120):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+def test_variants_differ_in_every_page():
+    size = 3 * 4096 + 100
+    a, b = payload.variant_bytes(size, 1), payload.variant_bytes(size, 2)
+    assert len(a) == len(b) == size
+    for p in range(0, size, 4096):
+        assert a[p:p + 4096] != b[p:p + 4096]
+    assert payload.variant_of("movie-12-v7.mkv") == 7 and payload.variant_of("movie-12.mkv") is None
+    exp = payload.Expectations(size, 3)
+    assert exp.expected("movie-0-v2.mkv", size) == payload.leaf_digest(b)
+    assert exp.expected("movie-0-v2.mkv", size + 1) is None
+    # the leaf list is plain SHA-256 per 64 KiB
+    big = payload.variant_bytes(200_000, 0)
+    assert payload.leaf_hashes(big) == b"".join(hashlib.sha256(big[i:i + 65536]).digest()
+                                                for i in range(0, len(big), 65536))
+
+
+@pytest.mark.skipif(rawhttp.relay_module() is None, reason="native relay not built")
+def test_native_verifier_returns_the_leaf_hashes():
+    """recv_verify_chunked's 4th value equals the leaf hashes of the payload."""
+    from tritondl.s3 import sigv4
+    relay = rawhttp.relay_module()
+    data = os.urandom(5 * 65536 + 1234)
+    key = b"k" * 32
+    amz, scope, seed = "20260101T000000Z", "20260101/us-east-1/s3/aws4_request", "0" * 64
+    from tritondl.ops import hashing
+    enc, _last = hashing.aws_chunk_encode(key, amz, scope, seed, data, sigv4.STREAM_CHUNK, final=True)
+    a, b = socket.socketpair()
+    try:
+        n, err, body, leaves = relay.recv_verify_chunked(b.fileno(), len(enc), enc, key, amz, scope, seed, False, 2,
+                                                         5.0)
+    finally:
+        a.close()
+        b.close()
+    assert err == "" and n == len(data) and body is None
+    assert leaves == payload.leaf_hashes(data)
+
+
+def _break_watermark(monkeypatch):
+    """The fault: right after the download starts, claim the whole file is on disk."""
+    real = HTTPDownloader.start
+
+    async def start(self, base_dir, progress, url):
+        h = await real(self, base_dir, progress, url)
+        if h.size and h.flow is not None:
+            h.flow.finish(h.size)
+
+        async def at_once(n):
+            return None
+        h.wait_bytes = at_once
+        return h
+    monkeypatch.setattr(HTTPDownloader, "start", start)
+
+
+SIZE = 4 << 20
+RATE = 16e6       # the origin writes 1 MiB, then pauses 65 ms: an upload not held back runs ahead
+
+
+async def _run(tmp_path, jobs, size=SIZE, rate=RATE, **kw):
+    st = JobStack(file_size=size, inproc=True, tag="wm", workdir=str(tmp_path / "w"), **kw)
+    await st.setup()
+    st.backends[-2].rate = rate
+    try:
+        await st.run_jobs(jobs)
+        return st.backends[-1].counts
+    finally:
+        await st.teardown()
+
+
+def test_correct_worker_passes_the_content_check(tmp_path):
+    counts = run(_run(tmp_path, 4))
+    assert counts == {"content_ok": 4, "content_bad": 0}
+
+
+def test_broken_watermark_fails_the_bench(tmp_path, monkeypatch):
+    _break_watermark(monkeypatch)
+    with pytest.raises(RuntimeError, match="jobs failed"):
+        run(_run(tmp_path, 3))
+
+
+def test_broken_watermark_undetected_without_variants_check(tmp_path, monkeypatch):
+    """Control: with the content check off, the r03 bench's blind spot —
+    objects whose bytes are not the origin's are accepted (only a torn read
+    that changes between hashing and sending trips the signature chain)."""
+    _break_watermark(monkeypatch)
+    from tritondl.s3.uploader import object_key
+
+    async def main():
+        st = JobStack(file_size=SIZE, inproc=True, tag="wm", workdir=str(tmp_path / "w"), content_check=False)
+        await st.setup()
+        st.backends[-2].rate = RATE
+        s3 = st.backends[-1]
+        try:
+            accepted_wrong = 0
+            for i in range(4):
+                try:
+                    await st.run_jobs(1)
+                except RuntimeError:
+                    continue                    # a torn read the signature chain caught
+                got = s3.object_bytes("triton-staging", object_key(f"bench-wm-{i}", st.job_name(i)))
+                want = payload.variant_bytes(SIZE, payload.variant_of(st.job_name(i)))
+                accepted_wrong += got != want
+            return accepted_wrong, s3.counts
+        finally:
+            await st.teardown()
+    wrong, counts = run(main())
+    assert wrong >= 1 and counts == {"content_ok": 0, "content_bad": 0}

@@ -129,7 +129,7 @@ def test_send_then_verify_roundtrip(tmp_path, size):
         t.start()
         _s, _l, err = relay.send_body(a.fileno(), b"", fd, 0, size, None, 1, KEY, AMZ, SCOPE, SEED, 65536, 2)
         t.join()
-        n, verr, body = out["r"]
+        n, verr, body, _leaf = out["r"]
         assert err == "" and verr == "" and n == size and body == data
     finally:
         os.close(fd)

@@ -11,6 +11,11 @@ fetch into ``downloading/<id>/`` → select → SigV4 aws-chunked PUT to
 ``triton-staging/<id>/original/<b64>`` → publish ``v1.convert`` → ack.
 A producer connection publishes the ``api.Download`` jobs; completion is
 observed as the job's ack, and each ``Convert`` is checked on the way out.
+
+Every job fetches a payload of its own (variant ``i % R`` of the synthetic
+file, ``R`` larger than the spare-file pool, :mod:`tritondl.fakes.payload`)
+and the S3 fake refuses any PUT whose 64 KiB-leaf SHA-256 list is not that
+variant's: a worker that uploads stale or torn bytes fails the run.
 """
 
 from __future__ import annotations
@@ -117,6 +122,10 @@ class JobStack:
     tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
     payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
     hash_device: str = "cpu"         # aws-chunked chunk SHA-256s: cpu (SHA-NI) | gpu (HIP)
+    cleanup: bool = True             # delete (or recycle) each job's dir once settled; False = the reference (B15)
+    recycle_bytes: int = -1          # -1: worker default (Config); 0: delete every file
+    variants: int = -1               # payload variants; -1: more than the spare pool can hold, 0: one payload
+    content_check: bool = True       # S3 refuses PUTs whose content is not the origin's variant
     cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
@@ -126,6 +135,23 @@ class JobStack:
     last_run: dict = field(default_factory=dict)     # the producer's report of the last run
     origin_urls: list = field(default_factory=list)
     _n: int = 0
+
+    def resolved_recycle_bytes(self) -> int:
+        if self.recycle_bytes >= 0:
+            return self.recycle_bytes
+        return int(os.environ.get("TRITONDL_RECYCLE_BYTES", Config().recycle_bytes))
+
+    def resolved_variants(self) -> int:
+        """More variants than spare files the pool can hold (max 64 files,
+        service.py), so a recycled spare never holds the new job's own bytes."""
+        if self.variants >= 0:
+            return self.variants
+        depth = min(64, self.resolved_recycle_bytes() // max(1, self.file_size)) if self.cleanup else 0
+        return depth + 3
+
+    def _variant_args(self) -> list[str]:
+        r = self.resolved_variants()
+        return ["--variants", str(r), "--variant-size", str(self.file_size)] if r else []
 
     def _tls_files(self) -> tuple[str, str, str]:
         """(ca_file, cert_file, key_file) of a throwaway PKI in the workdir."""
@@ -159,8 +185,13 @@ class JobStack:
                 b = await Broker().start()
                 self.backends.append(b)
                 out["broker"] = b.url
-            o = await SyntheticOrigin(tls=tls).start()
-            s3 = await FakeS3(store="memory", access_key=AK, secret_key=SK, tls=tls).start()
+            from .fakes.payload import Expectations
+            r = self.resolved_variants()
+            o = SyntheticOrigin(tls=tls)
+            o.precompute(self.file_size, r)
+            await o.start()
+            expect = Expectations(self.file_size, r) if r and self.content_check else None
+            s3 = await FakeS3(store="memory", access_key=AK, secret_key=SK, tls=tls, expect=expect).start()
             self.backends += [o, s3]
             out["origin"] = f"{'https' if tls else 'http'}://{o.host}:{o.port}"
             out["s3"] = s3.endpoint
@@ -175,8 +206,10 @@ class JobStack:
             self.backends.append(bk)
             out["broker"] = bk.info["url"]
             self.broker_pid = bk.proc.pid if bk.proc is not None else 0
-        og = await Backend("origin", tls_args).start()
-        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK, *tls_args]).start()
+        va = self._variant_args()
+        og = await Backend("origin", [*tls_args, *va]).start()
+        s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK, *tls_args,
+                                  *(va if self.content_check else [])]).start()
         self.backends += [og, s3]
         out["origin"], out["s3"] = og.info["url"], s3.info["url"]
         return out
@@ -193,9 +226,11 @@ class JobStack:
         cfg.download_dir = os.path.join(self.workdir, "downloading")
         cfg.concurrency = self.concurrency
         cfg.prefetch = self.prefetch
-        cfg.cleanup = True          # keep disk bounded across thousands of bench jobs
-        # spare-file recycling (utils/spares.py) is on with cleanup; 0 = the A/B switch
-        cfg.recycle_bytes = int(os.environ.get("TRITONDL_RECYCLE_BYTES", cfg.recycle_bytes))
+        # cleanup keeps disk bounded across thousands of bench jobs; the reference never
+        # deleted (B15): cleanup=False is its mode.  Spare-file recycling (utils/spares.py)
+        # is on with cleanup; recycle_bytes 0 = the A/B switch
+        cfg.cleanup = self.cleanup
+        cfg.recycle_bytes = self.resolved_recycle_bytes()
         cfg.retry_delay_s = 0.0
         cfg.max_retries = 0
         cfg.progress_log_interval_s = 0
@@ -232,7 +267,8 @@ class JobStack:
             # this worker's event loop (bench_producer.py)
             self.producer_proc = await Backend("producer", [
                 "--broker", broker_url, "--origins", ",".join(self.origin_urls), "--size", str(self.file_size),
-                "--tag", self.tag, "--broker-pid", str(self.broker_pid)], module="tritondl.bench_producer").start()
+                "--tag", self.tag, "--broker-pid", str(self.broker_pid),
+                "--variants", str(self.resolved_variants())], module="tritondl.bench_producer").start()
             return
         self.producer = await Connection.open(broker_url, heartbeat=0)
         self.pch = await self.producer.channel()
@@ -252,10 +288,14 @@ class JobStack:
         await self.convert_ch.basic_consume("v1.convert-0", on_convert)
         await self.convert_ch.basic_consume("v1.convert-1", on_convert)
 
+    def job_name(self, i: int) -> str:
+        r = self.resolved_variants()
+        return f"movie-{i}-v{i % r}.mkv" if r else f"movie-{i}.mkv"
+
     def job_body(self, i: int) -> tuple[str, bytes]:
         mid = f"bench-{self.tag}-{i}"
         origin = self.origin_urls[i % len(self.origin_urls)]
-        url = f"{origin}/synthetic/{self.file_size}/movie-{i}.mkv"
+        url = f"{origin}/synthetic/{self.file_size}/{self.job_name(i)}"
         d = Download(created_at="now", media=Media(id=mid, name=f"movie {i}", source=SourceType.HTTP,
                                                       source_uri=url))
         return mid, d.encode()
@@ -383,11 +423,13 @@ def run_single_job_smoke(size: int = 1 << 20) -> None:
             assert st.converts, "no v1.convert published"
             c = st.converts[0]
             assert c.media is not None and c.media.id == "bench-smoke-0"
-            from .fakes.serve import synthetic_bytes
+            from .fakes.payload import variant_bytes, variant_of
             s3 = st.backends[-1]
             from .s3.uploader import object_key
-            got = s3.object_bytes("triton-staging", object_key(c.media.id, "movie-0.mkv"))
-            assert hashlib.md5(got).digest() == hashlib.md5(synthetic_bytes(size)).digest()
+            got = s3.object_bytes("triton-staging", object_key(c.media.id, st.job_name(0)))
+            want = variant_bytes(size, variant_of(st.job_name(0)))
+            assert hashlib.md5(got).digest() == hashlib.md5(want).digest()
+            assert s3.counts["content_ok"] == 1
         finally:
             await st.teardown()
     asyncio.run(asyncio.wait_for(main(), 120))

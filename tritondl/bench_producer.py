@@ -17,6 +17,10 @@ lines:
         stdin   EOF                      exit
 
 Each ``Convert`` is checked on the way in (the job's media id, exactly once).
+Dead-lettered jobs (``v1.download.dead``) end a run at once with an error
+naming the failed stage (the bench runs with ``max_retries=0``), instead of
+waiting out the timeout.  ``--variants R``: job ``i`` fetches payload
+variant ``i % R`` (:mod:`tritondl.fakes.payload`).
 ``--broker-pid`` names the broker process whose CPU time the reply reports
 (psutil), so a run can tell when the single-process fake broker, not the
 workers, is the bottleneck.
@@ -54,8 +58,11 @@ def _cpu_of(pid: int) -> float:
 
 
 class Producer:
-    def __init__(self, broker: str, origins: list[str], size: int, tag: str = "p", shards: int = 2) -> None:
+    def __init__(self, broker: str, origins: list[str], size: int, tag: str = "p", shards: int = 2,
+                 variants: int = 0) -> None:
         self.broker, self.origins, self.size, self.tag, self.shards = broker, origins, size, tag, shards
+        self.variants = variants
+        self.dead: list[str] = []
         self.conn: Connection | None = None
         self.n = 0
         self.seen: set[str] = set()
@@ -74,7 +81,19 @@ class Producer:
             await self.pch.queue_bind(f"v1.download-{i}", "v1.download", f"v1.download-{i}")
             await self.cch.queue_declare(f"v1.convert-{i}", durable=True)
             await self.cch.basic_consume(f"v1.convert-{i}", self._on_convert)
+        await self.cch.exchange_declare("v1.download.dead", "direct", durable=True)
+        for i in range(self.shards):
+            q = f"v1.download.dead-{i}"
+            await self.cch.queue_declare(q, durable=True)
+            await self.cch.queue_bind(q, "v1.download.dead", q)
+            await self.cch.basic_consume(q, self._on_dead)
         return self
+
+    def _on_dead(self, m) -> None:
+        h = m.properties.headers or {}
+        self.dead.append(f"{h.get('X-Failed-Stage', '?')}: {h.get('X-Error', '?')}")
+        asyncio.ensure_future(m.ack())
+        self._got.set()
 
     def _on_convert(self, m) -> None:
         c = Convert.decode(m.body)
@@ -90,7 +109,8 @@ class Producer:
     def job_body(self, i: int) -> tuple[str, bytes]:
         mid = f"bench-{self.tag}-{i}"
         origin = self.origins[i % len(self.origins)]
-        url = f"{origin}/synthetic/{self.size}/movie-{i}.mkv"
+        name = f"movie-{i}-v{i % self.variants}.mkv" if self.variants else f"movie-{i}.mkv"
+        url = f"{origin}/synthetic/{self.size}/{name}"
         d = Download(created_at="now", media=Media(id=mid, name=f"movie {i}", source=SourceType.HTTP,
                                                       source_uri=url))
         return mid, d.encode()
@@ -120,11 +140,15 @@ class Producer:
         self._got.clear()
         t0 = time.perf_counter()
         await self.submit(n)
-        if len(self.seen) < self._target:
+        deadline = time.monotonic() + timeout
+        while len(self.seen) < self._target and not self.dead:
+            self._got.clear()
             try:
-                await asyncio.wait_for(self._got.wait(), timeout)
+                await asyncio.wait_for(self._got.wait(), max(0.0, deadline - time.monotonic()))
             except asyncio.TimeoutError:
                 raise TimeoutError(f"only {len(self.seen) - base}/{n} converts") from None
+        if self.dead:
+            raise RuntimeError(f"{len(self.dead)} jobs dead-lettered, first: {self.dead[0]}")
         return time.perf_counter() - t0
 
     async def close(self) -> None:
@@ -133,7 +157,7 @@ class Producer:
 
 
 async def _amain(a: argparse.Namespace) -> None:
-    p = await Producer(a.broker, a.origins.split(","), a.size, a.tag).start()
+    p = await Producer(a.broker, a.origins.split(","), a.size, a.tag, variants=a.variants).start()
     loop = asyncio.get_running_loop()
     reader = asyncio.StreamReader()
     await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
@@ -167,6 +191,7 @@ def main() -> None:
     ap.add_argument("--size", type=int, required=True)
     ap.add_argument("--tag", default="p")
     ap.add_argument("--broker-pid", type=int, default=0)
+    ap.add_argument("--variants", type=int, default=0, help="payload variants (job i fetches i %% R)")
     asyncio.run(_amain(ap.parse_args()))
 
 

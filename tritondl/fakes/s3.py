@@ -12,7 +12,12 @@ native relay built, aws-chunked and unsigned PUT bodies are received (and
 every chunk signature verified) by ``_relay.recv_verify_chunked`` /
 ``_relay.recv_body`` outside the interpreter, as MinIO would on its own box.
 Fault injection: :meth:`fail_next` returns 5xx for the next N requests,
-:meth:`fail_for` for every request during an outage window.
+:meth:`fail_for` for every request during an outage window.  Content check
+(``expect``, a :class:`~tritondl.fakes.payload.Expectations`): a PUT of a
+synthetic payload variant whose bytes are not the origin's is refused with
+400 ``BadDigest`` — in discard mode too, from the leaf hashes the native
+chunk verifier already computed (``counts["content_ok"]`` /
+``["content_bad"]``).
 
 AWS behaviours the client must cope with (minio-go does): every bucket lives
 in a region (``create_bucket(name, region)``, or a ``LocationConstraint``);
@@ -50,6 +55,7 @@ class Obj:
     data: bytes | None = None
     path: str | None = None
     content_type: str = ""
+    leaves: bytes | None = None        # 64 KiB leaf SHA-256s when a content check needs them
 
 
 @dataclass
@@ -70,8 +76,10 @@ class FakeS3:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, *, access_key: str | None = None,
                  secret_key: str | None = None, region: str = "us-east-1", store: str = "memory",
                  root: str | None = None, tls: tuple[str, str] | None = None, strict_parts: bool = True,
-                 names: tuple[str, ...] = ()) -> None:
+                 names: tuple[str, ...] = (), expect=None) -> None:
         self.host, self.port = host, port
+        self.expect = expect           # payload.Expectations: check PUT content against the origin's
+        self.counts: dict[str, int] = {"content_ok": 0, "content_bad": 0}
         self.names = set(names)        # other names of the service endpoint (path-style, not a bucket)
         self.tls = tls
         self.strict_parts = strict_parts
@@ -207,7 +215,8 @@ class FakeS3:
             if relay is not None and request.body_length:
                 return await self._read_chunked_native(relay, request, auth, keep)
             return await self._read_chunked(request, auth, keep)
-        if relay is not None and not keep and phash in (sigv4.UNSIGNED_PAYLOAD, "") and request.body_length:
+        if relay is not None and not keep and self.expect is None and phash in (sigv4.UNSIGNED_PAYLOAD, "") \
+                and request.body_length:
             n = request.body_length
             stream, pre = request.take_body()
             got, _eof, err = await asyncio.get_running_loop().run_in_executor(
@@ -230,7 +239,7 @@ class FakeS3:
         decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
         raw_len = request.body_length
         stream, pre = request.take_body()
-        n, err, data = await asyncio.get_running_loop().run_in_executor(
+        n, err, data, leaves = await asyncio.get_running_loop().run_in_executor(
             None, relay.recv_verify_chunked, stream, raw_len, pre, key, amzdate, scope, seed, keep,
             self.verify_threads, 300.0)
         self.bytes_received += raw_len
@@ -244,7 +253,7 @@ class FakeS3:
             raise _BadReq(code, "SignatureDoesNotMatch" if code == 403 else "IncompleteBody", err)
         if decoded_len >= 0 and decoded_len != n:
             raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
-        return data if keep else _Sized(n)
+        return data if keep else _Sized(n, leaves)
 
     async def _read_chunked(self, request: web.Request, auth, keep: bool = True):
         """Decode an aws-chunked body and verify EVERY chunk signature while it
@@ -320,6 +329,25 @@ class FakeS3:
         if decoded_len >= 0 and decoded_len != len(data):
             raise _BadReq(400, "IncompleteBody", "decoded length mismatch")
         return data
+
+    async def _leaves(self, data) -> bytes | None:
+        """Leaf hashes of a received body (free from the native verifier,
+        else computed off the loop); None if unknown."""
+        if isinstance(data, _Sized):
+            return data.leaves or None
+        from .payload import leaf_hashes
+        return await asyncio.get_running_loop().run_in_executor(None, leaf_hashes, bytes(data))
+
+    def _content_check(self, key: str, size: int, leaves: bytes | None) -> None:
+        if self.expect is None:
+            return
+        want = self.expect.expected_for_key(key, size)
+        if want is None:
+            return
+        if leaves is None or hashlib.sha256(leaves).digest() != want:
+            self.counts["content_bad"] += 1
+            raise _BadReq(400, "BadDigest", f"content of {key} is not the origin's payload")
+        self.counts["content_ok"] += 1
 
     def _save(self, data: bytes, content_type: str = "") -> Obj:
         if self.store == "discard":
@@ -423,10 +451,14 @@ class FakeS3:
                 return _xml_err(400, "InvalidArgument", "Part number must be an integer between 1 and 10000")
             data = await self._read_body(request, auth, keep=self.store != "discard")
             o = self._save(data)
+            if self.expect is not None:
+                o.leaves = await self._leaves(data)
             up.parts[int(q["partNumber"])] = o
             return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
         if m == "PUT":
             data = await self._read_body(request, auth, keep=self.store != "discard")
+            if self.expect is not None:
+                self._content_check(key, len(data), await self._leaves(data))
             o = self._save(data, request.headers.get("Content-Type", ""))
             objs[key] = o
             return web.Response(status=200, headers={"ETag": f"\"{o.etag}\""})
@@ -452,6 +484,11 @@ class FakeS3:
                                       any(up.parts[n].size < (5 << 20) for n in nums[:-1])):
                 return _xml_err(400, "EntityTooSmall", "Your proposed upload is smaller than the minimum "
                                 "allowed object size.")
+            if self.expect is not None:
+                aligned = all(up.parts[n].size % (64 << 10) == 0 for n in nums[:-1])
+                parts_leaves = [up.parts[n].leaves for n in nums]
+                self._content_check(up.key, sum(up.parts[n].size for n in nums),
+                                    b"".join(parts_leaves) if aligned and all(parts_leaves) else None)
             if self.store == "memory":
                 data = b"".join(up.parts[n].data or b"" for n in nums)
                 o = self._save(data)
@@ -508,12 +545,14 @@ class FakeS3:
 
 
 class _Sized:
-    """Length-only stand-in for a verified body we chose not to keep."""
+    """Length-only stand-in for a verified body we chose not to keep (with
+    the 64 KiB leaf hashes of its content, when the verifier had them)."""
 
-    __slots__ = ("n",)
+    __slots__ = ("n", "leaves")
 
-    def __init__(self, n: int) -> None:
+    def __init__(self, n: int, leaves: bytes | None = None) -> None:
         self.n = n
+        self.leaves = leaves
 
     def __len__(self) -> int:
         return self.n

@@ -3,12 +3,16 @@ not the fakes competing for its event loop).
 
     python -m tritondl.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
                                    [--tls-cert PEM --tls-key PEM]   # origin / s3 over https
+                                   [--variants N --variant-size BYTES]  # per-job payloads
     python -m tritondl.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
 
 Prints ONE JSON line ``{"kind":..., "endpoint": ..., "url": ...}`` on stdout
 once listening, then serves until stdin closes or SIGTERM.  The origin also
 serves ``/synthetic/<bytes>/<name>``: deterministic pseudo-random content of
-the requested size (generated once per size, cached in memory).
+the requested size (generated once per size, cached in memory); a name with
+a variant (``movie-3-v7.mkv``) gets that variant's distinct payload, and an
+S3 started with ``--variants`` refuses PUTs of variants whose content is not
+the origin's (:mod:`tritondl.fakes.payload`).
 """
 
 from __future__ import annotations
@@ -20,36 +24,41 @@ import os
 import signal
 import sys
 
-import numpy as np
-
 from .broker import Broker
 from .origin import Blob, Origin
+from .payload import Expectations, synthetic_bytes, variant_bytes, variant_of
 from .s3 import FakeS3
 
-
-def synthetic_bytes(size: int, seed: int = 1234) -> bytes:
-    return np.random.default_rng(seed).integers(0, 256, size, dtype=np.uint8).tobytes()
+__all__ = ["SyntheticOrigin", "synthetic_bytes"]
 
 
 class SyntheticOrigin(Origin):
     def __init__(self, *a, **kw) -> None:
         super().__init__(*a, **kw)
-        self._cache: dict[int, Blob] = {}
+        self._cache: dict[tuple[int, int | None], Blob] = {}
+
+    def blob(self, size: int, variant: int | None) -> Blob:
+        b = self._cache.get((size, variant))
+        if b is None:
+            tag = f'"syn-{size}"' if variant is None else f'"syn-{size}-v{variant}"'
+            b = self._cache[(size, variant)] = Blob(variant_bytes(size, variant), etag=tag)
+        return b
+
+    def precompute(self, size: int, variants: int) -> None:
+        for k in range(variants):
+            self.blob(size, k)
 
     async def _handle(self, request):  # type: ignore[override]
         parts = request.path.split("/")
         if len(parts) >= 4 and parts[1] == "synthetic" and parts[2].isdigit():
-            size = int(parts[2])
-            blob = self._cache.get(size)
-            if blob is None:
-                blob = self._cache[size] = Blob(synthetic_bytes(size), etag=f'"syn-{size}"')
-            self.blobs[request.path] = blob
+            self.blobs[request.path] = self.blob(int(parts[2]), variant_of(parts[-1]))
         return await super()._handle(request)
 
 
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
                  seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow",
-                 tls_cert: str | None = None, tls_key: str | None = None, rate_mbps: float = 0.0) -> None:
+                 tls_cert: str | None = None, tls_key: str | None = None, rate_mbps: float = 0.0,
+                 variants: int = 0, variant_size: int = 0) -> None:
     tls = None
     if tls_cert and tls_key:
         with open(tls_cert) as f1, open(tls_key) as f2:
@@ -80,11 +89,18 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         srv = await Broker(port=port).start()
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.url}
     elif kind == "origin":
-        srv = await SyntheticOrigin(port=port, tls=tls).start()
+        srv = SyntheticOrigin(port=port, tls=tls)
+        if variants and variant_size:
+            srv.precompute(variant_size, variants)        # before serving: no job pays for it
+        await srv.start()
         info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}",
                 "url": f"{'https' if tls else 'http'}://{srv.host}:{srv.port}"}
     elif kind == "s3":
-        srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk, tls=tls).start()
+        expect = None
+        if variants and variant_size:
+            expect = Expectations(variant_size, variants)
+            expect.precompute()
+        srv = await FakeS3(port=port, store=s3_store, access_key=ak, secret_key=sk, tls=tls, expect=expect).start()
         if rate_mbps:
             srv.rate = rate_mbps * 1e6 / 8
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.endpoint}
@@ -115,6 +131,10 @@ def main() -> None:
     ap.add_argument("--tls-cert", default=None, help="origin/s3: serve https with this PEM certificate")
     ap.add_argument("--tls-key", default=None)
     ap.add_argument("--rate-mbps", type=float, default=0.0, help="s3: cap ingest at this many Mbit/s (shared link)")
+    ap.add_argument("--variants", type=int, default=0,
+                    help="origin: precompute this many payload variants; s3: refuse PUTs of variants whose "
+                         "content is not the origin's")
+    ap.add_argument("--variant-size", type=int, default=0, help="payload size the variants are precomputed for")
     a = ap.parse_args()
     prof_path = os.environ.get("TRITONDL_FAKE_PROFILE")          # "<path>.<kind>" gets a cProfile dump
     if prof_path:
@@ -123,13 +143,13 @@ def main() -> None:
         prof.enable()
         try:
             asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb,
-                               a.encryption, a.tls_cert, a.tls_key, a.rate_mbps))
+                               a.encryption, a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size))
         finally:
             prof.disable()
             prof.dump_stats(f"{prof_path}.{a.kind}")
         return
     asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption,
-                       a.tls_cert, a.tls_key, a.rate_mbps))
+                       a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size))
 
 
 if __name__ == "__main__":
