@@ -373,6 +373,14 @@ def main() -> int:
                                     "first": round(done[0].seconds * 1000, 2),
                                     "last": round(done[-1].seconds * 1000, 2)} if done else None),
                 "cpu_mhz_pinned": {"start": mhz0, "end": mhz1},
+                # jobs slower than 3x the median (and 10 ms): index in the timed run, ms, stage marks
+                "slow_jobs": ([{"i": i, "ms": round(r.seconds * 1000, 1),
+                                "marks": {k: round(v * 1000, 1) for k, v in r.marks.items()}}
+                               for i, r in enumerate(done)
+                               if r.seconds > max(0.010, 3 * lat[len(lat) // 2])][:8] if done else []),
+                "slow_jobs_total_ms": round(sum(r.seconds for r in done
+                                                if r.seconds > max(0.010, 3 * lat[len(lat) // 2])) * 1000, 1)
+                if done else 0.0,
                 # worker process (this rank), per timed job
                 "minflt_per_job": round((ru1.ru_minflt - ru0.ru_minflt) / n_div, 1),
                 "majflt_per_job": round((ru1.ru_majflt - ru0.ru_majflt) / n_div, 2),

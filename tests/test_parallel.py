@@ -186,3 +186,80 @@ def test_idle_first_order_shared_by_local_ranks(tmp_path, monkeypatch):
     o1, _ = t.shared_idle_order(1, 2, "tagA")
     assert o1 == o0
     assert t._cpu_ticks()                                          # /proc/stat parses here
+
+
+def _crashy(tmp_path):
+    (tmp_path / "crashy.py").write_text(
+        "import os, sys, time\n"
+        "if os.environ.get('CRASH') == '1':\n"
+        "    sys.exit(3)\n"
+        "time.sleep(120)\n")
+    return {"PYTHONPATH": str(tmp_path)}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _get(port, path="/healthz"):
+    r, w = await asyncio.open_connection("127.0.0.1", port)
+    w.write(f"GET {path} HTTP/1.0\r\nHost: x\r\n\r\n".encode())
+    data = await r.read()
+    w.close()
+    return int(data.split(b" ", 2)[1]), data.split(b"\r\n\r\n", 1)[1]
+
+
+def test_pool_health_goes_503_while_a_worker_is_given_up(tmp_path):
+    """VERDICT r03 Weak #4: a given-up worker must be visible, not silent."""
+    async def main():
+        port = _free_port()
+        pool = WorkerPool(plan(2, gpus=0, cpus=2), env=_crashy(tmp_path), cwd=str(tmp_path), module="crashy",
+                          worker_env=lambda r: {"CRASH": "1" if r == 1 else "0"}, max_restarts=1,
+                          backoff_initial=0.02, min_workers=1, health_addr=f"127.0.0.1:{port}", grace=5)
+        run = asyncio.ensure_future(pool.run_until_signalled())
+        for _ in range(200):
+            await asyncio.sleep(0.05)
+            if pool._health_runner is not None:
+                break
+        assert (await _get(port))[0] == 200 or pool.live < 2
+        t0 = time.monotonic()
+        while pool.live == 2:
+            assert time.monotonic() - t0 < 30
+            await asyncio.sleep(0.05)
+        code, body = await _get(port)
+        assert code == 503
+        code, metrics = await _get(port, "/metrics")
+        assert b"pool_workers_given_up 1" in metrics and b"pool_workers_live 1" in metrics
+        assert not run.done()                # one healthy worker left: min_workers=1 holds
+        os.kill(os.getpid(), signal.SIGTERM)  # the pool's own signal handler
+        assert await asyncio.wait_for(run, 30) == 0
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_pool_exits_nonzero_when_too_few_workers_are_left(tmp_path):
+    async def main():
+        pool = WorkerPool(plan(2, gpus=0, cpus=2), env=_crashy(tmp_path), cwd=str(tmp_path), module="crashy",
+                          worker_env=lambda r: {"CRASH": "1" if r == 1 else "0"}, max_restarts=1,
+                          backoff_initial=0.02, min_workers=2, grace=5)
+        rc = await asyncio.wait_for(pool.run_until_signalled(), 30)
+        assert rc == 1
+        assert not pool.pids()               # the healthy worker was stopped too
+        assert [rc for r, rc in pool.exits if r == 1] == [3, 3]
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_pool_cli_exits_nonzero_when_every_worker_crash_loops(tmp_path):
+    """``python -m tritondl.parallel``: all workers given up -> exit 1 (default --min-workers 1)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=ROOT, CRASH="1")
+    p = subprocess.run([sys.executable, "-m", "tritondl.parallel", "--workers", "2", "--max-restarts", "1",
+                        "--grace", "2", "--bogus-worker-flag"], cwd=str(tmp_path), env=env, timeout=60,
+                       capture_output=True)
+    assert p.returncode == 1, p.stderr.decode()[-2000:]
+    assert b"too few workers left" in p.stderr + p.stdout

@@ -38,13 +38,20 @@ class SyntheticOrigin(Origin):
         self._cache: dict[tuple[int, int | None], Blob] = {}
 
     def blob(self, size: int, variant: int | None) -> Blob:
+        """The payload as a memfd-backed blob: sendfile serves it, and the bytes
+        are held once (in the memfd), not also as a Python object."""
         b = self._cache.get((size, variant))
         if b is None:
             tag = f'"syn-{size}"' if variant is None else f'"syn-{size}-v{variant}"'
-            b = self._cache[(size, variant)] = Blob(variant_bytes(size, variant), etag=tag)
+            fd = Blob(variant_bytes(size, variant)).fd()
+            b = Blob(path=f"/proc/self/fd/{fd}", etag=tag)
+            b._fd = fd
+            self._cache[(size, variant)] = b
         return b
 
     def precompute(self, size: int, variants: int) -> None:
+        """Build every variant's memfd before serving: writing a 10 MiB memfd
+        on a job's first request cost that job ~2 ms (r04 fresh-lease run)."""
         for k in range(variants):
             self.blob(size, k)
 

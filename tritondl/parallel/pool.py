@@ -12,7 +12,13 @@ The supervisor:
   worker with exponential backoff; a worker that crash-loops
   (``max_restarts`` within ``restart_window``) is given up on;
 * on SIGTERM/SIGINT forwards SIGTERM to every worker, waits ``grace`` s,
-  then SIGKILLs stragglers — by PID, never by name.
+  then SIGKILLs stragglers — by PID, never by name;
+* fails loudly: once fewer than ``min_workers`` workers are left (default
+  1: every worker given up), it stops the rest and exits non-zero so the
+  orchestrator restarts the pod — the reference's ``log.Fatal`` exits
+  (``cmd/downloader/downloader.go:64,70,83,92,97``).  ``/healthz`` on
+  ``--health-addr`` answers 503 while any worker is given up, and
+  ``/metrics`` carries live / given-up / restart counts.
 """
 
 from __future__ import annotations
@@ -26,6 +32,7 @@ import time
 from dataclasses import dataclass, field
 
 from ..utils.log import log
+from ..utils.metrics import Metrics, serve_metrics
 from .topology import WorkerSpec, plan
 
 
@@ -42,7 +49,8 @@ class WorkerPool:
     def __init__(self, specs: list[WorkerSpec], *, argv: list[str] | None = None, env: dict | None = None,
                  max_restarts: int = 5, restart_window: float = 60.0, grace: float = 30.0,
                  backoff_initial: float = 0.5, backoff_max: float = 30.0, cwd: str | None = None,
-                 module: str = "tritondl", worker_env=None) -> None:
+                 module: str = "tritondl", worker_env=None, min_workers: int = 1,
+                 health_addr: str = "") -> None:
         """``worker_env(rank) -> dict``: extra env for one worker (e.g. its
         nearest S3 node)."""
         self.workers = [_Worker(s) for s in specs]
@@ -56,9 +64,27 @@ class WorkerPool:
         self.backoff_max = backoff_max
         self.cwd = cwd
         self.module = module
+        self.min_workers = max(0, min(min_workers, len(self.workers)))
+        self.health_addr = health_addr
+        self.metrics = Metrics()
         self._stopping = False
         self._tasks: list[asyncio.Task] = []
+        self._failed: asyncio.Event | None = None
+        self._health_runner = None
         self.exits: list[tuple[int, int | None]] = []   # (rank, returncode)
+
+    @property
+    def live(self) -> int:
+        """Workers not given up on (running, or waiting out a restart backoff)."""
+        return sum(1 for w in self.workers if not w.given_up)
+
+    @property
+    def healthy(self) -> bool:
+        return not any(w.given_up for w in self.workers) and not self._stopping
+
+    def _gauges(self) -> None:
+        self.metrics.set("pool_workers_live", self.live)
+        self.metrics.set("pool_workers_given_up", len(self.workers) - self.live)
 
     async def _spawn(self, w: _Worker) -> None:
         env = dict(os.environ)
@@ -88,15 +114,26 @@ class WorkerPool:
             if now - w.started_at > self.restart_window:
                 delay = self.backoff_initial  # it ran healthily for a while
             w.restarts = [t for t in w.restarts if now - t < self.restart_window] + [now]
+            self.metrics.inc("pool_worker_restarts", rank=str(w.spec.rank))
             if len(w.restarts) > self.max_restarts:
                 w.given_up = True
-                log.with_fields(rank=w.spec.rank, rc=rc).error("worker is crash-looping; giving up on it")
+                self._gauges()
+                log.with_fields(rank=w.spec.rank, rc=rc, live=self.live).error(
+                    "worker is crash-looping; giving up on it")
+                if self.live < self.min_workers and self._failed is not None:
+                    log.with_fields(live=self.live, min_workers=self.min_workers).error(
+                        "fatal: too few workers left; stopping the pool")
+                    self._failed.set()
                 return
             log.with_fields(rank=w.spec.rank, rc=rc, restart_in=round(delay, 2)).warn("worker died; restarting")
             await asyncio.sleep(delay)
             delay = min(delay * 2, self.backoff_max)
 
     async def start(self) -> None:
+        self._failed = asyncio.Event()
+        self._gauges()
+        if self.health_addr:
+            self._health_runner = await serve_metrics(self.metrics, self.health_addr, health=lambda: self.healthy)
         for w in self.workers:
             self._tasks.append(asyncio.ensure_future(self._watch(w)))
         # wait until every worker has a process
@@ -127,16 +164,28 @@ class WorkerPool:
         for t in self._tasks:
             with contextlib.suppress(BaseException):
                 await t
+        if self._health_runner is not None:
+            await self._health_runner.cleanup()
+            self._health_runner = None
 
-    async def run_until_signalled(self) -> None:
+    async def run_until_signalled(self) -> int:
+        """Run until a signal (returns 0) or until fewer than ``min_workers``
+        workers are left (returns 1: the process should exit non-zero)."""
         loop = asyncio.get_running_loop()
         stop = asyncio.Event()
         for s in (signal.SIGINT, signal.SIGTERM, signal.SIGHUP):
             with contextlib.suppress(NotImplementedError, RuntimeError):
                 loop.add_signal_handler(s, stop.set)
         await self.start()
-        await stop.wait()
+        assert self._failed is not None
+        sig = asyncio.ensure_future(stop.wait())
+        bad = asyncio.ensure_future(self._failed.wait())
+        await asyncio.wait({sig, bad}, return_when=asyncio.FIRST_COMPLETED)
+        failed = self._failed.is_set()
+        for t in (sig, bad):
+            t.cancel()
         await self.stop()
+        return 1 if failed else 0
 
 
 def main(argv: list[str] | None = None) -> int:
@@ -146,7 +195,13 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--workers", type=int, default=None, help="default: one per GPU (or per 2 CPUs)")
     ap.add_argument("--base-port", type=int, default=0, help="BitTorrent listen port of worker 0 (+rank)")
     ap.add_argument("--grace", type=float, default=30.0)
+    ap.add_argument("--min-workers", type=int, default=1,
+                    help="exit non-zero once fewer workers than this are left (crash-looping ones are given up)")
+    ap.add_argument("--health-addr", default="", help="host:port for the pool's /healthz and /metrics")
+    ap.add_argument("--max-restarts", type=int, default=5, help="restarts within --restart-window before giving up")
+    ap.add_argument("--restart-window", type=float, default=60.0)
     a, rest = ap.parse_known_args(argv)
-    pool = WorkerPool(plan(a.workers, base_port=a.base_port), argv=rest, grace=a.grace)
-    asyncio.run(pool.run_until_signalled())
-    return 0
+    pool = WorkerPool(plan(a.workers, base_port=a.base_port), argv=rest, grace=a.grace,
+                      min_workers=a.min_workers, health_addr=a.health_addr, max_restarts=a.max_restarts,
+                      restart_window=a.restart_window)
+    return asyncio.run(pool.run_until_signalled())
