@@ -497,3 +497,32 @@ def test_cancelled_fallback_download_writes_nothing_after_close(tmp_path, monkey
         await h.close()
         await o.stop()
     run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_chunked_overrides_a_bogus_content_length(tmp_path, native):
+    """RFC 9112 §6.3: with Transfer-Encoding chunked, Content-Length is
+    ignored.  A server sending both (and a CL smaller than the body) must not
+    truncate an open-ended download, and its connection is not reused.  (The
+    aiohttp fallback refuses such a response outright: an error, never a
+    silently short file.)"""
+    async def main():
+        o = await Origin().start()
+        o.chunked = True
+        o.chunked_content_length = 1000
+        data = os.urandom(1_234_567)
+        url = o.add("/live/both.mkv", data)
+        h = _dl(native=native, segments=4)
+        if not native:
+            with pytest.raises(HTTPDownloadError, match="Content-Length can't be present"):
+                await h.download(str(tmp_path), Sink(), url)
+            await h.close()
+            await o.stop()
+            return
+        await h.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "both.mkv").read_bytes() == data
+        if native:
+            assert sum(len(v) for v in h._raw.idle.values()) == 0         # ambiguous framing: not pooled
+        await h.close()
+        await o.stop()
+    run(main())

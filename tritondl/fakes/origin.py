@@ -69,6 +69,7 @@ class Origin:
         self.fail = 0
         self.chunked = False                    # GET bodies with Transfer-Encoding: chunked (no ranges)
         self.rate: float | None = None
+        self.chunked_content_length: int | None = None   # chunked responses also claim this length
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
         self.redirects: dict[str, tuple[int, str]] = {}     # path -> (status, Location)
@@ -174,6 +175,8 @@ class Origin:
         import random
         hdrs = {k: v for k, v in hdrs.items() if k != "Accept-Ranges"}
         hdrs["Transfer-Encoding"] = "chunked"
+        if self.chunked_content_length is not None:      # a broken server: both framings
+            hdrs["Content-Length"] = str(self.chunked_content_length)
         resp = web.StreamResponse(status=200, headers=hdrs)
         await resp.prepare(request)
         rng = random.Random(len(self.requests))

@@ -389,6 +389,8 @@ class HTTPDownloader:
 
     def _probe_from(self, r: aiohttp.ClientResponse, url: str) -> _Probe:
         size = r.headers.get("Content-Length")
+        if "chunked" in r.headers.get("Transfer-Encoding", "").lower():
+            size = None                 # RFC 9112 §6.3: chunked framing overrides Content-Length
         name = filename_from_disposition(r.headers.get("Content-Disposition")) or \
             filename_from_url(str(r.url)) or filename_from_url(url)
         if not name:

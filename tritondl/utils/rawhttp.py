@@ -108,6 +108,10 @@ class Head:
 
     @property
     def content_length(self) -> int | None:
+        """None when absent, malformed, or overridden by chunked
+        Transfer-Encoding (RFC 9112 §6.3: Content-Length is then ignored)."""
+        if self.chunked:
+            return None
         v = self.headers.get("Content-Length")
         try:
             return int(v) if v is not None else None
@@ -686,6 +690,8 @@ async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int 
             hdrs.add(k.strip(), v.strip())
     conn = hdrs.get("Connection", "").lower()
     keep = (ver == "HTTP/1.1" and conn != "close") or conn == "keep-alive"
+    if keep and "Content-Length" in hdrs and "chunked" in hdrs.get("Transfer-Encoding", "").lower():
+        keep = False            # ambiguous framing (RFC 9112 §6.3): never reuse this connection
     return Head(int(code), reason, hdrs, buf[i + 4:], ver, keep)
 
 
