@@ -350,3 +350,41 @@ def test_s3_put_with_gpu_chunk_hashing(tmp_path):
         await c.close()
         await s3.stop()
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+_TAIL_CHECK = r"""
+import hashlib, os, random, sys
+from tritondl.ops import hashing
+rng = random.Random(7)
+lengths = list(range(0, 201)) + [55, 56, 63, 64, 119, 120, 65535, 65536, 65537]
+bad = []
+for kind in ("sha1", "sha256"):
+    h = getattr(hashlib, kind)
+    for n in lengths:
+        msgs = [bytes(rng.getrandbits(8) for _ in range(n)) if n <= 256 else os.urandom(n) for _ in range(17)]
+        want = b"".join(h(m).digest() for m in msgs)
+        # 17 equal-length pieces in one buffer: a 16-lane group plus a straggler
+        if n and hashing.piece_hashes(b"".join(msgs), n, kind=kind) != want:
+            bad.append((kind, n, "piece_hashes"))
+        ok = hashing.verify_buffers(kind, msgs, want)
+        if ok != b"\x01" * 17:
+            bad.append((kind, n, "verify_buffers"))
+print("MB", hashing.sha_mb(), "BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.parametrize("mb", ["1", "0"])
+def test_multibuffer_sha_tail_padding(mb):
+    """the 16-lane AVX-512 SHA-1/SHA-256 kernels' tail padding —
+    messages shorter than a block, ``rem >= 56`` (two tail blocks) and 64 KiB
+    +-1 — against hashlib, with the kernels on and off (the switch is read
+    once per process, hence a subprocess per mode)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, TRITONDL_SHA_MB=mb)
+    p = subprocess.run([sys.executable, "-c", _TAIL_CHECK], env=env, capture_output=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert p.returncode == 0, (p.stdout + p.stderr).decode()[-2000:]
+    if mb == "0":
+        assert b"MB False" in p.stdout
