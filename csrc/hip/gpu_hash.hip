@@ -553,11 +553,12 @@ class DirectSource {
 // and the pinned staging slots are recycled as soon as their H2D completes.
 class GpuHasher {
  public:
-  GpuHasher(int device, size_t stage_bytes, int reader_threads, size_t window_bytes)
+  GpuHasher(int device, size_t stage_bytes, int reader_threads, size_t window_bytes, size_t max_hbm = 0)
       : device_(device),
         stage_req_(std::max<size_t>(stage_bytes, 1 << 20)),
         readers_(std::max(1, reader_threads)),
         window_req_(window_bytes),
+        max_hbm_(max_hbm ? max_hbm : kDefaultMaxHbm),
         pool_(new ReaderPool(std::max(1, reader_threads))) {
     HIP_CHECK(hipSetDevice(device_));
     HIP_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
@@ -583,7 +584,39 @@ class GpuHasher {
     hipStreamDestroy(compute_stream_);
   }
 
-  // Free cached staging / window memory.
+  // Free cached staging / window memory, from Python: waits for a running
+  // call (GIL released while waiting; the call's thread re-takes the GIL).
+  void release_py() {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(call_mu_);
+    hipSetDevice(device_);
+    release();
+  }
+
+  // The idle reaper: free everything if nothing ran for idle_s seconds and no
+  // call is running.  True if memory was freed.
+  bool release_if_idle(double idle_s) {
+    py::gil_scoped_release nogil;
+    std::unique_lock<std::mutex> g(call_mu_, std::try_to_lock);
+    if (!g.owns_lock() || held_bytes_locked() == 0) return false;
+    const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - last_use_).count();
+    if (idle < idle_s) return false;
+    hipSetDevice(device_);
+    release();
+    return true;
+  }
+
+  // (device bytes, pinned host bytes) held between calls.
+  std::pair<size_t, size_t> held_bytes() {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(call_mu_);
+    size_t dev = 0, host = 0;
+    held_split_locked(&dev, &host);
+    return {dev, host};
+  }
+  size_t max_hbm() const { return max_hbm_; }
+
+  // Free cached staging / window memory (caller holds call_mu_ or is the destructor).
   void release() {
     for (auto& st : stage_) {
       if (st.h) hipHostFree(st.h);
@@ -615,6 +648,7 @@ class GpuHasher {
     std::string out(n * dl, '\0');
     {
       py::gil_scoped_release nogil;
+      CallGuard cg(this);
       run_gpu_only(alg, piece_len, total, n, [&](uint8_t* dst, size_t off, size_t len, char*) {
         std::memcpy(dst, src + off, len);
       }, [&](size_t first, size_t count, const uint8_t* digests, const std::vector<char>&) {
@@ -652,6 +686,7 @@ class GpuHasher {
     digests.assign(n * dl, '\0');
     complete.assign(n, '\0');
     py::gil_scoped_release nogil;
+    CallGuard cg(this);
     try {
       DirectSource ds(spans);  // unmapped before the spans' fds close
       if (cpu_threads > 0) {
@@ -716,9 +751,12 @@ class GpuHasher {
   size_t window_bytes_for(size_t total, size_t piece_len) {
     size_t budget = window_req_;
     if (budget == 0) {
+      // two windows live at once: each gets half the cap (TRITONDL_GPU_MAX_HBM,
+      // default 8 GiB) and at most a third of free HBM, so a co-located ingest
+      // worker never takes a big share of a GPU that serves other workloads
       size_t free_b = 0, tot_b = 0;
       if (hipMemGetInfo(&free_b, &tot_b) != hipSuccess) free_b = 8ull << 30;
-      budget = std::min<size_t>(free_b / 3, 48ull << 30);  // two windows + headroom
+      budget = std::min<size_t>(free_b / 3, max_hbm_ / 2);
     }
     const size_t aligned = (total + piece_len - 1) / piece_len * piece_len;
     const size_t per = std::max<size_t>(1, budget / piece_len) * piece_len;
@@ -727,6 +765,28 @@ class GpuHasher {
 
  private:
   static constexpr int kStages = 4;
+  static constexpr size_t kDefaultMaxHbm = 8ull << 30;
+
+  // Serialises the public calls with the idle reaper (which frees the
+  // staging and windows those calls use) and stamps the last use.
+  struct CallGuard {
+    GpuHasher* h;
+    std::lock_guard<std::mutex> g;
+    explicit CallGuard(GpuHasher* x) : h(x), g(x->call_mu_) {}
+    ~CallGuard() { h->last_use_ = std::chrono::steady_clock::now(); }
+  };
+  void held_split_locked(size_t* dev, size_t* host) const {
+    for (const auto& st : stage_) *host += st.h ? st.cap : 0;
+    for (const auto& w : win_) {
+      *dev += (w.d ? w.cap : 0) + (w.d_out ? w.out_cap : 0);
+      *host += w.h_out ? w.out_cap : 0;
+    }
+  }
+  size_t held_bytes_locked() const {
+    size_t dev = 0, host = 0;
+    held_split_locked(&dev, &host);
+    return dev + host;
+  }
   struct Stage {
     uint8_t* h = nullptr;
     size_t cap = 0;
@@ -1018,15 +1078,23 @@ class GpuHasher {
     const double kernel_s = static_cast<double>(piece_len) / 55e6 + 1e-3;
     // page cache -> HBM: ~57 GB/s direct (registered mapping), ~36-45 GB/s through pinned staging
     const double kCopyBps = ds && ds->on() ? 55e9 : 40e9;
-    // pieces per CPU claim: >= 16 for the host's 16-lane AVX-512 kernels
-    // (pieces up to 1 MiB: a claim's buffer is 16 pieces per CPU thread),
-    // else >= 2 for SHA-NI pairs
+    // pieces per CPU claim: >= 16 for the host's 16-lane AVX-512 kernels, else
+    // >= 2 for SHA-NI pairs, and about 1 MiB of small pieces.  SHA-1 pieces
+    // that are whole 64 KiB multiples stream through the 16-lane kernel: each
+    // lane's next 64 KiB is read into a 1 MiB staging area that stays in the
+    // core's L2 (the host verifier's loop, hash_core.h verify_pieces), so a
+    // claim of 16 x 1 MiB pieces holds 1 MiB, not 16 MiB, and hashes from L2
+    // instead of DRAM.  Claims that cannot stream hold at most ~2 MiB.
+    constexpr size_t kStage = 64u << 10;
     const size_t wide = piece_len <= (1u << 20) ? tritondl_hash::md_claim(md) : 2;
-    const size_t unit = std::max<size_t>(wide, (1u << 20) / piece_len);
+    const bool stream16 = alg == 1 && wide == 16 && piece_len > kStage && piece_len % kStage == 0 &&
+                          tritondl_hash::sha16::cpu_has_avx512();
+    size_t unit = std::max<size_t>(wide, (1u << 20) / piece_len);
+    if (!stream16 && unit * piece_len > (2u << 20)) unit = std::max<size_t>(2, (2u << 20) / piece_len);
     std::exception_ptr cpu_err;
     auto cpu_worker = [&] {
       try {
-        std::vector<uint8_t> buf(unit * piece_len);
+        std::vector<uint8_t> buf(stream16 ? 16 * kStage : unit * piece_len);
         std::vector<char> ok(unit);
         for (;;) {
           size_t s, e;
@@ -1039,6 +1107,31 @@ class GpuHasher {
           }
           const long long ga = static_cast<long long>(s * piece_len);
           const long long ge = std::min(static_cast<long long>(total), static_cast<long long>(e * piece_len));
+          if (stream16 && e - s == 16 && ge == static_cast<long long>(e * piece_len)) {
+            const void* lane[16];
+            char lane_ok[16];
+            for (size_t j = 0; j < 16; ++j) {
+              lane[j] = buf.data() + j * kStage;
+              lane_ok[j] = 1;
+            }
+            tritondl_hash::sha16::Sha1x16 st;
+            tritondl_hash::sha16::sha1_x16_init(&st);
+            for (size_t off = 0; off < piece_len; off += kStage) {
+              for (size_t j = 0; j < 16; ++j) {
+                const long long a = static_cast<long long>((s + j) * piece_len + off);
+                if (lane_ok[j])  // a failed lane keeps hashing whatever is staged; its digest is discarded
+                  read_range(spans, buf.data() + j * kStage, a, a + static_cast<long long>(kStage), a, kStage, 1,
+                             &lane_ok[j]);
+              }
+              tritondl_hash::sha16::sha1_x16_update(&st, lane, kStage / 64);
+            }
+            unsigned char d[16 * 20];
+            tritondl_hash::sha16::sha1_x16_finish(&st, lane, piece_len, d);  // piece_len % 64 == 0: no tail
+            std::memcpy(&digests[s * dl], d, 16 * 20);
+            for (size_t j = 0; j < 16; ++j) complete[s + j] = lane_ok[j];
+            cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
+            continue;
+          }
           std::fill(ok.begin(), ok.end(), 1);
           read_range(spans, buf.data(), ga, ge, ga, piece_len, e - s, ok.data());
           for (size_t p = s; p < e; p += 16) {  // 16-lane AVX-512 groups, else SHA-NI pairs (md_batch)
@@ -1126,7 +1219,10 @@ class GpuHasher {
   size_t stage_req_;
   int readers_;
   size_t window_req_;
+  size_t max_hbm_;
   size_t last_window_ = 0;
+  std::mutex call_mu_;
+  std::chrono::steady_clock::time_point last_use_ = std::chrono::steady_clock::now();
   hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
   Stage stage_[kStages];
   Window win_[2];
@@ -1238,6 +1334,18 @@ TdlGpuChunkApi g_chunk_api{1, &sha256_chunks_impl};
 PYBIND11_MODULE(_gpu_hash, m) {
   m.doc() = "tritondl HIP (gfx950) batched SHA-1/SHA-256 piece hashing";
   m.def("device_count", &device_count);
+  m.def(
+      "mem_get_info",
+      [](int device) {
+        size_t free_b = 0, total_b = 0;
+        {
+          py::gil_scoped_release nogil;
+          HIP_CHECK(hipSetDevice(device));
+          HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        }
+        return py::make_tuple(free_b, total_b);
+      },
+      py::arg("device") = 0, "(free, total) HBM bytes of a device (hipMemGetInfo)");
   m.def("chunk_api", [](int device) {
           g_chunk_device.store(device);
           return py::capsule(&g_chunk_api, TDL_GPU_CHUNK_API_NAME);
@@ -1276,10 +1384,11 @@ PYBIND11_MODULE(_gpu_hash, m) {
       py::arg("stream") = 0, py::arg("lanes") = 64,
       "Launch on caller-owned device memory (e.g. torch tensors); out holds n*digest_len bytes.");
   py::class_<GpuHasher>(m, "GpuHasher")
-      .def(py::init<int, size_t, int, size_t>(), py::arg("device") = 0, py::arg("batch_bytes") = 256u << 20,
-           py::arg("reader_threads") = 8, py::arg("window_bytes") = 0,
-           "batch_bytes: pinned staging chunk; window_bytes: HBM window per kernel launch (0 = auto, "
-           "a third of free HBM capped at 48 GiB)")
+      .def(py::init<int, size_t, int, size_t, size_t>(), py::arg("device") = 0, py::arg("batch_bytes") = 256u << 20,
+           py::arg("reader_threads") = 8, py::arg("window_bytes") = 0, py::arg("max_hbm") = 0,
+           "batch_bytes: pinned staging chunk (allocated on first use); window_bytes: HBM window per kernel "
+           "launch (0 = auto: half of max_hbm, at most a third of free HBM); max_hbm: HBM the two windows "
+           "may hold (0 = 8 GiB)")
       .def("hash_buffer", &GpuHasher::hash_buffer, py::arg("kind"), py::arg("buffer"), py::arg("piece_len"))
       .def("verify_files", &GpuHasher::verify_files, py::arg("files"), py::arg("piece_len"), py::arg("expected"),
            py::arg("kind") = "sha1", py::arg("cpu_threads") = 0,
@@ -1294,7 +1403,12 @@ PYBIND11_MODULE(_gpu_hash, m) {
                              "pieces the GPU hashed in the last verify/digest call (the rest: CPU threads)")
       .def_property_readonly("last_direct_bytes", &GpuHasher::last_direct_bytes,
                              "bytes of the last verify/digest call DMA'd straight from the page cache")
-      .def("release", &GpuHasher::release)
+      .def("release", &GpuHasher::release_py, "free staging + windows now (waits for a running call)")
+      .def("release_if_idle", &GpuHasher::release_if_idle, py::arg("idle_s"),
+           "free staging + windows if no call ran for idle_s seconds and none is running; True if freed")
+      .def_property_readonly("held_bytes", &GpuHasher::held_bytes,
+                             "(device, pinned host) bytes held between calls")
+      .def_property_readonly("max_hbm", &GpuHasher::max_hbm)
       .def("window_bytes_for", &GpuHasher::window_bytes_for)
       .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)
       .def_property_readonly("batch_bytes", &GpuHasher::batch_bytes);

@@ -388,3 +388,29 @@ def test_fast_method_codecs_match_the_generic_path():
     # malformed hot-method payloads still raise the codec's FrameError
     with pytest.raises(cd.FrameError):
         cd.decode_method(bytes.fromhex("003c003c05"))
+
+
+def test_fake_broker_heartbeats_both_ways():
+    """The fake broker sends heartbeats on a silent connection and drops a
+    peer that stopped sending them (RabbitMQ), so idle heartbeating clients
+    survive and dead ones are detected on both ends."""
+    import asyncio as aio
+
+    from tritondl.amqp.connection import Connection
+    from tritondl.fakes.broker import Broker
+
+    async def main():
+        b = await Broker(heartbeat=1).start()
+        c = await Connection.open(b.url, heartbeat=1)
+        await aio.sleep(3.0)                               # idle: only heartbeats flow
+        assert not c.is_closed and len(b.conns) == 1
+        assert b.stats["heartbeats_sent"] >= 3
+        for t in list(c._tasks):                           # the client goes silent (a hung peer)
+            t.cancel()
+        for _ in range(60):
+            if not b.conns:
+                break
+            await aio.sleep(0.1)
+        assert not b.conns and b.stats["heartbeat_timeouts"] == 1
+        await b.stop()
+    aio.run(aio.wait_for(main(), 30))

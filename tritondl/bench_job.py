@@ -126,6 +126,8 @@ class JobStack:
     recycle_bytes: int = -1          # -1: worker default (Config); 0: delete every file
     variants: int = -1               # payload variants; -1: more than the spare pool can hold, 0: one payload
     content_check: bool = True       # S3 refuses PUTs whose content is not the origin's variant
+    heartbeat: int = 0               # AMQP heartbeat (s) the broker proposes and the worker uses (0: off)
+    overrides: dict = field(default_factory=dict)    # worker Config fields set before the service starts
     cfg: Config | None = None
     backends: list = field(default_factory=list)
     svc: Service | None = None
@@ -182,7 +184,7 @@ class JobStack:
                     tls = (f1.read(), f2.read())
                 out["ca_file"] = ca_file
             if broker:
-                b = await Broker().start()
+                b = await Broker(heartbeat=self.heartbeat).start()
                 self.backends.append(b)
                 out["broker"] = b.url
             from .fakes.payload import Expectations
@@ -202,7 +204,7 @@ class JobStack:
             tls_args = ["--tls-cert", cert_f, "--tls-key", key_f]
             out["ca_file"] = ca_file
         if broker:
-            bk = await Backend("broker").start()
+            bk = await Backend("broker", ["--heartbeat", str(self.heartbeat)] if self.heartbeat else []).start()
             self.backends.append(bk)
             out["broker"] = bk.info["url"]
             self.broker_pid = bk.proc.pid if bk.proc is not None else 0
@@ -234,7 +236,7 @@ class JobStack:
         cfg.retry_delay_s = 0.0
         cfg.max_retries = 0
         cfg.progress_log_interval_s = 0
-        cfg.heartbeat_s = 0
+        cfg.heartbeat_s = self.heartbeat
         cfg.ca_file = endpoints.get("ca_file", "")
         if self.http_probe_bytes >= 0:
             cfg.http_probe_bytes = self.http_probe_bytes
@@ -248,10 +250,12 @@ class JobStack:
             cfg.s3_multipart_threshold = self.s3_multipart_threshold
         if self.sign_threads > 0:
             cfg.s3_sign_threads = self.sign_threads
+        for k, v in self.overrides.items():
+            setattr(cfg, k, v)
         self.cfg = cfg
         mode = self.payload_mode or ("unsigned" if s3_url.startswith("https://") else "streaming")
         self.payload_mode = mode
-        amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=0, retry_delay=0)
+        amqp = Client(broker_url, prefetch=self.prefetch, heartbeat=self.heartbeat, retry_delay=0)
         up = Uploader(cfg.bucket, S3Client(s3_url, Static(AK, SK), payload_mode=mode,
                                            sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file,
                                            part_size=cfg.s3_part_size, multipart_threshold=cfg.s3_multipart_threshold,

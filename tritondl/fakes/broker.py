@@ -156,6 +156,10 @@ class _ServerConn:
         self.client_properties: dict = {}
         self.user = ""
         self.perms: Perms | None = None            # None: every resource allowed
+        self.hb = 0                                # negotiated heartbeat (s), from tune_ok
+        self.last_read = time.monotonic()
+        self.last_write = time.monotonic()
+        self.hb_task: asyncio.Task | None = None
         self._wbuf: list[bytes] = []
         self._flush_scheduled = False
 
@@ -174,6 +178,7 @@ class _ServerConn:
             self._wbuf.clear()
             if not self.writer.is_closing():
                 self.writer.write(data)
+                self.last_write = time.monotonic()
 
     def send_method(self, ch: int, m: Method) -> None:
         self.send(codec.method_frame(ch, m))
@@ -193,6 +198,7 @@ class _FrameProtocol(asyncio.Protocol):
     def data_received(self, data: bytes) -> None:
         if self.done.done():
             return
+        self.c.last_read = time.monotonic()
         try:
             ok = self.broker._frames(self.c, self.parser.feed(data))
         except codec.FrameError:
@@ -399,10 +405,34 @@ class Broker:
                 return False
         return True
 
+    async def _heartbeats(self, c: _ServerConn) -> None:
+        """RabbitMQ's side of heartbeats: a frame every hb/2 s of write
+        silence, and a connection with 2*hb s of read silence is dead."""
+        hb = c.hb
+        try:
+            while not c.closed:
+                await asyncio.sleep(hb / 2)
+                now = time.monotonic()
+                if now - c.last_write >= hb / 2:
+                    c.send(codec.HEARTBEAT_FRAME)
+                    self.stats["heartbeats_sent"] += 1
+                if now - c.last_read > 2 * hb:
+                    self.stats["heartbeat_timeouts"] += 1
+                    self._teardown(c)
+                    try:
+                        c.writer.transport.abort()
+                    except Exception:
+                        pass
+                    return
+        except asyncio.CancelledError:
+            pass
+
     def _teardown(self, c: _ServerConn) -> None:
         if c in self.conns:
             self.conns.discard(c)
         c.closed = True
+        if c.hb_task is not None and c.hb_task is not asyncio.current_task():
+            c.hb_task.cancel()
         for ch in list(c.channels.values()):
             self._close_channel(ch)
         c.channels.clear()
@@ -494,9 +524,12 @@ class Broker:
                                                         "heartbeat": self.heartbeat}))
         elif n == "connection.tune_ok":
             c.frame_max = m.frame_max or self.frame_max
+            c.hb = m.heartbeat or 0
         elif n == "connection.open":
             c.open = True
             c.send_method(0, Method("connection.open_ok"))
+            if c.hb > 0:
+                c.hb_task = asyncio.ensure_future(self._heartbeats(c))
             if self.blocked:
                 c.send_method(0, Method("connection.blocked", {"reason": "low on memory"}))
         elif n == "connection.close":

@@ -65,7 +65,7 @@ class SyntheticOrigin(Origin):
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
                  seed_path: str | None = None, piece_kb: int = 1024, encryption: str = "allow",
                  tls_cert: str | None = None, tls_key: str | None = None, rate_mbps: float = 0.0,
-                 variants: int = 0, variant_size: int = 0) -> None:
+                 variants: int = 0, variant_size: int = 0, heartbeat: int = 0) -> None:
     tls = None
     if tls_cert and tls_key:
         with open(tls_cert) as f1, open(tls_key) as f2:
@@ -93,7 +93,7 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         await srv.close()
         return
     if kind == "broker":
-        srv = await Broker(port=port).start()
+        srv = await Broker(port=port, heartbeat=heartbeat).start()
         info = {"kind": kind, "endpoint": srv.endpoint, "url": srv.url}
     elif kind == "origin":
         srv = SyntheticOrigin(port=port, tls=tls)
@@ -142,6 +142,7 @@ def main() -> None:
                     help="origin: precompute this many payload variants; s3: refuse PUTs of variants whose "
                          "content is not the origin's")
     ap.add_argument("--variant-size", type=int, default=0, help="payload size the variants are precomputed for")
+    ap.add_argument("--heartbeat", type=int, default=0, help="broker: heartbeat (s) proposed in connection.tune")
     a = ap.parse_args()
     prof_path = os.environ.get("TRITONDL_FAKE_PROFILE")          # "<path>.<kind>" gets a cProfile dump
     if prof_path:
@@ -150,13 +151,13 @@ def main() -> None:
         prof.enable()
         try:
             asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb,
-                               a.encryption, a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size))
+                               a.encryption, a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size, a.heartbeat))
         finally:
             prof.disable()
             prof.dump_stats(f"{prof_path}.{a.kind}")
         return
     asyncio.run(_amain(a.kind, a.port, a.s3_store, a.access_key, a.secret_key, a.path, a.piece_kb, a.encryption,
-                       a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size))
+                       a.tls_cert, a.tls_key, a.rate_mbps, a.variants, a.variant_size, a.heartbeat))
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@ so the idle CPU cores add throughput instead of waiting).
 from __future__ import annotations
 
 import os
+import sys
 import threading
 from typing import Sequence
 
@@ -80,18 +81,40 @@ _gpu_lock = threading.Lock()
 _gpu_hashers: dict[tuple, object] = {}
 
 
+def _torch_hip_runtime() -> str | None:
+    """Path of the HIP runtime torch ships (``torch/lib/libamdhip64.so``),
+    found without importing torch."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return p if os.path.exists(p) else None
+
+
 def _load_gpu():
     global _gpu_mod
     if _gpu_mod is None:
-        # One HIP runtime per process: torch ships its own libamdhip64.so.7 and
-        # loads it by a different file name, so it must be mapped FIRST; our
-        # extension's DT_NEEDED libamdhip64.so.7 then binds to that same copy.
-        # (Loaded the other way round, two HSA runtimes fight over the device
-        # and torch reports "No HIP GPUs are available".)
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7, loaded by path from torch/lib); if our extension
+        # were loaded first its DT_NEEDED would bind ROCm's copy, and a later
+        # ``import torch`` would bring up a second HSA runtime that fights over
+        # the device ("No HIP GPUs are available").  So map torch's runtime
+        # first — by dlopen, not by importing torch: the worker needs only the
+        # HIP runtime, and ``import torch`` cost ~1.2 GB of RSS and a 1-2 s GIL
+        # stall per worker (VERDICT r03).  The extension's DT_NEEDED then binds
+        # to the already-loaded SONAME.  Without torch installed, ROCm's own.
+        if "torch" not in sys.modules:
+            hip = _torch_hip_runtime()
+            if hip is not None:
+                import ctypes
+                try:
+                    ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+                except OSError:
+                    pass
         from .. import _gpu_hash  # type: ignore[attr-defined]
         _gpu_mod = _gpu_hash
     return _gpu_mod
@@ -124,32 +147,90 @@ def default_device() -> int:
     return int(want) % n if n > 0 else 0
 
 
+def _env_bytes(name: str, default: int) -> int:
+    """``123``, ``64M``, ``8G`` (binary units)."""
+    v = os.environ.get(name, "").strip().upper()
+    if not v:
+        return default
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30, "T": 1 << 40}.get(v[-1:], 1)
+    return int(float(v[:-1] if mult > 1 else v) * mult)
+
+
+GPU_MAX_HBM_DEFAULT = 8 << 30     # the two HBM windows together (TRITONDL_GPU_MAX_HBM)
+GPU_IDLE_S_DEFAULT = 30.0         # free windows + pinned staging after this long unused (TRITONDL_GPU_IDLE_S)
+
+
 def gpu_hasher(device: int | None = None, batch_bytes: int = 0, reader_threads: int = 0, window_bytes: int = 0):
     """Cached per-device :class:`GpuHasher`.  ``batch_bytes`` is the pinned
     staging slot, one of a ring of 4 (0: ``TRITONDL_GPU_STAGE_MB`` or 128 MiB); ``reader_threads``
     the pread threads filling it (0: ``TRITONDL_GPU_READERS`` or
     :data:`GPU_READERS`); ``window_bytes`` the HBM window hashed per kernel
-    launch (0 = auto: a third of free HBM, capped at 48 GiB)."""
+    launch (0 = auto: half of ``TRITONDL_GPU_MAX_HBM`` (default 8 GiB), at
+    most a third of free HBM).  Nothing is allocated until a call needs it,
+    and everything is freed again after ``TRITONDL_GPU_IDLE_S`` (default 30 s)
+    without a call: an idle ingest worker holds no HBM and no pinned memory."""
     device = default_device() if device is None else device
     batch_bytes = batch_bytes or (int(os.environ.get("TRITONDL_GPU_STAGE_MB", "128")) << 20)
     reader_threads = reader_threads or int(os.environ.get("TRITONDL_GPU_READERS", str(GPU_READERS)))
-    key = (device, max(batch_bytes, 1 << 20), window_bytes, reader_threads)
+    max_hbm = _env_bytes("TRITONDL_GPU_MAX_HBM", GPU_MAX_HBM_DEFAULT)
+    key = (device, max(batch_bytes, 1 << 20), window_bytes, reader_threads, max_hbm)
     with _gpu_lock:
         h = _gpu_hashers.get(key)
         if h is None:
-            h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads, window_bytes)
+            h = _load_gpu().GpuHasher(device, batch_bytes, reader_threads, window_bytes, max_hbm)
             h.trace = os.environ.get("TRITONDL_GPU_TRACE", "") == "1"
             _gpu_hashers[key] = h
+            _start_idle_reaper()
         return h
 
 
+_reaper: threading.Thread | None = None
+
+
+def gpu_idle_seconds() -> float:
+    return float(os.environ.get("TRITONDL_GPU_IDLE_S", GPU_IDLE_S_DEFAULT))
+
+
+def release_idle_gpu(idle_s: float | None = None) -> int:
+    """Free the buffers of every hasher unused for ``idle_s`` seconds; returns
+    how many were released (the idle reaper's one step; tests call it)."""
+    idle = gpu_idle_seconds() if idle_s is None else idle_s
+    with _gpu_lock:
+        hs = list(_gpu_hashers.values())
+    return sum(1 for h in hs if h.release_if_idle(idle))
+
+
+def _start_idle_reaper() -> None:
+    """One daemon thread per process (caller holds _gpu_lock)."""
+    global _reaper
+    if _reaper is not None:
+        return
+
+    def loop() -> None:
+        import time
+        while True:
+            idle = gpu_idle_seconds()                 # re-read: <= 0 turns the reaper off
+            time.sleep(max(0.05, min(5.0, idle / 3)) if idle > 0 else 5.0)
+            if idle <= 0:
+                continue
+            try:
+                release_idle_gpu(idle)
+            except Exception:  # noqa: BLE001 - never let the reaper die; the next step retries
+                pass
+    _reaper = threading.Thread(target=loop, name="tdl-gpu-idle", daemon=True)
+    _reaper.start()
+
+
 def warm_gpu(device: int | None = None) -> bool:
-    """Create the cached hasher and run one tiny batch (HIP context, code
-    object, pinned staging) so the first resume-verify of a job does not pay
-    the one-time setup.  Returns False when no GPU path is available."""
+    """Bring up the HIP context and load the code object (one tiny batch) so
+    the first resume-verify of a job does not pay the one-time setup, then
+    free the batch's buffers again: warm-up leaves no HBM or pinned memory
+    allocated.  Returns False when no GPU path is available."""
     if not gpu_available():
         return False
-    gpu_hasher(device).hash_buffer("sha1", b"\0" * 16384, 16384)
+    h = gpu_hasher(device)
+    h.hash_buffer("sha1", b"\0" * 16384, 16384)
+    h.release()
     return True
 
 

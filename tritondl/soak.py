@@ -32,9 +32,25 @@ Every ``sample_every`` finished jobs it records:
     python -m tritondl.soak --jobs 5000 --torrent-jobs 100 --fail-every 50 --sample-every 500 \\
         [--file-kb 10240] [--out soak.jsonl]
 
+A job-count soak finishes in seconds, so nothing timer-driven cycles in it.
+The time-based form runs for wall-clock minutes at a paced job rate:
+
+    python -m tritondl.soak --minutes 60 --rate 50 --file-kb 1024 --torrent-every 200 \\
+        --fail-every 100 --retry-delay 2 --heartbeat 10 --tls --dht-nodes 8 --out soak.jsonl
+
+so the worker's timers go round many times: AMQP heartbeats both ways (the
+fake broker sends them and drops a silent peer, as RabbitMQ does), the
+delay queues' TTLs (every failing job waits ``--retry-delay`` s in one per
+retry), TLS session reuse against https origin and S3, the DHT node's
+token-secret rotation (5 min) and bucket refresh (15 min) against a small
+local DHT of ``--dht-nodes`` nodes, and the metrics histograms.  Samples are
+taken every ``--sample-seconds`` (60) and add the DHT routing-table size and
+stored peers, cached TLS sessions and the number of metrics series.
+
 Each sample is one JSON line, and a final summary follows.  The summary
 gives the drift of every series after warm-up: the last sample against the
-first sample taken after ``warmup`` jobs.
+first sample taken after ``warmup`` jobs (``--warmup-minutes`` in the time
+form).
 """
 
 from __future__ import annotations
@@ -55,119 +71,195 @@ from .models import Download, Media, SourceType
 from .utils import rawhttp
 
 
+def _torrent_impl(svc):
+    for impl in getattr(svc.dispatcher, "impls", []) or []:
+        if hasattr(impl, "_dht"):
+            return impl
+    return None
+
+
 def sample(svc) -> dict:
     """One resource sample of this process."""
     import psutil
     p = psutil.Process()
     relay = rawhttp.relay_module()
     pool = relay.pool_threads() if relay is not None and hasattr(relay, "pool_threads") else None
-    return {"jobs": svc.jobs_finished, "t": round(time.monotonic(), 3), "rss_mb": round(p.memory_info().rss / 2**20, 1),
-            "fds": len(os.listdir("/proc/self/fd")), "os_threads": len(os.listdir("/proc/self/task")),
-            "py_threads": threading.active_count(), "tasks": len(asyncio.all_tasks()),
-            "pool_threads": pool, "pumps": rawhttp.active_pumps()}
+    out = {"jobs": svc.jobs_finished, "t": round(time.monotonic(), 3), "rss_mb": round(p.memory_info().rss / 2**20, 1),
+           "fds": len(os.listdir("/proc/self/fd")), "os_threads": len(os.listdir("/proc/self/task")),
+           "py_threads": threading.active_count(), "tasks": len(asyncio.all_tasks()),
+           "pool_threads": pool, "pumps": rawhttp.active_pumps()}
+    m = svc.metrics
+    out["metrics_series"] = len(m.counters) + len(m.gauges) + len(m.hists)
+    tls = [c.cached_sessions for c in rawhttp._client_tls.values() if c is not None]
+    out["tls_sessions"] = sum(tls) if tls else None
+    bt = _torrent_impl(svc)
+    dht = getattr(bt, "_dht", None) if bt is not None else None
+    if dht is not None:
+        out["dht_nodes"] = sum(len(t) for t in dht.tables.values())
+        out["dht_peer_keys"] = len(dht.peers)
+    return out
 
 
-def drift(samples: list[dict], warmup: int) -> dict:
-    """Change of every series from the first post-warm-up sample to the last."""
-    after = [s for s in samples if s["jobs"] >= warmup]
+SERIES = ("rss_mb", "fds", "os_threads", "py_threads", "tasks", "pool_threads", "metrics_series", "tls_sessions",
+          "dht_nodes", "dht_peer_keys")
+
+
+def drift(samples: list[dict], warmup: int, key: str = "jobs") -> dict:
+    """Change of every series from the first post-warm-up sample to the last
+    (``key``: "jobs", or "minute" for time-based soaks)."""
+    after = [s for s in samples if s.get(key, 0) >= warmup]
     if len(after) < 2:
         return {}
     a, b = after[0], after[-1]
     out = {}
-    for k in ("rss_mb", "fds", "os_threads", "py_threads", "tasks", "pool_threads"):
+    for k in SERIES:
         if a.get(k) is None or b.get(k) is None:
             continue
-        out[k] = {"from": a[k], "to": b[k], "max": max(s[k] for s in after)}
+        out[k] = {"from": a[k], "to": b[k], "max": max(s[k] for s in after if s.get(k) is not None)}
     out["rss_drift_pct"] = round(100 * (b["rss_mb"] - a["rss_mb"]) / max(a["rss_mb"], 1e-9), 2)
     return out
 
 
+async def _local_dht(n: int) -> list:
+    """``n`` DHT nodes on 127.0.0.1 that know each other: the worker's node
+    bootstraps off them, so its table fills and its maintenance has peers."""
+    from .fetch.bt.dht import DHTNode
+    nodes = []
+    for _ in range(n):
+        boot = [("127.0.0.1", x.port) for x in nodes[-3:]]
+        nodes.append(await DHTNode(host="127.0.0.1", bootstrap=boot, timeout=1.0).start(maintain=True))
+    for x in nodes:
+        await x.bootstrap()
+    return nodes
+
+
 async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample_every: int = 500,
                    file_size: int = 10 << 20, torrent_mb: int = 8, max_retries: int = 2, warmup: int = 0,
-                   on_sample=None, workdir: str | None = None) -> dict:
-    st = JobStack(file_size=file_size, tag="soak", workdir=workdir)
+                   on_sample=None, workdir: str | None = None, *, minutes: float = 0.0, rate: float = 0.0,
+                   sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
+                   torrent_every: int = 0, dht_nodes: int = 0) -> dict:
+    """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
+    ``rate`` jobs/s (0: as fast as the worker goes)."""
+    timed = minutes > 0
+    st = JobStack(file_size=file_size, tag="soak", workdir=workdir, tls=tls, heartbeat=heartbeat,
+                  content_check=True)
     seed = None
     conn = None
+    dht = []
     try:
         ends = await st.start_backends(broker=True)
+        if dht_nodes:
+            dht = await _local_dht(dht_nodes)
+            st.overrides.update(bt_bootstrap=",".join(f"127.0.0.1:{x.port}" for x in dht), bt_dht=True,
+                                bt_dht_ipv6=False)
         await st.setup(ends, producer=False)
         svc = st.svc
         assert svc is not None and st.cfg is not None
         st.cfg.max_retries = max_retries
+        st.cfg.retry_delay_s = retry_delay
+        st.cfg.retry_backoff = 1.0
         magnet = ""
-        if torrent_jobs:
+        if torrent_jobs or torrent_every:
             from .fakes.swarm import make_payload
             src = os.path.join(st.workdir or "/tmp", "seed", "Show.S01")
             make_payload(src, {"season 1/e1.mkv": (torrent_mb << 20) // 2, "season 1/e2.mkv": (torrent_mb << 20) // 2,
                                "info.nfo": 100})
             seed = await Backend("seed", ["--path", src, "--piece-kb", "256"]).start()
             magnet = f"magnet:?xt=urn:btih:{seed.info['infohash']}&dn=Show.S01&x.pe={seed.info['endpoint']}"
-        conn = await Connection.open(ends["broker"], heartbeat=0)
+        conn = await Connection.open(ends["broker"], heartbeat=heartbeat)
         ch = await conn.channel()
         await ch.confirm_select()
         origin = ends["origin"]
-        # job kinds, interleaved evenly
-        kinds: list[str] = []
-        tor_every = max(1, jobs // torrent_jobs) if torrent_jobs else 0
-        for i in range(jobs):
+        tor_every = torrent_every or (max(1, jobs // torrent_jobs) if torrent_jobs else 0)
+        n_tor = [0]
+
+        def kind(i: int) -> str:
             if fail_every and i % fail_every == fail_every - 1:
-                kinds.append("fail")
-            elif tor_every and i % tor_every == tor_every // 2 and kinds.count("torrent") < torrent_jobs:
-                kinds.append("torrent")
-            else:
-                kinds.append("http")
-        n_fail = kinds.count("fail")
-        expect = jobs + n_fail * max_retries        # every failing job is attempted 1 + max_retries times
+                return "fail"
+            if tor_every and i % tor_every == tor_every // 2 and (timed or n_tor[0] < torrent_jobs):
+                n_tor[0] += 1
+                return "torrent"
+            return "http"
+        kinds: list[str] = []
         samples: list[dict] = []
         base = svc.jobs_finished
         next_sample = base
         t0 = time.monotonic()
+        next_t = t0
+        end_t = t0 + minutes * 60 if timed else float("inf")
         window = 8                                  # jobs in flight in the broker ahead of the worker
 
         async def publish(i: int) -> None:
-            k = kinds[i]
+            k = kind(i)
+            kinds.append(k)
             mid = f"soak-{i}"
             if k == "torrent":
                 uri, src = magnet, SourceType.TORRENT
             elif k == "fail":
                 uri, src = f"{origin}/missing/{i}.mkv", SourceType.HTTP
             else:
-                uri, src = f"{origin}/synthetic/{file_size}/movie-{i}.mkv", SourceType.HTTP
+                uri, src = f"{origin}/synthetic/{file_size}/{st.job_name(i)}", SourceType.HTTP
             body = Download(created_at="now", media=Media(id=mid, name=mid, source=src, source_uri=uri)).encode()
             await ch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
                                    Properties(delivery_mode=2, content_type="application/octet-stream"))
 
+        def take_sample() -> None:
+            gc.collect()
+            s = sample(svc)
+            s["jobs"] = svc.jobs_finished - base
+            s["minute"] = round((time.monotonic() - t0) / 60, 2)
+            samples.append(s)
+            if on_sample is not None:
+                on_sample(s)
+
+        def expected() -> int:                      # every failing job is attempted 1 + max_retries times
+            return len(kinds) + kinds.count("fail") * max_retries
+
         sent = 0
-        while svc.jobs_finished - base < expect:
-            while sent < jobs and sent - (svc.jobs_finished - base) < window:
+        while True:
+            now = time.monotonic()
+            more = (now < end_t) if timed else (sent < jobs)
+            if not more and svc.jobs_finished - base >= expected():
+                break
+            while more and sent - (svc.jobs_finished - base) < window and (not rate or now >= next_t):
                 await publish(sent)
                 sent += 1
-            await svc.wait_finished(svc.jobs_finished + 1, timeout=120)
-            if svc.jobs_finished >= next_sample:
-                gc.collect()
-                s = sample(svc)
-                s["jobs"] = svc.jobs_finished - base
-                samples.append(s)
-                if on_sample is not None:
-                    on_sample(s)
+                next_t += 1.0 / rate if rate else 0.0
+                now = time.monotonic()
+                more = (now < end_t) if timed else (sent < jobs)
+            wait = 1.0 if not more else max(0.0, min(1.0, next_t - time.monotonic())) if rate else None
+            try:
+                await svc.wait_finished(svc.jobs_finished + 1, timeout=wait if wait else 120)
+            except TimeoutError:
+                if not timed and not rate:
+                    raise
+            if timed:
+                if time.monotonic() - t0 >= len(samples) * sample_seconds:
+                    take_sample()
+            elif svc.jobs_finished >= next_sample:
+                take_sample()
                 next_sample += sample_every
         dt = time.monotonic() - t0
         res = svc.results
-        ok = sum(1 for r in res[-min(len(res), expect):] if r.ok)
+        n_att = svc.jobs_finished - base
+        ok = sum(1 for r in res[-min(len(res), n_att):] if r.ok)
         await asyncio.sleep(0.2)
-        s = sample(svc)
-        s["jobs"] = svc.jobs_finished - base
-        samples.append(s)
-        if on_sample is not None:
-            on_sample(s)
-        return {"jobs": jobs, "torrent_jobs": kinds.count("torrent"), "failing_jobs": n_fail,
-                "attempts": svc.jobs_finished - base, "ok_attempts": ok, "seconds": round(dt, 2),
-                "jobs_per_sec": round(jobs / dt, 1), "samples": samples, "drift": drift(samples, warmup)}
+        take_sample()
+        summary = {"jobs": len(kinds), "torrent_jobs": kinds.count("torrent"), "failing_jobs": kinds.count("fail"),
+                   "attempts": n_att, "ok_attempts": ok, "seconds": round(dt, 2),
+                   "jobs_per_sec": round(len(kinds) / dt, 1), "samples": samples,
+                   "drift": drift(samples, warmup, "minute" if timed else "jobs")}
+        if timed:
+            summary.update(minutes=minutes, rate=rate, tls=tls, heartbeat=heartbeat, retry_delay=retry_delay,
+                           dht_nodes=dht_nodes, reconnects=svc.amqp.reconnects if svc.amqp is not None else None)
+        return summary
     finally:
         if conn is not None:
             await conn.close()
         if seed is not None:
             await seed.stop()
+        for x in dht:
+            x.stop()
         await st.teardown()
 
 
@@ -183,6 +275,15 @@ def main() -> int:
     ap.add_argument("--out", default="")
     ap.add_argument("--cpus", default="", help="pin the worker like TRITONDL_CPUS (cpulist or auto); the fakes "
                                                "go to the next L3 domain with auto")
+    ap.add_argument("--minutes", type=float, default=0.0, help="wall-clock soak of this many minutes (0: --jobs)")
+    ap.add_argument("--rate", type=float, default=0.0, help="jobs/s to publish (0: as fast as the worker takes them)")
+    ap.add_argument("--sample-seconds", type=float, default=60.0)
+    ap.add_argument("--warmup-minutes", type=float, default=5.0)
+    ap.add_argument("--torrent-every", type=int, default=0, help="time form: every Nth job is a magnet job")
+    ap.add_argument("--retry-delay", type=float, default=0.0, help="seconds each failing job waits in a delay queue")
+    ap.add_argument("--heartbeat", type=int, default=0, help="AMQP heartbeat (s), broker and worker")
+    ap.add_argument("--tls", action="store_true", help="origin and S3 over https")
+    ap.add_argument("--dht-nodes", type=int, default=0, help="local DHT nodes the worker bootstraps from")
     a = ap.parse_args()
     if a.cpus:
         from .parallel import topology
@@ -202,7 +303,10 @@ def main() -> int:
             fh.flush()
     try:
         res = asyncio.run(run_soak(a.jobs, a.torrent_jobs, a.fail_every, a.sample_every, a.file_kb << 10,
-                                   a.torrent_mb, warmup=a.warmup, on_sample=emit))
+                                   a.torrent_mb, warmup=(a.warmup_minutes if a.minutes else a.warmup),
+                                   on_sample=emit, minutes=a.minutes, rate=a.rate, sample_seconds=a.sample_seconds,
+                                   tls=a.tls, heartbeat=a.heartbeat, retry_delay=a.retry_delay,
+                                   torrent_every=a.torrent_every, dht_nodes=a.dht_nodes))
     finally:
         if fh is not None:
             fh.close()
