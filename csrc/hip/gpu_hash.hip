@@ -1094,8 +1094,11 @@ class GpuHasher {
     std::exception_ptr cpu_err;
     auto cpu_worker = [&] {
       try {
-        std::vector<uint8_t> buf(stream16 ? 16 * kStage : unit * piece_len);
-        std::vector<char> ok(unit);
+        // stream16: the 1 MiB staging area, or two whole pieces for a short
+        // claim (the layout's tail); otherwise the whole claim
+        std::vector<uint8_t> buf(stream16 ? std::max<size_t>(16 * kStage, 2 * piece_len) : unit * piece_len);
+        const size_t cap_pieces = std::max<size_t>(1, buf.size() / piece_len);
+        std::vector<char> ok(cap_pieces);
         for (;;) {
           size_t s, e;
           {
@@ -1132,19 +1135,25 @@ class GpuHasher {
             cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
             continue;
           }
-          std::fill(ok.begin(), ok.end(), 1);
-          read_range(spans, buf.data(), ga, ge, ga, piece_len, e - s, ok.data());
-          for (size_t p = s; p < e; p += 16) {  // 16-lane AVX-512 groups, else SHA-NI pairs (md_batch)
-            const size_t cnt = std::min<size_t>(16, e - p);
-            const void* src[16];
-            size_t len[16];
-            for (size_t j = 0; j < cnt; ++j) {
-              const size_t po = (p + j - s) * piece_len;
-              src[j] = buf.data() + po;
-              len[j] = std::min<size_t>(piece_len, static_cast<size_t>(ge - ga) - po);
+          // whole pieces, as many at a time as the buffer holds
+          for (size_t q = s; q < e; q += cap_pieces) {
+            const size_t qe = std::min(e, q + cap_pieces);
+            const long long qa = static_cast<long long>(q * piece_len);
+            const long long qz = std::min(static_cast<long long>(total), static_cast<long long>(qe * piece_len));
+            std::fill(ok.begin(), ok.end(), 1);
+            read_range(spans, buf.data(), qa, qz, qa, piece_len, qe - q, ok.data());
+            for (size_t p = q; p < qe; p += 16) {  // 16-lane AVX-512 groups, else SHA-NI pairs (md_batch)
+              const size_t cnt = std::min<size_t>(16, qe - p);
+              const void* src[16];
+              size_t len[16];
+              for (size_t j = 0; j < cnt; ++j) {
+                const size_t po = (p + j - q) * piece_len;
+                src[j] = buf.data() + po;
+                len[j] = std::min<size_t>(piece_len, static_cast<size_t>(qz - qa) - po);
+              }
+              tritondl_hash::md_batch(md, src, len, cnt, reinterpret_cast<unsigned char*>(&digests[p * dl]));
+              for (size_t j = 0; j < cnt; ++j) complete[p + j] = ok[p + j - q];
             }
-            tritondl_hash::md_batch(md, src, len, cnt, reinterpret_cast<unsigned char*>(&digests[p * dl]));
-            for (size_t j = 0; j < cnt; ++j) complete[p + j] = ok[p + j - s];
           }
           cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
         }
