@@ -1,0 +1,103 @@
+"""The GPU verification helper process (ops/gpu_helper.py): the worker
+never brings up HIP itself; a helper does, and exits when idle.  These CPU
+tests drive the protocol with the helper's host stand-in
+(``TRITONDL_GPU_HELPER_FAKE=1``); the HIP helper is covered by the GPU
+tests (tests/test_hashing.py)."""
+
+import os
+import time
+
+import pytest
+
+from tritondl.ops import gpu_helper, hashing
+
+
+@pytest.fixture
+def fake_helper(monkeypatch):
+    monkeypatch.setenv("TRITONDL_GPU_HELPER_FAKE", "1")
+    monkeypatch.setenv("TRITONDL_GPU_IDLE_S", "30")
+    h = gpu_helper.GpuHelper()
+    yield h
+    h.close()
+
+
+def _layout(tmp_path, sizes, piece_len):
+    data = os.urandom(sum(sizes))
+    files, off = [], 0
+    for i, n in enumerate(sizes):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(data[off:off + n])
+        files.append((str(p), n))
+        off += n
+    exp = hashing.piece_hashes(data, piece_len, "sha1")
+    return files, data, exp
+
+
+def test_helper_verifies_and_reports(tmp_path, fake_helper):
+    files, data, exp = _layout(tmp_path, [100_000, 5, 70_000], 16384)
+    n = len(exp) // 20
+    assert fake_helper.verify_files(files, 16384, exp) == b"\x01" * n
+    pid = fake_helper.pid
+    assert pid and pid != os.getpid() and fake_helper.spawned == 1
+    with open(files[0][0], "r+b") as f:
+        f.seek(40_000)
+        f.write(b"\x00\xff")
+    ok = fake_helper.verify_files(files, 16384, exp)
+    assert [i for i, v in enumerate(ok) if not v] == [40_000 // 16384]
+    assert fake_helper.hash_buffer("sha256", data, 65536) == hashing.piece_hashes(data, 65536, "sha256")
+    d, complete = fake_helper.digest_files(files, 16384, "sha256")
+    assert len(d) == 32 * len(complete) and fake_helper.pid == pid       # one process served everything
+
+
+def test_helper_exits_idle_and_comes_back(tmp_path, fake_helper, monkeypatch):
+    monkeypatch.setenv("TRITONDL_GPU_IDLE_S", "0.5")
+    files, _data, exp = _layout(tmp_path, [50_000], 16384)
+    assert fake_helper.verify_files(files, 16384, exp) == b"\x01" * 4
+    assert fake_helper.wait_exit(10)                  # idle: gone, with everything it held
+    assert fake_helper.pid is None
+    assert fake_helper.verify_files(files, 16384, exp) == b"\x01" * 4
+    assert fake_helper.spawned == 2
+
+
+def test_helper_exiting_as_a_request_arrives_is_retried(tmp_path, fake_helper, monkeypatch):
+    """The idle exit can race a request: a clean exit (rc 0) gets one respawn."""
+    monkeypatch.setenv("TRITONDL_GPU_IDLE_S", "0.3")
+    files, _data, exp = _layout(tmp_path, [20_000], 16384)
+    for _ in range(6):
+        assert fake_helper.verify_files(files, 16384, exp) == b"\x01\x01"
+        time.sleep(0.3)
+
+
+def test_helper_crash_fails_the_call_loudly(tmp_path, fake_helper):
+    files, _data, exp = _layout(tmp_path, [20_000], 16384)
+    assert fake_helper.ping()
+    os.kill(fake_helper.pid, 9)
+    time.sleep(0.1)
+    # the next call starts a new helper (the old one is reaped, not waited on forever)
+    assert fake_helper.verify_files(files, 16384, exp) == b"\x01\x01"
+    with pytest.raises(gpu_helper.HelperError, match="unknown op"):
+        fake_helper._call({"op": "nope"})
+    assert fake_helper.ping()                          # a bad request does not kill it
+
+
+def test_helper_that_cannot_start_says_why(monkeypatch):
+    monkeypatch.delenv("TRITONDL_GPU_HELPER_FAKE", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")      # no device in the helper
+    h = gpu_helper.GpuHelper(start_timeout=60)
+    with pytest.raises(gpu_helper.HelperError, match="failed to start"):
+        h.ping()
+
+
+def test_worker_side_never_loads_hip(monkeypatch):
+    """gpu_available() in helper mode reads the KFD topology; it does not
+    import the HIP extension into the worker."""
+    import subprocess
+    import sys
+    code = ("import sys\n"
+            "from tritondl.ops import hashing\n"
+            "hashing.gpu_available(); hashing.choose_device(1000, 1 << 20, 1 << 30)\n"
+            "print('LOADED', 'tritondl._gpu_hash' in sys.modules, 'torch' in sys.modules)\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=60,
+                       cwd=gpu_helper.ROOT, env={k: v for k, v in os.environ.items() if k != "TRITONDL_GPU_HELPER"})
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    assert b"LOADED False False" in p.stdout

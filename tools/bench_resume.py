@@ -84,7 +84,7 @@ async def main() -> int:
                 for suffix in ("", "-wal", "-shm"):
                     if os.path.exists(db + suffix):
                         os.remove(db + suffix)
-                if a.trace and dev in ("gpu", "hybrid"):
+                if a.trace and dev in ("gpu", "hybrid") and not hashing.helper_mode():
                     hashing.gpu_hasher().trace = True
                 d = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device=dev), use_dht=False,
                                       progress_interval=1.0)
@@ -94,12 +94,12 @@ async def main() -> int:
                 dt = time.perf_counter() - t0
                 extra = {"verify_s": round(spent["verify_s"], 3)}
                 if dev in ("gpu", "hybrid", "auto") and hashing.gpu_available():
-                    h = hashing.gpu_hasher()
+                    h = hashing.gpu_backend()           # the helper process's hasher by default
                     if dev != "gpu":
                         extra["gpu_share"] = round(h.last_gpu_pieces / max(1, info.num_pieces if info.pieces
                                                                             else -(-info.total_length // 16384)), 3)
                     extra["direct_share"] = round(h.last_direct_bytes / max(1, info.total_length), 3)
-                    if h.trace:
+                    if getattr(h, "trace", False):
                         extra["gpu_timeline"] = hashing.timeline_summary(h.last_timeline)
                 print(json.dumps({"metric": "resume_job_seconds", "device": dev, "run": "cold" if rep == 0 else "warm",
                                   "value": round(dt, 3), "GBps": round(info.total_length / dt / 1e9, 1),

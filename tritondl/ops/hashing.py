@@ -125,13 +125,72 @@ def gpu_module():
     return _load_gpu()
 
 
+def helper_mode() -> bool:
+    """GPU verification runs in a helper process (``ops/gpu_helper.py``) so
+    the worker never brings up HIP (~850 MB of RSS it could not give back);
+    ``TRITONDL_GPU_HELPER=0`` runs it in-process.  The helper itself, tests
+    and benches that call :func:`gpu_hasher` directly are in-process."""
+    from .gpu_helper import CHILD_ENV
+    return os.environ.get("TRITONDL_GPU_HELPER", "1")[:1] not in ("0", "n", "o") and \
+        os.environ.get(CHILD_ENV) != "1"
+
+
+def _kfd_gpus() -> int:
+    """GPUs the kernel driver exposes (KFD topology nodes with a gpu_id),
+    minus what the visibility variables hide — without touching HIP."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() not in ("", "-1")]
+            if not ids:
+                return 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    return n if os.access("/dev/kfd", os.R_OK | os.W_OK) else 0
+
+
+def _gpu_ext_present() -> bool:
+    import importlib.util
+    try:
+        return importlib.util.find_spec("tritondl._gpu_hash") is not None
+    except (ImportError, ValueError):
+        return False
+
+
 def gpu_available() -> bool:
     if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off":
         return False
+    if helper_mode():
+        return _gpu_ext_present() and _kfd_gpus() > 0
     try:
         return _load_gpu().device_count() > 0
     except Exception:
         return False
+
+
+_helper = None
+
+
+def gpu_backend():
+    """What the verification paths hash on: the helper process's hasher
+    (default), or the in-process :func:`gpu_hasher`."""
+    global _helper
+    if not helper_mode():
+        return gpu_hasher()
+    with _gpu_lock:
+        if _helper is None:
+            from .gpu_helper import GpuHelper
+            _helper = GpuHelper()
+        return _helper
 
 
 def default_device() -> int:
@@ -225,9 +284,15 @@ def warm_gpu(device: int | None = None) -> bool:
     """Bring up the HIP context and load the code object (one tiny batch) so
     the first resume-verify of a job does not pay the one-time setup, then
     free the batch's buffers again: warm-up leaves no HBM or pinned memory
-    allocated.  Returns False when no GPU path is available."""
+    allocated.  In helper mode nothing is started unless
+    ``TRITONDL_GPU_WARMUP=1`` (the helper would exit idle again anyway).
+    Returns False when no GPU path is available."""
     if not gpu_available():
         return False
+    if helper_mode():
+        if os.environ.get("TRITONDL_GPU_WARMUP", "") == "1":
+            gpu_backend().hash_buffer("sha1", b"\0" * 16384, 16384)
+        return True
     h = gpu_hasher(device)
     h.hash_buffer("sha1", b"\0" * 16384, 16384)
     h.release()
@@ -363,7 +428,7 @@ def piece_hashes(data, piece_len: int, kind: str = "sha1", device: str = "cpu", 
     """Concatenated digests of ``data`` split into ``piece_len`` pieces."""
     dev = _resolve(device)
     if dev == "gpu":
-        return gpu_hasher().hash_buffer(kind, data, piece_len)
+        return gpu_backend().hash_buffer(kind, data, piece_len)
     return _host.piece_hashes(kind, data, piece_len, threads or effective_cpus())
 
 
@@ -387,9 +452,10 @@ def verify_pieces(files: Sequence[tuple[str, int]], piece_len: int, expected: by
     dev = _resolve(device)
     files = [(str(p), int(n)) for p, n in files]
     if dev == "gpu":
-        return gpu_hasher().verify_files(files, piece_len, expected, kind)
+        return gpu_backend().verify_files(files, piece_len, expected, kind)
     if dev == "hybrid":
-        return gpu_hasher().verify_files(files, piece_len, expected, kind, cpu_threads=threads or hybrid_cpu_threads())
+        return gpu_backend().verify_files(files, piece_len, expected, kind,
+                                          cpu_threads=threads or hybrid_cpu_threads())
     return _host.verify_pieces(files, piece_len, expected, threads or effective_cpus(), kind)
 
 
@@ -407,8 +473,8 @@ def verify_pieces_v2(files: Sequence[tuple[str, int]], piece_len: int, expected:
     kn = bytes(1 if k else 0 for k in (known if known is not None else [True] * n))
     thr = threads or effective_cpus()
     if dev in ("gpu", "hybrid"):
-        leaves, leaf_ok = gpu_hasher().digest_files(files, 16384, "sha256",
-                                                    cpu_threads=hybrid_cpu_threads() if dev == "hybrid" else 0)
+        leaves, leaf_ok = gpu_backend().digest_files(files, 16384, "sha256",
+                                                     cpu_threads=hybrid_cpu_threads() if dev == "hybrid" else 0)
         leaves, leaf_ok = bytearray(leaves), bytearray(leaf_ok)
         # the kernel hashed whole 16 KiB blocks of the padded stream; a file's
         # short last leaf must hash only its real bytes: redo those (<= one per file)
