@@ -249,7 +249,7 @@ def test_gpu_leaf_path_logic_emulated_on_host(tmp_path, monkeypatch):
         def digest_files(self, files, pl, kind, cpu_threads=0):
             blob = b"".join(bytes(n) if not p else open(p, "rb").read() for p, n in files)
             return hashing._host.piece_hashes(kind, blob, pl, 2), b"\x01" * (-(-len(blob) // pl))
-    monkeypatch.setattr(hashing, "gpu_hasher", lambda *a, **k: FakeGpu())
+    monkeypatch.setattr(hashing, "gpu_backend", lambda *a, **k: FakeGpu())
     monkeypatch.setattr(hashing, "_resolve", lambda d: d)
     ok = hashing.verify_pieces_v2(layout, info.piece_length, exp, widths, reals, known, device="gpu")
     assert ok == b"\x01" * info.num_pieces
