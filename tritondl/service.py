@@ -19,8 +19,13 @@ Differences, all documented fixes:
   is freed at once; the delay grows per retry) and, after ``max_retries``,
   published to the durable dead-letter topic ``<consume_topic>.dead`` with
   ``X-Failed-Stage`` / ``X-Error`` and acked.  A job is never dropped unless
-  ``drop_failed`` is set; if even the dead-letter publish fails the delivery
-  stays unacked and the broker redelivers it;
+  ``drop_failed`` is set.  Where the broker refuses this worker the delay
+  queue (no *configure* permission, or a queue of that name with other
+  arguments) the retry waits in-process instead and is re-published to the
+  job's own queue — the reference's ``Error()`` exactly, needing only the
+  *write* permission the reference needed; an unreachable dead-letter topic
+  parks the job the same way at the longest delay.  Never a nack-requeue
+  loop;
 * an unusable ``S3_ENDPOINT`` is fatal at start-up, before the broker is
   dialled (the reference ``log.Fatal``-ed in ``NewUploader``,
   ``downloader.go:95-98``);
