@@ -101,3 +101,26 @@ def test_worker_side_never_loads_hip(monkeypatch):
                        cwd=gpu_helper.ROOT, env={k: v for k, v in os.environ.items() if k != "TRITONDL_GPU_HELPER"})
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert b"LOADED False False" in p.stdout
+
+
+def test_auto_verify_falls_back_to_the_host_when_the_helper_cannot_start(tmp_path, monkeypatch):
+    """A node whose KFD lists a GPU but whose HIP stack is broken: the first
+    'auto' resume finds the helper dead on arrival, verifies on the host, and
+    the GPU is not offered again in this process."""
+    from tritondl.fakes.swarm import make_payload
+    from tritondl.fetch.bt.metainfo import make_info
+    from tritondl.fetch.bt.storage import FileStorage
+
+    src = tmp_path / "src" / "T"
+    make_payload(str(src), {"a.mkv": 300_000, "b.mkv": 120_000})
+    info = make_info(str(src), 32768)
+    monkeypatch.setattr(hashing, "_kfd_gpus", lambda: 1)
+    monkeypatch.setattr(hashing, "_gpu_ext_present", lambda: True)
+    monkeypatch.setattr(hashing, "choose_device", lambda *a, **k: "gpu")
+    monkeypatch.setattr(hashing, "_helper", gpu_helper.GpuHelper(start_timeout=60))
+    monkeypatch.setattr(hashing, "_gpu_disabled", None)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")       # what the helper sees: no device
+    st = FileStorage(str(tmp_path / "src"), info)
+    have = st.verify_existing("auto")
+    assert have == set(range(info.num_pieces))
+    assert hashing._gpu_disabled and not hashing.gpu_available()

@@ -181,23 +181,34 @@ class FileStorage:
         if not any(p and os.path.exists(p) and os.path.getsize(p) for p, _ in self.layout):
             return set()
         dev = device
-        if self.info.pieces:
-            if device == "auto":
-                dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length)
-            ok = hashing.verify_pieces(self.layout, self.info.piece_length, self.info.pieces, device=dev)
-        else:
-            # pure v2: per-piece merkle roots over 16 KiB leaves — every leaf is
-            # independent, so the GPU sees total/16 KiB lanes whatever the piece size
-            exp, widths, reals, known = self.info.v2_expectations()
-            if device == "auto":
-                dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length, lane_len=16384)
-            ok = hashing.verify_pieces_v2(self.layout, self.info.piece_length, exp, widths, reals, known,
-                                          device=dev)
+        try:
+            dev, ok = self._verify_batch(device)
+        except hashing.HelperError as e:
+            if device != "auto":
+                raise                      # the GPU was demanded: fail loudly
+            # the GPU helper could not run: this and every later "auto" batch hashes on the host
+            hashing.disable_gpu(str(e))
+            dev, ok = self._verify_batch("cpu")
         have = {i for i, v in enumerate(ok) if v}
         if self.db is not None:
             self.db.set_many(self.info.infohash, {i: bool(v) for i, v in enumerate(ok)})
         log.with_fields(pieces=n, verified=len(have), device=dev).info("verified existing torrent data")
         return have
+
+    def _verify_batch(self, device: str) -> tuple[str, bytes]:
+        n = self.info.num_pieces
+        dev = device
+        if self.info.pieces:
+            if device == "auto":
+                dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length)
+            return dev, hashing.verify_pieces(self.layout, self.info.piece_length, self.info.pieces, device=dev)
+        # pure v2: per-piece merkle roots over 16 KiB leaves — every leaf is
+        # independent, so the GPU sees total/16 KiB lanes whatever the piece size
+        exp, widths, reals, known = self.info.v2_expectations()
+        if device == "auto":
+            dev = hashing.choose_device(n, self.info.piece_length, self.info.total_length, lane_len=16384)
+        return dev, hashing.verify_pieces_v2(self.layout, self.info.piece_length, exp, widths, reals, known,
+                                             device=dev)
 
     def mark(self, piece: int, complete: bool = True) -> None:
         if self.db is not None:

@@ -166,8 +166,21 @@ def _gpu_ext_present() -> bool:
         return False
 
 
+_gpu_disabled: str | None = None
+
+
+def disable_gpu(reason: str) -> None:
+    """Stop offering the GPU to ``device="auto"`` callers in this process (the
+    helper could not start: a broken HIP stack must not fail every resume)."""
+    global _gpu_disabled
+    if _gpu_disabled is None:
+        from ..utils.log import log
+        log.with_field("reason", reason).warn("GPU verification disabled; hashing on the host")
+    _gpu_disabled = reason
+
+
 def gpu_available() -> bool:
-    if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off":
+    if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off" or _gpu_disabled is not None:
         return False
     if helper_mode():
         return _gpu_ext_present() and _kfd_gpus() > 0
@@ -178,6 +191,13 @@ def gpu_available() -> bool:
 
 
 _helper = None
+
+
+def __getattr__(name: str):
+    if name == "HelperError":            # lazily: gpu_helper imports this module
+        from .gpu_helper import HelperError
+        return HelperError
+    raise AttributeError(name)
 
 
 def gpu_backend():
