@@ -232,6 +232,8 @@ def main() -> int:
                                                                "default, 0: delete every file)")
     ap.add_argument("--variants", type=int, default=-1,
                     help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
+    ap.add_argument("--pipeline-commit", default="on", choices=["on", "off"],
+                    help="on: a job's publish confirm and ack overlap the next job (worker default)")
     ap.add_argument("--no-content-check", action="store_true",
                     help="S3 does not compare PUT content with the origin's payload")
     ap.add_argument("--fake-cpus", default="auto",
@@ -284,7 +286,8 @@ def main() -> int:
                      s3_part_size=a.s3_part_mb << 20, s3_multipart_threshold=a.s3_multipart_mb << 20,
                      payload_mode=a.payload, hash_device=a.s3_hash_device, cleanup=a.cleanup == "on",
                      recycle_bytes=(a.recycle_mb << 20) if a.recycle_mb >= 0 else -1, variants=a.variants,
-                     content_check=not a.no_content_check)
+                     content_check=not a.no_content_check,
+                     overrides={"pipeline_commit": a.pipeline_commit == "on"})
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 
@@ -439,7 +442,7 @@ def main() -> int:
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
                        "cpus_busy_before": os.environ.get("TRITONDL_BENCH_DOMAIN_BUSY", ""),
                        "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
-                       "cleanup": stack.cleanup,
+                       "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
                        **knobs},

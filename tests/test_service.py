@@ -651,3 +651,42 @@ def test_cleanup_redelivery_waiting_on_the_lock_gets_a_live_dir(tmp_path):
         await svc2.shutdown(grace=5)
         await e1.down()
     run(main())
+
+
+def test_pipelined_commit_overlaps_confirms_but_acks_after_them(tmp_path):
+    """A job frees its loop once its upload is done: its publish confirm and
+    ack overlap the next job.  Every ack still follows its own confirmed
+    v1.convert publish (at-least-once), and the reference's one-job-at-a-time
+    data path is kept (concurrency 1)."""
+    async def main():
+        e = await Env().up(tmp_path)
+        e.broker.confirm_delay = 0.25
+        for k in range(4):
+            url = e.origin.add(f"/p{k}.mkv", os.urandom(50_000))
+            e.submit(Media(id=f"p{k}", source_uri=url), i=k)
+        t0 = time.monotonic()
+        res = await e.wait_results(4, timeout=20)
+        dt = time.monotonic() - t0
+        assert all(r.ok for r in res)
+        assert dt < 0.8, dt                      # serial commits would take >= 4 x 0.25 s
+        ev = [x for x in e.broker.events if x[0] == "ack" or x[1] == "v1.convert"]
+        # the k-th ack comes after the k-th convert publish's confirm
+        confs = [i for i, x in enumerate(ev) if x[0] == "confirm"]
+        acks = [i for i, x in enumerate(ev) if x[0] == "ack"]
+        assert len(confs) == len(acks) == 4 and all(a > c for c, a in zip(confs, acks)), ev
+        await e.down()
+    run(main())
+
+
+def test_pipelined_commit_off_is_serial(tmp_path):
+    async def main():
+        e = await Env().up(tmp_path, pipeline_commit=False)
+        e.broker.confirm_delay = 0.2
+        for k in range(3):
+            url = e.origin.add(f"/s{k}.mkv", os.urandom(20_000))
+            e.submit(Media(id=f"s{k}", source_uri=url), i=k)
+        t0 = time.monotonic()
+        await e.wait_results(3, timeout=20)
+        assert time.monotonic() - t0 >= 0.6
+        await e.down()
+    run(main())

@@ -244,6 +244,8 @@ class Broker:
         self._qname = itertools.count(1)
         self.blocked = False
         self.fail_publishes = 0
+        self.confirm_delay = 0.0           # fault injection: publisher confirms arrive this much later
+        self.events: list[tuple[str, str]] = []   # ("publish", exchange) / ("ack", queue), in order
         self.published: list[QMsg] = []
         self.stats = collections.Counter()
         self.users: dict[str, tuple[str, Perms]] = {}
@@ -768,13 +770,20 @@ class Broker:
             c.send_method(ch.id, Method("basic.nack", {"delivery_tag": ch.pub_seq}))
             return
         self.published.append(msg)
+        self.events.append(("publish", m.exchange))
         n = self._route(msg)
         if n == 0 and m.mandatory:
             c.send(b"".join(codec.content_frames(ch.id, Method("basic.return", {
                 "reply_code": codec.NO_ROUTE, "reply_text": "NO_ROUTE", "exchange": m.exchange,
                 "routing_key": m.routing_key}), msg.body, msg.props, c.frame_max)))
         if ch.confirm:
-            c.send_method(ch.id, Method("basic.ack", {"delivery_tag": ch.pub_seq}))
+            if self.confirm_delay:
+                def confirm(tag=ch.pub_seq, ex=m.exchange) -> None:
+                    self.events.append(("confirm", ex))
+                    c.send_method(ch.id, Method("basic.ack", {"delivery_tag": tag}))
+                asyncio.get_running_loop().call_later(self.confirm_delay, confirm)
+            else:
+                c.send_method(ch.id, Method("basic.ack", {"delivery_tag": ch.pub_seq}))
 
     def _can_deliver(self, cons: _Consumer) -> bool:
         ch = cons.ch
@@ -872,6 +881,7 @@ class Broker:
             touched.add(q.name)
             if m.name == "basic.ack":
                 self.stats["acked"] += 1
+                self.events.append(("ack", q.name))
                 continue
             if requeue:
                 msg.redelivered = True

@@ -31,7 +31,14 @@ Differences, all documented fixes:
   ``downloader.go:95-98``);
 * B12 — broker connect errors are checked before use;
 * ``concurrency`` job loops per process (default 1 = reference), each job
-  fully async so downloads / uploads of different jobs overlap;
+  fully async so downloads / uploads of different jobs overlap.  A job
+  frees its loop once its upload is done: the ``v1.convert`` publish, its
+  broker confirm and the ack finish in the job's own task while the next
+  job starts (``pipeline_commit``).  The reference published without
+  confirms and acked at once (``downloader.go:147-153``), so its commit cost
+  no time; this keeps the confirm-before-ack guarantee without paying a
+  broker round trip per job.  The ack still follows the confirm, and the
+  job's dir stays locked until it is settled;
 * in-flight jobs are drained on shutdown (the Go job goroutine was never
   joined); the work dir can optionally be cleaned after success (B15).
 """
@@ -40,6 +47,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import contextvars
 import fcntl
 import os
 import queue
@@ -79,6 +87,10 @@ def default_impls(cfg: Config) -> list[ClientImpl]:
         log.warn("bittorrent downloader unavailable: %s", e)
     impls.append(http)
     return impls
+
+
+# the job slot of the delivery this task handles (pipelined commit, see Service._worker)
+_SLOT: contextvars.ContextVar[asyncio.Event | None] = contextvars.ContextVar("tritondl_job_slot", default=None)
 
 
 class JobBusy(Exception):
@@ -159,6 +171,7 @@ class Service:
         self.uploader = uploader
         self.metrics = metrics or Metrics()
         self._workers: list[asyncio.Task] = []
+        self._tails: set[asyncio.Task] = set()     # jobs past their upload: publish confirm, ack, cleanup
         self._stop = asyncio.Event()
         self._inflight = 0
         self._metrics_runner = None
@@ -347,11 +360,36 @@ class Service:
                 return
             self._inflight += 1
             self.metrics.set("jobs_inflight", self._inflight)
+            if not self.cfg.pipeline_commit:
+                try:
+                    await self.handle(d)
+                finally:
+                    self._inflight -= 1
+                    self.metrics.set("jobs_inflight", self._inflight)
+                continue
+            # pipelined commit: the slot is free once the job's upload is done; its
+            # publish confirm, ack and cleanup finish in the job's task meanwhile
+            slot = asyncio.Event()
+            t = asyncio.ensure_future(self._handle_with_slot(d, slot))
+            self._tails.add(t)
+            t.add_done_callback(self._tails.discard)
+            freed = asyncio.ensure_future(slot.wait())
             try:
-                await self.handle(d)
+                await asyncio.wait({t, freed}, return_when=asyncio.FIRST_COMPLETED)
             finally:
+                freed.cancel()
                 self._inflight -= 1
                 self.metrics.set("jobs_inflight", self._inflight)
+
+    async def _handle_with_slot(self, d: Delivery, slot: asyncio.Event) -> None:
+        token = _SLOT.set(slot)
+        try:
+            await self.handle(d)
+        except Exception as e:  # noqa: BLE001 - handle() settles the delivery itself; never lose the loop
+            log.with_field("error", str(e)).error("job task failed")
+        finally:
+            slot.set()
+            _SLOT.reset(token)
 
     async def handle(self, msg: Delivery) -> JobResult:
         """Process one delivery end-to-end; always settles it."""
@@ -415,6 +453,9 @@ class Service:
             self.metrics.observe("stage_seconds", time.monotonic() - t, stage="upload")
             mark("upload")
             stage = "publish"
+            free = _SLOT.get()
+            if free is not None:
+                free.set()                 # the next job may start: this one only commits from here on
             log.info("creating v1.convert message")
             conv = Convert.from_download(job, go_time_string())
             await self.amqp.publish(self.cfg.publish_topic, conv.encode())
@@ -620,8 +661,16 @@ class Service:
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
         self._stop.set()
+        t_end = time.monotonic() + grace
         if self._workers:
             done, pending = await asyncio.wait(self._workers, timeout=grace)
+            for t in pending:
+                t.cancel()
+            for t in pending:
+                with contextlib.suppress(BaseException):
+                    await t
+        if self._tails:                      # jobs still committing (publish confirm, ack)
+            done, pending = await asyncio.wait(set(self._tails), timeout=max(1.0, t_end - time.monotonic()))
             for t in pending:
                 t.cancel()
             for t in pending:

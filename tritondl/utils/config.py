@@ -69,6 +69,7 @@ class Config:
 
     # --- job processing ---
     concurrency: int = 1                        # one job loop (downloader.go:103)
+    pipeline_commit: bool = True                # a job's confirm + ack overlap the next job (service._worker)
     max_retries: int = 5                        # B4 fix: X-Retries budget
     retry_delay_s: float = 10.0                 # delivery.go:72 (first retry; waited in a broker delay queue)
     retry_backoff: float = 2.0                  # delay multiplier per retry (1.0 = the reference's fixed 10 s)
@@ -215,6 +216,7 @@ class Config:
         c.declare_publish = _env_bool(g("TRITONDL_DECLARE_PUBLISH"), c.declare_publish)
         c.declare_publish_queues = _env_bool(g("TRITONDL_DECLARE_PUBLISH_QUEUES"), c.declare_publish_queues)
         c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
+        c.pipeline_commit = _env_bool(g("TRITONDL_PIPELINE_COMMIT"), c.pipeline_commit)
         c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
         c.bt_dht_ipv6 = _env_bool(g("TRITONDL_BT_DHT_IPV6"), c.bt_dht_ipv6)
         c.bt_upnp = _env_bool(g("TRITONDL_BT_UPNP"), c.bt_upnp)
