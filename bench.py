@@ -232,8 +232,8 @@ def main() -> int:
                                                                "default, 0: delete every file)")
     ap.add_argument("--variants", type=int, default=-1,
                     help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
-    ap.add_argument("--pipeline-commit", default="on", choices=["on", "off"],
-                    help="on: a job's publish confirm and ack overlap the next job (worker default)")
+    ap.add_argument("--pipeline-commit", default="off", choices=["on", "off"],
+                    help="on: a job's publish confirm and ack overlap the next job (opt-in worker setting)")
     ap.add_argument("--no-content-check", action="store_true",
                     help="S3 does not compare PUT content with the origin's payload")
     ap.add_argument("--fake-cpus", default="auto",

@@ -659,7 +659,7 @@ def test_pipelined_commit_overlaps_confirms_but_acks_after_them(tmp_path):
     v1.convert publish (at-least-once), and the reference's one-job-at-a-time
     data path is kept (concurrency 1)."""
     async def main():
-        e = await Env().up(tmp_path)
+        e = await Env().up(tmp_path, pipeline_commit=True)
         e.broker.confirm_delay = 0.25
         for k in range(4):
             url = e.origin.add(f"/p{k}.mkv", os.urandom(50_000))

@@ -34,11 +34,14 @@ Differences, all documented fixes:
   fully async so downloads / uploads of different jobs overlap.  A job
   frees its loop once its upload is done: the ``v1.convert`` publish, its
   broker confirm and the ack finish in the job's own task while the next
-  job starts (``pipeline_commit``).  The reference published without
-  confirms and acked at once (``downloader.go:147-153``), so its commit cost
-  no time; this keeps the confirm-before-ack guarantee without paying a
-  broker round trip per job.  The ack still follows the confirm, and the
-  job's dir stays locked until it is settled;
+  job starts (``pipeline_commit``, opt-in).  The reference published
+  without confirms and acked at once (``downloader.go:147-153``), so its
+  commit cost no time; this keeps the confirm-before-ack guarantee without
+  a broker round trip per job.  The ack still follows the confirm, and the
+  job's dir stays locked until it is settled.  On the headline it measured
+  no faster (the single event loop does the commit's work either way, now
+  under the next job's start: ``profiles/r04_commit_ab/``), so it is off by
+  default;
 * in-flight jobs are drained on shutdown (the Go job goroutine was never
   joined); the work dir can optionally be cleaned after success (B15).
 """

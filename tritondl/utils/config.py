@@ -69,7 +69,9 @@ class Config:
 
     # --- job processing ---
     concurrency: int = 1                        # one job loop (downloader.go:103)
-    pipeline_commit: bool = True                # a job's confirm + ack overlap the next job (service._worker)
+    # a job's confirm + ack overlap the next job (service._worker); measured no faster on the
+    # headline (the loop does the same work either way), so opt-in (profiles/r04_commit_ab/)
+    pipeline_commit: bool = False
     max_retries: int = 5                        # B4 fix: X-Retries budget
     retry_delay_s: float = 10.0                 # delivery.go:72 (first retry; waited in a broker delay queue)
     retry_backoff: float = 2.0                  # delay multiplier per retry (1.0 = the reference's fixed 10 s)
