@@ -78,6 +78,24 @@ def _torrent_impl(svc):
     return None
 
 
+def _mallinfo() -> tuple[float, float] | None:
+    """glibc heap: (bytes in use, bytes the arenas hold), MiB — tells a leak
+    (in-use grows) from allocator fragmentation (only the arenas grow)."""
+    import ctypes
+
+    class MI2(ctypes.Structure):
+        _fields_ = [(n, ctypes.c_size_t) for n in ("arena", "ordblks", "smblks", "hblks", "hblkhd", "usmblks",
+                                                    "fsmblks", "uordblks", "fordblks", "keepcost")]
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        f = libc.mallinfo2
+    except (OSError, AttributeError):
+        return None
+    f.restype = MI2
+    m = f()
+    return round((m.uordblks + m.hblkhd) / 2**20, 1), round((m.arena + m.hblkhd) / 2**20, 1)
+
+
 def sample(svc) -> dict:
     """One resource sample of this process."""
     import psutil
@@ -90,6 +108,10 @@ def sample(svc) -> dict:
            "pool_threads": pool, "pumps": rawhttp.active_pumps()}
     m = svc.metrics
     out["metrics_series"] = len(m.counters) + len(m.gauges) + len(m.hists)
+    out["py_objects"] = len(gc.get_objects())
+    heap = _mallinfo()
+    if heap is not None:
+        out["heap_in_use_mb"], out["heap_arenas_mb"] = heap
     tls = [c.cached_sessions for c in rawhttp._client_tls.values() if c is not None]
     out["tls_sessions"] = sum(tls) if tls else None
     bt = _torrent_impl(svc)
@@ -101,7 +123,7 @@ def sample(svc) -> dict:
 
 
 SERIES = ("rss_mb", "fds", "os_threads", "py_threads", "tasks", "pool_threads", "metrics_series", "tls_sessions",
-          "dht_nodes", "dht_peer_keys")
+          "dht_nodes", "dht_peer_keys", "py_objects", "heap_in_use_mb", "heap_arenas_mb")
 
 
 def drift(samples: list[dict], warmup: int, key: str = "jobs") -> dict:
@@ -183,6 +205,7 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
         kinds: list[str] = []
         samples: list[dict] = []
         base = svc.jobs_finished
+        ok0 = svc.metrics.get("jobs", status="ok")
         next_sample = base
         t0 = time.monotonic()
         next_t = t0
@@ -240,9 +263,8 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                 take_sample()
                 next_sample += sample_every
         dt = time.monotonic() - t0
-        res = svc.results
         n_att = svc.jobs_finished - base
-        ok = sum(1 for r in res[-min(len(res), n_att):] if r.ok)
+        ok = int(svc.metrics.get("jobs", status="ok") - ok0)    # results[] keeps only the last 10,000
         await asyncio.sleep(0.2)
         take_sample()
         summary = {"jobs": len(kinds), "torrent_jobs": kinds.count("torrent"), "failing_jobs": kinds.count("fail"),
