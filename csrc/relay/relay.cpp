@@ -295,6 +295,21 @@ PYBIND11_MODULE(_relay, m) {
         "leaf_hashes = the payload SHA-256s of its 64 KiB leaves, concatenated (b'' unless every frame "
         "but the last is one 64 KiB leaf).");
 
+  m.def("recv_leaf_hashes",
+        [](const py::object& sock, uint64_t len, const py::bytes& prefix, int threads, double idle_timeout) {
+          std::string pre = prefix;
+          StreamArg io = as_stream(sock);
+          VerifyResult r;
+          {
+            py::gil_scoped_release nogil;
+            r = recv_leaf_hashes(*io.s, len, pre.data(), pre.size(), threads, idle_timeout);
+          }
+          return py::make_tuple(r.decoded, r.err, py::bytes(r.leaf_hashes));
+        },
+        py::arg("sock"), py::arg("length"), py::arg("prefix"), py::arg("threads") = 4,
+        py::arg("idle_timeout") = 300.0,
+        "Receive exactly `length` body bytes; returns (received, error, leaf_hashes): the SHA-256 of every "
+        "64 KiB leaf, concatenated (hashed while the body lands).");
   m.def("chunked_length", &chunked_length, py::arg("length"), py::arg("chunk") = 64 << 10);
   m.def("pool_threads", [] { return tritondl_hash::TaskPool::get().threads(); },
         "threads of this module's native task pool (chunk hashers; parked + busy)");

@@ -1720,6 +1720,81 @@ inline VerifyResult recv_verify_stream(Stream& io, uint64_t raw_len, const char*
   return r;
 }
 
+// recv_leaf_hashes: the fake S3's side of an UNSIGNED-PAYLOAD PUT with a
+// content check — receive exactly `len` body bytes and return the SHA-256 of
+// every 64 KiB leaf (VerifyResult.leaf_hashes).  Leaves are hashed by a
+// hasher pool as soon as they have landed, 16 at a time for the AVX-512
+// kernel when a backlog builds up, so little is left after the last byte.
+inline VerifyResult recv_leaf_hashes(Stream& io, uint64_t len, const char* prefix, size_t plen, int threads,
+                                     double idle_timeout) {
+  VerifyResult r;
+  Buf whole(static_cast<size_t>(len) + 1);
+  char* raw = whole.data();
+  const size_t pre = static_cast<size_t>(std::min<uint64_t>(plen, len));
+  std::memcpy(raw, prefix, pre);
+  const size_t nleaves = static_cast<size_t>((len + kLeafBytes - 1) / kLeafBytes);
+  std::string hashes(32 * nleaves, '\0');
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t landed = 0, claimed = 0;  // leaves fully received / taken by a hasher (guarded by mu)
+  bool done = false;
+  const size_t wide = tritondl_hash::sha256_claim();
+  auto hasher = [&] {
+    for (;;) {
+      size_t j, cnt;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return done || landed >= claimed + 2; });
+        if (landed == claimed) return;  // done, nothing left
+        const size_t avail = landed - claimed;
+        cnt = wide > 2 && avail >= 2 * wide ? wide : std::min<size_t>(2, avail);
+        j = claimed;
+        claimed += cnt;
+      }
+      const void* p[16];
+      size_t n[16];
+      for (size_t k = 0; k < cnt; ++k) {
+        const uint64_t off = static_cast<uint64_t>(j + k) * kLeafBytes;
+        p[k] = raw + off;
+        n[k] = static_cast<size_t>(std::min<uint64_t>(kLeafBytes, len - off));
+      }
+      tritondl_hash::sha256_batch(p, n, cnt, reinterpret_cast<unsigned char*>(&hashes[32 * j]));
+    }
+  };
+  const int nthreads = std::max(1, threads <= 0 ? 4 : threads);
+  auto pool = tritondl_hash::TaskPool::get().run(nthreads, hasher, "tdl-s3leaf");
+  size_t have = pre;
+  auto last = Clock::now();
+  auto publish = [&] {
+    const size_t full = have == len ? nleaves : have / kLeafBytes;
+    std::lock_guard<std::mutex> l(mu);
+    if (full > landed) {
+      landed = full;
+      cv.notify_all();
+    }
+  };
+  publish();
+  while (have < len) {
+    const ssize_t n = recv_wait(io, raw + have, static_cast<size_t>(len - have), &last, idle_timeout, nullptr, &r.err);
+    if (n <= 0) {
+      if (n == 0) r.err = "client closed inside the request body";
+      break;
+    }
+    have += static_cast<size_t>(n);
+    publish();
+  }
+  {
+    std::lock_guard<std::mutex> l(mu);
+    done = true;
+    if (!r.err.empty()) landed = claimed;  // drop what has not been claimed
+  }
+  cv.notify_all();
+  pool->wait();
+  r.decoded = have;
+  if (r.err.empty()) r.leaf_hashes = std::move(hashes);
+  return r;
+}
+
 inline VerifyResult recv_verify_chunked(Stream& io, uint64_t raw_len, const char* prefix, size_t plen,
                                         const std::string& key, const std::string& amzdate, const std::string& scope,
                                         const std::string& seed, bool keep, int threads, double idle_timeout) {

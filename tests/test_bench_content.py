@@ -131,3 +131,38 @@ def test_broken_watermark_undetected_without_variants_check(tmp_path, monkeypatc
             await st.teardown()
     wrong, counts = run(main())
     assert wrong >= 1 and counts == {"content_ok": 0, "content_bad": 0}
+
+
+@pytest.mark.skipif(rawhttp.relay_module() is None, reason="native relay not built")
+def test_native_unsigned_receiver_returns_the_leaf_hashes():
+    """recv_leaf_hashes (the fake S3's UNSIGNED-PAYLOAD path with a content
+    check) hashes every 64 KiB leaf while the body lands."""
+    import threading
+    relay = rawhttp.relay_module()
+    for size in (0, 1000, 65536, 5 * 65536 + 77, 3 << 20):
+        data = os.urandom(size)
+        a, b = socket.socketpair()
+        pre = data[:100]
+        t = threading.Thread(target=lambda: (a.sendall(data[100:]), a.close()))
+        t.start()
+        try:
+            got, err, leaves = relay.recv_leaf_hashes(b.fileno(), len(data), pre, 3, 5.0)
+        finally:
+            t.join()
+            b.close()
+        assert err == "" and got == len(data), (size, err)
+        assert leaves == payload.leaf_hashes(data), size
+
+
+def test_https_stack_checks_content(tmp_path):
+    """Over https the S3 payload is UNSIGNED (minio-go's choice); the content
+    check still runs, on the native receiver."""
+    async def main():
+        (tmp_path / "w").mkdir()
+        st = JobStack(file_size=1 << 20, inproc=False, tag="tls", workdir=str(tmp_path / "w"), tls=True)
+        await st.setup()
+        try:
+            await st.run_jobs(3)
+        finally:
+            await st.teardown()
+    run(main())

@@ -215,17 +215,21 @@ class FakeS3:
             if relay is not None and request.body_length:
                 return await self._read_chunked_native(relay, request, auth, keep)
             return await self._read_chunked(request, auth, keep)
-        if relay is not None and not keep and self.expect is None and phash in (sigv4.UNSIGNED_PAYLOAD, "") \
-                and request.body_length:
+        if relay is not None and not keep and phash in (sigv4.UNSIGNED_PAYLOAD, "") and request.body_length:
             n = request.body_length
             stream, pre = request.take_body()
-            got, _eof, err = await asyncio.get_running_loop().run_in_executor(
-                None, relay.recv_body, stream, -1, 0, n, pre, None, 0, 0, 300.0)
+            leaves = None
+            if self.expect is None:
+                got, _eof, err = await asyncio.get_running_loop().run_in_executor(
+                    None, relay.recv_body, stream, -1, 0, n, pre, None, 0, 0, 300.0)
+            else:                       # content check: leaf hashes computed while the body lands
+                got, err, leaves = await asyncio.get_running_loop().run_in_executor(
+                    None, relay.recv_leaf_hashes, stream, n, pre, self.verify_threads, 300.0)
             if err:
                 request.transport.close()
                 raise _BadReq(400, "IncompleteBody", err)
             self.bytes_received += got
-            return _Sized(got)
+            return _Sized(got, leaves)
         data = await request.read()
         self.bytes_received += len(data)
         if phash not in (sigv4.UNSIGNED_PAYLOAD, "") and auth is not None:

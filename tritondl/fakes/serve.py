@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import mmap
 import os
 import signal
 import sys
@@ -44,7 +45,9 @@ class SyntheticOrigin(Origin):
         if b is None:
             tag = f'"syn-{size}"' if variant is None else f'"syn-{size}-v{variant}"'
             fd = Blob(variant_bytes(size, variant)).fd()
-            b = Blob(path=f"/proc/self/fd/{fd}", etag=tag)
+            # the memfd is the one copy: sendfile serves it, and paths that send from
+            # user space (https, rate caps) slice a read-only mapping of it
+            b = Blob(data=mmap.mmap(fd, size, prot=mmap.PROT_READ) if size else b"", etag=tag)
             b._fd = fd
             self._cache[(size, variant)] = b
         return b
