@@ -690,3 +690,18 @@ def test_pipelined_commit_off_is_serial(tmp_path):
         assert time.monotonic() - t0 >= 0.6
         await e.down()
     run(main())
+
+
+def test_heap_trim_runs_periodically(tmp_path):
+    """glibc arenas' free memory is handed back on a timer (RSS stays flat
+    over a long run, profiles/r04_soak60/)."""
+    from tritondl.service import _malloc_trim
+
+    async def main():
+        e = await Env().up(tmp_path, malloc_trim_s=0.1)
+        await asyncio.sleep(0.5)
+        if _malloc_trim() is not None:
+            assert e.svc._trimmer is not None and not e.svc._trimmer.done()
+        await e.down()
+        assert e.svc._trimmer is None or e.svc._trimmer.done()
+    run(main())

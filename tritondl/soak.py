@@ -159,12 +159,14 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    file_size: int = 10 << 20, torrent_mb: int = 8, max_retries: int = 2, warmup: int = 0,
                    on_sample=None, workdir: str | None = None, *, minutes: float = 0.0, rate: float = 0.0,
                    sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
-                   torrent_every: int = 0, dht_nodes: int = 0) -> dict:
+                   torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None) -> dict:
     """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
     ``rate`` jobs/s (0: as fast as the worker goes)."""
     timed = minutes > 0
     st = JobStack(file_size=file_size, tag="soak", workdir=workdir, tls=tls, heartbeat=heartbeat,
                   content_check=True)
+    if malloc_trim_s is not None:
+        st.overrides["malloc_trim_s"] = malloc_trim_s
     seed = None
     conn = None
     dht = []
@@ -306,6 +308,7 @@ def main() -> int:
     ap.add_argument("--heartbeat", type=int, default=0, help="AMQP heartbeat (s), broker and worker")
     ap.add_argument("--tls", action="store_true", help="origin and S3 over https")
     ap.add_argument("--dht-nodes", type=int, default=0, help="local DHT nodes the worker bootstraps from")
+    ap.add_argument("--malloc-trim", type=float, default=None, help="worker's malloc_trim period (s; 0 = off)")
     a = ap.parse_args()
     if a.cpus:
         from .parallel import topology
@@ -328,7 +331,8 @@ def main() -> int:
                                    a.torrent_mb, warmup=(a.warmup_minutes if a.minutes else a.warmup),
                                    on_sample=emit, minutes=a.minutes, rate=a.rate, sample_seconds=a.sample_seconds,
                                    tls=a.tls, heartbeat=a.heartbeat, retry_delay=a.retry_delay,
-                                   torrent_every=a.torrent_every, dht_nodes=a.dht_nodes))
+                                   torrent_every=a.torrent_every, dht_nodes=a.dht_nodes,
+                                   malloc_trim_s=a.malloc_trim))
     finally:
         if fh is not None:
             fh.close()

@@ -78,6 +78,8 @@ class Config:
     retry_delay_max_s: float = 300.0            # cap on one retry delay
     dead_letter_topic: str = ""                 # "" => "<consume_topic>.dead"
     drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
+    # give glibc's free arena memory back to the OS this often (0: never); see Service._trim_heap
+    malloc_trim_s: float = 60.0
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
@@ -198,7 +200,8 @@ class Config:
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
-                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s"}
+                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
+                  "MALLOC_TRIM": "malloc_trim_s"}
         strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
                 "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
                 "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
