@@ -162,24 +162,32 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
     doms, busy = (topology.shared_idle_order(local_rank, local_world, tag) if cpus == "auto"
                   else (topology.l3_domains(), []))
     k = 2 if file_size >= 256 << 20 else 1
-    # with room for it, rank r takes domains [r(k+1), r(k+1)+k) and its fakes the next one:
-    # neighbours in L3 order share a socket, and ranks spread over both sockets as
-    # their GPUs do; otherwise the ranks come first and the fakes after them all
+    # with room for it, every rank gets k domains and its fakes one more, all on one
+    # NUMA node (the idle ranking alone can put the fakes across the socket:
+    # topology.pair_domains); otherwise the ranks come first and the fakes after them all
+    pairs = topology.pair_domains(doms, k, local_world) if cpus == "auto" else None
     packed = len(doms) >= (k + 1) * local_world
     first = local_rank * (k + 1) if packed else local_rank * k
     if fake_cpus not in ("", "same") and cpus not in ("", "none"):
-        fc = (doms[(first + k if packed else local_world * k + local_rank) % len(doms)]
-              if fake_cpus == "auto" else topology.parse_cpulist(fake_cpus))
+        if fake_cpus != "auto":
+            fc = topology.parse_cpulist(fake_cpus)
+        elif pairs is not None:
+            fc = pairs[local_rank][1]
+        else:
+            fc = doms[(first + k if packed else local_world * k + local_rank) % len(doms)]
     if cpus == "auto":
-        pinned = sorted({c for j in range(k) for c in doms[(first + j) % len(doms)]})
+        mine = pairs[local_rank][0] if pairs is not None else [doms[(first + j) % len(doms)] for j in range(k)]
+        pinned = sorted({c for d in mine for c in d})
         os.sched_setaffinity(0, pinned)
         if busy:
-            os.environ["TRITONDL_BENCH_DOMAIN_BUSY"] = f"{busy[first % len(busy)]:.2f}"
+            share = dict(zip((d[0] for d in doms), busy))
+            os.environ["TRITONDL_BENCH_DOMAIN_BUSY"] = f"{share[mine[0][0]]:.2f}"
             # every L3 domain's busy share at launch, in topology order (first CPU: share)
-            chosen = {doms[(first + j) % len(doms)][0] for j in range(k)}
-            _PLACEMENT["ccd_busy_at_launch"] = {str(d[0]): round(b, 3) for d, b in
-                                                 sorted(zip(doms, busy), key=lambda x: x[0][0])}
-            _PLACEMENT["chosen_ccds"] = sorted(chosen)
+            _PLACEMENT["ccd_busy_at_launch"] = {str(c): round(b, 3) for c, b in sorted(share.items())}
+            _PLACEMENT["chosen_ccds"] = sorted(d[0] for d in mine)
+        if fc:
+            _PLACEMENT["fake_ccd"] = fc[0]
+            _PLACEMENT["fakes_same_numa_node"] = topology.numa_node_of(fc[0]) == topology.numa_node_of(pinned[0])
     elif cpus not in ("", "none"):
         pinned = topology.pin(cpus, local_rank)
     if fc:

@@ -188,6 +188,31 @@ def test_idle_first_order_shared_by_local_ranks(tmp_path, monkeypatch):
     assert t._cpu_ticks()                                          # /proc/stat parses here
 
 
+def test_pair_domains_keeps_each_rank_and_its_fakes_on_one_node():
+    """bench --cpus auto: a rank's domains and its fakes' domain share a NUMA
+    node whenever a node has room, even when the idle ranking alternates
+    between sockets; a group spans nodes only when none has room left."""
+    from tritondl.parallel import topology as t
+    # 16 CCDs, 0-7 on node 0 and 8-15 on node 1; idle order alternates sockets
+    doms = [[c * 8] for c in (0, 8, 1, 9, 2, 10, 3, 11, 4, 12, 5, 13, 6, 14, 7, 15)]
+    node = lambda d: d[0] // 64                                  # noqa: E731
+    one = t.pair_domains(doms, 1, 1, node)
+    assert one == [([[0]], [8])]                                 # not the next in idle order (CCD 64, node 1)
+    eight = t.pair_domains(doms, 1, 8, node)
+    assert len(eight) == 8
+    assert all(node(r) == node(f) for rd, f in eight for r in rd)
+    used = [d[0] for rd, f in eight for d in rd + [f]]
+    assert sorted(used) == sorted(d[0] for d in doms)            # every domain once
+    two = t.pair_domains(doms, 2, 2, node)                       # big files: 2 domains + fakes each
+    assert all(len({node(d) for d in rd + [f]}) == 1 for rd, f in two)
+    # 3 free domains per node, 3 ranks: the third group has to span nodes
+    small = [[0], [64], [8], [72], [16], [80]]
+    three = t.pair_domains(small, 1, 3, node)
+    assert [len({node(d) for d in rd + [f]}) for rd, f in three] == [1, 1, 2]
+    assert t.pair_domains(small, 1, 4, node) is None
+    assert t.numa_node_of(0) >= 0
+
+
 def _crashy(tmp_path):
     (tmp_path / "crashy.py").write_text(
         "import os, sys, time\n"

@@ -237,6 +237,54 @@ def idle_first(doms: list[list[int]], busy: list[float]) -> list[list[int]]:
     return [doms[i] for i in order]
 
 
+def numa_node_of(cpu: int, sysfs: str = "/sys/devices/system/cpu") -> int:
+    """NUMA node of a CPU (its ``cpuN/nodeM`` link), else its socket
+    (``physical_package_id``), else 0."""
+    try:
+        for name in os.listdir(f"{sysfs}/cpu{cpu}"):
+            if name.startswith("node") and name[4:].isdigit():
+                return int(name[4:])
+    except OSError:
+        pass
+    try:
+        with open(f"{sysfs}/cpu{cpu}/topology/physical_package_id") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError):
+        return 0
+
+
+def pair_domains(doms: list[list[int]], k: int, n: int, node_of=None) -> list[tuple[list[list[int]], list[int]]] | None:
+    """Give each of ``n`` ranks ``k`` L3 domains plus one for its fakes, all
+    on ONE NUMA node where a node has room.  ``doms`` comes idle-first
+    (:func:`shared_idle_order`); rank after rank takes the node whose
+    ``k + 1`` most idle free domains rank best, its ``k`` most idle for
+    itself and the next for the fakes.  Only when no node has ``k + 1`` free
+    domains left does a group span nodes.
+
+    Taking "the next domain in idle order" for the fakes, as before, put
+    them on the other socket whenever the idle ranking crossed it: a 10 MiB
+    job's loopback fetch then took 2.5-2.8 ms instead of 1.6-1.9 and the
+    headline fell from 300-376 to 243-299 jobs/s (``profiles/r04_fresh4/``).
+    Returns None when there are fewer than ``n * (k + 1)`` domains."""
+    if n <= 0 or k <= 0 or len(doms) < n * (k + 1):
+        return None
+    node_of = node_of or (lambda d: numa_node_of(d[0]))
+    nodes = [node_of(d) for d in doms]
+    free = list(range(len(doms)))                  # positions in the idle order
+    out: list[tuple[list[list[int]], list[int]]] = []
+    for _ in range(n):
+        by_node: dict[int, list[int]] = {}
+        for i in free:
+            by_node.setdefault(nodes[i], []).append(i)
+        groups = [idx[:k + 1] for idx in by_node.values() if len(idx) >= k + 1]
+        # the group whose worst member is the most idle; else the k+1 most idle anywhere
+        g = min(groups, key=lambda x: (x[-1], x[0])) if groups else free[:k + 1]
+        for i in g:
+            free.remove(i)
+        out.append(([doms[i] for i in g[:k]], doms[g[k]]))
+    return out
+
+
 def shared_idle_order(local_rank: int, local_world: int, tag: str, timeout: float = 10.0) -> tuple[list, list]:
     """(domains idle-first, their busy fractions), sampled ONCE per launch:
     local rank 0 samples and publishes the order in a small file named by
