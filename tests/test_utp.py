@@ -107,6 +107,38 @@ def test_utp_connect_timeout():
     asyncio.run(main())
 
 
+def test_listen_moves_to_a_port_free_for_tcp_and_udp(tmp_path):
+    """A listen port free on TCP but taken on UDP (a DHT node, another
+    worker's uTP) moves the torrent to another port pair instead of running
+    without uTP, as anacrolix's listenAll retries; a fixed port without the
+    fallback keeps TCP and reports uTP off."""
+    import socket
+
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"film.mkv": 100_000})
+        info = torrent_for(str(src / "film.mkv"), 65536)
+        udp = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        udp.bind(("127.0.0.1", 0))
+        taken = udp.getsockname()[1]
+        try:
+            t = Torrent(info.infohash, str(src), TorrentConfig(listen_host="127.0.0.1", seed=True,
+                                                               verify_device="cpu", utp=True,
+                                                               listen_port=taken), info=info)
+            await t.start()
+            assert t.utp is not None and t.port != taken and t.utp.port == t.port
+            await t.close()
+            fixed = Torrent(info.infohash, str(src), TorrentConfig(listen_host="127.0.0.1", seed=True,
+                                                                   verify_device="cpu", utp=True, listen_port=taken,
+                                                                   listen_port_fallback=False), info=info)
+            await fixed.start()
+            assert fixed.port == taken and fixed.utp is None
+            await fixed.close()
+        finally:
+            udp.close()
+    asyncio.run(asyncio.wait_for(main(), 30))
+
+
 def test_bittorrent_over_utp_only(tmp_path, monkeypatch):
     async def main():
         src = tmp_path / "src"

@@ -243,9 +243,13 @@ class Torrent:
         t.add_done_callback(self._tasks.discard)
         return t
 
+    async def _listen(self, port: int) -> None:
+        self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, port)
+        self.port = self._server.sockets[0].getsockname()[1]
+
     async def start(self) -> None:
         try:
-            self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, self.cfg.listen_port)
+            await self._listen(self.cfg.listen_port)
         except OSError as e:
             # anacrolix fails NewClient on a busy port; here one worker process can run
             # several torrents (and a node several workers), so the later ones take an
@@ -253,8 +257,29 @@ class Torrent:
             if not (self.cfg.listen_port and self.cfg.listen_port_fallback and e.errno == errno.EADDRINUSE):
                 raise
             log.with_fields(port=self.cfg.listen_port).info("bittorrent listen port busy; using an ephemeral port")
-            self._server = await asyncio.start_server(self._on_inbound, self.cfg.listen_host, 0)
-        self.port = self._server.sockets[0].getsockname()[1]
+            await self._listen(0)
+        if self.cfg.utp:
+            from .utp import UtpSocket
+            # uTP shares the TCP port number, as anacrolix/libutp do.  A port the
+            # kernel picked for TCP can be taken on UDP (a DHT node, another
+            # worker's uTP): then move both to another ephemeral port, as
+            # anacrolix's listenAll retries, instead of running without uTP
+            for attempt in range(16):
+                try:
+                    self.utp = await UtpSocket().start(self.cfg.listen_host, self.port)
+                    self._spawn(self._utp_accept_loop())
+                    break
+                except OSError as e:
+                    self.utp = None
+                    movable = e.errno == errno.EADDRINUSE and (not self.cfg.listen_port or
+                                                               self.cfg.listen_port_fallback)
+                    if not movable or attempt == 15:
+                        log.with_field("error", str(e)).warn("uTP disabled: cannot bind UDP port")
+                        break
+                    log.with_fields(port=self.port).debug("UDP port busy; moving to another port pair")
+                    self._server.close()
+                    await self._server.wait_closed()
+                    await self._listen(0)
         if self.cfg.listen_host6 is not None:
             # dual stack like anacrolix: the same port on IPv6, so peers learnt from the
             # IPv6 DHT / PEX (announced with this port) can dial in
@@ -267,14 +292,6 @@ class Torrent:
             except OSError as e:
                 log.with_field("error", str(e)).debug("IPv6 listen socket unavailable")
                 self._server6 = None
-        if self.cfg.utp:
-            from .utp import UtpSocket
-            try:  # uTP shares the TCP port number, as anacrolix/libutp do
-                self.utp = await UtpSocket().start(self.cfg.listen_host, self.port)
-                self._spawn(self._utp_accept_loop())
-            except OSError as e:
-                log.with_field("error", str(e)).warn("uTP disabled: cannot bind UDP port")
-                self.utp = None
         if self.cfg.upnp:
             from .portfwd import SSDP_ADDR, PortForwarder
             self.portfwd = PortForwarder(self.port, ssdp_addr=self.cfg.upnp_ssdp or SSDP_ADDR)

@@ -173,7 +173,11 @@ class UtpSocket:
         for opt in (socket.SO_RCVBUF, socket.SO_SNDBUF):
             with contextlib.suppress(OSError):
                 sock.setsockopt(socket.SOL_SOCKET, opt, 8 << 20)   # capped by rmem_max/wmem_max
-        sock.bind((host, port))
+        try:
+            sock.bind((host, port))
+        except OSError:
+            sock.close()
+            raise
         self._sock = sock
         self._pump = _utp.Pump(self.engine, sock.fileno())
         self.local_addr = sock.getsockname()[:2]
