@@ -124,3 +124,44 @@ def test_auto_verify_falls_back_to_the_host_when_the_helper_cannot_start(tmp_pat
     have = st.verify_existing("auto")
     assert have == set(range(info.num_pieces))
     assert hashing._gpu_disabled and not hashing.gpu_available()
+
+
+def test_helper_stuck_in_a_call_is_killed_and_auto_verify_uses_the_host(tmp_path, monkeypatch):
+    """A helper that never answers (a kernel that does not finish) is killed
+    after the call timeout; the call fails with HelperError, which the 'auto'
+    verify path answers by hashing on the host — the worker's executor
+    thread and job slot are not held forever."""
+    monkeypatch.setenv("TRITONDL_GPU_HELPER_FAKE", "1")
+    monkeypatch.setenv("TRITONDL_GPU_HELPER_FAKE_STALL", "60")
+    h = gpu_helper.GpuHelper(call_timeout=0.5)
+    files, _data, exp = _layout(tmp_path, [20_000], 16384)
+    try:
+        assert h.ping()                                  # pings are answered at once
+        pid = h.pid
+        t0 = time.monotonic()
+        with pytest.raises(gpu_helper.HelperError, match="did not answer"):
+            h.verify_files(files, 16384, exp)
+        assert time.monotonic() - t0 < 10
+        assert h.pid is None
+        with pytest.raises(OSError):
+            os.kill(pid, 0)                              # reaped, not left running
+    finally:
+        h.close()
+
+    from tritondl.fakes.swarm import make_payload
+    from tritondl.fetch.bt.metainfo import make_info
+    from tritondl.fetch.bt.storage import FileStorage
+    src = tmp_path / "src" / "T"
+    make_payload(str(src), {"a.mkv": 200_000})
+    info = make_info(str(src), 32768)
+    monkeypatch.setattr(hashing, "_kfd_gpus", lambda: 1)
+    monkeypatch.setattr(hashing, "_gpu_ext_present", lambda: True)
+    monkeypatch.setattr(hashing, "choose_device", lambda *a, **k: "gpu")
+    monkeypatch.setattr(hashing, "_helper", gpu_helper.GpuHelper(call_timeout=0.5))
+    monkeypatch.setattr(hashing, "_gpu_disabled", None)
+    try:
+        have = FileStorage(str(tmp_path / "src"), info).verify_existing("auto")
+        assert have == set(range(info.num_pieces))
+        assert hashing._gpu_disabled and "did not answer" in hashing._gpu_disabled
+    finally:
+        hashing._helper.close()

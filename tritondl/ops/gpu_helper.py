@@ -119,6 +119,9 @@ def _dispatch(h, req: dict, blob: bytes) -> tuple[dict, bytes]:
     stats = {}
     if op == "ping":
         return {"ok": True}, b""
+    stall = float(os.environ.get("TRITONDL_GPU_HELPER_FAKE_STALL", "0") or 0)
+    if stall > 0 and os.environ.get("TRITONDL_GPU_HELPER_FAKE") == "1":
+        time.sleep(stall)                                   # tests: a helper stuck in a call
     if op == "verify_files":
         data = h.verify_files(files, int(req["piece_len"]), blob, req.get("kind", "sha1"),
                               cpu_threads=int(req.get("cpu_threads", 0)))
@@ -143,8 +146,16 @@ class GpuHelper:
     again after it exits idle.  One request at a time (callers are executor
     threads)."""
 
-    def __init__(self, start_timeout: float = 120.0) -> None:
+    def __init__(self, start_timeout: float = 120.0, call_timeout: float | None = None) -> None:
+        """``call_timeout``: seconds a call may take before the helper is
+        killed and the call fails (:class:`HelperError`, which the "auto"
+        verify paths answer by hashing on the host), plus one second per
+        256 MB the call hashes.  Default ``TRITONDL_GPU_CALL_TIMEOUT`` (120):
+        a helper stuck in the GPU must not pin the worker's executor thread,
+        and the job slot with it, forever."""
         self.start_timeout = start_timeout
+        self.call_timeout = (float(os.environ.get("TRITONDL_GPU_CALL_TIMEOUT", "120") or 120)
+                             if call_timeout is None else call_timeout)
         self._p: subprocess.Popen | None = None
         self._lock = threading.Lock()
         self.spawned = 0
@@ -200,10 +211,18 @@ class GpuHelper:
                     self._spawn()
                 p = self._p
                 assert p is not None and p.stdin is not None and p.stdout is not None
+                work = len(blob) + sum(int(n) for _p, n in req.get("files", []))
+                limit = self.call_timeout + work / 256e6
                 try:
                     p.stdin.write((json.dumps({**req, "blob": len(blob)}) + "\n").encode())
                     p.stdin.write(blob)
                     p.stdin.flush()
+                    # one request at a time, so nothing of a later reply can sit in stdout's buffer
+                    if not select.select([p.stdout], [], [], limit)[0]:
+                        self._reap(p, kill=True)
+                        self._p = None
+                        raise HelperError(f"GPU helper did not answer {req.get('op')!r} within {limit:.0f}s; "
+                                          "killed it")
                     line = p.stdout.readline()
                     if not line:
                         raise EOFError("helper closed its pipe")

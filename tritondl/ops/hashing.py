@@ -171,7 +171,8 @@ _gpu_disabled: str | None = None
 
 def disable_gpu(reason: str) -> None:
     """Stop offering the GPU to ``device="auto"`` callers in this process (the
-    helper could not start: a broken HIP stack must not fail every resume)."""
+    helper could not start, or stopped answering: a broken HIP stack must not
+    fail every resume)."""
     global _gpu_disabled
     if _gpu_disabled is None:
         from ..utils.log import log
