@@ -148,10 +148,10 @@ def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_si
     jobs of 256 MiB and up (a 1 GiB job's ~9 CPUs of pump and hashing work
     does not fit one CCD: 7.7-8.4 jobs/s on one, 9.8-12.3 on two,
     ``profiles/r03_place_ab2/``); the fakes, which stand in for remote
-    endpoints, get the domain right after their rank's (``--fake-cpus auto``),
-    so on an idle 16-CCD node 8 ranks and their fakes pair up on the same
-    socket.  Domains are taken idle-first (sampled once per launch by local
-    rank 0): a shared host's busy CCDs go last."""
+    endpoints, get one more domain on the rank's NUMA node (``--fake-cpus
+    auto``, ``topology.pair_domains``), so on a 16-CCD node 8 ranks and their
+    fakes pair up within the sockets.  Domains are taken idle-first (sampled
+    once per launch by local rank 0): a shared host's busy CCDs go last."""
     from tritondl.parallel import topology
     fc: list[int] = []
     pinned: list[int] = []
@@ -453,6 +453,7 @@ def main() -> int:
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
+                       "malloc_policy": stack.svc.malloc_policy if stack.svc is not None else {},
                        **knobs},
             "jobs_per_rank": per_rank,
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),

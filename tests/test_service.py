@@ -705,3 +705,40 @@ def test_heap_trim_runs_periodically(tmp_path):
         await e.down()
         assert e.svc._trimmer is None or e.svc._trimmer.done()
     run(main())
+
+
+def test_malloc_policy_keeps_big_blocks_out_of_the_arenas():
+    """tune_malloc pins glibc's mmap threshold: after a 4 MiB block is freed
+    (which, left dynamic, raises the threshold to 4 MiB) a 1 MiB block is
+    still mmapped rather than carved from an arena.  Run in a child so this
+    process's heap policy is untouched."""
+    import subprocess
+    import sys
+    code = r"""
+import ctypes, sys
+from tritondl.service import tune_malloc
+libc = ctypes.CDLL("libc.so.6")
+libc.malloc.restype = ctypes.c_void_p
+libc.malloc.argtypes = [ctypes.c_size_t]
+libc.free.argtypes = [ctypes.c_void_p]
+class MI2(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_size_t) for n in ("arena", "ordblks", "smblks", "hblks", "hblkhd", "usmblks",
+                                               "fsmblks", "uordblks", "fordblks", "keepcost")]
+libc.mallinfo2.restype = MI2
+fixed = sys.argv[1] == "fixed"
+applied = tune_malloc(262144 if fixed else 0)
+libc.free(libc.malloc(4 << 20))
+before = libc.mallinfo2().hblks
+q = libc.malloc(1 << 20)
+print(applied, libc.mallinfo2().hblks - before)
+libc.free(q)
+"""
+    out = {}
+    for arm in ("fixed", "dynamic"):
+        p = subprocess.run([sys.executable, "-c", code, arm], capture_output=True, text=True, timeout=60,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert p.returncode == 0, p.stderr
+        out[arm] = p.stdout.split()[-1]
+        if arm == "fixed":
+            assert "262144" in p.stdout
+    assert out == {"fixed": "1", "dynamic": "0"}

@@ -238,6 +238,10 @@ class JobStack:
         cfg.progress_log_interval_s = 0
         cfg.heartbeat_s = self.heartbeat
         cfg.ca_file = endpoints.get("ca_file", "")
+        for var, attr in (("TRITONDL_MALLOC_MMAP_THRESHOLD", "malloc_mmap_threshold"),
+                          ("TRITONDL_MALLOC_ARENA_MAX", "malloc_arena_max")):
+            if os.environ.get(var):                # heap-policy A/B (Service.start applies it)
+                setattr(cfg, attr, int(os.environ[var]))
         if self.http_probe_bytes >= 0:
             cfg.http_probe_bytes = self.http_probe_bytes
         if self.http_segments > 0:

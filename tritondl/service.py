@@ -179,6 +179,7 @@ class Service:
         self._inflight = 0
         self._metrics_runner = None
         self._trimmer: asyncio.Task | None = None
+        self.malloc_policy: dict = {}              # what tune_malloc applied at start
         self._reaper = _Reaper()                    # deletes finished job dirs off the loop
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
         self.jobs_finished = 0                     # monotonic count of results recorded
@@ -286,6 +287,7 @@ class Service:
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
         cfg = self.cfg
+        self.malloc_policy = tune_malloc(cfg.malloc_mmap_threshold, cfg.malloc_arena_max)
         self._size_executor()
         if self.uploader is None:
             # NewUploader (downloader.go:95-98) was fatal on a bad S3_ENDPOINT: validate
@@ -729,6 +731,32 @@ class Service:
         await self.start()
         await stop.wait()
         await self.shutdown()
+
+
+def tune_malloc(mmap_threshold: int, arena_max: int = 0) -> dict:
+    """Fix glibc's heap policy for a long-running process with many native
+    threads (``mallopt``; a no-op elsewhere).  ``mmap_threshold > 0`` pins
+    M_MMAP_THRESHOLD, which also turns off glibc's dynamic adjustment: left
+    dynamic it rises to the largest block ever freed, so MiB-sized buffers
+    are then carved from per-thread arenas that keep up to twice the
+    threshold free at their top.  A 6-minute soak (TLS, DHT, heartbeats):
+    arenas 102.6 MB and RSS 160 MB dynamic, 25 MB and 82 MB with 256 KiB,
+    heap in use 14.7 MB in both (``profiles/r04_malloc/``).  Returns what
+    was applied."""
+    import ctypes
+    out: dict = {}
+    try:
+        mallopt = ctypes.CDLL("libc.so.6").mallopt
+    except (OSError, AttributeError):
+        return out
+    mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
+    mallopt.restype = ctypes.c_int
+    M_MMAP_THRESHOLD, M_ARENA_MAX = -3, -8
+    if mmap_threshold > 0 and mallopt(M_MMAP_THRESHOLD, int(mmap_threshold)):
+        out["mmap_threshold"] = int(mmap_threshold)
+    if arena_max > 0 and mallopt(M_ARENA_MAX, int(arena_max)):
+        out["arena_max"] = int(arena_max)
+    return out
 
 
 def _malloc_trim():

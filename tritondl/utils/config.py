@@ -80,6 +80,12 @@ class Config:
     drop_failed: bool = False                   # opt-out: nack (drop) after max_retries instead of dead-lettering
     # give glibc's free arena memory back to the OS this often (0: never); see Service._trim_heap
     malloc_trim_s: float = 60.0
+    # glibc's mmap threshold, fixed (bytes; 0 = glibc's dynamic default).  Dynamic, it
+    # climbs to the size of the largest freed block (MiB-sized pump and hash buffers),
+    # after which every smaller block lands in a per-thread arena that keeps up to twice
+    # that free: a soak's arenas held ~100 MB for 15 MB in use (Service._tune_malloc)
+    malloc_mmap_threshold: int = 256 * 1024
+    malloc_arena_max: int = 0                   # glibc M_ARENA_MAX (0: glibc default, 8 per core)
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
@@ -196,7 +202,8 @@ class Config:
                 "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
                 "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
                 "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
-                "RECYCLE_BYTES": "recycle_bytes"}
+                "RECYCLE_BYTES": "recycle_bytes", "MALLOC_MMAP_THRESHOLD": "malloc_mmap_threshold",
+                "MALLOC_ARENA_MAX": "malloc_arena_max"}
         floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
                   "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
                   "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
