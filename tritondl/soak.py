@@ -159,10 +159,18 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    file_size: int = 10 << 20, torrent_mb: int = 8, max_retries: int = 2, warmup: int = 0,
                    on_sample=None, workdir: str | None = None, *, minutes: float = 0.0, rate: float = 0.0,
                    sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
-                   torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None) -> dict:
+                   torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None,
+                   tracemalloc_frames: int = 0) -> dict:
     """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
-    ``rate`` jobs/s (0: as fast as the worker goes)."""
+    ``rate`` jobs/s (0: as fast as the worker goes).  ``tracemalloc_frames``
+    > 0 traces Python allocations: the summary then lists the call sites
+    whose live memory grew most from the first post-warm-up sample to the
+    end (``tracemalloc_growth``)."""
+    import tracemalloc
     timed = minutes > 0
+    base_snap = None
+    if tracemalloc_frames > 0:
+        tracemalloc.start(tracemalloc_frames)
     st = JobStack(file_size=file_size, tag="soak", workdir=workdir, tls=tls, heartbeat=heartbeat,
                   content_check=True)
     if malloc_trim_s is not None:
@@ -229,10 +237,15 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                                    Properties(delivery_mode=2, content_type="application/octet-stream"))
 
         def take_sample() -> None:
+            nonlocal base_snap
             gc.collect()
             s = sample(svc)
             s["jobs"] = svc.jobs_finished - base
             s["minute"] = round((time.monotonic() - t0) / 60, 2)
+            if tracemalloc.is_tracing():
+                s["traced_mb"] = round(tracemalloc.get_traced_memory()[0] / 2**20, 2)
+                if base_snap is None and s["minute" if timed else "jobs"] >= warmup:
+                    base_snap = tracemalloc.take_snapshot()
             samples.append(s)
             if on_sample is not None:
                 on_sample(s)
@@ -273,6 +286,13 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    "attempts": n_att, "ok_attempts": ok, "seconds": round(dt, 2),
                    "jobs_per_sec": round(len(kinds) / dt, 1), "samples": samples,
                    "drift": drift(samples, warmup, "minute" if timed else "jobs")}
+        if base_snap is not None:
+            grown = tracemalloc.take_snapshot().compare_to(base_snap, "traceback")
+            summary["tracemalloc_growth"] = [
+                {"kb": round(g.size_diff / 1024, 1), "blocks": g.count_diff,
+                 "where": [f"{fr.filename.rsplit('/', 2)[-2:]}:{fr.lineno}".replace("'", "") for fr in g.traceback][-4:]}
+                for g in grown[:15]]
+            tracemalloc.stop()
         if timed:
             summary.update(minutes=minutes, rate=rate, tls=tls, heartbeat=heartbeat, retry_delay=retry_delay,
                            dht_nodes=dht_nodes, reconnects=svc.amqp.reconnects if svc.amqp is not None else None)
@@ -309,6 +329,8 @@ def main() -> int:
     ap.add_argument("--tls", action="store_true", help="origin and S3 over https")
     ap.add_argument("--dht-nodes", type=int, default=0, help="local DHT nodes the worker bootstraps from")
     ap.add_argument("--malloc-trim", type=float, default=None, help="worker's malloc_trim period (s; 0 = off)")
+    ap.add_argument("--tracemalloc", type=int, default=0,
+                    help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
     if a.cpus:
         from .parallel import topology
@@ -332,7 +354,7 @@ def main() -> int:
                                    on_sample=emit, minutes=a.minutes, rate=a.rate, sample_seconds=a.sample_seconds,
                                    tls=a.tls, heartbeat=a.heartbeat, retry_delay=a.retry_delay,
                                    torrent_every=a.torrent_every, dht_nodes=a.dht_nodes,
-                                   malloc_trim_s=a.malloc_trim))
+                                   malloc_trim_s=a.malloc_trim, tracemalloc_frames=a.tracemalloc))
     finally:
         if fh is not None:
             fh.close()
