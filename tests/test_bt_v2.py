@@ -10,10 +10,10 @@ import os
 import pytest
 
 from tritondl.fakes.origin import Origin
-from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_file_bytes
+from tritondl.fakes.swarm import Seeder, make_payload, torrent_file_bytes
 from tritondl.fetch.bt import merkle
 from tritondl.fetch.bt.client import TorrentDownloader
-from tritondl.fetch.bt.metainfo import Info, Metainfo, MetainfoError, make_info, parse_magnet
+from tritondl.fetch.bt.metainfo import Metainfo, MetainfoError, make_info, parse_magnet
 from tritondl.fetch.bt.torrent import TorrentConfig
 from tritondl.ops import hashing
 

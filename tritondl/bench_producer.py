@@ -31,7 +31,6 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
-import os
 import resource
 import sys
 import time

@@ -29,7 +29,6 @@ import errno
 import functools
 import hashlib
 import heapq
-import math
 import os
 import random
 import socket

@@ -17,7 +17,7 @@ without a rebuild (``TRITONDL_MEDIA_FIELDS="id=1,source_uri=7"``,
 
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from enum import IntEnum
 
 import os
