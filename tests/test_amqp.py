@@ -414,3 +414,50 @@ def test_fake_broker_heartbeats_both_ways():
         assert not b.conns and b.stats["heartbeat_timeouts"] == 1
         await b.stop()
     aio.run(aio.wait_for(main(), 30))
+
+
+def test_channel_housekeeping_methods():
+    """The rest of the channel surface against the fake broker: purge,
+    cancel, recover, unbind and exchange delete behave as RabbitMQ's."""
+    async def main():
+        b = await Broker().start()
+        conn = await Connection.open(b.url)
+        ch = await conn.channel()
+        await ch.exchange_declare("hk", "direct", durable=True)
+        await ch.queue_declare("hk-q", durable=True)
+        await ch.queue_bind("hk-q", "hk", "hk-q")
+        await ch.confirm_select()
+        for i in range(3):
+            await ch.basic_publish("hk", "hk-q", b"x%d" % i)
+        assert await ch.queue_purge("hk-q") == 3
+        assert b.queue_depth("hk-q") == 0
+        # a cancelled consumer gets nothing more; recover hands its unacked delivery back
+        cch = await conn.channel()
+        got = []
+        tag = await cch.basic_consume("hk-q", got.append)
+        await ch.basic_publish("hk", "hk-q", b"first")
+        for _ in range(50):
+            if got:
+                break
+            await asyncio.sleep(0.01)
+        await cch.basic_cancel(tag)
+        await ch.basic_publish("hk", "hk-q", b"second")
+        await asyncio.sleep(0.05)
+        assert [m.body for m in got] == [b"first"]
+        await cch.basic_recover(requeue=True)
+        for _ in range(50):
+            if b.queue_depth("hk-q") == 2:
+                break
+            await asyncio.sleep(0.01)
+        assert b.queue_depth("hk-q") == 2
+        # unbound: the routing key no longer reaches the queue
+        await ch.queue_unbind("hk-q", "hk", "hk-q")
+        await ch.basic_publish("hk", "hk-q", b"dropped")
+        assert b.queue_depth("hk-q") == 2
+        await ch.exchange_delete("hk")
+        with pytest.raises(ChannelClosed) as e:
+            await ch.exchange_declare("hk", "direct", passive=True)
+        assert e.value.code == codec.NOT_FOUND
+        await conn.close()
+        await b.stop()
+    run(main())

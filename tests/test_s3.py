@@ -139,6 +139,12 @@ def test_put_get_roundtrip_modes(tmp_path, mode):
         assert await c.get_object("b", key) == data
         assert srv.object_bytes("b", key) == data
         assert await c.list_objects("b", "id/") == [key]
+        head = {k.lower(): v for k, v in (await c.stat_object("b", key)).items()}
+        assert int(head["content-length"]) == len(data) and head["etag"].strip('"') == etag
+        await c.delete_object("b", key)
+        assert await c.list_objects("b", "id/") == []
+        with pytest.raises(S3Error):
+            await c.stat_object("b", key)
         await c.close()
         await srv.stop()
     run(main())

@@ -13,7 +13,6 @@ share one codec.
 
 from __future__ import annotations
 
-import asyncio
 import struct
 from dataclasses import dataclass, field
 from datetime import datetime, timezone
@@ -586,26 +585,3 @@ class FrameParser:
         if pos:
             del buf[:pos]
         return out
-
-
-async def read_frames(reader, parser: FrameParser) -> list[tuple[int, int, bytes]]:
-    """At least one complete frame (all that one socket read delivered)."""
-    while True:
-        data = await reader.read(1 << 16)
-        if not data:
-            raise asyncio.IncompleteReadError(b"", None)
-        frames = parser.feed(data)
-        if frames:
-            return frames
-
-
-async def read_frame(reader, frame_max: int = 0) -> tuple[int, int, bytes]:
-    """Read one frame from an asyncio.StreamReader."""
-    hdr = await reader.readexactly(7)
-    ftype, ch, size = struct.unpack(">BHI", hdr)
-    if frame_max and size > frame_max:
-        raise FrameError(f"frame size {size} exceeds frame_max {frame_max}")
-    payload = await reader.readexactly(size + 1)
-    if payload[-1] != FRAME_END:
-        raise FrameError("missing frame-end octet")
-    return ftype, ch, payload[:-1]

@@ -19,7 +19,7 @@ import ssl
 import struct
 import time
 from dataclasses import dataclass
-from typing import Any, Awaitable, Callable
+from typing import Any, Callable
 from urllib.parse import unquote, urlparse
 
 from . import codec
@@ -43,10 +43,6 @@ class ChannelClosed(AMQPError):
 
 
 class PublishNacked(AMQPError):
-    pass
-
-
-class Returned(AMQPError):
     pass
 
 
@@ -702,11 +698,6 @@ class Channel:
 
     async def basic_recover(self, requeue: bool = True) -> None:
         await self._rpc(Method("basic.recover", {"requeue": requeue}), "basic.recover_ok")
-
-
-async def gather_confirms(futs: list[Awaitable]) -> None:
-    for f in futs:
-        await f
 
 
 __all__ = ["Connection", "Channel", "Message", "ConnectionClosed", "ChannelClosed", "PublishNacked",

@@ -164,14 +164,6 @@ class FileStorage:
             out += os.pread(self._fds[i], n, fofs) if i in self._fds else bytes(n)
         return bytes(out)
 
-    def read_piece(self, piece: int) -> bytes:
-        return self.read(piece, 0, self.info.piece_size(piece))
-
-    def verify_piece(self, piece: int, data: bytes | None = None) -> bool:
-        if data is None:
-            data = self.read_piece(piece)
-        return hashing.digest("sha1", data) == self.info.piece_hash(piece)
-
     def verify_existing(self, device: str = "auto") -> set[int]:
         """Hash every piece on disk in one batch; returns the verified set and
         records it in the completion DB."""

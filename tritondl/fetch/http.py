@@ -755,9 +755,6 @@ class DownloadHandle:
                 break
         return w
 
-    def _progressed(self) -> None:
-        self._event.set()
-
     def _advance(self, i: int, done: int) -> None:
         if self.flow is not None:
             self.flow.advance(i, done)

@@ -116,16 +116,6 @@ def l3_domains(allowed: list[int] | None = None, sysfs: str = "/sys/devices/syst
     return sorted((sorted(g) for g in groups.values()), key=lambda g: g[0])
 
 
-def cpu_quota() -> float | None:
-    """CPUs' worth of time the cgroup allows (``cpu.max``), None if unlimited."""
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            quota, period = f.read().split()[:2]
-        return None if quota == "max" else int(quota) / int(period)
-    except (OSError, ValueError):
-        return None
-
-
 def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> list[int]:
     """``n`` CPUs packed into as few last-level-cache domains as possible;
     ``index`` selects the index-th such set (one per rank), wrapping round.

@@ -9,13 +9,9 @@ Also replaces the reference's broken publish backoff (``Backoff ^ 2`` XOR,
 
 from __future__ import annotations
 
-import asyncio
 import random
 import time
 from dataclasses import dataclass
-from typing import Awaitable, Callable, TypeVar
-
-T = TypeVar("T")
 
 
 class BackoffExhausted(Exception):
@@ -46,21 +42,3 @@ class ExponentialBackoff:
         d = random.uniform(cur - delta, cur + delta)
         self._current = min(cur * self.multiplier, self.max_interval)
         return d
-
-
-async def retry_async(fn: Callable[[], Awaitable[T]], policy: ExponentialBackoff | None = None,
-                      on_error: Callable[[BaseException, float], None] | None = None,
-                      retry_on: tuple = (Exception,)) -> T:
-    """backoff.Retry equivalent for coroutines."""
-    policy = policy or ExponentialBackoff()
-    policy.reset()
-    while True:
-        try:
-            return await fn()
-        except retry_on as e:  # type: ignore[misc]
-            d = policy.next_delay()
-            if d is None:
-                raise BackoffExhausted(str(e)) from e
-            if on_error:
-                on_error(e, d)
-            await asyncio.sleep(d)

@@ -91,9 +91,6 @@ class Logger:
         d.update(kw)
         return Entry(self, d)
 
-    def with_error(self, err: BaseException) -> "Entry":
-        return Entry(self, {"error": str(err)})
-
     def enabled(self, level: str) -> bool:
         """Would a record at ``level`` be emitted?  (Guards costly field building.)"""
         return LEVELS[level] <= self.level

@@ -641,16 +641,6 @@ def client_tls_context(ca_file: str = "", verify: bool = True):
     return ctx
 
 
-def register_client_ca(ca_pem: str):
-    """Client context trusting ``ca_pem`` (tests / fakes with a throwaway CA);
-    replaces the default context for this process."""
-    relay = relay_module()
-    ctx = relay.TlsContext.client(ca_pem=ca_pem)
-    _client_tls[("", True)] = ctx
-    _client_tls[(os.environ.get("TRITONDL_CA_FILE", ""), True)] = ctx
-    return ctx
-
-
 def request_head(method: str, target: str, headers: dict) -> bytes:
     lines = [f"{method} {target} HTTP/1.1"]
     lines += [f"{k}: {v}" for k, v in headers.items()]
