@@ -51,6 +51,9 @@ async def main() -> int:
                     help="--job: cap the fake S3's ingest link (Gbit/s; 0 = loopback speed)")
     ap.add_argument("--cpus", default="", help="pin the leecher (worker) to this cpulist")
     ap.add_argument("--fake-cpus", default="", help="pin the seeder (and fake S3) processes to this cpulist")
+    ap.add_argument("--malloc-mmap-threshold", type=int, default=-1,
+                    help="glibc mmap threshold for the leecher (0: glibc's dynamic default; -1: the worker "
+                         "default, which the plain download form leaves to glibc)")
     a = ap.parse_args()
     if a.fake_cpus:
         os.environ["TRITONDL_BENCH_FAKE_CPUS"] = a.fake_cpus   # the fakes pin themselves (topology.pin_from_env)
@@ -61,6 +64,9 @@ async def main() -> int:
         os.environ["TRITONDL_BT_NATIVE_WIRE"] = "0"     # read by the seeder processes (fakes/serve.py)
     if a.job:
         return await job_bench(a)
+    if a.malloc_mmap_threshold > 0:
+        from tritondl.service import tune_malloc
+        tune_malloc(a.malloc_mmap_threshold)
     from tritondl.bench_job import Backend
     from tritondl.fakes.swarm import make_payload
     from tritondl.fetch.bt.client import TorrentDownloader
@@ -157,6 +163,8 @@ async def job_bench(a) -> int:
         cfg.cleanup, cfg.max_retries, cfg.retry_delay_s = True, 0, 0.0
         cfg.recycle_bytes = int(os.environ.get("TRITONDL_RECYCLE_BYTES", cfg.recycle_bytes))
         cfg.progress_log_interval_s, cfg.heartbeat_s = 0, 0
+        if a.malloc_mmap_threshold >= 0:
+            cfg.malloc_mmap_threshold = a.malloc_mmap_threshold
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
                                              encryption=a.encryption, native_wire=not a.python_wire),
                                progress_interval=1.0, use_dht=False)
