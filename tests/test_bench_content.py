@@ -166,3 +166,16 @@ def test_https_stack_checks_content(tmp_path):
         finally:
             await st.teardown()
     run(main())
+
+
+def test_variant_key_with_a_slash_in_its_base64_name_is_checked():
+    """An object key's base64 file name may contain "/" (std alphabet): the
+    fake S3 still finds the variant, so such a PUT is content-checked."""
+    import base64
+
+    from tritondl.fakes.payload import Expectations
+    e = Expectations(100_000, 4)
+    name = "\xff\xfe-movie-3-v2.mkv"
+    enc = base64.b64encode(name.encode()).decode()
+    assert "/" in enc
+    assert e.expected_for_key("id1/original/" + enc, 100_000) == e.get(2)

@@ -90,7 +90,8 @@ class Expectations:
         (``uploader.go:86-89``) or a plain file name."""
         import base64
         import binascii
-        last = key.rsplit("/", 1)[-1]
+        # the std alphabet can put "/" inside the encoded name (SURVEY Appendix A.4)
+        last = key.split("/original/", 1)[1] if "/original/" in key else key.rsplit("/", 1)[-1]
         try:
             name = base64.b64decode(last, validate=True).decode()
         except (binascii.Error, UnicodeDecodeError, ValueError):
