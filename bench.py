@@ -220,6 +220,9 @@ def main() -> int:
                     help="multi-rank: every rank gets a private broker (default: one shared broker, "
                          "competing consumers)")
     ap.add_argument("--dist-backend", default="", help="torch.distributed backend (default nccl with a GPU)")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="set up torch.distributed (RCCL with a GPU) and do the closing max-reduce over it even "
+                         "for one rank: exercises the multi-GPU path's collectives on a one-GPU box")
     ap.add_argument("--log-level", default="warning")
     ap.add_argument("--s3-hash-device", default="cpu", choices=["cpu", "gpu"],
                     help="aws-chunked chunk SHA-256s on SHA-NI (default) or the HIP kernel")
@@ -270,14 +273,17 @@ def main() -> int:
     if cuda:
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     ctl = None
-    if world > 1:
-        dist.init_process_group(backend)
+    use_dist = world > 1 or a.dist_always
+    if use_dist:
+        import datetime
+        # a collective that cannot complete aborts the run in minutes, not at the driver's limit
+        dist.init_process_group(backend, timeout=datetime.timedelta(minutes=5))
         # control plane (endpoint exchange, phase barriers from a helper thread): gloo
         ctl = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
     shared = world > 1 and not a.isolated
 
     def barrier() -> None:
-        if world > 1:
+        if use_dist:
             dist.barrier(group=ctl)
         if cuda:
             torch.cuda.synchronize()
@@ -406,8 +412,8 @@ def main() -> int:
         loop.run_until_complete(stack.teardown())
         loop.close()
 
-    t = torch.tensor([elapsed, float(failed)], dtype=torch.float64, device="cuda" if cuda and world > 1 else "cpu")
-    if world > 1:
+    t = torch.tensor([elapsed, float(failed)], dtype=torch.float64, device="cuda" if cuda and use_dist else "cpu")
+    if use_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)        # RCCL on the GPU node
     max_elapsed = float(t[0].item())
     if int(t[1].item()):
@@ -454,6 +460,8 @@ def main() -> int:
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
                        "malloc_policy": stack.svc.malloc_policy if stack.svc is not None else {},
+                       # the closing max-reduce (RCCL on GPU nodes) and the gloo control group
+                       "collectives": (f"{backend} max-reduce + gloo control" if use_dist else "none (one rank)"),
                        **knobs},
             "jobs_per_rank": per_rank,
             "ingest_MB_per_sec": round(jobs_per_sec * file_size / 1e6, 1),
@@ -476,7 +484,7 @@ def main() -> int:
             res["harness_bound"] = True
         res.update(extra)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     return 0
 
