@@ -64,6 +64,21 @@ def test_bench_two_ranks_torchrun_gloo():
     assert d["config"]["topology"].startswith("one shared broker")
     assert len(d["jobs_per_rank"]) == 2 and all(n > 0 for n in d["jobs_per_rank"]), d["jobs_per_rank"]
     assert sum(d["jobs_per_rank"]) == 2 * 3
+    assert d["config"]["collectives"].startswith("gloo max-reduce")
+
+
+def test_bench_dist_always_one_rank():
+    """--dist-always runs the multi-rank collective path (process group,
+    gloo control group, closing max-reduce) with a single rank — what a
+    one-GPU box can exercise of the RCCL path."""
+    port = _free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--dist-always",
+                        "--steps", "3", "--warmup", "1", "--file-mb", "1", "--no-gpu-probe"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["n_gpus"] == 1 and d["config"]["collectives"].startswith("gloo max-reduce")
 
 
 def test_bench_tls_json():
