@@ -139,6 +139,13 @@ def drift(samples: list[dict], warmup: int, key: str = "jobs") -> dict:
             continue
         out[k] = {"from": a[k], "to": b[k], "max": max(s[k] for s in after if s.get(k) is not None)}
     out["rss_drift_pct"] = round(100 * (b["rss_mb"] - a["rss_mb"]) / max(a["rss_mb"], 1e-9), 2)
+    # the same from the medians of the first and last `w` post-warm-up samples: a
+    # single sample can land on a job in flight (a torrent's pieces, a retry burst)
+    w = max(1, min(5, len(after) // 4))
+    med = lambda xs: sorted(xs)[len(xs) // 2]                   # noqa: E731
+    m0, m1 = med([s["rss_mb"] for s in after[:w]]), med([s["rss_mb"] for s in after[-w:]])
+    out["rss_median_window"] = {"samples": w, "from": m0, "to": m1,
+                                "drift_pct": round(100 * (m1 - m0) / max(m0, 1e-9), 2)}
     return out
 
 
