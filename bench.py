@@ -91,6 +91,24 @@ def _gpu_hash_probe(total_mb: int = 4096) -> dict:
 _PLACEMENT: dict = {}
 
 
+def _memcpy_gbps(mb: int = 64, reps: int = 4) -> float | None:
+    """Single-thread copy bandwidth on this rank's CPUs (best of ``reps``
+    copies of ``mb`` MiB, GB/s of bytes copied): a co-tenant saturating the
+    socket's memory shows up here, where CCD busy shares do not."""
+    try:
+        import numpy as np
+        a = np.ones(mb << 20, dtype=np.uint8)
+        b = np.empty_like(a)
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            np.copyto(b, a)
+            best = min(best, time.perf_counter() - t0)
+        return round(a.nbytes / best / 1e9, 1)
+    except Exception:  # noqa: BLE001 - diagnostics only
+        return None
+
+
 def _cpu_mhz(cpus: list[int]) -> dict | None:
     """Current clock of the given CPUs (cpufreq, else /proc/cpuinfo): min/mean/max MHz."""
     vals: list[float] = []
@@ -350,6 +368,7 @@ def main() -> int:
         stack.cpu_seconds()              # first call imports psutil: keep it out of the profiled window
         import resource
         mhz0 = _cpu_mhz(pinned) if pinned else None
+        mem0 = _memcpy_gbps()
         barrier()
         if prof is not None:
             prof.start()
@@ -373,6 +392,7 @@ def main() -> int:
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         cpu1 = stack.cpu_seconds()
         mhz1 = _cpu_mhz(pinned) if pinned else None
+        mem1 = _memcpy_gbps()
         if loop_prof is not None:
             loop_prof.disable()
             loop_prof.dump_stats(os.environ["TRITONDL_BENCH_LOOP_PROFILE"])
@@ -390,6 +410,7 @@ def main() -> int:
                                     "first": round(done[0].seconds * 1000, 2),
                                     "last": round(done[-1].seconds * 1000, 2)} if done else None),
                 "cpu_mhz_pinned": {"start": mhz0, "end": mhz1},
+                "memcpy_GBps": {"start": mem0, "end": mem1},
                 # jobs slower than 3x the median (and 10 ms): index in the timed run, ms, stage marks
                 "slow_jobs": ([{"i": i, "ms": round(r.seconds * 1000, 1),
                                 "marks": {k: round(v * 1000, 1) for k, v in r.marks.items()}}
