@@ -45,3 +45,18 @@ def test_time_based_soak_cycles_timers(tmp_path):
     last = res["samples"][-1]
     assert last["tls_sessions"] >= 1 and last["dht_nodes"] >= 1
     assert len(res["samples"]) >= 3
+
+
+def test_drift_reports_point_and_median_window():
+    """drift(): the first-vs-last post-warm-up change, and the same from the
+    medians of the first and last few samples (one sample taken while a
+    big job is in flight cannot fake a trend)."""
+    from tritondl.soak import drift
+    rss = [60, 80, 90, 91, 90, 92, 91, 99, 90, 91, 92, 91, 90, 98]
+    samples = [{"minute": i, "rss_mb": v, "fds": 30} for i, v in enumerate(rss)]
+    d = drift(samples, 2, "minute")
+    assert d["rss_mb"] == {"from": 90, "to": 98, "max": 99}
+    assert d["rss_drift_pct"] == round(100 * 8 / 90, 2)
+    w = d["rss_median_window"]
+    assert w["samples"] == 3 and (w["from"], w["to"]) == (90, 91) and w["drift_pct"] == 1.11
+    assert d["fds"] == {"from": 30, "to": 30, "max": 30}
