@@ -1,0 +1,46 @@
+"""docs/CONFIG.md lists every environment variable the worker reads, and is
+regenerated from tritondl/utils/config.py (tools/gen_config_doc.py)."""
+
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_config_doc_is_current():
+    r = subprocess.run([sys.executable, "tools/gen_config_doc.py", "--check"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+
+
+def test_every_env_name_in_the_sources_is_documented():
+    doc = open(os.path.join(ROOT, "docs", "CONFIG.md")).read()
+    names = set()
+    for top in ("tritondl", "csrc"):
+        for dirpath, _dirs, files in os.walk(os.path.join(ROOT, top)):
+            for f in files:
+                if f.endswith((".py", ".h", ".cpp", ".hip")):
+                    with open(os.path.join(dirpath, f), errors="replace") as fh:
+                        names |= set(re.findall(r"TRITONDL_[A-Z0-9_]*[A-Z0-9]", fh.read()))
+    missing = sorted(n for n in names if f"`{n}`" not in doc)
+    assert not missing, missing
+
+
+def test_every_mapped_setting_parses():
+    """Each TRITONDL_<KEY> in the maps reaches its Config field."""
+    from tritondl.utils import config as C
+    env = {}
+    for k in C.ENV_INTS:
+        env["TRITONDL_" + k] = "7"
+    for k in C.ENV_FLOATS:
+        env["TRITONDL_" + k] = "2.5"
+    for k in C.ENV_BOOLS:
+        env["TRITONDL_" + k] = "0" if getattr(C.Config(), C.ENV_BOOLS[k]) else "1"
+    env["TRITONDL_S3_HASH_DEVICE"], env["TRITONDL_BT_ENCRYPTION"] = "gpu", "require"
+    c = C.Config.from_env(env)
+    assert all(getattr(c, f) == 7 for f in C.ENV_INTS.values())
+    assert all(getattr(c, f) == 2.5 for f in C.ENV_FLOATS.values())
+    assert all(getattr(c, f) != getattr(C.Config(), f) for f in C.ENV_BOOLS.values())
+    assert (c.s3_hash_device, c.bt_encryption) == ("gpu", "require")

@@ -41,6 +41,45 @@ def _default_sign_threads() -> int:
     return max(2, min(4, n // 2))
 
 
+# Worker settings under TRITONDL_<KEY> (values the reference hard-codes, and
+# this worker's own knobs): key -> Config field.  docs/CONFIG.md is generated
+# from these (tools/gen_config_doc.py) and kept in sync by a test.
+ENV_INTS = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES": "num_shard_queues",
+            "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port",
+            "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
+            "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
+            "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
+            "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
+            "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
+            "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
+            "RECYCLE_BYTES": "recycle_bytes", "MALLOC_MMAP_THRESHOLD": "malloc_mmap_threshold",
+            "MALLOC_ARENA_MAX": "malloc_arena_max"}
+ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
+              "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
+              "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
+              "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
+              "MALLOC_TRIM": "malloc_trim_s"}
+ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
+            "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
+            "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
+            "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file", "S3_HASH_DEVICE": "s3_hash_device",
+            "CPUS": "cpus"}
+ENV_BOOLS = {"CLEANUP": "cleanup", "DROP_FAILED": "drop_failed", "DECLARE_PUBLISH": "declare_publish",
+             "DECLARE_PUBLISH_QUEUES": "declare_publish_queues", "STREAM_UPLOAD": "stream_upload",
+             "PIPELINE_COMMIT": "pipeline_commit", "BT_DHT": "bt_dht", "BT_DHT_IPV6": "bt_dht_ipv6",
+             "BT_UPNP": "bt_upnp", "BT_NATIVE_WIRE": "bt_native_wire", "BT_UTP": "bt_utp", "BT_PEX": "bt_pex"}
+# The reference's own variables, same names: name -> Config field
+REFERENCE_ENV = {"LOG_LEVEL": "log_level", "LOG_FORMAT": "log_format", "RABBITMQ_ENDPOINT": "rabbitmq_endpoint",
+                 "RABBITMQ_USERNAME": "rabbitmq_username", "RABBITMQ_PASSWORD": "rabbitmq_password",
+                 "S3_ENDPOINT": "s3_endpoint", "S3_ACCESS_KEY": "s3_access_key", "S3_SECRET_KEY": "s3_secret_key",
+                 "AWS_ACCESS_KEY_ID": "aws_access_key_id", "AWS_SECRET_ACCESS_KEY": "aws_secret_access_key",
+                 "AWS_SESSION_TOKEN": "aws_session_token", "MINIO_ACCESS_KEY": "minio_access_key",
+                 "MINIO_SECRET_KEY": "minio_secret_key"}
+# Accepted beyond the reference: RABBITMQ_VHOST, S3_REGION, AWS_ACCESS_KEY / AWS_SECRET_KEY (minio-go aliases)
+EXTRA_ENV = {"RABBITMQ_VHOST": "rabbitmq_vhost", "S3_REGION": "s3_region",
+             "AWS_ACCESS_KEY": "aws_access_key_id", "AWS_SECRET_KEY": "aws_secret_access_key"}
+
+
 @dataclass
 class Config:
     # --- logging / profiling (downloader.go:26,45-52) ---
@@ -83,7 +122,7 @@ class Config:
     # glibc's mmap threshold, fixed (bytes; 0 = glibc's dynamic default).  Dynamic, it
     # climbs to the size of the largest freed block (MiB-sized pump and hash buffers),
     # after which every smaller block lands in a per-thread arena that keeps up to twice
-    # that free: a soak's arenas held ~100 MB for 15 MB in use (Service._tune_malloc)
+    # that free: a soak's arenas held ~100 MB for 15 MB in use (service.tune_malloc)
     malloc_mmap_threshold: int = 256 * 1024
     malloc_arena_max: int = 0                   # glibc M_ARENA_MAX (0: glibc default, 8 per core)
     # a delivery whose job dir another worker holds waits this long, then goes back to
@@ -194,47 +233,17 @@ class Config:
         c.minio_access_key = g("MINIO_ACCESS_KEY", "")
         c.minio_secret_key = g("MINIO_SECRET_KEY", "")
         # Extensions (TRITONDL_*) for values the reference hard-codes.
-        ints = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES": "num_shard_queues",
-                "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port",
-                "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
-                "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
-                "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
-                "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
-                "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
-                "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
-                "RECYCLE_BYTES": "recycle_bytes", "MALLOC_MMAP_THRESHOLD": "malloc_mmap_threshold",
-                "MALLOC_ARENA_MAX": "malloc_arena_max"}
-        floats = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
-                  "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
-                  "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
-                  "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
-                  "MALLOC_TRIM": "malloc_trim_s"}
-        strs = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
-                "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
-                "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
-                "BT_ENCRYPTION": "bt_encryption", "CA_FILE": "ca_file", "S3_HASH_DEVICE": "s3_hash_device",
-                "CPUS": "cpus"}
-        for k, a in ints.items():
+        for k, a in ENV_INTS.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, int(g("TRITONDL_" + k)))
-        for k, a in floats.items():
+        for k, a in ENV_FLOATS.items():
             if g("TRITONDL_" + k):
                 setattr(c, a, float(g("TRITONDL_" + k)))
-        for k, a in strs.items():
+        for k, a in ENV_STRS.items():
             if g("TRITONDL_" + k) is not None and g("TRITONDL_" + k) != "":
                 setattr(c, a, g("TRITONDL_" + k))
-        c.cleanup = _env_bool(g("TRITONDL_CLEANUP"), c.cleanup)
-        c.drop_failed = _env_bool(g("TRITONDL_DROP_FAILED"), c.drop_failed)
-        c.declare_publish = _env_bool(g("TRITONDL_DECLARE_PUBLISH"), c.declare_publish)
-        c.declare_publish_queues = _env_bool(g("TRITONDL_DECLARE_PUBLISH_QUEUES"), c.declare_publish_queues)
-        c.stream_upload = _env_bool(g("TRITONDL_STREAM_UPLOAD"), c.stream_upload)
-        c.pipeline_commit = _env_bool(g("TRITONDL_PIPELINE_COMMIT"), c.pipeline_commit)
-        c.bt_dht = _env_bool(g("TRITONDL_BT_DHT"), c.bt_dht)
-        c.bt_dht_ipv6 = _env_bool(g("TRITONDL_BT_DHT_IPV6"), c.bt_dht_ipv6)
-        c.bt_upnp = _env_bool(g("TRITONDL_BT_UPNP"), c.bt_upnp)
-        c.bt_native_wire = _env_bool(g("TRITONDL_BT_NATIVE_WIRE"), c.bt_native_wire)
-        c.bt_utp = _env_bool(g("TRITONDL_BT_UTP"), c.bt_utp)
-        c.bt_pex = _env_bool(g("TRITONDL_BT_PEX"), c.bt_pex)
+        for k, a in ENV_BOOLS.items():
+            setattr(c, a, _env_bool(g("TRITONDL_" + k), getattr(c, a)))
         if c.s3_hash_device not in ("cpu", "gpu"):
             raise ValueError(f"TRITONDL_S3_HASH_DEVICE must be cpu|gpu, got {c.s3_hash_device!r}")
         if c.bt_encryption not in ("disable", "allow", "prefer", "require"):
