@@ -44,3 +44,27 @@ def test_every_mapped_setting_parses():
     assert all(getattr(c, f) == 2.5 for f in C.ENV_FLOATS.values())
     assert all(getattr(c, f) != getattr(C.Config(), f) for f in C.ENV_BOOLS.values())
     assert (c.s3_hash_device, c.bt_encryption) == ("gpu", "require")
+
+
+def test_every_metric_family_has_help_and_type():
+    """Each metric the worker or the pool records has a HELP line, and the
+    exposition carries one HELP/TYPE pair per family."""
+    from tritondl.utils.metrics import HELP, Metrics
+    used = set()
+    for dirpath, _dirs, files in os.walk(os.path.join(ROOT, "tritondl")):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                for kind, name in re.findall(r"metrics\.(inc|set|observe)\(\"([a-z_]+)\"", src):
+                    used.add(name + "_total" if kind == "inc" else name)
+    assert used and used <= set(HELP), sorted(used - set(HELP))
+    m = Metrics()
+    m.inc("jobs", status="ok")
+    m.inc("jobs", status="failed", stage='say "hi"\n')
+    m.set("jobs_inflight", 1)
+    m.observe("stage_seconds", 0.2, stage="upload")
+    text = m.render()
+    for fam, kind in (("tritondl_jobs_total", "counter"), ("tritondl_jobs_inflight", "gauge"),
+                      ("tritondl_stage_seconds", "histogram"), ("tritondl_uptime_seconds", "gauge")):
+        assert text.count(f"# TYPE {fam} {kind}\n") == 1 and text.count(f"# HELP {fam} ") == 1
+    assert 'stage="say \\"hi\\"\\n"' in text

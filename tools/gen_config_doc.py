@@ -167,6 +167,12 @@ def render() -> str:
             "| variable | default | read in | effect |", "|---|---|---|---|"]
     for var, (dflt, where, what) in sorted(DIRECT.items()):
         out.append(f"| `{var}` | {dflt} | `{where}` | {what} |")
+    from tritondl.utils.metrics import HELP
+    out += ["", "## Metrics (`TRITONDL_METRICS_ADDR` / `--metrics-addr`: `/metrics`, `/healthz`)", "",
+            "Prometheus text format, prefix `tritondl_`; the pool (`python -m tritondl.parallel",
+            "--health-addr`) serves the `pool_*` families.", "", "| family | meaning |", "|---|---|"]
+    for name, what in sorted(HELP.items()):
+        out.append(f"| `tritondl_{name}` | {what} |")
     out += ["", "## Benchmark and test harness only", "", "| variable | effect |", "|---|---|"]
     for var, what in sorted(HARNESS.items()):
         out.append(f"| `{var}` | {what} |")

@@ -60,20 +60,41 @@ class Metrics:
         return self.counters.get(k, self.gauges.get(k, 0.0))
 
     def render(self) -> str:
+        """Prometheus text exposition (format 0.0.4): one ``# HELP`` / ``# TYPE``
+        pair per family, then its samples; label values escaped."""
         p = self.prefix
         out: list[str] = []
 
+        def esc(v) -> str:
+            return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
         def lab(items: tuple, extra: str = "") -> str:
-            parts = [f'{k}="{v}"' for k, v in items]
+            parts = [f'{k}="{esc(v)}"' for k, v in items]
             if extra:
                 parts.append(extra)
             return "{" + ",".join(parts) + "}" if parts else ""
 
+        def head(name: str, kind: str) -> None:
+            out.append(f"# HELP {name} {HELP.get(name[len(p) + 1:], name)}")
+            out.append(f"# TYPE {name} {kind}")
+
+        last = None
         for (n, ls), v in sorted(self.counters.items()):
+            if n != last:
+                head(f"{p}_{n}_total", "counter")
+                last = n
             out.append(f"{p}_{n}_total{lab(ls)} {v}")
+        last = None
         for (n, ls), v in sorted(self.gauges.items()):
+            if n != last:
+                head(f"{p}_{n}", "gauge")
+                last = n
             out.append(f"{p}_{n}{lab(ls)} {v}")
+        last = None
         for (n, ls), h in sorted(self.hists.items(), key=lambda x: x[0]):
+            if n != last:
+                head(f"{p}_{n}", "histogram")
+                last = n
             acc = 0
             for b, c in zip(h.buckets, h.counts):
                 acc += c
@@ -83,8 +104,28 @@ class Metrics:
             out.append(f"{p}_{n}_bucket{lab(ls, le)} {h.n}")
             out.append(f"{p}_{n}_sum{lab(ls)} {h.total}")
             out.append(f"{p}_{n}_count{lab(ls)} {h.n}")
+        head(f"{p}_uptime_seconds", "gauge")
         out.append(f"{p}_uptime_seconds {time.time() - self.started:.3f}")
         return "\n".join(out) + "\n"
+
+
+# one line per metric family (name without the prefix; counters without "_total")
+HELP = {
+    "jobs_total": "job attempts by status (ok, failed with its stage, busy)",
+    "jobs_inflight": "jobs being processed by this worker",
+    "jobs_retried_total": "failed jobs scheduled for a retry (broker delay queue or parked in-process)",
+    "jobs_parked_total": "retries waited in-process because the broker refused the delay queue or DLQ",
+    "jobs_dead_lettered_total": "jobs published to the dead-letter topic after max_retries",
+    "jobs_dropped_total": "jobs nacked without requeue after max_retries (drop_failed)",
+    "bytes_uploaded_total": "bytes uploaded to S3 by finished jobs",
+    "job_seconds": "time from delivery to ack of successful jobs",
+    "stage_seconds": "time per job stage (download, upload)",
+    "malloc_trims_total": "malloc_trim calls that returned memory to the OS",
+    "pool_workers_live": "pool: workers not given up on",
+    "pool_workers_given_up": "pool: crash-looping workers given up on",
+    "pool_worker_restarts_total": "pool: worker restarts by rank",
+    "uptime_seconds": "seconds since the process's metrics started",
+}
 
 
 async def serve_metrics(metrics: Metrics, addr: str, health=None):
