@@ -239,7 +239,8 @@ class JobStack:
         cfg.heartbeat_s = self.heartbeat
         cfg.ca_file = endpoints.get("ca_file", "")
         for var, attr in (("TRITONDL_MALLOC_MMAP_THRESHOLD", "malloc_mmap_threshold"),
-                          ("TRITONDL_MALLOC_ARENA_MAX", "malloc_arena_max")):
+                          ("TRITONDL_MALLOC_ARENA_MAX", "malloc_arena_max"),
+                          ("TRITONDL_MALLOC_TRIM_THRESHOLD", "malloc_trim_threshold")):
             if os.environ.get(var):                # heap-policy A/B (Service.start applies it)
                 setattr(cfg, attr, int(os.environ[var]))
         if self.http_probe_bytes >= 0:

@@ -287,7 +287,8 @@ class Service:
     # ------------------------------------------------------------ lifecycle
     async def start(self) -> None:
         cfg = self.cfg
-        self.malloc_policy = tune_malloc(cfg.malloc_mmap_threshold, cfg.malloc_arena_max)
+        self.malloc_policy = tune_malloc(cfg.malloc_mmap_threshold, cfg.malloc_arena_max,
+                                         cfg.malloc_trim_threshold)
         self._size_executor()
         if self.uploader is None:
             # NewUploader (downloader.go:95-98) was fatal on a bad S3_ENDPOINT: validate
@@ -733,7 +734,7 @@ class Service:
         await self.shutdown()
 
 
-def tune_malloc(mmap_threshold: int, arena_max: int = 0) -> dict:
+def tune_malloc(mmap_threshold: int, arena_max: int = 0, trim_threshold: int = 0) -> dict:
     """Fix glibc's heap policy for a long-running process with many native
     threads (``mallopt``; a no-op elsewhere).  ``mmap_threshold > 0`` pins
     M_MMAP_THRESHOLD, which also turns off glibc's dynamic adjustment: left
@@ -751,9 +752,13 @@ def tune_malloc(mmap_threshold: int, arena_max: int = 0) -> dict:
         return out
     mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
     mallopt.restype = ctypes.c_int
-    M_MMAP_THRESHOLD, M_ARENA_MAX = -3, -8
+    M_TRIM_THRESHOLD, M_MMAP_THRESHOLD, M_ARENA_MAX = -1, -3, -8
     if mmap_threshold > 0 and mallopt(M_MMAP_THRESHOLD, int(mmap_threshold)):
         out["mmap_threshold"] = int(mmap_threshold)
+    # pinning the mmap threshold also pins the trim threshold (128 KiB unless set):
+    # free space above it at an arena's top goes back to the OS on every free()
+    if trim_threshold > 0 and mallopt(M_TRIM_THRESHOLD, int(trim_threshold)):
+        out["trim_threshold"] = int(trim_threshold)
     if arena_max > 0 and mallopt(M_ARENA_MAX, int(arena_max)):
         out["arena_max"] = int(arena_max)
     return out

@@ -53,7 +53,7 @@ ENV_INTS = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES"
             "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
             "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
             "RECYCLE_BYTES": "recycle_bytes", "MALLOC_MMAP_THRESHOLD": "malloc_mmap_threshold",
-            "MALLOC_ARENA_MAX": "malloc_arena_max"}
+            "MALLOC_ARENA_MAX": "malloc_arena_max", "MALLOC_TRIM_THRESHOLD": "malloc_trim_threshold"}
 ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
               "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
@@ -125,6 +125,7 @@ class Config:
     # that free: a soak's arenas held ~100 MB for 15 MB in use (service.tune_malloc)
     malloc_mmap_threshold: int = 256 * 1024
     malloc_arena_max: int = 0                   # glibc M_ARENA_MAX (0: glibc default, 8 per core)
+    malloc_trim_threshold: int = 0              # glibc M_TRIM_THRESHOLD (0: 128 KiB once the mmap threshold is pinned)
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
