@@ -105,9 +105,12 @@ async def main() -> int:
             from tritondl.utils.profiler import CPUProfiler
             sprof = CPUProfiler(a.cpuprofile)
             sprof.start()
+        import resource
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         await d.download(dst, lambda u, p: None, magnet)
         dt = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
         if prof:
             prof.disable()
             prof.dump_stats(a.profile)
@@ -119,7 +122,10 @@ async def main() -> int:
                           "seconds": round(dt, 3), "mb": a.mb, "seeds": a.seeds, "piece_kb": a.piece_kb,
                           "transport": "utp" if a.utp else "tcp+utp",
                           "encryption": a.encryption, "wire": "python" if a.python_wire else "native",
-                          "seeders": "python" if a.python_seeders else "native"}),
+                          "seeders": "python" if a.python_seeders else "native",
+                          # the leecher process over the download: page faults and CPU
+                          "leecher_minflt": ru1.ru_minflt - ru0.ru_minflt,
+                          "leecher_cpu_s": round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 3)}),
               flush=True)
     finally:
         for s in seeds:
