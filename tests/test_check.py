@@ -1,0 +1,63 @@
+"""python -m tritondl.check: preflight against the fakes."""
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+
+from tritondl import check
+from tritondl.fakes.broker import Broker
+from tritondl.fakes.s3 import FakeS3
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(monkeypatch, tmp_path, broker_url_hostport: str, s3: str):
+    monkeypatch.setenv("RABBITMQ_ENDPOINT", broker_url_hostport)
+    monkeypatch.setenv("RABBITMQ_USERNAME", "guest")
+    monkeypatch.setenv("RABBITMQ_PASSWORD", "guest")
+    monkeypatch.setenv("S3_ENDPOINT", s3)
+    monkeypatch.setenv("S3_ACCESS_KEY", "ak")
+    monkeypatch.setenv("S3_SECRET_KEY", "sk")
+    monkeypatch.setenv("TRITONDL_DOWNLOAD_DIR", str(tmp_path / "dl"))
+    monkeypatch.setenv("TRITONDL_GPU_VERIFY", "off")
+
+
+def test_preflight_passes_and_reports_missing_topology(tmp_path, monkeypatch):
+    async def main():
+        b = await Broker(username="guest", password="guest").start()
+        s3 = await FakeS3(access_key="ak", secret_key="sk").start()
+        try:
+            _env(monkeypatch, tmp_path, b.url.split("@", 1)[1].rstrip("/"), s3.endpoint)
+            r = await check.run([])
+            by = {(i["area"], i["status"]) for i in r.items}
+            assert not r.failed, r.items
+            assert ("broker", "ok") in by and ("s3", "ok") in by and ("download_dir", "ok") in by
+            # nothing declared yet: the exchanges/queues are reported as missing, not created
+            warns = [i["detail"] for i in r.items if i["area"] == "broker" and i["status"] == "warn"]
+            assert any("v1.download does not exist" in w for w in warns)
+            assert "v1.download" not in b.exchanges
+            assert any("bucket triton-staging does not exist yet" in i["detail"] for i in r.items)
+            # a wrong secret fails the S3 check; a dead broker fails the broker check
+            monkeypatch.setenv("S3_SECRET_KEY", "nope")
+            monkeypatch.setenv("RABBITMQ_ENDPOINT", "127.0.0.1:1")
+            r2 = await check.run([], timeout=3)
+            bad = {i["area"] for i in r2.items if i["status"] == "fail"}
+            assert r2.failed and {"broker", "s3"} <= bad
+        finally:
+            await s3.stop()
+            await b.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_preflight_cli_fails_on_an_unusable_endpoint(tmp_path):
+    env = dict(os.environ, S3_ENDPOINT="ftp://", TRITONDL_DOWNLOAD_DIR=str(tmp_path / "dl"), PYTHONPATH=ROOT,
+               TRITONDL_GPU_VERIFY="off")
+    p = subprocess.run([sys.executable, "-m", "tritondl.check", "--json", "--no-broker"], capture_output=True,
+                       text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode == 1, p.stderr
+    doc = json.loads(p.stdout)
+    assert doc["ok"] is False
+    assert any(i["area"] == "s3" and i["status"] == "fail" and "unusable" in i["detail"] for i in doc["checks"])
+    assert any(i["area"] == "native" and i["status"] == "ok" for i in doc["checks"])
