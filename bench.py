@@ -263,6 +263,8 @@ def main() -> int:
                     help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
     ap.add_argument("--pipeline-commit", default="off", choices=["on", "off"],
                     help="on: a job's publish confirm and ack overlap the next job (opt-in worker setting)")
+    ap.add_argument("--no-reference-mode", action="store_true",
+                    help="skip the secondary run in the reference's cleanup-off mode after the timed region")
     ap.add_argument("--no-content-check", action="store_true",
                     help="S3 does not compare PUT content with the origin's payload")
     ap.add_argument("--fake-cpus", default="auto",
@@ -429,6 +431,21 @@ def main() -> int:
         for r in done:
             for k, v in r.marks.items():
                 spans.setdefault(k, []).append(v)
+        # secondary, after the headline's timed region: the same jobs in the
+        # reference's mode (cleanup off: every job dir kept, fresh files, B15)
+        reference_mode = None
+        if world == 1 and stack.cleanup and not a.no_reference_mode and stack.svc is not None:
+            stack.svc.cfg.cleanup = False
+            loop.run_until_complete(stack.run_jobs(max(a.warmup, 5)))   # drains the spare pool (4 files)
+            s0 = stack.svc.jobs_finished
+            t0r = time.perf_counter()
+            loop.run_until_complete(stack.run_jobs(a.steps))
+            dtr = time.perf_counter() - t0r
+            lat_r = sorted(r.seconds for r in stack.svc.results[-(stack.svc.jobs_finished - s0):])
+            reference_mode = {"cleanup": False, "jobs_per_sec": round(a.steps / dtr, 3),
+                              "ms_per_step": round(dtr / a.steps * 1000, 3),
+                              "job_latency_ms_p50": round(lat_r[len(lat_r) // 2] * 1000, 2) if lat_r else None,
+                              "steps": a.steps, "warmup": max(a.warmup, 5)}
     finally:
         loop.run_until_complete(stack.teardown())
         loop.close()
@@ -501,6 +518,9 @@ def main() -> int:
             "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3) if max_elapsed >= 0.5 else None,
             "diag": diag,
         }
+        if reference_mode is not None:
+            # not the number of record: timed after it, with the reference's cleanup-off mode
+            res["reference_mode"] = reference_mode
         if res["broker_core_share"] is not None and res["broker_core_share"] > 0.5:
             res["harness_bound"] = True
         res.update(extra)
