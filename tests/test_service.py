@@ -742,3 +742,35 @@ libc.free(q)
         if arm == "fixed":
             assert "262144" in p.stdout
     assert out == {"fixed": "1", "dynamic": "0"}
+
+
+def test_malloc_policy_trim_threshold_stops_medium_block_thrash():
+    """With the mmap threshold pinned, glibc's trim threshold stays at 128 KiB
+    and a 200 KiB malloc/free loop gives its pages back and faults them in on
+    every cycle; the worker's default trim threshold (4 MiB) stops that."""
+    import subprocess
+    import sys
+    code = r"""
+import ctypes, resource, sys
+from tritondl.service import tune_malloc
+libc = ctypes.CDLL("libc.so.6")
+libc.malloc.restype = ctypes.c_void_p
+libc.malloc.argtypes = [ctypes.c_size_t]
+libc.free.argtypes = [ctypes.c_void_p]
+libc.memset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+tune_malloc(262144, trim_threshold=int(sys.argv[1]))
+r0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
+for _ in range(2000):
+    p = libc.malloc(200 << 10)
+    libc.memset(p, 1, 200 << 10)
+    libc.free(p)
+print(resource.getrusage(resource.RUSAGE_SELF).ru_minflt - r0)
+"""
+    from tritondl.utils.config import Config
+    faults = {}
+    for trim in (128 << 10, Config().malloc_trim_threshold):     # glibc's 128 KiB set explicitly
+        p = subprocess.run([sys.executable, "-c", code, str(trim)], capture_output=True, text=True, timeout=60,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert p.returncode == 0, p.stderr
+        faults[trim] = int(p.stdout.split()[-1])
+    assert faults[128 << 10] > 10 * 2000 and faults[4 << 20] < 2000, faults

@@ -51,8 +51,8 @@ async def main() -> int:
                     help="--job: cap the fake S3's ingest link (Gbit/s; 0 = loopback speed)")
     ap.add_argument("--cpus", default="", help="pin the leecher (worker) to this cpulist")
     ap.add_argument("--fake-cpus", default="", help="pin the seeder (and fake S3) processes to this cpulist")
-    ap.add_argument("--malloc-trim-threshold", type=int, default=0, help="glibc trim threshold with a pinned mmap "
-                                                                         "threshold (0: glibc's 128 KiB)")
+    ap.add_argument("--malloc-trim-threshold", type=int, default=-1,
+                    help="glibc trim threshold with a pinned mmap threshold (0: glibc's 128 KiB; -1: worker default)")
     ap.add_argument("--malloc-mmap-threshold", type=int, default=-1,
                     help="glibc mmap threshold for the leecher (0: glibc's dynamic default; -1: the worker "
                          "default, which the plain download form leaves to glibc)")
@@ -68,7 +68,9 @@ async def main() -> int:
         return await job_bench(a)
     if a.malloc_mmap_threshold > 0:
         from tritondl.service import tune_malloc
-        tune_malloc(a.malloc_mmap_threshold, trim_threshold=a.malloc_trim_threshold)
+        from tritondl.utils.config import Config
+        tune_malloc(a.malloc_mmap_threshold, trim_threshold=(a.malloc_trim_threshold if a.malloc_trim_threshold >= 0
+                                                             else Config().malloc_trim_threshold))
     from tritondl.bench_job import Backend
     from tritondl.fakes.swarm import make_payload
     from tritondl.fetch.bt.client import TorrentDownloader
@@ -173,7 +175,8 @@ async def job_bench(a) -> int:
         cfg.progress_log_interval_s, cfg.heartbeat_s = 0, 0
         if a.malloc_mmap_threshold >= 0:
             cfg.malloc_mmap_threshold = a.malloc_mmap_threshold
-        cfg.malloc_trim_threshold = a.malloc_trim_threshold
+        if a.malloc_trim_threshold >= 0:
+            cfg.malloc_trim_threshold = a.malloc_trim_threshold
         bt = TorrentDownloader(TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", utp=True,
                                              encryption=a.encryption, native_wire=not a.python_wire),
                                progress_interval=1.0, use_dht=False)

@@ -756,8 +756,10 @@ def tune_malloc(mmap_threshold: int, arena_max: int = 0, trim_threshold: int = 0
     if mmap_threshold > 0 and mallopt(M_MMAP_THRESHOLD, int(mmap_threshold)):
         out["mmap_threshold"] = int(mmap_threshold)
     # pinning the mmap threshold also pins the trim threshold (128 KiB unless set):
-    # free space above it at an arena's top goes back to the OS on every free()
-    if trim_threshold > 0 and mallopt(M_TRIM_THRESHOLD, int(trim_threshold)):
+    # free space above it at an arena's top goes back to the OS on every free().
+    # Only alongside a pinned mmap threshold: setting it alone would also end
+    # glibc's dynamic policy, which mmap_threshold=0 asks to keep
+    if mmap_threshold > 0 and trim_threshold > 0 and mallopt(M_TRIM_THRESHOLD, int(trim_threshold)):
         out["trim_threshold"] = int(trim_threshold)
     if arena_max > 0 and mallopt(M_ARENA_MAX, int(arena_max)):
         out["arena_max"] = int(arena_max)

@@ -125,7 +125,11 @@ class Config:
     # that free: a soak's arenas held ~100 MB for 15 MB in use (service.tune_malloc)
     malloc_mmap_threshold: int = 256 * 1024
     malloc_arena_max: int = 0                   # glibc M_ARENA_MAX (0: glibc default, 8 per core)
-    malloc_trim_threshold: int = 0              # glibc M_TRIM_THRESHOLD (0: 128 KiB once the mmap threshold is pinned)
+    # glibc M_TRIM_THRESHOLD, set with a pinned mmap threshold (0: glibc's 128 KiB).  At
+    # 128 KiB every free() that leaves more than that at an arena's top returns pages
+    # the next allocation faults back: a 200 KiB malloc/free loop took 7x as long
+    # (18 faults per cycle); 4 MiB costs ~3 MB of RSS in a soak (profiles/r04_malloc/)
+    malloc_trim_threshold: int = 4 << 20
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
