@@ -96,12 +96,16 @@ def check_dir(cfg: Config, r: Report) -> None:
         free = st.f_bavail * st.f_frsize
         fs = "?"
         try:
-            best = ""
+            best, path = "", os.path.realpath(d)
             with open("/proc/mounts") as m:
                 for line in m:
                     parts = line.split()
-                    if len(parts) > 2 and os.path.abspath(d).startswith(parts[1]) and len(parts[1]) > len(best):
-                        best, fs = parts[1], parts[2]
+                    if len(parts) < 3:
+                        continue
+                    mnt = parts[1]
+                    inside = path == mnt or path.startswith(mnt.rstrip("/") + "/")
+                    if inside and len(mnt) > len(best):
+                        best, fs = mnt, parts[2]
         except OSError:
             pass
         status = OK if free > (1 << 30) else WARN
