@@ -464,6 +464,13 @@ def main() -> int:
         dist.all_gather_object(per_rank, n_done, group=ctl)
         cpu_all = [None] * world  # type: ignore[list-item]
         dist.all_gather_object(cpu_all, cpu, group=ctl)
+        # where every rank ran: its CCD(s), its fakes' CCD, one NUMA node or not, memory bandwidth
+        mine = {"ccds": _PLACEMENT.get("chosen_ccds"), "fake_ccd": _PLACEMENT.get("fake_ccd"),
+                "same_numa_node": _PLACEMENT.get("fakes_same_numa_node"),
+                "memcpy_GBps_start": diag["memcpy_GBps"]["start"]}
+        placement_all = [None] * world  # type: ignore[list-item]
+        dist.all_gather_object(placement_all, mine, group=ctl)
+        diag["placement_per_rank"] = placement_all
     extra = {} if (a.no_gpu_probe or rank != 0) else _gpu_hash_probe()
     if rank == 0:
         jobs_per_sec = world * a.steps / max_elapsed
