@@ -65,6 +65,7 @@ def test_bench_two_ranks_torchrun_gloo():
     assert len(d["jobs_per_rank"]) == 2 and all(n > 0 for n in d["jobs_per_rank"]), d["jobs_per_rank"]
     assert sum(d["jobs_per_rank"]) == 2 * 3
     assert d["config"]["collectives"].startswith("gloo max-reduce")
+    assert len(d["diag"]["placement_per_rank"]) == 2
 
 
 def test_bench_dist_always_one_rank():
