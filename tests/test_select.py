@@ -141,3 +141,71 @@ def test_predict_media_refuses_foreign_directories(tmp_path):
     os.rmdir(tmp_path / "leftover")
     assert predict_media(str(tmp_path), [str(tmp_path / "Show" / "season 1" / "e1.mkv")]) == \
         {str(tmp_path / "Show" / "season 1" / "e1.mkv")}
+
+
+# ------------------------------------------------------- property: the rules vs a model
+
+def _model(tree: dict) -> list[str]:
+    """SURVEY.md Appendix A.1, written independently of ``select.py``: an
+    in-memory tree ({name: subtree or None}) -> the relative paths
+    ``process.Dir`` returns, in its order."""
+    import re
+    top_dirs = [n for n, v in tree.items() if isinstance(v, dict)]
+    allowed = ["season"] + ([top_dirs[0]] if len(top_dirs) == 1 else [])
+    out: list[str] = []
+
+    def walk(node: dict, prefix: list[str]) -> None:
+        for name in sorted(node, key=lambda n: n.encode()):           # filepath.Walk: lexical
+            v = node[name]
+            if isinstance(v, dict):
+                if any(a in name for a in allowed) or re.search(r"s\d+", name):
+                    walk(v, prefix + [name])
+            else:
+                dot = name.rfind(".")                                  # filepath.Ext
+                if dot >= 0 and name[dot:] in (".mp4", ".mkv", ".mov", ".webm"):
+                    out.append("/".join(prefix + [name]))
+    walk(tree, [])
+    return out
+
+
+def test_dir_media_matches_the_rules_on_random_trees():
+    """Random trees (names built to hit the rules' edges: "season" as a
+    substring, capital S, s<digits> anywhere, the sole top-level directory,
+    dotfiles, upper-case and compound extensions) give exactly the model's
+    list, in its order."""
+    import tempfile
+
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    from tritondl.select import dir_media
+
+    stems = st.sampled_from(["season 1", "Season 2", "my season", "s01", "S01", "xs12y", "extras", "show",
+                             "a", "b", "c d", "Ab", "s", "sx", ""])
+    exts = st.sampled_from([".mkv", ".mp4", ".mov", ".webm", ".MKV", ".srt", ".mkv.part", ".tar.mkv", ""])
+    file_names = st.tuples(stems, exts).map(lambda t: t[0] + t[1]).filter(lambda n: n not in ("", ".", ".."))
+    dir_names = stems.filter(lambda n: n not in ("", ".", ".."))
+    trees = st.recursive(
+        st.dictionaries(file_names, st.none(), max_size=4),
+        lambda kids: st.dictionaries(dir_names | file_names, kids | st.none(), max_size=4),
+        max_leaves=14).filter(lambda t: isinstance(t, dict))
+
+    def make(root: str, node: dict) -> None:
+        for name, v in node.items():
+            p = os.path.join(root, name)
+            if isinstance(v, dict):
+                os.mkdir(p)
+                make(p, v)
+            else:
+                with open(p, "wb"):
+                    pass
+
+    @settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(trees)
+    def check(tree):
+        with tempfile.TemporaryDirectory() as root:
+            make(root, tree)
+            got = [os.path.relpath(p, root) for p in dir_media(root)]
+            assert got == _model(tree)
+
+    check()
