@@ -1,8 +1,9 @@
 """Property-based tests (hypothesis) for every hand-written codec: bencode,
 AMQP field tables and frames, protobuf varints and the Download envelope,
 peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
-native aws-chunked encoder/decoder pair.  Decoders must round-trip what the
-encoders produce and reject garbage only with their own error types."""
+native aws-chunked encoder/decoder pair, and the S3 multipart planner's
+invariants.  Decoders must round-trip what the encoders produce and reject
+garbage only with their own error types."""
 
 import asyncio
 import math
@@ -236,3 +237,28 @@ def test_aws_chunked_boundaries(n):
     data = bytes(range(256)) * 1 + b"z" * n
     enc, _ = hashing.aws_chunk_encode(KEY, DATE, SCOPE, SEED, data, 8192, final=True)
     assert hashing.aws_chunk_decode(KEY, DATE, SCOPE, SEED, enc)[1] == data
+
+
+# ------------------------------------------------------------ S3 multipart plan
+
+@SETTINGS
+@given(st.integers(min_value=0, max_value=5 << 40), st.integers(min_value=1, max_value=6 << 30))
+def test_multipart_plan_invariants(size, part_size):
+    """minio-go optimalPartInfo's contract for any object up to 5 TiB: parts of
+    5 MiB..5 GiB, at most 10,000 of them, covering the object with no empty
+    last part, the part size a multiple of the configured one unless capped."""
+    from tritondl.s3.client import MAX_PART_SIZE, MAX_PARTS, MIN_PART_SIZE, plan_parts
+    ps, n = plan_parts(size, part_size)
+    assert MIN_PART_SIZE <= ps <= MAX_PART_SIZE
+    assert 1 <= n <= MAX_PARTS and ps * n >= size
+    assert size == 0 or (n - 1) * ps < size
+    base = max(part_size, MIN_PART_SIZE)
+    assert ps == MAX_PART_SIZE or ps % base == 0
+
+
+@SETTINGS
+@given(st.integers(min_value=(5 << 40) + 1, max_value=1 << 50))
+def test_multipart_plan_refuses_objects_over_5_tib(size):
+    from tritondl.s3.client import S3Error, plan_parts
+    with pytest.raises(S3Error):
+        plan_parts(size, 16 << 20)
