@@ -1,8 +1,9 @@
 """Property-based tests (hypothesis) for every hand-written codec: bencode,
 AMQP field tables and frames, protobuf varints and the Download envelope,
 peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
-native aws-chunked encoder/decoder pair, and the S3 multipart planner's
-invariants.  Decoders must round-trip what the encoders produce and reject
+native aws-chunked encoder/decoder pair, the native HTTP chunked-transfer
+decoder under any chunking and head/body split, and the S3 multipart
+planner's invariants.  Decoders must round-trip what the encoders produce and reject
 garbage only with their own error types."""
 
 import asyncio
@@ -262,3 +263,43 @@ def test_multipart_plan_refuses_objects_over_5_tib(size):
     from tritondl.s3.client import S3Error, plan_parts
     with pytest.raises(S3Error):
         plan_parts(size, 16 << 20)
+
+
+# ------------------------------------------------- HTTP chunked transfer decoding
+
+@SETTINGS
+@given(st.binary(max_size=3000), st.lists(st.integers(1, 700), min_size=1, max_size=12),
+       st.booleans(), st.booleans(), st.integers(0, 4000))
+def test_native_chunked_decoder_roundtrip(payload, sizes, ext, trailer, cut):
+    """Any chunking of any payload (chunk extensions, trailer fields, and the
+    head/body boundary anywhere: ``prefix`` = bytes that arrived with the head)
+    decodes to exactly the payload, and the connection stays reusable."""
+    import os
+    import socket
+    import tempfile
+
+    from tritondl.utils import rawhttp
+    relay = rawhttp.relay_module()
+    if relay is None:
+        pytest.skip("native relay not built")
+    body, pos, k = bytearray(), 0, 0
+    while pos < len(payload):
+        n = min(sizes[k % len(sizes)], len(payload) - pos)
+        body += f"{n:x}{';a=b' if ext else ''}\r\n".encode() + payload[pos:pos + n] + b"\r\n"
+        pos += n
+        k += 1
+    body += b"0\r\n" + (b"X-Sum: 1\r\n" if trailer else b"") + b"\r\n"
+    cut = min(cut, len(body))
+    with tempfile.TemporaryDirectory() as d:
+        fd = os.open(os.path.join(d, "out"), os.O_RDWR | os.O_CREAT, 0o644)
+        a, b = socket.socketpair()
+        try:
+            a.sendall(bytes(body[cut:]))
+            got, _eof, err, reusable = relay.recv_body(b.fileno(), fd, 0, -1, bytes(body[:cut]), None,
+                                                       chunked=True)
+            assert err == "" and got == len(payload) and reusable
+            assert os.pread(fd, len(payload) + 1, 0) == payload
+        finally:
+            a.close()
+            b.close()
+            os.close(fd)
