@@ -209,3 +209,46 @@ def test_dir_media_matches_the_rules_on_random_trees():
             assert got == _model(tree)
 
     check()
+
+
+def test_predict_media_matches_dir_media_on_random_layouts():
+    """For any torrent layout (files only; directories exist because files do),
+    the prediction made from the path strings before a byte is written equals
+    the real walk once every file exists."""
+    import tempfile
+
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    from tritondl.select import dir_media, predict_media
+
+    stems = st.sampled_from(["season 1", "Season 2", "s01", "S01", "xs12y", "extras", "show", "a", "b c"])
+    exts = st.sampled_from([".mkv", ".mp4", ".mov", ".webm", ".MKV", ".srt", ".nfo", ""])
+    file_names = st.tuples(stems, exts).map(lambda t: t[0] + t[1])
+    trees = st.recursive(st.dictionaries(file_names, st.none(), max_size=4),
+                         lambda kids: st.dictionaries(stems | file_names, kids | st.none(), max_size=4),
+                         max_leaves=14)
+
+    def leaves(node: dict, prefix: tuple = ()) -> list[str]:
+        out = []
+        for name, v in node.items():
+            if isinstance(v, dict):
+                out += leaves(v, prefix + (name,))
+            else:
+                out.append("/".join(prefix + (name,)))
+        return out
+
+    @settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+    @given(trees)
+    def check(tree):
+        with tempfile.TemporaryDirectory() as root:
+            rels = leaves(tree)
+            paths = [os.path.join(root, r) for r in rels]
+            pred = predict_media(root, paths)
+            for r in rels:
+                os.makedirs(os.path.dirname(os.path.join(root, r)), exist_ok=True)
+                with open(os.path.join(root, r), "wb"):
+                    pass
+            assert pred == set(dir_media(root)), rels
+
+    check()
