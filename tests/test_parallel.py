@@ -288,3 +288,43 @@ def test_pool_cli_exits_nonzero_when_every_worker_crash_loops(tmp_path):
                        capture_output=True)
     assert p.returncode == 1, p.stderr.decode()[-2000:]
     assert b"too few workers left" in p.stderr + p.stdout
+
+
+def test_pair_domains_properties():
+    """Any node layout and idle ranking: every rank gets k domains plus one
+    for its fakes, no domain twice, and a group spans nodes only when no
+    node had k + 1 free domains left at that rank's turn."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from tritondl.parallel import topology as t
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(st.integers(1, 8), min_size=1, max_size=4), st.integers(1, 2), st.integers(1, 8),
+           st.randoms(use_true_random=False))
+    def check(per_node, k, n, rnd):
+        doms, node = [], {}
+        for nd, count in enumerate(per_node):
+            for _ in range(count):
+                d = [len(doms) * 8]
+                node[d[0]] = nd
+                doms.append(d)
+        rnd.shuffle(doms)                                   # an arbitrary idle ranking
+        got = t.pair_domains(doms, k, n, lambda d: node[d[0]])
+        if len(doms) < n * (k + 1):
+            assert got is None
+            return
+        assert got is not None and len(got) == n
+        used = [d[0] for rd, f in got for d in rd + [f]]
+        assert len(used) == len(set(used)) == n * (k + 1)
+        free = {d[0] for d in doms}
+        for rd, f in got:
+            group = [d[0] for d in rd + [f]]
+            counts: dict[int, int] = {}
+            for c in free:
+                counts[node[c]] = counts.get(node[c], 0) + 1
+            if max(counts.values()) >= k + 1:
+                assert len({node[c] for c in group}) == 1, (per_node, k, n, got)
+            free -= set(group)
+
+    check()
