@@ -2,12 +2,14 @@
 AMQP field tables and frames, protobuf varints and the Download envelope,
 peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
 native aws-chunked encoder/decoder pair, the native HTTP chunked-transfer
-decoder under any chunking and head/body split, and the S3 multipart
-planner's invariants.  Decoders must round-trip what the encoders produce and reject
-garbage only with their own error types."""
+decoder under any chunking and head/body split, the S3 multipart planner's
+invariants, and the safety of server-supplied file names.  Decoders must
+round-trip what the encoders produce and reject garbage only with their own
+error types."""
 
 import asyncio
 import math
+import os
 
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -303,3 +305,56 @@ def test_native_chunked_decoder_roundtrip(payload, sizes, ext, trailer, cut):
             a.close()
             b.close()
             os.close(fd)
+
+
+# ------------------------------------------------- server-supplied file names
+
+def _usable_name(n: str, d: str) -> None:
+    from tritondl.fetch.http import _NAME_MAX
+    assert n not in (".", "..") and "/" not in n and "\\" not in n
+    assert not any(ord(c) < 32 or c == "\x7f" for c in n)
+    assert len(n.encode()) <= _NAME_MAX          # encodes: no lone surrogates
+    # the download's own files land inside the job dir, whatever the server said
+    for suffix in ("", ".part", ".part.meta.tmp"):
+        with open(os.path.join(d, n + suffix), "wb"):
+            pass
+    assert sorted(os.listdir(d)) == sorted(n + s for s in ("", ".part", ".part.meta.tmp"))
+    for f in os.listdir(d):
+        os.unlink(os.path.join(d, f))
+
+
+names = st.text(max_size=300) | st.text(st.sampled_from("ab./\\\x00\n é"), max_size=12)
+
+
+@SETTINGS
+@given(names)
+def test_server_file_names_are_one_creatable_component(s):
+    """Any Content-Disposition (plain, quoted, RFC 5987) or URL path yields ""
+    or one component the job dir can hold with its sidecars."""
+    import tempfile
+    from urllib.parse import quote
+    from tritondl.fetch.http import filename_from_disposition, filename_from_url
+    got = [filename_from_disposition(cd) for cd in
+           (s, f'attachment; filename="{s}"', f"attachment; filename*=UTF-8''{quote(s, safe='')}")]
+    got.append(filename_from_url("http://h/dir/" + quote(s, safe="/")))
+    with tempfile.TemporaryDirectory() as d:
+        for n in got:
+            if n:
+                _usable_name(n, d)
+
+
+@SETTINGS
+@given(st.text(st.characters(blacklist_categories=("Cs", "Cc"), blacklist_characters="/\\\"'%;"),
+               min_size=1, max_size=400),
+       st.sampled_from(["mkv", "mp4", "avi", "en.srt"]))
+def test_long_names_keep_their_extension_and_short_ones_are_untouched(stem, ext):
+    from urllib.parse import quote
+    from tritondl.fetch.http import _NAME_MAX, filename_from_url
+    name = f"{stem}.{ext}"
+    n = filename_from_url("http://h/" + quote(name))
+    if len(name.encode()) <= _NAME_MAX:
+        assert n == name
+    else:
+        last = ext.rpartition(".")[2]
+        assert n.endswith("." + last) and len(n.encode()) <= _NAME_MAX
+        assert name.startswith(n[:-len(last) - 1])

@@ -124,10 +124,28 @@ def filename_from_disposition(cd: str | None) -> str:
     return _safe_name(name)
 
 
+# longest name the work dir can hold with the ``.part.meta.tmp`` sidecar suffix
+_NAME_MAX = 255 - len(".part.meta.tmp")
+_CONTROLS = re.compile(r"[\x00-\x1f\x7f]")
+
+
 def _safe_name(name: str) -> str:
+    """The last path component of a server- or URL-supplied name, "" when
+    there is none.  C0 controls and DEL (NUL cannot be in a file name) become
+    ``_``; text that is not valid UTF-8 becomes ``?``; a name longer than the
+    file system allows next to its sidecars is cut in its stem on a character
+    boundary, keeping the extension the media filter selects on.  The
+    reference takes ``filepath.Base`` and fails on the rest."""
     name = name.replace("\\", "/").split("/")[-1]
     if name in ("", ".", ".."):
         return ""
+    name = _CONTROLS.sub("_", name).encode("utf-8", "replace").decode("utf-8")
+    if len(name.encode()) > _NAME_MAX:
+        stem, dot, ext = name.rpartition(".")
+        if not (dot and stem and len(ext.encode()) < 32):
+            stem, dot, ext = name, "", ""
+        keep = _NAME_MAX - len((dot + ext).encode())
+        name = stem.encode()[:keep].decode("utf-8", "ignore") + dot + ext
     return name
 
 
