@@ -269,3 +269,67 @@ def test_native_merkle_root_matches_the_spec():
                 assert hashing.merkle_root(data, width) == mk.piece_root(data, width)
     with pytest.raises(ValueError):
         hashing.merkle_root(b"x" * 40000, 2)          # 3 leaves do not fit 2
+
+
+# ------------------------------------------------------ over-long file names
+
+def test_overlong_components_are_cut_distinct_and_keep_their_extension(tmp_path):
+    from tritondl.fetch.bt import bencode
+    from tritondl.fetch.bt.metainfo import COMPONENT_MAX, Info
+    long_a = "A" * 300 + ".part1.mkv"
+    long_b = "A" * 300 + ".part2.mkv"
+    cjk = "影" * 100 + ".mp4"                     # 100 chars, 304 UTF-8 bytes (fits NTFS, not ext4)
+    latin1 = b"\xe9" * 260 + b".avi"                  # not UTF-8: kept as raw bytes
+    raw = bencode.encode({b"name": "N" * 280, b"piece length": 16384, b"pieces": b"\0" * 20,
+                          b"files": [{b"length": 1, b"path": [p.encode() if isinstance(p, str) else p]}
+                                     for p in (long_a, long_b, cjk, latin1, "short.mkv")]})
+    info = Info.parse(raw)
+    names = [f.path[-1] for f in info.files]
+    assert names[-1] == "short.mkv"
+    assert len(set(names)) == 5
+    for n, ext in zip(names, (".mkv", ".mkv", ".mp4", ".avi")):
+        assert n.endswith(ext) and len(n.encode("utf-8", "surrogateescape")) <= COMPONENT_MAX
+    assert names[2].startswith("影") and "�" not in names[2]
+    assert len(info.name.encode()) <= COMPONENT_MAX
+    assert Info.parse(raw).files[0].path == info.files[0].path          # deterministic
+    for p, _n in info.file_paths(str(tmp_path)):
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        for suffix in ("", ".s3upload.tmp", ".part.meta.tmp"):
+            open(p + suffix, "wb").close()
+
+
+@pytest.mark.parametrize("version", [1, 3])
+def test_swarm_download_of_names_too_long_for_the_work_dir(tmp_path, version):
+    """250-byte names fit the seeder's disk but not next to the worker's
+    sidecars: the job lands them cut, hybrid v1/v2 file lists still agree."""
+    from tritondl.select import dir_media
+
+    async def main():
+        src = tmp_path / "src" / "Show"
+        names = {("E" * 240 + f".{k}.mkv"): 40_000 + k for k in range(2)}
+        make_payload(str(src), names)
+        info = make_info(str(src), 32768, version=version)
+        seed_root = tmp_path / "seed"
+        by_size = {n: os.path.join(src, f) for f, n in names.items()}
+        for p, n in info.file_paths(str(seed_root)):
+            if p:
+                os.makedirs(os.path.dirname(p), exist_ok=True)
+                os.link(by_size[n], p)
+        seed = await Seeder(info, str(seed_root)).start()
+        o = await Origin().start()
+        url = o.add("/t.torrent", torrent_file_bytes(info))
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        t, _ = await _dl().open(str(dst), url)
+        t.add_peer_addr(seed.addr)
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 30)
+        await t.close()
+        got = dir_media(str(dst))
+        assert len(got) == 2 and all(f.endswith(".mkv") for f in got)
+        for p, n in info.file_paths(str(dst)):
+            if p:
+                assert open(p, "rb").read() == open(by_size[n], "rb").read()
+        await seed.stop()
+        await o.stop()
+    run(main())

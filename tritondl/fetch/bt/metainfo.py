@@ -45,11 +45,37 @@ class FileEntry:
     pad: bool = False    # BEP 47 padding file (attr "p"): zeros, never written to disk
 
 
+# longest component the work dir can hold next to its ``.s3upload.tmp`` /
+# ``.part.meta.tmp`` sidecars (Linux NAME_MAX is 255 bytes)
+COMPONENT_MAX = 255 - len(".part.meta.tmp")
+
+
 def _safe_component(c: bytes | str) -> str:
+    """A path component of the info dict as it goes on disk.  ``..``, ``/``
+    and NUL are refused.  A component too long for the file system (names
+    from Windows may be 255 UTF-16 units, up to 765 UTF-8 bytes) is cut in
+    its stem on a character boundary, with ``~`` and 8 hex digits of its
+    SHA-1 so that names sharing a long prefix stay distinct, keeping the
+    extension the media filter selects on.  anacrolix opens the full name and
+    fails the download with ENAMETOOLONG."""
     s = c.decode("utf-8", "surrogateescape") if isinstance(c, bytes) else c
     if s in ("", ".", "..") or "/" in s or "\x00" in s:
         raise MetainfoError(f"unsafe path component {s!r}")
-    return s
+    raw = s.encode("utf-8", "surrogateescape")
+    if len(raw) <= COMPONENT_MAX:
+        return s
+    stem, dot, ext = s.rpartition(".")
+    if not (dot and stem and len(ext.encode("utf-8", "surrogateescape")) < 32):
+        stem, dot, ext = s, "", ""
+    tag = "~" + hashlib.sha1(raw).hexdigest()[:8]
+    room = COMPONENT_MAX - len(tag) - len((dot + ext).encode("utf-8", "surrogateescape"))
+    kept, n = [], 0
+    for ch in stem:
+        n += len(ch.encode("utf-8", "surrogateescape"))
+        if n > room:
+            break
+        kept.append(ch)
+    return "".join(kept) + tag + dot + ext
 
 
 @dataclass
