@@ -137,6 +137,39 @@ def test_http_resume_after_cut(tmp_path):
     run(main())
 
 
+def _gap(m):
+    m["segments"] = [[a + 1, b, 0] for a, b, _d in m["segments"]]
+    return m
+
+
+@pytest.mark.parametrize("tamper", [
+    _gap, lambda m: [m], lambda m: {**m, "segments": "x"},
+    lambda m: {**m, "segments": [[0, m["size"], -1]]}, lambda m: {**m, "segments": [[0, 1.5, 0]]}])
+def test_http_resume_ignores_a_plan_that_does_not_tile_the_file(tmp_path, tamper):
+    """A ``.part.meta`` whose segments do not tile [0, size) with sane done
+    counts (hand-edited, or written by another version) restarts the
+    download instead of leaving holes in the file or crashing."""
+    import json
+
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(5_000_000)
+        url = o.add("/f.mp4", data)
+        o.cut_after, o.cut_times = 1_500_000, 1
+        h = _dl(max_retries=0, write_block=256 * 1024)
+        with pytest.raises(HTTPDownloadError):
+            await h.download(str(tmp_path), Sink(), url)
+        mp = tmp_path / "f.mp4.part.meta"
+        mp.write_text(json.dumps(tamper(json.loads(mp.read_text()))))
+        h2 = _dl()
+        await h2.download(str(tmp_path), Sink(), url)
+        assert (tmp_path / "f.mp4").read_bytes() == data
+        await h.close()
+        await h2.close()
+        await o.stop()
+    run(main())
+
+
 def test_http_in_process_retry_and_segments(tmp_path):
     async def main():
         o = await Origin().start()

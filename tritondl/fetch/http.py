@@ -153,6 +153,26 @@ def filename_from_url(url: str) -> str:
     return _safe_name(unquote(urlparse(url).path))
 
 
+def _segments_ok(segs, size: int | None) -> bool:
+    """A resume plan read back from ``.part.meta`` is used only if its
+    ``[start, end, done]`` segments tile ``[0, size)`` in order with
+    ``0 <= done <= end - start`` (one open-ended ``[0, -1, done]`` segment
+    when the size is unknown); anything else restarts the download rather
+    than leaving unwritten holes in the file."""
+    if not isinstance(segs, list) or not segs:
+        return False
+    if not all(isinstance(sg, list) and len(sg) == 3 and all(type(v) is int for v in sg) for sg in segs):
+        return False
+    if size is None:
+        return len(segs) == 1 and segs[0][0] == 0 and segs[0][1] == -1 and segs[0][2] >= 0
+    at = 0
+    for a, b, d in segs:
+        if a != at or b < a or not 0 <= d <= b - a:
+            return False
+        at = b
+    return at == size
+
+
 class HTTPDownloader:
     def __init__(self, *, progress_interval: float = 1.0, segments: int = 4, segment_threshold: int = 64 << 20,
                  chunk: int = 1 << 20, write_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
@@ -442,9 +462,9 @@ class HTTPDownloader:
         validator = probe.etag or probe.last_modified
         segs = self._plan(probe)
         meta = self._load_meta(meta_path)
-        resumable = (meta is not None and os.path.exists(part) and probe.ranges and validator and
+        resumable = (isinstance(meta, dict) and os.path.exists(part) and probe.ranges and validator and
                      meta.get("url") == url and meta.get("validator") == validator and
-                     meta.get("size") == probe.size)
+                     meta.get("size") == probe.size and _segments_ok(meta.get("segments"), probe.size))
         if resumable:
             segs = [list(x) for x in meta["segments"]]
             log.with_fields(file=dst, done=sum(s[2] for s in segs)).info("resuming download")
