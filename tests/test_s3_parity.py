@@ -304,6 +304,13 @@ def test_stale_resume_state_starts_over(tmp_path):
             json.dump({"bucket": "other", "key": "k", "size": 1, "part_size": 5, "upload_id": "x"}, f)
         await c.put_object("b", "k", str(p), resume_path=state)
         assert s3.object_bytes("b", "k") == data
+        # malformed state (another version, hand-edited, torn): ignored, never a crash
+        same = {"bucket": "b", "key": "k", "size": len(data), "part_size": 5 << 20}
+        for bad in ([same], {**same, "upload_id": 7}, {**same, "upload_id": ""}, {**same}, "[", "\x00"):
+            with open(state, "w") as f:
+                f.write(bad if isinstance(bad, str) else json.dumps(bad))
+            await c.put_object("b", "k", str(p), resume_path=state)
+            assert s3.object_bytes("b", "k") == data and not os.path.exists(state)
         await c.close()
         await s3.stop()
     run(main())

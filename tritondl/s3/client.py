@@ -504,12 +504,15 @@ class S3Client:
                 st = json.load(f)
         except (OSError, ValueError):
             return "", {}
-        if (st.get("bucket"), st.get("key"), st.get("size"), st.get("part_size")) != (bucket, key, size, part_size):
+        if not isinstance(st, dict) or \
+                (st.get("bucket"), st.get("key"), st.get("size"), st.get("part_size")) != (bucket, key, size, part_size):
             return "", {}
-        uid = st.get("upload_id") or ""
+        uid = st.get("upload_id")
+        if not isinstance(uid, str) or not uid:
+            return "", {}
         try:
             listed = await self.list_parts(bucket, key, uid)
-        except S3Error as e:
+        except (S3Error, ET.ParseError, KeyError, ValueError) as e:
             log.with_fields(key=key, error=str(e)).info("interrupted multipart upload is gone; starting over")
             return "", {}
         path = src if isinstance(src, str) else f"/proc/self/fd/{src}" if isinstance(src, int) else None
