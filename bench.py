@@ -109,6 +109,55 @@ def _memcpy_gbps(mb: int = 64, reps: int = 4) -> float | None:
         return None
 
 
+_VMSTAT = ("nr_dirtied", "nr_written", "allocstall_normal", "allocstall_movable", "pgscan_direct",
+           "compact_stall", "workingset_refault_file", "pgfault")
+
+
+def _vm_snapshot() -> dict:
+    """Host page-cache state: selected ``/proc/vmstat`` counters and the
+    Dirty / Writeback totals of ``/proc/meminfo`` (kB).  Writeback by other
+    tenants and direct reclaim both stall a download's page-cache writes."""
+    out: dict = {}
+    try:
+        with open("/proc/vmstat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in _VMSTAT:
+                    out[k] = int(v)
+        with open("/proc/meminfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                if k in ("Dirty", "Writeback"):
+                    out[k + "_kB"] = int(v.split()[0])
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _vm_delta(v0: dict, v1: dict, n: int) -> dict:
+    """Per-job vmstat deltas plus the start/end Dirty and Writeback totals."""
+    out: dict = {k + "_per_job": round((v1[k] - v0[k]) / max(1, n), 1) for k in _VMSTAT if k in v0 and k in v1}
+    for k in ("Dirty_kB", "Writeback_kB"):
+        if k in v0 and k in v1:
+            out[k] = [v0[k], v1[k]]
+    return out
+
+
+def _work_fs(stack) -> dict | None:
+    """Filesystem of the worker's download dir, and its spare-file pool's use."""
+    try:
+        from tritondl.check import mount_of
+        from tritondl.utils import spares
+        d = stack.cfg.download_dir
+        out = mount_of(d)
+        pool = spares.pool_for(os.path.join(d, "x"))
+        if pool is not None:
+            out["spares_taken"], out["spares_offered"] = pool.taken, pool.offered
+        return out
+    except Exception:  # noqa: BLE001 - diagnostics only
+        return None
+
+
 def _cpu_mhz(cpus: list[int]) -> dict | None:
     """Current clock of the given CPUs (cpufreq, else /proc/cpuinfo): min/mean/max MHz."""
     vals: list[float] = []
@@ -371,6 +420,7 @@ def main() -> int:
         import resource
         mhz0 = _cpu_mhz(pinned) if pinned else None
         mem0 = _memcpy_gbps()
+        vm0 = _vm_snapshot()
         barrier()
         if prof is not None:
             prof.start()
@@ -392,6 +442,7 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        vm1 = _vm_snapshot()
         cpu1 = stack.cpu_seconds()
         mhz1 = _cpu_mhz(pinned) if pinned else None
         mem1 = _memcpy_gbps()
@@ -426,7 +477,9 @@ def main() -> int:
                 "majflt_per_job": round((ru1.ru_majflt - ru0.ru_majflt) / n_div, 2),
                 "nvcsw_per_job": round((ru1.ru_nvcsw - ru0.ru_nvcsw) / n_div, 1),
                 "nivcsw_per_job": round((ru1.ru_nivcsw - ru0.ru_nivcsw) / n_div, 1),
-                "s3_content_checked": bool(stack.content_check and stack.resolved_variants())}
+                "s3_content_checked": bool(stack.content_check and stack.resolved_variants()),
+                "vm": _vm_delta(vm0, vm1, n_div),
+                "work_fs": _work_fs(stack)}
         spans: dict[str, list[float]] = {}
         for r in done:
             for k, v in r.marks.items():

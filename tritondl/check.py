@@ -85,6 +85,26 @@ def check_native(r: Report) -> None:
         pass
 
 
+def mount_of(path: str) -> dict:
+    """The mount holding ``path``: {"mnt", "fs", "source"} from the longest
+    matching ``/proc/mounts`` entry (fs "?" when unknown)."""
+    out = {"mnt": "", "fs": "?", "source": ""}
+    try:
+        real = os.path.realpath(path)
+        with open("/proc/mounts") as m:
+            for line in m:
+                parts = line.split()
+                if len(parts) < 3:
+                    continue
+                mnt = parts[1]
+                inside = real == mnt or real.startswith(mnt.rstrip("/") + "/")
+                if inside and len(mnt) >= len(out["mnt"]):
+                    out = {"mnt": mnt, "fs": parts[2], "source": parts[0]}
+    except OSError:
+        pass
+    return out
+
+
 def check_dir(cfg: Config, r: Report) -> None:
     d = cfg.download_dir
     try:
@@ -94,20 +114,7 @@ def check_dir(cfg: Config, r: Report) -> None:
             f.flush()
         st = os.statvfs(d)
         free = st.f_bavail * st.f_frsize
-        fs = "?"
-        try:
-            best, path = "", os.path.realpath(d)
-            with open("/proc/mounts") as m:
-                for line in m:
-                    parts = line.split()
-                    if len(parts) < 3:
-                        continue
-                    mnt = parts[1]
-                    inside = path == mnt or path.startswith(mnt.rstrip("/") + "/")
-                    if inside and len(mnt) > len(best):
-                        best, fs = mnt, parts[2]
-        except OSError:
-            pass
+        fs = mount_of(d)["fs"]
         status = OK if free > (1 << 30) else WARN
         r.add("download_dir", status, f"{d} writable, {free / 2**30:.1f} GiB free, filesystem {fs}",
               free_bytes=free, fs=fs)
