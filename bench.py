@@ -491,13 +491,19 @@ def main() -> int:
             stack.svc.cfg.cleanup = False
             loop.run_until_complete(stack.run_jobs(max(a.warmup, 5)))   # drains the spare pool (4 files)
             s0 = stack.svc.jobs_finished
+            vr0 = _vm_snapshot()
             t0r = time.perf_counter()
             loop.run_until_complete(stack.run_jobs(a.steps))
             dtr = time.perf_counter() - t0r
-            lat_r = sorted(r.seconds for r in stack.svc.results[-(stack.svc.jobs_finished - s0):])
+            vr1 = _vm_snapshot()
+            done_r = stack.svc.results[-(stack.svc.jobs_finished - s0):]
+            lat_r = sorted(r.seconds for r in done_r)
+            fet_r = sorted(r.marks["fetched"] for r in done_r if "fetched" in r.marks)
             reference_mode = {"cleanup": False, "jobs_per_sec": round(a.steps / dtr, 3),
                               "ms_per_step": round(dtr / a.steps * 1000, 3),
                               "job_latency_ms_p50": round(lat_r[len(lat_r) // 2] * 1000, 2) if lat_r else None,
+                              "fetched_ms_p50": round(fet_r[len(fet_r) // 2] * 1000, 2) if fet_r else None,
+                              "vm": _vm_delta(vr0, vr1, len(done_r)),
                               "steps": a.steps, "warmup": max(a.warmup, 5)}
     finally:
         loop.run_until_complete(stack.teardown())
