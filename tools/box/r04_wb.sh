@@ -16,7 +16,7 @@ export TMPDIR=/tmp
   python3 -c "from tritondl.check import mount_of; print(mount_of('/tmp'))"
 } > $OUT/host.txt 2>&1
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver.log 2>&1 &&
-for i in 1 2 3; do
+for i in $(seq ${REPS:-3}); do
   for arm in spares nospares off; do
     case $arm in
       spares) args="--cleanup on";;
