@@ -3,7 +3,8 @@ AMQP field tables and frames, protobuf varints and the Download envelope,
 peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
 native aws-chunked encoder/decoder pair, the native HTTP chunked-transfer
 decoder under any chunking and head/body split, the S3 multipart planner's
-invariants, and the safety of server-supplied file names.  Decoders must
+invariants, SigV4 UriEncode and canonical queries against the spec's byte
+rule, and the safety of server-supplied file names.  Decoders must
 round-trip what the encoders produce and reject garbage only with their own
 error types."""
 
@@ -358,3 +359,33 @@ def test_long_names_keep_their_extension_and_short_ones_are_untouched(stem, ext)
         last = ext.rpartition(".")[2]
         assert n.endswith("." + last) and len(n.encode()) <= _NAME_MAX
         assert name.startswith(n[:-len(last) - 1])
+
+
+# ------------------------------------------------------------ SigV4 UriEncode
+
+_UNRESERVED = set(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_.~")
+
+
+def _uri_encode_model(s: str, encode_slash: bool) -> str:
+    """The AWS SigV4 UriEncode rule, byte by byte over UTF-8."""
+    keep = _UNRESERVED if encode_slash else _UNRESERVED | {ord("/")}
+    return "".join(chr(b) if b in keep else f"%{b:02X}" for b in s.encode())
+
+
+@SETTINGS
+@given(st.text(st.characters(blacklist_categories=("Cs",)), max_size=60) |
+       st.text(st.sampled_from("aZ09-_.~/ +=%&?é€😀"), max_size=20), st.booleans())
+def test_sigv4_uri_encode_matches_the_spec_rule(s, encode_slash):
+    from tritondl.s3 import sigv4
+    assert sigv4.uri_encode(s, encode_slash) == _uri_encode_model(s, encode_slash)
+
+
+@SETTINGS
+@given(st.lists(st.tuples(st.text(max_size=8, alphabet=st.characters(blacklist_categories=("Cs",))),
+                          st.text(max_size=8, alphabet=st.characters(blacklist_categories=("Cs",)))),
+                max_size=6))
+def test_sigv4_canonical_query_sorts_encoded_pairs(pairs):
+    from tritondl.s3 import sigv4
+    want = "&".join(f"{k}={v}" for k, v in sorted((_uri_encode_model(k, True), _uri_encode_model(v, True))
+                                                  for k, v in pairs))
+    assert sigv4.canonical_query(pairs) == want
