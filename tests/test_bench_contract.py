@@ -45,6 +45,13 @@ def test_bench_single_process_json():
     # the placement is part of the reported config (default: pinned to an L3 domain)
     assert d["config"]["cpus"].endswith(")") and "pinned" in d["config"]["cpus"]
     assert d["config"]["fake_cpus"]
+    # diagnostics that explain a slow lease: host page-cache counters, the work dir's
+    # filesystem and spare use, and the same for the reference's cleanup-off mode
+    vm = d["diag"]["vm"]
+    assert "nr_dirtied_per_job" in vm and len(vm["Dirty_kB"]) == 2
+    assert d["diag"]["work_fs"]["fs"] and d["diag"]["work_fs"]["spares_taken"] >= 1
+    rm = d["reference_mode"]
+    assert rm["cleanup"] is False and rm["fetched_ms_p50"] > 0 and "nr_dirtied_per_job" in rm["vm"]
 
 
 def test_bench_two_ranks_torchrun_gloo():
