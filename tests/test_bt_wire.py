@@ -321,3 +321,43 @@ def test_topup_dials_highest_bep40_priority_first(tmp_path):
     best = t._best_candidates(2)
     ranked = sorted(t.known, key=lambda a: priority(("123.213.32.10", 6881), a), reverse=True)
     assert best == ranked[:2]
+
+
+def test_unsolicited_or_out_of_range_metadata_pieces_are_not_kept(tmp_path):
+    """A peer sending ut_metadata data for pieces outside the announced
+    metadata size (or before any size is known, or bigger than a block)
+    cannot grow the session's memory; a request for a negative piece is
+    rejected instead of served from the end of the info dict."""
+    import asyncio
+    from tritondl.fetch.bt.metainfo import BLOCK
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig, _Peer
+
+    class W:
+        def __init__(self):
+            self.sent = []
+
+        def extended(self, eid, payload):
+            self.sent.append((eid, payload))
+
+    t = Torrent(b"\x01" * 20, str(tmp_path), TorrentConfig())
+    p = _Peer(W(), ("1.2.3.4", 5), None, 0)
+    p.ext = pw.ExtHandshake({"ut_metadata": 3}, None, None, "", None)
+
+    def data(piece, body=b"x"):
+        return bytes([pw.UT_METADATA_ID]) + pw.meta_msg(pw.META_DATA, piece, 40_000, body)
+
+    async def main():
+        await t._on_extended(p, data(0))                       # no size announced yet
+        assert t._meta == {}
+        t._meta_size = 40_000                                  # 3 pieces
+        for piece in (-1, 3, 1 << 40):
+            await t._on_extended(p, data(piece))
+        await t._on_extended(p, data(1, b"y" * (BLOCK + 1)))
+        assert t._meta == {}
+        await t._on_extended(p, data(1))
+        assert list(t._meta) == [1]
+        t.info = type("I", (), {"raw": b"z" * 100})()
+        await t._on_extended(p, bytes([pw.UT_METADATA_ID]) + pw.meta_msg(pw.META_REQUEST, -1))
+        d, body = pw.parse_meta_msg(p.wire.sent[-1][1])
+        assert d[b"msg_type"] == pw.META_REJECT and body == b""
+    asyncio.run(main())

@@ -4,7 +4,9 @@ peer-wire framing under arbitrary segmentation, MSE RC4 symmetry, and the
 native aws-chunked encoder/decoder pair, the native HTTP chunked-transfer
 decoder under any chunking and head/body split, the S3 multipart planner's
 invariants, SigV4 UriEncode and canonical queries against the spec's byte
-rule, and the safety of server-supplied file names.  Decoders must
+rule, the safety of server-supplied file names, and fuzzing of every parser of
+remote BitTorrent input (info dicts, magnets, tracker replies, extension
+messages).  Decoders must
 round-trip what the encoders produce and reject garbage only with their own
 error types."""
 
@@ -389,3 +391,64 @@ def test_sigv4_canonical_query_sorts_encoded_pairs(pairs):
     want = "&".join(f"{k}={v}" for k, v in sorted((_uri_encode_model(k, True), _uri_encode_model(v, True))
                                                   for k, v in pairs))
     assert sigv4.canonical_query(pairs) == want
+
+
+# ------------------------------------------- untrusted BitTorrent inputs (fuzz)
+# Peers, trackers and .torrent files are remote input: their parsers may only
+# raise their own error types, whatever shape the (valid) bencoding has.
+
+_bleaf = st.integers(-5, 70000) | st.binary(max_size=40) | st.sampled_from([b"..", b"x/y", b"", b"\x00", b"a.mkv"])
+_bkeys = st.sampled_from([b"", b"length", b"path", b"pieces root", b"attr", b"ip", b"port", b"m", b"ut_metadata",
+                          b"msg_type", b"piece", b"added", b"added6", b"dropped", b"name", b"files"])
+_bany = st.recursive(_bleaf, lambda k: st.lists(k, max_size=4) | st.dictionaries(_bkeys, k, max_size=4),
+                     max_leaves=14)
+
+
+@SETTINGS
+@given(st.dictionaries(st.sampled_from([b"name", b"piece length", b"pieces", b"files", b"length",
+                                        b"meta version", b"file tree", b"private"]), _bany, max_size=8))
+def test_info_dict_of_any_shape_raises_only_metainfo_error(d):
+    from tritondl.fetch.bt.metainfo import Info, MetainfoError
+    try:
+        info = Info.parse(bencode.encode(d))
+    except MetainfoError:
+        return
+    for f in info.files:                       # whatever was accepted is safe to put on disk
+        assert all(c not in ("", ".", "..") and "/" not in c for c in f.path)
+
+
+@SETTINGS
+@given(st.dictionaries(st.sampled_from([b"info", b"announce", b"announce-list", b"url-list", b"piece layers"]),
+                       _bany, max_size=5), st.text(max_size=80))
+def test_torrent_file_and_magnet_raise_only_metainfo_error(d, q):
+    from tritondl.fetch.bt.metainfo import Metainfo, MetainfoError, parse_magnet
+    for f in (lambda: Metainfo.parse(bencode.encode(d)), lambda: parse_magnet("magnet:?" + q)):
+        try:
+            f()
+        except MetainfoError:
+            pass
+
+
+@SETTINGS
+@given(_bany | st.dictionaries(st.sampled_from([b"failure reason", b"interval", b"peers", b"peers6",
+                                                b"complete", b"incomplete"]), _bany, max_size=6),
+       st.binary(max_size=30))
+def test_tracker_reply_of_any_shape_raises_only_tracker_error(d, junk):
+    from tritondl.fetch.bt.tracker import TrackerError, parse_announce_response
+    for body in (bencode.encode(d), junk):
+        try:
+            r = parse_announce_response(body)
+        except TrackerError:
+            continue
+        assert r.interval > 0 and all(0 < port < 65536 for _ip, port in r.peers)
+
+
+@SETTINGS
+@given(_bany, st.binary(max_size=30))
+def test_extension_messages_of_any_shape_raise_only_peer_error(d, tail):
+    for parse in (pw.parse_ext_handshake, pw.parse_pex, pw.parse_meta_msg):
+        for body in (bencode.encode(d) + tail, tail):
+            try:
+                parse(body)
+            except pw.PeerError:
+                pass

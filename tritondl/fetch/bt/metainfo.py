@@ -58,6 +58,8 @@ def _safe_component(c: bytes | str) -> str:
     SHA-1 so that names sharing a long prefix stay distinct, keeping the
     extension the media filter selects on.  anacrolix opens the full name and
     fails the download with ENAMETOOLONG."""
+    if not isinstance(c, (bytes, str)):
+        raise MetainfoError(f"path component is not a string: {type(c).__name__}")
     s = c.decode("utf-8", "surrogateescape") if isinstance(c, bytes) else c
     if s in ("", ".", "..") or "/" in s or "\x00" in s:
         raise MetainfoError(f"unsafe path component {s!r}")

@@ -429,7 +429,8 @@ def parse_ext_handshake(payload: bytes) -> ExtHandshake:
     if not isinstance(d, dict):
         raise PeerError("extended handshake is not a dict")
     m = {}
-    for k, v in (d.get(b"m") or {}).items():
+    mm = d.get(b"m")
+    for k, v in (mm.items() if isinstance(mm, dict) else ()):
         if isinstance(v, int):
             m[k.decode(errors="replace")] = v
     ms = d.get(b"metadata_size")
@@ -501,7 +502,10 @@ def meta_msg(msg_type: int, piece: int, total_size: int | None = None, data: byt
 
 
 def parse_meta_msg(payload: bytes) -> tuple[dict, bytes]:
-    d, n = bencode.decode_prefix(payload)
+    try:
+        d, n = bencode.decode_prefix(payload)
+    except bencode.BencodeError as e:
+        raise PeerError(f"bad ut_metadata message: {e}") from e
     if not isinstance(d, dict):
         raise PeerError("bad ut_metadata message")
     return d, payload[n:]

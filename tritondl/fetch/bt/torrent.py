@@ -1446,14 +1446,15 @@ class Torrent:
                 their = (p.ext.m.get("ut_metadata") if p.ext else None)
                 if not their:
                     return
-                if self.info is None or not isinstance(piece, int) or piece * BLOCK >= len(self.info.raw):
-                    p.wire.extended(their, pw.meta_msg(pw.META_REJECT, piece or 0))
+                if self.info is None or not isinstance(piece, int) or not 0 <= piece * BLOCK < len(self.info.raw):
+                    p.wire.extended(their, pw.meta_msg(pw.META_REJECT, piece if isinstance(piece, int) else 0))
                 else:
                     raw = self.info.raw
                     p.wire.extended(their, pw.meta_msg(pw.META_DATA, piece, len(raw),
                                                        raw[piece * BLOCK:(piece + 1) * BLOCK]))
-            elif t == pw.META_DATA and self.info is None and isinstance(piece, int):
-                self._meta[piece] = data
+            elif t == pw.META_DATA and self.info is None and isinstance(piece, int) and self._meta_size \
+                    and 0 <= piece < -(-self._meta_size // BLOCK) and len(data) <= BLOCK:
+                self._meta[piece] = data        # only pieces of the announced size: bounded memory
                 self._check_metadata()
             elif t == pw.META_REJECT:
                 p.meta_requested = False

@@ -79,12 +79,21 @@ async def http_announce(url: str, a: Announce, session: aiohttp.ClientSession | 
     finally:
         if own:
             await s.close()
+    return parse_announce_response(body)
+
+
+def parse_announce_response(body: bytes) -> AnnounceResult:
+    """BEP 3 / BEP 23 / BEP 7 HTTP announce reply: compact or dict peers,
+    ``peers6``; anything malformed is a TrackerError (never another type)."""
     try:
         d = bencode.decode(body)
     except bencode.BencodeError as e:
         raise TrackerError(f"bad tracker response: {e}") from e
+    if not isinstance(d, dict):
+        raise TrackerError("tracker response is not a dict")
     if b"failure reason" in d:
-        raise TrackerError(d[b"failure reason"].decode(errors="replace"))
+        why = d[b"failure reason"]
+        raise TrackerError(why.decode(errors="replace") if isinstance(why, bytes) else repr(why))
     peers: list[tuple[str, int]] = []
     p = d.get(b"peers", b"")
     if isinstance(p, bytes):
@@ -92,13 +101,22 @@ async def http_announce(url: str, a: Announce, session: aiohttp.ClientSession | 
     elif isinstance(p, list):
         for e in p:
             try:
-                peers.append((e[b"ip"].decode(), int(e[b"port"])))
-            except (KeyError, TypeError, ValueError):
-                pass
+                ip, port = e[b"ip"].decode(), int(e[b"port"])
+                ipaddress.ip_address(ip)
+            except (KeyError, TypeError, ValueError, AttributeError, UnicodeDecodeError):
+                continue
+            if 0 < port < 65536:
+                peers.append((ip, port))
     p6 = d.get(b"peers6", b"")
     if isinstance(p6, bytes):
         peers += parse_compact(p6, v6=True)
-    return AnnounceResult(int(d.get(b"interval", 1800)), peers, d.get(b"complete"), d.get(b"incomplete"))
+    iv = d.get(b"interval", 1800)
+
+    def count(k: bytes) -> int | None:
+        v = d.get(k)
+        return v if isinstance(v, int) and v >= 0 else None
+    return AnnounceResult(iv if isinstance(iv, int) and iv > 0 else 1800, peers, count(b"complete"),
+                          count(b"incomplete"))
 
 
 class _UDPProto(asyncio.DatagramProtocol):
