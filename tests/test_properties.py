@@ -6,9 +6,8 @@ decoder under any chunking and head/body split, the S3 multipart planner's
 invariants, SigV4 UriEncode and canonical queries against the spec's byte
 rule, the safety of server-supplied file names, and fuzzing of every parser of
 remote BitTorrent input (info dicts, magnets, tracker replies, extension
-messages).  Decoders must
-round-trip what the encoders produce and reject garbage only with their own
-error types."""
+messages).  Decoders must round-trip what the encoders produce and reject
+garbage only with their own error types."""
 
 import asyncio
 import math
