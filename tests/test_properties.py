@@ -14,7 +14,7 @@ import math
 import os
 
 import pytest
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, example, given, settings
 from hypothesis import strategies as st
 
 from tritondl.amqp import codec
@@ -451,3 +451,27 @@ def test_extension_messages_of_any_shape_raise_only_peer_error(d, tail):
                 parse(body)
             except pw.PeerError:
                 pass
+
+
+@SETTINGS
+@given(st.dictionaries(st.sampled_from([b"t", b"y", b"q", b"a", b"r", b"e"]),
+                       _bany | st.sampled_from([b"q", b"r", b"e", b"ping", b"find_node", b"get_peers",
+                                                b"announce_peer", b"aa"]), max_size=6) |
+       _bany, st.binary(max_size=30))
+@example({b"t": [1], b"y": b"r", b"r": {}}, b"")        # an unhashable transaction id
+def test_dht_datagram_of_any_shape_is_absorbed(msg, junk):
+    """Any KRPC datagram — query, reply or error, of any shape, from the
+    node a transaction waits on or another — is answered, resolves that
+    transaction or is dropped; nothing escapes into the event loop."""
+    from tritondl.fetch.bt import dht as D
+
+    async def main():
+        n = D.DHTNode()
+        f = asyncio.get_running_loop().create_future()
+        n._pending[b"aa"] = (("1.2.3.4", 5), f)
+        for data in (bencode.encode(msg), junk):
+            for addr in (("1.2.3.4", 5), ("5.6.7.8", 9)):
+                n._on_datagram(data, addr, 2)
+        if f.done() and not f.cancelled():
+            f.exception()
+    asyncio.run(main())

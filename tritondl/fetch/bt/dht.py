@@ -415,6 +415,8 @@ class DHTNode:
             return
         y = msg.get(b"y")
         t = msg.get(b"t", b"")
+        if not isinstance(t, bytes):
+            return                                           # transaction ids are strings (BEP 5)
         if y == b"q":
             self._on_query(msg, t, addr, fam)
         elif y in (b"r", b"e"):
