@@ -6,8 +6,9 @@ decoder under any chunking and head/body split, the S3 multipart planner's
 invariants, SigV4 UriEncode and canonical queries against the spec's byte
 rule, the safety of server-supplied file names, and fuzzing of every parser of
 remote BitTorrent input (info dicts, magnets, tracker replies, extension
-messages).  Decoders must round-trip what the encoders produce and reject
-garbage only with their own error types."""
+messages, KRPC datagrams) and of HTTP response heads.  Decoders must
+round-trip what the encoders produce and reject garbage only with their own
+error types."""
 
 import asyncio
 import math
@@ -475,3 +476,31 @@ def test_dht_datagram_of_any_shape_is_absorbed(msg, junk):
         if f.done() and not f.cancelled():
             f.exception()
     asyncio.run(main())
+
+
+# ------------------------------------------------- HTTP response heads (fuzz)
+
+_head_line = st.sampled_from(["Content-Length: 10", "Content-Length: -1", "Content-Length: 1e3",
+                              "Content-Length: 5, 5", "Content-Length: 5, 6", "Content-Length: ²",
+                              "Transfer-Encoding: chunked", "Connection: close", "Connection: keep-alive",
+                              "X: y", ": novalue", "bare"]) | st.text(max_size=30)
+
+
+@SETTINGS
+@given(st.sampled_from(["HTTP/1.1 200 OK", "HTTP/1.0 206 Partial", "HTTP/1.1 ²00 OK", "HTTP/1.1 20 OK",
+                        "ICY 200 OK", "HTTP/1.1 999"]) | st.text(max_size=20),
+       st.lists(_head_line, max_size=6))
+def test_response_head_of_any_shape(status, lines):
+    """Any response head parses to a status of three ASCII digits and a
+    Content-Length that is absent or a non-negative integer — or raises
+    RawHTTPError; never another exception (the relay sizes files by it)."""
+    from tritondl.utils.rawhttp import RawHTTPError, parse_head
+    raw = "\r\n".join([status] + lines).encode("latin-1", "replace")
+    try:
+        h = parse_head(raw)
+    except RawHTTPError:
+        return
+    assert 0 <= h.status <= 999
+    cl = h.content_length
+    assert cl is None or cl >= 0
+    assert not (h.keep_alive and h.chunked and "Content-Length" in h.headers)

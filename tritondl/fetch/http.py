@@ -433,6 +433,10 @@ class HTTPDownloader:
             filename_from_url(str(r.url)) or filename_from_url(url)
         if not name:
             raise HTTPDownloadError("no filename could be determined")
+        if size is not None:
+            size = size.split(",")[0].strip()            # "42, 42": a repeated, identical length
+            if not (size.isascii() and size.isdigit()):
+                raise HTTPDownloadError(f"GET {url}: bad Content-Length {r.headers.get('Content-Length')!r}")
         return _Probe(int(size) if size is not None and r.status == 200 else None,
                       r.headers.get("Accept-Ranges", "").lower() == "bytes", r.headers.get("ETag", ""),
                       r.headers.get("Last-Modified", ""), name, r.status)

@@ -114,7 +114,7 @@ class Head:
             return None
         v = self.headers.get("Content-Length")
         try:
-            return int(v) if v is not None else None
+            return int(v.split(",")[0]) if v is not None else None
         except ValueError:
             return None
 
@@ -668,10 +668,16 @@ async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int 
         if not d:
             raise RawHTTPError("connection closed before the response head")
         buf += d
-    lines = buf[:i].decode("latin-1").split("\r\n")
+    return parse_head(buf[:i], buf[i + 4:])
+
+
+def parse_head(raw: bytes, leftover: bytes = b"") -> Head:
+    """Status line and header fields of a response head (``raw`` without its
+    blank line); a malformed status line or Content-Length is a RawHTTPError."""
+    lines = raw.decode("latin-1").split("\r\n")
     ver, _, rest = lines[0].partition(" ")
     code, _, reason = rest.partition(" ")
-    if not ver.startswith("HTTP/") or not code.isdigit():
+    if not ver.startswith("HTTP/") or not (len(code) == 3 and code.isascii() and code.isdigit()):
         raise RawHTTPError(f"malformed status line {lines[0]!r}")
     hdrs: CIMultiDict = CIMultiDict()
     for ln in lines[1:]:
@@ -680,9 +686,14 @@ async def read_head(s: "RawConn | socket.socket", timeout: float, max_size: int 
             hdrs.add(k.strip(), v.strip())
     conn = hdrs.get("Connection", "").lower()
     keep = (ver == "HTTP/1.1" and conn != "close") or conn == "keep-alive"
-    if keep and "Content-Length" in hdrs and "chunked" in hdrs.get("Transfer-Encoding", "").lower():
+    chunked = "chunked" in hdrs.get("Transfer-Encoding", "").lower()
+    if keep and "Content-Length" in hdrs and chunked:
         keep = False            # ambiguous framing (RFC 9112 §6.3): never reuse this connection
-    return Head(int(code), reason, hdrs, buf[i + 4:], ver, keep)
+    if not chunked and "Content-Length" in hdrs:
+        cls = {x.strip() for v in hdrs.getall("Content-Length") for x in v.split(",")}   # "42, 42" is 42
+        if len(cls) != 1 or not all(v.isascii() and v.isdigit() for v in cls):
+            raise RawHTTPError(f"bad Content-Length {hdrs.getall('Content-Length')!r}")   # RFC 9112 §6.3
+    return Head(int(code), reason, hdrs, leftover, ver, keep)
 
 
 async def read_small_body(s: "RawConn | socket.socket", head: Head, timeout: float, limit: int = 16 << 20,
