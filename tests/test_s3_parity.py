@@ -314,3 +314,24 @@ def test_stale_resume_state_starts_over(tmp_path):
         await c.close()
         await s3.stop()
     run(main())
+
+
+def test_unparsable_xml_replies_are_s3_errors(tmp_path):
+    """A 2xx reply whose body is not XML (a proxy's HTML page, a truncated
+    body) fails the request as an S3Error like any other failure, never an
+    XML parser exception."""
+    async def main():
+        c = S3Client("http://127.0.0.1:9", Static("ak", "sk"), part_size=5 << 20, multipart_threshold=5 << 20)
+
+        async def garbage(*_a, **_k):
+            return 200, {}, b"<html>gateway"
+        c._do = garbage
+        p = tmp_path / "f.mkv"
+        p.write_bytes(os.urandom((5 << 20) + 1))
+        for call in (lambda: c.put_object("b", "k", str(p)), lambda: c.list_parts("b", "k", "u"),
+                     lambda: c.list_objects("b")):
+            with pytest.raises(S3Error) as ei:
+                await call()
+            assert ei.value.code == "MalformedXML"
+        await c.close()
+    run(main())

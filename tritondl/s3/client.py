@@ -69,6 +69,15 @@ class S3Error(Exception):
         self.region = region          # the bucket's region when S3 names it (XML <Region> / x-amz-bucket-region)
 
 
+def _xml(body: bytes, what: str) -> ET.Element:
+    """The root of a 2xx reply's XML body; a body that is not XML is an
+    S3Error (MalformedXML), like any other failed request."""
+    try:
+        return ET.fromstring(body)
+    except ET.ParseError as e:
+        raise S3Error(0, "MalformedXML", f"unparsable {what} reply: {e}") from e
+
+
 def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Error:
     code = msg = region = ""
     if body:
@@ -482,7 +491,7 @@ class S3Client:
         while True:
             _st, _h, body = await self._do("GET", bucket, key, query={"uploadId": upload_id,
                                                                        "part-number-marker": marker})
-            root = ET.fromstring(body)
+            root = _xml(body, "ListParts")
             for part in root.iter():
                 if part.tag.rsplit("}", 1)[-1] != "Part":
                     continue
@@ -541,7 +550,7 @@ class S3Client:
         if not upload_id:
             _st, _h, body = await self._do("POST", bucket, key, query={"uploads": ""},
                                            headers={"content-type": content_type}, body=b"")
-            root = ET.fromstring(body)
+            root = _xml(body, "InitiateMultipartUpload")
             upload_id = root.findtext(f"{S3_NS}UploadId") or root.findtext("UploadId") or ""
             if not upload_id:
                 raise S3Error(0, "MalformedXML", "no UploadId in InitiateMultipartUpload response")
@@ -577,7 +586,7 @@ class S3Client:
             _st, _h, rb = await self._do("POST", bucket, key, query={"uploadId": upload_id}, body=cbody)
             if b"<Error>" in rb:
                 raise _parse_error(200, rb, f"complete {key}")
-            r = ET.fromstring(rb)
+            r = _xml(rb, "CompleteMultipartUpload")
             if resume_path:
                 with contextlib.suppress(OSError):
                     os.remove(resume_path)
@@ -722,7 +731,7 @@ class S3Client:
             if token:
                 q["continuation-token"] = token
             _st, _h, b = await self._do("GET", bucket, query=q)
-            root = ET.fromstring(b)
+            root = _xml(b, "ListObjectsV2")
             for c in root.iter():
                 if c.tag.endswith("Contents"):
                     k = c.find(f"{S3_NS}Key")
