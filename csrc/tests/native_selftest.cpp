@@ -215,6 +215,84 @@ static void test_utp(double loss, size_t n, unsigned seed) {
   CHECK(cb >= 0 && B.eof(cb));
 }
 
+// Datagrams from a hostile peer into an engine with one live inbound
+// connection: random types, connection ids around the live one, sequence and
+// ack numbers near and far from the window, well-formed and truncated
+// extension chains, SACK bitmasks, payloads.  Under ASan/UBSan this is the
+// memory-safety check of the header parser and the ack / SACK / reorder paths
+// (tests/test_utp.py drives the same through the Python binding).
+static void test_utp_fuzz(unsigned seed, int rounds) {
+  using tritondl_utp::Engine;
+  std::mt19937_64 rng(seed);
+  auto put16 = [](std::string& s, size_t at, uint32_t v) {
+    s[at] = static_cast<char>(v >> 8);
+    s[at + 1] = static_cast<char>(v);
+  };
+  auto put32 = [](std::string& s, size_t at, uint32_t v) {
+    for (int k = 0; k < 4; ++k) s[at + k] = static_cast<char>(v >> (24 - 8 * k));
+  };
+  for (int r = 0; r < rounds; ++r) {
+    Engine e(seed + static_cast<unsigned>(r));
+    int64_t now = 1000000;
+    auto pkt = [&](unsigned type, uint16_t cid, uint16_t seq, uint16_t ack, uint8_t ext) {
+      std::string s(20, '\0');
+      s[0] = static_cast<char>((type << 4) | 1);
+      s[1] = static_cast<char>(ext);
+      put16(s, 2, cid);
+      put32(s, 4, static_cast<uint32_t>(rng()));
+      put32(s, 8, rng() % 2 ? 0u : static_cast<uint32_t>(rng()));
+      put32(s, 12, static_cast<uint32_t>(rng()));
+      put16(s, 16, seq);
+      put16(s, 18, ack);
+      return s;
+    };
+    e.incoming(pkt(4, 0x0fff, 100, 0, 0), "P:1", now);  // inbound SYN: connection 0x1000 is live
+    CHECK(!e.accepted().empty());
+    static const uint16_t ids[] = {0x1000, 0x1001, 0x0fff, 7};
+    for (int i = 0; i < 80; ++i) {
+      now += 997;
+      const unsigned type = static_cast<unsigned>(rng() % 7);
+      const uint16_t cid = ids[rng() % 4];
+      const uint16_t seq = static_cast<uint16_t>(rng() % 2 ? 100 + rng() % 40 : rng());
+      const uint16_t ack = static_cast<uint16_t>(rng());
+      std::string ext_chain;
+      uint8_t first = 0;
+      switch (rng() % 4) {
+        case 0: break;
+        case 1: {  // one SACK extension, bitmask of 4..12 bytes
+          first = 1;
+          const size_t len = 4 + (rng() % 3) * 4;
+          ext_chain = std::string{static_cast<char>(0), static_cast<char>(len)};
+          for (size_t k = 0; k < len; ++k) ext_chain += static_cast<char>(rng());
+          break;
+        }
+        case 2: {  // truncated / self-describing garbage chain
+          first = static_cast<uint8_t>(rng() % 4);
+          ext_chain.resize(rng() % 12);
+          for (auto& ch : ext_chain) ch = static_cast<char>(rng());
+          break;
+        }
+        default:  // unknown extension with a length past the end
+          first = 2;
+          ext_chain = std::string{static_cast<char>(0), static_cast<char>(200)} + "xy";
+      }
+      std::string payload(rng() % 1400, '\0');
+      for (auto& ch : payload) ch = static_cast<char>(rng());
+      e.incoming(pkt(type, cid, seq, ack, first) + ext_chain + payload, "P:1", now);
+      e.tick(now);
+      e.outgoing();
+    }
+    for (int c : e.accepted()) {
+      e.read(c);
+      e.state(c);
+    }
+    e.read(1);
+    e.state(1);
+    e.tick(now + 10000000);
+    e.outgoing();
+  }
+}
+
 static void test_merkle() {
   // one file of 3 leaves + 100 bytes in a 64 KiB piece: root over 4 leaves, 4th = zero hash
   std::mt19937 rng(11);
@@ -686,6 +764,7 @@ int main(int argc, char** argv) {
   test_tls_relay(quick ? (1u << 20) + 333 : (6u << 20) + 333);
   test_utp(0.0, quick ? 100000 : 400000, 1);
   test_utp(0.03, quick ? 60000 : 200000, 2);
+  test_utp_fuzz(5, quick ? 200 : 2000);
   test_btwire(7, quick ? 300 : 3000);
   test_chunked(3, quick ? 40 : 300);
   if (failures) {

@@ -193,3 +193,50 @@ def test_receive_batch_coalesces_acks():
     acks = b.outgoing()
     assert len(acks) == 1 and acks[0][1][0] >> 4 == 2     # one ST_STATE
     assert b.read(sid) == b"x" * (_utp.MSS * len(burst))
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+def _pkt(typ, conn_id, seq, ack, ext_chain=b"", first_ext=0, payload=b"", ts=0, ts_diff=0, wnd=1 << 20):
+    import struct
+    return struct.pack(">BBHIIIHH", (typ << 4) | 1, first_ext, conn_id, ts, ts_diff, wnd, seq, ack) + \
+        ext_chain + payload
+
+
+_packets = st.lists(st.tuples(
+    st.integers(0, 6),                                   # type (5, 6 invalid)
+    st.sampled_from([0x1000, 0x1001, 0x0fff, 7]),        # conn ids around the live connection
+    st.integers(0, 0xFFFF), st.integers(0, 0xFFFF),      # seq, ack
+    st.integers(0, 3),                                   # first extension (1 = selective ack)
+    st.binary(max_size=40),                              # extension chain bytes (often malformed)
+    st.binary(max_size=1500),                            # payload
+    st.integers(0, 2**32 - 1), st.integers(0, 2**32 - 1), st.integers(0, 2**32 - 1)),
+    max_size=40)
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(_packets, st.binary(max_size=64))
+def test_engine_survives_any_packet_sequence(pkts, junk):
+    """Remote peers control every byte of a uTP datagram: header fields,
+    the extension chain (lengths past the end, unknown types, odd SACK
+    bitmasks), sequence/ack numbers anywhere in the 16-bit space.  The
+    native engine must keep memory-safe (the sanitizer builds run the same
+    code) and keep answering; a live connection survives or is reset."""
+    e = _utp.Engine(11)
+    now = 1_000_000
+    e.incoming(_pkt(4, 0x0fff, 100, 0), "P:1", now)          # inbound SYN: conn 0x1000 live
+    assert e.accepted()
+    for typ, cid, seq, ack, ext, chain, payload, ts, tsd, wnd in pkts:
+        now += 997
+        r = e.incoming(_pkt(typ, cid, seq, ack, chain, ext, payload, ts, tsd, wnd), "P:1", now)
+        assert isinstance(r, int)
+        e.tick(now)
+        e.outgoing()
+    e.incoming(junk, "P:1", now)
+    for cid in list(e.accepted()) + [1]:
+        e.read(cid)
+        e.state(cid)
+    e.tick(now + 10_000_000)
+    e.outgoing()
