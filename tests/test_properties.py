@@ -504,3 +504,13 @@ def test_response_head_of_any_shape(status, lines):
     cl = h.content_length
     assert cl is None or cl >= 0
     assert not (h.keep_alive and h.chunked and "Content-Length" in h.headers)
+
+
+def test_tracker_dict_peers_take_ips_and_dns_names():
+    from tritondl.fetch.bt.tracker import parse_announce_response
+    body = bencode.encode({b"interval": 60, b"peers": [
+        {b"ip": b"10.0.0.1", b"port": 6881}, {b"ip": b"seed.example.org", b"port": 51413},
+        {b"ip": b"::1", b"port": 1}, {b"ip": b"bad host", b"port": 2}, {b"ip": b"10.0.0.2", b"port": 0},
+        {b"ip": 7, b"port": 3}, {b"port": 4}]})
+    r = parse_announce_response(body)
+    assert r.peers == [("10.0.0.1", 6881), ("seed.example.org", 51413), ("::1", 1)] and r.interval == 60

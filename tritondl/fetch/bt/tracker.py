@@ -9,6 +9,7 @@ import asyncio
 import ipaddress
 import os
 import random
+import re
 import socket
 import struct
 from dataclasses import dataclass
@@ -82,6 +83,18 @@ async def http_announce(url: str, a: Announce, session: aiohttp.ClientSession | 
     return parse_announce_response(body)
 
 
+_HOSTNAME = re.compile(r"[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)*\.?")
+
+
+def _peer_host(h: str) -> bool:
+    """BEP 3 dict peers: ``ip`` is an IP address or a DNS name."""
+    try:
+        ipaddress.ip_address(h)
+        return True
+    except ValueError:
+        return len(h) <= 253 and _HOSTNAME.fullmatch(h) is not None
+
+
 def parse_announce_response(body: bytes) -> AnnounceResult:
     """BEP 3 / BEP 23 / BEP 7 HTTP announce reply: compact or dict peers,
     ``peers6``; anything malformed is a TrackerError (never another type)."""
@@ -102,10 +115,9 @@ def parse_announce_response(body: bytes) -> AnnounceResult:
         for e in p:
             try:
                 ip, port = e[b"ip"].decode(), int(e[b"port"])
-                ipaddress.ip_address(ip)
             except (KeyError, TypeError, ValueError, AttributeError, UnicodeDecodeError):
                 continue
-            if 0 < port < 65536:
+            if 0 < port < 65536 and _peer_host(ip):
                 peers.append((ip, port))
     p6 = d.get(b"peers6", b"")
     if isinstance(p6, bytes):
