@@ -415,6 +415,9 @@ def test_redirects_followed_natively(tmp_path):
         o.redirect("/loop", "/loop")
         with pytest.raises(H.HTTPDownloadError):
             await _dl(max_retries=0).download(str(tmp_path), Sink(), o.url("/loop"))
+        o.redirect("/bad", "http://[::1")                                  # unparsable Location
+        with pytest.raises(H.HTTPDownloadError, match="bad redirect Location"):
+            await _dl(max_retries=0).download(str(tmp_path), Sink(), o.url("/bad"))
         await h.close()
         await o.stop()
     run(main())

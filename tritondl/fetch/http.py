@@ -348,7 +348,10 @@ class HTTPDownloader:
             loc = h.headers.get("Location")
             if h.status in (301, 302, 303, 307, 308) and loc:
                 conn.close()                  # small redirect body: not worth draining for keep-alive
-                url = str(u.join(URL(loc)))
+                try:
+                    url = str(u.join(URL(loc)))
+                except (ValueError, TypeError) as e:
+                    raise HTTPDownloadError(f"GET {url}: bad redirect Location {loc!r}") from e
                 if not url.startswith(("http://", "https://")):
                     return None
                 continue
