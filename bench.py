@@ -464,6 +464,7 @@ def main() -> int:
         diag = {**lease, **_PLACEMENT,
                 "job_latency_ms": ({"min": round(lat[0] * 1000, 2), "max": round(lat[-1] * 1000, 2),
                                     "first": round(done[0].seconds * 1000, 2),
+                                    "first_marks": {k: round(v * 1000, 2) for k, v in done[0].marks.items()},
                                     "last": round(done[-1].seconds * 1000, 2)} if done else None),
                 "cpu_mhz_pinned": {"start": mhz0, "end": mhz1},
                 "memcpy_GBps": {"start": mem0, "end": mem1},
