@@ -84,6 +84,24 @@ def test_compact_peers():
     assert parse_compact(bytes([127, 0, 0, 1, 0x1A, 0xE1])) == [("127.0.0.1", 6881)]
 
 
+def test_udp_tracker_over_ipv6_returns_ipv6_peers():
+    """BEP 15: over IPv6 the announce reply carries 18-byte peers; read as
+    6-byte IPv4 entries they would be three garbage addresses each."""
+    from tritondl.fetch.bt.tracker import udp_announce
+
+    async def main():
+        tr = await UDPTracker().start("::1")
+        assert tr.url.startswith("udp://[::1]:")
+        ih = hashlib.sha1(b"v6").digest()
+        a1 = Announce(ih, b"-A-" + bytes(17), 51413, 0, 0, 100, "started")
+        a2 = Announce(ih, b"-B-" + bytes(17), 6881, 0, 0, 100, "started")
+        assert (await udp_announce(tr.url, a1)).peers == []
+        r = await udp_announce(tr.url, a2)
+        assert r.peers == [("::1", 51413)]
+        tr.stop()
+    run(main())
+
+
 # ----------------------------------------------------------------- swarm
 
 

@@ -73,16 +73,19 @@ class UDPTracker(asyncio.DatagramProtocol):
         self.conn_ids: set[int] = set()
         self.transport: asyncio.DatagramTransport | None = None
         self.port = 0
+        self.host = "127.0.0.1"
 
     async def start(self, host: str = "127.0.0.1", port: int = 0) -> "UDPTracker":
         loop = asyncio.get_running_loop()
         self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(host, port))
         self.port = self.transport.get_extra_info("sockname")[1]
+        self.host = host
         return self
 
     @property
     def url(self) -> str:
-        return f"udp://127.0.0.1:{self.port}/announce"
+        h = f"[{self.host}]" if ":" in self.host else self.host
+        return f"udp://{h}:{self.port}/announce"
 
     def stop(self) -> None:
         if self.transport:
@@ -103,8 +106,9 @@ class UDPTracker(asyncio.DatagramProtocol):
             me = (addr[0], port)
             peers = [p for p in sw if p != me]
             sw.add(me)
-            self.transport.sendto(struct.pack(">IIIII", 1, tid, 10, 0, len(sw)) + compact_peers(peers),  # type: ignore[union-attr]
-                                  addr)
+            v6 = ":" in addr[0]                    # BEP 15: IPv6 transport, 18-byte peers
+            self.transport.sendto(struct.pack(">IIIII", 1, tid, 10, 0, len(sw)) +  # type: ignore[union-attr]
+                                  compact_peers(peers, v6=v6), addr)
         else:
             self.transport.sendto(struct.pack(">II", 3, tid) + b"bad request", addr)  # type: ignore[union-attr]
 

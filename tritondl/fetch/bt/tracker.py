@@ -55,7 +55,10 @@ def parse_compact(b: bytes, v6: bool = False) -> list[tuple[str, int]]:
     return out
 
 
-def compact_peers(peers: list[tuple[str, int]]) -> bytes:
+def compact_peers(peers: list[tuple[str, int]], v6: bool = False) -> bytes:
+    """Compact peer list: 6-byte IPv4 entries, or (``v6``) 18-byte IPv6 ones."""
+    if v6:
+        return b"".join(socket.inet_pton(socket.AF_INET6, h) + struct.pack(">H", p) for h, p in peers if ":" in h)
     return b"".join(socket.inet_aton(h) + struct.pack(">H", p) for h, p in peers if ":" not in h)
 
 
@@ -183,7 +186,10 @@ async def udp_announce(url: str, a: Announce, timeout: float = 5.0, retries: int
         if len(r) < 20:
             raise TrackerError("short announce response")
         interval, leech, seed = struct.unpack(">III", r[8:20])
-        return AnnounceResult(interval, parse_compact(r[20:]), seed, leech)
+        # BEP 15: a tracker reached over IPv6 answers with 18-byte IPv6 peers
+        sock = tr.get_extra_info("socket")
+        v6 = sock is not None and sock.family == socket.AF_INET6
+        return AnnounceResult(interval, parse_compact(r[20:], v6=v6), seed, leech)
     finally:
         tr.close()
 
