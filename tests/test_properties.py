@@ -420,6 +420,7 @@ def test_info_dict_of_any_shape_raises_only_metainfo_error(d):
 @SETTINGS
 @given(st.dictionaries(st.sampled_from([b"info", b"announce", b"announce-list", b"url-list", b"piece layers"]),
                        _bany, max_size=5), st.text(max_size=80))
+@example({}, "xt=urn:btih:" + "ab" * 20 + "&x.pe=1.2.3.4:²")      # a Unicode digit in a peer port
 def test_torrent_file_and_magnet_raise_only_metainfo_error(d, q):
     from tritondl.fetch.bt.metainfo import Metainfo, MetainfoError, parse_magnet
     for f in (lambda: Metainfo.parse(bencode.encode(d)), lambda: parse_magnet("magnet:?" + q)):

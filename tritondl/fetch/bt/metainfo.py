@@ -438,7 +438,7 @@ def parse_magnet(uri: str) -> Magnet:
     peers = []
     for pe in q.get("x.pe", []):
         host, _, port = pe.rpartition(":")
-        if host and port.isdigit():
+        if host and port.isascii() and port.isdigit() and 0 < int(port) < 65536:
             peers.append((host.strip("[]"), int(port)))
     return Magnet(ih, unquote(q.get("dn", [""])[0]), q.get("tr", []), peers, q.get("ws", []), ih2, has_v1)
 
