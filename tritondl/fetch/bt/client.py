@@ -42,7 +42,7 @@ def _parse_hostports(s: str) -> list[tuple[str, int]]:
         h, _, p = part.rpartition(":")
         if h.startswith("[") and h.endswith("]"):
             h = h[1:-1]                  # [v6 address]:port
-        if h and p.isdigit():
+        if h and p.isascii() and p.isdigit():
             out.append((h, int(p)))
     return out
 

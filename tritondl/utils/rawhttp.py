@@ -128,7 +128,7 @@ def split_host(hostport: str, default_port: int = 80) -> tuple[str, int]:
         h, _, rest = hostport[1:].partition("]")
         return h, int(rest[1:]) if rest.startswith(":") else default_port
     h, sep, p = hostport.rpartition(":")
-    if sep and p.isdigit() and ":" not in h:
+    if sep and p.isascii() and p.isdigit() and ":" not in h:
         return h, int(p)
     return hostport, default_port
 
