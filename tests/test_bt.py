@@ -352,6 +352,43 @@ def test_webseed_only_multi_file_torrent_file(tmp_path):
     run(main())
 
 
+def test_webseed_ignoring_range_is_streamed_not_buffered_and_dropped_when_far(tmp_path, monkeypatch):
+    """A web seed that answers Range requests with 200 and the whole file:
+    each span is read by streaming past the prefix, holding only the span;
+    once a span would stream past IGNORED_RANGE_MAX_SKIP the seed is
+    dropped rather than re-reading a large file per piece."""
+    from tritondl.fetch.bt import webseed as W
+
+    async def main(limit):
+        monkeypatch.setattr(W, "IGNORED_RANGE_MAX_SKIP", limit)
+        src = tmp_path / "src"
+        make_payload(str(src), {"film.mkv": 200_000})
+        info = torrent_for(str(src / "film.mkv"), 16384)
+        o = await Origin().start()
+        o.ranges = False
+        o.add("/seed/film.mkv", (src / "film.mkv").read_bytes())
+        url = o.add("/t.torrent", torrent_file_bytes(info, url_list=[f"http://127.0.0.1:{o.port}/seed/film.mkv"]))
+        dst = tmp_path / f"job{limit}"
+        os.makedirs(dst)
+        t, _ = await _dl().open(str(dst), url)
+        await t.download_all()
+        ws = t.webseed_clients[0]
+        if limit >= 200_000:
+            await asyncio.wait_for(t.complete.wait(), 30)
+            assert ws.pieces_ok == info.num_pieces and not ws.dead
+            assert (dst / "film.mkv").read_bytes() == (src / "film.mkv").read_bytes()
+        else:
+            for _ in range(200):
+                if ws.dead:
+                    break
+                await asyncio.sleep(0.05)
+            assert ws.dead and ws.pieces_ok <= limit // 16384 + 1
+        await t.close()
+        await o.stop()
+    run(main(1 << 20))
+    run(main(40_000))
+
+
 def test_webseed_via_magnet_ws_single_file_and_bad_seed_dropped(tmp_path):
     async def main():
         src = tmp_path / "src"

@@ -26,6 +26,28 @@ if TYPE_CHECKING:  # pragma: no cover
     from .torrent import Torrent
 
 
+# a web seed answering Range with 200 is streamed past at most this many bytes per span
+IGNORED_RANGE_MAX_SKIP = 64 << 20
+
+
+async def _read_span(r: aiohttp.ClientResponse, skip: int, n: int) -> bytes:
+    """``n`` bytes of the body after the first ``skip``; never holds more
+    than ``n`` bytes, whatever the server sends (an over-long body is left
+    unread and its connection closed)."""
+    while skip > 0:
+        chunk = await r.content.read(min(skip, 1 << 20))
+        if not chunk:
+            return b""
+        skip -= len(chunk)
+    out = bytearray()
+    while len(out) < n:
+        chunk = await r.content.read(min(n - len(out), 1 << 20))
+        if not chunk:
+            break
+        out += chunk
+    return bytes(out)
+
+
 class WebSeedError(Exception):
     pass
 
@@ -120,10 +142,15 @@ class WebSeed:
             hdr = {"Range": f"bytes={off}-{off + n - 1}"}
             async with session.get(url, headers=hdr) as r:
                 if r.status == 206:
-                    data = await r.read()
+                    data = await _read_span(r, 0, n)
                 elif r.status == 200:
-                    # server ignored Range: take our slice of the full body
-                    data = (await r.read())[off:off + n]
+                    # server ignored Range: take our slice of the full body, streaming
+                    # past the bytes before it; a seed that would make every piece
+                    # stream a large prefix is dropped (never buffered whole)
+                    if off > IGNORED_RANGE_MAX_SKIP:
+                        self.dead = True
+                        raise WebSeedError(f"{url} ignores Range requests; dropping the web seed")
+                    data = await _read_span(r, off, n)
                 else:
                     raise WebSeedError(f"HTTP {r.status} for {url}")
             if len(data) != n:
