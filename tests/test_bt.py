@@ -84,6 +84,23 @@ def test_compact_peers():
     assert parse_compact(bytes([127, 0, 0, 1, 0x1A, 0xE1])) == [("127.0.0.1", 6881)]
 
 
+def test_http_tracker_reply_is_size_capped():
+    """A tracker that streams an endless or huge reply is cut off at
+    MAX_REPLY instead of being buffered whole."""
+    from tritondl.fetch.bt import tracker as T
+
+    async def main():
+        o = await Origin().start()
+        url = o.add("/announce", b"d8:intervali60e5:peers" + b"6000000:" + bytes(6_000_000) + b"e")
+        a = Announce(hashlib.sha1(b"cap").digest(), b"-A-" + bytes(17), 51413)
+        with pytest.raises(T.TrackerError, match="larger than"):
+            await T.http_announce(url, a)
+        small = o.add("/small", bencode.encode({b"interval": 60, b"peers": bytes([10, 0, 0, 1, 0x1A, 0xE1])}))
+        assert (await T.http_announce(small, a)).peers == [("10.0.0.1", 6881)]
+        await o.stop()
+    run(main())
+
+
 def test_udp_tracker_over_ipv6_returns_ipv6_peers():
     """BEP 15: over IPv6 the announce reply carries 18-byte peers; read as
     6-byte IPv4 entries they would be three garbage addresses each."""

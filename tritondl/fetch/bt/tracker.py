@@ -44,6 +44,9 @@ class AnnounceResult:
     leechers: int | None = None
 
 
+MAX_REPLY = 4 << 20          # an HTTP announce reply (200 dict peers is ~20 KB): more is refused
+
+
 def parse_compact(b: bytes, v6: bool = False) -> list[tuple[str, int]]:
     step = 18 if v6 else 6
     out = []
@@ -75,15 +78,19 @@ async def http_announce(url: str, a: Announce, session: aiohttp.ClientSession | 
     try:
         from yarl import URL
         async with s.get(URL(full, encoded=True), timeout=aiohttp.ClientTimeout(total=timeout)) as r:
-            body = await r.read()
             if r.status != 200:
                 raise TrackerError(f"tracker HTTP {r.status}")
+            body = bytearray()
+            while chunk := await r.content.read(64 << 10):
+                body += chunk
+                if len(body) > MAX_REPLY:
+                    raise TrackerError(f"tracker reply larger than {MAX_REPLY} bytes")
     except (aiohttp.ClientError, asyncio.TimeoutError) as e:
         raise TrackerError(f"tracker request failed: {e}") from e
     finally:
         if own:
             await s.close()
-    return parse_announce_response(body)
+    return parse_announce_response(bytes(body))
 
 
 _HOSTNAME = re.compile(r"[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)*\.?")
