@@ -258,6 +258,7 @@ PYBIND11_MODULE(_utp, m) {
         d["timeouts"] = s.timeouts;
         d["fast_retransmits"] = s.fast_retransmits;
         d["window_full_drops"] = s.window_full_drops;
+        d["ooo_bytes"] = s.ooo_bytes;
         d["addr"] = s.addr;
         return d;
       })

@@ -146,6 +146,7 @@ struct Conn {
   uint32_t our_delay = 0;
   // receive side
   std::map<uint16_t, std::string> ooo;  // out-of-order payloads keyed by seq
+  size_t ooo_bytes = 0;                  // their total: held to the receive window
   std::string inbuf;                    // in-order bytes for the app
   bool fin_received = false;
   uint16_t fin_seq = 0;
@@ -421,6 +422,7 @@ class Engine {
     uint32_t inflight = 0, our_delay_us = 0;
     uint64_t bytes_sent = 0, bytes_recv = 0, retransmits = 0, timeouts = 0, fast_retransmits = 0;
     uint64_t window_full_drops = 0;
+    uint64_t ooo_bytes = 0;
     std::string addr;
   };
 
@@ -440,6 +442,7 @@ class Engine {
     s.timeouts = c->timeouts;
     s.fast_retransmits = c->fast_retransmits;
     s.window_full_drops = c->window_full_drops;
+    s.ooo_bytes = c->ooo_bytes;
     s.addr = c->addr;
     return s;
   }
@@ -636,8 +639,13 @@ class Engine {
       return;
     }
     if (seq != expect) {
-      if (seq_diff(seq, expect) < 1024 && !c.ooo.count(seq))
-        c.ooo[seq] = fin ? std::string() : std::string(payload, payload_n);
+      // a peer may send up to 1024 packets ahead, but what it parks here stays
+      // within the receive window we advertise (datagrams can be 64 KiB each)
+      const size_t n = fin ? 0 : payload_n;
+      if (seq_diff(seq, expect) < 1024 && !c.ooo.count(seq) && c.ooo_bytes + n <= kRecvWindow) {
+        c.ooo[seq] = std::string(payload, n);
+        c.ooo_bytes += n;
+      }
       c.need_ack = true;
       return;
     }
@@ -664,6 +672,7 @@ class Engine {
         c.bytes_recv += it->second.size();
       }
       c.ack_nr = it->first;
+      c.ooo_bytes -= it->second.size();
       c.ooo.erase(it);
     }
     c.need_ack = true;

@@ -240,3 +240,26 @@ def test_engine_survives_any_packet_sequence(pkts, junk):
         e.state(cid)
     e.tick(now + 10_000_000)
     e.outgoing()
+
+
+def test_out_of_order_buffer_stays_within_the_receive_window():
+    """A peer may send up to 1024 packets ahead of the next expected one;
+    with 60 KiB datagrams that parked 60 MiB per connection.  What the
+    engine holds out of order is capped at the advertised window, and the
+    stream still completes in order once the gap is filled."""
+    e = _utp.Engine(5)
+    now = 1_000_000
+    e.incoming(_pkt(4, 0x0fff, 99, 0), "P:1", now)         # SYN seq 99: next DATA expected is 100
+    (cid,) = e.accepted()
+    big = 60 * 1024
+    for k in range(1, 200):                                # seq 101..299, all ahead of 100
+        e.incoming(_pkt(0, 0x1000, 100 + k, 0, payload=bytes([k % 256]) * big), "P:1", now)
+    assert e.stats(cid)["ooo_bytes"] <= 1 << 20
+    small = [bytes([k]) * 1000 for k in range(1, 11)]
+    e2 = _utp.Engine(6)
+    e2.incoming(_pkt(4, 0x0fff, 99, 0), "P:1", now)
+    (c2,) = e2.accepted()
+    for k in range(10, 0, -1):                            # 110..101 arrive first, in reverse
+        e2.incoming(_pkt(0, 0x1000, 100 + k, 0, payload=small[k - 1]), "P:1", now)
+    e2.incoming(_pkt(0, 0x1000, 100, 0, payload=b"head"), "P:1", now)
+    assert e2.read(c2) == b"head" + b"".join(small) and e2.stats(c2)["ooo_bytes"] == 0
