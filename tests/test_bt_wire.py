@@ -23,6 +23,8 @@ import socket
 import struct
 from urllib.parse import unquote_to_bytes
 
+import pytest
+
 from tritondl.fetch.bt import bencode
 from tritondl.fetch.bt import dht as D
 from tritondl.fetch.bt import peer as pw
@@ -361,3 +363,40 @@ def test_unsolicited_or_out_of_range_metadata_pieces_are_not_kept(tmp_path):
         d, body = pw.parse_meta_msg(p.wire.sent[-1][1])
         assert d[b"msg_type"] == pw.META_REJECT and body == b""
     asyncio.run(main())
+
+
+def test_peer_messages_of_any_shape_end_only_that_peer(tmp_path):
+    """Every message id with any payload (short fixed fields, a bitfield
+    too short for the torrent, out-of-range indices) is handled or ends the
+    peer with PeerError / struct.error (caught per peer by the session);
+    nothing else escapes into the session."""
+    import asyncio
+    import struct
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig, _Peer
+
+    make_payload(str(tmp_path / "src"), {"a.mkv": 100_000})
+    info = torrent_for(str(tmp_path / "src" / "a.mkv"), 16384)
+
+    class AnyWire:
+        def __getattr__(self, _k):
+            return lambda *a, **kw: None
+
+    @settings(max_examples=300, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(st.lists(st.tuples(st.integers(0, 25), st.binary(max_size=40)), max_size=20))
+    def check(msgs):
+        async def main():
+            t = Torrent(info.infohash, str(tmp_path / "dst"), TorrentConfig(native_wire=False), info=info)
+            hs = pw.Handshake(bytes([0, 0, 0, 0, 0, 0x10, 0, 0x04]), info.infohash, b"x" * 20)
+            p = _Peer(AnyWire(), ("1.2.3.4", 5), hs, info.num_pieces)
+            for mid, pl in msgs:
+                try:
+                    await t._dispatch(p, mid, pl)
+                except (pw.PeerError, struct.error):
+                    pass
+        asyncio.run(main())
+    check()
+    with pytest.raises(pw.PeerError):
+        pw.bits_to_set(b"", 7)

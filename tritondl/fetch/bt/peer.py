@@ -512,6 +512,10 @@ def parse_meta_msg(payload: bytes) -> tuple[dict, bytes]:
 
 
 def bits_to_set(bits: bytes, n: int) -> set[int]:
+    """Pieces set in a BITFIELD; one shorter than ``n`` bits is a protocol
+    violation (BEP 3: drop the connection), a PeerError."""
+    if len(bits) < (n + 7) // 8:
+        raise PeerError(f"bitfield of {len(bits)} bytes for {n} pieces")
     out = set()
     for i in range(n):
         if bits[i >> 3] & (0x80 >> (i & 7)):

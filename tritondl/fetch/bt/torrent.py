@@ -889,7 +889,8 @@ class Torrent:
             if self.info is not None and self._downloading:
                 self._send_have_state(p)
             await self._peer_loop(p)
-        except (OSError, asyncio.IncompleteReadError, pw.PeerError, ConnectionError) as e:
+        except (OSError, asyncio.IncompleteReadError, pw.PeerError, ConnectionError, struct.error) as e:
+            # struct.error: a message shorter than its type's fixed fields (protocol violation)
             log.with_fields(peer=f"{addr[0]}:{addr[1]}", error=str(e) or type(e).__name__).debug("peer closed")
         finally:
             self._drop_peer(p)
@@ -1493,6 +1494,10 @@ class Torrent:
         for p in self.peers.values():
             pend = getattr(p, "pending_bitfield", None)
             if pend is not None:
-                self._peer_has(p, sorted(pw.bits_to_set(pend, info.num_pieces)))
+                try:
+                    self._peer_has(p, sorted(pw.bits_to_set(pend, info.num_pieces)))
+                except pw.PeerError:
+                    p.wire.close()           # its early bitfield does not fit the torrent: drop it
+                    continue
             if getattr(p, "pending_have_all", False):
                 self._peer_has(p, range(info.num_pieces))
