@@ -6,7 +6,7 @@ over days it starts and stops HIP hundreds of times.  This runs that cycle
 ``--cycles`` times with a short idle timeout and reports, per cycle: helper
 start + verify latency, its exit status, whether a corrupted piece was
 caught, and the driving process's RSS / fds / threads; plus the card's VRAM
-in use after each exit when the driver exposes it in sysfs.  Anything the
+in use after each exit when sysfs shows exactly one card.  Anything the
 helper leaks on the card or in the worker shows up as drift.
 
     python tools/gpu_churn.py --cycles 100 --mb 256 --out gpurun_out/churn.jsonl
@@ -27,16 +27,16 @@ sys.path.insert(0, ROOT)
 
 
 def _vram_used() -> int | None:
-    tot = 0
-    found = False
-    for f in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
-        try:
-            with open(f) as fh:
-                tot += int(fh.read())
-                found = True
-        except (OSError, ValueError):
-            pass
-    return tot if found else None
+    """VRAM in use on the card, when sysfs shows exactly one; with several
+    cards (other tenants' included) the sum would not be this process's."""
+    cards = glob.glob("/sys/class/drm/card*/device/mem_info_vram_used")
+    if len(cards) != 1:
+        return None
+    try:
+        with open(cards[0]) as fh:
+            return int(fh.read())
+    except (OSError, ValueError):
+        return None
 
 
 def _proc() -> dict:
