@@ -515,3 +515,19 @@ def test_tracker_dict_peers_take_ips_and_dns_names():
         {b"ip": 7, b"port": 3}, {b"port": 4}]})
     r = parse_announce_response(body)
     assert r.peers == [("10.0.0.1", 6881), ("seed.example.org", 51413), ("::1", 1)] and r.interval == 60
+
+
+@SETTINGS
+@given(st.binary(max_size=24) | st.sampled_from([b"-5", b"+5", b"0x5", b" 5", b"", b"5;ext=1", b"fffffffffffffffff",
+                                                 b"A", b"10 "]))
+def test_chunk_size_line_is_hex_or_an_error(line):
+    """A chunk-size line is parsed as RFC 9112 hex (with optional
+    extensions and trailing blanks) or refused; never a negative size."""
+    from tritondl.utils.rawhttp import RawHTTPError, _chunk_size
+    try:
+        n = _chunk_size(line)
+    except RawHTTPError:
+        return
+    assert n >= 0
+    digits = line.split(b";", 1)[0].rstrip(b" \t")
+    assert int(digits, 16) == n and not digits.startswith((b"-", b"+", b"0x", b"0X"))

@@ -696,6 +696,20 @@ def parse_head(raw: bytes, leftover: bytes = b"") -> Head:
     return Head(int(code), reason, hdrs, leftover, ver, keep)
 
 
+_HEX = frozenset(b"0123456789abcdefABCDEF")
+
+
+def _chunk_size(line: bytes) -> int:
+    """RFC 9112 §7.1 chunk-size (hex digits, optional ``;ext``).  Anything
+    else — a sign, ``0x``, spaces, an empty or over-long size — is a
+    RawHTTPError: ``int(x, 16)`` took "-5", whose negative length then moved
+    the parser backwards over the same line forever."""
+    size = line.split(b";", 1)[0].rstrip(b" \t")
+    if not size or len(size) > 16 or not all(c in _HEX for c in size):
+        raise RawHTTPError(f"bad chunk size {line[:40]!r}")
+    return int(size, 16)
+
+
 async def read_small_body(s: "RawConn | socket.socket", head: Head, timeout: float, limit: int = 16 << 20,
                           method: str = "GET") -> bytes:
     """Whole body of a small response (Content-Length, chunked, or until
@@ -724,7 +738,7 @@ async def read_small_body(s: "RawConn | socket.socket", head: Head, timeout: flo
             while (j := buf.find(b"\r\n", pos)) < 0:
                 if not await more():
                     raise RawHTTPError("connection closed inside a chunked body")
-            n = int(bytes(buf[pos:j]).split(b";")[0] or b"0", 16)
+            n = _chunk_size(bytes(buf[pos:j]))
             while len(buf) < j + 2 + n + 2:
                 if not await more():
                     raise RawHTTPError("connection closed inside a chunked body")
