@@ -113,3 +113,19 @@ def test_s3_hash_device_knob():
     assert Config.from_env({"TRITONDL_S3_HASH_DEVICE": "gpu"}).s3_hash_device == "gpu"
     with _p.raises(ValueError):
         Config.from_env({"TRITONDL_S3_HASH_DEVICE": "tpu"})
+
+
+def test_known_peers_are_bounded_at_the_high_water_mark():
+    """anacrolix TorrentPeersHighWater (500): a flood of PEX / tracker
+    addresses keeps the known set bounded; connected ones are never the ones
+    replaced."""
+    from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+    t = Torrent(b"\x05" * 20, "/tmp", TorrentConfig(established_conns=0, half_open_conns=0))
+    assert t.cfg.peers_high_water == 500
+    t.peers[("10.0.0.1", 1)] = object()
+    t.known.add(("10.0.0.1", 1))
+    t.add_peer_addrs([(f"10.{k >> 16 & 255}.{k >> 8 & 255}.{k & 255}", 6881) for k in range(5000)])
+    for k in range(2000):
+        t.add_peer_addr((f"11.0.{k >> 8}.{k & 255}", 51413))
+    assert len(t.known) == 500 and ("10.0.0.1", 1) in t.known
+    t.peers.clear()

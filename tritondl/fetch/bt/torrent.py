@@ -64,6 +64,9 @@ class TorrentConfig:
     # HalfOpenConnsPerTorrent 25 — peers with a finished handshake, and dials in flight
     established_conns: int = 50
     half_open_conns: int = 25
+    # anacrolix TorrentPeersHighWater: addresses remembered per torrent (trackers,
+    # DHT, PEX); past it a new one replaces an unconnected one
+    peers_high_water: int = 500
     pipeline: int = 128
     listen_host: str = "0.0.0.0"
     listen_port: int = 0             # 0 = ephemeral (the worker's Config passes anacrolix's 42069)
@@ -712,7 +715,7 @@ class Torrent:
         for a in addrs:
             if not self.closed and a not in self.banned and a[1] > 0 and \
                     not (a[1] == self.port and a[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host)):
-                self.known.add(a)
+                self._remember(a)
         free = self._dial_slots()
         if free > 0:
             for a in self._best_candidates(free):
@@ -725,10 +728,24 @@ class Torrent:
             return
         if addr[1] == self.port and addr[0] in ("127.0.0.1", "0.0.0.0", self.cfg.announce_host):
             return
-        self.known.add(addr)
+        self._remember(addr)
         if self._dial_slots() > 0:
             self.connecting.add(addr)
             self._spawn(self._connect(addr))
+
+    def _remember(self, a: tuple[str, int]) -> None:
+        """Add ``a`` to the known addresses, bounded at ``peers_high_water``:
+        a PEX or tracker flood cannot grow the set without limit."""
+        if a in self.known:
+            return
+        if len(self.known) >= self.cfg.peers_high_water:
+            for old in self.known:
+                if old not in self.peers and old not in self.connecting:
+                    self.known.discard(old)      # the loop ends here: no further iteration
+                    break
+            else:
+                return                           # every known address is in use
+        self.known.add(a)
 
     def _dial_slots(self) -> int:
         """Dials that may start now: half-open connections are capped at
