@@ -50,6 +50,8 @@ from ...utils.log import log
 from . import bencode
 
 K = 8
+LOOKUP_MAX_VALUES_PER_REPLY = 500    # BEP 5 replies fit a datagram: ~250 compact IPv4 peers at 1500 B
+LOOKUP_MAX_PEERS = 5000              # peers one get_peers lookup collects (the torrent keeps 500)
 ALPHA = 3
 ID_BITS = 160
 
@@ -684,6 +686,7 @@ class DHTNode:
         known: dict[bytes, tuple[str, int]] = {n.id: n.addr for n in table.closest(target, 2 * self.lookup_width)}
         state: dict[bytes, str] = {nid: "new" for nid in known}       # new | wait | ok | dead
         found: list[tuple[str, int]] = []
+        seen: set[tuple[str, int]] = set()
         tokens: dict[bytes, tuple[tuple[str, int], bytes]] = {}
         inflight: dict[asyncio.Task, bytes] = {}
         st = {"queries": 0, "responses": 0, "timeouts": 0}
@@ -727,10 +730,13 @@ class DHTNode:
                         tokens[nid] = (known[nid], tok)
                     vals = r.get(b"values")
                     if isinstance(vals, list):
-                        for p in parse_values(vals):
-                            if p not in found:
+                        # a datagram can carry thousands of values or nodes: take what an
+                        # honest node sends (values up to the lookup's cap, K nodes)
+                        for p in parse_values(vals[:LOOKUP_MAX_VALUES_PER_REPLY]):
+                            if p not in seen and len(found) < LOOKUP_MAX_PEERS:
+                                seen.add(p)
                                 found.append(p)
-                    for cid, ca in self._parse_reply_nodes(r, fam):
+                    for cid, ca in self._parse_reply_nodes(r, fam)[:2 * K]:
                         if cid == self.id or cid in state:
                             continue
                         known[cid] = ca
