@@ -5,7 +5,7 @@ ROCM_ARCH  ?= gfx950
 IMAGE      ?= tritondl:latest
 PYTEST     := $(PYTHON) -m pytest
 
-.PHONY: all build build-force test test-gpu test-all sanitize bench bench-multi profile-gpu docker-build clean lint
+.PHONY: all build build-force test test-gpu test-all sanitize odr-check bench bench-multi profile-gpu docker-build clean lint
 
 all: build
 
@@ -30,6 +30,10 @@ test-all: test test-gpu
 sanitize:
 	$(PYTHON) tools/native_selftest.py --sanitize
 
+## every shared native header linked into two translation units (no non-inline definitions)
+odr-check:
+	$(PYTHON) tools/odr_check.py
+
 ## flagship benchmark (BASELINE config #1), 1 worker
 bench: build
 	$(PYTHON) bench.py --steps 50 --warmup 5
@@ -45,7 +49,7 @@ profile-gpu: build
 	  --output-format csv -- $(PYTHON) $(CURDIR)/tools/bench_hash.py --no-files
 
 lint:
-	$(PYTHON) -m compileall -q tritondl tests tools bench.py __graft_entry__.py
+	$(PYTHON) -m compileall -q tritondl tritondl_testkit tests tools bench.py __graft_entry__.py
 
 docker-build:
 	DOCKER_BUILDKIT=1 docker build -t $(IMAGE) -f docker/Dockerfile .

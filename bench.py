@@ -357,7 +357,7 @@ def main() -> int:
         if cuda:
             torch.cuda.synchronize()
 
-    from tritondl.bench_job import JobStack
+    from tritondl_testkit.bench_job import JobStack
     from tritondl.utils.log import log
     log.configure(a.log_level, "")
 

@@ -43,15 +43,15 @@ struct Header {
   uint16_t seq, ack;
 };
 
-void put16(std::string& s, uint16_t v) {
+inline void put16(std::string& s, uint16_t v) {
   s.push_back(static_cast<char>(v >> 8));
   s.push_back(static_cast<char>(v & 0xFF));
 }
-void put32(std::string& s, uint32_t v) {
+inline void put32(std::string& s, uint32_t v) {
   for (int k = 3; k >= 0; --k) s.push_back(static_cast<char>((v >> (8 * k)) & 0xFF));
 }
-uint16_t get16(const uint8_t* p) { return static_cast<uint16_t>((p[0] << 8) | p[1]); }
-uint32_t get32(const uint8_t* p) {
+inline uint16_t get16(const uint8_t* p) { return static_cast<uint16_t>((p[0] << 8) | p[1]); }
+inline uint32_t get32(const uint8_t* p) {
   return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
 }
 

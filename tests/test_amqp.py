@@ -10,7 +10,7 @@ from tritondl.amqp import codec
 from tritondl.amqp.client import Client, _parse_retries
 from tritondl.amqp.codec import Method, Properties
 from tritondl.amqp.connection import ChannelClosed, Connection, ConnectionClosed, PublishNacked, parse_url
-from tritondl.fakes.broker import Broker
+from tritondl_testkit.fakes.broker import Broker
 from tritondl.utils.backoff import ExponentialBackoff
 
 
@@ -397,7 +397,7 @@ def test_fake_broker_heartbeats_both_ways():
     import asyncio as aio
 
     from tritondl.amqp.connection import Connection
-    from tritondl.fakes.broker import Broker
+    from tritondl_testkit.fakes.broker import Broker
 
     async def main():
         b = await Broker(heartbeat=1).start()

@@ -11,7 +11,7 @@ import gc
 import logging
 import warnings
 
-from tritondl.bench_job import JobStack
+from tritondl_testkit.bench_job import JobStack
 
 
 class _Catch(logging.Handler):

@@ -15,8 +15,8 @@ import socket
 
 import pytest
 
-from tritondl.bench_job import JobStack
-from tritondl.fakes import payload
+from tritondl_testkit.bench_job import JobStack
+from tritondl_testkit.fakes import payload
 from tritondl.fetch.http import HTTPDownloader
 from tritondl.utils import rawhttp
 
@@ -173,7 +173,7 @@ def test_variant_key_with_a_slash_in_its_base64_name_is_checked():
     fake S3 still finds the variant, so such a PUT is content-checked."""
     import base64
 
-    from tritondl.fakes.payload import Expectations
+    from tritondl_testkit.fakes.payload import Expectations
     e = Expectations(100_000, 4)
     name = "\xff\xfe-movie-3-v2.mkv"
     enc = base64.b64encode(name.encode()).decode()

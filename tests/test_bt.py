@@ -9,8 +9,8 @@ import shutil
 
 import pytest
 
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.swarm import (DHTNetwork, HTTPTracker, Seeder, UDPTracker, magnet_for, make_payload,
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.swarm import (DHTNetwork, HTTPTracker, Seeder, UDPTracker, magnet_for, make_payload,
                                   torrent_file_bytes, torrent_for)
 from tritondl.fetch.bt import bencode
 from tritondl.fetch.bt.client import TorrentDownloader, TorrentError

@@ -9,8 +9,8 @@ import os
 
 import pytest
 
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.swarm import Seeder, make_payload, torrent_file_bytes
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.swarm import Seeder, make_payload, torrent_file_bytes
 from tritondl.fetch.bt import merkle
 from tritondl.fetch.bt.client import TorrentDownloader
 from tritondl.fetch.bt.metainfo import Metainfo, MetainfoError, make_info, parse_magnet

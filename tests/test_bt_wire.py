@@ -374,7 +374,7 @@ def test_peer_messages_of_any_shape_end_only_that_peer(tmp_path):
     import struct
     from hypothesis import HealthCheck, given, settings
     from hypothesis import strategies as st
-    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import make_payload, torrent_for
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig, _Peer
 
     make_payload(str(tmp_path / "src"), {"a.mkv": 100_000})

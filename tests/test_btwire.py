@@ -189,7 +189,7 @@ def test_download_uses_zero_copy_receive(tmp_path):
     """A plain-TCP leecher switches its peer connections to LinkReader."""
     import asyncio
 
-    from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
     from tritondl.fetch.bt.client import TorrentDownloader
     from tritondl.fetch.bt.torrent import TorrentConfig
 
@@ -265,7 +265,7 @@ def test_malformed_block_from_a_scripted_peer_drops_it(tmp_path):
     and keeps the good block."""
     import asyncio
 
-    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import make_payload, torrent_for
     from tritondl.fetch.bt import peer as pw
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 
@@ -370,7 +370,7 @@ def test_download_completes_against_chaotic_scripted_peers(tmp_path, fast, nativ
     import asyncio
     import random
 
-    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import make_payload, torrent_for
     from tritondl.fetch.bt import peer as pw
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 
@@ -460,7 +460,7 @@ def test_native_serving_backpressure_bounds_the_write_buffer(tmp_path):
     once the peer reads, every request is answered with the right bytes."""
     import asyncio
 
-    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import make_payload, torrent_for
     from tritondl.fetch.bt import peer as pw
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 
@@ -514,7 +514,7 @@ def test_native_serving_backpressure_over_utp(tmp_path):
     flow-controlled the same way (pause_reading on the uTP transport)."""
     import asyncio
 
-    from tritondl.fakes.swarm import make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import make_payload, torrent_for
     from tritondl.fetch.bt import peer as pw
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
     from tritondl.fetch.bt.utp import UtpSocket
@@ -603,7 +603,7 @@ def test_seeding_falls_back_to_python_when_the_native_source_fails(tmp_path, mon
     import asyncio
     import types
 
-    from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+    from tritondl_testkit.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
     from tritondl.fetch.bt import torrent as tmod
     from tritondl.fetch.bt.client import TorrentDownloader
     from tritondl.fetch.bt.torrent import TorrentConfig

@@ -11,9 +11,9 @@ import pytest
 
 from tritondl.amqp.client import Client
 from tritondl.amqp.codec import Properties
-from tritondl.fakes.broker import Broker
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.broker import Broker
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.fetch.http import HTTPDownloader
 from tritondl.fetch.registry import Dispatcher
 from tritondl.models import Convert, Download, Media

@@ -7,8 +7,8 @@ import subprocess
 import sys
 
 from tritondl import check
-from tritondl.fakes.broker import Broker
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.broker import Broker
+from tritondl_testkit.fakes.s3 import FakeS3
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

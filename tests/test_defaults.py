@@ -18,7 +18,7 @@ import socket
 
 import pytest
 
-from tritondl.fakes.origin import Origin
+from tritondl_testkit.fakes.origin import Origin
 from tritondl.fetch.bt.client import TorrentDownloader
 from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 from tritondl.fetch.http import HTTPDownloader

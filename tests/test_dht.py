@@ -15,7 +15,7 @@ import socket
 
 import pytest
 
-from tritondl.fakes.swarm import DHTNetwork, Seeder, make_payload, torrent_for
+from tritondl_testkit.fakes.swarm import DHTNetwork, Seeder, make_payload, torrent_for
 from tritondl.fetch.bt import dht as D
 from tritondl.fetch.bt.client import TorrentDownloader, _parse_hostports
 from tritondl.fetch.bt.torrent import TorrentConfig

@@ -7,7 +7,7 @@ import os
 
 import pytest
 
-from tritondl.fakes.origin import Origin
+from tritondl_testkit.fakes.origin import Origin
 from tritondl.fetch.http import HTTPDownloader, HTTPDownloadError, filename_from_disposition
 from tritondl.fetch.registry import ClientRegister, Dispatcher, ProgressTracker, UnsupportedError
 

@@ -107,7 +107,7 @@ def test_auto_verify_falls_back_to_the_host_when_the_helper_cannot_start(tmp_pat
     """A node whose KFD lists a GPU but whose HIP stack is broken: the first
     'auto' resume finds the helper dead on arrival, verifies on the host, and
     the GPU is not offered again in this process."""
-    from tritondl.fakes.swarm import make_payload
+    from tritondl_testkit.fakes.swarm import make_payload
     from tritondl.fetch.bt.metainfo import make_info
     from tritondl.fetch.bt.storage import FileStorage
 
@@ -148,7 +148,7 @@ def test_helper_stuck_in_a_call_is_killed_and_auto_verify_uses_the_host(tmp_path
     finally:
         h.close()
 
-    from tritondl.fakes.swarm import make_payload
+    from tritondl_testkit.fakes.swarm import make_payload
     from tritondl.fetch.bt.metainfo import make_info
     from tritondl.fetch.bt.storage import FileStorage
     src = tmp_path / "src" / "T"

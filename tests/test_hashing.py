@@ -335,7 +335,7 @@ def test_s3_put_with_gpu_chunk_hashing(tmp_path):
     fake S3 verifies every chunk signature, so a wrong digest fails the PUT."""
     import asyncio
 
-    from tritondl.fakes.s3 import FakeS3
+    from tritondl_testkit.fakes.s3 import FakeS3
     from tritondl.s3.client import S3Client
     from tritondl.s3.credentials import Static
 

@@ -6,7 +6,7 @@ import os
 
 import pytest
 
-from tritondl.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
+from tritondl_testkit.fakes.swarm import Seeder, magnet_for, make_payload, torrent_for
 from tritondl.fetch.bt import mse
 from tritondl.fetch.bt.client import TorrentDownloader
 from tritondl.fetch.bt.torrent import TorrentConfig

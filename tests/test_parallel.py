@@ -7,9 +7,9 @@ import signal
 import time
 
 from tritondl.amqp.codec import Properties
-from tritondl.fakes.broker import Broker
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.broker import Broker
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.models import Download, Media
 from tritondl.parallel import WorkerPool, plan
 from tritondl.s3.uploader import object_key

@@ -15,9 +15,9 @@ import time
 from tritondl.amqp.client import Client
 from tritondl.amqp.codec import Method, Properties
 from tritondl.amqp.connection import ChannelClosed, Connection
-from tritondl.fakes.broker import Broker
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.broker import Broker
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.fetch.http import HTTPDownloader
 from tritondl.fetch.registry import Dispatcher
 from tritondl.models import Convert, Download, Media
@@ -264,7 +264,7 @@ def test_delay_queue_with_foreign_arguments_falls_back_to_parking(tmp_path):
     (406) must not turn a retry into a dead-letter."""
     async def main():
         e = await Env().up(tmp_path, max_retries=3, retry_delay_s=0.2, retry_backoff=1.0)
-        from tritondl.fakes.broker import Queue
+        from tritondl_testkit.fakes.broker import Queue
         e.broker.queues["v1.download-0.retry.200ms"] = Queue("v1.download-0.retry.200ms", True,
                                                              arguments={"x-max-length": 5})
         e.submit(Media(id="bad", source_uri=e.origin.url("/missing.mkv")))

@@ -7,7 +7,7 @@ and the Torrent's listen-port lifecycle."""
 import asyncio
 import socket
 
-from tritondl.fakes.igd import FakeIGD
+from tritondl_testkit.fakes.igd import FakeIGD
 from tritondl.fetch.bt import portfwd
 from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 

@@ -15,9 +15,9 @@ import os
 
 import pytest
 
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.proxy import FakeProxy
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.proxy import FakeProxy
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.fetch.http import HTTPDownloader, HTTPDownloadError
 from tritondl.s3.client import S3Client, S3Error
 from tritondl.s3.credentials import Static
@@ -275,7 +275,7 @@ def test_service_jobs_through_proxy_from_environment(tmp_path, pki, monkeypatch)
     endpoint — every byte through the proxy, which needs credentials."""
     from tritondl.amqp.client import Client
     from tritondl.amqp.codec import Properties
-    from tritondl.fakes.broker import Broker
+    from tritondl_testkit.fakes.broker import Broker
     from tritondl.fetch.registry import Dispatcher
     from tritondl.models import Download, Media
     from tritondl.s3.uploader import Uploader, object_key

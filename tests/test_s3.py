@@ -9,7 +9,7 @@ import os
 
 import pytest
 
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.s3 import sigv4
 from tritondl.s3.client import Endpoint, S3Client, S3Error
 from tritondl.s3.credentials import Static, default_chain

@@ -9,7 +9,7 @@ import time
 
 import pytest
 
-from tritondl.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.s3 import FakeS3
 from tritondl.s3.client import (MAX_OBJECT_SIZE, MAX_PARTS, Endpoint, S3Client, S3Error, _PartQueue,
                                 plan_parts)
 from tritondl.s3.credentials import Static

@@ -12,10 +12,10 @@ import time
 
 from tritondl.amqp.client import Client
 from tritondl.amqp.codec import Properties
-from tritondl.fakes.broker import Broker
-from tritondl.fakes.origin import Origin
-from tritondl.fakes.s3 import FakeS3
-from tritondl.fakes.swarm import HTTPTracker, Seeder, magnet_for, make_payload, torrent_for
+from tritondl_testkit.fakes.broker import Broker
+from tritondl_testkit.fakes.origin import Origin
+from tritondl_testkit.fakes.s3 import FakeS3
+from tritondl_testkit.fakes.swarm import HTTPTracker, Seeder, magnet_for, make_payload, torrent_for
 from tritondl.fetch.bt.client import TorrentDownloader
 from tritondl.fetch.bt.torrent import TorrentConfig
 from tritondl.fetch.http import HTTPDownloader

@@ -7,7 +7,7 @@ asyncio tasks and native pool threads must stay flat (reference job loop:
 
 import asyncio
 
-from tritondl.soak import run_soak
+from tritondl_testkit.soak import run_soak
 from tritondl.utils.log import log
 
 
@@ -51,7 +51,7 @@ def test_drift_reports_point_and_median_window():
     """drift(): the first-vs-last post-warm-up change, and the same from the
     medians of the first and last few samples (one sample taken while a
     big job is in flight cannot fake a trend)."""
-    from tritondl.soak import drift
+    from tritondl_testkit.soak import drift
     rss = [60, 80, 90, 91, 90, 92, 91, 99, 90, 91, 92, 91, 90, 98]
     samples = [{"minute": i, "rss_mb": v, "fds": 30} for i, v in enumerate(rss)]
     d = drift(samples, 2, "minute")

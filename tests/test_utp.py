@@ -9,7 +9,7 @@ import random
 import pytest
 
 from tritondl import _utp
-from tritondl.fakes.swarm import magnet_for, make_payload, torrent_for
+from tritondl_testkit.fakes.swarm import magnet_for, make_payload, torrent_for
 from tritondl.fetch.bt.client import TorrentDownloader
 from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
 from tritondl.fetch.bt.utp import UtpSocket

@@ -29,7 +29,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from tritondl.bench_job import AK, SK, Backend, JobStack  # noqa: E402
+from tritondl_testkit.bench_job import AK, SK, Backend, JobStack  # noqa: E402
 from tritondl.fetch.http import HTTPDownloader  # noqa: E402
 from tritondl.fetch.registry import ProgressSink  # noqa: E402
 from tritondl.ops import hashing  # noqa: E402

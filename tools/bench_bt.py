@@ -71,8 +71,8 @@ async def main() -> int:
         from tritondl.utils.config import Config
         tune_malloc(a.malloc_mmap_threshold, trim_threshold=(a.malloc_trim_threshold if a.malloc_trim_threshold >= 0
                                                              else Config().malloc_trim_threshold))
-    from tritondl.bench_job import Backend
-    from tritondl.fakes.swarm import make_payload
+    from tritondl_testkit.bench_job import Backend
+    from tritondl_testkit.fakes.swarm import make_payload
     from tritondl.fetch.bt.client import TorrentDownloader
     from tritondl.fetch.bt.metainfo import parse_magnet
     from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
@@ -140,8 +140,8 @@ async def job_bench(a) -> int:
     from tritondl.amqp.client import Client
     from tritondl.amqp.codec import Properties
     from tritondl.amqp.connection import Connection
-    from tritondl.bench_job import AK, SK, Backend
-    from tritondl.fakes.swarm import make_payload
+    from tritondl_testkit.bench_job import AK, SK, Backend
+    from tritondl_testkit.fakes.swarm import make_payload
     from tritondl.fetch.bt.client import TorrentDownloader
     from tritondl.fetch.bt.torrent import TorrentConfig
     from tritondl.fetch.registry import Dispatcher

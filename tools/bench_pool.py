@@ -47,7 +47,7 @@ async def main() -> int:
     a.jobs = a.jobs or a.workers * a.jobs_per_worker
     from tritondl.amqp.codec import Properties
     from tritondl.amqp.connection import Connection
-    from tritondl.bench_job import AK, SK, Backend
+    from tritondl_testkit.bench_job import AK, SK, Backend
     from tritondl.models import Convert, Download, Media, SourceType
     from tritondl.parallel import WorkerPool, plan
 

@@ -41,8 +41,8 @@ async def main() -> int:
         os.sched_setaffinity(0, parse_cpulist(a.cpus))
     import numpy as np
 
-    from tritondl.fakes.origin import Origin
-    from tritondl.fakes.swarm import torrent_file_bytes
+    from tritondl_testkit.fakes.origin import Origin
+    from tritondl_testkit.fakes.swarm import torrent_file_bytes
     from tritondl.fetch.bt.client import TorrentDownloader
     from tritondl.fetch.bt.metainfo import make_info
     from tritondl.fetch.bt.torrent import TorrentConfig

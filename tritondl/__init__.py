@@ -20,7 +20,10 @@ Layout (mirrors SURVEY.md §7.1):
                           competing consumers, rank wiring
 * ``tritondl.utils``    – config, logging, backoff, profiler, metrics
 * ``tritondl.service``  – the job orchestrator (C1), ``python -m tritondl``
-* ``tritondl.fakes``    – in-process AMQP broker, S3, HTTP origin, BT swarm
+
+The test harness (fake broker / S3 / origin / swarm, bench and soak
+drivers) lives in the separate ``tritondl_testkit`` package, which is not
+shipped in the wheel or the worker image.
 """
 
 __version__ = "0.1.0"

@@ -3,7 +3,7 @@ job via local RabbitMQ, 10 MB file", used by ``bench.py``, ``smoke()`` and
 the integration tests.
 
 Layout: the fake broker, HTTP origin and S3 each run in their OWN process
-(``tritondl.fakes.serve``) — as the real RabbitMQ / media server / MinIO
+(``tritondl_testkit.fakes.serve``) — as the real RabbitMQ / media server / MinIO
 would — and the worker (``Service``) runs in this process exactly as in
 production (multi-rank: one shared broker, per-rank origin + S3 nodes, see
 :class:`JobStack`): AMQP consume from ``v1.download-{0,1}`` → HTTP
@@ -13,7 +13,7 @@ A producer connection publishes the ``api.Download`` jobs; completion is
 observed as the job's ack, and each ``Convert`` is checked on the way out.
 
 Every job fetches a payload of its own (variant ``i % R`` of the synthetic
-file, ``R`` larger than the spare-file pool, :mod:`tritondl.fakes.payload`)
+file, ``R`` larger than the spare-file pool, :mod:`tritondl_testkit.fakes.payload`)
 and the S3 fake refuses any PUT whose 64 KiB-leaf SHA-256 list is not that
 variant's: a worker that uploads stale or torn bytes fails the run.
 """
@@ -31,21 +31,21 @@ import tempfile
 import time
 from dataclasses import dataclass, field
 
-from .amqp.client import Client
-from .amqp.codec import Properties
-from .amqp.connection import Connection
-from .models import Convert, Download, Media, SourceType
-from .s3.client import S3Client
-from .s3.credentials import Static
-from .s3.uploader import Uploader
-from .service import Service
-from .utils.config import Config
+from tritondl.amqp.client import Client
+from tritondl.amqp.codec import Properties
+from tritondl.amqp.connection import Connection
+from tritondl.models import Convert, Download, Media, SourceType
+from tritondl.s3.client import S3Client
+from tritondl.s3.credentials import Static
+from tritondl.s3.uploader import Uploader
+from tritondl.service import Service
+from tritondl.utils.config import Config
 
 AK, SK = "benchaccess", "benchsecret"
 
 
 class Backend:
-    def __init__(self, kind: str, extra: list[str] | None = None, module: str = "tritondl.fakes.serve") -> None:
+    def __init__(self, kind: str, extra: list[str] | None = None, module: str = "tritondl_testkit.fakes.serve") -> None:
         self.kind = kind
         self.extra = extra or []
         self.module = module
@@ -53,7 +53,7 @@ class Backend:
         self.info: dict = {}
 
     async def start(self) -> "Backend":
-        args = [self.kind] if self.module == "tritondl.fakes.serve" else []
+        args = [self.kind] if self.module == "tritondl_testkit.fakes.serve" else []
         # (TRITONDL_BENCH_FAKE_CPUS, if set, is inherited: the child pins itself first
         # thing, topology.pin_from_env — no preexec_fn in a process that has threads)
         self.proc = await asyncio.create_subprocess_exec(
@@ -157,7 +157,7 @@ class JobStack:
 
     def _tls_files(self) -> tuple[str, str, str]:
         """(ca_file, cert_file, key_file) of a throwaway PKI in the workdir."""
-        from .utils import rawhttp
+        from tritondl.utils import rawhttp
         assert self.workdir is not None
         ca, cert, key = rawhttp.relay_module().make_test_pki(["127.0.0.1", "localhost"])
         paths = []
@@ -277,7 +277,7 @@ class JobStack:
             self.producer_proc = await Backend("producer", [
                 "--broker", broker_url, "--origins", ",".join(self.origin_urls), "--size", str(self.file_size),
                 "--tag", self.tag, "--broker-pid", str(self.broker_pid),
-                "--variants", str(self.resolved_variants())], module="tritondl.bench_producer").start()
+                "--variants", str(self.resolved_variants())], module="tritondl_testkit.bench_producer").start()
             return
         self.producer = await Connection.open(broker_url, heartbeat=0)
         self.pch = await self.producer.channel()
@@ -434,7 +434,7 @@ def run_single_job_smoke(size: int = 1 << 20) -> None:
             assert c.media is not None and c.media.id == "bench-smoke-0"
             from .fakes.payload import variant_bytes, variant_of
             s3 = st.backends[-1]
-            from .s3.uploader import object_key
+            from tritondl.s3.uploader import object_key
             got = s3.object_bytes("triton-staging", object_key(c.media.id, st.job_name(0)))
             want = variant_bytes(size, variant_of(st.job_name(0)))
             assert hashlib.md5(got).digest() == hashlib.md5(want).digest()

@@ -9,7 +9,7 @@ event loop published every job, decoded every ``Convert`` and acked it,
 alongside its own worker.  Rank 0 starts this process and drives it with JSON
 lines:
 
-    python -m tritondl.bench_producer --broker URL --origins U1,U2 --size BYTES [--tag T]
+    python -m tritondl_testkit.bench_producer --broker URL --origins U1,U2 --size BYTES [--tag T]
         stdout  {"ready": true}
         stdin   {"cmd": "run", "n": N}   publish N jobs (pipelined confirms) and
                                          wait until N new converts arrived
@@ -20,7 +20,7 @@ Each ``Convert`` is checked on the way in (the job's media id, exactly once).
 Dead-lettered jobs (``v1.download.dead``) end a run at once with an error
 naming the failed stage (the bench runs with ``max_retries=0``), instead of
 waiting out the timeout.  ``--variants R``: job ``i`` fetches payload
-variant ``i % R`` (:mod:`tritondl.fakes.payload`).
+variant ``i % R`` (:mod:`tritondl_testkit.fakes.payload`).
 ``--broker-pid`` names the broker process whose CPU time the reply reports
 (psutil), so a run can tell when the single-process fake broker, not the
 workers, is the bottleneck.
@@ -35,9 +35,9 @@ import resource
 import sys
 import time
 
-from .amqp.codec import Properties
-from .amqp.connection import Connection
-from .models import Convert, Download, Media, SourceType
+from tritondl.amqp.codec import Properties
+from tritondl.amqp.connection import Connection
+from tritondl.models import Convert, Download, Media, SourceType
 
 
 def _cpu_self() -> float:

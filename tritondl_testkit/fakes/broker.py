@@ -37,8 +37,8 @@ import time
 from dataclasses import dataclass, field
 from typing import Any
 
-from ..amqp import codec
-from ..amqp.codec import Method, Properties
+from tritondl.amqp import codec
+from tritondl.amqp.codec import Method, Properties
 
 
 @dataclass

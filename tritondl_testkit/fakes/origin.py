@@ -19,7 +19,7 @@ import os
 import re
 from dataclasses import dataclass
 
-from ..utils import rawhttp
+from tritondl.utils import rawhttp
 from . import rawserver as web
 
 

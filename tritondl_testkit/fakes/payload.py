@@ -58,7 +58,7 @@ def variant_of(name: str) -> int | None:
 
 def leaf_hashes(data) -> bytes:
     """SHA-256 of each 64 KiB leaf, concatenated (native multi-buffer kernel)."""
-    from ..ops import hashing
+    from tritondl.ops import hashing
     return hashing.piece_hashes(data, LEAF, kind="sha256") if len(data) else b""
 
 

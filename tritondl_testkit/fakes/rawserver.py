@@ -26,7 +26,7 @@ from urllib.parse import unquote
 
 from multidict import CIMultiDict
 
-from ..utils import rawhttp
+from tritondl.utils import rawhttp
 
 _REASONS = {200: "OK", 204: "No Content", 206: "Partial Content", 301: "Moved Permanently", 302: "Found",
             304: "Not Modified", 400: "Bad Request", 403: "Forbidden", 404: "Not Found",

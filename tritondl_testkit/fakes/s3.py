@@ -13,7 +13,7 @@ every chunk signature verified) by ``_relay.recv_verify_chunked`` /
 ``_relay.recv_body`` outside the interpreter, as MinIO would on its own box.
 Fault injection: :meth:`fail_next` returns 5xx for the next N requests,
 :meth:`fail_for` for every request during an outage window.  Content check
-(``expect``, a :class:`~tritondl.fakes.payload.Expectations`): a PUT of a
+(``expect``, a :class:`~tritondl_testkit.fakes.payload.Expectations`): a PUT of a
 synthetic payload variant whose bytes are not the origin's is refused with
 400 ``BadDigest`` — in discard mode too, from the leaf hashes the native
 chunk verifier already computed (``counts["content_ok"]`` /
@@ -40,8 +40,8 @@ import time
 from dataclasses import dataclass, field
 from urllib.parse import parse_qsl, unquote
 
-from ..s3 import sigv4
-from ..utils import rawhttp
+from tritondl.s3 import sigv4
+from tritondl.utils import rawhttp
 from . import rawserver as web
 
 _CHUNK_HDR = re.compile(rb"([0-9a-fA-F]+);chunk-signature=([0-9a-f]{64})\r\n")
@@ -269,7 +269,7 @@ class FakeS3:
         key, seed, amzdate, scope = auth
         decoded_len = int(request.headers.get("x-amz-decoded-content-length", "-1"))
         loop = asyncio.get_running_loop()
-        from ..ops import hashing
+        from tritondl.ops import hashing
         buf = bytearray()
         pos = 0           # parse cursor in buf
         run_start = 0     # start of the current run of whole frames

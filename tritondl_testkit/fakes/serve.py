@@ -1,10 +1,10 @@
 """Run one fake backend in its own process (so benches measure the worker,
 not the fakes competing for its event loop).
 
-    python -m tritondl.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
+    python -m tritondl_testkit.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
                                    [--tls-cert PEM --tls-key PEM]   # origin / s3 over https
                                    [--variants N --variant-size BYTES]  # per-job payloads
-    python -m tritondl.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
+    python -m tritondl_testkit.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
 
 Prints ONE JSON line ``{"kind":..., "endpoint": ..., "url": ...}`` on stdout
 once listening, then serves until stdin closes or SIGTERM.  The origin also
@@ -12,7 +12,7 @@ serves ``/synthetic/<bytes>/<name>``: deterministic pseudo-random content of
 the requested size (generated once per size, cached in memory); a name with
 a variant (``movie-3-v7.mkv``) gets that variant's distinct payload, and an
 S3 started with ``--variants`` refuses PUTs of variants whose content is not
-the origin's (:mod:`tritondl.fakes.payload`).
+the origin's (:mod:`tritondl_testkit.fakes.payload`).
 """
 
 from __future__ import annotations
@@ -74,7 +74,7 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         with open(tls_cert) as f1, open(tls_key) as f2:
             tls = (f1.read(), f2.read())
     if kind == "seed":
-        from ..fetch.bt.torrent import Torrent, TorrentConfig
+        from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
         from .swarm import magnet_for, torrent_for
         assert seed_path, "--path required"
         info = torrent_for(seed_path, piece_kb << 10)

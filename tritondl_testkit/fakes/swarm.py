@@ -12,11 +12,11 @@ import time
 
 from aiohttp import web
 
-from ..fetch.bt import bencode
-from ..fetch.bt.dht import DHTNode
-from ..fetch.bt.metainfo import Info, Magnet, Metainfo, make_info
-from ..fetch.bt.torrent import Torrent, TorrentConfig
-from ..fetch.bt.tracker import compact_peers
+from tritondl.fetch.bt import bencode
+from tritondl.fetch.bt.dht import DHTNode
+from tritondl.fetch.bt.metainfo import Info, Magnet, Metainfo, make_info
+from tritondl.fetch.bt.torrent import Torrent, TorrentConfig
+from tritondl.fetch.bt.tracker import compact_peers
 
 
 class HTTPTracker:

@@ -29,13 +29,13 @@ Every ``sample_every`` finished jobs it records:
 * the native task pool's size;
 * the relay's active pumps.
 
-    python -m tritondl.soak --jobs 5000 --torrent-jobs 100 --fail-every 50 --sample-every 500 \\
+    python -m tritondl_testkit.soak --jobs 5000 --torrent-jobs 100 --fail-every 50 --sample-every 500 \\
         [--file-kb 10240] [--out soak.jsonl]
 
 A job-count soak finishes in seconds, so nothing timer-driven cycles in it.
 The time-based form runs for wall-clock minutes at a paced job rate:
 
-    python -m tritondl.soak --minutes 60 --rate 50 --file-kb 1024 --torrent-every 200 \\
+    python -m tritondl_testkit.soak --minutes 60 --rate 50 --file-kb 1024 --torrent-every 200 \\
         --fail-every 100 --retry-delay 2 --heartbeat 10 --tls --dht-nodes 8 --out soak.jsonl
 
 so the worker's timers go round many times: AMQP heartbeats both ways (the
@@ -64,11 +64,11 @@ import sys
 import threading
 import time
 
-from .amqp.codec import Properties
-from .amqp.connection import Connection
+from tritondl.amqp.codec import Properties
+from tritondl.amqp.connection import Connection
 from .bench_job import Backend, JobStack
-from .models import Download, Media, SourceType
-from .utils import rawhttp
+from tritondl.models import Download, Media, SourceType
+from tritondl.utils import rawhttp
 
 
 def _torrent_impl(svc):
@@ -152,7 +152,7 @@ def drift(samples: list[dict], warmup: int, key: str = "jobs") -> dict:
 async def _local_dht(n: int) -> list:
     """``n`` DHT nodes on 127.0.0.1 that know each other: the worker's node
     bootstraps off them, so its table fills and its maintenance has peers."""
-    from .fetch.bt.dht import DHTNode
+    from tritondl.fetch.bt.dht import DHTNode
     nodes = []
     for _ in range(n):
         boot = [("127.0.0.1", x.port) for x in nodes[-3:]]
@@ -340,12 +340,12 @@ def main() -> int:
                     help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
     if a.cpus:
-        from .parallel import topology
+        from tritondl.parallel import topology
         if a.cpus == "auto":
             doms = topology.l3_domains()
             os.environ["TRITONDL_BENCH_FAKE_CPUS"] = ",".join(map(str, doms[1 % len(doms)]))
         topology.pin(a.cpus)
-    from .utils.log import log
+    from tritondl.utils.log import log
     log.configure("warning", "")
     fh = open(a.out, "w") if a.out else None
 
