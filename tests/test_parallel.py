@@ -328,3 +328,66 @@ def test_pair_domains_properties():
             free -= set(group)
 
     check()
+
+
+def test_pool_healthz_inherits_a_worker_whose_shard_stopped_consuming(tmp_path):
+    """the pool's /healthz polls each worker's own /healthz.
+    A shard queue the workers may not re-declare (quorum, owned by someone
+    else) is deleted: both workers' consumers on it stay down, their
+    /healthz goes 503, and so does the pool's, naming the worker and shard.
+    Re-declared, the shard consumes again and every probe is 200."""
+    async def main():
+        b = await Broker().start()
+        b.declare("v1.download", queue_args={"x-queue-type": "quorum"})
+        s = await FakeS3().start()
+        port = _free_port()
+        while True:                      # workers serve on port+1+rank: keep those free too
+            import socket
+            try:
+                for k in (1, 2):
+                    x = socket.socket()
+                    x.bind(("127.0.0.1", port + k))
+                    x.close()
+                break
+            except OSError:
+                port = _free_port()
+        env = {"RABBITMQ_ENDPOINT": b.endpoint, "RABBITMQ_USERNAME": "guest", "RABBITMQ_PASSWORD": "guest",
+               "S3_ENDPOINT": s.endpoint, "PYTHONPATH": ROOT, "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning",
+               "TRITONDL_PROGRESS_LOG_INTERVAL": "0", "TRITONDL_HEALTH_DOWN": "0.5", "TRITONDL_GPU_VERIFY": "off"}
+        pool = WorkerPool(plan(2, gpus=0, cpus=2), env=env, cwd=str(tmp_path), grace=10,
+                          health_addr=f"127.0.0.1:{port}", worker_health_grace=60)
+        await pool.start()
+        for _ in range(600):
+            if all(len(b.queues[f"v1.download-{i}"].consumers) == 2 for i in range(2)):
+                break
+            await asyncio.sleep(0.05)
+        assert all(len(b.queues[f"v1.download-{i}"].consumers) == 2 for i in range(2))
+        for _ in range(200):             # both workers' endpoints up
+            try:
+                codes = [(await _get(port + 1 + r))[0] for r in (0, 1)]
+                if codes == [200, 200]:
+                    break
+            except OSError:
+                pass
+            await asyncio.sleep(0.1)
+        assert (await _get(port))[0] == 200
+        b.delete_queue("v1.download-1")
+        t0 = time.monotonic()
+        while True:
+            code, body = await _get(port)
+            if code == 503:
+                break
+            assert time.monotonic() - t0 < 10, body
+            await asyncio.sleep(0.1)
+        assert b"no consumer on v1.download-1" in body and b"worker " in body, body
+        code, m = await _get(port, "/metrics")
+        assert b"pool_workers_unhealthy 2" in m
+        b.declare("v1.download", queue_args={"x-queue-type": "quorum"})
+        t0 = time.monotonic()
+        while (await _get(port))[0] != 200:
+            assert time.monotonic() - t0 < 15
+            await asyncio.sleep(0.1)
+        await pool.stop()
+        await s.stop()
+        await b.stop()
+    asyncio.run(asyncio.wait_for(main(), 120))

@@ -274,3 +274,165 @@ def test_delay_queue_with_foreign_arguments_falls_back_to_parking(tmp_path):
         assert e.broker.queue_depth("v1.download-0.retry.200ms") == 0
         await e.down()
     run(main())
+
+
+# ---------------------------------------------------------------- quorum queues + per-consumer QoS
+def test_fake_refuses_global_qos_consumers_on_quorum_and_stream_queues():
+    """RabbitMQ's quorum (and stream) queues do not support global QoS: a
+    basic.consume from a channel with a global prefetch gets 540
+    NOT_IMPLEMENTED, a hard error that closes the connection.  Per-consumer
+    QoS is accepted; a stream also needs it set."""
+    from tritondl.amqp import codec
+    from tritondl.amqp.connection import ConnectionClosed
+
+    async def main():
+        b = await Broker().start()
+        b.declare("v1.download", queue_args={"x-queue-type": "quorum"})
+        b.queues["st"] = __import__("tritondl_testkit.fakes.broker", fromlist=["Queue"]).Queue(
+            "st", True, arguments={"x-queue-type": "stream"})
+        conn = await Connection.open(b.url, heartbeat=0)
+        ch = await conn.channel()
+        await ch.basic_qos(1, 0, True)                 # the reference's getChannel (client.go:366-369)
+        try:
+            await ch.basic_consume("v1.download-0", lambda m: None)
+            raise AssertionError("global QoS consumer accepted on a quorum queue")
+        except (ConnectionClosed, ChannelClosed) as e:
+            assert e.code == codec.NOT_IMPLEMENTED and "global qos" in str(e)
+        assert conn.is_closed and b.stats["refused_global_qos"] == 1
+        conn = await Connection.open(b.url, heartbeat=0)
+        ch = await conn.channel()
+        await ch.basic_qos(1, 0, False)                # per consumer: accepted
+        await ch.basic_consume("v1.download-0", lambda m: None)
+        ch2 = await conn.channel()
+        try:
+            await ch2.basic_consume("st", lambda m: None)
+            raise AssertionError("stream consumer without a prefetch accepted")
+        except ChannelClosed as e:
+            assert e.code == codec.PRECONDITION_FAILED
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_fake_per_consumer_qos_applies_only_to_later_consumers():
+    """basic.qos(global=false) is captured when a consumer starts: a later
+    qos on the channel leaves existing consumers at their old limit."""
+    async def main():
+        b = await Broker().start()
+        b.declare("t")
+        conn = await Connection.open(b.url, heartbeat=0)
+        ch = await conn.channel()
+        got_a, got_b = [], []
+        await ch.basic_qos(1, 0, False)
+        await ch.basic_consume("t-0", got_a.append)
+        await ch.basic_qos(3, 0, False)
+        for k in range(10):
+            b.inject("t", "t-0", b"%d" % k)
+        await asyncio.sleep(0.05)
+        assert len(got_a) == 1                        # still limited to 1
+        await ch.basic_consume("t-0", got_b.append)
+        await asyncio.sleep(0.05)
+        assert len(got_b) == 3                        # the new consumer got the new limit
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_worker_uses_per_consumer_qos():
+    """The worker's shard channels set basic.qos(prefetch, global=false): the
+    fake records a per-consumer limit and no channel limit."""
+    async def main():
+        b = await Broker().start()
+        c = await Client(b.url, prefetch=1, heartbeat=0).connect()
+        await c.consume("v1.download")
+        chans = [ch for conn in b.conns for ch in conn.channels.values() if ch.consumers]
+        assert len(chans) == 2
+        assert all(ch.prefetch_channel == 0 and ch.prefetch_consumer == 1 for ch in chans)
+        assert all(cons.prefetch == 1 for ch in chans for cons in ch.consumers.values())
+        assert all(sh.active for sh in c.shards.values())
+        await c.close()
+        await b.stop()
+    run(main())
+
+
+def test_write_only_user_parking_on_quorum_shard_queues(tmp_path):
+    """Quorum shard queues + a write-only user + an always-failing origin:
+    the failed job is parked in-process (the delay queue is refused) while
+    the same shard keeps delivering — the consumer is re-subscribed, so the
+    parked delivery no longer holds its per-consumer prefetch slot."""
+    async def main():
+        e = await Env().up(tmp_path, user="dl", perms=REF_PERMS,
+                           predeclare={"v1.convert": None, "v1.download": {"x-queue-type": "quorum"}},
+                           max_retries=3, retry_delay_s=1.0, retry_backoff=1.0, retry_delay_max_s=1.0)
+        assert e.amqp.external_queues == {"v1.download-0", "v1.download-1"}
+        e.submit(Media(id="bad", source_uri=e.origin.url("/missing.mkv")))
+        await e.wait_results(1)
+        good = e.origin.add("/ok.mkv", os.urandom(20_000))
+        t0 = time.monotonic()
+        e.submit(Media(id="good", source_uri=good))              # same shard as the parked one
+        await e.wait_results(2)
+        assert e.svc.results[1].ok and time.monotonic() - t0 < 0.8
+        assert e.amqp.parked == 1
+        assert e.amqp.shards["v1.download-0"].rotations >= 1
+        assert e.broker.stats["refused_global_qos"] == 0 and e.broker.stats["requeued"] == 0
+        await e.down()
+    run(main())
+
+
+# ---------------------------------------------------------------- poison jobs (VERDICT r04 #3)
+def test_poison_job_runs_exactly_max_retries_plus_one_times(tmp_path):
+    """Write-only user (delay queue and DLQ refused) and an always-failing
+    origin: the job runs max_retries + 1 times, then every later park cycle
+    only re-tries the dead-letter publish — no download (counted by origin
+    hits), X-Retries stays at max_retries + 1."""
+    async def main():
+        mr = 2
+        e = await Env().up(tmp_path, user="dl", perms=REF_PERMS, predeclare={"v1.convert": None},
+                           max_retries=mr, retry_delay_s=0.1, retry_backoff=1.0, retry_delay_max_s=0.2)
+        path = "/always-fails.mkv"
+        e.origin.fail = 10 ** 9                                   # every request: HTTP 500
+        e.origin.add(path, b"x" * 1000)
+        hits = lambda: sum(1 for r in e.origin.requests if r[1] == path)  # noqa: E731
+        e.submit(Media(id="poison", source_uri=e.origin.url(path)))
+        await e.wait_results(1)
+        per_run = hits()
+        assert per_run >= 1
+        retries_seen = []
+        real = e.svc.handle
+
+        async def handle(msg):
+            retries_seen.append(msg.metadata.retries)
+            return await real(msg)
+        e.svc.handle = handle
+        # runs 2..mr+1, then at least 3 park cycles past the budget
+        await e.wait_results(mr + 1 + 3, timeout=20)
+        assert hits() == per_run * (mr + 1), (hits(), per_run)
+        assert retries_seen[:mr] == list(range(1, mr + 1))
+        assert retries_seen[mr:] == [mr + 1] * (len(retries_seen) - mr)   # never grows past the budget
+        assert e.svc.metrics.get("jobs", status="poison") >= 3
+        assert e.svc.metrics.get("jobs_dead_lettered") == 0
+        e.svc._collect_gauges()
+        assert e.svc.metrics.get("jobs_poison_parked") == 1
+        await asyncio.sleep(0.5)
+        assert hits() == per_run * (mr + 1)
+        assert e.broker.stats["requeued"] == 0
+        await e.down()
+    run(main())
+
+
+def test_poison_job_is_dead_lettered_once_the_dlq_is_reachable(tmp_path):
+    """A delivery already past its budget (X-Retries > max_retries) goes to
+    the dead-letter topic without being run."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=2)
+        path = "/never-fetched.mkv"
+        e.origin.add(path, b"y" * 100)
+        e.submit(Media(id="old", source_uri=e.origin.url(path)), headers={"X-Retries": 3})
+        res = await e.wait_results(1)
+        assert res[0].stage == "poison"
+        assert not [r for r in e.origin.requests if r[1] == path]
+        assert e.svc.metrics.get("jobs_dead_lettered") == 1
+        dead = e.broker.queues.get("v1.download.dead-0") or e.broker.queues.get("v1.download.dead-1")
+        assert dead is not None
+        await e.down()
+    run(main())

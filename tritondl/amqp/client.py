@@ -21,9 +21,21 @@ Fixes vs the reference: one TCP connection with one
 channel per shard consumer + one confirm-mode publisher channel (B6); the
 publish retry is a real capped exponential instead of ``Backoff ^ 2`` with a
 self-deadlocking re-enqueue (B5); the publish exchange is declared before
-first use (B13); all state lives on one event loop (B7); QoS is applied per
-consumer channel with ``global=true`` exactly like ``getChannel``
-(``client.go:366-369``).
+first use (B13); all state lives on one event loop (B7).
+
+QoS is per consumer (``basic.qos(prefetch, global=false)``), not the
+reference's channel-wide ``Qos(prefetch, 0, true)`` (``client.go:366-369``).
+Each shard has its own channel with exactly one consumer on it, so the limit
+is the same number of unacked deliveries; but RabbitMQ refuses a consumer
+on a quorum (or stream) queue from a channel with global QoS (540
+NOT_IMPLEMENTED, which closes the connection), so per-consumer QoS is what
+lets the worker consume shard queues an operator declared as quorum queues.
+
+Every shard's consumer state is tracked (:class:`Shard`): whether it has a
+live consumer and since when, and since when the connection has been lost.
+``/healthz`` reads that (:meth:`Client.health`) — the reference's 1 s
+scheduler re-created a dead processor (``client.go:139-166``); here the
+re-creation is event-driven and the probe sees a shard that stays down.
 
 Topology this worker does not own never blocks it.  The reference declared
 nothing on the publish side (``client.go:224`` publishes straight to the
@@ -44,6 +56,7 @@ from __future__ import annotations
 import asyncio
 import contextlib
 import itertools
+import time
 from dataclasses import dataclass
 from typing import AsyncIterator
 
@@ -170,6 +183,38 @@ class Delivery:
         self.settled = True
 
 
+class Shard:
+    """One shard queue's consumer: its channel and consumer tag, and since when
+    it has (or has not) been consuming."""
+
+    def __init__(self, topic: str, queue: str) -> None:
+        self.topic = topic
+        self.queue = queue
+        self.channel: Channel | None = None
+        self.tag = ""
+        self.on_msg = None
+        self.active = False
+        self.since = time.monotonic()      # when ``active`` last changed
+        self.rotations = 0                 # consumer re-subscriptions made for parked deliveries
+        self.lock = asyncio.Lock()
+
+    def set_active(self, ch: Channel, tag: str, on_msg) -> None:
+        self.channel, self.tag, self.on_msg = ch, tag, on_msg
+        if not self.active:
+            self.active = True
+            self.since = time.monotonic()
+
+    def set_inactive(self) -> None:
+        self.tag = ""
+        if self.active:
+            self.active = False
+            self.since = time.monotonic()
+
+    def down_for(self, now: float | None = None) -> float:
+        """Seconds this shard has had no consumer (0 while it has one)."""
+        return 0.0 if self.active else (now or time.monotonic()) - self.since
+
+
 def _parse_retries(headers: dict | None) -> int:
     """X-Retries must be an int32; anything else → 0 (``delivery.go:32-44``)."""
     if not headers:
@@ -214,8 +259,10 @@ class Client:
         self.external_topics: set[str] = set()
         self.external_queues: set[str] = set()
         self._refused_delay: set[str] = set()
-        self._parked: dict[Channel, int] = {}      # consumer channel -> deliveries parked on it
+        self._parked = 0                           # deliveries waiting in-process (park)
         self.parked_total = 0
+        self.shards: dict[str, Shard] = {}         # shard queue -> its consumer state
+        self.lost_since: float | None = None       # monotonic time the connection was lost (None: up)
         self._consumer_chans: list[Channel] = []
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -252,7 +299,6 @@ class Client:
         self._pub = None
         self._declared_pub.clear()
         self._declared_delay.clear()
-        self._parked.clear()
         self._consumer_chans = []
         self._lost.clear()
         conn.add_close_callback(self._on_conn_lost)
@@ -261,6 +307,10 @@ class Client:
     def _on_conn_lost(self, err: BaseException) -> None:
         self._connected.clear()
         self._lost.set()
+        if self.lost_since is None:
+            self.lost_since = time.monotonic()
+        for sh in self.shards.values():
+            sh.set_inactive()
         if not self._closing:
             log.with_field("error", str(err)).warn("rabbitmq connection lost; reconnecting")
 
@@ -277,13 +327,21 @@ class Client:
                     self._out.put_nowait(None)
                     return
                 self.reconnects += 1
+                ok = True
                 for t in list(self._topics):
                     try:
+                        # a broker that lost its definitions (a fresh node, non-persistent
+                        # storage) gets the topology back before the consumers need it
+                        await self.ensure_exchange(t)
+                        await self.ensure_queues(t)
                         await self._start_consumers(t)
                     except AMQPError as e:
+                        ok = False
                         log.error("failed to restart consumers for %s: %s", t, e)
                         if self.conn is not None:  # force another reconnect round
                             self.conn._abort(ConnectionClosed(0, "consumer restart failed"))
+                if ok and self.connected:
+                    self.lost_since = None
                 log.info("reconnected to rabbitmq (generation %d)", self.generation)
         except asyncio.CancelledError:
             pass
@@ -298,7 +356,9 @@ class Client:
         assert self.conn is not None
         ch = await self.conn.channel()
         if qos:
-            await ch.basic_qos(self.prefetch, 0, True)  # getChannel: Qos(prefetch, 0, global=true)
+            # per-consumer limit (getChannel's Qos(prefetch, 0, true) was channel-wide; with
+            # one consumer per channel the limit is the same, and quorum queues accept it)
+            await ch.basic_qos(self.prefetch, 0, False)
         return ch
 
     async def ensure_exchange(self, topic: str) -> None:
@@ -368,6 +428,9 @@ class Client:
         except AMQPError as e:
             raise ConsumeError(f"{ErrorEnsureConsumerQueues}: {e}") from e
         self._topics.append(topic)
+        for i in range(self.num_shard_queues):
+            q = self.get_rk(topic, i)
+            self.shards.setdefault(q, Shard(topic, q))
         await self._start_consumers(topic)
         return self._iter()
 
@@ -393,6 +456,7 @@ class Client:
                 self._mark_external_queue(q, e)
                 ch = await self._channel(qos=True)
         self._consumer_chans.append(ch)
+        shard = self.shards.setdefault(q, Shard(topic, q))
 
         def on_msg(m: Message) -> None:
             if m.body is None:  # reference skips nil bodies (client.go:262)
@@ -400,12 +464,20 @@ class Client:
             self._out.put_nowait(Delivery(self, m, gen))
 
         def on_cancel(tag: str) -> None:
+            if shard.channel is ch and shard.tag == tag:
+                shard.set_inactive()
             log.with_fields(queue=q, consumer_tag=tag).warn("consumer cancelled by broker; resubscribing")
             self._spawn_bg(self._resubscribe(topic, ch, q, on_msg, gen))
+
+        started = False
 
         def on_close(exc) -> None:
             if ch in self._consumer_chans:
                 self._consumer_chans.remove(ch)
+            if shard.channel is ch:
+                shard.set_inactive()
+            if not started:
+                return          # the basic.consume itself failed: the caller's retry loop owns the shard
             if self._closing or gen != self.generation or getattr(exc, "code", 0) == 200 or \
                     self.conn is None or self.conn.is_closed or isinstance(exc, ConnectionClosed):
                 return
@@ -414,7 +486,15 @@ class Client:
 
         ch.on_cancel = on_cancel
         ch.add_close_callback(on_close)
-        await ch.basic_consume(q, on_msg, no_ack=False)
+        try:
+            tag = await ch.basic_consume(q, on_msg, no_ack=False)
+        except BaseException:
+            if not ch.is_closed:
+                with contextlib.suppress(Exception):
+                    await ch.close()
+            raise
+        started = True
+        shard.set_active(ch, tag, on_msg)
         log.info("worker on queue '%s' started", q)
 
     def _mark_external_queue(self, q: str, e: BaseException) -> None:
@@ -450,7 +530,10 @@ class Client:
                             raise
                         self._mark_external_queue(q, e)
                         return          # the refusal closed ch: its close callback reopens the shard
-                await ch.basic_consume(q, cb, no_ack=False)
+                tag = await ch.basic_consume(q, cb, no_ack=False)
+                shard = self.shards.get(q)
+                if shard is not None:
+                    shard.set_active(ch, tag, cb)
                 log.info("worker on queue '%s' resubscribed", q)
                 return
             except AMQPError as e:
@@ -594,24 +677,58 @@ class Client:
                 log.with_fields(error=str(e), attempt=attempt).warn("delayed publish failed; retrying in %.2fs", d)
                 await asyncio.sleep(d)
 
-    def park(self, d: Delivery, props: Properties, delay: float) -> None:
+    def park(self, d: Delivery, props: Properties, delay: float, on_done=None) -> None:
         """The reference's ``Error()`` (``delivery.go:66-84``) without holding the
         job slot: a task waits ``delay``, re-publishes the body to the delivery's
-        own exchange/routing key with ``props`` (confirmed) and acks.  While it
-        waits, the consumer channel's prefetch is raised by one so the shard
-        keeps delivering.  A crash or shutdown meanwhile leaves the delivery
-        unacked, so the broker redelivers it: nothing is lost."""
-        self.parked_total += 1
-        self._spawn_bg(self._parked_retry(d, props, delay))
+        own exchange/routing key with ``props`` (confirmed) and acks.  A crash
+        or shutdown meanwhile leaves the delivery unacked, so the broker
+        redelivers it: nothing is lost.
 
-    async def _parked_retry(self, d: Delivery, props: Properties, delay: float) -> None:
-        ch = d.msg.channel
-        bumped = False
+        The parked delivery stays unacked, so it would hold its consumer's
+        prefetch slot for the whole wait.  Under per-consumer QoS a new
+        ``basic.qos`` only applies to consumers started after it, so instead
+        of raising the limit the shard's consumer is replaced
+        (:meth:`_rotate`): ``basic.cancel`` + ``basic.consume`` on the same
+        channel.  The parked delivery stays unacked on the channel (acks by
+        delivery tag still work) but no longer counts against the new
+        consumer, so the shard keeps delivering.  With the default prefetch 1
+        the old consumer held only the parked delivery, so the limit stays
+        exact; with prefetch P > 1, deliveries the old consumer still has in
+        flight are not counted against the new one until they settle (at most
+        P - 1 extra, transiently)."""
+        self.parked_total += 1
+        self._spawn_bg(self._parked_retry(d, props, delay, on_done))
+
+    def _shard_of(self, ch: Channel | None) -> Shard | None:
+        for sh in self.shards.values():
+            if sh.channel is ch:
+                return sh
+        return None
+
+    async def _rotate(self, shard: Shard, tag: str) -> bool:
+        """Replace ``shard``'s consumer ``tag`` with a fresh one on the same
+        channel (its per-consumer unacked count starts at 0).  False if the
+        consumer is already gone or replaced."""
+        async with shard.lock:
+            ch = shard.channel
+            if ch is None or ch.is_closed or not shard.active or shard.tag != tag or self._closing:
+                return False
+            cb = shard.on_msg
+            await ch.basic_cancel(tag)
+            new = await ch.basic_consume(shard.queue, cb, no_ack=False)
+            shard.set_active(ch, new, cb)
+            shard.rotations += 1
+            return True
+
+    async def _parked_retry(self, d: Delivery, props: Properties, delay: float, on_done=None) -> None:
+        self._parked += 1
         try:
-            if ch is not None and not ch.is_closed:
-                self._parked[ch] = self._parked.get(ch, 0) + 1
-                bumped = True
-                await ch.basic_qos(self.prefetch + self._parked[ch], 0, True)
+            shard = self._shard_of(d.msg.channel)
+            if shard is not None and d.msg.consumer_tag:
+                try:
+                    await self._rotate(shard, d.msg.consumer_tag)
+                except AMQPError as e:       # the channel died: the broker requeued the delivery
+                    log.with_fields(queue=shard.queue, error=str(e)).warn("consumer re-subscribe failed")
             await asyncio.sleep(delay)
             if d.stale:
                 return                      # its channel died: the broker requeued it already
@@ -626,19 +743,47 @@ class Client:
             with contextlib.suppress(Exception):
                 await d.nack(requeue=True)
         finally:
-            if bumped and ch is not None:
-                n = self._parked.get(ch, 1) - 1
-                if n > 0:
-                    self._parked[ch] = n
-                else:
-                    self._parked.pop(ch, None)
-                if not ch.is_closed and not self._closing:
-                    with contextlib.suppress(Exception):
-                        await ch.basic_qos(self.prefetch + n, 0, True)
+            self._parked -= 1
+            if on_done is not None:
+                on_done()
 
     @property
     def parked(self) -> int:
-        return sum(self._parked.values())
+        """Deliveries currently waiting in-process (:meth:`park`)."""
+        return self._parked
+
+    # ------------------------------------------------------------ health
+    async def ready_count(self, topic: str) -> int:
+        """Ready (undelivered) messages on ``topic``'s shard queues, by passive
+        declare on a scratch channel (no permission needed)."""
+        ch = await self._channel(qos=False)
+        try:
+            n = 0
+            for i in range(self.num_shard_queues):
+                _q, count, _consumers = await ch.queue_declare(self.get_rk(topic, i), passive=True)
+                n += count
+            return n
+        finally:
+            if not ch.is_closed:
+                await ch.close()
+
+    def health(self, max_down_s: float) -> tuple[bool, list[str]]:
+        """(healthy, reasons).  Unhealthy once the connection has been down for
+        more than ``max_down_s`` (the supervisor is still reconnecting), or once
+        any shard of a consumed topic has had no consumer for that long (a
+        consumer stuck in its re-subscribe / reopen retry loop, a queue that
+        was deleted or that this user may no longer read)."""
+        now = time.monotonic()
+        why: list[str] = []
+        if self._closing:
+            why.append("closing")
+        if self.lost_since is not None and now - self.lost_since > max_down_s:
+            why.append(f"broker connection down for {now - self.lost_since:.0f}s")
+        for q, sh in sorted(self.shards.items()):
+            down = sh.down_for(now)
+            if down > max_down_s:
+                why.append(f"no consumer on {q} for {down:.0f}s")
+        return (not why, why)
 
     async def _publish_retry(self, exchange: str, rk: str, body: bytes, props: Properties, max_attempts: int,
                              declare: bool) -> None:

@@ -17,8 +17,13 @@ The supervisor:
   1: every worker given up), it stops the rest and exits non-zero so the
   orchestrator restarts the pod — the reference's ``log.Fatal`` exits
   (``cmd/downloader/downloader.go:64,70,83,92,97``).  ``/healthz`` on
-  ``--health-addr`` answers 503 while any worker is given up, and
-  ``/metrics`` carries live / given-up / restart counts.
+  ``--health-addr`` answers 503 while any worker is given up, or while any
+  running worker's own ``/healthz`` does (a worker whose shard consumer or
+  broker connection has been down too long, or that sits idle on a
+  backlog: :meth:`tritondl.service.Service.health`).  Each worker serves
+  its ``/healthz`` on loopback port ``health port + 1 + rank`` unless
+  ``TRITONDL_METRICS_ADDR`` is set for it.  ``/metrics`` carries live /
+  given-up / unhealthy / restart counts.
 """
 
 from __future__ import annotations
@@ -50,9 +55,12 @@ class WorkerPool:
                  max_restarts: int = 5, restart_window: float = 60.0, grace: float = 30.0,
                  backoff_initial: float = 0.5, backoff_max: float = 30.0, cwd: str | None = None,
                  module: str = "tritondl", worker_env=None, min_workers: int = 1,
-                 health_addr: str = "") -> None:
+                 health_addr: str = "", worker_health_base: int = 0, worker_health_grace: float = 60.0) -> None:
         """``worker_env(rank) -> dict``: extra env for one worker (e.g. its
-        nearest S3 node)."""
+        nearest S3 node).  ``worker_health_base``: worker ``r`` serves its
+        ``/healthz`` on ``127.0.0.1:base+r`` (default: the pool's health port
+        + 1); a worker whose endpoint does not answer within
+        ``worker_health_grace`` s of its start counts as unhealthy."""
         self.workers = [_Worker(s) for s in specs]
         self.argv = argv or []
         self.env = env or {}
@@ -66,6 +74,10 @@ class WorkerPool:
         self.module = module
         self.min_workers = max(0, min(min_workers, len(self.workers)))
         self.health_addr = health_addr
+        if health_addr and not worker_health_base:
+            worker_health_base = int(health_addr.rpartition(":")[2]) + 1
+        self.worker_health_base = worker_health_base
+        self.worker_health_grace = worker_health_grace
         self.metrics = Metrics()
         self._stopping = False
         self._tasks: list[asyncio.Task] = []
@@ -80,11 +92,48 @@ class WorkerPool:
 
     @property
     def healthy(self) -> bool:
+        """The pool's own view (no worker given up); :meth:`health` adds the workers'."""
         return not any(w.given_up for w in self.workers) and not self._stopping
 
     def _gauges(self) -> None:
         self.metrics.set("pool_workers_live", self.live)
         self.metrics.set("pool_workers_given_up", len(self.workers) - self.live)
+
+    def _health_port(self, w: _Worker) -> int:
+        return self.worker_health_base + w.spec.rank if self.worker_health_base else 0
+
+    async def _worker_health(self, w: _Worker) -> str:
+        """'' if worker ``w`` is healthy (or still within its start-up grace,
+        or between restarts), else why not."""
+        port = self._health_port(w)
+        if not port or w.proc is None or w.proc.returncode is not None:
+            return ""
+        young = time.monotonic() - w.started_at < self.worker_health_grace
+        try:
+            r, wr = await asyncio.wait_for(asyncio.open_connection("127.0.0.1", port), 2.0)
+            try:
+                wr.write(b"GET /healthz HTTP/1.0\r\nHost: localhost\r\n\r\n")
+                data = await asyncio.wait_for(r.read(1 << 16), 3.0)
+            finally:
+                wr.close()
+            code = int(data.split(b" ", 2)[1])
+        except (OSError, asyncio.TimeoutError, ValueError, IndexError) as e:
+            return "" if young else f"worker {w.spec.rank}: /healthz unreachable ({e.__class__.__name__})"
+        if code == 200:
+            return ""
+        body = data.split(b"\r\n\r\n", 1)[-1].decode(errors="replace").strip().replace("\n", "; ")
+        return f"worker {w.spec.rank}: {body}"
+
+    async def health(self) -> tuple[bool, list[str]]:
+        """The pool's ``/healthz``: given-up workers, then every running
+        worker's own ``/healthz``."""
+        why = [f"worker {w.spec.rank}: given up (crash-looping)" for w in self.workers if w.given_up]
+        if self._stopping:
+            why.append("stopping")
+        polled = await asyncio.gather(*(self._worker_health(w) for w in self.workers if not w.given_up))
+        bad = [x for x in polled if x]
+        self.metrics.set("pool_workers_unhealthy", len(bad))
+        return not (why or bad), why + bad
 
     async def _spawn(self, w: _Worker) -> None:
         env = dict(os.environ)
@@ -92,6 +141,8 @@ class WorkerPool:
         env.update(w.spec.env())
         if self.worker_env is not None:
             env.update(self.worker_env(w.spec.rank))
+        if self._health_port(w) and "TRITONDL_METRICS_ADDR" not in env:
+            env["TRITONDL_METRICS_ADDR"] = f"127.0.0.1:{self._health_port(w)}"
         if w.spec.cpus and "TRITONDL_CPUS" not in self.env:
             # the worker pins itself first thing (service.main, TRITONDL_CPUS): no
             # preexec_fn in this threaded supervisor
@@ -133,7 +184,7 @@ class WorkerPool:
         self._failed = asyncio.Event()
         self._gauges()
         if self.health_addr:
-            self._health_runner = await serve_metrics(self.metrics, self.health_addr, health=lambda: self.healthy)
+            self._health_runner = await serve_metrics(self.metrics, self.health_addr, health=self.health)
         for w in self.workers:
             self._tasks.append(asyncio.ensure_future(self._watch(w)))
         # wait until every worker has a process

@@ -42,6 +42,19 @@ Differences, all documented fixes:
   no faster (the single event loop does the commit's work either way, now
   under the next job's start: ``profiles/r04_commit_ab/``), so it is off by
   default;
+* a delivery whose ``X-Retries`` is past ``max_retries`` has already run
+  ``max_retries + 1`` times: it goes straight to the dead-letter topic and is
+  never run again (re-parked, without a download, while the dead-letter
+  topic stays unreachable; ``jobs_poison_parked``).  The reference left a
+  failed job unacked (a stall), never re-ran it in a loop
+  (``downloader.go:117-150``);
+* ``/healthz`` reflects consumption, not just the TCP connection: 503 once
+  the broker connection or any shard's consumer has been down for
+  ``health_down_s``, or once the worker has sat with a free job slot while
+  its shard queues held ready messages for ``health_stall_s``
+  (:meth:`Service.health`) — the reference's 1 s scheduler re-created dead
+  processors (``client.go:139-166``), and no probe could see one that stayed
+  dead;
 * in-flight jobs are drained on shutdown (the Go job goroutine was never
   joined); the work dir can optionally be cleaned after success (B15).
 """
@@ -186,6 +199,13 @@ class Service:
         self._finish_waiters: list[tuple[int, asyncio.Future]] = []
         self._id_locks: dict[str, list] = {}       # media id -> [asyncio.Lock, users]
         self._locked_dirs: set[str] = set()        # job dirs _job_lock created for running jobs
+        now = time.monotonic()
+        self._last_finished = now                  # last job result recorded (or start)
+        self._last_taken = now                     # last delivery a job loop took
+        self._poison_parked = 0                    # poison jobs waiting in-process (DLQ unreachable)
+        self._stall_since: float | None = None     # free slot + ready backlog, continuously since
+        self._backlog = (0.0, 0)                   # (monotonic time polled, ready messages on the shards)
+        self.metrics.collectors.append(self._collect_gauges)
 
     @contextlib.asynccontextmanager
     async def _job_lock(self, media_id: str):
@@ -238,12 +258,25 @@ class Service:
         deadline = time.monotonic() + max(0.0, self.cfg.job_lock_wait_s)
         pause = 0.005
         warned = False
+
+        async def again(why: str) -> None:
+            # every retry yields to the loop and honours the deadline and shutdown, whatever
+            # sent it round (a held lock, or a dir renamed away again and again)
+            nonlocal pause
+            if time.monotonic() >= deadline:
+                raise JobBusy(f"job dir {d} {why} for {self.cfg.job_lock_wait_s:.0f}s")
+            if self._stop.is_set():
+                raise JobBusy(f"job dir {d} {why} at shutdown")
+            await asyncio.sleep(pause)
+            pause = min(pause * 2, 0.5)
+
         while True:
             os.makedirs(d, mode=0o755, exist_ok=True)
             try:
                 fd = os.open(d, os.O_RDONLY | os.O_DIRECTORY)
             except FileNotFoundError:
-                continue                            # renamed away between makedirs and open
+                await again("kept being renamed away")  # between makedirs and open
+                continue
             try:
                 fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
             except BlockingIOError:
@@ -251,13 +284,7 @@ class Service:
                 if not warned:
                     warned = True
                     log.with_field("media_id", media_id).warn("job already running in another worker; waiting for it")
-                if time.monotonic() >= deadline:
-                    raise JobBusy(f"job dir {d} held by another worker for {self.cfg.job_lock_wait_s:.0f}s") \
-                        from None
-                if self._stop.is_set():
-                    raise JobBusy(f"job dir {d} held by another worker at shutdown") from None
-                await asyncio.sleep(pause)
-                pause = min(pause * 2, 0.5)
+                await again("held by another worker")
                 continue
             except BaseException:
                 os.close(fd)
@@ -269,6 +296,7 @@ class Service:
             if same:
                 return fd
             os.close(fd)                            # locked a dir that was renamed away: go again
+            await again("kept being renamed away")
 
     async def wait_finished(self, total: int, timeout: float | None = None) -> None:
         """Wait until ``jobs_finished >= total`` (woken by the result itself,
@@ -333,8 +361,7 @@ class Service:
                 log.warn("GPU hasher warm-up still running after %.0fs; consuming anyway",
                          cfg.gpu_warmup_timeout_s)
         if cfg.metrics_addr:
-            self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr,
-                                                       health=lambda: self.amqp is not None and self.amqp.connected)
+            self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr, health=self.health)
         await self.amqp.consume(cfg.consume_topic)
         if cfg.malloc_trim_s > 0:
             self._trimmer = asyncio.ensure_future(self._trim_heap(cfg.malloc_trim_s))
@@ -386,6 +413,7 @@ class Service:
             d = getter.result()
             if d is None:
                 return
+            self._last_taken = time.monotonic()
             self._inflight += 1
             self.metrics.set("jobs_inflight", self._inflight)
             if not self.cfg.pipeline_commit:
@@ -423,6 +451,16 @@ class Service:
         """Process one delivery end-to-end; always settles it."""
         t0 = time.monotonic()
         rawhttp.trace("job_start")
+        if msg.metadata.retries > self.cfg.max_retries:
+            # it has run max_retries + 1 times and the dead-letter publish failed after the last
+            # one (it was parked with X-Retries past the budget): never download it again
+            log.with_fields(retries=msg.metadata.retries, max_retries=self.cfg.max_retries).error(
+                "job is past its retry budget; dead-lettering it without running it")
+            self.metrics.inc("jobs", status="poison")
+            await self._dead_letter(msg, "retries-exhausted",
+                                    RuntimeError(f"X-Retries {msg.metadata.retries} > max_retries "
+                                                 f"{self.cfg.max_retries}"))
+            return self._record(JobResult(False, "poison", "retries exhausted", seconds=time.monotonic() - t0))
         try:
             job = Download.decode(msg.body)
             if job.media is None:
@@ -629,6 +667,7 @@ class Service:
             raise
 
     def _record(self, r: JobResult) -> JobResult:
+        self._last_finished = time.monotonic()
         self.results.append(r)
         if len(self.results) > 10000:
             del self.results[:5000]
@@ -683,8 +722,65 @@ class Service:
                 return                      # its channel is gone: the broker redelivers it anyway
             log.with_fields(error=str(e), delay_s=self.cfg.retry_delay_max_s).error(
                 "failed to dead-letter job; parking it")
-            self.amqp.park(msg, msg.retry_props(), self.cfg.retry_delay_max_s)
+            # X-Retries ends one past the budget, where handle() stops running the job
+            poison = msg.metadata.retries > self.cfg.max_retries
+            self._poison_parked += 1
+            self.amqp.park(msg, msg.retry_props(0 if poison else 1), self.cfg.retry_delay_max_s,
+                           on_done=self._poison_unparked)
             self.metrics.inc("jobs_parked")
+
+    def _poison_unparked(self) -> None:
+        self._poison_parked -= 1
+
+    # ------------------------------------------------------------ health
+    def _collect_gauges(self) -> None:
+        """Gauges computed when ``/metrics`` is scraped."""
+        m = self.metrics
+        now = time.monotonic()
+        m.set("last_job_finished_age_seconds", round(now - self._last_finished, 3))
+        m.set("jobs_poison_parked", self._poison_parked)
+        if self.amqp is not None:
+            m.set("jobs_parked_waiting", self.amqp.parked)
+            lost = self.amqp.lost_since
+            m.set("broker_down_seconds", 0.0 if lost is None else round(now - lost, 3))
+            for q, sh in self.amqp.shards.items():
+                m.set("consumer_active", 1.0 if sh.active else 0.0, queue=q)
+
+    async def health(self) -> tuple[bool, list[str]]:
+        """(healthy, reasons) for ``/healthz``: the broker client's view (connection
+        and per-shard consumers down longer than ``health_down_s``) plus a stall
+        check — a free job slot while the shard queues hold ready messages, with
+        no delivery taken, for ``health_stall_s``."""
+        if self.amqp is None:
+            return False, ["not started"]
+        ok, why = self.amqp.health(self.cfg.health_down_s)
+        stall = await self._stall_reason()
+        if stall:
+            why.append(stall)
+        return not why, why
+
+    async def _stall_reason(self) -> str:
+        limit = self.cfg.health_stall_s
+        now = time.monotonic()
+        if limit <= 0 or self._stop.is_set() or self.amqp is None or not self.amqp.connected or \
+                self._inflight >= max(1, self.cfg.concurrency):
+            self._stall_since = None
+            return ""
+        if now - self._backlog[0] >= 5.0:           # one passive declare per shard, at most every 5 s
+            try:
+                n = await asyncio.wait_for(self.amqp.ready_count(self.cfg.consume_topic), 5.0)
+                self._backlog = (now, n)
+            except Exception:  # noqa: BLE001 - a missing queue is the shard check's business
+                self._backlog = (now, 0)
+        if self._backlog[1] <= 0:
+            self._stall_since = None
+            return ""
+        if self._stall_since is None:
+            self._stall_since = now
+        idle = now - max(self._stall_since, self._last_taken)
+        if idle > limit:
+            return f"{self._backlog[1]} ready messages and a free job slot, no delivery taken for {idle:.0f}s"
+        return ""
 
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")

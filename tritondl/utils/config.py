@@ -58,7 +58,7 @@ ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_time
               "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
-              "MALLOC_TRIM": "malloc_trim_s"}
+              "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -133,6 +133,12 @@ class Config:
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
+    # /healthz answers 503 once the broker connection, or the consumer of any shard queue,
+    # has been down this long (the supervisor / shard re-subscribe loops keep retrying)
+    health_down_s: float = 30.0
+    # ... and once this worker has had a free job slot while its shard queues held ready
+    # messages for this long without taking one (a consumer that gets nothing; 0 = off)
+    health_stall_s: float = 120.0
     cleanup: bool = False                       # B15: off for parity
     # with cleanup: keep up to this many bytes of finished job files as spares that new
     # downloads are renamed into and overwrite, instead of freeing and re-allocating

@@ -7,6 +7,7 @@ needed on the hot path; the exposition snapshot is taken on the loop too.
 from __future__ import annotations
 
 import bisect
+import inspect
 import time
 from dataclasses import dataclass, field
 
@@ -36,6 +37,7 @@ class Metrics:
         self.gauges: dict[tuple[str, tuple], float] = {}
         self.hists: dict[tuple[str, tuple], _Hist] = {}
         self.started = time.time()
+        self.collectors: list = []      # callables run before each render (gauges computed on scrape)
 
     @staticmethod
     def _k(name: str, labels: dict | None) -> tuple[str, tuple]:
@@ -62,6 +64,8 @@ class Metrics:
     def render(self) -> str:
         """Prometheus text exposition (format 0.0.4): one ``# HELP`` / ``# TYPE``
         pair per family, then its samples; label values escaped."""
+        for fn in self.collectors:
+            fn()
         p = self.prefix
         out: list[str] = []
 
@@ -115,6 +119,11 @@ HELP = {
     "jobs_inflight": "jobs being processed by this worker",
     "jobs_retried_total": "failed jobs scheduled for a retry (broker delay queue or parked in-process)",
     "jobs_parked_total": "retries waited in-process because the broker refused the delay queue or DLQ",
+    "jobs_parked_waiting": "deliveries waiting in-process right now (parked)",
+    "jobs_poison_parked": "jobs past max_retries parked because the dead-letter topic is unreachable (never re-run)",
+    "consumer_active": "1 while the shard queue has a live consumer of this worker, else 0",
+    "last_job_finished_age_seconds": "seconds since this worker last recorded a job result (or started)",
+    "broker_down_seconds": "seconds the broker connection has been down (0 while up)",
     "jobs_dead_lettered_total": "jobs published to the dead-letter topic after max_retries",
     "jobs_dropped_total": "jobs nacked without requeue after max_retries (drop_failed)",
     "bytes_uploaded_total": "bytes uploaded to S3 by finished jobs",
@@ -123,6 +132,7 @@ HELP = {
     "malloc_trims_total": "malloc_trim calls that returned memory to the OS",
     "pool_workers_live": "pool: workers not given up on",
     "pool_workers_given_up": "pool: crash-looping workers given up on",
+    "pool_workers_unhealthy": "pool: running workers whose own /healthz answered 503 (or not at all) at the last probe",
     "pool_worker_restarts_total": "pool: worker restarts by rank",
     "uptime_seconds": "seconds since the process's metrics started",
 }
@@ -139,8 +149,13 @@ async def serve_metrics(metrics: Metrics, addr: str, health=None):
         return web.Response(text=metrics.render(), content_type="text/plain")
 
     async def hz(_req):
-        ok = True if health is None else bool(health())
-        return web.Response(status=200 if ok else 503, text="ok" if ok else "unhealthy")
+        """``health()`` may return a bool or (bool, [reasons]), or an awaitable of either."""
+        r = True if health is None else health()
+        if inspect.isawaitable(r):
+            r = await r
+        ok, why = (r[0], list(r[1])) if isinstance(r, tuple) else (bool(r), [])
+        text = "ok" if ok else "unhealthy" + "".join(f"\n{w}" for w in why)
+        return web.Response(status=200 if ok else 503, text=text + "\n")
 
     app.router.add_get("/metrics", m)
     app.router.add_get("/healthz", hz)

@@ -8,7 +8,11 @@ Implements the RabbitMQ semantics the worker depends on:
 * direct / fanout / topic exchanges plus the default exchange; durable /
   argument equivalence checks (406 PRECONDITION_FAILED on mismatch);
 * queues with round-robin consumers, ``basic.qos`` prefetch (RabbitMQ
-  reading: ``global=true`` → per-channel limit, ``false`` → per-consumer);
+  reading: ``global=true`` → per-channel limit, ``false`` → per-consumer,
+  captured when the consumer starts: a later ``basic.qos`` only applies to
+  consumers started after it).  Quorum and stream queues refuse a consumer
+  on a channel with global QoS, as RabbitMQ does (540 NOT_IMPLEMENTED, a
+  connection error); a stream also needs a per-consumer prefetch (406);
 * manual ack/nack/reject (+``multiple``), requeue with ``redelivered``;
   unacked messages requeued when a channel or connection closes;
 * dead-lettering via ``x-dead-letter-exchange`` / ``-routing-key`` on
@@ -243,6 +247,7 @@ class Broker:
         self._ctag = itertools.count(1)
         self._qname = itertools.count(1)
         self.blocked = False
+        self.delivery_paused = False
         self.fail_publishes = 0
         self.confirm_delay = 0.0           # fault injection: publisher confirms arrive this much later
         self.events: list[tuple[str, str]] = []   # ("publish", exchange) / ("ack", queue), in order
@@ -311,6 +316,27 @@ class Broker:
             if c.open:
                 c.send_method(0, Method("connection.blocked", {"reason": "low on memory"}) if blocked
                               else Method("connection.unblocked"))
+
+    def delete_queue(self, name: str) -> int:
+        """Delete a queue from outside any connection (an operator's
+        ``rabbitmqctl delete_queue``): its consumers get ``basic.cancel``."""
+        q = self.queues.pop(name, None)
+        if q is None:
+            return 0
+        for cons in list(q.consumers):
+            cons.ch.conn.send_method(cons.ch.id, Method("basic.cancel", {"consumer_tag": cons.tag}))
+            self._remove_consumer(cons)
+        for ex in self.exchanges.values():
+            ex.bindings = [b for b in ex.bindings if b[0] != name]
+        return len(q.messages)
+
+    def pause_delivery(self, paused: bool) -> None:
+        """Fault injection: consumers stay registered but get nothing (a stuck
+        queue process); resuming dispatches what queued up meanwhile."""
+        self.delivery_paused = paused
+        if not paused:
+            for q in list(self.queues.values()):
+                self._dispatch(q)
 
     def fail_next_publishes(self, n: int) -> None:
         """Fault injection: nack the next ``n`` confirmed publishes."""
@@ -623,6 +649,16 @@ class Broker:
         elif n == "basic.consume":
             self._check(c, "read", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
+            qtype = q.arguments.get("x-queue-type")
+            if qtype in ("quorum", "stream") and ch.prefetch_channel > 0:
+                # rabbit_channel: {error, global_qos_not_supported_for_queue_type} ->
+                # protocol_error(not_implemented, ...); 540 is a hard (connection) error
+                self.stats["refused_global_qos"] += 1
+                raise ConnError(codec.NOT_IMPLEMENTED,
+                                f"NOT_IMPLEMENTED - queue '{q.name}' in vhost '/' does not support global qos", m.ids)
+            if qtype == "stream" and not ch.prefetch_consumer:
+                raise ChannelError(codec.PRECONDITION_FAILED,
+                                   f"PRECONDITION_FAILED - consumer prefetch count is not set for '{q.name}'", m.ids)
             if a["exclusive"] and q.consumers:
                 raise ChannelError(codec.ACCESS_REFUSED, "ACCESS_REFUSED - queue in use", m.ids)
             tag = a["consumer_tag"] or f"amq.ctag-{next(self._ctag)}"
@@ -835,6 +871,8 @@ class Broker:
             self._schedule_expiry(qname, max(0.0, q.messages[0].expires_at - now))
 
     def _dispatch(self, q: Queue) -> None:
+        if self.delivery_paused:
+            return
         if q.messages and q.messages[0].expires_at is not None and q.messages[0].expires_at <= time.monotonic():
             self._expire_head(q.name)
         while q.messages and q.consumers:
