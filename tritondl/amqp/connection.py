@@ -22,6 +22,7 @@ from dataclasses import dataclass
 from typing import Any, Callable
 from urllib.parse import unquote, urlparse
 
+from ..utils import dial
 from . import codec
 from .codec import AMQPError, Method, Properties
 
@@ -158,19 +159,24 @@ class Connection:
         self.unblocked = asyncio.Event()
         self.unblocked.set()
         self._handshake_q: asyncio.Queue | None = None
+        self.connect_timeout = 10.0
 
     # ---------------------------------------------------------------- open
     @classmethod
     async def open(cls, url: str, *, heartbeat: int = 30, connect_timeout: float = 10.0,
                    frame_max: int = codec.DEFAULT_FRAME_MAX, client_properties: dict | None = None) -> "Connection":
         c = cls(parse_url(url), heartbeat=heartbeat, frame_max=frame_max, client_properties=client_properties)
+        c.connect_timeout = connect_timeout
         await asyncio.wait_for(c._connect(), connect_timeout)
         return c
 
     async def _connect(self) -> None:
         p = self.params
         sslctx = ssl.create_default_context() if p.tls else None
-        self._reader, self._writer = await asyncio.open_connection(p.host, p.port, ssl=sslctx)
+        # fast fallback across the broker's addresses (amqp.Dial used Go's net.Dialer,
+        # client.go:308-309: 300 ms before the next family joins)
+        self._reader, self._writer = await dial.open_connection(p.host, p.port, ssl=sslctx,
+                                                                timeout=self.connect_timeout)
         loop = asyncio.get_running_loop()
         self._closed = loop.create_future()
         self._handshake_q = asyncio.Queue()

@@ -37,6 +37,7 @@ import time
 from dataclasses import dataclass, field
 
 from ...ops import hashing
+from ...utils import dial as tcpdial
 from ...utils.disk import check_space
 from ...utils.log import log
 from . import bep40, merkle, mse
@@ -800,7 +801,9 @@ class Torrent:
 
     # ------------------------------------------------------------ connections
     async def _dial_tcp(self, addr: tuple[str, int]):
-        return await asyncio.wait_for(asyncio.open_connection(*addr), self.cfg.connect_timeout)
+        # fast fallback for a peer given by name (BEP 3 dictionary peer lists; anacrolix
+        # dials through Go's net.Dialer); an IP literal is one address, dialled directly
+        return await tcpdial.open_connection(addr[0], addr[1], timeout=self.cfg.connect_timeout)
 
     async def _dial_utp(self, addr: tuple[str, int]):
         assert self.utp is not None

@@ -43,6 +43,7 @@ from ..ops import hashing
 from ..utils.backoff import ExponentialBackoff
 from ..utils import proxy as _proxy
 from ..utils import rawhttp
+from ..utils.dial import FALLBACK_DELAY
 from ..utils.log import log
 from . import sigv4
 from .credentials import Chain, Provider, Value, default_chain
@@ -233,7 +234,8 @@ class S3Client:
             ssl_ctx = self._ssl()
             self._session = aiohttp.ClientSession(
                 timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=300),
-                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx if ssl_ctx is not None else True),
+                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx if ssl_ctx is not None else True,
+                                             happy_eyeballs_delay=FALLBACK_DELAY),
                 auto_decompress=False)
             self._own_session = True
         return self._session

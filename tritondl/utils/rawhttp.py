@@ -27,6 +27,7 @@ from dataclasses import dataclass, field
 
 from multidict import CIMultiDict
 
+from . import dial
 from .log import log
 
 _relay = None
@@ -375,28 +376,18 @@ class Pool:
 
 
 async def _dial(host: str, port: int, timeout: float) -> socket.socket:
-    """A connected non-blocking TCP socket (first address that answers)."""
+    """A connected non-blocking TCP socket: addresses raced with RFC 8305
+    fast fallback (300 ms stagger, Go's net.Dialer default; utils/dial.py),
+    ``timeout`` bounding the whole dial."""
     loop = asyncio.get_running_loop()
     try:
         infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
     except OSError as e:
         raise RawHTTPError(f"connect {host}:{port}: {e}") from e
-    err: Exception | None = None
-    for fam, typ, proto, _cn, addr in infos:
-        s = socket.socket(fam, typ, proto)
-        s.setblocking(False)
-        try:
-            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            await asyncio.wait_for(loop.sock_connect(s, addr), timeout)
-        except (OSError, asyncio.TimeoutError) as e:
-            s.close()
-            err = e
-            continue
-        except BaseException:
-            s.close()
-            raise
-        return s
-    raise RawHTTPError(f"connect {host}:{port}: {err}")
+    try:
+        return await dial.connect_any(infos, timeout)
+    except (OSError, asyncio.TimeoutError) as e:
+        raise RawHTTPError(f"connect {host}:{port}: {e or type(e).__name__}") from e
 
 
 def _hostport(host: str, port: int) -> str:
