@@ -940,6 +940,7 @@ class GpuHasher {
       Fill f = fills.front();
       fills.pop_front();
       f.latch->wait();
+      progress_.fetch_add(f.len, std::memory_order_relaxed);  // read into pinned staging
       Stage& st = stage_[f.slot];
       trace_begin(copy_stream_, "h2d", f.len);
       HIP_CHECK(hipMemcpyAsync(w.d + f.dst, st.h, f.len, hipMemcpyHostToDevice, copy_stream_));
@@ -977,6 +978,7 @@ class GpuHasher {
               trace_begin(copy_stream_, "h2d_direct", len);
               ds->enqueue(w.d + count * piece_len, off, len, copy_stream_, w.regs);
               trace_end(copy_stream_);
+              progress_.fetch_add(len, std::memory_order_relaxed);
               count += got.second;
               continue;
             }
@@ -1133,6 +1135,7 @@ class GpuHasher {
             std::memcpy(&digests[s * dl], d, 16 * 20);
             for (size_t j = 0; j < 16; ++j) complete[s + j] = lane_ok[j];
             cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
+            progress_.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
             continue;
           }
           // whole pieces, as many at a time as the buffer holds
@@ -1156,6 +1159,7 @@ class GpuHasher {
             }
           }
           cpu_bytes.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
+          progress_.fetch_add(static_cast<unsigned long long>(ge - ga), std::memory_order_relaxed);
         }
       } catch (...) {
         std::lock_guard<std::mutex> g(mu);
@@ -1217,6 +1221,10 @@ class GpuHasher {
 
   size_t last_gpu_pieces() const { return last_gpu_pieces_; }
   size_t last_direct_bytes() const { return last_direct_bytes_; }
+  // Bytes read so far (into staging, mapped for direct DMA, or hashed by the
+  // host threads), over the hasher's lifetime: a monotonic counter another
+  // thread may read while a call runs (the GPU helper's progress heartbeat).
+  unsigned long long progress() const { return progress_.load(std::memory_order_relaxed); }
   bool trace() const { return trace_; }
   void set_trace(bool on) { trace_ = on; }
   std::vector<std::tuple<std::string, float, float, size_t>> last_timeline() const { return timeline_; }
@@ -1231,6 +1239,7 @@ class GpuHasher {
   size_t max_hbm_;
   size_t last_window_ = 0;
   std::mutex call_mu_;
+  std::atomic<unsigned long long> progress_{0};
   std::chrono::steady_clock::time_point last_use_ = std::chrono::steady_clock::now();
   hipStream_t copy_stream_ = nullptr, compute_stream_ = nullptr;
   Stage stage_[kStages];
@@ -1420,5 +1429,6 @@ PYBIND11_MODULE(_gpu_hash, m) {
       .def_property_readonly("max_hbm", &GpuHasher::max_hbm)
       .def("window_bytes_for", &GpuHasher::window_bytes_for)
       .def_property_readonly("last_window_bytes", &GpuHasher::last_window_bytes)
+      .def("progress", &GpuHasher::progress, "bytes read so far (lifetime counter; safe during a call)")
       .def_property_readonly("batch_bytes", &GpuHasher::batch_bytes);
 }

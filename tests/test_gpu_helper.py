@@ -119,11 +119,17 @@ def test_auto_verify_falls_back_to_the_host_when_the_helper_cannot_start(tmp_pat
     monkeypatch.setattr(hashing, "choose_device", lambda *a, **k: "gpu")
     monkeypatch.setattr(hashing, "_helper", gpu_helper.GpuHelper(start_timeout=60))
     monkeypatch.setattr(hashing, "_gpu_disabled", None)
+    monkeypatch.setattr(hashing, "_gpu_failures", 0)
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")       # what the helper sees: no device
     st = FileStorage(str(tmp_path / "src"), info)
     have = st.verify_existing("auto")
     assert have == set(range(info.num_pieces))
+    # a helper that cannot start sets the GPU aside at once ...
     assert hashing._gpu_disabled and not hashing.gpu_available()
+    # ... for the cool-down only: then it is offered again
+    monkeypatch.setattr(hashing, "_gpu_disabled_until", 0.0)
+    assert hashing.gpu_available()
+    assert hashing._gpu_disabled is None
 
 
 def test_helper_stuck_in_a_call_is_killed_and_auto_verify_uses_the_host(tmp_path, monkeypatch):
@@ -139,7 +145,7 @@ def test_helper_stuck_in_a_call_is_killed_and_auto_verify_uses_the_host(tmp_path
         assert h.ping()                                  # pings are answered at once
         pid = h.pid
         t0 = time.monotonic()
-        with pytest.raises(gpu_helper.HelperError, match="did not answer"):
+        with pytest.raises(gpu_helper.HelperError, match="no progress"):
             h.verify_files(files, 16384, exp)
         assert time.monotonic() - t0 < 10
         assert h.pid is None
@@ -159,9 +165,63 @@ def test_helper_stuck_in_a_call_is_killed_and_auto_verify_uses_the_host(tmp_path
     monkeypatch.setattr(hashing, "choose_device", lambda *a, **k: "gpu")
     monkeypatch.setattr(hashing, "_helper", gpu_helper.GpuHelper(call_timeout=0.5))
     monkeypatch.setattr(hashing, "_gpu_disabled", None)
+    monkeypatch.setattr(hashing, "_gpu_failures", 0)
     try:
+        # one stuck call costs that batch the GPU, not the worker: still offered
         have = FileStorage(str(tmp_path / "src"), info).verify_existing("auto")
         assert have == set(range(info.num_pieces))
-        assert hashing._gpu_disabled and "did not answer" in hashing._gpu_disabled
+        assert hashing._gpu_disabled is None and hashing._gpu_failures == 1 and hashing.gpu_available()
+        # repeated faults set it aside (for the cool-down)
+        for _ in range(gpu_helper_max := hashing.GPU_MAX_FAILURES - 1):
+            FileStorage(str(tmp_path / "src"), info).verify_existing("auto")
+        assert gpu_helper_max >= 1
+        assert hashing._gpu_disabled and "no progress" in hashing._gpu_disabled
+        assert not hashing.gpu_available()
     finally:
         hashing._helper.close()
+
+
+def test_slow_but_progressing_call_is_not_killed(tmp_path, monkeypatch):
+    """a call that keeps reading (a cold HDD or NFS resume) runs
+    past the no-progress limit: every heartbeat whose byte count grew
+    extends it.  A successful call also resets the failure count."""
+    monkeypatch.setenv("TRITONDL_GPU_HELPER_FAKE", "1")
+    monkeypatch.setenv("TRITONDL_GPU_HELPER_FAKE_SLOW", "2.0")
+    monkeypatch.setenv("TRITONDL_GPU_PROGRESS_S", "0.1")
+    monkeypatch.setattr(hashing, "_gpu_failures", 2)
+    h = gpu_helper.GpuHelper(call_timeout=0.6)
+    files, _data, exp = _layout(tmp_path, [50_000], 16384)
+    try:
+        t0 = time.monotonic()
+        assert h.verify_files(files, 16384, exp) == b"\x01" * 4
+        assert time.monotonic() - t0 >= 2.0          # far past the 0.6 s no-progress limit
+        assert h.spawned == 1
+        assert hashing._gpu_failures == 0
+    finally:
+        h.close()
+
+
+def test_reap_does_not_block_on_an_unkillable_helper(monkeypatch):
+    """after SIGKILL the wait is bounded; a child stuck in the
+    kernel (D state) is left to a daemon thread instead of blocking the call
+    lock forever."""
+    import subprocess
+
+    class Stuck:
+        stdin = None
+        killed = 0
+
+        def poll(self):
+            return None
+
+        def kill(self):
+            self.killed += 1
+
+        def wait(self, timeout=None):
+            if timeout is None:
+                return -9
+            raise subprocess.TimeoutExpired("helper", timeout)
+    p = Stuck()
+    t0 = time.monotonic()
+    assert gpu_helper.GpuHelper._reap(p, kill=True) is None
+    assert time.monotonic() - t0 < 1 and p.killed >= 2

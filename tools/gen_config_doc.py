@@ -38,7 +38,12 @@ DIRECT = {
                             "the helper exits (and an in-process hasher frees HBM + pinned stages) after this long idle"),
     "TRITONDL_GPU_MAX_HBM": ("8 GiB", "ops/hashing.py, hip/gpu_hash.hip", "cap on the hasher's two HBM windows"),
     "TRITONDL_GPU_CALL_TIMEOUT": ("120", "ops/gpu_helper.py",
-                                  "seconds (+1 per 256 MB) before a silent helper is killed; `auto` then hashes on the host"),
+                                  "seconds a helper call may go without progress (bytes read) before the helper is "
+                                  "killed; `auto` then hashes that batch on the host"),
+    "TRITONDL_GPU_COOLDOWN_S": ("600", "ops/hashing.py",
+                                "after 3 consecutive failed GPU calls (or a helper that cannot start) `auto` "
+                                "hashes on the host for this long, then offers the GPU again"),
+    "TRITONDL_GPU_PROGRESS_S": ("1", "ops/gpu_helper.py", "interval of the helper's progress heartbeat during a call"),
     "TRITONDL_GPU_DEVICE": ("LOCAL_RANK or 0", "ops/hashing.py", "the worker's GPU"),
     "TRITONDL_GPU_DIRECT": ("1", "ops/hashing.py, hip/gpu_hash.hip",
                             "0: stage piece data through pinned host buffers instead of DMA from the page cache"),
@@ -96,6 +101,7 @@ HARNESS = {
     "TRITONDL_FAKE_PROFILE": "cProfile dump of a fake endpoint process",
     "TRITONDL_GPU_HELPER_FAKE": "tests: a host stand-in for the GPU helper's hasher",
     "TRITONDL_GPU_HELPER_FAKE_STALL": "tests: seconds the stand-in helper stalls per call",
+    "TRITONDL_GPU_HELPER_FAKE_SLOW": "tests: seconds the stand-in helper takes per call while reporting progress",
     "TRITONDL_GPU_HELPER_CHILD": "internal: set in the helper process itself",
 }
 

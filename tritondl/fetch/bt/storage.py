@@ -178,8 +178,10 @@ class FileStorage:
         except hashing.HelperError as e:
             if device != "auto":
                 raise                      # the GPU was demanded: fail loudly
-            # the GPU helper could not run: this and every later "auto" batch hashes on the host
-            hashing.disable_gpu(str(e))
+            # the GPU helper could not run this batch: it hashes on the host; repeated
+            # failures (or a helper that cannot start) set the GPU aside for a cool-down
+            from ...ops.gpu_helper import HelperStartError
+            hashing.note_gpu_failure(str(e), fatal=isinstance(e, HelperStartError))
             dev, ok = self._verify_batch("cpu")
         have = {i for i, v in enumerate(ok) if v}
         if self.db is not None:

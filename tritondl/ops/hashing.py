@@ -167,21 +167,65 @@ def _gpu_ext_present() -> bool:
 
 
 _gpu_disabled: str | None = None
+_gpu_disabled_until = 0.0          # monotonic time the GPU is offered again
+_gpu_failures = 0                  # consecutive failed GPU calls
+GPU_MAX_FAILURES = 3               # consecutive failures before the GPU is set aside
+GPU_COOLDOWN_S_DEFAULT = 600.0     # TRITONDL_GPU_COOLDOWN_S
 
 
-def disable_gpu(reason: str) -> None:
-    """Stop offering the GPU to ``device="auto"`` callers in this process (the
-    helper could not start, or stopped answering: a broken HIP stack must not
-    fail every resume)."""
-    global _gpu_disabled
+def disable_gpu(reason: str, cooldown: float | None = None) -> None:
+    """Stop offering the GPU to ``device="auto"`` callers in this process for
+    ``cooldown`` seconds (default ``TRITONDL_GPU_COOLDOWN_S``, 600): a broken
+    HIP stack must not fail every resume, and a transient fault (a driver
+    reset, one slow call) must not cost the worker its GPU for good."""
+    global _gpu_disabled, _gpu_disabled_until
+    import time
+    if cooldown is None:
+        cooldown = float(os.environ.get("TRITONDL_GPU_COOLDOWN_S", "") or GPU_COOLDOWN_S_DEFAULT)
     if _gpu_disabled is None:
         from ..utils.log import log
-        log.with_field("reason", reason).warn("GPU verification disabled; hashing on the host")
+        log.with_fields(reason=reason, retry_in_s=cooldown).warn("GPU verification set aside; hashing on the host")
     _gpu_disabled = reason
+    _gpu_disabled_until = time.monotonic() + cooldown
+
+
+def note_gpu_failure(reason: str, *, fatal: bool = False) -> bool:
+    """A GPU call failed (the helper died, made no progress, or could not
+    start).  The GPU is set aside after :data:`GPU_MAX_FAILURES` consecutive
+    failures, or at once when ``fatal`` (the helper cannot start).  True if
+    it was set aside."""
+    global _gpu_failures
+    _gpu_failures += 1
+    if fatal or _gpu_failures >= GPU_MAX_FAILURES:
+        disable_gpu(reason)
+        return True
+    from ..utils.log import log
+    log.with_fields(reason=reason, failures=_gpu_failures).warn("GPU call failed; this batch hashes on the host")
+    return False
+
+
+def note_gpu_success() -> None:
+    global _gpu_failures
+    _gpu_failures = 0
+
+
+def _gpu_set_aside() -> bool:
+    """True while the GPU is set aside; clears it once the cool-down is over."""
+    global _gpu_disabled, _gpu_failures
+    if _gpu_disabled is None:
+        return False
+    import time
+    if time.monotonic() < _gpu_disabled_until:
+        return True
+    from ..utils.log import log
+    log.with_field("after", _gpu_disabled).info("offering the GPU for verification again")
+    _gpu_disabled = None
+    _gpu_failures = 0
+    return False
 
 
 def gpu_available() -> bool:
-    if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off" or _gpu_disabled is not None:
+    if os.environ.get("TRITONDL_GPU_VERIFY", "").lower() == "off" or _gpu_set_aside():
         return False
     if helper_mode():
         return _gpu_ext_present() and _kfd_gpus() > 0
