@@ -83,12 +83,14 @@ PYBIND11_MODULE(_btwire, m) {
       .def("received", &PieceStore::received)
       .def("blocks", &PieceStore::blocks)
       .def("piece_size", &PieceStore::piece_size)
-      .def("put", [](PieceStore& s, uint32_t i, uint32_t off, const py::bytes& b) {
+      .def("put", [](PieceStore& s, uint32_t i, uint32_t off, const py::bytes& b, uint32_t who) {
         char* p = nullptr;
         Py_ssize_t n = 0;
         PyBytes_AsStringAndSize(b.ptr(), &p, &n);
-        return s.put(i, off, reinterpret_cast<const uint8_t*>(p), size_t(n));
-      })
+        return s.put(i, off, reinterpret_cast<const uint8_t*>(p), size_t(n), who);
+      }, py::arg("i"), py::arg("off"), py::arg("data"), py::arg("who") = 0)
+      .def("block_sources", &PieceStore::block_sources,
+           "per block of buffered piece i: id of the link that supplied it (0 = missing); call before take()")
       .def("take", &PieceStore::take)
       .def_property_readonly("pooled", &PieceStore::pooled)
       .def("reset", &PieceStore::reset)
@@ -117,8 +119,9 @@ PYBIND11_MODULE(_btwire, m) {
              return py::bytes(out);
            });
   py::class_<Link>(m, "Link")
-      .def(py::init<std::shared_ptr<PieceStore>, int, bool>(), py::arg("store"), py::arg("pipeline") = 128,
-           py::arg("fast") = false)
+      .def(py::init<std::shared_ptr<PieceStore>, int, bool, uint32_t>(), py::arg("store"), py::arg("pipeline") = 128,
+           py::arg("fast") = false, py::arg("id") = 0)
+      .def_property_readonly("id", &Link::id)
       .def("feed", &feed_bytes,
            "Parse bytes read from the peer; returns (events, bytes to send).  events: ('piece', i) when a "
            "block from this link completed piece i; ('msg', id, payload) for every non-data message; "

@@ -100,6 +100,7 @@ class Piece {
 struct PieceBuf {
   std::vector<uint8_t> data;
   std::vector<uint8_t> got;
+  std::vector<uint32_t> from;  // per block: id of the link that supplied it (blame on a hash failure)
   uint32_t nblocks = 0, ngot = 0;
   uint64_t nbytes = 0;
 };
@@ -127,6 +128,7 @@ class PieceStore {
     b.data = pool_->get(piece_size(i));
     b.nblocks = blocks(i);
     b.got.assign(b.nblocks, 0);
+    b.from.assign(b.nblocks, 0);
     return true;
   }
   bool active(uint32_t i) const { return pieces_.count(i) != 0; }
@@ -138,9 +140,9 @@ class PieceStore {
     auto it = pieces_.find(i);
     return it == pieces_.end() ? 0 : it->second.ngot;
   }
-  // Copy one block in.  Returns 1 if it completed the piece, 0 if stored /
-  // duplicate / not wanted, -1 on bad geometry.
-  int put(uint32_t i, uint32_t off, const uint8_t* p, size_t n) {
+  // Copy one block in, supplied by link `who`.  Returns 1 if it completed the
+  // piece, 0 if stored / duplicate / not wanted, -1 on bad geometry.
+  int put(uint32_t i, uint32_t off, const uint8_t* p, size_t n, uint32_t who = 0) {
     auto it = pieces_.find(i);
     if (it == pieces_.end()) return 0;
     PieceBuf& b = it->second;
@@ -152,9 +154,21 @@ class PieceStore {
     if (b.got[bi]) return 0;
     std::memcpy(b.data.data() + off, p, n);
     b.got[bi] = 1;
+    b.from[bi] = who;
     b.nbytes += n;
     bytes_ += n;
     return ++b.ngot == b.nblocks ? 1 : 0;
+  }
+  // Per block of a buffered piece: the id of the link that supplied it (0 =
+  // not received).  Call before take(): blame / smart ban on a hash failure.
+  std::vector<uint32_t> block_sources(uint32_t i) const {
+    auto it = pieces_.find(i);
+    if (it == pieces_.end()) return {};
+    const PieceBuf& b = it->second;
+    std::vector<uint32_t> v(b.nblocks, 0);
+    for (uint32_t k = 0; k < b.nblocks; ++k)
+      if (b.got[k]) v[k] = b.from[k];
+    return v;
   }
   std::unique_ptr<Piece> take(uint32_t i) {
     auto it = pieces_.find(i);
@@ -276,8 +290,10 @@ class Source {
 
 class Link {
  public:
-  Link(std::shared_ptr<PieceStore> store, int pipeline, bool fast)
-      : store_(std::move(store)), pipeline_(std::max(1, pipeline)), refill_(std::max(1, pipeline_ / 4)), fast_(fast) {}
+  Link(std::shared_ptr<PieceStore> store, int pipeline, bool fast, uint32_t id = 0)
+      : store_(std::move(store)), pipeline_(std::max(1, pipeline)), refill_(std::max(1, pipeline_ / 4)), fast_(fast),
+        id_(id) {}
+  uint32_t id() const { return id_; }
 
   // Parse `n` more bytes of the stream.  Appends to *ev: kPieceDone when a
   // block from this link completed a piece; kMsg (id, payload) for every
@@ -367,7 +383,7 @@ class Link {
           wasted_ += pn - 8;
           continue;
         }
-        const int r = store_->put(i, off, pl + 8, pn - 8);
+        const int r = store_->put(i, off, pl + 8, pn - 8, id_);
         if (r < 0) {
           ev->push_back(Event::bad("bad block geometry"));
           bad = true;
@@ -561,6 +577,7 @@ class Link {
   }
 
   std::shared_ptr<PieceStore> store_;
+  uint32_t id_ = 0;  // stamped on every block this link stores (PieceStore::contributors)
   std::shared_ptr<Source> source_;
   bool serving_ = true;
   bool stalled_ = false;

@@ -713,3 +713,107 @@ def test_completion_db_batches_marks_and_flushes_on_read_and_close(tmp_path):
     assert {r[0] for r in other.execute("SELECT idx FROM piece_completion WHERE complete=1")} == \
         set(range(9)) - {3} | {20, 21}
     other.close()
+
+
+# ----------------------------------------------------------------- bad-piece blame
+def test_bad_piece_blame_rules():
+    """anacrolix's pieceHashed(correct=false): every contributor is charged;
+    a sole contributor is banned on its first failure; with several, the
+    unique least-trusted (net good - bad pieces) is banned.  A tie bans
+    nobody: the piece is re-fetched from one contributor only, and once it
+    verifies, a peer whose earlier block differs from the verified data is
+    banned (smart ban)."""
+    from tritondl.fetch.bt.torrent import BLOCK, Torrent
+
+    async def main():
+        t = Torrent(b"\x01" * 20, "/nonexistent", TorrentConfig(listen_host="127.0.0.1"))
+        H, C = ("10.0.0.1", 1), ("10.0.0.2", 2)
+        good = os.urandom(4 * BLOCK)
+        bad = bytearray(good)
+        bad[2 * BLOCK + 5] ^= 0xFF                        # C's block 2 is corrupt
+        t._bad_piece(0, [H, H, C, H], bad)                # shared, both untried: a tie
+        assert not t.banned and t.trust[H] == [0, 1] and t.trust[C] == [0, 1]
+        assert t._isolate[0] == H                         # re-fetched from the one that sent most of it
+        t._good_piece(0, [H, H, H, H], good)              # it verifies: C's block 2 differed
+        assert t.banned == {C} and 0 not in t._isolate and 0 not in t._failed_blocks
+        assert t.trust[H] == [1, 1]
+        t2 = Torrent(b"\x02" * 20, "/nonexistent", TorrentConfig(listen_host="127.0.0.1"))
+        t2._bad_piece(0, [C, C], bad)                     # a sole contributor: banned at once
+        assert t2.banned == {C}
+        t2._bad_piece(1, [None, None], bad)               # a web seed's piece: nobody to blame
+        assert t2.banned == {C}
+        t3 = Torrent(b"\x03" * 20, "/nonexistent", TorrentConfig(listen_host="127.0.0.1"))
+        t3._good_piece(5, [H], good)
+        t3._bad_piece(1, [C, H, C, H], bad)               # H has a good piece: C is least trusted
+        assert t3.banned == {C}
+    run(main())
+
+
+def test_native_store_records_which_link_supplied_each_block():
+    from tritondl import _btwire as W
+    B = W.BLOCK
+    store = W.PieceStore(1, 3 * B, 3 * B)
+    a, b = W.Link(store, 8, False, 7), W.Link(store, 8, False, 9)
+    assert (a.id, b.id) == (7, 9)
+    for link in (a, b):
+        link.assign(0)
+        link.peer_choking = False
+        link.pump()
+    import struct
+
+    def piece_msg(i, off, data):
+        return struct.pack(">IBII", 9 + len(data), 7, i, off) + data
+    a.feed(piece_msg(0, 0, b"x" * B))
+    assert list(store.block_sources(0)) == [7, 0, 0]
+    b.feed(piece_msg(0, B, b"y" * B))
+    ev, _ = a.feed(piece_msg(0, 2 * B, b"z" * B))
+    assert list(ev) == [("piece", 0)]
+    assert list(store.block_sources(0)) == [7, 9, 7]
+    store.take(0)
+    assert list(store.block_sources(0)) == []
+
+
+@pytest.mark.parametrize("native", [True, False], ids=["native-wire", "python-wire"])
+def test_corrupter_sharing_pieces_with_an_honest_peer_is_banned_never_the_honest_one(tmp_path, native):
+    """One honest and one corrupting seeder (every block it serves is
+    flipped); blocks of the same piece come from both (the Python picker
+    fills open pieces from every peer; native links share pieces in end
+    game).  Over several swarms the corrupter is always banned, the honest
+    peer never is, and the download completes from the honest peer's data."""
+    from tritondl.fetch.bt.torrent import Torrent
+
+    async def one(k: int, piece_len: int, pieces: int) -> tuple[int, int]:
+        src = tmp_path / f"src{k}"
+        make_payload(str(src), {"a.mkv": pieces * piece_len}, seed=k)
+        info = torrent_for(str(src / "a.mkv"), piece_len)
+        bad = await Seeder(info, str(src), corrupt=True).start()
+        good = await Seeder(info, str(src)).start()
+        cfg = TorrentConfig(listen_host="127.0.0.1", verify_device="cpu", request_timeout=3, utp=False,
+                            pipeline=4, native_wire=native)
+        t = Torrent(info.infohash, str(tmp_path / f"dst{k}"), cfg, info=info, peers=[bad.addr, good.addr])
+        await t.start()
+        await t.download_all()
+        await asyncio.wait_for(t.complete.wait(), 60)
+        assert (tmp_path / f"dst{k}" / "a.mkv").read_bytes() == (src / "a.mkv").read_bytes()
+        for _ in range(100):
+            if bad.addr in t.banned:
+                break
+            await asyncio.sleep(0.02)
+        assert good.addr not in t.banned, t.trust
+        banned = bad.addr in t.banned or bad.addr not in t.trust   # (never delivered: nothing to judge)
+        shared = t.trust.get(good.addr, [0, 0])[1]             # failed pieces the honest peer shared in
+        await t.close()
+        await bad.stop()
+        await good.stop()
+        return int(banned), shared
+
+    async def main():
+        # 16-block pieces: the Python picker spreads each piece over both peers; a few
+        # 2-piece swarms put the native links into end game on shared pieces
+        res = [await one(k, 16 * 16384, 6) for k in range(3)]
+        res += [await one(10 + k, 8 * 16384, 2) for k in range(3)]
+        assert all(b for b, _s in res), res
+        return res
+    res = run(main(), timeout=240)
+    print("(banned, shared failures) per swarm:", res)
+    assert any(s for _b, s in res), res                        # pieces really were shared

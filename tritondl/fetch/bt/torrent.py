@@ -29,6 +29,7 @@ import errno
 import functools
 import hashlib
 import heapq
+import itertools
 import os
 import random
 import socket
@@ -79,7 +80,6 @@ class TorrentConfig:
     verify_device: str = "auto"
     tracker_min_interval: float = 30.0
     dht_interval: float = 60.0
-    max_bad_pieces: int = 3
     utp: bool = False
     pex: bool = True                 # BEP 11 peer exchange (off for private torrents regardless)
     pex_interval: float = 60.0
@@ -93,6 +93,11 @@ class TorrentConfig:
     native_wire: bool = True         # per-block work in csrc/btwire (False: the pure-Python path)
 
 
+def _block_digest(piece, b: int) -> bytes:
+    """Short digest of block ``b`` of a piece buffer (smart-ban evidence)."""
+    return hashlib.sha1(piece[b * BLOCK:(b + 1) * BLOCK]).digest()[:12]
+
+
 @dataclass
 class _Piece:
     size: int
@@ -102,6 +107,7 @@ class _Piece:
     requested: dict = field(default_factory=dict)          # block idx -> set(peer keys)
     next_b: int = 0                                        # blocks < next_b were handed out once
     redo: list = field(default_factory=list)               # handed-out blocks whose requests all lapsed
+    src: dict = field(default_factory=dict)                # block idx -> key of the peer that supplied it
 
     def take(self) -> int | None:
         """Next never-requested (or lapsed) block; O(1) amortised instead of a
@@ -143,7 +149,9 @@ class _Peer:
         self.outstanding: dict[tuple[int, int], float] = {}
         self.listen_addr: tuple[str, int] | None = None   # where others can dial it (PEX)
         self.pex_sent: set[tuple[str, int]] = set()
-        self.bad = 0
+        self.bad = 0                                        # failed pieces it supplied blocks of
+        self.good = 0                                       # verified pieces it supplied blocks of
+        self.lid = 0                                        # its native link's id (PieceStore blame)
         self.wants = 0                                      # pieces it has that we lack
         self.downloaded = 0
         self.meta_requested = False
@@ -220,6 +228,16 @@ class Torrent:
         self.known: set[tuple[str, int]] = set()
         self.connecting: set[tuple[str, int]] = set()
         self.banned: set[tuple[str, int]] = set()
+        # (good, bad) pieces each peer address supplied blocks of: anacrolix's
+        # netGoodPiecesDirtied, outliving a connection so a reconnect keeps its record
+        self.trust: dict[tuple[str, int], list[int]] = {}
+        self._lid_key: dict[int, tuple[str, int]] = {}  # native link id -> peer key
+        self._lids = itertools.count(1)
+        # failed pieces: (block, peer key, block digest) of what each peer sent, checked
+        # against the data once the piece verifies (smart ban); and the one peer a piece
+        # whose blame was a tie is re-fetched from
+        self._failed_blocks: dict[int, list[tuple[int, tuple, bytes]]] = {}
+        self._isolate: dict[int, tuple[str, int]] = {}
         self.got_info = asyncio.Event()
         self.complete = asyncio.Event()
         self._downloading = False
@@ -425,7 +443,9 @@ class Torrent:
         Torrent assigns it."""
         if self.store is None or p.link is not None or p.wire.closed:
             return
-        p.link = _W.Link(self.store, self.cfg.pipeline, p.hs.fast)
+        p.lid = next(self._lids)
+        self._lid_key[p.lid] = p.key
+        p.link = _W.Link(self.store, self.cfg.pipeline, p.hs.fast, p.lid)
         p.link.peer_choking = p.peer_choking
         if self.source is not None:
             p.link.set_source(self.source)
@@ -453,7 +473,8 @@ class Torrent:
         assert self.store is not None
         have, store, assigned = self.have, self.store, self.assigned
         for i in store.active_pieces():
-            if p.have[i] and not have[i] and not assigned.get(i) and i not in self.verifying:
+            if p.have[i] and not have[i] and not assigned.get(i) and i not in self.verifying and \
+                    not self._isolated_from(i, p):
                 return i
         order = self._rarest_order()
         pos = self._rare_pos
@@ -463,11 +484,12 @@ class Torrent:
         for k in range(pos, len(order)):
             i = order[k]
             if p.have[i] and not have[i] and not store.active(i) and i not in self.verifying \
-                    and i not in self.ws_busy:
+                    and i not in self.ws_busy and not self._isolated_from(i, p):
                 return i
         for i in store.active_pieces():
             owners = assigned.get(i, ())
-            if p.have[i] and not have[i] and p.key not in owners and len(owners) < 3 and i not in self.verifying:
+            if p.have[i] and not have[i] and p.key not in owners and len(owners) < 3 and i not in self.verifying \
+                    and not self._isolated_from(i, p):
                 return i
         return None
 
@@ -488,6 +510,8 @@ class Torrent:
         """A link completed piece i: take its bytes, stop the other links
         fetching it (end-game CANCELs), verify + write off-loop."""
         assert self.store is not None
+        # who supplied which block (end game: several links), for blame on a hash failure
+        keys = [self._lid_key.get(lid) if lid else None for lid in self.store.block_sources(i)]
         data = memoryview(self.store.take(i))     # pooled buffer, no copy
         for key in self.assigned.pop(i, set()):
             q = self.peers.get(key)
@@ -505,7 +529,7 @@ class Torrent:
             # group: 16 for the host's 16-lane AVX-512 SHA-1 (flushed after
             # VERIFY_WAIT_S if fewer arrive), else pairs in SHA-NI lockstep
             # (a lone piece goes at the end of this loop iteration)
-            self._vq.append((i, data, src))
+            self._vq.append((i, data, keys))
             if len(self._vq) >= VERIFY_GROUP:
                 self._submit_verify()
             elif not self._vflush:
@@ -516,7 +540,7 @@ class Torrent:
                 else:
                     loop.call_soon(self._submit_verify)
             return
-        t = asyncio.get_running_loop().create_task(self._finish_native(i, data, src))
+        t = asyncio.get_running_loop().create_task(self._finish_native(i, data, keys))
         self._finishers.add(t)
         t.add_done_callback(self._finishers.discard)
 
@@ -553,19 +577,22 @@ class Torrent:
         finally:
             for i, _d, _s in batch:
                 self.verifying.discard(i)
-        for (i, _d, s), good in zip(batch, ok):
+        for (i, d, keys), good in zip(batch, ok):
             if good:
                 self._record_piece(i)
+                self._good_piece(i, keys, d)
             else:
-                self._bad_piece(i, s)
+                self._bad_piece(i, keys, d)
 
-    async def _finish_native(self, i: int, data: memoryview, src: _Peer) -> None:
+    async def _finish_native(self, i: int, data: memoryview, keys: list) -> None:
         try:
             ok = await self.commit_piece(i, data)
         finally:
             self.verifying.discard(i)
         if ok is False:
-            self._bad_piece(i, src)
+            self._bad_piece(i, keys, data)
+        elif ok:
+            self._good_piece(i, keys, data)
 
     def _fatal(self, e: BaseException) -> None:
         """A storage error (disk full, I/O error): record it and wake whoever
@@ -575,18 +602,87 @@ class Torrent:
             log.with_field("error", str(e)).error("torrent storage failed")
         self.failed.set()
 
-    def _bad_piece(self, i: int, src: _Peer) -> None:
-        """Piece i from src failed its hash: count it against src (ban at the
-        limit) and let the links fetch it again."""
-        src.bad += 1
-        log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
-        if src.bad >= self.cfg.max_bad_pieces:
-            self.banned.add(src.addr)
-            src.wire.close()
+    def _trust_of(self, key) -> list[int]:
+        t = self.trust.get(key)
+        if t is None:
+            t = self.trust[key] = [0, 0]
+        return t
+
+    def _net(self, key) -> int:
+        g, b = self.trust.get(key, (0, 0))
+        return g - b
+
+    def _good_piece(self, i: int, blocks, data=None) -> None:
+        """Every peer that supplied blocks of a verified piece earns trust.  If
+        the piece failed before, each block a peer sent then is compared with
+        the verified data: a peer whose block differs sent corrupt data and is
+        banned (smart ban: evidence, not a guess)."""
+        self._isolate.pop(i, None)
+        for k in dict.fromkeys(k for k in blocks if k is not None):
+            self._trust_of(k)[0] += 1
+            q = self.peers.get(k)
+            if q is not None:
+                q.good += 1
+        sent = self._failed_blocks.pop(i, None)
+        if sent and data is not None:
+            mv = memoryview(data)
+            for b, k, dg in sent:
+                if k not in self.banned and _block_digest(mv, b) != dg:
+                    log.with_fields(piece=i, block=b, peer=f"{k[0]}:{k[1]}").warn(
+                        "peer sent a block that differs from the verified piece")
+                    self._ban(k)
+
+    def _bad_piece(self, i: int, blocks, data=None) -> None:
+        """Piece i failed its hash (anacrolix ``pieceHashed`` with
+        ``correct=false``, the default client of ``torrent.go:40-48``):
+        ``blocks`` holds, per block, the key of the peer that supplied it.
+        Every contributor is charged a bad piece, and the least trusted of
+        them — fewest net good pieces — is banned at once; a piece one peer
+        supplied alone bans that peer on its first failure.  When the least
+        trusted are tied there is no evidence yet: nobody is banned, the
+        blocks each peer sent are remembered (checked once the piece verifies,
+        see :meth:`_good_piece`), and the piece is re-fetched from one of them
+        only, so the next attempt either verifies (and convicts whoever sent
+        a differing block) or fails with a single contributor.  An honest peer
+        is therefore never banned, and a corrupter sharing every piece with it
+        cannot stall the download."""
+        keys = list(dict.fromkeys(k for k in blocks if k is not None))
+        for k in keys:
+            self._trust_of(k)[1] += 1
+            q = self.peers.get(k)
+            if q is not None:
+                q.bad += 1
+        log.with_fields(piece=i, peers=",".join(f"{k[0]}:{k[1]}" for k in keys)).warn("piece failed hash check")
+        self._isolate.pop(i, None)
+        victim = None
+        if len(keys) == 1:
+            victim = keys[0]
+        elif keys:
+            ranked = sorted(keys, key=self._net)
+            if self._net(ranked[0]) < self._net(ranked[1]):
+                victim = ranked[0]
+        if len(keys) > 1 and data is not None:
+            mv = memoryview(data)
+            sent = self._failed_blocks.setdefault(i, [])
+            for b, k in enumerate(blocks):
+                if k is not None and len(sent) < 4096:
+                    sent.append((b, k, _block_digest(mv, b)))
+        if victim is not None:
+            self._ban(victim)
+        elif len(keys) > 1:
+            # a tie: fetch it again from one contributor only — the most trusted, then
+            # the one that supplied most of it
+            pick = max(keys, key=lambda k: (self._net(k), sum(1 for x in blocks if x == k)))
+            self._isolate[i] = pick
         self._rare_dirty = True
         for q in list(self.peers.values()):
             if q.link is not None:
                 self._fill(q)
+
+    def _isolated_from(self, i: int, p: _Peer) -> bool:
+        """Piece i is being re-fetched from another single peer (still connected)."""
+        k = self._isolate.get(i)
+        return k is not None and k != p.key and k in self.peers
 
     async def _native_loop(self, p: _Peer) -> None:
         data = await p.wire.read_raw()
@@ -1115,7 +1211,7 @@ class Torrent:
         exhausted = []
         try:
             for i, pc in self.open_pieces.items():
-                if not p.have[i]:
+                if not p.have[i] or self._isolated_from(i, p):
                     continue
                 b = pc.take()
                 if b is not None:
@@ -1137,7 +1233,7 @@ class Torrent:
         for k in range(pos, len(order)):
             i = order[k]
             if p.have[i] and not self.have[i] and i not in self.pieces and i not in self.verifying \
-                    and i not in self.ws_busy:
+                    and i not in self.ws_busy and not self._isolated_from(i, p):
                 best = i
                 break
         if best is not None:
@@ -1150,7 +1246,7 @@ class Torrent:
             return best, 0, min(BLOCK, size)
         # 3) end game: duplicate outstanding requests of other peers
         for i, pc in self.pieces.items():
-            if not p.have[i]:
+            if not p.have[i] or self._isolated_from(i, p):
                 continue
             for b, who in pc.requested.items():
                 if b not in pc.received and p.key not in who and len(who) < 3:
@@ -1201,6 +1297,7 @@ class Torrent:
         if b not in pc.received:
             pc.buf[off:off + len(data)] = data
             pc.received.add(b)
+            pc.src[b] = p.key
             p.downloaded += len(data)
             self.downloaded += len(data)
             # cancel duplicates (end game)
@@ -1224,15 +1321,25 @@ class Torrent:
         self._fill(p)
 
     async def _finish_piece(self, i: int, pc: _Piece, src: _Peer) -> None:
+        blocks = [pc.src.get(b, src.key) for b in range(pc.nblocks)]
         ok = await self.commit_piece(i, pc.buf)   # the buffer is no longer shared: the piece left self.pieces
         if ok is None:
             return                                # unverifiable yet (v2 layer missing): not the peer's fault
-        if not ok:
-            src.bad += 1
-            log.with_fields(piece=i, peer=f"{src.addr[0]}:{src.addr[1]}").warn("piece failed hash check")
-            if src.bad >= self.cfg.max_bad_pieces:
-                self.banned.add(src.addr)
-                src.wire.close()
+        if ok:
+            self._good_piece(i, blocks, pc.buf)
+        else:
+            self._bad_piece(i, blocks, pc.buf)
+            for q in list(self.peers.values()):
+                if q.link is None and not q.wire.closed:
+                    self._fill(q)
+
+    def _ban(self, key) -> None:
+        """No more connections to (or from) this peer address; drop it now."""
+        self.banned.add(key)
+        q = self.peers.get(key)
+        log.with_fields(peer=f"{key[0]}:{key[1]}", trust=self._net(key)).warn("banning peer for bad pieces")
+        if q is not None:
+            q.wire.close()
 
     async def commit_piece(self, i: int, data) -> bool | None:
         """Verify a whole piece off-loop, write it and record completion; then
