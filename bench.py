@@ -269,12 +269,14 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--file-mb", type=float, default=10.0)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
+    ap.add_argument("--prefetch", type=int, default=0, help="AMQP prefetch per shard consumer (0: = concurrency)")
     ap.add_argument("--no-gpu-probe", action="store_true")
     ap.add_argument("--probe-kb", type=int, default=-1,
                     help="HTTP GET probe size in KiB, the rest as parallel Range streams "
                          "(-1: worker default, 0: open-ended probe)")
     ap.add_argument("--http-segments", type=int, default=0, help="max parallel Range streams (0: worker default)")
     ap.add_argument("--s3-part-mb", type=int, default=0, help="S3 multipart part size (0: worker default)")
+    ap.add_argument("--s3-parallel-parts", type=int, default=0, help="S3 parts in flight per file (0: worker default)")
     ap.add_argument("--s3-multipart-mb", type=int, default=0,
                     help="objects at least this big go multipart (0: worker default, 64 MiB like minio-go)")
     ap.add_argument("--stripe-kb", type=int, default=-1,
@@ -316,12 +318,23 @@ def main() -> int:
                     help="skip the secondary run in the reference's cleanup-off mode after the timed region")
     ap.add_argument("--no-content-check", action="store_true",
                     help="S3 does not compare PUT content with the origin's payload")
+    ap.add_argument("--rtt-ms", type=float, default=0.0,
+                    help="emulated network round trip of the fake broker / origin / S3 (ms): every new "
+                         "connection, TLS handshake, request/response and broker frame waits one RTT "
+                         "(a latency model; loopback bandwidth).  0 = loopback, the headline")
+    ap.add_argument("--stream-mbps", type=float, default=0.0,
+                    help="cap each origin response / S3 PUT stream of the fakes at this many Mbit/s (one TCP "
+                         "stream's window / RTT on a real path); 0 = uncapped, the headline")
     ap.add_argument("--fake-cpus", default="auto",
                     help="pin the fake broker/origin/S3/producer processes (remote endpoints in "
                          "production) elsewhere: a cpulist, auto = the L3 domain after the last rank's, "
                          "'same' = the rank's own set")
     a = ap.parse_args()
     lease = _lease_state()
+    if a.rtt_ms > 0:
+        os.environ["TRITONDL_FAKE_RTT_MS"] = str(a.rtt_ms)   # the fake processes inherit it
+    if a.stream_mbps > 0:
+        os.environ["TRITONDL_FAKE_STREAM_MBPS"] = str(a.stream_mbps)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,7 +375,8 @@ def main() -> int:
     log.configure(a.log_level, "")
 
     file_size = int(a.file_mb * 1024 * 1024)
-    stack = JobStack(file_size=file_size, concurrency=a.concurrency, prefetch=max(1, a.concurrency),
+    prefetch = a.prefetch if a.prefetch > 0 else max(1, a.concurrency)
+    stack = JobStack(file_size=file_size, concurrency=a.concurrency, prefetch=prefetch,
                      tag=f"r{rank}", http_probe_bytes=(a.probe_kb << 10) if a.probe_kb >= 0 else -1,
                      http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
                      http_stripe_bytes=(a.stripe_kb << 10) if a.stripe_kb >= 0 else -1,
@@ -370,7 +384,8 @@ def main() -> int:
                      payload_mode=a.payload, hash_device=a.s3_hash_device, cleanup=a.cleanup == "on",
                      recycle_bytes=(a.recycle_mb << 20) if a.recycle_mb >= 0 else -1, variants=a.variants,
                      content_check=not a.no_content_check,
-                     overrides={"pipeline_commit": a.pipeline_commit == "on"})
+                     overrides={"pipeline_commit": a.pipeline_commit == "on",
+                                **({"s3_parallel_parts": a.s3_parallel_parts} if a.s3_parallel_parts > 0 else {})})
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 
@@ -404,7 +419,8 @@ def main() -> int:
         c = stack.cfg
         knobs = ({"http_probe_bytes": c.http_probe_bytes, "http_segments": c.http_segments,
                   "http_stripe_bytes": c.http_stripe_bytes, "s3_sign_threads": c.s3_sign_threads,
-                  "s3_part_size": c.s3_part_size, "s3_multipart_threshold": c.s3_multipart_threshold}
+                  "s3_part_size": c.s3_part_size, "s3_multipart_threshold": c.s3_multipart_threshold,
+                  "s3_parallel_parts": c.s3_parallel_parts}
                  if c is not None else {})
         # probes that touch a lot of memory or import modules run BEFORE the
         # warm-up: between warm-up and the timed region they evicted the
@@ -563,8 +579,9 @@ def main() -> int:
                        "cpus": (f"{len(pinned)} pinned ({pinned[0]}..{pinned[-1]})" if pinned else "unpinned"),
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
                        "cpus_busy_before": os.environ.get("TRITONDL_BENCH_DOMAIN_BUSY", ""),
-                       "concurrency_per_worker": a.concurrency, "prefetch": max(1, a.concurrency),
+                       "concurrency_per_worker": a.concurrency, "prefetch": prefetch,
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
+                       "rtt_ms": a.rtt_ms, "stream_mbps": a.stream_mbps or None,
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
                        "malloc_policy": stack.svc.malloc_policy if stack.svc is not None else {},

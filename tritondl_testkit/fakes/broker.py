@@ -166,6 +166,7 @@ class _ServerConn:
         self.hb_task: asyncio.Task | None = None
         self._wbuf: list[bytes] = []
         self._flush_scheduled = False
+        self._delayed: collections.deque = collections.deque()   # (due, bytes) under an emulated RTT
 
     def send(self, data: bytes) -> None:
         """Corked: frames queued in one loop iteration go out in one write."""
@@ -180,9 +181,26 @@ class _ServerConn:
         if self._wbuf:
             data = self._wbuf[0] if len(self._wbuf) == 1 else b"".join(self._wbuf)
             self._wbuf.clear()
+            rtt = self.broker.rtt
+            if rtt and not self.closed:
+                # emulated network: what the broker sends arrives one RTT later, in order
+                self._delayed.append((time.monotonic() + rtt, data))
+                if len(self._delayed) == 1:
+                    asyncio.get_running_loop().call_later(rtt, self._release)
+                return
             if not self.writer.is_closing():
                 self.writer.write(data)
                 self.last_write = time.monotonic()
+
+    def _release(self) -> None:
+        now = time.monotonic()
+        while self._delayed and self._delayed[0][0] <= now + 1e-4:
+            _due, data = self._delayed.popleft()
+            if not self.writer.is_closing():
+                self.writer.write(data)
+                self.last_write = now
+        if self._delayed:
+            asyncio.get_running_loop().call_later(max(0.0, self._delayed[0][0] - now), self._release)
 
     def send_method(self, ch: int, m: Method) -> None:
         self.send(codec.method_frame(ch, m))
@@ -255,6 +273,8 @@ class Broker:
         self.stats = collections.Counter()
         self.users: dict[str, tuple[str, Perms]] = {}
         self.refusals: list[tuple[str, str, str, str]] = []   # (user, kind, resource type, name)
+        from .rawserver import fake_rtt
+        self.rtt = fake_rtt()              # emulated round trip: every frame sent arrives this much later
 
     def add_user(self, user: str, password: str, *, configure: str = ".*", write: str = ".*",
                  read: str = ".*") -> None:
@@ -379,6 +399,8 @@ class Broker:
         self.conns.add(c)
         try:
             hdr = await reader.readexactly(8)
+            if self.rtt:
+                await asyncio.sleep(self.rtt)      # the TCP handshake before the protocol header
             if hdr != codec.PROTOCOL_HEADER:
                 writer.write(codec.PROTOCOL_HEADER)
                 return

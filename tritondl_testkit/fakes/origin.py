@@ -68,7 +68,7 @@ class Origin:
         self.cut_match: str | None = None       # only cut requests whose Range header starts with this
         self.fail = 0
         self.chunked = False                    # GET bodies with Transfer-Encoding: chunked (no ranges)
-        self.rate: float | None = None
+        self.rate: float | None = web.fake_stream_rate()     # bytes/s per response stream (None: uncapped)
         self.chunked_content_length: int | None = None   # chunked responses also claim this length
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []

@@ -232,9 +232,14 @@ class _Conn:
 
     async def serve(self) -> None:
         buf = b""
+        rtt = self.server.rtt
         try:
+            if rtt:
+                await asyncio.sleep(rtt)                 # TCP handshake (SYN / SYN-ACK)
             if self.raw.tls is not None:
                 await self.raw.handshake(30.0)
+                if rtt:
+                    await asyncio.sleep(rtt)             # TLS 1.3: one more round trip
             while not self.closed:
                 while b"\r\n\r\n" not in buf:
                     d = await self.recv(256 << 10)
@@ -258,6 +263,8 @@ class _Conn:
                 req = Request(self, method, target, version, hdrs, buf)
                 buf = b""
                 self.streamed = None
+                if rtt:
+                    await asyncio.sleep(rtt)             # request -> response round trip
                 resp = await self.server.handler(req)
                 if self.closed:
                     return
@@ -323,10 +330,38 @@ class _FdFile:
         return os.read(self._fd, n if n >= 0 else 1 << 30)
 
 
+def fake_rtt() -> float:
+    """Emulated network round trip of the fakes, seconds (``TRITONDL_FAKE_RTT_MS``;
+    bench.py ``--rtt-ms``).  A latency model, not a bandwidth one: every new
+    connection, TLS handshake and request/response exchange waits one RTT
+    (the broker delays every frame it sends by one RTT); bytes then flow at
+    loopback speed."""
+    import os
+    try:
+        return max(0.0, float(os.environ.get("TRITONDL_FAKE_RTT_MS", "0") or 0) / 1000.0)
+    except ValueError:
+        return 0.0
+
+
+def fake_stream_rate() -> float | None:
+    """Per-stream bandwidth cap of the fake origin / S3, bytes/s
+    (``TRITONDL_FAKE_STREAM_MBPS``, Mbit/s; bench.py ``--stream-mbps``): one
+    TCP stream's window / RTT on a real path, which is what parallel Range
+    streams and parallel multipart parts exist to beat.  None = uncapped."""
+    import os
+    try:
+        v = float(os.environ.get("TRITONDL_FAKE_STREAM_MBPS", "0") or 0)
+    except ValueError:
+        return None
+    return v * 1e6 / 8 if v > 0 else None
+
+
 class Server:
-    def __init__(self, handler, tls: tuple[str, str] | None = None) -> None:
-        """``tls``: (cert_pem, key_pem) to serve https."""
+    def __init__(self, handler, tls: tuple[str, str] | None = None, rtt: float | None = None) -> None:
+        """``tls``: (cert_pem, key_pem) to serve https.  ``rtt``: emulated round
+        trip (s; default :func:`fake_rtt`)."""
         self.handler = handler
+        self.rtt = fake_rtt() if rtt is None else rtt
         self.tls = rawhttp.relay_module().TlsContext.server(*tls) if tls is not None else None
         self._srv: asyncio.base_events.Server | None = None
         self._conns: set[asyncio.Task] = set()

@@ -86,6 +86,7 @@ class FakeS3:
         self.bucket_regions: dict[str, str] = {}
         self._outage_until = 0.0
         self.rate: float | None = None          # bytes/s of a shared ingest link (None: unlimited)
+        self.stream_rate = web.fake_stream_rate()   # bytes/s of one PUT's stream (None: unlimited)
         self._link_free = 0.0
         self.access_key, self.secret_key = access_key, secret_key
         self.region = region
@@ -199,7 +200,12 @@ class FakeS3:
         With ``rate`` set, the reply waits until a shared link of that many
         bytes/s would have carried the body (all requests queue on it)."""
         n = request.body_length or 0                 # remaining bytes: read it before the body is consumed
+        t0 = time.monotonic()
         body = await self._read_body_raw(request, auth, keep)
+        if self.stream_rate:                         # this stream cannot have carried it faster
+            wait = t0 + n / self.stream_rate - time.monotonic()
+            if wait > 0:
+                await asyncio.sleep(wait)
         if self.rate:
             now = time.monotonic()
             self._link_free = max(now, self._link_free) + n / self.rate
