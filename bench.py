@@ -306,8 +306,9 @@ def main() -> int:
                          "16-CPU box share one CCD measured 323-336 vs 222-279 jobs/s unpinned, "
                          "profiles/r03_pin_ab/)")
     ap.add_argument("--cleanup", default="on", choices=["on", "off"],
-                    help="on: each settled job's dir is deleted (its file kept as a spare the next download "
-                         "is renamed into, up to --recycle-mb); off: the reference, which never deletes (B15)")
+                    help="on (the worker default): each settled job's dir is deleted (its file kept as a spare "
+                         "the next download is renamed into, up to --recycle-mb); off: the reference, which never "
+                         "deletes (B15)")
     ap.add_argument("--recycle-mb", type=int, default=-1, help="spare-file budget with cleanup on (-1: worker "
                                                                "default, 0: delete every file)")
     ap.add_argument("--variants", type=int, default=-1,
@@ -598,8 +599,15 @@ def main() -> int:
             # native pump threads, from getrusage; the out-of-process fakes, producer included,
             # separately): the node's CPU count divided by this bounds how far job-level data
             # parallelism can scale.  null when the timed region is too short to mean much
-            "cpu_ms_per_job": ({k: round(sum(c[k] for c in cpu_all) / (world * a.steps) * 1000, 3)
-                                for k in ("worker", "fakes", "broker")} if max_elapsed >= 0.5 else None),
+            # worker_recv / worker_send: thread CPU of the download / upload pumps (part of
+            # "worker"); origin / s3 / broker / producer: each fake process (parts of "fakes")
+            "cpu_ms_per_job": ({k: round(sum(c.get(k, 0.0) for c in cpu_all) / (world * a.steps) * 1000, 3)
+                                for k in ("worker", "worker_recv", "worker_send", "fakes", "origin", "s3",
+                                          "broker", "producer")} if max_elapsed >= 0.5 else None),
+            # share of one core each fake process used over the timed region (rank 0's): a
+            # fake near 1.0 on a one-job-at-a-time run is what bounds it, not the worker
+            "fake_core_share": ({k: round(cpu_all[0].get(k, 0.0) / max_elapsed, 3)
+                                 for k in ("origin", "s3", "broker", "producer")} if max_elapsed >= 0.5 else None),
             # the one fake broker serves every rank: the share of a core it used.  Above
             # 0.5 the harness, not the workers, may be what limits the run
             "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3) if max_elapsed >= 0.5 else None,

@@ -139,7 +139,10 @@ class Config:
     # ... and once this worker has had a free job slot while its shard queues held ready
     # messages for this long without taking one (a consumer that gets nothing; 0 = off)
     health_stall_s: float = 120.0
-    cleanup: bool = False                       # B15: off for parity
+    # B15: a settled job's dir is deleted (its largest file kept as a spare for the next
+    # download, up to recycle_bytes).  The reference never deleted anything, so its work
+    # dir grew by every job ever run; TRITONDL_CLEANUP=0 is that behaviour
+    cleanup: bool = True
     # with cleanup: keep up to this many bytes of finished job files as spares that new
     # downloads are renamed into and overwrite, instead of freeing and re-allocating
     # their page cache per job (utils/spares.py; 0 = delete every file)

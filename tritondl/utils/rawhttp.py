@@ -483,6 +483,7 @@ async def _socks5_connect(c: RawConn, proxy, host: str, port: int, timeout: floa
 
 _active_pumps = 0
 _active_lock = __import__("threading").Lock()
+_thread_time = __import__("time").thread_time
 
 
 def active_pumps() -> int:
@@ -490,15 +491,28 @@ def active_pumps() -> int:
     return _active_pumps
 
 
+# thread CPU seconds and calls per relay pump (recv_body, send_body, ...) run
+# on executor threads: the worker's CPU split by data-plane stage (bench diag)
+PUMP_CPU: dict[str, list] = {}
+
+
 def _counted(fn, *args):
     global _active_pumps
     with _active_lock:
         _active_pumps += 1
+    t0 = _thread_time()
     try:
         return fn(*args)
     finally:
+        dt = _thread_time() - t0
+        name = getattr(fn, "__name__", "pump")
         with _active_lock:
             _active_pumps -= 1
+            ent = PUMP_CPU.get(name)
+            if ent is None:
+                ent = PUMP_CPU[name] = [0.0, 0]
+            ent[0] += dt
+            ent[1] += 1
 
 
 class _Port:

@@ -382,8 +382,14 @@ class JobStack:
         import resource
 
         import psutil
+        from tritondl.utils import rawhttp
         ru = resource.getrusage(resource.RUSAGE_SELF)
-        out = {"worker": ru.ru_utime + ru.ru_stime, "fakes": 0.0, "broker": 0.0}
+        out = {"worker": ru.ru_utime + ru.ru_stime, "fakes": 0.0, "broker": 0.0, "origin": 0.0, "s3": 0.0,
+               "producer": 0.0}
+        # the worker's data-plane pumps, by stage (thread CPU of the executor threads
+        # running them; native helper threads they start are in "worker" only)
+        for name, key in (("recv_body", "worker_recv"), ("send_body", "worker_send")):
+            out[key] = float(rawhttp.PUMP_CPU.get(name, (0.0, 0))[0])
         for b in self.backends + ([self.producer_proc] if self.producer_proc is not None else []):
             p = getattr(b, "proc", None)
             if p is None:
@@ -393,8 +399,8 @@ class JobStack:
             except psutil.Error:
                 continue
             out["fakes"] += ft.user + ft.system
-            if b.kind == "broker":
-                out["broker"] += ft.user + ft.system
+            if b.kind in out:
+                out[b.kind] += ft.user + ft.system
         return out
 
     def failures(self) -> list:
