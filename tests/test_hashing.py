@@ -514,3 +514,30 @@ def test_worker_gpu_verify_runs_in_a_helper_that_exits_idle(tmp_path):
     finally:
         p.kill()
         p.wait()
+
+
+@pytest.mark.gpu
+def test_helper_call_reports_progress_from_the_hip_hasher(tmp_path, monkeypatch):
+    """the helper's heartbeat carries the HIP hasher's
+    byte counter (``GpuHasher.progress``) while a call runs, so the worker
+    times a call out on *no progress*, not on its size.  A 0.01 s heartbeat
+    over a 1 GiB resume: several beats, rising to the layout's size."""
+    from tritondl.ops.gpu_helper import GpuHelper
+    monkeypatch.setenv("TRITONDL_GPU_PROGRESS_S", "0.01")
+    monkeypatch.delenv("TRITONDL_GPU_HELPER_FAKE", raising=False)
+    piece_len = 1 << 20
+    files, _blob, exp = _make_torrent_layout(tmp_path, [768 << 20, 256 << 20], piece_len)
+    h = GpuHelper(call_timeout=60)
+    try:
+        ok = h.verify_files(files, piece_len, exp)
+        assert ok == b"\x01" * (len(exp) // 20)
+        total = sum(n for _p, n in files)
+        assert h.last_beats >= 1, (h.last_beats, h.last_progress)
+        assert 0 < h.last_progress <= total
+        # the in-process hasher's counter is monotonic over its lifetime
+        hh = hashing.gpu_hasher()
+        p0 = hh.progress()
+        hh.verify_files(files, piece_len, exp, "sha1", 0)
+        assert hh.progress() - p0 == total
+    finally:
+        h.close()

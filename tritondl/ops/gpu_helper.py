@@ -225,6 +225,8 @@ class GpuHelper:
         self._rbuf = bytearray()                 # bytes read from the helper's stdout, not yet consumed
         self._lock = threading.Lock()
         self.spawned = 0
+        self.last_beats = 0                      # progress heartbeats received during the last call
+        self.last_progress = 0                   # bytes the last heartbeat of the last call reported
         self.last_gpu_pieces = 0
         self.last_direct_bytes = 0
         self.last_window_bytes = 0
@@ -323,6 +325,7 @@ class GpuHelper:
                     # the call may run as long as it keeps making progress: every heartbeat
                     # whose byte count grew pushes the deadline out by `gap`
                     done, deadline = 0, time.monotonic() + gap
+                    self.last_beats = self.last_progress = 0
                     while True:
                         try:
                             line = self._readline(p, deadline)
@@ -333,6 +336,8 @@ class GpuHelper:
                                               f"{gap:.0f}s ({done} bytes read); killed it") from None
                         rep = json.loads(line)
                         if "progress" in rep and "ok" not in rep and "error" not in rep:
+                            self.last_beats += 1
+                            self.last_progress = int(rep["progress"])
                             if int(rep["progress"]) > done:
                                 done = int(rep["progress"])
                                 deadline = time.monotonic() + gap
