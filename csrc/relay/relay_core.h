@@ -801,13 +801,55 @@ struct ChunkSigner {
   const std::string& prev() const { return chain.prev(); }
 };
 
+// A read-only MAP_SHARED view of [off, off + length) of fd, for encrypting
+// straight from the page cache (TLS): no pread copy into a user buffer.  Only
+// when the file already spans the range (a mapping read past EOF is SIGBUS);
+// otherwise empty and the caller preads.  `populate`: fault the whole range
+// in with one call (complete files; a range still being downloaded is
+// faulted in as it is read, behind the flow).
+struct FileView {
+  const char* p = nullptr;  // byte `off` of the file
+  void* base = MAP_FAILED;
+  size_t len = 0;
+  FileView(int fd, uint64_t off, uint64_t length, bool populate) {
+    struct stat st;
+    if (!length || ::fstat(fd, &st) != 0 || static_cast<uint64_t>(st.st_size) < off + length) return;
+    const uint64_t page = static_cast<uint64_t>(::sysconf(_SC_PAGESIZE));
+    const uint64_t a = off & ~(page - 1);
+    len = static_cast<size_t>(off + length - a);
+    base = ::mmap(nullptr, len, PROT_READ, MAP_SHARED | (populate ? MAP_POPULATE : 0), fd, static_cast<off_t>(a));
+    if (base == MAP_FAILED) return;
+    ::madvise(base, len, MADV_SEQUENTIAL);
+    p = static_cast<const char*>(base) + (off - a);
+  }
+  ~FileView() {
+    if (base != MAP_FAILED) ::munmap(base, len);
+  }
+  FileView(const FileView&) = delete;
+  FileView& operator=(const FileView&) = delete;
+};
+
+inline bool tls_send_mapped() {
+  static const bool on = [] {
+    const char* v = std::getenv("TRITONDL_TLS_SEND_MAP");
+    return !(v && (std::string(v) == "0" || std::string(v) == "off"));
+  }();
+  return on;
+}
+
 inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, Flow* flow, double idle_timeout) {
   SendResult r;
-  // sendfile moves 4 MiB per call; TLS encrypts from a user buffer, kept
-  // L2-sized so the pread'd bytes are still cache-hot when encrypted
+  // sendfile moves 4 MiB per call; TLS encrypts from user-space bytes: a
+  // mapping of the file's page cache (no copy), else an L2-sized buffer so
+  // the pread'd bytes are still cache-hot when encrypted
   const uint64_t step = io.plain() ? (4u << 20) : (256u << 10);
   auto last = Clock::now();
-  Buf buf(io.plain() ? 0 : static_cast<size_t>(std::min<uint64_t>(step, std::max<uint64_t>(length, 1))));
+  std::unique_ptr<FileView> view;
+  if (!io.plain() && tls_send_mapped()) {
+    view.reset(new FileView(fd, off, length, flow == nullptr && length <= (256ull << 20)));
+    if (!view->p) view.reset();
+  }
+  Buf buf(io.plain() || view ? 0 : static_cast<size_t>(std::min<uint64_t>(step, std::max<uint64_t>(length, 1))));
   while (r.sent < length) {
     const uint64_t n = std::min(step, length - r.sent);
     if (flow) {
@@ -822,6 +864,11 @@ inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, 
     }
     if (!io.plain()) {  // TLS: the record layer needs the bytes in user space
       const size_t m = static_cast<size_t>(n);
+      if (view) {
+        if (!send_all(io, view->p + r.sent, m, idle_timeout, flow, &r.err)) return r;
+        r.sent += n;
+        continue;
+      }
       if (tritondl_hash::pread_full(fd, buf.data(), m, static_cast<off_t>(off + r.sent)) != m) {
         r.err = "source file shorter than expected";
         return r;

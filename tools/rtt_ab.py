@@ -47,6 +47,18 @@ BIG = [
     ("big_segments_8_parts_8", ["--http-segments", "8", "--s3-parallel-parts", "8"],
      "256 MiB: 8 download streams and 8 parts in flight"),
 ]
+# a 32 MiB job (between one part and the 64 MiB multipart threshold), each stream capped
+MID = [
+    ("mid_default", [], "32 MiB: defaults (one PUT below the 64 MiB multipart threshold)"),
+    ("mid_multipart_16", ["--s3-multipart-mb", "16"], "32 MiB: multipart from 16 MiB (2 parts in parallel)"),
+    ("mid_multipart_16_segments_probe", ["--s3-multipart-mb", "16", "--http-segments", "4", "--probe-kb", "4096"],
+     "32 MiB: 2 parts + a 4 MiB probe and parallel Range streams"),
+]
+# uncapped (loopback bandwidth), 1 GiB: do more streams cost anything when no stream is capped?
+UNCAPPED = [
+    ("gib_default", [], "1 GiB, no stream cap: defaults"),
+    ("gib_segments_8_parts_8", ["--http-segments", "8", "--s3-parallel-parts", "8"], "1 GiB, no stream cap: 8 x 8"),
+]
 
 
 def run(args: list[str], timeout: float) -> dict:
@@ -71,32 +83,42 @@ def main() -> int:
     ap.add_argument("--stream-mbps", type=float, default=800.0, help="per-stream cap of the 256 MiB runs")
     ap.add_argument("--quick", action="store_true", help="fewer steps (a smoke run of the matrix)")
     ap.add_argument("--only", default="", help="comma-separated run names")
+    ap.add_argument("--repeat", type=int, default=1, help="alternate the selected runs this many times")
+    ap.add_argument("--sets", default="small,big", help="small,big,mid,uncapped")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     only = set(filter(None, a.only.split(",")))
     rows = []
     jl = open(os.path.join(a.out, "runs.jsonl"), "a")
-    for rtt in [float(x) for x in a.rtts.split(",")]:
-        small_steps = 10 if a.quick else (200 if rtt <= 2 else 60)
-        for name, extra, what in SMALL:
-            if only and name not in only:
-                continue
-            args = ["--rtt-ms", str(rtt), "--steps", str(small_steps), "--warmup", "5", *extra]
-            d = run(args, 240)
-            rows.append((rtt, name, what, d))
-            jl.write(json.dumps({"rtt_ms": rtt, "name": name, "args": args, "result": d}) + "\n")
-            jl.flush()
-            print(f"[{time.strftime('%T')}] rtt={rtt} {name}: {d.get('value', d.get('error'))}", flush=True)
-        for name, extra, what in BIG:
-            if only and name not in only:
-                continue
-            args = ["--rtt-ms", str(rtt), "--stream-mbps", str(a.stream_mbps), "--file-mb", "256",
-                    "--steps", "3" if a.quick else "8", "--warmup", "1", "--cleanup", "on", *extra]
-            d = run(args, 300)
-            rows.append((rtt, name, what, d))
-            jl.write(json.dumps({"rtt_ms": rtt, "name": name, "args": args, "result": d}) + "\n")
-            jl.flush()
-            print(f"[{time.strftime('%T')}] rtt={rtt} {name}: {d.get('value', d.get('error'))}", flush=True)
+    sets = set(a.sets.split(","))
+
+    def one(rtt: float, name: str, what: str, args: list[str], timeout: float) -> None:
+        d = run(args, timeout)
+        rows.append((rtt, name, what, d))
+        jl.write(json.dumps({"rtt_ms": rtt, "name": name, "args": args, "result": d}) + "\n")
+        jl.flush()
+        print(f"[{time.strftime('%T')}] rtt={rtt} {name}: {d.get('value', d.get('error'))}", flush=True)
+
+    for _rep in range(a.repeat):
+        for rtt in [float(x) for x in a.rtts.split(",")]:
+            small_steps = 10 if a.quick else (200 if rtt <= 2 else 60)
+            cap = ["--stream-mbps", str(a.stream_mbps)]
+            plan = []
+            if "small" in sets:
+                plan += [(n, ["--steps", str(small_steps), "--warmup", "5", *x], w, 240) for n, x, w in SMALL]
+            if "mid" in sets:
+                plan += [(n, [*cap, "--file-mb", "32", "--steps", "5" if a.quick else "20", "--warmup", "2", *x], w, 240)
+                         for n, x, w in MID]
+            if "big" in sets:
+                plan += [(n, [*cap, "--file-mb", "256", "--steps", "3" if a.quick else "8", "--warmup", "1", *x], w, 300)
+                         for n, x, w in BIG]
+            if "uncapped" in sets and rtt == 0:
+                plan += [(n, ["--file-mb", "1024", "--steps", "3" if a.quick else "6", "--warmup", "1", *x], w, 300)
+                         for n, x, w in UNCAPPED]
+            for name, extra, what, lim in plan:
+                if only and name not in only:
+                    continue
+                one(rtt, name, what, ["--rtt-ms", str(rtt), *extra], lim)
     jl.close()
     with open(os.path.join(a.out, "TABLE.md"), "w") as f:
         f.write("| RTT ms | run | jobs/s | MB/s | job p50 ms | fetched p50 | upload p50 | ack p50 | what |\n")
