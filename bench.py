@@ -313,8 +313,8 @@ def main() -> int:
                                                                "default, 0: delete every file)")
     ap.add_argument("--variants", type=int, default=-1,
                     help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
-    ap.add_argument("--pipeline-commit", default="off", choices=["on", "off"],
-                    help="on: a job's publish confirm and ack overlap the next job (opt-in worker setting)")
+    ap.add_argument("--pipeline-commit", default="on", choices=["on", "off"],
+                    help="on (the worker default): a job's publish confirm and ack overlap the next job")
     ap.add_argument("--no-reference-mode", action="store_true",
                     help="skip the secondary run in the reference's cleanup-off mode after the timed region")
     ap.add_argument("--no-content-check", action="store_true",

@@ -44,6 +44,8 @@ DIRECT = {
                                 "after 3 consecutive failed GPU calls (or a helper that cannot start) `auto` "
                                 "hashes on the host for this long, then offers the GPU again"),
     "TRITONDL_GPU_PROGRESS_S": ("1", "ops/gpu_helper.py", "interval of the helper's progress heartbeat during a call"),
+    "TRITONDL_TLS_SEND_MAP": ("1", "relay/relay_core.h",
+                              "0: TLS uploads pread into a buffer instead of encrypting from a mapping of the file"),
     "TRITONDL_GPU_DEVICE": ("LOCAL_RANK or 0", "ops/hashing.py", "the worker's GPU"),
     "TRITONDL_GPU_DIRECT": ("1", "ops/hashing.py, hip/gpu_hash.hip",
                             "0: stage piece data through pinned host buffers instead of DMA from the page cache"),
@@ -102,6 +104,8 @@ HARNESS = {
     "TRITONDL_GPU_HELPER_FAKE": "tests: a host stand-in for the GPU helper's hasher",
     "TRITONDL_GPU_HELPER_FAKE_STALL": "tests: seconds the stand-in helper stalls per call",
     "TRITONDL_GPU_HELPER_FAKE_SLOW": "tests: seconds the stand-in helper takes per call while reporting progress",
+    "TRITONDL_FAKE_RTT_MS": "emulated round trip of the fake broker / origin / S3 (set by `bench.py --rtt-ms`)",
+    "TRITONDL_FAKE_STREAM_MBPS": "per-stream bandwidth cap of the fake origin / S3 (set by `bench.py --stream-mbps`)",
     "TRITONDL_GPU_HELPER_CHILD": "internal: set in the helper process itself",
 }
 

@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # (name, bench args, what it tests)
 SMALL = [
-    ("default", [], "worker defaults (concurrency 1, prefetch 1, pipeline_commit off)"),
+    ("default", ["--pipeline-commit", "off"], "round-4 defaults (concurrency 1, prefetch 1, pipeline_commit off)"),
     ("pipeline_commit", ["--pipeline-commit", "on"], "publish confirm + ack overlap the next job (prefetch 1)"),
     ("pipeline_commit+prefetch2", ["--pipeline-commit", "on", "--prefetch", "2"],
      "pipelined commit with room on the shard for the next delivery"),

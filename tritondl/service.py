@@ -34,14 +34,18 @@ Differences, all documented fixes:
   fully async so downloads / uploads of different jobs overlap.  A job
   frees its loop once its upload is done: the ``v1.convert`` publish, its
   broker confirm and the ack finish in the job's own task while the next
-  job starts (``pipeline_commit``, opt-in).  The reference published
+  job starts (``pipeline_commit``, on by default).  The reference published
   without confirms and acked at once (``downloader.go:147-153``), so its
   commit cost no time; this keeps the confirm-before-ack guarantee without
-  a broker round trip per job.  The ack still follows the confirm, and the
-  job's dir stays locked until it is settled.  On the headline it measured
-  no faster (the single event loop does the commit's work either way, now
-  under the next job's start: ``profiles/r04_commit_ab/``), so it is off by
-  default;
+  a broker round trip per job on the critical path.  The ack still follows
+  the confirm, and the job's dir stays locked until it is settled.  The next
+  job comes from the *other* shard's consumer (prefetch 1 per shard
+  consumer: the committing delivery still holds its own shard's slot until
+  its ack).  On loopback, where a confirm costs ~0.05 ms, it measured
+  neutral (380 vs 379 jobs/s); with a 20 ms broker round trip it took the
+  job rate from 15.8 to 23.1 jobs/s, and prefetch 2 added nothing
+  (``profiles/r05_rtt_ab/``; the r04 explanation, "the event loop does the
+  work either way", was a loopback artefact);
 * a delivery whose ``X-Retries`` is past ``max_retries`` has already run
   ``max_retries + 1`` times: it goes straight to the dead-letter topic and is
   never run again (re-parked, without a download, while the dead-letter
