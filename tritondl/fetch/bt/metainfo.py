@@ -37,6 +37,19 @@ class MetainfoError(ValueError):
     pass
 
 
+def _bint(v) -> int:
+    """A bencoded integer field (not a string of digits, not a list)."""
+    if isinstance(v, bool) or not isinstance(v, int):
+        raise TypeError(f"expected an integer, got {type(v).__name__}")
+    return v
+
+
+def _bbytes(v) -> bytes:
+    if not isinstance(v, (bytes, bytearray)):
+        raise TypeError(f"expected a byte string, got {type(v).__name__}")
+    return bytes(v)
+
+
 @dataclass
 class FileEntry:
     path: list[str]      # path components below the torrent root
@@ -203,6 +216,8 @@ class Info:
 
     @classmethod
     def parse(cls, raw: bytes) -> "Info":
+        """Parse a bencoded info dict (remote input: any malformation is a
+        :class:`MetainfoError`, never another exception)."""
         try:
             d = bencode.decode(raw)
         except BencodeError as e:
@@ -213,8 +228,8 @@ class Info:
             return cls._parse_v2_only(d, raw)
         try:
             name = _safe_component(d[b"name"])
-            plen = int(d[b"piece length"])
-            pieces = bytes(d[b"pieces"])
+            plen = _bint(d[b"piece length"])
+            pieces = _bbytes(d[b"pieces"])
         except (KeyError, TypeError, ValueError) as e:
             raise MetainfoError(f"info dict missing field: {e}") from e
         if plen <= 0 or len(pieces) % 20:
@@ -224,23 +239,28 @@ class Info:
             v2_files = _parse_file_tree(d.get(b"file tree"), plen)
         files: list[FileEntry] = []
         off = 0
-        if b"files" in d:
-            multi = True
-            for f in d[b"files"]:
-                path = [_safe_component(c) for c in f[b"path"]]
-                if not path:
-                    raise MetainfoError("empty file path")
-                ln = int(f[b"length"])
+        try:
+            if b"files" in d:
+                multi = True
+                for f in d[b"files"]:
+                    path = [_safe_component(c) for c in f[b"path"]]
+                    if not path:
+                        raise MetainfoError("empty file path")
+                    ln = _bint(f[b"length"])
+                    if ln < 0:
+                        raise MetainfoError("negative length")
+                    attr = f.get(b"attr", b"")
+                    files.append(FileEntry(path, ln, off, isinstance(attr, bytes) and b"p" in attr))
+                    off += ln
+            else:
+                multi = False
+                ln = _bint(d[b"length"])
                 if ln < 0:
                     raise MetainfoError("negative length")
-                attr = f.get(b"attr", b"")
-                files.append(FileEntry(path, ln, off, isinstance(attr, bytes) and b"p" in attr))
-                off += ln
-        else:
-            multi = False
-            ln = int(d[b"length"])
-            files.append(FileEntry([name], ln, 0))
-            off = ln
+                files.append(FileEntry([name], ln, 0))
+                off = ln
+        except (KeyError, TypeError, ValueError, AttributeError) as e:   # remote input of any shape
+            raise MetainfoError(f"bad file list: {type(e).__name__}: {e}") from e
         npieces = len(pieces) // 20
         if npieces != (off + plen - 1) // plen:
             raise MetainfoError(f"piece count {npieces} does not match total length {off}")
