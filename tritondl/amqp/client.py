@@ -124,9 +124,11 @@ class Delivery:
         """True once the channel it arrived on is gone (the broker requeued it)."""
         return self.msg.channel is None or self.msg.channel.is_closed
 
-    async def ack(self) -> None:
-        """``Ack`` (single, ``delivery.go:55-57``)."""
-        await self._settle(lambda: self.msg.ack())
+    async def ack(self) -> bool:
+        """``Ack`` (single, ``delivery.go:55-57``).  False if the ack could not
+        be sent because the delivery's channel is gone (the broker requeues
+        it: it will be delivered again)."""
+        return await self._settle(lambda: self.msg.ack())
 
     async def nack(self, requeue: bool = False) -> None:
         """``Nack`` (single, no requeue by default, ``delivery.go:60-62``)."""
@@ -171,16 +173,17 @@ class Delivery:
         await self.ack()
         return "now"
 
-    async def _settle(self, fn) -> None:
+    async def _settle(self, fn) -> bool:
         if self.settled:
-            return
+            return False
         if self.stale:
             self.settled = True
             log.with_field("delivery_tag", self.msg.delivery_tag).warn(
                 "delivery's channel is gone; broker will redeliver it")
-            return
+            return False
         await fn()
         self.settled = True
+        return True
 
 
 class Shard:
@@ -263,6 +266,7 @@ class Client:
         self.parked_total = 0
         self.shards: dict[str, Shard] = {}         # shard queue -> its consumer state
         self.lost_since: float | None = None       # monotonic time the connection was lost (None: up)
+        self.consumer_timeouts = 0                 # shard channels the broker closed for a late ack
         self._consumer_chans: list[Channel] = []
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -476,6 +480,14 @@ class Client:
                 self._consumer_chans.remove(ch)
             if shard.channel is ch:
                 shard.set_inactive()
+            if getattr(exc, "code", 0) == codec.PRECONDITION_FAILED and "acknowledgement" in str(exc):
+                # RabbitMQ's consumer_timeout (30 min by default): a job ran longer than the broker
+                # lets a delivery sit unacked; the delivery goes back to the queue
+                self.consumer_timeouts += 1
+                log.with_fields(queue=q, error=str(exc)).error(
+                    "the broker closed this shard's channel: a job ran longer than its consumer_timeout "
+                    "allows; raise consumer_timeout (rabbitmq.conf, or the consumer-timeout policy / "
+                    "x-consumer-timeout on the shard queues) above the longest job")
             if not started:
                 return          # the basic.consume itself failed: the caller's retry loop owns the shard
             if self._closing or gen != self.generation or getattr(exc, "code", 0) == 200 or \

@@ -249,10 +249,16 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--min-workers", type=int, default=1,
                     help="exit non-zero once fewer workers than this are left (crash-looping ones are given up)")
     ap.add_argument("--health-addr", default="", help="host:port for the pool's /healthz and /metrics")
+    ap.add_argument("--worker-health-base", type=int, default=0,
+                    help="worker r serves its own /healthz on 127.0.0.1:BASE+r, which the pool's /healthz polls "
+                         "(default: the --health-addr port + 1; unless TRITONDL_METRICS_ADDR is set)")
+    ap.add_argument("--worker-health-grace", type=float, default=60.0,
+                    help="seconds after a worker starts before an unreachable /healthz counts against it")
     ap.add_argument("--max-restarts", type=int, default=5, help="restarts within --restart-window before giving up")
     ap.add_argument("--restart-window", type=float, default=60.0)
     a, rest = ap.parse_known_args(argv)
     pool = WorkerPool(plan(a.workers, base_port=a.base_port), argv=rest, grace=a.grace,
                       min_workers=a.min_workers, health_addr=a.health_addr, max_restarts=a.max_restarts,
-                      restart_window=a.restart_window)
+                      restart_window=a.restart_window, worker_health_base=a.worker_health_base,
+                      worker_health_grace=a.worker_health_grace)
     return asyncio.run(pool.run_until_signalled())

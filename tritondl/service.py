@@ -66,9 +66,11 @@ Differences, all documented fixes:
 from __future__ import annotations
 
 import asyncio
+import collections
 import contextlib
 import contextvars
 import fcntl
+import hashlib
 import os
 import queue
 import shutil
@@ -209,6 +211,10 @@ class Service:
         self._poison_parked = 0                    # poison jobs waiting in-process (DLQ unreachable)
         self._stall_since: float | None = None     # free slot + ready backlog, continuously since
         self._backlog = (0.0, 0)                   # (monotonic time polled, ready messages on the shards)
+        # jobs this worker finished whose ack was lost with its channel (the broker's consumer
+        # timeout, a channel error): body digest -> monotonic time.  Their redelivery is acked
+        # without running the job again (it was uploaded and its v1.convert published)
+        self._done_unacked: collections.OrderedDict[bytes, float] = collections.OrderedDict()
         self.metrics.collectors.append(self._collect_gauges)
 
     @contextlib.asynccontextmanager
@@ -480,6 +486,14 @@ class Service:
             log.with_field("job", job.to_dict()).info("got message")
         try:
             async with self._job_lock(job.media.id):
+                if msg.redelivered and self._already_done(msg.body):
+                    # the first delivery finished here, but its ack went nowhere: its channel was
+                    # closed under it (consumer_timeout, a channel error) and the broker requeued it
+                    log.with_field("media_id", job.media.id).warn(
+                        "redelivered job was already completed by this worker (its ack was lost); acking it")
+                    await msg.ack()
+                    self.metrics.inc("jobs", status="duplicate")
+                    return self._record(JobResult(True, "duplicate", seconds=time.monotonic() - t0))
                 return await self._run_job(msg, job, t0)
         except JobBusy as e:
             # not the job's failure: hand it back without spending a retry
@@ -533,7 +547,8 @@ class Service:
             stage = "ack"
             if log.enabled("info"):
                 log.with_field("job", job.to_dict()).info("finished processing")
-            await msg.ack()
+            if not await msg.ack():
+                self._note_done_unacked(msg.body)
             mark("ack")
         except asyncio.CancelledError:
             raise
@@ -732,6 +747,23 @@ class Service:
             self.amqp.park(msg, msg.retry_props(0 if poison else 1), self.cfg.retry_delay_max_s,
                            on_done=self._poison_unparked)
             self.metrics.inc("jobs_parked")
+
+    _DONE_TTL_S = 24 * 3600.0
+    _DONE_MAX = 4096
+
+    def _note_done_unacked(self, body: bytes) -> None:
+        self._done_unacked[hashlib.sha256(body).digest()] = time.monotonic()
+        while len(self._done_unacked) > self._DONE_MAX:
+            self._done_unacked.popitem(last=False)
+
+    def _already_done(self, body: bytes) -> bool:
+        now = time.monotonic()
+        while self._done_unacked:
+            k, t = next(iter(self._done_unacked.items()))
+            if now - t <= self._DONE_TTL_S:
+                break
+            self._done_unacked.popitem(last=False)
+        return self._done_unacked.pop(hashlib.sha256(body).digest(), None) is not None
 
     def _poison_unparked(self) -> None:
         self._poison_parked -= 1

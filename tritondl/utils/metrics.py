@@ -115,7 +115,7 @@ class Metrics:
 
 # one line per metric family (name without the prefix; counters without "_total")
 HELP = {
-    "jobs_total": "job attempts by status (ok, failed with its stage, busy)",
+    "jobs_total": "job attempts by status (ok, failed with its stage, busy, poison, duplicate)",
     "jobs_inflight": "jobs being processed by this worker",
     "jobs_retried_total": "failed jobs scheduled for a retry (broker delay queue or parked in-process)",
     "jobs_parked_total": "retries waited in-process because the broker refused the delay queue or DLQ",

@@ -137,6 +137,7 @@ class _ServerChannel:
         self.prefetch_channel = 0      # global=true
         self.prefetch_consumer = 0     # global=false (applies to new consumers)
         self.unacked: dict[int, tuple[QMsg, Queue, _Consumer | None]] = {}
+        self.delivered_at: dict[int, float] = {}       # delivery tag -> monotonic time (consumer timeout)
         self.tags = itertools.count(1)
         self.consumers: dict[str, _Consumer] = {}
         self.confirm = False
@@ -266,6 +267,10 @@ class Broker:
         self._qname = itertools.count(1)
         self.blocked = False
         self.delivery_paused = False
+        # RabbitMQ's consumer_timeout (3.8.15+, 30 min by default there; None = off): a
+        # delivery left unacked longer closes its channel with 406 PRECONDITION_FAILED
+        self.consumer_timeout: float | None = None
+        self._timeout_task: asyncio.Task | None = None
         self.fail_publishes = 0
         self.confirm_delay = 0.0           # fault injection: publisher confirms arrive this much later
         self.events: list[tuple[str, str]] = []   # ("publish", exchange) / ("ack", queue), in order
@@ -296,7 +301,37 @@ class Broker:
     async def start(self) -> "Broker":
         self._server = await asyncio.start_server(self._handle, self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
+        self._timeout_task = asyncio.ensure_future(self._consumer_timeouts())
         return self
+
+    async def _consumer_timeouts(self) -> None:
+        """rabbit_channel's delivery-acknowledgement timeout: a channel holding
+        a consumer delivery unacked for longer than ``consumer_timeout`` is
+        closed with 406 (its unacked deliveries go back to their queues)."""
+        try:
+            while True:
+                to = self.consumer_timeout
+                await asyncio.sleep(min(0.05, to / 4) if to else 0.2)
+                if not to:
+                    continue
+                now = time.monotonic()
+                for c in list(self.conns):
+                    for sc in list(c.channels.values()):
+                        old = [t for t, at in sc.delivered_at.items() if now - at > to and t in sc.unacked
+                               and sc.unacked[t][2] is not None]
+                        if not old:
+                            continue
+                        self.stats["consumer_timeouts"] += 1
+                        c.channels.pop(sc.id, None)
+                        self._close_channel(sc)
+                        c.send_method(sc.id, Method("channel.close", {
+                            "reply_code": codec.PRECONDITION_FAILED,
+                            "reply_text": f"PRECONDITION_FAILED - delivery acknowledgement on channel {sc.id} "
+                                          f"timed out. Timeout value used: {int(to * 1000)} ms. This timeout "
+                                          "value can be configured, see consumers doc guide to learn more",
+                            "class_id": 0, "method_id": 0}))
+        except asyncio.CancelledError:
+            pass
 
     @property
     def url(self) -> str:
@@ -309,6 +344,9 @@ class Broker:
         return f"{self.host}:{self.port}"
 
     async def stop(self) -> None:
+        if self._timeout_task is not None:
+            self._timeout_task.cancel()
+            self._timeout_task = None
         if self._server is not None:
             self._server.close()
             await self.drop_connections()
@@ -500,6 +538,7 @@ class Broker:
                 q.messages.appendleft(msg)
         touched = {q.name for _m, q, _c in ch.unacked.values()}
         ch.unacked.clear()
+        ch.delivered_at.clear()
         for name in touched:
             if name in self.queues:
                 self._dispatch(self.queues[name])
@@ -728,6 +767,7 @@ class Broker:
     def _close_channel_unacked_only(self, ch: _ServerChannel) -> None:
         for tag in sorted(ch.unacked, reverse=True):
             msg, q, cons = ch.unacked.pop(tag)
+            ch.delivered_at.pop(tag, None)
             if cons:
                 cons.unacked -= 1
             msg.redelivered = True
@@ -913,6 +953,7 @@ class Broker:
             tag = next(ch.tags)
             if not chosen.no_ack:
                 ch.unacked[tag] = (msg, q, chosen)
+                ch.delivered_at[tag] = time.monotonic()
                 chosen.unacked += 1
             q.delivered_total += 1
             ch.conn.send(b"".join(codec.content_frames(ch.id, Method("basic.deliver", {
@@ -936,6 +977,7 @@ class Broker:
         touched: set[str] = set()
         for t in tags:
             msg, q, cons = ch.unacked.pop(t)
+            ch.delivered_at.pop(t, None)
             if cons is not None:
                 cons.unacked -= 1
             touched.add(q.name)
