@@ -570,3 +570,38 @@ def test_chunked_overrides_a_bogus_content_length(tmp_path, native):
         await h.close()
         await o.stop()
     run(main())
+
+
+def test_retry_after_is_waited_out_inside_the_job(tmp_path):
+    """429 / 503 with a short Retry-After: the download waits that long and
+    retries inside the job (grab gave up on any status); a long one fails
+    the job at once, for the broker-side retry path to re-run later."""
+    import time as _t
+    from tritondl.fetch.http import HTTPDownloadError, retry_after
+
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(200_000)
+        url = o.add("/t.mkv", data)
+        o.throttle = (2, 429, "1")
+        h = HTTPDownloader(progress_interval=0.05)
+        t0 = _t.monotonic()
+        await h.download(str(tmp_path), Sink(), url)
+        assert 1.9 <= _t.monotonic() - t0 < 6
+        assert (tmp_path / "t.mkv").read_bytes() == data
+        o.throttle = (1, 503, "3600")
+        t0 = _t.monotonic()
+        with pytest.raises(HTTPDownloadError, match="retry after 3600"):
+            await HTTPDownloader(progress_interval=0.05).download(str(tmp_path / "b"), Sink(), url)
+        assert _t.monotonic() - t0 < 2
+        await o.stop()
+
+    class R:
+        status = 429
+        headers = {"Retry-After": "Wed, 21 Oct 2015 07:28:00 GMT"}
+    assert retry_after(R()) == 0.0                       # a date in the past: retry now
+    R.headers = {"Retry-After": "12"}
+    assert retry_after(R()) == 12.0
+    R.status = 500
+    assert retry_after(R()) is None
+    run(main())

@@ -73,6 +73,33 @@ class _FatalHTTPError(HTTPDownloadError):
     pass
 
 
+class _RetryLater(HTTPDownloadError):
+    """429 / 503 with a ``Retry-After`` the job can wait out in place."""
+
+    def __init__(self, msg: str, after: float) -> None:
+        super().__init__(msg)
+        self.after = after
+
+
+def retry_after(r) -> float | None:
+    """Seconds a 429 / 503 response asks the client to wait (``Retry-After``:
+    delta-seconds or an HTTP-date, RFC 9110 §10.2.3), else None."""
+    if r.status not in (429, 503):
+        return None
+    v = (r.headers.get("Retry-After") or "").strip()
+    if not v:
+        return None
+    if v.isdigit():
+        return float(v)
+    try:
+        from email.utils import parsedate_to_datetime
+        import datetime
+        when = parsedate_to_datetime(v)
+        return max(0.0, (when - datetime.datetime.now(datetime.timezone.utc)).total_seconds())
+    except (TypeError, ValueError, IndexError):
+        return None
+
+
 class _RawResponse:
     """The bits of an aiohttp response this module uses, over a raw
     connection (plain or TLS) whose body the native pump reads."""
@@ -208,6 +235,10 @@ class HTTPDownloader:
         self._session = session
         self.headers = headers or {"User-Agent": "tritondl/0.1"}
         self.max_retries = max_retries
+        # a 429 / 503 whose Retry-After is at most this long is waited out inside the job
+        # (it counts as a retry); a longer one fails the job, which the broker-side retry
+        # path re-runs later with its own growing delay.  grab gave up on any status
+        self.retry_after_max = 30.0
         # native data plane (csrc/relay): plain-http bodies go socket -> file in C++
         self.native = native
         self.read_timeout = read_timeout
@@ -400,17 +431,21 @@ class HTTPDownloader:
                 if r.status == 416:                      # empty resource: no satisfiable range
                     r.release()
                     r = await self._open(url, dict(self.headers))
-                if r.status < 500:
+                wait = retry_after(r)
+                if r.status < 500 and wait is None:
                     break
                 r.release()
                 err: Exception = HTTPDownloadError(f"GET {url}: HTTP {r.status}")
             except (aiohttp.ClientError, asyncio.TimeoutError) as e:
-                err = e
-            attempt += 1                                 # 5xx / transport error: transient
+                err, wait = e, None
+            attempt += 1                                 # 5xx / 429 / transport error: transient
             if attempt > self.max_retries:
                 raise HTTPDownloadError(f"probe of {url} failed: {err}") from err
-            log.with_fields(error=str(err), attempt=attempt).warn("download probe failed; retrying")
-            await asyncio.sleep(min(0.2 * 2 ** attempt, 5.0))
+            if wait is not None and wait > self.retry_after_max:
+                raise HTTPDownloadError(f"GET {url}: HTTP {getattr(r, 'status', '?')}, retry after {wait:.0f}s")
+            d = min(0.2 * 2 ** attempt, 5.0) if wait is None else wait
+            log.with_fields(error=str(err), attempt=attempt, delay_s=round(d, 2)).warn("download probe failed; retrying")
+            await asyncio.sleep(d)
         if r.status >= 400:
             r.release()
             raise HTTPDownloadError(f"GET {url}: HTTP {r.status}")
@@ -659,6 +694,9 @@ class HTTPDownloader:
                         hdrs["If-Range"] = validator
                 r = await self._open(url, hdrs)
                 try:
+                    wait = retry_after(r)
+                    if wait is not None:
+                        raise _RetryLater(f"GET {url}: HTTP {r.status}, retry after {wait:.1f}s", wait)
                     if r.status >= 400:
                         raise HTTPDownloadError(f"GET {url}: HTTP {r.status}")
                     if "Range" in hdrs and r.status != 206:
@@ -676,10 +714,12 @@ class HTTPDownloader:
                 attempt += 1
                 if h is not None and h.flow is not None and h.flow.cancelled:
                     raise _FatalHTTPError(f"segment {i} of {url}: download cancelled") from e
+                later = e.after if isinstance(e, _RetryLater) else None
                 if attempt > self.max_retries or isinstance(e, _FatalHTTPError) or \
-                        (isinstance(e, HTTPDownloadError) and "HTTP 4" in str(e)):
+                        (later is not None and later > self.retry_after_max) or \
+                        (later is None and isinstance(e, HTTPDownloadError) and "HTTP 4" in str(e)):
                     raise HTTPDownloadError(f"segment {i} of {url} failed: {e}") from e
-                d = min(0.2 * 2 ** attempt, 5.0)
+                d = min(0.2 * 2 ** attempt, 5.0) if later is None else later
                 log.with_fields(error=str(e), attempt=attempt, segment=i).warn("download stream failed; retrying")
                 await asyncio.sleep(d)
 

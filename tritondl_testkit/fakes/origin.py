@@ -5,7 +5,8 @@ servers the HTTP downloader talks to (the reference had no test origin).
 ``tls=(cert_pem, key_pem)`` serves https (OpenSSL via the relay module).
 Fault knobs: ``ranges`` (advertise/honour Range), ``head`` (support HEAD),
 ``cut_after`` (drop the connection after N body bytes, once per request
-count in ``cut_times``; ``cut_match`` limits it to one Range), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap).
+count in ``cut_times``; ``cut_match`` limits it to one Range), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap),
+``throttle`` (N × 429/503 with a ``Retry-After``).
 Without faults or a rate cap, GET bodies leave through ``sendfile`` from a
 native thread (``SendfileResponse``) — blobs held in memory are mirrored to
 a memfd once.
@@ -67,6 +68,7 @@ class Origin:
         self.cut_times = 0
         self.cut_match: str | None = None       # only cut requests whose Range header starts with this
         self.fail = 0
+        self.throttle: tuple[int, int, str] | None = None   # (n, 429|503, Retry-After) for the next n GETs
         self.chunked = False                    # GET bodies with Transfer-Encoding: chunked (no ranges)
         self.rate: float | None = web.fake_stream_rate()     # bytes/s per response stream (None: uncapped)
         self.chunked_content_length: int | None = None   # chunked responses also claim this length
@@ -106,6 +108,10 @@ class Origin:
         if self.fail > 0:
             self.fail -= 1
             return web.Response(status=500, text="injected")
+        if self.throttle and request.method == "GET":
+            n, status, after = self.throttle
+            self.throttle = (n - 1, status, after) if n > 1 else None
+            return web.Response(status=status, text="slow down", headers={"Retry-After": str(after)})
         rd = self.redirects.get(request.path)
         if rd is not None:
             return web.Response(status=rd[0], headers={"Location": rd[1]})
