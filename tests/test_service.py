@@ -659,7 +659,7 @@ def test_pipelined_commit_overlaps_confirms_but_acks_after_them(tmp_path):
     v1.convert publish (at-least-once), and the reference's one-job-at-a-time
     data path is kept (concurrency 1)."""
     async def main():
-        e = await Env().up(tmp_path, pipeline_commit=True)
+        e = await Env().up(tmp_path, pipeline_commit=True, pipeline_commit_min_ms=0)
         e.broker.confirm_delay = 0.25
         for k in range(4):
             url = e.origin.add(f"/p{k}.mkv", os.urandom(50_000))
@@ -778,3 +778,27 @@ print(resource.getrusage(resource.RUSAGE_SELF).ru_minflt - r0)
         assert p.returncode == 0, p.stderr
         faults[trim] = int(p.stdout.split()[-1])
     assert faults[128 << 10] > 10 * 2000 and faults[4 << 20] < 2000, faults
+
+
+def test_pipelined_commit_follows_the_confirm_round_trip(tmp_path):
+    """Commits are pipelined only while the broker's publish -> confirm round
+    trip is long enough to be worth it (on loopback the overlap cost ~4 %,
+    under a 2-20 ms round trip it gained 30-47 %: profiles/r05_rtt_ab/)."""
+    async def main():
+        e = await Env().up(tmp_path, pipeline_commit=True, pipeline_commit_min_ms=10.0)
+        for k in range(3):
+            url = e.origin.add(f"/f{k}.mkv", os.urandom(20_000))
+            e.submit(Media(id=f"f{k}", source_uri=url), i=k)
+        await e.wait_results(3)
+        assert e.svc.amqp.confirm_ewma is not None and e.svc.amqp.confirm_ewma < 0.010
+        assert e.svc.metrics.get("pipeline_commit_active") == 0.0
+        e.broker.confirm_delay = 0.05                    # a 50 ms confirm: pipeline
+        for k in range(3, 12):
+            url = e.origin.add(f"/f{k}.mkv", os.urandom(20_000))
+            e.submit(Media(id=f"f{k}", source_uri=url), i=k)
+        await e.wait_results(12, timeout=20)
+        assert e.svc.amqp.confirm_ewma >= 0.010
+        assert e.svc.metrics.get("pipeline_commit_active") == 1.0
+        assert all(r.ok for r in e.svc.results)
+        await e.down()
+    run(main())

@@ -267,6 +267,7 @@ class Client:
         self.shards: dict[str, Shard] = {}         # shard queue -> its consumer state
         self.lost_since: float | None = None       # monotonic time the connection was lost (None: up)
         self.consumer_timeouts = 0                 # shard channels the broker closed for a late ack
+        self.confirm_ewma: float | None = None     # publish -> broker confirm, seconds (EWMA, alpha 0.2)
         self._consumer_chans: list[Channel] = []
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -808,9 +809,13 @@ class Client:
                     ch = await self._publisher()
                     # frames leave in order under the lock; the confirm is awaited outside
                     # it, so concurrent jobs' publishes share broker round trips
+                    t_pub = time.monotonic()
                     confirm = await ch.basic_publish(exchange, rk, body, props, wait_confirm=False)
                 if confirm is not None:
                     await confirm
+                    dt = time.monotonic() - t_pub
+                    e = self.confirm_ewma
+                    self.confirm_ewma = dt if e is None else e + 0.2 * (dt - e)
                 log.info("published message on topic %s", exchange)
                 return
             except (AMQPError, ConnectionError, OSError) as e:

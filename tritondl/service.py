@@ -426,7 +426,7 @@ class Service:
             self._last_taken = time.monotonic()
             self._inflight += 1
             self.metrics.set("jobs_inflight", self._inflight)
-            if not self.cfg.pipeline_commit:
+            if not self._pipeline_now():
                 try:
                     await self.handle(d)
                 finally:
@@ -446,6 +446,20 @@ class Service:
                 freed.cancel()
                 self._inflight -= 1
                 self.metrics.set("jobs_inflight", self._inflight)
+
+    def _pipeline_now(self) -> bool:
+        """Pipeline this job's commit?  Only when it is on and the broker's
+        publish -> confirm round trip (EWMA over recent jobs) is long enough
+        to be worth overlapping; until a confirm has been timed, not."""
+        if not self.cfg.pipeline_commit:
+            return False
+        floor = self.cfg.pipeline_commit_min_ms / 1000.0
+        if floor <= 0:
+            return True
+        e = self.amqp.confirm_ewma if self.amqp is not None else None
+        on = e is not None and e >= floor
+        self.metrics.set("pipeline_commit_active", 1.0 if on else 0.0)
+        return on
 
     async def _handle_with_slot(self, d: Delivery, slot: asyncio.Event) -> None:
         token = _SLOT.set(slot)

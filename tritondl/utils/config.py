@@ -58,7 +58,8 @@ ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_time
               "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
-              "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s"}
+              "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s",
+              "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -108,10 +109,14 @@ class Config:
 
     # --- job processing ---
     concurrency: int = 1                        # one job loop (downloader.go:103)
-    # a job's publish confirm + ack overlap the next job (service._worker): neutral on loopback
-    # (380 vs 379 jobs/s), +46 % at a 20 ms broker round trip (23.1 vs 15.8) because the
-    # confirm's RTT leaves the job's critical path (profiles/r05_rtt_ab/)
+    # a job's publish confirm + ack overlap the next job (service._worker): +30 % at a 2 ms and
+    # +47 % at a 20 ms broker round trip, because the confirm's RTT leaves the job's critical
+    # path (profiles/r05_rtt_ab/) ...
     pipeline_commit: bool = True
+    # ... but on loopback, where a confirm takes ~0.05 ms, the overlap cost ~4 % (372 vs 389
+    # jobs/s, profiles/r05_regress/): jobs are pipelined only while the publish -> confirm
+    # round trip (EWMA) is at least this long (ms; 0 = always)
+    pipeline_commit_min_ms: float = 0.3
     max_retries: int = 5                        # B4 fix: X-Retries budget
     retry_delay_s: float = 10.0                 # delivery.go:72 (first retry; waited in a broker delay queue)
     retry_backoff: float = 2.0                  # delay multiplier per retry (1.0 = the reference's fixed 10 s)

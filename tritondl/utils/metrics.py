@@ -124,6 +124,7 @@ HELP = {
     "consumer_active": "1 while the shard queue has a live consumer of this worker, else 0",
     "last_job_finished_age_seconds": "seconds since this worker last recorded a job result (or started)",
     "broker_down_seconds": "seconds the broker connection has been down (0 while up)",
+    "pipeline_commit_active": "1 while job commits are pipelined (the publish -> confirm round trip is long enough)",
     "jobs_dead_lettered_total": "jobs published to the dead-letter topic after max_retries",
     "jobs_dropped_total": "jobs nacked without requeue after max_retries (drop_failed)",
     "bytes_uploaded_total": "bytes uploaded to S3 by finished jobs",
