@@ -41,11 +41,12 @@ Differences, all documented fixes:
   the confirm, and the job's dir stays locked until it is settled.  The next
   job comes from the *other* shard's consumer (prefetch 1 per shard
   consumer: the committing delivery still holds its own shard's slot until
-  its ack).  On loopback, where a confirm costs ~0.05 ms, it measured
-  neutral (380 vs 379 jobs/s); with a 20 ms broker round trip it took the
-  job rate from 15.8 to 23.1 jobs/s, and prefetch 2 added nothing
-  (``profiles/r05_rtt_ab/``; the r04 explanation, "the event loop does the
-  work either way", was a loopback artefact);
+  its ack).  With a 2 / 20 ms broker round trip it took the job rate from
+  120 to 164 and from 15.8 to 23.2 jobs/s; prefetch 2 added nothing.  On
+  loopback, where a confirm costs ~0.05 ms, the overlap itself cost ~4 %, so
+  the worker times each publish -> confirm round trip and pipelines only
+  while its EWMA is at least ``pipeline_commit_min_ms``
+  (``profiles/r05_rtt_ab/``, ``profiles/r05_adaptive/``);
 * a delivery whose ``X-Retries`` is past ``max_retries`` has already run
   ``max_retries + 1`` times: it goes straight to the dead-letter topic and is
   never run again (re-parked, without a download, while the dead-letter
