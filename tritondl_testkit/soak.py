@@ -280,7 +280,14 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                     raise
             if timed:
                 if time.monotonic() - t0 >= len(samples) * sample_seconds:
+                    ok_h, why = await svc.health()          # what /healthz would answer now
                     take_sample()
+                    samples[-1]["healthy"] = ok_h
+                    if why:
+                        samples[-1]["health_why"] = why[:3]
+                    e = svc.amqp.confirm_ewma if svc.amqp is not None else None
+                    samples[-1]["confirm_ms"] = round(e * 1000, 3) if e is not None else None
+                    samples[-1]["pipelined"] = svc._pipeline_now()
             elif svc.jobs_finished >= next_sample:
                 take_sample()
                 next_sample += sample_every
@@ -334,11 +341,14 @@ def main() -> int:
     ap.add_argument("--retry-delay", type=float, default=0.0, help="seconds each failing job waits in a delay queue")
     ap.add_argument("--heartbeat", type=int, default=0, help="AMQP heartbeat (s), broker and worker")
     ap.add_argument("--tls", action="store_true", help="origin and S3 over https")
+    ap.add_argument("--rtt-ms", type=float, default=0.0, help="emulated round trip of the fakes (ms)")
     ap.add_argument("--dht-nodes", type=int, default=0, help="local DHT nodes the worker bootstraps from")
     ap.add_argument("--malloc-trim", type=float, default=None, help="worker's malloc_trim period (s; 0 = off)")
     ap.add_argument("--tracemalloc", type=int, default=0,
                     help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
+    if a.rtt_ms > 0:
+        os.environ["TRITONDL_FAKE_RTT_MS"] = str(a.rtt_ms)   # the fake processes inherit it
     if a.cpus:
         from tritondl.parallel import topology
         if a.cpus == "auto":
