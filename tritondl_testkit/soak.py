@@ -243,10 +243,11 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
             await ch.basic_publish("v1.download", f"v1.download-{i % 2}", body,
                                    Properties(delivery_mode=2, content_type="application/octet-stream"))
 
-        def take_sample() -> None:
+        def take_sample(extra: dict | None = None) -> None:
             nonlocal base_snap
             gc.collect()
             s = sample(svc)
+            s.update(extra or {})
             s["jobs"] = svc.jobs_finished - base
             s["minute"] = round((time.monotonic() - t0) / 60, 2)
             if tracemalloc.is_tracing():
@@ -281,13 +282,10 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
             if timed:
                 if time.monotonic() - t0 >= len(samples) * sample_seconds:
                     ok_h, why = await svc.health()          # what /healthz would answer now
-                    take_sample()
-                    samples[-1]["healthy"] = ok_h
-                    if why:
-                        samples[-1]["health_why"] = why[:3]
                     e = svc.amqp.confirm_ewma if svc.amqp is not None else None
-                    samples[-1]["confirm_ms"] = round(e * 1000, 3) if e is not None else None
-                    samples[-1]["pipelined"] = svc._pipeline_now()
+                    take_sample({"healthy": ok_h, **({"health_why": why[:3]} if why else {}),
+                                 "confirm_ms": round(e * 1000, 3) if e is not None else None,
+                                 "pipelined": svc._pipeline_now()})
             elif svc.jobs_finished >= next_sample:
                 take_sample()
                 next_sample += sample_every
