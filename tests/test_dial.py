@@ -190,3 +190,9 @@ def test_http_job_s3_put_and_amqp_connect_each_fall_back_in_under_a_second(duals
 
     t_amqp, t_s3, t_job = asyncio.run(asyncio.wait_for(main(), 60))
     assert t_amqp < 1.0 and t_s3 < 1.0 and t_job < 1.0, (t_amqp, t_s3, t_job)
+
+
+def test_ip_literals_skip_the_resolver():
+    assert dial.literal_infos("127.0.0.1", 80)[0][4] == ("127.0.0.1", 80)
+    assert dial.literal_infos("[::1]", 443)[0][0] == socket.AF_INET6
+    assert dial.literal_infos("example.com", 80) is None

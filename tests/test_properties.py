@@ -24,7 +24,7 @@ from tritondl.fetch.bt import peer as pw
 from tritondl.models import messages, wire
 from tritondl.ops import hashing
 
-SETTINGS = settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+SETTINGS = settings(max_examples=int(__import__("os").environ.get("TRITONDL_HYPOTHESIS_EXAMPLES", "150")), deadline=None, suppress_health_check=[HealthCheck.too_slow])
 
 # ----------------------------------------------------------------- bencode
 

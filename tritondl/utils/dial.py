@@ -108,12 +108,30 @@ async def connect_any(infos: list, timeout: float, delay: float = FALLBACK_DELAY
                     r.close()
 
 
+def literal_infos(host: str, port: int) -> list | None:
+    """``getaddrinfo``-shaped entries for an IP literal (no resolver thread hop,
+    as asyncio's own fast path), else None."""
+    import ipaddress
+    try:
+        ip = ipaddress.ip_address(host.strip("[]"))
+    except ValueError:
+        return None
+    fam = socket.AF_INET6 if ip.version == 6 else socket.AF_INET
+    addr = (str(ip), port, 0, 0) if ip.version == 6 else (str(ip), port)
+    return [(fam, socket.SOCK_STREAM, socket.IPPROTO_TCP, "", addr)]
+
+
+async def resolve(host: str, port: int) -> list:
+    infos = literal_infos(host, port)
+    if infos is None:
+        infos = await asyncio.get_running_loop().getaddrinfo(host, port, type=socket.SOCK_STREAM)
+    return infos
+
+
 async def dial(host: str, port: int, timeout: float = 30.0, delay: float = FALLBACK_DELAY) -> socket.socket:
     """Resolve ``host`` and connect with fast fallback; a connected
     non-blocking TCP socket (``TCP_NODELAY`` set)."""
-    loop = asyncio.get_running_loop()
-    infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
-    return await connect_any(infos, timeout, delay)
+    return await connect_any(await resolve(host, port), timeout, delay)
 
 
 async def open_connection(host: str, port: int, *, timeout: float = 30.0, delay: float = FALLBACK_DELAY,
@@ -130,4 +148,4 @@ async def open_connection(host: str, port: int, *, timeout: float = 30.0, delay:
         raise
 
 
-__all__ = ["FALLBACK_DELAY", "interleave", "connect_any", "dial", "open_connection"]
+__all__ = ["FALLBACK_DELAY", "interleave", "connect_any", "literal_infos", "resolve", "dial", "open_connection"]

@@ -379,9 +379,8 @@ async def _dial(host: str, port: int, timeout: float) -> socket.socket:
     """A connected non-blocking TCP socket: addresses raced with RFC 8305
     fast fallback (300 ms stagger, Go's net.Dialer default; utils/dial.py),
     ``timeout`` bounding the whole dial."""
-    loop = asyncio.get_running_loop()
     try:
-        infos = await loop.getaddrinfo(host, port, type=socket.SOCK_STREAM)
+        infos = await dial.resolve(host, port)
     except OSError as e:
         raise RawHTTPError(f"connect {host}:{port}: {e}") from e
     try:
