@@ -165,3 +165,24 @@ def test_metrics_collectors_run_on_render():
     m = Metrics()
     m.collectors.append(lambda: m.set("x", 7))
     assert "tritondl_x 7" in m.render()
+
+
+def test_healthz_answers_at_once_while_the_backlog_poll_is_slow(tmp_path):
+    """The backlog count behind the stall check is polled in the background:
+    a broker slow to answer the passive declares never makes /healthz slow
+    (a probe's own timeout is often 1 s)."""
+    async def main():
+        e = await Env().up(tmp_path, health_stall_s=0.3)
+
+        async def slow(topic):
+            await asyncio.sleep(10)
+            return 0
+        e.amqp.ready_count = slow
+        t0 = time.monotonic()
+        for _ in range(5):
+            ok, why = await e.svc.health()
+            assert ok, why
+        assert time.monotonic() - t0 < 0.5
+        e.svc._backlog_task.cancel()
+        await e.down()
+    run(main())

@@ -212,6 +212,7 @@ class Service:
         self._poison_parked = 0                    # poison jobs waiting in-process (DLQ unreachable)
         self._stall_since: float | None = None     # free slot + ready backlog, continuously since
         self._backlog = (0.0, 0)                   # (monotonic time polled, ready messages on the shards)
+        self._backlog_task: asyncio.Task | None = None
         # jobs this worker finished whose ack was lost with its channel (the broker's consumer
         # timeout, a channel error): body digest -> monotonic time.  Their redelivery is acked
         # without running the job again (it was uploaded and its v1.convert published)
@@ -810,6 +811,13 @@ class Service:
             why.append(stall)
         return not why, why
 
+    async def _poll_backlog(self, now: float) -> None:
+        try:
+            n = await asyncio.wait_for(self.amqp.ready_count(self.cfg.consume_topic), 5.0)
+            self._backlog = (now, n)
+        except Exception:  # noqa: BLE001 - a missing queue is the shard check's business
+            self._backlog = (now, 0)
+
     async def _stall_reason(self) -> str:
         limit = self.cfg.health_stall_s
         now = time.monotonic()
@@ -817,12 +825,10 @@ class Service:
                 self._inflight >= max(1, self.cfg.concurrency):
             self._stall_since = None
             return ""
-        if now - self._backlog[0] >= 5.0:           # one passive declare per shard, at most every 5 s
-            try:
-                n = await asyncio.wait_for(self.amqp.ready_count(self.cfg.consume_topic), 5.0)
-                self._backlog = (now, n)
-            except Exception:  # noqa: BLE001 - a missing queue is the shard check's business
-                self._backlog = (now, 0)
+        if now - self._backlog[0] >= 5.0 and (self._backlog_task is None or self._backlog_task.done()):
+            # one passive declare per shard, at most every 5 s, in the background: /healthz
+            # answers from the last count at once (a probe's own timeout is often 1 s)
+            self._backlog_task = asyncio.ensure_future(self._poll_backlog(now))
         if self._backlog[1] <= 0:
             self._stall_since = None
             return ""
