@@ -11,8 +11,10 @@ b https_c2 --steps 400 --warmup 10 --tls --concurrency 2 &&
 b https_c4 --steps 600 --warmup 20 --tls --concurrency 4 &&
 b https_c2_probe2560 --steps 400 --warmup 10 --tls --concurrency 2 --probe-kb 2560 &&
 b http_c2 --steps 400 --warmup 10 --concurrency 2 &&
-b http_c4 --steps 600 --warmup 20 --concurrency 4
+b http_c4 --steps 600 --warmup 20 --concurrency 4 &&
+TRITONDL_BENCH_LOOP_PROFILE=$OUT/loop.prof b http_c1_loopprof --steps 600 --warmup 20
 rc=$?
+python -c "import pstats; pstats.Stats('$OUT/loop.prof').sort_stats('tottime').print_stats(40)" > $OUT/loop_top.txt 2>&1
 for f in $OUT/*.log; do
   python - "$f" <<'PY'
 import json, sys
