@@ -510,6 +510,18 @@ class Service:
                     await msg.ack()
                     self.metrics.inc("jobs", status="duplicate")
                     return self._record(JobResult(True, "duplicate", seconds=time.monotonic() - t0))
+                if msg.redelivered and self.cfg.redelivery_limit > 0:
+                    n = self._count_redelivery(job.media.id, msg)
+                    if n > self.cfg.redelivery_limit:
+                        log.with_fields(media_id=job.media.id, redeliveries=n).error(
+                            "job keeps coming back unacknowledged (its workers die or lose their channel "
+                            "mid-job); dead-lettering it without running it")
+                        self.metrics.inc("jobs", status="redelivery-limit")
+                        await self._dead_letter(msg, "redelivery-limit",
+                                                RuntimeError(f"redelivered {n} times without an ack"))
+                        self._clear_redeliveries(job.media.id)
+                        return self._record(JobResult(False, "redelivery-limit", f"redelivered {n} times",
+                                                      seconds=time.monotonic() - t0))
                 return await self._run_job(msg, job, t0)
         except JobBusy as e:
             # not the job's failure: hand it back without spending a retry
@@ -566,6 +578,8 @@ class Service:
             if not await msg.ack():
                 self._note_done_unacked(msg.body)
             mark("ack")
+            if msg.redelivered:
+                self._clear_redeliveries(job.media.id)
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - any stage failure must settle the message
@@ -573,6 +587,8 @@ class Service:
                 stage = "upload"             # a streamed upload fails inside the download stage
             log.with_fields(stage=stage, error=str(e)).error("job failed")
             self.metrics.inc("jobs", status="failed", stage=stage)
+            if msg.redelivered:
+                self._clear_redeliveries(job.media.id)   # a failure handled here is X-Retries' business
             await self._dispose_failed(msg, stage, e)
             return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
         if self.cfg.cleanup:
@@ -780,6 +796,40 @@ class Service:
                 break
             self._done_unacked.popitem(last=False)
         return self._done_unacked.pop(hashlib.sha256(body).digest(), None) is not None
+
+    _REDELIVERIES = ".tritondl-redeliveries"
+
+    def _count_redelivery(self, media_id: str, msg: Delivery) -> int:
+        """Count one more unacknowledged return of this job: a small file in its
+        job dir (the dir survives a crashed worker, and every worker sharing
+        ``downloading/`` sees it), or RabbitMQ's ``x-delivery-count`` header
+        (quorum queues), whichever is higher.  Only redelivered deliveries
+        touch the file, so the first delivery of a job costs nothing."""
+        hdr = (msg.msg.properties.headers or {}).get("x-delivery-count")
+        n_hdr = hdr if isinstance(hdr, int) and not isinstance(hdr, bool) else 0
+        n = 0
+        try:
+            path = os.path.join(self.dispatcher.job_dir(media_id), self._REDELIVERIES)
+        except (ValueError, AttributeError):
+            return n_hdr
+        try:
+            with open(path) as f:
+                n = int(f.read().strip() or 0)
+        except (OSError, ValueError):
+            n = 0
+        n += 1
+        try:
+            with open(path, "w") as f:
+                f.write(str(n))
+        except OSError:
+            pass
+        return max(n, n_hdr)
+
+    def _clear_redeliveries(self, media_id: str) -> None:
+        try:
+            os.unlink(os.path.join(self.dispatcher.job_dir(media_id), self._REDELIVERIES))
+        except (OSError, ValueError, AttributeError):
+            pass
 
     def _poison_unparked(self) -> None:
         self._poison_parked -= 1

@@ -45,7 +45,7 @@ def _default_sign_threads() -> int:
 # this worker's own knobs): key -> Config field.  docs/CONFIG.md is generated
 # from these (tools/gen_config_doc.py) and kept in sync by a test.
 ENV_INTS = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES": "num_shard_queues",
-            "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port",
+            "MAX_RETRIES": "max_retries", "BT_LISTEN_PORT": "bt_listen_port", "REDELIVERY_LIMIT": "redelivery_limit",
             "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
             "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
             "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
@@ -118,6 +118,12 @@ class Config:
     # round trip (EWMA) is at least this long (ms; 0 = always)
     pipeline_commit_min_ms: float = 0.3
     max_retries: int = 5                        # B4 fix: X-Retries budget
+    # a job whose delivery keeps coming back unacknowledged (the worker died or lost its
+    # channel mid-job: an OOM kill, a crash in native code, a consumer timeout) is
+    # dead-lettered once it has been redelivered more than this many times (counted in the
+    # job dir, or RabbitMQ's x-delivery-count on quorum queues) instead of taking down
+    # every worker that picks it up; 0 = off
+    redelivery_limit: int = 5
     retry_delay_s: float = 10.0                 # delivery.go:72 (first retry; waited in a broker delay queue)
     retry_backoff: float = 2.0                  # delay multiplier per retry (1.0 = the reference's fixed 10 s)
     retry_delay_max_s: float = 300.0            # cap on one retry delay
