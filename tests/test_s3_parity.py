@@ -283,6 +283,48 @@ def test_interrupted_multipart_upload_resumes_from_landed_parts(tmp_path):
     run(main())
 
 
+def test_complete_multipart_200_error_and_lost_reply(tmp_path):
+    """S3 quirks of CompleteMultipartUpload: a 200 whose body is <Error>
+    (InternalError/SlowDown: retried in place, the parts are not re-sent; any
+    other code fails the upload), and a reply lost after the commit (the
+    retry answers NoSuchUpload; the object's multipart ETag proves it landed)."""
+    from tritondl.s3.client import multipart_etag
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk", store="memory").start()
+        s3.create_bucket("b")
+        c = S3Client(s3.endpoint, Static("ak", "sk"), part_size=5 << 20, multipart_threshold=5 << 20)
+        data = os.urandom((10 << 20) + 7)
+        p = tmp_path / "f.bin"
+        p.write_bytes(data)
+
+        s3.complete_error_200 = 2
+        n0 = len(s3.requests)
+        etag = await c.put_object("b", "k1", str(p))
+        assert s3.object_bytes("b", "k1") == data and s3.buckets["b"]["k1"].etag == etag
+        reqs = s3.requests[n0:]
+        assert sum(1 for m, u in reqs if m == "PUT") == 3                  # each part went once
+        assert sum(1 for m, u in reqs if m == "POST" and "uploadId" in u) == 3
+        assert not s3.uploads
+
+        s3.complete_lose_reply = 1
+        etag = await c.put_object("b", "k2", str(p))
+        assert etag == s3.buckets["b"]["k2"].etag and etag.endswith("-3")
+        assert s3.object_bytes("b", "k2") == data
+
+        # a non-transient 200 error fails (and aborts) the upload
+        s3.complete_error_200, s3.complete_error_code = 1, "InvalidPart"
+        with pytest.raises(S3Error) as ei:
+            await c.put_object("b", "k3", str(p))
+        assert ei.value.code == "InvalidPart" and "k3" not in s3.buckets["b"] and not s3.uploads
+        await c.close()
+        await s3.stop()
+    run(main())
+    md5 = __import__("hashlib").md5
+    a, b = md5(b"x").hexdigest(), md5(b"y").hexdigest()
+    assert multipart_etag([f'"{a}"', b]) == md5(bytes.fromhex(a) + bytes.fromhex(b)).hexdigest() + "-2"
+    assert multipart_etag(["not-an-md5"]) == "" and multipart_etag([]) == ""
+
+
 def test_stale_resume_state_starts_over(tmp_path):
     """A state file whose upload the server no longer has (aborted by a
     lifecycle rule) or that describes another object is ignored."""

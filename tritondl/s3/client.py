@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import hashlib
 import json
 import os
 import re
@@ -95,6 +96,24 @@ def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Err
         code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
                 resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
     return S3Error(status, code, msg, resource, region)
+
+
+def multipart_etag(part_etags: list[str]) -> str:
+    """The ETag S3 gives a multipart object: hex MD5 over the concatenated
+    binary part MD5s, then ``-<parts>``.  "" when a part ETag is not a plain
+    MD5 (SSE-KMS / SSE-C parts), where nothing can be predicted."""
+    raw = []
+    for e in part_etags:
+        e = e.strip('"')
+        if len(e) != 32:
+            return ""
+        try:
+            raw.append(bytes.fromhex(e))
+        except ValueError:
+            return ""
+    if not raw:
+        return ""
+    return hashlib.md5(b"".join(raw)).hexdigest() + f"-{len(raw)}"
 
 
 def _proxy_auth_error(px, resource: str, status: int = 407, detail: str = "") -> S3Error:
@@ -585,14 +604,11 @@ class S3Client:
             xml = "".join(f"<Part><PartNumber>{i + 1}</PartNumber><ETag>\"{e}\"</ETag></Part>"
                           for i, e in enumerate(etags))
             cbody = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
-            _st, _h, rb = await self._do("POST", bucket, key, query={"uploadId": upload_id}, body=cbody)
-            if b"<Error>" in rb:
-                raise _parse_error(200, rb, f"complete {key}")
-            r = _xml(rb, "CompleteMultipartUpload")
+            etag = await self._complete(bucket, key, upload_id, cbody, etags)
             if resume_path:
                 with contextlib.suppress(OSError):
                     os.remove(resume_path)
-            return (r.findtext(f"{S3_NS}ETag") or r.findtext("ETag") or "").strip('"')
+            return etag
         except BaseException as e:
             if resume_path and not isinstance(e, asyncio.CancelledError):
                 # keep the upload: a retry of this job continues from the parts that landed
@@ -608,6 +624,57 @@ class S3Client:
             except Exception:
                 pass
             raise
+
+    # S3 sends CompleteMultipartUpload's status line before it stitches the
+    # parts, so a failure while stitching comes back as 200 with an <Error>
+    # body; the API reference asks clients to retry these.
+    COMPLETE_RETRY_CODES = frozenset({"InternalError", "SlowDown", "ServiceUnavailable", "RequestTimeout"})
+
+    async def _complete(self, bucket: str, key: str, upload_id: str, cbody: bytes, etags: list[str]) -> str:
+        """CompleteMultipartUpload with both of its failure shapes handled.
+
+        * 200 + ``<Error>``: a transient code (:attr:`COMPLETE_RETRY_CODES`)
+          is retried in place; the upload is still open.  minio-go
+          (``api-put-object-multipart.go`` ``completeMultipartUploadCore``)
+          returned it as the job's error, so the whole job ran again.
+        * A reply lost after S3 committed (reset, a proxy's 5xx): the retry
+          that ``_do`` makes answers NoSuchUpload.  The object is then HEADed
+          and accepted when its ETag is the multipart ETag of exactly these
+          parts (MD5 over the part MD5s, ``-N``), else the error stands.
+        """
+        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
+        attempt = 0
+        while True:
+            attempt += 1
+            try:
+                _st, _h, rb = await self._do("POST", bucket, key, query={"uploadId": upload_id}, body=cbody)
+            except S3Error as e:
+                want = multipart_etag(etags)
+                if e.code == "NoSuchUpload" and want:
+                    got = await self._stat_etag(bucket, key)
+                    if got == want:
+                        log.with_fields(key=key, etag=got).info("complete reply lost; object already committed")
+                        return got
+                raise
+            if b"<Error>" not in rb:
+                r = _xml(rb, "CompleteMultipartUpload")
+                return (r.findtext(f"{S3_NS}ETag") or r.findtext("ETag") or "").strip('"')
+            err = _parse_error(200, rb, f"complete {key}")
+            if err.code not in self.COMPLETE_RETRY_CODES or attempt > self.max_retries:
+                raise err
+            d = pol.next_delay() or 1.0
+            log.with_fields(key=key, code=err.code, attempt=attempt).warn(
+                "complete multipart answered 200 with an error; retrying in %.2fs", d)
+            await asyncio.sleep(d)
+
+    async def _stat_etag(self, bucket: str, key: str) -> str:
+        try:
+            h = await self.stat_object(bucket, key)
+        except S3Error as e:
+            if e.status == 404:
+                return ""
+            raise
+        return (h.get("ETag") or "").strip('"')
 
     async def _put_native(self, relay, bucket: str, key: str, src: str | int, offset: int, length: int,
                           headers: dict, query: dict | None, mode: str, flow) -> str:

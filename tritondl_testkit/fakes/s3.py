@@ -97,6 +97,11 @@ class FakeS3:
         self.list_parts_page = 1000
         self.fail_parts: set[int] = set()       # fault injection: these part numbers get HTTP 500
         self.fail_parts_once = False            # ... only the first time each is sent
+        # CompleteMultipartUpload faults: the next N completes answer 200 with an
+        # <Error> body (upload left open), or commit and then lose the reply (503)
+        self.complete_error_200 = 0
+        self.complete_error_code = "InternalError"
+        self.complete_lose_reply = 0
         self._ids = itertools.count(1)
         self._fail = 0
         self._fail_status = 503
@@ -482,6 +487,11 @@ class FakeS3:
             return web.Response(body=body.encode(), content_type="application/xml")
         if m == "POST" and "uploadId" in q:
             body = await self._read_body(request, auth)
+            if self.complete_error_200 > 0 and q["uploadId"] in self.uploads:
+                self.complete_error_200 -= 1
+                eb = (f"<Error><Code>{self.complete_error_code}</Code><Message>We encountered an internal "
+                      f"error. Please try again.</Message><Resource>{_xml_escape(key)}</Resource></Error>")
+                return web.Response(body=eb.encode(), content_type="application/xml")
             up = self.uploads.pop(q["uploadId"], None)
             if up is None:
                 return _xml_err(404, "NoSuchUpload", "no such upload")
@@ -516,6 +526,9 @@ class FakeS3:
             md5s = b"".join(bytes.fromhex(up.parts[n].etag) for n in nums)
             o.etag = hashlib.md5(md5s).hexdigest() + f"-{len(nums)}"
             objs[up.key] = o
+            if self.complete_lose_reply > 0:
+                self.complete_lose_reply -= 1
+                return _xml_err(503, "ServiceUnavailable", "reply lost after commit")
             rb = (f"<CompleteMultipartUploadResult xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\">"
                   f"<Bucket>{bucket}</Bucket><Key>{_xml_escape(up.key)}</Key><ETag>\"{o.etag}\"</ETag>"
                   f"</CompleteMultipartUploadResult>")
