@@ -513,7 +513,10 @@ def test_watch_files_fires_in_file_order_and_on_resume(tmp_path):
         await _dl().download(str(dst), Sink(), magnet_for(info, [tr.url]), pick_files=pick, on_file=order.append)
         base = str(dst / "Pack")
         assert sorted(offered) == sorted(os.path.join(base, n) for n in ("a.mkv", "b.mkv", "c.txt", "d.mkv"))
-        assert order == [os.path.join(base, n) for n in ("a.mkv", "b.mkv", "d.mkv")]
+        # layout order is the picker's priority, not a guarantee: a request that
+        # times out on a loaded box is re-sent and can finish its file late
+        want = [os.path.join(base, n) for n in ("a.mkv", "b.mkv", "d.mkv")]
+        assert sorted(order) == sorted(want) and order.index(want[0]) < order.index(want[2]), order
         _check_tree(str(src), str(dst))
         # redelivery: everything is on disk; the resume verify fires each watched file
         again = []

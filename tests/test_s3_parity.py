@@ -325,6 +325,53 @@ def test_complete_multipart_200_error_and_lost_reply(tmp_path):
     assert multipart_etag(["not-an-md5"]) == "" and multipart_etag([]) == ""
 
 
+@pytest.mark.parametrize("offset", [3600.0, -7200.0])
+def test_clock_skew_is_learned_from_request_time_too_skewed(tmp_path, offset):
+    """A node whose clock drifted past S3's 15-minute window gets 403
+    RequestTimeTooSkewed naming S3's time; the client signs on S3's clock
+    from then on (one refusal, not one per request) on the aiohttp path, the
+    native PUT pump and multipart."""
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk", store="memory").start()
+        s3.create_bucket("b")
+        s3.clock_offset = offset
+        c = S3Client(s3.endpoint, Static("ak", "sk"), region="us-east-1", max_retries=0,
+                     part_size=5 << 20, multipart_threshold=5 << 20)
+        await c.put_object("b", "small", b"x" * 1000)
+        assert abs(c.clock_skew - offset) < 5 and s3.skew_refusals == 1
+        small = tmp_path / "s.bin"
+        small.write_bytes(os.urandom(300_000))
+        big = tmp_path / "b.bin"
+        big.write_bytes(os.urandom((11 << 20) + 3))
+        await c.put_object("b", "file", str(small))
+        await c.put_object("b", "multi", str(big))
+        assert s3.object_bytes("b", "multi") == big.read_bytes() and s3.skew_refusals == 1
+        # a fresh client learns it on the native PUT path too
+        c2 = S3Client(s3.endpoint, Static("ak", "sk"), region="us-east-1", max_retries=0)
+        await c2.put_object("b", "file2", str(small))
+        assert abs(c2.clock_skew - offset) < 5 and s3.object_bytes("b", "file2") == small.read_bytes()
+        # the server's clock moves back: the skew is re-learned, never looped on
+        s3.clock_offset = 0.0
+        await c2.put_object("b", "file3", str(small))
+        assert abs(c2.clock_skew) < 5
+        await c.close()
+        await c2.close()
+        await s3.stop()
+    run(main())
+
+
+def test_server_time_parsing():
+    from tritondl.s3.client import _parse_error
+    body = (b"<Error><Code>RequestTimeTooSkewed</Code><Message>m</Message><RequestTime>20260101T000000Z"
+            b"</RequestTime><ServerTime>2026-10-18T02:40:49.123Z</ServerTime></Error>")
+    e = _parse_error(403, body, "PUT /b/k")
+    assert e.server_time == 1792291249.0
+    e = _parse_error(403, b"<Error><Code>RequestTimeTooSkewed</Code></Error>", "PUT /b/k",
+                     {"Date": "Sun, 18 Oct 2026 02:40:49 GMT"})
+    assert e.server_time == 1792291249.0
+    assert _parse_error(403, b"<Error><Code>AccessDenied</Code></Error>", "x").server_time is None
+
+
 def test_stale_resume_state_starts_over(tmp_path):
     """A state file whose upload the server no longer has (aborted by a
     lifecycle rule) or that describes another object is ignored."""

@@ -26,11 +26,15 @@ minio-go library behaviours the reference relied on without naming them:
 from __future__ import annotations
 
 import asyncio
+import calendar
 import contextlib
+import datetime as _dt
+import email.utils
 import hashlib
 import json
 import os
 import re
+import time
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass
 from typing import AsyncIterator
@@ -69,6 +73,7 @@ class S3Error(Exception):
         super().__init__(f"S3 {status} {code}: {message} ({resource})")
         self.status, self.code, self.message, self.resource = status, code, message, resource
         self.region = region          # the bucket's region when S3 names it (XML <Region> / x-amz-bucket-region)
+        self.server_time: float | None = None   # RequestTimeTooSkewed: S3's clock (epoch s)
 
 
 def _xml(body: bytes, what: str) -> ET.Element:
@@ -80,14 +85,27 @@ def _xml(body: bytes, what: str) -> ET.Element:
         raise S3Error(0, "MalformedXML", f"unparsable {what} reply: {e}") from e
 
 
+def _server_time(xml_time: str, date_header: str) -> float | None:
+    """S3's clock from a RequestTimeTooSkewed reply: ``<ServerTime>``
+    (ISO 8601, AWS) or else the ``Date`` header (RFC 7231, minio and AWS)."""
+    if xml_time:
+        with contextlib.suppress(ValueError):
+            return calendar.timegm(time.strptime(xml_time.split(".")[0].rstrip("Z"), "%Y-%m-%dT%H:%M:%S"))
+    if date_header:
+        with contextlib.suppress(TypeError, ValueError):
+            return email.utils.parsedate_to_datetime(date_header).timestamp()
+    return None
+
+
 def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Error:
-    code = msg = region = ""
+    code = msg = region = stime = ""
     if body:
         try:
             root = ET.fromstring(body)
             code = (root.findtext("Code") or "")
             msg = (root.findtext("Message") or "")
             region = (root.findtext("Region") or "")
+            stime = (root.findtext("ServerTime") or "")
         except ET.ParseError:
             msg = body[:200].decode(errors="replace")
     if headers is not None:
@@ -95,7 +113,10 @@ def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Err
     if not code:     # HEAD replies carry no body: name the error like minio does
         code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
                 resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
-    return S3Error(status, code, msg, resource, region)
+    err = S3Error(status, code, msg, resource, region)
+    if code == "RequestTimeTooSkewed":
+        err.server_time = _server_time(stime, (headers.get("Date", "") or "") if headers is not None else "")
+    return err
 
 
 def multipart_etag(part_etags: list[str]) -> str:
@@ -210,6 +231,7 @@ class S3Client:
         self.creds = creds or default_chain()
         self.region = region            # "" = discover each bucket's region (minio-go without Region)
         self._regions: dict[str, str] = {}
+        self.clock_skew = 0.0               # seconds S3's clock is ahead of this host's (learned)
         self.lookup = lookup
         self.payload_mode = payload_mode
         self.part_size = max(part_size, 5 << 20)
@@ -373,6 +395,28 @@ class S3Client:
             return True
         return False
 
+    def _amzdate(self) -> str:
+        """``x-amz-date`` on S3's clock: the host's plus the learned skew."""
+        now = _dt.datetime.now(_dt.timezone.utc)
+        if self.clock_skew:
+            now += _dt.timedelta(seconds=self.clock_skew)
+        return sigv4.amz_dates(now)[0]
+
+    def _learn_skew(self, err: S3Error) -> bool:
+        """True when S3 refused the request as signed too far from its clock
+        (RequestTimeTooSkewed, > 15 min) and named its time: later requests
+        are dated on S3's clock and the caller re-signs without counting a
+        try.  AWS SDKs correct skew this way; minio-go did not, so a worker
+        on a drifted node failed every upload."""
+        if err.code != "RequestTimeTooSkewed" or err.server_time is None:
+            return False
+        skew = err.server_time - time.time()
+        if abs(skew - self.clock_skew) < 2.0:
+            return False                    # already dated on S3's clock: something else is wrong
+        log.with_fields(skew_s=round(skew, 1)).warn("host clock differs from S3's; signing on S3's clock")
+        self.clock_skew = skew
+        return True
+
     async def _do(self, method: str, bucket: str, key: str = "", query: dict | None = None,
                   headers: dict | None = None, body: bytes | None = None, *, body_factory=None,
                   payload_hash: str | None = None, expect: tuple[int, ...] = (200,),
@@ -380,12 +424,12 @@ class S3Client:
         """One signed request with retries on connection errors / 5xx."""
         pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         attempt = 0
-        region_hops = 0
+        region_hops = skew_hops = 0
         while True:
             attempt += 1
             host, path = self._target(bucket, key, path_style)
             sreg = region if region is not None else await self.bucket_region(bucket)
-            amzdate, _ = sigv4.amz_dates()
+            amzdate = self._amzdate()
             hdrs = {"host": host, "x-amz-date": amzdate}
             hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
             cred = self._creds()
@@ -424,6 +468,10 @@ class S3Client:
                     err = _parse_error(r.status, rbody, f"{method} {path}", r.headers)
                     if region is None and region_hops < 2 and self._learn_region(bucket, err, sreg):
                         region_hops += 1
+                        attempt -= 1
+                        continue
+                    if skew_hops < 2 and self._learn_skew(err):
+                        skew_hops += 1
                         attempt -= 1
                         continue
                     if r.status < 500 or not retry or attempt > self.max_retries:
@@ -691,7 +739,7 @@ class S3Client:
         pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         fd = os.dup(src) if isinstance(src, int) else os.open(src, os.O_RDONLY)
         attempt = 0
-        region_hops = 0
+        region_hops = skew_hops = 0
         try:
             while True:
                 attempt += 1
@@ -699,7 +747,7 @@ class S3Client:
                 m = "unsigned" if (cred.anonymous and mode == "streaming") else mode
                 host, path = self._target(bucket, key)
                 sreg = await self.bucket_region(bucket)
-                amzdate, _ = sigv4.amz_dates()
+                amzdate = self._amzdate()
                 hdrs = {"host": host, "x-amz-date": amzdate}
                 hdrs.update({k.lower(): str(v) for k, v in (headers or {}).items()})
                 if m == "streaming":
@@ -762,6 +810,10 @@ class S3Client:
                     err = _parse_error(resp.status, body, f"PUT {path}", resp.headers)
                     if region_hops < 2 and self._learn_region(bucket, err, sreg):
                         region_hops += 1
+                        attempt -= 1
+                        continue
+                    if skew_hops < 2 and self._learn_skew(err):
+                        skew_hops += 1
                         attempt -= 1
                         continue
                     if resp.status < 500 or attempt > self.max_retries:

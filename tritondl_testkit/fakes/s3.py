@@ -102,6 +102,8 @@ class FakeS3:
         self.complete_error_200 = 0
         self.complete_error_code = "InternalError"
         self.complete_lose_reply = 0
+        self.clock_offset = 0.0                 # seconds this server's clock is ahead of the host's
+        self.skew_refusals = 0
         self._ids = itertools.count(1)
         self._fail = 0
         self._fail_status = 503
@@ -196,7 +198,31 @@ class FakeS3:
         if not hmac.compare_digest(s.signature, sig):
             return _xml_err(403, "SignatureDoesNotMatch",
                             "The request signature we calculated does not match the signature you provided.")
+        skewed = self._skewed(amzdate)
+        if skewed is not None:
+            return skewed
         return s.key, sig, amzdate, s.scope
+
+    def _skewed(self, amzdate: str) -> web.Response | None:
+        """S3 refuses a request signed more than 15 minutes from its clock
+        (403 RequestTimeTooSkewed, naming both times); ``clock_offset``
+        moves this server's clock."""
+        import calendar
+        try:
+            t = calendar.timegm(time.strptime(amzdate, "%Y%m%dT%H%M%SZ"))
+        except ValueError:
+            return _xml_err(403, "AccessDenied", "bad x-amz-date")
+        now = time.time() + self.clock_offset
+        if abs(t - now) <= 900:
+            return None
+        self.skew_refusals += 1
+        st = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(now))
+        body = (f"<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>RequestTimeTooSkewed</Code>"
+                f"<Message>The difference between the request time and the current time is too large."
+                f"</Message><RequestTime>{amzdate}</RequestTime><ServerTime>{st}</ServerTime>"
+                f"<MaxAllowedSkewMilliseconds>900000</MaxAllowedSkewMilliseconds></Error>")
+        return web.Response(status=403, body=body.encode(), content_type="application/xml",
+                            headers={"Date": time.strftime("%a, %d %b %Y %H:%M:%S GMT", time.gmtime(now))})
 
     async def _read_body(self, request: web.Request, auth, keep: bool = True):
         """Verified request body.  ``keep=False`` (object data in discard
