@@ -40,6 +40,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import gc
 import json
 import os
 import sys
@@ -453,6 +454,7 @@ def main() -> int:
             loop_prof.enable()
         cpu0 = stack.cpu_seconds()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
+        gc0 = [g["collections"] for g in gc.get_stats()]
         t0 = time.perf_counter()
         if shared:
             loop.run_until_complete(phase(a.steps))
@@ -462,6 +464,7 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        gc1 = [g["collections"] for g in gc.get_stats()]
         vm1 = _vm_snapshot()
         cpu1 = stack.cpu_seconds()
         mhz1 = _cpu_mhz(pinned) if pinned else None
@@ -500,6 +503,10 @@ def main() -> int:
                 "nivcsw_per_job": round((ru1.ru_nivcsw - ru0.ru_nivcsw) / n_div, 1),
                 "s3_content_checked": bool(stack.content_check and stack.resolved_variants()),
                 "vm": _vm_delta(vm0, vm1, n_div),
+                # CPython collections per generation inside the timed region (the worker
+                # froze its start-up heap: Service.start -> freeze_startup_heap)
+                "gc_collections": {f"gen{i}": b - a for i, (a, b) in enumerate(zip(gc0, gc1))},
+                "gc_frozen": gc.get_freeze_count(),
                 "work_fs": _work_fs(stack)}
         spans: dict[str, list[float]] = {}
         for r in done:

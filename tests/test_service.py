@@ -802,3 +802,19 @@ def test_pipelined_commit_follows_the_confirm_round_trip(tmp_path):
         assert all(r.ok for r in e.svc.results)
         await e.down()
     run(main())
+
+
+def test_startup_heap_is_frozen_and_the_knob_turns_it_off(monkeypatch):
+    """Service.start moves the start-up heap to the permanent generation
+    (a full collection over torch's ~180k objects stalls the loop 40-100 ms);
+    TRITONDL_GC_FREEZE=0 leaves the collector alone."""
+    import gc
+    from tritondl.service import freeze_startup_heap
+    from tritondl.utils.config import Config
+    try:
+        assert freeze_startup_heap() > 1000 and gc.get_freeze_count() > 1000
+    finally:
+        gc.unfreeze()
+    assert Config().gc_freeze is True
+    monkeypatch.setenv("TRITONDL_GC_FREEZE", "0")
+    assert Config.from_env(argv=[]).gc_freeze is False

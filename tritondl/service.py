@@ -374,6 +374,8 @@ class Service:
                          cfg.gpu_warmup_timeout_s)
         if cfg.metrics_addr:
             self._metrics_runner = await serve_metrics(self.metrics, cfg.metrics_addr, health=self.health)
+        if cfg.gc_freeze:
+            freeze_startup_heap()
         await self.amqp.consume(cfg.consume_topic)
         if cfg.malloc_trim_s > 0:
             self._trimmer = asyncio.ensure_future(self._trim_heap(cfg.malloc_trim_s))
@@ -935,6 +937,18 @@ class Service:
         await self.start()
         await stop.wait()
         await self.shutdown()
+
+
+def freeze_startup_heap() -> int:
+    """Collect once, then move every surviving object to CPython's permanent
+    generation (``gc.freeze``), so later full collections skip them.  With
+    torch imported a process holds ~180k tracked objects.  A full collection
+    walks all of them on the event loop, which takes 40-100 ms: longer than
+    thirty 10 MiB jobs.  Returns the number of objects frozen."""
+    import gc
+    gc.collect()
+    gc.freeze()
+    return gc.get_freeze_count()
 
 
 def tune_malloc(mmap_threshold: int, arena_max: int = 0, trim_threshold: int = 0) -> dict:

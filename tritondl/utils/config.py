@@ -68,7 +68,8 @@ ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", 
 ENV_BOOLS = {"CLEANUP": "cleanup", "DROP_FAILED": "drop_failed", "DECLARE_PUBLISH": "declare_publish",
              "DECLARE_PUBLISH_QUEUES": "declare_publish_queues", "STREAM_UPLOAD": "stream_upload",
              "PIPELINE_COMMIT": "pipeline_commit", "BT_DHT": "bt_dht", "BT_DHT_IPV6": "bt_dht_ipv6",
-             "BT_UPNP": "bt_upnp", "BT_NATIVE_WIRE": "bt_native_wire", "BT_UTP": "bt_utp", "BT_PEX": "bt_pex"}
+             "BT_UPNP": "bt_upnp", "BT_NATIVE_WIRE": "bt_native_wire", "BT_UTP": "bt_utp", "BT_PEX": "bt_pex",
+             "GC_FREEZE": "gc_freeze"}
 # The reference's own variables, same names: name -> Config field
 REFERENCE_ENV = {"LOG_LEVEL": "log_level", "LOG_FORMAT": "log_format", "RABBITMQ_ENDPOINT": "rabbitmq_endpoint",
                  "RABBITMQ_USERNAME": "rabbitmq_username", "RABBITMQ_PASSWORD": "rabbitmq_password",
@@ -142,6 +143,11 @@ class Config:
     # the next allocation faults back: a 200 KiB malloc/free loop took 7x as long
     # (18 faults per cycle); 4 MiB costs ~3 MB of RSS in a soak (profiles/r04_malloc/)
     malloc_trim_threshold: int = 4 << 20
+    # move every object alive once the worker is wired (modules, native bindings, torch
+    # when the GPU path loaded it: ~180k objects) to CPython's permanent generation before
+    # consuming.  A full collection otherwise walks all of them on the event loop: 40-100 ms,
+    # a stall in the middle of a job and of the heartbeats (Service.start)
+    gc_freeze: bool = True
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
