@@ -461,3 +461,103 @@ def test_channel_housekeeping_methods():
         await conn.close()
         await b.stop()
     run(main())
+
+
+def test_mandatory_publish_surfaces_unroutable_messages():
+    """RabbitMQ confirms a message no queue is bound for and drops it.  With
+    ``mandatory`` it sends ``basic.return`` first; the channel matches the
+    return to its publish by message_id (an unroutable message is confirmed
+    at once, ahead of routable ones still being persisted, so order cannot
+    match them) and fails that publish's confirm with PublishReturned."""
+    from tritondl.amqp.connection import PublishReturned
+
+    async def main():
+        b = await Broker().start()
+        conn = await Connection.open(b.url)
+        ch = await conn.channel()
+        await ch.exchange_declare("ex", "direct", durable=True)
+        await ch.queue_declare("bound", durable=True)
+        await ch.queue_bind("bound", "ex", "bound")
+        await ch.confirm_select()
+        futs = [await ch.basic_publish("ex", rk, b"m", Properties(delivery_mode=2), mandatory=True,
+                                       wait_confirm=False) for rk in ("bound", "nowhere", "bound", "nowhere")]
+        res = await asyncio.gather(*futs, return_exceptions=True)
+        assert res[0] is True and res[2] is True
+        assert isinstance(res[1], PublishReturned) and isinstance(res[3], PublishReturned)
+        assert res[1].code == codec.NO_ROUTE and res[1].routing_key == "nowhere"
+        assert b.queue_depth("bound") == 2
+        # a caller's own message_id is kept and still matched
+        with pytest.raises(PublishReturned):
+            await ch.basic_publish("ex", "nowhere", b"m", Properties(message_id="job-42"), mandatory=True)
+        assert not ch._mandatory_ids and not ch._returned
+        # without mandatory the broker drops it and confirms (the reference's publish)
+        await ch.basic_publish("ex", "nowhere", b"m")
+        await conn.close()
+        await b.stop()
+    run(main())
+
+
+def test_client_redeclares_a_deleted_publish_queue_instead_of_losing_the_message():
+    """An operator deletes a v1.convert shard queue under a running worker:
+    the next publish to it comes back unroutable; the client forgets its
+    declared-topology cache, declares the queue and binding again and
+    publishes, so the message lands instead of vanishing."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        await cl.publish("v1.convert", b"first")
+        await cl.publish("v1.convert", b"second")
+        assert b.queue_depth("v1.convert-0") == 1 and b.queue_depth("v1.convert-1") == 1
+        b.delete_queue("v1.convert-0")
+        await cl.publish("v1.convert", b"third")          # round robin: shard 0, now gone
+        assert cl.returned == 1
+        assert [m.body for m in b.drain_queue("v1.convert-0")] == [b"third"]
+        await cl.close()
+        await b.stop()
+    run(main())
+
+
+def test_unroutable_publish_on_foreign_topology_fails_after_retries():
+    """A topology the worker may not declare (write-only user) that has no
+    queue for a routing key: the publish is retried, then fails loudly, so
+    the job is not acked as if its result had been delivered."""
+    from tritondl.amqp.connection import PublishReturned
+
+    async def main():
+        b = await Broker().start()
+        b.add_user("w", "w", configure="^$", write=".*", read=".*")
+        b.declare("v1.convert", 1)                        # only v1.convert-0 exists
+        cl = await Client(b.url.replace("guest:guest", "w:w"), prefetch=1).connect()
+        await cl.publish("v1.convert", b"ok", max_attempts=3)
+        with pytest.raises(PublishReturned):
+            await cl.publish("v1.convert", b"lost?", max_attempts=3)
+        assert cl.returned == 3 and "v1.convert" in cl.external_topics
+        assert b.queue_depth("v1.convert-0") == 1
+        await cl.close()
+        await b.stop()
+    run(main())
+
+
+def test_deleted_delay_queue_is_declared_again_not_lost():
+    """The retry copy goes to a delay queue through the default exchange; if
+    the queue was deleted after it was declared, the copy would be dropped
+    and the original acked.  The return makes the client declare it again."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1, retry_delay=5).connect()
+        await cl.consume("t")
+        names = [cl.delay_queue_name(f"t-{i}", 5) for i in range(2)]
+        for body in (b"j0", b"j1"):                       # one per shard: both delay queues declared
+            await cl.publish("t", body)
+            await (await cl.get(2)).retry(5)
+        assert [b.queue_depth(n) for n in names] == [1, 1]
+        for n in names:
+            b.delete_queue(n)
+        await cl.publish("t", b"j2")
+        d = await cl.get(2)
+        await d.retry(5)
+        name = cl.delay_queue_name(d.routing_key, 5)
+        assert b.queue_depth(name) == 1 and b.drain_queue(name)[0].body == b"j2"
+        await cl.close()
+        await b.stop()
+    run(main())

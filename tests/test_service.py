@@ -269,6 +269,10 @@ def test_failing_job_does_not_hold_the_slot(tmp_path):
         assert e.broker.queue_depth("v1.download-0.retry.5000ms") == 1
         held = e.broker.queues["v1.download-0.retry.5000ms"].messages[0]
         assert held.props.headers["X-Retries"] == 1
+        for _ in range(100):            # the result is recorded before the (pipelined) ack lands
+            if e.broker.unacked_count() == 0:
+                break
+            await asyncio.sleep(0.02)
         assert e.broker.unacked_count() == 0
         await e.down()
     run(main())

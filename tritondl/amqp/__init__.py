@@ -4,7 +4,8 @@ reconnect)."""
 
 from .client import Client, ConsumeError, Delivery, DeliveryMetadata
 from .codec import AMQPError, Properties
-from .connection import Channel, ChannelClosed, Connection, ConnectionClosed, Message, PublishNacked
+from .connection import Channel, ChannelClosed, Connection, ConnectionClosed, Message, PublishNacked, PublishReturned
 
 __all__ = ["Client", "Delivery", "DeliveryMetadata", "ConsumeError", "Connection", "Channel", "Message",
-           "Properties", "AMQPError", "ConnectionClosed", "ChannelClosed", "PublishNacked"]
+           "Properties", "AMQPError", "ConnectionClosed", "ChannelClosed", "PublishNacked",
+           "PublishReturned"]

@@ -65,7 +65,7 @@ from ..utils.gocompat import durafmt
 from ..utils.log import log
 from . import codec
 from .codec import AMQPError, Properties
-from .connection import Channel, ChannelClosed, Connection, ConnectionClosed, Message
+from .connection import Channel, ChannelClosed, Connection, ConnectionClosed, Message, PublishReturned
 
 ErrorEnsureExchange = "failed to ensure exchange"
 ErrorEnsureConsumerQueues = "failed to ensure consumer queues"
@@ -235,12 +235,15 @@ class Client:
 
     def __init__(self, url: str, *, prefetch: int = 10, num_shard_queues: int = 2, heartbeat: int = 30,
                  backoff: ExponentialBackoff | None = None, retry_delay: float = 10.0,
-                 declare_publish: bool = True, declare_publish_queues: bool = True) -> None:
+                 declare_publish: bool = True, declare_publish_queues: bool = True, mandatory: bool = True) -> None:
         """``declare_publish=False`` is the reference exactly (nothing declared on
         the publish side, ``client.go:224``); with it on (default) the exchange,
         and with ``declare_publish_queues`` its shard queues, are declared
         best-effort before the first publish so messages are not lost to a
-        missing exchange (B13)."""
+        missing exchange (B13).  ``mandatory`` (default) publishes so that a
+        message no queue is bound for comes back (``basic.return``) instead of
+        being confirmed and dropped; the reference's publishes were not
+        mandatory (``client.go:224-240``)."""
         self.url = url
         self.prefetch = prefetch                   # reference default 10 (client.go:107)
         self.num_shard_queues = num_shard_queues   # reference: 2 (client.go:108)
@@ -249,6 +252,8 @@ class Client:
         self.retry_delay = retry_delay
         self.declare_publish = declare_publish
         self.declare_publish_queues = declare_publish_queues
+        self.mandatory = mandatory
+        self.returned = 0                          # publishes the broker could not route (basic.return)
         self.conn: Connection | None = None
         self.generation = 0
         self._topics: list[str] = []
@@ -671,7 +676,8 @@ class Client:
                 q = await self._ensure_delay_queue(exchange, routing_key, delay)
                 async with self._pub_lock:
                     ch = await self._publisher()
-                    confirm = await ch.basic_publish("", q, body, props, wait_confirm=False)
+                    confirm = await ch.basic_publish("", q, body, props, mandatory=self.mandatory,
+                                                     wait_confirm=False)
                 if confirm is not None:
                     try:
                         await confirm
@@ -683,6 +689,13 @@ class Client:
                 return
             except DelayUnavailable:
                 raise
+            except PublishReturned as e:
+                # the delay queue was deleted after it was declared: without mandatory the
+                # retry copy vanished and the caller acked the original (a lost job)
+                self._declared_delay.discard(q)
+                if attempt == max_attempts or self._closing:
+                    raise
+                log.with_fields(queue=q, error=str(e)).warn("delay queue gone; declaring it again")
             except (AMQPError, ConnectionError, OSError) as e:
                 if attempt == max_attempts or self._closing:
                     raise
@@ -810,7 +823,8 @@ class Client:
                     # frames leave in order under the lock; the confirm is awaited outside
                     # it, so concurrent jobs' publishes share broker round trips
                     t_pub = time.monotonic()
-                    confirm = await ch.basic_publish(exchange, rk, body, props, wait_confirm=False)
+                    confirm = await ch.basic_publish(exchange, rk, body, props, mandatory=self.mandatory,
+                                                     wait_confirm=False)
                 if confirm is not None:
                     await confirm
                     dt = time.monotonic() - t_pub
@@ -818,6 +832,19 @@ class Client:
                     self.confirm_ewma = dt if e is None else e + 0.2 * (dt - e)
                 log.info("published message on topic %s", exchange)
                 return
+            except PublishReturned as e:
+                # confirmed but routed nowhere: RabbitMQ would have dropped it silently (and
+                # so did the reference's publish).  Re-declare the shard queue and binding
+                # (when the topology is ours) and publish again; a topology that stays
+                # unroutable fails the publish, so the job is retried, never lost
+                self.returned += 1
+                self._declared_pub.discard(exchange)
+                if attempt == max_attempts or self._closing:
+                    log.with_fields(error=str(e)).error("publish unroutable; giving up")
+                    raise
+                d = pol.next_delay() or 0.0
+                log.with_fields(error=str(e), attempt=attempt).warn("publish unroutable; retrying in %.2fs", d)
+                await asyncio.sleep(d)
             except (AMQPError, ConnectionError, OSError) as e:
                 if attempt == max_attempts or self._closing or self._permanent(exchange, e):
                     raise

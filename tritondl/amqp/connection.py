@@ -13,7 +13,9 @@ the reference opened a new TCP connection per channel, ``client.go:362``).
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import inspect
+import os
 import itertools
 import ssl
 import struct
@@ -45,6 +47,17 @@ class ChannelClosed(AMQPError):
 
 class PublishNacked(AMQPError):
     pass
+
+
+class PublishReturned(AMQPError):
+    """A mandatory publish the broker could not route to any queue
+    (``basic.return``, e.g. 312 NO_ROUTE): without ``mandatory`` RabbitMQ
+    drops such a message and still confirms it."""
+
+    def __init__(self, code: int, text: str, exchange: str, routing_key: str) -> None:
+        super().__init__(f"{code} {text}: no queue bound to exchange '{exchange}' for routing key "
+                         f"'{routing_key}'")
+        self.code, self.text, self.exchange, self.routing_key = code, text, exchange, routing_key
 
 
 @dataclass
@@ -422,7 +435,15 @@ class Channel:
         self._closed_exc: AMQPError | None = None
         self.confirm_mode = False
         self._pub_seq = 0
+        self._mid_seq = 0
+        self._mid_base = f"{os.getpid():x}.{id(self) & 0xffffff:x}"
         self._unconfirmed: dict[int, asyncio.Future] = {}
+        # mandatory publishes in confirm mode: seq -> message_id, and the returns seen for
+        # them (RabbitMQ sends basic.return before the basic.ack of the same message; an
+        # unroutable message is confirmed at once, possibly ahead of routable ones still
+        # being persisted, so returns are matched by message_id, not by order)
+        self._mandatory_ids: dict[int, str] = {}
+        self._returned: dict[str, PublishReturned] = {}
         self.on_return: Callable[[Message], Any] | None = None
         self.on_cancel: Callable[[str], Any] | None = None
         self._get_waiter: asyncio.Future | None = None
@@ -474,6 +495,10 @@ class Channel:
             if self._get_waiter and not self._get_waiter.done():
                 self._get_waiter.set_result(msg)
         elif m.name == "basic.return":
+            mid = msg.properties.message_id
+            if mid and mid in self._mandatory_ids.values():
+                self._returned[mid] = PublishReturned(m.args.get("reply_code", 0), m.args.get("reply_text", ""),
+                                                      m.args.get("exchange", ""), m.args.get("routing_key", ""))
             if self.on_return:
                 self.on_return(msg)
 
@@ -521,9 +546,13 @@ class Channel:
         tags = [t for t in self._unconfirmed if (t <= tag if multiple else t == tag)]
         for t in tags:
             f = self._unconfirmed.pop(t)
+            mid = self._mandatory_ids.pop(t, None)
+            ret = self._returned.pop(mid, None) if mid else None
             if not f.done():
                 if exc:
                     f.set_exception(exc)
+                elif ret is not None:
+                    f.set_exception(ret)
                 else:
                     f.set_result(True)
 
@@ -535,6 +564,8 @@ class Channel:
             if f is not None and not f.done():
                 f.set_exception(exc)
         self._unconfirmed.clear()
+        self._mandatory_ids.clear()
+        self._returned.clear()
         for cb in self._close_callbacks:
             try:
                 cb(exc)
@@ -655,6 +686,14 @@ class Channel:
         if not self.flow_active.is_set():
             await self.flow_active.wait()
         self._check()
+        mid = None
+        if mandatory and self.confirm_mode:
+            props = properties or Properties()
+            mid = props.message_id
+            if not mid:
+                self._mid_seq += 1
+                mid = f"tdl-{self._mid_base}-{self._mid_seq}"
+                properties = dataclasses.replace(props, message_id=mid)
         frames = codec.content_frames(self.id, Method("basic.publish", {
             "exchange": exchange, "routing_key": routing_key, "mandatory": mandatory, "immediate": immediate}),
             body, properties or Properties(), self.conn.frame_max or codec.DEFAULT_FRAME_MAX)
@@ -665,6 +704,8 @@ class Channel:
             seq = self._pub_seq
             fut = asyncio.get_running_loop().create_future()
             self._unconfirmed[seq] = fut
+            if mid is not None:
+                self._mandatory_ids[seq] = mid
         self.conn._write(b"".join(frames))
         try:
             await self.conn.drain()
@@ -672,6 +713,7 @@ class Channel:
             # nobody will await this confirm: drop it so its eventual failure is not orphaned
             if fut is not None:
                 self._unconfirmed.pop(seq, None)
+                self._mandatory_ids.pop(seq, None)
                 fut.cancel()
             raise
         if fut is not None and wait_confirm:
@@ -707,4 +749,4 @@ class Channel:
 
 
 __all__ = ["Connection", "Channel", "Message", "ConnectionClosed", "ChannelClosed", "PublishNacked",
-           "parse_url", "URLParams", "struct"]
+           "PublishReturned", "parse_url", "URLParams", "struct"]
