@@ -605,3 +605,44 @@ def test_retry_after_is_waited_out_inside_the_job(tmp_path):
     R.status = 500
     assert retry_after(R()) is None
     run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_url_userinfo_is_sent_as_basic_auth(tmp_path, native):
+    """Go's http.Client (under grab) sends a source URL's userinfo as
+    ``Authorization: Basic`` on every request for that URL; the password is
+    percent-decoded first, never put on the request line, and never logged."""
+    import io
+    from tritondl.utils.log import log
+
+    async def main():
+        o = await Origin().start()
+        data = os.urandom(1_200_000)
+        o.add("/private/show.mkv", data)
+        o.basic_auth["/private/show.mkv"] = "alice:p@ss w0rd"
+        url = o.url("/private/show.mkv").replace("http://", "http://alice:p%40ss%20w0rd@")
+        h = _dl(segments=3, probe_bytes=256 * 1024, native=native)
+        os.makedirs(tmp_path / "ok")
+        os.makedirs(tmp_path / "no")
+        await h.download(str(tmp_path / "ok"), Sink(), url)
+        assert (tmp_path / "ok" / "show.mkv").read_bytes() == data
+        gets = [a for (m, _p, _r), a in zip(o.requests, o.auth_seen) if m == "GET"]
+        assert len(gets) >= 3 and all(a.startswith("Basic ") for a in gets)
+        # no credentials: the origin's 401 fails the job
+        with pytest.raises(HTTPDownloadError):
+            await _dl(max_retries=0, native=native).download(str(tmp_path / "no"), Sink(),
+                                                              o.url("/private/show.mkv"))
+        await h.close()
+        await o.stop()
+    run(main())
+    buf = io.StringIO()
+    old = log.stream
+    log.stream = buf
+    try:
+        log.with_field("url", "https://alice:s3cret@media.example/x.mkv").info("download status")
+        log.error("dial amqp://guest:guest@rabbit:5672/ failed")
+    finally:
+        log.stream = old
+    out = buf.getvalue()
+    assert "s3cret" not in out and "guest:guest" not in out
+    assert "alice:xxxxx@media.example" in out and "guest:xxxxx@rabbit" in out

@@ -342,7 +342,8 @@ class HTTPDownloader:
             if not rawhttp.native_proxy_ok(px, secure):
                 return None
             target = rawhttp.request_target(u, px, secure)
-            hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity", **headers,
+            hh = {"Host": host if port == dport else f"{host}:{port}", "Accept-Encoding": "identity",
+                  **({} if "Authorization" in headers else rawhttp.basic_auth_header(u)), **headers,
                   **rawhttp.proxy_auth_header(px)}
             head = rawhttp.request_head("GET", target, hh)
             tls = self._tls_ctx() if secure else None
@@ -460,7 +461,9 @@ class HTTPDownloader:
                 r.release()
                 raise HTTPDownloadError(f"GET {url}: bad Content-Range {r.headers.get('Content-Range')!r}")
             p.size, p.ranges, p.first_end = int(m.group(3)), True, int(m.group(2)) + 1
-        if str(r.url) != url:
+        # aiohttp reports the URL without its userinfo: that is not a redirect, and
+        # the Range requests must keep the credentials (Go's later requests do)
+        if str(r.url) != url and str(r.url) != str(URL(url).with_user(None)):
             p.final_url = str(r.url)
         return p, r
 

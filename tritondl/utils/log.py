@@ -14,10 +14,15 @@ hashing callbacks, torch.distributed ranks) never interleave lines.
 from __future__ import annotations
 
 import json
+import re
 import sys
 import threading
 import time
 from typing import Any, TextIO
+
+# scheme://user:password@ in any line (a source URL with credentials, the AMQP
+# URL) is written as scheme://user:xxxxx@, as Go's url.URL.Redacted()
+_CREDS = re.compile(r"([A-Za-z][A-Za-z0-9+.-]*://[^/\s:@\"]*):[^@\s/\"]+@")
 
 LEVELS = {"trace": 6, "debug": 5, "info": 4, "warning": 3, "error": 2, "fatal": 1, "panic": 0}
 
@@ -137,6 +142,8 @@ class Logger:
             parts += [f"{k}={_text_value(v)}" for k, v in sorted(fields.items())]
             parts += [f"{k}={_text_value(v)}" for k, v in rec.items()]
             line = " ".join(parts)
+        if "@" in line:
+            line = _CREDS.sub(r"\1:xxxxx@", line)
         stream = self.stream or sys.stderr
         with self._lock:
             stream.write(line + "\n")

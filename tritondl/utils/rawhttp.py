@@ -20,6 +20,7 @@ downloads, no redirects.  Idle keep-alive connections are pooled per
 from __future__ import annotations
 
 import asyncio
+import base64
 import os
 import socket
 import weakref
@@ -88,8 +89,19 @@ def request_target(url, proxy, secure: bool) -> str:
     """Request-line target of ``url`` (a yarl URL): origin form, or absolute
     form when it goes through an http(s) proxy without a tunnel."""
     if not secure and absolute_form(proxy):
-        return str(url.with_fragment(None))
+        return str(url.with_fragment(None).with_user(None))     # userinfo never goes on the wire
     return url.raw_path_qs or "/"
+
+
+def basic_auth_header(url) -> dict:
+    """Go's http.Client sends a URL's userinfo as ``Authorization: Basic``
+    (``net/http/client.go`` ``send``) on that request only: a redirect to a
+    URL without userinfo goes without it.  ``url`` is a yarl URL (user and
+    password percent-decoded, as Go's ``Username()`` / ``Password()``)."""
+    if url.user is None:
+        return {}
+    raw = f"{url.user}:{url.password or ''}".encode()
+    return {"Authorization": "Basic " + base64.b64encode(raw).decode()}
 
 
 def native_proxy_ok(proxy, secure: bool) -> bool:

@@ -75,6 +75,8 @@ class Origin:
         self.latency = 0.0
         self.requests: list[tuple[str, str, str]] = []
         self.redirects: dict[str, tuple[int, str]] = {}     # path -> (status, Location)
+        self.basic_auth: dict[str, str] = {}    # path -> required "user:password" (401 otherwise)
+        self.auth_seen: list[str] = []          # Authorization headers of the requests
         self._server: web.Server | None = None
 
     def add(self, path: str, data: bytes | None = None, *, file: str | None = None,
@@ -112,6 +114,13 @@ class Origin:
             n, status, after = self.throttle
             self.throttle = (n - 1, status, after) if n > 1 else None
             return web.Response(status=status, text="slow down", headers={"Retry-After": str(after)})
+        self.auth_seen.append(request.headers.get("Authorization", ""))
+        need = self.basic_auth.get(request.path)
+        if need is not None:
+            import base64
+            if request.headers.get("Authorization", "") != "Basic " + base64.b64encode(need.encode()).decode():
+                return web.Response(status=401, text="unauthorized",
+                                    headers={"WWW-Authenticate": 'Basic realm="media"'})
         rd = self.redirects.get(request.path)
         if rd is not None:
             return web.Response(status=rd[0], headers={"Location": rd[1]})
