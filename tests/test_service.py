@@ -822,3 +822,29 @@ def test_startup_heap_is_frozen_and_the_knob_turns_it_off(monkeypatch):
     assert Config().gc_freeze is True
     monkeypatch.setenv("TRITONDL_GC_FREEZE", "0")
     assert Config.from_env(argv=[]).gc_freeze is False
+
+
+def test_dead_lettered_job_leaves_no_files_but_a_retried_one_keeps_them(tmp_path):
+    """With cleanup on, a job that failed for good (dead-lettered) has its
+    partial download removed, or a poison torrent's GBs would stay on disk
+    forever; while retries remain, the files stay for the next attempt to
+    resume from."""
+    async def main():
+        e = await Env().up(tmp_path, max_retries=1, retry_delay_s=0.3, cleanup=True)
+        e.svc.uploader.client.max_retries = 0
+        e.s3.fail_for(60.0)
+        url = e.origin.add("/keep.mkv", os.urandom(200_000))
+        e.submit(Media(id="pz", source_uri=url))
+        await e.wait_results(1, timeout=30)
+        job_dir = os.path.join(e.cfg.download_dir, "pz")
+        assert os.path.exists(os.path.join(job_dir, "keep.mkv"))        # retry pending: kept
+        await e.wait_results(2, timeout=30)
+        for _ in range(100):
+            if not os.path.exists(job_dir) and not any(".deleting-" in n for n in os.listdir(e.cfg.download_dir)):
+                break
+            await asyncio.sleep(0.02)
+        assert len(_dlq(e.broker)) == 1
+        assert not os.path.exists(job_dir)
+        assert not any(".deleting-" in n for n in os.listdir(e.cfg.download_dir))
+        await e.down()
+    run(main())

@@ -519,8 +519,9 @@ class Service:
                             "job keeps coming back unacknowledged (its workers die or lose their channel "
                             "mid-job); dead-lettering it without running it")
                         self.metrics.inc("jobs", status="redelivery-limit")
-                        await self._dead_letter(msg, "redelivery-limit",
-                                                RuntimeError(f"redelivered {n} times without an ack"))
+                        if await self._dead_letter(msg, "redelivery-limit",
+                                                   RuntimeError(f"redelivered {n} times without an ack")):
+                            self._reap_job_dir(job.media.id, msg)
                         self._clear_redeliveries(job.media.id)
                         return self._record(JobResult(False, "redelivery-limit", f"redelivered {n} times",
                                                       seconds=time.monotonic() - t0))
@@ -591,17 +592,11 @@ class Service:
             self.metrics.inc("jobs", status="failed", stage=stage)
             if msg.redelivered:
                 self._clear_redeliveries(job.media.id)   # a failure handled here is X-Retries' business
-            await self._dispose_failed(msg, stage, e)
+            if await self._dispose_failed(msg, stage, e):
+                self._reap_job_dir(job.media.id, msg)     # dead-lettered: no retry will resume it
             return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
         if self.cfg.cleanup:
-            # the job is settled: move its dir aside (one rename, so a redelivered job with the
-            # same id starts clean) and delete it off the critical path (drained on shutdown)
-            trash = f"{dl_dir}.deleting-{os.getpid()}-{id(msg):x}"
-            try:
-                os.rename(dl_dir, trash)
-            except OSError:
-                trash = dl_dir
-            self._reaper.submit(trash)
+            self._reap_job_dir(dl_dir, msg, is_path=True)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -730,10 +725,11 @@ class Service:
                 fut.set_result(None)
         return r
 
-    async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> None:
+    async def _dispose_failed(self, msg: Delivery, stage: str, err: Exception) -> bool:
         """B4 fix: retry with X-Retries+1 through a broker delay queue (the slot
         is free at once; parked in-process if the broker refuses the delay
-        queue), dead-letter after ``max_retries``."""
+        queue), dead-letter after ``max_retries``.  True once the job has
+        left for good (dead-lettered or dropped): nothing will resume it."""
         assert self.amqp is not None
         try:
             if msg.metadata.retries < self.cfg.max_retries:
@@ -743,26 +739,27 @@ class Service:
                 self.metrics.inc("jobs_retried")
                 if how == "parked":
                     self.metrics.inc("jobs_parked")
-                return
+                return False
         except Exception as e:  # noqa: BLE001
             # the retry publish itself failed: the delivery must still be settled, or a
             # prefetch-1 consumer stalls (B4)
             log.with_field("error", str(e)).error("failed to schedule retry; dead-lettering the job")
-        await self._dead_letter(msg, stage, err)
+        return await self._dead_letter(msg, stage, err)
 
-    async def _dead_letter(self, msg: Delivery, stage: str, err: Exception) -> None:
+    async def _dead_letter(self, msg: Delivery, stage: str, err: Exception) -> bool:
         """Publish the job (confirmed) to the durable dead-letter topic, then ack.
         If the dead-letter topic cannot be reached (a user that may neither
         declare nor write it), the job is parked: re-published to its own
         queue with ``X-Retries+1`` after ``retry_delay_max_s`` — the
         reference's ``Error()`` at the longest delay, never a nack-requeue
-        loop, and never dropped."""
+        loop, and never dropped.  True when the job was dead-lettered (or
+        dropped), False when it was parked or its channel was lost."""
         assert self.amqp is not None
         try:
             if self.cfg.drop_failed:
                 await msg.nack(requeue=False)
                 self.metrics.inc("jobs_dropped")
-                return
+                return True
             hdrs = dict(msg.msg.properties.headers or {})
             hdrs.update({"X-Retries": msg.metadata.retries, "X-Failed-Stage": stage, "X-Error": str(err)[:512],
                          "X-Original-Routing-Key": msg.routing_key})
@@ -770,9 +767,10 @@ class Service:
             await msg.ack()
             log.with_fields(topic=self.cfg.dlq_topic, stage=stage).warn("job dead-lettered")
             self.metrics.inc("jobs_dead_lettered")
+            return True
         except Exception as e:  # noqa: BLE001
             if msg.settled or msg.stale:
-                return                      # its channel is gone: the broker redelivers it anyway
+                return False                # its channel is gone: the broker redelivers it anyway
             log.with_fields(error=str(e), delay_s=self.cfg.retry_delay_max_s).error(
                 "failed to dead-letter job; parking it")
             # X-Retries ends one past the budget, where handle() stops running the job
@@ -781,6 +779,28 @@ class Service:
             self.amqp.park(msg, msg.retry_props(0 if poison else 1), self.cfg.retry_delay_max_s,
                            on_done=self._poison_unparked)
             self.metrics.inc("jobs_parked")
+            return False
+
+    def _reap_job_dir(self, media_id: str, msg: Delivery, is_path: bool = False) -> None:
+        """With cleanup on, a settled job's dir is moved aside (one rename, so a
+        redelivered job with the same id starts clean) and deleted off the
+        critical path (drained on shutdown).  After a success, and after a
+        dead-letter: a poison job's partial download (GBs of torrent) would
+        otherwise stay on disk forever.  Called with the job lock held."""
+        if not self.cfg.cleanup:
+            return
+        try:
+            d = media_id if is_path else self.dispatcher.job_dir(media_id)  # type: ignore[union-attr]
+        except (ValueError, AttributeError):
+            return
+        if not os.path.isdir(d):
+            return
+        trash = f"{d}.deleting-{os.getpid()}-{id(msg):x}"
+        try:
+            os.rename(d, trash)
+        except OSError:
+            trash = d
+        self._reaper.submit(trash)
 
     _DONE_TTL_S = 24 * 3600.0
     _DONE_MAX = 4096
