@@ -5,6 +5,7 @@ broker loss mid-job (at-least-once), concurrency, CLI + cpuprofile."""
 
 import asyncio
 import os
+import shutil
 import signal
 import subprocess
 import sys
@@ -766,13 +767,22 @@ libc.malloc.restype = ctypes.c_void_p
 libc.malloc.argtypes = [ctypes.c_size_t]
 libc.free.argtypes = [ctypes.c_void_p]
 libc.memset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+import threading
 tune_malloc(262144, trim_threshold=int(sys.argv[1]))
-r0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
-for _ in range(2000):
-    p = libc.malloc(200 << 10)
-    libc.memset(p, 1, 200 << 10)
-    libc.free(p)
-print(resource.getrusage(resource.RUSAGE_SELF).ru_minflt - r0)
+out = []
+def loop():
+    # on a fresh thread: its own arena has no free holes left by imports, so each
+    # block comes from the arena's top (the main heap's layout shifts with every import)
+    r0 = resource.getrusage(resource.RUSAGE_THREAD).ru_minflt
+    for _ in range(2000):
+        p = libc.malloc(200 << 10)
+        libc.memset(p, 1, 200 << 10)
+        libc.free(p)
+    out.append(resource.getrusage(resource.RUSAGE_THREAD).ru_minflt - r0)
+t = threading.Thread(target=loop)
+t.start()
+t.join()
+print(out[0])
 """
     from tritondl.utils.config import Config
     faults = {}
@@ -846,5 +856,58 @@ def test_dead_lettered_job_leaves_no_files_but_a_retried_one_keeps_them(tmp_path
         assert len(_dlq(e.broker)) == 1
         assert not os.path.exists(job_dir)
         assert not any(".deleting-" in n for n in os.listdir(e.cfg.download_dir))
+        await e.down()
+    run(main())
+
+
+def test_stale_job_dir_sweep(tmp_path):
+    """Job dirs untouched for the age limit go; a fresh one, one a worker
+    holds (flock), spare pools and live workers' trash stay; a dead worker's
+    half-deleted trash goes."""
+    import fcntl
+    import subprocess
+    from tritondl.service import sweep_stale_job_dirs
+    base = tmp_path / "downloading"
+    old, fresh, held = base / "old", base / "fresh", base / "held"
+    for d in (old / "sub", fresh, held, base / ".tritondl-spare-1"):
+        os.makedirs(d)
+    (old / "sub" / "part.mkv").write_bytes(b"x")
+    (held / "f.mkv").write_bytes(b"y")
+    t_old = time.time() - 10 * 86400
+    for p in (old / "sub" / "part.mkv", old / "sub", old, held / "f.mkv", held):
+        os.utime(p, (t_old, t_old))
+    dead = subprocess.Popen(["true"])
+    dead.wait()
+    os.makedirs(base / f"gone.deleting-{dead.pid}-abc")
+    os.makedirs(base / f"busy.deleting-{os.getpid()}-abc")
+    fd = os.open(held, os.O_RDONLY | os.O_DIRECTORY)
+    fcntl.flock(fd, fcntl.LOCK_EX)
+    try:
+        out = sweep_stale_job_dirs(str(base), 7 * 86400)
+    finally:
+        os.close(fd)
+    names = sorted(os.path.basename(p) for p in out)
+    assert names == [f"gone.deleting-{dead.pid}-abc", f"old.deleting-{os.getpid()}-stale"]
+    assert not old.exists() and fresh.exists() and held.exists() and (base / ".tritondl-spare-1").exists()
+    assert (base / f"busy.deleting-{os.getpid()}-abc").exists()
+    for p in out:                                    # the reaper's part
+        shutil.rmtree(p)
+    # the lock released, the held dir is taken on the next sweep
+    assert [os.path.basename(p) for p in sweep_stale_job_dirs(str(base), 7 * 86400)] == \
+        [f"held.deleting-{os.getpid()}-stale"]
+
+
+def test_service_sweeps_stale_job_dirs_at_start(tmp_path):
+    async def main():
+        base = tmp_path / "downloading"
+        os.makedirs(base / "ancient")
+        t_old = time.time() - 30 * 86400
+        os.utime(base / "ancient", (t_old, t_old))
+        e = await Env().up(tmp_path, cleanup=True, stale_job_days=7.0)
+        for _ in range(100):
+            if not any(n.startswith("ancient") for n in os.listdir(base)):
+                break
+            await asyncio.sleep(0.02)
+        assert not any(n.startswith("ancient") for n in os.listdir(base))
         await e.down()
     run(main())

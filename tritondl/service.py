@@ -185,6 +185,83 @@ class _Reaper:
         return done.wait(timeout)
 
 
+def _newest_mtime(d: str, limit: int = 10000) -> float:
+    """Newest mtime of ``d`` and anything under it (at most ``limit`` entries)."""
+    newest = os.lstat(d).st_mtime
+    n = 0
+    for root, dirs, files in os.walk(d):
+        for name in dirs + files:
+            n += 1
+            if n > limit:
+                return newest
+            try:
+                newest = max(newest, os.lstat(os.path.join(root, name)).st_mtime)
+            except OSError:
+                pass
+    return newest
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset = frozenset(),
+                         now: float | None = None) -> list[str]:
+    """Job dirs under ``base`` that nothing has touched for ``max_age_s``, and
+    half-deleted ``*.deleting-<pid>-*`` dirs whose worker is gone, renamed
+    aside for deletion; returns the new paths.  A job dir some worker holds
+    (``flock``, :meth:`Service._job_lock`) is never taken.  These are the
+    partial downloads of jobs that will not come back: their message was
+    purged, or another node finished them.  The reference's work dir only
+    ever grew."""
+    now = time.time() if now is None else now
+    out: list[str] = []
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for name in names:
+        path = os.path.join(base, name)
+        if path in skip or name.startswith("."):
+            continue                                  # spare pools (.tritondl-spare-*)
+        if ".deleting-" in name:
+            try:
+                pid = int(name.rsplit(".deleting-", 1)[1].split("-", 1)[0])
+            except ValueError:
+                continue
+            if not _pid_alive(pid):
+                out.append(path)                      # its reaper died with it
+            continue
+        try:
+            fd = os.open(path, os.O_RDONLY | os.O_DIRECTORY)
+        except OSError:
+            continue
+        try:
+            try:
+                fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+            except BlockingIOError:
+                continue                              # a job is running in it
+            if now - _newest_mtime(path) < max_age_s:
+                continue
+            trash = f"{path}.deleting-{os.getpid()}-stale"
+            try:
+                os.rename(path, trash)
+            except OSError:
+                continue
+            out.append(trash)
+        except OSError:
+            continue
+        finally:
+            os.close(fd)
+    return out
+
+
 class Service:
     def __init__(self, cfg: Config, *, amqp: Client | None = None, dispatcher: Dispatcher | None = None,
                  uploader: Uploader | None = None, metrics: Metrics | None = None) -> None:
@@ -199,6 +276,7 @@ class Service:
         self._inflight = 0
         self._metrics_runner = None
         self._trimmer: asyncio.Task | None = None
+        self._janitor: asyncio.Task | None = None
         self.malloc_policy: dict = {}              # what tune_malloc applied at start
         self._reaper = _Reaper()                    # deletes finished job dirs off the loop
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
@@ -379,8 +457,29 @@ class Service:
         await self.amqp.consume(cfg.consume_topic)
         if cfg.malloc_trim_s > 0:
             self._trimmer = asyncio.ensure_future(self._trim_heap(cfg.malloc_trim_s))
+        if cfg.cleanup and cfg.stale_job_days > 0:
+            self._janitor = asyncio.ensure_future(self._sweep_stale(cfg.stale_job_days * 86400.0))
         for i in range(max(1, cfg.concurrency)):
             self._workers.append(asyncio.ensure_future(self._worker(i)))
+
+    async def _sweep_stale(self, max_age_s: float, period: float = 3600.0) -> None:
+        """At start and every ``period`` s: delete job dirs untouched for
+        ``max_age_s`` that no worker holds (:func:`sweep_stale_job_dirs`)."""
+        loop = asyncio.get_running_loop()
+        assert self.dispatcher is not None
+        base = self.dispatcher.base_dir
+        while True:
+            try:
+                gone = await loop.run_in_executor(None, sweep_stale_job_dirs, base, max_age_s,
+                                                  frozenset(self._locked_dirs))
+                for p in gone:
+                    self._reaper.submit(p)
+                if gone:
+                    log.with_fields(dirs=len(gone)).info("removed stale job dirs")
+                    self.metrics.inc("stale_job_dirs_removed", len(gone))
+            except Exception as e:  # noqa: BLE001 - housekeeping must not end the worker
+                log.with_field("error", str(e)).warn("stale job dir sweep failed")
+            await asyncio.sleep(period)
 
     async def _trim_heap(self, period: float) -> None:
         """Give glibc's free arena memory back to the OS every ``period`` s.
@@ -914,8 +1013,9 @@ class Service:
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
         self._stop.set()
-        if self._trimmer is not None:
-            self._trimmer.cancel()
+        for t in (self._trimmer, self._janitor):
+            if t is not None:
+                t.cancel()
         t_end = time.monotonic() + grace
         if self._workers:
             done, pending = await asyncio.wait(self._workers, timeout=grace)

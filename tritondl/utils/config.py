@@ -59,7 +59,7 @@ ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_time
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
               "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s",
-              "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms"}
+              "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms", "STALE_JOB_DAYS": "stale_job_days"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -148,6 +148,10 @@ class Config:
     # consuming.  A full collection otherwise walks all of them on the event loop: 40-100 ms,
     # a stall in the middle of a job and of the heartbeats (Service.start)
     gc_freeze: bool = True
+    # with cleanup on: job dirs nothing has touched for this many days and no worker holds
+    # (partial downloads of jobs whose message was purged or finished elsewhere) are
+    # deleted, at start and hourly; 0 = never (the reference's work dir only grew)
+    stale_job_days: float = 7.0
     # a delivery whose job dir another worker holds waits this long, then goes back to
     # the broker (same X-Retries) instead of pinning the job slot
     job_lock_wait_s: float = 60.0
