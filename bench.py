@@ -208,6 +208,21 @@ def _lease_state() -> dict:
     return out
 
 
+def _trace_p50(events: list) -> dict:
+    """p50 offset (ms) of each data-plane event from its job's ``job_start``
+    (``TRITONDL_TRACE=1``; meaningful at concurrency 1, where a job's events
+    follow its start)."""
+    per: dict[str, list[float]] = {}
+    start = None
+    for name, t in events:
+        if name == "job_start":
+            start = t
+            continue
+        if start is not None:
+            per.setdefault(name, []).append((t - start) * 1000)
+    return {k: round(sorted(v)[len(v) // 2], 3) for k, v in sorted(per.items(), key=lambda kv: sorted(kv[1])[0])}
+
+
 def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_size: int) -> list[int]:
     """Pin this rank's process (inherited by every native thread and by the
     fakes it spawns) before anything starts, and choose the fakes' set.
@@ -455,6 +470,9 @@ def main() -> int:
         cpu0 = stack.cpu_seconds()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
         gc0 = [g["collections"] for g in gc.get_stats()]
+        from tritondl.utils import rawhttp as _rh
+        if _rh.TRACE is not None:
+            _rh.TRACE.clear()               # TRITONDL_TRACE=1: data-plane events of the timed jobs only
         t0 = time.perf_counter()
         if shared:
             loop.run_until_complete(phase(a.steps))
@@ -506,6 +524,7 @@ def main() -> int:
                 # CPython collections per generation inside the timed region (the worker
                 # froze its start-up heap: Service.start -> freeze_startup_heap)
                 "gc_collections": {f"gen{i}": b - a for i, (a, b) in enumerate(zip(gc0, gc1))},
+                **({"trace_p50_ms": _trace_p50(_rh.TRACE)} if _rh.TRACE else {}),
                 "gc_frozen": gc.get_freeze_count(),
                 "work_fs": _work_fs(stack)}
         spans: dict[str, list[float]] = {}

@@ -787,6 +787,7 @@ class S3Client:
                         1 if m == "streaming" else 0, signed.key if signed else b"", amzdate,
                         signed.scope if signed else "", signed.signature if signed else "", sigv4.STREAM_CHUNK,
                         self.sign_threads, 300.0, self._chunk_gpu() if m == "streaming" else None)
+                    rawhttp.trace("put_sent")
                     if perr and ("source" in perr or perr == "cancelled"):
                         raise S3Error(0, "SourceFailed", perr, f"PUT {path}")
                     try:
