@@ -1153,6 +1153,15 @@ inline size_t zc_tail_pairs() {
   static const size_t n = zc_env_chunks("TRITONDL_SHA_MB_TAIL", 32);
   return n;
 }
+// Frames per writev when the file is mapped (TRITONDL_ZC_WRITE_BATCH; 0/1 =
+// a header send + a sendfile per frame).  A sender that fell behind the
+// hashers sends every ready frame in one syscall: the 10 MiB headline job
+// ran 361.6 vs 342.9 jobs/s (mean of 7 alternated runs each, 16 vs
+// sendfile; 64 was no better than 16), profiles/r05_batch_ab/.
+inline size_t zc_write_batch() {
+  static const size_t n = zc_env_chunks("TRITONDL_ZC_WRITE_BATCH", 16);
+  return n;
+}
 
 // send_chunked_zc: the aws-chunked body over a PLAIN socket with no payload
 // copy through user space.  send_chunked reads every chunk into a ring
@@ -1320,7 +1329,11 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
 
   std::string head;
   char hx[32];
+  const size_t batch = map ? zc_write_batch() : 0;
+  std::vector<std::string> heads;
+  std::vector<struct iovec> iov;
   for (size_t c = 0; c < n && r.err.empty(); ++c) {
+    size_t avail = 1;  // chunks from c on whose digests are ready
     {
       std::unique_lock<std::mutex> l(mu);
       sender_wants = c;
@@ -1337,6 +1350,33 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
         r.err = worker_err;
         break;
       }
+      while (batch > 1 && avail < batch && c + avail < n && ready[c + avail]) ++avail;
+    }
+    if (batch > 1) {
+      // every ready frame in one writev from the mapping: headers and payloads
+      // interleaved, one syscall per batch instead of two per 64 KiB frame
+      heads.assign(avail, std::string());
+      iov.clear();
+      uint64_t bytes = 0;
+      for (size_t k = 0; k < avail; ++k) {
+        const size_t cc = c + k;
+        const uint64_t a = off + static_cast<uint64_t>(cc) * chunk;
+        const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(cc) * chunk));
+        std::snprintf(hx, sizeof hx, "%zx", m);
+        std::string& h = heads[k];
+        h.assign(cc ? "\r\n" : "");
+        h += hx;
+        h += ";chunk-signature=";
+        h += signer.next(tritondl_hash::hex_raw(dig[cc].data(), 32));
+        h += "\r\n";
+        iov.push_back({h.data(), h.size()});
+        iov.push_back({const_cast<char*>(map + (a - base)), m});
+        bytes += m;
+      }
+      if (!writev_all(io, iov, idle_timeout, flow, &r.err)) break;
+      r.sent += bytes;
+      c += avail - 1;
+      continue;
     }
     const uint64_t a = off + static_cast<uint64_t>(c) * chunk;
     const size_t m = static_cast<size_t>(std::min<uint64_t>(chunk, length - static_cast<uint64_t>(c) * chunk));
