@@ -61,7 +61,7 @@ def test_chaos_soak_every_job_lands(tmp_path, seed):
             broker.inject("v1.download", f"v1.download-{i % 2}", body, Properties(delivery_mode=2))
 
         stop = asyncio.Event()
-        fired = {"drop": 0, "nack": 0, "block": 0, "s3": 0, "cut": 0}
+        fired = {"drop": 0, "nack": 0, "block": 0, "s3": 0, "cut": 0, "unbind": 0, "complete200": 0}
 
         async def chaos():
             while not stop.is_set():
@@ -78,6 +78,12 @@ def test_chaos_soak_every_job_lands(tmp_path, seed):
                     broker.set_blocked(False)
                 elif f == "s3":
                     s3.fail_next(2, 503)
+                elif f == "unbind":
+                    # v1.convert's binding removed: publishes come back (mandatory) and the
+                    # worker binds the queue again instead of losing the Convert
+                    broker.unbind_queue(f"v1.convert-{rng.randrange(2)}")
+                elif f == "complete200":
+                    s3.complete_error_200 = 1        # S3's 200-with-<Error> CompleteMultipartUpload
                 else:
                     origin.cut_after, origin.cut_times = 200_000, 1
         chaos_task = asyncio.ensure_future(chaos())

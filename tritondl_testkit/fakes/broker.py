@@ -388,6 +388,17 @@ class Broker:
             ex.bindings = [b for b in ex.bindings if b[0] != name]
         return len(q.messages)
 
+    def unbind_queue(self, name: str) -> int:
+        """Remove every binding of queue ``name`` (an operator's mistake, a
+        policy change): publishes routed to it are unroutable until someone
+        binds it again; its messages stay.  Returns the bindings removed."""
+        n = 0
+        for ex in self.exchanges.values():
+            keep = [b for b in ex.bindings if b[0] != name]
+            n += len(ex.bindings) - len(keep)
+            ex.bindings = keep
+        return n
+
     def pause_delivery(self, paused: bool) -> None:
         """Fault injection: consumers stay registered but get nothing (a stuck
         queue process); resuming dispatches what queued up meanwhile."""
