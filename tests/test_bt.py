@@ -6,6 +6,7 @@ import asyncio
 import hashlib
 import os
 import shutil
+import time
 
 import pytest
 
@@ -820,3 +821,29 @@ def test_corrupter_sharing_pieces_with_an_honest_peer_is_banned_never_the_honest
     res = run(main(), timeout=240)
     print("(banned, shared failures) per swarm:", res)
     assert any(s for _b, s in res), res                        # pieces really were shared
+
+
+@pytest.mark.parametrize("lie", ["data", "size"])
+def test_metadata_from_a_lying_peer_does_not_stall_the_job(tmp_path, lie):
+    """BEP 9 metadata comes from untrusted peers.  One that serves metadata
+    not matching the info-hash (flipped bytes, or another announced size) is
+    found out: a sole contributor is never asked again, several are asked one
+    at a time, and the size is re-chosen from the other peers.  The job gets
+    its metadata from the honest peer instead of failing every assembly until
+    the metadata timeout."""
+    async def main():
+        src = tmp_path / "src"
+        make_payload(str(src), {"big.mkv": 14 << 20})
+        info = torrent_for(str(src / "big.mkv"), 16384)            # > 16 KiB of metadata: 2 pieces
+        assert len(info.raw) > 16384
+        liar = await Seeder(info, str(src), lie_metadata=lie).start()
+        honest = await Seeder(info, str(src)).start()
+        dst = tmp_path / "job"
+        os.makedirs(dst)
+        t0 = time.monotonic()
+        await _dl().download(str(dst), Sink(), magnet_for(info, peers=[liar.addr, honest.addr]))
+        assert (dst / "big.mkv").read_bytes() == (src / "big.mkv").read_bytes()
+        assert time.monotonic() - t0 < 30
+        await liar.stop()
+        await honest.stop()
+    run(main())

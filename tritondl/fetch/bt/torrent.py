@@ -24,6 +24,7 @@ WaitAll, Close), implemented from the BEPs:
 from __future__ import annotations
 
 import asyncio
+import collections
 import contextlib
 import errno
 import functools
@@ -155,6 +156,7 @@ class _Peer:
         self.wants = 0                                      # pieces it has that we lack
         self.downloaded = 0
         self.meta_requested = False
+        self.meta_asked_at = 0.0
         self.link = None                                    # _btwire.Link once the native data plane runs
         self.rx: pw.LinkReader | None = None                # zero-copy receive into the link (plain TCP)
         self.rx_tried = False
@@ -243,6 +245,12 @@ class Torrent:
         self._downloading = False
         self._meta_size: int | None = None
         self._meta: dict[int, bytes] = {}
+        # BEP 9 metadata from untrusted peers: which peer sent each piece, peers whose
+        # metadata failed the info-hash (never asked again), and one-source mode after a
+        # failure with several contributors (the next failure then names its culprit)
+        self._meta_src: dict[int, tuple] = {}
+        self._meta_bad: set = set()
+        self._meta_single = False
         self._tasks: set[asyncio.Task] = set()
         self._server: asyncio.AbstractServer | None = None
         self._server6: asyncio.AbstractServer | None = None
@@ -1554,7 +1562,8 @@ class Torrent:
             if p.listen_addr is None and p.ext.port and 0 < p.ext.port < 65536:
                 p.listen_addr = (p.addr[0], p.ext.port)
             if self.info is None and "ut_metadata" in p.ext.m and p.ext.metadata_size:
-                if self._meta_size is None and 0 < p.ext.metadata_size < 16 * 1024 * 1024:
+                if self._meta_size is None and p.key not in self._meta_bad and \
+                        0 < p.ext.metadata_size < 16 * 1024 * 1024:
                     self._meta_size = p.ext.metadata_size
                 self._request_metadata(p)
             return
@@ -1581,8 +1590,10 @@ class Torrent:
                     p.wire.extended(their, pw.meta_msg(pw.META_DATA, piece, len(raw),
                                                        raw[piece * BLOCK:(piece + 1) * BLOCK]))
             elif t == pw.META_DATA and self.info is None and isinstance(piece, int) and self._meta_size \
-                    and 0 <= piece < -(-self._meta_size // BLOCK) and len(data) <= BLOCK:
+                    and 0 <= piece < -(-self._meta_size // BLOCK) and len(data) <= BLOCK \
+                    and p.key not in self._meta_bad and d.get(b"total_size", self._meta_size) == self._meta_size:
                 self._meta[piece] = data        # only pieces of the announced size: bounded memory
+                self._meta_src[piece] = p.key
                 self._check_metadata()
             elif t == pw.META_REJECT:
                 p.meta_requested = False
@@ -1590,10 +1601,20 @@ class Torrent:
     def _request_metadata(self, p: _Peer) -> None:
         if self.info is not None or not self._meta_size or p.meta_requested or not p.ext:
             return
+        if p.key in self._meta_bad or p.ext.metadata_size != self._meta_size:
+            return                          # a peer that lied, or one announcing other metadata
         their = p.ext.m.get("ut_metadata")
         if not their:
             return
+        if self._meta_single:
+            now = time.monotonic()
+            for q in self.peers.values():
+                if q is not p and q.meta_requested and now - q.meta_asked_at > 15.0:
+                    q.meta_requested = False      # a silent source does not hold the others back
+            if any(q.meta_requested for q in self.peers.values() if q is not p):
+                return                      # one source at a time until the culprit is known
         p.meta_requested = True
+        p.meta_asked_at = time.monotonic()
         for k in range(-(-self._meta_size // BLOCK)):
             if k not in self._meta:
                 p.wire.extended(their, pw.meta_msg(pw.META_REQUEST, k))
@@ -1606,18 +1627,36 @@ class Torrent:
             return
         raw = b"".join(self._meta[k] for k in range(n))[:self._meta_size]
         if hashlib.sha1(raw).digest() != self.infohash and hashlib.sha256(raw).digest()[:20] != self.infohash:
-            log.warn("received metadata does not match info-hash; retrying")
-            self._meta.clear()
-            for p in self.peers.values():
-                p.meta_requested = False
+            self._metadata_failed("received metadata does not match info-hash")
             return
         try:
             info = Info.parse(raw)
         except MetainfoError as e:
-            log.warn("bad metadata: %s", e)
-            self._meta.clear()
+            self._metadata_failed(f"bad metadata: {e}")
             return
         self._set_info(info)
+
+    def _metadata_failed(self, why: str) -> None:
+        """Assembled metadata failed the info-hash.  A sole contributor lied:
+        it is never asked again (anacrolix drops such a peer).  Several: the
+        pieces are fetched again one peer at a time, so the next failure has
+        one contributor.  The size to assemble is re-chosen from the peers not
+        known to lie (the liar may be the one whose size was taken)."""
+        srcs = set(self._meta_src.values())
+        if len(srcs) == 1:
+            self._meta_bad |= srcs
+        else:
+            self._meta_single = True
+        log.with_fields(contributors=len(srcs), liars=len(self._meta_bad)).warn("%s; retrying", why)
+        self._meta.clear()
+        self._meta_src.clear()
+        sizes = collections.Counter(q.ext.metadata_size for q in self.peers.values()
+                                    if q.ext and q.key not in self._meta_bad and "ut_metadata" in q.ext.m
+                                    and q.ext.metadata_size and 0 < q.ext.metadata_size < 16 * 1024 * 1024)
+        self._meta_size = sizes.most_common(1)[0][0] if sizes else None
+        for q in self.peers.values():
+            q.meta_requested = False
+            self._request_metadata(q)
         for p in self.peers.values():
             pend = getattr(p, "pending_bitfield", None)
             if pend is not None:

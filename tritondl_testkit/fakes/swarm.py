@@ -166,12 +166,26 @@ class DHTNetwork:
             nd.stop()
 
 
+class _LyingInfo:
+    """An Info whose raw info-dict (what BEP 9 serves and announces the size
+    of) is not the one that hashes to the info-hash."""
+
+    def __init__(self, info: Info, raw: bytes) -> None:
+        self._info = info
+        self.raw = raw
+
+    def __getattr__(self, k):
+        return getattr(self._info, k)
+
+
 class Seeder:
-    """Seed an existing file/dir: serves pieces to any peer that connects."""
+    """Seed an existing file/dir: serves pieces to any peer that connects.
+    ``lie_metadata``: "data" serves flipped metadata bytes of the right
+    size, "size" announces and serves metadata of another size."""
 
     def __init__(self, info: Info, data_dir: str, *, trackers: list[str] | None = None,
                  dht_bootstrap: list[tuple[str, int]] | None = None, corrupt: bool = False,
-                 encryption: str = "allow", listen_host6: str | None = None) -> None:
+                 encryption: str = "allow", listen_host6: str | None = None, lie_metadata: str = "") -> None:
         self.info = info
         self.data_dir = data_dir
         self.trackers = trackers or []
@@ -179,6 +193,7 @@ class Seeder:
         self.corrupt = corrupt
         self.encryption = encryption
         self.listen_host6 = listen_host6
+        self.lie_metadata = lie_metadata
         self.torrent: Torrent | None = None
         self.dht: DHTNode | None = None
 
@@ -199,6 +214,10 @@ class Seeder:
                 data = t.storage.read(i, off, n)
                 p.wire.piece(i, off, bytes(x ^ 0xFF for x in data))
             t._on_request = bad  # type: ignore[assignment]
+        if self.lie_metadata:
+            raw = self.info.raw
+            bad_raw = bytes(x ^ 0x5A for x in raw) if self.lie_metadata == "data" else raw + b"x" * 40000
+            t.info = _LyingInfo(t.info, bad_raw)  # type: ignore[assignment]
         self.torrent = t
         return self
 
