@@ -1635,6 +1635,16 @@ class Torrent:
             self._metadata_failed(f"bad metadata: {e}")
             return
         self._set_info(info)
+        for p in self.peers.values():
+            pend = getattr(p, "pending_bitfield", None)
+            if pend is not None:
+                try:
+                    self._peer_has(p, sorted(pw.bits_to_set(pend, info.num_pieces)))
+                except pw.PeerError:
+                    p.wire.close()           # its early bitfield does not fit the torrent: drop it
+                    continue
+            if getattr(p, "pending_have_all", False):
+                self._peer_has(p, range(info.num_pieces))
 
     def _metadata_failed(self, why: str) -> None:
         """Assembled metadata failed the info-hash.  A sole contributor lied:
@@ -1657,13 +1667,3 @@ class Torrent:
         for q in self.peers.values():
             q.meta_requested = False
             self._request_metadata(q)
-        for p in self.peers.values():
-            pend = getattr(p, "pending_bitfield", None)
-            if pend is not None:
-                try:
-                    self._peer_has(p, sorted(pw.bits_to_set(pend, info.num_pieces)))
-                except pw.PeerError:
-                    p.wire.close()           # its early bitfield does not fit the torrent: drop it
-                    continue
-            if getattr(p, "pending_have_all", False):
-                self._peer_has(p, range(info.num_pieces))
