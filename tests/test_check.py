@@ -61,3 +61,22 @@ def test_preflight_cli_fails_on_an_unusable_endpoint(tmp_path):
     assert doc["ok"] is False
     assert any(i["area"] == "s3" and i["status"] == "fail" and "unusable" in i["detail"] for i in doc["checks"])
     assert any(i["area"] == "native" and i["status"] == "ok" for i in doc["checks"])
+
+
+def test_preflight_warns_about_a_skewed_clock(tmp_path, monkeypatch):
+    """S3's clock two hours ahead: the bucket check still passes (the client
+    re-dates its requests) and the report says how far off the host is."""
+    async def main():
+        s3 = await FakeS3(access_key="ak", secret_key="sk").start()
+        s3.create_bucket("triton-staging")
+        s3.clock_offset = 7200.0
+        try:
+            _env(monkeypatch, tmp_path, "127.0.0.1:1", s3.endpoint)
+            r = await check.run([], timeout=5, skip_broker=True)
+            s3_items = [i for i in r.items if i["area"] == "s3"]
+            assert any(i["status"] == "ok" and "exists" in i["detail"] for i in s3_items), s3_items
+            skew = [i for i in s3_items if i["status"] == "warn" and "clock" in i["detail"]]
+            assert skew and abs(skew[0]["skew_s"] - 7200) < 5
+        finally:
+            await s3.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))

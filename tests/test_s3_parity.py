@@ -337,15 +337,19 @@ def test_clock_skew_is_learned_from_request_time_too_skewed(tmp_path, offset):
         s3.clock_offset = offset
         c = S3Client(s3.endpoint, Static("ak", "sk"), region="us-east-1", max_retries=0,
                      part_size=5 << 20, multipart_threshold=5 << 20)
+        # the uploader's first request is a HEAD bucket: its 403 has no body, S3's Date tells
+        h = S3Client(s3.endpoint, Static("ak", "sk"), region="us-east-1", max_retries=0)
+        assert await h.bucket_exists("b") and abs(h.clock_skew - offset) < 5 and s3.skew_refusals == 1
+        await h.close()
         await c.put_object("b", "small", b"x" * 1000)
-        assert abs(c.clock_skew - offset) < 5 and s3.skew_refusals == 1
+        assert abs(c.clock_skew - offset) < 5 and s3.skew_refusals == 2
         small = tmp_path / "s.bin"
         small.write_bytes(os.urandom(300_000))
         big = tmp_path / "b.bin"
         big.write_bytes(os.urandom((11 << 20) + 3))
         await c.put_object("b", "file", str(small))
         await c.put_object("b", "multi", str(big))
-        assert s3.object_bytes("b", "multi") == big.read_bytes() and s3.skew_refusals == 1
+        assert s3.object_bytes("b", "multi") == big.read_bytes() and s3.skew_refusals == 2
         # a fresh client learns it on the native PUT path too
         c2 = S3Client(s3.endpoint, Static("ak", "sk"), region="us-east-1", max_retries=0)
         await c2.put_object("b", "file2", str(small))
@@ -369,7 +373,12 @@ def test_server_time_parsing():
     e = _parse_error(403, b"<Error><Code>RequestTimeTooSkewed</Code></Error>", "PUT /b/k",
                      {"Date": "Sun, 18 Oct 2026 02:40:49 GMT"})
     assert e.server_time == 1792291249.0
-    assert _parse_error(403, b"<Error><Code>AccessDenied</Code></Error>", "x").server_time is None
+    assert _parse_error(404, b"<Error><Code>NoSuchKey</Code></Error>", "x").server_time is None
+    # a genuine 403 from a server whose clock agrees is not taken for skew
+    from tritondl.s3.client import S3Client
+    c = S3Client("http://127.0.0.1:9", Static("ak", "sk"))
+    now = __import__("email.utils").utils.formatdate(usegmt=True)
+    assert not c._learn_skew(_parse_error(403, b"", "HEAD /b", {"Date": now})) and c.clock_skew == 0.0
 
 
 def test_stale_resume_state_starts_over(tmp_path):

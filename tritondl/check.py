@@ -190,6 +190,9 @@ async def check_s3(cfg: Config, r: Report, timeout: float) -> None:
         exists = await asyncio.wait_for(client.bucket_exists(cfg.bucket), timeout)
         r.add("s3", OK if exists else WARN, f"bucket {cfg.bucket} " +
               ("exists" if exists else "does not exist yet: the worker creates it (MakeBucket, region \"\")"))
+        if client.clock_skew:
+            r.add("s3", WARN, f"this host's clock is {client.clock_skew:+.0f} s off S3's: the worker signs on "
+                  "S3's clock after its first refused request, but fix the host's time sync", skew_s=client.clock_skew)
     except (S3Error, OSError, asyncio.TimeoutError) as e:
         r.add("s3", FAIL, f"HEAD bucket {cfg.bucket} failed: {e}")
     finally:

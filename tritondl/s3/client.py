@@ -114,7 +114,8 @@ def _parse_error(status: int, body: bytes, resource: str, headers=None) -> S3Err
         code = {301: "PermanentRedirect", 400: "BadRequest", 403: "AccessDenied", 404: "NoSuchBucket" if
                 resource.count("/") <= 1 and "?" not in resource else "NoSuchKey"}.get(status, "")
     err = S3Error(status, code, msg, resource, region)
-    if code == "RequestTimeTooSkewed":
+    if code == "RequestTimeTooSkewed" or status in (401, 403):
+        # a HEAD's 403 has no body to name the skew: S3's Date header still tells its clock
         err.server_time = _server_time(stime, (headers.get("Date", "") or "") if headers is not None else "")
     return err
 
@@ -404,13 +405,17 @@ class S3Client:
 
     def _learn_skew(self, err: S3Error) -> bool:
         """True when S3 refused the request as signed too far from its clock
-        (RequestTimeTooSkewed, > 15 min) and named its time: later requests
-        are dated on S3's clock and the caller re-signs without counting a
-        try.  AWS SDKs correct skew this way; minio-go did not, so a worker
-        on a drifted node failed every upload."""
-        if err.code != "RequestTimeTooSkewed" or err.server_time is None:
+        and told its time: RequestTimeTooSkewed (> 15 min) with
+        ``<ServerTime>``, or any 401/403 whose ``Date`` header is more than
+        4 minutes off (a HEAD's 403 has no body; the AWS SDKs' clock-skew
+        adjuster uses the same rule).  Later requests are dated on S3's clock
+        and the caller re-signs without counting a try.  minio-go did not
+        correct skew, so a worker on a drifted node failed every upload."""
+        if err.server_time is None:
             return False
         skew = err.server_time - time.time()
+        if err.code != "RequestTimeTooSkewed" and abs(skew) < 240.0:
+            return False                    # a 403 from a server whose clock agrees: a real refusal
         if abs(skew - self.clock_skew) < 2.0:
             return False                    # already dated on S3's clock: something else is wrong
         log.with_fields(skew_s=round(skew, 1)).warn("host clock differs from S3's; signing on S3's clock")
