@@ -561,3 +561,21 @@ def test_deleted_delay_queue_is_declared_again_not_lost():
         await cl.close()
         await b.stop()
     run(main())
+
+
+def test_client_redeclares_a_deleted_publish_exchange():
+    """The v1.convert exchange is deleted under a running worker: the publish
+    is a 404 channel error; the client forgets it ever declared the topic,
+    declares it again on the retry, and the message lands."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        await cl.publish("v1.convert", b"first")
+        assert b.delete_exchange("v1.convert")
+        await cl.publish("v1.convert", b"second", max_attempts=4)
+        assert "v1.convert" in b.exchanges
+        got = [m.body for q in ("v1.convert-0", "v1.convert-1") for m in b.drain_queue(q)]
+        assert sorted(got) == [b"first", b"second"]
+        await cl.close()
+        await b.stop()
+    run(main())

@@ -848,6 +848,8 @@ class Client:
             except (AMQPError, ConnectionError, OSError) as e:
                 if attempt == max_attempts or self._closing or self._permanent(exchange, e):
                     raise
+                if isinstance(e, ChannelClosed) and e.code == codec.NOT_FOUND:
+                    self._declared_pub.discard(exchange)   # deleted since we declared it: declare again
                 d = pol.next_delay() or 0.0
                 log.with_fields(error=str(e), attempt=attempt).warn("publish failed; retrying in %.2fs", d)
                 await asyncio.sleep(d)

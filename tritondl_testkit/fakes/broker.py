@@ -388,6 +388,12 @@ class Broker:
             ex.bindings = [b for b in ex.bindings if b[0] != name]
         return len(q.messages)
 
+    def delete_exchange(self, name: str) -> bool:
+        """Delete an exchange from outside any connection (an operator's
+        ``rabbitmqctl``/management-UI delete): publishing to it is then a
+        404 channel error until someone declares it again."""
+        return self.exchanges.pop(name, None) is not None
+
     def unbind_queue(self, name: str) -> int:
         """Remove every binding of queue ``name`` (an operator's mistake, a
         policy change): publishes routed to it are unroutable until someone
