@@ -49,7 +49,7 @@ profile-gpu: build
 	  --output-format csv -- $(PYTHON) $(CURDIR)/tools/bench_hash.py --no-files
 
 lint:
-	$(PYTHON) -m compileall -q tritondl tritondl_testkit tests tools bench.py __graft_entry__.py
+	$(PYTHON) tools/lint.py
 
 docker-build:
 	DOCKER_BUILDKIT=1 docker build -t $(IMAGE) -f docker/Dockerfile .

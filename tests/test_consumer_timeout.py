@@ -9,10 +9,8 @@ broker redelivers it."""
 
 import asyncio
 import os
-import time
 
-from tritondl.amqp.codec import Properties
-from tritondl.models import Convert, Download, Media
+from tritondl.models import Media
 from tritondl.s3.uploader import object_key
 
 from .test_permissions import Env, run

@@ -75,3 +75,13 @@ def test_product_package_does_not_ship_or_import_the_harness():
     assert 'include = ["tritondl", "tritondl.*"]' in py
     df = open(os.path.join(ROOT, "docker", "Dockerfile")).read()
     assert "COPY --from=build /src/tritondl/tritondl /app/tritondl" in df and "tritondl_testkit" in df
+
+
+def test_lint_clean():
+    """tools/lint.py (compile + unused imports, standard library only) finds nothing."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "lint.py")], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr

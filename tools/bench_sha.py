@@ -14,7 +14,6 @@ line per (mode, threads).
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import subprocess
 import sys
