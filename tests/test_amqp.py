@@ -579,3 +579,22 @@ def test_client_redeclares_a_deleted_publish_exchange():
         await cl.close()
         await b.stop()
     run(main())
+
+
+def test_connection_names_its_worker_process():
+    """client_properties.connection_name: the management UI shows which
+    worker process on which host holds a connection."""
+    import os
+    import socket
+
+    async def main():
+        b = await Broker().start()
+        conn = await Connection.open(b.url)
+        props = next(iter(b.conns)).client_properties
+        name = props["connection_name"]
+        name = name.decode() if isinstance(name, bytes) else name
+        assert name == f"tritondl@{socket.gethostname()} pid {os.getpid()}"
+        assert props["capabilities"]["publisher_confirms"] is True
+        await conn.close()
+        await b.stop()
+    run(main())

@@ -217,9 +217,12 @@ def test_client_handshake_and_first_frames_against_scripted_peer():
         srv.close()
 
     asyncio.run(asyncio.wait_for(main(), 20))
+    import os
+    import socket
     props = {"product": "tritondl", "version": "0.1", "platform": "python-asyncio",
              "capabilities": {"publisher_confirms": True, "consumer_cancel_notify": True, "basic.nack": True,
-                              "connection.blocked": True, "authentication_failure_close": True}}
+                              "connection.blocked": True, "authentication_failure_close": True},
+             "connection_name": f"tritondl@{socket.gethostname()} pid {os.getpid()}"}
     start_ok = H("000a 000b") + tbl(props) + b"\x05PLAIN" + H("0000000c") + b"\x00guest\x00guest" + b"\x05en_US"
     # tune-ok echoes the negotiated values: channel_max 2047, frame_max 131072, heartbeat min(60, 60)
     expect = (H("414d515000000901")

@@ -15,8 +15,9 @@ from __future__ import annotations
 import asyncio
 import dataclasses
 import inspect
-import os
 import itertools
+import os
+import socket
 import ssl
 import struct
 import time
@@ -208,7 +209,10 @@ class Connection:
             props = {"product": "tritondl", "version": "0.1", "platform": "python-asyncio",
                      "capabilities": {"publisher_confirms": True, "consumer_cancel_notify": True,
                                       "basic.nack": True, "connection.blocked": True,
-                                      "authentication_failure_close": True}}
+                                      "authentication_failure_close": True},
+                     # shown by RabbitMQ's management UI and `rabbitmqctl list_connections
+                     # client_properties`: which worker process on which host holds the channel
+                     "connection_name": f"tritondl@{socket.gethostname()} pid {os.getpid()}"}
             props.update(self.client_properties)
             resp = b"\x00" + p.username.encode() + b"\x00" + p.password.encode()
             self._send_method(0, Method("connection.start_ok", {"client_properties": props, "mechanism": "PLAIN",
