@@ -880,12 +880,20 @@ def test_stale_job_dir_sweep(tmp_path):
     dead.wait()
     os.makedirs(base / f"gone.deleting-{dead.pid}-abc")
     os.makedirs(base / f"busy.deleting-{os.getpid()}-abc")
+    # a media id that merely looks like trash, with its job running: never taken
+    odd = base / f"id.deleting-{dead.pid}-x"
+    os.makedirs(odd)
     fd = os.open(held, os.O_RDONLY | os.O_DIRECTORY)
     fcntl.flock(fd, fcntl.LOCK_EX)
+    fd2 = os.open(odd, os.O_RDONLY | os.O_DIRECTORY)
+    fcntl.flock(fd2, fcntl.LOCK_EX)
     try:
         out = sweep_stale_job_dirs(str(base), 7 * 86400)
     finally:
         os.close(fd)
+        os.close(fd2)
+    assert odd.exists()
+    shutil.rmtree(odd)
     names = sorted(os.path.basename(p) for p in out)
     assert names == [f"gone.deleting-{dead.pid}-abc", f"old.deleting-{os.getpid()}-stale"]
     assert not old.exists() and fresh.exists() and held.exists() and (base / ".tritondl-spare-1").exists()

@@ -230,14 +230,14 @@ def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset
         path = os.path.join(base, name)
         if path in skip or name.startswith("."):
             continue                                  # spare pools (.tritondl-spare-*)
+        trash_pid = None
         if ".deleting-" in name:
             try:
-                pid = int(name.rsplit(".deleting-", 1)[1].split("-", 1)[0])
+                trash_pid = int(name.rsplit(".deleting-", 1)[1].split("-", 1)[0])
             except ValueError:
                 continue
-            if not _pid_alive(pid):
-                out.append(path)                      # its reaper died with it
-            continue
+            if _pid_alive(trash_pid):
+                continue                              # its worker's reaper is on it
         try:
             fd = os.open(path, os.O_RDONLY | os.O_DIRECTORY)
         except OSError:
@@ -246,7 +246,10 @@ def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset
             try:
                 fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
             except BlockingIOError:
-                continue                              # a job is running in it
+                continue                              # a job is running in it (whatever its name)
+            if trash_pid is not None:
+                out.append(path)                      # half-deleted; its reaper died with its worker
+                continue
             if now - _newest_mtime(path) < max_age_s:
                 continue
             trash = f"{path}.deleting-{os.getpid()}-stale"
