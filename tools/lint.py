@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Minimal static checks with the standard library only (no linters are
-installed in the build image): every file compiles, and no module imports a
-name it never uses.  ``__init__.py`` re-exports and names listed in
+installed in the build image): every file compiles, no module imports a
+name it never uses, and no function reads a global the module never binds.  ``__init__.py`` re-exports and names listed in
 ``__all__`` count as used; ``# noqa`` on the import line skips it.
 
     python tools/lint.py [paths...]        # exit 1 and one line per finding
@@ -76,6 +76,32 @@ def unused_imports(path: str, src: str) -> list[str]:
             if name not in used]
 
 
+def undefined_globals(path: str, src: str) -> list[str]:
+    """Names a function or class body reads as globals that the module never
+    binds and that are not builtins (a missing import, a typo): what a
+    NameError at run time would be.  From the compiler's own symbol tables."""
+    import builtins
+    import symtable
+    top = symtable.symtable(src, path, "exec")
+    bound = {s.get_name() for s in top.get_symbols() if s.is_assigned() or s.is_imported()
+             or s.is_namespace() or s.is_parameter()}
+    if any(s.get_name() == "*" for s in top.get_symbols()) or "__getattr__" in bound:
+        return []
+    known = bound | set(dir(builtins)) | {"__file__", "__name__", "__doc__", "__spec__", "__builtins__",
+                                          "__path__", "__package__", "__loader__", "__class__"}
+    out = []
+
+    def walk(t) -> None:
+        for c in t.get_children():
+            for sym in c.get_symbols():
+                if sym.is_referenced() and (sym.is_global() or sym.is_declared_global()) \
+                        and sym.get_name() not in known:
+                    out.append(f"{path}: '{sym.get_name()}' is used in {c.get_name()}() but never defined")
+            walk(c)
+    walk(top)
+    return sorted(set(out))
+
+
 def main(argv: list[str]) -> int:
     paths = argv or DEFAULT
     problems: list[str] = []
@@ -88,6 +114,7 @@ def main(argv: list[str]) -> int:
             problems.append(f"{f}:{e.lineno}: {e.msg}")
             continue
         problems += unused_imports(f, src)
+        problems += undefined_globals(f, src)
     for p in problems:
         print(os.path.relpath(p, ROOT) if p.startswith(ROOT) else p)
     return 1 if problems else 0
