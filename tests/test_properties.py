@@ -106,6 +106,46 @@ def test_amqp_table_garbage_raises_frame_error(b):
         pass
 
 
+def _known_method_prefix():
+    """A class/method id pair the codec knows, then arbitrary argument bytes."""
+    ids = sorted(codec.METHODS)
+    return st.builds(lambda k, tail: bytes(__import__("struct").pack(">HH", *ids[k % len(ids)])) + tail,
+                     st.integers(min_value=0, max_value=10 ** 6), st.binary(max_size=120))
+
+
+@SETTINGS
+@given(st.one_of(st.binary(max_size=120), _known_method_prefix()))
+def test_amqp_method_garbage_raises_only_amqp_errors(b):
+    """A broker (or a man in the middle) sending a malformed method frame:
+    the decoder returns a Method or raises AMQPError, nothing else
+    (IndexError, struct.error, UnicodeDecodeError would kill the reader)."""
+    try:
+        codec.decode_method(b)
+    except codec.AMQPError:
+        pass
+
+
+@SETTINGS
+@given(st.binary(max_size=200))
+def test_amqp_content_header_garbage_raises_only_amqp_errors(b):
+    try:
+        codec.decode_header(b)
+    except codec.AMQPError:
+        pass
+
+
+@SETTINGS
+@given(st.lists(st.binary(max_size=64), max_size=8))
+def test_amqp_frame_parser_garbage_raises_only_amqp_errors(chunks):
+    p = codec.FrameParser()
+    p.frame_max = 4096
+    try:
+        for c in chunks:
+            p.feed(c)
+    except codec.AMQPError:
+        pass
+
+
 @SETTINGS
 @given(st.binary(max_size=3000), st.integers(min_value=4096, max_value=8192),
        st.text(max_size=20), st.dictionaries(keys, st.integers(min_value=-5, max_value=5), max_size=3))
