@@ -195,6 +195,24 @@ class Flow {
     return got;
   }
 
+  // Bytes of [a, b) on disk contiguously from a (stops at the first gap).
+  uint64_t covered_prefix(uint64_t a, uint64_t b) const {
+    std::lock_guard<std::mutex> l(mu_);
+    if (b <= a) return 0;
+    if (finished_) return std::min(b, total_) > a ? std::min(b, total_) - a : 0;
+    uint64_t need = a;
+    for (;;) {
+      uint64_t best = need;
+      for (const Seg& s : segs_) {
+        const uint64_t s_end = s.end < 0 ? UINT64_MAX : static_cast<uint64_t>(s.end);
+        if (s.start > need || s_end <= need) continue;
+        best = std::max(best, std::min(s.start + s.done, s_end));
+      }
+      if (best <= need || best >= b) return std::min(best, b) - a;
+      need = best;
+    }
+  }
+
   // Length of the contiguous prefix on disk.
   uint64_t watermark() const {
     std::lock_guard<std::mutex> l(mu_);
@@ -851,9 +869,13 @@ inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, 
   }
   Buf buf(io.plain() || view ? 0 : static_cast<size_t>(std::min<uint64_t>(step, std::max<uint64_t>(length, 1))));
   while (r.sent < length) {
-    const uint64_t n = std::min(step, length - r.sent);
+    uint64_t n = std::min(step, length - r.sent);
     if (flow) {
-      const int w = flow->wait_covered(off + r.sent, off + r.sent + n, idle_timeout, io.abort_flag());
+      // follow the download closely: wait for a slice (not a whole 4 MiB step, which
+      // left up to 4 MiB to send after the last byte landed), then send everything
+      // already on disk from here, up to the step
+      const uint64_t slice = std::min<uint64_t>(n, 256u << 10);
+      const int w = flow->wait_covered(off + r.sent, off + r.sent + slice, idle_timeout, io.abort_flag());
       if (w) {
         r.err = io.aborted() ? "cancelled"
                 : w == 3     ? "source shorter than expected"
@@ -861,6 +883,7 @@ inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, 
                              : "source transfer failed: " + flow->error();
         return r;
       }
+      n = std::max(slice, std::min(n, flow->covered_prefix(off + r.sent, off + r.sent + n)));
     }
     if (!io.plain()) {  // TLS: the record layer needs the bytes in user space
       const size_t m = static_cast<size_t>(n);
