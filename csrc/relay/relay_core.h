@@ -1176,6 +1176,12 @@ inline size_t zc_tail_pairs() {
   static const size_t n = zc_env_chunks("TRITONDL_SHA_MB_TAIL", 32);
   return n;
 }
+// Streamed signed PUTs (a Flow): wide hash claims only over bytes already on
+// disk, pairs at the receive frontier (TRITONDL_SHA_MB_FOLLOW=0: by position).
+inline bool zc_follow() {
+  static const bool on = zc_env_chunks("TRITONDL_SHA_MB_FOLLOW", 1) != 0;
+  return on;
+}
 // Frames per writev when the file is mapped (TRITONDL_ZC_WRITE_BATCH; 0/1 =
 // a header send + a sendfile per frame).  A sender that fell behind the
 // hashers sends every ready frame in one syscall: the 10 MiB headline job
@@ -1267,14 +1273,24 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
   const size_t wide = gpu ? 0 : tritondl_hash::sha256_claim();
   const size_t per = gpu ? std::max<size_t>(1, gpu_batch) : wide;
   const size_t lead = flow ? zc_head_pairs() : 0, trail = zc_tail_pairs();
+  const bool follow = flow != nullptr && zc_follow();
   auto claim = [&](size_t* take) {
     if (gpu || wide <= 2) {
       *take = per;
       return next.fetch_add(per);
     }
     size_t i = next.load();
-    do *take = i >= lead && i + wide + trail <= n ? wide : 2;
-    while (!next.compare_exchange_weak(i, i + *take));
+    do {
+      bool w = i >= lead && i + wide + trail <= n;
+      if (w && follow) {
+        // a wide claim waits for all its bytes: take one only where the download
+        // has already landed them (a hasher catching up); at the receive frontier
+        // pairs keep each chunk's digest right behind its bytes
+        const uint64_t a = off + static_cast<uint64_t>(i) * chunk, span = static_cast<uint64_t>(wide) * chunk;
+        w = flow->covered_prefix(a, a + span) >= span;
+      }
+      *take = w ? wide : 2;
+    } while (!next.compare_exchange_weak(i, i + *take));
     return i;
   };
   auto hasher = [&] {

@@ -59,6 +59,9 @@ DIRECT = {
     "TRITONDL_SHA_MB": ("1", "hash/sha256_mb.h, hash/hash_host.cpp", "0: no 16-lane AVX-512 multi-buffer SHA"),
     "TRITONDL_SHA_MB_HEAD": ("0", "relay/relay_core.h", "chunks hashed one by one before the multi-buffer groups start"),
     "TRITONDL_SHA_MB_TAIL": ("32", "relay/relay_core.h", "chunks at a PUT's end hashed one by one (tail latency)"),
+    "TRITONDL_SHA_MB_FOLLOW": ("1", "relay/relay_core.h",
+                               "streamed signed PUT: 16-chunk hash claims only over bytes already downloaded "
+                               "(0: by position)"),
     "TRITONDL_ZC_WRITE_BATCH": ("16", "relay/relay_core.h",
                                 "signed plain-http PUT: ready frames per writev from the file mapping "
                                 "(0/1: a header send + sendfile per 64 KiB frame)"),
