@@ -185,20 +185,24 @@ class _Reaper:
         return done.wait(timeout)
 
 
-def _newest_mtime(d: str, limit: int = 10000) -> float:
-    """Newest mtime of ``d`` and anything under it (at most ``limit`` entries)."""
-    newest = os.lstat(d).st_mtime
+def _touched_since(d: str, cutoff: float, limit: int = 10000) -> bool:
+    """Whether ``d`` or anything under it was modified at or after ``cutoff``.
+    Stops at the first such entry; a tree of more than ``limit`` entries
+    counts as touched (a huge job is not worth walking to delete)."""
+    if os.lstat(d).st_mtime >= cutoff:
+        return True
     n = 0
     for root, dirs, files in os.walk(d):
         for name in dirs + files:
             n += 1
             if n > limit:
-                return newest
+                return True
             try:
-                newest = max(newest, os.lstat(os.path.join(root, name)).st_mtime)
+                if os.lstat(os.path.join(root, name)).st_mtime >= cutoff:
+                    return True
             except OSError:
                 pass
-    return newest
+    return False
 
 
 def _pid_alive(pid: int) -> bool:
@@ -250,7 +254,7 @@ def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset
             if trash_pid is not None:
                 out.append(path)                      # half-deleted; its reaper died with its worker
                 continue
-            if now - _newest_mtime(path) < max_age_s:
+            if _touched_since(path, now - max_age_s):
                 continue
             trash = f"{path}.deleting-{os.getpid()}-stale"
             try:
@@ -471,18 +475,28 @@ class Service:
         loop = asyncio.get_running_loop()
         assert self.dispatcher is not None
         base = self.dispatcher.base_dir
-        while True:
-            try:
-                gone = await loop.run_in_executor(None, sweep_stale_job_dirs, base, max_age_s,
-                                                  frozenset(self._locked_dirs))
-                for p in gone:
-                    self._reaper.submit(p)
-                if gone:
-                    log.with_fields(dirs=len(gone)).info("removed stale job dirs")
-                    self.metrics.inc("stale_job_dirs_removed", len(gone))
-            except Exception as e:  # noqa: BLE001 - housekeeping must not end the worker
-                log.with_field("error", str(e)).warn("stale job dir sweep failed")
-            await asyncio.sleep(period)
+        # its own thread: a walk over a large work dir must not hold a thread of the
+        # default executor that jobs use (dir_media, warm-ups)
+        pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tdl-janitor")
+        try:
+            while True:
+                await self._sweep_once(loop, pool, base, max_age_s)
+                await asyncio.sleep(period)
+        finally:
+            pool.shutdown(wait=False)
+
+    async def _sweep_once(self, loop, pool, base: str, max_age_s: float) -> None:
+        try:
+            gone = await loop.run_in_executor(pool, sweep_stale_job_dirs, base, max_age_s,
+                                              frozenset(self._locked_dirs))
+        except Exception as e:  # noqa: BLE001 - housekeeping must not end the worker
+            log.with_field("error", str(e)).warn("stale job dir sweep failed")
+            return
+        for p in gone:
+            self._reaper.submit(p)
+        if gone:
+            log.with_fields(dirs=len(gone)).info("removed stale job dirs")
+            self.metrics.inc("stale_job_dirs_removed", len(gone))
 
     async def _trim_heap(self, period: float) -> None:
         """Give glibc's free arena memory back to the OS every ``period`` s.
