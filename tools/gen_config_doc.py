@@ -62,6 +62,9 @@ DIRECT = {
     "TRITONDL_SHA_MB_FOLLOW": ("1", "relay/relay_core.h",
                                "streamed signed PUT: 16-chunk hash claims only over bytes already downloaded "
                                "(0: by position)"),
+    "TRITONDL_ZC_POPULATE": ("0", "relay/relay_core.h",
+                             "1: map a signed PUT's whole file mapping up front (MADV_POPULATE_READ) "
+                             "instead of a minor fault per page"),
     "TRITONDL_ZC_WRITE_BATCH": ("16", "relay/relay_core.h",
                                 "signed plain-http PUT: ready frames per writev from the file mapping "
                                 "(0/1: a header send + sendfile per 64 KiB frame)"),
