@@ -136,8 +136,11 @@ def _vm_snapshot() -> dict:
 
 
 def _vm_delta(v0: dict, v1: dict, n: int) -> dict:
-    """Per-job vmstat deltas plus the start/end Dirty and Writeback totals."""
+    """Per-job vmstat deltas plus the start/end Dirty and Writeback totals.
+    These are HOST-wide counters (every process on the machine, the fakes and
+    other tenants included); the worker's own faults are ``minflt_per_job``."""
     out: dict = {k + "_per_job": round((v1[k] - v0[k]) / max(1, n), 1) for k in _VMSTAT if k in v0 and k in v1}
+    out["scope"] = "host"
     for k in ("Dirty_kB", "Writeback_kB"):
         if k in v0 and k in v1:
             out[k] = [v0[k], v1[k]]
