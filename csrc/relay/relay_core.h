@@ -1079,15 +1079,16 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
     cv_free.notify_all();
     cv_ready.notify_all();
   }
-  if (pool) pool->wait();
-  if (!r.err.empty()) return r;
-  const std::string fin = "0;chunk-signature=" + signer.next(signer.empty_hash) + "\r\n\r\n";
-  std::string e;
-  if (!send_all(io, fin.data(), fin.size(), idle_timeout, flow, &e)) {
-    r.err = e;
-    return r;
+  if (r.err.empty()) {
+    // the final frame first; the hashers are joined after it (off the critical path)
+    const std::string fin = "0;chunk-signature=" + signer.next(signer.empty_hash) + "\r\n\r\n";
+    std::string e;
+    if (send_all(io, fin.data(), fin.size(), idle_timeout, flow, &e))
+      r.last_sig = signer.prev();
+    else
+      r.err = e;
   }
-  r.last_sig = signer.prev();
+  if (pool) pool->wait();
   return r;
 }
 
@@ -1438,13 +1439,16 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     r.sent += m;
   }
   if (!r.err.empty()) set_err(r.err);
+  if (r.err.empty()) {
+    // the final frame goes out before the clean-up: joining the hashers and
+    // unmapping the file (a TLB shootdown on every core that touched it) are
+    // not on the request's critical path
+    const std::string fin = std::string(n ? "\r\n" : "") + "0;chunk-signature=" + signer.next(signer.empty_hash) +
+                            "\r\n\r\n";
+    if (send_all(io, fin.data(), fin.size(), idle_timeout, flow, &r.err)) r.last_sig = signer.prev();
+  }
   if (pool) pool->wait();
   if (map) ::munmap(const_cast<char*>(map), map_len);
-  if (!r.err.empty()) return r;
-  const std::string fin = std::string(n ? "\r\n" : "") + "0;chunk-signature=" + signer.next(signer.empty_hash) +
-                          "\r\n\r\n";
-  if (!send_all(io, fin.data(), fin.size(), idle_timeout, flow, &r.err)) return r;
-  r.last_sig = signer.prev();
   return r;
 }
 
