@@ -1183,6 +1183,11 @@ inline bool zc_follow() {
   static const bool on = zc_env_chunks("TRITONDL_SHA_MB_FOLLOW", 1) != 0;
   return on;
 }
+// One timing line per signed PUT on stderr (TRITONDL_ZC_TRACE=1; diagnostics).
+inline bool zc_trace() {
+  static const bool on = zc_env_chunks("TRITONDL_ZC_TRACE", 0) != 0;
+  return on;
+}
 // Pre-map a streamed signed PUT's file mapping (TRITONDL_ZC_POPULATE=1).
 inline bool zc_populate() {
   static const bool on = zc_env_chunks("TRITONDL_ZC_POPULATE", 0) != 0;
@@ -1231,6 +1236,16 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
   const size_t n = static_cast<size_t>((length + chunk - 1) / chunk);
   std::vector<std::array<unsigned char, 32>> dig(n);
   std::vector<uint8_t> ready(n, 0);
+  // TRITONDL_ZC_TRACE=1: per chunk, when its bytes were on disk for its hasher,
+  // when its digest was ready, when the sender wrote it (ns since the pump began);
+  // one summary line per PUT on stderr
+  const bool ztrace = zc_trace();
+  const auto t_start = Clock::now();
+  std::vector<int64_t> t_cov(ztrace ? n : 0), t_hash(ztrace ? n : 0), t_sent(ztrace ? n : 0);
+  std::atomic<size_t> n_wide{0}, n_pair{0};
+  auto ns_now = [&] {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t_start).count();
+  };
   std::mutex mu;
   std::condition_variable cv_ready;
   std::atomic<bool> abort{false};
@@ -1353,6 +1368,11 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
           return;
         }
       }
+      if (ztrace) {
+        const int64_t t = ns_now();
+        for (size_t j = 0; j < cnt; ++j) t_cov[i + j] = t;
+        (cnt > 2 ? n_wide : n_pair).fetch_add(1);
+      }
       const void* src[16];
       for (size_t j = 0; j < cnt; ++j) {
         if (map) {
@@ -1367,6 +1387,10 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
         }
       }
       tritondl_hash::sha256_batch(src, m, cnt, dig[i].data());
+      if (ztrace) {
+        const int64_t t = ns_now();
+        for (size_t j = 0; j < cnt; ++j) t_hash[i + j] = t;
+      }
       publish(i, cnt);
     }
   };
@@ -1423,6 +1447,10 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
       }
       if (!writev_all(io, iov, idle_timeout, flow, &r.err)) break;
       r.sent += bytes;
+      if (ztrace) {
+        const int64_t t = ns_now();
+        for (size_t k = 0; k < avail; ++k) t_sent[c + k] = t;
+      }
       c += avail - 1;
       continue;
     }
@@ -1446,6 +1474,20 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
     const std::string fin = std::string(n ? "\r\n" : "") + "0;chunk-signature=" + signer.next(signer.empty_hash) +
                             "\r\n\r\n";
     if (send_all(io, fin.data(), fin.size(), idle_timeout, flow, &r.err)) r.last_sig = signer.prev();
+  }
+  if (ztrace && n && r.err.empty()) {
+    // the last chunk's bytes landing = the download's end, as its hasher saw it
+    int64_t cov_last = 0, hash_last = 0, sent_last = t_sent[n - 1], max_lag = 0;
+    for (size_t k = 0; k < n; ++k) {
+      cov_last = std::max(cov_last, t_cov[k]);
+      hash_last = std::max(hash_last, t_hash[k]);
+      max_lag = std::max(max_lag, t_sent[k] - t_cov[k]);
+    }
+    std::fprintf(stderr,
+                 "zc-trace n=%zu wide=%zu pair=%zu cov_last_us=%.1f hash_last_us=%.1f sent_last_us=%.1f "
+                 "fin_us=%.1f max_cov_to_sent_us=%.1f\n",
+                 n, n_wide.load(), n_pair.load(), cov_last / 1e3, hash_last / 1e3, sent_last / 1e3, ns_now() / 1e3,
+                 max_lag / 1e3);
   }
   if (pool) pool->wait();
   if (map) ::munmap(const_cast<char*>(map), map_len);
