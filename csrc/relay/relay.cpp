@@ -75,6 +75,8 @@ PYBIND11_MODULE(_relay, m) {
       .def("done", &Flow::done, py::arg("seg"))
       .def("watermark", &Flow::watermark)
       .def("covered_bytes", &Flow::covered_bytes, py::arg("start"), py::arg("end"))
+      .def("covered_prefix", &Flow::covered_prefix, py::arg("start"), py::arg("end"),
+           "bytes of [start, end) on disk contiguously from start")
       .def("bytes_until_covered", &Flow::bytes_until_covered, py::arg("start"), py::arg("end"))
       .def("frontiers", &Flow::frontiers, "receive frontier of every unfinished segment")
       .def("open_starts", &Flow::open_starts, "start offset of every unfinished segment")

@@ -69,6 +69,14 @@ def test_flow_coverage_and_states():
     assert m.bytes_until_covered(0, 100) == 0 and m.bytes_until_covered(100, 200) == 50
     assert m.bytes_until_covered(400, 500) == 100 and m.bytes_until_covered(350, 450) == 250
     assert m.covered_bytes(100, 500) == 50
+    # contiguous coverage from a point (what a streamed PUT may send now): stops at a gap
+    m.advance(1, 30)                               # [0,150) and [400,430) on disk
+    assert m.covered_prefix(0, 400) == 150 and m.covered_prefix(100, 120) == 20
+    assert m.covered_prefix(150, 400) == 0 and m.covered_prefix(400, 800) == 30
+    m.advance(0, 400)                              # the gap closes: [0, 430) contiguous
+    assert m.covered_prefix(0, 800) == 430 and m.covered_prefix(390, 420) == 30
+    m.finish(800)
+    assert m.covered_prefix(0, 900) == 800 and m.covered_prefix(900, 950) == 0
     g = relay.Flow([(0, 10, 0)])
     threading.Timer(0.05, g.fail, args=("boom",)).start()
     assert g.wait_covered(0, 10, 5.0) == 1 and g.error == "boom"
