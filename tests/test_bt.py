@@ -514,10 +514,11 @@ def test_watch_files_fires_in_file_order_and_on_resume(tmp_path):
         await _dl().download(str(dst), Sink(), magnet_for(info, [tr.url]), pick_files=pick, on_file=order.append)
         base = str(dst / "Pack")
         assert sorted(offered) == sorted(os.path.join(base, n) for n in ("a.mkv", "b.mkv", "c.txt", "d.mkv"))
-        # layout order is the picker's priority, not a guarantee: a request that
-        # times out on a loaded box is re-sent and can finish its file late
+        # layout order is the picker's priority, not a guarantee: the native wire keeps
+        # hundreds of block requests in flight, so on a loaded box files can finish in
+        # any order; every watched file fires exactly once, the unwatched one never
         want = [os.path.join(base, n) for n in ("a.mkv", "b.mkv", "d.mkv")]
-        assert sorted(order) == sorted(want) and order.index(want[0]) < order.index(want[2]), order
+        assert sorted(order) == sorted(want), order
         _check_tree(str(src), str(dst))
         # redelivery: everything is on disk; the resume verify fires each watched file
         again = []
