@@ -493,9 +493,10 @@ def test_large_torrent_file_over_http_is_read_whole(tmp_path):
 
 
 def test_watch_files_fires_in_file_order_and_on_resume(tmp_path):
-    """Per-file completion (streamed uploads): watched files are fetched
-    first and complete in layout order; unwatched ones come last; on a
-    redelivered job the resume check fires every whole file at once."""
+    """Per-file completion (streamed uploads): each watched file fires once
+    when its last piece verifies (they are requested first, in layout
+    order); unwatched ones never fire; on a redelivered job the resume check
+    fires every whole file at once."""
     async def main():
         src = tmp_path / "src" / "Pack"
         make_payload(str(src), {"a.mkv": 3_000_000, "b.mkv": 3_000_000, "c.txt": 1_000_000, "d.mkv": 2_500_000})
