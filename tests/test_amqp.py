@@ -598,3 +598,40 @@ def test_connection_names_its_worker_process():
         await conn.close()
         await b.stop()
     run(main())
+
+
+def test_pause_hands_buffered_deliveries_back_and_resume_consumes_again():
+    """A worker busy with a long job holds one more delivery per other shard.
+    pause() cancels the consumers, re-publishes the buffered delivery (a
+    fresh message: not marked redelivered) and acks the original; while
+    paused nothing more arrives and health stays green; resume() consumes."""
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        await cl.consume("t")
+        await cl.publish("t", b"long")                 # shard 0
+        await cl.publish("t", b"waiting")              # shard 1: buffered behind the long job
+        running = await cl.get(2)
+        for _ in range(50):
+            if not cl._out.empty():
+                break
+            await asyncio.sleep(0.01)
+        assert not cl._out.empty()
+        assert await cl.pause() == 1 and cl.paused and cl.handed_back == 1
+        assert all(not sh.active and sh.paused for sh in cl.shards.values())
+        assert cl.health(0.0) == (True, [])
+        other = "t-1" if running.routing_key == "t-0" else "t-0"
+        back = b.queues[other].messages
+        assert len(back) == 1 and back[0].body == b"waiting" and not back[0].redelivered
+        await cl.publish("t", b"later")
+        await asyncio.sleep(0.1)
+        assert cl._out.empty()                         # paused: nothing delivered
+        assert await cl.pause() == 0                   # idempotent
+        await running.ack()                            # acks still work on the paused channel
+        await cl.resume()
+        assert not cl.paused and all(sh.active for sh in cl.shards.values())
+        got = sorted([(await cl.get(2)).body, (await cl.get(2)).body])
+        assert got == [b"later", b"waiting"]
+        await cl.close()
+        await b.stop()
+    run(main())

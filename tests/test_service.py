@@ -919,3 +919,49 @@ def test_service_sweeps_stale_job_dirs_at_start(tmp_path):
         assert not any(n.startswith("ancient") for n in os.listdir(base))
         await e.down()
     run(main())
+
+
+def test_long_job_hands_its_buffered_delivery_to_an_idle_worker(tmp_path):
+    """Head-of-line blocking: worker A runs a slow download and holds the
+    other shard's delivery in its buffer (prefetch 1 per shard, as the
+    reference).  After TRITONDL_HANDBACK seconds A gives it back; idle worker
+    B runs it and finishes while A's long job is still downloading.  A
+    consumes again once its slot frees."""
+    async def main():
+        e = await Env().up(tmp_path / "a", handback_s=0.4)
+        e.origin.rate = 1_500_000                         # the 4.5 MB job takes ~3 s
+        long_url = e.origin.add("/long.mkv", os.urandom(4_500_000))
+        short_url = e.origin.add("/short.mkv", os.urandom(30_000))
+        e.submit(Media(id="long", source_uri=long_url), i=0)
+        e.submit(Media(id="short", source_uri=short_url), i=1)
+        for _ in range(100):                              # A took one and buffers the other
+            if not e.svc.amqp._out.empty():
+                break
+            await asyncio.sleep(0.02)
+        assert not e.svc.amqp._out.empty()
+        cfg_b = Config()
+        for k in ("retry_delay_s", "progress_log_interval_s", "heartbeat_s"):
+            setattr(cfg_b, k, getattr(e.cfg, k))
+        cfg_b.download_dir = str(tmp_path / "b" / "downloading")
+        b = Service(cfg_b, amqp=Client(e.broker.url, heartbeat=0, retry_delay=0),
+                    dispatcher=Dispatcher(cfg_b.download_dir, [HTTPDownloader(progress_interval=0.05)], 0),
+                    uploader=Uploader(cfg_b.bucket, S3Client(e.s3.endpoint, Static("ak", "sk"))))
+        await b.start()
+        t0 = time.monotonic()
+        while not b.results:
+            assert time.monotonic() - t0 < 10, "the buffered job never reached the idle worker"
+            await asyncio.sleep(0.02)
+        assert b.results[0].ok and not e.svc.results            # B finished while A still downloads
+        assert e.svc.metrics.get("jobs_handed_back") == 1 and e.svc.amqp.paused
+        assert e.svc.amqp.health(0.0)[0]                         # paused on purpose is not an outage
+        res = await e.wait_results(1, timeout=20)
+        assert res[0].ok
+        for _ in range(100):
+            if not e.svc.amqp.paused:
+                break
+            await asyncio.sleep(0.02)
+        assert not e.svc.amqp.paused and all(sh.active for sh in e.svc.amqp.shards.values())
+        assert {c.media.id for c in e.converts()} == {"long", "short"} and e.broker.unacked_count() == 0
+        await b.shutdown(grace=5)
+        await e.down()
+    run(main())

@@ -197,12 +197,14 @@ class Shard:
         self.tag = ""
         self.on_msg = None
         self.active = False
+        self.paused = False                # consumer cancelled on purpose (Client.pause)
         self.since = time.monotonic()      # when ``active`` last changed
         self.rotations = 0                 # consumer re-subscriptions made for parked deliveries
         self.lock = asyncio.Lock()
 
     def set_active(self, ch: Channel, tag: str, on_msg) -> None:
         self.channel, self.tag, self.on_msg = ch, tag, on_msg
+        self.paused = False
         if not self.active:
             self.active = True
             self.since = time.monotonic()
@@ -214,8 +216,9 @@ class Shard:
             self.since = time.monotonic()
 
     def down_for(self, now: float | None = None) -> float:
-        """Seconds this shard has had no consumer (0 while it has one)."""
-        return 0.0 if self.active else (now or time.monotonic()) - self.since
+        """Seconds this shard has had no consumer (0 while it has one, or while
+        its consumer is paused on purpose)."""
+        return 0.0 if (self.active or self.paused) else (now or time.monotonic()) - self.since
 
 
 def _parse_retries(headers: dict | None) -> int:
@@ -254,6 +257,8 @@ class Client:
         self.declare_publish_queues = declare_publish_queues
         self.mandatory = mandatory
         self.returned = 0                          # publishes the broker could not route (basic.return)
+        self.paused = False                        # consumers stopped by pause() (a long job holds the slots)
+        self.handed_back = 0                       # buffered deliveries given back by pause()
         self.conn: Connection | None = None
         self.generation = 0
         self._topics: list[str] = []
@@ -319,8 +324,10 @@ class Client:
         self._lost.set()
         if self.lost_since is None:
             self.lost_since = time.monotonic()
+        self.paused = False                 # a reconnect consumes afresh; a pause must be taken again
         for sh in self.shards.values():
             sh.set_inactive()
+            sh.paused = False
         if not self._closing:
             log.with_field("error", str(err)).warn("rabbitmq connection lost; reconnecting")
 
@@ -745,6 +752,84 @@ class Client:
             shard.set_active(ch, new, cb)
             shard.rotations += 1
             return True
+
+    # ------------------------------------------------------------ hand-back
+    async def pause(self) -> int:
+        """Stop taking deliveries and give back the ones buffered here.
+
+        With prefetch per shard consumer, a worker busy with a long job holds
+        one more delivery per other shard.  That delivery waits behind the job,
+        maybe for hours of a torrent, while other workers sit idle, and
+        RabbitMQ's ``consumer_timeout`` runs for it too.  The reference worked
+        the same way (``client.go:360-373``, one goroutine per worker).  This
+        method cancels every shard consumer, so no more deliveries arrive, and
+        keeps the channels open, so deliveries still unacked can be acked.
+        Each buffered delivery is then re-published to its own exchange and
+        routing key (confirmed; a fresh message, so no redelivery count) and
+        the original acked.  If the re-publish fails, the delivery is
+        nack-requeued.  Returns how many were handed back; :meth:`resume`
+        consumes again."""
+        if self.paused:
+            return 0
+        self.paused = True
+        for sh in list(self.shards.values()):
+            async with sh.lock:
+                ch = sh.channel
+                if not sh.active or ch is None or ch.is_closed:
+                    continue
+                try:
+                    # deliveries the broker sent before its cancel-ok are in _out when this returns
+                    await ch.basic_cancel(sh.tag)
+                except AMQPError as e:
+                    log.with_fields(queue=sh.queue, error=str(e)).warn("pausing the consumer failed")
+                    continue
+                sh.set_inactive()
+                sh.paused = True
+        held: list[Delivery] = []
+        stop = False
+        while not self._out.empty():
+            d = self._out.get_nowait()
+            if d is None:
+                stop = True                 # the shutdown sentinel goes back after them
+                continue
+            held.append(d)
+        if stop:
+            self._out.put_nowait(None)
+        n = 0
+        for d in held:
+            if d.stale:
+                continue                    # its channel died: the broker requeued it already
+            try:
+                await self.publish_raw(d.exchange, d.routing_key, d.body, d.msg.properties, max_attempts=3)
+                await d.ack()
+                n += 1
+            except Exception as e:  # noqa: BLE001 - the original is still unacked: requeue it
+                log.with_field("error", str(e)).warn("hand-back re-publish failed; requeueing the delivery")
+                with contextlib.suppress(Exception):
+                    await d.nack(requeue=True)
+        self.handed_back += n
+        if n:
+            log.with_fields(deliveries=n).info("busy with a long job: handed buffered deliveries back to the broker")
+        return n
+
+    async def resume(self) -> None:
+        """Consume again on every shard :meth:`pause` stopped."""
+        if not self.paused:
+            return
+        self.paused = False
+        for sh in list(self.shards.values()):
+            async with sh.lock:
+                ch = sh.channel
+                if sh.active or not sh.paused or ch is None or ch.is_closed or sh.on_msg is None:
+                    sh.paused = False
+                    continue
+                try:
+                    tag = await ch.basic_consume(sh.queue, sh.on_msg, no_ack=False)
+                except AMQPError as e:
+                    sh.paused = False        # now a real outage: health and the reopen paths see it
+                    log.with_fields(queue=sh.queue, error=str(e)).warn("resuming the consumer failed")
+                    continue
+                sh.set_active(ch, tag, sh.on_msg)
 
     async def _parked_retry(self, d: Delivery, props: Properties, delay: float, on_done=None) -> None:
         self._parked += 1

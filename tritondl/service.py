@@ -284,6 +284,8 @@ class Service:
         self._metrics_runner = None
         self._trimmer: asyncio.Task | None = None
         self._janitor: asyncio.Task | None = None
+        self._handback: asyncio.Task | None = None
+        self._busy_since = 0.0
         self.malloc_policy: dict = {}              # what tune_malloc applied at start
         self._reaper = _Reaper()                    # deletes finished job dirs off the loop
         self.results: list[JobResult] = []        # recent results (trimmed past 10,000)
@@ -466,8 +468,28 @@ class Service:
             self._trimmer = asyncio.ensure_future(self._trim_heap(cfg.malloc_trim_s))
         if cfg.cleanup and cfg.stale_job_days > 0:
             self._janitor = asyncio.ensure_future(self._sweep_stale(cfg.stale_job_days * 86400.0))
+        if cfg.handback_s > 0:
+            self._handback = asyncio.ensure_future(self._handback_loop(cfg.handback_s))
         for i in range(max(1, cfg.concurrency)):
             self._workers.append(asyncio.ensure_future(self._worker(i)))
+
+    async def _handback_loop(self, after_s: float) -> None:
+        """Give buffered deliveries back to the broker while every job slot
+        has been busy for ``after_s`` (:meth:`Client.pause`), so a long job
+        does not hold other jobs that idle workers could run; the worker loop
+        resumes consuming as soon as a slot frees."""
+        assert self.amqp is not None
+        while not self._stop.is_set():
+            await asyncio.sleep(max(0.05, after_s / 4))
+            busy = self._inflight >= max(1, self.cfg.concurrency)
+            if busy and not self.amqp.paused and time.monotonic() - self._busy_since >= after_s:
+                try:
+                    n = await self.amqp.pause()
+                except Exception as e:  # noqa: BLE001 - an optimisation: the job carries on regardless
+                    log.with_field("error", str(e)).warn("hand-back failed")
+                    continue
+                if n:
+                    self.metrics.inc("jobs_handed_back", n)
 
     async def _sweep_stale(self, max_age_s: float, period: float = 3600.0) -> None:
         """At start and every ``period`` s: delete job dirs untouched for
@@ -531,6 +553,8 @@ class Service:
     async def _worker(self, idx: int) -> None:
         assert self.amqp is not None
         while not self._stop.is_set():
+            if self.amqp.paused:
+                await self.amqp.resume()    # a slot is free again: take deliveries
             getter = asyncio.ensure_future(self.amqp.get())
             stopper = asyncio.ensure_future(self._stop.wait())
             done, _ = await asyncio.wait({getter, stopper}, return_when=asyncio.FIRST_COMPLETED)
@@ -545,6 +569,8 @@ class Service:
                 return
             self._last_taken = time.monotonic()
             self._inflight += 1
+            if self._inflight >= max(1, self.cfg.concurrency):
+                self._busy_since = time.monotonic()
             self.metrics.set("jobs_inflight", self._inflight)
             if not self._pipeline_now():
                 try:
@@ -1030,7 +1056,7 @@ class Service:
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
         self._stop.set()
-        for t in (self._trimmer, self._janitor):
+        for t in (self._trimmer, self._janitor, self._handback):
             if t is not None:
                 t.cancel()
         t_end = time.monotonic() + grace

@@ -59,7 +59,8 @@ ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_time
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
               "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s",
-              "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms", "STALE_JOB_DAYS": "stale_job_days"}
+              "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms", "STALE_JOB_DAYS": "stale_job_days",
+              "HANDBACK": "handback_s"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -148,6 +149,10 @@ class Config:
     # consuming.  A full collection otherwise walks all of them on the event loop: 40-100 ms,
     # a stall in the middle of a job and of the heartbeats (Service.start)
     gc_freeze: bool = True
+    # once every job slot has been busy this long (a long download), deliveries buffered
+    # behind it (one per other shard consumer) go back to the broker for idle workers and
+    # the consumers pause until a slot frees (Client.pause); 0 = hold them (the reference)
+    handback_s: float = 60.0
     # with cleanup on: job dirs nothing has touched for this many days and no worker holds
     # (partial downloads of jobs whose message was purged or finished elsewhere) are
     # deleted, at start and hourly; 0 = never (the reference's work dir only grew)

@@ -126,6 +126,7 @@ HELP = {
     "broker_down_seconds": "seconds the broker connection has been down (0 while up)",
     "pipeline_commit_active": "1 while job commits are pipelined (the publish -> confirm round trip is long enough)",
     "jobs_dead_lettered_total": "jobs published to the dead-letter topic after max_retries",
+    "jobs_handed_back_total": "buffered deliveries given back to the broker while a long job held every slot",
     "stale_job_dirs_removed_total": "job dirs removed after TRITONDL_STALE_JOB_DAYS untouched (no worker held them)",
     "jobs_dropped_total": "jobs nacked without requeue after max_retries (drop_failed)",
     "bytes_uploaded_total": "bytes uploaded to S3 by finished jobs",
