@@ -954,6 +954,7 @@ def test_long_job_hands_its_buffered_delivery_to_an_idle_worker(tmp_path):
         assert b.results[0].ok and not e.svc.results            # B finished while A still downloads
         assert e.svc.metrics.get("jobs_handed_back") == 1 and e.svc.amqp.paused
         assert e.svc.amqp.health(0.0)[0]                         # paused on purpose is not an outage
+        assert "tritondl_consumers_paused 1.0" in e.svc.metrics.render()
         res = await e.wait_results(1, timeout=20)
         assert res[0].ok
         for _ in range(100):

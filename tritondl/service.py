@@ -1009,6 +1009,7 @@ class Service:
             m.set("jobs_parked_waiting", self.amqp.parked)
             lost = self.amqp.lost_since
             m.set("broker_down_seconds", 0.0 if lost is None else round(now - lost, 3))
+            m.set("consumers_paused", 1.0 if self.amqp.paused else 0.0)
             for q, sh in self.amqp.shards.items():
                 m.set("consumer_active", 1.0 if sh.active else 0.0, queue=q)
 

@@ -122,6 +122,7 @@ HELP = {
     "jobs_parked_waiting": "deliveries waiting in-process right now (parked)",
     "jobs_poison_parked": "jobs past max_retries parked because the dead-letter topic is unreachable (never re-run)",
     "consumer_active": "1 while the shard queue has a live consumer of this worker, else 0",
+    "consumers_paused": "1 while this worker's consumers are paused on purpose (a long job holds every slot: hand-back)",
     "last_job_finished_age_seconds": "seconds since this worker last recorded a job result (or started)",
     "broker_down_seconds": "seconds the broker connection has been down (0 while up)",
     "pipeline_commit_active": "1 while job commits are pipelined (the publish -> confirm round trip is long enough)",
