@@ -332,6 +332,8 @@ def main() -> int:
                                                                "default, 0: delete every file)")
     ap.add_argument("--variants", type=int, default=-1,
                     help="distinct payloads jobs rotate through (-1: more than the spare pool holds)")
+    ap.add_argument("--pipeline-min-ms", type=float, default=-1.0,
+                    help="pipeline commits only while the confirm round trip is at least this (ms; -1: worker default)")
     ap.add_argument("--pipeline-commit", default="on", choices=["on", "off"],
                     help="on (the worker default): a job's publish confirm and ack overlap the next job")
     ap.add_argument("--no-reference-mode", action="store_true",
@@ -405,6 +407,7 @@ def main() -> int:
                      recycle_bytes=(a.recycle_mb << 20) if a.recycle_mb >= 0 else -1, variants=a.variants,
                      content_check=not a.no_content_check,
                      overrides={"pipeline_commit": a.pipeline_commit == "on",
+                                **({"pipeline_commit_min_ms": a.pipeline_min_ms} if a.pipeline_min_ms >= 0 else {}),
                                 **({"s3_parallel_parts": a.s3_parallel_parts} if a.s3_parallel_parts > 0 else {})})
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
