@@ -294,6 +294,8 @@ def main() -> int:
                     help="HTTP GET probe size in KiB, the rest as parallel Range streams "
                          "(-1: worker default, 0: open-ended probe)")
     ap.add_argument("--http-segments", type=int, default=0, help="max parallel Range streams (0: worker default)")
+    ap.add_argument("--segment-threshold-mb", type=float, default=0,
+                    help="files at least this big are fetched as parallel Range streams (0: worker default)")
     ap.add_argument("--s3-part-mb", type=int, default=0, help="S3 multipart part size (0: worker default)")
     ap.add_argument("--s3-parallel-parts", type=int, default=0, help="S3 parts in flight per file (0: worker default)")
     ap.add_argument("--s3-multipart-mb", type=int, default=0,
@@ -408,6 +410,8 @@ def main() -> int:
                      content_check=not a.no_content_check,
                      overrides={"pipeline_commit": a.pipeline_commit == "on",
                                 **({"pipeline_commit_min_ms": a.pipeline_min_ms} if a.pipeline_min_ms >= 0 else {}),
+                                **({"http_segment_threshold": int(a.segment_threshold_mb * (1 << 20))}
+                                   if a.segment_threshold_mb > 0 else {}),
                                 **({"s3_parallel_parts": a.s3_parallel_parts} if a.s3_parallel_parts > 0 else {})})
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
