@@ -118,9 +118,20 @@ def test_listen_moves_to_a_port_free_for_tcp_and_udp(tmp_path):
         src = tmp_path / "src"
         make_payload(str(src), {"film.mkv": 100_000})
         info = torrent_for(str(src / "film.mkv"), 65536)
-        udp = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-        udp.bind(("127.0.0.1", 0))
-        taken = udp.getsockname()[1]
+        # a UDP port we hold whose TCP twin is free right now (tests running in parallel
+        # take ephemeral TCP ports too: pick again if the twin is busy)
+        for _ in range(20):
+            udp = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            udp.bind(("127.0.0.1", 0))
+            taken = udp.getsockname()[1]
+            probe = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            try:
+                probe.bind(("127.0.0.1", taken))
+                break
+            except OSError:
+                udp.close()
+            finally:
+                probe.close()
         try:
             t = Torrent(info.infohash, str(src), TorrentConfig(listen_host="127.0.0.1", seed=True,
                                                                verify_device="cpu", utp=True,
