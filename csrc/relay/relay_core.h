@@ -1199,12 +1199,14 @@ inline std::atomic<int>& zc_active_pumps() {
   return n;
 }
 // Frames per writev when the file is mapped (TRITONDL_ZC_WRITE_BATCH; 0/1 =
-// a header send + a sendfile per frame).  A sender that fell behind the
-// hashers sends every ready frame in one syscall: the 10 MiB headline job
-// ran 361.6 vs 342.9 jobs/s (mean of 7 alternated runs each, 16 vs
-// sendfile; 64 was no better than 16), profiles/r05_batch_ab/.
+// a header send + a zero-copy sendfile per frame, the default).  Batching
+// every ready frame into one writev won 5 % on the 10 MiB job while the
+// hashers lagged the download (profiles/r05_batch_ab/); once they followed
+// the receive frontier and the final frame went out first it lost 3 %
+// (402.4 vs 390.3 jobs/s, 6 alternated runs, profiles/r05_batch_ab3/), and
+// on parallel multipart parts its payload copy cost 10 % (r05_gib_ab/).
 inline size_t zc_write_batch() {
-  static const size_t n = zc_env_chunks("TRITONDL_ZC_WRITE_BATCH", 16);
+  static const size_t n = zc_env_chunks("TRITONDL_ZC_WRITE_BATCH", 0);
   return n;
 }
 

@@ -67,7 +67,7 @@ DIRECT = {
     "TRITONDL_ZC_POPULATE": ("0", "relay/relay_core.h",
                              "1: map a signed PUT's whole file mapping up front (MADV_POPULATE_READ) "
                              "instead of a minor fault per page"),
-    "TRITONDL_ZC_WRITE_BATCH": ("16", "relay/relay_core.h",
+    "TRITONDL_ZC_WRITE_BATCH": ("0", "relay/relay_core.h",
                                 "signed plain-http PUT: ready frames per writev from the file mapping "
                                 "(0/1: a header send + sendfile per 64 KiB frame)"),
     "TRITONDL_SHA_NI": ("1", "hash/sha_ni.h, hash/hash_host.cpp", "0: OpenSSL instead of the two-stream SHA-NI path"),
