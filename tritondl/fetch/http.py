@@ -361,6 +361,7 @@ class HTTPDownloader:
                     raise aiohttp.ClientConnectionError(f"GET {url}: {e}") from e
                 try:
                     await conn.sendall(head, self.read_timeout)
+                    rawhttp.trace("get_sent")
                     h = await rawhttp.read_head(conn, self.read_timeout)
                     rawhttp.trace("get_head")
                     break

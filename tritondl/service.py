@@ -667,6 +667,7 @@ class Service:
                         self._clear_redeliveries(job.media.id)
                         return self._record(JobResult(False, "redelivery-limit", f"redelivered {n} times",
                                                       seconds=time.monotonic() - t0))
+                rawhttp.trace("job_locked")
                 return await self._run_job(msg, job, t0)
         except JobBusy as e:
             # not the job's failure: hand it back without spending a retry
