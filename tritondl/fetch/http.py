@@ -571,9 +571,9 @@ class HTTPDownloader:
         fd = os.open(h.part, os.O_WRONLY)
         rep = asyncio.ensure_future(reporter())
         src = probe.final_url or url          # follow-up ranges skip the redirect hop(s)
-        # (a single stream is a task too: running it inline in this coroutine, so
-        # its pump starts before the streamed upload's first step, measured ~20 %
-        # slower on the headline job — profiles/r02_ctrl_ab/)
+        # (a single stream is a task too; the service gives this coroutine and the
+        # stream task two loop turns before the streamed upload's first step, so
+        # the receive pump starts first: service._GET_FIRST, profiles/r05_gil_ab/)
         if len(segs) <= self.segments:
             tasks = [asyncio.ensure_future(self._fetch_segment(src, fd, i, segs, done, validator, probe, h,
                                                                first if i == 0 else None))

@@ -95,6 +95,14 @@ from .utils.log import log
 from .utils.metrics import Metrics, serve_metrics
 from .utils.profiler import CPUProfiler
 
+# Loop turns the download gets before the streamed upload's first step: turn 1
+# runs HTTPDownloader._run (it spawns the stream task), turn 2 the stream task
+# up to its native receive pump.  The upload (SigV4 setup, connection) then
+# follows a download already running instead of delaying it: 427.7 vs 395.1
+# jobs/s, PUT done at 2.02 vs 2.20 ms (profiles/r05_gil_ab/).  Round 2 measured
+# the opposite order faster, before the sender followed the download's frontier.
+_GET_FIRST = int(os.environ.get("TRITONDL_GET_FIRST", "2"))
+
 
 def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
@@ -771,6 +779,8 @@ class Service:
         up: asyncio.Task | None = None
         fd = None
         if h.size and go_ext(h.filename) in MEDIA_EXTS:
+            for _ in range(_GET_FIRST):
+                await asyncio.sleep(0)
             fd = h.open_reader()
             up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes,
                                                                    flow=h.flow,
