@@ -62,9 +62,6 @@ DIRECT = {
     "TRITONDL_SHA_MB_FOLLOW": ("1", "relay/relay_core.h",
                                "streamed signed PUT: 16-chunk hash claims only over bytes already downloaded "
                                "(0: by position)"),
-    "TRITONDL_GET_FIRST": ("2", "service.py",
-                           "event-loop turns a streamed HTTP job's download gets before its S3 upload starts "
-                           "(0: the upload first)"),
     "TRITONDL_ZC_TRACE": ("0", "relay/relay_core.h",
                           "1: one timing line per signed PUT on stderr (when each chunk landed, was hashed, was sent)"),
     "TRITONDL_ZC_POPULATE": ("0", "relay/relay_core.h",

@@ -575,6 +575,14 @@ class Client:
                 continue  # its channel died before we got to it; the broker requeued it
             yield d
 
+    def get_nowait(self) -> Delivery | None:
+        """The next delivery already received (None: shutdown); raises
+        ``asyncio.QueueEmpty`` when none is waiting."""
+        while True:
+            d = self._out.get_nowait()
+            if d is None or not d.stale:
+                return d
+
     async def get(self, timeout: float | None = None) -> Delivery | None:
         """Pull the next delivery (None on shutdown / timeout)."""
         try:

@@ -95,14 +95,6 @@ from .utils.log import log
 from .utils.metrics import Metrics, serve_metrics
 from .utils.profiler import CPUProfiler
 
-# Loop turns the download gets before the streamed upload's first step: turn 1
-# runs HTTPDownloader._run (it spawns the stream task), turn 2 the stream task
-# up to its native receive pump.  The upload (SigV4 setup, connection) then
-# follows a download already running instead of delaying it: 427.7 vs 395.1
-# jobs/s, PUT done at 2.02 vs 2.20 ms (profiles/r05_gil_ab/).  Round 2 measured
-# the opposite order faster, before the sender followed the download's frontier.
-_GET_FIRST = int(os.environ.get("TRITONDL_GET_FIRST", "2"))
-
 
 def default_impls(cfg: Config) -> list[ClientImpl]:
     """``[torrent.NewClient(), http.NewClient()]`` (``downloader.go:87-90``)."""
@@ -563,16 +555,21 @@ class Service:
         while not self._stop.is_set():
             if self.amqp.paused:
                 await self.amqp.resume()    # a slot is free again: take deliveries
-            getter = asyncio.ensure_future(self.amqp.get())
-            stopper = asyncio.ensure_future(self._stop.wait())
-            done, _ = await asyncio.wait({getter, stopper}, return_when=asyncio.FIRST_COMPLETED)
-            if getter not in done:
-                getter.cancel()
-                with contextlib.suppress(asyncio.CancelledError):
-                    await getter
-                return
-            stopper.cancel()
-            d = getter.result()
+            try:
+                # a delivery already waiting (prefetch) starts at once: no getter and
+                # stopper tasks to create, race and cancel
+                d = self.amqp.get_nowait()
+            except asyncio.QueueEmpty:
+                getter = asyncio.ensure_future(self.amqp.get())
+                stopper = asyncio.ensure_future(self._stop.wait())
+                done, _ = await asyncio.wait({getter, stopper}, return_when=asyncio.FIRST_COMPLETED)
+                if getter not in done:
+                    getter.cancel()
+                    with contextlib.suppress(asyncio.CancelledError):
+                        await getter
+                    return
+                stopper.cancel()
+                d = getter.result()
             if d is None:
                 return
             self._last_taken = time.monotonic()
@@ -779,8 +776,8 @@ class Service:
         up: asyncio.Task | None = None
         fd = None
         if h.size and go_ext(h.filename) in MEDIA_EXTS:
-            for _ in range(_GET_FIRST):
-                await asyncio.sleep(0)
+            # the download's task (made in impl.start) runs its first step before this
+            # upload's: a single stream's receive pump starts ahead of the SigV4 setup
             fd = h.open_reader()
             up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes,
                                                                    flow=h.flow,
