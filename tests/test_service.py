@@ -11,6 +11,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from tritondl.amqp.client import Client
 from tritondl.amqp.codec import Properties
 from tritondl_testkit.fakes.broker import Broker
@@ -423,6 +425,31 @@ def test_stream_upload_overlaps_and_fails_cleanly(tmp_path):
         assert object_key("s2", "dies.mkv") not in e.s3.buckets["triton-staging"]
         await e.down()
     run(main())
+
+
+def test_streamed_job_starts_the_download_pump_before_the_upload(tmp_path, monkeypatch):
+    """The single-stream fetch runs inline in the downloader's task, which is
+    made before the upload's, so the receive pump starts ahead of the PUT's
+    SigV4 setup (profiles/r05_gil_ab/: +8 % on the headline job)."""
+    from tritondl.utils import rawhttp
+    if rawhttp.relay_module() is None:
+        pytest.skip("native relay not built")
+    events: list = []
+    monkeypatch.setattr(rawhttp, "TRACE", events)
+
+    async def main():
+        e = await Env().up(tmp_path)
+        for k in range(3):
+            e.submit(Media(id=f"o{k}", source_uri=e.origin.add(f"/o{k}.mkv", os.urandom(2_000_000))))
+        res = await e.wait_results(3)
+        assert all(r.ok for r in res), res
+        await e.down()
+    run(main())
+    names = [n for n, _t in events]
+    starts = [i for i, n in enumerate(names) if n == "job_start"] + [len(names)]
+    for a, b in zip(starts, starts[1:]):
+        job = names[a:b]
+        assert job.index("get_pump_start") < job.index("put_pump_start"), job
 
 
 def test_magnet_job_streams_each_file_as_it_completes(tmp_path):
