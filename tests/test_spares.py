@@ -72,6 +72,38 @@ def test_pool_bounds_and_lifo(tmp_path):
     assert spares.pool_for(str(base / "m1")) is None and not os.path.exists(pool.root)
 
 
+def test_reaper_named_files_fast_path_and_fallback(tmp_path):
+    """A streamed job names its one file: it is offered and the dir removed
+    with one rmdir.  A dir holding anything else falls back to the walk, and
+    nothing is left either way; a named file the pool refuses is deleted."""
+    from tritondl.service import _Reaper
+    base = tmp_path / "dl"
+    base.mkdir()
+    pool = spares.register(spares.SparePool(str(base), max_files=2, min_file_bytes=1 << 20))
+    r = _Reaper()
+    r.pool = pool
+    try:
+        one = base / "j1"
+        one.mkdir()
+        _file(one / "a.mkv", 2 << 20)
+        r.submit(str(one), ["a.mkv"])
+        two = base / "j2"
+        (two / "extra").mkdir(parents=True)
+        _file(two / "b.mkv", 2 << 20)
+        _file(two / "extra" / "c.nfo", 10)
+        r.submit(str(two), ["b.mkv"])
+        three = base / "j3"
+        three.mkdir()
+        _file(three / "small.mkv", 1000)                 # below min_file_bytes: deleted, not kept
+        r.submit(str(three), ["small.mkv"])
+        assert r.drain(10)
+        assert not one.exists() and not two.exists() and not three.exists()
+        assert pool.offered == 2 and len(os.listdir(pool.root)) == 2
+    finally:
+        spares.unregister(pool)
+        pool.clear()
+
+
 def test_stale_pools_of_dead_processes(tmp_path):
     mine = tmp_path / f"{spares.PREFIX}{os.getpid()}"
     mine.mkdir()

@@ -155,13 +155,19 @@ class _Reaper:
         self._lock = threading.Lock()
         self.pool: spares.SparePool | None = None
 
-    def submit(self, path: str) -> None:
+    def submit(self, path: str, names: list[str] | None = None) -> None:
+        """Delete ``path``.  ``names``: the files the job is known to have left
+        there (a streamed HTTP job's one file); they are offered to the pool
+        and the dir removed with one ``rmdir`` when nothing else is in it,
+        instead of walking the tree twice.  That walk runs Python on this
+        thread, contending for the GIL with the event loop while it starts
+        the next job."""
         if self._thread is None:
             with self._lock:
                 if self._thread is None:
                     self._thread = threading.Thread(target=self._run, name="tdl-reaper", daemon=True)
                     self._thread.start()
-        self._q.put(path)
+        self._q.put((path, names))
 
     def _run(self) -> None:
         while True:
@@ -169,13 +175,25 @@ class _Reaper:
             if isinstance(item, threading.Event):
                 item.set()
                 continue
+            path, names = item
             pool = self.pool
+            if names:
+                for n in names:
+                    p = os.path.join(path, n)
+                    if pool is None or not pool.offer(p):
+                        with contextlib.suppress(OSError):
+                            os.unlink(p)
+                try:
+                    os.rmdir(path)
+                    continue
+                except OSError:
+                    pass                     # something else is in it: the full walk below
             if pool is not None:
                 try:
-                    pool.offer_dir(item)
+                    pool.offer_dir(path)
                 except OSError:
                     pass
-            shutil.rmtree(item, ignore_errors=True)
+            shutil.rmtree(path, ignore_errors=True)
 
     def drain(self, timeout: float = 60.0) -> bool:
         if self._thread is None:
@@ -744,7 +762,9 @@ class Service:
                 self._reap_job_dir(job.media.id, msg)     # dead-lettered: no retry will resume it
             return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
         if self.cfg.cleanup:
-            self._reap_job_dir(dl_dir, msg, is_path=True)
+            # a streamed single-file job left exactly its file (the .part.meta is gone)
+            names = [os.path.basename(p) for p in streamed] if len(streamed) == 1 and len(files) == 1 else None
+            self._reap_job_dir(dl_dir, msg, is_path=True, names=names)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -931,7 +951,8 @@ class Service:
             self.metrics.inc("jobs_parked")
             return False
 
-    def _reap_job_dir(self, media_id: str, msg: Delivery, is_path: bool = False) -> None:
+    def _reap_job_dir(self, media_id: str, msg: Delivery, is_path: bool = False,
+                      names: list[str] | None = None) -> None:
         """With cleanup on, a settled job's dir is moved aside (one rename, so a
         redelivered job with the same id starts clean) and deleted off the
         critical path (drained on shutdown).  After a success, and after a
@@ -950,7 +971,7 @@ class Service:
             os.rename(d, trash)
         except OSError:
             trash = d
-        self._reaper.submit(trash)
+        self._reaper.submit(trash, names)
 
     _DONE_TTL_S = 24 * 3600.0
     _DONE_MAX = 4096

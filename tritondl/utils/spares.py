@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import os
 import shutil
+import stat
 import threading
 
 PREFIX = ".tritondl-spare-"
@@ -62,7 +63,7 @@ class SparePool:
         except OSError:
             return False
         size = st.st_size
-        if not (os.path.isfile(path) and self.min_file_bytes <= size <= self.max_file_bytes):
+        if not (stat.S_ISREG(st.st_mode) and self.min_file_bytes <= size <= self.max_file_bytes):
             return False
         with self._mu:
             if len(self._files) >= self.max_files or self._bytes + size > self.max_bytes:
