@@ -619,6 +619,7 @@ def main() -> int:
                        "concurrency_per_worker": a.concurrency, "prefetch": prefetch,
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "rtt_ms": a.rtt_ms, "stream_mbps": a.stream_mbps or None,
+                       "log_level": a.log_level,
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
                        "malloc_policy": stack.svc.malloc_policy if stack.svc is not None else {},
