@@ -984,8 +984,8 @@ def test_long_job_hands_its_buffered_delivery_to_an_idle_worker(tmp_path):
         assert "tritondl_consumers_paused 1.0" in e.svc.metrics.render()
         res = await e.wait_results(1, timeout=20)
         assert res[0].ok
-        for _ in range(100):
-            if not e.svc.amqp.paused:
+        for _ in range(250):                              # resume() re-consumes shard by shard
+            if not e.svc.amqp.paused and all(sh.active for sh in e.svc.amqp.shards.values()):
                 break
             await asyncio.sleep(0.02)
         assert not e.svc.amqp.paused and all(sh.active for sh in e.svc.amqp.shards.values())

@@ -8,9 +8,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 b() { local name=$1; shift; timeout -k 10 200 python bench.py --steps 300 --warmup 10 --no-gpu-probe \
       --no-reference-mode "$@" > $OUT/$name.log 2> $OUT/$name.err; }
-for i in 1 2 3; do
-  b warning_$i &&
-  b info_$i --log-level info || break
+for i in ${RUNS:-1 2 3}; do
+  b info_$i --log-level info &&
+  b warning_$i || break
 done
 rc=$?
 for f in $OUT/*.log; do
