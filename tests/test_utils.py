@@ -58,57 +58,6 @@ def test_logger_level_filter():
     assert s.getvalue() == ""
 
 
-def test_logger_coalesces_info_lines_per_loop_iteration():
-    """On a loop thread, info lines of one iteration go out in one write; a
-    warning writes what is pending first, so the order holds; off the loop,
-    lines are written at once; a loop that stopped before its flush ran hands
-    the pending lines to the next loop (or to exit)."""
-    import asyncio
-
-    class Counting(io.StringIO):
-        writes = 0
-
-        def write(self, s):
-            self.writes += 1
-            return super().write(s)
-
-    s = Counting()
-    lg = Logger(s)
-
-    async def burst():
-        lg.info("one")
-        lg.with_field("k", 1).info("two")
-        assert s.getvalue() == ""                       # pending until the iteration ends
-        await asyncio.sleep(0)
-        assert s.writes == 1 and s.getvalue().count("\n") == 2
-        lg.info("three")
-        lg.warn("four")                                 # flushes "three" first, one write
-        assert s.writes == 2
-        lg.info("five")
-    asyncio.run(burst())
-    asyncio.run(asyncio.sleep(0))
-    lg.info("six")                                      # no loop: written at once
-    msgs = [ln.split("msg=")[1].split()[0] for ln in s.getvalue().splitlines()]
-    assert msgs == ["one", "two", "three", "four", "five", "six"], msgs
-
-    s2 = io.StringIO()
-    lg2 = Logger(s2)
-    loop = asyncio.new_event_loop()
-    loop.run_until_complete(asyncio.sleep(0))
-    asyncio.set_event_loop(loop)
-    asyncio.events._set_running_loop(loop)              # a line logged as a loop stops
-    lg2.info("late")
-    asyncio.events._set_running_loop(None)
-    loop.close()
-    asyncio.set_event_loop(None)
-
-    async def next_loop():
-        lg2.info("next")
-        await asyncio.sleep(0)
-    asyncio.run(next_loop())
-    assert [ln.split("msg=")[1] for ln in s2.getvalue().splitlines()] == ["late", "next"]
-
-
 def test_backoff_grows_and_caps():
     b = ExponentialBackoff(initial=1, multiplier=2, randomization=0, max_interval=5, max_elapsed=None)
     assert [b.next_delay() for _ in range(5)] == [1, 2, 4, 5, 5]

@@ -9,19 +9,10 @@
 
 Thread-safe: one lock around the final write, so worker threads (native
 hashing callbacks, torch.distributed ranks) never interleave lines.
-
-Info and debug lines logged on a thread running an asyncio loop are written
-together once per loop iteration (one ``write`` + flush for the job's burst
-of lines instead of one each: six to ten per job, ~7 % of the headline job
-at info level, ``profiles/r05_loglevel_ab/``).  Warnings and worse, and
-every line from other threads, are written at once, after anything pending,
-so lines stay in order; pending lines are flushed at exit.
 """
 
 from __future__ import annotations
 
-import asyncio
-import atexit
 import json
 import re
 import sys
@@ -41,7 +32,7 @@ _ts_cache: tuple[int, str] = (-1, "")
 
 def _fmt_ts(t: float) -> str:
     global _ts_cache
-    sec = int(t)
+    sec = int(t)                        # the string changes once a second: build it once
     if _ts_cache[0] == sec:
         return _ts_cache[1]
     lt = time.localtime(t)
@@ -96,9 +87,6 @@ class Logger:
         self.json = False
         self.report_caller = False
         self._lock = threading.Lock()
-        self._pending: list[str] = []      # info/debug lines waiting for the loop iteration's end
-        self._flush_loop = None            # the loop a flush is scheduled on
-        atexit.register(self.flush)
 
     def configure(self, log_level: str = "", log_format: str = "") -> None:
         if log_level.lower() == "debug":
@@ -165,40 +153,13 @@ class Logger:
             line = " ".join(parts)
         if "@" in line:
             line = _CREDS.sub(r"\1:xxxxx@", line)
-        if LEVELS[level] > LEVELS["warning"]:
-            loop = asyncio.events._get_running_loop()
-            if loop is not None:
-                with self._lock:
-                    self._pending.append(line)
-                    if self._flush_loop is loop:
-                        return
-                    self._flush_loop = loop      # (a loop that stopped first left it to this one)
-                try:
-                    loop.call_soon(self.flush)
-                    return
-                except RuntimeError:         # the loop is closing: write it now
-                    pass
-        with self._lock:
-            self._write_locked(line)
-
-    def _write_locked(self, line: str | None) -> None:
-        pending, self._pending = self._pending, []
-        self._flush_loop = None
-        if line is not None:
-            pending.append(line)
-        if not pending:
-            return
         stream = self.stream or sys.stderr
-        try:
-            stream.write("\n".join(pending) + "\n")
-            stream.flush()
-        except Exception:
-            pass
-
-    def flush(self) -> None:
-        """Write the pending info/debug lines (end of a loop iteration, exit)."""
         with self._lock:
-            self._write_locked(None)
+            stream.write(line + "\n")
+            try:
+                stream.flush()
+            except Exception:
+                pass
 
 
 class Entry:
