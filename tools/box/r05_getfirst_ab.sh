@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 5: the get-first default confirmed in the driver's own form (`python
 # bench.py`, no flags), alternated with the upload-first order (TRITONDL_GET_FIRST=0).
+# (Historical: TRITONDL_GET_FIRST was removed once the single-stream fetch ran
+# inline, r05_inline_ab.sh; on this tree both arms run the same order.)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r05_getfirst_ab}
 mkdir -p $OUT
