@@ -62,6 +62,8 @@ DIRECT = {
     "TRITONDL_SHA_MB_FOLLOW": ("1", "relay/relay_core.h",
                                "streamed signed PUT: 16-chunk hash claims only over bytes already downloaded "
                                "(0: by position)"),
+    "TRITONDL_S3_CHUNK_KB": ("64", "s3/sigv4.py",
+                             "aws-chunked payload chunk of a signed streaming PUT (minio-go's 64 KiB; 8 and up)"),
     "TRITONDL_ZC_TRACE": ("0", "relay/relay_core.h",
                           "1: one timing line per signed PUT on stderr (when each chunk landed, was hashed, was sent)"),
     "TRITONDL_ZC_POPULATE": ("0", "relay/relay_core.h",

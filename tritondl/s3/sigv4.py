@@ -17,6 +17,7 @@ import datetime as _dt
 import functools
 import hashlib
 import hmac
+import os
 import re
 from dataclasses import dataclass
 from urllib.parse import quote
@@ -27,7 +28,8 @@ ALGO = "AWS4-HMAC-SHA256"
 UNSIGNED_PAYLOAD = "UNSIGNED-PAYLOAD"
 STREAMING_PAYLOAD = "STREAMING-AWS4-HMAC-SHA256-PAYLOAD"
 EMPTY_SHA256 = hashlib.sha256(b"").hexdigest()
-STREAM_CHUNK = 64 * 1024
+# aws-chunked payload chunk: minio-go's 64 KiB (TRITONDL_S3_CHUNK_KB: 8 KiB and up, any size S3 accepts)
+STREAM_CHUNK = max(8, int(os.environ.get("TRITONDL_S3_CHUNK_KB", "64"))) * 1024
 SIGN_THREADS = 4
 
 
