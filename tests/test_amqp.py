@@ -486,9 +486,18 @@ def test_mandatory_publish_surfaces_unroutable_messages():
         assert isinstance(res[1], PublishReturned) and isinstance(res[3], PublishReturned)
         assert res[1].code == codec.NO_ROUTE and res[1].routing_key == "nowhere"
         assert b.queue_depth("bound") == 2
-        # a caller's own message_id is kept and still matched
+        # a caller's own message_id is left alone, and two publishes in flight may share it:
+        # the return is charged to the unroutable one only
         with pytest.raises(PublishReturned):
             await ch.basic_publish("ex", "nowhere", b"m", Properties(message_id="job-42"), mandatory=True)
+        f1 = await ch.basic_publish("ex", "bound", b"a", Properties(message_id="job-42"), mandatory=True,
+                                    wait_confirm=False)
+        f2 = await ch.basic_publish("ex", "nowhere", b"b", Properties(message_id="job-42"), mandatory=True,
+                                    wait_confirm=False)
+        r = await asyncio.gather(f1, f2, return_exceptions=True)
+        assert r[0] is True and isinstance(r[1], PublishReturned), r
+        assert b.queues["bound"].messages[-1].props.message_id == "job-42"
+        assert b.queues["bound"].messages[-1].body == b"a"
         assert not ch._mandatory_ids and not ch._returned
         # without mandatory the broker drops it and confirms (the reference's publish)
         await ch.basic_publish("ex", "nowhere", b"m")

@@ -37,7 +37,8 @@ def test_redelivered_past_the_limit_is_dead_lettered_without_running(tmp_path):
         d = os.path.join(e.cfg.download_dir, "r1")
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, ".tritondl-redeliveries"), "w") as f:
-            f.write("2")                                   # two earlier workers died on it
+            f.write("2")                                   # two earlier workers died on it ...
+        open(os.path.join(d, ".tritondl-running"), "w").close()   # ... and so did the last one
         e.broker.pause_delivery(True)
         e.broker.inject("v1.download", "v1.download-0", body, Properties(delivery_mode=2))
         e.broker.queues["v1.download-0"].messages[-1].redelivered = True

@@ -888,25 +888,36 @@ def test_dead_lettered_job_leaves_no_files_but_a_retried_one_keeps_them(tmp_path
 
 
 def test_stale_job_dir_sweep(tmp_path):
-    """Job dirs untouched for the age limit go; a fresh one, one a worker
-    holds (flock), spare pools and live workers' trash stay; a dead worker's
-    half-deleted trash goes."""
+    """Job dirs a worker made (run marker) untouched for the age limit go; a
+    fresh one, one a worker holds (flock), spare pools and live workers'
+    recent trash stay; a dead worker's half-deleted trash goes, and so does
+    trash past the grace whatever its pid (another container's pid
+    namespace).  A dir without a marker (an operator's data, a reference
+    deployment's finished download) is never taken."""
     import fcntl
     import subprocess
     from tritondl.service import sweep_stale_job_dirs
     base = tmp_path / "downloading"
-    old, fresh, held = base / "old", base / "fresh", base / "held"
-    for d in (old / "sub", fresh, held, base / ".tritondl-spare-1"):
+    old, fresh, held, foreign = base / "old", base / "fresh", base / "held", base / "foreign"
+    for d in (old / "sub", fresh, held, foreign, base / ".tritondl-spare-1"):
         os.makedirs(d)
     (old / "sub" / "part.mkv").write_bytes(b"x")
+    (old / ".tritondl-job").write_bytes(b"")          # a failed job's dir, waiting for a retry
     (held / "f.mkv").write_bytes(b"y")
+    (held / ".tritondl-running").write_bytes(b"")     # a run in progress
+    (fresh / ".tritondl-job").write_bytes(b"")
+    (foreign / "movie.mkv").write_bytes(b"z")
     t_old = time.time() - 10 * 86400
-    for p in (old / "sub" / "part.mkv", old / "sub", old, held / "f.mkv", held):
+    for p in (old / "sub" / "part.mkv", old / "sub", old / ".tritondl-job", old, held / "f.mkv",
+              held / ".tritondl-running", held, foreign / "movie.mkv", foreign):
         os.utime(p, (t_old, t_old))
     dead = subprocess.Popen(["true"])
     dead.wait()
     os.makedirs(base / f"gone.deleting-{dead.pid}-abc")
     os.makedirs(base / f"busy.deleting-{os.getpid()}-abc")
+    stuck = base / f"stuck.deleting-{os.getpid()}-abc"   # "alive" pid, but untouched for 2 h
+    os.makedirs(stuck)
+    os.utime(stuck, (time.time() - 7200, time.time() - 7200))
     # a media id that merely looks like trash, with its job running: never taken
     odd = base / f"id.deleting-{dead.pid}-x"
     os.makedirs(odd)
@@ -922,8 +933,10 @@ def test_stale_job_dir_sweep(tmp_path):
     assert odd.exists()
     shutil.rmtree(odd)
     names = sorted(os.path.basename(p) for p in out)
-    assert names == [f"gone.deleting-{dead.pid}-abc", f"old.deleting-{os.getpid()}-stale"]
+    assert names == [f"gone.deleting-{dead.pid}-abc", f"old.deleting-{os.getpid()}-stale",
+                     f"stuck.deleting-{os.getpid()}-abc"]
     assert not old.exists() and fresh.exists() and held.exists() and (base / ".tritondl-spare-1").exists()
+    assert (foreign / "movie.mkv").exists()
     assert (base / f"busy.deleting-{os.getpid()}-abc").exists()
     for p in out:                                    # the reaper's part
         shutil.rmtree(p)
@@ -936,14 +949,18 @@ def test_service_sweeps_stale_job_dirs_at_start(tmp_path):
     async def main():
         base = tmp_path / "downloading"
         os.makedirs(base / "ancient")
+        os.makedirs(base / "operator-data")
+        (base / "ancient" / ".tritondl-running").write_bytes(b"")    # a worker died in it long ago
         t_old = time.time() - 30 * 86400
-        os.utime(base / "ancient", (t_old, t_old))
+        for p in (base / "ancient" / ".tritondl-running", base / "ancient", base / "operator-data"):
+            os.utime(p, (t_old, t_old))
         e = await Env().up(tmp_path, cleanup=True, stale_job_days=7.0)
         for _ in range(100):
             if not any(n.startswith("ancient") for n in os.listdir(base)):
                 break
             await asyncio.sleep(0.02)
         assert not any(n.startswith("ancient") for n in os.listdir(base))
+        assert (base / "operator-data").is_dir()
         await e.down()
     run(main())
 

@@ -55,7 +55,11 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import dataclasses
 import itertools
+import os
+import secrets
+import socket
 import time
 from dataclasses import dataclass
 from typing import AsyncIterator
@@ -79,6 +83,14 @@ class DelayUnavailable(AMQPError):
     """The broker refused the retry delay queue (its declare or the publish into it)."""
 
 
+class LeaseRefused(AMQPError):
+    """The broker refused a job lease queue (no *configure* on it, or no
+    *write* on the default exchange)."""
+
+
+_HOLDER = f"{socket.gethostname()}:{os.getpid()}"
+
+
 # channel errors that say "this topology is not yours": the entity exists with other
 # arguments (406) or this user may not configure / write it (403)
 _NOT_OURS = (codec.ACCESS_REFUSED, codec.PRECONDITION_FAILED)
@@ -93,15 +105,72 @@ class DeliveryMetadata:
     retries: int = 0
 
 
+# Headers this worker adds (the reference's own is X-Retries, delivery.go:32-44).
+LEASE_RETURNS = "X-Lease-Returns"   # times the job came back because its holder's lease ran out
+LEASE_HOLDER = "X-Lease-Holder"     # host:pid that holds the lease copy (diagnostics)
+BUSY = "X-Busy"                     # hand-backs because another worker was running the same job
+
+
+def _int_header(headers: dict | None, name: str) -> int:
+    v = (headers or {}).get(name)
+    return v if isinstance(v, int) and not isinstance(v, bool) and v > 0 else 0
+
+
+def _lease_expired(headers: dict | None) -> bool:
+    """Did this message just come back from a lease queue whose TTL ran out?
+    RabbitMQ prepends the newest death to ``x-death``."""
+    deaths = (headers or {}).get("x-death")
+    if not isinstance(deaths, list) or not deaths or not isinstance(deaths[0], dict):
+        return False
+    d = deaths[0]
+    return d.get("reason") == "expired" and ".lease." in str(d.get("queue", ""))
+
+
+class Lease:
+    """Where a leased delivery lives while its job runs: a copy in a per-job
+    queue ``<rk>.lease.<token>.<n>`` whose ``x-message-ttl`` is the lease and
+    whose dead-letter target is the job's own exchange and routing key."""
+
+    def __init__(self, token: str, ttl: float) -> None:
+        self.token = token
+        self.ttl = ttl
+        self.n = 0
+        self.queue = ""
+        self.lost = False                 # the copy ran out before a renewal: the job went back
+        self.renewed_at = time.monotonic()
+
+
 class Delivery:
-    """One job message (reference ``Delivery``, ``delivery.go:17-28``)."""
+    """One job message (reference ``Delivery``, ``delivery.go:17-28``).
+
+    A delivery can be *leased* (:meth:`hold`): after ``after`` seconds the
+    broker keeps a copy in a lease queue (:class:`Lease`) and the original
+    is acked, so the delivery no longer sits unacked on its channel.
+    RabbitMQ closes a channel that holds a delivery longer than its
+    ``consumer_timeout`` (30 min by default) and requeues the delivery, and
+    another worker then runs the job a second time.  The reference held
+    every delivery unacked for its whole job (``cmd/downloader/
+    downloader.go:103-155``), so its torrent jobs hit that timeout.  The
+    lease is renewed every ``ttl / 2`` while the job runs.  If the worker
+    dies, the copy expires and dead-letters back to the shard queue, so the
+    job is run again.  ``ack`` / ``nack`` / ``retry`` of a leased delivery
+    act on the copy."""
 
     def __init__(self, client: "Client", msg: Message, generation: int) -> None:
         self.client = client
         self.msg = msg
         self.generation = generation
-        self.metadata = DeliveryMetadata(retries=_parse_retries(msg.properties.headers))
+        h = msg.properties.headers
+        self.metadata = DeliveryMetadata(retries=_parse_retries(h))
         self.settled = False
+        self.lease_return = _lease_expired(h)
+        self.lease_returns = _int_header(h, LEASE_RETURNS) + (1 if self.lease_return else 0)
+        self.busy = _int_header(h, BUSY)
+        self.lease: Lease | None = None
+        self.requeue_props: Properties | None = None   # what a requeue publishes (a park's retry headers)
+        self._hold: asyncio.Task | None = None
+        self._hold_timer: asyncio.TimerHandle | None = None
+        self._lock: asyncio.Lock | None = None
 
     @property
     def body(self) -> bytes:
@@ -120,28 +189,76 @@ class Delivery:
         return self.msg.redelivered
 
     @property
+    def maybe_duplicate(self) -> bool:
+        """Could this job have been run to the end already?  Redelivered
+        (an ack went nowhere), back from an expired lease, or handed back
+        because another worker was running it."""
+        return self.msg.redelivered or self.lease_return or self.busy > 0
+
+    @property
     def stale(self) -> bool:
-        """True once the channel it arrived on is gone (the broker requeued it)."""
+        """True once the broker has taken the job back: the channel it arrived
+        on is gone (the broker requeued it), or its lease ran out."""
+        if self.lease is not None:
+            return self.lease.lost
         return self.msg.channel is None or self.msg.channel.is_closed
 
     async def ack(self) -> bool:
         """``Ack`` (single, ``delivery.go:55-57``).  False if the ack could not
         be sent because the delivery's channel is gone (the broker requeues
-        it: it will be delivered again)."""
-        return await self._settle(lambda: self.msg.ack())
+        it: it will be delivered again), or because its lease had run out."""
+        return await self._settle(lambda: self.msg.ack(), lambda: self.client._lease_release(self))
 
     async def nack(self, requeue: bool = False) -> None:
         """``Nack`` (single, no requeue by default, ``delivery.go:60-62``)."""
-        await self._settle(lambda: self.msg.nack(requeue=requeue))
+        await self._settle(lambda: self.msg.nack(requeue=requeue),
+                           lambda: self.client._lease_release(self, requeue=requeue))
 
-    def retry_props(self, increment: int = 1) -> Properties:
+    def retry_props(self, increment: int = 1, *, busy: bool = False) -> Properties:
+        """Headers for the next copy of this job: ``X-Retries + increment``;
+        ``busy`` counts a hand-back in ``X-Busy`` (another worker runs the
+        job); lease returns so far are carried in ``X-Lease-Returns``."""
         hdrs = dict(self.msg.properties.headers or {})
         hdrs["X-Retries"] = self.metadata.retries + increment
         hdrs.pop("x-death", None)
+        hdrs.pop(LEASE_HOLDER, None)
+        if busy:
+            hdrs[BUSY] = self.busy + 1
+        else:
+            hdrs.pop(BUSY, None)
+        if self.lease_returns:
+            hdrs[LEASE_RETURNS] = self.lease_returns
         return Properties(headers=hdrs, delivery_mode=self.msg.properties.delivery_mode or codec.PERSISTENT,
                           content_type=self.msg.properties.content_type)
 
-    async def retry(self, delay: float | None = None, *, increment: int = 1) -> str:
+    def hold(self, after: float | None = None, ttl: float | None = None) -> None:
+        """Lease this delivery ``after`` seconds from now unless it is settled
+        by then, and renew the lease every ``ttl / 2`` until it is (defaults:
+        the client's ``lease_after`` / ``lease_ttl``; off when either is 0 or
+        the broker refused a lease queue for this routing key before)."""
+        after = self.client.lease_after if after is None else after
+        ttl = self.client.lease_ttl if ttl is None else ttl
+        if self._hold is not None or self._hold_timer is not None or self.settled or after <= 0 or ttl <= 0 or \
+                self.routing_key in self.client._lease_refused:
+            return
+        # a timer, not a task: most jobs settle long before it fires (no task per job)
+        self._hold_timer = asyncio.get_running_loop().call_later(after, self._start_hold, ttl)
+
+    def _start_hold(self, ttl: float) -> None:
+        self._hold_timer = None
+        if self.settled or self.client._closing:
+            return
+        holding = self.client._holding
+        holding.add(self)
+        self._hold = asyncio.ensure_future(self.client._hold(self, 0.0, ttl))
+        self._hold.add_done_callback(lambda _t: holding.discard(self))
+
+    def _settle_lock(self) -> asyncio.Lock:
+        if self._lock is None:
+            self._lock = asyncio.Lock()
+        return self._lock
+
+    async def retry(self, delay: float | None = None, *, increment: int = 1, busy: bool = False) -> str:
         """Reference ``Error()``: re-publish the same body with ``X-Retries + 1``
         after ``delay`` and ack (``delivery.go:66-84``).  Returns how: "now",
         "delay-queue" or "parked".
@@ -156,9 +273,10 @@ class Delivery:
         queue of that name with other arguments) the delivery is parked
         in-process instead (:meth:`Client.park`): the reference's own
         sleep-republish-ack, run as a task so the job slot is still free.
-        ``increment=0`` hands a delivery back without spending a retry."""
+        ``increment=0`` hands a delivery back without spending a retry
+        (``busy``: because another worker is running the same job)."""
         d = self.client.retry_delay if delay is None else delay
-        props = self.retry_props(increment)
+        props = self.retry_props(increment, busy=busy)
         if d > 0:
             log.info("retrying message in %s", durafmt(d))
             try:
@@ -173,17 +291,29 @@ class Delivery:
         await self.ack()
         return "now"
 
-    async def _settle(self, fn) -> bool:
-        if self.settled:
-            return False
-        if self.stale:
+    async def _settle(self, fn, leased_fn) -> bool:
+        # under the lease lock: a lease being taken or renewed finishes first, so the
+        # settlement acts on whichever of the original and the copy is the live one
+        async with self._settle_lock():
+            if self.settled:
+                return False
+            if self._hold_timer is not None:
+                self._hold_timer.cancel()
+                self._hold_timer = None
+            if self._hold is not None:
+                self._hold.cancel()      # between renewals (the lock is ours): nothing half-done
+            if self.lease is not None:
+                self.settled = True
+                self.client._leased.discard(self)
+                return await leased_fn()
+            if self.stale:
+                self.settled = True
+                log.with_field("delivery_tag", self.msg.delivery_tag).warn(
+                    "delivery's channel is gone; broker will redeliver it")
+                return False
+            await fn()
             self.settled = True
-            log.with_field("delivery_tag", self.msg.delivery_tag).warn(
-                "delivery's channel is gone; broker will redeliver it")
-            return False
-        await fn()
-        self.settled = True
-        return True
+            return True
 
 
 class Shard:
@@ -279,6 +409,15 @@ class Client:
         self.consumer_timeouts = 0                 # shard channels the broker closed for a late ack
         self.confirm_ewma: float | None = None     # publish -> broker confirm, seconds (EWMA, alpha 0.2)
         self._consumer_chans: list[Channel] = []
+        # leases (Delivery.hold): taken this long after a delivery arrives, TTL of the copy
+        # (renewed every ttl / 2); 0 = off, the delivery is held unacked as the reference did
+        self.lease_after = 0.0
+        self.lease_ttl = 0.0
+        self._lease_refused: set[str] = set()      # routing keys whose lease queues the broker refused
+        self._leased: set[Delivery] = set()        # leased deliveries not settled yet
+        self._holding: set[Delivery] = set()       # deliveries whose lease task runs (Delivery.hold)
+        self._ops_ch: Channel | None = None
+        self.lease_stats = {"taken": 0, "renewed": 0, "released": 0, "lost": 0, "requeued": 0, "refused": 0}
         self._closing = False
         self._bg: set[asyncio.Task] = set()
         self._connected = asyncio.Event()
@@ -738,7 +877,205 @@ class Client:
         flight are not counted against the new one until they settle (at most
         P - 1 extra, transiently)."""
         self.parked_total += 1
+        d.requeue_props = props
+        d.hold()                            # a long park must not sit unacked past consumer_timeout
         self._spawn_bg(self._parked_retry(d, props, delay, on_done))
+
+    # ------------------------------------------------------------ leases
+    def _lease_props(self, d: Delivery) -> Properties:
+        base = d.requeue_props or d.msg.properties
+        hdrs = dict(base.headers or {})
+        hdrs.pop("x-death", None)
+        hdrs[LEASE_HOLDER] = _HOLDER
+        if d.lease_returns:
+            hdrs[LEASE_RETURNS] = d.lease_returns
+        else:
+            hdrs.pop(LEASE_RETURNS, None)
+        return dataclasses.replace(base, headers=hdrs, delivery_mode=codec.PERSISTENT, expiration=None)
+
+    async def _ops(self) -> Channel:
+        """A plain channel for lease declares and deletes, kept open between
+        uses (a refusal closes it; the next use opens another)."""
+        ch = self._ops_ch
+        if ch is None or ch.is_closed or self.conn is None or ch.conn is not self.conn:
+            ch = self._ops_ch = await self._channel(qos=False)
+        return ch
+
+    async def _lease_put(self, d: Delivery, lease: Lease) -> str:
+        """Declare lease queue number ``lease.n`` and put the job's copy in it
+        (confirmed, mandatory).  :class:`LeaseRefused` when the broker will not
+        let this user have it (403/406 on the declare, or on the publish into
+        the default exchange)."""
+        name = f"{d.routing_key}.lease.{lease.token}.{lease.n}"
+        ms = max(1, int(round(lease.ttl * 1000)))
+        ch = await self._ops()
+        try:
+            # x-expires well past the TTL: the copy dead-letters first, then the empty queue goes
+            await ch.queue_declare(name, durable=True, arguments={
+                "x-message-ttl": ms, "x-expires": 2 * ms + 10_000,
+                "x-dead-letter-exchange": d.exchange, "x-dead-letter-routing-key": d.routing_key})
+        except ChannelClosed as e:
+            if _refused(e):
+                raise LeaseRefused(str(e)) from e
+            raise
+        async with self._pub_lock:
+            pub = await self._publisher()
+            confirm = await pub.basic_publish("", name, d.body, self._lease_props(d), mandatory=self.mandatory,
+                                              wait_confirm=False)
+        if confirm is not None:
+            try:
+                await confirm
+            except ChannelClosed as e:
+                if _refused(e):
+                    with contextlib.suppress(AMQPError, ConnectionError, OSError):
+                        await self._lease_drop(name)
+                    raise LeaseRefused(str(e)) from e
+                raise
+        return name
+
+    async def _lease_drop(self, name: str) -> int:
+        """Delete a lease queue; returns how many copies were still in it
+        (RabbitMQ discards them, it does not dead-letter on delete)."""
+        ch = await self._ops()
+        return await ch.queue_delete(name)
+
+    async def _lease_take(self, d: Delivery, ttl: float) -> bool:
+        lease = Lease(secrets.token_hex(6), ttl)
+        try:
+            lease.queue = await self._lease_put(d, lease)
+        except LeaseRefused as e:
+            self._lease_refused.add(d.routing_key)
+            self.lease_stats["refused"] += 1
+            log.with_fields(routing_key=d.routing_key, error=str(e)).warn(
+                "the broker refused a lease queue; holding deliveries unacked for the whole job instead (a job "
+                "longer than the broker's consumer_timeout will be requeued): grant configure on '<shard>.lease.*'")
+            return False
+        try:
+            if d.msg.channel is None or d.msg.channel.is_closed:
+                raise ChannelClosed(0, "delivery channel gone")
+            await d.msg.ack()
+        except (AMQPError, ConnectionError, OSError):
+            # the broker took the original back already (consumer timeout, channel error):
+            # the copy must not come back as a second job
+            with contextlib.suppress(AMQPError, ConnectionError, OSError):
+                await self._lease_drop(lease.queue)
+            return False
+        d.lease = lease
+        self._leased.add(d)
+        self.lease_stats["taken"] += 1
+        log.with_fields(queue=lease.queue, ttl_s=ttl).info("job leased: its delivery is acked, the broker holds a copy")
+        return True
+
+    async def _lease_renew(self, d: Delivery) -> None:
+        """Copy ``n + 1`` first, then delete copy ``n``: there is always a copy.
+        If copy ``n`` was gone, the lease had run out (a long broker outage)
+        and the job went back to its queue; the new copy is dropped too."""
+        lease = d.lease
+        assert lease is not None
+        old = lease.queue
+        lease.n += 1
+        try:
+            new = await self._lease_put(d, lease)
+        except BaseException:
+            with contextlib.suppress(BaseException):
+                await asyncio.wait_for(self._lease_drop(f"{d.routing_key}.lease.{lease.token}.{lease.n}"), 5.0)
+            raise
+        lease.queue = new
+        if await self._lease_drop(old) == 0:
+            lease.lost = True
+            self.lease_stats["lost"] += 1
+            log.with_fields(queue=old).error("job lease ran out before it was renewed; the job went back to its "
+                                             "queue and may run twice")
+            with contextlib.suppress(AMQPError, ConnectionError, OSError):
+                await self._lease_drop(new)
+            self._leased.discard(d)
+            return
+        lease.renewed_at = time.monotonic()
+        self.lease_stats["renewed"] += 1
+
+    async def _lease_release(self, d: Delivery, requeue: bool = False) -> bool:
+        """Settle a leased delivery: with ``requeue`` the job goes back to its
+        queue now (a graceful shutdown), then the lease copy is deleted.  False
+        when the lease had already run out (the job went back on its own)."""
+        lease = d.lease
+        assert lease is not None
+        if lease.lost:
+            return False
+        if requeue:
+            try:
+                await self.publish_raw(d.exchange, d.routing_key, d.body, d.requeue_props or d.retry_props(0),
+                                       max_attempts=3)
+            except Exception as e:  # noqa: BLE001 - the lease copy stays: it comes back when it expires
+                log.with_fields(error=str(e), queue=lease.queue).warn("could not requeue a leased job; it comes "
+                                                                     "back when its lease runs out")
+                return False
+            self.lease_stats["requeued"] += 1
+        pol = ExponentialBackoff(initial=0.05, max_interval=2.0, max_elapsed=None)
+        while True:
+            try:
+                n = await self._lease_drop(lease.queue)
+                break
+            except (AMQPError, ConnectionError, OSError) as e:
+                if time.monotonic() - lease.renewed_at > lease.ttl or (self._closing and not requeue):
+                    n = 0                    # ran out meanwhile: the broker has given the job back
+                    break
+                d2 = pol.next_delay() or 1.0
+                log.with_fields(error=str(e), queue=lease.queue).warn("releasing the job lease failed; retrying")
+                await asyncio.sleep(d2)
+        if n == 0:
+            lease.lost = True
+            self.lease_stats["lost"] += 1
+            if not requeue:
+                log.with_fields(queue=lease.queue).error("job lease had run out; the job went back to its queue")
+            return False
+        self.lease_stats["released"] += 1
+        return True
+
+    async def _hold(self, d: Delivery, after: float, ttl: float) -> None:
+        """Take ``d``'s lease after ``after`` s, then renew it every ``ttl / 2``
+        until it is settled.  Every step runs under the delivery's settle lock
+        and retries outside it, so an ack never waits on an outage."""
+        try:
+            await asyncio.sleep(after)
+            pol = ExponentialBackoff(initial=0.2, max_interval=5.0, max_elapsed=None)
+            while True:
+                async with d._settle_lock():
+                    if d.settled or d.stale or self._closing or d.routing_key in self._lease_refused:
+                        return
+                    try:
+                        if not await self._lease_take(d, ttl):
+                            return
+                        break
+                    except (AMQPError, ConnectionError, OSError) as e:
+                        log.with_field("error", str(e)).warn("taking a job lease failed; retrying")
+                await asyncio.sleep(pol.next_delay() or 1.0)
+            pol.reset()
+            wait = ttl / 2
+            while True:
+                await asyncio.sleep(wait)
+                async with d._settle_lock():
+                    if d.settled or d.lease is None or d.lease.lost or self._closing:
+                        return
+                    try:
+                        await self._lease_renew(d)
+                        wait = ttl / 2
+                        pol.reset()
+                    except (AMQPError, ConnectionError, OSError) as e:
+                        wait = min(ttl / 4, pol.next_delay() or 1.0)
+                        log.with_field("error", str(e)).warn("renewing a job lease failed; retrying in %.1fs", wait)
+        except asyncio.CancelledError:
+            pass
+
+    async def _release_leases(self) -> None:
+        """Shutdown: every held delivery stops renewing; a leased one that is
+        not settled goes back to its queue at once (not after its TTL)."""
+        for d in list(self._holding):
+            async with d._settle_lock():
+                if d._hold is not None:
+                    d._hold.cancel()
+            if d.lease is not None and not d.settled:
+                with contextlib.suppress(Exception):
+                    await asyncio.wait_for(d.nack(requeue=True), 10.0)
 
     def _shard_of(self, ch: Channel | None) -> Shard | None:
         for sh in self.shards.values():
@@ -842,7 +1179,7 @@ class Client:
     async def _parked_retry(self, d: Delivery, props: Properties, delay: float, on_done=None) -> None:
         self._parked += 1
         try:
-            shard = self._shard_of(d.msg.channel)
+            shard = self._shard_of(d.msg.channel) if d.lease is None else None
             if shard is not None and d.msg.consumer_tag:
                 try:
                     await self._rotate(shard, d.msg.consumer_tag)
@@ -956,8 +1293,14 @@ class Client:
 
     # ------------------------------------------------------------ shutdown
     async def close(self) -> None:
-        """Stop consuming and close the connection (``Done`` semantics)."""
+        """Stop consuming and close the connection (``Done`` semantics).
+        Leased jobs still running go back to their queues first."""
+        if self._holding and self.connected:
+            await self._release_leases()
         self._closing = True
+        for d in list(self._holding):
+            if d._hold is not None:
+                d._hold.cancel()
         self._lost.set()
         if self._supervisor is not None:
             self._supervisor.cancel()

@@ -31,6 +31,9 @@ from .codec import AMQPError, Method, Properties
 
 DeliverCallback = Callable[["Message"], Any]
 
+# private header that matches a basic.return to its mandatory publish
+RETURN_CORRELATION = "x-tdl-seq"
+
 
 class ConnectionClosed(AMQPError):
     def __init__(self, code: int = 0, text: str = "connection closed") -> None:
@@ -439,13 +442,13 @@ class Channel:
         self._closed_exc: AMQPError | None = None
         self.confirm_mode = False
         self._pub_seq = 0
-        self._mid_seq = 0
         self._mid_base = f"{os.getpid():x}.{id(self) & 0xffffff:x}"
         self._unconfirmed: dict[int, asyncio.Future] = {}
-        # mandatory publishes in confirm mode: seq -> message_id, and the returns seen for
-        # them (RabbitMQ sends basic.return before the basic.ack of the same message; an
-        # unroutable message is confirmed at once, possibly ahead of routable ones still
-        # being persisted, so returns are matched by message_id, not by order)
+        # mandatory publishes in confirm mode: seq -> correlation id (RETURN_CORRELATION
+        # header), and the returns seen for them (RabbitMQ sends basic.return before the
+        # basic.ack of the same message; an unroutable message is confirmed at once, possibly
+        # ahead of routable ones still being persisted, so returns are matched by that id,
+        # not by order)
         self._mandatory_ids: dict[int, str] = {}
         self._returned: dict[str, PublishReturned] = {}
         self.on_return: Callable[[Message], Any] | None = None
@@ -499,8 +502,8 @@ class Channel:
             if self._get_waiter and not self._get_waiter.done():
                 self._get_waiter.set_result(msg)
         elif m.name == "basic.return":
-            mid = msg.properties.message_id
-            if mid and mid in self._mandatory_ids.values():
+            mid = (msg.properties.headers or {}).get(RETURN_CORRELATION)
+            if isinstance(mid, str) and mid in self._mandatory_ids.values():
                 self._returned[mid] = PublishReturned(m.args.get("reply_code", 0), m.args.get("reply_text", ""),
                                                       m.args.get("exchange", ""), m.args.get("routing_key", ""))
             if self.on_return:
@@ -692,12 +695,14 @@ class Channel:
         self._check()
         mid = None
         if mandatory and self.confirm_mode:
+            # correlate a basic.return with its publish by a private header carrying this
+            # channel's publish sequence number; the producer's message_id is left alone (two
+            # in-flight publishes may share one: parked, handed-back and dead-letter copies)
             props = properties or Properties()
-            mid = props.message_id
-            if not mid:
-                self._mid_seq += 1
-                mid = f"tdl-{self._mid_base}-{self._mid_seq}"
-                properties = dataclasses.replace(props, message_id=mid)
+            mid = f"{self._mid_base}.{self._pub_seq + 1}"
+            hdrs = dict(props.headers or {})
+            hdrs[RETURN_CORRELATION] = mid
+            properties = dataclasses.replace(props, headers=hdrs)
         frames = codec.content_frames(self.id, Method("basic.publish", {
             "exchange": exchange, "routing_key": routing_key, "mandatory": mandatory, "immediate": immediate}),
             body, properties or Properties(), self.conn.frame_max or codec.DEFAULT_FRAME_MAX)

@@ -67,11 +67,9 @@ Differences, all documented fixes:
 from __future__ import annotations
 
 import asyncio
-import collections
 import contextlib
 import contextvars
 import fcntl
-import hashlib
 import os
 import queue
 import shutil
@@ -88,7 +86,7 @@ from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
 from .s3.uploader import RESUME_SUFFIX, UploadError, Uploader
 from .select import MEDIA_EXTS, dir_media, predict_media
-from .utils import rawhttp, spares
+from .utils import ledger as jobdir, rawhttp, spares
 from .utils.config import Config
 from .utils.gocompat import go_ext, go_join, go_time_string
 from .utils.log import log
@@ -233,6 +231,9 @@ def _pid_alive(pid: int) -> bool:
     return True
 
 
+TRASH_GRACE_S = 3600.0
+
+
 def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset = frozenset(),
                          now: float | None = None) -> list[str]:
     """Job dirs under ``base`` that nothing has touched for ``max_age_s``, and
@@ -241,7 +242,14 @@ def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset
     (``flock``, :meth:`Service._job_lock`) is never taken.  These are the
     partial downloads of jobs that will not come back: their message was
     purged, or another node finished them.  The reference's work dir only
-    ever grew."""
+    ever grew.
+
+    Only dirs a worker made are swept: they carry a run marker
+    (:mod:`tritondl.utils.ledger`).  Anything else in ``DOWNLOAD_DIR`` (an
+    operator's data, finished downloads a reference deployment kept) is left
+    alone.  A trash dir whose pid is alive is skipped only while it was
+    touched within ``TRASH_GRACE_S``: workers in other containers sharing
+    the dir have other pid namespaces."""
     now = time.time() if now is None else now
     out: list[str] = []
     try:
@@ -258,8 +266,14 @@ def sweep_stale_job_dirs(base: str, max_age_s: float, skip: set[str] | frozenset
                 trash_pid = int(name.rsplit(".deleting-", 1)[1].split("-", 1)[0])
             except ValueError:
                 continue
-            if _pid_alive(trash_pid):
+            try:
+                fresh = now - os.lstat(path).st_mtime < TRASH_GRACE_S
+            except OSError:
+                continue
+            if _pid_alive(trash_pid) and fresh:
                 continue                              # its worker's reaper is on it
+        elif not jobdir.is_ours(path):
+            continue                                  # not made by a worker
         try:
             fd = os.open(path, os.O_RDONLY | os.O_DIRECTORY)
         except OSError:
@@ -318,10 +332,11 @@ class Service:
         self._stall_since: float | None = None     # free slot + ready backlog, continuously since
         self._backlog = (0.0, 0)                   # (monotonic time polled, ready messages on the shards)
         self._backlog_task: asyncio.Task | None = None
-        # jobs this worker finished whose ack was lost with its channel (the broker's consumer
-        # timeout, a channel error): body digest -> monotonic time.  Their redelivery is acked
-        # without running the job again (it was uploaded and its v1.convert published)
-        self._done_unacked: collections.OrderedDict[bytes, float] = collections.OrderedDict()
+        # jobs this node finished (shared by the workers on one DOWNLOAD_DIR): a copy of one
+        # that comes back (a lost ack, a lease that ran out, a busy hand-back) is acked without
+        # running the job again (it was uploaded and its v1.convert published)
+        self.ledger: jobdir.DoneLedger | None = None
+        self._housekeeper: asyncio.Task | None = None
         self.metrics.collectors.append(self._collect_gauges)
 
     @contextlib.asynccontextmanager
@@ -332,14 +347,23 @@ class Service:
         another worker whose channel died mid-job, or concurrency > 1 — would
         otherwise truncate and rewrite the very file the first delivery is
         uploading from (and the send pump maps that file).  The second
-        delivery waits (see :meth:`_lock_dir`), then finds the file complete
-        and re-uploads it (at-least-once, as the reference)."""
+        delivery waits at most ``job_lock_wait_s`` (the first one's commit may
+        be ending), then raises :class:`JobBusy` and goes back to the broker:
+        an idle slot is never pinned for the length of someone else's run."""
         ent = self._id_locks.setdefault(media_id, [asyncio.Lock(), 0])
         ent[1] += 1
         fd = -1
         d = ""
+        lock: asyncio.Lock = ent[0]
         try:
-            async with ent[0]:
+            if lock.locked():
+                try:
+                    await asyncio.wait_for(lock.acquire(), max(0.0, self.cfg.job_lock_wait_s))
+                except asyncio.TimeoutError:
+                    raise JobBusy(f"job {media_id} is running in another slot of this worker") from None
+            else:
+                await lock.acquire()
+            try:
                 try:
                     d = self.dispatcher.job_dir(media_id) if self.dispatcher is not None else ""
                 except ValueError:
@@ -351,6 +375,8 @@ class Service:
                     except OSError as e:
                         log.with_fields(media_id=media_id, error=str(e)).warn("job lock unavailable")
                 yield
+            finally:
+                lock.release()
         finally:
             self._locked_dirs.discard(d)
             if fd >= 0:
@@ -458,9 +484,12 @@ class Service:
             self.amqp.set_prefetch(cfg.prefetch)
             if not self.amqp.connected:
                 await self.amqp.connect()
+        self.amqp.lease_after = cfg.lease_after_s
+        self.amqp.lease_ttl = cfg.lease_s
         if self.dispatcher is None:
             self.dispatcher = Dispatcher(cfg.download_dir, default_impls(cfg), cfg.progress_log_interval_s)
         self.dispatcher.start()
+        self.ledger = jobdir.DoneLedger(self.dispatcher.base_dir)
         if cfg.cleanup and cfg.recycle_bytes > 0:
             base = self.dispatcher.base_dir
             for stale in spares.stale_pools(base):
@@ -488,6 +517,7 @@ class Service:
             self._janitor = asyncio.ensure_future(self._sweep_stale(cfg.stale_job_days * 86400.0))
         if cfg.handback_s > 0:
             self._handback = asyncio.ensure_future(self._handback_loop(cfg.handback_s))
+        self._housekeeper = asyncio.ensure_future(self._housekeeping())
         for i in range(max(1, cfg.concurrency)):
             self._workers.append(asyncio.ensure_future(self._worker(i)))
 
@@ -508,6 +538,23 @@ class Service:
                     continue
                 if n:
                     self.metrics.inc("jobs_handed_back", n)
+
+    async def _housekeeping(self, period: float = 3600.0) -> None:
+        """Hourly: drop done-ledger entries past their TTL."""
+        loop = asyncio.get_running_loop()
+        try:
+            while True:
+                await asyncio.sleep(period)
+                if self.ledger is not None:
+                    try:
+                        n = await loop.run_in_executor(None, self.ledger.sweep)
+                    except Exception as e:  # noqa: BLE001 - housekeeping must not end the worker
+                        log.with_field("error", str(e)).warn("done-ledger sweep failed")
+                        continue
+                    if n:
+                        self.metrics.inc("done_ledger_swept", n)
+        except asyncio.CancelledError:
+            pass
 
     async def _sweep_stale(self, max_age_s: float, period: float = 3600.0) -> None:
         """At start and every ``period`` s: delete job dirs untouched for
@@ -644,6 +691,7 @@ class Service:
         """Process one delivery end-to-end; always settles it."""
         t0 = time.monotonic()
         rawhttp.trace("job_start")
+        msg.hold()                  # leased if the job outlives lease_after_s (Client.lease_after)
         if msg.metadata.retries > self.cfg.max_retries:
             # it has run max_retries + 1 times and the dead-letter publish failed after the last
             # one (it was parked with X-Retries past the budget): never download it again
@@ -669,15 +717,20 @@ class Service:
             log.with_field("job", job.to_dict()).info("got message")
         try:
             async with self._job_lock(job.media.id):
-                if msg.redelivered and self._already_done(msg.body):
-                    # the first delivery finished here, but its ack went nowhere: its channel was
-                    # closed under it (consumer_timeout, a channel error) and the broker requeued it
-                    log.with_field("media_id", job.media.id).warn(
-                        "redelivered job was already completed by this worker (its ack was lost); acking it")
+                if msg.maybe_duplicate and self.ledger is not None and self.ledger.has(msg.body):
+                    # a worker on this node finished this job, and this copy came back anyway: its
+                    # ack went nowhere (consumer_timeout, a channel error), its lease ran out, or
+                    # it was handed back while the job ran
+                    log.with_fields(media_id=job.media.id, redelivered=msg.redelivered,
+                                    lease_return=msg.lease_return, busy=msg.busy).warn(
+                        "job was already completed on this node; acking the copy without running it")
                     await msg.ack()
+                    self._reap_job_dir(job.media.id, msg)    # the empty dir the job lock made
                     self.metrics.inc("jobs", status="duplicate")
                     return self._record(JobResult(True, "duplicate", seconds=time.monotonic() - t0))
-                if msg.redelivered and self.cfg.redelivery_limit > 0:
+                if msg.lease_return:
+                    self.metrics.inc("lease_returns")
+                if (msg.redelivered or msg.lease_returns) and self.cfg.redelivery_limit > 0:
                     n = self._count_redelivery(job.media.id, msg)
                     if n > self.cfg.redelivery_limit:
                         log.with_fields(media_id=job.media.id, redeliveries=n).error(
@@ -688,21 +741,33 @@ class Service:
                                                    RuntimeError(f"redelivered {n} times without an ack")):
                             self._reap_job_dir(job.media.id, msg)
                         self._clear_redeliveries(job.media.id)
+                        with contextlib.suppress(ValueError, OSError):
+                            jobdir.mark_ended(self.dispatcher.job_dir(job.media.id))
                         return self._record(JobResult(False, "redelivery-limit", f"redelivered {n} times",
                                                       seconds=time.monotonic() - t0))
                 rawhttp.trace("job_locked")
                 return await self._run_job(msg, job, t0)
         except JobBusy as e:
-            # not the job's failure: hand it back without spending a retry
-            log.with_field("media_id", job.media.id).warn("%s; handing the delivery back", e)
+            # not the job's failure: hand it back without spending a retry, after a delay that
+            # doubles per hand-back (X-Busy), so a copy of a long job costs a broker round trip
+            # now and then, not an idle slot for the whole run
+            delay = self.busy_delay(msg.busy)
+            log.with_fields(media_id=job.media.id, delay_s=delay, busy=msg.busy + 1).warn(
+                "%s; handing the delivery back", e)
             self.metrics.inc("jobs", status="busy")
             try:
-                await msg.retry(max(self.cfg.retry_delay_s, 1.0), increment=0)
+                await msg.retry(delay, increment=0, busy=True)
             except Exception as e2:  # noqa: BLE001
                 log.with_field("error", str(e2)).error("failed to hand a busy job back; parking it")
                 if not (msg.settled or msg.stale):
-                    self.amqp.park(msg, msg.retry_props(0), self.cfg.retry_delay_max_s)
+                    self.amqp.park(msg, msg.retry_props(0, busy=True), max(delay, self.cfg.retry_delay_max_s))
             return self._record(JobResult(False, "lock", str(e), seconds=time.monotonic() - t0))
+
+    def busy_delay(self, busy: int) -> float:
+        """Delay before hand-back number ``busy + 1`` of a job another worker
+        runs: max(1 s, ``retry_delay_s``) doubling, capped at ``retry_delay_max_s``."""
+        base = max(1.0, self.cfg.retry_delay_s)
+        return min(max(base, self.cfg.retry_delay_max_s), base * 2.0 ** min(max(0, busy), 30))
 
     async def _run_job(self, msg: Delivery, job: Download, t0: float) -> JobResult:
         stage = "download"
@@ -712,6 +777,21 @@ class Service:
         def mark(name: str) -> None:
             marks[name] = time.monotonic() - t0
 
+        # a run is in progress in the job dir until it settles: a dir still marked after its
+        # lock is free was left by a worker that died mid-job (see _count_redelivery)
+        jd = ""
+        returned = msg.redelivered or msg.lease_returns > 0
+        try:
+            jd = self.dispatcher.job_dir(job.media.id) if self.dispatcher is not None else ""
+        except ValueError:
+            pass
+        if jd and jd in self._locked_dirs:
+            try:
+                jobdir.mark_running(jd)
+            except OSError:
+                jd = ""
+        else:
+            jd = ""
         try:
             assert self.dispatcher is not None and self.uploader is not None and self.amqp is not None
             t = time.monotonic()
@@ -744,27 +824,42 @@ class Service:
             stage = "ack"
             if log.enabled("info"):
                 log.with_field("job", job.to_dict()).info("finished processing")
-            if not await msg.ack():
-                self._note_done_unacked(msg.body)
+            if self.ledger is not None:
+                # before the ack: a copy that comes back (the ack lost with its channel, a busy
+                # hand-back by another worker on this node) is acked instead of run again
+                try:
+                    self.ledger.add(msg.body)
+                except OSError as e:
+                    log.with_field("error", str(e)).warn("could not record the finished job")
+            await msg.ack()
             mark("ack")
-            if msg.redelivered:
+            if returned:
                 self._clear_redeliveries(job.media.id)
         except asyncio.CancelledError:
+            if jd:
+                jobdir.mark_ended(jd)         # shutdown interrupted the run: not a crash
             raise
         except Exception as e:  # noqa: BLE001 - any stage failure must settle the message
             if isinstance(e, UploadError):
                 stage = "upload"             # a streamed upload fails inside the download stage
             log.with_fields(stage=stage, error=str(e)).error("job failed")
             self.metrics.inc("jobs", status="failed", stage=stage)
-            if msg.redelivered:
+            if returned:
                 self._clear_redeliveries(job.media.id)   # a failure handled here is X-Retries' business
+            if jd:
+                jobdir.mark_ended(jd)
             if await self._dispose_failed(msg, stage, e):
                 self._reap_job_dir(job.media.id, msg)     # dead-lettered: no retry will resume it
             return self._record(JobResult(False, stage, str(e), seconds=time.monotonic() - t0))
         if self.cfg.cleanup:
-            # a streamed single-file job left exactly its file (the .part.meta is gone)
+            # a streamed single-file job left exactly its file (the .part.meta is gone) and
+            # the run marker
             names = [os.path.basename(p) for p in streamed] if len(streamed) == 1 and len(files) == 1 else None
+            if names is not None and jd:
+                names.append(jobdir.RUNNING)
             self._reap_job_dir(dl_dir, msg, is_path=True, names=names)
+        elif jd:
+            jobdir.mark_ended(jd)
         dt = time.monotonic() - t0
         self.metrics.inc("jobs", status="ok")
         self.metrics.inc("bytes_uploaded", nbytes)
@@ -973,50 +1068,44 @@ class Service:
             trash = d
         self._reaper.submit(trash, names)
 
-    _DONE_TTL_S = 24 * 3600.0
-    _DONE_MAX = 4096
-
-    def _note_done_unacked(self, body: bytes) -> None:
-        self._done_unacked[hashlib.sha256(body).digest()] = time.monotonic()
-        while len(self._done_unacked) > self._DONE_MAX:
-            self._done_unacked.popitem(last=False)
-
-    def _already_done(self, body: bytes) -> bool:
-        now = time.monotonic()
-        while self._done_unacked:
-            k, t = next(iter(self._done_unacked.items()))
-            if now - t <= self._DONE_TTL_S:
-                break
-            self._done_unacked.popitem(last=False)
-        return self._done_unacked.pop(hashlib.sha256(body).digest(), None) is not None
-
     _REDELIVERIES = ".tritondl-redeliveries"
 
     def _count_redelivery(self, media_id: str, msg: Delivery) -> int:
-        """Count one more unacknowledged return of this job: a small file in its
-        job dir (the dir survives a crashed worker, and every worker sharing
-        ``downloading/`` sees it), or RabbitMQ's ``x-delivery-count`` header
-        (quorum queues), whichever is higher.  Only redelivered deliveries
-        touch the file, so the first delivery of a job costs nothing."""
-        hdr = (msg.msg.properties.headers or {}).get("x-delivery-count")
-        n_hdr = hdr if isinstance(hdr, int) and not isinstance(hdr, bool) else 0
-        n = 0
+        """How many times this job came back from a run that died: the larger
+        of a count kept in its job dir (it survives a crashed worker, and every
+        worker sharing ``downloading/`` sees it) and the lease returns carried
+        in ``X-Lease-Returns`` (a lease runs out only when its holder stopped
+        renewing it, on any node).
+
+        The dir count goes up only when the previous run left its
+        ``.tritondl-running`` marker (:mod:`tritondl.utils.ledger`): the run
+        started and never settled.  A delivery that comes back because of a
+        graceful shutdown, a broker or connection restart, or a prefetched
+        delivery that never started, is not counted.  RabbitMQ's
+        ``x-delivery-count`` (quorum queues) counts all of those too, so it
+        is used only next to a crash marker.  Called only for returned
+        deliveries, so a job's first delivery costs nothing."""
         try:
-            path = os.path.join(self.dispatcher.job_dir(media_id), self._REDELIVERIES)
+            d = self.dispatcher.job_dir(media_id)
         except (ValueError, AttributeError):
-            return n_hdr
+            return msg.lease_returns
+        path = os.path.join(d, self._REDELIVERIES)
         try:
             with open(path) as f:
                 n = int(f.read().strip() or 0)
         except (OSError, ValueError):
             n = 0
-        n += 1
-        try:
-            with open(path, "w") as f:
-                f.write(str(n))
-        except OSError:
-            pass
-        return max(n, n_hdr)
+        if jobdir.was_running(d):
+            n += 1
+            try:
+                with open(path, "w") as f:
+                    f.write(str(n))
+            except OSError:
+                pass
+            hdr = (msg.msg.properties.headers or {}).get("x-delivery-count")
+            if isinstance(hdr, int) and not isinstance(hdr, bool):
+                n = max(n, hdr)
+        return max(n, msg.lease_returns)
 
     def _clear_redeliveries(self, media_id: str) -> None:
         try:
@@ -1039,6 +1128,9 @@ class Service:
             lost = self.amqp.lost_since
             m.set("broker_down_seconds", 0.0 if lost is None else round(now - lost, 3))
             m.set("consumers_paused", 1.0 if self.amqp.paused else 0.0)
+            m.set("leases_held", len(self.amqp._leased))
+            for kind, v in self.amqp.lease_stats.items():
+                m.set("lease_events", v, kind=kind)
             for q, sh in self.amqp.shards.items():
                 m.set("consumer_active", 1.0 if sh.active else 0.0, queue=q)
 
@@ -1086,7 +1178,7 @@ class Service:
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
         self._stop.set()
-        for t in (self._trimmer, self._janitor, self._handback):
+        for t in (self._trimmer, self._janitor, self._handback, self._housekeeper):
             if t is not None:
                 t.cancel()
         t_end = time.monotonic() + grace

@@ -60,7 +60,7 @@ ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_time
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
               "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s",
               "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms", "STALE_JOB_DAYS": "stale_job_days",
-              "HANDBACK": "handback_s"}
+              "HANDBACK": "handback_s", "LEASE_AFTER": "lease_after_s", "LEASE": "lease_s"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -157,9 +157,21 @@ class Config:
     # (partial downloads of jobs whose message was purged or finished elsewhere) are
     # deleted, at start and hourly; 0 = never (the reference's work dir only grew)
     stale_job_days: float = 7.0
-    # a delivery whose job dir another worker holds waits this long, then goes back to
-    # the broker (same X-Retries) instead of pinning the job slot
-    job_lock_wait_s: float = 60.0
+    # a delivery whose job another worker (or another slot of this one) is running waits
+    # this long for it, then goes back to the broker (same X-Retries, X-Busy + 1) after a
+    # delay that doubles per hand-back from max(1 s, retry_delay_s) up to retry_delay_max_s,
+    # instead of pinning an idle job slot for the whole run
+    job_lock_wait_s: float = 0.5
+    # job leases (amqp.client.Delivery.hold): a job still running this long after its
+    # delivery arrived has its delivery acked and a copy kept by the broker in a per-job
+    # lease queue instead, renewed every lease_s / 2.  RabbitMQ closes the channel of a
+    # delivery left unacked past its consumer_timeout (30 min by default) and requeues it,
+    # so another worker would download the job again.  A worker that dies stops renewing:
+    # its copy expires after lease_s and goes back to the shard queue.  Needs configure on
+    # '<shard>.lease.*' (refused: the delivery is held unacked, the reference's way);
+    # 0 = off
+    lease_after_s: float = 30.0
+    lease_s: float = 300.0
     # /healthz answers 503 once the broker connection, or the consumer of any shard queue,
     # has been down this long (the supervisor / shard re-subscribe loops keep retrying)
     health_down_s: float = 30.0

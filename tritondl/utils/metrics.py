@@ -139,6 +139,10 @@ HELP = {
     "pool_workers_unhealthy": "pool: running workers whose own /healthz answered 503 (or not at all) at the last probe",
     "pool_worker_restarts_total": "pool: worker restarts by rank",
     "uptime_seconds": "seconds since the process's metrics started",
+    "lease_returns_total": "jobs that came back because the lease of the worker running them ran out",
+    "done_ledger_swept_total": "done-ledger entries removed past their TTL",
+    "leases_held": "leased deliveries (job running, copy held by the broker) not settled yet",
+    "lease_events": "job lease operations since start by kind (taken, renewed, released, lost, requeued, refused)",
 }
 
 

@@ -78,6 +78,7 @@ class Queue:
     rr: int = 0
     owner: Any = None
     delivered_total: int = 0
+    last_used: float = field(default_factory=time.monotonic)   # x-expires: declare, consume, get
 
 
 @dataclass
@@ -561,6 +562,7 @@ class Broker:
                 self._dispatch(self.queues[name])
 
     def _remove_consumer(self, cons: _Consumer) -> None:
+        cons.queue.last_used = time.monotonic()
         if cons in cons.queue.consumers:
             cons.queue.consumers.remove(cons)
         cons.ch.consumers.pop(cons.tag, None)
@@ -714,7 +716,13 @@ class Broker:
                 ok("queue.purge_ok", message_count=cnt)
         elif n == "queue.delete":
             self._check(c, "configure", "queue", a["queue"], m)
-            q = self._get_queue(a["queue"], m)
+            q = self.queues.get(a["queue"])
+            if q is None:
+                # RabbitMQ: deleting a queue that does not exist succeeds (rabbit_channel
+                # answers delete_ok with message_count 0)
+                if not a["nowait"]:
+                    ok("queue.delete_ok", message_count=0)
+                return
             cnt = len(q.messages)
             for cons in list(q.consumers):
                 cons.ch.conn.send_method(cons.ch.id, Method("basic.cancel", {"consumer_tag": cons.tag}))
@@ -759,6 +767,7 @@ class Broker:
         elif n == "basic.get":
             self._check(c, "read", "queue", a["queue"], m)
             q = self._get_queue(a["queue"], m)
+            q.last_used = time.monotonic()
             if not q.messages:
                 ok("basic.get_empty")
             else:
@@ -828,11 +837,38 @@ class Broker:
                     (q.arguments or {}) != (a["arguments"] or {}):
                 raise ChannelError(codec.PRECONDITION_FAILED,
                                    f"PRECONDITION_FAILED - inequivalent arg for queue '{name}'", m.ids)
+            q.last_used = time.monotonic()
             return q
         q = Queue(name, a["durable"], a["exclusive"], a["auto_delete"], a["arguments"] or {},
                   owner=c if a["exclusive"] else None)
         self.queues[name] = q
+        exp = q.arguments.get("x-expires")
+        if isinstance(exp, int) and not isinstance(exp, bool) and exp > 0:
+            self._schedule_queue_expiry(q, exp / 1000.0)
         return q
+
+    def _schedule_queue_expiry(self, q: Queue, after: float) -> None:
+        try:
+            asyncio.get_running_loop().call_later(after, self._expire_queue, q)
+        except RuntimeError:
+            pass
+
+    def _expire_queue(self, q: Queue) -> None:
+        """RabbitMQ's ``x-expires``: a queue with no consumers that nobody has
+        declared or polled for that long is deleted, and its messages are
+        discarded (not dead-lettered)."""
+        if self.queues.get(q.name) is not q:
+            return
+        ttl = q.arguments["x-expires"] / 1000.0
+        idle = time.monotonic() - q.last_used
+        if q.consumers or idle < ttl:
+            self._schedule_queue_expiry(q, ttl if q.consumers else ttl - idle)
+            return
+        self.queues.pop(q.name, None)
+        for ex in self.exchanges.values():
+            ex.bindings = [b for b in ex.bindings if b[0] != q.name]
+        self.stats["queues_expired"] += 1
+        self.stats["expired_discarded"] += len(q.messages)
 
     def _get_queue(self, name: str, m: Method) -> Queue:
         q = self.queues.get(name)
