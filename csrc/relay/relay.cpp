@@ -84,12 +84,14 @@ PYBIND11_MODULE(_relay, m) {
       .def_property_readonly("failed", &Flow::failed)
       .def_property_readonly("finished", &Flow::finished)
       .def_property_readonly("error", &Flow::error)
+      .def_property("stall", &Flow::stall, &Flow::set_stall,
+                    "seconds without progress after which readers waiting for bytes give up (0 = never)")
       .def("wait_covered", [](Flow& f, uint64_t a, uint64_t b, double timeout) {
              py::gil_scoped_release nogil;
              return f.wait_covered(a, b, timeout);
            },
            py::arg("start"), py::arg("end"), py::arg("timeout"),
-           "0 = on disk, 1 = failed/cancelled, 2 = timeout, 3 = download ended short");
+           "0 = on disk, 1 = failed/cancelled, 2 = timeout, 3 = download ended short, 4 = stalled");
 
   py::class_<Stream, std::shared_ptr<Stream>>(m, "Stream")
       .def("abort", &Stream::abort, "stop any pump running on this stream (sticky; the fd stays open)")

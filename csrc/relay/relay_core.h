@@ -80,9 +80,27 @@ class Flow {
     uint64_t start;
     int64_t end;  // exclusive; < 0 = unknown length
     uint64_t done;
+    Clock::time_point moved{};  // last advance (stall detection)
   };
 
-  explicit Flow(std::vector<Seg> segs) : segs_(std::move(segs)) {}
+  explicit Flow(std::vector<Seg> segs) : segs_(std::move(segs)) {
+    const auto now = Clock::now();
+    for (Seg& s : segs_) s.moved = now;
+  }
+
+  // A reader waiting for bytes gives up with rc 4 ("stalled") once no segment
+  // it needs has advanced for this long (0 = never).  An upload that follows
+  // the download must not sit idle on its PUT past the store's request
+  // timeout (S3 drops a body that sends nothing for ~20 s with 400
+  // RequestTimeout); the caller falls back to uploading after the download.
+  void set_stall(double s) {
+    std::lock_guard<std::mutex> l(mu_);
+    stall_s_ = s;
+  }
+  double stall() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return stall_s_;
+  }
 
   // Wakes exactly the waiters whose range became covered: the upload's chunk
   // hashers wait for ranges ahead of the receive frontier, and waking all of
@@ -94,7 +112,10 @@ class Flow {
   void advance(size_t seg, uint64_t done) {
     std::lock_guard<std::mutex> l(mu_);
     if (seg >= segs_.size()) return;
-    if (done > segs_[seg].done) segs_[seg].done = done;
+    if (done > segs_[seg].done) {
+      segs_[seg].done = done;
+      segs_[seg].moved = Clock::now();
+    }
     for (Waiter* w : waiters_)
       if (!w->woken && covered_locked(w->a, w->b)) {
         w->woken = true;
@@ -220,12 +241,13 @@ class Flow {
   }
 
   // 0 = [a, b) is on disk, 1 = flow failed/cancelled, 2 = timed out,
-  // 3 = the download finished short of b.
+  // 3 = the download finished short of b, 4 = stalled (see set_stall).
   int wait_covered(uint64_t a, uint64_t b, double timeout_s, const std::atomic<bool>* abort = nullptr) {
     std::unique_lock<std::mutex> l(mu_);
     if (covered_locked(a, b)) return 0;
-    const auto deadline = Clock::now() + std::chrono::duration_cast<Clock::duration>(
-                                             std::chrono::duration<double>(std::max(0.0, timeout_s)));
+    const auto entered = Clock::now();
+    const auto deadline = entered + std::chrono::duration_cast<Clock::duration>(
+                                        std::chrono::duration<double>(std::max(0.0, timeout_s)));
     Waiter me{a, b};
     waiters_.push_back(&me);  // advance() wakes us once this range is covered
     int rc;
@@ -234,7 +256,12 @@ class Flow {
       if (failed_) { rc = 1; break; }
       if (finished_) { rc = 3; break; }
       if (abort && abort->load()) { rc = 1; break; }
-      if (Clock::now() >= deadline) { rc = 2; break; }
+      const auto now = Clock::now();
+      if (now >= deadline) { rc = 2; break; }
+      if (stall_s_ > 0 && std::chrono::duration<double>(now - last_move_locked(a, b, entered)).count() >= stall_s_) {
+        rc = 4;
+        break;
+      }
       // short slices so an aborting caller (the upload pump's sender) is seen promptly
       cv_wait_ms(me.cv, l, 20);
     }
@@ -254,6 +281,18 @@ class Flow {
       w->woken = true;
       w->cv.notify_one();
     }
+  }
+  // Latest advance of any unfinished segment that still owes bytes of [a, b)
+  // (not before `floor`, the time the wait began).
+  Clock::time_point last_move_locked(uint64_t a, uint64_t b, Clock::time_point floor) const {
+    Clock::time_point t = floor;
+    for (const Seg& s : segs_) {
+      const uint64_t s_end = s.end < 0 ? UINT64_MAX : static_cast<uint64_t>(s.end);
+      const uint64_t frontier = s.start + s.done;
+      if (std::min(b, s_end) <= std::max(a, frontier)) continue;  // owes nothing of [a, b)
+      if (s.moved > t) t = s.moved;
+    }
+    return t;
   }
   uint64_t watermark_locked() const {
     if (finished_) return total_;
@@ -285,9 +324,18 @@ class Flow {
   bool finished_ = false;
   uint64_t total_ = 0;
   bool failed_ = false;
+  double stall_s_ = 0;
   std::string err_;
   std::atomic<bool> cancel_{false};
 };
+
+// Why a send pump's wait for source bytes ended (Flow::wait_covered rc 1-4).
+inline std::string flow_wait_error(int w, const Flow& flow) {
+  return w == 3   ? "source shorter than expected"
+         : w == 2 ? "timed out waiting for source bytes"
+         : w == 4 ? "source stalled"
+                  : "source transfer failed: " + flow.error();
+}
 
 // ---------------------------------------------------------------------------
 // Buffer cache.  A 10 MiB job touches ~20 MiB of pump buffers; fresh
@@ -877,10 +925,7 @@ inline SendResult send_plain(Stream& io, int fd, uint64_t off, uint64_t length, 
       const uint64_t slice = std::min<uint64_t>(n, 256u << 10);
       const int w = flow->wait_covered(off + r.sent, off + r.sent + slice, idle_timeout, io.abort_flag());
       if (w) {
-        r.err = io.aborted() ? "cancelled"
-                : w == 3     ? "source shorter than expected"
-                : w == 2     ? "timed out waiting for source bytes"
-                             : "source transfer failed: " + flow->error();
+        r.err = io.aborted() ? "cancelled" : flow_wait_error(w, *flow);
         return r;
       }
       n = std::max(slice, std::min(n, flow->covered_prefix(off + r.sent, off + r.sent + n)));
@@ -984,8 +1029,7 @@ inline SendResult send_chunked(Stream& io, int fd, uint64_t off, uint64_t length
         const int w = flow->wait_covered(a, a + m[0] + m[1], idle_timeout, &abort);
         if (w) {
           if (!abort.load())
-            set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
-                                                                       : "source transfer failed: " + flow->error());
+            set_err(flow_wait_error(w, *flow));
           return;
         }
       }
@@ -1338,8 +1382,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
           const int w = flow->wait_covered(a, a + len, idle_timeout, &abort);
           if (w) {
             if (!abort.load())
-              set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
-                                                                         : "source transfer failed: " + flow->error());
+              set_err(flow_wait_error(w, *flow));
             return;
           }
         }
@@ -1370,8 +1413,7 @@ inline SendResult send_chunked_zc(Stream& io, int fd, uint64_t off, uint64_t len
         const int w = flow->wait_covered(a, a + span, idle_timeout, &abort);
         if (w) {
           if (!abort.load())
-            set_err(w == 3 ? "source shorter than expected" : w == 2 ? "timed out waiting for source bytes"
-                                                                       : "source transfer failed: " + flow->error());
+            set_err(flow_wait_error(w, *flow));
           return;
         }
       }

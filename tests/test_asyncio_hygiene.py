@@ -38,7 +38,7 @@ def test_jobs_clean_under_asyncio_debug(tmp_path):
             await st.run_jobs(6)
             # a job whose upload is refused (403, not retried) fails and is dead-lettered
             s3 = st.backends[-1]
-            s3.fail_next(100, status=403)
+            s3.fail_next(100, status=403, code="AccessDenied")
             start = st.svc.jobs_finished
             await st.submit(1)
             await st.wait_done(start + 1)

@@ -20,7 +20,13 @@ minio-go library behaviours the reference relied on without naming them:
   and refuses objects over 5 TiB (minio ``optimalPartInfo``; :func:`plan_parts`);
 * an empty or malformed endpoint is an error when the client is built
   (minio ``NewWithOptions`` → ``log.Fatal`` in ``downloader.go:95-98``;
-  :meth:`Endpoint.parse`).
+  :meth:`Endpoint.parse`);
+* every request is retried on connection errors, on 429/500/502/503 (and
+  504) and on minio's retryable S3 codes (``RequestTimeout``, ``SlowDown``,
+  ``ExpiredToken``, ... :data:`RETRYABLE_CODES`), up to 10 attempts spaced
+  1 s × 2^k up to 30 s (minio ``retry.go``; :meth:`S3Client.retry_delay`),
+  so a throttling burst or a MinIO rolling restart of a minute or two does
+  not fail the job.
 """
 
 from __future__ import annotations
@@ -33,6 +39,7 @@ import email.utils
 import hashlib
 import json
 import os
+import random
 import re
 import time
 import xml.etree.ElementTree as ET
@@ -45,7 +52,7 @@ from multidict import CIMultiDict
 from yarl import URL
 
 from ..ops import hashing
-from ..utils.backoff import ExponentialBackoff
+
 from ..utils import proxy as _proxy
 from ..utils import rawhttp
 from ..utils.dial import FALLBACK_DELAY
@@ -65,6 +72,21 @@ MAX_SINGLE_PUT = 5 << 30
 MAX_OBJECT_SIZE = 5 << 40
 DEFAULT_REGION = "us-east-1"
 _REGION_CODES = ("AuthorizationHeaderMalformed", "InvalidRegion", "PermanentRedirect", "IllegalLocationConstraintException")
+
+
+# minio-go v6's retry classifier (retry.go: retryableS3Codes, retryableHTTPStatusCodes),
+# which every reference S3 call went through (internal/uploader/uploader.go:43-51,64-65,89);
+# 504 is retried as well (a gateway in front of the store timing out).
+RETRYABLE_CODES = frozenset({"RequestError", "RequestTimeout", "Throttling", "ThrottlingException",
+                             "RequestLimitExceeded", "RequestThrottled", "InternalError", "ExpiredToken",
+                             "ExpiredTokenException", "SlowDown"})
+RETRYABLE_STATUS = frozenset({429, 500, 502, 503, 504})
+
+
+def is_retryable(err: "S3Error") -> bool:
+    """Worth another attempt: a retryable status or S3 error code.  Any other
+    4xx, and 501 NotImplemented, fail at once."""
+    return err.status in RETRYABLE_STATUS or err.code in RETRYABLE_CODES
 
 
 class S3Error(Exception):
@@ -216,7 +238,8 @@ class Endpoint:
 class S3Client:
     def __init__(self, endpoint: Endpoint | str, creds: Provider | None = None, *, region: str = "",
                  lookup: str = "auto", payload_mode: str = "auto", part_size: int = 64 << 20,
-                 multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 5,
+                 multipart_threshold: int = 64 << 20, parallel_parts: int = 4, max_retries: int = 9,
+                 retry_unit: float = 1.0, retry_cap: float = 30.0,
                  io_block: int = 4 << 20, session: aiohttp.ClientSession | None = None,
                  native: bool = True, sign_threads: int = 4, ca_pem: str = "", ca_file: str = "",
                  proxies: "_proxy.ProxyConfig | None" = None, hash_device: str = "cpu") -> None:
@@ -238,7 +261,13 @@ class S3Client:
         self.part_size = max(part_size, 5 << 20)
         self.multipart_threshold = multipart_threshold
         self.parallel_parts = max(1, parallel_parts)
+        # minio-go's budget (retry.go: MaxRetry 10 attempts, DefaultRetryUnit 1 s, DefaultRetryCap
+        # 30 s): a request is tried up to max_retries + 1 times, waiting unit * 2^k (capped)
+        # between tries, half of it jittered (minio-go jitters all of it: "equal" jitter keeps
+        # the herd spread and guarantees the budget rides out an outage of about a minute)
         self.max_retries = max_retries
+        self.retry_unit = retry_unit
+        self.retry_cap = retry_cap
         self.io_block = max(io_block, sigv4.STREAM_CHUNK)
         self._session = session
         self._own_session = session is None
@@ -396,6 +425,11 @@ class S3Client:
             return True
         return False
 
+    def retry_delay(self, attempt: int) -> float:
+        """Wait after failed attempt number ``attempt`` (1-based)."""
+        d = min(self.retry_cap, self.retry_unit * (2.0 ** min(attempt - 1, 30)))
+        return d / 2 + random.uniform(0.0, d / 2)
+
     def _amzdate(self) -> str:
         """``x-amz-date`` on S3's clock: the host's plus the learned skew."""
         now = _dt.datetime.now(_dt.timezone.utc)
@@ -426,8 +460,8 @@ class S3Client:
                   headers: dict | None = None, body: bytes | None = None, *, body_factory=None,
                   payload_hash: str | None = None, expect: tuple[int, ...] = (200,),
                   retry: bool = True, region: str | None = None, path_style: bool = False) -> tuple[int, dict, bytes]:
-        """One signed request with retries on connection errors / 5xx."""
-        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
+        """One signed request, retried (:meth:`retry_delay`) on connection errors
+        and on the statuses and S3 error codes minio-go retries (:func:`is_retryable`)."""
         attempt = 0
         region_hops = skew_hops = 0
         while True:
@@ -479,7 +513,7 @@ class S3Client:
                         skew_hops += 1
                         attempt -= 1
                         continue
-                    if r.status < 500 or not retry or attempt > self.max_retries:
+                    if not is_retryable(err) or not retry or attempt > self.max_retries:
                         raise err
             except aiohttp.ClientHttpProxyError as e:
                 if e.status in (401, 403, 407):
@@ -491,7 +525,7 @@ class S3Client:
                 if not retry or attempt > self.max_retries:
                     raise S3Error(0, "ConnectionError", str(e), f"{method} {path}") from e
                 err = e  # type: ignore[assignment]
-            d = pol.next_delay() or 1.0
+            d = self.retry_delay(attempt)
             log.with_fields(error=str(err), attempt=attempt).warn("s3 request failed; retrying in %.2fs", d)
             await asyncio.sleep(d)
 
@@ -695,7 +729,6 @@ class S3Client:
           and accepted when its ETag is the multipart ETag of exactly these
           parts (MD5 over the part MD5s, ``-N``), else the error stands.
         """
-        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         attempt = 0
         while True:
             attempt += 1
@@ -713,9 +746,10 @@ class S3Client:
                 r = _xml(rb, "CompleteMultipartUpload")
                 return (r.findtext(f"{S3_NS}ETag") or r.findtext("ETag") or "").strip('"')
             err = _parse_error(200, rb, f"complete {key}")
-            if err.code not in self.COMPLETE_RETRY_CODES or attempt > self.max_retries:
+            if (err.code not in self.COMPLETE_RETRY_CODES and err.code not in RETRYABLE_CODES) or \
+                    attempt > self.max_retries:
                 raise err
-            d = pol.next_delay() or 1.0
+            d = self.retry_delay(attempt)
             log.with_fields(key=key, code=err.code, attempt=attempt).warn(
                 "complete multipart answered 200 with an error; retrying in %.2fs", d)
             await asyncio.sleep(d)
@@ -735,13 +769,14 @@ class S3Client:
         then ``_relay.send_body`` writes head + body (aws-chunked with chunk
         signatures hashed on a native pool, or sendfile for unsigned) from the
         file straight to the socket; the reply is parsed here.  Same retry
-        policy as :meth:`_do` (connection errors and 5xx).
+        policy as :meth:`_do`.  When the download it follows stalls for the
+        flow's ``stall`` seconds the pump stops and this raises S3Error
+        ``SourceStalled`` (the caller uploads after the download instead).
 
         The pump owns ``sock`` and ``fd`` while it runs: if this coroutine is
         cancelled the pump is stopped (socket shut down, native cancel token
         set) and awaited before either is closed, so a reused fd number can
         never receive its writes."""
-        pol = ExponentialBackoff(initial=0.2, multiplier=2, max_interval=5, max_elapsed=None)
         fd = os.dup(src) if isinstance(src, int) else os.open(src, os.O_RDONLY)
         attempt = 0
         region_hops = skew_hops = 0
@@ -793,6 +828,9 @@ class S3Client:
                         signed.scope if signed else "", signed.signature if signed else "", sigv4.STREAM_CHUNK,
                         self.sign_threads, 300.0, self._chunk_gpu() if m == "streaming" else None)
                     rawhttp.trace("put_sent")
+                    if perr and "source stalled" in perr:
+                        raise S3Error(0, "SourceStalled", f"no download progress for {flow.stall:g}s",
+                                      f"PUT {path}")
                     if perr and ("source" in perr or perr == "cancelled"):
                         raise S3Error(0, "SourceFailed", perr, f"PUT {path}")
                     try:
@@ -822,7 +860,7 @@ class S3Client:
                         skew_hops += 1
                         attempt -= 1
                         continue
-                    if resp.status < 500 or attempt > self.max_retries:
+                    if not is_retryable(err) or attempt > self.max_retries:
                         raise err
                 except (rawhttp.RawHTTPError, OSError, asyncio.TimeoutError) as e:
                     if attempt > self.max_retries:
@@ -833,7 +871,7 @@ class S3Client:
                         conn.close()
                 if attempt <= 0:
                     continue
-                d = pol.next_delay() or 1.0
+                d = self.retry_delay(attempt)
                 log.with_fields(error=str(err), attempt=attempt).warn("s3 request failed; retrying in %.2fs", d)
                 await asyncio.sleep(d)
         finally:

@@ -58,6 +58,7 @@ RESUME_SUFFIX = ".s3upload"
 class Uploader:
     def __init__(self, bucket: str, client: S3Client, *, file_concurrency: int = 2) -> None:
         self.heals = 0
+        self.stalls = 0                      # streamed uploads that fell back to upload-after-download
         self.bucket = bucket
         self.client = client
         self.file_concurrency = max(1, file_concurrency)
@@ -66,12 +67,14 @@ class Uploader:
     @classmethod
     def from_env(cls, bucket: str, s3_endpoint: str | None = None, *, region: str = "",
                  part_size: int = 16 << 20, multipart_threshold: int = 64 << 20, parallel_parts: int = 4,
-                 env=None, sign_threads: int = 4, ca_file: str = "", hash_device: str = "cpu") -> "Uploader":
+                 env=None, sign_threads: int = 4, ca_file: str = "", hash_device: str = "cpu",
+                 max_retries: int = 9, retry_unit: float = 1.0, retry_cap: float = 30.0) -> "Uploader":
         ep = s3_endpoint if s3_endpoint is not None else os.environ.get("S3_ENDPOINT", "")
         Endpoint.parse(ep)                       # ValueError on an endpoint minio-go would refuse
         client = S3Client(ep, default_chain(env), region=region, part_size=part_size,
                           multipart_threshold=multipart_threshold, parallel_parts=parallel_parts,
-                          sign_threads=sign_threads, ca_file=ca_file, hash_device=hash_device)
+                          sign_threads=sign_threads, ca_file=ca_file, hash_device=hash_device,
+                          max_retries=max_retries, retry_unit=retry_unit, retry_cap=retry_cap)
         return cls(bucket, client)
 
     async def ensure_bucket(self) -> None:
@@ -131,14 +134,32 @@ class Uploader:
     async def upload_stream(self, media_id: str, name: str, src: int | str, size: int, wait_bytes=None,
                             flow=None, resume_path: str | None = None) -> UploadResult:
         """Upload one file that may still be growing (``wait_bytes`` gates reads;
-        ``flow`` is the download's native progress, followed without Python)."""
+        ``flow`` is the download's native progress, followed without Python).
+
+        If the download stalls under the upload (no progress for the flow's
+        ``stall`` seconds), the PUT is dropped before the store's own request
+        timeout fails it (S3: 400 ``RequestTimeout`` after ~20 s of silence),
+        and the file is uploaded once the download has finished.  A multipart
+        upload keeps the parts that landed (``resume_path``) and sends only
+        the rest.  The reference always uploaded after the download
+        (``uploader.go:89`` after ``downloader.go:116-130``)."""
         await self.ensure_bucket()
         key = object_key(media_id, name)
         log.info("starting upload of file '%s'", go_base(key))
         try:
-            etag = await self._healing(lambda: self.client.put_object(self.bucket, key, src, size,
-                                                                      wait_bytes=wait_bytes, flow=flow,
-                                                                      resume_path=resume_path))
+            try:
+                etag = await self._healing(lambda: self.client.put_object(self.bucket, key, src, size,
+                                                                          wait_bytes=wait_bytes, flow=flow,
+                                                                          resume_path=resume_path))
+            except S3Error as e:
+                if e.code != "SourceStalled" or wait_bytes is None:
+                    raise
+                self.stalls += 1
+                log.with_fields(key=go_base(key), error=e.message).warn(
+                    "download stalled under a streamed upload; uploading once the download is done")
+                await wait_bytes(size)
+                etag = await self._healing(lambda: self.client.put_object(self.bucket, key, src, size,
+                                                                          resume_path=resume_path))
         except (S3Error, OSError) as e:
             raise UploadError(f"failed to upload file {name}: {e}") from e
         log.info("finished upload")

@@ -469,7 +469,8 @@ class Service:
                                               multipart_threshold=cfg.s3_multipart_threshold,
                                               parallel_parts=cfg.s3_parallel_parts,
                                               sign_threads=cfg.s3_sign_threads, ca_file=cfg.ca_file,
-                                              hash_device=cfg.s3_hash_device)
+                                              hash_device=cfg.s3_hash_device, max_retries=cfg.s3_max_retries,
+                                              retry_unit=cfg.s3_retry_unit_s, retry_cap=cfg.s3_retry_cap_s)
         if self.amqp is None:
             if cfg.rabbitmq_endpoint_defaulted:
                 log.warn("RABBITMQ_ENDPOINT not defined, defaulting to local config: %s", cfg.rabbitmq_endpoint)
@@ -894,6 +895,9 @@ class Service:
             # the download's task (made in impl.start) runs its first step before this
             # upload's: a single stream's receive pump starts ahead of the SigV4 setup
             fd = h.open_reader()
+            if h.flow is not None:
+                # a PUT that follows a stalled download would idle into the store's request timeout
+                h.flow.stall = self.cfg.s3_stream_stall_s
             up = asyncio.ensure_future(self.uploader.upload_stream(media_id, h.filename, fd, h.size, h.wait_bytes,
                                                                    flow=h.flow,
                                                                    resume_path=h.dst + RESUME_SUFFIX))

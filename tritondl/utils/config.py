@@ -53,14 +53,16 @@ ENV_INTS = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "SHARD_QUEUES"
             "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
             "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
             "RECYCLE_BYTES": "recycle_bytes", "MALLOC_MMAP_THRESHOLD": "malloc_mmap_threshold",
-            "MALLOC_ARENA_MAX": "malloc_arena_max", "MALLOC_TRIM_THRESHOLD": "malloc_trim_threshold"}
+            "MALLOC_ARENA_MAX": "malloc_arena_max", "MALLOC_TRIM_THRESHOLD": "malloc_trim_threshold",
+            "S3_MAX_RETRIES": "s3_max_retries"}
 ENV_FLOATS = {"RETRY_DELAY": "retry_delay_s", "METADATA_TIMEOUT": "metadata_timeout_s",
               "RETRY_BACKOFF": "retry_backoff", "RETRY_DELAY_MAX": "retry_delay_max_s",
               "PROGRESS_INTERVAL": "progress_interval_s", "PROGRESS_LOG_INTERVAL": "progress_log_interval_s",
               "GPU_WARMUP_TIMEOUT": "gpu_warmup_timeout_s", "JOB_LOCK_WAIT": "job_lock_wait_s",
               "MALLOC_TRIM": "malloc_trim_s", "HEALTH_DOWN": "health_down_s", "HEALTH_STALL": "health_stall_s",
               "PIPELINE_COMMIT_MIN_MS": "pipeline_commit_min_ms", "STALE_JOB_DAYS": "stale_job_days",
-              "HANDBACK": "handback_s", "LEASE_AFTER": "lease_after_s", "LEASE": "lease_s"}
+              "HANDBACK": "handback_s", "LEASE_AFTER": "lease_after_s", "LEASE": "lease_s",
+              "S3_RETRY_UNIT": "s3_retry_unit_s", "S3_RETRY_CAP": "s3_retry_cap_s", "S3_STREAM_STALL": "s3_stream_stall_s"}
 ENV_STRS = {"CONSUME_TOPIC": "consume_topic", "PUBLISH_TOPIC": "publish_topic", "BUCKET": "bucket",
             "DOWNLOAD_DIR": "download_dir", "DEAD_LETTER_TOPIC": "dead_letter_topic",
             "METRICS_ADDR": "metrics_addr", "GPU_VERIFY": "gpu_verify", "BT_BOOTSTRAP": "bt_bootstrap",
@@ -241,6 +243,15 @@ class Config:
     # "gpu" (the HIP piece kernel, a lane per 64 KiB chunk: ~2.6 ms per batch, so it
     # pays only when the node is CPU-bound, e.g. many workers per CPU share)
     s3_hash_device: str = "cpu"
+    # request retries (minio-go retry.go: 10 attempts, 1 s unit, 30 s cap): connection errors,
+    # 429/500/502/503/504 and minio's retryable codes (RequestTimeout, SlowDown, ExpiredToken, ...)
+    s3_max_retries: int = 9
+    s3_retry_unit_s: float = 1.0
+    s3_retry_cap_s: float = 30.0
+    # a streamed PUT (the upload following its download) gives up after the download made no
+    # progress for this long, and the file is uploaded once the download is done: S3 answers
+    # 400 RequestTimeout to a request body that sends nothing for ~20 s (0 = follow forever)
+    s3_stream_stall_s: float = 10.0
     aws_access_key_id: str = ""
     aws_secret_access_key: str = ""
     aws_session_token: str = ""

@@ -6,7 +6,8 @@ servers the HTTP downloader talks to (the reference had no test origin).
 Fault knobs: ``ranges`` (advertise/honour Range), ``head`` (support HEAD),
 ``cut_after`` (drop the connection after N body bytes, once per request
 count in ``cut_times``; ``cut_match`` limits it to one Range), ``fail_next`` (N × HTTP 500), ``rate`` (bytes/s cap),
-``throttle`` (N × 429/503 with a ``Retry-After``).
+``throttle`` (N × 429/503 with a ``Retry-After``), ``stall`` ((offset, seconds):
+the next response goes silent for ``seconds`` after ``offset`` body bytes).
 Without faults or a rate cap, GET bodies leave through ``sendfile`` from a
 native thread (``SendfileResponse``) — blobs held in memory are mirrored to
 a memfd once.
@@ -73,6 +74,7 @@ class Origin:
         self.rate: float | None = web.fake_stream_rate()     # bytes/s per response stream (None: uncapped)
         self.chunked_content_length: int | None = None   # chunked responses also claim this length
         self.latency = 0.0
+        self.stall: tuple[int, float] | None = None   # (body offset, seconds): one mid-body silence
         self.requests: list[tuple[str, str, str]] = []
         self.redirects: dict[str, tuple[int, str]] = {}     # path -> (status, Location)
         self.basic_auth: dict[str, str] = {}    # path -> required "user:password" (401 otherwise)
@@ -157,7 +159,7 @@ class Origin:
                     return web.Response(status=416, headers={"Content-Range": f"bytes */{size}"})
                 status = 206
                 hdrs["Content-Range"] = f"bytes {start}-{end - 1}/{size}"
-        if self.cut_after is None and not self.rate and rawhttp.relay_module() is not None:
+        if self.cut_after is None and not self.rate and self.stall is None and rawhttp.relay_module() is not None:
             return web.SendfileResponse(status, hdrs, blob.fd(), start, end - start)
         hdrs["Content-Length"] = str(end - start)
         resp = web.StreamResponse(status=status, headers=hdrs)
@@ -175,6 +177,14 @@ class Origin:
                 self.cut_times -= 1
                 request.transport.close()  # type: ignore[union-attr]
                 return resp
+            if self.stall is not None and sent <= self.stall[0] < sent + n:
+                at, secs = self.stall
+                self.stall = None
+                k = at - sent
+                if k:
+                    await resp.write(blob.read(pos, pos + k))
+                    pos, sent, n = pos + k, sent + k, n - k
+                await asyncio.sleep(secs)       # the origin goes silent mid-body
             await resp.write(blob.read(pos, pos + n))
             pos += n
             sent += n

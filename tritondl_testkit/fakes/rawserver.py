@@ -76,6 +76,7 @@ class Request:
         self._remaining = -1 if self._chunked else (int(cl) if cl else 0)
         self._taken = False
         self.transport_close_after = False   # reply, then drop the connection (body not fully read)
+        self.idle_timeout: float | None = None   # body reads raise asyncio.TimeoutError after this silence
 
     @property
     def body_length(self) -> int | None:
@@ -85,6 +86,8 @@ class Request:
         if self._buf:
             d, self._buf = self._buf[:n], self._buf[n:]
             return d
+        if self.idle_timeout:
+            return await asyncio.wait_for(self._conn.recv(n), self.idle_timeout)
         return await self._conn.recv(n)
 
     async def _read_some(self, n: int) -> bytes:
@@ -268,8 +271,9 @@ class _Conn:
                 resp = await self.server.handler(req)
                 if self.closed:
                     return
-                # drain what the handler left of the body (keeps the connection in sync)
-                if not req._taken:
+                # drain what the handler left of the body (keeps the connection in sync),
+                # unless the connection is dropped after this reply anyway
+                if not req._taken and not req.transport_close_after:
                     while await req._read_some(1 << 20):
                         pass
                 buf = req._buf
@@ -283,7 +287,7 @@ class _Conn:
                 conn_hdr = hdrs.get("Connection", "").lower()
                 if req.transport_close_after or conn_hdr == "close" or (version == "HTTP/1.0" and conn_hdr != "keep-alive"):
                     return
-        except (ConnectionError, OSError):
+        except (ConnectionError, OSError, asyncio.TimeoutError):
             return
         finally:
             self.closed = True

@@ -11,8 +11,14 @@ Storage modes: ``memory`` (default), ``disk`` (under ``root``) or
 native relay built, aws-chunked and unsigned PUT bodies are received (and
 every chunk signature verified) by ``_relay.recv_verify_chunked`` /
 ``_relay.recv_body`` outside the interpreter, as MinIO would on its own box.
-Fault injection: :meth:`fail_next` returns 5xx for the next N requests,
-:meth:`fail_for` for every request during an outage window.  Content check
+Fault injection, with the codes AWS S3 uses: :meth:`fail_next` answers the
+next N requests with a status and S3 error code (503 ``SlowDown``, 429,
+500 ``InternalError``, 400 ``RequestTimeout``, 403 ``ExpiredToken``, ...),
+:meth:`fail_for` every request during an outage window, :meth:`down_for`
+refuses connections for a while (the listener is closed, as during a
+restart), and ``idle_timeout`` answers 400 ``RequestTimeout`` and drops the
+connection when a request body sends nothing for that long (AWS does after
+~20 s).  Content check
 (``expect``, a :class:`~tritondl_testkit.fakes.payload.Expectations`): a PUT of a
 synthetic payload variant whose bytes are not the origin's is refused with
 400 ``BadDigest`` — in discard mode too, from the leaf hashes the native
@@ -65,6 +71,10 @@ class Upload:
     parts: dict = field(default_factory=dict)  # n -> Obj
 
 
+_IDLE_MSG = ("Your socket connection to the server was not read from or written to within the timeout "
+             "period. Idle connections will be closed.")
+
+
 def _xml_err(status: int, code: str, msg: str, region: str = "") -> web.Response:
     reg = f"<Region>{region}</Region>" if region else ""
     body = (f"<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>{code}</Code><Message>{msg}</Message>"
@@ -107,6 +117,12 @@ class FakeS3:
         self._ids = itertools.count(1)
         self._fail = 0
         self._fail_status = 503
+        self._fail_code = "ServiceUnavailable"
+        self._fail_methods: tuple[str, ...] = ()
+        self.failed = 0                          # requests answered with an injected failure
+        # AWS: 400 RequestTimeout when a request body sends nothing for ~20 s (None: wait forever)
+        self.idle_timeout: float | None = None
+        self.idle_timeouts = 0
         self.requests: list[tuple[str, str]] = []
         self.bytes_received = 0
         # native aws-chunked verifier threads per PUT (stands in for a remote S3's capacity)
@@ -129,12 +145,34 @@ class FakeS3:
     def endpoint(self) -> str:
         return f"{'https' if self.tls else 'http'}://{self.host}:{self.port}"
 
-    def fail_next(self, n: int, status: int = 503) -> None:
-        self._fail, self._fail_status = n, status
+    # the S3 error code AWS sends with each status (RequestTimeout, ExpiredToken: see fail_next)
+    DEFAULT_CODES = {500: "InternalError", 502: "BadGateway", 503: "ServiceUnavailable", 504: "GatewayTimeout",
+                     429: "SlowDown", 400: "RequestTimeout", 403: "ExpiredToken", 501: "NotImplemented"}
 
-    def fail_for(self, seconds: float, status: int = 503) -> None:
+    def fail_next(self, n: int, status: int = 503, code: str | None = None, methods: tuple[str, ...] = ()) -> None:
+        """The next ``n`` requests (of ``methods``, default any) get ``status``
+        with S3 error ``code`` (default: the one AWS sends with that status)."""
+        self._fail, self._fail_status = n, status
+        self._fail_code = code or self.DEFAULT_CODES.get(status, "ServiceUnavailable")
+        self._fail_methods = tuple(methods)
+
+    def fail_for(self, seconds: float, status: int = 503, code: str | None = None) -> None:
         """Outage: every request gets ``status`` for the next ``seconds``."""
         self._outage_until, self._fail_status = time.monotonic() + seconds, status
+        self._fail_code = code or self.DEFAULT_CODES.get(status, "ServiceUnavailable")
+        self._fail_methods = ()
+
+    async def down_for(self, seconds: float) -> None:
+        """Outage: the server stops listening and drops its connections, then
+        comes back on the same port after ``seconds`` (a MinIO restart)."""
+        port = self.port
+        await self.stop()
+
+        async def back() -> None:
+            await asyncio.sleep(seconds)
+            self.port = port
+            await self.start()
+        self._restart = asyncio.ensure_future(back())
 
     def create_bucket(self, name: str, region: str | None = None) -> None:
         self.buckets.setdefault(name, {})
@@ -258,12 +296,14 @@ class FakeS3:
             leaves = None
             if self.expect is None:
                 got, _eof, err = await asyncio.get_running_loop().run_in_executor(
-                    None, relay.recv_body, stream, -1, 0, n, pre, None, 0, 0, 300.0)
+                    None, relay.recv_body, stream, -1, 0, n, pre, None, 0, 0, self.idle_timeout or 300.0)
             else:                       # content check: leaf hashes computed while the body lands
                 got, err, leaves = await asyncio.get_running_loop().run_in_executor(
-                    None, relay.recv_leaf_hashes, stream, n, pre, self.verify_threads, 300.0)
+                    None, relay.recv_leaf_hashes, stream, n, pre, self.verify_threads, self.idle_timeout or 300.0)
             if err:
                 request.transport.close()
+                if "timeout" in err:
+                    raise _BadReq(400, "RequestTimeout", _IDLE_MSG)
                 raise _BadReq(400, "IncompleteBody", err)
             self.bytes_received += got
             return _Sized(got, leaves)
@@ -282,7 +322,7 @@ class FakeS3:
         stream, pre = request.take_body()
         n, err, data, leaves = await asyncio.get_running_loop().run_in_executor(
             None, relay.recv_verify_chunked, stream, raw_len, pre, key, amzdate, scope, seed, keep,
-            self.verify_threads, 300.0)
+            self.verify_threads, self.idle_timeout or 300.0)
         self.bytes_received += raw_len
         if err:
             if "closed" in err or "timeout" in err or "socket" in err or "recv" in err:
@@ -290,6 +330,8 @@ class FakeS3:
             else:
                 # the body was consumed up to the error: drop the connection after replying
                 request.transport_close_after = True
+            if "timeout" in err:
+                raise _BadReq(400, "RequestTimeout", _IDLE_MSG)
             code = 403 if "signature" in err else 400
             raise _BadReq(code, "SignatureDoesNotMatch" if code == 403 else "IncompleteBody", err)
         if decoded_len >= 0 and decoded_len != n:
@@ -406,10 +448,17 @@ class FakeS3:
 
     async def _handle(self, request: web.Request) -> web.StreamResponse:
         self.requests.append((request.method, request.raw_path))
-        if self._fail > 0 or time.monotonic() < self._outage_until:
-            self._fail = max(0, self._fail - 1)
-            await request.read()
-            return _xml_err(self._fail_status, "ServiceUnavailable", "injected failure")
+        request.idle_timeout = self.idle_timeout
+        outage = time.monotonic() < self._outage_until
+        if outage or (self._fail > 0 and (not self._fail_methods or request.method in self._fail_methods)):
+            if not outage:
+                self._fail -= 1
+            self.failed += 1
+            try:
+                await request.read()
+            except (asyncio.TimeoutError, ConnectionError):
+                request.transport.close()
+            return _xml_err(self._fail_status, self._fail_code, "injected failure")
         request.signed_region = None
         auth = self._verify(request)
         if isinstance(auth, web.Response):
@@ -432,7 +481,13 @@ class FakeS3:
             if not key:
                 return await self._bucket_op(request, bucket, q, auth)
             return await self._object_op(request, bucket, key, q, auth)
+        except asyncio.TimeoutError:
+            self.idle_timeouts += 1
+            request.transport_close_after = True
+            return _xml_err(400, "RequestTimeout", _IDLE_MSG)
         except _BadReq as e:
+            if e.code == "RequestTimeout":
+                self.idle_timeouts += 1
             return _xml_err(e.status, e.code, e.msg)
 
     async def _bucket_op(self, request: web.Request, bucket: str, q: dict, auth) -> web.StreamResponse:
