@@ -967,6 +967,10 @@ class Torrent:
 
     async def _on_inbound(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         addr = writer.get_extra_info("peername")[:2]
+        sock = writer.get_extra_info("socket")
+        if sock is not None:
+            with contextlib.suppress(OSError):
+                tcpdial.tcp_options(sock)      # Go's net.ListenConfig: keep-alive on accepted conns too
         policy = self.cfg.encryption
         try:
             first = await asyncio.wait_for(reader.readexactly(len(mse.PLAIN_PREFIX)), self.cfg.connect_timeout)

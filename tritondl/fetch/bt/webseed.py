@@ -20,7 +20,7 @@ from urllib.parse import quote
 
 import aiohttp
 
-from ...utils.dial import FALLBACK_DELAY
+from ...utils.dial import FALLBACK_DELAY, socket_factory
 from ...utils.log import log
 
 if TYPE_CHECKING:  # pragma: no cover
@@ -84,7 +84,7 @@ class WebSeed:
         session = self._session or aiohttp.ClientSession(
             timeout=aiohttp.ClientTimeout(total=None, sock_connect=15, sock_read=60),
             connector=aiohttp.TCPConnector(limit=self.conns, force_close=False,
-                                           happy_eyeballs_delay=FALLBACK_DELAY))
+                                           happy_eyeballs_delay=FALLBACK_DELAY, socket_factory=socket_factory))
         try:
             await asyncio.gather(*(self._worker(session) for _ in range(self.conns)))
         finally:

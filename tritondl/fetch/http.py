@@ -59,7 +59,7 @@ from yarl import URL
 
 from ..utils import proxy as _proxy
 from ..utils import rawhttp, spares
-from ..utils.dial import FALLBACK_DELAY
+from ..utils.dial import FALLBACK_DELAY, socket_factory
 from ..utils.disk import DiskSpaceError, check_space
 from ..utils.log import log
 from .registry import ClientRegister, ProgressSink
@@ -273,7 +273,8 @@ class HTTPDownloader:
                 ssl_ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
             self._session = aiohttp.ClientSession(
                 timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=120),
-                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx, happy_eyeballs_delay=FALLBACK_DELAY), auto_decompress=False)
+                connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx, happy_eyeballs_delay=FALLBACK_DELAY,
+                                             socket_factory=socket_factory), auto_decompress=False)
         return self._session
 
     async def close(self) -> None:

@@ -52,10 +52,9 @@ from multidict import CIMultiDict
 from yarl import URL
 
 from ..ops import hashing
-
 from ..utils import proxy as _proxy
 from ..utils import rawhttp
-from ..utils.dial import FALLBACK_DELAY
+from ..utils.dial import FALLBACK_DELAY, socket_factory
 from ..utils.log import log
 from . import sigv4
 from .credentials import Chain, Provider, Value, default_chain
@@ -306,7 +305,7 @@ class S3Client:
             self._session = aiohttp.ClientSession(
                 timeout=aiohttp.ClientTimeout(total=None, sock_connect=30, sock_read=300),
                 connector=aiohttp.TCPConnector(limit=64, ssl=ssl_ctx if ssl_ctx is not None else True,
-                                             happy_eyeballs_delay=FALLBACK_DELAY),
+                                             happy_eyeballs_delay=FALLBACK_DELAY, socket_factory=socket_factory),
                 auto_decompress=False)
             self._own_session = True
         return self._session
