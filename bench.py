@@ -226,6 +226,44 @@ def _trace_p50(events: list) -> dict:
     return {k: round(sorted(v)[len(v) // 2], 3) for k, v in sorted(per.items(), key=lambda kv: sorted(kv[1])[0])}
 
 
+_CPU_KEYS = ("worker", "worker_loop", "worker_recv", "worker_send", "fakes", "origin", "s3", "broker", "producer")
+
+
+def _cpu_per_job(cpu_all: list, jobs: int) -> dict:
+    return {k: round(sum(c.get(k, 0.0) for c in cpu_all) / max(1, jobs) * 1000, 3) for k in _CPU_KEYS}
+
+
+# Run-to-run spread of this bench in the driver's form (--steps 20 --warmup 5), measured by
+# the builder on MI355X boxes (profiles/r06_noise/SUMMARY.md).  One run's number moves this much
+# between back-to-back runs on one box: a change smaller than it is not resolved by one record.
+BUILDER_SPREAD = None
+
+
+def _noise(done: list, lat: list) -> dict:
+    """How much to trust one run's number: the per-job latency IQR, the job
+    rate of each quarter of the timed jobs (by completion time), and the
+    run-to-run spread of this bench measured by the builder on the MI355X
+    boxes (:data:`BUILDER_SPREAD`)."""
+    out: dict = {}
+    if lat:
+        q = lambda f: round(lat[min(len(lat) - 1, int(len(lat) * f))] * 1000, 3)  # noqa: E731
+        out["latency_ms_p25_p75"] = [q(0.25), q(0.75)]
+        out["latency_ms_iqr"] = round(q(0.75) - q(0.25), 3)
+    ts = [r.finished_at for r in done if getattr(r, "finished_at", 0.0)]
+    if len(ts) >= 8:
+        k = len(ts) // 4
+        rates = []
+        for i in range(4):
+            seg = ts[i * k:(i + 1) * k + 1] if i < 3 else ts[3 * k:]
+            if len(seg) >= 2 and seg[-1] > seg[0]:
+                rates.append(round((len(seg) - 1) / (seg[-1] - seg[0]), 1))
+        if len(rates) == 4:
+            out["quarter_jobs_per_sec"] = rates
+            out["quarter_spread_pct"] = round((max(rates) - min(rates)) / (sum(rates) / 4) * 100, 1)
+    out["builder_run_to_run"] = BUILDER_SPREAD
+    return out
+
+
 def _place(cpus: str, fake_cpus: str, local_rank: int, local_world: int, file_size: int) -> list[int]:
     """Pin this rank's process (inherited by every native thread and by the
     fakes it spawns) before anything starts, and choose the fakes' set.
@@ -454,6 +492,7 @@ def main() -> int:
         # caches the first timed job runs from (first job 4.4 vs 2.5 ms p50)
         stack.cpu_seconds()              # first call imports psutil: keep it out of the timed window
         mem0 = _memcpy_gbps()
+        cpu_w0 = stack.cpu_seconds()     # warm-up + timed window (fakes' /proc ticks are 10 ms)
         if a.warmup:
             if shared:
                 loop.run_until_complete(phase(a.warmup))
@@ -537,6 +576,7 @@ def main() -> int:
                 **({"trace_p50_ms": _trace_p50(_rh.TRACE)} if _rh.TRACE else {}),
                 "gc_frozen": gc.get_freeze_count(),
                 "work_fs": _work_fs(stack)}
+        noise = _noise(done, lat)
         spans: dict[str, list[float]] = {}
         for r in done:
             for k, v in r.marks.items():
@@ -574,12 +614,16 @@ def main() -> int:
         raise SystemExit(f"{int(t[1].item())} jobs failed on some rank")
     per_rank = [n_done]
     cpu = {k: cpu1[k] - cpu0[k] for k in cpu0}
+    cpu_w = {k: cpu1[k] - cpu_w0[k] for k in cpu_w0}
     cpu_all = [cpu]
+    cpu_w_all = [cpu_w]
     if world > 1:
         per_rank = [None] * world  # type: ignore[list-item]
         dist.all_gather_object(per_rank, n_done, group=ctl)
         cpu_all = [None] * world  # type: ignore[list-item]
         dist.all_gather_object(cpu_all, cpu, group=ctl)
+        cpu_w_all = [None] * world  # type: ignore[list-item]
+        dist.all_gather_object(cpu_w_all, cpu_w, group=ctl)
         # where every rank ran: its CCD(s), its fakes' CCD, one NUMA node or not, memory bandwidth
         mine = {"ccds": _PLACEMENT.get("chosen_ccds"), "fake_ccd": _PLACEMENT.get("fake_ccd"),
                 "same_numa_node": _PLACEMENT.get("fakes_same_numa_node"),
@@ -633,21 +677,24 @@ def main() -> int:
             # median ms from taking the job to the end of each stage (rank 0)
             "job_spans_ms_p50": {k: round(sorted(v)[len(v) // 2] * 1000, 2) for k, v in spans.items()},
             # CPU cost per job over the timed region, all ranks (worker processes incl. their
-            # native pump threads, from getrusage; the out-of-process fakes, producer included,
-            # separately): the node's CPU count divided by this bounds how far job-level data
-            # parallelism can scale.  null when the timed region is too short to mean much
-            # worker_recv / worker_send: thread CPU of the download / upload pumps (part of
+            # native pump threads, from getrusage, microsecond resolution; the out-of-process
+            # fakes, producer included, from /proc at 10 ms ticks: read those over a short run
+            # as +-10 ms / steps).  The node's CPU count divided by "worker" bounds how far
+            # job-level data parallelism can scale.  worker_loop / worker_recv / worker_send:
+            # the event-loop thread and the download / upload pump threads (parts of
             # "worker"); origin / s3 / broker / producer: each fake process (parts of "fakes")
-            "cpu_ms_per_job": ({k: round(sum(c.get(k, 0.0) for c in cpu_all) / (world * a.steps) * 1000, 3)
-                                for k in ("worker", "worker_recv", "worker_send", "fakes", "origin", "s3",
-                                          "broker", "producer")} if max_elapsed >= 0.5 else None),
+            "cpu_ms_per_job": _cpu_per_job(cpu_all, world * a.steps),
+            # the same over warm-up + timed jobs (a window long enough for the fakes' ticks)
+            "cpu_ms_per_job_with_warmup": _cpu_per_job(cpu_w_all, world * (a.steps + a.warmup)),
+            "cpu_window_s": {"timed": round(max_elapsed, 4), "fakes_tick_ms": 10},
             # share of one core each fake process used over the timed region (rank 0's): a
             # fake near 1.0 on a one-job-at-a-time run is what bounds it, not the worker
-            "fake_core_share": ({k: round(cpu_all[0].get(k, 0.0) / max_elapsed, 3)
-                                 for k in ("origin", "s3", "broker", "producer")} if max_elapsed >= 0.5 else None),
+            "fake_core_share": {k: round(cpu_all[0].get(k, 0.0) / max_elapsed, 3)
+                                for k in ("origin", "s3", "broker", "producer")},
             # the one fake broker serves every rank: the share of a core it used.  Above
             # 0.5 the harness, not the workers, may be what limits the run
-            "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3) if max_elapsed >= 0.5 else None,
+            "broker_core_share": round(cpu_all[0]["broker"] / max_elapsed, 3),
+            "noise": noise,
             "diag": diag,
         }
         if reference_mode is not None:

@@ -128,6 +128,7 @@ class JobResult:
     seconds: float = 0.0
     # per-job span log: stage -> seconds since the job was taken
     marks: dict = field(default_factory=dict)
+    finished_at: float = 0.0           # time.monotonic() when the result was recorded
 
 
 def _warm_gpu_quietly() -> bool:
@@ -984,7 +985,7 @@ class Service:
             raise
 
     def _record(self, r: JobResult) -> JobResult:
-        self._last_finished = time.monotonic()
+        self._last_finished = r.finished_at = time.monotonic()
         self.results.append(r)
         if len(self.results) > 10000:
             del self.results[:5000]

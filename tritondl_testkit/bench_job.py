@@ -377,15 +377,19 @@ class JobStack:
 
     def cpu_seconds(self) -> dict:
         """CPU time (user+sys, s) so far of this worker process (all threads:
-        native pumps included; getrusage, microsecond resolution) and of this
-        stack's out-of-process fakes (producer included)."""
+        native pumps included; getrusage, microsecond resolution), of its
+        event-loop thread (``worker_loop``, when called from it) and pump
+        threads, and of this stack's out-of-process fakes (producer included;
+        /proc clock ticks, 10 ms resolution)."""
         import resource
 
         import psutil
         from tritondl.utils import rawhttp
         ru = resource.getrusage(resource.RUSAGE_SELF)
         out = {"worker": ru.ru_utime + ru.ru_stime, "fakes": 0.0, "broker": 0.0, "origin": 0.0, "s3": 0.0,
-               "producer": 0.0}
+               "producer": 0.0,
+               # the calling thread: the bench runs the worker's event loop on it
+               "worker_loop": time.thread_time()}
         # the worker's data-plane pumps, by stage (thread CPU of the executor threads
         # running them; native helper threads they start are in "worker" only)
         for name, key in (("recv_body", "worker_recv"), ("send_body", "worker_send")):
