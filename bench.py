@@ -325,7 +325,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--file-mb", type=float, default=10.0)
-    ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
+    ap.add_argument("--concurrency", type=int, default=0,
+                    help="jobs in flight per worker: 0 = the worker default (adaptive, 1..4), N = fixed "
+                         "(reference: 1)")
     ap.add_argument("--prefetch", type=int, default=0, help="AMQP prefetch per shard consumer (0: = concurrency)")
     ap.add_argument("--no-gpu-probe", action="store_true")
     ap.add_argument("--probe-kb", type=int, default=-1,
@@ -530,6 +532,9 @@ def main() -> int:
         if cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        svc = stack.svc
+        conc = {"limit": svc._limit, "changes": int(svc.metrics.get("concurrency_changes")),
+                "last_decision": svc._adapt.last if svc._adapt is not None else None}
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         gc1 = [g["collections"] for g in gc.get_stats()]
         vm1 = _vm_snapshot()
@@ -575,6 +580,7 @@ def main() -> int:
                 "gc_collections": {f"gen{i}": b - a for i, (a, b) in enumerate(zip(gc0, gc1))},
                 **({"trace_p50_ms": _trace_p50(_rh.TRACE)} if _rh.TRACE else {}),
                 "gc_frozen": gc.get_freeze_count(),
+                "concurrency": conc,
                 "work_fs": _work_fs(stack)}
         noise = _noise(done, lat)
         spans: dict[str, list[float]] = {}
@@ -651,7 +657,7 @@ def main() -> int:
             "data": f"synthetic ({stack.resolved_variants() or 1} distinct deterministic pseudo-random "
                     f"{file_size / 2**20:g} MiB payloads, one per job in rotation, S3 content-checked; "
                     f"local fake broker/origin/S3{' over https' if a.tls else ''})",
-            "config": {"model": name, "global_batch": world * a.concurrency, "seq_len": None,
+            "config": {"model": name, "global_batch": world * (a.concurrency or 1), "seq_len": None,
                        "file_bytes": file_size, "parallelism": f"dp{world}",
                        "topology": ("one shared broker, competing consumers; per-rank origin+S3 nodes"
                                     if shared else "private broker/origin/S3 per rank"),
@@ -660,7 +666,9 @@ def main() -> int:
                        "cpus": (f"{len(pinned)} pinned ({pinned[0]}..{pinned[-1]})" if pinned else "unpinned"),
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",
                        "cpus_busy_before": os.environ.get("TRITONDL_BENCH_DOMAIN_BUSY", ""),
-                       "concurrency_per_worker": a.concurrency, "prefetch": prefetch,
+                       "concurrency_per_worker": a.concurrency or "adaptive",
+                       "concurrency_limit_end": conc["limit"],
+                       "prefetch": prefetch,
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "rtt_ms": a.rtt_ms, "stream_mbps": a.stream_mbps or None,
                        "log_level": a.log_level,

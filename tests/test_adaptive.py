@@ -1,0 +1,108 @@
+"""Adaptive job concurrency (``tritondl/parallel/adaptive.py``): one job at a
+time while jobs keep the CPUs busy (the reference's serial loop,
+``cmd/downloader/downloader.go:103-155``), more while they mostly wait on
+the network, up to the cap; pinned to one by a tight disk reserve."""
+
+import asyncio
+import os
+import time
+
+from tritondl.models import Media
+from tritondl.parallel.adaptive import Controller
+
+from .test_permissions import Env, run
+
+WAITING = {"probe": 0.040, "fetched": 0.045, "upload": 0.070}     # 20 ms RTT: mostly waits
+BUSY = {"probe": 0.0002, "fetched": 0.0021, "upload": 0.0022}      # loopback: the CPU moves bytes
+
+
+def _feed(c: Controller, marks: dict, n: int) -> list[int]:
+    seen = []
+    for _ in range(n):
+        if c.observe(marks, 10 << 20):
+            seen.append(c.limit)
+    return seen
+
+
+def test_waiting_jobs_double_the_limit_up_to_the_cap():
+    c = Controller(4, cpus=64)
+    assert c.limit == 1
+    assert _feed(c, WAITING, 20) == [2, 4]
+    assert c.limit == 4 and c.last["why"] == "network waits dominate"
+    assert _feed(c, WAITING, 20) == []          # the cap holds
+    c8 = Controller(8, cpus=64)
+    _feed(c8, WAITING, 40)
+    assert c8.limit == 8
+
+
+def test_cpu_bound_jobs_stay_at_one_and_bring_the_limit_back_down():
+    c = Controller(4, cpus=64)
+    assert _feed(c, BUSY, 50) == [] and c.limit == 1
+    _feed(c, WAITING, 10)
+    assert c.limit == 4
+    assert _feed(c, BUSY, 30) == [3, 2, 1]
+    assert c.last["why"] == "jobs are cpu-bound"
+
+
+def test_a_busy_cpu_lowers_the_limit_whatever_the_waits():
+    c = Controller(4, cpus=1, cpu_high=0.6)
+    c.limit = 4
+    t_end = time.process_time() + 0.3
+    while time.process_time() < t_end:            # burn this process's CPU: share ~1.0 of one CPU
+        pass
+    c._t0 = time.monotonic() - 0.3
+    assert c._decide(time.monotonic()) and c.limit == 3 and c.last["why"] == "cpu busy"
+
+
+def test_a_tight_disk_reserve_pins_the_limit_to_one():
+    free = [100 << 30]
+    c = Controller(4, cpus=64, free_bytes=lambda: free[0], reserve=10 << 30)
+    _feed(c, WAITING, 10)
+    assert c.limit == 4
+    free[0] = (10 << 30) + (15 << 20)             # less than reserve + 2 jobs of 10 MiB
+    _feed(c, WAITING, 4)
+    assert c.limit == 1 and c.last["why"] == "disk reserve"
+
+
+def test_long_jobs_with_idle_cpus_raise_the_limit_on_ticks():
+    c = Controller(4, cpus=64, period_s=0.05)
+    time.sleep(0.06)
+    assert c.tick(all_busy=True) and c.limit == 2
+    time.sleep(0.06)
+    assert not c.tick(all_busy=False) and c.limit == 2   # a free slot: nothing to gain
+
+
+def test_worker_raises_concurrency_when_jobs_wait_and_keeps_one_on_loopback(tmp_path):
+    """End to end: an origin that answers each request 30 ms late makes the
+    jobs wait, the limit climbs to the cap and the shard consumers' prefetch
+    follows; the same jobs without the latency keep one job at a time."""
+    async def main():
+        e = await Env().up(tmp_path, concurrency=0, concurrency_max=4)
+        assert e.svc._limit == 1 and e.amqp.prefetch == 1
+        data = os.urandom(200_000)
+        e.origin.latency = 0.03
+        for i in range(24):
+            e.submit(Media(id=f"w{i}", source_uri=e.origin.add(f"/w{i}.mkv", data)), i)
+        res = await e.wait_results(24, timeout=60)
+        assert all(r.ok for r in res), [r for r in res if not r.ok]
+        assert e.svc._limit == 4, e.svc._adapt.last
+        await asyncio.sleep(0.2)
+        assert e.amqp.prefetch == 3                 # (4 running + 1 committing) over 2 shards
+        assert e.svc.metrics.get("concurrency_limit") == 4
+        assert len(e.converts()) == 24
+        await e.down()
+    run(main())
+
+
+def test_fixed_concurrency_is_not_adapted(tmp_path):
+    async def main():
+        e = await Env().up(tmp_path, concurrency=1)
+        assert e.svc._adapt is None and e.svc._limit == 1 and len(e.svc._workers) == 1
+        e.origin.latency = 0.03
+        data = os.urandom(100_000)
+        for i in range(6):
+            e.submit(Media(id=f"f{i}", source_uri=e.origin.add(f"/f{i}.mkv", data)), i)
+        await e.wait_results(6)
+        assert e.svc._limit == 1
+        await e.down()
+    run(main())

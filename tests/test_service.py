@@ -972,7 +972,7 @@ def test_long_job_hands_its_buffered_delivery_to_an_idle_worker(tmp_path):
     B runs it and finishes while A's long job is still downloading.  A
     consumes again once its slot frees."""
     async def main():
-        e = await Env().up(tmp_path / "a", handback_s=0.4)
+        e = await Env().up(tmp_path / "a", handback_s=0.4, concurrency=1)   # every slot busy
         e.origin.rate = 1_500_000                         # the 4.5 MB job takes ~3 s
         long_url = e.origin.add("/long.mkv", os.urandom(4_500_000))
         short_url = e.origin.add("/short.mkv", os.urandom(30_000))

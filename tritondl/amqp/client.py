@@ -1098,6 +1098,26 @@ class Client:
             shard.rotations += 1
             return True
 
+    async def set_live_prefetch(self, prefetch: int) -> None:
+        """Change every shard consumer's prefetch while consuming: per-consumer
+        ``basic.qos`` applies only to consumers started after it, so each
+        shard's consumer is re-subscribed on its channel (its unacked
+        deliveries stay ackable there).  Channels opened later (a reconnect)
+        use the new value too."""
+        self.prefetch = prefetch
+        for sh in list(self.shards.values()):
+            async with sh.lock:
+                ch = sh.channel
+                if ch is None or ch.is_closed or self._closing:
+                    continue
+                await ch.basic_qos(prefetch, 0, False)
+                if not sh.active or sh.paused or sh.on_msg is None:
+                    continue                 # resume() / reopen consume with the new qos
+                cb = sh.on_msg
+                await ch.basic_cancel(sh.tag)
+                new = await ch.basic_consume(sh.queue, cb, no_ack=False)
+                sh.set_active(ch, new, cb)
+
     # ------------------------------------------------------------ hand-back
     async def pause(self) -> int:
         """Stop taking deliveries and give back the ones buffered here.

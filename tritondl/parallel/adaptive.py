@@ -1,0 +1,147 @@
+"""Adaptive job concurrency: how many jobs one worker runs at a time.
+
+The reference ran one job at a time (a single job goroutine,
+``cmd/downloader/downloader.go:103-155``, with ``SetPrefetch(1)``).  That is
+the right choice when a job keeps the worker's CPUs busy (a loopback or LAN
+origin and S3: the worker hashes and moves ~3-4 GB/s, and a second job only
+contends).  It is the wrong one when a job mostly waits on the network: at a
+20 ms round trip one 10 MiB job spends most of its ~40 ms in the origin's
+first byte, the S3 reply and the broker confirm, and four jobs in flight ran
+2.6x as many jobs per second (``profiles/r05_rtt_ab/``).
+
+:class:`Controller` decides from what the jobs themselves measure:
+
+* **wait share** — for HTTP jobs, the part of the slot time (taken -> upload
+  done) spent waiting on the network: the origin's connect and response head
+  (``probe - dispatch``) plus the S3 reply after the last byte landed
+  (``upload - fetched``);
+* **CPU use** — the process's CPU seconds per second over the window, as a
+  share of the CPUs it may use (affinity and cgroup quota).
+
+After every ``max(2, limit)`` finished jobs (or 2 s), while the median wait
+share is at least ``raise_at`` and CPU use is below ``cpu_high`` the limit
+doubles (up to ``cap``); when the wait share falls below ``lower_at`` or CPU
+use passes ``cpu_high`` it drops by one.  Jobs without HTTP marks (torrents)
+count as waiting when CPU use is below ``cpu_low``.  A disk reserve below
+two of the largest recent jobs pins the limit to 1 (``utils/disk.py``).
+"""
+
+from __future__ import annotations
+
+import os
+import resource
+import time
+
+
+def usable_cpus() -> int:
+    """CPUs this process may run on: affinity, capped by a cgroup v2 quota."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def _cpu_now() -> float:
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
+
+
+class Controller:
+    def __init__(self, cap: int, *, start: int = 1, raise_at: float = 0.4, lower_at: float = 0.2,
+                 cpu_high: float = 0.6, cpu_low: float = 0.25, period_s: float = 2.0,
+                 free_bytes=None, reserve: int = 0, cpus: int | None = None) -> None:
+        self.cap = max(1, cap)
+        self.limit = min(self.cap, max(1, start))
+        self.raise_at, self.lower_at = raise_at, lower_at
+        self.cpu_high, self.cpu_low = cpu_high, cpu_low
+        self.period_s = period_s
+        self.free_bytes = free_bytes          # callable -> bytes free on the download fs (None: no guard)
+        self.reserve = reserve
+        self.cpus = cpus or usable_cpus()
+        self.changes = 0
+        self.last = {"wait_share": None, "cpu_share": None, "why": "start"}
+        self._shares: list[float] = []
+        self._other = 0                       # finished jobs without HTTP marks
+        self._max_job_bytes = 0
+        self._t0 = time.monotonic()
+        self._cpu0 = _cpu_now()
+        self._n = 0
+
+    def observe(self, marks: dict, nbytes: int = 0) -> bool:
+        """Record one finished job; True when the limit changed."""
+        self._n += 1
+        if nbytes > self._max_job_bytes:
+            self._max_job_bytes = nbytes
+        up, fet, probe = marks.get("upload"), marks.get("fetched"), marks.get("probe")
+        if up and fet is not None and probe is not None and up > 0:
+            head = max(0.0, probe - marks.get("dispatch", 0.0))
+            self._shares.append(min(1.0, max(0.0, (head + max(0.0, up - fet)) / up)))
+        else:
+            self._other += 1
+        now = time.monotonic()
+        if self._n < max(2, self.limit) and now - self._t0 < self.period_s:
+            return False
+        return self._decide(now)
+
+    def tick(self, all_busy: bool) -> bool:
+        """Periodic check while no job finishes (long torrents): every slot
+        busy for a whole period with the CPUs mostly idle raises the limit."""
+        now = time.monotonic()
+        if self._n or now - self._t0 < self.period_s:
+            return False
+        cpu = _cpu_now()
+        cpu_share = (cpu - self._cpu0) / max(1e-6, now - self._t0) / self.cpus
+        self._t0, self._cpu0 = now, cpu
+        old = self.limit
+        if all_busy and cpu_share < self.cpu_low and not self._disk_tight():
+            self.limit = min(self.cap, self.limit * 2)
+            self.last = {"wait_share": None, "cpu_share": round(cpu_share, 3), "why": "long jobs wait (cpu idle)"}
+        if self.limit != old:
+            self.changes += 1
+            return True
+        return False
+
+    def _decide(self, now: float) -> bool:
+        dt = max(1e-6, now - self._t0)
+        cpu = _cpu_now()
+        cpu_share = (cpu - self._cpu0) / dt / self.cpus
+        shares = sorted(self._shares)
+        wait = shares[len(shares) // 2] if shares else None
+        old = self.limit
+        why = "hold"
+        if self._disk_tight():
+            self.limit, why = 1, "disk reserve"
+        elif cpu_share > self.cpu_high:
+            self.limit, why = max(1, self.limit - 1), "cpu busy"
+        elif wait is not None and wait >= self.raise_at:
+            self.limit, why = min(self.cap, self.limit * 2), "network waits dominate"
+        elif wait is None and self._other and cpu_share < self.cpu_low:
+            self.limit, why = min(self.cap, self.limit * 2), "jobs wait (cpu idle)"
+        elif wait is not None and wait < self.lower_at:
+            self.limit, why = max(1, self.limit - 1), "jobs are cpu-bound"
+        self.last = {"wait_share": None if wait is None else round(wait, 3), "cpu_share": round(cpu_share, 3),
+                     "why": why}
+        self._shares.clear()
+        self._other = self._n = 0
+        self._t0, self._cpu0 = now, cpu
+        if self.limit != old:
+            self.changes += 1
+            return True
+        return False
+
+    def _disk_tight(self) -> bool:
+        if self.free_bytes is None or self.reserve <= 0:
+            return False
+        try:
+            free = self.free_bytes()
+        except OSError:
+            return False
+        return free < self.reserve + 2 * self._max_job_bytes

@@ -84,6 +84,7 @@ from .amqp.client import Client, Delivery
 from .fetch.http import HTTPDownloader
 from .fetch.registry import ClientImpl, Dispatcher
 from .models import Convert, DecodeError, Download
+from .parallel.adaptive import Controller
 from .s3.uploader import RESUME_SUFFIX, UploadError, Uploader
 from .select import MEDIA_EXTS, dir_media, predict_media
 from .utils import ledger as jobdir, rawhttp, spares
@@ -314,6 +315,11 @@ class Service:
         self._tails: set[asyncio.Task] = set()     # jobs past their upload: publish confirm, ack, cleanup
         self._stop = asyncio.Event()
         self._inflight = 0
+        self._limit = 1                            # jobs that may run now (see _set_limit)
+        self._limit_ev = asyncio.Event()           # set (and replaced) whenever _limit changes
+        self._adapt: Controller | None = None      # adaptive concurrency (cfg.concurrency == 0)
+        self._adapt_task: asyncio.Task | None = None
+        self._prefetch_task: asyncio.Task | None = None
         self._metrics_runner = None
         self._trimmer: asyncio.Task | None = None
         self._janitor: asyncio.Task | None = None
@@ -488,10 +494,16 @@ class Service:
                 await self.amqp.connect()
         self.amqp.lease_after = cfg.lease_after_s
         self.amqp.lease_ttl = cfg.lease_s
+        self._limit = self._cap if cfg.concurrency > 0 else 1
+        self.amqp.set_prefetch(self._prefetch_for(self._limit))
         if self.dispatcher is None:
             self.dispatcher = Dispatcher(cfg.download_dir, default_impls(cfg), cfg.progress_log_interval_s)
         self.dispatcher.start()
         self.ledger = jobdir.DoneLedger(self.dispatcher.base_dir)
+        if cfg.concurrency <= 0 and self._cap > 1:
+            from .utils.disk import free_bytes
+            base = self.dispatcher.base_dir
+            self._adapt = Controller(self._cap, free_bytes=lambda: free_bytes(base), reserve=cfg.disk_reserve_bytes)
         if cfg.cleanup and cfg.recycle_bytes > 0:
             base = self.dispatcher.base_dir
             for stale in spares.stale_pools(base):
@@ -520,7 +532,10 @@ class Service:
         if cfg.handback_s > 0:
             self._handback = asyncio.ensure_future(self._handback_loop(cfg.handback_s))
         self._housekeeper = asyncio.ensure_future(self._housekeeping())
-        for i in range(max(1, cfg.concurrency)):
+        self.metrics.set("concurrency_limit", self._limit)
+        if self._adapt is not None:
+            self._adapt_task = asyncio.ensure_future(self._adapt_ticks())
+        for i in range(self._cap):
             self._workers.append(asyncio.ensure_future(self._worker(i)))
 
     async def _handback_loop(self, after_s: float) -> None:
@@ -531,7 +546,7 @@ class Service:
         assert self.amqp is not None
         while not self._stop.is_set():
             await asyncio.sleep(max(0.05, after_s / 4))
-            busy = self._inflight >= max(1, self.cfg.concurrency)
+            busy = self._inflight >= self._limit
             if busy and not self.amqp.paused and time.monotonic() - self._busy_since >= after_s:
                 try:
                     n = await self.amqp.pause()
@@ -613,13 +628,80 @@ class Service:
         ``concurrency`` jobs' streams can never starve it."""
         cfg = self.cfg
         per_job = max(1, cfg.http_segments) + 2 + max(1, cfg.s3_parallel_parts)
-        need = max(1, cfg.concurrency) * per_job + 8
+        need = self._cap * per_job + 8
         asyncio.get_running_loop().set_default_executor(
             ThreadPoolExecutor(max_workers=max(32, need), thread_name_prefix="tritondl-io"))
+
+    @property
+    def _cap(self) -> int:
+        """Most jobs this worker ever runs at once (job loops started)."""
+        c = self.cfg
+        return c.concurrency if c.concurrency > 0 else max(1, c.concurrency_max)
+
+    def _prefetch_for(self, limit: int) -> int:
+        """Per-shard-consumer prefetch that keeps ``limit`` jobs fed: the
+        configured value (1: the reference) or enough for ``limit`` running
+        jobs plus one committing (pipelined commit), spread over the shards."""
+        shards = max(1, self.cfg.num_shard_queues)
+        return max(self.cfg.prefetch, -(-(limit + 1) // shards) if limit > 1 else 1)
+
+    def _set_limit(self, n: int) -> None:
+        """Let ``n`` jobs run at once; job loops beyond it finish their job and
+        wait.  The shard consumers' prefetch follows (re-subscribed)."""
+        n = max(1, min(self._cap, n))
+        if n == self._limit:
+            return
+        log.with_fields(limit=n, was=self._limit, **(self._adapt.last if self._adapt else {})).info(
+            "job concurrency changed")
+        self._limit = n
+        ev, self._limit_ev = self._limit_ev, asyncio.Event()
+        ev.set()
+        self.metrics.set("concurrency_limit", n)
+        self.metrics.inc("concurrency_changes")
+        want = self._prefetch_for(n)
+        if self.amqp is not None and want != self.amqp.prefetch and \
+                (self._prefetch_task is None or self._prefetch_task.done()):
+            self._prefetch_task = asyncio.ensure_future(self._apply_prefetch())
+
+    async def _apply_prefetch(self) -> None:
+        assert self.amqp is not None
+        while not self._stop.is_set():
+            want = self._prefetch_for(self._limit)
+            if want == self.amqp.prefetch:
+                return
+            try:
+                await self.amqp.set_live_prefetch(want)
+            except Exception as e:  # noqa: BLE001 - the next reconnect applies self.amqp.prefetch anyway
+                log.with_field("error", str(e)).warn("changing the consumers' prefetch failed")
+                return
+
+    async def _adapt_ticks(self) -> None:
+        assert self._adapt is not None
+        try:
+            while not self._stop.is_set():
+                await asyncio.sleep(self._adapt.period_s)
+                if self._adapt.tick(self._inflight >= self._limit):
+                    self._set_limit(self._adapt.limit)
+        except asyncio.CancelledError:
+            pass
+
+    async def _await_slot(self, idx: int) -> bool:
+        """Wait until job loop ``idx`` may take a job (False: shutting down)."""
+        while idx >= self._limit:
+            if self._stop.is_set():
+                return False
+            waiter = asyncio.ensure_future(self._limit_ev.wait())
+            stopper = asyncio.ensure_future(self._stop.wait())
+            await asyncio.wait({waiter, stopper}, return_when=asyncio.FIRST_COMPLETED)
+            waiter.cancel()
+            stopper.cancel()
+        return not self._stop.is_set()
 
     async def _worker(self, idx: int) -> None:
         assert self.amqp is not None
         while not self._stop.is_set():
+            if idx >= self._limit and not await self._await_slot(idx):
+                return
             if self.amqp.paused:
                 await self.amqp.resume()    # a slot is free again: take deliveries
             try:
@@ -641,7 +723,7 @@ class Service:
                 return
             self._last_taken = time.monotonic()
             self._inflight += 1
-            if self._inflight >= max(1, self.cfg.concurrency):
+            if self._inflight >= self._limit:
                 self._busy_since = time.monotonic()
             self.metrics.set("jobs_inflight", self._inflight)
             if not self._pipeline_now():
@@ -887,6 +969,8 @@ class Service:
         d = self.dispatcher.job_dir(media_id)
         if d not in self._locked_dirs:          # _job_lock made, locked and checked it already
             os.makedirs(d, mode=0o755, exist_ok=True)
+        if marks is not None:
+            marks["dispatch"] = time.monotonic() - t0
         h = await impl.start(d, self.dispatcher.sink, url)
         if marks is not None:
             marks["probe"] = time.monotonic() - t0
@@ -986,6 +1070,8 @@ class Service:
 
     def _record(self, r: JobResult) -> JobResult:
         self._last_finished = r.finished_at = time.monotonic()
+        if self._adapt is not None and r.ok and r.stage == "done" and self._adapt.observe(r.marks, r.bytes):
+            self._set_limit(self._adapt.limit)
         self.results.append(r)
         if len(self.results) > 10000:
             del self.results[:5000]
@@ -1163,7 +1249,7 @@ class Service:
         limit = self.cfg.health_stall_s
         now = time.monotonic()
         if limit <= 0 or self._stop.is_set() or self.amqp is None or not self.amqp.connected or \
-                self._inflight >= max(1, self.cfg.concurrency):
+                self._inflight >= self._limit:
             self._stall_since = None
             return ""
         if now - self._backlog[0] >= 5.0 and (self._backlog_task is None or self._backlog_task.done()):
@@ -1183,7 +1269,8 @@ class Service:
     async def shutdown(self, grace: float = 30.0) -> None:
         log.info("shutting down")
         self._stop.set()
-        for t in (self._trimmer, self._janitor, self._handback, self._housekeeper):
+        for t in (self._trimmer, self._janitor, self._handback, self._housekeeper, self._adapt_task,
+                  self._prefetch_task):
             if t is not None:
                 t.cancel()
         t_end = time.monotonic() + grace

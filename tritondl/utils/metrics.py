@@ -141,6 +141,8 @@ HELP = {
     "uptime_seconds": "seconds since the process's metrics started",
     "lease_returns_total": "jobs that came back because the lease of the worker running them ran out",
     "done_ledger_swept_total": "done-ledger entries removed past their TTL",
+    "concurrency_limit": "jobs this worker may run at once now (adaptive concurrency, or the fixed TRITONDL_CONCURRENCY)",
+    "concurrency_changes_total": "changes of the adaptive concurrency limit",
     "leases_held": "leased deliveries (job running, copy held by the broker) not settled yet",
     "lease_events": "job lease operations since start by kind (taken, renewed, released, lost, requeued, refused)",
 }
