@@ -176,13 +176,47 @@ def test_healthz_answers_at_once_while_the_backlog_poll_is_slow(tmp_path):
 
         async def slow(topic):
             await asyncio.sleep(10)
-            return 0
-        e.amqp.ready_count = slow
+            return {}
+        e.amqp.ready_counts = slow
         t0 = time.monotonic()
         for _ in range(5):
             ok, why = await e.svc.health()
             assert ok, why
         assert time.monotonic() - t0 < 0.5
         e.svc._backlog_task.cancel()
+        await e.down()
+    run(main())
+
+
+def test_a_backlog_behind_a_full_shard_consumer_is_not_a_stall(tmp_path):
+    """two job slots, one shard consumer's prefetch taken by a
+    long job, a backlog on that same shard and the other shard empty.  The
+    free slot cannot be given shard 0's backlog (its consumer is full), so
+    the worker is not stalled and /healthz stays 200; once the long job ends
+    the backlog runs."""
+    async def main():
+        e = await Env().up(tmp_path, health_stall_s=0.3, concurrency=2)
+        e.svc._prefetch_for = lambda limit: 1          # the case the advice describes: prefetch 1 per shard
+        await e.amqp.set_live_prefetch(1)
+        e.origin.rate = 1_000_000
+        long_url = e.origin.add("/long.mkv", os.urandom(2_500_000))
+        short_url = e.origin.add("/short.mkv", os.urandom(5000))
+        e.submit(Media(id="long", source_uri=long_url), i=0)
+        t0 = time.monotonic()
+        while not any(r[1] == "/long.mkv" for r in e.origin.requests):
+            assert time.monotonic() - t0 < 5
+            await asyncio.sleep(0.01)
+        for k in range(3):
+            e.submit(Media(id=f"b{k}", source_uri=short_url), i=0)      # same shard as the long job
+        assert not e.amqp.shards["v1.download-0"].has_room(1) and e.amqp.shards["v1.download-1"].has_room(1)
+        t1 = time.monotonic()
+        while time.monotonic() - t1 < 1.2:
+            e.svc._backlog = (0.0, e.svc._backlog[1])  # re-poll on every probe
+            ok, why = await e.svc.health()
+            assert ok, why
+            await asyncio.sleep(0.1)
+        assert e.svc._backlog[1] == 0                  # shard 0's ready messages were not counted
+        res = await e.wait_results(4, timeout=30)
+        assert all(r.ok for r in res), res
         await e.down()
     run(main())

@@ -391,3 +391,51 @@ def test_pool_healthz_inherits_a_worker_whose_shard_stopped_consuming(tmp_path):
         await s.stop()
         await b.stop()
     asyncio.run(asyncio.wait_for(main(), 120))
+
+
+def test_pool_polls_the_metrics_address_its_workers_were_given(tmp_path):
+    """with TRITONDL_METRICS_ADDR in the workers' environment the
+    pool polled base+rank, where nothing listened, and its /healthz stayed
+    503 for good once the start-up grace ran out.  Now every worker serves
+    the shared address's port + rank, and the pool polls exactly that."""
+    async def main():
+        import socket
+        b = await Broker().start()
+        s = await FakeS3().start()
+
+        def free_run(n):
+            while True:
+                p = _free_port()
+                try:
+                    for k in range(n):
+                        x = socket.socket()
+                        x.bind(("127.0.0.1", p + k))
+                        x.close()
+                    return p
+                except OSError:
+                    continue
+        pool_port, wport = free_run(3), free_run(2)
+        env = {"RABBITMQ_ENDPOINT": b.endpoint, "RABBITMQ_USERNAME": "guest", "RABBITMQ_PASSWORD": "guest",
+               "S3_ENDPOINT": s.endpoint, "PYTHONPATH": ROOT, "TRITONDL_BT_DHT": "0", "LOG_LEVEL": "warning",
+               "TRITONDL_PROGRESS_LOG_INTERVAL": "0", "TRITONDL_GPU_VERIFY": "off",
+               "TRITONDL_METRICS_ADDR": f"0.0.0.0:{wport}"}
+        pool = WorkerPool(plan(2, gpus=0, cpus=2), env=env, cwd=str(tmp_path), grace=10,
+                          health_addr=f"127.0.0.1:{pool_port}", worker_health_grace=0.5)
+        await pool.start()
+        assert sorted(w.health_addr for w in pool.workers) == [("127.0.0.1", wport), ("127.0.0.1", wport + 1)]
+        t0 = time.monotonic()
+        while True:
+            try:
+                if [(await _get(wport + r))[0] for r in (0, 1)] == [200, 200]:
+                    break
+            except OSError:
+                pass
+            assert time.monotonic() - t0 < 60
+            await asyncio.sleep(0.1)
+        await asyncio.sleep(0.6)                        # past the grace: the polls count now
+        code, body = await _get(pool_port)
+        assert code == 200, body
+        await pool.stop()
+        await s.stop()
+        await b.stop()
+    asyncio.run(asyncio.wait_for(main(), 120))

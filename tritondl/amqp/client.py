@@ -313,6 +313,7 @@ class Delivery:
                 return False
             await fn()
             self.settled = True
+            self.client._unhold(self)
             return True
 
 
@@ -330,6 +331,7 @@ class Shard:
         self.paused = False                # consumer cancelled on purpose (Client.pause)
         self.since = time.monotonic()      # when ``active`` last changed
         self.rotations = 0                 # consumer re-subscriptions made for parked deliveries
+        self.held: dict[int, str] = {}     # delivery tag -> consumer tag, delivered and not yet settled
         self.lock = asyncio.Lock()
 
     def set_active(self, ch: Channel, tag: str, on_msg) -> None:
@@ -344,6 +346,13 @@ class Shard:
         if self.active:
             self.active = False
             self.since = time.monotonic()
+
+    def has_room(self, prefetch: int) -> bool:
+        """Could the broker deliver one more message to this shard's consumer
+        (its per-consumer prefetch counts only the current consumer tag)?"""
+        if not self.active:
+            return False
+        return prefetch <= 0 or sum(1 for t in self.held.values() if t == self.tag) < prefetch
 
     def down_for(self, now: float | None = None) -> float:
         """Seconds this shard has had no consumer (0 while it has one, or while
@@ -617,6 +626,7 @@ class Client:
         def on_msg(m: Message) -> None:
             if m.body is None:  # reference skips nil bodies (client.go:262)
                 return
+            shard.held[m.delivery_tag] = m.consumer_tag
             self._out.put_nowait(Delivery(self, m, gen))
 
         def on_cancel(tag: str) -> None:
@@ -632,6 +642,7 @@ class Client:
                 self._consumer_chans.remove(ch)
             if shard.channel is ch:
                 shard.set_inactive()
+                shard.held.clear()          # the broker requeued them with the channel
             if getattr(exc, "code", 0) == codec.PRECONDITION_FAILED and "acknowledgement" in str(exc):
                 # RabbitMQ's consumer_timeout (30 min by default): a job ran longer than the broker
                 # lets a delivery sit unacked; the delivery goes back to the queue
@@ -954,6 +965,7 @@ class Client:
             if d.msg.channel is None or d.msg.channel.is_closed:
                 raise ChannelClosed(0, "delivery channel gone")
             await d.msg.ack()
+            self._unhold(d)
         except (AMQPError, ConnectionError, OSError):
             # the broker took the original back already (consumer timeout, channel error):
             # the copy must not come back as a second job
@@ -1076,6 +1088,12 @@ class Client:
             if d.lease is not None and not d.settled:
                 with contextlib.suppress(Exception):
                     await asyncio.wait_for(d.nack(requeue=True), 10.0)
+
+    def _unhold(self, d: Delivery) -> None:
+        """``d`` no longer counts against its shard consumer's prefetch."""
+        sh = self._shard_of(d.msg.channel)
+        if sh is not None:
+            sh.held.pop(d.msg.delivery_tag, None)
 
     def _shard_of(self, ch: Channel | None) -> Shard | None:
         for sh in self.shards.values():
@@ -1229,19 +1247,23 @@ class Client:
         return self._parked
 
     # ------------------------------------------------------------ health
-    async def ready_count(self, topic: str) -> int:
-        """Ready (undelivered) messages on ``topic``'s shard queues, by passive
-        declare on a scratch channel (no permission needed)."""
+    async def ready_counts(self, topic: str) -> dict[str, int]:
+        """Ready (undelivered) messages on each of ``topic``'s shard queues, by
+        passive declare on a scratch channel (no permission needed)."""
         ch = await self._channel(qos=False)
         try:
-            n = 0
+            out = {}
             for i in range(self.num_shard_queues):
-                _q, count, _consumers = await ch.queue_declare(self.get_rk(topic, i), passive=True)
-                n += count
-            return n
+                q = self.get_rk(topic, i)
+                _q, count, _consumers = await ch.queue_declare(q, passive=True)
+                out[q] = count
+            return out
         finally:
             if not ch.is_closed:
                 await ch.close()
+
+    async def ready_count(self, topic: str) -> int:
+        return sum((await self.ready_counts(topic)).values())
 
     def health(self, max_down_s: float) -> tuple[bool, list[str]]:
         """(healthy, reasons).  Unhealthy once the connection has been down for

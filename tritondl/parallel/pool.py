@@ -21,9 +21,10 @@ The supervisor:
   running worker's own ``/healthz`` does (a worker whose shard consumer or
   broker connection has been down too long, or that sits idle on a
   backlog: :meth:`tritondl.service.Service.health`).  Each worker serves
-  its ``/healthz`` on loopback port ``health port + 1 + rank`` unless
-  ``TRITONDL_METRICS_ADDR`` is set for it.  ``/metrics`` carries live /
-  given-up / unhealthy / restart counts.
+  its ``/healthz`` on loopback port ``health port + 1 + rank``, or where
+  ``TRITONDL_METRICS_ADDR`` says (set for all workers, worker ``r`` serves
+  its port + ``r``); the pool polls the address each worker serves.
+  ``/metrics`` carries live / given-up / unhealthy / restart counts.
 """
 
 from __future__ import annotations
@@ -48,6 +49,7 @@ class _Worker:
     restarts: list[float] = field(default_factory=list)
     given_up: bool = False
     started_at: float = 0.0
+    health_addr: tuple[str, int] | None = None   # where this worker serves /healthz (None: nowhere known)
 
 
 class WorkerPool:
@@ -102,15 +104,36 @@ class WorkerPool:
     def _health_port(self, w: _Worker) -> int:
         return self.worker_health_base + w.spec.rank if self.worker_health_base else 0
 
+    @staticmethod
+    def _probe_addr(metrics_addr: str) -> tuple[str, int] | None:
+        """The address to poll for a worker serving ``host:port``: a wildcard
+        host is polled on loopback; None if the value is not host:port."""
+        host, _, port = metrics_addr.strip().rpartition(":")
+        try:
+            p = int(port)
+        except ValueError:
+            return None
+        if not 0 < p < 65536:
+            return None
+        host = host.strip("[]")
+        if host in ("", "0.0.0.0"):
+            host = "127.0.0.1"
+        elif host == "::":
+            host = "::1"
+        return host, p
+
     async def _worker_health(self, w: _Worker) -> str:
         """'' if worker ``w`` is healthy (or still within its start-up grace,
-        or between restarts), else why not."""
-        port = self._health_port(w)
-        if not port or w.proc is None or w.proc.returncode is not None:
+        or between restarts), else why not.  Polled where the worker actually
+        serves its ``/healthz`` (its TRITONDL_METRICS_ADDR, the pool's
+        ``base + rank`` or an operator's own); a worker with no metrics
+        address is not polled."""
+        if w.health_addr is None or w.proc is None or w.proc.returncode is not None:
             return ""
+        host, port = w.health_addr
         young = time.monotonic() - w.started_at < self.worker_health_grace
         try:
-            r, wr = await asyncio.wait_for(asyncio.open_connection("127.0.0.1", port), 2.0)
+            r, wr = await asyncio.wait_for(asyncio.open_connection(host, port), 2.0)
             try:
                 wr.write(b"GET /healthz HTTP/1.0\r\nHost: localhost\r\n\r\n")
                 data = await asyncio.wait_for(r.read(1 << 16), 3.0)
@@ -139,10 +162,20 @@ class WorkerPool:
         env = dict(os.environ)
         env.update(self.env)
         env.update(w.spec.env())
-        if self.worker_env is not None:
-            env.update(self.worker_env(w.spec.rank))
-        if self._health_port(w) and "TRITONDL_METRICS_ADDR" not in env:
-            env["TRITONDL_METRICS_ADDR"] = f"127.0.0.1:{self._health_port(w)}"
+        per_worker = self.worker_env(w.spec.rank) if self.worker_env is not None else {}
+        env.update(per_worker)
+        addr = env.get("TRITONDL_METRICS_ADDR", "")
+        if not addr and self._health_port(w):
+            addr = f"127.0.0.1:{self._health_port(w)}"
+        elif addr and "TRITONDL_METRICS_ADDR" not in per_worker and len(self.workers) > 1:
+            # one address for every worker (the pool's own environment): they cannot all bind
+            # it, so worker r serves port + r
+            host, _, port = addr.rpartition(":")
+            if port.isdigit():
+                addr = f"{host}:{int(port) + w.spec.rank}"
+        if addr:
+            env["TRITONDL_METRICS_ADDR"] = addr
+        w.health_addr = self._probe_addr(addr) if addr else None
         if w.spec.cpus and "TRITONDL_CPUS" not in self.env:
             # the worker pins itself first thing (service.main, TRITONDL_CPUS): no
             # preexec_fn in this threaded supervisor

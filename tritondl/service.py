@@ -1239,8 +1239,14 @@ class Service:
         return not why, why
 
     async def _poll_backlog(self, now: float) -> None:
+        """Ready messages this worker could be given now: only shards whose
+        consumer has prefetch to spare count.  A shard whose consumer is full
+        (a long job holds its delivery) cannot hand its backlog to a free slot
+        here, and that is not a stall of this worker."""
         try:
-            n = await asyncio.wait_for(self.amqp.ready_count(self.cfg.consume_topic), 5.0)
+            counts = await asyncio.wait_for(self.amqp.ready_counts(self.cfg.consume_topic), 5.0)
+            sh = self.amqp.shards
+            n = sum(c for q, c in counts.items() if q in sh and sh[q].has_room(self.amqp.prefetch))
             self._backlog = (now, n)
         except Exception:  # noqa: BLE001 - a missing queue is the shard check's business
             self._backlog = (now, 0)
