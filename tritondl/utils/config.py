@@ -235,7 +235,7 @@ class Config:
     s3_secret_key: str = ""
     s3_region: str = ""                         # "" => discover per bucket (GET ?location), like minio-go
     # 16 MiB parts: an upload that follows a live download ends ~3 ms after its
-    # last byte lands instead of ~11 ms (1 GiB job, profiles/r02_big_ab2); the
+    # last byte lands instead of ~11 ms (1 GiB job, profiles/r02_big_ab/); the
     # multipart threshold stays minio-go's 64 MiB, and plan_parts still grows
     # parts to keep any object within 10,000
     s3_part_size: int = 16 * 1024 * 1024
@@ -243,7 +243,7 @@ class Config:
     s3_parallel_parts: int = 4
     # native SHA-256 chunk hashers per streaming PUT: the aws-chunked hashing is on the
     # job's critical path (box A/B, 10 MiB job: 4 -> 245-270, 6 -> 295, 8 -> 307 jobs/s;
-    # profiles/r02_fill_ab); half the CPUs this process may use, 2..8
+    # profiles/r03_st_ab/); half the CPUs this process may use, 2..8
     s3_sign_threads: int = field(default_factory=lambda: _default_sign_threads())
     # where the aws-chunked chunk SHA-256s run: "cpu" (SHA-NI; lowest per-job latency) or
     # "gpu" (the HIP piece kernel, a lane per 64 KiB chunk: ~2.6 ms per batch, so it
