@@ -1,5 +1,5 @@
 """Resource-leak soak, reduced for the CPU suite (the full run —
-5,000 headline jobs + 100 magnet jobs — is ``tools/box/r03_soak.sh``, log in
+5,000 headline jobs + 100 magnet jobs — is ``tools/box/r03_soak.sh`` (archived, profiles/ARCHIVE.md), log in
 profiles/).  One worker runs HTTP jobs, magnet jobs and failing jobs that
 are retried and dead-lettered; after warm-up its descriptors, threads,
 asyncio tasks and native pool threads must stay flat (reference job loop:

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Minimal static checks with the standard library only (no linters are
 installed in the build image): every file compiles, no module imports a
-name it never uses, and no function reads a global the module never binds.  ``__init__.py`` re-exports and names listed in
+name it never uses, no function reads a global the module never binds, and
+every ``profiles/`` path the docs and code cite exists
+(``tools/prune_profiles.py --check``).  ``__init__.py`` re-exports and names listed in
 ``__all__`` count as used; ``# noqa`` on the import line skips it.
 
     python tools/lint.py [paths...]        # exit 1 and one line per finding
@@ -115,6 +117,10 @@ def main(argv: list[str]) -> int:
             continue
         problems += unused_imports(f, src)
         problems += undefined_globals(f, src)
+    if not argv:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from prune_profiles import check_citations
+        problems += [f"cited but missing: {m}" for m in check_citations()]
     for p in problems:
         print(os.path.relpath(p, ROOT) if p.startswith(ROOT) else p)
     return 1 if problems else 0
