@@ -508,3 +508,53 @@ def test_lease_returns_from_other_nodes_count_towards_the_limit(tmp_path):
         assert len(dead) == 1 and not _gets(e.origin, "/n.mkv")
         await e.down()
     run(main())
+
+
+def test_a_leased_job_survives_a_broker_connection_drop(tmp_path):
+    """The connection drops while a leased job runs: the lease copy sits in
+    its durable queue, the worker reconnects, keeps renewing, finishes the
+    job and deletes the copy.  Nothing comes back and nothing is redelivered."""
+    async def main():
+        e = await Env().up(tmp_path, lease_after_s=0.1, lease_s=1.0)
+        e.origin.rate = 1_000_000
+        data = os.urandom(2_500_000)
+        url = e.origin.add("/drop.mkv", data)
+        e.submit(Media(id="drop", source_uri=url))
+        t0 = time.monotonic()
+        while not e.amqp.lease_stats["taken"]:
+            assert time.monotonic() - t0 < 10
+            await asyncio.sleep(0.02)
+        await e.broker.drop_connections()
+        res = await e.wait_results(1, timeout=30)
+        assert res[0].ok, res
+        await asyncio.sleep(1.5)                          # past a TTL: nothing returns
+        assert all(e.broker.queue_depth(q) == 0 for q in e.broker.queues if q.startswith("v1.download"))
+        assert e.amqp.lease_stats["released"] == 1 and e.amqp.lease_stats["lost"] == 0
+        assert len(_gets(e.origin, "/drop.mkv")) == 1 and len(e.converts()) == 1
+        await e.down()
+    run(main())
+
+
+def test_a_job_parked_past_the_consumer_timeout_is_leased(tmp_path):
+    """A failed job parked in-process (the broker refused its delay queue)
+    waits retry_delay_max_s unacked: the lease keeps consumer_timeout away
+    from it too, and the parked retry still goes out after the wait."""
+    from .test_permissions import REF_PERMS
+
+    async def main():
+        # the reference's permissions plus what a lease needs: configure and read on the lease
+        # queues (a queue with a dead-letter exchange needs read), write on the default exchange
+        perms = dict(REF_PERMS, configure=r"^v1\.download(-\d+)?(\.lease\..*)?$",
+                     read=r"^v1\.download(-\d+)?(\.lease\..*)?$",
+                     write=r"^(v1\.download(-\d+)?|v1\.convert|amq\.default)$")
+        e = await Env().up(tmp_path, user="ref", perms=perms, lease_after_s=0.1, lease_s=1.0, retry_delay_s=1.5,
+                           max_retries=1)
+        e.amqp.lease_after, e.amqp.lease_ttl = 0.1, 1.0
+        e.broker.consumer_timeout = 0.5
+        e.submit(Media(id="pk", source_uri=e.origin.url("/missing.mkv")))
+        res = await e.wait_results(2, timeout=30)
+        assert [r.ok for r in res] == [False, False]
+        assert e.amqp.parked_total >= 1 and e.amqp.lease_stats["taken"] >= 1
+        assert e.broker.stats["consumer_timeouts"] == 0
+        await e.down()
+    run(main())
