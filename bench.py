@@ -380,6 +380,9 @@ def main() -> int:
                     help="pipeline commits only while the confirm round trip is at least this (ms; -1: worker default)")
     ap.add_argument("--pipeline-commit", default="on", choices=["on", "off"],
                     help="on (the worker default): a job's publish confirm and ack overlap the next job")
+    ap.add_argument("--lease-after", type=float, default=-1.0,
+                    help="lease a job's delivery once it has run this long (s; -1: worker default 30 s, which a "
+                         "10 MiB job never reaches; a tiny value leases every job, to price the lease)")
     ap.add_argument("--no-reference-mode", action="store_true",
                     help="skip the secondary run in the reference's cleanup-off mode after the timed region")
     ap.add_argument("--no-content-check", action="store_true",
@@ -451,6 +454,7 @@ def main() -> int:
                      recycle_bytes=(a.recycle_mb << 20) if a.recycle_mb >= 0 else -1, variants=a.variants,
                      content_check=not a.no_content_check,
                      overrides={"pipeline_commit": a.pipeline_commit == "on",
+                                **({"lease_after_s": a.lease_after} if a.lease_after >= 0 else {}),
                                 **({"pipeline_commit_min_ms": a.pipeline_min_ms} if a.pipeline_min_ms >= 0 else {}),
                                 **({"http_segment_threshold": int(a.segment_threshold_mb * (1 << 20))}
                                    if a.segment_threshold_mb > 0 else {}),
@@ -673,6 +677,7 @@ def main() -> int:
                        "prefetch": prefetch,
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "rtt_ms": a.rtt_ms, "stream_mbps": a.stream_mbps or None,
+                       "lease_after_s": stack.cfg.lease_after_s if stack.cfg is not None else None,
                        "log_level": a.log_level,
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),
