@@ -30,8 +30,11 @@ Differences, all documented fixes:
   dialled (the reference ``log.Fatal``-ed in ``NewUploader``,
   ``downloader.go:95-98``);
 * B12 — broker connect errors are checked before use;
-* ``concurrency`` job loops per process (default 1 = reference), each job
-  fully async so downloads / uploads of different jobs overlap.  A job
+* jobs in flight per process: adaptive by default (1 while jobs keep the
+  CPUs busy, up to ``concurrency_max`` while they wait on the network,
+  :mod:`tritondl.parallel.adaptive`), or a fixed ``concurrency`` (1 = the
+  reference), each job fully async so downloads / uploads of different
+  jobs overlap.  A job
   frees its loop once its upload is done: the ``v1.convert`` publish, its
   broker confirm and the ack finish in the job's own task while the next
   job starts (``pipeline_commit``, on by default).  The reference published
@@ -60,6 +63,11 @@ Differences, all documented fixes:
   (:meth:`Service.health`) — the reference's 1 s scheduler re-created dead
   processors (``client.go:139-166``), and no probe could see one that stayed
   dead;
+* a job that outlives ``lease_after_s`` is leased (its delivery acked, a
+  renewed copy held by the broker; :meth:`Delivery.hold`), so RabbitMQ's
+  ``consumer_timeout`` never sends a running job to a second worker; a copy
+  of a running job is handed back within ``job_lock_wait_s`` and a copy of a
+  finished one acked through the node's done-ledger;
 * in-flight jobs are drained on shutdown (the Go job goroutine was never
   joined); the work dir can optionally be cleaned after success (B15).
 """
