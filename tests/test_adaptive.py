@@ -16,6 +16,10 @@ WAITING = {"probe": 0.040, "fetched": 0.045, "upload": 0.070}     # 20 ms RTT: m
 BUSY = {"probe": 0.0002, "fetched": 0.0021, "upload": 0.0022}      # loopback: the CPU moves bytes
 
 
+def _ctl(cap: int, **kw) -> Controller:
+    return Controller(cap, warmup_jobs=0, **kw)
+
+
 def _feed(c: Controller, marks: dict, n: int) -> list[int]:
     seen = []
     for _ in range(n):
@@ -25,27 +29,44 @@ def _feed(c: Controller, marks: dict, n: int) -> list[int]:
 
 
 def test_waiting_jobs_double_the_limit_up_to_the_cap():
-    c = Controller(4, cpus=64)
+    c = _ctl(4, cpus=64)
     assert c.limit == 1
     assert _feed(c, WAITING, 20) == [2, 4]
     assert c.limit == 4 and c.last["why"] == "network waits dominate"
     assert _feed(c, WAITING, 20) == []          # the cap holds
-    c8 = Controller(8, cpus=64)
+    c8 = _ctl(8, cpus=64)
     _feed(c8, WAITING, 40)
     assert c8.limit == 8
 
 
 def test_cpu_bound_jobs_stay_at_one_and_bring_the_limit_back_down():
-    c = Controller(4, cpus=64)
+    c = _ctl(4, cpus=64)
     assert _feed(c, BUSY, 50) == [] and c.limit == 1
-    _feed(c, WAITING, 10)
+    _feed(c, WAITING, 12)
     assert c.limit == 4
-    assert _feed(c, BUSY, 30) == [3, 2, 1]
+    assert _feed(c, BUSY, 40) == [3, 2, 1]
     assert c.last["why"] == "jobs are cpu-bound"
 
 
+def test_the_first_decision_waits_for_the_warm_up_jobs():
+    c = Controller(4, cpus=64)                  # warmup_jobs=8: connection set-up looks like waiting
+    assert _feed(c, WAITING, 8) == [] and c.limit == 1
+    assert _feed(c, WAITING, 4) == [2]
+
+
+def test_loopback_shaped_jobs_keep_one_job_at_a_time():
+    """The box's loopback job: response head 0.15 ms after dispatch, S3 reply
+    0.27 ms after the last byte, 2.15 ms in all: wait share ~0.2."""
+    c = _ctl(4, cpus=16)
+    loop = {"dispatch": 0.0001, "probe": 0.00025, "fetched": 0.00188, "upload": 0.00215}
+    assert _feed(c, loop, 60) == [] and c.limit == 1
+    c.limit = 2                                  # a transient raise drops back while jobs look like that
+    hot = {"dispatch": 0.00013, "probe": 0.0008, "fetched": 0.0030, "upload": 0.0034}   # ~0.32 at 2 in flight
+    assert _feed(c, hot, 8) == [1]
+
+
 def test_a_busy_cpu_lowers_the_limit_whatever_the_waits():
-    c = Controller(4, cpus=1, cpu_high=0.6)
+    c = _ctl(4, cpus=1, cpu_high=0.6)
     c.limit = 4
     t_end = time.process_time() + 0.3
     while time.process_time() < t_end:            # burn this process's CPU: share ~1.0 of one CPU
@@ -56,16 +77,16 @@ def test_a_busy_cpu_lowers_the_limit_whatever_the_waits():
 
 def test_a_tight_disk_reserve_pins_the_limit_to_one():
     free = [100 << 30]
-    c = Controller(4, cpus=64, free_bytes=lambda: free[0], reserve=10 << 30)
-    _feed(c, WAITING, 10)
+    c = _ctl(4, cpus=64, free_bytes=lambda: free[0], reserve=10 << 30)
+    _feed(c, WAITING, 12)
     assert c.limit == 4
     free[0] = (10 << 30) + (15 << 20)             # less than reserve + 2 jobs of 10 MiB
-    _feed(c, WAITING, 4)
+    _feed(c, WAITING, 8)
     assert c.limit == 1 and c.last["why"] == "disk reserve"
 
 
 def test_long_jobs_with_idle_cpus_raise_the_limit_on_ticks():
-    c = Controller(4, cpus=64, period_s=0.05)
+    c = _ctl(4, cpus=64, period_s=0.05)
     time.sleep(0.06)
     assert c.tick(all_busy=True) and c.limit == 2
     time.sleep(0.06)

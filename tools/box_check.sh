@@ -23,7 +23,11 @@ for i in 1 2; do
   b rtt20_default_$i --steps 100 --warmup 10 --rtt-ms 20 || exit 1
   b rtt20_c1_$i --steps 40 --warmup 5 --rtt-ms 20 --concurrency 1 || exit 1
 done
+# price of a lease per job: every job leased at once (--lease-after ~0), default concurrency
+b lease_rtt0 --steps 200 --warmup 20 --lease-after 0.0001 || exit 1
+b lease_rtt2 --steps 200 --warmup 20 --rtt-ms 2 --lease-after 0.0001 || exit 1
+b lease_rtt20 --steps 100 --warmup 10 --rtt-ms 20 --lease-after 0.0001 || exit 1
 python tools/bench_summary.py "$out"/*.log > "$out/SUMMARY.txt" 2>&1 || true
-for f in "$out"/drv*.log "$out"/rtt*.log; do
+for f in "$out"/drv*.log "$out"/rtt*.log "$out"/lease*.log; do
   tail -n 1 "$f" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$f', d['value'], d['config']['concurrency_limit_end'], d['cpu_ms_per_job']['worker'], d['diag']['concurrency']['last_decision'])"
 done
