@@ -1,0 +1,364 @@
+"""HTTP/2 client connections (RFC 9113) for the HTTP downloader.
+
+grab's transport was Go's ``http.Transport`` (``internal/downloader/http/
+http.go:18-22``), which offers ``h2`` in the TLS handshake (ALPN) and speaks
+HTTP/2 to any https origin that accepts it, carrying every request to that
+origin as a stream of one TCP connection.  :class:`H2Connection` does the
+same for :class:`~tritondl.fetch.http.HTTPDownloader` (``http2=True``): a job's
+probe and its Range segments become concurrent streams of one connection
+per origin.  An origin that answers ALPN with ``http/1.1`` (or nothing) is
+remembered and served by the HTTP/1.1 paths.
+
+What is implemented is what a downloading client needs: the connection
+preface and SETTINGS exchange, HEADERS + CONTINUATION with HPACK
+(:mod:`tritondl.utils.hpack`), DATA with padding, receive flow control with
+large windows (16 MiB per stream, 256 MiB per connection) replenished as the
+body is consumed (back-pressure reaches the server), RST_STREAM, PING,
+GOAWAY (streams above the last processed id fail retryably), and
+SETTINGS_MAX_CONCURRENT_STREAMS.  Server push is disabled.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import collections
+import ssl
+import struct
+
+from multidict import CIMultiDict
+
+from ..utils import dial
+from ..utils.hpack import Decoder, Encoder, HPACKError
+
+PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+DATA, HEADERS, PRIORITY, RST_STREAM, SETTINGS, PUSH_PROMISE, PING, GOAWAY, WINDOW_UPDATE, CONTINUATION = range(10)
+END_STREAM = ACK = 0x1
+END_HEADERS = 0x4
+PADDED = 0x8
+PRIORITY_FLAG = 0x20
+S_HEADER_TABLE_SIZE, S_ENABLE_PUSH, S_MAX_CONCURRENT_STREAMS, S_INITIAL_WINDOW_SIZE, S_MAX_FRAME_SIZE, \
+    S_MAX_HEADER_LIST_SIZE = range(1, 7)
+NO_ERROR, PROTOCOL_ERROR, INTERNAL_ERROR, FLOW_CONTROL_ERROR, SETTINGS_TIMEOUT, STREAM_CLOSED, FRAME_SIZE_ERROR, \
+    REFUSED_STREAM, CANCEL, COMPRESSION_ERROR = range(10)
+
+STREAM_WINDOW = 16 << 20          # what the server may send on one stream before we consume it
+CONN_WINDOW = 256 << 20           # ... on the whole connection
+MAX_FRAME = 1 << 20               # largest frame we accept (the server may use 16 KiB..this)
+
+
+def frame(ftype: int, flags: int, stream: int, payload: bytes = b"") -> bytes:
+    n = len(payload)
+    return struct.pack(">BHBBI", n >> 16, n & 0xFFFF, ftype, flags, stream & 0x7FFFFFFF) + payload
+
+
+class H2Error(ConnectionError):
+    """The connection failed (a protocol error, GOAWAY for this stream, EOF)."""
+
+
+class StreamReset(H2Error):
+    def __init__(self, stream: int, code: int) -> None:
+        super().__init__(f"stream {stream} reset by the server (error code {code})")
+        self.code = code
+
+
+class H2Stream:
+    """One request's response: ``status`` / ``headers`` once :meth:`response`
+    returns, then the body through :meth:`read`."""
+
+    def __init__(self, conn: "H2Connection", sid: int) -> None:
+        self.conn, self.id = conn, sid
+        self.status = 0
+        self.headers: CIMultiDict = CIMultiDict()
+        self._head = asyncio.get_running_loop().create_future()
+        self._chunks: collections.deque = collections.deque()
+        self._event = asyncio.Event()
+        self.eof = False
+        self.error: BaseException | None = None
+        self._unacked = 0                  # bytes consumed and not yet returned as window credit
+        self.window = STREAM_WINDOW        # bytes the server may still send on this stream
+        self.buffered = 0                  # body bytes received and not yet read
+        self.body_read = 0
+        self.limit: int | None = None      # body bytes the reader will take in all (see want())
+
+    async def response(self) -> "H2Stream":
+        await self._head
+        return self
+
+    def _fail(self, e: BaseException) -> None:
+        if self.error is None and not self.eof:
+            self.error = e
+        if not self._head.done():
+            self._head.set_exception(e)
+        self._event.set()
+
+    async def read(self, n: int = -1) -> bytes:
+        """Up to ``n`` body bytes (all that is buffered for ``n < 0``); b"" at
+        the end of the body."""
+        while not self._chunks:
+            if self.error is not None:
+                raise self.error
+            if self.eof:
+                return b""
+            self._event.clear()
+            await self._event.wait()
+        c = self._chunks.popleft()
+        if 0 <= n < len(c):
+            self._chunks.appendleft(c[n:])
+            c = c[:n]
+        self.buffered -= len(c)
+        self.body_read += len(c)
+        self.conn._consumed(self, len(c))
+        return c
+
+    def want(self, n: int) -> None:
+        """The reader takes only ``n`` more body bytes (then cancels): window
+        credit stops there, so the server overshoots by no more than what
+        was already granted.  A probe stream opened at ``bytes=0-`` that
+        becomes segment 0 uses this to keep the next segments' bytes from
+        being sent twice."""
+        self.limit = self.body_read + n
+
+    def at_eof(self) -> bool:
+        return self.eof and not self._chunks
+
+    def cancel(self) -> None:
+        """Stop the response (RST_STREAM CANCEL) unless it has ended."""
+        if not self.eof and self.error is None:
+            self.error = H2Error("cancelled")
+            self.conn._reset(self.id, CANCEL)
+        self.conn.streams.pop(self.id, None)
+
+
+class H2Connection:
+    def __init__(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter, authority: str) -> None:
+        self.r, self.w = reader, writer
+        self.authority = authority
+        self.streams: dict[int, H2Stream] = {}
+        self.next_id = 1
+        self.peer = {S_MAX_CONCURRENT_STREAMS: 1 << 31, S_MAX_FRAME_SIZE: 16384, S_HEADER_TABLE_SIZE: 4096}
+        self.encoder = Encoder(huffman=True, index=False)
+        self.decoder = Decoder(4096)
+        self.closed: BaseException | None = None
+        self.goaway_last: int | None = None
+        self._conn_unacked = 0
+        self._slots = asyncio.Event()
+        self._slots.set()
+        self._reader: asyncio.Task | None = None
+        self.streams_opened = 0
+
+    @classmethod
+    async def open(cls, host: str, port: int, ctx: ssl.SSLContext, *, timeout: float = 30.0) -> "H2Connection | None":
+        """Dial (fast fallback, keep-alive) and handshake offering ``h2``;
+        None when the server picks HTTP/1.1 (or no protocol)."""
+        ctx.set_alpn_protocols(["h2", "http/1.1"])
+        r, w = await asyncio.wait_for(dial.open_connection(host, port, timeout=timeout, ssl=ctx), timeout)
+        sslobj = w.get_extra_info("ssl_object")
+        if sslobj is None or sslobj.selected_alpn_protocol() != "h2":
+            w.close()
+            return None
+        c = cls(r, w, host if port == 443 else f"{host}:{port}")
+        w.write(PREFACE + frame(SETTINGS, 0, 0, struct.pack(">HIHIHIHI", S_ENABLE_PUSH, 0, S_INITIAL_WINDOW_SIZE,
+                                                               STREAM_WINDOW, S_MAX_FRAME_SIZE, MAX_FRAME,
+                                                               S_HEADER_TABLE_SIZE, 4096))
+                + frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", CONN_WINDOW - 65535)))
+        await w.drain()
+        c._reader = asyncio.ensure_future(c._read_loop())
+        return c
+
+    @property
+    def alive(self) -> bool:
+        return self.closed is None and self.goaway_last is None
+
+    # ------------------------------------------------------------ requests
+    async def request(self, headers: list[tuple[bytes, bytes]]) -> H2Stream:
+        """Send a GET (``headers`` include the pseudo-headers) as a new stream."""
+        while len(self.streams) >= self.peer[S_MAX_CONCURRENT_STREAMS]:
+            if not self.alive:
+                break
+            self._slots.clear()
+            await self._slots.wait()
+        if not self.alive:
+            raise H2Error(f"connection to {self.authority} is closing: {self.closed or 'GOAWAY'}")
+        sid = self.next_id
+        self.next_id += 2
+        st = H2Stream(self, sid)
+        self.streams[sid] = st
+        self.streams_opened += 1
+        block = self.encoder.encode(headers)
+        mx = self.peer[S_MAX_FRAME_SIZE]
+        first, rest = block[:mx], block[mx:]
+        out = [frame(HEADERS, END_STREAM | (0 if rest else END_HEADERS), sid, first)]
+        while rest:
+            part, rest = rest[:mx], rest[mx:]
+            out.append(frame(CONTINUATION, 0 if rest else END_HEADERS, sid, part))
+        self.w.write(b"".join(out))      # one write: no other frame can land between them
+        await self.w.drain()
+        return st
+
+    def _reset(self, sid: int, code: int) -> None:
+        if self.closed is None:
+            self.w.write(frame(RST_STREAM, 0, sid, struct.pack(">I", code)))
+        self._slots.set()
+
+    def _consumed(self, st: H2Stream | None, n: int) -> None:
+        """Return window credit once a quarter of a window has been read (or
+        the stream's window runs low), never past a stream's ``limit``."""
+        self._conn_unacked += n
+        out = []
+        if st is not None:
+            st._unacked += n
+        if st is not None and st._unacked and not st.eof:
+            inc = st._unacked
+            if st.limit is not None:
+                need = st.limit - st.body_read - st.buffered
+                inc = min(inc, max(0, need - st.window))
+            if inc and (inc >= STREAM_WINDOW // 4 or st.window < STREAM_WINDOW // 4):
+                out.append(frame(WINDOW_UPDATE, 0, st.id, struct.pack(">I", inc)))
+                st._unacked -= inc
+                st.window += inc
+        if self._conn_unacked >= CONN_WINDOW // 4:
+            out.append(frame(WINDOW_UPDATE, 0, 0, struct.pack(">I", self._conn_unacked)))
+            self._conn_unacked = 0
+        if out and self.closed is None:
+            self.w.write(b"".join(out))
+
+    async def close(self) -> None:
+        if self.closed is None:
+            self.closed = H2Error("closed by client")
+            try:
+                self.w.write(frame(GOAWAY, 0, 0, struct.pack(">II", 0, NO_ERROR)))
+                self.w.close()
+            except (ConnectionError, RuntimeError):
+                pass
+        if self._reader is not None:
+            self._reader.cancel()
+        for st in list(self.streams.values()):
+            st._fail(self.closed)
+
+    # ------------------------------------------------------------ frames in
+    async def _read_loop(self) -> None:
+        hblock: bytearray | None = None
+        hstream = hflags = 0
+        try:
+            while True:
+                head = await self.r.readexactly(9)
+                ln = (head[0] << 16) | (head[1] << 8) | head[2]
+                ftype, flags = head[3], head[4]
+                sid = struct.unpack(">I", head[5:9])[0] & 0x7FFFFFFF
+                if ln > MAX_FRAME:
+                    raise H2Error(f"frame of {ln} bytes above the {MAX_FRAME} we allow")
+                payload = await self.r.readexactly(ln) if ln else b""
+                if hblock is not None and (ftype != CONTINUATION or sid != hstream):
+                    raise H2Error("header block interrupted by another frame")
+                if ftype == DATA:
+                    self._on_data(sid, flags, payload)
+                elif ftype in (HEADERS, CONTINUATION):
+                    if ftype == HEADERS:
+                        hblock, hstream, hflags = bytearray(self._strip(flags, payload, ftype)), sid, flags
+                    else:
+                        if hblock is None:
+                            raise H2Error("CONTINUATION without HEADERS")
+                        hblock += payload
+                    if flags & END_HEADERS:
+                        self._on_headers(hstream, hflags, bytes(hblock))
+                        hblock = None
+                elif ftype == RST_STREAM:
+                    st = self.streams.pop(sid, None)
+                    if st is not None:
+                        st._fail(StreamReset(sid, struct.unpack(">I", payload[:4])[0]))
+                    self._slots.set()
+                elif ftype == SETTINGS:
+                    if not flags & ACK:
+                        for k in range(0, len(payload) - 5, 6):
+                            key, val = struct.unpack(">HI", payload[k:k + 6])
+                            self.peer[key] = val
+                        self.w.write(frame(SETTINGS, ACK, 0))
+                        self._slots.set()
+                elif ftype == PING:
+                    if not flags & ACK:
+                        self.w.write(frame(PING, ACK, 0, payload))
+                elif ftype == GOAWAY:
+                    last, code = struct.unpack(">II", payload[:8])
+                    self.goaway_last = last & 0x7FFFFFFF
+                    for k, st in list(self.streams.items()):
+                        if k > self.goaway_last:
+                            self.streams.pop(k, None)
+                            st._fail(H2Error(f"GOAWAY (code {code}): stream {k} was not processed; retry it"))
+                    self._slots.set()
+                elif ftype == PUSH_PROMISE:
+                    raise H2Error("PUSH_PROMISE with push disabled")
+                # WINDOW_UPDATE (we send no DATA), PRIORITY and unknown types are ignored
+        except asyncio.CancelledError:
+            return
+        except (asyncio.IncompleteReadError, ConnectionError, OSError, HPACKError, struct.error) as e:
+            err = e if isinstance(e, H2Error) else H2Error(f"HTTP/2 connection to {self.authority}: {e}")
+            if isinstance(e, HPACKError):
+                err = H2Error(f"HTTP/2 header block from {self.authority} does not decode: {e}")
+            self.closed = err
+            for st in list(self.streams.values()):
+                st._fail(err)
+            self.streams.clear()
+            self._slots.set()
+            try:
+                self.w.close()
+            except RuntimeError:
+                pass
+
+    @staticmethod
+    def _strip(flags: int, payload: bytes, ftype: int) -> bytes:
+        pad = 0
+        if flags & PADDED:
+            pad = payload[0]
+            payload = payload[1:]
+        if ftype == HEADERS and flags & PRIORITY_FLAG:
+            payload = payload[5:]
+        if pad:
+            if pad > len(payload):
+                raise H2Error("padding longer than the frame")
+            payload = payload[:-pad]
+        return payload
+
+    def _on_data(self, sid: int, flags: int, payload: bytes) -> None:
+        st = self.streams.get(sid)
+        body = self._strip(flags, payload, DATA)
+        if st is None:
+            # a stream we reset or finished: its bytes still count against the connection window
+            self._consumed(None, len(payload))
+            return
+        st.window -= len(payload)
+        if len(payload) > len(body):                # padding is flow-controlled too
+            st._unacked += len(payload) - len(body)
+            self._conn_unacked += len(payload) - len(body)
+        if body:
+            st._chunks.append(body)
+            st.buffered += len(body)
+        if flags & END_STREAM:
+            st.eof = True
+            self.streams.pop(sid, None)
+            self._slots.set()
+        st._event.set()
+
+    def _on_headers(self, sid: int, flags: int, block: bytes) -> None:
+        fields = self.decoder.decode(block)        # always: the HPACK state must follow every block
+        st = self.streams.get(sid)
+        if st is None:
+            return
+        if not st._head.done():
+            status = next((v for n, v in fields if n == b":status"), None)
+            if status is None:
+                raise H2Error(f"response on stream {sid} without :status")
+            code = int(status)
+            if 100 <= code < 200:
+                return                                  # informational: the real head follows
+            st.status = code
+            st.headers = CIMultiDict((n.decode("latin-1"), v.decode("latin-1")) for n, v in fields
+                                     if not n.startswith(b":"))
+            st._head.set_result(st)
+        if flags & END_STREAM:                          # (trailers are read and dropped)
+            st.eof = True
+            self.streams.pop(sid, None)
+            self._slots.set()
+            st._event.set()
+
+
+__all__ = ["H2Connection", "H2Stream", "H2Error", "StreamReset", "frame"]

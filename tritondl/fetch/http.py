@@ -40,7 +40,12 @@ Beyond the reference:
 * the file's mtime is set from ``Last-Modified``, as grab does;
 * when one segment fails, its siblings are cancelled and their pumps
   stopped and awaited before the file or any socket is closed (no write
-  through a recycled fd number).
+  through a recycled fd number);
+* with ``http2`` (``TRITONDL_HTTP2=1``) an https origin is first offered
+  HTTP/2 in the TLS handshake, as Go's transport under grab did: if it
+  accepts, the probe and every Range segment are streams of one connection
+  (:mod:`tritondl.fetch.h2`); an origin that keeps to HTTP/1.1 is
+  remembered and served by the paths above.
 """
 
 from __future__ import annotations
@@ -62,6 +67,7 @@ from ..utils import rawhttp, spares
 from ..utils.dial import FALLBACK_DELAY, socket_factory
 from ..utils.disk import DiskSpaceError, check_space
 from ..utils.log import log
+from . import h2 as _h2
 from .registry import ClientRegister, ProgressSink
 
 
@@ -98,6 +104,39 @@ def retry_after(r) -> float | None:
         return max(0.0, (when - datetime.datetime.now(datetime.timezone.utc)).total_seconds())
     except (TypeError, ValueError, IndexError):
         return None
+
+
+class _H2Content:
+    def __init__(self, st: "_h2.H2Stream") -> None:
+        self._st = st
+
+    async def iter_chunked(self, n: int):
+        while True:
+            b = await self._st.read(n)
+            if not b:
+                return
+            yield b
+
+    def at_eof(self) -> bool:
+        return self._st.at_eof()
+
+
+class _H2Response:
+    """The bits of an aiohttp response this module uses, over one HTTP/2
+    stream (its body is read by :meth:`HTTPDownloader._consume`)."""
+
+    def __init__(self, st: "_h2.H2Stream", url: str) -> None:
+        self.st = st
+        self.status = st.status
+        self.headers = st.headers
+        self.url = URL(url)
+        self.content = _H2Content(st)
+
+    def release(self) -> None:
+        self.st.cancel()            # a no-op once the body has ended
+
+    def close(self) -> None:
+        self.st.cancel()
 
 
 class _RawResponse:
@@ -207,8 +246,14 @@ class HTTPDownloader:
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
                  ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
-                 disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None) -> None:
+                 disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None, http2: bool = False) -> None:
         self.progress_interval = progress_interval
+        # offer HTTP/2 to https origins (ALPN), as Go's transport under grab did
+        self.http2 = http2
+        self._h2conns: dict[tuple[str, int], "_h2.H2Connection"] = {}
+        self._h2locks: dict[tuple[str, int], asyncio.Lock] = {}
+        self._h1_only: dict[tuple[str, int], float] = {}     # origins that answered ALPN with http/1.1
+        self.h2_streams = 0
         # egress proxy (HTTP_PROXY / HTTPS_PROXY / NO_PROXY, Go semantics); None = the environment
         self.proxies = proxies
         self.disk_reserve = disk_reserve            # bytes to keep free (utils.disk preflight)
@@ -278,6 +323,9 @@ class HTTPDownloader:
         return self._session
 
     async def close(self) -> None:
+        for c in list(self._h2conns.values()):
+            await c.close()
+        self._h2conns.clear()
         self._raw.close()
         if self._session is not None:
             await self._session.close()
@@ -317,8 +365,13 @@ class HTTPDownloader:
             raise
 
     async def _open(self, url: str, headers: dict):
-        """GET ``url``: a :class:`_RawResponse` on the native path (plain
+        """GET ``url``: an :class:`_H2Response` when the origin speaks HTTP/2
+        (``http2``), a :class:`_RawResponse` on the native path (plain
         http, identity body, no redirect), else an open aiohttp response."""
+        if self.http2 and url.startswith("https://"):
+            r = await self._h2_get(url, headers)
+            if r is not None:
+                return r
         if self._native_for(url) is not None:
             r = await self._raw_get(url, headers)
             if r is not None:
@@ -328,6 +381,75 @@ class HTTPDownloader:
             r.release()
             raise _FatalHTTPError(f"GET {url}: proxy authentication required (407)")
         return r
+
+    def _h2_ssl(self):
+        import ssl
+        ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
+        return ctx
+
+    async def _h2_conn(self, host: str, port: int) -> "_h2.H2Connection | None":
+        """The origin's live HTTP/2 connection (opened on first use; one per
+        origin, shared by every stream), or None if it speaks HTTP/1.1."""
+        key = (host, port)
+        c = self._h2conns.get(key)
+        if c is not None and c.alive:
+            return c
+        if time.monotonic() < self._h1_only.get(key, 0.0):
+            return None
+        lock = self._h2locks.setdefault(key, asyncio.Lock())
+        async with lock:
+            c = self._h2conns.get(key)
+            if c is not None and c.alive:
+                return c
+            try:
+                c = await _h2.H2Connection.open(host, port, self._h2_ssl(), timeout=30.0)
+            except (OSError, asyncio.TimeoutError) as e:
+                raise aiohttp.ClientConnectionError(f"https://{host}:{port}: {e}") from e
+            if c is None:
+                self._h1_only[key] = time.monotonic() + 3600.0
+                log.with_fields(origin=f"{host}:{port}").debug("origin does not speak HTTP/2; using HTTP/1.1")
+                return None
+            self._h2conns[key] = c
+            return c
+
+    async def _h2_get(self, url: str, headers: dict) -> "_H2Response | None":
+        """GET over HTTP/2, following redirects like :meth:`_raw_get`; None
+        when the origin (or a redirect target) does not speak it, or a proxy
+        is in the way (the HTTP/1.1 paths handle those)."""
+        for _hop in range(self.max_redirects + 1):
+            u = URL(url)
+            if u.scheme != "https" or self._proxy(url) is not None:
+                return None
+            host, port = u.raw_host or "", u.port or 443
+            c = await self._h2_conn(host, port)
+            if c is None:
+                return None
+            hh = {"Accept-Encoding": "identity",
+                  **({} if "Authorization" in headers else rawhttp.basic_auth_header(u)), **headers}
+            path = u.raw_path_qs or "/"
+            fields = [(b":method", b"GET"), (b":scheme", b"https"), (b":authority", c.authority.encode()),
+                      (b":path", path.encode())]
+            fields += [(k.lower().encode(), str(v).encode()) for k, v in hh.items()
+                       if k.lower() not in ("host", "connection", "keep-alive", "transfer-encoding", "upgrade")]
+            try:
+                st = await c.request(fields)
+                await asyncio.wait_for(st.response(), self.read_timeout)
+            except (_h2.H2Error, asyncio.TimeoutError) as e:
+                raise aiohttp.ClientConnectionError(f"GET {url} (HTTP/2): {e}") from e
+            self.h2_streams += 1
+            loc = st.headers.get("Location")
+            if st.status in (301, 302, 303, 307, 308) and loc:
+                st.cancel()
+                try:
+                    url = str(u.join(URL(loc)))
+                except (ValueError, TypeError) as e:
+                    raise HTTPDownloadError(f"GET {url}: bad redirect Location {loc!r}") from e
+                continue
+            if 300 <= st.status < 400:
+                st.cancel()
+                return None
+            return _H2Response(st, url)
+        raise HTTPDownloadError(f"GET {url}: stopped after {self.max_redirects} redirects")
 
     async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":
         """Native GET.  Redirects (301/302/303/307/308, relative or absolute,
@@ -746,6 +868,8 @@ class HTTPDownloader:
         loop = asyncio.get_running_loop()
         start = segs[i][0]
         limit = (end - pos) if end >= 0 else -1
+        if limit >= 0 and isinstance(r, _H2Response):
+            r.st.want(limit)
         bufs: list[bytes] = []
         nbuf = 0
         wpos = pos
