@@ -109,6 +109,7 @@ class DeliveryMetadata:
 LEASE_RETURNS = "X-Lease-Returns"   # times the job came back because its holder's lease ran out
 LEASE_HOLDER = "X-Lease-Holder"     # host:pid that holds the lease copy (diagnostics)
 BUSY = "X-Busy"                     # hand-backs because another worker was running the same job
+OPS_CHANNELS = 8                    # idle lease-ops channels kept open
 
 
 def _int_header(headers: dict | None, name: str) -> int:
@@ -425,7 +426,7 @@ class Client:
         self._lease_refused: set[str] = set()      # routing keys whose lease queues the broker refused
         self._leased: set[Delivery] = set()        # leased deliveries not settled yet
         self._holding: set[Delivery] = set()       # deliveries whose lease task runs (Delivery.hold)
-        self._ops_ch: Channel | None = None
+        self._ops_free: list[Channel] = []     # idle lease-ops channels (one RPC in flight per channel)
         self.lease_stats = {"taken": 0, "renewed": 0, "released": 0, "lost": 0, "requeued": 0, "refused": 0}
         self._closing = False
         self._bg: set[asyncio.Task] = set()
@@ -904,13 +905,29 @@ class Client:
             hdrs.pop(LEASE_RETURNS, None)
         return dataclasses.replace(base, headers=hdrs, delivery_mode=codec.PERSISTENT, expiration=None)
 
-    async def _ops(self) -> Channel:
-        """A plain channel for lease declares and deletes, kept open between
-        uses (a refusal closes it; the next use opens another)."""
-        ch = self._ops_ch
-        if ch is None or ch.is_closed or self.conn is None or ch.conn is not self.conn:
-            ch = self._ops_ch = await self._channel(qos=False)
-        return ch
+    @contextlib.asynccontextmanager
+    async def _ops(self):
+        """A plain channel for lease declares and deletes.  AMQP allows one
+        synchronous method in flight per channel, so concurrent jobs take
+        channels of their own from a small free list instead of queueing
+        behind one (at 20 ms RTT a shared channel capped leasing at ~25
+        jobs/s).  A refusal closes a channel; it is not returned."""
+        ch = None
+        while self._ops_free:
+            c = self._ops_free.pop()
+            if not c.is_closed and self.conn is not None and c.conn is self.conn:
+                ch = c
+                break
+        if ch is None:
+            ch = await self._channel(qos=False)
+        try:
+            yield ch
+        finally:
+            if not ch.is_closed and ch.conn is self.conn and len(self._ops_free) < OPS_CHANNELS:
+                self._ops_free.append(ch)
+            elif not ch.is_closed:
+                with contextlib.suppress(AMQPError, ConnectionError, OSError):
+                    await ch.close()
 
     async def _lease_put(self, d: Delivery, lease: Lease) -> str:
         """Declare lease queue number ``lease.n`` and put the job's copy in it
@@ -919,12 +936,12 @@ class Client:
         the default exchange)."""
         name = f"{d.routing_key}.lease.{lease.token}.{lease.n}"
         ms = max(1, int(round(lease.ttl * 1000)))
-        ch = await self._ops()
         try:
-            # x-expires well past the TTL: the copy dead-letters first, then the empty queue goes
-            await ch.queue_declare(name, durable=True, arguments={
-                "x-message-ttl": ms, "x-expires": 2 * ms + 10_000,
-                "x-dead-letter-exchange": d.exchange, "x-dead-letter-routing-key": d.routing_key})
+            async with self._ops() as ch:
+                # x-expires well past the TTL: the copy dead-letters first, then the empty queue goes
+                await ch.queue_declare(name, durable=True, arguments={
+                    "x-message-ttl": ms, "x-expires": 2 * ms + 10_000,
+                    "x-dead-letter-exchange": d.exchange, "x-dead-letter-routing-key": d.routing_key})
         except ChannelClosed as e:
             if _refused(e):
                 raise LeaseRefused(str(e)) from e
@@ -947,8 +964,8 @@ class Client:
     async def _lease_drop(self, name: str) -> int:
         """Delete a lease queue; returns how many copies were still in it
         (RabbitMQ discards them, it does not dead-letter on delete)."""
-        ch = await self._ops()
-        return await ch.queue_delete(name)
+        async with self._ops() as ch:
+            return await ch.queue_delete(name)
 
     async def _lease_take(self, d: Delivery, ttl: float) -> bool:
         lease = Lease(secrets.token_hex(6), ttl)
