@@ -466,7 +466,8 @@ def test_channel_housekeeping_methods():
 def test_mandatory_publish_surfaces_unroutable_messages():
     """RabbitMQ confirms a message no queue is bound for and drops it.  With
     ``mandatory`` it sends ``basic.return`` first; the channel matches the
-    return to its publish by message_id (an unroutable message is confirmed
+    return to its publish by a private ``x-tdl-seq`` header, not the
+    producer's message_id (an unroutable message is confirmed
     at once, ahead of routable ones still being persisted, so order cannot
     match them) and fails that publish's confirm with PublishReturned."""
     from tritondl.amqp.connection import PublishReturned

@@ -166,6 +166,22 @@ def test_goaway_fails_unprocessed_streams_retryably_and_the_connection_is_replac
     run(main())
 
 
+def test_a_silent_stream_times_out_and_the_segment_is_retried(tmp_path):
+    async def main():
+        o = await H2Origin().start()
+        data = os.urandom(12 << 20)
+        url = o.add("/s.mkv", data)
+        o.stall = (6 << 20, 5.0)                           # past the first 4 MiB write block
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, read_timeout=0.5)
+        await asyncio.wait_for(dl.download(str(tmp_path), lambda u, p: None, url), 4.0)
+        assert (tmp_path / "s.mkv").read_bytes() == data
+        assert o.resets >= 1 and len(o.requests) >= 2
+        assert o.requests[-1][2] == "bytes=4194304-12582911"  # the retry resumes after what was written
+        await dl.close()
+        await o.stop()
+    run(main())
+
+
 def test_an_origin_without_h2_is_remembered_and_served_over_http1(tmp_path):
     async def main():
         from tritondl.utils import rawhttp

@@ -107,12 +107,20 @@ def retry_after(r) -> float | None:
 
 
 class _H2Content:
-    def __init__(self, st: "_h2.H2Stream") -> None:
+    def __init__(self, st: "_h2.H2Stream", read_timeout: float) -> None:
         self._st = st
+        self._timeout = read_timeout
 
     async def iter_chunked(self, n: int):
+        """Body chunks; a stream silent for the read timeout fails like an
+        HTTP/1.1 body would (a retryable connection error)."""
         while True:
-            b = await self._st.read(n)
+            try:
+                b = await asyncio.wait_for(self._st.read(n), self._timeout)
+            except asyncio.TimeoutError:
+                self._st.cancel()
+                raise aiohttp.ServerTimeoutError(
+                    f"HTTP/2 stream {self._st.id}: no body bytes for {self._timeout:g} s") from None
             if not b:
                 return
             yield b
@@ -125,12 +133,12 @@ class _H2Response:
     """The bits of an aiohttp response this module uses, over one HTTP/2
     stream (its body is read by :meth:`HTTPDownloader._consume`)."""
 
-    def __init__(self, st: "_h2.H2Stream", url: str) -> None:
+    def __init__(self, st: "_h2.H2Stream", url: str, read_timeout: float = 120.0) -> None:
         self.st = st
         self.status = st.status
         self.headers = st.headers
         self.url = URL(url)
-        self.content = _H2Content(st)
+        self.content = _H2Content(st, read_timeout)
 
     def release(self) -> None:
         self.st.cancel()            # a no-op once the body has ended
@@ -448,7 +456,7 @@ class HTTPDownloader:
             if 300 <= st.status < 400:
                 st.cancel()
                 return None
-            return _H2Response(st, url)
+            return _H2Response(st, url, self.read_timeout)
         raise HTTPDownloadError(f"GET {url}: stopped after {self.max_redirects} redirects")
 
     async def _raw_get(self, url: str, headers: dict) -> "_RawResponse | None":

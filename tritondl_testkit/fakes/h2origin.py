@@ -11,7 +11,8 @@ SETTINGS_MAX_FRAME_SIZE, and PING / RST_STREAM / GOAWAY are honoured.
 Fault and shaping knobs: ``stream_rate`` (bytes/s per stream),
 ``conn_rate`` (bytes/s per connection: one TCP window over a WAN path),
 ``pad`` (pad every DATA frame), ``max_streams`` (SETTINGS_MAX_CONCURRENT_
-STREAMS), ``goaway_after`` (GOAWAY after that many streams), ``alpn``
+STREAMS), ``goaway_after`` (GOAWAY after that many streams), ``stall`` ((offset,
+seconds): one stream goes silent mid-body), ``alpn``
 (offer only ``http/1.1`` to test the fallback); ``redirects`` maps a path
 to the Location of a 301.
 """
@@ -150,6 +151,13 @@ class _Conn:
                 self.credit.clear()
                 await self.credit.wait()
             n = min(end - pos, self.max_frame - (8 if srv.pad else 0), self.conn_window, self.windows[sid], 1 << 20)
+            if srv.stall is not None and pos - start <= srv.stall[0] < pos - start + n:
+                at, secs = srv.stall
+                if at > pos - start:
+                    n = at - (pos - start)
+                else:
+                    srv.stall = None
+                    await asyncio.sleep(secs)     # this stream goes silent mid-body
             body = data[pos:pos + n]
             flags = END_STREAM if pos + n >= end else 0
             if srv.pad:
@@ -206,6 +214,7 @@ class H2Origin:
         self.pad = False
         self.max_streams = 100
         self.goaway_after = 0
+        self.stall: tuple[int, float] | None = None   # (body offset, seconds): the next stream to reach it goes silent
         ca, cert, key = rawhttp.relay_module().make_test_pki([host, "localhost"])
         self._dir = tempfile.mkdtemp(prefix="tdl-h2-")
         self.ca_file = os.path.join(self._dir, "ca.pem")
