@@ -167,19 +167,24 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    on_sample=None, workdir: str | None = None, *, minutes: float = 0.0, rate: float = 0.0,
                    sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
                    torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None,
-                   tracemalloc_frames: int = 0) -> dict:
+                   tracemalloc_frames: int = 0, concurrency: int = 1, lease_after_s: float | None = None) -> dict:
     """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
     ``rate`` jobs/s (0: as fast as the worker goes).  ``tracemalloc_frames``
     > 0 traces Python allocations: the summary then lists the call sites
     whose live memory grew most from the first post-warm-up sample to the
-    end (``tracemalloc_growth``)."""
+    end (``tracemalloc_growth``).  ``concurrency`` 0 is the worker's
+    adaptive default; ``lease_after_s`` leases every job running longer
+    (the summary then carries the lease events: taken, renewed, released,
+    lost)."""
     import tracemalloc
     timed = minutes > 0
     base_snap = None
     if tracemalloc_frames > 0:
         tracemalloc.start(tracemalloc_frames)
     st = JobStack(file_size=file_size, tag="soak", workdir=workdir, tls=tls, heartbeat=heartbeat,
-                  content_check=True)
+                  content_check=True, concurrency=concurrency)
+    if lease_after_s is not None:
+        st.overrides["lease_after_s"] = lease_after_s
     if malloc_trim_s is not None:
         st.overrides["malloc_trim_s"] = malloc_trim_s
     seed = None
@@ -285,7 +290,8 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                     e = svc.amqp.confirm_ewma if svc.amqp is not None else None
                     take_sample({"healthy": ok_h, **({"health_why": why[:3]} if why else {}),
                                  "confirm_ms": round(e * 1000, 3) if e is not None else None,
-                                 "pipelined": svc._pipeline_now()})
+                                 "pipelined": svc._pipeline_now(), "concurrency_limit": svc._limit,
+                                 "leases_held": len(svc.amqp._leased) if svc.amqp is not None else None})
             elif svc.jobs_finished >= next_sample:
                 take_sample()
                 next_sample += sample_every
@@ -305,6 +311,9 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                  "where": [f"{fr.filename.rsplit('/', 2)[-2:]}:{fr.lineno}".replace("'", "") for fr in g.traceback][-4:]}
                 for g in grown[:15]]
             tracemalloc.stop()
+        if svc.amqp is not None:
+            summary["lease_stats"] = dict(svc.amqp.lease_stats)
+            summary["leases_held_at_end"] = len(svc.amqp._leased)
         if timed:
             summary.update(minutes=minutes, rate=rate, tls=tls, heartbeat=heartbeat, retry_delay=retry_delay,
                            dht_nodes=dht_nodes, reconnects=svc.amqp.reconnects if svc.amqp is not None else None)
@@ -342,6 +351,8 @@ def main() -> int:
     ap.add_argument("--rtt-ms", type=float, default=0.0, help="emulated round trip of the fakes (ms)")
     ap.add_argument("--dht-nodes", type=int, default=0, help="local DHT nodes the worker bootstraps from")
     ap.add_argument("--malloc-trim", type=float, default=None, help="worker's malloc_trim period (s; 0 = off)")
+    ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight (0: the worker's adaptive default)")
+    ap.add_argument("--lease-after", type=float, default=None, help="lease every job running longer than this (s)")
     ap.add_argument("--tracemalloc", type=int, default=0,
                     help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
@@ -369,7 +380,8 @@ def main() -> int:
                                    on_sample=emit, minutes=a.minutes, rate=a.rate, sample_seconds=a.sample_seconds,
                                    tls=a.tls, heartbeat=a.heartbeat, retry_delay=a.retry_delay,
                                    torrent_every=a.torrent_every, dht_nodes=a.dht_nodes,
-                                   malloc_trim_s=a.malloc_trim, tracemalloc_frames=a.tracemalloc))
+                                   malloc_trim_s=a.malloc_trim, tracemalloc_frames=a.tracemalloc,
+                                   concurrency=a.concurrency, lease_after_s=a.lease_after))
     finally:
         if fh is not None:
             fh.close()
