@@ -108,7 +108,7 @@ def test_worker_raises_concurrency_when_jobs_wait_and_keeps_one_on_loopback(tmp_
         assert all(r.ok for r in res), [r for r in res if not r.ok]
         assert e.svc._limit == 4, e.svc._adapt.last
         await asyncio.sleep(0.2)
-        assert e.amqp.prefetch == 3                 # (4 running + 1 committing) over 2 shards
+        assert e.amqp.prefetch == 5                 # (4 running + 4 committing + 1 buffered) over 2 shards
         assert e.svc.metrics.get("concurrency_limit") == 4
         assert len(e.converts()) == 24
         await e.down()
