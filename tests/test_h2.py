@@ -265,3 +265,93 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path):
         await s3.stop()
         await b.stop()
     run(main(), 300)
+
+
+# ----------------------------------------------------------------- property tests
+
+from hypothesis import given, settings, strategies as hs  # noqa: E402
+
+
+@settings(max_examples=400, deadline=None)
+@given(hs.binary(max_size=200))
+def test_hpack_decoder_fails_only_with_hpack_errors_on_arbitrary_input(block):
+    """A server's header block is untrusted: anything that is not HPACK must
+    end as HPACKError (the connection then fails as COMPRESSION_ERROR), never
+    as an IndexError, a hang or a huge allocation."""
+    d = hpack.Decoder()
+    try:
+        out = d.decode(block)
+    except hpack.HPACKError:
+        return
+    assert all(isinstance(n, bytes) and isinstance(v, bytes) for n, v in out)
+    assert d.table.size <= d.limit
+
+
+# HTTP/2 field names are lower case (RFC 9113 8.2.1): the encoder lowers them
+_field = hs.tuples(hs.binary(min_size=1, max_size=40).map(bytes.lower), hs.binary(max_size=80))
+
+
+@settings(max_examples=200, deadline=None)
+@given(hs.lists(hs.lists(_field, max_size=12), min_size=1, max_size=6), hs.booleans(), hs.booleans(),
+       hs.sampled_from([0, 64, 256, 4096]))
+def test_hpack_blocks_round_trip_through_one_connection_s_tables(blocks, huffman, index, table):
+    """Encoder and decoder tables stay in step across a connection's blocks,
+    whatever the strings, the Huffman choice, indexing and the table size
+    (evictions included)."""
+    enc = hpack.Encoder(huffman=huffman, index=index, max_table_size=table)
+    dec = hpack.Decoder(table)
+    for hdrs in blocks:
+        assert dec.decode(enc.encode(hdrs)) == hdrs
+        assert dec.table.size == enc.table.size
+
+
+class _Sink:
+    """A writer that keeps what the client sends (no socket)."""
+    def __init__(self) -> None:
+        self.out = bytearray()
+
+    def write(self, b: bytes) -> None:
+        self.out += b
+
+    async def drain(self) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+    def get_extra_info(self, *_a):
+        return None
+
+
+_frames = hs.lists(hs.tuples(hs.sampled_from([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 0x0a]), hs.integers(0, 255),
+                             hs.sampled_from([0, 1, 3]), hs.binary(max_size=64)), max_size=8)
+
+
+@settings(max_examples=300, deadline=None)
+@given(_frames)
+def test_any_server_frames_end_a_stream_with_its_body_or_a_connection_error(frames):
+    """Whatever frames a server sends (random types, flags, streams and
+    payloads, then EOF), an open stream ends: its response and body either
+    arrive or fail with a ConnectionError (H2Error / StreamReset); the reader
+    never dies with another exception and nothing waits forever."""
+    from tritondl.fetch.h2 import H2Connection, frame
+
+    async def main():
+        r = asyncio.StreamReader()
+        c = H2Connection(r, _Sink(), "origin.test")
+        c._reader = asyncio.ensure_future(c._read_loop())
+        st = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", b"origin.test"),
+                              (b":path", b"/")])
+        for ftype, flags, sid, payload in frames:
+            r.feed_data(frame(ftype, flags, sid, payload))
+        r.feed_eof()
+        try:
+            await asyncio.wait_for(st.response(), 0.5)
+            while await asyncio.wait_for(st.read(), 0.5):
+                pass
+        except ConnectionError:
+            pass
+        await asyncio.wait_for(c._reader, 0.5)
+        assert c.closed is not None or st.eof
+        await c.close()
+    asyncio.run(main())

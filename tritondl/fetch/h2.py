@@ -51,6 +51,9 @@ def frame(ftype: int, flags: int, stream: int, payload: bytes = b"") -> bytes:
     return struct.pack(">BHBBI", n >> 16, n & 0xFFFF, ftype, flags, stream & 0x7FFFFFFF) + payload
 
 
+_FIXED_LEN = {PRIORITY: 5, RST_STREAM: 4, PING: 8, WINDOW_UPDATE: 4}   # RFC 9113 6.3-6.9
+
+
 class H2Error(ConnectionError):
     """The connection failed (a protocol error, GOAWAY for this stream, EOF)."""
 
@@ -248,6 +251,10 @@ class H2Connection:
                 if ln > MAX_FRAME:
                     raise H2Error(f"frame of {ln} bytes above the {MAX_FRAME} we allow")
                 payload = await self.r.readexactly(ln) if ln else b""
+                want = _FIXED_LEN.get(ftype)
+                if want is not None and ln != want or ftype == GOAWAY and ln < 8 or \
+                        ftype == SETTINGS and ln % 6:
+                    raise H2Error(f"frame type {ftype} with a {ln}-byte payload (FRAME_SIZE_ERROR)")
                 if hblock is not None and (ftype != CONTINUATION or sid != hstream):
                     raise H2Error("header block interrupted by another frame")
                 if ftype == DATA:
@@ -290,8 +297,8 @@ class H2Connection:
                 # WINDOW_UPDATE (we send no DATA), PRIORITY and unknown types are ignored
         except asyncio.CancelledError:
             return
-        except (asyncio.IncompleteReadError, ConnectionError, OSError, HPACKError, struct.error) as e:
-            err = e if isinstance(e, H2Error) else H2Error(f"HTTP/2 connection to {self.authority}: {e}")
+        except Exception as e:  # noqa: BLE001 - whatever the server sent, every stream fails instead of hanging
+            err = e if isinstance(e, H2Error) else H2Error(f"HTTP/2 connection to {self.authority}: {e!r}")
             if isinstance(e, HPACKError):
                 err = H2Error(f"HTTP/2 header block from {self.authority} does not decode: {e}")
             self.closed = err
@@ -308,6 +315,8 @@ class H2Connection:
     def _strip(flags: int, payload: bytes, ftype: int) -> bytes:
         pad = 0
         if flags & PADDED:
+            if not payload:
+                raise H2Error("padded frame without a pad length")
             pad = payload[0]
             payload = payload[1:]
         if ftype == HEADERS and flags & PRIORITY_FLAG:
@@ -325,6 +334,10 @@ class H2Connection:
             # a stream we reset or finished: its bytes still count against the connection window
             self._consumed(None, len(payload))
             return
+        if not st._head.done():                     # RFC 9113 8.1: a response starts with HEADERS
+            self._stream_error(st, H2Error(f"DATA before the response head on stream {sid}"))
+            self._consumed(None, len(payload))
+            return
         st.window -= len(payload)
         if len(payload) > len(body):                # padding is flow-controlled too
             st._unacked += len(payload) - len(body)
@@ -338,6 +351,12 @@ class H2Connection:
             self._slots.set()
         st._event.set()
 
+    def _stream_error(self, st: H2Stream, e: H2Error) -> None:
+        """Fail one stream (RST_STREAM PROTOCOL_ERROR); the connection lives on."""
+        self.streams.pop(st.id, None)
+        st._fail(e)
+        self._reset(st.id, PROTOCOL_ERROR)
+
     def _on_headers(self, sid: int, flags: int, block: bytes) -> None:
         fields = self.decoder.decode(block)        # always: the HPACK state must follow every block
         st = self.streams.get(sid)
@@ -347,8 +366,13 @@ class H2Connection:
             status = next((v for n, v in fields if n == b":status"), None)
             if status is None:
                 raise H2Error(f"response on stream {sid} without :status")
-            code = int(status)
+            try:
+                code = int(status)
+            except ValueError:
+                raise H2Error(f"response on stream {sid} with :status {status!r}") from None
             if 100 <= code < 200:
+                if flags & END_STREAM:
+                    self._stream_error(st, H2Error(f"stream {sid} ended after an informational {code}"))
                 return                                  # informational: the real head follows
             st.status = code
             st.headers = CIMultiDict((n.decode("latin-1"), v.decode("latin-1")) for n, v in fields
