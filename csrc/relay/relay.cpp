@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "h2.h"
 #include "relay_core.h"
 
 namespace py = pybind11;
@@ -159,12 +160,53 @@ PYBIND11_MODULE(_relay, m) {
              return static_cast<int>(want);
            },
            "send buffered ciphertext: 0 = all out, else the poll events to wait for")
+      .def("set_alpn", &TlsStream::set_alpn, py::arg("protocols"), "offer these ALPN protocols (before the handshake)")
+      .def_property_readonly("alpn", &TlsStream::alpn, "the ALPN protocol the server selected ('' = none)")
       .def("pending", &TlsStream::pending)
       .def("alive", &TlsStream::alive)
       .def("shutdown_notify", &TlsStream::shutdown_notify)
       .def_property_readonly("version", &TlsStream::version)
       .def_property_readonly("cipher", &TlsStream::cipher)
       .def_property_readonly("resumed", &TlsStream::resumed);
+
+  py::class_<H2Session, std::shared_ptr<H2Session>>(m, "H2Session")
+      .def(py::init([](const py::object& sock, uint32_t stream_window, uint64_t conn_window, uint32_t max_frame) {
+             return std::make_shared<H2Session>(stream_ptr(sock), stream_window, conn_window, max_frame);
+           }),
+           py::arg("sock"), py::arg("stream_window"), py::arg("conn_window"), py::arg("max_frame"),
+           "HTTP/2 client session pump over a connected stream (TlsConn after an h2 ALPN handshake, or Sock); "
+           "the windows and max_frame are what this side advertises")
+      .def("start", &H2Session::start, "start the pump thread (it owns the stream from now on)")
+      .def("fileno", &H2Session::notify_fd, "eventfd, readable while events wait to be taken")
+      .def("send", [](H2Session& h, const py::bytes& frames) { h.send(std::string(frames)); }, py::arg("frames"),
+           "queue frames to write, in order")
+      .def("open_stream", &H2Session::open_stream, py::arg("sid"),
+           "register a stream before its HEADERS are sent (its DATA is buffered until a sink is attached)")
+      .def("sink_file", &H2Session::sink_file, py::arg("sid"), py::arg("fd"), py::arg("offset"), py::arg("limit"),
+           py::arg("flow"), py::arg("seg") = 0, py::arg("seg_done0") = 0, py::call_guard<py::gil_scoped_release>(),
+           "write the stream's body into fd at offset (at most limit bytes, < 0 = all), publishing progress on flow")
+      .def("sink_events", &H2Session::sink_events, py::arg("sid"), py::call_guard<py::gil_scoped_release>(),
+           "deliver the stream's body as DATA events")
+      .def("drop", &H2Session::drop, py::arg("sid"), py::call_guard<py::gil_scoped_release>(),
+           "stop the stream; no write into its sink happens after this returns")
+      .def("written", &H2Session::written, py::arg("sid"), py::call_guard<py::gil_scoped_release>())
+      .def("take_events", [](H2Session& h) {
+             std::vector<H2Event> ev = h.take_events();
+             py::list out;
+             for (H2Event& e : ev)
+               out.append(py::make_tuple(e.type, e.flags, e.sid, py::bytes(e.payload), e.n));
+             return out;
+           },
+           "[(type, flags, sid, payload, n), ...]: frames (type < 256), or SINK_DONE (n = bytes written, flags 1 = "
+           "END_STREAM), SINK_ERROR (payload = error, n = bytes written) and CONN_ERROR (payload = error)")
+      .def("close", &H2Session::close, py::call_guard<py::gil_scoped_release>(),
+           "stop the pump after it has written what was queued, and join it")
+      .def_property_readonly("running", &H2Session::running)
+      .def_property_readonly("bytes_in", &H2Session::bytes_in)
+      .def_property_readonly("bytes_written", &H2Session::bytes_written)
+      .def_readonly_static("SINK_DONE", &H2Session::kSinkDone)
+      .def_readonly_static("SINK_ERROR", &H2Session::kSinkError)
+      .def_readonly_static("CONN_ERROR", &H2Session::kConnError);
 
   m.def("make_test_pki", [](const std::vector<std::string>& hosts, long days) {
           TestPki p = make_test_pki(hosts, days);

@@ -483,6 +483,26 @@ class TlsStream : public Stream {
     flush_nb(&w, &err);
   }
 
+  // ALPN (RFC 7301), client side, before the handshake: protocols in order of preference.
+  void set_alpn(const std::vector<std::string>& protos) {
+    std::string wire;
+    for (const std::string& p : protos) {
+      if (p.empty() || p.size() > 255) throw std::invalid_argument("bad ALPN protocol name");
+      wire += char(p.size());
+      wire += p;
+    }
+    if (SSL_set_alpn_protos(ssl_, reinterpret_cast<const unsigned char*>(wire.data()),
+                            static_cast<unsigned>(wire.size())) != 0)
+      throw std::runtime_error(ssl_errors("SSL_set_alpn_protos"));
+  }
+  // The protocol the server picked ("" = none).
+  std::string alpn() const {
+    const unsigned char* p = nullptr;
+    unsigned n = 0;
+    SSL_get0_alpn_selected(ssl_, &p, &n);
+    return p ? std::string(reinterpret_cast<const char*>(p), n) : std::string();
+  }
+
   std::string version() const { return SSL_get_version(ssl_); }
   std::string cipher() const {
     const SSL_CIPHER* c = SSL_get_current_cipher(ssl_);

@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "../hash/hash_core.h"
+#include "../relay/h2.h"
 #include "../relay/relay_core.h"
 #include "../utp/utp_engine.h"
 #include "../btwire/btwire_core.h"
@@ -405,6 +406,120 @@ static void test_relay(size_t size) {
 // every frame is published at once, so the hashers start far behind and
 // claim 16 frames at a time (the AVX-512 path); a flipped payload byte in
 // one frame must still fail the signature chain.
+// HTTP/2 session pump (relay/h2.h) over a socket pair: a server thread sends
+// two streams' DATA (padded and not, frames split anywhere), stream 3 with a
+// sink limit below its body; the sinks must hold exactly the bodies, the
+// credit frames must never grant stream 3 past its limit, and drop/close race
+// cleanly with the pump (TSan build).
+static std::string h2_frame(uint8_t type, uint8_t flags, uint32_t sid, const std::string& p) {
+  std::string f;
+  const uint32_t n = static_cast<uint32_t>(p.size());
+  const char h[9] = {char(n >> 16), char(n >> 8), char(n), char(type), char(flags),
+                     char((sid >> 24) & 0x7f), char(sid >> 16), char(sid >> 8), char(sid)};
+  f.append(h, 9);
+  f += p;
+  return f;
+}
+
+static void test_h2(unsigned seed) {
+  using namespace tritondl_relay;
+  std::mt19937 rng(seed);
+  int sv[2];
+  CHECK(::socketpair(AF_UNIX, SOCK_STREAM, 0, sv) == 0);
+  ::fcntl(sv[0], F_SETFL, O_NONBLOCK);
+  const size_t n1 = (3u << 20) + 123, n3 = (2u << 20) + 45, limit3 = (1u << 20) + 7;
+  std::string b1(n1, '\0'), b3(n3, '\0');
+  for (auto& c : b1) c = static_cast<char>(rng());
+  for (auto& c : b3) c = static_cast<char>(rng());
+  std::string wire;
+  wire += h2_frame(1, 0x4, 1, "h1");  // HEADERS: forwarded to the caller as an event
+  wire += h2_frame(1, 0x4, 3, "h3");
+  size_t o1 = 0, o3 = 0, pad3 = 0;
+  while (o1 < n1 || o3 < n3) {
+    const bool one = o3 >= n3 || (o1 < n1 && (rng() & 1));
+    std::string& b = one ? b1 : b3;
+    size_t& o = one ? o1 : o3;
+    const size_t take = std::min<size_t>(b.size() - o, 1 + rng() % 60000);
+    const bool last = o + take == b.size();
+    if (rng() % 3 == 0) {
+      const uint8_t pad = static_cast<uint8_t>(rng() % 40);
+      if (!one) pad3 += 1 + pad;
+      wire += h2_frame(0, 0x8 | (last ? 1 : 0), one ? 1 : 3, std::string(1, char(pad)) + b.substr(o, take) +
+                                                          std::string(pad, '\0'));
+    } else {
+      wire += h2_frame(0, last ? 1 : 0, one ? 1 : 3, b.substr(o, take));
+    }
+    o += take;
+  }
+  char path[] = "/tmp/tdl_h2XXXXXX";
+  const int fd = ::mkstemp(path);
+  CHECK(fd >= 0);
+  auto flow = std::make_shared<Flow>(std::vector<Flow::Seg>{{0, int64_t(n1), 0}, {uint64_t(n1), int64_t(n1 + limit3), 0}});
+  auto sess = std::make_shared<H2Session>(std::make_shared<PlainStream>(sv[0]), 1u << 20, 64u << 20, 1u << 20);
+  sess->open_stream(1);
+  sess->open_stream(3);
+  sess->open_stream(5);  // never answered: dropped while the pump runs
+  sess->start();
+  sess->sink_file(1, fd, 0, -1, flow, 0, 0);
+  std::atomic<uint64_t> granted3{0};
+  std::thread server([&, sseed = rng()] {
+    std::mt19937 srng(sseed);
+    size_t off = 0;
+    std::string back;
+    while (off < wire.size()) {
+      const size_t m = std::min<size_t>(wire.size() - off, 1 + srng() % 200000);
+      CHECK(::send(sv[1], wire.data() + off, m, MSG_NOSIGNAL) == ssize_t(m));
+      off += m;
+      char buf[4096];
+      for (ssize_t r; (r = ::recv(sv[1], buf, sizeof buf, MSG_DONTWAIT)) > 0;) back.append(buf, size_t(r));
+    }
+    ::usleep(200000);
+    char buf[4096];
+    for (ssize_t r; (r = ::recv(sv[1], buf, sizeof buf, MSG_DONTWAIT)) > 0;) back.append(buf, size_t(r));
+    for (size_t p = 0; p + 9 <= back.size();) {  // the credit the client returned
+      const unsigned char* h = reinterpret_cast<const unsigned char*>(back.data() + p);
+      const uint32_t len = (uint32_t(h[0]) << 16) | (uint32_t(h[1]) << 8) | h[2];
+      const uint32_t sid = ((uint32_t(h[5]) << 24) | (uint32_t(h[6]) << 16) | (uint32_t(h[7]) << 8) | h[8]) & 0x7fffffffu;
+      if (h[3] == 8 && sid == 3 && len == 4)
+        granted3 += (uint32_t(h[9]) << 24 | uint32_t(h[10]) << 16 | uint32_t(h[11]) << 8 | h[12]) & 0x7fffffffu;
+      p += 9 + len;
+    }
+  });
+  ::usleep(1000 * (rng() % 20));
+  sess->sink_file(3, fd, n1, int64_t(limit3), flow, 1, 0);
+  sess->drop(5);
+  int done = 0, headers = 0;
+  uint64_t w1 = 0, w3 = 0;
+  for (int spin = 0; done < 2 && spin < 20000; ++spin) {
+    for (H2Event& e : sess->take_events()) {
+      if (e.type == 1) ++headers;
+      if (e.type == H2Session::kSinkDone) {
+        ++done;
+        (e.sid == 1 ? w1 : w3) = e.n;
+        CHECK(e.sid == 1 ? e.flags == 1 : true);
+      }
+      CHECK(e.type != H2Session::kSinkError && e.type != H2Session::kConnError);
+    }
+    ::usleep(500);
+  }
+  server.join();
+  CHECK(done == 2 && headers == 2 && w1 == n1 && w3 == limit3);
+  // stream 3 was granted credit only up to its limit (initial window 1 MiB; padding costs window too)
+  CHECK(granted3.load() + (1u << 20) <= limit3 + pad3);
+  std::string back(n1 + limit3, '\0');
+  CHECK(pread_full(fd, &back[0], back.size(), 0) == back.size());
+  CHECK(back.substr(0, n1) == b1 && back.substr(n1) == b3.substr(0, limit3));
+  CHECK(flow->done(0) == n1 && flow->done(1) == limit3);
+  sess->close();
+  bool conn_end = false;
+  for (H2Event& e : sess->take_events()) conn_end = conn_end || e.type == H2Session::kConnError;
+  CHECK(conn_end);
+  ::close(sv[0]);
+  ::close(sv[1]);
+  ::close(fd);
+  ::unlink(path);
+}
+
 static void test_verify_backlog() {
   using namespace tritondl_relay;
   const size_t size = (3u << 20) + 77;
@@ -767,6 +882,7 @@ int main(int argc, char** argv) {
   test_utp_fuzz(5, quick ? 200 : 2000);
   test_btwire(7, quick ? 300 : 3000);
   test_chunked(3, quick ? 40 : 300);
+  for (unsigned seed = 1; seed <= (quick ? 3u : 10u); ++seed) test_h2(seed);
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

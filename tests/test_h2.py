@@ -120,14 +120,30 @@ def test_hpack_interoperates_with_nghttp2():
 
 # ----------------------------------------------------------------- the client connection
 
-def test_streams_share_one_connection_with_flow_control_and_padding():
+TRANSPORTS = pytest.mark.parametrize("native", [True, False], ids=["native", "asyncio"])
+
+
+async def _connect(o: H2Origin, native: bool) -> H2Connection:
+    """An HTTP/2 connection to the fake origin: the relay's TLS with the
+    native session pump, or asyncio's TLS."""
+    if native:
+        from tritondl.utils import rawhttp
+        ctx = rawhttp.relay_module().TlsContext.client(ca_pem=o.ca_pem)
+        c = await H2Connection.open_native("127.0.0.1", o.port, ctx)
+    else:
+        c = await H2Connection.open("127.0.0.1", o.port, ssl.create_default_context(cafile=o.ca_file))
+    assert c is not None and c.native == native
+    return c
+
+
+@TRANSPORTS
+def test_streams_share_one_connection_with_flow_control_and_padding(native):
     async def main():
         o = await H2Origin().start()
         o.pad = True
         data = os.urandom(40 << 20)                  # > the 16 MiB stream window: WINDOW_UPDATEs needed
         o.add("/f.bin", data)
-        c = await H2Connection.open("127.0.0.1", o.port, ssl.create_default_context(cafile=o.ca_file))
-        assert c is not None
+        c = await _connect(o, native)
 
         async def get(a: int, b: int) -> bytes:
             st = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", c.authority.encode()),
@@ -148,12 +164,13 @@ def test_streams_share_one_connection_with_flow_control_and_padding():
     run(main())
 
 
-def test_goaway_fails_unprocessed_streams_retryably_and_the_connection_is_replaced():
+@TRANSPORTS
+def test_goaway_fails_unprocessed_streams_retryably_and_the_connection_is_replaced(native):
     async def main():
         o = await H2Origin().start()
         o.goaway_after = 1
         o.add("/a", b"x" * 1000)
-        c = await H2Connection.open("127.0.0.1", o.port, ssl.create_default_context(cafile=o.ca_file))
+        c = await _connect(o, native)
         hdr = [(b":method", b"GET"), (b":scheme", b"https"), (b":authority", c.authority.encode()), (b":path", b"/a")]
         st1 = await c.request(hdr)
         await st1.response()
@@ -166,30 +183,34 @@ def test_goaway_fails_unprocessed_streams_retryably_and_the_connection_is_replac
     run(main())
 
 
-def test_a_silent_stream_times_out_and_the_segment_is_retried(tmp_path):
+@TRANSPORTS
+def test_a_silent_stream_times_out_and_the_segment_is_retried(tmp_path, native):
     async def main():
         o = await H2Origin().start()
         data = os.urandom(12 << 20)
         url = o.add("/s.mkv", data)
         o.stall = (6 << 20, 5.0)                           # past the first 4 MiB write block
-        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, read_timeout=0.5)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, read_timeout=0.5,
+                            h2_native=native)
         await asyncio.wait_for(dl.download(str(tmp_path), lambda u, p: None, url), 4.0)
         assert (tmp_path / "s.mkv").read_bytes() == data
         assert o.resets >= 1 and len(o.requests) >= 2
-        assert o.requests[-1][2] == "bytes=4194304-12582911"  # the retry resumes after what was written
+        # the retry resumes after what was written: every byte (native sink), whole write blocks (asyncio)
+        assert o.requests[-1][2] == ("bytes=6291456-12582911" if native else "bytes=4194304-12582911")
         await dl.close()
         await o.stop()
     run(main())
 
 
-def test_an_origin_without_h2_is_remembered_and_served_over_http1(tmp_path):
+@TRANSPORTS
+def test_an_origin_without_h2_is_remembered_and_served_over_http1(tmp_path, native):
     async def main():
         from tritondl.utils import rawhttp
         ca, cert, key = rawhttp.relay_module().make_test_pki(["127.0.0.1"])
         o = await Origin(tls=(cert, key)).start()
         data = os.urandom(300_000)
         url = o.add("/h1.mkv", data)
-        dl = HTTPDownloader(progress_interval=0.05, ca_pem=ca, http2=True)
+        dl = HTTPDownloader(progress_interval=0.05, ca_pem=ca, http2=True, h2_native=native)
         dl.ca_file = ""
         await dl.download(str(tmp_path), lambda u, p: None, url)
         assert (tmp_path / "h1.mkv").read_bytes() == data
@@ -199,13 +220,14 @@ def test_an_origin_without_h2_is_remembered_and_served_over_http1(tmp_path):
     run(main())
 
 
-def test_redirects_are_followed_over_h2(tmp_path):
+@TRANSPORTS
+def test_redirects_are_followed_over_h2(tmp_path, native):
     async def main():
         o = await H2Origin().start()
         data = os.urandom(200_000)
         o.add("/real.mkv", data)
         o.redirects["/old.mkv"] = "/real.mkv"
-        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, h2_native=native)
         await dl.download(str(tmp_path), lambda u, p: None, o.url("/old.mkv"))
         assert (tmp_path / "real.mkv").read_bytes() == data and dl.h2_streams == 2
         assert o.connections == 1 and [r[1] for r in o.requests] == ["/old.mkv", "/real.mkv"]
@@ -216,7 +238,8 @@ def test_redirects_are_followed_over_h2(tmp_path):
 
 # ----------------------------------------------------------------- a whole job over HTTP/2
 
-def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path):
+@TRANSPORTS
+def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path, native):
     """VERDICT r05 #7's done-when: a 256 MiB job whose probe and Range
     segments are streams of ONE HTTP/2 connection, uploaded to the fake S3
     (the streamed PUT follows the download) with its content intact."""
@@ -245,7 +268,8 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path):
         cfg.progress_log_interval_s = 0
         cfg.heartbeat_s = 0
         cfg.concurrency = 1
-        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, segment_threshold=64 << 20)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, segment_threshold=64 << 20,
+                            h2_native=native)
         svc = Service(cfg, amqp=Client(b.url, heartbeat=0, retry_delay=0,
                                        backoff=ExponentialBackoff(initial=0.02, max_interval=0.1)),
                       dispatcher=Dispatcher(cfg.download_dir, [dl], 0),
@@ -259,6 +283,7 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path):
         assert o.connections == 1 and o.streams == 4          # probe + 3 more Range segments, one connection
         assert sorted(x[2] for x in o.requests)[0].startswith("bytes=0-")
         assert o.bytes_sent == len(data)                      # nothing fetched twice
+        assert dl._h2conns[("127.0.0.1", o.port)].native == native
         assert s3.object_bytes("triton-staging", object_key("h2", "big.mkv")) == data
         await svc.shutdown(grace=5)
         await o.stop()
@@ -354,4 +379,118 @@ def test_any_server_frames_end_a_stream_with_its_body_or_a_connection_error(fram
         await asyncio.wait_for(c._reader, 0.5)
         assert c.closed is not None or st.eof
         await c.close()
+    asyncio.run(main())
+
+
+@settings(max_examples=200, deadline=None)
+@given(_frames, hs.booleans())
+def test_native_pump_survives_any_server_frames(frames, to_file):
+    """The same for the native session pump (csrc/relay/h2.h), over a plain
+    socket pair: random frames then EOF end the stream's body, file sink or
+    events, with its bytes or a ConnectionError; the pump never crashes or
+    hangs and always reports the connection's end."""
+    import socket
+    import tempfile
+    from tritondl.fetch import h2 as h2mod
+    from tritondl.fetch.h2 import frame
+    from tritondl.utils import rawhttp
+
+    relay = rawhttp.relay_module()
+
+    async def main():
+        a, b = socket.socketpair()
+        a.setblocking(False)
+        sess = relay.H2Session(relay.Sock(a.fileno()), h2mod.STREAM_WINDOW, h2mod.CONN_WINDOW, h2mod.MAX_FRAME)
+        c = H2Connection(None, None, "origin.test", native=sess)
+        sess.start()
+        asyncio.get_running_loop().add_reader(sess.fileno(), c._on_native_events)
+        st = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", b"origin.test"),
+                              (b":path", b"/")])
+        b.sendall(b"".join(frame(t, f, s, p) for t, f, s, p in frames))
+        b.shutdown(socket.SHUT_WR)
+        with tempfile.TemporaryFile() as f:
+            try:
+                await asyncio.wait_for(st.response(), 2.0)
+                if to_file:
+                    await asyncio.wait_for(st.sink(f.fileno(), 0, -1, None, idle_timeout=2.0), 4.0)
+                else:
+                    while await asyncio.wait_for(st.read(), 2.0):
+                        pass
+            except ConnectionError:
+                pass
+        for _ in range(200):                               # EOF reaches the pump: it reports the end
+            if c.closed is not None:
+                break
+            await asyncio.sleep(0.01)
+        assert c.closed is not None
+        await c.close()
+        a.close()
+        b.close()
+    asyncio.run(main())
+
+
+_data_frames = hs.lists(hs.tuples(hs.binary(max_size=3000), hs.integers(0, 40), hs.booleans()), max_size=12)
+
+
+@settings(max_examples=150, deadline=None)
+@given(_data_frames, hs.booleans(), hs.integers(-1, 20000))
+def test_native_sink_writes_exactly_the_unpadded_bodies(chunks, end, limit):
+    """A valid head, then DATA frames with and without padding, split
+    anywhere by the socket: the native file sink holds exactly the body bytes
+    (up to its limit), in order, at its offset, and reports END_STREAM."""
+    import socket
+    import struct as st_
+    import tempfile
+    from tritondl.fetch import h2 as h2mod
+    from tritondl.fetch.h2 import frame
+    from tritondl.utils import rawhttp
+
+    relay = rawhttp.relay_module()
+    body = b"".join(c for c, _p, _x in chunks)
+
+    async def main():
+        a, b = socket.socketpair()
+        a.setblocking(False)
+        sess = relay.H2Session(relay.Sock(a.fileno()), h2mod.STREAM_WINDOW, h2mod.CONN_WINDOW, h2mod.MAX_FRAME)
+        c = H2Connection(None, None, "origin.test", native=sess)
+        sess.start()
+        asyncio.get_running_loop().add_reader(sess.fileno(), c._on_native_events)
+        s = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", b"origin.test"),
+                             (b":path", b"/")])
+        b.sendall(frame(1, 0x4, 1, hpack.Encoder().encode([(b":status", b"200")])))
+        out = []
+        for i, (data, pad, padded) in enumerate(chunks):
+            flags = 0x1 if end and i == len(chunks) - 1 else 0
+            if padded:
+                out.append(frame(0, flags | 0x8, 1, st_.pack(">B", pad) + data + b"\0" * pad))
+            else:
+                out.append(frame(0, flags, 1, data))
+        if end and not chunks:
+            out.append(frame(0, 0x1, 1, b""))
+        wire = b"".join(out)
+        await asyncio.wait_for(s.response(), 5.0)
+        with tempfile.TemporaryFile() as f:
+            f.write(b"P" * 7)
+            f.flush()
+            sink = asyncio.ensure_future(s.sink(f.fileno(), 7, limit, None, idle_timeout=1.0))
+            for k in range(0, len(wire), 1000):          # the socket splits frames anywhere
+                b.sendall(wire[k:k + 1000])
+                await asyncio.sleep(0)
+            want = body if limit < 0 else body[:limit]
+            if end or (0 <= limit <= len(body)):
+                got, eof = await asyncio.wait_for(sink, 5.0)
+                assert got == len(want)
+                assert end or not eof                  # END_STREAM seen only if sent
+                if end and (limit < 0 or limit > len(body)):
+                    assert eof                         # (at the limit it may end either way first)
+            else:
+                b.shutdown(socket.SHUT_WR)
+                with pytest.raises(ConnectionError) as ei:
+                    await asyncio.wait_for(sink, 5.0)
+                assert ei.value.written == len(want)
+            f.seek(0)
+            assert f.read() == b"P" * 7 + want
+        await c.close()
+        a.close()
+        b.close()
     asyncio.run(main())

@@ -1,6 +1,9 @@
 """A/B: one HTTP/2 connection (``TRITONDL_HTTP2=1``, :mod:`tritondl.fetch.h2`)
 against the default HTTP/1.1 path (one TLS connection per Range segment,
-bodies read by the native relay) on the same https download.
+bodies read by the native relay) on the same https download.  HTTP/2 runs
+on both of its transports: ``h2n``, the relay's TLS with the native session
+pump (csrc/relay/h2.h, the default), and ``h2``, asyncio's TLS with bodies
+in Python.
 
 Arms, each ``--runs`` times on a fresh origin:
 
@@ -40,7 +43,7 @@ def _serve(conn, arm: str, proto: str, mib: int, rate: float) -> None:
     """The origin, in a child process: its CPU is not the client's."""
     async def run() -> None:
         data = os.urandom(1 << 20) * mib
-        if proto == "h2":
+        if proto in ("h2", "h2n"):
             o = await H2Origin().start()
             if arm == "stream":
                 o.stream_rate = rate
@@ -54,7 +57,7 @@ def _serve(conn, arm: str, proto: str, mib: int, rate: float) -> None:
         conn.send((o.add("/ab.mkv", data), ca))
         await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         gets = len([r for r in o.requests if r[0] == "GET"])
-        conn.send(o.connections if proto == "h2" else gets)
+        conn.send(o.connections if proto in ("h2", "h2n") else gets)
         await o.stop()
     asyncio.run(run())
 
@@ -63,10 +66,13 @@ async def one(arm: str, proto: str, mib: int, rate: float) -> dict:
     parent, child = mp.Pipe()
     p = mp.get_context("fork").Process(target=_serve, args=(child, arm, proto, mib, rate), daemon=True)
     p.start()
+    if not parent.poll(60):
+        raise RuntimeError(f"the {proto} origin did not start")
     url, ca = parent.recv()
     d = tempfile.mkdtemp(prefix="tdl-h2ab-")
-    if proto == "h2":
-        dl = HTTPDownloader(progress_interval=1.0, ca_pem=ca, http2=True, segment_threshold=16 << 20)
+    if proto in ("h2", "h2n"):
+        dl = HTTPDownloader(progress_interval=1.0, ca_pem=ca, http2=True, segment_threshold=16 << 20,
+                            h2_native=proto == "h2n")
     else:
         dl = HTTPDownloader(progress_interval=1.0, ca_pem=ca, segment_threshold=16 << 20)
     t0 = time.perf_counter()
@@ -79,7 +85,7 @@ async def one(arm: str, proto: str, mib: int, rate: float) -> dict:
     os.rmdir(d)
     await dl.close()
     parent.send("done")
-    conns = parent.recv()
+    conns = parent.recv() if parent.poll(30) else None
     p.join(30)
     data_len = mib << 20
     ok = size == data_len
@@ -98,7 +104,7 @@ async def main() -> None:
     rows = []
     for arm in ("open", "stream", "conn"):
         for _ in range(a.runs):
-            for proto in ("h1", "h2"):
+            for proto in ("h1", "h2n", "h2"):
                 r = await one(arm, proto, a.mib if arm == "open" else a.capped_mib, a.rate)
                 rows.append(r)
                 print(json.dumps(r), flush=True)
@@ -107,15 +113,15 @@ async def main() -> None:
         with open(os.path.join(a.out, "runs.jsonl"), "w") as f:
             for r in rows:
                 f.write(json.dumps(r) + "\n")
-    print("\n| arm | HTTP/1.1 MB/s | HTTP/2 MB/s | h2/h1 | HTTP/1.1 CPU s | HTTP/2 CPU s |")
+    print("\n| arm | HTTP/1.1 MB/s | HTTP/2 native MB/s | HTTP/2 asyncio MB/s | native/h1 | "
+          "client CPU s: h1 / h2 native / h2 asyncio |")
     print("|---|---|---|---|---|---|")
     for arm in ("open", "stream", "conn"):
-        h1 = [r for r in rows if r["arm"] == arm and r["proto"] == "h1"]
-        h2 = [r for r in rows if r["arm"] == arm and r["proto"] == "h2"]
-        m1 = statistics.median(r["MBps"] for r in h1)
-        m2 = statistics.median(r["MBps"] for r in h2)
-        print(f"| {arm} | {m1:.1f} | {m2:.1f} | {m2 / m1:.2f} | "
-              f"{statistics.median(r['cpu_s'] for r in h1):.3f} | {statistics.median(r['cpu_s'] for r in h2):.3f} |")
+        med = {p: (statistics.median(r["MBps"] for r in rows if r["arm"] == arm and r["proto"] == p),
+                   statistics.median(r["cpu_s"] for r in rows if r["arm"] == arm and r["proto"] == p))
+               for p in ("h1", "h2n", "h2")}
+        print(f"| {arm} | {med['h1'][0]:.1f} | {med['h2n'][0]:.1f} | {med['h2'][0]:.1f} | "
+              f"{med['h2n'][0] / med['h1'][0]:.2f} | {med['h1'][1]:.3f} / {med['h2n'][1]:.3f} / {med['h2'][1]:.3f} |")
 
 
 if __name__ == "__main__":

@@ -254,10 +254,13 @@ class HTTPDownloader:
                  headers: dict | None = None, max_retries: int = 5, probe: str = "get",
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
                  ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
-                 disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None, http2: bool = False) -> None:
+                 disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None, http2: bool = False,
+                 h2_native: bool = True) -> None:
         self.progress_interval = progress_interval
         # offer HTTP/2 to https origins (ALPN), as Go's transport under grab did
         self.http2 = http2
+        # HTTP/2 over the relay's TLS with a native session pump (False: asyncio's TLS, bodies in Python)
+        self.h2_native = h2_native
         self._h2conns: dict[tuple[str, int], "_h2.H2Connection"] = {}
         self._h2locks: dict[tuple[str, int], asyncio.Lock] = {}
         self._h1_only: dict[tuple[str, int], float] = {}     # origins that answered ALPN with http/1.1
@@ -410,8 +413,11 @@ class HTTPDownloader:
             if c is not None and c.alive:
                 return c
             try:
-                c = await _h2.H2Connection.open(host, port, self._h2_ssl(), timeout=30.0)
-            except (OSError, asyncio.TimeoutError) as e:
+                if self.h2_native and rawhttp.relay_module() is not None:
+                    c = await _h2.H2Connection.open_native(host, port, self._tls_ctx(), timeout=30.0)
+                else:
+                    c = await _h2.H2Connection.open(host, port, self._h2_ssl(), timeout=30.0)
+            except (OSError, RuntimeError, asyncio.TimeoutError) as e:
                 raise aiohttp.ClientConnectionError(f"https://{host}:{port}: {e}") from e
             if c is None:
                 self._h1_only[key] = time.monotonic() + 3600.0
@@ -876,6 +882,8 @@ class HTTPDownloader:
         loop = asyncio.get_running_loop()
         start = segs[i][0]
         limit = (end - pos) if end >= 0 else -1
+        if isinstance(r, _H2Response) and r.st.conn.native:
+            return await self._consume_h2_native(r, i, segs, done, h, fd, pos, end, limit)
         if limit >= 0 and isinstance(r, _H2Response):
             r.st.want(limit)
         bufs: list[bytes] = []
@@ -906,6 +914,26 @@ class HTTPDownloader:
             if h is not None:
                 h._advance(i, done[i])
         if end >= 0 and start + done[i] < end:
+            raise HTTPDownloadError("connection closed early")
+
+    async def _consume_h2_native(self, r: "_H2Response", i: int, segs: list[list[int]], done: list[int],
+                                 h: "DownloadHandle | None", fd: int, pos: int, end: int, limit: int) -> None:
+        """An HTTP/2 stream on a native connection: the session pump writes
+        the body into the file and onto the handle's flow (csrc/relay/h2.h)."""
+        flow = h.flow if h is not None else None
+        try:
+            got, eof = await r.st.sink(fd, pos, limit, flow, i, done[i], self.read_timeout)
+        except _h2.H2Error as e:
+            done[i] += e.written
+            if h is not None:
+                h._advance(i, done[i])
+            raise aiohttp.ClientConnectionError(str(e)) from e
+        done[i] += got
+        if h is not None:
+            h._advance(i, done[i])
+        if not eof:
+            r.st.cancel()                           # the probe stream runs on into the next segment
+        if end >= 0 and segs[i][0] + done[i] < end:
             raise HTTPDownloadError("connection closed early")
 
     async def _consume_native(self, r: _RawResponse, fd: int, i: int, segs: list[list[int]], done: list[int],

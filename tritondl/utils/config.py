@@ -72,7 +72,7 @@ ENV_BOOLS = {"CLEANUP": "cleanup", "DROP_FAILED": "drop_failed", "DECLARE_PUBLIS
              "DECLARE_PUBLISH_QUEUES": "declare_publish_queues", "STREAM_UPLOAD": "stream_upload",
              "PIPELINE_COMMIT": "pipeline_commit", "BT_DHT": "bt_dht", "BT_DHT_IPV6": "bt_dht_ipv6",
              "BT_UPNP": "bt_upnp", "BT_NATIVE_WIRE": "bt_native_wire", "BT_UTP": "bt_utp", "BT_PEX": "bt_pex",
-             "GC_FREEZE": "gc_freeze", "HTTP2": "http2"}
+             "GC_FREEZE": "gc_freeze", "HTTP2": "http2", "H2_NATIVE": "h2_native"}
 # The reference's own variables, same names: name -> Config field
 REFERENCE_ENV = {"LOG_LEVEL": "log_level", "LOG_FORMAT": "log_format", "RABBITMQ_ENDPOINT": "rabbitmq_endpoint",
                  "RABBITMQ_USERNAME": "rabbitmq_username", "RABBITMQ_PASSWORD": "rabbitmq_password",
@@ -200,10 +200,11 @@ class Config:
     http_segment_threshold: int = 64 * 1024 * 1024   # open-ended probe only: segment files at least this big
     http_probe_bytes: int = 0                   # >0: GET probe = bytes=0-(N-1), the rest as parallel Range streams
     # offer HTTP/2 to https origins (ALPN): the probe and the Range segments become streams of
-    # one connection, as under grab's Go transport.  Opt-in: against four HTTP/1.1 connections
-    # it ties under per-request pacing and loses uncapped (0.44x) and per-connection capped
-    # (0.28x) (profiles/r06_h2_ab/)
+    # one connection, as under grab's Go transport; DATA lands in the file from a native session
+    # pump.  Opt-in: against four HTTP/1.1 connections it uses less CPU and ties under per-request
+    # pacing, but one connection gets 0.28x where each TCP flow is capped (profiles/r06_h2_ab/)
     http2: bool = False
+    h2_native: bool = True                      # HTTP/2 DATA via the native session pump (off: asyncio's TLS)
     http_stripe_bytes: int = 0                  # >0: parallel streams pull in-order stripes of this size
                                                 # (0 measured faster on the 10 MiB headline job: profiles/r01_probe)
 
