@@ -80,3 +80,27 @@ def test_preflight_warns_about_a_skewed_clock(tmp_path, monkeypatch):
         finally:
             await s3.stop()
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_lease_probe_tells_whether_leases_will_work(tmp_path, monkeypatch):
+    """--lease-probe declares and deletes one lease-shaped queue: OK for a
+    user who may, a warning naming the permission for one who may not (the
+    worker then holds deliveries unacked, as the reference did)."""
+    async def main():
+        b = await Broker(username="guest", password="guest").start()
+        b.add_user("narrow", "pw", configure=r"^v1\.download(-\d+)?$", write=".*", read=r"^v1\.download-\d+$")
+        try:
+            _env(monkeypatch, tmp_path, b.url.split("@", 1)[1].rstrip("/"), "http://127.0.0.1:1")
+            r = await check.run([], timeout=5, skip_s3=True, lease_probe=True)
+            leases = [i for i in r.items if i["area"] == "leases"]
+            assert leases and leases[0]["status"] == "ok", leases
+            assert not [q for q in b.queues if ".lease." in q]          # nothing left behind
+            monkeypatch.setenv("RABBITMQ_USERNAME", "narrow")
+            monkeypatch.setenv("RABBITMQ_PASSWORD", "pw")
+            r2 = await check.run([], timeout=5, skip_s3=True, lease_probe=True)
+            leases = [i for i in r2.items if i["area"] == "leases"]
+            assert leases and leases[0]["status"] == "warn" and "configure and read" in leases[0]["detail"]
+            assert not r2.failed or {i["area"] for i in r2.items if i["status"] == "fail"} == set()
+        finally:
+            await b.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))

@@ -14,6 +14,12 @@ before it joins the queue:
   exchange, its shard queues and the publish exchange — declares nothing,
   consumes nothing (a 404 / 403 there is reported, with what the worker
   would do about it);
+* with ``--lease-probe``, whether this user may hold job leases: a queue
+  named and shaped like a lease queue (``<shard>.lease.check-<hex>.0``: TTL,
+  dead-letter exchange = the consume exchange, ``x-expires``) is declared
+  and deleted at once.  Without that permission the worker holds
+  deliveries unacked for the whole job, as the reference did, and a job
+  longer than the broker's ``consumer_timeout`` runs again;
 * S3: the endpoint parses, which credential provider answers, and a HEAD on
   the bucket (missing is fine: the worker creates it);
 * the GPU: visible devices, and with ``--gpu`` the helper process is started
@@ -172,6 +178,41 @@ async def check_broker(cfg: Config, r: Report, timeout: float) -> None:
         await conn.close()
 
 
+async def check_leases(cfg: Config, r: Report, timeout: float) -> None:
+    """Declare and delete one lease-shaped queue (amqp/client.py::_lease_put)."""
+    import secrets
+    from .amqp.connection import ChannelClosed, Connection
+    if cfg.lease_after_s <= 0:
+        r.add("leases", OK, "leases are off (TRITONDL_LEASE_AFTER=0): deliveries stay unacked for the whole job")
+        return
+    name = f"{cfg.consume_topic}-0.lease.check-{secrets.token_hex(4)}.0"
+    ms = max(1, int(cfg.lease_s * 1000))
+    try:
+        conn = await asyncio.wait_for(Connection.open(cfg.rabbitmq_url(), heartbeat=cfg.heartbeat_s), timeout)
+    except Exception as e:  # noqa: BLE001 - reported
+        r.add("leases", FAIL, f"cannot log in to {cfg.rabbitmq_endpoint}: {e}")
+        return
+    try:
+        ch = await conn.channel()
+        try:
+            await asyncio.wait_for(ch.queue_declare(name, durable=True, arguments={
+                "x-message-ttl": ms, "x-expires": 10_000, "x-dead-letter-exchange": cfg.consume_topic,
+                "x-dead-letter-routing-key": f"{cfg.consume_topic}-0"}), timeout)
+            await asyncio.wait_for(ch.queue_delete(name), timeout)
+            r.add("leases", OK, f"this user may hold job leases (declared and deleted {name}): a job running "
+                  f"longer than {cfg.lease_after_s:g} s is leased, whatever the broker's consumer_timeout")
+        except ChannelClosed as e:
+            r.add("leases", WARN, f"the broker refused a lease queue ({e}): the worker will hold deliveries "
+                  "unacked for the whole job, so a job longer than the broker's consumer_timeout runs again. "
+                  f"Grant configure and read on '^{cfg.consume_topic}-\\d+\\.lease\\.' and write on the "
+                  "default exchange")
+        finally:
+            if not ch.is_closed:
+                await ch.close()
+    finally:
+        await conn.close()
+
+
 async def check_s3(cfg: Config, r: Report, timeout: float) -> None:
     from .s3.client import Endpoint, S3Client, S3Error
     from .s3.credentials import default_chain
@@ -221,7 +262,7 @@ def check_gpu(cfg: Config, r: Report, start_helper: bool) -> None:
 
 
 async def run(argv: list[str], *, timeout: float = 10.0, gpu: bool = False, skip_broker: bool = False,
-              skip_s3: bool = False) -> Report:
+              skip_s3: bool = False, lease_probe: bool = False) -> Report:
     r = Report()
     cfg = check_config(argv, r)
     check_native(r)
@@ -231,6 +272,8 @@ async def run(argv: list[str], *, timeout: float = 10.0, gpu: bool = False, skip
     check_dir(cfg, r)
     if not skip_broker:
         await check_broker(cfg, r, timeout)
+        if lease_probe:
+            await check_leases(cfg, r, timeout)
     if not skip_s3:
         await check_s3(cfg, r, timeout)
     check_gpu(cfg, r, gpu)
@@ -244,9 +287,12 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--timeout", type=float, default=10.0, help="seconds per network check")
     ap.add_argument("--no-broker", action="store_true")
     ap.add_argument("--no-s3", action="store_true")
+    ap.add_argument("--lease-probe", action="store_true",
+                    help="declare and delete one lease-shaped queue to see whether job leases will work")
     a, rest = ap.parse_known_args(argv)
     parse_args(rest)                                  # the worker's own flags must parse too
-    r = asyncio.run(run(rest, timeout=a.timeout, gpu=a.gpu, skip_broker=a.no_broker, skip_s3=a.no_s3))
+    r = asyncio.run(run(rest, timeout=a.timeout, gpu=a.gpu, skip_broker=a.no_broker, skip_s3=a.no_s3,
+                        lease_probe=a.lease_probe))
     if a.json:
         print(json.dumps({"ok": not r.failed, "checks": r.items}, indent=1))
     else:
