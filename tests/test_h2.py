@@ -294,7 +294,7 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path, native):
 
 # ----------------------------------------------------------------- property tests
 
-from hypothesis import given, settings, strategies as hs  # noqa: E402
+from hypothesis import example, given, settings, strategies as hs  # noqa: E402
 
 
 @settings(max_examples=400, deadline=None)
@@ -354,6 +354,8 @@ _frames = hs.lists(hs.tuples(hs.sampled_from([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 0x0a
 
 @settings(max_examples=300, deadline=None)
 @given(_frames)
+@example([(3, 0, 1, b"")])          # found: RST_STREAM with no error code left the stream waiting forever
+@example([(0, 1, 1, b"")])          # found: END_STREAM DATA before any HEADERS left response() waiting
 def test_any_server_frames_end_a_stream_with_its_body_or_a_connection_error(frames):
     """Whatever frames a server sends (random types, flags, streams and
     payloads, then EOF), an open stream ends: its response and body either
