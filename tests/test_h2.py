@@ -236,6 +236,34 @@ def test_redirects_are_followed_over_h2(tmp_path, native):
     run(main())
 
 
+@TRANSPORTS
+def test_idle_connections_are_closed_and_their_pumps_stop(tmp_path, native):
+    """A worker meets many origins: a connection with no stream for
+    ``h2_idle_s`` is closed at the next use of the downloader (its socket,
+    and the native pump thread, go with it)."""
+    async def main():
+        a, b = await H2Origin().start(), await H2Origin().start()
+        da, db = os.urandom(100_000), os.urandom(100_000)
+        ua, ub = a.add("/a.mkv", da), b.add("/b.mkv", db)
+        dl = HTTPDownloader(progress_interval=0.05, ca_pem=a.ca_pem + b.ca_pem, http2=True, h2_native=native,
+                            h2_idle_s=0.05)
+        dl.ca_file = ""
+        await dl.download(str(tmp_path), lambda u, p: None, ua)
+        ca = dl._h2conns[("127.0.0.1", a.port)]
+        await asyncio.sleep(0.15)
+        await dl.download(str(tmp_path), lambda u, p: None, ub)
+        assert list(dl._h2conns) == [("127.0.0.1", b.port)]
+        await asyncio.gather(*dl._h2closing)
+        assert ca.closed is not None
+        if native:
+            assert not ca._native.running
+        assert (tmp_path / "a.mkv").read_bytes() == da and (tmp_path / "b.mkv").read_bytes() == db
+        await dl.close()
+        await a.stop()
+        await b.stop()
+    run(main())
+
+
 # ----------------------------------------------------------------- a whole job over HTTP/2
 
 @TRANSPORTS

@@ -37,6 +37,7 @@ import asyncio
 import collections
 import ssl
 import struct
+import time
 
 from multidict import CIMultiDict
 
@@ -234,6 +235,7 @@ class H2Connection:
         self._native = native                      # _relay.H2Session (native transport)
         self._raw = None                           # its rawhttp.RawConn (owns the socket)
         self._sinks: dict[int, H2Stream] = {}      # native: streams whose body a pump sink takes
+        self.last_active = time.monotonic()        # last request or frame (idle-connection reaping)
 
     @classmethod
     async def open(cls, host: str, port: int, ctx: ssl.SSLContext, *, timeout: float = 30.0) -> "H2Connection | None":
@@ -286,6 +288,10 @@ class H2Connection:
     def alive(self) -> bool:
         return self.closed is None and self.goaway_last is None
 
+    def idle_for(self, now: float) -> float:
+        """Seconds without a stream open (0 while one is)."""
+        return 0.0 if self.streams or self._sinks else now - self.last_active
+
     def _write(self, data: bytes) -> None:
         if self._native is not None:
             self._native.send(data)
@@ -304,6 +310,7 @@ class H2Connection:
             raise H2Error(f"connection to {self.authority} is closing: {self.closed or 'GOAWAY'}")
         sid = self.next_id
         self.next_id += 2
+        self.last_active = time.monotonic()
         st = H2Stream(self, sid)
         self.streams[sid] = st
         self.streams_opened += 1
@@ -437,6 +444,7 @@ class H2Connection:
                     self._stop_native()
                     return
             elif ftype == SINK_DONE:
+                self.last_active = time.monotonic()
                 st = self._sinks.pop(sid, None)
                 if st is not None:
                     self.streams.pop(sid, None)
@@ -454,6 +462,7 @@ class H2Connection:
 
     def _on_frame(self, ftype: int, flags: int, sid: int, payload: bytes) -> None:
         """One frame from the server (any transport); H2Error on a protocol error."""
+        self.last_active = time.monotonic()
         ln = len(payload)
         want = _FIXED_LEN.get(ftype)
         if want is not None and ln != want or ftype == GOAWAY and ln < 8 or ftype == SETTINGS and ln % 6:

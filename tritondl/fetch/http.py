@@ -255,12 +255,16 @@ class HTTPDownloader:
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
                  ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
                  disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None, http2: bool = False,
-                 h2_native: bool = True) -> None:
+                 h2_native: bool = True, h2_idle_s: float = 90.0) -> None:
         self.progress_interval = progress_interval
         # offer HTTP/2 to https origins (ALPN), as Go's transport under grab did
         self.http2 = http2
         # HTTP/2 over the relay's TLS with a native session pump (False: asyncio's TLS, bodies in Python)
         self.h2_native = h2_native
+        # an HTTP/2 connection with no stream for this long is closed (Go's IdleConnTimeout): a worker
+        # that meets thousands of origins keeps a socket (and, native, a pump thread) only for live ones
+        self.h2_idle_s = h2_idle_s
+        self._h2closing: set[asyncio.Task] = set()
         self._h2conns: dict[tuple[str, int], "_h2.H2Connection"] = {}
         self._h2locks: dict[tuple[str, int], asyncio.Lock] = {}
         self._h1_only: dict[tuple[str, int], float] = {}     # origins that answered ALPN with http/1.1
@@ -336,6 +340,8 @@ class HTTPDownloader:
     async def close(self) -> None:
         for c in list(self._h2conns.values()):
             await c.close()
+        if self._h2closing:
+            await asyncio.gather(*self._h2closing, return_exceptions=True)
         self._h2conns.clear()
         self._raw.close()
         if self._session is not None:
@@ -398,9 +404,27 @@ class HTTPDownloader:
         ctx = ssl.create_default_context(cafile=self.ca_file or None, cadata=self.ca_pem or None)
         return ctx
 
+    def _h2_sweep(self) -> None:
+        """Close HTTP/2 connections that died or sat without a stream for
+        ``h2_idle_s``; forget expired HTTP/1.1-only verdicts."""
+        now = time.monotonic()
+        for key, c in list(self._h2conns.items()):
+            if not c.alive and not c.streams or c.idle_for(now) > self.h2_idle_s:
+                del self._h2conns[key]
+                lock = self._h2locks.get(key)
+                if lock is not None and not lock.locked():
+                    del self._h2locks[key]
+                t = asyncio.ensure_future(c.close())
+                self._h2closing.add(t)
+                t.add_done_callback(self._h2closing.discard)
+        for key, until in list(self._h1_only.items()):
+            if until <= now:
+                del self._h1_only[key]
+
     async def _h2_conn(self, host: str, port: int) -> "_h2.H2Connection | None":
         """The origin's live HTTP/2 connection (opened on first use; one per
         origin, shared by every stream), or None if it speaks HTTP/1.1."""
+        self._h2_sweep()
         key = (host, port)
         c = self._h2conns.get(key)
         if c is not None and c.alive:
