@@ -206,6 +206,8 @@ class TlsContext {
   TlsContext(const TlsContext&) = delete;
   TlsContext& operator=(const TlsContext&) = delete;
 
+  static constexpr size_t kMaxSessions = 512;  // resumption tickets kept (one per host:port)
+
   SSL_CTX* ctx() const { return ctx_; }
   bool is_server() const { return server_; }
   bool verify() const { return verify_; }
@@ -587,7 +589,14 @@ inline int TlsContext::on_new_session(SSL* ssl, SSL_SESSION* sess) {
   TlsContext* c = st->context();
   std::lock_guard<std::mutex> l(c->mu_);
   auto it = c->sessions_.find(st->session_key());
-  if (it != c->sessions_.end()) SSL_SESSION_free(it->second);
+  if (it != c->sessions_.end()) {
+    SSL_SESSION_free(it->second);
+  } else if (c->sessions_.size() >= TlsContext::kMaxSessions) {
+    // a worker that meets thousands of origins keeps tickets for a bounded few
+    auto victim = c->sessions_.begin();
+    SSL_SESSION_free(victim->second);
+    c->sessions_.erase(victim);
+  }
   c->sessions_[st->session_key()] = sess;
   return 1;  // we keep the reference
 }

@@ -646,3 +646,28 @@ def test_url_userinfo_is_sent_as_basic_auth(tmp_path, native):
     out = buf.getvalue()
     assert "s3cret" not in out and "guest:guest" not in out
     assert "alice:xxxxx@media.example" in out and "guest:xxxxx@rabbit" in out
+
+
+def test_idle_pooled_connections_expire_and_are_capped():
+    """The keep-alive pool closes a connection idle past ``idle_s`` (Go's
+    IdleConnTimeout, 90 s) and keeps at most ``max_idle_total``, oldest
+    closed first, so a worker that meets many origins does not hoard fds."""
+    import socket
+    import time as _t
+    from tritondl.utils import rawhttp
+
+    async def main():
+        pool = rawhttp.Pool(idle_s=0.05, max_idle_total=2)
+        pairs = [socket.socketpair() for _ in range(3)]
+        conns = [rawhttp.RawConn(a) for a, _b in pairs]
+        for i, c in enumerate(conns):
+            pool.release(f"origin{i}", 443, c)
+            _t.sleep(0.001)
+        assert conns[0].sock.fileno() == -1                      # the oldest went over the cap
+        assert sum(len(v) for v in pool.idle.values()) == 2
+        await asyncio.sleep(0.1)
+        pool.sweep(force=True)
+        assert not pool.idle and all(c.sock.fileno() == -1 for c in conns)
+        for _a, b in pairs:
+            b.close()
+    asyncio.run(main())

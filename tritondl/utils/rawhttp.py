@@ -23,6 +23,7 @@ import asyncio
 import base64
 import os
 import socket
+import time
 import weakref
 from dataclasses import dataclass, field
 
@@ -307,6 +308,11 @@ class Pool:
     host, port, tls) for tunnels."""
     max_idle: int = 16
     idle: dict = field(default_factory=dict)
+    # Go's http.Transport closes a connection idle for 90 s (IdleConnTimeout) and keeps at most
+    # 100 idle in all: a worker that meets thousands of origins must not keep a socket for each
+    idle_s: float = 90.0
+    max_idle_total: int = 100
+    _next_sweep: float = 0.0
 
     async def connect(self, host: str, port: int, timeout: float = 30.0, tls=None,
                       server_hostname: str | None = None, proxy=None, proxy_tls=None) -> tuple[RawConn, bool]:
@@ -322,6 +328,7 @@ class Pool:
         the transport's TLS config, i.e. the same trust as for targets;
         default: the shared system-store context).
         """
+        self.sweep()
         tid = id(tls) if tls is not None else 0
         if proxy is None:
             key: tuple = (host, port, tid)
@@ -378,7 +385,38 @@ class Pool:
         if len(lst) >= self.max_idle:
             c.close()
         else:
+            c.idle_at = time.monotonic()
             lst.append(c)
+        self.sweep()
+
+    def sweep(self, force: bool = False) -> None:
+        """Close connections idle longer than ``idle_s``, then the oldest
+        ones beyond ``max_idle_total`` (checked at most every few seconds)."""
+        now = time.monotonic()
+        total = sum(len(v) for v in self.idle.values())
+        if not force and now < self._next_sweep and total <= self.max_idle_total:
+            return
+        self._next_sweep = now + min(5.0, self.idle_s / 4)
+        every = []
+        for key, lst in list(self.idle.items()):
+            keep = []
+            for c in lst:
+                if now - getattr(c, "idle_at", now) > self.idle_s:
+                    c.close()
+                else:
+                    keep.append(c)
+                    every.append((getattr(c, "idle_at", now), key, c))
+            if keep:
+                self.idle[key] = keep
+            else:
+                del self.idle[key]
+        if len(every) > self.max_idle_total:
+            every.sort(key=lambda t: t[0])
+            for _t, key, c in every[:len(every) - self.max_idle_total]:
+                self.idle[key].remove(c)
+                if not self.idle[key]:
+                    del self.idle[key]
+                c.close()
 
     def close(self) -> None:
         for lst in self.idle.values():
