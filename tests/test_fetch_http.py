@@ -671,3 +671,29 @@ def test_idle_pooled_connections_expire_and_are_capped():
         for _a, b in pairs:
             b.close()
     asyncio.run(main())
+
+
+def test_many_origins_leave_a_bounded_number_of_sockets(tmp_path):
+    """300 downloads from 300 distinct origins (127.0.x.y, one server bound
+    to all of loopback): the keep-alive pool keeps at most its cap of idle
+    sockets, so the worker's fds do not grow with the origins it has met."""
+    from tritondl_testkit.fakes.origin import Origin
+
+    async def main():
+        o = await Origin(host="0.0.0.0").start()
+        data = os.urandom(20_000)
+        o.add("/m.mkv", data)
+        dl = HTTPDownloader(progress_interval=1.0)
+        dl._raw.max_idle_total = 40
+        fds0 = len(os.listdir("/proc/self/fd"))
+        for i in range(300):
+            d = tmp_path / str(i)
+            d.mkdir()
+            await dl.download(str(d), lambda u, p: None, f"http://127.0.{i // 250}.{i % 250 + 1}:{o.port}/m.mkv")
+        assert sum(len(v) for v in dl._raw.idle.values()) <= 40
+        # the in-process origin holds the far end of each pooled socket: 2 fds per idle connection
+        assert len(os.listdir("/proc/self/fd")) - fds0 < 2 * 40 + 20
+        assert (tmp_path / "299" / "m.mkv").read_bytes() == data
+        await dl.close()
+        await o.stop()
+    asyncio.run(main())
