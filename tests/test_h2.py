@@ -237,6 +237,37 @@ def test_redirects_are_followed_over_h2(tmp_path, native):
 
 
 @TRANSPORTS
+def test_streams_stripe_over_up_to_h2_conns_connections(tmp_path, native):
+    """With ``h2_conns`` 4 a segmented download opens a connection per busy
+    stream, up to 4 (four TCP windows, like four HTTP/1.1 connections); two
+    downloads at once share those 4; ``h2_conns`` 1 keeps one connection."""
+    async def main():
+        o = await H2Origin().start()
+        o.stream_rate = 100e6                          # streams stay open while the others start
+        d1, d2 = os.urandom(1 << 20) * 40, os.urandom(1 << 20) * 40
+        u1, u2 = o.add("/x.mkv", d1), o.add("/y.mkv", d2)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, h2_native=native,
+                            segment_threshold=16 << 20)
+        (tmp_path / "a").mkdir()
+        (tmp_path / "b").mkdir()
+        await dl.download(str(tmp_path / "a"), lambda u, p: None, u1)
+        assert o.connections == 4 and o.streams == 4
+        await asyncio.gather(dl.download(str(tmp_path / "b"), lambda u, p: None, u2),
+                             dl.download(str(tmp_path), lambda u, p: None, u1))
+        assert o.connections == 4 and o.streams == 12
+        assert (tmp_path / "a" / "x.mkv").read_bytes() == d1 and (tmp_path / "b" / "y.mkv").read_bytes() == d2
+        await dl.close()
+        one = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, h2_native=native,
+                             segment_threshold=16 << 20, h2_conns=1)
+        (tmp_path / "c").mkdir()
+        await one.download(str(tmp_path / "c"), lambda u, p: None, u2)
+        assert o.connections == 5 and o.streams == 16
+        await one.close()
+        await o.stop()
+    run(main())
+
+
+@TRANSPORTS
 def test_idle_connections_are_closed_and_their_pumps_stop(tmp_path, native):
     """A worker meets many origins: a connection with no stream for
     ``h2_idle_s`` is closed at the next use of the downloader (its socket,
@@ -249,7 +280,7 @@ def test_idle_connections_are_closed_and_their_pumps_stop(tmp_path, native):
                             h2_idle_s=0.05)
         dl.ca_file = ""
         await dl.download(str(tmp_path), lambda u, p: None, ua)
-        ca = dl._h2conns[("127.0.0.1", a.port)]
+        ca, = dl._h2conns[("127.0.0.1", a.port)]
         await asyncio.sleep(0.15)
         await dl.download(str(tmp_path), lambda u, p: None, ub)
         assert list(dl._h2conns) == [("127.0.0.1", b.port)]
@@ -297,7 +328,7 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path, native):
         cfg.heartbeat_s = 0
         cfg.concurrency = 1
         dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, segment_threshold=64 << 20,
-                            h2_native=native)
+                            h2_native=native, h2_conns=1)
         svc = Service(cfg, amqp=Client(b.url, heartbeat=0, retry_delay=0,
                                        backoff=ExponentialBackoff(initial=0.02, max_interval=0.1)),
                       dispatcher=Dispatcher(cfg.download_dir, [dl], 0),
@@ -311,7 +342,7 @@ def test_a_256mib_job_over_h2_range_streams_on_one_connection(tmp_path, native):
         assert o.connections == 1 and o.streams == 4          # probe + 3 more Range segments, one connection
         assert sorted(x[2] for x in o.requests)[0].startswith("bytes=0-")
         assert o.bytes_sent == len(data)                      # nothing fetched twice
-        assert dl._h2conns[("127.0.0.1", o.port)].native == native
+        assert [c.native for c in dl._h2conns[("127.0.0.1", o.port)]] == [native]
         assert s3.object_bytes("triton-staging", object_key("h2", "big.mkv")) == data
         await svc.shutdown(grace=5)
         await o.stop()

@@ -1,9 +1,10 @@
 """A/B: one HTTP/2 connection (``TRITONDL_HTTP2=1``, :mod:`tritondl.fetch.h2`)
 against the default HTTP/1.1 path (one TLS connection per Range segment,
 bodies read by the native relay) on the same https download.  HTTP/2 runs
-on both of its transports: ``h2n``, the relay's TLS with the native session
-pump (csrc/relay/h2.h, the default), and ``h2``, asyncio's TLS with bodies
-in Python.
+three ways: ``h2n``, the relay's TLS with the native session pump
+(csrc/relay/h2.h) and up to 4 connections per origin (the default);
+``h2n1``, the same on one connection; ``h2``, asyncio's TLS with bodies in
+Python, one connection.
 
 Arms, each ``--runs`` times on a fresh origin:
 
@@ -43,7 +44,7 @@ def _serve(conn, arm: str, proto: str, mib: int, rate: float) -> None:
     """The origin, in a child process: its CPU is not the client's."""
     async def run() -> None:
         data = os.urandom(1 << 20) * mib
-        if proto in ("h2", "h2n"):
+        if proto in ("h2", "h2n", "h2n1"):
             o = await H2Origin().start()
             if arm == "stream":
                 o.stream_rate = rate
@@ -57,7 +58,7 @@ def _serve(conn, arm: str, proto: str, mib: int, rate: float) -> None:
         conn.send((o.add("/ab.mkv", data), ca))
         await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         gets = len([r for r in o.requests if r[0] == "GET"])
-        conn.send(o.connections if proto in ("h2", "h2n") else gets)
+        conn.send(o.connections if proto in ("h2", "h2n", "h2n1") else gets)
         await o.stop()
     asyncio.run(run())
 
@@ -70,9 +71,9 @@ async def one(arm: str, proto: str, mib: int, rate: float) -> dict:
         raise RuntimeError(f"the {proto} origin did not start")
     url, ca = parent.recv()
     d = tempfile.mkdtemp(prefix="tdl-h2ab-")
-    if proto in ("h2", "h2n"):
+    if proto in ("h2", "h2n", "h2n1"):
         dl = HTTPDownloader(progress_interval=1.0, ca_pem=ca, http2=True, segment_threshold=16 << 20,
-                            h2_native=proto == "h2n")
+                            h2_native=proto != "h2", h2_conns=4 if proto == "h2n" else 1)
     else:
         dl = HTTPDownloader(progress_interval=1.0, ca_pem=ca, segment_threshold=16 << 20)
     t0 = time.perf_counter()
@@ -104,7 +105,7 @@ async def main() -> None:
     rows = []
     for arm in ("open", "stream", "conn"):
         for _ in range(a.runs):
-            for proto in ("h1", "h2n", "h2"):
+            for proto in ("h1", "h2n", "h2n1", "h2"):
                 r = await one(arm, proto, a.mib if arm == "open" else a.capped_mib, a.rate)
                 rows.append(r)
                 print(json.dumps(r), flush=True)
@@ -113,15 +114,16 @@ async def main() -> None:
         with open(os.path.join(a.out, "runs.jsonl"), "w") as f:
             for r in rows:
                 f.write(json.dumps(r) + "\n")
-    print("\n| arm | HTTP/1.1 MB/s | HTTP/2 native MB/s | HTTP/2 asyncio MB/s | native/h1 | "
-          "client CPU s: h1 / h2 native / h2 asyncio |")
-    print("|---|---|---|---|---|---|")
+    print("\n| arm | HTTP/1.1 MB/s | HTTP/2 native, 4 conns | native, 1 conn | asyncio, 1 conn | "
+          "4 conns / HTTP/1.1 | client CPU s: h1 / 4 conns / 1 conn / asyncio |")
+    print("|---|---|---|---|---|---|---|")
     for arm in ("open", "stream", "conn"):
         med = {p: (statistics.median(r["MBps"] for r in rows if r["arm"] == arm and r["proto"] == p),
                    statistics.median(r["cpu_s"] for r in rows if r["arm"] == arm and r["proto"] == p))
-               for p in ("h1", "h2n", "h2")}
-        print(f"| {arm} | {med['h1'][0]:.1f} | {med['h2n'][0]:.1f} | {med['h2'][0]:.1f} | "
-              f"{med['h2n'][0] / med['h1'][0]:.2f} | {med['h1'][1]:.3f} / {med['h2n'][1]:.3f} / {med['h2'][1]:.3f} |")
+               for p in ("h1", "h2n", "h2n1", "h2")}
+        print(f"| {arm} | {med['h1'][0]:.1f} | {med['h2n'][0]:.1f} | {med['h2n1'][0]:.1f} | {med['h2'][0]:.1f} | "
+              f"{med['h2n'][0] / med['h1'][0]:.2f} | {med['h1'][1]:.3f} / {med['h2n'][1]:.3f} / "
+              f"{med['h2n1'][1]:.3f} / {med['h2'][1]:.3f} |")
 
 
 if __name__ == "__main__":

@@ -236,6 +236,7 @@ class H2Connection:
         self._raw = None                           # its rawhttp.RawConn (owns the socket)
         self._sinks: dict[int, H2Stream] = {}      # native: streams whose body a pump sink takes
         self.last_active = time.monotonic()        # last request or frame (idle-connection reaping)
+        self.pending = 0                           # requests a caller has picked this connection for
 
     @classmethod
     async def open(cls, host: str, port: int, ctx: ssl.SSLContext, *, timeout: float = 30.0) -> "H2Connection | None":
@@ -290,7 +291,12 @@ class H2Connection:
 
     def idle_for(self, now: float) -> float:
         """Seconds without a stream open (0 while one is)."""
-        return 0.0 if self.streams or self._sinks else now - self.last_active
+        return 0.0 if self.streams or self._sinks or self.pending else now - self.last_active
+
+    @property
+    def load(self) -> int:
+        """Open streams plus the requests about to open one."""
+        return len(self.streams) + self.pending
 
     def _write(self, data: bytes) -> None:
         if self._native is not None:

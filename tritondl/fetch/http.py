@@ -255,7 +255,7 @@ class HTTPDownloader:
                  native: bool = True, read_timeout: float = 120.0, probe_bytes: int = 0,
                  ca_pem: str = "", ca_file: str = "", stripe_bytes: int = 0, max_redirects: int = 10,
                  disk_reserve: int = 0, proxies: "_proxy.ProxyConfig | None" = None, http2: bool = False,
-                 h2_native: bool = True, h2_idle_s: float = 90.0) -> None:
+                 h2_native: bool = True, h2_idle_s: float = 90.0, h2_conns: int = 4) -> None:
         self.progress_interval = progress_interval
         # offer HTTP/2 to https origins (ALPN), as Go's transport under grab did
         self.http2 = http2
@@ -264,8 +264,11 @@ class HTTPDownloader:
         # an HTTP/2 connection with no stream for this long is closed (Go's IdleConnTimeout): a worker
         # that meets thousands of origins keeps a socket (and, native, a pump thread) only for live ones
         self.h2_idle_s = h2_idle_s
+        # HTTP/2 connections per origin: a stream goes to the least busy one, and a new one opens
+        # while every open one carries a stream (1 = one connection per origin, as Go's transport)
+        self.h2_conns = max(1, h2_conns)
         self._h2closing: set[asyncio.Task] = set()
-        self._h2conns: dict[tuple[str, int], "_h2.H2Connection"] = {}
+        self._h2conns: dict[tuple[str, int], list["_h2.H2Connection"]] = {}
         self._h2locks: dict[tuple[str, int], asyncio.Lock] = {}
         self._h1_only: dict[tuple[str, int], float] = {}     # origins that answered ALPN with http/1.1
         self.h2_streams = 0
@@ -338,8 +341,9 @@ class HTTPDownloader:
         return self._session
 
     async def close(self) -> None:
-        for c in list(self._h2conns.values()):
-            await c.close()
+        for conns in list(self._h2conns.values()):
+            for c in conns:
+                await c.close()
         if self._h2closing:
             await asyncio.gather(*self._h2closing, return_exceptions=True)
         self._h2conns.clear()
@@ -408,33 +412,53 @@ class HTTPDownloader:
         """Close HTTP/2 connections that died or sat without a stream for
         ``h2_idle_s``; forget expired HTTP/1.1-only verdicts."""
         now = time.monotonic()
-        for key, c in list(self._h2conns.items()):
-            if not c.alive and not c.streams or c.idle_for(now) > self.h2_idle_s:
+        for key, conns in list(self._h2conns.items()):
+            keep = []
+            for c in conns:
+                if not c.alive and not c.streams or c.idle_for(now) > self.h2_idle_s:
+                    t = asyncio.ensure_future(c.close())
+                    self._h2closing.add(t)
+                    t.add_done_callback(self._h2closing.discard)
+                else:
+                    keep.append(c)
+            if keep:
+                self._h2conns[key] = keep
+            else:
                 del self._h2conns[key]
                 lock = self._h2locks.get(key)
                 if lock is not None and not lock.locked():
                     del self._h2locks[key]
-                t = asyncio.ensure_future(c.close())
-                self._h2closing.add(t)
-                t.add_done_callback(self._h2closing.discard)
         for key, until in list(self._h1_only.items()):
             if until <= now:
                 del self._h1_only[key]
 
+    def _h2_pick(self, key: tuple[str, int]) -> "_h2.H2Connection | None":
+        """The least busy live connection to the origin, unless a new one
+        should open (every one carries a stream and there are fewer than
+        ``h2_conns``)."""
+        conns = [c for c in self._h2conns.get(key, ()) if c.alive]
+        if not conns:
+            return None
+        best = min(conns, key=lambda c: c.load)
+        if best.load and len(conns) < self.h2_conns:
+            return None
+        best.pending += 1                            # the caller's request() settles it
+        return best
+
     async def _h2_conn(self, host: str, port: int) -> "_h2.H2Connection | None":
-        """The origin's live HTTP/2 connection (opened on first use; one per
-        origin, shared by every stream), or None if it speaks HTTP/1.1."""
+        """A live HTTP/2 connection to the origin (see :meth:`_h2_pick`;
+        opened on first use), or None if the origin speaks HTTP/1.1."""
         self._h2_sweep()
         key = (host, port)
-        c = self._h2conns.get(key)
-        if c is not None and c.alive:
+        c = self._h2_pick(key)
+        if c is not None:
             return c
         if time.monotonic() < self._h1_only.get(key, 0.0):
             return None
         lock = self._h2locks.setdefault(key, asyncio.Lock())
         async with lock:
-            c = self._h2conns.get(key)
-            if c is not None and c.alive:
+            c = self._h2_pick(key)
+            if c is not None:
                 return c
             try:
                 if self.h2_native and rawhttp.relay_module() is not None:
@@ -447,7 +471,8 @@ class HTTPDownloader:
                 self._h1_only[key] = time.monotonic() + 3600.0
                 log.with_fields(origin=f"{host}:{port}").debug("origin does not speak HTTP/2; using HTTP/1.1")
                 return None
-            self._h2conns[key] = c
+            self._h2conns.setdefault(key, []).append(c)
+            c.pending += 1
             return c
 
     async def _h2_get(self, url: str, headers: dict) -> "_H2Response | None":
@@ -470,7 +495,10 @@ class HTTPDownloader:
             fields += [(k.lower().encode(), str(v).encode()) for k, v in hh.items()
                        if k.lower() not in ("host", "connection", "keep-alive", "transfer-encoding", "upgrade")]
             try:
-                st = await c.request(fields)
+                try:
+                    st = await c.request(fields)
+                finally:
+                    c.pending -= 1
                 await asyncio.wait_for(st.response(), self.read_timeout)
             except (_h2.H2Error, asyncio.TimeoutError) as e:
                 raise aiohttp.ClientConnectionError(f"GET {url} (HTTP/2): {e}") from e

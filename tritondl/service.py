@@ -108,7 +108,8 @@ def default_impls(cfg: Config) -> list[ClientImpl]:
     http = HTTPDownloader(progress_interval=cfg.progress_interval_s, segments=cfg.http_segments,
                           segment_threshold=cfg.http_segment_threshold, probe_bytes=cfg.http_probe_bytes,
                           ca_file=cfg.ca_file, stripe_bytes=cfg.http_stripe_bytes,
-                          disk_reserve=cfg.disk_reserve_bytes, http2=cfg.http2, h2_native=cfg.h2_native)
+                          disk_reserve=cfg.disk_reserve_bytes, http2=cfg.http2, h2_native=cfg.h2_native,
+                          h2_conns=cfg.http2_conns)
     impls: list[ClientImpl] = []
     try:
         from .fetch.bt.client import TorrentDownloader

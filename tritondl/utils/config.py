@@ -49,6 +49,7 @@ ENV_INTS = {"PREFETCH": "prefetch", "CONCURRENCY": "concurrency", "CONCURRENCY_M
             "S3_PART_SIZE": "s3_part_size", "S3_MULTIPART_THRESHOLD": "s3_multipart_threshold",
             "S3_PARALLEL_PARTS": "s3_parallel_parts", "HEARTBEAT": "heartbeat_s",
             "HTTP_SEGMENTS": "http_segments", "HTTP_SEGMENT_THRESHOLD": "http_segment_threshold",
+            "HTTP2_CONNS": "http2_conns",
             "HTTP_PROBE_BYTES": "http_probe_bytes", "S3_SIGN_THREADS": "s3_sign_threads",
             "HTTP_STRIPE_BYTES": "http_stripe_bytes", "DISK_RESERVE_BYTES": "disk_reserve_bytes",
             "BT_ESTABLISHED_CONNS": "bt_established_conns", "BT_HALF_OPEN_CONNS": "bt_half_open_conns",
@@ -205,6 +206,9 @@ class Config:
     # pacing, but one connection gets 0.28x where each TCP flow is capped (profiles/r06_h2_ab/)
     http2: bool = False
     h2_native: bool = True                      # HTTP/2 DATA via the native session pump (off: asyncio's TLS)
+    # HTTP/2 connections per origin: streams go to the least busy one, a new one opens while each
+    # carries a stream (four TCP windows, like four HTTP/1.1 connections); 1 = one per origin as Go
+    http2_conns: int = 4
     http_stripe_bytes: int = 0                  # >0: parallel streams pull in-order stripes of this size
                                                 # (0 measured faster on the 10 MiB headline job: profiles/r01_probe)
 
