@@ -555,3 +555,33 @@ def test_native_sink_writes_exactly_the_unpadded_bodies(chunks, end, limit):
         a.close()
         b.close()
     asyncio.run(main())
+
+
+def test_a_cancelled_native_sink_stops_writing_before_the_file_closes(tmp_path):
+    """Cancelling the task that waits on a native sink (a job torn down)
+    resets the stream and stops the pump's writes at once, so the caller
+    may close the file right after."""
+    async def main():
+        o = await H2Origin().start()
+        o.stream_rate = 20e6
+        data = os.urandom(8 << 20)
+        o.add("/c.mkv", data)
+        from tritondl.utils import rawhttp
+        c = await H2Connection.open_native("127.0.0.1", o.port, rawhttp.relay_module().TlsContext.client(ca_pem=o.ca_pem))
+        st = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", c.authority.encode()),
+                              (b":path", b"/c.mkv")])
+        await st.response()
+        fd = os.open(str(tmp_path / "c.part"), os.O_RDWR | os.O_CREAT, 0o644)
+        t = asyncio.ensure_future(st.sink(fd, 0, -1, None))
+        await asyncio.sleep(0.1)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        n = os.fstat(fd).st_size
+        os.close(fd)
+        await asyncio.sleep(0.2)
+        assert 0 < n < len(data) and os.path.getsize(tmp_path / "c.part") == n   # nothing written after
+        assert c._native.written(st.id) == 0 and st.error is not None
+        await c.close()
+        await o.stop()
+    run(main())

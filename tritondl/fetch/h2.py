@@ -169,19 +169,25 @@ class H2Stream:
         self.conn._sinks[self.id] = self            # the pump's answer is routed here
         native.sink_file(self.id, fd, offset, limit, flow, seg, done0)
         last = -1
-        while True:
-            try:
-                return await asyncio.wait_for(asyncio.shield(self._sink), idle_timeout)
-            except asyncio.TimeoutError:
-                if self._sink.done():
-                    return self._sink.result()
-                n = native.written(self.id)
-                if n == last:
-                    e = H2Error(f"HTTP/2 stream {self.id}: no body bytes for {idle_timeout:g} s")
-                    e.written = n
-                    self.cancel()
-                    raise e from None
-                last = n
+        try:
+            while True:
+                try:
+                    return await asyncio.wait_for(asyncio.shield(self._sink), idle_timeout)
+                except asyncio.TimeoutError:
+                    if self._sink.done():
+                        return self._sink.result()
+                    n = native.written(self.id)
+                    if n == last:
+                        e = H2Error(f"HTTP/2 stream {self.id}: no body bytes for {idle_timeout:g} s")
+                        e.written = n
+                        self.cancel()
+                        raise e from None
+                    last = n
+        except asyncio.CancelledError:
+            # the download is being torn down: the pump must stop writing into fd before the
+            # caller closes it (drop() returns only once no write is in flight)
+            self.cancel()
+            raise
 
     def _sink_done(self, written: int, eof: bool) -> None:
         self.eof = eof
