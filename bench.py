@@ -383,6 +383,8 @@ def main() -> int:
     ap.add_argument("--lease-after", type=float, default=-1.0,
                     help="lease a job's delivery once it has run this long (s; -1: worker default 30 s, which a "
                          "10 MiB job never reaches; a tiny value leases every job, to price the lease)")
+    ap.add_argument("--http2", default="default", choices=["default", "on", "off"],
+                    help="offer HTTP/2 to https origins (default: the worker's, on); matters with --tls only")
     ap.add_argument("--no-reference-mode", action="store_true",
                     help="skip the secondary run in the reference's cleanup-off mode after the timed region")
     ap.add_argument("--no-content-check", action="store_true",
@@ -455,6 +457,7 @@ def main() -> int:
                      content_check=not a.no_content_check,
                      overrides={"pipeline_commit": a.pipeline_commit == "on",
                                 **({"lease_after_s": a.lease_after} if a.lease_after >= 0 else {}),
+                                **({"http2": a.http2 == "on"} if a.http2 != "default" else {}),
                                 **({"pipeline_commit_min_ms": a.pipeline_min_ms} if a.pipeline_min_ms >= 0 else {}),
                                 **({"http_segment_threshold": int(a.segment_threshold_mb * (1 << 20))}
                                    if a.segment_threshold_mb > 0 else {}),
@@ -678,6 +681,7 @@ def main() -> int:
                        "cleanup": stack.cleanup, "pipeline_commit": a.pipeline_commit == "on",
                        "rtt_ms": a.rtt_ms, "stream_mbps": a.stream_mbps or None,
                        "lease_after_s": stack.cfg.lease_after_s if stack.cfg is not None else None,
+                       "http2": stack.cfg.http2 if stack.cfg is not None else None,
                        "log_level": a.log_level,
                        "recycle_bytes": stack.resolved_recycle_bytes() if stack.cleanup else 0,
                        "payload_variants": stack.resolved_variants(),

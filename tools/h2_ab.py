@@ -56,9 +56,10 @@ def _serve(conn, arm: str, proto: str, mib: int, rate: float) -> None:
             o = await Origin(tls=(cert, key)).start()
             o.rate = rate if arm in ("stream", "conn") else None     # one response per connection: the same cap
         conn.send((o.add("/ab.mkv", data), ca))
+        c0 = time.process_time()
         await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         gets = len([r for r in o.requests if r[0] == "GET"])
-        conn.send(o.connections if proto in ("h2", "h2n", "h2n1") else gets)
+        conn.send((o.connections if proto in ("h2", "h2n", "h2n1") else gets, time.process_time() - c0))
         await o.stop()
     asyncio.run(run())
 
@@ -86,12 +87,13 @@ async def one(arm: str, proto: str, mib: int, rate: float) -> dict:
     os.rmdir(d)
     await dl.close()
     parent.send("done")
-    conns = parent.recv() if parent.poll(30) else None
+    conns, origin_cpu = parent.recv() if parent.poll(30) else (None, None)
     p.join(30)
     data_len = mib << 20
     ok = size == data_len
     return {"arm": arm, "proto": proto, "bytes": data_len, "wall_s": round(wall, 4),
-            "MBps": round(data_len / wall / 1e6, 1), "cpu_s": round(cpu, 4), "ok": ok, "connections": conns}
+            "MBps": round(data_len / wall / 1e6, 1), "cpu_s": round(cpu, 4), "ok": ok, "connections": conns,
+            "origin_cpu_s": round(origin_cpu, 4) if origin_cpu is not None else None}
 
 
 async def main() -> None:

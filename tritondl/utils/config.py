@@ -200,11 +200,11 @@ class Config:
     http_segments: int = 4                      # max parallel Range streams per HTTP file
     http_segment_threshold: int = 64 * 1024 * 1024   # open-ended probe only: segment files at least this big
     http_probe_bytes: int = 0                   # >0: GET probe = bytes=0-(N-1), the rest as parallel Range streams
-    # offer HTTP/2 to https origins (ALPN): the probe and the Range segments become streams of
-    # one connection, as under grab's Go transport; DATA lands in the file from a native session
-    # pump.  Opt-in: against four HTTP/1.1 connections it uses less CPU and ties under per-request
-    # pacing, but one connection gets 0.28x where each TCP flow is capped (profiles/r06_h2_ab/)
-    http2: bool = False
+    # offer HTTP/2 to https origins (ALPN), as grab's Go transport did: the probe and the Range
+    # segments become streams, DATA lands in the file from a native session pump, and streams stripe
+    # over up to http2_conns connections.  Ties or beats four HTTP/1.1 connections under per-request
+    # and per-connection caps with less client CPU (profiles/r06_h2_ab/)
+    http2: bool = True
     h2_native: bool = True                      # HTTP/2 DATA via the native session pump (off: asyncio's TLS)
     # HTTP/2 connections per origin: streams go to the least busy one, a new one opens while each
     # carries a stream (four TCP windows, like four HTTP/1.1 connections); 1 = one per origin as Go
