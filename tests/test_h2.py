@@ -585,3 +585,46 @@ def test_a_cancelled_native_sink_stops_writing_before_the_file_closes(tmp_path):
         await c.close()
         await o.stop()
     run(main())
+
+
+def test_many_downloads_over_native_h2_keep_threads_and_fds_flat(tmp_path):
+    """200 downloads (8 at a time, segmented, some cancelled midway) over the
+    native transport: every completed file is intact, and the process ends
+    with as many threads and fds as after the first few (pump threads and
+    sockets belong to live connections only)."""
+    import threading
+
+    async def main():
+        o = await H2Origin().start()
+        o.stream_rate = 400e6
+        blobs = [os.urandom(1 << 20) * 3 for _ in range(4)]
+        urls = [o.add(f"/m{i}.mkv", b) for i, b in enumerate(blobs)]
+        dl = HTTPDownloader(progress_interval=1.0, ca_file=o.ca_file, http2=True, segment_threshold=1 << 20,
+                            h2_idle_s=0.2)
+        sem = asyncio.Semaphore(8)
+        counts = []
+
+        async def one(i: int) -> None:
+            async with sem:
+                d = tmp_path / str(i)
+                d.mkdir()
+                t = asyncio.ensure_future(dl.download(str(d), lambda u, p: None, urls[i % 4]))
+                if i % 10 == 9:
+                    await asyncio.sleep(0.002)
+                    t.cancel()
+                    with pytest.raises((asyncio.CancelledError, Exception)):
+                        await t
+                    return
+                await t
+                assert (d / f"m{i % 4}.mkv").read_bytes() == blobs[i % 4]
+                if i in (20, 198):
+                    counts.append((threading.active_count(), len(os.listdir("/proc/self/fd")),
+                                   len(os.listdir("/proc/self/task"))))
+        await asyncio.gather(*(one(i) for i in range(200)))
+        await asyncio.sleep(0.3)
+        (t0, f0, k0), (t1, f1, k1) = counts
+        assert k1 <= k0 + 2 and f1 <= f0 + 8, counts
+        assert o.connections <= 12
+        await dl.close()
+        await o.stop()
+    run(main(), 120)
