@@ -383,6 +383,8 @@ def main() -> int:
     ap.add_argument("--lease-after", type=float, default=-1.0,
                     help="lease a job's delivery once it has run this long (s; -1: worker default 30 s, which a "
                          "10 MiB job never reaches; a tiny value leases every job, to price the lease)")
+    ap.add_argument("--h2-origin", action="store_true",
+                    help="with --tls: the fake origin serves HTTP/2 (ALPN h2; Python frames) instead of HTTP/1.1")
     ap.add_argument("--http2", default="default", choices=["default", "on", "off"],
                     help="offer HTTP/2 to https origins (default: the worker's, on); matters with --tls only")
     ap.add_argument("--no-reference-mode", action="store_true",
@@ -450,6 +452,7 @@ def main() -> int:
     stack = JobStack(file_size=file_size, concurrency=a.concurrency, prefetch=prefetch,
                      tag=f"r{rank}", http_probe_bytes=(a.probe_kb << 10) if a.probe_kb >= 0 else -1,
                      http_segments=a.http_segments, sign_threads=a.sign_threads, tls=a.tls,
+                     h2_origin=a.h2_origin,
                      http_stripe_bytes=(a.stripe_kb << 10) if a.stripe_kb >= 0 else -1,
                      s3_part_size=a.s3_part_mb << 20, s3_multipart_threshold=a.s3_multipart_mb << 20,
                      payload_mode=a.payload, hash_device=a.s3_hash_device, cleanup=a.cleanup == "on",
@@ -583,6 +586,8 @@ def main() -> int:
                 "nvcsw_per_job": round((ru1.ru_nvcsw - ru0.ru_nvcsw) / n_div, 1),
                 "nivcsw_per_job": round((ru1.ru_nivcsw - ru0.ru_nivcsw) / n_div, 1),
                 "s3_content_checked": bool(stack.content_check and stack.resolved_variants()),
+                "h2_streams": sum(getattr(i, "h2_streams", 0) for i in getattr(stack.svc.dispatcher, "impls", [])
+                                  or []) if stack.svc is not None else None,
                 "vm": _vm_delta(vm0, vm1, n_div),
                 # CPython collections per generation inside the timed region (the worker
                 # froze its start-up heap: Service.start -> freeze_startup_heap)
@@ -670,7 +675,8 @@ def main() -> int:
                        "file_bytes": file_size, "parallelism": f"dp{world}",
                        "topology": ("one shared broker, competing consumers; per-rank origin+S3 nodes"
                                     if shared else "private broker/origin/S3 per rank"),
-                       "transport": "https (TLS 1.3, native OpenSSL data plane)" if a.tls else "http",
+                       "transport": ("https, HTTP/2 origin (TLS 1.3, native session pump)" if a.tls and a.h2_origin
+                                     else "https (TLS 1.3, native OpenSSL data plane)" if a.tls else "http"),
                        "s3_payload": stack.payload_mode, "s3_hash_device": a.s3_hash_device,
                        "cpus": (f"{len(pinned)} pinned ({pinned[0]}..{pinned[-1]})" if pinned else "unpinned"),
                        "fake_cpus": os.environ.get("TRITONDL_BENCH_FAKE_CPUS", "") or "same as the rank",

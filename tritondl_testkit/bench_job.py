@@ -120,6 +120,7 @@ class JobStack:
     s3_multipart_threshold: int = 0  # 0: worker default
     sign_threads: int = 0            # 0: worker default
     tls: bool = False                # origin + S3 over https (OpenSSL in the native data plane)
+    h2_origin: bool = False          # with tls: the origin serves HTTP/2 (ALPN h2) instead of HTTP/1.1
     payload_mode: str = ""           # "" → aws-chunked over http, unsigned over https (minio-go's choice)
     hash_device: str = "cpu"         # aws-chunked chunk SHA-256s: cpu (SHA-NI) | gpu (HIP)
     cleanup: bool = True             # delete (or recycle) each job's dir once settled; False = the reference (B15)
@@ -189,7 +190,11 @@ class JobStack:
                 out["broker"] = b.url
             from .fakes.payload import Expectations
             r = self.resolved_variants()
-            o = SyntheticOrigin(tls=tls)
+            if self.h2_origin and tls is not None:
+                from .fakes.serve import SyntheticH2Origin
+                o = SyntheticH2Origin(cert_pem=tls[0], key_pem=tls[1])
+            else:
+                o = SyntheticOrigin(tls=tls)
             o.precompute(self.file_size, r)
             await o.start()
             expect = Expectations(self.file_size, r) if r and self.content_check else None
@@ -209,7 +214,7 @@ class JobStack:
             out["broker"] = bk.info["url"]
             self.broker_pid = bk.proc.pid if bk.proc is not None else 0
         va = self._variant_args()
-        og = await Backend("origin", [*tls_args, *va]).start()
+        og = await Backend("h2origin" if self.h2_origin and self.tls else "origin", [*tls_args, *va]).start()
         s3 = await Backend("s3", ["--s3-store", "discard", "--access-key", AK, "--secret-key", SK, *tls_args,
                                   *(va if self.content_check else [])]).start()
         self.backends += [og, s3]

@@ -120,7 +120,7 @@ class _Conn:
         if loc is not None:
             await self._head(sid, [(b":status", b"301"), (b"location", loc.encode())], end=True)
             return
-        blob = srv.blobs.get(path.split("?", 1)[0])
+        blob = srv.lookup(path.split("?", 1)[0])
         if blob is None:
             await self._head(sid, [(b":status", b"404")], end=True)
             return
@@ -198,9 +198,12 @@ class _Conn:
 
 
 class H2Origin:
-    def __init__(self, host: str = "127.0.0.1", *, alpn: tuple[str, ...] = ("h2", "http/1.1")) -> None:
+    def __init__(self, host: str = "127.0.0.1", *, alpn: tuple[str, ...] = ("h2", "http/1.1"), port: int = 0,
+                 cert_pem: str = "", key_pem: str = "") -> None:
+        """``cert_pem`` / ``key_pem``: serve this certificate (else a throwaway
+        test PKI whose CA is ``ca_pem`` / ``ca_file``)."""
         from tritondl.utils import rawhttp
-        self.host, self.port = host, 0
+        self.host, self.port = host, port
         self.alpn = alpn
         self.blobs: dict[str, tuple[bytes, str, str]] = {}
         self.redirects: dict[str, str] = {}          # path -> Location of a 301
@@ -215,7 +218,10 @@ class H2Origin:
         self.max_streams = 100
         self.goaway_after = 0
         self.stall: tuple[int, float] | None = None   # (body offset, seconds): the next stream to reach it goes silent
-        ca, cert, key = rawhttp.relay_module().make_test_pki([host, "localhost"])
+        if cert_pem and key_pem:
+            ca, cert, key = "", cert_pem, key_pem
+        else:
+            ca, cert, key = rawhttp.relay_module().make_test_pki([host, "localhost"])
         self._dir = tempfile.mkdtemp(prefix="tdl-h2-")
         self.ca_file = os.path.join(self._dir, "ca.pem")
         for name, pem in (("ca.pem", ca), ("cert.pem", cert), ("key.pem", key)):
@@ -223,6 +229,10 @@ class H2Origin:
                 f.write(pem)
         self.ca_pem = ca
         self._server: asyncio.AbstractServer | None = None
+
+    def lookup(self, path: str):
+        """(data, etag, disposition) served at ``path``, or None (404)."""
+        return self.blobs.get(path)
 
     def add(self, path: str, data: bytes, disposition: str = "") -> str:
         self.blobs[path] = (data, '"' + hashlib.md5(data).hexdigest() + '"', disposition)
@@ -244,7 +254,7 @@ class H2Origin:
                 return
             await _Conn(self, r, w).run()
 
-        self._server = await asyncio.start_server(handle, self.host, 0, ssl=ctx)
+        self._server = await asyncio.start_server(handle, self.host, self.port, ssl=ctx)
         self.port = self._server.sockets[0].getsockname()[1]
         return self
 

@@ -1,7 +1,7 @@
 """Run one fake backend in its own process (so benches measure the worker,
 not the fakes competing for its event loop).
 
-    python -m tritondl_testkit.fakes.serve broker|origin|s3 [--port P] [--s3-store discard]
+    python -m tritondl_testkit.fakes.serve broker|origin|h2origin|s3 [--port P] [--s3-store discard]
                                    [--tls-cert PEM --tls-key PEM]   # origin / s3 over https
                                    [--variants N --variant-size BYTES]  # per-job payloads
     python -m tritondl_testkit.fakes.serve seed --path FILE_OR_DIR [--piece-kb 1024]
@@ -12,7 +12,9 @@ serves ``/synthetic/<bytes>/<name>``: deterministic pseudo-random content of
 the requested size (generated once per size, cached in memory); a name with
 a variant (``movie-3-v7.mkv``) gets that variant's distinct payload, and an
 S3 started with ``--variants`` refuses PUTs of variants whose content is not
-the origin's (:mod:`tritondl_testkit.fakes.payload`).
+the origin's (:mod:`tritondl_testkit.fakes.payload`).  ``h2origin`` serves
+the same synthetic payloads over HTTP/2 (TLS with ALPN ``h2``; needs
+``--tls-cert`` / ``--tls-key``).
 """
 
 from __future__ import annotations
@@ -26,6 +28,7 @@ import signal
 import sys
 
 from .broker import Broker
+from .h2origin import H2Origin
 from .origin import Blob, Origin
 from .payload import Expectations, synthetic_bytes, variant_bytes, variant_of
 from .s3 import FakeS3
@@ -63,6 +66,29 @@ class SyntheticOrigin(Origin):
         if len(parts) >= 4 and parts[1] == "synthetic" and parts[2].isdigit():
             self.blobs[request.path] = self.blob(int(parts[2]), variant_of(parts[-1]))
         return await super()._handle(request)
+
+
+class SyntheticH2Origin(H2Origin):
+    """The synthetic payloads of :class:`SyntheticOrigin`, served over HTTP/2."""
+
+    def __init__(self, *a, **kw) -> None:
+        super().__init__(*a, **kw)
+        self._cache: dict[tuple[int, int | None], tuple[bytes, str, str]] = {}
+
+    def lookup(self, path: str):
+        parts = path.split("/")
+        if len(parts) >= 4 and parts[1] == "synthetic" and parts[2].isdigit():
+            size, variant = int(parts[2]), variant_of(parts[-1])
+            b = self._cache.get((size, variant))
+            if b is None:
+                tag = f'"syn-{size}"' if variant is None else f'"syn-{size}-v{variant}"'
+                b = self._cache[(size, variant)] = (variant_bytes(size, variant), tag, "")
+            return b
+        return super().lookup(path)
+
+    def precompute(self, size: int, variants: int) -> None:
+        for k in range(variants):
+            self.lookup(f"/synthetic/{size}/x-{k}-v{k}.mkv")
 
 
 async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | None,
@@ -105,6 +131,14 @@ async def _amain(kind: str, port: int, s3_store: str, ak: str | None, sk: str | 
         await srv.start()
         info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}",
                 "url": f"{'https' if tls else 'http'}://{srv.host}:{srv.port}"}
+    elif kind == "h2origin":
+        if tls is None:
+            raise SystemExit("h2origin needs --tls-cert and --tls-key")
+        srv = SyntheticH2Origin("127.0.0.1", port=port, cert_pem=tls[0], key_pem=tls[1])
+        if variants and variant_size:
+            srv.precompute(variant_size, variants)
+        await srv.start()
+        info = {"kind": kind, "endpoint": f"{srv.host}:{srv.port}", "url": f"https://{srv.host}:{srv.port}"}
     elif kind == "s3":
         expect = None
         if variants and variant_size:
@@ -130,7 +164,7 @@ def main() -> None:
     from tritondl.parallel.topology import pin_from_env
     pin_from_env()
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["broker", "origin", "s3", "seed"])
+    ap.add_argument("kind", choices=["broker", "origin", "h2origin", "s3", "seed"])
     ap.add_argument("--path", default=None, help="seed: file or directory to seed")
     ap.add_argument("--piece-kb", type=int, default=1024)
     ap.add_argument("--encryption", default="allow", help="seed: MSE policy")

@@ -167,7 +167,8 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    on_sample=None, workdir: str | None = None, *, minutes: float = 0.0, rate: float = 0.0,
                    sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
                    torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None,
-                   tracemalloc_frames: int = 0, concurrency: int = 1, lease_after_s: float | None = None) -> dict:
+                   tracemalloc_frames: int = 0, concurrency: int = 1, lease_after_s: float | None = None,
+                   h2_origin: bool = False) -> dict:
     """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
     ``rate`` jobs/s (0: as fast as the worker goes).  ``tracemalloc_frames``
     > 0 traces Python allocations: the summary then lists the call sites
@@ -182,7 +183,7 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
     if tracemalloc_frames > 0:
         tracemalloc.start(tracemalloc_frames)
     st = JobStack(file_size=file_size, tag="soak", workdir=workdir, tls=tls, heartbeat=heartbeat,
-                  content_check=True, concurrency=concurrency)
+                  content_check=True, concurrency=concurrency, h2_origin=h2_origin)
     if lease_after_s is not None:
         st.overrides["lease_after_s"] = lease_after_s
     if malloc_trim_s is not None:
@@ -311,6 +312,7 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                  "where": [f"{fr.filename.rsplit('/', 2)[-2:]}:{fr.lineno}".replace("'", "") for fr in g.traceback][-4:]}
                 for g in grown[:15]]
             tracemalloc.stop()
+        summary["h2_streams"] = sum(getattr(i, "h2_streams", 0) for i in getattr(svc.dispatcher, "impls", []) or [])
         if svc.amqp is not None:
             summary["lease_stats"] = dict(svc.amqp.lease_stats)
             summary["leases_held_at_end"] = len(svc.amqp._leased)
@@ -353,6 +355,7 @@ def main() -> int:
     ap.add_argument("--malloc-trim", type=float, default=None, help="worker's malloc_trim period (s; 0 = off)")
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight (0: the worker's adaptive default)")
     ap.add_argument("--lease-after", type=float, default=None, help="lease every job running longer than this (s)")
+    ap.add_argument("--h2-origin", action="store_true", help="with --tls: the origin serves HTTP/2")
     ap.add_argument("--tracemalloc", type=int, default=0,
                     help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
@@ -381,7 +384,8 @@ def main() -> int:
                                    tls=a.tls, heartbeat=a.heartbeat, retry_delay=a.retry_delay,
                                    torrent_every=a.torrent_every, dht_nodes=a.dht_nodes,
                                    malloc_trim_s=a.malloc_trim, tracemalloc_frames=a.tracemalloc,
-                                   concurrency=a.concurrency, lease_after_s=a.lease_after))
+                                   concurrency=a.concurrency, lease_after_s=a.lease_after,
+                                   h2_origin=a.h2_origin))
     finally:
         if fh is not None:
             fh.close()
