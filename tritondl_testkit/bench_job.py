@@ -408,8 +408,9 @@ class JobStack:
             except psutil.Error:
                 continue
             out["fakes"] += ft.user + ft.system
-            if b.kind in out:
-                out[b.kind] += ft.user + ft.system
+            kind = "origin" if b.kind == "h2origin" else b.kind
+            if kind in out:
+                out[kind] += ft.user + ft.system
         return out
 
     def failures(self) -> list:
