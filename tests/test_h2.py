@@ -267,6 +267,25 @@ def test_streams_stripe_over_up_to_h2_conns_connections(tmp_path, native):
     run(main())
 
 
+@pytest.mark.parametrize("conns", [1, 4])
+def test_an_origin_allowing_one_stream_per_connection_still_serves_every_segment(tmp_path, conns):
+    """SETTINGS_MAX_CONCURRENT_STREAMS 1: with one connection the segments
+    take turns; with up to four, each gets a connection of its own."""
+    async def main():
+        o = await H2Origin().start()
+        o.max_streams = 1
+        data = os.urandom(1 << 20) * 12
+        url = o.add("/one.mkv", data)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, segment_threshold=4 << 20,
+                            h2_conns=conns)
+        await asyncio.wait_for(dl.download(str(tmp_path), lambda u, p: None, url), 30)
+        assert (tmp_path / "one.mkv").read_bytes() == data
+        assert o.streams == 4 and (o.connections == 1 if conns == 1 else 2 <= o.connections <= 4)
+        await dl.close()
+        await o.stop()
+    run(main())
+
+
 @TRANSPORTS
 def test_idle_connections_are_closed_and_their_pumps_stop(tmp_path, native):
     """A worker meets many origins: a connection with no stream for

@@ -93,6 +93,12 @@ class _Conn:
                             async with self.lock:
                                 self.w.write(frame(GOAWAY, 0, 0, struct.pack(">II", hsid - 2, 0)))
                             continue
+                        if len(self.tasks) >= self.srv.max_streams:
+                            # RFC 9113 5.1.2: over SETTINGS_MAX_CONCURRENT_STREAMS: refuse, retryable
+                            async with self.lock:
+                                self.w.write(frame(RST_STREAM, 0, hsid, struct.pack(">I", 7)))
+                            self.srv.refused += 1
+                            continue
                         self.windows[hsid] = self.init_window
                         self.tasks[hsid] = asyncio.ensure_future(self._serve(hsid, fields))
                 elif ftype == RST_STREAM:
@@ -112,6 +118,13 @@ class _Conn:
             self.w.close()
 
     async def _serve(self, sid: int, req: dict) -> None:
+        try:
+            await self._respond(sid, req)
+        finally:                                    # every way out frees the stream's slot
+            self.windows.pop(sid, None)
+            self.tasks.pop(sid, None)
+
+    async def _respond(self, sid: int, req: dict) -> None:
         srv = self.srv
         path = req.get(b":path", b"/").decode()
         rng = req.get(b"range", b"").decode()
@@ -181,8 +194,6 @@ class _Conn:
                 wait = self.sent_at + self.sent / srv.conn_rate - time.monotonic()
                 if wait > 0:
                     await asyncio.sleep(wait)
-        self.windows.pop(sid, None)
-        self.tasks.pop(sid, None)
 
     async def _head(self, sid: int, fields: list, end: bool) -> None:
         async with self.lock:
@@ -211,6 +222,7 @@ class H2Origin:
         self.connections = 0
         self.streams = 0
         self.resets = 0
+        self.refused = 0                             # streams refused over max_streams (RST REFUSED_STREAM)
         self.bytes_sent = 0
         self.stream_rate: float | None = None
         self.conn_rate: float | None = None
