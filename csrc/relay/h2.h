@@ -119,6 +119,7 @@ class H2Session {
       if (!write_file(sid, s, b.data(), b.size())) return;
       if (s.limit >= 0 && s.written >= uint64_t(s.limit)) break;
     }
+    if (!flush_file(sid, s)) return;
     if (s.limit >= 0 && s.written >= uint64_t(s.limit)) {
       finish_sink(sid, s, s.ended ? 1 : 0);
     } else if (s.ended) {
@@ -163,7 +164,7 @@ class H2Session {
   uint64_t written(uint32_t sid) {
     std::lock_guard<std::mutex> l(io_mu_);
     auto it = streams_.find(sid);
-    return it == streams_.end() ? 0 : it->second.written;
+    return it == streams_.end() ? 0 : it->second.flushed;
   }
 
   std::vector<H2Event> take_events() {
@@ -193,7 +194,9 @@ class H2Session {
     std::shared_ptr<Flow> flow;
     size_t seg = 0;
     uint64_t done0 = 0;
-    uint64_t written = 0;
+    uint64_t written = 0;  // body bytes the sink took (on disk or in wbuf)
+    uint64_t flushed = 0;  // ... of which on disk
+    std::string wbuf;      // taken, not yet written: small DATA frames become one pwrite
     std::deque<std::string> pend;  // body bytes received before a sink was attached
     uint64_t pend_bytes = 0;
     int64_t window = 0;    // what the server may still send on this stream
@@ -256,28 +259,52 @@ class H2Session {
   }
 
   void finish_sink(uint32_t sid, St& s, int eof) {
-    push_event(H2Event{kSinkDone, eof, sid, std::string(), s.written});
+    if (!flush_file(sid, s)) return;
+    push_event(H2Event{kSinkDone, eof, sid, std::string(), s.flushed});
     streams_.erase(sid);
   }
 
-  // Write body bytes into the stream's file (io_mu_ held).  false: the write
-  // failed, the stream is gone (`s` dangles) and Python has the error.
+  // Take body bytes into the stream's file sink (io_mu_ held): buffered, and
+  // written once kFlush bytes are waiting (or at the end of a receive batch),
+  // so 16 KiB frames do not cost a pwrite each.  false: a write failed, the
+  // stream is gone (`s` dangles) and Python has the error.
+  static constexpr size_t kFlush = 256u << 10;
   bool write_file(uint32_t sid, St& s, const char* p, size_t n) {
     size_t take = n;
     if (s.limit >= 0) take = size_t(std::min<uint64_t>(n, uint64_t(s.limit) - s.written));
     if (take) {
-      std::string err;
-      if (!pwrite_full(s.fd, p, take, s.pos + s.written, &err)) {
-        push_event(H2Event{kSinkError, 0, sid, err, s.written});
-        streams_.erase(sid);
-        return false;
-      }
+      s.wbuf.append(p, take);
       s.written += take;
-      bytes_written_.fetch_add(take, std::memory_order_relaxed);
-      if (s.flow) s.flow->advance(s.seg, s.done0 + s.written);
-      s.unacked += take;
+      if (s.wbuf.size() >= kFlush) return flush_file(sid, s);
     }
     return true;
+  }
+  bool flush_file(uint32_t sid, St& s) {
+    if (s.wbuf.empty()) return true;
+    std::string err;
+    if (!pwrite_full(s.fd, s.wbuf.data(), s.wbuf.size(), s.pos + s.flushed, &err)) {
+      push_event(H2Event{kSinkError, 0, sid, err, s.flushed});
+      streams_.erase(sid);
+      return false;
+    }
+    s.flushed += s.wbuf.size();
+    bytes_written_.fetch_add(s.wbuf.size(), std::memory_order_relaxed);
+    s.unacked += s.wbuf.size();
+    s.wbuf.clear();
+    if (s.flow) s.flow->advance(s.seg, s.done0 + s.flushed);
+    return true;
+  }
+  // End of a receive batch: what the file sinks took goes to disk (and its credit out).
+  void flush_all() {
+    std::lock_guard<std::mutex> l(io_mu_);
+    std::vector<uint32_t> sids;
+    for (auto& kv : streams_)
+      if (kv.second.mode == kFile && !kv.second.wbuf.empty()) sids.push_back(kv.first);
+    for (uint32_t sid : sids) {
+      auto it = streams_.find(sid);
+      if (it != streams_.end() && flush_file(sid, it->second)) credit_stream(sid, it->second);
+    }
+    flush_credit();
   }
 
   void on_data(uint8_t flags, uint32_t sid, const char* p, size_t len) {
@@ -354,9 +381,9 @@ class H2Session {
       std::lock_guard<std::mutex> l(io_mu_);
       auto it = streams_.find(sid);  // writes stop now; Python fails the stream from the event
       if (it != streams_.end()) {
-        if (it->second.mode == kFile)
-          push_event(H2Event{kSinkError, 0, sid, "reset by the server", it->second.written});
-        streams_.erase(it);
+        if (it->second.mode == kFile && flush_file(sid, it->second))
+          push_event(H2Event{kSinkError, 0, sid, "reset by the server", it->second.flushed});
+        streams_.erase(sid);
       }
     } else if (type == HEADERS && (flags & F_END_STREAM)) {
       // trailers (or a bodiless response) end the stream: a sink ends with what it wrote
@@ -399,8 +426,14 @@ class H2Session {
   void fail_all(const std::string& why) {
     {
       std::lock_guard<std::mutex> l(io_mu_);
+      std::vector<uint32_t> sids;
       for (auto& kv : streams_)
-        if (kv.second.mode == kFile) push_event(H2Event{kSinkError, 0, kv.first, why, kv.second.written});
+        if (kv.second.mode == kFile) sids.push_back(kv.first);
+      for (uint32_t sid : sids) {
+        auto it = streams_.find(sid);
+        if (it != streams_.end() && flush_file(sid, it->second))
+          push_event(H2Event{kSinkError, 0, sid, why, it->second.flushed});
+      }
       streams_.clear();
     }
     push_event(H2Event{kConnError, 0, 0, why, 0});
@@ -458,6 +491,7 @@ class H2Session {
             parse();
             continue;
           }
+          flush_all();  // nothing more to read right now: the sinks' buffers go to disk
           if (n == 0) throw std::runtime_error("connection closed by the server");
           if (n == IO_ERR) throw std::runtime_error(err);
           want_in = w;

@@ -137,10 +137,12 @@ async def _connect(o: H2Origin, native: bool) -> H2Connection:
 
 
 @TRANSPORTS
-def test_streams_share_one_connection_with_flow_control_and_padding(native):
+@pytest.mark.parametrize("frame_size", [1 << 20, 16384], ids=["1MiB-frames", "16KiB-frames"])
+def test_streams_share_one_connection_with_flow_control_and_padding(native, frame_size):
     async def main():
         o = await H2Origin().start()
         o.pad = True
+        o.frame_size = frame_size
         data = os.urandom(40 << 20)                  # > the 16 MiB stream window: WINDOW_UPDATEs needed
         o.add("/f.bin", data)
         c = await _connect(o, native)
@@ -263,6 +265,29 @@ def test_streams_stripe_over_up_to_h2_conns_connections(tmp_path, native):
         await one.download(str(tmp_path / "c"), lambda u, p: None, u2)
         assert o.connections == 5 and o.streams == 16
         await one.close()
+        await o.stop()
+    run(main())
+
+
+@TRANSPORTS
+def test_small_frames_from_an_nginx_like_origin_land_intact(tmp_path, native):
+    """16 KiB DATA frames (nginx-sized), some padded: a segmented download is
+    byte-exact (the native sink gathers them into large writes)."""
+    async def main():
+        o = await H2Origin().start()
+        o.frame_size = 16384
+        o.pad = True
+        data = os.urandom(1 << 20) * 24
+        url = o.add("/small.mkv", data)
+        dl = HTTPDownloader(progress_interval=0.05, ca_file=o.ca_file, http2=True, h2_native=native,
+                            segment_threshold=8 << 20)
+        await asyncio.wait_for(dl.download(str(tmp_path), lambda u, p: None, url), 60)
+        assert (tmp_path / "small.mkv").read_bytes() == data
+        # segments (6 MiB) below the 16 MiB initial stream window: the probe stream may overshoot by
+        # up to that window before its credit stops (at the default 64 MiB threshold it cannot)
+        from tritondl.fetch.h2 import STREAM_WINDOW
+        assert o.bytes_sent <= len(data) + STREAM_WINDOW
+        await dl.close()
         await o.stop()
     run(main())
 

@@ -10,7 +10,8 @@ follow), DATA frames respect the client's flow-control windows and its
 SETTINGS_MAX_FRAME_SIZE, and PING / RST_STREAM / GOAWAY are honoured.
 Fault and shaping knobs: ``stream_rate`` (bytes/s per stream),
 ``conn_rate`` (bytes/s per connection: one TCP window over a WAN path),
-``pad`` (pad every DATA frame), ``max_streams`` (SETTINGS_MAX_CONCURRENT_
+``pad`` (pad every DATA frame), ``frame_size`` (largest DATA frame),
+``max_streams`` (SETTINGS_MAX_CONCURRENT_
 STREAMS), ``goaway_after`` (GOAWAY after that many streams), ``stall`` ((offset,
 seconds): one stream goes silent mid-body), ``alpn``
 (offer only ``http/1.1`` to test the fallback); ``redirects`` maps a path
@@ -163,7 +164,8 @@ class _Conn:
             while self.conn_window <= 0 or self.windows.get(sid, 0) <= 0:
                 self.credit.clear()
                 await self.credit.wait()
-            n = min(end - pos, self.max_frame - (8 if srv.pad else 0), self.conn_window, self.windows[sid], 1 << 20)
+            n = min(end - pos, min(self.max_frame, srv.frame_size) - (8 if srv.pad else 0), self.conn_window,
+                    self.windows[sid])
             if srv.stall is not None and pos - start <= srv.stall[0] < pos - start + n:
                 at, secs = srv.stall
                 if at > pos - start:
@@ -223,6 +225,7 @@ class H2Origin:
         self.streams = 0
         self.resets = 0
         self.refused = 0                             # streams refused over max_streams (RST REFUSED_STREAM)
+        self.frame_size = 1 << 20                    # largest DATA frame sent (nginx sends ~16 KiB ones)
         self.bytes_sent = 0
         self.stream_rate: float | None = None
         self.conn_rate: float | None = None
