@@ -272,7 +272,19 @@ class H2Session {
   bool write_file(uint32_t sid, St& s, const char* p, size_t n) {
     size_t take = n;
     if (s.limit >= 0) take = size_t(std::min<uint64_t>(n, uint64_t(s.limit) - s.written));
-    if (take) {
+    if (take >= kFlush && s.wbuf.empty()) {  // a big frame goes straight from the record buffer
+      std::string err;
+      if (!pwrite_full(s.fd, p, take, s.pos + s.flushed, &err)) {
+        push_event(H2Event{kSinkError, 0, sid, err, s.flushed});
+        streams_.erase(sid);
+        return false;
+      }
+      s.written += take;
+      s.flushed += take;
+      s.unacked += take;
+      bytes_written_.fetch_add(take, std::memory_order_relaxed);
+      if (s.flow) s.flow->advance(s.seg, s.done0 + s.flushed);
+    } else if (take) {
       s.wbuf.append(p, take);
       s.written += take;
       if (s.wbuf.size() >= kFlush) return flush_file(sid, s);
