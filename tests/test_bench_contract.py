@@ -96,3 +96,15 @@ def test_bench_tls_json():
     d = _json_lines(r.stdout)[0]
     assert d["config"]["transport"].startswith("https") and d["config"]["s3_payload"] == "unsigned"
     assert d["value"] > 0
+
+
+def test_bench_tls_over_an_http2_origin_json():
+    """--tls --h2-origin: every job's download is an HTTP/2 stream (the worker
+    offers h2 by default) and its upload is content-checked like any other."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "1", "--file-mb", "1",
+                        "--no-gpu-probe", "--tls", "--h2-origin", "--no-reference-mode"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_lines(r.stdout)[0]
+    assert "HTTP/2" in d["config"]["transport"] and d["config"]["http2"] is True
+    assert d["diag"]["h2_streams"] >= 5 and d["diag"]["s3_content_checked"]
