@@ -8,6 +8,8 @@ server where a client can go wrong: response headers are HPACK-coded with
 Huffman strings and incremental indexing (the client's dynamic table must
 follow), DATA frames respect the client's flow-control windows and its
 SETTINGS_MAX_FRAME_SIZE, and PING / RST_STREAM / GOAWAY are honoured.
+``TRITONDL_FAKE_RTT_MS`` delays a new connection by two round trips and
+each response head by one, as the HTTP/1.1 fakes do.
 Fault and shaping knobs: ``stream_rate`` (bytes/s per stream),
 ``conn_rate`` (bytes/s per connection: one TCP window over a WAN path),
 ``pad`` (pad every DATA frame), ``frame_size`` (largest DATA frame),
@@ -127,6 +129,8 @@ class _Conn:
 
     async def _respond(self, sid: int, req: dict) -> None:
         srv = self.srv
+        if srv.rtt:
+            await asyncio.sleep(srv.rtt)              # emulated round trip: request out, head back
         path = req.get(b":path", b"/").decode()
         rng = req.get(b"range", b"").decode()
         srv.requests.append(("GET", path, rng))
@@ -226,6 +230,8 @@ class H2Origin:
         self.resets = 0
         self.refused = 0                             # streams refused over max_streams (RST REFUSED_STREAM)
         self.frame_size = 1 << 20                    # largest DATA frame sent (nginx sends ~16 KiB ones)
+        from .rawserver import fake_rtt
+        self.rtt = fake_rtt()                        # TRITONDL_FAKE_RTT_MS: connection + TLS + each request
         self.bytes_sent = 0
         self.stream_rate: float | None = None
         self.conn_rate: float | None = None
@@ -263,6 +269,8 @@ class H2Origin:
 
         async def handle(r: asyncio.StreamReader, w: asyncio.StreamWriter) -> None:
             self.connections += 1
+            if self.rtt:
+                await asyncio.sleep(2 * self.rtt)     # TCP connect + TLS handshake round trips
             sslobj = w.get_extra_info("ssl_object")
             if sslobj is None or sslobj.selected_alpn_protocol() != "h2":
                 w.close()                      # this fake serves HTTP/2 only
