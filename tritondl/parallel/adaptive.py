@@ -16,14 +16,24 @@ first byte, the S3 reply and the broker confirm, and four jobs in flight ran
   (``probe - dispatch``) plus the S3 reply after the last byte landed
   (``upload - fetched``);
 * **CPU use** — the process's CPU seconds per second over the window, as a
-  share of the CPUs it may use (affinity and cgroup quota).
+  share of the CPUs it may use (affinity and cgroup quota);
+* **job intensity** — the CPU its threads asked for (ran on a CPU, or waited
+  on a run queue: ``/proc/self/task/*/schedstat``) over at least half a
+  second, divided by the slot time of the jobs that finished in it: how
+  many cores one job in flight keeps busy.  Counting run-queue waits keeps
+  a starved worker on a busy host from looking idle.  A loopback job keeps ~2.8 busy (its pumps and hashers
+  run in parallel).  A job fed by a bandwidth-limited origin (a CDN at
+  100 MB/s per connection: 100 ms per 10 MiB) keeps ~0.07 busy.  Its wait
+  share is low, because its time goes to the transfer, not to first bytes
+  and replies, yet a second job would run beside it at no cost.
 
 After every ``max(4, limit)`` finished jobs (or 2 s; the first decision
 waits for ``warmup_jobs``, whose connection set-up would read as waiting),
-while the median wait share is at least ``raise_at`` (0.5) and CPU use is
-below ``cpu_high`` the limit doubles (up to ``cap``); when the wait share
-falls below ``lower_at`` (0.4) or CPU use passes ``cpu_high`` it drops by
-one.  On the MI355X box's loopback fakes one job's wait share is ~0.2 and
+while the median wait share is at least ``raise_at`` (0.5), or a job in
+flight keeps less than ``idle_job`` (1.0) core busy, and CPU use is below
+``cpu_high``, the limit doubles (up to ``cap``).  When the wait share falls
+below ``lower_at`` (0.4) with jobs keeping at least ``busy_job`` (1.5) cores
+busy each, or CPU use passes ``cpu_high``, it drops by one.  On the MI355X box's loopback fakes one job's wait share is ~0.2 and
 the limit stays at 1 (the reference's pace, and round 5's headline); at a
 2 ms round trip it is ~0.7 and at 20 ms ~0.94, and the limit goes to 4
 (``profiles/r06_noise/SUMMARY.md``).  More jobs in flight on loopback run
@@ -62,25 +72,59 @@ def _cpu_now() -> float:
     return ru.ru_utime + ru.ru_stime
 
 
+def _cpu_demand() -> float:
+    """Seconds this process's threads ran on a CPU plus the seconds they
+    waited on a run queue (``/proc/self/task/*/schedstat``): what the jobs
+    asked of the CPUs, even where a busy or oversubscribed host did not give
+    it.  Falls back to CPU time alone."""
+    try:
+        tot = 0
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                with open(f"/proc/self/task/{tid}/schedstat") as f:
+                    run, wait = f.read().split()[:2]
+                tot += int(run) + int(wait)
+            except (OSError, ValueError):
+                continue
+        if tot:
+            return tot / 1e9
+    except OSError:
+        pass
+    return _cpu_now()
+
+
 class Controller:
     def __init__(self, cap: int, *, start: int = 1, raise_at: float = 0.5, lower_at: float = 0.4,
-                 cpu_high: float = 0.6, cpu_low: float = 0.25, period_s: float = 2.0, warmup_jobs: int = 8,
-                 free_bytes=None, reserve: int = 0, cpus: int | None = None) -> None:
+                 cpu_high: float = 0.6, cpu_low: float = 0.25, idle_job: float = 1.0, busy_job: float = 1.5,
+                 period_s: float = 2.0, warmup_jobs: int = 8, free_bytes=None, reserve: int = 0,
+                 cpus: int | None = None, clock=time.monotonic, cpu_clock=None, demand_clock=None,
+                 intensity_s: float = 0.5) -> None:
+        """``clock`` / ``cpu_clock`` / ``demand_clock``: wall, process-CPU and
+        CPU-demand seconds (tests pass their own); ``intensity_s``: the
+        shortest span job intensity is measured over."""
         self.cap = max(1, cap)
         self.limit = min(self.cap, max(1, start))
         self.raise_at, self.lower_at = raise_at, lower_at
         self.cpu_high, self.cpu_low = cpu_high, cpu_low
+        self.idle_job, self.busy_job = idle_job, busy_job
+        self._clock = clock
+        self._cpu_now = cpu_clock or _cpu_now
+        self._demand_now = demand_clock or (cpu_clock if cpu_clock is not None else _cpu_demand)
+        self.intensity_s = intensity_s
+        self.job_cores: float | None = None   # latest job intensity (cores per job in flight)
         self.period_s = period_s
         self.free_bytes = free_bytes          # callable -> bytes free on the download fs (None: no guard)
         self.reserve = reserve
         self.cpus = cpus or usable_cpus()
         self.changes = 0
-        self.last = {"wait_share": None, "cpu_share": None, "why": "start"}
+        self.last = {"wait_share": None, "cpu_share": None, "job_cores": None, "why": "start"}
         self._shares: list[float] = []
+        self._slot_s = 0.0                    # slot time of the jobs finished since the last intensity sample
         self._other = 0                       # finished jobs without HTTP marks
         self._max_job_bytes = 0
-        self._t0 = time.monotonic()
-        self._cpu0 = _cpu_now()
+        self._t0 = self._clock()
+        self._cpu0 = self._cpu_now()
+        self._d_t0, self._d0 = self._t0, self._demand_now()
         self._n = 0
         self._warm = warmup_jobs              # finished jobs still to see before the first decision
 
@@ -89,18 +133,25 @@ class Controller:
         if self._warm > 0:
             self._warm -= 1
             if self._warm == 0:
-                self._t0, self._cpu0 = time.monotonic(), _cpu_now()
+                self._t0, self._cpu0 = self._clock(), self._cpu_now()
+                self._d_t0, self._d0, self._slot_s = self._t0, self._demand_now(), 0.0
             return False
         self._n += 1
         if nbytes > self._max_job_bytes:
             self._max_job_bytes = nbytes
         up, fet, probe = marks.get("upload"), marks.get("fetched"), marks.get("probe")
+        if up and up > 0:
+            self._slot_s += up
         if up and fet is not None and probe is not None and up > 0:
             head = max(0.0, probe - marks.get("dispatch", 0.0))
             self._shares.append(min(1.0, max(0.0, (head + max(0.0, up - fet)) / up)))
         else:
             self._other += 1
-        now = time.monotonic()
+        now = self._clock()
+        if now - self._d_t0 >= self.intensity_s and self._slot_s > 0:
+            d = self._demand_now()
+            self.job_cores = max(0.0, d - self._d0) / self._slot_s
+            self._d_t0, self._d0, self._slot_s = now, d, 0.0
         if self._n < max(4, self.limit) and now - self._t0 < self.period_s:
             return False
         return self._decide(now)
@@ -108,16 +159,17 @@ class Controller:
     def tick(self, all_busy: bool) -> bool:
         """Periodic check while no job finishes (long torrents): every slot
         busy for a whole period with the CPUs mostly idle raises the limit."""
-        now = time.monotonic()
+        now = self._clock()
         if self._n or now - self._t0 < self.period_s:
             return False
-        cpu = _cpu_now()
+        cpu = self._cpu_now()
         cpu_share = (cpu - self._cpu0) / max(1e-6, now - self._t0) / self.cpus
         self._t0, self._cpu0 = now, cpu
         old = self.limit
         if all_busy and cpu_share < self.cpu_low and not self._disk_tight():
             self.limit = min(self.cap, self.limit * 2)
-            self.last = {"wait_share": None, "cpu_share": round(cpu_share, 3), "why": "long jobs wait (cpu idle)"}
+            self.last = {"wait_share": None, "cpu_share": round(cpu_share, 3), "job_cores": None,
+                         "why": "long jobs wait (cpu idle)"}
         if self.limit != old:
             self.changes += 1
             return True
@@ -125,8 +177,9 @@ class Controller:
 
     def _decide(self, now: float) -> bool:
         dt = max(1e-6, now - self._t0)
-        cpu = _cpu_now()
+        cpu = self._cpu_now()
         cpu_share = (cpu - self._cpu0) / dt / self.cpus
+        job_cores = self.job_cores            # cores one job in flight keeps busy (sampled above)
         shares = sorted(self._shares)
         wait = shares[len(shares) // 2] if shares else None
         old = self.limit
@@ -137,12 +190,14 @@ class Controller:
             self.limit, why = max(1, self.limit - 1), "cpu busy"
         elif wait is not None and wait >= self.raise_at:
             self.limit, why = min(self.cap, self.limit * 2), "network waits dominate"
+        elif job_cores is not None and job_cores < self.idle_job:
+            self.limit, why = min(self.cap, self.limit * 2), "jobs leave the cpus idle"
         elif wait is None and self._other and cpu_share < self.cpu_low:
             self.limit, why = min(self.cap, self.limit * 2), "jobs wait (cpu idle)"
-        elif wait is not None and wait < self.lower_at:
+        elif wait is not None and wait < self.lower_at and (job_cores is None or job_cores >= self.busy_job):
             self.limit, why = max(1, self.limit - 1), "jobs are cpu-bound"
         self.last = {"wait_share": None if wait is None else round(wait, 3), "cpu_share": round(cpu_share, 3),
-                     "why": why}
+                     "job_cores": None if job_cores is None else round(job_cores, 3), "why": why}
         self._shares.clear()
         self._other = self._n = 0
         self._t0, self._cpu0 = now, cpu
