@@ -33,10 +33,12 @@ while the median wait share is at least ``raise_at`` (0.5), or a job in
 flight keeps less than ``idle_job`` (1.0) core busy, and CPU use is below
 ``cpu_high``, the limit doubles (up to ``cap``).  When the wait share falls
 below ``lower_at`` (0.4) with jobs keeping at least ``busy_job`` (1.5) cores
-busy each, or CPU use passes ``cpu_high``, it drops by one.  On the MI355X box's loopback fakes one job's wait share is ~0.2 and
-the limit stays at 1 (the reference's pace, and round 5's headline); at a
-2 ms round trip it is ~0.7 and at 20 ms ~0.94, and the limit goes to 4
-(``profiles/r06_noise/SUMMARY.md``).  More jobs in flight on loopback run
+busy each, or CPU use passes ``cpu_high``, it drops by one.  On the MI355X box's loopback fakes one job's wait share is ~0.2, a
+job keeps ~2.9 cores busy, and the limit stays at 1 (the reference's pace,
+and round 5's headline); at a 2 ms round trip the wait share is ~0.7 and at
+20 ms ~0.94, and an origin capped at 100 MB/s per connection leaves ~0.07
+cores busy per job: the limit goes to 4 in all three
+(``profiles/r06_adaptive_v3/SUMMARY.md``).  More jobs in flight on loopback run
 more jobs per second too, but only because the fake S3 verifies each PUT on
 one stream: the wait there is the harness, not the network, so the
 thresholds keep it out.  Jobs without HTTP marks (torrents)
