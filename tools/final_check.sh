@@ -4,6 +4,8 @@
 #                                             2 / 20 ms RTT with the default, every job leased at 0 / 20 ms
 #   bash tools/final_check.sh OUTDIR configs  BASELINE's other configs (1 GiB job, 8-worker pool,
 #                                             2 GiB magnet, uTP, 8 GiB hybrid resume) + the RCCL one-rank path
+#   bash tools/final_check.sh OUTDIR scale    1 / 2 / 4 ranks on one shared broker (gloo; the box's CPU
+#                                             share is shared by every rank; the 8-rank run is the driver's)
 set -o pipefail
 out=${1:-gpurun_out/r06_final}
 part=${2:-core}
@@ -21,6 +23,12 @@ if [ "$part" = core ]; then
   b rtt20_default --steps 100 --warmup 10 --rtt-ms 20 || exit 1
   b lease_rtt0 --steps 200 --warmup 20 --lease-after 0.0001 || exit 1
   b lease_rtt20 --steps 100 --warmup 10 --rtt-ms 20 --lease-after 0.0001 || exit 1
+elif [ "$part" = scale ]; then
+  step n1 300 python bench.py --gpus 1 --steps 100 --warmup 10 --no-gpu-probe || exit 1
+  for n in 2 4; do
+    step n$n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+        --master-port $((29540 + n)) bench.py --gpus $n --steps 100 --warmup 10 --no-gpu-probe --dist-backend gloo || exit 1
+  done
 else
   b gib --file-mb 1024 --steps 6 --warmup 1 || exit 1
   step pool 240 python tools/bench_pool.py --workers 8 --jobs-per-worker 100 --file-kb 1024 || exit 1
