@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 closing check on an MI355X box, in two parts (each fits one gpurun call).
+# Round-6 closing check on an MI355X box, in three parts (each fits one gpurun call).
 #   bash tools/final_check.sh OUTDIR core     GPU tests + smoke, the driver's bench command x3,
 #                                             2 / 20 ms RTT with the default, every job leased at 0 / 20 ms
 #   bash tools/final_check.sh OUTDIR configs  BASELINE's other configs (1 GiB job, 8-worker pool,
