@@ -973,8 +973,10 @@ class HTTPDownloader:
         """An HTTP/2 stream on a native connection: the session pump writes
         the body into the file and onto the handle's flow (csrc/relay/h2.h)."""
         flow = h.flow if h is not None else None
+        rawhttp.trace("get_pump_start")
         try:
             got, eof = await r.st.sink(fd, pos, limit, flow, i, done[i], self.read_timeout)
+            rawhttp.trace("get_pump_end")
         except _h2.H2Error as e:
             done[i] += e.written
             if h is not None:
