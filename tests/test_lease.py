@@ -471,6 +471,36 @@ def test_graceful_restarts_and_connection_drops_do_not_count_as_crashes(tmp_path
     run(main())
 
 
+def test_a_resubmitted_job_interrupted_mid_run_runs_again(tmp_path):
+    """The same body was submitted again after this node finished it once
+    (its done-ledger entry is still inside the TTL).  The second run is
+    interrupted; its redelivered copy must run, not be acked as already
+    done: the entry is dropped when a fresh submission starts."""
+    async def main():
+        e = await Env().up(tmp_path, lease_after_s=0)
+        data = os.urandom(3_000_000)
+        url = e.origin.add("/again.mkv", data)
+        body = Download(created_at="t", media=Media(id="again", source_uri=url)).encode()
+        e.svc.ledger.add(body)                           # the first submission finished earlier
+        e.origin.rate = 1_000_000
+        e.broker.inject("v1.download", "v1.download-0", body, Properties(delivery_mode=2))
+        t0 = time.monotonic()
+        while not _gets(e.origin, "/again.mkv"):
+            assert time.monotonic() - t0 < 10
+            await asyncio.sleep(0.02)
+        assert not e.svc.ledger.has(body)
+        await e.svc.shutdown(grace=0.1)                  # the run is cut short; the delivery goes back
+        e.origin.rate = None
+        await _restart(e)
+        res = await e.wait_results(1, timeout=20)
+        assert res[0].stage == "done", res
+        assert len(_gets(e.origin, "/again.mkv")) >= 2 and len(e.converts()) == 1
+        assert e.svc.ledger.has(body)
+        assert e.s3.object_bytes("triton-staging", object_key("again", "again.mkv")) == data
+        await e.down()
+    run(main())
+
+
 def test_a_crashed_run_is_counted(tmp_path):
     async def main():
         e = await Env().up(tmp_path, redelivery_limit=1, lease_after_s=0)

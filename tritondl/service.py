@@ -844,6 +844,11 @@ class Service:
                             jobdir.mark_ended(self.dispatcher.job_dir(job.media.id))
                         return self._record(JobResult(False, "redelivery-limit", f"redelivered {n} times",
                                                       seconds=time.monotonic() - t0))
+                if self.ledger is not None and not msg.maybe_duplicate:
+                    # a new submission of a body this node finished before (within the ledger's
+                    # TTL): from here on an entry stands for THIS run, so a copy of it that comes
+                    # back after a crash mid-run is run again, not acked as done
+                    self.ledger.forget(msg.body)
                 rawhttp.trace("job_locked")
                 return await self._run_job(msg, job, t0)
         except JobBusy as e:
