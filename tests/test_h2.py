@@ -4,7 +4,7 @@ connection and the downloader's use of it.
 grab's ``http.Transport`` (``internal/downloader/http/http.go:18-22``)
 negotiated HTTP/2 with any https origin that offered it and carried every
 request as a stream of one connection.  The worker does the same with
-``TRITONDL_HTTP2=1``."""
+``TRITONDL_HTTP2`` (on by default)."""
 
 import asyncio
 import ctypes
@@ -12,6 +12,7 @@ import os
 import random
 import ssl
 
+import aiohttp
 import pytest
 
 from tritondl.fetch.h2 import H2Connection
@@ -199,6 +200,34 @@ def test_a_silent_stream_times_out_and_the_segment_is_retried(tmp_path, native):
         assert o.resets >= 1 and len(o.requests) >= 2
         # the retry resumes after what was written: every byte (native sink), whole write blocks (asyncio)
         assert o.requests[-1][2] == ("bytes=6291456-12582911" if native else "bytes=4194304-12582911")
+        await dl.close()
+        await o.stop()
+    run(main())
+
+
+@TRANSPORTS
+def test_a_request_whose_head_never_comes_frees_its_stream(native):
+    """The head does not arrive within the read timeout, or the job is
+    cancelled while waiting for it: the stream is reset and leaves the
+    connection, so it counts against neither the stream limit nor the
+    idle reaper."""
+    async def main():
+        o = await H2Origin().start()
+        url = o.add("/h.mkv", b"x" * 1000)
+        dl = HTTPDownloader(ca_file=o.ca_file, http2=True, read_timeout=0.3, h2_native=native)
+        await dl._h2_conn("127.0.0.1", o.port)            # connected before the head delay starts
+        (c,) = dl._h2conns[("127.0.0.1", o.port)]
+        c.pending -= 1
+        o.rtt = 2.0
+        with pytest.raises(aiohttp.ClientConnectionError):
+            await dl._h2_get(url, {})
+        assert not c.streams and c.load == 0
+        t = asyncio.ensure_future(dl._h2_get(url, {}))
+        await asyncio.sleep(0.1)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        assert not c.streams and c.load == 0 and c.alive
         await dl.close()
         await o.stop()
     run(main())

@@ -494,14 +494,19 @@ class HTTPDownloader:
                       (b":path", path.encode())]
             fields += [(k.lower().encode(), str(v).encode()) for k, v in hh.items()
                        if k.lower() not in ("host", "connection", "keep-alive", "transfer-encoding", "upgrade")]
+            st = None
             try:
                 try:
                     st = await c.request(fields)
                 finally:
                     c.pending -= 1
                 await asyncio.wait_for(st.response(), self.read_timeout)
-            except (_h2.H2Error, asyncio.TimeoutError) as e:
-                raise aiohttp.ClientConnectionError(f"GET {url} (HTTP/2): {e}") from e
+            except BaseException as e:
+                if st is not None:
+                    st.cancel()             # no head (timeout, error, the job cancelled): free the stream
+                if isinstance(e, (_h2.H2Error, asyncio.TimeoutError)):
+                    raise aiohttp.ClientConnectionError(f"GET {url} (HTTP/2): {e}") from e
+                raise
             self.h2_streams += 1
             loc = st.headers.get("Location")
             if st.status in (301, 302, 303, 307, 308) and loc:
