@@ -8,7 +8,7 @@ import os
 import time
 
 from tritondl.models import Media
-from tritondl.parallel.adaptive import Controller
+from tritondl.parallel.adaptive import Controller, DemandClock
 
 from .test_permissions import Env, run
 
@@ -116,6 +116,23 @@ def test_a_tight_disk_reserve_pins_the_limit_to_one():
     free[0] = (10 << 30) + (15 << 20)             # less than reserve + 2 jobs of 10 MiB
     _feed(c, sim, WAITING, 8)
     assert c.limit == 1 and c.last["why"] == "disk reserve"
+
+
+def test_cpu_demand_survives_threads_that_exit_between_samples():
+    """A thread that exits takes its schedstat counters with it; the demand
+    clock keeps what every thread did up to the last sample, so it never
+    goes backwards (which would read as jobs that leave the CPUs idle)."""
+    samples = iter([{"1": 10**9, "2": 2 * 10**9},      # 3.0 s so far
+                    {"1": 15 * 10**8},                  # thread 2 exited; thread 1 +0.5 s
+                    {"1": 2 * 10**9, "3": 5 * 10**8},   # thread 3 started: all of it is new
+                    None])                              # unreadable: CPU time instead
+    clk = DemandClock(read=lambda: next(samples), fallback=lambda: 42.0)
+    assert [clk(), clk(), clk()] == [3.0, 3.5, 4.5]
+    assert clk() == 42.0
+    live = DemandClock()
+    a = live()
+    sum(i * i for i in range(200_000))
+    assert live() > a
 
 
 def test_long_jobs_with_idle_cpus_raise_the_limit_on_ticks():

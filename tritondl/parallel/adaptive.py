@@ -74,25 +74,50 @@ def _cpu_now() -> float:
     return ru.ru_utime + ru.ru_stime
 
 
-def _cpu_demand() -> float:
-    """Seconds this process's threads ran on a CPU plus the seconds they
-    waited on a run queue (``/proc/self/task/*/schedstat``): what the jobs
-    asked of the CPUs, even where a busy or oversubscribed host did not give
-    it.  Falls back to CPU time alone."""
+def _task_demand() -> dict[str, int] | None:
+    """Per thread: nanoseconds on a CPU plus nanoseconds waiting on a run
+    queue (``/proc/self/task/*/schedstat``); None where that is unreadable."""
+    out: dict[str, int] = {}
     try:
-        tot = 0
-        for tid in os.listdir("/proc/self/task"):
-            try:
-                with open(f"/proc/self/task/{tid}/schedstat") as f:
-                    run, wait = f.read().split()[:2]
-                tot += int(run) + int(wait)
-            except (OSError, ValueError):
-                continue
-        if tot:
-            return tot / 1e9
+        tids = os.listdir("/proc/self/task")
     except OSError:
-        pass
-    return _cpu_now()
+        return None
+    for tid in tids:
+        try:
+            with open(f"/proc/self/task/{tid}/schedstat") as f:
+                run, wait = f.read().split()[:2]
+            out[tid] = int(run) + int(wait)
+        except (OSError, ValueError):
+            continue
+    return out or None
+
+
+class DemandClock:
+    """Seconds this process's threads ran on a CPU plus the seconds they
+    waited on a run queue: what the jobs asked of the CPUs, even where a busy
+    or oversubscribed host did not give it.
+
+    A thread that exits takes its counters with it, so a plain sum over the
+    live threads can drop between two samples (a pump thread reaped, an
+    executor shrinking) and read as an idle worker.  This accumulates each
+    thread's growth since the last sample instead: monotonic, and a thread
+    that exits loses only what it did after the last sample.  Falls back to
+    CPU time alone."""
+
+    def __init__(self, read=_task_demand, fallback=None) -> None:
+        self._read = read
+        self._fallback = fallback or _cpu_now
+        self._last: dict[str, int] = {}
+        self._total = 0
+
+    def __call__(self) -> float:
+        cur = self._read()
+        if cur is None:
+            return self._fallback()
+        last = self._last
+        self._total += sum(max(0, v - last.get(t, 0)) for t, v in cur.items())
+        self._last = cur
+        return self._total / 1e9
 
 
 class Controller:
@@ -111,7 +136,7 @@ class Controller:
         self.idle_job, self.busy_job = idle_job, busy_job
         self._clock = clock
         self._cpu_now = cpu_clock or _cpu_now
-        self._demand_now = demand_clock or (cpu_clock if cpu_clock is not None else _cpu_demand)
+        self._demand_now = demand_clock or (cpu_clock if cpu_clock is not None else DemandClock())
         self.intensity_s = intensity_s
         self.job_cores: float | None = None   # latest job intensity (cores per job in flight)
         self.period_s = period_s
