@@ -630,6 +630,66 @@ def test_native_sink_writes_exactly_the_unpadded_bodies(chunks, end, limit):
     asyncio.run(main())
 
 
+@pytest.mark.parametrize("to_file", [True, False], ids=["file-sink", "events"])
+@pytest.mark.parametrize("read_late", [True, False], ids=["read-after-trailers", "read-before"])
+def test_a_body_ended_by_trailers_reaches_a_native_reader(to_file, read_late):
+    """Head, DATA without END_STREAM, then trailers (HEADERS with
+    END_STREAM) on a connection that stays open.  Whether the reader picks
+    its mode (file sink or events) before or after the trailers arrive, it
+    gets the whole body and the end of the stream, not a read timeout."""
+    import socket
+    import tempfile
+    from tritondl.fetch import h2 as h2mod
+    from tritondl.fetch.h2 import frame
+    from tritondl.utils import rawhttp
+
+    relay = rawhttp.relay_module()
+
+    async def main():
+        a, b = socket.socketpair()
+        a.setblocking(False)
+        sess = relay.H2Session(relay.Sock(a.fileno()), h2mod.STREAM_WINDOW, h2mod.CONN_WINDOW, h2mod.MAX_FRAME)
+        c = H2Connection(None, None, "origin.test", native=sess)
+        sess.start()
+        asyncio.get_running_loop().add_reader(sess.fileno(), c._on_native_events)
+        s = await c.request([(b":method", b"GET"), (b":scheme", b"https"), (b":authority", b"origin.test"),
+                             (b":path", b"/")])
+        enc = hpack.Encoder()
+        b.sendall(frame(1, 0x4, 1, enc.encode([(b":status", b"200")])))
+        await asyncio.wait_for(s.response(), 5.0)
+        wire = frame(0, 0, 1, b"abc") + frame(0, 0, 1, b"defg") + frame(1, 0x5, 1, enc.encode([(b"x-sum", b"1")]))
+
+        async def read(f) -> bytes:
+            if to_file:
+                n, eof = await s.sink(f.fileno(), 0, -1, None, idle_timeout=5.0)
+                assert eof
+                f.seek(0)
+                return f.read()
+            out = b""
+            while True:
+                x = await s.read()
+                if not x:
+                    return out
+                out += x
+
+        with tempfile.TemporaryFile() as f:
+            if read_late:
+                b.sendall(wire)
+                await asyncio.sleep(0.2)                   # the pump has the trailers before any reader
+                got = await asyncio.wait_for(read(f), 2.0)
+            else:
+                t = asyncio.ensure_future(read(f))
+                await asyncio.sleep(0.05)
+                b.sendall(wire)
+                got = await asyncio.wait_for(t, 2.0)
+        assert got == b"abcdefg"
+        assert not c.streams and not c._sinks and c.closed is None
+        await c.close()
+        a.close()
+        b.close()
+    asyncio.run(main())
+
+
 def test_a_cancelled_native_sink_stops_writing_before_the_file_closes(tmp_path):
     """Cancelling the task that waits on a native sink (a job torn down)
     resets the stream and stops the pump's writes at once, so the caller
