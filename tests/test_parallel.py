@@ -177,6 +177,8 @@ def test_idle_first_order_shared_by_local_ranks(tmp_path, monkeypatch):
     doms = [[0], [1], [2], [3]]
     assert t.idle_first(doms, [0.0, 0.5, 0.02, 0.3]) == [[0], [2], [3], [1]]
     assert t.idle_first(doms, [0.0] * 4) == doms                 # idle host: topology order
+    # a domain a tenant touches now and then (3 %) goes after the idle ones; sampling noise does not
+    assert t.idle_first(doms, [0.03, 0.0, 0.005, 0.5]) == [[1], [2], [0], [3]]
     monkeypatch.setattr(tempfile, "gettempdir", lambda: str(tmp_path))
     monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
     monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.9, 0.0, 0.0, 0.4])

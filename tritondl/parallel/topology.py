@@ -219,11 +219,25 @@ def domain_busy(doms: list[list[int]], interval: float = 0.2) -> list[float]:
     return out
 
 
+# Load step for ordering L3 domains.  10 % steps ranked a domain another
+# tenant touches now and then (2-10 % busy over the sample) with the idle
+# ones, and L3 order then often picked it.  Over 31 driver-form runs on
+# shared MI355X hosts, the 13 placed on a domain <= 1 % busy ran 362-409
+# jobs/s; the 18 on busier ones ran 238-411, and all five runs under 310
+# were among them (profiles/r06_final4/SUMMARY.md).
+IDLE_STEP = 0.02
+
+
+def _load_step(b: float) -> int:
+    return round(b / IDLE_STEP)
+
+
 def idle_first(doms: list[list[int]], busy: list[float]) -> list[list[int]]:
-    """Domains ordered by load in 10 % steps, L3 order within a step: an
-    idle host keeps the topology order (neighbours share a socket), a shared
-    one sends our ranks past the CCDs another tenant keeps busy."""
-    order = sorted(range(len(doms)), key=lambda i: (round(busy[i] * 10), i))
+    """Domains ordered by load in :data:`IDLE_STEP` steps, L3 order within
+    a step: an idle host keeps the topology order (neighbours share a
+    socket), a shared one sends our ranks past the CCDs another tenant
+    keeps busy, even a little."""
+    order = sorted(range(len(doms)), key=lambda i: (_load_step(busy[i]), i))
     return [doms[i] for i in order]
 
 
@@ -290,7 +304,7 @@ def shared_idle_order(local_rank: int, local_world: int, tag: str, timeout: floa
     path = os.path.join(tempfile.gettempdir(), f"tritondl-place-{tag}.json")
     if local_rank == 0 or local_world <= 1:
         busy = domain_busy(doms)
-        order = sorted(range(len(doms)), key=lambda i: (round(busy[i] * 10), i))
+        order = sorted(range(len(doms)), key=lambda i: (_load_step(busy[i]), i))
         if local_world > 1:
             tmp = f"{path}.{os.getpid()}"
             with open(tmp, "w") as f:
@@ -308,4 +322,4 @@ def shared_idle_order(local_rank: int, local_world: int, tag: str, timeout: floa
             pass
         time.sleep(0.05)
     busy = domain_busy(doms)
-    return idle_first(doms, busy), sorted(busy, key=lambda b: round(b * 10))
+    return idle_first(doms, busy), sorted(busy, key=_load_step)
