@@ -6,6 +6,8 @@ import os
 import signal
 import time
 
+import pytest
+
 from tritondl.amqp.codec import Properties
 from tritondl_testkit.fakes.broker import Broker
 from tritondl_testkit.fakes.origin import Origin
@@ -132,6 +134,7 @@ def test_pin_auto_takes_whole_l3_domain(monkeypatch):
     cpus = sorted(os.sched_getaffinity(0))
     doms = [cpus[:1], cpus[1:]] if len(cpus) > 1 else [cpus]
     monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
+    monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.0] * len(d))
     before = os.sched_getaffinity(0)
     try:
         assert t.pin("auto", 0) == doms[0]
@@ -144,6 +147,26 @@ def test_pin_auto_takes_whole_l3_domain(monkeypatch):
         if four:
             monkeypatch.setattr(t, "l3_domains", lambda allowed=None: four)
             assert t.pin("auto", 1, count=2) == four[2]          # 2 workers on 4 domains: 0 and 2
+    finally:
+        os.sched_setaffinity(0, before)
+
+
+def test_a_lone_auto_worker_takes_the_idlest_domain(monkeypatch):
+    """TRITONDL_CPUS=auto on one worker: the domain other tenants leave
+    idle, not always the first; several workers keep the even spread (their
+    GPUs' sockets)."""
+    from tritondl.parallel import topology as t
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 3:
+        pytest.skip("needs 3 CPUs")
+    doms = [[c] for c in cpus[:3]]
+    monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
+    monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.3, 0.04, 0.0])
+    before = os.sched_getaffinity(0)
+    try:
+        assert t.pin("auto") == doms[2]
+        os.sched_setaffinity(0, before)
+        assert t.pin("auto", 0, count=3) == doms[0]           # a pool's worker 0: the spread, not the load
     finally:
         os.sched_setaffinity(0, before)
 

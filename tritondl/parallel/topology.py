@@ -132,7 +132,8 @@ def compact_cpuset(n: int, index: int = 0, allowed: list[int] | None = None) -> 
 def pin(spec: str, index: int = 0, count: int = 1) -> list[int]:
     """Pin the calling process (and every thread and child it starts later)
     to ``spec``: a cpulist; ``auto`` = the ``index``-th of ``count`` whole
-    last-level-cache domains spaced evenly over the node (one CCD with its
+    last-level-cache domains spaced evenly over the node (a lone worker:
+    the idlest domain, :func:`idle_first`; one CCD with its
     SMT siblings per worker: on the box that beat 8 cores without siblings
     and two CCDs, ``profiles/r03_pin_ab/``);
     ``auto:N`` = the ``index``-th :func:`compact_cpuset` of N CPUs.  Returns
@@ -145,10 +146,15 @@ def pin(spec: str, index: int = 0, count: int = 1) -> list[int]:
             cpus = compact_cpuset(int(spec.split(":", 1)[1]), index)
         else:
             doms = l3_domains()
-            # ``count`` workers on this node (LOCAL_WORLD_SIZE) spread over all the
-            # domains, so half of 8 GPU workers land on each socket with their GPUs
-            stride = max(1, len(doms) // max(1, count, index + 1))
-            cpus = doms[(index * stride) % len(doms)]
+            if max(1, count) == 1 and index == 0 and len(doms) > 1:
+                # a lone worker: the idlest domain (sampled for 0.2 s), not always the
+                # first one, which a shared node's other tenants may keep busy
+                cpus = idle_first(doms, domain_busy(doms))[0]
+            else:
+                # ``count`` workers on this node (LOCAL_WORLD_SIZE) spread over all the
+                # domains, so half of 8 GPU workers land on each socket with their GPUs
+                stride = max(1, len(doms) // max(1, count, index + 1))
+                cpus = doms[(index * stride) % len(doms)]
     else:
         cpus = parse_cpulist(spec)
     os.sched_setaffinity(0, cpus)

@@ -279,8 +279,8 @@ class Config:
 
     # --- placement ---
     # CPU set the worker pins itself to at start-up: a cpulist ("0-7,128-135"),
-    # "auto" (one whole L3 domain, the LOCAL_RANK-th of LOCAL_WORLD_SIZE spread
-    # evenly over the node), "auto:N" (N CPUs packed into the fewest L3
+    # "auto" (one whole L3 domain: a lone worker the idlest one, else the
+    # LOCAL_RANK-th of LOCAL_WORLD_SIZE spread evenly over the node), "auto:N" (N CPUs packed into the fewest L3
     # domains) or "" (no pinning; the pool sets a cpulist per worker).  One CCD
     # keeps a job's bytes in its L3 as they pass receive pump -> hashers ->
     # send pump (profiles/r03_pin_ab/)
