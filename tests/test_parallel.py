@@ -175,7 +175,11 @@ def test_plan_gives_each_worker_an_l3_domain(monkeypatch):
     from tritondl.parallel import topology as t
     doms = [[0, 1, 8, 9], [2, 3, 10, 11], [4, 5, 12, 13], [6, 7, 14, 15]]
     monkeypatch.setattr(t, "l3_domains", lambda allowed=None: doms)
-    assert [w.cpus for w in t.plan(2, gpus=0)] == [doms[0], doms[2]]     # spread, like the GPUs
+    assert [w.cpus for w in t.plan(2, gpus=0, busy=[0.0] * 4)] == [doms[0], doms[2]]   # spread, like the GPUs
+    # each worker takes the idlest domain of its share of the spread (a tenant keeps 0 and 3 busy)
+    assert [w.cpus for w in t.plan(2, gpus=0, busy=[0.3, 0.0, 0.01, 0.2])] == [doms[1], doms[2]]
+    monkeypatch.setattr(t, "domain_busy", lambda d, interval=0.2: [0.0, 0.5, 0.5, 0.0])
+    assert [w.cpus for w in t.plan(2, gpus=0)] == [doms[0], doms[3]]     # sampled when not given
     assert [w.cpus for w in t.plan(4, gpus=0)] == doms
     # more workers than domains: consecutive slices of the L3-ordered CPUs
     assert [w.cpus for w in t.plan(8, gpus=0)][:2] == [[0, 1], [8, 9]]

@@ -49,7 +49,13 @@ def detect_gpus() -> int:
 
 
 def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | None = None,
-         cpus_per_worker: int = 2, base_port: int = 0, node_rank: int = 0, nnodes: int = 1) -> list[WorkerSpec]:
+         cpus_per_worker: int = 2, base_port: int = 0, node_rank: int = 0, nnodes: int = 1,
+         busy: list[float] | None = None) -> list[WorkerSpec]:
+    """One :class:`WorkerSpec` per worker: its rank, GPU and CPU set.  With at
+    least one L3 domain per worker, each worker gets a whole domain, spread
+    evenly over the node like the GPUs; within its share of the spread it
+    takes the idlest domain (``busy``: each domain's load, sampled for 0.2 s
+    when not given)."""
     gpus = detect_gpus() if gpus is None else gpus
     doms: list[list[int]] = []
     if cpus is None:
@@ -69,10 +75,15 @@ def plan(workers: int | None = None, *, gpus: int | None = None, cpus: int | Non
     # a single worker measured faster on one CCD than on two (profiles/r03_pin_ab/)
     by_domain = len(doms) > 1 and len(doms) >= workers
     stride = max(1, len(doms) // max(1, workers))   # spread over both sockets, as the GPUs are
+    if by_domain and stride > 1 and busy is None:
+        busy = domain_busy(doms)
     for i in range(workers):
         gpu = (i % gpus) if gpus > 0 else None
         if by_domain:
-            cset = doms[i * stride]
+            # the idlest domain of the worker's own stride window (a window stays on its
+            # socket, so the spread over the GPUs' sockets holds)
+            window = range(i * stride, min(len(doms), (i + 1) * stride))
+            cset = doms[min(window, key=lambda j: (_load_step(busy[j]), j)) if busy else i * stride]
         else:
             cset = avail[i * per:(i + 1) * per] if cpus >= workers else []
         out.append(WorkerSpec(node_rank * workers + i, i, world, gpu, cset,
