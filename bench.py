@@ -238,7 +238,11 @@ def _cpu_per_job(cpu_all: list, jobs: int) -> dict:
 # between back-to-back runs on one box: a change smaller than it is not resolved by one record.
 BUILDER_SPREAD = {"form": "--steps 20 --warmup 5", "runs": 6, "concurrency": 1,
                   "jobs_per_sec": [385.6, 411.5, 408.1, 419.9, 402.9, 393.5], "mean": 403.6, "stdev": 11.4,
-                  "range_pct_of_mean": 8.5}
+                  "range_pct_of_mean": 8.5,
+                  # 26 driver-form runs of the late round-6 trees on several boxes, co-tenant load
+                  # included (profiles/r06_final4/, r06_final5/): the tail is the host, not the tree
+                  "late_trees": {"runs": 26, "median": 380.2, "mean": 363.6, "stdev": 46.2, "min": 238.1,
+                                 "max": 411.3, "runs_below_310": 5}}
 
 
 def _noise(done: list, lat: list) -> dict:
