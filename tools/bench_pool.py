@@ -39,8 +39,10 @@ async def main() -> int:
     ap.add_argument("--file-kb", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight per worker (reference: 1)")
     ap.add_argument("--nodes", type=int, default=1, help="origin + S3 fake processes (sharded)")
-    ap.add_argument("--placement", default="l3", choices=["l3", "slice"],
-                    help="worker CPU sets: one L3 domain each (default) or consecutive CPU-id slices")
+    ap.add_argument("--placement", default="l3", choices=["l3", "l3-fixed", "slice"],
+                    help="worker CPU sets: one L3 domain each, the idlest of each worker's share (default), "
+                         "one L3 domain each at fixed strides (the plan before load sampling), or "
+                         "consecutive CPU-id slices")
     ap.add_argument("--s3-hash-device", default="cpu", choices=["cpu", "gpu"],
                     help="workers hash aws-chunked chunks on SHA-NI or the HIP kernel")
     a = ap.parse_args()
@@ -74,8 +76,13 @@ async def main() -> int:
                "TRITONDL_S3_HASH_DEVICE": a.s3_hash_device}
         ncpu = len(os.sched_getaffinity(0))
         # --placement l3: one CCD per worker (topology.plan); slice: consecutive CPU ids
-        specs = (plan(a.workers, gpus=0) if a.placement == "l3" else
-                 plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers)))
+        if a.placement == "l3":
+            specs = plan(a.workers, gpus=0)
+        elif a.placement == "l3-fixed":
+            from tritondl.parallel.topology import l3_domains
+            specs = plan(a.workers, gpus=0, busy=[0.0] * len(l3_domains()))
+        else:
+            specs = plan(a.workers, gpus=0, cpus=ncpu, cpus_per_worker=max(1, ncpu // a.workers))
         pool = WorkerPool(specs,
                           env=env, cwd=work, grace=10,
                           worker_env=lambda r: {"S3_ENDPOINT": s3s[r % len(s3s)]})
