@@ -168,7 +168,7 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                    sample_seconds: float = 60.0, tls: bool = False, heartbeat: int = 0, retry_delay: float = 0.0,
                    torrent_every: int = 0, dht_nodes: int = 0, malloc_trim_s: float | None = None,
                    tracemalloc_frames: int = 0, concurrency: int = 1, lease_after_s: float | None = None,
-                   h2_origin: bool = False) -> dict:
+                   h2_origin: bool = False, lease_s: float | None = None, stream_mbps: float = 0.0) -> dict:
     """Job-count soak (``jobs``) or, with ``minutes``, a wall-clock soak at
     ``rate`` jobs/s (0: as fast as the worker goes).  ``tracemalloc_frames``
     > 0 traces Python allocations: the summary then lists the call sites
@@ -176,7 +176,11 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
     end (``tracemalloc_growth``).  ``concurrency`` 0 is the worker's
     adaptive default; ``lease_after_s`` leases every job running longer
     (the summary then carries the lease events: taken, renewed, released,
-    lost)."""
+    lost), ``lease_s`` is the lease TTL (renewed every half of it), and
+    ``stream_mbps`` caps each origin / S3 stream (Mbit/s), so jobs run long
+    enough for their leases to be renewed."""
+    if stream_mbps > 0:
+        os.environ["TRITONDL_FAKE_STREAM_MBPS"] = str(stream_mbps)   # the fake processes inherit it
     import tracemalloc
     timed = minutes > 0
     base_snap = None
@@ -186,6 +190,8 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
                   content_check=True, concurrency=concurrency, h2_origin=h2_origin)
     if lease_after_s is not None:
         st.overrides["lease_after_s"] = lease_after_s
+    if lease_s is not None:
+        st.overrides["lease_s"] = lease_s
     if malloc_trim_s is not None:
         st.overrides["malloc_trim_s"] = malloc_trim_s
     seed = None
@@ -356,6 +362,9 @@ def main() -> int:
     ap.add_argument("--concurrency", type=int, default=1, help="jobs in flight (0: the worker's adaptive default)")
     ap.add_argument("--lease-after", type=float, default=None, help="lease every job running longer than this (s)")
     ap.add_argument("--h2-origin", action="store_true", help="with --tls: the origin serves HTTP/2")
+    ap.add_argument("--lease-ttl", type=float, default=None, help="lease TTL (s), renewed every half of it")
+    ap.add_argument("--stream-mbps", type=float, default=0.0,
+                    help="cap each fake origin / S3 stream (Mbit/s): long jobs whose leases renew")
     ap.add_argument("--tracemalloc", type=int, default=0,
                     help="trace Python allocations with this many frames; the summary lists the biggest growth")
     a = ap.parse_args()
@@ -385,7 +394,7 @@ def main() -> int:
                                    torrent_every=a.torrent_every, dht_nodes=a.dht_nodes,
                                    malloc_trim_s=a.malloc_trim, tracemalloc_frames=a.tracemalloc,
                                    concurrency=a.concurrency, lease_after_s=a.lease_after,
-                                   h2_origin=a.h2_origin))
+                                   h2_origin=a.h2_origin, lease_s=a.lease_ttl, stream_mbps=a.stream_mbps))
     finally:
         if fh is not None:
             fh.close()
