@@ -47,6 +47,25 @@ def test_time_based_soak_cycles_timers(tmp_path):
     assert len(res["samples"]) >= 3
 
 
+def test_lease_renewal_soak_loses_no_lease(tmp_path):
+    """The lease-renewal soak (``tools/soak_lease.sh``), reduced: capped
+    origin and S3 streams make every job run about a second, so each one is
+    leased after 0.2 s and renewed every 0.3 s while adaptive concurrency
+    runs several at once, beside failing jobs in delay-queue retries."""
+    import os
+    log.configure("error", "")
+    res = asyncio.run(asyncio.wait_for(
+        run_soak(jobs=0, fail_every=10, file_size=1 << 20, warmup=0, workdir=str(tmp_path), minutes=0.25, rate=6,
+                 sample_seconds=5, retry_delay=0.3, concurrency=0, lease_after_s=0.2, lease_s=0.6, stream_mbps=8),
+        150))
+    assert "TRITONDL_FAKE_STREAM_MBPS" not in os.environ             # restored for the tests after this one
+    assert res["ok_attempts"] == res["jobs"] - res["failing_jobs"] and res["jobs"] >= 20
+    ls = res["lease_stats"]
+    assert ls["lost"] == 0 and ls["taken"] >= res["jobs"] // 2, ls
+    assert ls["renewed"] >= ls["taken"] and ls["released"] == ls["taken"], ls
+    assert res["leases_held_at_end"] == 0 and res["reconnects"] == 0
+
+
 def test_drift_reports_point_and_median_window():
     """drift(): the first-vs-last post-warm-up change, and the same from the
     medians of the first and last few samples (one sample taken while a

@@ -179,6 +179,7 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
     lost), ``lease_s`` is the lease TTL (renewed every half of it), and
     ``stream_mbps`` caps each origin / S3 stream (Mbit/s), so jobs run long
     enough for their leases to be renewed."""
+    prev_mbps = os.environ.get("TRITONDL_FAKE_STREAM_MBPS")
     if stream_mbps > 0:
         os.environ["TRITONDL_FAKE_STREAM_MBPS"] = str(stream_mbps)   # the fake processes inherit it
     import tracemalloc
@@ -334,6 +335,11 @@ async def run_soak(jobs: int, torrent_jobs: int = 0, fail_every: int = 0, sample
         for x in dht:
             x.stop()
         await st.teardown()
+        if stream_mbps > 0:
+            if prev_mbps is None:
+                os.environ.pop("TRITONDL_FAKE_STREAM_MBPS", None)
+            else:
+                os.environ["TRITONDL_FAKE_STREAM_MBPS"] = prev_mbps
 
 
 def main() -> int:
