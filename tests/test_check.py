@@ -104,3 +104,16 @@ def test_lease_probe_tells_whether_leases_will_work(tmp_path, monkeypatch):
         finally:
             await b.stop()
     asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_cpu_check_reports_each_l3_domain_s_load(monkeypatch):
+    """The preflight shows how busy other tenants keep each L3 domain, as
+    placement sees it (TRITONDL_CPUS=auto and the pool take idle ones first)."""
+    from tritondl.parallel import topology
+    monkeypatch.setattr(topology, "l3_domains", lambda allowed=None: [[0, 1], [2, 3], [4, 5]])
+    monkeypatch.setattr(topology, "domain_busy", lambda d, interval=0.2: [0.0, 0.25, 0.004])
+    r = check.Report()
+    check.check_cpus(r)
+    (item,) = [i for i in r.items if i["area"] == "cpus"]
+    assert "2 of 3 L3 domains idle now" in item["detail"]
+    assert item["domain_busy"] == {"0": 0.0, "2": 0.25, "4": 0.004}

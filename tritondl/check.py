@@ -142,7 +142,15 @@ def check_cpus(r: Report) -> None:
     detail = f"{sum(len(d) for d in doms)} CPUs in {len(doms)} L3 domain(s) on NUMA node(s) {nodes}"
     if quota is not None:
         detail += f"; cgroup quota {quota:g} CPUs"
-    r.add("cpus", OK, detail, l3_domains=len(doms), numa_nodes=nodes, cpu_quota=quota)
+    extra: dict = {}
+    if len(doms) > 1:
+        # other tenants' load per domain, as placement sees it (TRITONDL_CPUS=auto and the pool
+        # take idle domains first; a domain another tenant uses slows the jobs pinned there)
+        busy = topology.domain_busy(doms)
+        idle = sum(1 for b in busy if b <= 0.01)
+        detail += f"; {idle} of {len(doms)} L3 domains idle now (placement takes idle ones first)"
+        extra["domain_busy"] = {str(d[0]): round(b, 3) for d, b in zip(doms, busy)}
+    r.add("cpus", OK, detail, l3_domains=len(doms), numa_nodes=nodes, cpu_quota=quota, **extra)
 
 
 async def check_broker(cfg: Config, r: Report, timeout: float) -> None:
