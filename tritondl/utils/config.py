@@ -119,6 +119,7 @@ class Config:
     # trip 4 jobs in flight ran 2.6x the jobs/s of one; on loopback one job keeps the CPUs
     # busy and the limit stays at 1)
     concurrency: int = 0
+    # the adaptive limit's cap (job loops started; each holds its streams' executor threads)
     concurrency_max: int = 4
     # a job's publish confirm + ack overlap the next job (service._worker): +30 % at a 2 ms and
     # +47 % at a 20 ms broker round trip, because the confirm's RTT leaves the job's critical
@@ -180,6 +181,8 @@ class Config:
     # '<shard>.lease.*' (refused: the delivery is held unacked, the reference's way);
     # 0 = off
     lease_after_s: float = 30.0
+    # the lease's TTL: how long a dead worker's job waits in its lease queue before it goes
+    # back to the shard queue; renewed every half of it while the job runs
     lease_s: float = 300.0
     # /healthz answers 503 once the broker connection, or the consumer of any shard queue,
     # has been down this long (the supervisor / shard re-subscribe loops keep retrying)
@@ -262,7 +265,9 @@ class Config:
     # request retries (minio-go retry.go: 10 attempts, 1 s unit, 30 s cap): connection errors,
     # 429/500/502/503/504 and minio's retryable codes (RequestTimeout, SlowDown, ExpiredToken, ...)
     s3_max_retries: int = 9
+    # backoff before retry n: unit * 2^n, capped, half of it jittered (the budget spans ~75 s)
     s3_retry_unit_s: float = 1.0
+    # the longest wait between two attempts
     s3_retry_cap_s: float = 30.0
     # a streamed PUT (the upload following its download) gives up after the download made no
     # progress for this long, and the file is uploaded once the download is done: S3 answers
