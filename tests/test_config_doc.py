@@ -15,6 +15,15 @@ def test_config_doc_is_current():
     assert r.returncode == 0, r.stderr
 
 
+def test_every_setting_has_a_description():
+    """A field without a comment in config.py lands in CONFIG.md with a
+    blank description: every row's last cell must say something."""
+    doc = open(os.path.join(ROOT, "docs", "CONFIG.md")).read()
+    blank = [ln.split("|")[1].strip() for ln in doc.splitlines()
+             if ln.startswith("| `TRITONDL_") and ln.rstrip().endswith("|  |")]
+    assert not blank, blank
+
+
 def test_every_env_name_in_the_sources_is_documented():
     doc = open(os.path.join(ROOT, "docs", "CONFIG.md")).read()
     names = set()
