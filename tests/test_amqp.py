@@ -645,3 +645,40 @@ def test_pause_hands_buffered_deliveries_back_and_resume_consumes_again():
         await cl.close()
         await b.stop()
     run(main())
+
+
+def test_a_redelivered_delivery_handed_back_stays_a_possible_duplicate():
+    """pause() re-publishes buffered deliveries as fresh messages.  One the
+    broker had flagged redelivered (an ack that went nowhere) keeps being
+    checked against the done-ledger: its copy carries X-Tdl-Redelivered.
+    A retry of it drops the mark."""
+    from tritondl.amqp.client import REDELIVERED
+
+    async def main():
+        b = await Broker().start()
+        cl = await Client(b.url, prefetch=1).connect()
+        await cl.consume("t")
+        b.inject("t", "t-0", b"long", Properties(delivery_mode=2))
+        running = await cl.get(2)
+        assert running.body == b"long"
+        b.pause_delivery(True)
+        b.inject("t", "t-1", b"dup", Properties(delivery_mode=2, headers={"X-Retries": 1}))
+        b.queues["t-1"].messages[-1].redelivered = True
+        b.pause_delivery(False)
+        for _ in range(50):
+            if not cl._out.empty():
+                break
+            await asyncio.sleep(0.01)
+        assert await cl.pause() == 1
+        back = b.queues["t-1"].messages
+        assert len(back) == 1 and not back[0].redelivered
+        assert back[0].props.headers[REDELIVERED] == 1 and back[0].props.headers["X-Retries"] == 1
+        await running.ack()
+        await cl.resume()
+        d = await cl.get(2)
+        assert d.body == b"dup" and not d.redelivered and d.maybe_duplicate
+        assert REDELIVERED not in d.retry_props().headers
+        await d.ack()
+        await cl.close()
+        await b.stop()
+    run(main())

@@ -109,6 +109,9 @@ class DeliveryMetadata:
 LEASE_RETURNS = "X-Lease-Returns"   # times the job came back because its holder's lease ran out
 LEASE_HOLDER = "X-Lease-Holder"     # host:pid that holds the lease copy (diagnostics)
 BUSY = "X-Busy"                     # hand-backs because another worker was running the same job
+# a buffered delivery the broker had flagged redelivered, handed back by pause(): the copy is a
+# fresh message, so this keeps it checked against the done-ledger like the redelivery it was
+REDELIVERED = "X-Tdl-Redelivered"
 OPS_CHANNELS = 8                    # idle lease-ops channels kept open
 
 
@@ -167,6 +170,7 @@ class Delivery:
         self.lease_return = _lease_expired(h)
         self.lease_returns = _int_header(h, LEASE_RETURNS) + (1 if self.lease_return else 0)
         self.busy = _int_header(h, BUSY)
+        self.handed_back_redelivered = _int_header(h, REDELIVERED) > 0
         self.lease: Lease | None = None
         self.requeue_props: Properties | None = None   # what a requeue publishes (a park's retry headers)
         self._hold: asyncio.Task | None = None
@@ -192,9 +196,10 @@ class Delivery:
     @property
     def maybe_duplicate(self) -> bool:
         """Could this job have been run to the end already?  Redelivered
-        (an ack went nowhere), back from an expired lease, or handed back
-        because another worker was running it."""
-        return self.msg.redelivered or self.lease_return or self.busy > 0
+        (an ack went nowhere; also a redelivered delivery :meth:`Client.pause`
+        handed back), back from an expired lease, or handed back because
+        another worker was running it."""
+        return self.msg.redelivered or self.handed_back_redelivered or self.lease_return or self.busy > 0
 
     @property
     def stale(self) -> bool:
@@ -223,6 +228,7 @@ class Delivery:
         hdrs["X-Retries"] = self.metadata.retries + increment
         hdrs.pop("x-death", None)
         hdrs.pop(LEASE_HOLDER, None)
+        hdrs.pop(REDELIVERED, None)
         if busy:
             hdrs[BUSY] = self.busy + 1
         else:
@@ -1199,8 +1205,11 @@ class Client:
         for d in held:
             if d.stale:
                 continue                    # its channel died: the broker requeued it already
+            props = d.msg.properties
+            if d.msg.redelivered:
+                props = dataclasses.replace(props, headers={**(props.headers or {}), REDELIVERED: 1})
             try:
-                await self.publish_raw(d.exchange, d.routing_key, d.body, d.msg.properties, max_attempts=3)
+                await self.publish_raw(d.exchange, d.routing_key, d.body, props, max_attempts=3)
                 await d.ack()
                 n += 1
             except Exception as e:  # noqa: BLE001 - the original is still unacked: requeue it

@@ -829,7 +829,8 @@ class Service:
                     return self._record(JobResult(True, "duplicate", seconds=time.monotonic() - t0))
                 if msg.lease_return:
                     self.metrics.inc("lease_returns")
-                if (msg.redelivered or msg.lease_returns) and self.cfg.redelivery_limit > 0:
+                if (msg.redelivered or msg.handed_back_redelivered or msg.lease_returns) and \
+                        self.cfg.redelivery_limit > 0:
                     n = self._count_redelivery(job.media.id, msg)
                     if n > self.cfg.redelivery_limit:
                         log.with_fields(media_id=job.media.id, redeliveries=n).error(
@@ -884,7 +885,7 @@ class Service:
         # a run is in progress in the job dir until it settles: a dir still marked after its
         # lock is free was left by a worker that died mid-job (see _count_redelivery)
         jd = ""
-        returned = msg.redelivered or msg.lease_returns > 0
+        returned = msg.redelivered or msg.handed_back_redelivered or msg.lease_returns > 0
         try:
             jd = self.dispatcher.job_dir(job.media.id) if self.dispatcher is not None else ""
         except ValueError:
